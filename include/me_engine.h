@@ -1,0 +1,227 @@
+/*
+ * me_engine.h — C-ABI of the MI355X batched matching core.
+ *
+ * This is the drop-in boundary between the (C++) submit-order host side and the
+ * gfx950 HIP kernels. Plain C: no exceptions cross it, every call returns an int
+ * status (0 = ok), buffers are caller-owned unless stated, no torch types.
+ *
+ * What each entry point replaces in the reference (julien-mrty/Matching_Engine,
+ * paths relative to the reference root):
+ *
+ *   me_service_*        MatchingEngineServiceImpl (include/server/matching_engine_service.hpp:9-30,
+ *                       src/server/matching_engine_service.cpp:17-121): ctor seeds the OID counter,
+ *                       me_service_submit_order == SubmitOrder (validate :66-83 -> OID :85 ->
+ *                       Order::FromRaw/normalize_to_q4 :89-97 -> persist :99-104 -> response :107-114).
+ *                       Persistence is deferred to the batched flush (me_service_flush).
+ *   me_normalize_to_q4  normalize_to_q4 (include/domain/price.hpp:15-29), exceptions mapped to codes.
+ *   me_create/...       the engine slot include/engine/model.hpp (0 bytes in the reference): there is no
+ *                       reference matcher; matching semantics are defined in DESIGN.md §2 and pinned by
+ *                       the CPU oracle under oracle/.
+ *   me_book_snapshot    GetOrderBook (src/server/matching_engine_service.cpp:123-129, a stub returning an
+ *                       empty OrderBookResponse) and Storage::best_bid/best_ask
+ *                       (src/storage/storage.cpp:212-252, broken: always nullopt).
+ *   me_fill             FillRow (include/storage/storage.hpp:11-17) + fills table (src/storage/storage.cpp:53-63).
+ *   ME_ST_*             OrderUpdate.Status (proto/matching_engine.proto:79-85).
+ */
+#ifndef ME_ENGINE_H
+#define ME_ENGINE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- domain encodings --------------------------------------------------------------- */
+/* Side (proto/matching_engine.proto:5-9; include/domain/side.hpp:8-9 static_asserts 1/2). */
+enum { ME_SIDE_UNSPECIFIED = 0, ME_SIDE_BUY = 1, ME_SIDE_SELL = 2 };
+/* OrderType (proto/matching_engine.proto:11-14). Any value != LIMIT is treated as MARKET,
+ * mirroring type_str / the LIMIT-only price check (matching_engine_service.cpp:50,78). */
+enum { ME_TYPE_LIMIT = 0, ME_TYPE_MARKET = 1 };
+/* Operation carried by a batch record. CANCEL is a build extension (no reference RPC). */
+enum { ME_OP_NEW = 0, ME_OP_CANCEL = 1 };
+/* OrderUpdate.Status (proto/matching_engine.proto:79-85). */
+enum {
+  ME_ST_NEW = 0,
+  ME_ST_PARTIALLY_FILLED = 1,
+  ME_ST_FILLED = 2,
+  ME_ST_CANCELED = 3,
+  ME_ST_REJECTED = 4
+};
+/* Why a batch record was rejected by the matcher (me_order_result.reason). */
+enum {
+  ME_RJ_NONE = 0,
+  ME_RJ_BAD_QTY = 1,       /* qty <= 0 (the service rejects these before they reach a batch) */
+  ME_RJ_BAD_SIDE = 2,      /* side not BUY/SELL (reference: CHECK side IN (1,2) -> "DB insert failed") */
+  ME_RJ_OUT_OF_WINDOW = 3, /* LIMIT price outside the symbol's fixed-depth level window */
+  ME_RJ_BAD_SYMBOL = 4,    /* symbol id >= num_symbols */
+  ME_RJ_UNKNOWN_ORDER = 5, /* CANCEL target is not a live resting order of this symbol */
+  ME_RJ_BAD_SEQ = 6        /* seq outside [1, max_seq) (locator capacity) */
+};
+
+/* kind byte of a batch record: bits 0-1 side, bit 2 type (1 = MARKET), bit 3 op (1 = CANCEL). */
+#define ME_KIND(side, type, op) ((uint8_t)(((side) & 3) | (((type) & 1) << 2) | (((op) & 1) << 3)))
+
+/* Slots per FIFO chunk (one wave-wide load of a level's queue). */
+#define ME_CHUNK_SLOTS 32
+
+/* Error codes returned by every entry point. */
+enum {
+  ME_OK = 0,
+  ME_E_INVALID = -1,   /* bad argument / config */
+  ME_E_HIP = -2,       /* HIP runtime failure (no device, launch failure, ...) */
+  ME_E_CAPACITY = -3,  /* a fixed-capacity pool (chunks, locator, scratch, tape) overflowed */
+  ME_E_STATE = -4,     /* engine in a failed state (a previous capacity/HIP error) */
+  ME_E_SQLITE = -5     /* persistence failure */
+};
+
+/* ---- domain helper ------------------------------------------------------------------- */
+/* normalize_to_q4 (include/domain/price.hpp:15-29). Returns 0 and *out on success,
+ * 1 for invalid_argument("scale out of range"), 2 for overflow_error("overflow"),
+ * 3 for overflow_error("underflow"). */
+int me_normalize_to_q4(int64_t price, int32_t scale, int64_t* out);
+
+/* ---- the batched matching engine (one shard = one GPU) ------------------------------- */
+typedef struct me_engine me_engine;
+
+typedef struct me_config {
+  int32_t device;              /* HIP device ordinal */
+  uint32_t num_symbols;        /* local symbols of this shard, ids 0..num_symbols-1 */
+  uint32_t levels;             /* L: fixed-depth price levels per symbol (power of two, 64..2^20) */
+  uint32_t max_batch;          /* largest n accepted by me_submit_batch* */
+  uint64_t max_resting;        /* resting orders the scratch/tape bound is sized for */
+  uint64_t max_chunks;         /* FIFO chunk pool (ME_CHUNK_SLOTS slots each); 0 = 2*max_resting/32 + 2*S */
+  uint64_t max_seq;            /* locator capacity: accepted seqs are 1 <= seq < max_seq */
+  const int64_t* base_price;   /* [num_symbols] price_q4 of level 0 of each symbol's window */
+  const uint32_t* symbol_ids;  /* optional [num_symbols] ids written to me_fill.symbol (NULL = local id) */
+} me_config;
+
+/* One batch in structure-of-arrays form, ascending seq (= numeric OID). */
+typedef struct me_order_soa {
+  const uint64_t* seq;      /* numeric OID of the record */
+  const int64_t* price_q4;  /* NEW: normalized Q4 price (ignored for MARKET); CANCEL: target seq */
+  const int32_t* qty;       /* NEW: quantity (wire int32, proto:44); CANCEL: ignored */
+  const uint32_t* symbol;   /* local symbol id */
+  const uint8_t* kind;      /* ME_KIND(side, type, op) */
+} me_order_soa;
+
+/* One trade (32 B): the maker rests, the taker crosses; price is the maker's level. */
+typedef struct me_fill {
+  uint64_t taker_seq;
+  uint64_t maker_seq;
+  int64_t price_q4;
+  int32_t qty;
+  uint32_t symbol;
+} me_fill;
+
+/* Per-record outcome (20 B). For CANCEL records: status CANCELED and remaining_qty = the
+ * quantity removed from the book, or REJECTED/UNKNOWN_ORDER. */
+typedef struct me_order_result {
+  int32_t filled_qty;
+  int32_t remaining_qty;  /* LIMIT: resting remainder; MARKET: discarded remainder */
+  uint32_t fill_count;
+  uint32_t tape_offset;   /* index of this record's first fill in the batch tape */
+  uint8_t status;         /* ME_ST_* */
+  uint8_t reason;         /* ME_RJ_* */
+  uint8_t pad[2];
+} me_order_result;
+
+/* One price level of a snapshot. */
+typedef struct me_level {
+  int64_t price_q4;
+  int64_t total_qty;
+  uint32_t order_count;
+  uint32_t pad;
+} me_level;
+
+/* One resting order of a full book dump, in priority order (bids best-first, then asks best-first). */
+typedef struct me_book_entry {
+  uint64_t seq;
+  int64_t price_q4;
+  int32_t qty;
+  uint8_t side;  /* ME_SIDE_BUY / ME_SIDE_SELL */
+  uint8_t pad[3];
+} me_book_entry;
+
+/* Creation fails (NULL) without a usable HIP device; the reason is then in me_last_error(NULL,..). */
+me_engine* me_create(const me_config* cfg);
+void me_destroy(me_engine* e);
+
+/* Host-memory batch: H2D -> group by symbol -> match -> compact tape -> D2H, synchronous.
+ * out_fills must hold me_fill_bound(e, n) records (or NULL to skip the tape copy);
+ * out_results holds n records (or NULL). *n_fills receives the tape length. */
+int me_submit_batch(me_engine* e, const me_order_soa* batch, size_t n, me_fill* out_fills,
+                    size_t fills_cap, size_t* n_fills, me_order_result* out_results);
+/* Upper bound on the tape length of one batch of n records (resting capacity + 2n). */
+uint64_t me_fill_bound(const me_engine* e, size_t n);
+
+/* Device-resident batch (pointers in HBM), enqueued on the engine stream, asynchronous.
+ * Outputs stay on the device until me_fetch_outputs. */
+int me_submit_batch_device(me_engine* e, const me_order_soa* dev_batch, size_t n);
+/* Wait for all enqueued work; returns ME_E_CAPACITY if a pool overflowed in any batch. */
+int me_sync(me_engine* e);
+/* Copy the last batch's tape/results to host memory (synchronous). */
+int me_fetch_outputs(me_engine* e, me_fill* out_fills, size_t fills_cap, size_t* n_fills,
+                     me_order_result* out_results, size_t n_results);
+/* Device-to-device copy of the last batch's tape into dst (HBM), on the engine stream;
+ * *n_fills is the synchronous tape length. */
+int me_copy_tape_device(me_engine* e, void* dst, size_t cap_fills, size_t* n_fills);
+
+/* Device memory helpers so a C/Python caller can keep batches resident without torch. */
+int me_device_alloc(me_engine* e, size_t bytes, void** dptr);
+int me_device_free(me_engine* e, void* dptr);
+int me_memcpy_h2d(me_engine* e, void* dst, const void* src, size_t bytes);
+/* Use an external hipStream_t (e.g. torch's current stream); NULL restores the engine's own. */
+int me_set_stream(me_engine* e, void* hip_stream);
+
+/* GetOrderBook: top `depth` levels per side, best first. */
+int me_book_snapshot(me_engine* e, uint32_t symbol, me_level* bids, me_level* asks, size_t depth,
+                     size_t* n_bids, size_t* n_asks);
+/* Full resting state of one symbol (side, price, FIFO). *n receives the count even when cap is short. */
+int me_book_dump(me_engine* e, uint32_t symbol, me_book_entry* out, size_t cap, size_t* n);
+/* Resting orders over all symbols (device counter). */
+int me_resting_count(me_engine* e, uint64_t* n);
+
+/* Kernel timing: when enabled, HIP events bracket every match-kernel launch on the engine stream. */
+int me_timing_enable(me_engine* e, int enable);
+/* Sum (ms) and count of match-kernel durations since enable, plus the whole-pipeline sum. */
+int me_timing_read(me_engine* e, double* match_ms, double* pipeline_ms, uint64_t* launches,
+                   uint64_t* fills, uint64_t* orders);
+
+/* Last error text of e (or of the last failed me_create when e == NULL). */
+int me_last_error(const me_engine* e, char* buf, size_t cap);
+
+/* ---- synthetic order streams (bench + tests; stands in for the reference client CLI) --- */
+typedef struct me_gen_params {
+  uint32_t config;          /* 1..5, SURVEY.md §8(d) */
+  uint64_t seed;
+  uint32_t num_symbols;     /* global symbols */
+  uint32_t levels;          /* window L per symbol (must cover the price spread) */
+  int32_t spread_ticks;     /* LIMIT offsets U[-spread, +spread] around the symbol mid */
+  int32_t max_qty;          /* qty ~ U[1, max_qty] */
+  uint32_t market_pct;      /* % MARKET among new orders */
+  uint32_t cancel_pct;      /* % CANCEL among records */
+  double zipf_s;            /* > 0: Zipf(s) symbol popularity, 0 = uniform */
+  int32_t market_qty_mult;  /* > 0: MARKET qty = U[1, market_qty_mult] * max_qty (sweeps) */
+} me_gen_params;
+
+typedef struct me_gen me_gen;
+me_gen* me_gen_create(const me_gen_params* p);
+void me_gen_destroy(me_gen* g);
+/* Per-symbol window base (level 0 price) for all num_symbols global symbols. */
+int me_gen_base_prices(const me_gen* g, int64_t* out);
+/* Next n records of the global stream (already normalized, global symbol ids, seq from 1).
+ * Any pointer may be NULL. */
+int me_gen_next(me_gen* g, size_t n, uint64_t* seq, int64_t* price_q4, int32_t* qty,
+                uint32_t* symbol, uint8_t* kind);
+/* Pre-seed records (config 4): `per_side` resting orders per side per symbol at distinct levels. */
+int me_gen_seed_book(me_gen* g, uint32_t symbol, uint32_t per_side, uint64_t* seq, int64_t* price_q4,
+                     int32_t* qty, uint8_t* kind);
+/* shard of a global symbol: splitmix64(symbol) % shards. */
+uint32_t me_shard_of(uint32_t symbol, uint32_t shards);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ME_ENGINE_H */

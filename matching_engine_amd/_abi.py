@@ -1,0 +1,150 @@
+"""ctypes view of include/me_engine.h (the C-ABI of libme_engine.so).
+
+The library is built in-tree (``make -C matching_engine_amd``); loading fails loudly when it is
+missing — there is no Python or CPU fallback for the matching path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libme_engine.so")
+
+# ---- enums (include/me_engine.h) -------------------------------------------------------------
+SIDE_UNSPECIFIED, SIDE_BUY, SIDE_SELL = 0, 1, 2
+TYPE_LIMIT, TYPE_MARKET = 0, 1
+OP_NEW, OP_CANCEL = 0, 1
+ST_NEW, ST_PARTIALLY_FILLED, ST_FILLED, ST_CANCELED, ST_REJECTED = 0, 1, 2, 3, 4
+RJ_NONE, RJ_BAD_QTY, RJ_BAD_SIDE, RJ_OUT_OF_WINDOW, RJ_BAD_SYMBOL, RJ_UNKNOWN_ORDER, RJ_BAD_SEQ = range(7)
+ME_OK, ME_E_INVALID, ME_E_HIP, ME_E_CAPACITY, ME_E_STATE, ME_E_SQLITE = 0, -1, -2, -3, -4, -5
+CHUNK_SLOTS = 32
+
+
+def kind(side: int, otype: int = TYPE_LIMIT, op: int = OP_NEW) -> int:
+    """ME_KIND(side, type, op)."""
+    return (side & 3) | ((otype & 1) << 2) | ((op & 1) << 3)
+
+
+# ---- structs ---------------------------------------------------------------------------------
+class MeConfig(C.Structure):
+    _fields_ = [
+        ("device", C.c_int32),
+        ("num_symbols", C.c_uint32),
+        ("levels", C.c_uint32),
+        ("max_batch", C.c_uint32),
+        ("max_resting", C.c_uint64),
+        ("max_chunks", C.c_uint64),
+        ("max_seq", C.c_uint64),
+        ("base_price", C.POINTER(C.c_int64)),
+        ("symbol_ids", C.POINTER(C.c_uint32)),
+    ]
+
+
+class MeOrderSoa(C.Structure):
+    _fields_ = [
+        ("seq", C.c_void_p),
+        ("price_q4", C.c_void_p),
+        ("qty", C.c_void_p),
+        ("symbol", C.c_void_p),
+        ("kind", C.c_void_p),
+    ]
+
+
+class MeGenParams(C.Structure):
+    _fields_ = [
+        ("config", C.c_uint32),
+        ("seed", C.c_uint64),
+        ("num_symbols", C.c_uint32),
+        ("levels", C.c_uint32),
+        ("spread_ticks", C.c_int32),
+        ("max_qty", C.c_int32),
+        ("market_pct", C.c_uint32),
+        ("cancel_pct", C.c_uint32),
+        ("zipf_s", C.c_double),
+        ("market_qty_mult", C.c_int32),
+    ]
+
+
+FILL_DTYPE = np.dtype(
+    [("taker_seq", "<u8"), ("maker_seq", "<u8"), ("price_q4", "<i8"), ("qty", "<i4"), ("symbol", "<u4")]
+)
+RESULT_DTYPE = np.dtype(
+    [
+        ("filled_qty", "<i4"),
+        ("remaining_qty", "<i4"),
+        ("fill_count", "<u4"),
+        ("tape_offset", "<u4"),
+        ("status", "u1"),
+        ("reason", "u1"),
+        ("pad", "u1", (2,)),
+    ]
+)
+LEVEL_DTYPE = np.dtype([("price_q4", "<i8"), ("total_qty", "<i8"), ("order_count", "<u4"), ("pad", "<u4")])
+BOOK_ENTRY_DTYPE = np.dtype(
+    [("seq", "<u8"), ("price_q4", "<i8"), ("qty", "<i4"), ("side", "u1"), ("pad", "u1", (3,))]
+)
+assert FILL_DTYPE.itemsize == 32 and RESULT_DTYPE.itemsize == 20
+assert LEVEL_DTYPE.itemsize == 24 and BOOK_ENTRY_DTYPE.itemsize == 24
+
+# every symbol include/me_engine.h declares -> (restype, argtypes)
+_P = C.c_void_p
+_SZ = C.c_size_t
+PROTOTYPES = {
+    "me_normalize_to_q4": (C.c_int, [C.c_int64, C.c_int32, C.POINTER(C.c_int64)]),
+    "me_create": (_P, [C.POINTER(MeConfig)]),
+    "me_destroy": (None, [_P]),
+    "me_submit_batch": (C.c_int, [_P, C.POINTER(MeOrderSoa), _SZ, _P, _SZ, C.POINTER(_SZ), _P]),
+    "me_fill_bound": (C.c_uint64, [_P, _SZ]),
+    "me_submit_batch_device": (C.c_int, [_P, C.POINTER(MeOrderSoa), _SZ]),
+    "me_sync": (C.c_int, [_P]),
+    "me_fetch_outputs": (C.c_int, [_P, _P, _SZ, C.POINTER(_SZ), _P, _SZ]),
+    "me_copy_tape_device": (C.c_int, [_P, _P, _SZ, C.POINTER(_SZ)]),
+    "me_device_alloc": (C.c_int, [_P, _SZ, C.POINTER(_P)]),
+    "me_device_free": (C.c_int, [_P, _P]),
+    "me_memcpy_h2d": (C.c_int, [_P, _P, _P, _SZ]),
+    "me_set_stream": (C.c_int, [_P, _P]),
+    "me_book_snapshot": (C.c_int, [_P, C.c_uint32, _P, _P, _SZ, C.POINTER(_SZ), C.POINTER(_SZ)]),
+    "me_book_dump": (C.c_int, [_P, C.c_uint32, _P, _SZ, C.POINTER(_SZ)]),
+    "me_resting_count": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
+    "me_timing_enable": (C.c_int, [_P, C.c_int]),
+    "me_timing_read": (
+        C.c_int,
+        [_P, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+         C.POINTER(C.c_uint64)],
+    ),
+    "me_last_error": (C.c_int, [_P, C.c_char_p, _SZ]),
+    "me_gen_create": (_P, [C.POINTER(MeGenParams)]),
+    "me_gen_destroy": (None, [_P]),
+    "me_gen_base_prices": (C.c_int, [_P, _P]),
+    "me_gen_next": (C.c_int, [_P, _SZ, _P, _P, _P, _P, _P]),
+    "me_gen_seed_book": (C.c_int, [_P, C.c_uint32, C.c_uint32, _P, _P, _P, _P]),
+    "me_shard_of": (C.c_uint32, [C.c_uint32, C.c_uint32]),
+}
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    """Load libme_engine.so (built in-tree). Raises if it is missing: no fallback exists."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"{LIB_PATH} is missing: build it with `make -C matching_engine_amd` "
+            "(the matching path has no CPU/Python fallback)"
+        )
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in PROTOTYPES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def ptr(a: np.ndarray) -> int:
+    return a.ctypes.data

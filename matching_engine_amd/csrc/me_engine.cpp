@@ -1,0 +1,675 @@
+// me_engine.cpp — host side of the batched matching core: owns the HBM-resident books of one
+// shard, stages batches, enqueues the gfx950 pipeline (me_kernels.hip) and implements the
+// C-ABI of include/me_engine.h. No CPU matching path exists here: without a HIP device
+// me_create fails and every call reports it.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "me_engine.h"
+#include "me_layout.hpp"
+
+static_assert(me::ME_C == ME_CHUNK_SLOTS, "chunk width mismatch");
+static_assert(sizeof(me_fill) == 32, "me_fill must be 32 B");
+static_assert(sizeof(me_order_result) == 20, "me_order_result must be 20 B");
+
+namespace me {
+hipError_t launch_sort_pass(hipStream_t st, const uint32_t* keys_in, const uint32_t* idx_in, uint32_t n,
+                            uint32_t clamp_key, int shift, int dbits, uint32_t* hist, uint32_t* keys_out,
+                            uint32_t* idx_out, uint32_t* zero_buf, uint32_t zero_words,
+                            unsigned long long* scratch_top);
+hipError_t launch_match(hipStream_t st, const BookDev& bk, const BatchDev& bt);
+hipError_t launch_tape(hipStream_t st, const BatchDev& bt, me_fill* tape, unsigned long long tape_cap,
+                       unsigned long long* tape_count, unsigned long long* fills_acc, uint32_t* err);
+hipError_t launch_init_levels(hipStream_t st, Level* levels, size_t count);
+}  // namespace me
+
+using namespace me;
+
+namespace {
+std::mutex g_err_mu;
+std::string g_create_err;
+
+struct TimedLaunch {
+  hipEvent_t p0, m0, m1, p1;
+  uint64_t orders;
+};
+}  // namespace
+
+struct me_engine {
+  me_config cfg{};
+  int dev = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  BookDev bk{};
+  std::vector<int64_t> base_host;
+  // grouping sort plan
+  int passes = 1;
+  int dbits[2] = {0, 0};
+  // batch buffers
+  uint64_t* d_seq = nullptr;
+  int64_t* d_px = nullptr;
+  int32_t* d_qty = nullptr;
+  uint32_t* d_sym = nullptr;
+  uint8_t* d_kind = nullptr;
+  uint32_t* d_keys[2] = {nullptr, nullptr};
+  uint32_t* d_idx[2] = {nullptr, nullptr};
+  uint32_t* d_hist = nullptr;
+  me_order_result* d_res = nullptr;
+  uint32_t* d_fstart = nullptr;
+  uint32_t* d_tile_sum = nullptr;
+  me_fill* d_scratch = nullptr;
+  unsigned long long* d_scratch_top = nullptr;
+  me_fill* d_tape = nullptr;
+  unsigned long long* d_tape_count = nullptr;
+  unsigned long long* d_fills_acc = nullptr;  // fills since timing was (re)enabled
+  unsigned long long scratch_cap = 0;
+  // pinned staging for host batches
+  void* h_pin = nullptr;
+  size_t h_pin_bytes = 0;
+  uint32_t last_n = 0;
+  bool failed = false;
+  std::string err;
+  // timing
+  bool timing = false;
+  std::vector<TimedLaunch> timed;
+  std::vector<void*> user_allocs;
+
+  int fail(int code, const std::string& msg) {
+    err = msg;
+    if (code == ME_E_CAPACITY || code == ME_E_HIP) failed = true;
+    return code;
+  }
+  int hip_fail(hipError_t e, const char* what) {
+    return fail(ME_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+  }
+};
+
+#define HIP_TRY(expr, what)                         \
+  do {                                              \
+    hipError_t _e = (expr);                         \
+    if (_e != hipSuccess) return e->hip_fail(_e, what); \
+  } while (0)
+
+static int set_create_err(const std::string& s) {
+  std::lock_guard<std::mutex> lk(g_err_mu);
+  g_create_err = s;
+  return 0;
+}
+
+static void free_all(me_engine* e) {
+  void* ptrs[] = {e->bk.levels,   e->bk.occ,      e->bk.sym,      e->bk.chdr,       e->bk.cseq,
+                  e->bk.cqty,     e->bk.loc,      e->bk.chunk_top, e->bk.err,       (void*)e->bk.gsym,
+                  e->d_seq,       e->d_px,        e->d_qty,       e->d_sym,         e->d_kind,
+                  e->d_keys[0],   e->d_keys[1],   e->d_idx[0],    e->d_idx[1],      e->d_hist,
+                  e->d_res,       e->d_fstart,    e->d_tile_sum,  e->d_scratch,     e->d_scratch_top,
+                  e->d_tape,      e->d_tape_count, e->d_fills_acc};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  for (void* p : e->user_allocs) (void)hipFree(p);
+  e->user_allocs.clear();
+  if (e->h_pin) (void)hipHostFree(e->h_pin);
+  for (auto& t : e->timed) {
+    (void)hipEventDestroy(t.p0);
+    (void)hipEventDestroy(t.m0);
+    (void)hipEventDestroy(t.m1);
+    (void)hipEventDestroy(t.p1);
+  }
+  e->timed.clear();
+  if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
+}
+
+extern "C" int me_normalize_to_q4(int64_t price, int32_t scale, int64_t* out) {
+  // include/domain/price.hpp:15-29: target scale 4, *10^diff with overflow checks, /10^-diff
+  // truncating toward zero.
+  static const int64_t P10[19] = {1LL,
+                                  10LL,
+                                  100LL,
+                                  1000LL,
+                                  10000LL,
+                                  100000LL,
+                                  1000000LL,
+                                  10000000LL,
+                                  100000000LL,
+                                  1000000000LL,
+                                  10000000000LL,
+                                  100000000000LL,
+                                  1000000000000LL,
+                                  10000000000000LL,
+                                  100000000000000LL,
+                                  1000000000000000LL,
+                                  10000000000000000LL,
+                                  100000000000000000LL,
+                                  1000000000000000000LL};
+  if (scale < 0 || scale > 18) return 1;
+  if (scale == 4) {
+    *out = price;
+    return 0;
+  }
+  const int diff = 4 - scale;
+  if (diff > 0) {
+    const int64_t mul = P10[diff];
+    if (price > 0 && price > INT64_MAX / mul) return 2;
+    if (price < 0 && price < INT64_MIN / mul) return 3;
+    *out = price * mul;
+    return 0;
+  }
+  *out = price / P10[-diff];
+  return 0;
+}
+
+template <class T>
+static hipError_t dalloc(T** p, size_t count) {
+  return hipMalloc((void**)p, std::max<size_t>(count, 1) * sizeof(T));
+}
+
+extern "C" me_engine* me_create(const me_config* cfg) {
+  if (!cfg || cfg->num_symbols == 0 || cfg->levels < 64 || (cfg->levels & (cfg->levels - 1)) ||
+      cfg->levels > (1u << 20) || cfg->max_batch == 0 || !cfg->base_price || cfg->max_seq < 2) {
+    set_create_err("me_create: invalid config (num_symbols>0, levels power of two in [64,2^20], "
+                   "max_batch>0, base_price, max_seq>=2)");
+    return nullptr;
+  }
+  const uint64_t S = cfg->num_symbols;
+  // key range 0..S (S = reject bin) -> radix plan
+  int bits = 1;
+  while ((1ull << bits) < S + 1) ++bits;
+  int passes, d0, d1;
+  if (bits <= MAX_DIGIT_BITS) {
+    passes = 1;
+    d0 = bits;
+    d1 = 0;
+  } else if (bits <= 2 * MAX_DIGIT_BITS) {
+    passes = 2;
+    d0 = (bits + 1) / 2;
+    d1 = bits - d0;
+  } else {
+    set_create_err("me_create: num_symbols too large for the 2-pass grouping sort (max 4M)");
+    return nullptr;
+  }
+  int ndev = 0;
+  hipError_t he = hipGetDeviceCount(&ndev);
+  if (he != hipSuccess || ndev <= 0) {
+    set_create_err(std::string("me_create: no HIP device (") + hipGetErrorString(he) + ")");
+    return nullptr;
+  }
+  if (cfg->device < 0 || cfg->device >= ndev) {
+    set_create_err("me_create: device ordinal out of range");
+    return nullptr;
+  }
+  me_engine* e = new me_engine();
+  e->cfg = *cfg;
+  e->dev = cfg->device;
+  e->passes = passes;
+  e->dbits[0] = d0;
+  e->dbits[1] = d1;
+  const uint64_t L = cfg->levels;
+  uint64_t nchunks = cfg->max_chunks;
+  if (nchunks == 0) nchunks = 2 * ((cfg->max_resting + ME_C - 1) / ME_C) + 2 * S;
+  const uint64_t n = cfg->max_batch;
+  const unsigned long long scap = cfg->max_resting + 2 * n;
+  auto bail = [&](const std::string& m) -> me_engine* {
+    set_create_err(m);
+    free_all(e);
+    delete e;
+    return nullptr;
+  };
+  if (nchunks * ME_C >= 0xFFFFFFFFull) return bail("me_create: chunk pool exceeds 32-bit slot ids");
+  if (scap >= 0xFFFFFFFFull) return bail("me_create: scratch bound exceeds 32-bit fill ids");
+  if (n >= 0x7FFFFFFFull) return bail("me_create: max_batch too large");
+  he = hipSetDevice(e->dev);
+  if (he != hipSuccess) return bail(std::string("hipSetDevice: ") + hipGetErrorString(he));
+  he = hipStreamCreateWithFlags(&e->own_stream, hipStreamNonBlocking);
+  if (he != hipSuccess) return bail(std::string("hipStreamCreate: ") + hipGetErrorString(he));
+  e->stream = e->own_stream;
+  BookDev& bk = e->bk;
+  bk.S = (uint32_t)S;
+  bk.L = (uint32_t)L;
+  bk.Lwords = (uint32_t)(L / 64);
+  bk.nchunks = (uint32_t)nchunks;
+  bk.max_seq = cfg->max_seq;
+  const uint32_t ntiles_sort = (uint32_t)((n + TILE_SORT - 1) / TILE_SORT);
+  const uint32_t ntiles_tape = (uint32_t)((n + TILE_TAPE - 1) / TILE_TAPE);
+#define ALLOC(p, cnt)                                                              \
+  do {                                                                             \
+    hipError_t _e = dalloc(&(p), (cnt));                                           \
+    if (_e != hipSuccess) return bail(std::string("hipMalloc " #p ": ") + hipGetErrorString(_e)); \
+  } while (0)
+  ALLOC(bk.levels, S * L);
+  ALLOC(bk.occ, S * (L / 64));
+  ALLOC(bk.sym, S);
+  ALLOC(bk.chdr, nchunks);
+  ALLOC(bk.cseq, nchunks * ME_C);
+  ALLOC(bk.cqty, nchunks * ME_C);
+  ALLOC(bk.loc, cfg->max_seq);
+  ALLOC(bk.chunk_top, 1);
+  ALLOC(bk.err, 1);
+  uint32_t* gsym = nullptr;
+  ALLOC(gsym, S);
+  bk.gsym = gsym;
+  ALLOC(e->d_seq, n);
+  ALLOC(e->d_px, n);
+  ALLOC(e->d_qty, n);
+  ALLOC(e->d_sym, n);
+  ALLOC(e->d_kind, n);
+  for (int k = 0; k < 2; ++k) {
+    ALLOC(e->d_keys[k], n);
+    ALLOC(e->d_idx[k], n);
+  }
+  ALLOC(e->d_hist, (size_t)(1u << MAX_DIGIT_BITS) * ntiles_sort);
+  ALLOC(e->d_res, n);
+  ALLOC(e->d_fstart, n);
+  ALLOC(e->d_tile_sum, ntiles_tape);
+  ALLOC(e->d_scratch, scap);
+  ALLOC(e->d_scratch_top, 1);
+  ALLOC(e->d_tape, scap);
+  ALLOC(e->d_tape_count, 1);
+  ALLOC(e->d_fills_acc, 1);
+#undef ALLOC
+  e->scratch_cap = scap;
+  // initial book state
+  hipStream_t st = e->stream;
+  std::vector<SymState> ss(S);
+  std::vector<uint32_t> gs(S);
+  e->base_host.assign(cfg->base_price, cfg->base_price + S);
+  for (uint64_t i = 0; i < S; ++i) {
+    ss[i].base = cfg->base_price[i];
+    ss[i].best_bid = -1;
+    ss[i].best_ask = (int)L;
+    ss[i].free_head = NIL;
+    ss[i].resting = 0;
+    ss[i].pad[0] = ss[i].pad[1] = 0;
+    gs[i] = cfg->symbol_ids ? cfg->symbol_ids[i] : (uint32_t)i;
+  }
+  bool ok = launch_init_levels(st, bk.levels, S * L) == hipSuccess &&
+            hipMemsetAsync(bk.occ, 0, S * (L / 64) * 8, st) == hipSuccess &&
+            hipMemsetAsync(bk.chdr, 0xFF, nchunks * sizeof(ChunkHdr), st) == hipSuccess &&
+            hipMemsetAsync(bk.cqty, 0, nchunks * ME_C * sizeof(int), st) == hipSuccess &&
+            hipMemsetAsync(bk.loc, 0xFF, cfg->max_seq * sizeof(uint32_t), st) == hipSuccess &&
+            hipMemsetAsync(bk.chunk_top, 0, 4, st) == hipSuccess && hipMemsetAsync(bk.err, 0, 4, st) == hipSuccess &&
+            hipMemcpyAsync(bk.sym, ss.data(), S * sizeof(SymState), hipMemcpyHostToDevice, st) == hipSuccess &&
+            hipMemcpyAsync(gsym, gs.data(), S * 4, hipMemcpyHostToDevice, st) == hipSuccess &&
+            hipMemsetAsync(e->d_tape_count, 0, 8, st) == hipSuccess &&
+            hipMemsetAsync(e->d_fills_acc, 0, 8, st) == hipSuccess &&
+            hipStreamSynchronize(st) == hipSuccess;
+  if (!ok) return bail(std::string("me_create: book init failed: ") + hipGetErrorString(hipGetLastError()));
+  e->h_pin_bytes = n * (8 + 8 + 4 + 4 + 1) + 64;
+  he = hipHostMalloc(&e->h_pin, e->h_pin_bytes, hipHostMallocDefault);
+  if (he != hipSuccess) return bail(std::string("hipHostMalloc: ") + hipGetErrorString(he));
+  return e;
+}
+
+extern "C" void me_destroy(me_engine* e) {
+  if (!e) return;
+  (void)hipSetDevice(e->dev);
+  if (e->stream) (void)hipStreamSynchronize(e->stream);
+  free_all(e);
+  delete e;
+}
+
+extern "C" uint64_t me_fill_bound(const me_engine* e, size_t n) {
+  return e ? (uint64_t)e->cfg.max_resting + 2ull * n : 0;
+}
+
+// Enqueue the whole pipeline for a device-resident batch.
+static int enqueue_batch(me_engine* e, const uint64_t* seq, const int64_t* px, const int32_t* qty,
+                         const uint32_t* sym, const uint8_t* kind, uint32_t n) {
+  hipStream_t st = e->stream;
+  TimedLaunch tl{};
+  if (e->timing) {
+    HIP_TRY(hipEventCreate(&tl.p0), "hipEventCreate");
+    HIP_TRY(hipEventCreate(&tl.m0), "hipEventCreate");
+    HIP_TRY(hipEventCreate(&tl.m1), "hipEventCreate");
+    HIP_TRY(hipEventCreate(&tl.p1), "hipEventCreate");
+    tl.orders = n;
+    HIP_TRY(hipEventRecord(tl.p0, st), "hipEventRecord");
+  }
+  const uint32_t S = e->bk.S;
+  const uint32_t ntiles_tape = (n + TILE_TAPE - 1) / TILE_TAPE;
+  // grouping sort
+  const uint32_t* kin = sym;
+  const uint32_t* iin = nullptr;
+  int shift = 0;
+  for (int p = 0; p < e->passes; ++p) {
+    hipError_t he = launch_sort_pass(st, kin, iin, n, S, shift, e->dbits[p], e->d_hist, e->d_keys[p], e->d_idx[p],
+                                     p == 0 ? e->d_tile_sum : nullptr, p == 0 ? ntiles_tape : 0,
+                                     e->d_scratch_top);
+    if (he != hipSuccess) return e->hip_fail(he, "grouping sort launch");
+    kin = e->d_keys[p];
+    iin = e->d_idx[p];
+    shift += e->dbits[p];
+  }
+  BatchDev bt{};
+  bt.seq = seq;
+  bt.px = px;
+  bt.qty = qty;
+  bt.sym = sym;
+  bt.kind = kind;
+  bt.n = n;
+  bt.skeys = kin;
+  bt.perm = iin;
+  bt.res = e->d_res;
+  bt.fstart = e->d_fstart;
+  bt.tile_sum = e->d_tile_sum;
+  bt.scratch = e->d_scratch;
+  bt.scratch_cap = e->scratch_cap;
+  bt.scratch_top = e->d_scratch_top;
+  if (e->timing) HIP_TRY(hipEventRecord(tl.m0, st), "hipEventRecord");
+  hipError_t he = launch_match(st, e->bk, bt);
+  if (he != hipSuccess) return e->hip_fail(he, "match launch");
+  if (e->timing) HIP_TRY(hipEventRecord(tl.m1, st), "hipEventRecord");
+  he = launch_tape(st, bt, e->d_tape, e->scratch_cap, e->d_tape_count, e->d_fills_acc, e->bk.err);
+  if (he != hipSuccess) return e->hip_fail(he, "tape launch");
+  if (e->timing) {
+    HIP_TRY(hipEventRecord(tl.p1, st), "hipEventRecord");
+    e->timed.push_back(tl);
+  }
+  e->last_n = n;
+  return ME_OK;
+}
+
+static int check_err_word(me_engine* e) {
+  uint32_t w = 0;
+  HIP_TRY(hipMemcpy(&w, e->bk.err, 4, hipMemcpyDeviceToHost), "read error word");
+  if (w) {
+    std::string m = "device pool overflow/inconsistency (bits=" + std::to_string(w) + "):";
+    if (w & ERR_CHUNK_OOM) m += " chunk pool exhausted (raise max_chunks);";
+    if (w & ERR_SCRATCH_OOM) m += " fill scratch/tape bound exceeded (raise max_resting);";
+    if (w & ERR_INCONSISTENT) m += " book inconsistency;";
+    return e->fail(ME_E_CAPACITY, m);
+  }
+  return ME_OK;
+}
+
+extern "C" int me_submit_batch_device(me_engine* e, const me_order_soa* b, size_t n) {
+  if (!e) return ME_E_INVALID;
+  if (e->failed) return ME_E_STATE;
+  if (!b || !b->seq || !b->price_q4 || !b->qty || !b->symbol || !b->kind) return e->fail(ME_E_INVALID, "null batch");
+  if (n == 0) {
+    e->last_n = 0;
+    return ME_OK;
+  }
+  if (n > e->cfg.max_batch) return e->fail(ME_E_INVALID, "batch larger than max_batch");
+  HIP_TRY(hipSetDevice(e->dev), "hipSetDevice");
+  return enqueue_batch(e, b->seq, b->price_q4, b->qty, b->symbol, b->kind, (uint32_t)n);
+}
+
+extern "C" int me_sync(me_engine* e) {
+  if (!e) return ME_E_INVALID;
+  HIP_TRY(hipSetDevice(e->dev), "hipSetDevice");
+  HIP_TRY(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
+  if (e->failed) return ME_E_STATE;
+  return check_err_word(e);
+}
+
+extern "C" int me_fetch_outputs(me_engine* e, me_fill* out_fills, size_t fills_cap, size_t* n_fills,
+                                me_order_result* out_results, size_t n_results) {
+  if (!e) return ME_E_INVALID;
+  int rc = me_sync(e);
+  if (rc) return rc;
+  unsigned long long cnt = 0;
+  if (e->last_n) HIP_TRY(hipMemcpy(&cnt, e->d_tape_count, 8, hipMemcpyDeviceToHost), "read tape count");
+  if (n_fills) *n_fills = (size_t)cnt;
+  if (out_results && n_results) {
+    if (n_results > e->last_n) return e->fail(ME_E_INVALID, "n_results exceeds last batch size");
+    HIP_TRY(hipMemcpy(out_results, e->d_res, n_results * sizeof(me_order_result), hipMemcpyDeviceToHost),
+            "D2H results");
+  }
+  if (out_fills && cnt) {
+    if (cnt > fills_cap) return e->fail(ME_E_INVALID, "fills_cap smaller than the tape");
+    HIP_TRY(hipMemcpy(out_fills, e->d_tape, cnt * sizeof(me_fill), hipMemcpyDeviceToHost), "D2H tape");
+  }
+  return ME_OK;
+}
+
+extern "C" int me_submit_batch(me_engine* e, const me_order_soa* b, size_t n, me_fill* out_fills,
+                               size_t fills_cap, size_t* n_fills, me_order_result* out_results) {
+  if (!e) return ME_E_INVALID;
+  if (e->failed) return ME_E_STATE;
+  if (n_fills) *n_fills = 0;
+  if (n == 0) {
+    e->last_n = 0;
+    return ME_OK;
+  }
+  if (!b || !b->seq || !b->price_q4 || !b->qty || !b->symbol || !b->kind) return e->fail(ME_E_INVALID, "null batch");
+  if (n > e->cfg.max_batch) return e->fail(ME_E_INVALID, "batch larger than max_batch");
+  HIP_TRY(hipSetDevice(e->dev), "hipSetDevice");
+  HIP_TRY(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
+  // stage into pinned memory, one H2D per column
+  char* p = (char*)e->h_pin;
+  uint64_t* hs = (uint64_t*)p;
+  int64_t* hp = (int64_t*)(p + 8 * n);
+  int32_t* hq = (int32_t*)(p + 16 * n);
+  uint32_t* hy = (uint32_t*)(p + 20 * n);
+  uint8_t* hk = (uint8_t*)(p + 24 * n);
+  memcpy(hs, b->seq, 8 * n);
+  memcpy(hp, b->price_q4, 8 * n);
+  memcpy(hq, b->qty, 4 * n);
+  memcpy(hy, b->symbol, 4 * n);
+  memcpy(hk, b->kind, n);
+  hipStream_t st = e->stream;
+  HIP_TRY(hipMemcpyAsync(e->d_seq, hs, 8 * n, hipMemcpyHostToDevice, st), "H2D seq");
+  HIP_TRY(hipMemcpyAsync(e->d_px, hp, 8 * n, hipMemcpyHostToDevice, st), "H2D price");
+  HIP_TRY(hipMemcpyAsync(e->d_qty, hq, 4 * n, hipMemcpyHostToDevice, st), "H2D qty");
+  HIP_TRY(hipMemcpyAsync(e->d_sym, hy, 4 * n, hipMemcpyHostToDevice, st), "H2D symbol");
+  HIP_TRY(hipMemcpyAsync(e->d_kind, hk, n, hipMemcpyHostToDevice, st), "H2D kind");
+  int rc = enqueue_batch(e, e->d_seq, e->d_px, e->d_qty, e->d_sym, e->d_kind, (uint32_t)n);
+  if (rc) return rc;
+  return me_fetch_outputs(e, out_fills, fills_cap, n_fills, out_results, out_results ? n : 0);
+}
+
+extern "C" int me_copy_tape_device(me_engine* e, void* dst, size_t cap_fills, size_t* n_fills) {
+  if (!e) return ME_E_INVALID;
+  int rc = me_sync(e);
+  if (rc) return rc;
+  unsigned long long cnt = 0;
+  if (e->last_n) HIP_TRY(hipMemcpy(&cnt, e->d_tape_count, 8, hipMemcpyDeviceToHost), "read tape count");
+  if (n_fills) *n_fills = (size_t)cnt;
+  if (cnt > cap_fills) return e->fail(ME_E_INVALID, "cap_fills smaller than the tape");
+  if (cnt) HIP_TRY(hipMemcpyAsync(dst, e->d_tape, cnt * sizeof(me_fill), hipMemcpyDeviceToDevice, e->stream),
+                   "D2D tape");
+  return ME_OK;
+}
+
+extern "C" int me_device_alloc(me_engine* e, size_t bytes, void** dptr) {
+  if (!e || !dptr) return ME_E_INVALID;
+  HIP_TRY(hipSetDevice(e->dev), "hipSetDevice");
+  HIP_TRY(hipMalloc(dptr, std::max<size_t>(bytes, 1)), "hipMalloc");
+  e->user_allocs.push_back(*dptr);
+  return ME_OK;
+}
+
+extern "C" int me_device_free(me_engine* e, void* dptr) {
+  if (!e) return ME_E_INVALID;
+  auto it = std::find(e->user_allocs.begin(), e->user_allocs.end(), dptr);
+  if (it == e->user_allocs.end()) return e->fail(ME_E_INVALID, "pointer not allocated by me_device_alloc");
+  e->user_allocs.erase(it);
+  HIP_TRY(hipSetDevice(e->dev), "hipSetDevice");
+  HIP_TRY(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
+  HIP_TRY(hipFree(dptr), "hipFree");
+  return ME_OK;
+}
+
+extern "C" int me_memcpy_h2d(me_engine* e, void* dst, const void* src, size_t bytes) {
+  if (!e) return ME_E_INVALID;
+  HIP_TRY(hipSetDevice(e->dev), "hipSetDevice");
+  HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice), "hipMemcpy H2D");
+  return ME_OK;
+}
+
+extern "C" int me_set_stream(me_engine* e, void* s) {
+  if (!e) return ME_E_INVALID;
+  HIP_TRY(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
+  e->stream = s ? (hipStream_t)s : e->own_stream;
+  return ME_OK;
+}
+
+// ---- book inspection (GetOrderBook / test dumps): host walk of device state ----------------
+namespace {
+struct HostLevelView {
+  std::vector<Level> levels;
+  SymState st;
+};
+}  // namespace
+
+static int load_symbol(me_engine* e, uint32_t s, HostLevelView& v) {
+  const size_t L = e->bk.L;
+  v.levels.resize(L);
+  HIP_TRY(hipMemcpy(v.levels.data(), e->bk.levels + (size_t)s * L, L * sizeof(Level), hipMemcpyDeviceToHost),
+          "D2H levels");
+  HIP_TRY(hipMemcpy(&v.st, e->bk.sym + s, sizeof(SymState), hipMemcpyDeviceToHost), "D2H symbol");
+  return ME_OK;
+}
+
+// Live (seq, qty) of a level FIFO in priority order.
+static int walk_fifo(me_engine* e, const Level& lv, std::vector<std::pair<uint64_t, int32_t>>& out) {
+  out.clear();
+  uint32_t ch = lv.head;
+  uint64_t guard = 0;
+  while (ch != NIL) {
+    if (ch >= e->bk.nchunks || ++guard > e->bk.nchunks) return e->fail(ME_E_STATE, "corrupt FIFO chain");
+    ChunkHdr h;
+    uint64_t seqs[ME_C];
+    int32_t qs[ME_C];
+    HIP_TRY(hipMemcpy(&h, e->bk.chdr + ch, sizeof(h), hipMemcpyDeviceToHost), "D2H chunk");
+    HIP_TRY(hipMemcpy(seqs, e->bk.cseq + (size_t)ch * ME_C, sizeof(seqs), hipMemcpyDeviceToHost), "D2H chunk");
+    HIP_TRY(hipMemcpy(qs, e->bk.cqty + (size_t)ch * ME_C, sizeof(qs), hipMemcpyDeviceToHost), "D2H chunk");
+    const uint32_t b = h.begin_end & 0xFFFF, en = h.begin_end >> 16;
+    for (uint32_t k = b; k < en && k < (uint32_t)ME_C; ++k)
+      if (qs[k] > 0) out.emplace_back(seqs[k], qs[k]);
+    if (ch == lv.tail) break;
+    ch = h.next;
+  }
+  return ME_OK;
+}
+
+extern "C" int me_book_snapshot(me_engine* e, uint32_t symbol, me_level* bids, me_level* asks, size_t depth,
+                                size_t* n_bids, size_t* n_asks) {
+  if (!e) return ME_E_INVALID;
+  if (symbol >= e->bk.S) return e->fail(ME_E_INVALID, "symbol out of range");
+  int rc = me_sync(e);
+  if (rc) return rc;
+  HostLevelView v;
+  if ((rc = load_symbol(e, symbol, v))) return rc;
+  std::vector<std::pair<uint64_t, int32_t>> fifo;
+  size_t nb = 0, na = 0;
+  for (int l = v.st.best_bid; l >= 0 && nb < depth; --l) {
+    if (v.levels[l].total <= 0) continue;
+    if ((rc = walk_fifo(e, v.levels[l], fifo))) return rc;
+    if (bids) bids[nb] = me_level{v.st.base + l, v.levels[l].total, (uint32_t)fifo.size(), 0};
+    ++nb;
+  }
+  for (int l = v.st.best_ask; l < (int)e->bk.L && na < depth; ++l) {
+    if (v.levels[l].total <= 0) continue;
+    if ((rc = walk_fifo(e, v.levels[l], fifo))) return rc;
+    if (asks) asks[na] = me_level{v.st.base + l, v.levels[l].total, (uint32_t)fifo.size(), 0};
+    ++na;
+  }
+  if (n_bids) *n_bids = nb;
+  if (n_asks) *n_asks = na;
+  return ME_OK;
+}
+
+extern "C" int me_book_dump(me_engine* e, uint32_t symbol, me_book_entry* out, size_t cap, size_t* n) {
+  if (!e) return ME_E_INVALID;
+  if (symbol >= e->bk.S) return e->fail(ME_E_INVALID, "symbol out of range");
+  int rc = me_sync(e);
+  if (rc) return rc;
+  HostLevelView v;
+  if ((rc = load_symbol(e, symbol, v))) return rc;
+  std::vector<std::pair<uint64_t, int32_t>> fifo;
+  size_t k = 0;
+  for (int pass = 0; pass < 2; ++pass) {
+    const bool bid = pass == 0;
+    int l = bid ? v.st.best_bid : v.st.best_ask;
+    for (; bid ? l >= 0 : l < (int)e->bk.L; l += bid ? -1 : 1) {
+      if (v.levels[l].total <= 0) continue;
+      if ((rc = walk_fifo(e, v.levels[l], fifo))) return rc;
+      for (auto& pr : fifo) {
+        if (out && k < cap) {
+          me_book_entry be{};
+          be.seq = pr.first;
+          be.price_q4 = v.st.base + l;
+          be.qty = pr.second;
+          be.side = bid ? ME_SIDE_BUY : ME_SIDE_SELL;
+          out[k] = be;
+        }
+        ++k;
+      }
+    }
+  }
+  if (n) *n = k;
+  return ME_OK;
+}
+
+extern "C" int me_resting_count(me_engine* e, uint64_t* n) {
+  if (!e || !n) return ME_E_INVALID;
+  int rc = me_sync(e);
+  if (rc) return rc;
+  std::vector<SymState> ss(e->bk.S);
+  HIP_TRY(hipMemcpy(ss.data(), e->bk.sym, ss.size() * sizeof(SymState), hipMemcpyDeviceToHost), "D2H symbols");
+  uint64_t t = 0;
+  for (auto& s : ss) t += s.resting;
+  *n = t;
+  return ME_OK;
+}
+
+extern "C" int me_timing_enable(me_engine* e, int enable) {
+  if (!e) return ME_E_INVALID;
+  HIP_TRY(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
+  for (auto& t : e->timed) {
+    (void)hipEventDestroy(t.p0);
+    (void)hipEventDestroy(t.m0);
+    (void)hipEventDestroy(t.m1);
+    (void)hipEventDestroy(t.p1);
+  }
+  e->timed.clear();
+  HIP_TRY(hipMemsetAsync(e->d_fills_acc, 0, 8, e->stream), "reset fill counter");
+  HIP_TRY(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
+  e->timing = enable != 0;
+  return ME_OK;
+}
+
+extern "C" int me_timing_read(me_engine* e, double* match_ms, double* pipeline_ms, uint64_t* launches,
+                              uint64_t* fills, uint64_t* orders) {
+  if (!e) return ME_E_INVALID;
+  HIP_TRY(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
+  double m = 0, p = 0;
+  uint64_t o = 0;
+  for (auto& t : e->timed) {
+    float a = 0, b = 0;
+    HIP_TRY(hipEventElapsedTime(&a, t.m0, t.m1), "hipEventElapsedTime");
+    HIP_TRY(hipEventElapsedTime(&b, t.p0, t.p1), "hipEventElapsedTime");
+    m += a;
+    p += b;
+    o += t.orders;
+  }
+  if (match_ms) *match_ms = m;
+  if (pipeline_ms) *pipeline_ms = p;
+  if (launches) *launches = e->timed.size();
+  unsigned long long f = 0;
+  HIP_TRY(hipMemcpy(&f, e->d_fills_acc, 8, hipMemcpyDeviceToHost), "read fill counter");
+  if (orders) *orders = o;
+  if (fills) *fills = f;
+  return ME_OK;
+}
+
+extern "C" int me_last_error(const me_engine* e, char* buf, size_t cap) {
+  std::string s;
+  if (e) {
+    s = e->err;
+  } else {
+    std::lock_guard<std::mutex> lk(g_err_mu);
+    s = g_create_err;
+  }
+  if (buf && cap) {
+    size_t k = std::min(cap - 1, s.size());
+    memcpy(buf, s.data(), k);
+    buf[k] = 0;
+  }
+  return (int)s.size();
+}

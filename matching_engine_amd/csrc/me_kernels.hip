@@ -1,0 +1,821 @@
+// me_kernels.hip — gfx950 kernels of the batched matching core.
+//
+// One batch (n records, ascending seq) goes through:
+//   1. k_sort_hist / k_sort_scatter  stable LSD counting sort of the records by symbol
+//                                    (1 pass for <= 2047 symbols, 2 passes up to 4M): groups
+//                                    every symbol's records contiguously, seq order kept.
+//   2. k_match                       one wavefront per symbol walks its records in seq order
+//                                    against the HBM-resident book (price-time priority), using
+//                                    ballot + 64-lane prefix scans over levels and FIFO chunks;
+//                                    fills go to a per-wave scratch run.
+//   3. k_tape_compact                exclusive scan of per-record fill counts (batch order) and
+//                                    a coalesced copy scratch -> tape ordered (taker_seq, fill#).
+//
+// Matching semantics are pinned by oracle/oracle_book.cpp; there is no
+// reference matcher (include/engine/model.hpp is empty in julien-mrty/Matching_Engine).
+#include <hip/hip_runtime.h>
+
+#include "me_layout.hpp"
+
+namespace me {
+
+// ------------------------------------------------------------------ wave helpers
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
+
+__device__ __forceinline__ uint32_t rl32(uint32_t v, int k) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, k);
+}
+__device__ __forceinline__ int32_t rli32(int32_t v, int k) { return __builtin_amdgcn_readlane(v, k); }
+__device__ __forceinline__ unsigned long long rl64(unsigned long long v, int k) {
+  uint32_t lo = rl32((uint32_t)v, k), hi = rl32((uint32_t)(v >> 32), k);
+  return ((unsigned long long)hi << 32) | lo;
+}
+__device__ __forceinline__ long long rli64(long long v, int k) {
+  return (long long)rl64((unsigned long long)v, k);
+}
+__device__ __forceinline__ unsigned long long lanemask_lt() {
+  return (1ull << lane_id()) - 1ull;
+}
+// Inclusive 64-lane prefix sum of an int64.
+__device__ __forceinline__ long long wave_incl_scan(long long x) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    long long t = __shfl_up(x, d, 64);
+    if (lane >= d) x += t;
+  }
+  return x;
+}
+// Orders the wave's own global stores before its later loads of the same lines (another lane
+// may read what this lane wrote). Same-CU ordering: no cache maintenance, a compiler barrier.
+__device__ __forceinline__ void wave_mem_order() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
+
+// First index p in [0, n) with keys[p] >= key (keys ascending), by a 64-ary search:
+// every step the wave samples 64 positions, ballots, and narrows the range 64x.
+__device__ uint32_t wave_lower_bound(const uint32_t* keys, uint32_t n, uint32_t key) {
+  const int lane = lane_id();
+  uint32_t lo = 0, hi = n;  // answer in [lo, hi]
+  while (hi - lo > 64) {
+    uint32_t step = (hi - lo + 63) / 64;
+    uint32_t p = lo + (uint32_t)lane * step;
+    bool less = (p < hi) && (keys[p] < key);
+    unsigned long long m = __ballot(less);
+    uint32_t c = (uint32_t)__popcll(m);  // samples < key form a prefix of the lanes
+    if (c == 0) return lo;                // keys[lo] >= key
+    uint32_t nlo = lo + (c - 1) * step + 1;
+    uint32_t nhi = lo + c * step;
+    if (nhi > hi) nhi = hi;
+    lo = nlo;
+    hi = nhi;
+  }
+  uint32_t p = lo + (uint32_t)lane;
+  bool less = (p < hi) && (keys[p] < key);
+  return lo + (uint32_t)__popcll(__ballot(less));
+}
+
+// ------------------------------------------------------------------ grouping sort
+// Pass histogram: per-tile digit counts, stored bin-major [bin][tile].
+__global__ __launch_bounds__(256) void k_sort_hist(const uint32_t* __restrict__ keys_in, uint32_t n,
+                                                   uint32_t clamp_key, int shift, int dbits,
+                                                   uint32_t* __restrict__ hist, uint32_t ntiles,
+                                                   uint32_t* zero_buf, uint32_t zero_words,
+                                                   unsigned long long* scratch_top) {
+  __shared__ uint32_t h[1u << MAX_DIGIT_BITS];
+  const uint32_t nb = 1u << dbits, mask = nb - 1;
+  for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) h[b] = 0;
+  __syncthreads();
+  const uint32_t t0 = blockIdx.x * TILE_SORT;
+  const uint32_t t1 = min(n, t0 + TILE_SORT);
+  for (uint32_t i = t0 + threadIdx.x; i < t1; i += blockDim.x) {
+    uint32_t k = keys_in[i];
+    if (k > clamp_key) k = clamp_key;
+    atomicAdd(&h[(k >> shift) & mask], 1u);
+  }
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) hist[(size_t)b * ntiles + blockIdx.x] = h[b];
+  // Per-batch resets folded into the first kernel of the batch.
+  if (zero_buf) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < zero_words; i += gridDim.x * blockDim.x)
+      zero_buf[i] = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *scratch_top = 0ull;
+  }
+}
+
+// Block-wide exclusive scan of LDS array a[0..cnt) (cnt <= 2048) with 256 threads; returns total.
+__device__ uint32_t block_excl_scan_lds(uint32_t* a, uint32_t cnt, uint32_t* wsum) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint32_t per = (cnt + 255) / 256;
+  uint32_t b0 = tid * per, local = 0;
+  for (uint32_t j = 0; j < per; ++j)
+    if (b0 + j < cnt) local += a[b0 + j];
+  // wave inclusive scan of local
+  uint32_t x = local;
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t t = __shfl_up(x, d, 64);
+    if (lane >= d) x += t;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  uint32_t wpre = 0, total = 0;
+  for (int k = 0; k < 4; ++k) {
+    if (k < w) wpre += wsum[k];
+    total += wsum[k];
+  }
+  uint32_t run = wpre + x - local;
+  for (uint32_t j = 0; j < per; ++j)
+    if (b0 + j < cnt) {
+      uint32_t v = a[b0 + j];
+      a[b0 + j] = run;
+      run += v;
+    }
+  __syncthreads();
+  return total;
+}
+
+// Stable scatter of one tile: dest = (#keys with smaller digit) + (#equal-digit keys in earlier
+// tiles) + (#equal-digit keys earlier in this tile). Each wave owns a quarter of the tile and
+// ranks 64 records at a time with a ballot multisplit (one ballot per digit bit).
+__global__ __launch_bounds__(256) void k_sort_scatter(const uint32_t* __restrict__ keys_in,
+                                                      const uint32_t* __restrict__ idx_in, uint32_t n,
+                                                      uint32_t clamp_key, int shift, int dbits,
+                                                      const uint32_t* __restrict__ hist, uint32_t ntiles,
+                                                      uint32_t* __restrict__ keys_out,
+                                                      uint32_t* __restrict__ idx_out) {
+  __shared__ uint32_t base[1u << MAX_DIGIT_BITS];
+  __shared__ uint32_t wcnt[4][1u << MAX_DIGIT_BITS];
+  __shared__ uint32_t wsum[4];
+  const uint32_t nb = 1u << dbits, mask = nb - 1;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint32_t tile = blockIdx.x;
+  // 1) column sums of the histogram: total per bin and count in earlier tiles
+  for (uint32_t b = tid; b < nb; b += 256) {
+    const uint32_t* row = hist + (size_t)b * ntiles;
+    uint32_t tot = 0, before = 0;
+    for (uint32_t t = 0; t < ntiles; ++t) {
+      uint32_t v = row[t];
+      tot += v;
+      before += (t < tile) ? v : 0u;
+    }
+    base[b] = tot;
+    wcnt[0][b] = before;
+  }
+  __syncthreads();
+  // 2) exclusive scan of bin totals -> bin start; plus earlier-tile count
+  block_excl_scan_lds(base, nb, wsum);
+  for (uint32_t b = tid; b < nb; b += 256) base[b] += wcnt[0][b];
+  __syncthreads();
+  // 3) per-wave histogram of the tile quarters
+  for (uint32_t b = tid; b < nb; b += 256) wcnt[0][b] = wcnt[1][b] = wcnt[2][b] = wcnt[3][b] = 0;
+  __syncthreads();
+  const uint32_t t0 = tile * TILE_SORT, t1 = min(n, t0 + TILE_SORT);
+  const uint32_t q = TILE_SORT / 4;
+  const uint32_t w0 = min(t1, t0 + w * q), w1 = min(t1, w0 + q);
+  for (uint32_t i = w0 + lane; i < w1; i += 64) {
+    uint32_t k = keys_in[i];
+    if (k > clamp_key) k = clamp_key;
+    atomicAdd(&wcnt[w][(k >> shift) & mask], 1u);
+  }
+  __syncthreads();
+  // 4) per-bin prefix over the 4 waves
+  for (uint32_t b = tid; b < nb; b += 256) {
+    uint32_t run = base[b];
+    for (int k = 0; k < 4; ++k) {
+      uint32_t c = wcnt[k][b];
+      wcnt[k][b] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+  // 5) ranked scatter, 64 records per step, in record order
+  for (uint32_t c0 = w0; c0 < w1; c0 += 64) {
+    uint32_t i = c0 + lane;
+    bool v = i < w1;
+    uint32_t k = v ? keys_in[i] : 0u;
+    if (k > clamp_key) k = clamp_key;
+    uint32_t val = v ? (idx_in ? idx_in[i] : i) : 0u;
+    uint32_t d = (k >> shift) & mask;
+    unsigned long long peers = __ballot(v);
+    for (int bit = 0; bit < dbits; ++bit) {
+      unsigned long long bb = __ballot((d >> bit) & 1u);
+      peers &= ((d >> bit) & 1u) ? bb : ~bb;
+    }
+    uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
+    uint32_t cnt = (uint32_t)__popcll(peers);
+    uint32_t start = v ? wcnt[w][d] : 0u;
+    if (v) {
+      keys_out[start + rank] = k;
+      idx_out[start + rank] = val;
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (v && rank == 0) wcnt[w][d] = start + cnt;
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// ------------------------------------------------------------------ matching
+struct WaveCtx {
+  BookDev bk;
+  uint32_t s;          // local symbol
+  uint32_t gs;         // symbol id written in fills
+  long long base;
+  int bb, ba;          // best bid / best ask level
+  uint32_t free_head;
+  int resting_delta;
+  unsigned long long wptr;  // next scratch slot of this wave
+  me_fill* scratch;
+};
+
+__device__ __forceinline__ uint32_t occ_words(const BookDev& bk) { return bk.Lwords; }
+
+// Smallest occupied level >= x, or L.
+__device__ int next_occ(const WaveCtx& c, int x) {
+  const BookDev& bk = c.bk;
+  const int L = (int)bk.L;
+  if (x >= L) return L;
+  if (x < 0) x = 0;
+  const unsigned long long* occ = bk.occ + (size_t)c.s * bk.Lwords;
+  int w = x >> 6;
+  unsigned long long word = occ[w] & (~0ull << (x & 63));
+  if (word) return (w << 6) + __builtin_ctzll(word);
+  const int lane = lane_id();
+  for (int b = w + 1; b < (int)bk.Lwords; b += 64) {
+    int idx = b + lane;
+    unsigned long long v = idx < (int)bk.Lwords ? occ[idx] : 0ull;
+    unsigned long long m = __ballot(v != 0ull);
+    if (m) {
+      int t = __builtin_ctzll(m);
+      unsigned long long wv = rl64(v, t);
+      return ((b + t) << 6) + __builtin_ctzll(wv);
+    }
+  }
+  return L;
+}
+
+// Largest occupied level <= x, or -1.
+__device__ int prev_occ(const WaveCtx& c, int x) {
+  const BookDev& bk = c.bk;
+  if (x < 0) return -1;
+  if (x >= (int)bk.L) x = (int)bk.L - 1;
+  const unsigned long long* occ = bk.occ + (size_t)c.s * bk.Lwords;
+  int w = x >> 6;
+  int r = x & 63;
+  unsigned long long keep = (r == 63) ? ~0ull : ((1ull << (r + 1)) - 1ull);
+  unsigned long long word = occ[w] & keep;
+  if (word) return (w << 6) + 63 - __builtin_clzll(word);
+  const int lane = lane_id();
+  for (int t0 = w - 1; t0 >= 0; t0 -= 64) {
+    int idx = t0 - lane;
+    unsigned long long v = idx >= 0 ? occ[idx] : 0ull;
+    unsigned long long m = __ballot(v != 0ull);
+    if (m) {
+      int t = __builtin_ctzll(m);
+      unsigned long long wv = rl64(v, t);
+      return ((t0 - t) << 6) + 63 - __builtin_clzll(wv);
+    }
+  }
+  return -1;
+}
+
+__device__ __forceinline__ void occ_set(const WaveCtx& c, int lvl) {
+  if (lane_id() == 0) {
+    unsigned long long* p = c.bk.occ + (size_t)c.s * c.bk.Lwords + (lvl >> 6);
+    *p |= (1ull << (lvl & 63));
+  }
+}
+__device__ __forceinline__ void occ_clear(const WaveCtx& c, int lvl) {
+  if (lane_id() == 0) {
+    unsigned long long* p = c.bk.occ + (size_t)c.s * c.bk.Lwords + (lvl >> 6);
+    *p &= ~(1ull << (lvl & 63));
+  }
+}
+
+__device__ __forceinline__ void set_err(const BookDev& bk, uint32_t bits) {
+  if (lane_id() == 0) atomicOr(bk.err, bits);
+}
+
+__device__ __forceinline__ void free_chunk(WaveCtx& c, uint32_t ch) {
+  if (lane_id() == 0) c.bk.chdr[ch].next = c.free_head;
+  c.free_head = ch;
+}
+
+__device__ __forceinline__ uint32_t alloc_chunk(WaveCtx& c) {
+  uint32_t ch;
+  if (c.free_head != NIL) {
+    ch = c.free_head;
+    if (ch >= c.bk.nchunks) {
+      set_err(c.bk, ERR_INCONSISTENT);
+      return NIL;
+    }
+    c.free_head = rl32(c.bk.chdr[ch].next, 0);
+    return ch;
+  }
+  uint32_t got = 0;
+  if (lane_id() == 0) got = atomicAdd(c.bk.chunk_top, 1u);
+  ch = rl32(got, 0);
+  if (ch >= c.bk.nchunks) {
+    set_err(c.bk, ERR_CHUNK_OOM);
+    return NIL;
+  }
+  return ch;
+}
+
+// Append one fill per lane where e holds, in lane order, to the wave's scratch run.
+__device__ __forceinline__ void emit_fills(WaveCtx& c, bool e, unsigned long long taker,
+                                           unsigned long long maker, long long price, int qty) {
+  unsigned long long m = __ballot(e);
+  if (e) {
+    unsigned long long pos = c.wptr + (unsigned long long)__popcll(m & lanemask_lt());
+    me_fill f;
+    f.taker_seq = taker;
+    f.maker_seq = maker;
+    f.price_q4 = price;
+    f.qty = qty;
+    f.symbol = c.gs;
+    c.scratch[pos] = f;
+  }
+  c.wptr += (unsigned long long)__popcll(m);
+}
+
+// Consume `take` (> 0, <= level total) from the FIFO of level `lvl`, oldest first. Emits one
+// fill per maker touched; exhausted chunks go back to the symbol free list. Returns the level's
+// new head chunk (NIL when the level emptied). 32 slots of a chunk are ranked at once with a
+// 64-lane prefix scan of the slot quantities.
+__device__ uint32_t walk_level(WaveCtx& c, int lvl, long long take, uint32_t head, uint32_t tail,
+                               unsigned long long taker) {
+  const int lane = lane_id();
+  const BookDev& bk = c.bk;
+  const long long price = c.base + lvl;
+  long long need = take;
+  uint32_t ch = head;
+  while (need > 0) {
+    if (ch >= bk.nchunks) {  // NIL or corrupt: never index with it
+      set_err(bk, ERR_INCONSISTENT);
+      return NIL;
+    }
+    const uint32_t be = rl32(bk.chdr[ch].begin_end, 0);
+    const uint32_t b = be & 0xFFFFu, e = be >> 16;
+    const uint32_t slot = b + (uint32_t)lane;
+    const bool act = (lane < ME_C) && (slot < e);
+    const size_t g = (size_t)ch * ME_C + slot;
+    const int qv = act ? bk.cqty[g] : 0;
+    const unsigned long long sv = act ? bk.cseq[g] : 0ull;
+    const long long inc = wave_incl_scan((long long)qv);
+    const long long ex = inc - qv;
+    long long f = need - ex;
+    if (f < 0) f = 0;
+    if (f > qv) f = qv;
+    const bool fe = act && f > 0;
+    emit_fills(c, fe, taker, sv, price, (int)f);
+    if (fe) bk.cqty[g] = qv - (int)f;
+    const long long live = rli64(inc, 63);
+    need -= (need < live ? need : live);
+    const unsigned long long alive = __ballot(act && (qv - f) > 0);
+    const uint32_t nb = alive ? b + (uint32_t)__builtin_ctzll(alive) : e;
+    if (nb == e) {  // every written slot of the chunk is consumed
+      if (ch == tail) {
+        free_chunk(c, ch);
+        if (need > 0) set_err(bk, ERR_INCONSISTENT);
+        return NIL;
+      }
+      const uint32_t nxt = rl32(bk.chdr[ch].next, 0);
+      free_chunk(c, ch);
+      ch = nxt;
+    } else {
+      if (lane == 0) bk.chdr[ch].begin_end = nb | (e << 16);
+      if (need > 0) {  // impossible: a live slot remains only once the take is met
+        set_err(bk, ERR_INCONSISTENT);
+        return ch;
+      }
+    }
+  }
+  return ch;
+}
+
+// Sweep the opposite side for a taker. dir = +1 (BUY: asks upward from best_ask) or
+// -1 (SELL: bids downward from best_bid). lim = last level the taker may trade at.
+// Lanes cover 64 consecutive levels; an inclusive scan of their totals gives how far the taker
+// reaches; fully consumed levels are emptied, the last one partially.
+__device__ long long sweep(WaveCtx& c, int dir, int lim, long long want, unsigned long long taker,
+                           uint32_t& nfill) {
+  const int lane = lane_id();
+  const BookDev& bk = c.bk;
+  Level* lv_base = bk.levels + (size_t)c.s * bk.L;
+  long long rem = want;
+  int cur = (dir > 0) ? c.ba : c.bb;
+  bool emptied_best = false;
+  const unsigned long long w_start = c.wptr;
+  while (rem > 0) {
+    if (dir > 0 ? (cur > lim || cur >= (int)bk.L) : (cur < lim || cur < 0)) break;
+    const int lv = cur + dir * lane;
+    const bool valid = (dir > 0) ? (lv <= lim && lv < (int)bk.L) : (lv >= lim && lv >= 0);
+    Level L;
+    L.total = 0;
+    L.head = NIL;
+    L.tail = NIL;
+    if (valid) L = lv_base[lv];
+    const long long tot = L.total;
+    const long long inc = wave_incl_scan(tot);
+    const long long ex = inc - tot;
+    const long long rem0 = rem;
+    unsigned long long tm = __ballot(valid && tot > 0 && ex < rem0);
+    while (tm) {
+      const int t = __builtin_ctzll(tm);
+      tm &= tm - 1;
+      const int lvl = cur + dir * t;
+      const long long ltot = rli64(tot, t);
+      const long long lex = rli64(ex, t);
+      long long take = rem0 - lex;
+      if (take > ltot) take = ltot;
+      const uint32_t head = rl32(L.head, t), tail = rl32(L.tail, t);
+      const uint32_t nh = walk_level(c, lvl, take, head, tail, taker);
+      rem -= take;
+      const long long ntot = ltot - take;
+      if (lane == 0) {
+        Level o;
+        o.total = ntot;
+        o.head = ntot ? nh : NIL;
+        o.tail = ntot ? tail : NIL;
+        lv_base[lvl] = o;
+      }
+      if (ntot == 0) {
+        occ_clear(c, lvl);
+        emptied_best = true;
+      }
+    }
+    if (rem == 0) break;
+    // every valid level of this window is now empty; jump to the next occupied one
+    const int nxt = cur + dir * 64;
+    wave_mem_order();
+    if (dir > 0) {
+      if (nxt > lim) break;
+      cur = next_occ(c, nxt);
+    } else {
+      if (nxt < lim) break;
+      cur = prev_occ(c, nxt);
+    }
+  }
+  if (emptied_best) {
+    wave_mem_order();
+    if (dir > 0)
+      c.ba = next_occ(c, c.ba);
+    else
+      c.bb = prev_occ(c, c.bb);
+  }
+  nfill = (uint32_t)(c.wptr - w_start);
+  return want - rem;
+}
+
+// Append a resting order at the tail of level lvl's FIFO.
+__device__ bool rest_order(WaveCtx& c, int lvl, unsigned long long seq, int qty, bool buy) {
+  const int lane = lane_id();
+  const BookDev& bk = c.bk;
+  Level* lp = bk.levels + (size_t)c.s * bk.L + lvl;
+  wave_mem_order();
+  Level L = *lp;
+  L.total = rli64(L.total, 0);
+  L.head = rl32(L.head, 0);
+  L.tail = rl32(L.tail, 0);
+  uint32_t ch, slot;
+  uint32_t e = ME_C;
+  uint32_t b = 0;
+  if (L.tail != NIL && L.tail >= bk.nchunks) {
+    set_err(bk, ERR_INCONSISTENT);
+    return false;
+  }
+  if (L.tail != NIL) {
+    const uint32_t be = rl32(bk.chdr[L.tail].begin_end, 0);
+    b = be & 0xFFFFu;
+    e = be >> 16;
+  }
+  if (L.tail == NIL || e >= (uint32_t)ME_C) {
+    ch = alloc_chunk(c);
+    if (ch == NIL) return false;
+    slot = 0;
+    if (lane == 0) {
+      ChunkHdr h;
+      h.next = NIL;
+      h.level = (uint32_t)lvl;
+      h.owner = c.s;
+      h.begin_end = 1u << 16;
+      bk.chdr[ch] = h;
+      if (L.tail != NIL) bk.chdr[L.tail].next = ch;
+    }
+    if (L.tail == NIL) L.head = ch;
+    L.tail = ch;
+  } else {
+    ch = L.tail;
+    slot = e;
+    if (lane == 0) bk.chdr[ch].begin_end = b | ((e + 1) << 16);
+  }
+  const size_t g = (size_t)ch * ME_C + slot;
+  const bool was_empty = (L.total == 0);
+  L.total += qty;
+  if (lane == 0) {
+    bk.cseq[g] = seq;
+    bk.cqty[g] = qty;
+    *lp = L;
+    if (seq < bk.max_seq) bk.loc[seq] = (uint32_t)g;
+  }
+  if (was_empty) occ_set(c, lvl);
+  if (buy) {
+    if (lvl > c.bb) c.bb = lvl;
+  } else {
+    if (lvl < c.ba) c.ba = lvl;
+  }
+  c.resting_delta += 1;
+  return true;
+}
+
+// Cancel the live resting order `tgt` of this symbol. Returns the removed qty, 0 if not live.
+__device__ int cancel_order(WaveCtx& c, unsigned long long tgt) {
+  const BookDev& bk = c.bk;
+  const int lane = lane_id();
+  if (tgt == 0ull || tgt >= bk.max_seq) return 0;
+  wave_mem_order();
+  const uint32_t g = rl32(bk.loc[tgt], 0);
+  if (g == NIL) return 0;
+  const uint32_t ch = g / ME_C;
+  if (ch >= bk.nchunks) return 0;
+  const uint32_t owner = rl32(bk.chdr[ch].owner, 0);
+  if (owner != c.s) return 0;  // another symbol's order: never touch its book
+  const int q = rli32(bk.cqty[g], 0);
+  const unsigned long long sq = rl64(bk.cseq[g], 0);
+  if (sq != tgt || q <= 0) return 0;
+  const int lvl = (int)rl32(bk.chdr[ch].level, 0);
+  if (lvl < 0 || lvl >= (int)bk.L) {
+    set_err(bk, ERR_INCONSISTENT);
+    return 0;
+  }
+  Level* lp = bk.levels + (size_t)c.s * bk.L + lvl;
+  Level L = *lp;
+  L.total = rli64(L.total, 0) - q;
+  L.head = rl32(L.head, 0);
+  L.tail = rl32(L.tail, 0);
+  if (lane == 0) bk.cqty[g] = 0;
+  if (L.total == 0 && (L.tail >= bk.nchunks || L.head >= bk.nchunks)) {
+    set_err(bk, ERR_INCONSISTENT);
+    return q;
+  }
+  if (L.total == 0) {
+    // splice the whole (now dead) FIFO onto the free list
+    if (lane == 0) bk.chdr[L.tail].next = c.free_head;
+    c.free_head = L.head;
+    L.head = NIL;
+    L.tail = NIL;
+    if (lane == 0) *lp = L;
+    occ_clear(c, lvl);
+    wave_mem_order();
+    if (lvl == c.bb) c.bb = prev_occ(c, lvl);
+    if (lvl == c.ba) c.ba = next_occ(c, lvl);
+  } else {
+    if (lane == 0) *lp = L;
+  }
+  c.resting_delta -= 1;
+  return q;
+}
+
+__device__ __forceinline__ void write_result(const BatchDev& bt, uint32_t i, int filled, int remaining,
+                                             uint32_t nfill, uint8_t status, uint8_t reason,
+                                             unsigned long long fstart) {
+  if (lane_id() == 0) {
+    me_order_result r;
+    r.filled_qty = filled;
+    r.remaining_qty = remaining;
+    r.fill_count = nfill;
+    r.tape_offset = 0;
+    r.status = status;
+    r.reason = reason;
+    r.pad[0] = 0;
+    r.pad[1] = 0;
+    bt.res[i] = r;
+    bt.fstart[i] = (uint32_t)fstart;
+    if (nfill) atomicAdd(&bt.tile_sum[i / TILE_TAPE], nfill);
+  }
+}
+
+// One wavefront per symbol (4 per workgroup). Block s/4, wave s%4. Symbol S is the reject bin
+// of records whose symbol id is out of range.
+__global__ __launch_bounds__(256) void k_match(BookDev bk, BatchDev bt) {
+  const int lane = lane_id();
+  const uint32_t s = blockIdx.x * 4u + (threadIdx.x >> 6);
+  if (s > bk.S) return;
+  const uint32_t lo = wave_lower_bound(bt.skeys, bt.n, s);
+  const uint32_t hi = wave_lower_bound(bt.skeys, bt.n, s + 1);
+  if (lo >= hi) return;
+  if (s == bk.S) {
+    for (uint32_t j = lo + lane; j < hi; j += 64) {
+      uint32_t i = bt.perm[j];
+      me_order_result r;
+      r.filled_qty = 0;
+      r.remaining_qty = 0;
+      r.fill_count = 0;
+      r.tape_offset = 0;
+      r.status = ME_ST_REJECTED;
+      r.reason = ME_RJ_BAD_SYMBOL;
+      r.pad[0] = r.pad[1] = 0;
+      bt.res[i] = r;
+      bt.fstart[i] = 0;
+    }
+    return;
+  }
+  WaveCtx c;
+  c.bk = bk;
+  c.s = s;
+  c.gs = bk.gsym ? bk.gsym[s] : s;
+  const SymState st = bk.sym[s];
+  c.base = rli64(st.base, 0);
+  c.bb = rli32(st.best_bid, 0);
+  c.ba = rli32(st.best_ask, 0);
+  c.free_head = rl32(st.free_head, 0);
+  c.resting_delta = 0;
+  c.scratch = bt.scratch;
+  // scratch run of this wave: fills <= resting makers + 2 * records
+  const unsigned long long need = (unsigned long long)rl32(st.resting, 0) + 2ull * (hi - lo);
+  unsigned long long w0 = 0;
+  if (lane == 0) w0 = atomicAdd(bt.scratch_top, need);
+  w0 = rl64(w0, 0);
+  if (w0 + need > bt.scratch_cap) {
+    set_err(bk, ERR_SCRATCH_OOM);
+    return;
+  }
+  c.wptr = w0;
+  const long long L = (long long)bk.L;
+
+  for (uint32_t blk = lo; blk < hi; blk += 64) {
+    const uint32_t j = blk + (uint32_t)lane;
+    const bool v = j < hi;
+    const uint32_t oi = v ? bt.perm[j] : 0u;
+    const unsigned long long oseq = v ? bt.seq[oi] : 0ull;
+    const long long opx = v ? bt.px[oi] : 0ll;
+    const int oq = v ? bt.qty[oi] : 0;
+    const uint32_t ok = v ? (uint32_t)bt.kind[oi] : 0u;
+    const uint32_t cnt = min(64u, hi - blk);
+    for (uint32_t k = 0; k < cnt; ++k) {
+      const uint32_t i = rl32(oi, (int)k);
+      const unsigned long long seq = rl64(oseq, (int)k);
+      const long long px = rli64(opx, (int)k);
+      const int q = rli32(oq, (int)k);
+      const uint32_t kind = rl32(ok, (int)k);
+      const uint32_t side = kind & 3u;
+      const bool market = (kind >> 2) & 1u;
+      const bool cancel = (kind >> 3) & 1u;
+      const unsigned long long fstart = c.wptr;
+      if (cancel) {
+        const int got = cancel_order(c, (unsigned long long)px);
+        if (got > 0)
+          write_result(bt, i, 0, got, 0, ME_ST_CANCELED, ME_RJ_NONE, fstart);
+        else
+          write_result(bt, i, 0, 0, 0, ME_ST_REJECTED, ME_RJ_UNKNOWN_ORDER, fstart);
+        continue;
+      }
+      if (q <= 0) {
+        write_result(bt, i, 0, 0, 0, ME_ST_REJECTED, ME_RJ_BAD_QTY, fstart);
+        continue;
+      }
+      if (side != ME_SIDE_BUY && side != ME_SIDE_SELL) {
+        write_result(bt, i, 0, q, 0, ME_ST_REJECTED, ME_RJ_BAD_SIDE, fstart);
+        continue;
+      }
+      int li = 0;
+      if (!market) {
+        if (px < c.base || (unsigned long long)px - (unsigned long long)c.base >= (unsigned long long)L) {
+          write_result(bt, i, 0, q, 0, ME_ST_REJECTED, ME_RJ_OUT_OF_WINDOW, fstart);
+          continue;
+        }
+        li = (int)(px - c.base);
+      }
+      if (seq == 0ull || seq >= bk.max_seq) {
+        write_result(bt, i, 0, q, 0, ME_ST_REJECTED, ME_RJ_BAD_SEQ, fstart);
+        continue;
+      }
+      const bool buy = side == ME_SIDE_BUY;
+      const int lim = market ? (buy ? (int)L - 1 : 0) : li;
+      uint32_t nfill = 0;
+      const long long got = sweep(c, buy ? 1 : -1, lim, (long long)q, seq, nfill);
+      const int filled = (int)got;
+      const int rem = q - filled;
+      uint8_t st;
+      if (market) {
+        st = rem == 0 ? ME_ST_FILLED : ME_ST_CANCELED;
+      } else {
+        if (rem > 0) {
+          if (!rest_order(c, li, seq, rem, buy)) return;  // chunk pool exhausted: batch fails
+        }
+        st = rem == 0 ? ME_ST_FILLED : (filled > 0 ? ME_ST_PARTIALLY_FILLED : ME_ST_NEW);
+      }
+      write_result(bt, i, filled, rem, nfill, st, ME_RJ_NONE, fstart);
+    }
+  }
+  if (lane == 0) {
+    SymState o;
+    o.base = c.base;
+    o.best_bid = c.bb;
+    o.best_ask = c.ba;
+    o.free_head = c.free_head;
+    o.resting = (uint32_t)((int)st.resting + c.resting_delta);
+    o.pad[0] = o.pad[1] = 0;
+    bk.sym[s] = o;
+  }
+}
+
+// ------------------------------------------------------------------ tape compaction
+// Block b owns records [b*1024, +1024). Tape offset of record i = sum of fills of records < i
+// (batch order == seq order). Fills are then copied scratch -> tape with consecutive threads
+// writing consecutive 32-B records (each thread finds its record by binary search in LDS).
+__global__ __launch_bounds__(256) void k_tape_compact(const uint32_t* __restrict__ tile_sum, uint32_t ntiles,
+                                                      me_order_result* res, const uint32_t* __restrict__ fstart,
+                                                      uint32_t n, const me_fill* __restrict__ scratch,
+                                                      me_fill* __restrict__ tape, unsigned long long tape_cap,
+                                                      unsigned long long* tape_count, unsigned long long* fills_acc,
+                                                      uint32_t* err) {
+  __shared__ uint32_t off[TILE_TAPE + 1];
+  __shared__ unsigned long long red[4];
+  __shared__ uint32_t wsum[4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint32_t b = blockIdx.x;
+  unsigned long long acc = 0;
+  for (uint32_t t = tid; t < b; t += 256) acc += tile_sum[t];
+  for (int d = 32; d >= 1; d >>= 1) acc += __shfl_xor(acc, d, 64);
+  if (lane == 0) red[w] = acc;
+  const uint32_t r0 = b * TILE_TAPE;
+  const uint32_t cnt = min((uint32_t)TILE_TAPE, n - r0);
+  for (uint32_t k = tid; k < cnt; k += 256) off[k] = res[r0 + k].fill_count;
+  __syncthreads();
+  const unsigned long long base = red[0] + red[1] + red[2] + red[3];
+  const uint32_t total = block_excl_scan_lds(off, cnt, wsum);
+  if (tid == 0) off[cnt] = total;
+  for (uint32_t k = tid; k < cnt; k += 256) res[r0 + k].tape_offset = (uint32_t)(base + off[k]);
+  __syncthreads();
+  if (base + total > tape_cap) {
+    if (tid == 0) atomicOr(err, ERR_SCRATCH_OOM);
+    return;
+  }
+  for (uint32_t f = tid; f < total; f += 256) {
+    // last k with off[k] <= f
+    uint32_t lo = 0, hi = cnt;  // off[lo] <= f < off[hi]
+    while (hi - lo > 1) {
+      uint32_t mid = (lo + hi) >> 1;
+      if (off[mid] <= f)
+        lo = mid;
+      else
+        hi = mid;
+    }
+    const uint32_t src = fstart[r0 + lo] + (f - off[lo]);
+    tape[base + f] = scratch[src];
+  }
+  if (b == gridDim.x - 1 && tid == 0) {
+    *tape_count = base + total;
+    atomicAdd(fills_acc, base + total);
+  }
+}
+
+__global__ void k_init_levels(Level* lv, size_t count) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < count; i += (size_t)gridDim.x * blockDim.x) {
+    Level o;
+    o.total = 0;
+    o.head = NIL;
+    o.tail = NIL;
+    lv[i] = o;
+  }
+}
+
+}  // namespace me
+
+// ------------------------------------------------------------------ launch wrappers (host)
+namespace me {
+
+hipError_t launch_sort_pass(hipStream_t st, const uint32_t* keys_in, const uint32_t* idx_in, uint32_t n,
+                            uint32_t clamp_key, int shift, int dbits, uint32_t* hist, uint32_t* keys_out,
+                            uint32_t* idx_out, uint32_t* zero_buf, uint32_t zero_words,
+                            unsigned long long* scratch_top) {
+  const uint32_t ntiles = (n + TILE_SORT - 1) / TILE_SORT;
+  hipLaunchKernelGGL(k_sort_hist, dim3(ntiles), dim3(256), 0, st, keys_in, n, clamp_key, shift, dbits, hist,
+                     ntiles, zero_buf, zero_words, scratch_top);
+  hipLaunchKernelGGL(k_sort_scatter, dim3(ntiles), dim3(256), 0, st, keys_in, idx_in, n, clamp_key, shift,
+                     dbits, hist, ntiles, keys_out, idx_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_match(hipStream_t st, const BookDev& bk, const BatchDev& bt) {
+  const uint32_t waves = bk.S + 1;
+  hipLaunchKernelGGL(k_match, dim3((waves + 3) / 4), dim3(256), 0, st, bk, bt);
+  return hipGetLastError();
+}
+
+hipError_t launch_tape(hipStream_t st, const BatchDev& bt, me_fill* tape, unsigned long long tape_cap,
+                       unsigned long long* tape_count, unsigned long long* fills_acc, uint32_t* err) {
+  const uint32_t ntiles = (bt.n + TILE_TAPE - 1) / TILE_TAPE;
+  hipLaunchKernelGGL(k_tape_compact, dim3(ntiles), dim3(256), 0, st, bt.tile_sum, ntiles, bt.res, bt.fstart,
+                     bt.n, bt.scratch, tape, tape_cap, tape_count, fills_acc, err);
+  return hipGetLastError();
+}
+
+hipError_t launch_init_levels(hipStream_t st, Level* levels, size_t count) {
+  size_t blocks = (count + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  if (blocks == 0) blocks = 1;
+  hipLaunchKernelGGL(k_init_levels, dim3((uint32_t)blocks), dim3(256), 0, st, levels, count);
+  return hipGetLastError();
+}
+
+}  // namespace me

@@ -1,0 +1,92 @@
+// me_layout.hpp — HBM layout of the resident books and of one in-flight batch.
+//
+// Shared by the gfx950 kernels (me_kernels.hip) and the host engine (me_engine.cpp).
+// Everything is plain-old-data; the host allocates, the kernels own the contents.
+//
+// Book of one shard:
+//   levels [S][L]   16 B {total, head chunk, tail chunk}: the fixed-depth price ladder. Bids and
+//                   asks share one ladder per symbol: after every order best_bid < best_ask, so
+//                   a level's side is implied by its position.
+//   occ    [S][L/64] occupancy bitmap of the ladder (bit set <=> total > 0).
+//   sym    [S]      32 B per-symbol scalars (window base, best bid/ask level, chunk free list).
+//   chunks [NC]     FIFO storage: a level's queue is a linked list of chunks of ME_C slots
+//                   {seq u64, qty i32} (SoA: cseq / cqty); a wave reads one chunk per load.
+//   loc    [max_seq] seq -> global slot (chunk * ME_C + slot) for cancels.
+#pragma once
+#include <stdint.h>
+
+#include "me_engine.h"
+
+namespace me {
+
+constexpr int ME_C = 32;                 // slots per chunk (one wave-load of qty + seq)
+constexpr uint32_t NIL = 0xFFFFFFFFu;
+constexpr int TILE_SORT = 4096;          // records per workgroup in the grouping sort
+constexpr int TILE_TAPE = 1024;          // records per workgroup in the tape compaction
+constexpr int MAX_DIGIT_BITS = 11;       // radix digit width (LDS histogram of 2048 bins)
+
+// Sticky error bits (BookDev::err).
+enum : uint32_t {
+  ERR_CHUNK_OOM = 1u,
+  ERR_SCRATCH_OOM = 2u,
+  ERR_INCONSISTENT = 4u,
+};
+
+struct alignas(16) Level {
+  long long total;   // live quantity on the level (0 <=> empty, head == tail == NIL)
+  uint32_t head;     // first chunk of the FIFO
+  uint32_t tail;     // last chunk (appends go here)
+};
+
+struct alignas(16) ChunkHdr {
+  uint32_t next;       // next chunk of the level FIFO, or of the symbol free list
+  uint32_t level;      // level index the chunk belongs to
+  uint32_t owner;      // symbol that allocated it (chunks never migrate between symbols)
+  uint32_t begin_end;  // begin (first possibly-live slot) | end (slots written) << 16
+};
+
+struct alignas(32) SymState {
+  long long base;      // price_q4 of level 0
+  int best_bid;        // highest occupied bid level, -1 if none
+  int best_ask;        // lowest occupied ask level, L if none
+  uint32_t free_head;  // chunk free list of this symbol
+  uint32_t resting;    // live resting orders
+  uint32_t pad[2];
+};
+
+struct BookDev {
+  Level* levels;
+  unsigned long long* occ;
+  SymState* sym;
+  ChunkHdr* chdr;
+  unsigned long long* cseq;
+  int* cqty;
+  uint32_t* loc;
+  uint32_t* chunk_top;
+  uint32_t* err;
+  const uint32_t* gsym;  // [S] id written into me_fill.symbol
+  unsigned long long max_seq;
+  uint32_t nchunks;
+  uint32_t S;
+  uint32_t L;
+  uint32_t Lwords;
+};
+
+struct BatchDev {
+  const uint64_t* seq;
+  const int64_t* px;
+  const int32_t* qty;
+  const uint32_t* sym;
+  const uint8_t* kind;
+  uint32_t n;
+  const uint32_t* skeys;    // symbol of each grouped position (ascending)
+  const uint32_t* perm;     // grouped position -> batch index
+  me_order_result* res;     // [n], batch order
+  uint32_t* fstart;         // [n] first fill of the record in scratch
+  uint32_t* tile_sum;       // [ceil(n / TILE_TAPE)] fills per tape tile
+  me_fill* scratch;
+  unsigned long long scratch_cap;
+  unsigned long long* scratch_top;
+};
+
+}  // namespace me

@@ -1,0 +1,319 @@
+"""Host-side mirror of the batched matching core (C-ABI include/me_engine.h).
+
+``Engine`` is one shard (one GPU): HBM-resident books for ``num_symbols`` local symbols, driven
+batch by batch. Every call goes through libme_engine.so; nothing here computes a match.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _abi
+from ._abi import BOOK_ENTRY_DTYPE, FILL_DTYPE, LEVEL_DTYPE, RESULT_DTYPE, MeConfig, MeGenParams, MeOrderSoa, ptr
+
+
+class EngineError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"me error {code}: {msg}")
+        self.code = code
+
+
+def _check(lib, handle, rc: int) -> None:
+    if rc != _abi.ME_OK:
+        buf = C.create_string_buffer(1024)
+        lib.me_last_error(handle, buf, 1024)
+        raise EngineError(rc, buf.value.decode(errors="replace"))
+
+
+def normalize_to_q4(price: int, scale: int) -> int:
+    """include/domain/price.hpp:15-29 through the product library; raises like the reference."""
+    lib = _abi.load()
+    out = C.c_int64(0)
+    rc = lib.me_normalize_to_q4(int(price), int(scale), C.byref(out))
+    if rc == 1:
+        raise ValueError("scale out of range")
+    if rc == 2:
+        raise OverflowError("overflow")
+    if rc == 3:
+        raise OverflowError("underflow")
+    return out.value
+
+
+@dataclass
+class Batch:
+    """One batch in SoA form (host numpy arrays), ascending seq."""
+
+    seq: np.ndarray
+    price_q4: np.ndarray
+    qty: np.ndarray
+    symbol: np.ndarray
+    kind: np.ndarray
+
+    def __post_init__(self):
+        self.seq = np.ascontiguousarray(self.seq, dtype=np.uint64)
+        self.price_q4 = np.ascontiguousarray(self.price_q4, dtype=np.int64)
+        self.qty = np.ascontiguousarray(self.qty, dtype=np.int32)
+        self.symbol = np.ascontiguousarray(self.symbol, dtype=np.uint32)
+        self.kind = np.ascontiguousarray(self.kind, dtype=np.uint8)
+        n = len(self.seq)
+        assert all(len(a) == n for a in (self.price_q4, self.qty, self.symbol, self.kind))
+
+    def __len__(self) -> int:
+        return len(self.seq)
+
+    def take(self, idx) -> "Batch":
+        return Batch(self.seq[idx], self.price_q4[idx], self.qty[idx], self.symbol[idx], self.kind[idx])
+
+    def soa(self) -> MeOrderSoa:
+        return MeOrderSoa(ptr(self.seq), ptr(self.price_q4), ptr(self.qty), ptr(self.symbol), ptr(self.kind))
+
+
+class DeviceBatch:
+    """A batch copied once into HBM (me_device_alloc), for device-resident submission."""
+
+    def __init__(self, engine: "Engine", b: Batch):
+        self.engine = engine
+        self.n = len(b)
+        self.ptrs = []
+        for a in (b.seq, b.price_q4, b.qty, b.symbol, b.kind):
+            p = C.c_void_p()
+            _check(engine.lib, engine.h, engine.lib.me_device_alloc(engine.h, max(a.nbytes, 1), C.byref(p)))
+            if a.nbytes:
+                _check(engine.lib, engine.h, engine.lib.me_memcpy_h2d(engine.h, p, ptr(a), a.nbytes))
+            self.ptrs.append(p.value)
+        self._soa = MeOrderSoa(*self.ptrs)
+
+    def free(self):
+        for p in self.ptrs:
+            self.engine.lib.me_device_free(self.engine.h, p)
+        self.ptrs = []
+
+
+class Engine:
+    """One shard of HBM-resident books (include/me_engine.h me_create ... me_destroy)."""
+
+    def __init__(
+        self,
+        num_symbols: int,
+        levels: int,
+        base_prices,
+        max_batch: int,
+        max_resting: int,
+        max_seq: int,
+        max_chunks: int = 0,
+        device: int = 0,
+        symbol_ids=None,
+    ):
+        self.lib = _abi.load()
+        self.num_symbols = int(num_symbols)
+        self.levels = int(levels)
+        self._base = np.ascontiguousarray(base_prices, dtype=np.int64)
+        assert len(self._base) == num_symbols
+        self._ids = None if symbol_ids is None else np.ascontiguousarray(symbol_ids, dtype=np.uint32)
+        cfg = MeConfig(
+            device,
+            num_symbols,
+            levels,
+            max_batch,
+            max_resting,
+            max_chunks,
+            max_seq,
+            self._base.ctypes.data_as(C.POINTER(C.c_int64)),
+            None if self._ids is None else self._ids.ctypes.data_as(C.POINTER(C.c_uint32)),
+        )
+        self.max_batch = int(max_batch)
+        h = self.lib.me_create(C.byref(cfg))
+        if not h:
+            buf = C.create_string_buffer(1024)
+            self.lib.me_last_error(None, buf, 1024)
+            raise EngineError(_abi.ME_E_HIP, buf.value.decode(errors="replace"))
+        self.h = h
+
+    # -- lifecycle
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.me_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- batches
+    def fill_bound(self, n: int) -> int:
+        return int(self.lib.me_fill_bound(self.h, n))
+
+    def submit_batch(self, b: Batch, want_fills: bool = True):
+        """Host batch -> (results[n] RESULT_DTYPE, fills[k] FILL_DTYPE), synchronous."""
+        n = len(b)
+        res = np.zeros(n, dtype=RESULT_DTYPE)
+        cap = self.fill_bound(n) if want_fills else 0
+        fills = np.zeros(cap, dtype=FILL_DTYPE) if want_fills else None
+        nf = C.c_size_t(0)
+        soa = b.soa()
+        rc = self.lib.me_submit_batch(
+            self.h, C.byref(soa), n, ptr(fills) if want_fills else None, cap, C.byref(nf), ptr(res)
+        )
+        _check(self.lib, self.h, rc)
+        return res, (fills[: nf.value].copy() if want_fills else nf.value)
+
+    def upload(self, b: Batch) -> DeviceBatch:
+        return DeviceBatch(self, b)
+
+    def submit_device(self, db: DeviceBatch):
+        _check(self.lib, self.h, self.lib.me_submit_batch_device(self.h, C.byref(db._soa), db.n))
+
+    def sync(self):
+        _check(self.lib, self.h, self.lib.me_sync(self.h))
+
+    def fetch_outputs(self, n: int):
+        res = np.zeros(n, dtype=RESULT_DTYPE)
+        nf = C.c_size_t(0)
+        _check(self.lib, self.h, self.lib.me_fetch_outputs(self.h, None, 0, C.byref(nf), ptr(res), n))
+        fills = np.zeros(nf.value, dtype=FILL_DTYPE)
+        _check(self.lib, self.h, self.lib.me_fetch_outputs(self.h, ptr(fills), nf.value, C.byref(nf), None, 0))
+        return res, fills
+
+    def set_stream(self, stream_handle: int | None):
+        _check(self.lib, self.h, self.lib.me_set_stream(self.h, stream_handle))
+
+    # -- book inspection
+    def snapshot(self, symbol: int, depth: int = 10):
+        bids = np.zeros(depth, dtype=LEVEL_DTYPE)
+        asks = np.zeros(depth, dtype=LEVEL_DTYPE)
+        nb, na = C.c_size_t(0), C.c_size_t(0)
+        rc = self.lib.me_book_snapshot(self.h, symbol, ptr(bids), ptr(asks), depth, C.byref(nb), C.byref(na))
+        _check(self.lib, self.h, rc)
+        return bids[: nb.value], asks[: na.value]
+
+    def dump(self, symbol: int) -> np.ndarray:
+        n = C.c_size_t(0)
+        _check(self.lib, self.h, self.lib.me_book_dump(self.h, symbol, None, 0, C.byref(n)))
+        out = np.zeros(n.value, dtype=BOOK_ENTRY_DTYPE)
+        _check(self.lib, self.h, self.lib.me_book_dump(self.h, symbol, ptr(out), n.value, C.byref(n)))
+        return out
+
+    def resting_count(self) -> int:
+        v = C.c_uint64(0)
+        _check(self.lib, self.h, self.lib.me_resting_count(self.h, C.byref(v)))
+        return v.value
+
+    # -- timing
+    def timing_enable(self, on: bool = True):
+        _check(self.lib, self.h, self.lib.me_timing_enable(self.h, 1 if on else 0))
+
+    def timing_read(self):
+        m, p = C.c_double(0), C.c_double(0)
+        k, f, o = C.c_uint64(0), C.c_uint64(0), C.c_uint64(0)
+        rc = self.lib.me_timing_read(self.h, C.byref(m), C.byref(p), C.byref(k), C.byref(f), C.byref(o))
+        _check(self.lib, self.h, rc)
+        return {"match_ms": m.value, "pipeline_ms": p.value, "launches": k.value, "fills": f.value,
+                "orders": o.value}
+
+
+# ---------------------------------------------------------------------------------------------
+# Synthetic streams (SURVEY.md §8(d) configurations)
+@dataclass
+class StreamConfig:
+    config: int
+    seed: int
+    num_symbols: int
+    levels: int
+    spread_ticks: int = 32
+    max_qty: int = 100
+    market_pct: int = 20
+    cancel_pct: int = 0
+    zipf_s: float = 0.0
+    market_qty_mult: int = 0
+    batch: int = 65536
+    batches: int = 1024
+    seed_levels_per_side: int = 0
+
+
+def preset(config: int, **over) -> StreamConfig:
+    """The five benchmark configurations of SURVEY.md §8(d) (override any field for small tests)."""
+    base = {
+        1: dict(config=1, seed=1, num_symbols=1, levels=128, batch=62500, batches=16),  # 1M orders on "SYM"
+        2: dict(config=2, seed=2, num_symbols=1024, levels=128, batch=65536, batches=1024),
+        3: dict(config=3, seed=3, num_symbols=100_000, levels=128, batch=1 << 20, batches=128),
+        4: dict(config=4, seed=4, num_symbols=100_000, levels=32768, spread_ticks=5000, zipf_s=1.1,
+                seed_levels_per_side=10_000, batch=65536, batches=256),
+        5: dict(config=5, seed=5, num_symbols=1024, levels=128, cancel_pct=60, market_pct=15,
+                market_qty_mult=20, batch=65536, batches=1024),
+    }[config]
+    base.update(over)
+    return StreamConfig(**base)
+
+
+class Stream:
+    """Deterministic global order stream (me_gen_*), seq = 1, 2, ... across batches."""
+
+    def __init__(self, sc: StreamConfig):
+        self.lib = _abi.load()
+        self.sc = sc
+        p = MeGenParams(sc.config, sc.seed, sc.num_symbols, sc.levels, sc.spread_ticks, sc.max_qty,
+                        sc.market_pct, sc.cancel_pct, float(sc.zipf_s), sc.market_qty_mult)
+        self.g = self.lib.me_gen_create(C.byref(p))
+        if not self.g:
+            raise ValueError(f"invalid stream config {sc}")
+
+    def close(self):
+        if self.g:
+            self.lib.me_gen_destroy(self.g)
+            self.g = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def base_prices(self) -> np.ndarray:
+        out = np.zeros(self.sc.num_symbols, dtype=np.int64)
+        self.lib.me_gen_base_prices(self.g, ptr(out))
+        return out
+
+    def next(self, n: int) -> Batch:
+        a = [np.zeros(n, dtype=t) for t in (np.uint64, np.int64, np.int32, np.uint32, np.uint8)]
+        self.lib.me_gen_next(self.g, n, *[ptr(x) for x in a])
+        return Batch(*a)
+
+    def seed_books(self, symbols, per_side: int) -> Batch:
+        """Config 4 pre-seed: per_side resting orders per side for every symbol in `symbols`."""
+        parts = []
+        for s in symbols:
+            m = 2 * per_side
+            a = [np.zeros(m, dtype=t) for t in (np.uint64, np.int64, np.int32, np.uint8)]
+            rc = self.lib.me_gen_seed_book(self.g, int(s), per_side, *[ptr(x) for x in a])
+            if rc:
+                raise ValueError("seed_book failed")
+            parts.append(Batch(a[0], a[1], a[2], np.full(m, s, dtype=np.uint32), a[3]))
+        return Batch(*[np.concatenate([getattr(p, f) for p in parts]) for f in
+                       ("seq", "price_q4", "qty", "symbol", "kind")])
+
+
+def shard_of(symbol: int, shards: int) -> int:
+    return int(_abi.load().me_shard_of(symbol, shards))
+
+
+def shard_table(num_symbols: int, shards: int):
+    """global symbol -> (shard, local id); per shard the global ids in local-id order."""
+    lib = _abi.load()
+    shard = np.array([lib.me_shard_of(s, shards) for s in range(num_symbols)], dtype=np.uint32)
+    local = np.zeros(num_symbols, dtype=np.uint32)
+    members = []
+    for r in range(shards):
+        ids = np.nonzero(shard == r)[0].astype(np.uint32)
+        local[ids] = np.arange(len(ids), dtype=np.uint32)
+        members.append(ids)
+    return shard, local, members

@@ -1,0 +1,212 @@
+"""GPU parity: the HIP engine (through the C-ABI) against the CPU oracle and the committed golden
+fixtures — bit-exact per-record results, trade tapes and resting books. Needs an MI355X."""
+import numpy as np
+import pytest
+
+from tests._parity import (assert_books_equal, assert_fills_equal, assert_results_equal, load_fixture,
+                           run_both)
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def me(built):
+    import matching_engine_amd
+
+    return matching_engine_amd
+
+
+@pytest.fixture(scope="module")
+def orc(built):
+    from oracle import oracle
+
+    return oracle
+
+
+def engine_for(me, S, L, base, max_batch, max_resting, max_seq=1 << 22, **kw):
+    return me.Engine(S, L, base, max_batch=max_batch, max_resting=max_resting, max_seq=max_seq, **kw)
+
+
+# ---------------------------------------------------------------- committed fixtures
+@pytest.mark.parametrize("cid", [1, 2, 3, 4, 5])
+def test_golden_fixture_on_gpu(me, cid):
+    meta, batches, res, fills, book = load_fixture(cid)
+    mb = max(len(b) for b in batches)
+    with engine_for(me, meta["num_symbols"], meta["levels"], meta["base"], mb, 1 << 18, meta["max_seq"]) as eng:
+        for k, b in enumerate(batches):
+            r, f = eng.submit_batch(b)
+            assert_results_equal(r, res[k], f"fixture c{cid} b{k}")
+            assert_fills_equal(f, fills[k], f"fixture c{cid} b{k}")
+        dumps = np.concatenate([eng.dump(s) for s in range(meta["num_symbols"])])
+        assert np.array_equal(dumps, book), f"fixture c{cid}: resting book differs"
+
+
+# ---------------------------------------------------------------- live differential runs
+def _stream_run(me, orc, cfg, nbatches, seed_per_side=0, max_seq=1 << 26, book_symbols=None, **over):
+    sc = me.preset(cfg, **over)
+    st = me.Stream(sc)
+    base = st.base_prices()
+    batches = []
+    if seed_per_side:
+        batches.append(st.seed_books(range(sc.num_symbols), seed_per_side))
+    batches += [st.next(sc.batch) for _ in range(nbatches)]
+    mb = max(len(b) for b in batches)
+    total = sum(len(b) for b in batches)
+    ob = orc.OracleBook(sc.num_symbols, sc.levels, base, max_seq)
+    with engine_for(me, sc.num_symbols, sc.levels, base, mb, total + 1024, max_seq) as eng:
+        nf = run_both(eng, ob, batches, book_symbols=book_symbols, ctx=f"config {cfg}")
+    return nf, total
+
+
+def test_config1_single_symbol(me, orc):
+    nf, total = _stream_run(me, orc, 1, 4, batch=62500)
+    assert nf > 0.5 * total
+
+
+def test_config2_uniform_1024(me, orc):
+    nf, total = _stream_run(me, orc, 2, 8)
+    assert nf > 0.5 * total
+
+
+def test_config3_100k_symbols_two_pass_sort(me, orc):
+    nf, total = _stream_run(me, orc, 3, 2, batch=1 << 19, book_symbols=range(0, 100_000, 97))
+    assert nf > 0
+
+
+def test_config4_zipf_deep_books(me, orc):
+    nf, total = _stream_run(me, orc, 4, 3, seed_per_side=2000, num_symbols=200, levels=8192, spread_ticks=2500)
+    assert nf > 0
+
+
+def test_config5_cancel_heavy_sweeps(me, orc):
+    nf, total = _stream_run(me, orc, 5, 8)
+    assert nf > 0
+
+
+# ---------------------------------------------------------------- edge cases
+def _rows(me, rows, start_seq=1):
+    n = len(rows)
+    return me.Batch(np.arange(start_seq, start_seq + n, dtype=np.uint64), [r[4] for r in rows],
+                    [r[5] for r in rows], [r[0] for r in rows], [me.kind(r[1], r[2], r[3]) for r in rows])
+
+
+def test_edge_semantics_and_rejects(me, orc):
+    B, S, L, M = me.SIDE_BUY, me.SIDE_SELL, me.TYPE_LIMIT, me.TYPE_MARKET
+    rows = [
+        (0, B, L, 0, 1000, 5), (0, B, L, 0, 999, 5), (0, B, L, 0, 1128, 5), (1, 0, L, 0, 5001, 5),
+        (0, B, L, 0, 1001, 0), (7, B, L, 0, 1001, 1), (1, S, L, 1, 1, 0), (0, S, L, 1, 1, 0), (0, S, L, 1, 1, 0),
+        (0, S, L, 1, 12, 0), (0, B, M, 0, 0, 3), (1, 3, M, 0, 0, 3), (0, S, L, 1, 1 << 40, 0),
+        (1, S, L, 0, 5127, 2), (1, B, M, 0, 123, 5), (1, S, L, 0, 5000, 7), (1, B, L, 0, 5127, 9),
+    ]
+    b = _rows(me, rows)
+    ob = orc.OracleBook(2, 128, [1000, 5000], 1 << 10)
+    with engine_for(me, 2, 128, [1000, 5000], 64, 256, 1 << 10) as eng:
+        run_both(eng, ob, [b], ctx="edge")
+        run_both(eng, ob, [_rows(me, [(0, B, L, 0, 1000, 1)], start_seq=1 << 10)], ctx="bad seq")
+        r, f = eng.submit_batch(_rows(me, [], start_seq=2000))
+        assert len(r) == 0 and len(f) == 0
+
+
+def test_edge_deep_sweep_multi_window_multi_chunk(me, orc):
+    """Sweeps crossing >64 levels (several ballot windows) and levels holding >32 orders (several
+    FIFO chunks), cancels inside chunks, then chunk reuse from the free list."""
+    B, S, L, M = me.SIDE_BUY, me.SIDE_SELL, me.TYPE_LIMIT, me.TYPE_MARKET
+    rows = []
+    for lvl in range(300):                     # 300 ask levels, 1..3 orders each
+        for k in range(1 + lvl % 3):
+            rows.append((0, S, L, 0, 10000 + 2 * lvl, 1 + (lvl * 7 + k) % 50))
+    for k in range(100):                       # one level with 100 orders (4 chunks)
+        rows.append((0, B, L, 0, 9000, 1 + k % 9))
+    b1 = _rows(me, rows)
+    seq = len(rows) + 1
+    cancels = [(0, S, L, 1, s, 0) for s in range(len(rows) - 99, len(rows) + 1, 3)]  # every 3rd bid
+    b2 = _rows(me, cancels, start_seq=seq)
+    seq += len(cancels)
+    sweeps = [(0, B, M, 0, 0, 5000), (0, S, M, 0, 0, 120), (0, B, L, 0, 10500, 900), (0, S, L, 0, 9000, 50)]
+    b3 = _rows(me, sweeps, start_seq=seq)
+    seq += len(sweeps)
+    refill = _rows(me, [(0, B, L, 0, 9000 + (k % 5), 3) for k in range(200)], start_seq=seq)
+    base = [8000]
+    ob = orc.OracleBook(1, 4096, base, 1 << 20)
+    with engine_for(me, 1, 4096, base, 1024, 4096, 1 << 20) as eng:
+        run_both(eng, ob, [b1, b2, b3, refill], ctx="deep sweep")
+        bids, asks = eng.snapshot(0, 5)
+        obids, oasks = ob.snapshot(0, 5)
+        assert np.array_equal(bids, obids) and np.array_equal(asks, oasks)
+
+
+def test_edge_one_symbol_whole_batch_and_tile_boundaries(me, orc):
+    """All records of a max-size batch on one symbol (one wave walks 65536 records) plus batch
+    sizes around the sort/tape tile boundaries."""
+    sc = me.preset(1)
+    st = me.Stream(sc)
+    base = st.base_prices()
+    sizes = [65536, 4095, 4096, 4097, 1023, 1024, 1025, 1, 63, 64, 65]
+    batches = [st.next(n) for n in sizes]
+    ob = orc.OracleBook(1, sc.levels, base, 1 << 22)
+    with engine_for(me, 1, sc.levels, base, 65536, 1 << 18, 1 << 22) as eng:
+        run_both(eng, ob, batches, ctx="tiles")
+
+
+def test_edge_symbol_count_sort_plans(me, orc):
+    """1-pass sort up to 2047 symbols, 2-pass from 2048: exercise both sides of the switch."""
+    for S in (1, 2, 2047, 2048, 70_000):
+        sc = me.preset(2, num_symbols=S, batch=20000)
+        st = me.Stream(sc)
+        base = st.base_prices()
+        batches = [st.next(20000) for _ in range(2)]
+        ob = orc.OracleBook(S, sc.levels, base, 1 << 22)
+        with engine_for(me, S, sc.levels, base, 20000, 1 << 17, 1 << 22) as eng:
+            run_both(eng, ob, batches, book_symbols=range(0, S, max(1, S // 50)), ctx=f"S={S}")
+
+
+def test_capacity_exhaustion_is_loud(me):
+    B, L = me.SIDE_BUY, me.TYPE_LIMIT
+    rows = [(0, B, L, 0, 1000 + (k % 64), 1) for k in range(200)]  # 64 levels -> needs >= 64 chunks
+    with engine_for(me, 1, 128, [1000], 256, 16, 1 << 20, max_chunks=8) as eng:
+        with pytest.raises(me.EngineError, match="chunk pool"):
+            eng.submit_batch(_rows(me, rows))
+        with pytest.raises(me.EngineError):
+            eng.submit_batch(_rows(me, rows[:1], start_seq=500))  # failed state is sticky
+
+
+def test_device_resident_path_matches_host_path(me, orc):
+    sc = me.preset(2, num_symbols=256, batch=16384)
+    st = me.Stream(sc)
+    base = st.base_prices()
+    batches = [st.next(sc.batch) for _ in range(6)]
+    ob = orc.OracleBook(sc.num_symbols, sc.levels, base, 1 << 22)
+    with engine_for(me, sc.num_symbols, sc.levels, base, sc.batch, 1 << 18, 1 << 22) as eng:
+        dbs = [eng.upload(b) for b in batches]
+        for b, db in zip(batches, dbs):
+            eng.submit_device(db)
+            r, f = eng.fetch_outputs(len(b))
+            ro, fo = ob.submit(b)
+            assert_results_equal(r, ro, "device path")
+            assert_fills_equal(f, fo, "device path")
+        assert_books_equal(eng, ob, range(sc.num_symbols), "device path")
+
+
+# ---------------------------------------------------------------- BASELINE size (config 2)
+def test_full_size_config2_bitexact(me, orc):
+    """BASELINE.json configs[1] at its real size (1,024 symbols, 65,536-record batches): 24
+    consecutive batches compared record-for-record and fill-for-fill, plus size-independent
+    properties of every tape."""
+    sc = me.preset(2)
+    st = me.Stream(sc)
+    base = st.base_prices()
+    ob = orc.OracleBook(sc.num_symbols, sc.levels, base, 1 << 26)
+    with engine_for(me, sc.num_symbols, sc.levels, base, sc.batch, 1 << 21, 1 << 26) as eng:
+        for k in range(24):
+            b = st.next(sc.batch)
+            r, f = eng.submit_batch(b)
+            ro, fo = ob.submit(b)
+            assert_results_equal(r, ro, f"full c2 b{k}")
+            assert_fills_equal(f, fo, f"full c2 b{k}")
+            # properties: tape ordered by taker seq; per-taker fill qty sums to filled_qty
+            assert np.all(np.diff(f["taker_seq"].astype(np.int64)) >= 0)
+            sums = np.bincount(np.repeat(np.arange(len(b)), r["fill_count"]), weights=f["qty"], minlength=len(b))
+            assert np.array_equal(sums.astype(np.int64), r["filled_qty"].astype(np.int64))
+            assert np.all(f["maker_seq"] < f["taker_seq"])
+        assert_books_equal(eng, ob, range(0, sc.num_symbols, 7), "full c2")
+        assert eng.resting_count() == ob.resting()
