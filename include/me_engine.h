@@ -64,7 +64,7 @@ enum {
 #define ME_KIND(side, type, op) ((uint8_t)(((side) & 3) | (((type) & 1) << 2) | (((op) & 1) << 3)))
 
 /* Slots per FIFO chunk (one wave-wide load of a level's queue). */
-#define ME_CHUNK_SLOTS 32
+#define ME_CHUNK_SLOTS 16
 
 /* Error codes returned by every entry point. */
 enum {
@@ -91,7 +91,7 @@ typedef struct me_config {
   uint32_t levels;             /* L: fixed-depth price levels per symbol (power of two, 64..2^20) */
   uint32_t max_batch;          /* largest n accepted by me_submit_batch* */
   uint64_t max_resting;        /* resting orders the scratch/tape bound is sized for */
-  uint64_t max_chunks;         /* FIFO chunk pool (ME_CHUNK_SLOTS slots each); 0 = 2*max_resting/32 + 2*S */
+  uint64_t max_chunks;         /* FIFO chunk pool (ME_CHUNK_SLOTS slots each); 0 = max_resting + 2*S */
   uint64_t max_seq;            /* locator capacity: accepted seqs are 1 <= seq < max_seq */
   const int64_t* base_price;   /* [num_symbols] price_q4 of level 0 of each symbol's window */
   const uint32_t* symbol_ids;  /* optional [num_symbols] ids written to me_fill.symbol (NULL = local id) */

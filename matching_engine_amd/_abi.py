@@ -20,7 +20,7 @@ OP_NEW, OP_CANCEL = 0, 1
 ST_NEW, ST_PARTIALLY_FILLED, ST_FILLED, ST_CANCELED, ST_REJECTED = 0, 1, 2, 3, 4
 RJ_NONE, RJ_BAD_QTY, RJ_BAD_SIDE, RJ_OUT_OF_WINDOW, RJ_BAD_SYMBOL, RJ_UNKNOWN_ORDER, RJ_BAD_SEQ = range(7)
 ME_OK, ME_E_INVALID, ME_E_HIP, ME_E_CAPACITY, ME_E_STATE, ME_E_SQLITE = 0, -1, -2, -3, -4, -5
-CHUNK_SLOTS = 32
+CHUNK_SLOTS = 16
 
 
 def kind(side: int, otype: int = TYPE_LIMIT, op: int = OP_NEW) -> int:

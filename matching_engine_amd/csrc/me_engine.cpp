@@ -102,7 +102,7 @@ static int set_create_err(const std::string& s) {
 }
 
 static void free_all(me_engine* e) {
-  void* ptrs[] = {e->bk.levels,   e->bk.occ,      e->bk.sym,      e->bk.chdr,       e->bk.cseq,
+  void* ptrs[] = {e->bk.levels,   e->bk.occ,      e->bk.sym,      e->bk.chdr,       e->bk.cseq, e->bk.owner,
                   e->bk.cqty,     e->bk.loc,      e->bk.chunk_top, e->bk.err,       (void*)e->bk.gsym,
                   e->d_seq,       e->d_px,        e->d_qty,       e->d_sym,         e->d_kind,
                   e->d_keys[0],   e->d_keys[1],   e->d_idx[0],    e->d_idx[1],      e->d_hist,
@@ -209,7 +209,8 @@ extern "C" me_engine* me_create(const me_config* cfg) {
   e->dbits[1] = d1;
   const uint64_t L = cfg->levels;
   uint64_t nchunks = cfg->max_chunks;
-  if (nchunks == 0) nchunks = 2 * ((cfg->max_resting + ME_C - 1) / ME_C) + 2 * S;
+  // chunks in use <= resting orders (every linked chunk holds a live order), whatever the book shape
+  if (nchunks == 0) nchunks = cfg->max_resting + 2 * S;
   const uint64_t n = cfg->max_batch;
   const unsigned long long scap = cfg->max_resting + 2 * n;
   auto bail = [&](const std::string& m) -> me_engine* {
@@ -243,6 +244,7 @@ extern "C" me_engine* me_create(const me_config* cfg) {
   ALLOC(bk.occ, S * (L / 64));
   ALLOC(bk.sym, S);
   ALLOC(bk.chdr, nchunks);
+  ALLOC(bk.owner, nchunks);
   ALLOC(bk.cseq, nchunks * ME_C);
   ALLOC(bk.cqty, nchunks * ME_C);
   ALLOC(bk.loc, cfg->max_seq);
@@ -288,6 +290,7 @@ extern "C" me_engine* me_create(const me_config* cfg) {
   bool ok = launch_init_levels(st, bk.levels, S * L) == hipSuccess &&
             hipMemsetAsync(bk.occ, 0, S * (L / 64) * 8, st) == hipSuccess &&
             hipMemsetAsync(bk.chdr, 0xFF, nchunks * sizeof(ChunkHdr), st) == hipSuccess &&
+            hipMemsetAsync(bk.owner, 0xFF, nchunks * sizeof(uint32_t), st) == hipSuccess &&
             hipMemsetAsync(bk.cqty, 0, nchunks * ME_C * sizeof(int), st) == hipSuccess &&
             hipMemsetAsync(bk.loc, 0xFF, cfg->max_seq * sizeof(uint32_t), st) == hipSuccess &&
             hipMemsetAsync(bk.chunk_top, 0, 4, st) == hipSuccess && hipMemsetAsync(bk.err, 0, 4, st) == hipSuccess &&
@@ -538,7 +541,7 @@ static int walk_fifo(me_engine* e, const Level& lv, std::vector<std::pair<uint64
     HIP_TRY(hipMemcpy(&h, e->bk.chdr + ch, sizeof(h), hipMemcpyDeviceToHost), "D2H chunk");
     HIP_TRY(hipMemcpy(seqs, e->bk.cseq + (size_t)ch * ME_C, sizeof(seqs), hipMemcpyDeviceToHost), "D2H chunk");
     HIP_TRY(hipMemcpy(qs, e->bk.cqty + (size_t)ch * ME_C, sizeof(qs), hipMemcpyDeviceToHost), "D2H chunk");
-    const uint32_t b = h.begin_end & 0xFFFF, en = h.begin_end >> 16;
+    const uint32_t b = bel_begin(h.bel), en = bel_end(h.bel);
     for (uint32_t k = b; k < en && k < (uint32_t)ME_C; ++k)
       if (qs[k] > 0) out.emplace_back(seqs[k], qs[k]);
     if (ch == lv.tail) break;

@@ -338,8 +338,8 @@ __device__ __forceinline__ void emit_fills(WaveCtx& c, bool e, unsigned long lon
 
 // Consume `take` (> 0, <= level total) from the FIFO of level `lvl`, oldest first. Emits one
 // fill per maker touched; exhausted chunks go back to the symbol free list. Returns the level's
-// new head chunk (NIL when the level emptied). 32 slots of a chunk are ranked at once with a
-// 64-lane prefix scan of the slot quantities.
+// new head chunk (NIL when the level emptied). The ME_C slots of a chunk are ranked at once with
+// a 64-lane prefix scan of the slot quantities.
 __device__ uint32_t walk_level(WaveCtx& c, int lvl, long long take, uint32_t head, uint32_t tail,
                                unsigned long long taker) {
   const int lane = lane_id();
@@ -352,8 +352,8 @@ __device__ uint32_t walk_level(WaveCtx& c, int lvl, long long take, uint32_t hea
       set_err(bk, ERR_INCONSISTENT);
       return NIL;
     }
-    const uint32_t be = rl32(bk.chdr[ch].begin_end, 0);
-    const uint32_t b = be & 0xFFFFu, e = be >> 16;
+    const uint32_t bel = rl32(bk.chdr[ch].bel, 0);
+    const uint32_t b = bel_begin(bel), e = bel_end(bel);
     const uint32_t slot = b + (uint32_t)lane;
     const bool act = (lane < ME_C) && (slot < e);
     const size_t g = (size_t)ch * ME_C + slot;
@@ -367,11 +367,11 @@ __device__ uint32_t walk_level(WaveCtx& c, int lvl, long long take, uint32_t hea
     const bool fe = act && f > 0;
     emit_fills(c, fe, taker, sv, price, (int)f);
     if (fe) bk.cqty[g] = qv - (int)f;
+    c.resting_delta -= __popcll(__ballot(fe && f == qv));  // makers filled completely leave the book
     const long long live = rli64(inc, 63);
     need -= (need < live ? need : live);
     const unsigned long long alive = __ballot(act && (qv - f) > 0);
-    const uint32_t nb = alive ? b + (uint32_t)__builtin_ctzll(alive) : e;
-    if (nb == e) {  // every written slot of the chunk is consumed
+    if (!alive) {  // every written slot of the chunk is consumed
       if (ch == tail) {
         free_chunk(c, ch);
         if (need > 0) set_err(bk, ERR_INCONSISTENT);
@@ -381,13 +381,15 @@ __device__ uint32_t walk_level(WaveCtx& c, int lvl, long long take, uint32_t hea
       free_chunk(c, ch);
       ch = nxt;
     } else {
-      if (lane == 0) bk.chdr[ch].begin_end = nb | (e << 16);
+      const uint32_t nb = b + (uint32_t)__builtin_ctzll(alive);
+      if (lane == 0) bk.chdr[ch].bel = bel_pack(nb, e, (uint32_t)__popcll(alive));
       if (need > 0) {  // impossible: a live slot remains only once the take is met
         set_err(bk, ERR_INCONSISTENT);
         return ch;
       }
     }
   }
+  if (ch != head && ch < bk.nchunks && lane == 0) bk.chdr[ch].prev = NIL;  // new FIFO head
   return ch;
 }
 
@@ -476,36 +478,32 @@ __device__ bool rest_order(WaveCtx& c, int lvl, unsigned long long seq, int qty,
   L.head = rl32(L.head, 0);
   L.tail = rl32(L.tail, 0);
   uint32_t ch, slot;
-  uint32_t e = ME_C;
-  uint32_t b = 0;
+  uint32_t bel = bel_pack(0, ME_C, 0);
   if (L.tail != NIL && L.tail >= bk.nchunks) {
     set_err(bk, ERR_INCONSISTENT);
     return false;
   }
-  if (L.tail != NIL) {
-    const uint32_t be = rl32(bk.chdr[L.tail].begin_end, 0);
-    b = be & 0xFFFFu;
-    e = be >> 16;
-  }
-  if (L.tail == NIL || e >= (uint32_t)ME_C) {
+  if (L.tail != NIL) bel = rl32(bk.chdr[L.tail].bel, 0);
+  if (L.tail == NIL || bel_end(bel) >= (uint32_t)ME_C) {
     ch = alloc_chunk(c);
     if (ch == NIL) return false;
     slot = 0;
     if (lane == 0) {
       ChunkHdr h;
       h.next = NIL;
+      h.prev = L.tail;
       h.level = (uint32_t)lvl;
-      h.owner = c.s;
-      h.begin_end = 1u << 16;
+      h.bel = bel_pack(0, 1, 1);
       bk.chdr[ch] = h;
+      bk.owner[ch] = c.s;
       if (L.tail != NIL) bk.chdr[L.tail].next = ch;
     }
     if (L.tail == NIL) L.head = ch;
     L.tail = ch;
   } else {
     ch = L.tail;
-    slot = e;
-    if (lane == 0) bk.chdr[ch].begin_end = b | ((e + 1) << 16);
+    slot = bel_end(bel);
+    if (lane == 0) bk.chdr[ch].bel = bel_pack(bel_begin(bel), slot + 1, bel_live(bel) + 1);
   }
   const size_t g = (size_t)ch * ME_C + slot;
   const bool was_empty = (L.total == 0);
@@ -527,6 +525,8 @@ __device__ bool rest_order(WaveCtx& c, int lvl, unsigned long long seq, int qty,
 }
 
 // Cancel the live resting order `tgt` of this symbol. Returns the removed qty, 0 if not live.
+// A chunk left without live orders is unlinked from its FIFO at once (so chunks in use never
+// exceed resting orders); a level left empty returns its whole FIFO to the free list.
 __device__ int cancel_order(WaveCtx& c, unsigned long long tgt) {
   const BookDev& bk = c.bk;
   const int lane = lane_id();
@@ -536,13 +536,16 @@ __device__ int cancel_order(WaveCtx& c, unsigned long long tgt) {
   if (g == NIL) return 0;
   const uint32_t ch = g / ME_C;
   if (ch >= bk.nchunks) return 0;
-  const uint32_t owner = rl32(bk.chdr[ch].owner, 0);
+  const uint32_t owner = rl32(bk.owner[ch], 0);
   if (owner != c.s) return 0;  // another symbol's order: never touch its book
   const int q = rli32(bk.cqty[g], 0);
   const unsigned long long sq = rl64(bk.cseq[g], 0);
   if (sq != tgt || q <= 0) return 0;
-  const int lvl = (int)rl32(bk.chdr[ch].level, 0);
-  if (lvl < 0 || lvl >= (int)bk.L) {
+  const ChunkHdr hd = bk.chdr[ch];
+  const int lvl = (int)rl32(hd.level, 0);
+  const uint32_t bel = rl32(hd.bel, 0);
+  const uint32_t nxt = rl32(hd.next, 0), prv = rl32(hd.prev, 0);
+  if (lvl < 0 || lvl >= (int)bk.L || bel_live(bel) == 0) {
     set_err(bk, ERR_INCONSISTENT);
     return 0;
   }
@@ -551,11 +554,12 @@ __device__ int cancel_order(WaveCtx& c, unsigned long long tgt) {
   L.total = rli64(L.total, 0) - q;
   L.head = rl32(L.head, 0);
   L.tail = rl32(L.tail, 0);
-  if (lane == 0) bk.cqty[g] = 0;
-  if (L.total == 0 && (L.tail >= bk.nchunks || L.head >= bk.nchunks)) {
+  if (L.tail >= bk.nchunks || L.head >= bk.nchunks) {
     set_err(bk, ERR_INCONSISTENT);
     return q;
   }
+  if (lane == 0) bk.cqty[g] = 0;
+  const uint32_t live = bel_live(bel) - 1;
   if (L.total == 0) {
     // splice the whole (now dead) FIFO onto the free list
     if (lane == 0) bk.chdr[L.tail].next = c.free_head;
@@ -567,8 +571,27 @@ __device__ int cancel_order(WaveCtx& c, unsigned long long tgt) {
     wave_mem_order();
     if (lvl == c.bb) c.bb = prev_occ(c, lvl);
     if (lvl == c.ba) c.ba = next_occ(c, lvl);
+  } else if (live == 0) {
+    // unlink the dead chunk (the level still has live orders elsewhere, so ch != head || ch != tail)
+    if (lane == 0) {
+      if (ch == L.head) {
+        L.head = nxt;
+        bk.chdr[nxt].prev = NIL;
+      } else if (ch == L.tail) {
+        L.tail = prv;
+        bk.chdr[prv].next = NIL;
+      } else {
+        bk.chdr[prv].next = nxt;
+        bk.chdr[nxt].prev = prv;
+      }
+      *lp = L;
+    }
+    free_chunk(c, ch);
   } else {
-    if (lane == 0) *lp = L;
+    if (lane == 0) {
+      bk.chdr[ch].bel = bel_pack(bel_begin(bel), bel_end(bel), live);
+      *lp = L;
+    }
   }
   c.resting_delta -= 1;
   return q;

@@ -9,17 +9,20 @@
 //                   a level's side is implied by its position.
 //   occ    [S][L/64] occupancy bitmap of the ladder (bit set <=> total > 0).
 //   sym    [S]      32 B per-symbol scalars (window base, best bid/ask level, chunk free list).
-//   chunks [NC]     FIFO storage: a level's queue is a linked list of chunks of ME_C slots
-//                   {seq u64, qty i32} (SoA: cseq / cqty); a wave reads one chunk per load.
+//   chunks [NC]     FIFO storage: a level's queue is a doubly linked list of chunks of ME_C
+//                   slots {seq u64, qty i32} (SoA: cseq / cqty); a wave reads one chunk per load.
+//                   Every linked chunk holds >= 1 live order (a chunk emptied by cancels is
+//                   unlinked at once), so chunks in use <= resting orders.
 //   loc    [max_seq] seq -> global slot (chunk * ME_C + slot) for cancels.
 #pragma once
+#include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "me_engine.h"
 
 namespace me {
 
-constexpr int ME_C = 32;                 // slots per chunk (one wave-load of qty + seq)
+constexpr int ME_C = 16;                 // slots per chunk (one wave-load of qty + seq)
 constexpr uint32_t NIL = 0xFFFFFFFFu;
 constexpr int TILE_SORT = 4096;          // records per workgroup in the grouping sort
 constexpr int TILE_TAPE = 1024;          // records per workgroup in the tape compaction
@@ -39,11 +42,17 @@ struct alignas(16) Level {
 };
 
 struct alignas(16) ChunkHdr {
-  uint32_t next;       // next chunk of the level FIFO, or of the symbol free list
-  uint32_t level;      // level index the chunk belongs to
-  uint32_t owner;      // symbol that allocated it (chunks never migrate between symbols)
-  uint32_t begin_end;  // begin (first possibly-live slot) | end (slots written) << 16
+  uint32_t next;   // next chunk of the level FIFO, or of the symbol free list
+  uint32_t prev;   // previous chunk of the level FIFO (NIL at the head)
+  uint32_t level;  // level index the chunk belongs to
+  uint32_t bel;    // begin (first possibly-live slot) | end (slots written) << 8 | live << 16
 };
+__host__ __device__ inline uint32_t bel_pack(uint32_t b, uint32_t e, uint32_t live) {
+  return b | (e << 8) | (live << 16);
+}
+__host__ __device__ inline uint32_t bel_begin(uint32_t v) { return v & 0xFFu; }
+__host__ __device__ inline uint32_t bel_end(uint32_t v) { return (v >> 8) & 0xFFu; }
+__host__ __device__ inline uint32_t bel_live(uint32_t v) { return (v >> 16) & 0xFFu; }
 
 struct alignas(32) SymState {
   long long base;      // price_q4 of level 0
@@ -59,6 +68,7 @@ struct BookDev {
   unsigned long long* occ;
   SymState* sym;
   ChunkHdr* chdr;
+  uint32_t* owner;        // [NC] symbol that allocated the chunk (chunks never change symbol)
   unsigned long long* cseq;
   int* cqty;
   uint32_t* loc;

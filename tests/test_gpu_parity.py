@@ -32,7 +32,9 @@ def engine_for(me, S, L, base, max_batch, max_resting, max_seq=1 << 22, **kw):
 def test_golden_fixture_on_gpu(me, cid):
     meta, batches, res, fills, book = load_fixture(cid)
     mb = max(len(b) for b in batches)
-    with engine_for(me, meta["num_symbols"], meta["levels"], meta["base"], mb, 1 << 18, meta["max_seq"]) as eng:
+    # deep sparse books (config 4) keep ~one chunk per resting order: size the pool for that
+    with engine_for(me, meta["num_symbols"], meta["levels"], meta["base"], mb, 1 << 18, meta["max_seq"],
+                    max_chunks=1 << 17) as eng:
         for k, b in enumerate(batches):
             r, f = eng.submit_batch(b)
             assert_results_equal(r, res[k], f"fixture c{cid} b{k}")
@@ -53,7 +55,8 @@ def _stream_run(me, orc, cfg, nbatches, seed_per_side=0, max_seq=1 << 26, book_s
     mb = max(len(b) for b in batches)
     total = sum(len(b) for b in batches)
     ob = orc.OracleBook(sc.num_symbols, sc.levels, base, max_seq)
-    with engine_for(me, sc.num_symbols, sc.levels, base, mb, total + 1024, max_seq) as eng:
+    with engine_for(me, sc.num_symbols, sc.levels, base, mb, total + 1024, max_seq,
+                    max_chunks=total + 2 * sc.num_symbols) as eng:
         nf = run_both(eng, ob, batches, book_symbols=book_symbols, ctx=f"config {cfg}")
     return nf, total
 
@@ -128,7 +131,7 @@ def test_edge_deep_sweep_multi_window_multi_chunk(me, orc):
     refill = _rows(me, [(0, B, L, 0, 9000 + (k % 5), 3) for k in range(200)], start_seq=seq)
     base = [8000]
     ob = orc.OracleBook(1, 4096, base, 1 << 20)
-    with engine_for(me, 1, 4096, base, 1024, 4096, 1 << 20) as eng:
+    with engine_for(me, 1, 4096, base, 1024, 4096, 1 << 20, max_chunks=4096) as eng:
         run_both(eng, ob, [b1, b2, b3, refill], ctx="deep sweep")
         bids, asks = eng.snapshot(0, 5)
         obids, oasks = ob.snapshot(0, 5)
@@ -158,6 +161,32 @@ def test_edge_symbol_count_sort_plans(me, orc):
         ob = orc.OracleBook(S, sc.levels, base, 1 << 22)
         with engine_for(me, S, sc.levels, base, 20000, 1 << 17, 1 << 22) as eng:
             run_both(eng, ob, batches, book_symbols=range(0, S, max(1, S // 50)), ctx=f"S={S}")
+
+
+def test_cancelled_chunks_are_unlinked(me, orc):
+    """A level that never empties, with chunk after chunk filled and then cancelled: dead chunks
+    (head, middle, tail) must be unlinked and reused, so a 4-chunk pool suffices for 30 rounds."""
+    B, S, L, M = me.SIDE_BUY, me.SIDE_SELL, me.TYPE_LIMIT, me.TYPE_MARKET
+    C = me._abi.CHUNK_SLOTS
+    ob = orc.OracleBook(1, 128, [1000], 1 << 20)
+    seq = 1
+    with engine_for(me, 1, 128, [1000], 4 * C, 4 * C, 1 << 20, max_chunks=4) as eng:
+        run_both(eng, ob, [_rows(me, [(0, B, L, 0, 1050, 7)], start_seq=seq)], ctx="anchor")
+        seq += 1
+        for rnd in range(30):
+            adds = [(0, B, L, 0, 1050, 1 + k) for k in range(2 * C)]
+            b = _rows(me, adds, start_seq=seq)
+            first = seq
+            seq += len(adds)
+            # cancel in an order that kills the middle chunk first, then the tail, then the rest
+            order = list(range(C // 2, C + C // 2)) + list(range(C + C // 2, 2 * C)) + list(range(C // 2))
+            if rnd % 3 == 2:
+                order = order[::-1]
+            cancels = _rows(me, [(0, B, L, 1, first + k, 0) for k in order], start_seq=seq)
+            seq += len(order)
+            run_both(eng, ob, [b, cancels], ctx=f"round {rnd}")
+        sweep = _rows(me, [(0, S, M, 0, 0, 5)], start_seq=seq)
+        run_both(eng, ob, [sweep], ctx="final sweep")
 
 
 def test_capacity_exhaustion_is_loud(me):
