@@ -1,0 +1,230 @@
+#!/usr/bin/env python3
+"""bench.py — orders matched/sec of the MI355X batched matching core (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1]): 1,024 symbols per GPU, uniform
+synthetic stream (80% LIMIT at mid +-32 ticks / 20% MARKET, qty U[1,100]), 65,536-order batches
+per GPU. With N GPUs the global stream has 1,024*N symbols and 65,536*N-order batches,
+hash-sharded by symbol (splitmix64(symbol) % N) with no cross-GPU matching: weak scaling.
+
+One step = one batch through the whole device pipeline (group-by-symbol sort -> match ->
+tape compaction) with the batch already resident in HBM. W warmup steps, then K timed steps
+bracketed by barrier + device sync; the max over ranks is the job time.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import matching_engine_amd as me  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+BYTES_PER_ORDER = 48   # 32 B record read + 16 B resting insert / cancel
+BYTES_PER_FILL = 48    # 32 B tape record + 16 B maker-slot RMW
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--symbols-per-gpu", type=int, default=1024)
+    ap.add_argument("--batch-per-gpu", type=int, default=65536)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--traffic-from", default=None,
+                    help="JSON {bytes_per_launch: ...} from tools/pmc_traffic.py for roofline.traffic")
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def barrier_sync(world, local):
+    import torch
+
+    torch.cuda.synchronize(local)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+        torch.cuda.synchronize(local)
+
+
+def allreduce(v, world, op, local):
+    if world == 1:
+        return v
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([v], dtype=torch.float64, device=f"cuda:{local}")
+    dist.all_reduce(t, op=op)
+    return float(t.item())
+
+
+def build_rank_batches(args, world, rank, nbatches):
+    """Global stream, hash-sharded; this rank's batches with local symbol ids."""
+    S = args.symbols_per_gpu * world
+    sc = me.preset(2, num_symbols=S, batch=args.batch_per_gpu * world)
+    st = me.Stream(sc)
+    base = st.base_prices()
+    shard, local, members = me.shard_table(S, world)
+    ids = members[rank]
+    out = []
+    for _ in range(nbatches):
+        b = st.next(sc.batch)
+        sel = np.nonzero(shard[b.symbol] == rank)[0]
+        lb = b.take(sel)
+        lb.symbol = np.ascontiguousarray(local[lb.symbol], dtype=np.uint32)
+        out.append(lb)
+    return sc, base[ids], ids, out, sc.batch * nbatches
+
+
+def cpu_baseline(args):
+    """Scalar CPU oracle (oracle/, a port of the build-defined matching semantics; the reference
+    itself has no matcher) on a bounded prefix of the same N=1 stream, 1 thread."""
+    from oracle.oracle import OracleBook
+
+    sc = me.preset(2, num_symbols=args.symbols_per_gpu, batch=args.batch_per_gpu)
+    st = me.Stream(sc)
+    ob = OracleBook(sc.num_symbols, sc.levels, st.base_prices(), 1 << 40)
+    done, t_cpu, k = 0, 0.0, 0
+    while t_cpu < args.cpu_seconds:
+        b = st.next(sc.batch)
+        t0 = time.perf_counter()
+        ob.submit(b)
+        t_cpu += time.perf_counter() - t0
+        done += len(b)
+        k += 1
+    return {"value": done / t_cpu, "unit": "orders/s", "cores": 1, "kind": "port",
+            "sample": f"first {k} batches ({done} orders) of the config-2 stream, oracle/oracle_book.cpp "
+                      f"scalar price-time book, {t_cpu:.1f}s"}
+
+
+def main():
+    args = parse()
+    world, rank, local = dist_setup(args)
+    import torch
+
+    nb = args.warmup + args.steps
+    sc, base, ids, batches, global_orders = build_rank_batches(args, world, rank, nb + (0 if args.no_e2e else 10))
+    e2e_batches = batches[nb:]
+    batches = batches[:nb]
+    total_local = sum(len(b) for b in batches)
+    eng = me.Engine(len(ids), sc.levels, base, max_batch=max(len(b) for b in batches) + 1,
+                    max_resting=total_local // 3 + 65536, max_seq=global_orders + 16, device=local,
+                    symbol_ids=ids)
+    dbs = [eng.upload(b) for b in batches]
+    for db in dbs[: args.warmup]:
+        eng.submit_device(db)
+    eng.sync()
+    eng.timing_enable(True)
+    barrier_sync(world, local)
+    t0 = time.perf_counter()
+    for db in dbs[args.warmup:]:
+        eng.submit_device(db)
+    eng.sync()
+    barrier_sync(world, local)
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    tm = eng.timing_read()
+    orders_local = sum(db.n for db in dbs[args.warmup:])
+    import torch.distributed as tdist
+
+    MAX = tdist.ReduceOp.MAX if world > 1 else None
+    SUM = tdist.ReduceOp.SUM if world > 1 else None
+    job_time = allreduce(elapsed, world, MAX, local)
+    orders_all = allreduce(float(orders_local), world, SUM, local)
+    fills_all = allreduce(float(tm["fills"]), world, SUM, local)
+
+    # roofline of the dominant kernel (k_match) on this rank, from HIP events on its stream
+    launches = max(tm["launches"], 1)
+    avg_match_s = tm["match_ms"] / 1e3 / launches
+    bytes_per_launch = (BYTES_PER_ORDER * orders_local + BYTES_PER_FILL * tm["fills"]) / launches
+    achieved = bytes_per_launch / avg_match_s / 1e9
+    traffic = None
+    if args.traffic_from and os.path.exists(args.traffic_from):
+        traffic = json.load(open(args.traffic_from)).get("bytes_per_launch")
+
+    # PCIe-inclusive host path (me_submit_batch: H2D + pipeline + D2H of results and tape), informational
+    e2e = None
+    if e2e_batches:
+        torch.cuda.synchronize(local)
+        t2 = time.perf_counter()
+        n2 = 0
+        for b in e2e_batches:
+            eng.submit_batch(b)
+            n2 += len(b)
+        e2e = n2 / (time.perf_counter() - t2)
+
+    if rank == 0:
+        cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args)
+        line = {
+            "metric": "orders matched/sec (whole node); fills bit-exact vs CPU oracle",
+            "value": orders_all / job_time,
+            "unit": "orders/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": job_time / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64",
+            "data": "synthetic (me_gen config 2 stream, seed 2)",
+            "config": {
+                "workload": "BASELINE configs[1]: 1,024 symbols/GPU x uniform stream, 65,536-order batches/GPU, "
+                            "80% LIMIT +-32 ticks / 20% MARKET, qty U[1,100]",
+                "symbols": args.symbols_per_gpu * world,
+                "global_batch": args.batch_per_gpu * world,
+                "levels": sc.levels,
+                "parallelism": f"symbol-hash shards x{world} (no cross-GPU matching)",
+            },
+            "fills_per_order": fills_all / max(orders_all, 1),
+            "kernel_match_ms_avg": tm["match_ms"] / launches,
+            "pipeline_ms_avg": tm["pipeline_ms"] / launches,
+            "e2e_host_path_orders_per_s_rank0": e2e,
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "kernel": "k_match",
+                "algorithmic_bytes_per_launch": bytes_per_launch,
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    for db in dbs:
+        db.free()
+    eng.close()
+    if world > 1:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

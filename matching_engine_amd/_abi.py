@@ -137,6 +137,13 @@ def load() -> C.CDLL:
             f"{LIB_PATH} is missing: build it with `make -C matching_engine_amd` "
             "(the matching path has no CPU/Python fallback)"
         )
+    # libme_engine.so and torch's ROCm wheel both need libamdhip64.so.7; torch resolves it by a
+    # different file name, so if our library were loaded first the process would end up with two
+    # HIP runtimes. Letting torch (when installed) load first keeps one runtime per process.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(LIB_PATH)
     for name, (res, args) in PROTOTYPES.items():
         fn = getattr(lib, name)
