@@ -11,7 +11,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libme_engine.so")
+# ME_ENGINE_LIB selects a diagnostic variant (e.g. build/libme_engine_stamps.so) for profiling runs.
+LIB_PATH = os.environ.get("ME_ENGINE_LIB") or os.path.join(_HERE, "libme_engine.so")
 
 # ---- enums (include/me_engine.h) -------------------------------------------------------------
 SIDE_UNSPECIFIED, SIDE_BUY, SIDE_SELL = 0, 1, 2

@@ -102,12 +102,12 @@ static int set_create_err(const std::string& s) {
 }
 
 static void free_all(me_engine* e) {
-  void* ptrs[] = {e->bk.levels,   e->bk.occ,      e->bk.sym,      e->bk.chdr,       e->bk.cseq, e->bk.owner,
+  void* ptrs[] = {e->bk.levels,   e->bk.occ,      e->bk.sym,      e->bk.chdr,       e->bk.cseq, e->bk.owner, e->bk.tend,
                   e->bk.cqty,     e->bk.loc,      e->bk.chunk_top, e->bk.err,       (void*)e->bk.gsym,
                   e->d_seq,       e->d_px,        e->d_qty,       e->d_sym,         e->d_kind,
                   e->d_keys[0],   e->d_keys[1],   e->d_idx[0],    e->d_idx[1],      e->d_hist,
                   e->d_res,       e->d_fstart,    e->d_tile_sum,  e->d_scratch,     e->d_scratch_top,
-                  e->d_tape,      e->d_tape_count, e->d_fills_acc};
+                  e->d_tape,      e->d_tape_count, e->d_fills_acc, e->bk.dbg};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (void* p : e->user_allocs) (void)hipFree(p);
@@ -242,6 +242,7 @@ extern "C" me_engine* me_create(const me_config* cfg) {
   } while (0)
   ALLOC(bk.levels, S * L);
   ALLOC(bk.occ, S * (L / 64));
+  ALLOC(bk.tend, S * L);
   ALLOC(bk.sym, S);
   ALLOC(bk.chdr, nchunks);
   ALLOC(bk.owner, nchunks);
@@ -271,6 +272,10 @@ extern "C" me_engine* me_create(const me_config* cfg) {
   ALLOC(e->d_tape, scap);
   ALLOC(e->d_tape_count, 1);
   ALLOC(e->d_fills_acc, 1);
+#ifdef ME_STAMPS
+  ALLOC(bk.dbg, S * 16);
+  (void)hipMemset(bk.dbg, 0, S * 16 * 8);
+#endif
 #undef ALLOC
   e->scratch_cap = scap;
   // initial book state
@@ -289,6 +294,7 @@ extern "C" me_engine* me_create(const me_config* cfg) {
   }
   bool ok = launch_init_levels(st, bk.levels, S * L) == hipSuccess &&
             hipMemsetAsync(bk.occ, 0, S * (L / 64) * 8, st) == hipSuccess &&
+            hipMemsetAsync(bk.tend, 0, S * L, st) == hipSuccess &&
             hipMemsetAsync(bk.chdr, 0xFF, nchunks * sizeof(ChunkHdr), st) == hipSuccess &&
             hipMemsetAsync(bk.owner, 0xFF, nchunks * sizeof(uint32_t), st) == hipSuccess &&
             hipMemsetAsync(bk.cqty, 0, nchunks * ME_C * sizeof(int), st) == hipSuccess &&
@@ -541,8 +547,7 @@ static int walk_fifo(me_engine* e, const Level& lv, std::vector<std::pair<uint64
     HIP_TRY(hipMemcpy(&h, e->bk.chdr + ch, sizeof(h), hipMemcpyDeviceToHost), "D2H chunk");
     HIP_TRY(hipMemcpy(seqs, e->bk.cseq + (size_t)ch * ME_C, sizeof(seqs), hipMemcpyDeviceToHost), "D2H chunk");
     HIP_TRY(hipMemcpy(qs, e->bk.cqty + (size_t)ch * ME_C, sizeof(qs), hipMemcpyDeviceToHost), "D2H chunk");
-    const uint32_t b = bel_begin(h.bel), en = bel_end(h.bel);
-    for (uint32_t k = b; k < en && k < (uint32_t)ME_C; ++k)
+    for (uint32_t k = 0; k < (uint32_t)ME_C; ++k)  // a slot is live iff qty > 0; slot order = time order
       if (qs[k] > 0) out.emplace_back(seqs[k], qs[k]);
     if (ch == lv.tail) break;
     ch = h.next;
@@ -676,3 +681,14 @@ extern "C" int me_last_error(const me_engine* e, char* buf, size_t cap) {
   }
   return (int)s.size();
 }
+
+#ifdef ME_STAMPS
+// Diagnostic builds only: per-symbol phase cycles of the last k_match launch ([S][16]).
+extern "C" int me_debug_stamps(me_engine* e, unsigned long long* out, size_t n) {
+  if (!e || !e->bk.dbg) return ME_E_INVALID;
+  HIP_TRY(hipStreamSynchronize(e->stream), "sync");
+  size_t k = std::min(n, (size_t)e->bk.S * 16);
+  HIP_TRY(hipMemcpy(out, e->bk.dbg, k * 8, hipMemcpyDeviceToHost), "D2H stamps");
+  return ME_OK;
+}
+#endif

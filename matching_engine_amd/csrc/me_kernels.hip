@@ -36,19 +36,55 @@ __device__ __forceinline__ long long rli64(long long v, int k) {
 __device__ __forceinline__ unsigned long long lanemask_lt() {
   return (1ull << lane_id()) - 1ull;
 }
-// Inclusive 64-lane prefix sum of an int64.
+// DPP row shift / broadcast of a 32-bit value: lanes whose source is outside the pattern get 0.
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ uint32_t dpp32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kCtrl, kRowMask, 0xF, false);
+}
+template <int kCtrl, int kRowMask>
+__device__ __forceinline__ long long dpp64(long long v) {
+  const uint32_t lo = dpp32<kCtrl, kRowMask>((uint32_t)v);
+  const uint32_t hi = dpp32<kCtrl, kRowMask>((uint32_t)((unsigned long long)v >> 32));
+  return (long long)(((unsigned long long)hi << 32) | lo);
+}
+// Inclusive 64-lane prefix sum of an int64 on the VALU with DPP (no LDS permutes): row_shr
+// 1/2/4/8 scans each 16-lane row, row_bcast:15 / row_bcast:31 carry the row totals.
 __device__ __forceinline__ long long wave_incl_scan(long long x) {
-  const int lane = lane_id();
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    long long t = __shfl_up(x, d, 64);
-    if (lane >= d) x += t;
-  }
+  x += dpp64<0x111, 0xF>(x);  // row_shr:1
+  x += dpp64<0x112, 0xF>(x);  // row_shr:2
+  x += dpp64<0x114, 0xF>(x);  // row_shr:4
+  x += dpp64<0x118, 0xF>(x);  // row_shr:8
+  x += dpp64<0x142, 0xA>(x);  // row_bcast:15 into rows 1, 3
+  x += dpp64<0x143, 0xC>(x);  // row_bcast:31 into rows 2, 3
   return x;
 }
 // Orders the wave's own global stores before its later loads of the same lines (another lane
 // may read what this lane wrote). Same-CU ordering: no cache maintenance, a compiler barrier.
 __device__ __forceinline__ void wave_mem_order() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
+
+// Diagnostic build only (-DME_STAMPS): per-wave cycle shares of the matching phases, read with
+// me_debug_stamps(). The product build compiles every stamp away.
+enum { PH_PROLOGUE, PH_FETCH, PH_SWEEP, PH_WALK, PH_REST, PH_CANCEL, PH_RESULT, PH_EPILOGUE,
+       PH_SW_WINDOW, PH_SW_UPDATE, PH_SW_JUMP, PH_SW_BEST, PH_N };
+#ifdef ME_STAMPS
+__device__ __forceinline__ unsigned long long stamp_now() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define STAMP_MARK(c) (c).st_t = stamp_now()
+#define STAMP_ADD(c, ph)                    \
+  do {                                      \
+    unsigned long long _n = stamp_now();    \
+    (c).st[ph] += _n - (c).st_t;            \
+    (c).st_t = _n;                          \
+  } while (0)
+#else
+#define STAMP_MARK(c) ((void)0)
+#define STAMP_ADD(c, ph) ((void)0)
+#endif
 
 // First index p in [0, n) with keys[p] >= key (keys ascending), by a 64-ary search:
 // every step the wave samples 64 positions, ballots, and narrows the range 64x.
@@ -213,34 +249,44 @@ __global__ __launch_bounds__(256) void k_sort_scatter(const uint32_t* __restrict
 }
 
 // ------------------------------------------------------------------ matching
+// Where a wave's view of its symbol's ladder lives: LDS (L <= LDS_MAX_LEVELS, staged in at
+// kernel start and written back at the end) or HBM (deep windows).
 struct WaveCtx {
   BookDev bk;
-  uint32_t s;          // local symbol
-  uint32_t gs;         // symbol id written in fills
+  Level* lv;                 // [L] ladder of this symbol (LDS or HBM)
+  unsigned long long* occ;   // [L/64] occupancy bitmap
+  uint8_t* tend;             // [L] slots written in each level's tail chunk
+  uint32_t s;                // local symbol
+  uint32_t gs;               // symbol id written in fills
   long long base;
-  int bb, ba;          // best bid / best ask level
-  uint32_t free_head;
+  int bb, ba;                // best bid / best ask level
+  uint32_t free_head;        // chunk free list of this symbol ...
+  uint32_t free_next;        // ... and chdr[free_head].next, loaded ahead of the pop that needs it
+  uint32_t bump_cur, bump_end;  // chunk ids reserved from the global bump allocator
+  uint32_t recs_left;        // records of this wave not processed yet (>= chunks it can still need)
   int resting_delta;
-  unsigned long long wptr;  // next scratch slot of this wave
+  unsigned long long wptr;   // next scratch slot of this wave
   me_fill* scratch;
+#ifdef ME_STAMPS
+  unsigned long long st[PH_N];
+  unsigned long long st_t;
+#endif
 };
-
-__device__ __forceinline__ uint32_t occ_words(const BookDev& bk) { return bk.Lwords; }
 
 // Smallest occupied level >= x, or L.
 __device__ int next_occ(const WaveCtx& c, int x) {
-  const BookDev& bk = c.bk;
-  const int L = (int)bk.L;
+  const int L = (int)c.bk.L;
   if (x >= L) return L;
   if (x < 0) x = 0;
-  const unsigned long long* occ = bk.occ + (size_t)c.s * bk.Lwords;
+  const unsigned long long* occ = c.occ;
   int w = x >> 6;
   unsigned long long word = occ[w] & (~0ull << (x & 63));
   if (word) return (w << 6) + __builtin_ctzll(word);
   const int lane = lane_id();
-  for (int b = w + 1; b < (int)bk.Lwords; b += 64) {
+  const int nw = (int)c.bk.Lwords;
+  for (int b = w + 1; b < nw; b += 64) {
     int idx = b + lane;
-    unsigned long long v = idx < (int)bk.Lwords ? occ[idx] : 0ull;
+    unsigned long long v = idx < nw ? occ[idx] : 0ull;
     unsigned long long m = __ballot(v != 0ull);
     if (m) {
       int t = __builtin_ctzll(m);
@@ -253,10 +299,9 @@ __device__ int next_occ(const WaveCtx& c, int x) {
 
 // Largest occupied level <= x, or -1.
 __device__ int prev_occ(const WaveCtx& c, int x) {
-  const BookDev& bk = c.bk;
   if (x < 0) return -1;
-  if (x >= (int)bk.L) x = (int)bk.L - 1;
-  const unsigned long long* occ = bk.occ + (size_t)c.s * bk.Lwords;
+  if (x >= (int)c.bk.L) x = (int)c.bk.L - 1;
+  const unsigned long long* occ = c.occ;
   int w = x >> 6;
   int r = x & 63;
   unsigned long long keep = (r == 63) ? ~0ull : ((1ull << (r + 1)) - 1ull);
@@ -277,46 +322,52 @@ __device__ int prev_occ(const WaveCtx& c, int x) {
 }
 
 __device__ __forceinline__ void occ_set(const WaveCtx& c, int lvl) {
-  if (lane_id() == 0) {
-    unsigned long long* p = c.bk.occ + (size_t)c.s * c.bk.Lwords + (lvl >> 6);
-    *p |= (1ull << (lvl & 63));
-  }
+  if (lane_id() == 0) c.occ[lvl >> 6] |= (1ull << (lvl & 63));
 }
 __device__ __forceinline__ void occ_clear(const WaveCtx& c, int lvl) {
-  if (lane_id() == 0) {
-    unsigned long long* p = c.bk.occ + (size_t)c.s * c.bk.Lwords + (lvl >> 6);
-    *p &= ~(1ull << (lvl & 63));
-  }
+  if (lane_id() == 0) c.occ[lvl >> 6] &= ~(1ull << (lvl & 63));
 }
 
 __device__ __forceinline__ void set_err(const BookDev& bk, uint32_t bits) {
   if (lane_id() == 0) atomicOr(bk.err, bits);
 }
 
+// Free-list push: the popped-next is known without a load.
 __device__ __forceinline__ void free_chunk(WaveCtx& c, uint32_t ch) {
   if (lane_id() == 0) c.bk.chdr[ch].next = c.free_head;
+  c.free_next = c.free_head;
   c.free_head = ch;
 }
 
+__device__ __forceinline__ void prefetch_free_next(WaveCtx& c) {
+  c.free_next = (c.free_head < c.bk.nchunks) ? rl32(c.bk.chdr[c.free_head].next, 0) : NIL;
+}
+
 __device__ __forceinline__ uint32_t alloc_chunk(WaveCtx& c) {
-  uint32_t ch;
   if (c.free_head != NIL) {
-    ch = c.free_head;
+    const uint32_t ch = c.free_head;
     if (ch >= c.bk.nchunks) {
       set_err(c.bk, ERR_INCONSISTENT);
       return NIL;
     }
-    c.free_head = rl32(c.bk.chdr[ch].next, 0);
+    c.free_head = c.free_next;
+    prefetch_free_next(c);  // consumed by the next pop, usually much later
     return ch;
   }
-  uint32_t got = 0;
-  if (lane_id() == 0) got = atomicAdd(c.bk.chunk_top, 1u);
-  ch = rl32(got, 0);
-  if (ch >= c.bk.nchunks) {
-    set_err(c.bk, ERR_CHUNK_OOM);
-    return NIL;
+  if (c.bump_cur >= c.bump_end) {
+    // each record needs at most one new chunk: never reserve more than the records left
+    const uint32_t BLK = min(16u, max(c.recs_left, 1u));
+    uint32_t got = 0;
+    if (lane_id() == 0) got = atomicAdd(c.bk.chunk_top, BLK);
+    got = rl32(got, 0);
+    if (got >= c.bk.nchunks) {
+      set_err(c.bk, ERR_CHUNK_OOM);
+      return NIL;
+    }
+    c.bump_cur = got;
+    c.bump_end = min(got + BLK, c.bk.nchunks);
   }
-  return ch;
+  return c.bump_cur++;
 }
 
 // Append one fill per lane where e holds, in lane order, to the wave's scratch run.
@@ -336,10 +387,10 @@ __device__ __forceinline__ void emit_fills(WaveCtx& c, bool e, unsigned long lon
   c.wptr += (unsigned long long)__popcll(m);
 }
 
-// Consume `take` (> 0, <= level total) from the FIFO of level `lvl`, oldest first. Emits one
-// fill per maker touched; exhausted chunks go back to the symbol free list. Returns the level's
-// new head chunk (NIL when the level emptied). The ME_C slots of a chunk are ranked at once with
-// a 64-lane prefix scan of the slot quantities.
+// Consume `take` (> 0, <= level total) from the FIFO of level `lvl`, oldest first. A slot is
+// live iff its qty > 0 (consumed, cancelled and unwritten slots hold 0), so one round trip loads
+// a chunk's header and all ME_C slots together; the slots are ranked with one wave prefix scan.
+// Exhausted chunks go back to the free list. Returns the new head chunk (NIL: level emptied).
 __device__ uint32_t walk_level(WaveCtx& c, int lvl, long long take, uint32_t head, uint32_t tail,
                                unsigned long long taker) {
   const int lane = lane_id();
@@ -352,11 +403,9 @@ __device__ uint32_t walk_level(WaveCtx& c, int lvl, long long take, uint32_t hea
       set_err(bk, ERR_INCONSISTENT);
       return NIL;
     }
-    const uint32_t bel = rl32(bk.chdr[ch].bel, 0);
-    const uint32_t b = bel_begin(bel), e = bel_end(bel);
-    const uint32_t slot = b + (uint32_t)lane;
-    const bool act = (lane < ME_C) && (slot < e);
-    const size_t g = (size_t)ch * ME_C + slot;
+    const uint32_t nxt = rl32(bk.chdr[ch].next, 0);
+    const bool act = lane < ME_C;
+    const size_t g = (size_t)ch * ME_C + (act ? lane : 0);
     const int qv = act ? bk.cqty[g] : 0;
     const unsigned long long sv = act ? bk.cseq[g] : 0ull;
     const long long inc = wave_incl_scan((long long)qv);
@@ -364,29 +413,23 @@ __device__ uint32_t walk_level(WaveCtx& c, int lvl, long long take, uint32_t hea
     long long f = need - ex;
     if (f < 0) f = 0;
     if (f > qv) f = qv;
-    const bool fe = act && f > 0;
+    const bool fe = f > 0;
     emit_fills(c, fe, taker, sv, price, (int)f);
     if (fe) bk.cqty[g] = qv - (int)f;
     c.resting_delta -= __popcll(__ballot(fe && f == qv));  // makers filled completely leave the book
     const long long live = rli64(inc, 63);
     need -= (need < live ? need : live);
-    const unsigned long long alive = __ballot(act && (qv - f) > 0);
-    if (!alive) {  // every written slot of the chunk is consumed
+    const unsigned long long alive = __ballot((qv - f) > 0);
+    if (!alive) {  // every slot of the chunk is consumed
+      free_chunk(c, ch);
       if (ch == tail) {
-        free_chunk(c, ch);
         if (need > 0) set_err(bk, ERR_INCONSISTENT);
         return NIL;
       }
-      const uint32_t nxt = rl32(bk.chdr[ch].next, 0);
-      free_chunk(c, ch);
       ch = nxt;
-    } else {
-      const uint32_t nb = b + (uint32_t)__builtin_ctzll(alive);
-      if (lane == 0) bk.chdr[ch].bel = bel_pack(nb, e, (uint32_t)__popcll(alive));
-      if (need > 0) {  // impossible: a live slot remains only once the take is met
-        set_err(bk, ERR_INCONSISTENT);
-        return ch;
-      }
+    } else if (need > 0) {  // impossible: a live slot remains only once the take is met
+      set_err(bk, ERR_INCONSISTENT);
+      return ch;
     }
   }
   if (ch != head && ch < bk.nchunks && lane == 0) bk.chdr[ch].prev = NIL;  // new FIFO head
@@ -401,10 +444,9 @@ __device__ long long sweep(WaveCtx& c, int dir, int lim, long long want, unsigne
                            uint32_t& nfill) {
   const int lane = lane_id();
   const BookDev& bk = c.bk;
-  Level* lv_base = bk.levels + (size_t)c.s * bk.L;
   long long rem = want;
   int cur = (dir > 0) ? c.ba : c.bb;
-  bool emptied_best = false;
+  bool emptied = false;
   const unsigned long long w_start = c.wptr;
   while (rem > 0) {
     if (dir > 0 ? (cur > lim || cur >= (int)bk.L) : (cur < lim || cur < 0)) break;
@@ -414,12 +456,13 @@ __device__ long long sweep(WaveCtx& c, int dir, int lim, long long want, unsigne
     L.total = 0;
     L.head = NIL;
     L.tail = NIL;
-    if (valid) L = lv_base[lv];
+    if (valid) L = c.lv[lv];
     const long long tot = L.total;
     const long long inc = wave_incl_scan(tot);
     const long long ex = inc - tot;
     const long long rem0 = rem;
     unsigned long long tm = __ballot(valid && tot > 0 && ex < rem0);
+    STAMP_ADD(c, PH_SW_WINDOW);
     while (tm) {
       const int t = __builtin_ctzll(tm);
       tm &= tm - 1;
@@ -429,7 +472,9 @@ __device__ long long sweep(WaveCtx& c, int dir, int lim, long long want, unsigne
       long long take = rem0 - lex;
       if (take > ltot) take = ltot;
       const uint32_t head = rl32(L.head, t), tail = rl32(L.tail, t);
+      STAMP_ADD(c, PH_SWEEP);
       const uint32_t nh = walk_level(c, lvl, take, head, tail, taker);
+      STAMP_ADD(c, PH_WALK);
       rem -= take;
       const long long ntot = ltot - take;
       if (lane == 0) {
@@ -437,12 +482,13 @@ __device__ long long sweep(WaveCtx& c, int dir, int lim, long long want, unsigne
         o.total = ntot;
         o.head = ntot ? nh : NIL;
         o.tail = ntot ? tail : NIL;
-        lv_base[lvl] = o;
+        c.lv[lvl] = o;
       }
       if (ntot == 0) {
         occ_clear(c, lvl);
-        emptied_best = true;
+        emptied = true;
       }
+      STAMP_ADD(c, PH_SW_UPDATE);
     }
     if (rem == 0) break;
     // every valid level of this window is now empty; jump to the next occupied one
@@ -455,36 +501,37 @@ __device__ long long sweep(WaveCtx& c, int dir, int lim, long long want, unsigne
       if (nxt < lim) break;
       cur = prev_occ(c, nxt);
     }
+    STAMP_ADD(c, PH_SW_JUMP);
   }
-  if (emptied_best) {
+  if (emptied) {
     wave_mem_order();
     if (dir > 0)
       c.ba = next_occ(c, c.ba);
     else
       c.bb = prev_occ(c, c.bb);
+    STAMP_ADD(c, PH_SW_BEST);
   }
   nfill = (uint32_t)(c.wptr - w_start);
   return want - rem;
 }
 
-// Append a resting order at the tail of level lvl's FIFO.
+// Append a resting order at the tail of level lvl's FIFO. With the ladder in LDS the common case
+// (room in the tail chunk) issues no HBM load at all: the tail fill count lives beside the level.
 __device__ bool rest_order(WaveCtx& c, int lvl, unsigned long long seq, int qty, bool buy) {
   const int lane = lane_id();
   const BookDev& bk = c.bk;
-  Level* lp = bk.levels + (size_t)c.s * bk.L + lvl;
   wave_mem_order();
-  Level L = *lp;
+  Level L = c.lv[lvl];
   L.total = rli64(L.total, 0);
   L.head = rl32(L.head, 0);
   L.tail = rl32(L.tail, 0);
+  const uint32_t te = rl32((uint32_t)c.tend[lvl], 0);
   uint32_t ch, slot;
-  uint32_t bel = bel_pack(0, ME_C, 0);
   if (L.tail != NIL && L.tail >= bk.nchunks) {
     set_err(bk, ERR_INCONSISTENT);
     return false;
   }
-  if (L.tail != NIL) bel = rl32(bk.chdr[L.tail].bel, 0);
-  if (L.tail == NIL || bel_end(bel) >= (uint32_t)ME_C) {
+  if (L.tail == NIL || te >= (uint32_t)ME_C) {
     ch = alloc_chunk(c);
     if (ch == NIL) return false;
     slot = 0;
@@ -493,7 +540,7 @@ __device__ bool rest_order(WaveCtx& c, int lvl, unsigned long long seq, int qty,
       h.next = NIL;
       h.prev = L.tail;
       h.level = (uint32_t)lvl;
-      h.bel = bel_pack(0, 1, 1);
+      h.pad = 0;
       bk.chdr[ch] = h;
       bk.owner[ch] = c.s;
       if (L.tail != NIL) bk.chdr[L.tail].next = ch;
@@ -502,8 +549,7 @@ __device__ bool rest_order(WaveCtx& c, int lvl, unsigned long long seq, int qty,
     L.tail = ch;
   } else {
     ch = L.tail;
-    slot = bel_end(bel);
-    if (lane == 0) bk.chdr[ch].bel = bel_pack(bel_begin(bel), slot + 1, bel_live(bel) + 1);
+    slot = te;
   }
   const size_t g = (size_t)ch * ME_C + slot;
   const bool was_empty = (L.total == 0);
@@ -511,7 +557,8 @@ __device__ bool rest_order(WaveCtx& c, int lvl, unsigned long long seq, int qty,
   if (lane == 0) {
     bk.cseq[g] = seq;
     bk.cqty[g] = qty;
-    *lp = L;
+    c.lv[lvl] = L;
+    c.tend[lvl] = (uint8_t)(slot + 1);
     if (seq < bk.max_seq) bk.loc[seq] = (uint32_t)g;
   }
   if (was_empty) occ_set(c, lvl);
@@ -534,23 +581,25 @@ __device__ int cancel_order(WaveCtx& c, unsigned long long tgt) {
   wave_mem_order();
   const uint32_t g = rl32(bk.loc[tgt], 0);
   if (g == NIL) return 0;
-  const uint32_t ch = g / ME_C;
+  const uint32_t ch = g / ME_C, slot = g % ME_C;
   if (ch >= bk.nchunks) return 0;
+  // one round trip: owner, header, the whole chunk's quantities and the target seq
   const uint32_t owner = rl32(bk.owner[ch], 0);
-  if (owner != c.s) return 0;  // another symbol's order: never touch its book
-  const int q = rli32(bk.cqty[g], 0);
-  const unsigned long long sq = rl64(bk.cseq[g], 0);
-  if (sq != tgt || q <= 0) return 0;
   const ChunkHdr hd = bk.chdr[ch];
+  const bool act = lane < ME_C;
+  const int qv = act ? bk.cqty[(size_t)ch * ME_C + lane] : 0;
+  const unsigned long long sq = rl64(bk.cseq[g], 0);
+  if (owner != c.s) return 0;  // another symbol's order: never touch its book
+  const int q = rli32(qv, (int)slot);
+  if (sq != tgt || q <= 0) return 0;
   const int lvl = (int)rl32(hd.level, 0);
-  const uint32_t bel = rl32(hd.bel, 0);
   const uint32_t nxt = rl32(hd.next, 0), prv = rl32(hd.prev, 0);
-  if (lvl < 0 || lvl >= (int)bk.L || bel_live(bel) == 0) {
+  if (lvl < 0 || lvl >= (int)bk.L) {
     set_err(bk, ERR_INCONSISTENT);
     return 0;
   }
-  Level* lp = bk.levels + (size_t)c.s * bk.L + lvl;
-  Level L = *lp;
+  const uint32_t live_after = (uint32_t)__popcll(__ballot(qv > 0)) - 1;
+  Level L = c.lv[lvl];
   L.total = rli64(L.total, 0) - q;
   L.head = rl32(L.head, 0);
   L.tail = rl32(L.tail, 0);
@@ -559,39 +608,41 @@ __device__ int cancel_order(WaveCtx& c, unsigned long long tgt) {
     return q;
   }
   if (lane == 0) bk.cqty[g] = 0;
-  const uint32_t live = bel_live(bel) - 1;
   if (L.total == 0) {
     // splice the whole (now dead) FIFO onto the free list
     if (lane == 0) bk.chdr[L.tail].next = c.free_head;
+    c.free_next = (L.head == L.tail) ? c.free_head : NIL;
     c.free_head = L.head;
+    if (L.head != L.tail) prefetch_free_next(c);
     L.head = NIL;
     L.tail = NIL;
-    if (lane == 0) *lp = L;
+    if (lane == 0) c.lv[lvl] = L;
     occ_clear(c, lvl);
     wave_mem_order();
     if (lvl == c.bb) c.bb = prev_occ(c, lvl);
     if (lvl == c.ba) c.ba = next_occ(c, lvl);
-  } else if (live == 0) {
-    // unlink the dead chunk (the level still has live orders elsewhere, so ch != head || ch != tail)
-    if (lane == 0) {
-      if (ch == L.head) {
-        L.head = nxt;
-        bk.chdr[nxt].prev = NIL;
-      } else if (ch == L.tail) {
-        L.tail = prv;
+  } else if (live_after == 0) {
+    // unlink the dead chunk (the level keeps live orders elsewhere, so ch is not both ends)
+    uint32_t nh = L.head, nt = L.tail;
+    if (ch == L.head) {
+      nh = nxt;
+      if (lane == 0) bk.chdr[nxt].prev = NIL;
+    } else if (ch == L.tail) {
+      nt = prv;
+      if (lane == 0) {
         bk.chdr[prv].next = NIL;
-      } else {
-        bk.chdr[prv].next = nxt;
-        bk.chdr[nxt].prev = prv;
+        c.tend[lvl] = (uint8_t)ME_C;  // a non-tail chunk is always full
       }
-      *lp = L;
+    } else if (lane == 0) {
+      bk.chdr[prv].next = nxt;
+      bk.chdr[nxt].prev = prv;
     }
+    L.head = nh;
+    L.tail = nt;
+    if (lane == 0) c.lv[lvl] = L;
     free_chunk(c, ch);
   } else {
-    if (lane == 0) {
-      bk.chdr[ch].bel = bel_pack(bel_begin(bel), bel_end(bel), live);
-      *lp = L;
-    }
+    if (lane == 0) c.lv[lvl] = L;
   }
   c.resting_delta -= 1;
   return q;
@@ -616,11 +667,19 @@ __device__ __forceinline__ void write_result(const BatchDev& bt, uint32_t i, int
   }
 }
 
+// Bytes of LDS one wave needs to hold its symbol's ladder (levels + occupancy + tail fill).
+__host__ __device__ constexpr size_t lds_wave_bytes(uint32_t L) {
+  return (size_t)L * sizeof(Level) + (size_t)(L / 64) * 8 + (size_t)L;
+}
+
 // One wavefront per symbol (4 per workgroup). Block s/4, wave s%4. Symbol S is the reject bin
-// of records whose symbol id is out of range.
+// of records whose symbol id is out of range. kLds: the symbol's ladder is staged in LDS.
+template <bool kLds>
 __global__ __launch_bounds__(256) void k_match(BookDev bk, BatchDev bt) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = lane_id();
-  const uint32_t s = blockIdx.x * 4u + (threadIdx.x >> 6);
+  const uint32_t wv = threadIdx.x >> 6;
+  const uint32_t s = blockIdx.x * 4u + wv;
   if (s > bk.S) return;
   const uint32_t lo = wave_lower_bound(bt.skeys, bt.n, s);
   const uint32_t hi = wave_lower_bound(bt.skeys, bt.n, s + 1);
@@ -641,15 +700,41 @@ __global__ __launch_bounds__(256) void k_match(BookDev bk, BatchDev bt) {
     }
     return;
   }
+  const uint32_t L = bk.L;
+  Level* g_lv = bk.levels + (size_t)s * L;
+  unsigned long long* g_occ = bk.occ + (size_t)s * bk.Lwords;
+  uint8_t* g_tend = bk.tend + (size_t)s * L;
   WaveCtx c;
+#ifdef ME_STAMPS
+  for (int p = 0; p < PH_N; ++p) c.st[p] = 0;
+  STAMP_MARK(c);
+#endif
   c.bk = bk;
   c.s = s;
+  if (kLds) {
+    unsigned char* base = smem + (size_t)wv * lds_wave_bytes(L);
+    c.lv = (Level*)base;
+    c.occ = (unsigned long long*)(base + (size_t)L * sizeof(Level));
+    c.tend = base + (size_t)L * sizeof(Level) + (size_t)(L / 64) * 8;
+    for (uint32_t i = lane; i < L; i += 64) {
+      c.lv[i] = g_lv[i];
+      c.tend[i] = g_tend[i];
+    }
+    for (uint32_t i = lane; i < bk.Lwords; i += 64) c.occ[i] = g_occ[i];
+    wave_mem_order();
+  } else {
+    c.lv = g_lv;
+    c.occ = g_occ;
+    c.tend = g_tend;
+  }
   c.gs = bk.gsym ? bk.gsym[s] : s;
   const SymState st = bk.sym[s];
   c.base = rli64(st.base, 0);
   c.bb = rli32(st.best_bid, 0);
   c.ba = rli32(st.best_ask, 0);
   c.free_head = rl32(st.free_head, 0);
+  prefetch_free_next(c);
+  c.bump_cur = c.bump_end = 0;
   c.resting_delta = 0;
   c.scratch = bt.scratch;
   // scratch run of this wave: fills <= resting makers + 2 * records
@@ -662,29 +747,34 @@ __global__ __launch_bounds__(256) void k_match(BookDev bk, BatchDev bt) {
     return;
   }
   c.wptr = w0;
-  const long long L = (long long)bk.L;
+  STAMP_ADD(c, PH_PROLOGUE);
+  const long long Lw = (long long)L;
 
-  for (uint32_t blk = lo; blk < hi; blk += 64) {
+  bool ok = true;
+  for (uint32_t blk = lo; blk < hi && ok; blk += 64) {
     const uint32_t j = blk + (uint32_t)lane;
     const bool v = j < hi;
     const uint32_t oi = v ? bt.perm[j] : 0u;
     const unsigned long long oseq = v ? bt.seq[oi] : 0ull;
     const long long opx = v ? bt.px[oi] : 0ll;
     const int oq = v ? bt.qty[oi] : 0;
-    const uint32_t ok = v ? (uint32_t)bt.kind[oi] : 0u;
+    const uint32_t ok_ = v ? (uint32_t)bt.kind[oi] : 0u;
     const uint32_t cnt = min(64u, hi - blk);
+    STAMP_ADD(c, PH_FETCH);
     for (uint32_t k = 0; k < cnt; ++k) {
       const uint32_t i = rl32(oi, (int)k);
       const unsigned long long seq = rl64(oseq, (int)k);
       const long long px = rli64(opx, (int)k);
       const int q = rli32(oq, (int)k);
-      const uint32_t kind = rl32(ok, (int)k);
+      const uint32_t kind = rl32(ok_, (int)k);
+      c.recs_left = hi - (blk + k);
       const uint32_t side = kind & 3u;
       const bool market = (kind >> 2) & 1u;
       const bool cancel = (kind >> 3) & 1u;
       const unsigned long long fstart = c.wptr;
       if (cancel) {
         const int got = cancel_order(c, (unsigned long long)px);
+        STAMP_ADD(c, PH_CANCEL);
         if (got > 0)
           write_result(bt, i, 0, got, 0, ME_ST_CANCELED, ME_RJ_NONE, fstart);
         else
@@ -701,7 +791,7 @@ __global__ __launch_bounds__(256) void k_match(BookDev bk, BatchDev bt) {
       }
       int li = 0;
       if (!market) {
-        if (px < c.base || (unsigned long long)px - (unsigned long long)c.base >= (unsigned long long)L) {
+        if (px < c.base || (unsigned long long)px - (unsigned long long)c.base >= (unsigned long long)Lw) {
           write_result(bt, i, 0, q, 0, ME_ST_REJECTED, ME_RJ_OUT_OF_WINDOW, fstart);
           continue;
         }
@@ -712,22 +802,37 @@ __global__ __launch_bounds__(256) void k_match(BookDev bk, BatchDev bt) {
         continue;
       }
       const bool buy = side == ME_SIDE_BUY;
-      const int lim = market ? (buy ? (int)L - 1 : 0) : li;
+      const int lim = market ? (buy ? (int)Lw - 1 : 0) : li;
       uint32_t nfill = 0;
       const long long got = sweep(c, buy ? 1 : -1, lim, (long long)q, seq, nfill);
+      STAMP_ADD(c, PH_SWEEP);
       const int filled = (int)got;
       const int rem = q - filled;
-      uint8_t st;
+      uint8_t stt;
       if (market) {
-        st = rem == 0 ? ME_ST_FILLED : ME_ST_CANCELED;
+        stt = rem == 0 ? ME_ST_FILLED : ME_ST_CANCELED;
       } else {
-        if (rem > 0) {
-          if (!rest_order(c, li, seq, rem, buy)) return;  // chunk pool exhausted: batch fails
+        const bool rested = rem > 0 && !rest_order(c, li, seq, rem, buy);
+        STAMP_ADD(c, PH_REST);
+        if (rested) {
+          ok = false;  // chunk pool exhausted: the batch fails (sticky error word)
+          break;
         }
-        st = rem == 0 ? ME_ST_FILLED : (filled > 0 ? ME_ST_PARTIALLY_FILLED : ME_ST_NEW);
+        stt = rem == 0 ? ME_ST_FILLED : (filled > 0 ? ME_ST_PARTIALLY_FILLED : ME_ST_NEW);
       }
-      write_result(bt, i, filled, rem, nfill, st, ME_RJ_NONE, fstart);
+      write_result(bt, i, filled, rem, nfill, stt, ME_RJ_NONE, fstart);
+      STAMP_ADD(c, PH_RESULT);
     }
+  }
+  // return unused bump-reserved chunks to this symbol's free list
+  while (c.bump_cur < c.bump_end) free_chunk(c, c.bump_cur++);
+  if (kLds) {
+    wave_mem_order();
+    for (uint32_t i = lane; i < L; i += 64) {
+      g_lv[i] = c.lv[i];
+      g_tend[i] = c.tend[i];
+    }
+    for (uint32_t i = lane; i < bk.Lwords; i += 64) g_occ[i] = c.occ[i];
   }
   if (lane == 0) {
     SymState o;
@@ -739,6 +844,11 @@ __global__ __launch_bounds__(256) void k_match(BookDev bk, BatchDev bt) {
     o.pad[0] = o.pad[1] = 0;
     bk.sym[s] = o;
   }
+#ifdef ME_STAMPS
+  STAMP_ADD(c, PH_EPILOGUE);
+  if (lane == 0 && bk.dbg)
+    for (int p = 0; p < PH_N; ++p) bk.dbg[(size_t)s * 16 + p] = c.st[p];
+#endif
 }
 
 // ------------------------------------------------------------------ tape compaction
@@ -821,7 +931,13 @@ hipError_t launch_sort_pass(hipStream_t st, const uint32_t* keys_in, const uint3
 
 hipError_t launch_match(hipStream_t st, const BookDev& bk, const BatchDev& bt) {
   const uint32_t waves = bk.S + 1;
-  hipLaunchKernelGGL(k_match, dim3((waves + 3) / 4), dim3(256), 0, st, bk, bt);
+  const dim3 grid((waves + 3) / 4), block(256);
+  if (bk.L <= LDS_MAX_LEVELS) {
+    const size_t lds = 4 * lds_wave_bytes(bk.L);
+    hipLaunchKernelGGL(k_match<true>, grid, block, lds, st, bk, bt);
+  } else {
+    hipLaunchKernelGGL(k_match<false>, grid, block, 0, st, bk, bt);
+  }
   return hipGetLastError();
 }
 

@@ -9,10 +9,11 @@
 //                   a level's side is implied by its position.
 //   occ    [S][L/64] occupancy bitmap of the ladder (bit set <=> total > 0).
 //   sym    [S]      32 B per-symbol scalars (window base, best bid/ask level, chunk free list).
+//   tend   [S][L]   slots written in each level's tail chunk (appends need no chunk read).
 //   chunks [NC]     FIFO storage: a level's queue is a doubly linked list of chunks of ME_C
 //                   slots {seq u64, qty i32} (SoA: cseq / cqty); a wave reads one chunk per load.
-//                   Every linked chunk holds >= 1 live order (a chunk emptied by cancels is
-//                   unlinked at once), so chunks in use <= resting orders.
+//                   A slot is live iff qty > 0. Every linked chunk holds >= 1 live order (a chunk
+//                   emptied by cancels is unlinked at once), so chunks in use <= resting orders.
 //   loc    [max_seq] seq -> global slot (chunk * ME_C + slot) for cancels.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -27,6 +28,7 @@ constexpr uint32_t NIL = 0xFFFFFFFFu;
 constexpr int TILE_SORT = 4096;          // records per workgroup in the grouping sort
 constexpr int TILE_TAPE = 1024;          // records per workgroup in the tape compaction
 constexpr int MAX_DIGIT_BITS = 11;       // radix digit width (LDS histogram of 2048 bins)
+constexpr uint32_t LDS_MAX_LEVELS = 1024; // ladders up to this depth are staged in LDS (17.5 KB/wave)
 
 // Sticky error bits (BookDev::err).
 enum : uint32_t {
@@ -45,14 +47,8 @@ struct alignas(16) ChunkHdr {
   uint32_t next;   // next chunk of the level FIFO, or of the symbol free list
   uint32_t prev;   // previous chunk of the level FIFO (NIL at the head)
   uint32_t level;  // level index the chunk belongs to
-  uint32_t bel;    // begin (first possibly-live slot) | end (slots written) << 8 | live << 16
+  uint32_t pad;
 };
-__host__ __device__ inline uint32_t bel_pack(uint32_t b, uint32_t e, uint32_t live) {
-  return b | (e << 8) | (live << 16);
-}
-__host__ __device__ inline uint32_t bel_begin(uint32_t v) { return v & 0xFFu; }
-__host__ __device__ inline uint32_t bel_end(uint32_t v) { return (v >> 8) & 0xFFu; }
-__host__ __device__ inline uint32_t bel_live(uint32_t v) { return (v >> 16) & 0xFFu; }
 
 struct alignas(32) SymState {
   long long base;      // price_q4 of level 0
@@ -66,6 +62,7 @@ struct alignas(32) SymState {
 struct BookDev {
   Level* levels;
   unsigned long long* occ;
+  uint8_t* tend;          // [S][L] slots written in the level's tail chunk (valid when tail != NIL)
   SymState* sym;
   ChunkHdr* chdr;
   uint32_t* owner;        // [NC] symbol that allocated the chunk (chunks never change symbol)
@@ -75,6 +72,7 @@ struct BookDev {
   uint32_t* chunk_top;
   uint32_t* err;
   const uint32_t* gsym;  // [S] id written into me_fill.symbol
+  unsigned long long* dbg;  // [S][8] phase cycles, diagnostic (-DME_STAMPS) builds only
   unsigned long long max_seq;
   uint32_t nchunks;
   uint32_t S;

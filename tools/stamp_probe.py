@@ -1,0 +1,56 @@
+"""Diagnostic: phase cycle shares of k_match from the -DME_STAMPS build (never the product).
+
+    ME_ENGINE_LIB=matching_engine_amd/build/libme_engine_stamps.so python tools/stamp_probe.py [--config 2]
+"""
+import argparse
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import matching_engine_amd as me  # noqa: E402
+
+PH = ["prologue", "fetch", "sweep", "walk", "rest", "cancel", "result", "epilogue", "sw_window", "sw_update",
+      "sw_jump", "sw_best", "-", "-", "-", "-"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--batches", type=int, default=30)
+    ap.add_argument("--symbols", type=int, default=0)
+    a = ap.parse_args()
+    assert "stamps" in me._abi.LIB_PATH, "set ME_ENGINE_LIB to the stamps build"
+    over = {"num_symbols": a.symbols} if a.symbols else {}
+    sc = me.preset(a.config, **over)
+    st = me.Stream(sc)
+    base = st.base_prices()
+    lib = me._abi.load()
+    lib.me_debug_stamps.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
+    eng = me.Engine(sc.num_symbols, sc.levels, base, max_batch=sc.batch, max_resting=1 << 22, max_seq=1 << 30)
+    buf = np.zeros(sc.num_symbols * 16, dtype=np.uint64)
+    tot = np.zeros(16, dtype=np.float64)
+    maxwave = []
+    norders = 0
+    for k in range(a.batches):
+        b = st.next(sc.batch)
+        eng.submit_batch(b, want_fills=False)
+        if k < 5:
+            continue  # warm
+        lib.me_debug_stamps(eng.h, buf.ctypes.data, buf.size)
+        m = buf.reshape(-1, 16).astype(np.float64)
+        tot += m.sum(0)
+        maxwave.append(m.sum(1).max())
+        norders += len(b)
+    share = tot / tot.sum()
+    per_order = tot / norders
+    print(f"config {a.config}: {norders} orders, {sc.num_symbols} symbols")
+    for p, s_, c in zip(PH, share, per_order):
+        print(f"  {p:9s} {100 * s_:6.2f}%  {c:9.1f} cycles/order")
+    print(f"  total {tot.sum() / norders:.1f} cycles/order/wave; slowest wave {np.mean(maxwave):.0f} cycles/batch")
+
+
+if __name__ == "__main__":
+    main()
