@@ -233,7 +233,7 @@ extern "C" me_engine* me_create(const me_config* cfg) {
   bk.Lwords = (uint32_t)(L / 64);
   bk.nchunks = (uint32_t)nchunks;
   bk.max_seq = cfg->max_seq;
-  const uint32_t ntiles_sort = (uint32_t)((n + TILE_SORT - 1) / TILE_SORT);
+  const uint32_t ntiles_sort = MAX_SORT_TILES;
   const uint32_t ntiles_tape = (uint32_t)((n + TILE_TAPE - 1) / TILE_TAPE);
 #define ALLOC(p, cnt)                                                              \
   do {                                                                             \

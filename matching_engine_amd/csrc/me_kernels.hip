@@ -1,7 +1,8 @@
 // me_kernels.hip — gfx950 kernels of the batched matching core.
 //
 // One batch (n records, ascending seq) goes through:
-//   1. k_sort_hist / k_sort_scatter  stable LSD counting sort of the records by symbol
+//   1. k_sort_hist / k_sort_offsets / k_sort_scatter
+//                                    stable LSD counting sort of the records by symbol
 //                                    (1 pass for <= 2047 symbols, 2 passes up to 4M): groups
 //                                    every symbol's records contiguously, seq order kept.
 //   2. k_match                       one wavefront per symbol walks its records in seq order
@@ -110,25 +111,31 @@ __device__ uint32_t wave_lower_bound(const uint32_t* keys, uint32_t n, uint32_t 
 }
 
 // ------------------------------------------------------------------ grouping sort
-// Pass histogram: per-tile digit counts, stored bin-major [bin][tile].
-__global__ __launch_bounds__(256) void k_sort_hist(const uint32_t* __restrict__ keys_in, uint32_t n,
-                                                   uint32_t clamp_key, int shift, int dbits,
-                                                   uint32_t* __restrict__ hist, uint32_t ntiles,
-                                                   uint32_t* zero_buf, uint32_t zero_words,
-                                                   unsigned long long* scratch_top) {
+// One pass of a stable LSD counting sort of the batch by symbol id. digit(key) =
+// (min(key, clamp) >> shift) & mask over nbins <= 2048 bins (the last pass uses only the bins that
+// occur). Three launches: per-tile histograms -> one-workgroup exclusive scan of the histogram
+// matrix in bin-major order (= global start of every (bin, tile) run) -> stable scatter.
+struct SortPass {
+  uint32_t shift, mask, nbins, tile, ntiles, clamp;
+};
+
+__device__ __forceinline__ uint32_t sort_digit(uint32_t k, const SortPass& p) {
+  if (k > p.clamp) k = p.clamp;
+  return (k >> p.shift) & p.mask;
+}
+
+// Per-tile histograms, bin-major [bin][tile].
+__global__ __launch_bounds__(256) void k_sort_hist(const uint32_t* __restrict__ keys_in, uint32_t n, SortPass p,
+                                                   uint32_t* __restrict__ hist, uint32_t* zero_buf,
+                                                   uint32_t zero_words, unsigned long long* scratch_top) {
   __shared__ uint32_t h[1u << MAX_DIGIT_BITS];
-  const uint32_t nb = 1u << dbits, mask = nb - 1;
-  for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) h[b] = 0;
+  for (uint32_t b = threadIdx.x; b < p.nbins; b += blockDim.x) h[b] = 0;
   __syncthreads();
-  const uint32_t t0 = blockIdx.x * TILE_SORT;
-  const uint32_t t1 = min(n, t0 + TILE_SORT);
-  for (uint32_t i = t0 + threadIdx.x; i < t1; i += blockDim.x) {
-    uint32_t k = keys_in[i];
-    if (k > clamp_key) k = clamp_key;
-    atomicAdd(&h[(k >> shift) & mask], 1u);
-  }
+  const uint32_t t0 = blockIdx.x * p.tile;
+  const uint32_t t1 = min(n, t0 + p.tile);
+  for (uint32_t i = t0 + threadIdx.x; i < t1; i += blockDim.x) atomicAdd(&h[sort_digit(keys_in[i], p)], 1u);
   __syncthreads();
-  for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) hist[(size_t)b * ntiles + blockIdx.x] = h[b];
+  for (uint32_t b = threadIdx.x; b < p.nbins; b += blockDim.x) hist[(size_t)b * p.ntiles + blockIdx.x] = h[b];
   // Per-batch resets folded into the first kernel of the batch.
   if (zero_buf) {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < zero_words; i += gridDim.x * blockDim.x)
@@ -144,7 +151,6 @@ __device__ uint32_t block_excl_scan_lds(uint32_t* a, uint32_t cnt, uint32_t* wsu
   uint32_t b0 = tid * per, local = 0;
   for (uint32_t j = 0; j < per; ++j)
     if (b0 + j < cnt) local += a[b0 + j];
-  // wave inclusive scan of local
   uint32_t x = local;
   for (int d = 1; d < 64; d <<= 1) {
     uint32_t t = __shfl_up(x, d, 64);
@@ -168,76 +174,74 @@ __device__ uint32_t block_excl_scan_lds(uint32_t* a, uint32_t cnt, uint32_t* wsu
   return total;
 }
 
-// Stable scatter of one tile: dest = (#keys with smaller digit) + (#equal-digit keys in earlier
-// tiles) + (#equal-digit keys earlier in this tile). Each wave owns a quarter of the tile and
-// ranks 64 records at a time with a ballot multisplit (one ballot per digit bit).
+// In-place exclusive scan of the histogram matrix (count = nbins * ntiles), one workgroup of
+// 1024 threads: each thread owns a contiguous run, runs are combined by a wave + LDS scan.
+__global__ __launch_bounds__(1024) void k_sort_offsets(uint32_t* __restrict__ hist, uint32_t count) {
+  __shared__ uint32_t wsum[16];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint32_t per = (count + 1023) / 1024;
+  const uint32_t b0 = tid * per, b1 = min(count, b0 + per);
+  uint32_t local = 0;
+  for (uint32_t j = b0; j < b1; ++j) local += hist[j];
+  uint32_t x = local;
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t t = __shfl_up(x, d, 64);
+    if (lane >= d) x += t;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  uint32_t run = x - local;
+  for (uint32_t k = 0; k < w; ++k) run += wsum[k];
+  for (uint32_t j = b0; j < b1; ++j) {
+    const uint32_t v = hist[j];
+    hist[j] = run;
+    run += v;
+  }
+}
+
+// Stable scatter of one tile: dest = start of this tile's run of its digit (k_sort_offsets) +
+// rank among equal digits earlier in the tile. Each wave owns a quarter of the tile and ranks
+// 64 records at a time with a ballot multisplit (one ballot per digit bit).
 __global__ __launch_bounds__(256) void k_sort_scatter(const uint32_t* __restrict__ keys_in,
-                                                      const uint32_t* __restrict__ idx_in, uint32_t n,
-                                                      uint32_t clamp_key, int shift, int dbits,
-                                                      const uint32_t* __restrict__ hist, uint32_t ntiles,
+                                                      const uint32_t* __restrict__ idx_in, uint32_t n, SortPass p,
+                                                      uint32_t dbits, const uint32_t* __restrict__ offsets,
                                                       uint32_t* __restrict__ keys_out,
                                                       uint32_t* __restrict__ idx_out) {
-  __shared__ uint32_t base[1u << MAX_DIGIT_BITS];
   __shared__ uint32_t wcnt[4][1u << MAX_DIGIT_BITS];
-  __shared__ uint32_t wsum[4];
-  const uint32_t nb = 1u << dbits, mask = nb - 1;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const uint32_t tile = blockIdx.x;
-  // 1) column sums of the histogram: total per bin and count in earlier tiles
-  for (uint32_t b = tid; b < nb; b += 256) {
-    const uint32_t* row = hist + (size_t)b * ntiles;
-    uint32_t tot = 0, before = 0;
-    for (uint32_t t = 0; t < ntiles; ++t) {
-      uint32_t v = row[t];
-      tot += v;
-      before += (t < tile) ? v : 0u;
-    }
-    base[b] = tot;
-    wcnt[0][b] = before;
-  }
+  for (uint32_t b = tid; b < p.nbins; b += 256) wcnt[0][b] = wcnt[1][b] = wcnt[2][b] = wcnt[3][b] = 0;
   __syncthreads();
-  // 2) exclusive scan of bin totals -> bin start; plus earlier-tile count
-  block_excl_scan_lds(base, nb, wsum);
-  for (uint32_t b = tid; b < nb; b += 256) base[b] += wcnt[0][b];
-  __syncthreads();
-  // 3) per-wave histogram of the tile quarters
-  for (uint32_t b = tid; b < nb; b += 256) wcnt[0][b] = wcnt[1][b] = wcnt[2][b] = wcnt[3][b] = 0;
-  __syncthreads();
-  const uint32_t t0 = tile * TILE_SORT, t1 = min(n, t0 + TILE_SORT);
-  const uint32_t q = TILE_SORT / 4;
+  const uint32_t t0 = tile * p.tile, t1 = min(n, t0 + p.tile);
+  const uint32_t q = p.tile / 4;
   const uint32_t w0 = min(t1, t0 + w * q), w1 = min(t1, w0 + q);
-  for (uint32_t i = w0 + lane; i < w1; i += 64) {
-    uint32_t k = keys_in[i];
-    if (k > clamp_key) k = clamp_key;
-    atomicAdd(&wcnt[w][(k >> shift) & mask], 1u);
-  }
+  for (uint32_t i = w0 + lane; i < w1; i += 64) atomicAdd(&wcnt[w][sort_digit(keys_in[i], p)], 1u);
   __syncthreads();
-  // 4) per-bin prefix over the 4 waves
-  for (uint32_t b = tid; b < nb; b += 256) {
-    uint32_t run = base[b];
+  // per-bin start of each wave's quarter
+  for (uint32_t b = tid; b < p.nbins; b += 256) {
+    uint32_t run = offsets[(size_t)b * p.ntiles + tile];
     for (int k = 0; k < 4; ++k) {
-      uint32_t c = wcnt[k][b];
+      const uint32_t c = wcnt[k][b];
       wcnt[k][b] = run;
       run += c;
     }
   }
   __syncthreads();
-  // 5) ranked scatter, 64 records per step, in record order
   for (uint32_t c0 = w0; c0 < w1; c0 += 64) {
-    uint32_t i = c0 + lane;
-    bool v = i < w1;
+    const uint32_t i = c0 + lane;
+    const bool v = i < w1;
     uint32_t k = v ? keys_in[i] : 0u;
-    if (k > clamp_key) k = clamp_key;
-    uint32_t val = v ? (idx_in ? idx_in[i] : i) : 0u;
-    uint32_t d = (k >> shift) & mask;
+    if (k > p.clamp) k = p.clamp;
+    const uint32_t val = v ? (idx_in ? idx_in[i] : i) : 0u;
+    const uint32_t d = (k >> p.shift) & p.mask;
     unsigned long long peers = __ballot(v);
-    for (int bit = 0; bit < dbits; ++bit) {
-      unsigned long long bb = __ballot((d >> bit) & 1u);
+    for (uint32_t bit = 0; bit < dbits; ++bit) {
+      const unsigned long long bb = __ballot((d >> bit) & 1u);
       peers &= ((d >> bit) & 1u) ? bb : ~bb;
     }
-    uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
-    uint32_t cnt = (uint32_t)__popcll(peers);
-    uint32_t start = v ? wcnt[w][d] : 0u;
+    const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
+    const uint32_t cnt = (uint32_t)__popcll(peers);
+    const uint32_t start = v ? wcnt[w][d] : 0u;
     if (v) {
       keys_out[start + rank] = k;
       idx_out[start + rank] = val;
@@ -339,8 +343,12 @@ __device__ __forceinline__ void free_chunk(WaveCtx& c, uint32_t ch) {
   c.free_head = ch;
 }
 
+// Issue the load of chdr[free_head].next without waiting for it: the value stays in a VGPR and is
+// only read (readlane -> s_waitcnt) by the next pop, usually many records later.
 __device__ __forceinline__ void prefetch_free_next(WaveCtx& c) {
-  c.free_next = (c.free_head < c.bk.nchunks) ? rl32(c.bk.chdr[c.free_head].next, 0) : NIL;
+  const bool ok = c.free_head < c.bk.nchunks;
+  const uint32_t v = c.bk.chdr[ok ? c.free_head : 0].next;
+  c.free_next = ok ? v : NIL;
 }
 
 __device__ __forceinline__ uint32_t alloc_chunk(WaveCtx& c) {
@@ -350,7 +358,7 @@ __device__ __forceinline__ uint32_t alloc_chunk(WaveCtx& c) {
       set_err(c.bk, ERR_INCONSISTENT);
       return NIL;
     }
-    c.free_head = c.free_next;
+    c.free_head = rl32(c.free_next, 0);
     prefetch_free_next(c);  // consumed by the next pop, usually much later
     return ch;
   }
@@ -403,7 +411,8 @@ __device__ uint32_t walk_level(WaveCtx& c, int lvl, long long take, uint32_t hea
       set_err(bk, ERR_INCONSISTENT);
       return NIL;
     }
-    const uint32_t nxt = rl32(bk.chdr[ch].next, 0);
+    // issue every load of the chunk before the first use (one round trip, not two)
+    const uint32_t nxt_v = bk.chdr[ch].next;
     const bool act = lane < ME_C;
     const size_t g = (size_t)ch * ME_C + (act ? lane : 0);
     const int qv = act ? bk.cqty[g] : 0;
@@ -426,7 +435,7 @@ __device__ uint32_t walk_level(WaveCtx& c, int lvl, long long take, uint32_t hea
         if (need > 0) set_err(bk, ERR_INCONSISTENT);
         return NIL;
       }
-      ch = nxt;
+      ch = rl32(nxt_v, 0);
     } else if (need > 0) {  // impossible: a live slot remains only once the take is met
       set_err(bk, ERR_INCONSISTENT);
       return ch;
@@ -448,6 +457,35 @@ __device__ long long sweep(WaveCtx& c, int dir, int lim, long long want, unsigne
   int cur = (dir > 0) ? c.ba : c.bb;
   bool emptied = false;
   const unsigned long long w_start = c.wptr;
+  // fast path: the best level alone fills the taker (no window scan)
+  if (dir > 0 ? (cur <= lim && cur < (int)bk.L) : (cur >= lim && cur >= 0)) {
+    Level B = c.lv[cur];
+    const long long btot = rli64(B.total, 0);
+    if (btot >= want) {
+      const uint32_t head = rl32(B.head, 0), tail = rl32(B.tail, 0);
+      STAMP_ADD(c, PH_SWEEP);
+      const uint32_t nh = walk_level(c, cur, want, head, tail, taker);
+      STAMP_ADD(c, PH_WALK);
+      const long long ntot = btot - want;
+      if (lane == 0) {
+        Level o;
+        o.total = ntot;
+        o.head = ntot ? nh : NIL;
+        o.tail = ntot ? tail : NIL;
+        c.lv[cur] = o;
+      }
+      if (ntot == 0) {
+        occ_clear(c, cur);
+        wave_mem_order();
+        if (dir > 0)
+          c.ba = next_occ(c, cur + 1);
+        else
+          c.bb = prev_occ(c, cur - 1);
+      }
+      nfill = (uint32_t)(c.wptr - w_start);
+      return want;
+    }
+  }
   while (rem > 0) {
     if (dir > 0 ? (cur > lim || cur >= (int)bk.L) : (cur < lim || cur < 0)) break;
     const int lv = cur + dir * lane;
@@ -917,15 +955,29 @@ __global__ void k_init_levels(Level* lv, size_t count) {
 // ------------------------------------------------------------------ launch wrappers (host)
 namespace me {
 
+// tile = records per sort workgroup: >= 1024 and large enough that ntiles <= 256
+uint32_t sort_tile(uint32_t n) {
+  uint32_t t = 1024;
+  while ((n + t - 1) / t > 256) t <<= 1;
+  return t;
+}
+
 hipError_t launch_sort_pass(hipStream_t st, const uint32_t* keys_in, const uint32_t* idx_in, uint32_t n,
                             uint32_t clamp_key, int shift, int dbits, uint32_t* hist, uint32_t* keys_out,
                             uint32_t* idx_out, uint32_t* zero_buf, uint32_t zero_words,
                             unsigned long long* scratch_top) {
-  const uint32_t ntiles = (n + TILE_SORT - 1) / TILE_SORT;
-  hipLaunchKernelGGL(k_sort_hist, dim3(ntiles), dim3(256), 0, st, keys_in, n, clamp_key, shift, dbits, hist,
-                     ntiles, zero_buf, zero_words, scratch_top);
-  hipLaunchKernelGGL(k_sort_scatter, dim3(ntiles), dim3(256), 0, st, keys_in, idx_in, n, clamp_key, shift,
-                     dbits, hist, ntiles, keys_out, idx_out);
+  SortPass p;
+  p.shift = (uint32_t)shift;
+  p.mask = (1u << dbits) - 1u;
+  p.nbins = min(1u << dbits, (clamp_key >> shift) + 1u);
+  p.tile = sort_tile(n);
+  p.ntiles = (n + p.tile - 1) / p.tile;
+  p.clamp = clamp_key;
+  hipLaunchKernelGGL(k_sort_hist, dim3(p.ntiles), dim3(256), 0, st, keys_in, n, p, hist, zero_buf, zero_words,
+                     scratch_top);
+  hipLaunchKernelGGL(k_sort_offsets, dim3(1), dim3(1024), 0, st, hist, p.nbins * p.ntiles);
+  hipLaunchKernelGGL(k_sort_scatter, dim3(p.ntiles), dim3(256), 0, st, keys_in, idx_in, n, p, (uint32_t)dbits, hist,
+                     keys_out, idx_out);
   return hipGetLastError();
 }
 

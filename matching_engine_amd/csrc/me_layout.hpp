@@ -25,8 +25,8 @@ namespace me {
 
 constexpr int ME_C = 16;                 // slots per chunk (one wave-load of qty + seq)
 constexpr uint32_t NIL = 0xFFFFFFFFu;
-constexpr int TILE_SORT = 4096;          // records per workgroup in the grouping sort
-constexpr int TILE_TAPE = 1024;          // records per workgroup in the tape compaction
+constexpr int MAX_SORT_TILES = 256;      // sort tiles per pass (tile = records / workgroup >= 1024)
+constexpr int TILE_TAPE = 256;           // records per workgroup in the tape compaction
 constexpr int MAX_DIGIT_BITS = 11;       // radix digit width (LDS histogram of 2048 bins)
 constexpr uint32_t LDS_MAX_LEVELS = 1024; // ladders up to this depth are staged in LDS (17.5 KB/wave)
 

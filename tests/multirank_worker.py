@@ -1,0 +1,76 @@
+"""One rank of the multi-GPU sharding check (launched by tests/test_multirank.py).
+
+Each rank owns the symbols splitmix64(symbol) % world == rank, runs its shard of the global
+stream through a per-shard book, and the per-shard tapes/results are gathered to rank 0
+(torch.distributed, gloo) and merged; rank 0 compares with ONE book over the whole stream.
+
+env: RANK, WORLD_SIZE, MASTER_ADDR, MASTER_PORT; argv: ENGINE(oracle|gpu) OUT_JSON
+  oracle: the per-shard book is the CPU oracle (CPU test of the split/gather/merge host logic)
+  gpu:    the per-shard book is the HIP engine on cuda:0 (all ranks share the box's one GPU)
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    engine_kind, out_path = sys.argv[1], sys.argv[2]
+    import torch.distributed as dist
+
+    import matching_engine_amd as me
+    from matching_engine_amd.sharding import ShardPlan, merge_results, merge_tapes
+    from oracle.oracle import OracleBook
+
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    S, nb = 300, 5
+    sc = me.preset(5, num_symbols=S, batch=6000)
+    st = me.Stream(sc)
+    base = st.base_prices()
+    plan = ShardPlan(S, world)
+    ids = plan.members[rank]
+    max_seq = 1 << 20
+    if engine_kind == "gpu":
+        book = me.Engine(len(ids), sc.levels, base[ids], max_batch=sc.batch, max_resting=1 << 16, max_seq=max_seq,
+                         symbol_ids=ids)
+        submit = book.submit_batch
+    else:
+        book = OracleBook(len(ids), sc.levels, base[ids], max_seq, symbol_ids=ids)
+        submit = book.submit
+    ref = OracleBook(S, sc.levels, base, max_seq) if rank == 0 else None
+    ok, fills_total = True, 0
+    msg = ""
+    for k in range(nb):
+        b = st.next(sc.batch)
+        # a few out-of-range symbol ids too: rejected as BAD_SYMBOL on shard 0
+        if k == 1:
+            b.symbol[::997] = S + 5
+        lb, pos = plan.split(b)[rank]
+        r, f = submit(lb)
+        got = [None] * world
+        dist.all_gather_object(got, (r, pos, f))
+        if rank == 0:
+            tape = merge_tapes([g[2] for g in got])
+            res = merge_results(len(b), [(g[0], g[1]) for g in got])
+            ro, fo = ref.submit(b)
+            fills_total += len(fo)
+            same_t = len(tape) == len(fo) and bool(np.all(tape == fo))
+            same_r = all(np.array_equal(res[x], ro[x]) for x in
+                         ("filled_qty", "remaining_qty", "fill_count", "tape_offset", "status", "reason"))
+            if not (same_t and same_r):
+                ok = False
+                msg = f"batch {k}: tape equal {same_t}, results equal {same_r}"
+                break
+    if rank == 0:
+        json.dump({"ok": ok, "msg": msg, "fills": fills_total, "world": world}, open(out_path, "w"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
