@@ -1,0 +1,78 @@
+/*
+ * me_service.h — the SubmitOrder drop-in: MatchingEngineServiceImpl's request path re-hosted on
+ * the batched GPU core (C-ABI, plain C structs mirroring the proto messages, no gRPC types).
+ *
+ *   me_service_create         MatchingEngineServiceImpl(db_path) + Impl ctor
+ *                             (src/server/matching_engine_service.cpp:17-22, :36): opens/creates the
+ *                             SQLite DB with the reference pragmas + schema (src/storage/storage.cpp:9-69)
+ *                             and seeds the OID counter from MAX(OID)+1 (storage.cpp:254-267).
+ *   me_service_submit_order   SubmitOrder (matching_engine_service.cpp:41-121): identical validation
+ *                             order and strings (:66-83), OID allocation (:85, consumed even when
+ *                             normalisation throws), normalize_to_q4 (:89-97), side CHECK -> "DB insert
+ *                             failed" with order_id set (:107-111). The order joins the open time slice.
+ *   me_service_flush          the time-slice batcher: runs the slice through the engine and ingests the
+ *                             whole batch in ONE SQLite transaction (orders rows as insert_new_order
+ *                             writes them, final status/remaining from the match, fills rows, maker
+ *                             status updates) — the batched rewrite of storage.cpp:78-208.
+ *   me_service_book           GetOrderBook (matching_engine_service.cpp:123-129) from the GPU book.
+ */
+#ifndef ME_SERVICE_H
+#define ME_SERVICE_H
+
+#include "me_engine.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* OrderRequest (proto/matching_engine.proto:37-45). */
+typedef struct me_order_request {
+  const char* client_id;
+  const char* symbol;
+  int32_t order_type; /* OrderType; != LIMIT is MARKET */
+  int32_t side;       /* Side */
+  int64_t price;      /* raw scaled integer */
+  int32_t scale;
+  int32_t quantity;
+} me_order_request;
+
+/* OrderResponse (proto:47-51) + the gRPC status code of the call. */
+typedef struct me_order_response {
+  char order_id[32];      /* "OID-<n>", empty when none was allocated */
+  int32_t success;
+  int32_t grpc_status;    /* 0 OK; 2 UNKNOWN: normalize_to_q4 threw (price.hpp:16,23-24) */
+  char error_message[64];
+} me_order_response;
+
+typedef struct me_service me_service;
+
+/* engine: the shard the slices are matched on (NULL: submit works, flush fails loudly).
+ * symbols[num_symbols]: symbol strings of the engine's local ids 0..num_symbols-1.
+ * db_path: SQLite file (NULL: no persistence). */
+me_service* me_service_create(me_engine* engine, const char* const* symbols, uint32_t num_symbols,
+                              const char* db_path);
+void me_service_destroy(me_service* s);
+
+/* Always returns 0 (the RPC itself succeeded or failed in-band, like the reference). */
+int me_service_submit_order(me_service* s, const me_order_request* req, me_order_response* resp);
+
+/* Orders waiting in the open time slice. */
+size_t me_service_pending(const me_service* s);
+/* Next OID number the service will allocate. */
+uint64_t me_service_next_oid(const me_service* s);
+
+/* Match the open slice and persist it. Any output may be NULL; *n_results = records matched
+ * (order of submission), out_seq[i] their numeric OIDs. */
+int me_service_flush(me_service* s, me_fill* out_fills, size_t fills_cap, size_t* n_fills,
+                     me_order_result* out_results, uint64_t* out_seq, size_t results_cap, size_t* n_results);
+
+/* GetOrderBook for a symbol string (top depth levels per side). */
+int me_service_book(me_service* s, const char* symbol, me_level* bids, me_level* asks, size_t depth,
+                    size_t* n_bids, size_t* n_asks);
+
+int me_service_last_error(const me_service* s, char* buf, size_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ME_SERVICE_H */

@@ -12,3 +12,4 @@ from ._abi import (  # noqa: F401
 from .engine import (  # noqa: F401
     Batch, DeviceBatch, Engine, EngineError, Stream, StreamConfig, normalize_to_q4, preset, shard_of, shard_table,
 )
+from .service import MatchingEngineService, ServiceError  # noqa: F401,E402

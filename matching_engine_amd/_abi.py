@@ -156,3 +156,37 @@ def load() -> C.CDLL:
 
 def ptr(a: np.ndarray) -> int:
     return a.ctypes.data
+
+
+# ---- include/me_service.h ---------------------------------------------------------------------
+class MeOrderRequest(C.Structure):
+    _fields_ = [
+        ("client_id", C.c_char_p),
+        ("symbol", C.c_char_p),
+        ("order_type", C.c_int32),
+        ("side", C.c_int32),
+        ("price", C.c_int64),
+        ("scale", C.c_int32),
+        ("quantity", C.c_int32),
+    ]
+
+
+class MeOrderResponse(C.Structure):
+    _fields_ = [
+        ("order_id", C.c_char * 32),
+        ("success", C.c_int32),
+        ("grpc_status", C.c_int32),
+        ("error_message", C.c_char * 64),
+    ]
+
+
+PROTOTYPES.update({
+    "me_service_create": (_P, [_P, C.POINTER(C.c_char_p), C.c_uint32, C.c_char_p]),
+    "me_service_destroy": (None, [_P]),
+    "me_service_submit_order": (C.c_int, [_P, C.POINTER(MeOrderRequest), C.POINTER(MeOrderResponse)]),
+    "me_service_pending": (_SZ, [_P]),
+    "me_service_next_oid": (C.c_uint64, [_P]),
+    "me_service_flush": (C.c_int, [_P, _P, _SZ, C.POINTER(_SZ), _P, _P, _SZ, C.POINTER(_SZ)]),
+    "me_service_book": (C.c_int, [_P, C.c_char_p, _P, _P, _SZ, C.POINTER(_SZ), C.POINTER(_SZ)]),
+    "me_service_last_error": (C.c_int, [_P, C.c_char_p, _SZ]),
+})

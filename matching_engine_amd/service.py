@@ -1,0 +1,86 @@
+"""MatchingEngineService — Python view of include/me_service.h, the SubmitOrder drop-in
+(src/server/matching_engine_service.cpp:41-121 re-hosted on the batched GPU core)."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _abi
+from ._abi import FILL_DTYPE, LEVEL_DTYPE, RESULT_DTYPE, MeOrderRequest, MeOrderResponse, ptr
+
+
+class ServiceError(RuntimeError):
+    pass
+
+
+class MatchingEngineService:
+    """SubmitOrder / GetOrderBook over one engine shard; SQLite persistence when db_path is given."""
+
+    def __init__(self, engine, symbols, db_path=None):
+        self.lib = _abi.load()
+        self.engine = engine
+        self.symbols = list(symbols)
+        arr = (C.c_char_p * len(self.symbols))(*[s.encode() for s in self.symbols])
+        self._arr = arr
+        self.h = self.lib.me_service_create(engine.h if engine is not None else None, arr, len(self.symbols),
+                                            db_path.encode() if db_path else None)
+        err = self.last_error()
+        if db_path and err:
+            raise ServiceError(err)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.me_service_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def last_error(self) -> str:
+        buf = C.create_string_buffer(1024)
+        self.lib.me_service_last_error(self.h, buf, 1024)
+        return buf.value.decode(errors="replace")
+
+    def submit_order(self, client_id, symbol, order_type, side, price, scale, quantity) -> dict:
+        """OrderRequest -> OrderResponse fields + grpc status (0 OK, 2 UNKNOWN)."""
+        req = MeOrderRequest(client_id.encode(), symbol.encode(), order_type, side, price, scale, quantity)
+        resp = MeOrderResponse()
+        self.lib.me_service_submit_order(self.h, C.byref(req), C.byref(resp))
+        return {"order_id": resp.order_id.decode(), "success": bool(resp.success),
+                "error_message": resp.error_message.decode(), "grpc_status": resp.grpc_status}
+
+    @property
+    def pending(self) -> int:
+        return int(self.lib.me_service_pending(self.h))
+
+    @property
+    def next_oid(self) -> int:
+        return int(self.lib.me_service_next_oid(self.h))
+
+    def flush(self):
+        """Match + persist the open time slice -> (seq[n], results[n], fills[k])."""
+        n = self.pending
+        res = np.zeros(max(n, 1), dtype=RESULT_DTYPE)
+        seq = np.zeros(max(n, 1), dtype=np.uint64)
+        cap = (self.engine.fill_bound(n) if self.engine is not None else 0) + 1
+        fills = np.zeros(cap, dtype=FILL_DTYPE)
+        nf, nr = C.c_size_t(0), C.c_size_t(0)
+        rc = self.lib.me_service_flush(self.h, ptr(fills), cap, C.byref(nf), ptr(res), ptr(seq), len(res),
+                                       C.byref(nr))
+        if rc != 0:
+            raise ServiceError(f"flush failed ({rc}): {self.last_error()}")
+        return seq[: nr.value].copy(), res[: nr.value].copy(), fills[: nf.value].copy()
+
+    def get_order_book(self, symbol, depth=10):
+        bids = np.zeros(depth, dtype=LEVEL_DTYPE)
+        asks = np.zeros(depth, dtype=LEVEL_DTYPE)
+        nb, na = C.c_size_t(0), C.c_size_t(0)
+        rc = self.lib.me_service_book(self.h, symbol.encode(), ptr(bids), ptr(asks), depth, C.byref(nb),
+                                      C.byref(na))
+        if rc != 0:
+            raise ServiceError(self.last_error())
+        return bids[: nb.value], asks[: na.value]
