@@ -273,8 +273,8 @@ extern "C" me_engine* me_create(const me_config* cfg) {
   ALLOC(e->d_tape_count, 1);
   ALLOC(e->d_fills_acc, 1);
 #ifdef ME_STAMPS
-  ALLOC(bk.dbg, S * 16);
-  (void)hipMemset(bk.dbg, 0, S * 16 * 8);
+  ALLOC(bk.dbg, S * 24);
+  (void)hipMemset(bk.dbg, 0, S * 24 * 8);
 #endif
 #undef ALLOC
   e->scratch_cap = scap;
@@ -687,7 +687,7 @@ extern "C" int me_last_error(const me_engine* e, char* buf, size_t cap) {
 extern "C" int me_debug_stamps(me_engine* e, unsigned long long* out, size_t n) {
   if (!e || !e->bk.dbg) return ME_E_INVALID;
   HIP_TRY(hipStreamSynchronize(e->stream), "sync");
-  size_t k = std::min(n, (size_t)e->bk.S * 16);
+  size_t k = std::min(n, (size_t)e->bk.S * 24);
   HIP_TRY(hipMemcpy(out, e->bk.dbg, k * 8, hipMemcpyDeviceToHost), "D2H stamps");
   return ME_OK;
 }

@@ -66,7 +66,8 @@ __device__ __forceinline__ void wave_mem_order() { __builtin_amdgcn_fence(__ATOM
 // Diagnostic build only (-DME_STAMPS): per-wave cycle shares of the matching phases, read with
 // me_debug_stamps(). The product build compiles every stamp away.
 enum { PH_PROLOGUE, PH_FETCH, PH_SWEEP, PH_WALK, PH_REST, PH_CANCEL, PH_RESULT, PH_EPILOGUE,
-       PH_SW_WINDOW, PH_SW_UPDATE, PH_SW_JUMP, PH_SW_BEST, PH_N };
+       PH_SW_WINDOW, PH_SW_UPDATE, PH_SW_JUMP, PH_SW_BEST, CT_MISS, CT_WALK, CT_EVICT, CT_FAST,
+       WK_GET, WK_SCAN, WK_EMIT, WK_TAIL, PH_N };
 #ifdef ME_STAMPS
 __device__ __forceinline__ unsigned long long stamp_now() {
   unsigned long long t;
@@ -76,6 +77,7 @@ __device__ __forceinline__ unsigned long long stamp_now() {
   return t;
 }
 #define STAMP_MARK(c) (c).st_t = stamp_now()
+#define COUNT(c, ct) ((c).st[ct] += 1)
 #define STAMP_ADD(c, ph)                    \
   do {                                      \
     unsigned long long _n = stamp_now();    \
@@ -85,6 +87,7 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 #else
 #define STAMP_MARK(c) ((void)0)
 #define STAMP_ADD(c, ph) ((void)0)
+#define COUNT(c, ct) ((void)0)
 #endif
 
 // First index p in [0, n) with keys[p] >= key (keys ascending), by a 64-ary search:
@@ -177,25 +180,40 @@ __device__ uint32_t block_excl_scan_lds(uint32_t* a, uint32_t cnt, uint32_t* wsu
 // In-place exclusive scan of the histogram matrix (count = nbins * ntiles), one workgroup of
 // 1024 threads: each thread owns a contiguous run, runs are combined by a wave + LDS scan.
 __global__ __launch_bounds__(1024) void k_sort_offsets(uint32_t* __restrict__ hist, uint32_t count) {
+  // 16 waves; wave w owns the contiguous segment [w*seg, (w+1)*seg), read 64 consecutive words per
+  // wave-load (coalesced: one CU's address path handles whole lines, not 64 scattered ones).
   __shared__ uint32_t wsum[16];
   const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const uint32_t per = (count + 1023) / 1024;
-  const uint32_t b0 = tid * per, b1 = min(count, b0 + per);
+  const uint32_t seg = ((count + 16 * 64 - 1) / (16 * 64)) * 64;
+  const uint32_t s0 = min(count, w * seg), s1 = min(count, s0 + seg);
   uint32_t local = 0;
-  for (uint32_t j = b0; j < b1; ++j) local += hist[j];
-  uint32_t x = local;
-  for (int d = 1; d < 64; d <<= 1) {
-    uint32_t t = __shfl_up(x, d, 64);
-    if (lane >= d) x += t;
+  for (uint32_t j = s0; j < s1; j += 8 * 64) {
+    uint32_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint32_t i = j + u * 64 + lane;
+      v[u] = hist[min(i, count - 1)];  // clamp the index, never branch around a load
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) local += (j + u * 64 + lane < s1) ? v[u] : 0u;
   }
-  if (lane == 63) wsum[w] = x;
+  for (int d = 32; d >= 1; d >>= 1) local += __shfl_xor(local, d, 64);
+  if (lane == 0) wsum[w] = local;
   __syncthreads();
-  uint32_t run = x - local;
-  for (uint32_t k = 0; k < w; ++k) run += wsum[k];
-  for (uint32_t j = b0; j < b1; ++j) {
-    const uint32_t v = hist[j];
-    hist[j] = run;
-    run += v;
+  uint32_t carry = 0;
+  for (uint32_t k = 0; k < w; ++k) carry += wsum[k];
+  for (uint32_t j = s0; j < s1; j += 8 * 64) {
+    uint32_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = hist[min(j + u * 64 + lane, count - 1)];  // 8 loads in flight
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint32_t i = j + u * 64 + lane;
+      const uint32_t x = i < s1 ? v[u] : 0u;
+      const uint32_t inc = (uint32_t)wave_incl_scan((long long)x);
+      if (i < s1) hist[i] = carry + inc - x;
+      carry += rl32(inc, 63);
+    }
   }
 }
 
@@ -253,13 +271,177 @@ __global__ __launch_bounds__(256) void k_sort_scatter(const uint32_t* __restrict
 }
 
 // ------------------------------------------------------------------ matching
-// Where a wave's view of its symbol's ladder lives: LDS (L <= LDS_MAX_LEVELS, staged in at
-// kernel start and written back at the end) or HBM (deep windows).
+// Head-chunk cache (LDS): entry (lvl & cmask) holds the FIFO head chunk of one level — its 16
+// slot quantities/seqs and its next pointer — so walks and appends on top-of-book levels stay
+// on chip. The HBM copy is stale while an entry is dirty; write-back on eviction, on free
+// (freed chunks must hold qty 0 in HBM) and at kernel end. With the register ladder (L <= 128)
+// every level has its own entry (no evictions).
+constexpr int CK_MEM = 64;  // entries with the LDS ladder (direct-mapped by level)
+constexpr int CK_REG = 128;
+struct alignas(16) CacheEntry {
+  uint32_t cid;    // cached chunk id, NIL = empty
+  uint32_t dirty;  // slots differ from HBM
+  uint32_t next;   // chdr[cid].next (kept in sync by set_next)
+  uint32_t pad;
+  int qty[ME_C];
+  unsigned long long seq[ME_C];
+};
+
+// ---- ladders: where a wave keeps its symbol's price levels ---------------------------------
+// LadderMem: levels / occupancy / tail-fill arrays behind pointers (LDS for L <= 1024, else HBM).
+struct LadderMem {
+  Level* lv;
+  unsigned long long* occ;
+  uint8_t* tend;
+  uint32_t L, Lwords;
+
+  __device__ __forceinline__ Level get(int l) const {
+    Level x = lv[l];
+    x.total = rli64(x.total, 0);
+    x.head = rl32(x.head, 0);
+    x.tail = rl32(x.tail, 0);
+    return x;
+  }
+  __device__ __forceinline__ void set(int l, const Level& x) {
+    if (lane_id() == 0) lv[l] = x;
+  }
+  __device__ __forceinline__ uint32_t get_te(int l) const { return rl32((uint32_t)tend[l], 0); }
+  __device__ __forceinline__ void set_te(int l, uint32_t v) {
+    if (lane_id() == 0) tend[l] = (uint8_t)v;
+  }
+  __device__ __forceinline__ void occ_set(int l) {
+    if (lane_id() == 0) occ[l >> 6] |= (1ull << (l & 63));
+  }
+  __device__ __forceinline__ void occ_clear(int l) {
+    if (lane_id() == 0) occ[l >> 6] &= ~(1ull << (l & 63));
+  }
+  // Smallest occupied level >= x, or L.
+  __device__ int next_occ(int x) const {
+    const int Li = (int)L;
+    if (x >= Li) return Li;
+    if (x < 0) x = 0;
+    wave_mem_order();
+    int w = x >> 6;
+    unsigned long long word = occ[w] & (~0ull << (x & 63));
+    if (word) return (w << 6) + __builtin_ctzll(word);
+    const int lane = lane_id();
+    const int nw = (int)Lwords;
+    for (int b = w + 1; b < nw; b += 64) {
+      int idx = b + lane;
+      unsigned long long v = idx < nw ? occ[idx] : 0ull;
+      unsigned long long m = __ballot(v != 0ull);
+      if (m) {
+        int t = __builtin_ctzll(m);
+        unsigned long long wv = rl64(v, t);
+        return ((b + t) << 6) + __builtin_ctzll(wv);
+      }
+    }
+    return Li;
+  }
+  // Largest occupied level <= x, or -1.
+  __device__ int prev_occ(int x) const {
+    if (x < 0) return -1;
+    if (x >= (int)L) x = (int)L - 1;
+    wave_mem_order();
+    int w = x >> 6;
+    int r = x & 63;
+    unsigned long long keep = (r == 63) ? ~0ull : ((1ull << (r + 1)) - 1ull);
+    unsigned long long word = occ[w] & keep;
+    if (word) return (w << 6) + 63 - __builtin_clzll(word);
+    const int lane = lane_id();
+    for (int t0 = w - 1; t0 >= 0; t0 -= 64) {
+      int idx = t0 - lane;
+      unsigned long long v = idx >= 0 ? occ[idx] : 0ull;
+      unsigned long long m = __ballot(v != 0ull);
+      if (m) {
+        int t = __builtin_ctzll(m);
+        unsigned long long wv = rl64(v, t);
+        return ((t0 - t) << 6) + 63 - __builtin_clzll(wv);
+      }
+    }
+    return -1;
+  }
+};
+
+// LadderReg (L <= 128): level l lives in lane (l & 63) of register row (l >> 6). Reads are
+// readlanes, writes are per-lane selects, occupancy is a ballot of the totals: the whole ladder
+// bookkeeping runs on the VALU/SALU with no memory round trip.
+struct LadderReg {
+  long long t0, t1;  // total
+  uint32_t h0, h1;   // head chunk
+  uint32_t l0, l1;   // tail chunk
+  uint32_t e0, e1;   // slots written in the tail chunk
+  uint32_t L;
+
+  __device__ __forceinline__ Level get(int l) const {
+    const int j = l & 63;
+    Level x;
+    if (l < 64) {
+      x.total = rli64(t0, j);
+      x.head = rl32(h0, j);
+      x.tail = rl32(l0, j);
+    } else {
+      x.total = rli64(t1, j);
+      x.head = rl32(h1, j);
+      x.tail = rl32(l1, j);
+    }
+    return x;
+  }
+  __device__ __forceinline__ void set(int l, const Level& x) {
+    const bool me = lane_id() == (l & 63);
+    if (l < 64) {
+      t0 = me ? x.total : t0;
+      h0 = me ? x.head : h0;
+      l0 = me ? x.tail : l0;
+    } else {
+      t1 = me ? x.total : t1;
+      h1 = me ? x.head : h1;
+      l1 = me ? x.tail : l1;
+    }
+  }
+  __device__ __forceinline__ uint32_t get_te(int l) const { return l < 64 ? rl32(e0, l & 63) : rl32(e1, l & 63); }
+  __device__ __forceinline__ void set_te(int l, uint32_t v) {
+    const bool me = lane_id() == (l & 63);
+    if (l < 64)
+      e0 = me ? v : e0;
+    else
+      e1 = me ? v : e1;
+  }
+  __device__ __forceinline__ void occ_set(int) {}
+  __device__ __forceinline__ void occ_clear(int) {}
+  __device__ __forceinline__ int next_occ(int x) const {
+    if (x >= (int)L) return (int)L;
+    if (x < 0) x = 0;
+    const unsigned long long m0 = __ballot(t0 > 0), m1 = __ballot(t1 > 0);
+    if (x < 64) {
+      const unsigned long long w = m0 & (~0ull << x);
+      if (w) return __builtin_ctzll(w);
+      return m1 ? 64 + __builtin_ctzll(m1) : (int)L;
+    }
+    const unsigned long long w = m1 & (~0ull << (x - 64));
+    return w ? 64 + __builtin_ctzll(w) : (int)L;
+  }
+  __device__ __forceinline__ int prev_occ(int x) const {
+    if (x < 0) return -1;
+    if (x >= (int)L) x = (int)L - 1;
+    const unsigned long long m0 = __ballot(t0 > 0), m1 = __ballot(t1 > 0);
+    if (x >= 64) {
+      const int r = x - 64;
+      const unsigned long long w = m1 & ((r == 63) ? ~0ull : ((1ull << (r + 1)) - 1ull));
+      if (w) return 64 + 63 - __builtin_clzll(w);
+      return m0 ? 63 - __builtin_clzll(m0) : -1;
+    }
+    const unsigned long long w = m0 & ((x == 63) ? ~0ull : ((1ull << (x + 1)) - 1ull));
+    return w ? 63 - __builtin_clzll(w) : -1;
+  }
+};
+
+template <class Lad>
 struct WaveCtx {
   BookDev bk;
-  Level* lv;                 // [L] ladder of this symbol (LDS or HBM)
-  unsigned long long* occ;   // [L/64] occupancy bitmap
-  uint8_t* tend;             // [L] slots written in each level's tail chunk
+  Lad lad;
+  CacheEntry* cache;         // head-chunk cache in LDS, or nullptr (HBM ladder)
+  uint32_t cmask;            // cache entry of level l = l & cmask
   uint32_t s;                // local symbol
   uint32_t gs;               // symbol id written in fills
   long long base;
@@ -277,67 +459,105 @@ struct WaveCtx {
 #endif
 };
 
-// Smallest occupied level >= x, or L.
-__device__ int next_occ(const WaveCtx& c, int x) {
-  const int L = (int)c.bk.L;
-  if (x >= L) return L;
-  if (x < 0) x = 0;
-  const unsigned long long* occ = c.occ;
-  int w = x >> 6;
-  unsigned long long word = occ[w] & (~0ull << (x & 63));
-  if (word) return (w << 6) + __builtin_ctzll(word);
-  const int lane = lane_id();
-  const int nw = (int)c.bk.Lwords;
-  for (int b = w + 1; b < nw; b += 64) {
-    int idx = b + lane;
-    unsigned long long v = idx < nw ? occ[idx] : 0ull;
-    unsigned long long m = __ballot(v != 0ull);
-    if (m) {
-      int t = __builtin_ctzll(m);
-      unsigned long long wv = rl64(v, t);
-      return ((b + t) << 6) + __builtin_ctzll(wv);
-    }
-  }
-  return L;
-}
-
-// Largest occupied level <= x, or -1.
-__device__ int prev_occ(const WaveCtx& c, int x) {
-  if (x < 0) return -1;
-  if (x >= (int)c.bk.L) x = (int)c.bk.L - 1;
-  const unsigned long long* occ = c.occ;
-  int w = x >> 6;
-  int r = x & 63;
-  unsigned long long keep = (r == 63) ? ~0ull : ((1ull << (r + 1)) - 1ull);
-  unsigned long long word = occ[w] & keep;
-  if (word) return (w << 6) + 63 - __builtin_clzll(word);
-  const int lane = lane_id();
-  for (int t0 = w - 1; t0 >= 0; t0 -= 64) {
-    int idx = t0 - lane;
-    unsigned long long v = idx >= 0 ? occ[idx] : 0ull;
-    unsigned long long m = __ballot(v != 0ull);
-    if (m) {
-      int t = __builtin_ctzll(m);
-      unsigned long long wv = rl64(v, t);
-      return ((t0 - t) << 6) + 63 - __builtin_clzll(wv);
-    }
-  }
-  return -1;
-}
-
-__device__ __forceinline__ void occ_set(const WaveCtx& c, int lvl) {
-  if (lane_id() == 0) c.occ[lvl >> 6] |= (1ull << (lvl & 63));
-}
-__device__ __forceinline__ void occ_clear(const WaveCtx& c, int lvl) {
-  if (lane_id() == 0) c.occ[lvl >> 6] &= ~(1ull << (lvl & 63));
-}
-
 __device__ __forceinline__ void set_err(const BookDev& bk, uint32_t bits) {
   if (lane_id() == 0) atomicOr(bk.err, bits);
 }
 
+// ---- head-chunk cache -------------------------------------------------------------------
+template <class C>
+__device__ __forceinline__ CacheEntry* centry(const C& c, int lvl) { return c.cache + ((uint32_t)lvl & c.cmask); }
+
+template <class C>
+__device__ __forceinline__ bool cache_holds(const C& c, int lvl, uint32_t ch) {
+  return c.cache && rl32(centry(c, lvl)->cid, 0) == ch;
+}
+
+template <class C>
+__device__ __forceinline__ void cache_writeback(const C& c, CacheEntry* E) {
+  const uint32_t cid = rl32(E->cid, 0);
+  if (cid == NIL || !rl32(E->dirty, 0)) return;
+  const int lane = lane_id();
+  if (lane < ME_C) {
+    const size_t g = (size_t)cid * ME_C + lane;
+    c.bk.cqty[g] = E->qty[lane];
+    c.bk.cseq[g] = E->seq[lane];
+  }
+}
+
+// Make `ch` (the head chunk of level lvl) the cached chunk of its entry; returns the entry.
+template <class C>
+__device__ CacheEntry* cache_get(C& c, int lvl, uint32_t ch) {
+  CacheEntry* E = centry(c, lvl);
+  const uint32_t cur = rl32(E->cid, 0);
+  if (cur == ch) return E;
+  COUNT(c, CT_MISS);
+  if (cur != NIL) COUNT(c, CT_EVICT);
+  cache_writeback(c, E);
+  const int lane = lane_id();
+  const bool act = lane < ME_C;
+  const size_t g = (size_t)ch * ME_C + (act ? lane : 0);
+  const int q = act ? c.bk.cqty[g] : 0;
+  const unsigned long long sq = act ? c.bk.cseq[g] : 0ull;
+  const uint32_t nx = c.bk.chdr[ch].next;
+  if (act) {
+    E->qty[lane] = q;
+    E->seq[lane] = sq;
+  }
+  if (lane == 0) {
+    E->cid = ch;
+    E->dirty = 0;
+    E->next = nx;
+  }
+  wave_mem_order();
+  return E;
+}
+
+// A brand-new (all-empty) chunk becomes the head of an empty level: install it without a load.
+template <class C>
+__device__ void cache_install_new(C& c, int lvl, uint32_t ch) {
+  CacheEntry* E = centry(c, lvl);
+  cache_writeback(c, E);
+  const int lane = lane_id();
+  if (lane < ME_C) {
+    E->qty[lane] = 0;
+    E->seq[lane] = 0ull;
+  }
+  if (lane == 0) {
+    E->cid = ch;
+    E->dirty = 1;
+    E->next = NIL;
+  }
+  wave_mem_order();
+}
+
+// The cached chunk of lvl (if it is ch) is being freed or unlinked: HBM must hold its final
+// (all-zero) quantities before the chunk is reused.
+template <class C>
+__device__ __forceinline__ void cache_drop(C& c, int lvl, uint32_t ch) {
+  if (!c.cache) return;
+  CacheEntry* E = centry(c, lvl);
+  if (rl32(E->cid, 0) != ch) return;
+  cache_writeback(c, E);
+  if (lane_id() == 0) E->cid = NIL;
+  wave_mem_order();
+}
+
+// chdr[ch].next = v, mirrored into the cache entry of lvl when it holds ch.
+template <class C>
+__device__ __forceinline__ void set_next(C& c, int lvl, uint32_t ch, uint32_t v) {
+  if (lane_id() == 0) {
+    c.bk.chdr[ch].next = v;
+    if (c.cache) {
+      CacheEntry* E = centry(c, lvl);
+      if (E->cid == ch) E->next = v;
+    }
+  }
+}
+
+// ---- chunk allocation -------------------------------------------------------------------
 // Free-list push: the popped-next is known without a load.
-__device__ __forceinline__ void free_chunk(WaveCtx& c, uint32_t ch) {
+template <class C>
+__device__ __forceinline__ void free_chunk(C& c, uint32_t ch) {
   if (lane_id() == 0) c.bk.chdr[ch].next = c.free_head;
   c.free_next = c.free_head;
   c.free_head = ch;
@@ -345,13 +565,15 @@ __device__ __forceinline__ void free_chunk(WaveCtx& c, uint32_t ch) {
 
 // Issue the load of chdr[free_head].next without waiting for it: the value stays in a VGPR and is
 // only read (readlane -> s_waitcnt) by the next pop, usually many records later.
-__device__ __forceinline__ void prefetch_free_next(WaveCtx& c) {
+template <class C>
+__device__ __forceinline__ void prefetch_free_next(C& c) {
   const bool ok = c.free_head < c.bk.nchunks;
   const uint32_t v = c.bk.chdr[ok ? c.free_head : 0].next;
   c.free_next = ok ? v : NIL;
 }
 
-__device__ __forceinline__ uint32_t alloc_chunk(WaveCtx& c) {
+template <class C>
+__device__ __forceinline__ uint32_t alloc_chunk(C& c) {
   if (c.free_head != NIL) {
     const uint32_t ch = c.free_head;
     if (ch >= c.bk.nchunks) {
@@ -379,8 +601,9 @@ __device__ __forceinline__ uint32_t alloc_chunk(WaveCtx& c) {
 }
 
 // Append one fill per lane where e holds, in lane order, to the wave's scratch run.
-__device__ __forceinline__ void emit_fills(WaveCtx& c, bool e, unsigned long long taker,
-                                           unsigned long long maker, long long price, int qty) {
+template <class C>
+__device__ __forceinline__ void emit_fills(C& c, bool e, unsigned long long taker, unsigned long long maker,
+                                           long long price, int qty) {
   unsigned long long m = __ballot(e);
   if (e) {
     unsigned long long pos = c.wptr + (unsigned long long)__popcll(m & lanemask_lt());
@@ -396,46 +619,71 @@ __device__ __forceinline__ void emit_fills(WaveCtx& c, bool e, unsigned long lon
 }
 
 // Consume `take` (> 0, <= level total) from the FIFO of level `lvl`, oldest first. A slot is
-// live iff its qty > 0 (consumed, cancelled and unwritten slots hold 0), so one round trip loads
-// a chunk's header and all ME_C slots together; the slots are ranked with one wave prefix scan.
-// Exhausted chunks go back to the free list. Returns the new head chunk (NIL: level emptied).
-__device__ uint32_t walk_level(WaveCtx& c, int lvl, long long take, uint32_t head, uint32_t tail,
+// live iff its qty > 0 (consumed, cancelled and unwritten slots hold 0). A chunk's 16 slots are
+// ranked with one wave prefix scan; with the cache they come from LDS, otherwise one HBM round
+// trip loads header and slots together. Exhausted chunks go back to the free list. Returns the
+// new head chunk (NIL: level emptied).
+template <class C>
+__device__ uint32_t walk_level(C& c, int lvl, long long take, uint32_t head, uint32_t tail,
                                unsigned long long taker) {
   const int lane = lane_id();
   const BookDev& bk = c.bk;
   const long long price = c.base + lvl;
+  const bool act = lane < ME_C;
   long long need = take;
   uint32_t ch = head;
+  COUNT(c, CT_WALK);
   while (need > 0) {
     if (ch >= bk.nchunks) {  // NIL or corrupt: never index with it
       set_err(bk, ERR_INCONSISTENT);
       return NIL;
     }
-    // issue every load of the chunk before the first use (one round trip, not two)
-    const uint32_t nxt_v = bk.chdr[ch].next;
-    const bool act = lane < ME_C;
+    CacheEntry* E = nullptr;
+    int qv;
+    unsigned long long sv;
+    uint32_t nxt_v;
     const size_t g = (size_t)ch * ME_C + (act ? lane : 0);
-    const int qv = act ? bk.cqty[g] : 0;
-    const unsigned long long sv = act ? bk.cseq[g] : 0ull;
+    STAMP_ADD(c, PH_WALK);
+    if (c.cache) {
+      E = cache_get(c, lvl, ch);
+      STAMP_ADD(c, WK_GET);
+      qv = act ? E->qty[lane] : 0;
+      sv = act ? E->seq[lane] : 0ull;
+      nxt_v = E->next;
+    } else {
+      nxt_v = bk.chdr[ch].next;  // issue every load of the chunk before the first use
+      qv = act ? bk.cqty[g] : 0;
+      sv = act ? bk.cseq[g] : 0ull;
+    }
     const long long inc = wave_incl_scan((long long)qv);
     const long long ex = inc - qv;
     long long f = need - ex;
     if (f < 0) f = 0;
     if (f > qv) f = qv;
     const bool fe = f > 0;
+    STAMP_ADD(c, WK_SCAN);
     emit_fills(c, fe, taker, sv, price, (int)f);
-    if (fe) bk.cqty[g] = qv - (int)f;
+    if (E) {
+      if (fe) E->qty[lane] = qv - (int)f;
+      if (lane == 0) E->dirty = 1;
+    } else if (fe) {
+      bk.cqty[g] = qv - (int)f;
+    }
     c.resting_delta -= __popcll(__ballot(fe && f == qv));  // makers filled completely leave the book
     const long long live = rli64(inc, 63);
     need -= (need < live ? need : live);
     const unsigned long long alive = __ballot((qv - f) > 0);
+    STAMP_ADD(c, WK_EMIT);
     if (!alive) {  // every slot of the chunk is consumed
+      cache_drop(c, lvl, ch);
       free_chunk(c, ch);
       if (ch == tail) {
         if (need > 0) set_err(bk, ERR_INCONSISTENT);
+        STAMP_ADD(c, WK_TAIL);
         return NIL;
       }
       ch = rl32(nxt_v, 0);
+      STAMP_ADD(c, WK_TAIL);
     } else if (need > 0) {  // impossible: a live slot remains only once the take is met
       set_err(bk, ERR_INCONSISTENT);
       return ch;
@@ -445,125 +693,153 @@ __device__ uint32_t walk_level(WaveCtx& c, int lvl, long long take, uint32_t hea
   return ch;
 }
 
-// Sweep the opposite side for a taker. dir = +1 (BUY: asks upward from best_ask) or
-// -1 (SELL: bids downward from best_bid). lim = last level the taker may trade at.
-// Lanes cover 64 consecutive levels; an inclusive scan of their totals gives how far the taker
-// reaches; fully consumed levels are emptied, the last one partially.
-__device__ long long sweep(WaveCtx& c, int dir, int lim, long long want, unsigned long long taker,
-                           uint32_t& nfill) {
+// Write back level lvl after `take` was consumed from it.
+template <class C>
+__device__ __forceinline__ void level_after_take(C& c, int lvl, long long ntot, uint32_t nh, uint32_t tail) {
+  Level o;
+  o.total = ntot;
+  o.head = ntot ? nh : NIL;
+  o.tail = ntot ? tail : NIL;
+  c.lad.set(lvl, o);
+  if (ntot == 0) c.lad.occ_clear(lvl);
+}
+
+// Consume `take` at level lvl whose header is (tot, head, tail); returns true if it emptied.
+template <class C>
+__device__ __forceinline__ bool take_level(C& c, int lvl, long long tot, long long take, uint32_t head,
+                                           uint32_t tail, unsigned long long taker) {
+  STAMP_ADD(c, PH_SWEEP);
+  const uint32_t nh = walk_level(c, lvl, take, head, tail, taker);
+  STAMP_ADD(c, PH_WALK);
+  level_after_take(c, lvl, tot - take, nh, tail);
+  STAMP_ADD(c, PH_SW_UPDATE);
+  return tot == take;
+}
+
+// Sweep the opposite side for a taker. dir = +1 (BUY: asks upward from best_ask) or -1 (SELL:
+// bids downward from best_bid); lim = last level the taker may trade at. Returns qty filled.
+// LadderMem: 64-level windows — lanes load consecutive levels, an inclusive scan of their totals
+// says how far the taker reaches. LadderReg: one masked scan over the register-resident ladder.
+template <class C>
+__device__ long long sweep(C& c, int dir, int lim, long long want, unsigned long long taker, uint32_t& nfill) {
   const int lane = lane_id();
-  const BookDev& bk = c.bk;
+  const int L = (int)c.bk.L;
   long long rem = want;
   int cur = (dir > 0) ? c.ba : c.bb;
   bool emptied = false;
   const unsigned long long w_start = c.wptr;
-  // fast path: the best level alone fills the taker (no window scan)
-  if (dir > 0 ? (cur <= lim && cur < (int)bk.L) : (cur >= lim && cur >= 0)) {
-    Level B = c.lv[cur];
-    const long long btot = rli64(B.total, 0);
-    if (btot >= want) {
-      const uint32_t head = rl32(B.head, 0), tail = rl32(B.tail, 0);
-      STAMP_ADD(c, PH_SWEEP);
-      const uint32_t nh = walk_level(c, cur, want, head, tail, taker);
-      STAMP_ADD(c, PH_WALK);
-      const long long ntot = btot - want;
-      if (lane == 0) {
-        Level o;
-        o.total = ntot;
-        o.head = ntot ? nh : NIL;
-        o.tail = ntot ? tail : NIL;
-        c.lv[cur] = o;
-      }
-      if (ntot == 0) {
-        occ_clear(c, cur);
-        wave_mem_order();
+  nfill = 0;
+  if (dir > 0 ? (cur > lim || cur >= L) : (cur < lim || cur < 0)) return 0;  // does not cross
+  // fast path: the best level alone fills the taker (no scan)
+  {
+    const Level B = c.lad.get(cur);
+    if (B.total >= want) {
+      COUNT(c, CT_FAST);
+      if (take_level(c, cur, B.total, want, B.head, B.tail, taker)) {
         if (dir > 0)
-          c.ba = next_occ(c, cur + 1);
+          c.ba = c.lad.next_occ(cur + 1);
         else
-          c.bb = prev_occ(c, cur - 1);
+          c.bb = c.lad.prev_occ(cur - 1);
+        STAMP_ADD(c, PH_SW_BEST);
       }
       nfill = (uint32_t)(c.wptr - w_start);
       return want;
     }
   }
-  while (rem > 0) {
-    if (dir > 0 ? (cur > lim || cur >= (int)bk.L) : (cur < lim || cur < 0)) break;
-    const int lv = cur + dir * lane;
-    const bool valid = (dir > 0) ? (lv <= lim && lv < (int)bk.L) : (lv >= lim && lv >= 0);
-    Level L;
-    L.total = 0;
-    L.head = NIL;
-    L.tail = NIL;
-    if (valid) L = c.lv[lv];
-    const long long tot = L.total;
-    const long long inc = wave_incl_scan(tot);
-    const long long ex = inc - tot;
-    const long long rem0 = rem;
-    unsigned long long tm = __ballot(valid && tot > 0 && ex < rem0);
+  if constexpr (__is_same(decltype(c.lad), LadderReg)) {
+    // masked totals of the levels the taker may reach, in natural lane order (row 0 = levels
+    // 0..63, row 1 = 64..127); prefix for BUY (upward), suffix for SELL (downward)
+    const int lo = dir > 0 ? cur : lim, hi = dir > 0 ? lim : cur;
+    const int l0v = lane, l1v = 64 + lane;
+    const long long m0 = (l0v >= lo && l0v <= hi) ? c.lad.t0 : 0;
+    const long long m1 = (l1v >= lo && l1v <= hi && l1v < L) ? c.lad.t1 : 0;
+    const long long i0 = wave_incl_scan(m0);
+    const long long c0 = rli64(i0, 63);
+    const long long i1 = wave_incl_scan(m1) + c0;
+    const long long all = rli64(i1, 63);
+    // amount strictly before a level in sweep order
+    const long long b0 = dir > 0 ? i0 - m0 : all - i0;
+    const long long b1 = dir > 0 ? i1 - m1 : all - i1;
+    unsigned long long t0m = __ballot(m0 > 0 && b0 < want);
+    unsigned long long t1m = __ballot(m1 > 0 && b1 < want);
     STAMP_ADD(c, PH_SW_WINDOW);
-    while (tm) {
-      const int t = __builtin_ctzll(tm);
-      tm &= tm - 1;
-      const int lvl = cur + dir * t;
-      const long long ltot = rli64(tot, t);
-      const long long lex = rli64(ex, t);
-      long long take = rem0 - lex;
-      if (take > ltot) take = ltot;
-      const uint32_t head = rl32(L.head, t), tail = rl32(L.tail, t);
-      STAMP_ADD(c, PH_SWEEP);
-      const uint32_t nh = walk_level(c, lvl, take, head, tail, taker);
-      STAMP_ADD(c, PH_WALK);
-      rem -= take;
-      const long long ntot = ltot - take;
-      if (lane == 0) {
-        Level o;
-        o.total = ntot;
-        o.head = ntot ? nh : NIL;
-        o.tail = ntot ? tail : NIL;
-        c.lv[lvl] = o;
+    // visit touched levels in sweep order: ascending (BUY) or descending (SELL)
+    for (int pass = 0; pass < 2; ++pass) {
+      const int row = dir > 0 ? pass : 1 - pass;
+      unsigned long long tm = row ? t1m : t0m;
+      while (tm) {
+        const int t = dir > 0 ? __builtin_ctzll(tm) : 63 - __builtin_clzll(tm);
+        tm &= ~(1ull << t);
+        const int lvl = row * 64 + t;
+        const long long ltot = row ? rli64(c.lad.t1, t) : rli64(c.lad.t0, t);
+        const long long before = row ? rli64(b1, t) : rli64(b0, t);
+        long long take = want - before;
+        if (take > ltot) take = ltot;
+        const uint32_t head = row ? rl32(c.lad.h1, t) : rl32(c.lad.h0, t);
+        const uint32_t tail = row ? rl32(c.lad.l1, t) : rl32(c.lad.l0, t);
+        emptied |= take_level(c, lvl, ltot, take, head, tail, taker);
+        rem -= take;
       }
-      if (ntot == 0) {
-        occ_clear(c, lvl);
-        emptied = true;
+    }
+  } else {
+    while (rem > 0) {
+      if (dir > 0 ? (cur > lim || cur >= L) : (cur < lim || cur < 0)) break;
+      const int lv = cur + dir * lane;
+      const bool valid = (dir > 0) ? (lv <= lim && lv < L) : (lv >= lim && lv >= 0);
+      Level W;
+      W.total = 0;
+      W.head = NIL;
+      W.tail = NIL;
+      if (valid) W = c.lad.lv[lv];
+      const long long tot = W.total;
+      const long long inc = wave_incl_scan(tot);
+      const long long ex = inc - tot;
+      const long long rem0 = rem;
+      unsigned long long tm = __ballot(valid && tot > 0 && ex < rem0);
+      STAMP_ADD(c, PH_SW_WINDOW);
+      while (tm) {
+        const int t = __builtin_ctzll(tm);
+        tm &= tm - 1;
+        const int lvl = cur + dir * t;
+        const long long ltot = rli64(tot, t);
+        const long long lex = rli64(ex, t);
+        long long take = rem0 - lex;
+        if (take > ltot) take = ltot;
+        emptied |= take_level(c, lvl, ltot, take, rl32(W.head, t), rl32(W.tail, t), taker);
+        rem -= take;
       }
-      STAMP_ADD(c, PH_SW_UPDATE);
+      if (rem == 0) break;
+      // every valid level of this window is now empty; jump to the next occupied one
+      const int nxt = cur + dir * 64;
+      if (dir > 0) {
+        if (nxt > lim) break;
+        cur = c.lad.next_occ(nxt);
+      } else {
+        if (nxt < lim) break;
+        cur = c.lad.prev_occ(nxt);
+      }
+      STAMP_ADD(c, PH_SW_JUMP);
     }
-    if (rem == 0) break;
-    // every valid level of this window is now empty; jump to the next occupied one
-    const int nxt = cur + dir * 64;
-    wave_mem_order();
-    if (dir > 0) {
-      if (nxt > lim) break;
-      cur = next_occ(c, nxt);
-    } else {
-      if (nxt < lim) break;
-      cur = prev_occ(c, nxt);
-    }
-    STAMP_ADD(c, PH_SW_JUMP);
   }
   if (emptied) {
-    wave_mem_order();
     if (dir > 0)
-      c.ba = next_occ(c, c.ba);
+      c.ba = c.lad.next_occ(c.ba);
     else
-      c.bb = prev_occ(c, c.bb);
+      c.bb = c.lad.prev_occ(c.bb);
     STAMP_ADD(c, PH_SW_BEST);
   }
   nfill = (uint32_t)(c.wptr - w_start);
   return want - rem;
 }
 
-// Append a resting order at the tail of level lvl's FIFO. With the ladder in LDS the common case
-// (room in the tail chunk) issues no HBM load at all: the tail fill count lives beside the level.
-__device__ bool rest_order(WaveCtx& c, int lvl, unsigned long long seq, int qty, bool buy) {
+// Append a resting order at the tail of level lvl's FIFO. The tail fill count lives beside the
+// level, so the common case issues no HBM load; a tail that is the cached head is written on chip.
+template <class C>
+__device__ bool rest_order(C& c, int lvl, unsigned long long seq, int qty, bool buy) {
   const int lane = lane_id();
   const BookDev& bk = c.bk;
-  wave_mem_order();
-  Level L = c.lv[lvl];
-  L.total = rli64(L.total, 0);
-  L.head = rl32(L.head, 0);
-  L.tail = rl32(L.tail, 0);
-  const uint32_t te = rl32((uint32_t)c.tend[lvl], 0);
+  Level L = c.lad.get(lvl);
+  const uint32_t te = c.lad.get_te(lvl);
   uint32_t ch, slot;
   if (L.tail != NIL && L.tail >= bk.nchunks) {
     set_err(bk, ERR_INCONSISTENT);
@@ -581,9 +857,12 @@ __device__ bool rest_order(WaveCtx& c, int lvl, unsigned long long seq, int qty,
       h.pad = 0;
       bk.chdr[ch] = h;
       bk.owner[ch] = c.s;
-      if (L.tail != NIL) bk.chdr[L.tail].next = ch;
     }
-    if (L.tail == NIL) L.head = ch;
+    if (L.tail != NIL) set_next(c, lvl, L.tail, ch);
+    if (L.tail == NIL) {
+      L.head = ch;
+      if (c.cache) cache_install_new(c, lvl, ch);
+    }
     L.tail = ch;
   } else {
     ch = L.tail;
@@ -592,14 +871,22 @@ __device__ bool rest_order(WaveCtx& c, int lvl, unsigned long long seq, int qty,
   const size_t g = (size_t)ch * ME_C + slot;
   const bool was_empty = (L.total == 0);
   L.total += qty;
+  const bool in_cache = c.cache && ch == L.head && cache_holds(c, lvl, ch);
   if (lane == 0) {
-    bk.cseq[g] = seq;
-    bk.cqty[g] = qty;
-    c.lv[lvl] = L;
-    c.tend[lvl] = (uint8_t)(slot + 1);
+    if (in_cache) {
+      CacheEntry* E = centry(c, lvl);
+      E->seq[slot] = seq;
+      E->qty[slot] = qty;
+      E->dirty = 1;
+    } else {
+      bk.cseq[g] = seq;
+      bk.cqty[g] = qty;
+    }
     if (seq < bk.max_seq) bk.loc[seq] = (uint32_t)g;
   }
-  if (was_empty) occ_set(c, lvl);
+  c.lad.set(lvl, L);
+  c.lad.set_te(lvl, slot + 1);
+  if (was_empty) c.lad.occ_set(lvl);
   if (buy) {
     if (lvl > c.bb) c.bb = lvl;
   } else {
@@ -612,7 +899,8 @@ __device__ bool rest_order(WaveCtx& c, int lvl, unsigned long long seq, int qty,
 // Cancel the live resting order `tgt` of this symbol. Returns the removed qty, 0 if not live.
 // A chunk left without live orders is unlinked from its FIFO at once (so chunks in use never
 // exceed resting orders); a level left empty returns its whole FIFO to the free list.
-__device__ int cancel_order(WaveCtx& c, unsigned long long tgt) {
+template <class C>
+__device__ int cancel_order(C& c, unsigned long long tgt) {
   const BookDev& bk = c.bk;
   const int lane = lane_id();
   if (tgt == 0ull || tgt >= bk.max_seq) return 0;
@@ -625,40 +913,51 @@ __device__ int cancel_order(WaveCtx& c, unsigned long long tgt) {
   const uint32_t owner = rl32(bk.owner[ch], 0);
   const ChunkHdr hd = bk.chdr[ch];
   const bool act = lane < ME_C;
-  const int qv = act ? bk.cqty[(size_t)ch * ME_C + lane] : 0;
-  const unsigned long long sq = rl64(bk.cseq[g], 0);
+  int qv = act ? bk.cqty[(size_t)ch * ME_C + lane] : 0;
+  unsigned long long sq = rl64(bk.cseq[g], 0);
   if (owner != c.s) return 0;  // another symbol's order: never touch its book
-  const int q = rli32(qv, (int)slot);
-  if (sq != tgt || q <= 0) return 0;
   const int lvl = (int)rl32(hd.level, 0);
-  const uint32_t nxt = rl32(hd.next, 0), prv = rl32(hd.prev, 0);
   if (lvl < 0 || lvl >= (int)bk.L) {
     set_err(bk, ERR_INCONSISTENT);
     return 0;
   }
+  CacheEntry* E = cache_holds(c, lvl, ch) ? centry(c, lvl) : nullptr;
+  if (E) {  // the on-chip copy is authoritative
+    qv = act ? E->qty[lane] : 0;
+    sq = rl64(E->seq[slot], 0);
+  }
+  const int q = rli32(qv, (int)slot);
+  if (sq != tgt || q <= 0) return 0;
+  const uint32_t nxt = rl32(hd.next, 0), prv = rl32(hd.prev, 0);
   const uint32_t live_after = (uint32_t)__popcll(__ballot(qv > 0)) - 1;
-  Level L = c.lv[lvl];
-  L.total = rli64(L.total, 0) - q;
-  L.head = rl32(L.head, 0);
-  L.tail = rl32(L.tail, 0);
+  Level L = c.lad.get(lvl);
+  L.total -= q;
   if (L.tail >= bk.nchunks || L.head >= bk.nchunks) {
     set_err(bk, ERR_INCONSISTENT);
     return q;
   }
-  if (lane == 0) bk.cqty[g] = 0;
+  if (lane == 0) {
+    if (E) {
+      E->qty[slot] = 0;
+      E->dirty = 1;
+    } else {
+      bk.cqty[g] = 0;
+    }
+  }
+  wave_mem_order();
   if (L.total == 0) {
     // splice the whole (now dead) FIFO onto the free list
+    cache_drop(c, lvl, L.head);
     if (lane == 0) bk.chdr[L.tail].next = c.free_head;
     c.free_next = (L.head == L.tail) ? c.free_head : NIL;
     c.free_head = L.head;
     if (L.head != L.tail) prefetch_free_next(c);
     L.head = NIL;
     L.tail = NIL;
-    if (lane == 0) c.lv[lvl] = L;
-    occ_clear(c, lvl);
-    wave_mem_order();
-    if (lvl == c.bb) c.bb = prev_occ(c, lvl);
-    if (lvl == c.ba) c.ba = next_occ(c, lvl);
+    c.lad.set(lvl, L);
+    c.lad.occ_clear(lvl);
+    if (lvl == c.bb) c.bb = c.lad.prev_occ(lvl);
+    if (lvl == c.ba) c.ba = c.lad.next_occ(lvl);
   } else if (live_after == 0) {
     // unlink the dead chunk (the level keeps live orders elsewhere, so ch is not both ends)
     uint32_t nh = L.head, nt = L.tail;
@@ -667,52 +966,222 @@ __device__ int cancel_order(WaveCtx& c, unsigned long long tgt) {
       if (lane == 0) bk.chdr[nxt].prev = NIL;
     } else if (ch == L.tail) {
       nt = prv;
-      if (lane == 0) {
-        bk.chdr[prv].next = NIL;
-        c.tend[lvl] = (uint8_t)ME_C;  // a non-tail chunk is always full
-      }
-    } else if (lane == 0) {
-      bk.chdr[prv].next = nxt;
-      bk.chdr[nxt].prev = prv;
+      set_next(c, lvl, prv, NIL);
+      c.lad.set_te(lvl, ME_C);  // a non-tail chunk is always full
+    } else {
+      set_next(c, lvl, prv, nxt);
+      if (lane == 0) bk.chdr[nxt].prev = prv;
     }
+    cache_drop(c, lvl, ch);
     L.head = nh;
     L.tail = nt;
-    if (lane == 0) c.lv[lvl] = L;
+    c.lad.set(lvl, L);
     free_chunk(c, ch);
   } else {
-    if (lane == 0) c.lv[lvl] = L;
+    c.lad.set(lvl, L);
   }
   c.resting_delta -= 1;
   return q;
 }
 
-__device__ __forceinline__ void write_result(const BatchDev& bt, uint32_t i, int filled, int remaining,
-                                             uint32_t nfill, uint8_t status, uint8_t reason,
-                                             unsigned long long fstart) {
-  if (lane_id() == 0) {
-    me_order_result r;
-    r.filled_qty = filled;
-    r.remaining_qty = remaining;
-    r.fill_count = nfill;
-    r.tape_offset = 0;
-    r.status = status;
-    r.reason = reason;
-    r.pad[0] = 0;
-    r.pad[1] = 0;
-    bt.res[i] = r;
-    bt.fstart[i] = (uint32_t)fstart;
-    if (nfill) atomicAdd(&bt.tile_sum[i / TILE_TAPE], nfill);
+// Per-record results are collected in lane k for record k of the current 64-record block and
+// stored by the whole wave once per block (a handful of vector stores instead of ~6 per record).
+struct ResultLanes {
+  int filled, remaining;
+  uint32_t nfill, fstart, st;  // st = status | reason << 8
+};
+
+__device__ __forceinline__ void put_result(ResultLanes& r, uint32_t k, int filled, int remaining, uint32_t nfill,
+                                           uint8_t status, uint8_t reason, unsigned long long fstart) {
+  const bool me_ = (uint32_t)lane_id() == k;  // v_cmp + v_cndmask per field
+  r.filled = me_ ? filled : r.filled;
+  r.remaining = me_ ? remaining : r.remaining;
+  r.nfill = me_ ? nfill : r.nfill;
+  r.fstart = me_ ? (uint32_t)fstart : r.fstart;
+  r.st = me_ ? (uint32_t)(status | (reason << 8)) : r.st;
+}
+
+__device__ __forceinline__ void store_results(const BatchDev& bt, const ResultLanes& r, bool v, uint32_t oi) {
+  if (!v) return;
+  me_order_result o;
+  o.filled_qty = r.filled;
+  o.remaining_qty = r.remaining;
+  o.fill_count = r.nfill;
+  o.tape_offset = 0;
+  o.status = (uint8_t)(r.st & 0xFF);
+  o.reason = (uint8_t)(r.st >> 8);
+  o.pad[0] = o.pad[1] = 0;
+  bt.res[oi] = o;
+  bt.fstart[oi] = r.fstart;
+  if (r.nfill) atomicAdd(&bt.tile_sum[oi / TILE_TAPE], r.nfill);
+}
+
+// LDS bytes of one wave: LDS ladder (levels + occupancy + tail fill) + head-chunk cache.
+__host__ __device__ constexpr size_t lds_ladder_bytes(uint32_t L) {
+  return (((size_t)L * sizeof(Level) + (size_t)(L / 64) * 8 + (size_t)L) + 15) & ~(size_t)15;
+}
+__host__ __device__ constexpr size_t lds_wave_bytes(uint32_t L) {
+  return lds_ladder_bytes(L) + CK_MEM * sizeof(CacheEntry);
+}
+__host__ __device__ constexpr size_t lds_wave_bytes_reg() { return CK_REG * sizeof(CacheEntry); }
+
+// Ladder placement of a k_match instantiation.
+enum LadderKind { LAD_HBM = 0, LAD_LDS = 1, LAD_REG = 2 };
+
+// The per-record loop of one symbol, shared by every ladder kind.
+template <class C>
+__device__ void match_records(C& c, const BatchDev& bt, uint32_t lo, uint32_t hi) {
+  const int lane = lane_id();
+  const BookDev& bk = c.bk;
+  const long long Lw = (long long)bk.L;
+  bool ok = true;
+  for (uint32_t blk = lo; blk < hi && ok; blk += 64) {
+    const uint32_t j = blk + (uint32_t)lane;
+    const bool v = j < hi;
+    const uint32_t oi = v ? bt.perm[j] : 0u;
+    const unsigned long long oseq = v ? bt.seq[oi] : 0ull;
+    const long long opx = v ? bt.px[oi] : 0ll;
+    const int oq = v ? bt.qty[oi] : 0;
+    const uint32_t ok_ = v ? (uint32_t)bt.kind[oi] : 0u;
+    const uint32_t cnt = min(64u, hi - blk);
+    ResultLanes R;
+    R.filled = R.remaining = 0;
+    R.nfill = R.fstart = R.st = 0;
+    STAMP_ADD(c, PH_FETCH);
+    uint32_t k = 0;
+    for (; k < cnt; ++k) {
+      const unsigned long long seq = rl64(oseq, (int)k);
+      const long long px = rli64(opx, (int)k);
+      const int q = rli32(oq, (int)k);
+      const uint32_t kind = rl32(ok_, (int)k);
+      c.recs_left = hi - (blk + k);
+      const uint32_t side = kind & 3u;
+      const bool market = (kind >> 2) & 1u;
+      const bool cancel = (kind >> 3) & 1u;
+      const unsigned long long fstart = c.wptr;
+      if (cancel) {
+        const int got = cancel_order(c, (unsigned long long)px);
+        STAMP_ADD(c, PH_CANCEL);
+        if (got > 0)
+          put_result(R, k, 0, got, 0, ME_ST_CANCELED, ME_RJ_NONE, fstart);
+        else
+          put_result(R, k, 0, 0, 0, ME_ST_REJECTED, ME_RJ_UNKNOWN_ORDER, fstart);
+        continue;
+      }
+      if (q <= 0) {
+        put_result(R, k, 0, 0, 0, ME_ST_REJECTED, ME_RJ_BAD_QTY, fstart);
+        continue;
+      }
+      if (side != ME_SIDE_BUY && side != ME_SIDE_SELL) {
+        put_result(R, k, 0, q, 0, ME_ST_REJECTED, ME_RJ_BAD_SIDE, fstart);
+        continue;
+      }
+      int li = 0;
+      if (!market) {
+        if (px < c.base || (unsigned long long)px - (unsigned long long)c.base >= (unsigned long long)Lw) {
+          put_result(R, k, 0, q, 0, ME_ST_REJECTED, ME_RJ_OUT_OF_WINDOW, fstart);
+          continue;
+        }
+        li = (int)(px - c.base);
+      }
+      if (seq == 0ull || seq >= bk.max_seq) {
+        put_result(R, k, 0, q, 0, ME_ST_REJECTED, ME_RJ_BAD_SEQ, fstart);
+        continue;
+      }
+      const bool buy = side == ME_SIDE_BUY;
+      const int lim = market ? (buy ? (int)Lw - 1 : 0) : li;
+      uint32_t nfill = 0;
+      const long long got = sweep(c, buy ? 1 : -1, lim, (long long)q, seq, nfill);
+      STAMP_ADD(c, PH_SWEEP);
+      const int filled = (int)got;
+      const int rem = q - filled;
+      uint8_t stt;
+      if (market) {
+        stt = rem == 0 ? ME_ST_FILLED : ME_ST_CANCELED;
+      } else {
+        const bool failed = rem > 0 && !rest_order(c, li, seq, rem, buy);
+        STAMP_ADD(c, PH_REST);
+        if (failed) {
+          ok = false;  // chunk pool exhausted: the batch fails (sticky error word)
+          break;
+        }
+        stt = rem == 0 ? ME_ST_FILLED : (filled > 0 ? ME_ST_PARTIALLY_FILLED : ME_ST_NEW);
+      }
+      put_result(R, k, filled, rem, nfill, stt, ME_RJ_NONE, fstart);
+    }
+    store_results(bt, R, v && (uint32_t)lane < k, oi);
+    STAMP_ADD(c, PH_RESULT);
+  }
+  // return unused bump-reserved chunks to this symbol's free list
+  while (c.bump_cur < c.bump_end) free_chunk(c, c.bump_cur++);
+}
+
+// Dirty cached head chunks back to HBM: lane = (entry, slot) pairs, 4 entries per pass.
+template <class C>
+__device__ void cache_flush_all(C& c, uint32_t entries) {
+  const int lane = lane_id();
+  wave_mem_order();
+  for (uint32_t e0 = 0; e0 < entries; e0 += 64 / ME_C) {
+    const uint32_t e = e0 + lane / ME_C, sl = lane % ME_C;
+    const CacheEntry* E = c.cache + e;
+    const uint32_t cid = E->cid;
+    if (cid != NIL && E->dirty) {
+      c.bk.cqty[(size_t)cid * ME_C + sl] = E->qty[sl];
+      c.bk.cseq[(size_t)cid * ME_C + sl] = E->seq[sl];
+    }
   }
 }
 
-// Bytes of LDS one wave needs to hold its symbol's ladder (levels + occupancy + tail fill).
-__host__ __device__ constexpr size_t lds_wave_bytes(uint32_t L) {
-  return (size_t)L * sizeof(Level) + (size_t)(L / 64) * 8 + (size_t)L;
+template <class C>
+__device__ bool wave_begin(C& c, const BookDev& bk, const BatchDev& bt, uint32_t s, uint32_t lo, uint32_t hi) {
+  const int lane = lane_id();
+  c.bk = bk;
+  c.s = s;
+  c.gs = bk.gsym ? bk.gsym[s] : s;
+  const SymState st = bk.sym[s];
+  c.base = rli64(st.base, 0);
+  c.bb = rli32(st.best_bid, 0);
+  c.ba = rli32(st.best_ask, 0);
+  c.free_head = rl32(st.free_head, 0);
+  prefetch_free_next(c);
+  c.bump_cur = c.bump_end = 0;
+  c.resting_delta = (int)rl32(st.resting, 0);  // becomes the new resting count
+  c.scratch = bt.scratch;
+  // scratch run of this wave: fills <= resting makers + 2 * records (DESIGN.md §3)
+  const unsigned long long need = (unsigned long long)rl32(st.resting, 0) + 2ull * (hi - lo);
+  unsigned long long w0 = 0;
+  if (lane == 0) w0 = atomicAdd(bt.scratch_top, need);
+  w0 = rl64(w0, 0);
+  if (w0 + need > bt.scratch_cap) {
+    set_err(bk, ERR_SCRATCH_OOM);
+    return false;
+  }
+  c.wptr = w0;
+  return true;
+}
+
+template <class C>
+__device__ void wave_end(C& c) {
+  if (lane_id() == 0) {
+    SymState o;
+    o.base = c.base;
+    o.best_bid = c.bb;
+    o.best_ask = c.ba;
+    o.free_head = c.free_head;
+    o.resting = (uint32_t)c.resting_delta;
+    o.pad[0] = o.pad[1] = 0;
+    c.bk.sym[c.s] = o;
+  }
+#ifdef ME_STAMPS
+  STAMP_ADD(c, PH_EPILOGUE);
+  if (lane_id() == 0 && c.bk.dbg)
+    for (int p = 0; p < PH_N; ++p) c.bk.dbg[(size_t)c.s * 24 + p] = c.st[p];
+#endif
 }
 
 // One wavefront per symbol (4 per workgroup). Block s/4, wave s%4. Symbol S is the reject bin
-// of records whose symbol id is out of range. kLds: the symbol's ladder is staged in LDS.
-template <bool kLds>
+// of records whose symbol id is out of range.
+template <int kLad>
 __global__ __launch_bounds__(256) void k_match(BookDev bk, BatchDev bt) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int lane = lane_id();
@@ -742,151 +1211,90 @@ __global__ __launch_bounds__(256) void k_match(BookDev bk, BatchDev bt) {
   Level* g_lv = bk.levels + (size_t)s * L;
   unsigned long long* g_occ = bk.occ + (size_t)s * bk.Lwords;
   uint8_t* g_tend = bk.tend + (size_t)s * L;
-  WaveCtx c;
+  if constexpr (kLad == LAD_REG) {
+    WaveCtx<LadderReg> c;
 #ifdef ME_STAMPS
-  for (int p = 0; p < PH_N; ++p) c.st[p] = 0;
-  STAMP_MARK(c);
+    for (int p = 0; p < PH_N; ++p) c.st[p] = 0;
+    STAMP_MARK(c);
 #endif
-  c.bk = bk;
-  c.s = s;
-  if (kLds) {
-    unsigned char* base = smem + (size_t)wv * lds_wave_bytes(L);
-    c.lv = (Level*)base;
-    c.occ = (unsigned long long*)(base + (size_t)L * sizeof(Level));
-    c.tend = base + (size_t)L * sizeof(Level) + (size_t)(L / 64) * 8;
-    for (uint32_t i = lane; i < L; i += 64) {
-      c.lv[i] = g_lv[i];
-      c.tend[i] = g_tend[i];
-    }
-    for (uint32_t i = lane; i < bk.Lwords; i += 64) c.occ[i] = g_occ[i];
+    // levels lane and 64 + lane; the occupancy bitmap is implied by the totals
+    Level a = g_lv[lane];
+    Level b;
+    b.total = 0;
+    b.head = b.tail = NIL;
+    if (64 + (uint32_t)lane < L) b = g_lv[64 + lane];
+    c.lad.t0 = a.total;
+    c.lad.h0 = a.head;
+    c.lad.l0 = a.tail;
+    c.lad.t1 = b.total;
+    c.lad.h1 = b.head;
+    c.lad.l1 = b.tail;
+    c.lad.e0 = g_tend[lane];
+    c.lad.e1 = (64 + (uint32_t)lane < L) ? g_tend[64 + lane] : 0u;
+    c.lad.L = L;
+    c.cache = (CacheEntry*)(smem + (size_t)wv * lds_wave_bytes_reg());
+    c.cmask = CK_REG - 1;
+    for (uint32_t i = lane; i < (uint32_t)CK_REG; i += 64) c.cache[i].cid = NIL;
     wave_mem_order();
+    if (!wave_begin(c, bk, bt, s, lo, hi)) return;
+    STAMP_ADD(c, PH_PROLOGUE);
+    match_records(c, bt, lo, hi);
+    cache_flush_all(c, CK_REG);
+    g_lv[lane] = Level{c.lad.t0, c.lad.h0, c.lad.l0};
+    g_tend[lane] = (uint8_t)c.lad.e0;
+    if (64 + (uint32_t)lane < L) {
+      g_lv[64 + lane] = Level{c.lad.t1, c.lad.h1, c.lad.l1};
+      g_tend[64 + lane] = (uint8_t)c.lad.e1;
+    }
+    // keep the HBM occupancy bitmap valid for the host-side book dump
+    const unsigned long long m0 = __ballot(c.lad.t0 > 0), m1 = __ballot(c.lad.t1 > 0);
+    if (lane == 0) {
+      g_occ[0] = m0;
+      if (bk.Lwords > 1) g_occ[1] = m1;
+    }
+    wave_end(c);
   } else {
-    c.lv = g_lv;
-    c.occ = g_occ;
-    c.tend = g_tend;
-  }
-  c.gs = bk.gsym ? bk.gsym[s] : s;
-  const SymState st = bk.sym[s];
-  c.base = rli64(st.base, 0);
-  c.bb = rli32(st.best_bid, 0);
-  c.ba = rli32(st.best_ask, 0);
-  c.free_head = rl32(st.free_head, 0);
-  prefetch_free_next(c);
-  c.bump_cur = c.bump_end = 0;
-  c.resting_delta = 0;
-  c.scratch = bt.scratch;
-  // scratch run of this wave: fills <= resting makers + 2 * records (DESIGN.md §3)
-  const unsigned long long need = (unsigned long long)rl32(st.resting, 0) + 2ull * (hi - lo);
-  unsigned long long w0 = 0;
-  if (lane == 0) w0 = atomicAdd(bt.scratch_top, need);
-  w0 = rl64(w0, 0);
-  if (w0 + need > bt.scratch_cap) {
-    set_err(bk, ERR_SCRATCH_OOM);
-    return;
-  }
-  c.wptr = w0;
-  STAMP_ADD(c, PH_PROLOGUE);
-  const long long Lw = (long long)L;
-
-  bool ok = true;
-  for (uint32_t blk = lo; blk < hi && ok; blk += 64) {
-    const uint32_t j = blk + (uint32_t)lane;
-    const bool v = j < hi;
-    const uint32_t oi = v ? bt.perm[j] : 0u;
-    const unsigned long long oseq = v ? bt.seq[oi] : 0ull;
-    const long long opx = v ? bt.px[oi] : 0ll;
-    const int oq = v ? bt.qty[oi] : 0;
-    const uint32_t ok_ = v ? (uint32_t)bt.kind[oi] : 0u;
-    const uint32_t cnt = min(64u, hi - blk);
-    STAMP_ADD(c, PH_FETCH);
-    for (uint32_t k = 0; k < cnt; ++k) {
-      const uint32_t i = rl32(oi, (int)k);
-      const unsigned long long seq = rl64(oseq, (int)k);
-      const long long px = rli64(opx, (int)k);
-      const int q = rli32(oq, (int)k);
-      const uint32_t kind = rl32(ok_, (int)k);
-      c.recs_left = hi - (blk + k);
-      const uint32_t side = kind & 3u;
-      const bool market = (kind >> 2) & 1u;
-      const bool cancel = (kind >> 3) & 1u;
-      const unsigned long long fstart = c.wptr;
-      if (cancel) {
-        const int got = cancel_order(c, (unsigned long long)px);
-        STAMP_ADD(c, PH_CANCEL);
-        if (got > 0)
-          write_result(bt, i, 0, got, 0, ME_ST_CANCELED, ME_RJ_NONE, fstart);
-        else
-          write_result(bt, i, 0, 0, 0, ME_ST_REJECTED, ME_RJ_UNKNOWN_ORDER, fstart);
-        continue;
-      }
-      if (q <= 0) {
-        write_result(bt, i, 0, 0, 0, ME_ST_REJECTED, ME_RJ_BAD_QTY, fstart);
-        continue;
-      }
-      if (side != ME_SIDE_BUY && side != ME_SIDE_SELL) {
-        write_result(bt, i, 0, q, 0, ME_ST_REJECTED, ME_RJ_BAD_SIDE, fstart);
-        continue;
-      }
-      int li = 0;
-      if (!market) {
-        if (px < c.base || (unsigned long long)px - (unsigned long long)c.base >= (unsigned long long)Lw) {
-          write_result(bt, i, 0, q, 0, ME_ST_REJECTED, ME_RJ_OUT_OF_WINDOW, fstart);
-          continue;
-        }
-        li = (int)(px - c.base);
-      }
-      if (seq == 0ull || seq >= bk.max_seq) {
-        write_result(bt, i, 0, q, 0, ME_ST_REJECTED, ME_RJ_BAD_SEQ, fstart);
-        continue;
-      }
-      const bool buy = side == ME_SIDE_BUY;
-      const int lim = market ? (buy ? (int)Lw - 1 : 0) : li;
-      uint32_t nfill = 0;
-      const long long got = sweep(c, buy ? 1 : -1, lim, (long long)q, seq, nfill);
-      STAMP_ADD(c, PH_SWEEP);
-      const int filled = (int)got;
-      const int rem = q - filled;
-      uint8_t stt;
-      if (market) {
-        stt = rem == 0 ? ME_ST_FILLED : ME_ST_CANCELED;
-      } else {
-        const bool rested = rem > 0 && !rest_order(c, li, seq, rem, buy);
-        STAMP_ADD(c, PH_REST);
-        if (rested) {
-          ok = false;  // chunk pool exhausted: the batch fails (sticky error word)
-          break;
-        }
-        stt = rem == 0 ? ME_ST_FILLED : (filled > 0 ? ME_ST_PARTIALLY_FILLED : ME_ST_NEW);
-      }
-      write_result(bt, i, filled, rem, nfill, stt, ME_RJ_NONE, fstart);
-      STAMP_ADD(c, PH_RESULT);
-    }
-  }
-  // return unused bump-reserved chunks to this symbol's free list
-  while (c.bump_cur < c.bump_end) free_chunk(c, c.bump_cur++);
-  if (kLds) {
-    wave_mem_order();
-    for (uint32_t i = lane; i < L; i += 64) {
-      g_lv[i] = c.lv[i];
-      g_tend[i] = c.tend[i];
-    }
-    for (uint32_t i = lane; i < bk.Lwords; i += 64) g_occ[i] = c.occ[i];
-  }
-  if (lane == 0) {
-    SymState o;
-    o.base = c.base;
-    o.best_bid = c.bb;
-    o.best_ask = c.ba;
-    o.free_head = c.free_head;
-    o.resting = (uint32_t)((int)st.resting + c.resting_delta);
-    o.pad[0] = o.pad[1] = 0;
-    bk.sym[s] = o;
-  }
+    WaveCtx<LadderMem> c;
 #ifdef ME_STAMPS
-  STAMP_ADD(c, PH_EPILOGUE);
-  if (lane == 0 && bk.dbg)
-    for (int p = 0; p < PH_N; ++p) bk.dbg[(size_t)s * 16 + p] = c.st[p];
+    for (int p = 0; p < PH_N; ++p) c.st[p] = 0;
+    STAMP_MARK(c);
 #endif
+    c.lad.L = L;
+    c.lad.Lwords = bk.Lwords;
+    if constexpr (kLad == LAD_LDS) {
+      unsigned char* base = smem + (size_t)wv * lds_wave_bytes(L);
+      c.lad.lv = (Level*)base;
+      c.lad.occ = (unsigned long long*)(base + (size_t)L * sizeof(Level));
+      c.lad.tend = base + (size_t)L * sizeof(Level) + (size_t)(L / 64) * 8;
+      c.cache = (CacheEntry*)(base + lds_ladder_bytes(L));
+      c.cmask = CK_MEM - 1;
+      for (uint32_t i = lane; i < L; i += 64) {
+        c.lad.lv[i] = g_lv[i];
+        c.lad.tend[i] = g_tend[i];
+      }
+      for (uint32_t i = lane; i < bk.Lwords; i += 64) c.lad.occ[i] = g_occ[i];
+      for (uint32_t i = lane; i < (uint32_t)CK_MEM; i += 64) c.cache[i].cid = NIL;
+      wave_mem_order();
+    } else {
+      c.lad.lv = g_lv;
+      c.lad.occ = g_occ;
+      c.lad.tend = g_tend;
+      c.cache = nullptr;
+      c.cmask = 0;
+    }
+    if (!wave_begin(c, bk, bt, s, lo, hi)) return;
+    STAMP_ADD(c, PH_PROLOGUE);
+    match_records(c, bt, lo, hi);
+    if constexpr (kLad == LAD_LDS) {
+      cache_flush_all(c, CK_MEM);
+      for (uint32_t i = lane; i < L; i += 64) {
+        g_lv[i] = c.lad.lv[i];
+        g_tend[i] = c.lad.tend[i];
+      }
+      for (uint32_t i = lane; i < bk.Lwords; i += 64) g_occ[i] = c.lad.occ[i];
+    }
+    wave_end(c);
+  }
 }
 
 // ------------------------------------------------------------------ tape compaction
@@ -984,11 +1392,12 @@ hipError_t launch_sort_pass(hipStream_t st, const uint32_t* keys_in, const uint3
 hipError_t launch_match(hipStream_t st, const BookDev& bk, const BatchDev& bt) {
   const uint32_t waves = bk.S + 1;
   const dim3 grid((waves + 3) / 4), block(256);
-  if (bk.L <= LDS_MAX_LEVELS) {
-    const size_t lds = 4 * lds_wave_bytes(bk.L);
-    hipLaunchKernelGGL(k_match<true>, grid, block, lds, st, bk, bt);
+  if (bk.L <= 128) {
+    hipLaunchKernelGGL(k_match<LAD_REG>, grid, block, 4 * lds_wave_bytes_reg(), st, bk, bt);
+  } else if (bk.L <= LDS_MAX_LEVELS) {
+    hipLaunchKernelGGL(k_match<LAD_LDS>, grid, block, 4 * lds_wave_bytes(bk.L), st, bk, bt);
   } else {
-    hipLaunchKernelGGL(k_match<false>, grid, block, 0, st, bk, bt);
+    hipLaunchKernelGGL(k_match<LAD_HBM>, grid, block, 0, st, bk, bt);
   }
   return hipGetLastError();
 }

@@ -1,0 +1,57 @@
+"""HBM traffic per k_match launch from rocprofv3 PMC passes (one counter per pass).
+
+    rocprofv3 --pmc FETCH_SIZE --output-format csv -d OUT/fetch -o pmc -- python3 bench.py ...
+    rocprofv3 --pmc WRITE_SIZE --output-format csv -d OUT/write -o pmc -- python3 bench.py ...
+    python tools/pmc_traffic.py OUT/fetch OUT/write --kernel k_match > profiles/r1_pmc_traffic.json
+
+FETCH_SIZE / WRITE_SIZE are kilobytes (derived from TCC_EA0_RDREQ / _WRREQ). gfx950 correction
+(MI355X_MICROARCH.md §HBM): FETCH_SIZE reports half the bytes of wide coalesced reads, so it is
+doubled; WRITE_SIZE is taken as is. Other access widths are uncalibrated (documented caveat).
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def per_dispatch(d, counter, kernel):
+    vals = []
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            name = r.get("Kernel_Name") or r.get("Kernel-Name") or ""
+            cn = r.get("Counter_Name") or r.get("Counter-Name") or ""
+            if kernel in name and cn == counter:
+                vals.append(float(r.get("Counter_Value") or r.get("Counter-Value")))
+    return vals
+
+
+def main():
+    a = sys.argv[1:]
+    kernel = "k_match"
+    if "--kernel" in a:
+        i = a.index("--kernel")
+        kernel = a[i + 1]
+        del a[i:i + 2]
+    fdir, wdir = a[0], a[1]
+    f = per_dispatch(fdir, "FETCH_SIZE", kernel)
+    w = per_dispatch(wdir, "WRITE_SIZE", kernel)
+    if not f or not w:
+        print(json.dumps({"error": "no samples", "fetch": len(f), "write": len(w)}))
+        return 1
+    fetch_kb = sum(f) / len(f)
+    write_kb = sum(w) / len(w)
+    out = {
+        "kernel": kernel,
+        "dispatches": [len(f), len(w)],
+        "fetch_size_kb_avg": fetch_kb,
+        "write_size_kb_avg": write_kb,
+        "bytes_per_launch": (2.0 * fetch_kb + write_kb) * 1024.0,
+        "correction": "FETCH_SIZE x2 (gfx950 half-count of wide reads), WRITE_SIZE x1, KB->B x1024",
+    }
+    print(json.dumps(out, indent=1))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -13,7 +13,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import matching_engine_amd as me  # noqa: E402
 
 PH = ["prologue", "fetch", "sweep", "walk", "rest", "cancel", "result", "epilogue", "sw_window", "sw_update",
-      "sw_jump", "sw_best", "-", "-", "-", "-"]
+      "sw_jump", "sw_best"]
+WK = ["wk_get", "wk_scan", "wk_emit", "wk_tail"]
+CT = ["cache_miss", "walks", "evictions", "fast_path"]
 
 
 def main():
@@ -30,8 +32,8 @@ def main():
     lib = me._abi.load()
     lib.me_debug_stamps.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
     eng = me.Engine(sc.num_symbols, sc.levels, base, max_batch=sc.batch, max_resting=1 << 22, max_seq=1 << 30)
-    buf = np.zeros(sc.num_symbols * 16, dtype=np.uint64)
-    tot = np.zeros(16, dtype=np.float64)
+    buf = np.zeros(sc.num_symbols * 24, dtype=np.uint64)
+    tot = np.zeros(24, dtype=np.float64)
     maxwave = []
     norders = 0
     for k in range(a.batches):
@@ -40,16 +42,19 @@ def main():
         if k < 5:
             continue  # warm
         lib.me_debug_stamps(eng.h, buf.ctypes.data, buf.size)
-        m = buf.reshape(-1, 16).astype(np.float64)
+        m = buf.reshape(-1, 24).astype(np.float64)
         tot += m.sum(0)
-        maxwave.append(m.sum(1).max())
+        maxwave.append((m[:, :12].sum(1) + m[:, 16:20].sum(1)).max())
         norders += len(b)
-    share = tot / tot.sum()
-    per_order = tot / norders
+    cyc = np.concatenate([tot[:12], tot[16:20]])
+    share = cyc / cyc.sum()
+    per_order = cyc / norders
     print(f"config {a.config}: {norders} orders, {sc.num_symbols} symbols")
-    for p, s_, c in zip(PH, share, per_order):
+    for p, s_, c in zip(PH + WK, share, per_order):
         print(f"  {p:9s} {100 * s_:6.2f}%  {c:9.1f} cycles/order")
-    print(f"  total {tot.sum() / norders:.1f} cycles/order/wave; slowest wave {np.mean(maxwave):.0f} cycles/batch")
+    for name, v in zip(CT, tot[12:16]):
+        print(f"  {name:10s} {v / norders:.3f} per order")
+    print(f"  total {cyc.sum() / norders:.1f} cycles/order/wave; slowest wave {np.mean(maxwave):.0f} cycles/batch")
 
 
 if __name__ == "__main__":
