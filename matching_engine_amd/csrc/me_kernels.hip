@@ -17,101 +17,10 @@
 #include <hip/hip_runtime.h>
 
 #include "me_layout.hpp"
+#include "me_wave.hpp"
 
 namespace me {
 
-// ------------------------------------------------------------------ wave helpers
-__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & 63); }
-
-__device__ __forceinline__ uint32_t rl32(uint32_t v, int k) {
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, k);
-}
-__device__ __forceinline__ int32_t rli32(int32_t v, int k) { return __builtin_amdgcn_readlane(v, k); }
-__device__ __forceinline__ unsigned long long rl64(unsigned long long v, int k) {
-  uint32_t lo = rl32((uint32_t)v, k), hi = rl32((uint32_t)(v >> 32), k);
-  return ((unsigned long long)hi << 32) | lo;
-}
-__device__ __forceinline__ long long rli64(long long v, int k) {
-  return (long long)rl64((unsigned long long)v, k);
-}
-__device__ __forceinline__ unsigned long long lanemask_lt() {
-  return (1ull << lane_id()) - 1ull;
-}
-// DPP row shift / broadcast of a 32-bit value: lanes whose source is outside the pattern get 0.
-template <int kCtrl, int kRowMask>
-__device__ __forceinline__ uint32_t dpp32(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, kCtrl, kRowMask, 0xF, false);
-}
-template <int kCtrl, int kRowMask>
-__device__ __forceinline__ long long dpp64(long long v) {
-  const uint32_t lo = dpp32<kCtrl, kRowMask>((uint32_t)v);
-  const uint32_t hi = dpp32<kCtrl, kRowMask>((uint32_t)((unsigned long long)v >> 32));
-  return (long long)(((unsigned long long)hi << 32) | lo);
-}
-// Inclusive 64-lane prefix sum of an int64 on the VALU with DPP (no LDS permutes): row_shr
-// 1/2/4/8 scans each 16-lane row, row_bcast:15 / row_bcast:31 carry the row totals.
-__device__ __forceinline__ long long wave_incl_scan(long long x) {
-  x += dpp64<0x111, 0xF>(x);  // row_shr:1
-  x += dpp64<0x112, 0xF>(x);  // row_shr:2
-  x += dpp64<0x114, 0xF>(x);  // row_shr:4
-  x += dpp64<0x118, 0xF>(x);  // row_shr:8
-  x += dpp64<0x142, 0xA>(x);  // row_bcast:15 into rows 1, 3
-  x += dpp64<0x143, 0xC>(x);  // row_bcast:31 into rows 2, 3
-  return x;
-}
-// Orders the wave's own global stores before its later loads of the same lines (another lane
-// may read what this lane wrote). Same-CU ordering: no cache maintenance, a compiler barrier.
-__device__ __forceinline__ void wave_mem_order() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }
-
-// Diagnostic build only (-DME_STAMPS): per-wave cycle shares of the matching phases, read with
-// me_debug_stamps(). The product build compiles every stamp away.
-enum { PH_PROLOGUE, PH_FETCH, PH_SWEEP, PH_WALK, PH_REST, PH_CANCEL, PH_RESULT, PH_EPILOGUE,
-       PH_SW_WINDOW, PH_SW_UPDATE, PH_SW_JUMP, PH_SW_BEST, CT_MISS, CT_WALK, CT_EVICT, CT_FAST,
-       WK_GET, WK_SCAN, WK_EMIT, WK_TAIL, PH_N };
-#ifdef ME_STAMPS
-__device__ __forceinline__ unsigned long long stamp_now() {
-  unsigned long long t;
-  __builtin_amdgcn_sched_barrier(0);
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  __builtin_amdgcn_sched_barrier(0);
-  return t;
-}
-#define STAMP_MARK(c) (c).st_t = stamp_now()
-#define COUNT(c, ct) ((c).st[ct] += 1)
-#define STAMP_ADD(c, ph)                    \
-  do {                                      \
-    unsigned long long _n = stamp_now();    \
-    (c).st[ph] += _n - (c).st_t;            \
-    (c).st_t = _n;                          \
-  } while (0)
-#else
-#define STAMP_MARK(c) ((void)0)
-#define STAMP_ADD(c, ph) ((void)0)
-#define COUNT(c, ct) ((void)0)
-#endif
-
-// First index p in [0, n) with keys[p] >= key (keys ascending), by a 64-ary search:
-// every step the wave samples 64 positions, ballots, and narrows the range 64x.
-__device__ uint32_t wave_lower_bound(const uint32_t* keys, uint32_t n, uint32_t key) {
-  const int lane = lane_id();
-  uint32_t lo = 0, hi = n;  // answer in [lo, hi]
-  while (hi - lo > 64) {
-    uint32_t step = (hi - lo + 63) / 64;
-    uint32_t p = lo + (uint32_t)lane * step;
-    bool less = (p < hi) && (keys[p] < key);
-    unsigned long long m = __ballot(less);
-    uint32_t c = (uint32_t)__popcll(m);  // samples < key form a prefix of the lanes
-    if (c == 0) return lo;                // keys[lo] >= key
-    uint32_t nlo = lo + (c - 1) * step + 1;
-    uint32_t nhi = lo + c * step;
-    if (nhi > hi) nhi = hi;
-    lo = nlo;
-    hi = nhi;
-  }
-  uint32_t p = lo + (uint32_t)lane;
-  bool less = (p < hi) && (keys[p] < key);
-  return lo + (uint32_t)__popcll(__ballot(less));
-}
 
 // ------------------------------------------------------------------ grouping sort
 // One pass of a stable LSD counting sort of the batch by symbol id. digit(key) =
@@ -364,14 +273,18 @@ struct LadderMem {
 };
 
 // LadderReg (L <= 128): level l lives in lane (l & 63) of register row (l >> 6). Reads are
-// readlanes, writes are per-lane selects, occupancy is a ballot of the totals: the whole ladder
-// bookkeeping runs on the VALU/SALU with no memory round trip.
+// readlanes, writes are per-lane selects; occupancy is a 128-bit mask in SGPRs (best-price search
+// = one bit scan). The head-chunk cache entry of level l is l itself (no evictions) and its
+// valid / dirty state are SGPR masks too: no memory round trip for any ladder bookkeeping.
 struct LadderReg {
   long long t0, t1;  // total
   uint32_t h0, h1;   // head chunk
   uint32_t l0, l1;   // tail chunk
   uint32_t e0, e1;   // slots written in the tail chunk
   uint32_t L;
+  unsigned long long occ0, occ1;  // occupancy (wave-uniform)
+  unsigned long long cv0, cv1;    // cache entry l holds the head chunk of l
+  unsigned long long cd0, cd1;    // cache entry l is dirty
 
   __device__ __forceinline__ Level get(int l) const {
     const int j = l & 63;
@@ -387,51 +300,60 @@ struct LadderReg {
     }
     return x;
   }
+  // (branch-free on purpose: a row-dependent if/else over members turns into a pointer select
+  // that keeps the whole context in scratch memory)
   __device__ __forceinline__ void set(int l, const Level& x) {
     const bool me = lane_id() == (l & 63);
-    if (l < 64) {
-      t0 = me ? x.total : t0;
-      h0 = me ? x.head : h0;
-      l0 = me ? x.tail : l0;
-    } else {
-      t1 = me ? x.total : t1;
-      h1 = me ? x.head : h1;
-      l1 = me ? x.tail : l1;
-    }
+    const bool m0 = me && l < 64, m1 = me && l >= 64;
+    t0 = m0 ? x.total : t0;
+    h0 = m0 ? x.head : h0;
+    l0 = m0 ? x.tail : l0;
+    t1 = m1 ? x.total : t1;
+    h1 = m1 ? x.head : h1;
+    l1 = m1 ? x.tail : l1;
   }
   __device__ __forceinline__ uint32_t get_te(int l) const { return l < 64 ? rl32(e0, l & 63) : rl32(e1, l & 63); }
   __device__ __forceinline__ void set_te(int l, uint32_t v) {
     const bool me = lane_id() == (l & 63);
-    if (l < 64)
-      e0 = me ? v : e0;
-    else
-      e1 = me ? v : e1;
+    e0 = (me && l < 64) ? v : e0;
+    e1 = (me && l >= 64) ? v : e1;
   }
-  __device__ __forceinline__ void occ_set(int) {}
-  __device__ __forceinline__ void occ_clear(int) {}
+  static __device__ __forceinline__ unsigned long long lo_bit(int l) { return l < 64 ? (1ull << (l & 63)) : 0ull; }
+  static __device__ __forceinline__ unsigned long long hi_bit(int l) { return l >= 64 ? (1ull << (l & 63)) : 0ull; }
+  static __device__ __forceinline__ void bit_set(unsigned long long& a, unsigned long long& b, int l) {
+    a |= lo_bit(l);
+    b |= hi_bit(l);
+  }
+  static __device__ __forceinline__ void bit_clr(unsigned long long& a, unsigned long long& b, int l) {
+    a &= ~lo_bit(l);
+    b &= ~hi_bit(l);
+  }
+  static __device__ __forceinline__ bool bit_get(unsigned long long a, unsigned long long b, int l) {
+    return l < 64 ? ((a >> l) & 1ull) : ((b >> (l - 64)) & 1ull);
+  }
+  __device__ __forceinline__ void occ_set(int l) { bit_set(occ0, occ1, l); }
+  __device__ __forceinline__ void occ_clear(int l) { bit_clr(occ0, occ1, l); }
   __device__ __forceinline__ int next_occ(int x) const {
     if (x >= (int)L) return (int)L;
     if (x < 0) x = 0;
-    const unsigned long long m0 = __ballot(t0 > 0), m1 = __ballot(t1 > 0);
     if (x < 64) {
-      const unsigned long long w = m0 & (~0ull << x);
+      const unsigned long long w = occ0 & (~0ull << x);
       if (w) return __builtin_ctzll(w);
-      return m1 ? 64 + __builtin_ctzll(m1) : (int)L;
+      return occ1 ? 64 + __builtin_ctzll(occ1) : (int)L;
     }
-    const unsigned long long w = m1 & (~0ull << (x - 64));
+    const unsigned long long w = occ1 & (~0ull << (x - 64));
     return w ? 64 + __builtin_ctzll(w) : (int)L;
   }
   __device__ __forceinline__ int prev_occ(int x) const {
     if (x < 0) return -1;
     if (x >= (int)L) x = (int)L - 1;
-    const unsigned long long m0 = __ballot(t0 > 0), m1 = __ballot(t1 > 0);
     if (x >= 64) {
       const int r = x - 64;
-      const unsigned long long w = m1 & ((r == 63) ? ~0ull : ((1ull << (r + 1)) - 1ull));
+      const unsigned long long w = occ1 & ((r == 63) ? ~0ull : ((1ull << (r + 1)) - 1ull));
       if (w) return 64 + 63 - __builtin_clzll(w);
-      return m0 ? 63 - __builtin_clzll(m0) : -1;
+      return occ0 ? 63 - __builtin_clzll(occ0) : -1;
     }
-    const unsigned long long w = m0 & ((x == 63) ? ~0ull : ((1ull << (x + 1)) - 1ull));
+    const unsigned long long w = occ0 & ((x == 63) ? ~0ull : ((1ull << (x + 1)) - 1ull));
     return w ? 63 - __builtin_clzll(w) : -1;
   }
 };
@@ -464,18 +386,51 @@ __device__ __forceinline__ void set_err(const BookDev& bk, uint32_t bits) {
 }
 
 // ---- head-chunk cache -------------------------------------------------------------------
+// Generic ladders keep the entry's chunk id and dirty flag in LDS; the register ladder keeps
+// them as SGPR masks (valid bit l <=> entry l holds the current head chunk of level l), so a
+// lookup there is a bit test, never an LDS round trip.
+template <class C>
+constexpr bool kRegLadder = __is_same(decltype(C::lad), LadderReg);
+
 template <class C>
 __device__ __forceinline__ CacheEntry* centry(const C& c, int lvl) { return c.cache + ((uint32_t)lvl & c.cmask); }
 
 template <class C>
-__device__ __forceinline__ bool cache_holds(const C& c, int lvl, uint32_t ch) {
-  return c.cache && rl32(centry(c, lvl)->cid, 0) == ch;
+__device__ __forceinline__ uint32_t head_of(const C& c, int lvl) {
+  if constexpr (kRegLadder<C>)
+    return lvl < 64 ? rl32(c.lad.h0, lvl & 63) : rl32(c.lad.h1, lvl & 63);
+  else
+    return rl32(c.lad.lv[lvl].head, 0);
 }
 
 template <class C>
-__device__ __forceinline__ void cache_writeback(const C& c, CacheEntry* E) {
-  const uint32_t cid = rl32(E->cid, 0);
-  if (cid == NIL || !rl32(E->dirty, 0)) return;
+__device__ __forceinline__ bool cache_holds(const C& c, int lvl, uint32_t ch) {
+  if constexpr (kRegLadder<C>)
+    return LadderReg::bit_get(c.lad.cv0, c.lad.cv1, lvl) && head_of(c, lvl) == ch;
+  else
+    return c.cache && rl32(centry(c, lvl)->cid, 0) == ch;
+}
+
+template <class C>
+__device__ __forceinline__ void cache_mark_dirty(C& c, int lvl) {
+  if constexpr (kRegLadder<C>)
+    LadderReg::bit_set(c.lad.cd0, c.lad.cd1, lvl);
+  else if (lane_id() == 0)
+    centry(c, lvl)->dirty = 1;
+}
+
+// Write entry E of level lvl back to HBM if dirty. Register ladder: the caller passes the chunk
+// the (valid) entry holds; generic ladders read it from the entry.
+template <class C>
+__device__ __forceinline__ void cache_writeback(const C& c, int lvl, CacheEntry* E, uint32_t held = NIL) {
+  uint32_t cid;
+  if constexpr (kRegLadder<C>) {
+    if (!LadderReg::bit_get(c.lad.cv0, c.lad.cv1, lvl) || !LadderReg::bit_get(c.lad.cd0, c.lad.cd1, lvl)) return;
+    cid = held;
+  } else {
+    cid = rl32(E->cid, 0);
+    if (cid == NIL || !rl32(E->dirty, 0)) return;
+  }
   const int lane = lane_id();
   if (lane < ME_C) {
     const size_t g = (size_t)cid * ME_C + lane;
@@ -484,15 +439,34 @@ __device__ __forceinline__ void cache_writeback(const C& c, CacheEntry* E) {
   }
 }
 
+template <class C>
+__device__ __forceinline__ void cache_set_state(C& c, int lvl, CacheEntry* E, uint32_t ch, bool dirty) {
+  if constexpr (kRegLadder<C>) {
+    LadderReg::bit_set(c.lad.cv0, c.lad.cv1, lvl);
+    if (dirty)
+      LadderReg::bit_set(c.lad.cd0, c.lad.cd1, lvl);
+    else
+      LadderReg::bit_clr(c.lad.cd0, c.lad.cd1, lvl);
+    if (lane_id() == 0) E->cid = ch;
+  } else if (lane_id() == 0) {
+    E->cid = ch;
+    E->dirty = dirty ? 1u : 0u;
+  }
+}
+
 // Make `ch` (the head chunk of level lvl) the cached chunk of its entry; returns the entry.
 template <class C>
-__device__ CacheEntry* cache_get(C& c, int lvl, uint32_t ch) {
+__device__ __forceinline__ CacheEntry* cache_get(C& c, int lvl, uint32_t ch) {
   CacheEntry* E = centry(c, lvl);
-  const uint32_t cur = rl32(E->cid, 0);
-  if (cur == ch) return E;
+  if constexpr (kRegLadder<C>) {
+    if (LadderReg::bit_get(c.lad.cv0, c.lad.cv1, lvl)) return E;  // valid => holds the head
+  } else {
+    const uint32_t cur = rl32(E->cid, 0);
+    if (cur == ch) return E;
+    if (cur != NIL) COUNT(c, CT_EVICT);
+    cache_writeback(c, lvl, E);
+  }
   COUNT(c, CT_MISS);
-  if (cur != NIL) COUNT(c, CT_EVICT);
-  cache_writeback(c, E);
   const int lane = lane_id();
   const bool act = lane < ME_C;
   const size_t g = (size_t)ch * ME_C + (act ? lane : 0);
@@ -503,54 +477,53 @@ __device__ CacheEntry* cache_get(C& c, int lvl, uint32_t ch) {
     E->qty[lane] = q;
     E->seq[lane] = sq;
   }
-  if (lane == 0) {
-    E->cid = ch;
-    E->dirty = 0;
-    E->next = nx;
-  }
-  wave_mem_order();
+  if (lane == 0) E->next = nx;
+  cache_set_state(c, lvl, E, ch, false);
   return E;
 }
 
 // A brand-new (all-empty) chunk becomes the head of an empty level: install it without a load.
 template <class C>
-__device__ void cache_install_new(C& c, int lvl, uint32_t ch) {
+__device__ __forceinline__ void cache_install_new(C& c, int lvl, uint32_t ch) {
   CacheEntry* E = centry(c, lvl);
-  cache_writeback(c, E);
+  if constexpr (!kRegLadder<C>) cache_writeback(c, lvl, E);  // register ladder: entry of an empty level is invalid
   const int lane = lane_id();
   if (lane < ME_C) {
     E->qty[lane] = 0;
     E->seq[lane] = 0ull;
   }
-  if (lane == 0) {
-    E->cid = ch;
-    E->dirty = 1;
-    E->next = NIL;
-  }
-  wave_mem_order();
+  if (lane == 0) E->next = NIL;
+  cache_set_state(c, lvl, E, ch, true);
 }
 
-// The cached chunk of lvl (if it is ch) is being freed or unlinked: HBM must hold its final
-// (all-zero) quantities before the chunk is reused.
+// The cached chunk ch of lvl is being freed or unlinked: HBM must hold its final (all-zero)
+// quantities before the chunk is reused. Callers pass the chunk the entry holds (the level's
+// head, or the chunk a walk just loaded); generic ladders double-check the id.
 template <class C>
 __device__ __forceinline__ void cache_drop(C& c, int lvl, uint32_t ch) {
   if (!c.cache) return;
   CacheEntry* E = centry(c, lvl);
-  if (rl32(E->cid, 0) != ch) return;
-  cache_writeback(c, E);
-  if (lane_id() == 0) E->cid = NIL;
-  wave_mem_order();
+  if constexpr (kRegLadder<C>) {
+    if (!LadderReg::bit_get(c.lad.cv0, c.lad.cv1, lvl)) return;
+  } else {
+    if (rl32(E->cid, 0) != ch) return;
+  }
+  cache_writeback(c, lvl, E, ch);
+  if constexpr (kRegLadder<C>) {
+    LadderReg::bit_clr(c.lad.cv0, c.lad.cv1, lvl);
+    LadderReg::bit_clr(c.lad.cd0, c.lad.cd1, lvl);
+  } else if (lane_id() == 0) {
+    E->cid = NIL;
+  }
 }
 
 // chdr[ch].next = v, mirrored into the cache entry of lvl when it holds ch.
 template <class C>
 __device__ __forceinline__ void set_next(C& c, int lvl, uint32_t ch, uint32_t v) {
+  const bool mirror = c.cache && cache_holds(c, lvl, ch);
   if (lane_id() == 0) {
     c.bk.chdr[ch].next = v;
-    if (c.cache) {
-      CacheEntry* E = centry(c, lvl);
-      if (E->cid == ch) E->next = v;
-    }
+    if (mirror) centry(c, lvl)->next = v;
   }
 }
 
@@ -624,7 +597,7 @@ __device__ __forceinline__ void emit_fills(C& c, bool e, unsigned long long take
 // trip loads header and slots together. Exhausted chunks go back to the free list. Returns the
 // new head chunk (NIL: level emptied).
 template <class C>
-__device__ uint32_t walk_level(C& c, int lvl, long long take, uint32_t head, uint32_t tail,
+__device__ __forceinline__ uint32_t walk_level(C& c, int lvl, long long take, uint32_t head, uint32_t tail,
                                unsigned long long taker) {
   const int lane = lane_id();
   const BookDev& bk = c.bk;
@@ -665,7 +638,7 @@ __device__ uint32_t walk_level(C& c, int lvl, long long take, uint32_t head, uin
     emit_fills(c, fe, taker, sv, price, (int)f);
     if (E) {
       if (fe) E->qty[lane] = qv - (int)f;
-      if (lane == 0) E->dirty = 1;
+      cache_mark_dirty(c, lvl);
     } else if (fe) {
       bk.cqty[g] = qv - (int)f;
     }
@@ -721,7 +694,7 @@ __device__ __forceinline__ bool take_level(C& c, int lvl, long long tot, long lo
 // LadderMem: 64-level windows — lanes load consecutive levels, an inclusive scan of their totals
 // says how far the taker reaches. LadderReg: one masked scan over the register-resident ladder.
 template <class C>
-__device__ long long sweep(C& c, int dir, int lim, long long want, unsigned long long taker, uint32_t& nfill) {
+__device__ __forceinline__ long long sweep(C& c, int dir, int lim, long long want, unsigned long long taker, uint32_t& nfill) {
   const int lane = lane_id();
   const int L = (int)c.bk.L;
   long long rem = want;
@@ -746,40 +719,18 @@ __device__ long long sweep(C& c, int dir, int lim, long long want, unsigned long
       return want;
     }
   }
-  if constexpr (__is_same(decltype(c.lad), LadderReg)) {
-    // masked totals of the levels the taker may reach, in natural lane order (row 0 = levels
-    // 0..63, row 1 = 64..127); prefix for BUY (upward), suffix for SELL (downward)
-    const int lo = dir > 0 ? cur : lim, hi = dir > 0 ? lim : cur;
-    const int l0v = lane, l1v = 64 + lane;
-    const long long m0 = (l0v >= lo && l0v <= hi) ? c.lad.t0 : 0;
-    const long long m1 = (l1v >= lo && l1v <= hi && l1v < L) ? c.lad.t1 : 0;
-    const long long i0 = wave_incl_scan(m0);
-    const long long c0 = rli64(i0, 63);
-    const long long i1 = wave_incl_scan(m1) + c0;
-    const long long all = rli64(i1, 63);
-    // amount strictly before a level in sweep order
-    const long long b0 = dir > 0 ? i0 - m0 : all - i0;
-    const long long b1 = dir > 0 ? i1 - m1 : all - i1;
-    unsigned long long t0m = __ballot(m0 > 0 && b0 < want);
-    unsigned long long t1m = __ballot(m1 > 0 && b1 < want);
-    STAMP_ADD(c, PH_SW_WINDOW);
-    // visit touched levels in sweep order: ascending (BUY) or descending (SELL)
-    for (int pass = 0; pass < 2; ++pass) {
-      const int row = dir > 0 ? pass : 1 - pass;
-      unsigned long long tm = row ? t1m : t0m;
-      while (tm) {
-        const int t = dir > 0 ? __builtin_ctzll(tm) : 63 - __builtin_clzll(tm);
-        tm &= ~(1ull << t);
-        const int lvl = row * 64 + t;
-        const long long ltot = row ? rli64(c.lad.t1, t) : rli64(c.lad.t0, t);
-        const long long before = row ? rli64(b1, t) : rli64(b0, t);
-        long long take = want - before;
-        if (take > ltot) take = ltot;
-        const uint32_t head = row ? rl32(c.lad.h1, t) : rl32(c.lad.h0, t);
-        const uint32_t tail = row ? rl32(c.lad.l1, t) : rl32(c.lad.l0, t);
-        emptied |= take_level(c, lvl, ltot, take, head, tail, taker);
-        rem -= take;
-      }
+  if constexpr (kRegLadder<C>) {
+    // level by level from the best: the occupancy bit scan finds the next level in SALU, the
+    // level header is a readlane — no scan, no memory round trip
+    while (rem > 0 && (dir > 0 ? (cur <= lim && cur < L) : (cur >= lim && cur >= 0))) {
+      const Level B = c.lad.get(cur);
+      const long long take = B.total < rem ? B.total : rem;
+      const bool gone = take_level(c, cur, B.total, take, B.head, B.tail, taker);
+      rem -= take;
+      if (!gone) break;  // partially consumed: the taker is done
+      emptied = true;
+      cur = dir > 0 ? c.lad.next_occ(cur + 1) : c.lad.prev_occ(cur - 1);
+      STAMP_ADD(c, PH_SW_JUMP);
     }
   } else {
     while (rem > 0) {
@@ -835,12 +786,13 @@ __device__ long long sweep(C& c, int dir, int lim, long long want, unsigned long
 // Append a resting order at the tail of level lvl's FIFO. The tail fill count lives beside the
 // level, so the common case issues no HBM load; a tail that is the cached head is written on chip.
 template <class C>
-__device__ bool rest_order(C& c, int lvl, unsigned long long seq, int qty, bool buy) {
+__device__ __forceinline__ bool rest_order(C& c, int lvl, unsigned long long seq, int qty, bool buy) {
   const int lane = lane_id();
   const BookDev& bk = c.bk;
   Level L = c.lad.get(lvl);
   const uint32_t te = c.lad.get_te(lvl);
   uint32_t ch, slot;
+  bool in_cache = false;  // does the slot live in the cached head chunk?
   if (L.tail != NIL && L.tail >= bk.nchunks) {
     set_err(bk, ERR_INCONSISTENT);
     return false;
@@ -861,23 +813,26 @@ __device__ bool rest_order(C& c, int lvl, unsigned long long seq, int qty, bool 
     if (L.tail != NIL) set_next(c, lvl, L.tail, ch);
     if (L.tail == NIL) {
       L.head = ch;
-      if (c.cache) cache_install_new(c, lvl, ch);
+      if (c.cache) {
+        cache_install_new(c, lvl, ch);
+        in_cache = true;
+      }
     }
     L.tail = ch;
   } else {
     ch = L.tail;
     slot = te;
+    in_cache = ch == L.head && cache_holds(c, lvl, ch);  // the ladder still names the current head
   }
   const size_t g = (size_t)ch * ME_C + slot;
   const bool was_empty = (L.total == 0);
   L.total += qty;
-  const bool in_cache = c.cache && ch == L.head && cache_holds(c, lvl, ch);
+  if (in_cache) cache_mark_dirty(c, lvl);
   if (lane == 0) {
     if (in_cache) {
       CacheEntry* E = centry(c, lvl);
       E->seq[slot] = seq;
       E->qty[slot] = qty;
-      E->dirty = 1;
     } else {
       bk.cseq[g] = seq;
       bk.cqty[g] = qty;
@@ -900,7 +855,7 @@ __device__ bool rest_order(C& c, int lvl, unsigned long long seq, int qty, bool 
 // A chunk left without live orders is unlinked from its FIFO at once (so chunks in use never
 // exceed resting orders); a level left empty returns its whole FIFO to the free list.
 template <class C>
-__device__ int cancel_order(C& c, unsigned long long tgt) {
+__device__ __forceinline__ int cancel_order(C& c, unsigned long long tgt) {
   const BookDev& bk = c.bk;
   const int lane = lane_id();
   if (tgt == 0ull || tgt >= bk.max_seq) return 0;
@@ -936,10 +891,10 @@ __device__ int cancel_order(C& c, unsigned long long tgt) {
     set_err(bk, ERR_INCONSISTENT);
     return q;
   }
+  if (E) cache_mark_dirty(c, lvl);
   if (lane == 0) {
     if (E) {
       E->qty[slot] = 0;
-      E->dirty = 1;
     } else {
       bk.cqty[g] = 0;
     }
@@ -972,7 +927,7 @@ __device__ int cancel_order(C& c, unsigned long long tgt) {
       set_next(c, lvl, prv, nxt);
       if (lane == 0) bk.chdr[nxt].prev = prv;
     }
-    cache_drop(c, lvl, ch);
+    if (ch == L.head) cache_drop(c, lvl, ch);  // the cache only ever holds a level's head
     L.head = nh;
     L.tail = nt;
     c.lad.set(lvl, L);
@@ -1030,7 +985,7 @@ enum LadderKind { LAD_HBM = 0, LAD_LDS = 1, LAD_REG = 2 };
 
 // The per-record loop of one symbol, shared by every ladder kind.
 template <class C>
-__device__ void match_records(C& c, const BatchDev& bt, uint32_t lo, uint32_t hi) {
+__device__ __forceinline__ void match_records(C& c, const BatchDev& bt, uint32_t lo, uint32_t hi) {
   const int lane = lane_id();
   const BookDev& bk = c.bk;
   const long long Lw = (long long)bk.L;
@@ -1118,7 +1073,7 @@ __device__ void match_records(C& c, const BatchDev& bt, uint32_t lo, uint32_t hi
 
 // Dirty cached head chunks back to HBM: lane = (entry, slot) pairs, 4 entries per pass.
 template <class C>
-__device__ void cache_flush_all(C& c, uint32_t entries) {
+__device__ __forceinline__ void cache_flush_all(C& c, uint32_t entries) {
   const int lane = lane_id();
   wave_mem_order();
   for (uint32_t e0 = 0; e0 < entries; e0 += 64 / ME_C) {
@@ -1133,7 +1088,7 @@ __device__ void cache_flush_all(C& c, uint32_t entries) {
 }
 
 template <class C>
-__device__ bool wave_begin(C& c, const BookDev& bk, const BatchDev& bt, uint32_t s, uint32_t lo, uint32_t hi) {
+__device__ __forceinline__ bool wave_begin(C& c, const BookDev& bk, const BatchDev& bt, uint32_t s, uint32_t lo, uint32_t hi) {
   const int lane = lane_id();
   c.bk = bk;
   c.s = s;
@@ -1161,7 +1116,7 @@ __device__ bool wave_begin(C& c, const BookDev& bk, const BatchDev& bt, uint32_t
 }
 
 template <class C>
-__device__ void wave_end(C& c) {
+__device__ __forceinline__ void wave_end(C& c) {
   if (lane_id() == 0) {
     SymState o;
     o.base = c.base;
@@ -1192,19 +1147,7 @@ __global__ __launch_bounds__(256) void k_match(BookDev bk, BatchDev bt) {
   const uint32_t hi = wave_lower_bound(bt.skeys, bt.n, s + 1);
   if (lo >= hi) return;
   if (s == bk.S) {
-    for (uint32_t j = lo + lane; j < hi; j += 64) {
-      uint32_t i = bt.perm[j];
-      me_order_result r;
-      r.filled_qty = 0;
-      r.remaining_qty = 0;
-      r.fill_count = 0;
-      r.tape_offset = 0;
-      r.status = ME_ST_REJECTED;
-      r.reason = ME_RJ_BAD_SYMBOL;
-      r.pad[0] = r.pad[1] = 0;
-      bt.res[i] = r;
-      bt.fstart[i] = 0;
-    }
+    reject_bad_symbols(bt, lo, hi);
     return;
   }
   const uint32_t L = bk.L;
@@ -1232,14 +1175,28 @@ __global__ __launch_bounds__(256) void k_match(BookDev bk, BatchDev bt) {
     c.lad.e0 = g_tend[lane];
     c.lad.e1 = (64 + (uint32_t)lane < L) ? g_tend[64 + lane] : 0u;
     c.lad.L = L;
+    c.lad.occ0 = __ballot(a.total > 0);
+    c.lad.occ1 = __ballot(b.total > 0);
+    c.lad.cv0 = c.lad.cv1 = c.lad.cd0 = c.lad.cd1 = 0ull;
     c.cache = (CacheEntry*)(smem + (size_t)wv * lds_wave_bytes_reg());
     c.cmask = CK_REG - 1;
-    for (uint32_t i = lane; i < (uint32_t)CK_REG; i += 64) c.cache[i].cid = NIL;
-    wave_mem_order();
     if (!wave_begin(c, bk, bt, s, lo, hi)) return;
     STAMP_ADD(c, PH_PROLOGUE);
     match_records(c, bt, lo, hi);
-    cache_flush_all(c, CK_REG);
+    // dirty cached heads back to HBM (valid entry l holds the head of level l)
+    for (int row = 0; row < 2; ++row) {
+      unsigned long long d = row ? (c.lad.cd1 & c.lad.cv1) : (c.lad.cd0 & c.lad.cv0);
+      while (d) {
+        const int j = __builtin_ctzll(d);
+        d &= d - 1;
+        const uint32_t cid = row ? rl32(c.lad.h1, j) : rl32(c.lad.h0, j);
+        const CacheEntry* E = c.cache + row * 64 + j;
+        if (lane < ME_C) {
+          c.bk.cqty[(size_t)cid * ME_C + lane] = E->qty[lane];
+          c.bk.cseq[(size_t)cid * ME_C + lane] = E->seq[lane];
+        }
+      }
+    }
     g_lv[lane] = Level{c.lad.t0, c.lad.h0, c.lad.l0};
     g_tend[lane] = (uint8_t)c.lad.e0;
     if (64 + (uint32_t)lane < L) {
@@ -1389,11 +1346,13 @@ hipError_t launch_sort_pass(hipStream_t st, const uint32_t* keys_in, const uint3
   return hipGetLastError();
 }
 
+hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev& bt);
+
 hipError_t launch_match(hipStream_t st, const BookDev& bk, const BatchDev& bt) {
   const uint32_t waves = bk.S + 1;
   const dim3 grid((waves + 3) / 4), block(256);
   if (bk.L <= 128) {
-    hipLaunchKernelGGL(k_match<LAD_REG>, grid, block, 4 * lds_wave_bytes_reg(), st, bk, bt);
+    return launch_match_reg(st, bk, bt);
   } else if (bk.L <= LDS_MAX_LEVELS) {
     hipLaunchKernelGGL(k_match<LAD_LDS>, grid, block, 4 * lds_wave_bytes(bk.L), st, bk, bt);
   } else {

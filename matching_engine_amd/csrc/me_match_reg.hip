@@ -1,0 +1,644 @@
+// me_match_reg.hip — k_match_reg: the matching kernel for ladders of at most 128 levels (the
+// depth of benchmark configurations 1, 2, 3 and 5). Same book layout in HBM and same semantics as
+// the generic k_match (me_kernels.hip; pinned by oracle/oracle_book.cpp), built for the shortest
+// per-record instruction chain, since a symbol's records are an inherently serial chain and one
+// wavefront per symbol leaves nothing else to hide latency behind:
+//
+//   * the ladder's FIFO ends (head chunk, tail chunk, tail fill) live in VGPRs — level l is lane
+//     l & 63 of row l >> 6 — so reading one is a v_readlane and writing one a lane select;
+//   * occupancy and the head-chunk cache's valid / dirty state are 128-bit SGPR masks, so the
+//     next best price is a bit scan and a cache lookup a bit test;
+//   * the head chunk of every level can sit in LDS (16 slots of qty + seq: 26 KB per wave, no
+//     evictions); fills, appends and cancels of a cached head never touch HBM, and it is written
+//     back once at the end of the launch;
+//   * level totals are only ever added to on the hot path: fire-and-forget LDS atomics;
+//   * a chunk's 16 slots are ranked with a 4-step DPP scan of 32-bit saturating adds (one DPP row;
+//     saturation keeps the comparison with the remaining taker quantity exact);
+//   * reject reasons, prices -> levels and the per-record result records are computed for 64
+//     records at a time in vector form; the serial loop visits only records that touch the book
+//     and hands back two numbers per record (quantity, fill count).
+#include <hip/hip_runtime.h>
+
+#include "me_layout.hpp"
+#include "me_wave.hpp"
+
+namespace me {
+
+constexpr int RL = 128;  // levels covered by this kernel
+
+// One wave's LDS: the head-chunk cache (entry l = head chunk of level l) and the level totals.
+struct RegLds {
+  int cq[RL][ME_C];
+  unsigned long long cs[RL][ME_C];
+  long long tot[RL];
+  uint32_t cnext[RL];  // chdr[head].next of the cached head (kept in step with HBM)
+};
+constexpr int REG_WAVES = 4;  // waves (symbols) per workgroup
+
+// One 32-bit field of the 128-level ladder: level l is lane (l & 63) of row (l >> 6).
+struct Row2 {
+  uint32_t r0, r1;
+  __device__ __forceinline__ uint32_t get(int l) const { return rl32(l < 64 ? r0 : r1, l & 63); }
+  __device__ __forceinline__ void put(int l, uint32_t v) {
+    const int lane = lane_id();
+    r0 = lane == l ? v : r0;  // l >= 64 never matches a lane of row 0
+    r1 = lane == l - 64 ? v : r1;
+  }
+};
+
+// 128-bit wave-uniform bit set over the levels.
+struct Mask2 {
+  unsigned long long w0, w1;
+  static __device__ __forceinline__ unsigned long long lo(int l) { return l < 64 ? (1ull << (l & 63)) : 0ull; }
+  static __device__ __forceinline__ unsigned long long hi(int l) { return l >= 64 ? (1ull << (l & 63)) : 0ull; }
+  __device__ __forceinline__ bool bit(int l) const { return ((l < 64 ? w0 : w1) >> (l & 63)) & 1ull; }
+  __device__ __forceinline__ void set(int l) {
+    w0 |= lo(l);
+    w1 |= hi(l);
+  }
+  __device__ __forceinline__ void clr(int l) {
+    w0 &= ~lo(l);
+    w1 &= ~hi(l);
+  }
+  // smallest set bit >= x (x may be 128), or 128 if none
+  __device__ __forceinline__ int next(int x) const {
+    if (x < 64) {
+      const unsigned long long w = w0 & (~0ull << x);
+      if (w) return __builtin_ctzll(w);
+      return w1 ? 64 + __builtin_ctzll(w1) : RL;
+    }
+    if (x >= RL) return RL;
+    const unsigned long long w = w1 & (~0ull << (x - 64));
+    return w ? 64 + __builtin_ctzll(w) : RL;
+  }
+  // largest set bit <= x (x may be -1), or -1 if none
+  __device__ __forceinline__ int prev(int x) const {
+    if (x >= 64) {
+      const unsigned long long w = w1 & (~0ull >> (63 - (x - 64)));
+      if (w) return 127 - __builtin_clzll(w);
+      return w0 ? 63 - __builtin_clzll(w0) : -1;
+    }
+    if (x < 0) return -1;
+    const unsigned long long w = w0 & (~0ull >> (63 - x));
+    return w ? 63 - __builtin_clzll(w) : -1;
+  }
+};
+
+struct RegCtx {
+  ChunkHdr* chdr;
+  uint32_t* owner;
+  unsigned long long* cseq;
+  int* cqty;
+  uint32_t* loc;
+  uint32_t* chunk_top;
+  uint32_t* err;
+  me_fill* scratch;
+  RegLds* M;
+  unsigned long long max_seq;
+  long long base;
+  uint32_t nchunks, L;
+  uint32_t s, gs;
+  Row2 hd, tl, te;     // head chunk, tail chunk, slots written in the tail chunk
+  Mask2 occ, cv, cd;   // occupied levels, cache entry valid (holds the head), cache entry dirty
+  int bb, ba;          // best bid level (-1: none), best ask level (RL: none)
+  uint32_t free_head;  // this symbol's chunk free list ...
+  uint32_t free_next;  // ... and chdr[free_head].next (VGPR, loaded ahead of the pop)
+  uint32_t bump_cur, bump_end, recs_left;
+  int resting;
+  uint32_t wptr;       // next scratch fill of this wave
+};
+
+__device__ __forceinline__ void reg_err(const RegCtx& c, uint32_t bits) {
+  if (lane_id() == 0) atomicOr(c.err, bits);
+}
+
+// Inclusive scan of a 16-lane row (each DPP row scans on its own), saturating at 2^32 - 1.
+__device__ __forceinline__ uint32_t scan16_sat(uint32_t x) {
+  x = __builtin_elementwise_add_sat(x, dpp32<0x111, 0xF>(x));  // row_shr:1
+  x = __builtin_elementwise_add_sat(x, dpp32<0x112, 0xF>(x));  // row_shr:2
+  x = __builtin_elementwise_add_sat(x, dpp32<0x114, 0xF>(x));  // row_shr:4
+  x = __builtin_elementwise_add_sat(x, dpp32<0x118, 0xF>(x));  // row_shr:8
+  return x;
+}
+
+// Exclusive 64-lane scan of a 32-bit count.
+__device__ __forceinline__ uint32_t wave_excl_scan32(uint32_t x) {
+  uint32_t v = x;
+  v += dpp32<0x111, 0xF>(v);
+  v += dpp32<0x112, 0xF>(v);
+  v += dpp32<0x114, 0xF>(v);
+  v += dpp32<0x118, 0xF>(v);
+  v += dpp32<0x142, 0xA>(v);  // row_bcast:15
+  v += dpp32<0x143, 0xC>(v);  // row_bcast:31
+  return v - x;
+}
+
+__device__ __forceinline__ void tot_add(RegCtx& c, int lvl, long long d) {
+  if (lane_id() == 0) __hip_atomic_fetch_add(&c.M->tot[lvl], d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// ---- chunk pool ----------------------------------------------------------------------------
+__device__ __forceinline__ void reg_prefetch_free_next(RegCtx& c) {
+  const bool ok = c.free_head < c.nchunks;
+  const uint32_t v = c.chdr[ok ? c.free_head : 0].next;
+  c.free_next = ok ? v : NIL;
+}
+
+// Free-list push of a chunk whose HBM quantities are all zero.
+__device__ __forceinline__ void reg_free(RegCtx& c, uint32_t ch) {
+  if (lane_id() == 0) c.chdr[ch].next = c.free_head;
+  c.free_next = c.free_head;
+  c.free_head = ch;
+}
+
+__device__ __forceinline__ uint32_t reg_alloc(RegCtx& c) {
+  if (c.free_head != NIL) {
+    const uint32_t ch = c.free_head;
+    if (ch >= c.nchunks) {
+      reg_err(c, ERR_INCONSISTENT);
+      return NIL;
+    }
+    c.free_head = rl32(c.free_next, 0);
+    reg_prefetch_free_next(c);
+    return ch;
+  }
+  if (c.bump_cur >= c.bump_end) {
+    // each record needs at most one new chunk: never reserve more than the records left
+    const uint32_t blk = min(16u, max(c.recs_left, 1u));
+    uint32_t got = 0;
+    if (lane_id() == 0) got = atomicAdd(c.chunk_top, blk);
+    got = rl32(got, 0);
+    if (got >= c.nchunks) {
+      reg_err(c, ERR_CHUNK_OOM);
+      return NIL;
+    }
+    c.bump_cur = got;
+    c.bump_end = min(got + blk, c.nchunks);
+  }
+  return c.bump_cur++;
+}
+
+// ---- taking liquidity ----------------------------------------------------------------------
+// Consume up to `rem` from the FIFO of level lvl, oldest first, emitting one fill per maker slot
+// touched. Returns true if the level emptied. A slot is live iff its qty > 0.
+__device__ __forceinline__ bool reg_walk(RegCtx& c, int lvl, uint32_t& rem, unsigned long long taker) {
+  const int lane = lane_id();
+  const bool act = lane < ME_C;
+  const int sl = lane & (ME_C - 1);
+  const long long price = c.base + lvl;
+  const uint32_t head = c.hd.get(lvl);
+  const uint32_t tail = c.tl.get(lvl);
+  uint32_t ch = head;
+  uint32_t taken = 0;
+  for (;;) {
+    int qv;
+    unsigned long long sv;
+    uint32_t nx;
+    if (c.cv.bit(lvl)) {
+      qv = act ? c.M->cq[lvl][sl] : 0;
+      sv = c.M->cs[lvl][sl];
+      nx = c.M->cnext[lvl];
+    } else {
+      if (ch >= c.nchunks) {  // NIL or corrupt: never index with it
+        reg_err(c, ERR_INCONSISTENT);
+        return false;
+      }
+      const size_t g = (size_t)ch * ME_C + sl;
+      nx = c.chdr[ch].next;
+      qv = act ? c.cqty[g] : 0;
+      sv = c.cseq[g];
+      if (act) {
+        c.M->cq[lvl][sl] = qv;
+        c.M->cs[lvl][sl] = sv;
+      }
+      if (lane == 0) c.M->cnext[lvl] = nx;
+      c.cv.set(lvl);
+      c.cd.clr(lvl);
+    }
+    const uint32_t uq = (uint32_t)qv;
+    const uint32_t inc = scan16_sat(uq);
+    const uint32_t ex = inc - uq;
+    uint32_t f = rem > ex ? rem - ex : 0u;
+    f = f < uq ? f : uq;
+    const bool fe = f != 0u;
+    const unsigned long long fm = __ballot(fe);
+    if (fe) {
+      me_fill F;
+      F.taker_seq = taker;
+      F.maker_seq = sv;
+      F.price_q4 = price;
+      F.qty = (int)f;
+      F.symbol = c.gs;
+      c.scratch[c.wptr + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u))] = F;
+      c.M->cq[lvl][sl] = (int)(uq - f);
+    }
+    c.wptr += (uint32_t)__popcll(fm);
+    c.cd.set(lvl);
+    c.resting -= __popcll(__ballot(fe && f == uq));  // makers filled completely leave the book
+    const uint32_t live = rl32(inc, 15);
+    const uint32_t t = rem < live ? rem : live;
+    rem -= t;
+    taken += t;
+    if (__ballot(act && uq > f)) break;  // a live slot remains: the taker is done
+    // chunk exhausted: its HBM copy must read all-zero before the chunk is reused
+    if (act) c.cqty[(size_t)ch * ME_C + sl] = 0;
+    c.cv.clr(lvl);
+    c.cd.clr(lvl);
+    reg_free(c, ch);
+    if (ch == tail) {
+      c.hd.put(lvl, NIL);
+      c.tl.put(lvl, NIL);
+      c.occ.clr(lvl);
+      tot_add(c, lvl, -(long long)taken);
+      return true;
+    }
+    ch = rl32(nx, 0);
+    if (rem == 0u) break;
+  }
+  tot_add(c, lvl, -(long long)taken);
+  if (ch != head) {
+    c.hd.put(lvl, ch);
+    if (lane == 0 && ch < c.nchunks) c.chdr[ch].prev = NIL;  // new FIFO head
+  }
+  return false;
+}
+
+// ---- resting -------------------------------------------------------------------------------
+// Append (seq, qty) at the tail of level lvl. A tail that is the cached head is written on chip.
+__device__ __forceinline__ bool reg_rest(RegCtx& c, int lvl, unsigned long long seq, uint32_t qty, bool buy) {
+  const int lane = lane_id();
+  const uint32_t tl = c.tl.get(lvl);
+  const uint32_t te = c.te.get(lvl);
+  uint32_t ch, slot;
+  bool in_cache;
+  if (tl == NIL || te >= (uint32_t)ME_C) {
+    ch = reg_alloc(c);
+    if (ch == NIL) return false;
+    slot = 0;
+    if (lane == 0) {
+      ChunkHdr h;
+      h.next = NIL;
+      h.prev = tl;
+      h.level = (uint32_t)lvl;
+      h.pad = 0;
+      c.chdr[ch] = h;
+      c.owner[ch] = c.s;
+    }
+    if (tl == NIL) {  // empty level: the new chunk is its head, installed in the cache zeroed
+      c.hd.put(lvl, ch);
+      if (lane < ME_C) c.M->cq[lvl][lane] = 0;
+      if (lane == 0) c.M->cnext[lvl] = NIL;
+      c.cv.set(lvl);
+      in_cache = true;
+    } else {
+      const bool tl_cached = c.cv.bit(lvl) && c.hd.get(lvl) == tl;
+      if (lane == 0) {
+        if (tl < c.nchunks) c.chdr[tl].next = ch;
+        if (tl_cached) c.M->cnext[lvl] = ch;
+      }
+      in_cache = false;
+    }
+    c.tl.put(lvl, ch);
+  } else {
+    if (tl >= c.nchunks) {
+      reg_err(c, ERR_INCONSISTENT);
+      return false;
+    }
+    ch = tl;
+    slot = te;
+    in_cache = c.cv.bit(lvl) && c.hd.get(lvl) == tl;
+  }
+  const uint32_t g = ch * ME_C + slot;
+  if (lane == 0) {
+    if (in_cache) {
+      c.M->cq[lvl][slot] = (int)qty;
+      c.M->cs[lvl][slot] = seq;
+    } else {
+      c.cqty[g] = (int)qty;
+      c.cseq[g] = seq;
+    }
+    c.loc[seq] = g;
+  }
+  tot_add(c, lvl, (long long)qty);
+  if (in_cache) c.cd.set(lvl);
+  c.te.put(lvl, slot + 1);
+  c.occ.set(lvl);
+  if (buy) {
+    if (lvl > c.bb) c.bb = lvl;
+  } else {
+    if (lvl < c.ba) c.ba = lvl;
+  }
+  c.resting += 1;
+  return true;
+}
+
+// ---- cancelling ----------------------------------------------------------------------------
+// Remove the live resting order `tgt` of this symbol; returns its qty, 0 if not live. A chunk
+// left without live orders is unlinked at once (chunks in use never exceed resting orders).
+__device__ __forceinline__ uint32_t reg_cancel(RegCtx& c, unsigned long long tgt) {
+  const int lane = lane_id();
+  const bool act = lane < ME_C;
+  if (tgt == 0ull || tgt >= c.max_seq) return 0;
+  wave_mem_order();
+  const uint32_t g = rl32(c.loc[tgt], 0);
+  if (g == NIL) return 0;
+  const uint32_t ch = g / ME_C, slot = g % ME_C;
+  if (ch >= c.nchunks) return 0;
+  // one round trip: owner, header, the chunk's quantities and the target seq
+  const uint32_t own = rl32(c.owner[ch], 0);
+  const ChunkHdr hdr = c.chdr[ch];
+  int qv = act ? c.cqty[(size_t)ch * ME_C + lane] : 0;
+  unsigned long long sq = rl64(c.cseq[g], 0);
+  if (own != c.s) return 0;  // another symbol's order: never touch its book
+  const int lvl = (int)rl32(hdr.level, 0);
+  if (lvl < 0 || lvl >= (int)c.L) {
+    reg_err(c, ERR_INCONSISTENT);
+    return 0;
+  }
+  const uint32_t h = c.hd.get(lvl), t = c.tl.get(lvl);
+  const bool in_cache = c.cv.bit(lvl) && h == ch;  // the on-chip copy is authoritative
+  if (in_cache) {
+    qv = act ? c.M->cq[lvl][lane & (ME_C - 1)] : 0;
+    sq = rl64(c.M->cs[lvl][slot], 0);
+  }
+  const int q = rli32(qv, (int)slot);
+  if (sq != tgt || q <= 0) return 0;
+  const uint32_t live_after = (uint32_t)__popcll(__ballot(qv > 0)) - 1u;
+  if (lane == 0) {
+    if (in_cache)
+      c.M->cq[lvl][slot] = 0;
+    else
+      c.cqty[g] = 0;
+  }
+  tot_add(c, lvl, -(long long)q);
+  if (in_cache) c.cd.set(lvl);
+  if (live_after == 0u) {
+    if (h >= c.nchunks || t >= c.nchunks) {
+      reg_err(c, ERR_INCONSISTENT);
+      return (uint32_t)q;
+    }
+    if (in_cache) {  // the chunk leaves the cache; its HBM copy must read all-zero
+      if (act) c.cqty[(size_t)ch * ME_C + lane] = 0;
+      c.cv.clr(lvl);
+      c.cd.clr(lvl);
+    }
+    const uint32_t nxt = rl32(hdr.next, 0), prv = rl32(hdr.prev, 0);
+    const bool mirror = c.cv.bit(lvl) && h == prv;  // the cached head is ch's predecessor
+    if (h == t) {  // ch was the level's only chunk: the level empties
+      c.hd.put(lvl, NIL);
+      c.tl.put(lvl, NIL);
+      c.occ.clr(lvl);
+      if (lvl == c.bb) c.bb = c.occ.prev(lvl);
+      if (lvl == c.ba) c.ba = c.occ.next(lvl);
+    } else if (ch == h) {
+      c.hd.put(lvl, nxt);
+      if (lane == 0) c.chdr[nxt].prev = NIL;
+    } else if (ch == t) {
+      c.tl.put(lvl, prv);
+      c.te.put(lvl, ME_C);  // a non-tail chunk is always full
+      if (lane == 0) {
+        c.chdr[prv].next = NIL;
+        if (mirror) c.M->cnext[lvl] = NIL;
+      }
+    } else {
+      if (lane == 0) {
+        c.chdr[prv].next = nxt;
+        c.chdr[nxt].prev = prv;
+        if (mirror) c.M->cnext[lvl] = nxt;
+      }
+    }
+    reg_free(c, ch);
+  }
+  c.resting -= 1;
+  return (uint32_t)q;
+}
+
+// ---- the kernel ----------------------------------------------------------------------------
+// Per-record control word built in vector form: lim level | BUY | MARKET | CANCEL.
+constexpr uint32_t CW_BUY = 1u << 8, CW_MKT = 1u << 9, CW_CXL = 1u << 10;
+
+__global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
+  __shared__ RegLds lds[REG_WAVES];
+  const int lane = lane_id();
+  const uint32_t wv = threadIdx.x >> 6;
+  const uint32_t s = blockIdx.x * REG_WAVES + wv;
+  if (s > bk.S) return;
+  const uint32_t lo = wave_lower_bound(bt.skeys, bt.n, s);
+  const uint32_t hi = wave_lower_bound(bt.skeys, bt.n, s + 1);
+  if (lo >= hi) return;
+  if (s == bk.S) {
+    reject_bad_symbols(bt, lo, hi);
+    return;
+  }
+  const uint32_t L = bk.L;
+  Level* g_lv = bk.levels + (size_t)s * L;
+  uint8_t* g_tend = bk.tend + (size_t)s * L;
+  RegCtx c;
+  c.chdr = bk.chdr;
+  c.owner = bk.owner;
+  c.cseq = bk.cseq;
+  c.cqty = bk.cqty;
+  c.loc = bk.loc;
+  c.chunk_top = bk.chunk_top;
+  c.err = bk.err;
+  c.scratch = bt.scratch;
+  c.M = &lds[wv];
+  c.max_seq = bk.max_seq;
+  c.nchunks = bk.nchunks;
+  c.L = L;
+  c.s = s;
+  c.gs = bk.gsym ? bk.gsym[s] : s;
+  // ladder rows; totals to LDS; occupancy = levels with a FIFO
+  const bool in1 = 64u + (uint32_t)lane < L;
+  Level a = g_lv[lane];
+  Level b;
+  b.total = 0;
+  b.head = b.tail = NIL;
+  if (in1) b = g_lv[64 + lane];
+  c.hd.r0 = a.head;
+  c.hd.r1 = b.head;
+  c.tl.r0 = a.tail;
+  c.tl.r1 = b.tail;
+  c.te.r0 = g_tend[lane];
+  c.te.r1 = in1 ? (uint32_t)g_tend[64 + lane] : 0u;
+  c.M->tot[lane] = a.total;
+  c.M->tot[64 + lane] = b.total;
+  c.occ.w0 = __ballot(a.total > 0);
+  c.occ.w1 = __ballot(b.total > 0);
+  c.cv.w0 = c.cv.w1 = c.cd.w0 = c.cd.w1 = 0ull;
+  const SymState st = bk.sym[s];
+  c.base = rli64(st.base, 0);
+  c.bb = rli32(st.best_bid, 0);
+  c.ba = rli32(st.best_ask, 0);
+  if (c.ba > RL) c.ba = RL;
+  c.free_head = rl32(st.free_head, 0);
+  reg_prefetch_free_next(c);
+  c.bump_cur = c.bump_end = 0;
+  c.resting = (int)rl32(st.resting, 0);
+  {
+    // scratch run of this wave: fills <= resting makers + 2 * records
+    const unsigned long long need = (unsigned long long)(uint32_t)c.resting + 2ull * (hi - lo);
+    unsigned long long w0 = 0;
+    if (lane == 0) w0 = atomicAdd(bt.scratch_top, need);
+    w0 = rl64(w0, 0);
+    if (w0 + need > bt.scratch_cap) {
+      reg_err(c, ERR_SCRATCH_OOM);
+      return;
+    }
+    c.wptr = (uint32_t)w0;
+  }
+  const long long Lw = (long long)L;
+  for (uint32_t blk = lo; blk < hi; blk += 64) {
+    // ---- 64 records in vector form
+    const uint32_t j = blk + (uint32_t)lane;
+    const bool v = j < hi;
+    const uint32_t oi = v ? bt.perm[j] : 0u;
+    const unsigned long long oseq = v ? bt.seq[oi] : 0ull;
+    const long long opx = v ? bt.px[oi] : 0ll;
+    const int oq = v ? bt.qty[oi] : 0;
+    const uint32_t kd = v ? (uint32_t)bt.kind[oi] : 0u;
+    const uint32_t side = kd & 3u;
+    const bool market = (kd >> 2) & 1u, cancel = (kd >> 3) & 1u;
+    const bool buy = side == ME_SIDE_BUY;
+    const bool oow = opx < c.base || (unsigned long long)(opx - c.base) >= (unsigned long long)Lw;
+    uint32_t rj = ME_RJ_NONE;
+    if (!cancel) {
+      if (oq <= 0)
+        rj = ME_RJ_BAD_QTY;
+      else if (side != ME_SIDE_BUY && side != ME_SIDE_SELL)
+        rj = ME_RJ_BAD_SIDE;
+      else if (!market && oow)
+        rj = ME_RJ_OUT_OF_WINDOW;
+      else if (oseq == 0ull || oseq >= c.max_seq)
+        rj = ME_RJ_BAD_SEQ;
+    }
+    const uint32_t lim = market ? (buy ? L - 1u : 0u) : (oow ? 0u : (uint32_t)(opx - c.base));
+    const uint32_t cw = lim | (buy ? CW_BUY : 0u) | (market ? CW_MKT : 0u) | (cancel ? CW_CXL : 0u);
+    unsigned long long work = __ballot(v && rj == ME_RJ_NONE);
+    const uint32_t cnt = min(64u, hi - blk);
+    uint32_t stop = cnt;  // records [0, stop) of the block get results
+    uint32_t out_q = 0, out_n = 0;
+    const uint32_t w_blk = c.wptr;
+    // ---- the serial chain: records that touch the book, in seq order
+    while (work) {
+      const int k = __builtin_ctzll(work);
+      work &= work - 1ull;
+      const uint32_t ctl = rl32(cw, k);
+      const uint32_t w_in = c.wptr;
+      c.recs_left = hi - (blk + (uint32_t)k);
+      uint32_t outq;
+      if (ctl & CW_CXL) {
+        outq = reg_cancel(c, (unsigned long long)rli64(opx, k));
+      } else {
+        const unsigned long long seq = rl64(oseq, k);
+        const uint32_t q = (uint32_t)rli32(oq, k);
+        const int lm = (int)(ctl & 0xFFu);
+        uint32_t rem = q;
+        if (ctl & CW_BUY) {
+          while (rem != 0u && c.ba <= lm) {
+            const int lvl = c.ba;
+            if (!reg_walk(c, lvl, rem, seq)) break;
+            c.ba = c.occ.next(lvl + 1);
+          }
+        } else {
+          while (rem != 0u && c.bb >= lm) {
+            const int lvl = c.bb;
+            if (!reg_walk(c, lvl, rem, seq)) break;
+            c.bb = c.occ.prev(lvl - 1);
+          }
+        }
+        outq = q - rem;
+        if (!(ctl & CW_MKT) && rem != 0u && !reg_rest(c, lm, seq, rem, (ctl & CW_BUY) != 0u)) {
+          stop = (uint32_t)k;  // chunk pool exhausted: the batch fails (sticky error word)
+          break;
+        }
+      }
+      const bool me_ = lane == k;
+      out_q = me_ ? outq : out_q;
+      out_n = me_ ? c.wptr - w_in : out_n;
+    }
+    // ---- results of the block in vector form
+    const uint32_t ex = wave_excl_scan32(out_n);  // fills of the block's earlier records
+    if (v && (uint32_t)lane < stop) {
+      me_order_result r;
+      r.tape_offset = 0;
+      r.pad[0] = r.pad[1] = 0;
+      r.fill_count = out_n;
+      r.reason = (uint8_t)rj;
+      if (rj != ME_RJ_NONE) {
+        r.filled_qty = 0;
+        r.remaining_qty = rj == ME_RJ_BAD_QTY ? 0 : oq;
+        r.status = ME_ST_REJECTED;
+      } else if (cancel) {
+        r.filled_qty = 0;
+        r.remaining_qty = (int)out_q;
+        r.status = out_q ? ME_ST_CANCELED : ME_ST_REJECTED;
+        r.reason = out_q ? ME_RJ_NONE : ME_RJ_UNKNOWN_ORDER;
+      } else {
+        const int rem = oq - (int)out_q;
+        r.filled_qty = (int)out_q;
+        r.remaining_qty = rem;
+        r.status = rem == 0 ? ME_ST_FILLED
+                 : market   ? ME_ST_CANCELED
+                 : out_q    ? ME_ST_PARTIALLY_FILLED
+                            : ME_ST_NEW;
+      }
+      bt.res[oi] = r;
+      bt.fstart[oi] = w_blk + ex;
+      if (out_n) atomicAdd(&bt.tile_sum[oi / TILE_TAPE], out_n);
+    }
+    if (stop < cnt) break;
+  }
+  // ---- write the symbol back
+  while (c.bump_cur < c.bump_end) reg_free(c, c.bump_cur++);  // unused reserved chunks
+  for (int row = 0; row < 2; ++row) {  // dirty cached heads (valid entry l holds the head of l)
+    unsigned long long d = row ? (c.cd.w1 & c.cv.w1) : (c.cd.w0 & c.cv.w0);
+    while (d) {
+      const int jj = __builtin_ctzll(d);
+      d &= d - 1ull;
+      const uint32_t cid = rl32(row ? c.hd.r1 : c.hd.r0, jj);
+      const int e = row * 64 + jj;
+      if (lane < ME_C) {
+        c.cqty[(size_t)cid * ME_C + lane] = c.M->cq[e][lane];
+        c.cseq[(size_t)cid * ME_C + lane] = c.M->cs[e][lane];
+      }
+    }
+  }
+  wave_mem_order();
+  Level o;
+  o.total = c.M->tot[lane];
+  o.head = c.hd.r0;
+  o.tail = c.tl.r0;
+  g_lv[lane] = o;
+  g_tend[lane] = (uint8_t)c.te.r0;
+  if (in1) {
+    o.total = c.M->tot[64 + lane];
+    o.head = c.hd.r1;
+    o.tail = c.tl.r1;
+    g_lv[64 + lane] = o;
+    g_tend[64 + lane] = (uint8_t)c.te.r1;
+  }
+  unsigned long long* g_occ = bk.occ + (size_t)s * bk.Lwords;  // for the host-side book dump
+  if (lane == 0) {
+    g_occ[0] = c.occ.w0;
+    if (bk.Lwords > 1) g_occ[1] = c.occ.w1;
+    SymState so;
+    so.base = c.base;
+    so.best_bid = c.bb;
+    so.best_ask = c.ba >= (int)L ? (int)L : c.ba;
+    so.free_head = c.free_head;
+    so.resting = (uint32_t)c.resting;
+    so.pad[0] = so.pad[1] = 0;
+    bk.sym[s] = so;
+  }
+}
+
+hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev& bt) {
+  if (bk.L > (uint32_t)RL || bk.L < 64u) return hipErrorInvalidValue;
+  const uint32_t waves = bk.S + 1;
+  hipLaunchKernelGGL(k_match_reg, dim3((waves + REG_WAVES - 1) / REG_WAVES), dim3(64 * REG_WAVES), 0, st, bk, bt);
+  return hipGetLastError();
+}
+
+}  // namespace me
