@@ -23,6 +23,7 @@ hipError_t launch_sort_pass(hipStream_t st, const uint32_t* keys_in, const uint3
                             uint32_t* idx_out, uint32_t* zero_buf, uint32_t zero_words,
                             unsigned long long* scratch_top);
 hipError_t launch_match(hipStream_t st, const BookDev& bk, const BatchDev& bt);
+uint32_t sort_tile(uint32_t n);
 hipError_t launch_tape(hipStream_t st, const BatchDev& bt, me_fill* tape, unsigned long long tape_cap,
                        unsigned long long* tape_count, unsigned long long* fills_acc, uint32_t* err);
 hipError_t launch_init_levels(hipStream_t st, Level* levels, size_t count);
@@ -67,7 +68,10 @@ struct me_engine {
   me_fill* d_tape = nullptr;
   unsigned long long* d_tape_count = nullptr;
   unsigned long long* d_fills_acc = nullptr;  // fills since timing was (re)enabled
-  unsigned long long scratch_cap = 0;
+  unsigned long long scratch_cap = 0;  // fill scratch: per-symbol slabs + overflow region
+  unsigned long long tape_cap = 0;     // tape bound of one batch (max_resting + 2 * max_batch)
+  uint32_t slab = 0;                   // scratch fills per symbol slab (register-ladder kernel)
+  uint32_t ntiles_sort = 0;            // sort tiles of a max_batch batch (histogram row stride)
   // pinned staging for host batches
   void* h_pin = nullptr;
   size_t h_pin_bytes = 0;
@@ -107,7 +111,7 @@ static void free_all(me_engine* e) {
                   e->d_seq,       e->d_px,        e->d_qty,       e->d_sym,         e->d_kind,
                   e->d_keys[0],   e->d_keys[1],   e->d_idx[0],    e->d_idx[1],      e->d_hist,
                   e->d_res,       e->d_fstart,    e->d_tile_sum,  e->d_scratch,     e->d_scratch_top,
-                  e->d_tape,      e->d_tape_count, e->d_fills_acc, e->bk.dbg};
+                  e->d_tape,      e->d_tape_count, e->d_fills_acc, e->bk.dbg,      e->bk.fcache};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   for (void* p : e->user_allocs) (void)hipFree(p);
@@ -220,7 +224,17 @@ extern "C" me_engine* me_create(const me_config* cfg) {
     return nullptr;
   };
   if (nchunks * ME_C >= 0xFFFFFFFFull) return bail("me_create: chunk pool exceeds 32-bit slot ids");
-  if (scap >= 0xFFFFFFFFull) return bail("me_create: scratch bound exceeds 32-bit fill ids");
+  // Register-ladder kernel (L <= 128): every symbol owns a scratch slab sized for ~4x its mean
+  // share of a batch; a wave that might outgrow it reserves its batch bound in the overflow region.
+  uint64_t slab = 0;
+  if (L <= 128) {
+    slab = 4 * ((n + S - 1) / S) + 16;
+    slab = (slab + 15) & ~15ull;
+    if (slab < 64) slab = 64;
+    if (slab > 4096) slab = 4096;
+  }
+  const unsigned long long ovf_base = (S + 1) * slab;
+  if (scap + ovf_base >= 0xFFFFFFFFull) return bail("me_create: scratch bound exceeds 32-bit fill ids");
   if (n >= 0x7FFFFFFFull) return bail("me_create: max_batch too large");
   he = hipSetDevice(e->dev);
   if (he != hipSuccess) return bail(std::string("hipSetDevice: ") + hipGetErrorString(he));
@@ -267,7 +281,8 @@ extern "C" me_engine* me_create(const me_config* cfg) {
   ALLOC(e->d_res, n);
   ALLOC(e->d_fstart, n);
   ALLOC(e->d_tile_sum, ntiles_tape);
-  ALLOC(e->d_scratch, scap);
+  ALLOC(e->d_scratch, ovf_base + scap);
+  ALLOC(bk.fcache, S * 64);
   ALLOC(e->d_scratch_top, 1);
   ALLOC(e->d_tape, scap);
   ALLOC(e->d_tape_count, 1);
@@ -277,7 +292,9 @@ extern "C" me_engine* me_create(const me_config* cfg) {
   (void)hipMemset(bk.dbg, 0, S * 24 * 8);
 #endif
 #undef ALLOC
-  e->scratch_cap = scap;
+  e->scratch_cap = ovf_base + scap;
+  e->tape_cap = scap;
+  e->slab = (uint32_t)slab;
   // initial book state
   hipStream_t st = e->stream;
   std::vector<SymState> ss(S);
@@ -289,7 +306,8 @@ extern "C" me_engine* me_create(const me_config* cfg) {
     ss[i].best_ask = (int)L;
     ss[i].free_head = NIL;
     ss[i].resting = 0;
-    ss[i].pad[0] = ss[i].pad[1] = 0;
+    ss[i].nfree = 0;
+    ss[i].pad = 0;
     gs[i] = cfg->symbol_ids ? cfg->symbol_ids[i] : (uint32_t)i;
   }
   bool ok = launch_init_levels(st, bk.levels, S * L) == hipSuccess &&
@@ -299,6 +317,7 @@ extern "C" me_engine* me_create(const me_config* cfg) {
             hipMemsetAsync(bk.owner, 0xFF, nchunks * sizeof(uint32_t), st) == hipSuccess &&
             hipMemsetAsync(bk.cqty, 0, nchunks * ME_C * sizeof(int), st) == hipSuccess &&
             hipMemsetAsync(bk.loc, 0xFF, cfg->max_seq * sizeof(uint32_t), st) == hipSuccess &&
+            hipMemsetAsync(bk.fcache, 0xFF, S * 64 * sizeof(uint32_t), st) == hipSuccess &&
             hipMemsetAsync(bk.chunk_top, 0, 4, st) == hipSuccess && hipMemsetAsync(bk.err, 0, 4, st) == hipSuccess &&
             hipMemcpyAsync(bk.sym, ss.data(), S * sizeof(SymState), hipMemcpyHostToDevice, st) == hipSuccess &&
             hipMemcpyAsync(gsym, gs.data(), S * 4, hipMemcpyHostToDevice, st) == hipSuccess &&
@@ -367,11 +386,18 @@ static int enqueue_batch(me_engine* e, const uint64_t* seq, const int64_t* px, c
   bt.scratch = e->d_scratch;
   bt.scratch_cap = e->scratch_cap;
   bt.scratch_top = e->d_scratch_top;
+  bt.slab = e->slab;
+  bt.ovf_base = (unsigned long long)(S + 1) * e->slab;
+  if (e->passes == 1) {  // bins are symbols: the scanned histogram is the run table
+    bt.bin_start = e->d_hist;
+    bt.bin_stride = (n + sort_tile(n) - 1) / sort_tile(n);
+    bt.nbins = S + 1;
+  }
   if (e->timing) HIP_TRY(hipEventRecord(tl.m0, st), "hipEventRecord");
   hipError_t he = launch_match(st, e->bk, bt);
   if (he != hipSuccess) return e->hip_fail(he, "match launch");
   if (e->timing) HIP_TRY(hipEventRecord(tl.m1, st), "hipEventRecord");
-  he = launch_tape(st, bt, e->d_tape, e->scratch_cap, e->d_tape_count, e->d_fills_acc, e->bk.err);
+  he = launch_tape(st, bt, e->d_tape, e->tape_cap, e->d_tape_count, e->d_fills_acc, e->bk.err);
   if (he != hipSuccess) return e->hip_fail(he, "tape launch");
   if (e->timing) {
     HIP_TRY(hipEventRecord(tl.p1, st), "hipEventRecord");

@@ -1124,7 +1124,8 @@ __device__ __forceinline__ void wave_end(C& c) {
     o.best_ask = c.ba;
     o.free_head = c.free_head;
     o.resting = (uint32_t)c.resting_delta;
-    o.pad[0] = o.pad[1] = 0;
+    o.nfree = 0;
+    o.pad = 0;
     c.bk.sym[c.s] = o;
   }
 #ifdef ME_STAMPS

@@ -15,6 +15,8 @@
 //                   A slot is live iff qty > 0. Every linked chunk holds >= 1 live order (a chunk
 //                   emptied by cancels is unlinked at once), so chunks in use <= resting orders.
 //   loc    [max_seq] seq -> global slot (chunk * ME_C + slot) for cancels.
+//   fcache [S][64]  free chunk ids a symbol keeps between launches (the register-ladder kernel
+//                   holds them in one VGPR: pops and pushes never touch memory).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -56,7 +58,8 @@ struct alignas(32) SymState {
   int best_ask;        // lowest occupied ask level, L if none
   uint32_t free_head;  // chunk free list of this symbol
   uint32_t resting;    // live resting orders
-  uint32_t pad[2];
+  uint32_t nfree;      // free chunk ids parked in fcache[sym][0..nfree) (register-ladder kernel)
+  uint32_t pad;
 };
 
 struct BookDev {
@@ -70,6 +73,7 @@ struct BookDev {
   int* cqty;
   uint32_t* loc;
   uint32_t* chunk_top;
+  uint32_t* fcache;       // [S][64] free chunk ids parked between launches (register-ladder kernel)
   uint32_t* err;
   const uint32_t* gsym;  // [S] id written into me_fill.symbol
   unsigned long long* dbg;  // [S][8] phase cycles, diagnostic (-DME_STAMPS) builds only
@@ -95,6 +99,15 @@ struct BatchDev {
   me_fill* scratch;
   unsigned long long scratch_cap;
   unsigned long long* scratch_top;
+  // Register-ladder kernel: symbol s owns the scratch slab [s * slab, (s + 1) * slab); a wave whose
+  // fills may outgrow it reserves the rest of its batch bound at ovf_base + atomicAdd(scratch_top).
+  uint32_t slab;
+  unsigned long long ovf_base;
+  // Single-pass grouping sort: the scanned histogram gives every symbol's run directly,
+  // run(s) = [bin_start[s * bin_stride], bin_start[(s + 1) * bin_stride]) (n for the last bin).
+  const uint32_t* bin_start;
+  uint32_t bin_stride;
+  uint32_t nbins;
 };
 
 }  // namespace me

@@ -16,7 +16,14 @@
 //     saturation keeps the comparison with the remaining taker quantity exact);
 //   * reject reasons, prices -> levels and the per-record result records are computed for 64
 //     records at a time in vector form; the serial loop visits only records that touch the book
-//     and hands back two numbers per record (quantity, fill count).
+//     and hands back three numbers per record (quantity, fill count, first scratch fill).
+//
+// Memory-counter discipline (gfx950 counts loads AND stores in vmcnt, in issue order): a wait for a
+// load also waits for every store issued before it, i.e. a full HBM write round trip. So the serial
+// loop issues no global load on its common paths: the miss path of the head-chunk cache copies a
+// chunk into LDS and the walk then reads LDS only; free chunk ids live in a VGPR stack (never a
+// prefetched list pointer); every symbol owns a scratch slab (no per-wave atomic reservation);
+// global loads are never predicated (clamped indices + selects, no branch around a load).
 #include <hip/hip_runtime.h>
 
 #include "me_layout.hpp"
@@ -25,6 +32,7 @@
 namespace me {
 
 constexpr int RL = 128;  // levels covered by this kernel
+constexpr int FSTK = 64; // free chunk ids a wave keeps in its VGPR stack (= fcache row length)
 
 // One wave's LDS: the head-chunk cache (entry l = head chunk of level l) and the level totals.
 struct RegLds {
@@ -34,6 +42,7 @@ struct RegLds {
   uint32_t cnext[RL];  // chdr[head].next of the cached head (kept in step with HBM)
 };
 constexpr int REG_WAVES = 4;  // waves (symbols) per workgroup
+constexpr int VMCNT0 = 0x0F70;  // s_waitcnt immediate: vmcnt(0), expcnt / lgkmcnt untouched (gfx9 encoding)
 
 // One 32-bit field of the 128-level ladder: level l is lane (l & 63) of row (l >> 6).
 struct Row2 {
@@ -101,11 +110,16 @@ struct RegCtx {
   Row2 hd, tl, te;     // head chunk, tail chunk, slots written in the tail chunk
   Mask2 occ, cv, cd;   // occupied levels, cache entry valid (holds the head), cache entry dirty
   int bb, ba;          // best bid level (-1: none), best ask level (RL: none)
-  uint32_t free_head;  // this symbol's chunk free list ...
-  uint32_t free_next;  // ... and chdr[free_head].next (VGPR, loaded ahead of the pop)
+  uint32_t fstk;       // VGPR stack of free chunk ids: lane i holds entry i ...
+  uint32_t nfs;        // ... entries [0, nfs) are valid
+  uint32_t free_head;  // overflow free list in HBM (chdr[].next links), NIL if empty
   uint32_t bump_cur, bump_end, recs_left;
   int resting;
-  uint32_t wptr;       // next scratch fill of this wave
+  uint32_t wptr, wend; // next scratch fill of this wave and the end of its reservation
+#ifdef ME_STAMPS
+  unsigned long long st[PH_N];
+  unsigned long long st_t;
+#endif
 };
 
 __device__ __forceinline__ void reg_err(const RegCtx& c, uint32_t bits) {
@@ -121,45 +135,35 @@ __device__ __forceinline__ uint32_t scan16_sat(uint32_t x) {
   return x;
 }
 
-// Exclusive 64-lane scan of a 32-bit count.
-__device__ __forceinline__ uint32_t wave_excl_scan32(uint32_t x) {
-  uint32_t v = x;
-  v += dpp32<0x111, 0xF>(v);
-  v += dpp32<0x112, 0xF>(v);
-  v += dpp32<0x114, 0xF>(v);
-  v += dpp32<0x118, 0xF>(v);
-  v += dpp32<0x142, 0xA>(v);  // row_bcast:15
-  v += dpp32<0x143, 0xC>(v);  // row_bcast:31
-  return v - x;
-}
-
 __device__ __forceinline__ void tot_add(RegCtx& c, int lvl, long long d) {
   if (lane_id() == 0) __hip_atomic_fetch_add(&c.M->tot[lvl], d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 // ---- chunk pool ----------------------------------------------------------------------------
-__device__ __forceinline__ void reg_prefetch_free_next(RegCtx& c) {
-  const bool ok = c.free_head < c.nchunks;
-  const uint32_t v = c.chdr[ok ? c.free_head : 0].next;
-  c.free_next = ok ? v : NIL;
-}
-
-// Free-list push of a chunk whose HBM quantities are all zero.
+// Free-list push of a chunk whose HBM quantities are all zero: onto the VGPR stack, or (stack
+// full) onto the HBM overflow list — a store, never a load.
 __device__ __forceinline__ void reg_free(RegCtx& c, uint32_t ch) {
-  if (lane_id() == 0) c.chdr[ch].next = c.free_head;
-  c.free_next = c.free_head;
-  c.free_head = ch;
+  if (c.nfs < (uint32_t)FSTK) {
+    c.fstk = lane_id() == (int)c.nfs ? ch : c.fstk;
+    c.nfs += 1;
+  } else {
+    if (lane_id() == 0) c.chdr[ch].next = c.free_head;
+    c.free_head = ch;
+  }
 }
 
 __device__ __forceinline__ uint32_t reg_alloc(RegCtx& c) {
-  if (c.free_head != NIL) {
+  if (c.nfs) {
+    c.nfs -= 1;
+    return rl32(c.fstk, (int)c.nfs);
+  }
+  if (c.free_head != NIL) {  // overflow list: one dependent load (rare: the stack ran dry)
     const uint32_t ch = c.free_head;
     if (ch >= c.nchunks) {
       reg_err(c, ERR_INCONSISTENT);
       return NIL;
     }
-    c.free_head = rl32(c.free_next, 0);
-    reg_prefetch_free_next(c);
+    c.free_head = rl32(c.chdr[ch].next, 0);
     return ch;
   }
   if (c.bump_cur >= c.bump_end) {
@@ -178,6 +182,31 @@ __device__ __forceinline__ uint32_t reg_alloc(RegCtx& c) {
   return c.bump_cur++;
 }
 
+// ---- head-chunk cache ------------------------------------------------------------------------
+// Miss: copy chunk ch (the head of level lvl) into cache entry lvl. The only global load of a walk;
+// its registers die at the LDS writes, so no wait on it leaks into the hit path.
+__device__ __forceinline__ bool reg_fill_entry(RegCtx& c, int lvl, uint32_t ch) {
+  if (ch >= c.nchunks) {  // NIL or corrupt: never index with it
+    reg_err(c, ERR_INCONSISTENT);
+    return false;
+  }
+  const int lane = lane_id();
+  const int sl = lane & (ME_C - 1);
+  const size_t g = (size_t)ch * ME_C + sl;
+  const uint32_t nx = c.chdr[ch].next;
+  const int qv = c.cqty[g];
+  const unsigned long long sv = c.cseq[g];
+  // Resolve the loads on every path here (vmcnt(0)): a load left pending behind the lane-masked
+  // LDS writes below would make the compiler wait for it (and all later stores) in the hit path.
+  __builtin_amdgcn_s_waitcnt(VMCNT0);
+  if (lane < ME_C) {
+    c.M->cq[lvl][sl] = qv;
+    c.M->cs[lvl][sl] = sv;
+  }
+  if (lane == 0) c.M->cnext[lvl] = nx;
+  return true;
+}
+
 // ---- taking liquidity ----------------------------------------------------------------------
 // Consume up to `rem` from the FIFO of level lvl, oldest first, emitting one fill per maker slot
 // touched. Returns true if the level emptied. A slot is live iff its qty > 0.
@@ -191,31 +220,19 @@ __device__ __forceinline__ bool reg_walk(RegCtx& c, int lvl, uint32_t& rem, unsi
   uint32_t ch = head;
   uint32_t taken = 0;
   for (;;) {
-    int qv;
-    unsigned long long sv;
-    uint32_t nx;
-    if (c.cv.bit(lvl)) {
-      qv = act ? c.M->cq[lvl][sl] : 0;
-      sv = c.M->cs[lvl][sl];
-      nx = c.M->cnext[lvl];
-    } else {
-      if (ch >= c.nchunks) {  // NIL or corrupt: never index with it
-        reg_err(c, ERR_INCONSISTENT);
-        return false;
-      }
-      const size_t g = (size_t)ch * ME_C + sl;
-      nx = c.chdr[ch].next;
-      qv = act ? c.cqty[g] : 0;
-      sv = c.cseq[g];
-      if (act) {
-        c.M->cq[lvl][sl] = qv;
-        c.M->cs[lvl][sl] = sv;
-      }
-      if (lane == 0) c.M->cnext[lvl] = nx;
+    if (!c.cv.bit(lvl)) {
+      COUNT(c, CT_MISS);
+      STAMP_ADD(c, PH_WALK);
+      if (!reg_fill_entry(c, lvl, ch)) return false;
       c.cv.set(lvl);
       c.cd.clr(lvl);
+      STAMP_ADD(c, WK_GET);
     }
-    const uint32_t uq = (uint32_t)qv;
+    COUNT(c, CT_WALK);
+    const int q_ = c.M->cq[lvl][sl];
+    const unsigned long long sv = c.M->cs[lvl][sl];
+    const uint32_t nx = c.M->cnext[lvl];
+    const uint32_t uq = act ? (uint32_t)q_ : 0u;
     const uint32_t inc = scan16_sat(uq);
     const uint32_t ex = inc - uq;
     uint32_t f = rem > ex ? rem - ex : 0u;
@@ -342,14 +359,17 @@ __device__ __forceinline__ uint32_t reg_cancel(RegCtx& c, unsigned long long tgt
   if (tgt == 0ull || tgt >= c.max_seq) return 0;
   wave_mem_order();
   const uint32_t g = rl32(c.loc[tgt], 0);
+  __builtin_amdgcn_s_waitcnt(VMCNT0);
   if (g == NIL) return 0;
   const uint32_t ch = g / ME_C, slot = g % ME_C;
   if (ch >= c.nchunks) return 0;
   // one round trip: owner, header, the chunk's quantities and the target seq
   const uint32_t own = rl32(c.owner[ch], 0);
   const ChunkHdr hdr = c.chdr[ch];
-  int qv = act ? c.cqty[(size_t)ch * ME_C + lane] : 0;
+  const int qg = c.cqty[(size_t)ch * ME_C + (lane & (ME_C - 1))];
   unsigned long long sq = rl64(c.cseq[g], 0);
+  __builtin_amdgcn_s_waitcnt(VMCNT0);  // resolved on every path (see reg_fill_entry)
+  int qv = act ? qg : 0;
   if (own != c.s) return 0;  // another symbol's order: never touch its book
   const int lvl = (int)rl32(hdr.level, 0);
   if (lvl < 0 || lvl >= (int)c.L) {
@@ -359,7 +379,8 @@ __device__ __forceinline__ uint32_t reg_cancel(RegCtx& c, unsigned long long tgt
   const uint32_t h = c.hd.get(lvl), t = c.tl.get(lvl);
   const bool in_cache = c.cv.bit(lvl) && h == ch;  // the on-chip copy is authoritative
   if (in_cache) {
-    qv = act ? c.M->cq[lvl][lane & (ME_C - 1)] : 0;
+    const int qc = c.M->cq[lvl][lane & (ME_C - 1)];
+    qv = act ? qc : 0;
     sq = rl64(c.M->cs[lvl][slot], 0);
   }
   const int q = rli32(qv, (int)slot);
@@ -414,6 +435,25 @@ __device__ __forceinline__ uint32_t reg_cancel(RegCtx& c, unsigned long long tgt
   return (uint32_t)q;
 }
 
+// ---- scratch ---------------------------------------------------------------------------------
+// The taker about to run may emit up to `resting` fills. If they might not fit the wave's slab,
+// reserve the batch bound of everything left (resting + 2 * records left) in the
+// shared overflow region once; after that no further check can fail.
+__device__ __forceinline__ bool reg_reserve_overflow(RegCtx& c, unsigned long long* top, unsigned long long base,
+                                                  unsigned long long cap) {
+  const unsigned long long need = (unsigned long long)(uint32_t)c.resting + 2ull * c.recs_left;
+  unsigned long long w0 = 0;
+  if (lane_id() == 0) w0 = atomicAdd(top, need);
+  w0 = base + rl64(w0, 0);
+  if (w0 + need > cap) {
+    reg_err(c, ERR_SCRATCH_OOM);
+    return false;
+  }
+  c.wptr = (uint32_t)w0;
+  c.wend = 0xFFFFFFFFu;  // never re-checked
+  return true;
+}
+
 // ---- the kernel ----------------------------------------------------------------------------
 // Per-record control word built in vector form: lim level | BUY | MARKET | CANCEL.
 constexpr uint32_t CW_BUY = 1u << 8, CW_MKT = 1u << 9, CW_CXL = 1u << 10;
@@ -424,8 +464,17 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
   const uint32_t wv = threadIdx.x >> 6;
   const uint32_t s = blockIdx.x * REG_WAVES + wv;
   if (s > bk.S) return;
-  const uint32_t lo = wave_lower_bound(bt.skeys, bt.n, s);
-  const uint32_t hi = wave_lower_bound(bt.skeys, bt.n, s + 1);
+#ifdef ME_STAMPS
+  unsigned long long st_t0 = stamp_now();
+#endif
+  uint32_t lo, hi;
+  if (bt.bin_start) {  // single-pass sort: the scanned histogram is the run table
+    lo = bt.bin_start[(size_t)s * bt.bin_stride];
+    hi = s + 1 < bt.nbins ? bt.bin_start[(size_t)(s + 1) * bt.bin_stride] : bt.n;
+  } else {
+    lo = wave_lower_bound(bt.skeys, bt.n, s);
+    hi = wave_lower_bound(bt.skeys, bt.n, s + 1);
+  }
   if (lo >= hi) return;
   if (s == bk.S) {
     reject_bad_symbols(bt, lo, hi);
@@ -434,6 +483,17 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
   const uint32_t L = bk.L;
   Level* g_lv = bk.levels + (size_t)s * L;
   uint8_t* g_tend = bk.tend + (size_t)s * L;
+  // one round trip: ladder rows, tail fills, symbol scalars, parked free chunks (no predicated
+  // loads: row 1 of a 64-level ladder re-reads row 0 and is then discarded)
+  const bool in1 = 64u + (uint32_t)lane < L;
+  const uint32_t l1 = in1 ? 64u + (uint32_t)lane : (uint32_t)lane;
+  const Level a = g_lv[lane];
+  const Level b = g_lv[l1];
+  const uint32_t te0 = g_tend[lane];
+  const uint32_t te1 = g_tend[l1];
+  const SymState st = bk.sym[s];
+  const uint32_t fst = bk.fcache[(size_t)s * FSTK + lane];
+  const uint32_t gsv = bk.gsym[s];
   RegCtx c;
   c.chdr = bk.chdr;
   c.owner = bk.owner;
@@ -448,56 +508,50 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
   c.nchunks = bk.nchunks;
   c.L = L;
   c.s = s;
-  c.gs = bk.gsym ? bk.gsym[s] : s;
-  // ladder rows; totals to LDS; occupancy = levels with a FIFO
-  const bool in1 = 64u + (uint32_t)lane < L;
-  Level a = g_lv[lane];
-  Level b;
-  b.total = 0;
-  b.head = b.tail = NIL;
-  if (in1) b = g_lv[64 + lane];
+  c.gs = rl32(gsv, 0);
+#ifdef ME_STAMPS
+  for (int p = 0; p < PH_N; ++p) c.st[p] = 0;
+  c.st_t = st_t0;
+  STAMP_ADD(c, PH_SW_WINDOW);  // run bounds
+#endif
   c.hd.r0 = a.head;
-  c.hd.r1 = b.head;
+  c.hd.r1 = in1 ? b.head : NIL;
   c.tl.r0 = a.tail;
-  c.tl.r1 = b.tail;
-  c.te.r0 = g_tend[lane];
-  c.te.r1 = in1 ? (uint32_t)g_tend[64 + lane] : 0u;
+  c.tl.r1 = in1 ? b.tail : NIL;
+  c.te.r0 = te0;
+  c.te.r1 = in1 ? te1 : 0u;
+  const long long tb = in1 ? b.total : 0ll;
   c.M->tot[lane] = a.total;
-  c.M->tot[64 + lane] = b.total;
+  c.M->tot[64 + lane] = tb;
   c.occ.w0 = __ballot(a.total > 0);
-  c.occ.w1 = __ballot(b.total > 0);
+  c.occ.w1 = __ballot(tb > 0);
   c.cv.w0 = c.cv.w1 = c.cd.w0 = c.cd.w1 = 0ull;
-  const SymState st = bk.sym[s];
   c.base = rli64(st.base, 0);
   c.bb = rli32(st.best_bid, 0);
   c.ba = rli32(st.best_ask, 0);
   if (c.ba > RL) c.ba = RL;
   c.free_head = rl32(st.free_head, 0);
-  reg_prefetch_free_next(c);
+  c.nfs = min(rl32(st.nfree, 0), (uint32_t)FSTK);
+  c.fstk = fst;
   c.bump_cur = c.bump_end = 0;
   c.resting = (int)rl32(st.resting, 0);
-  {
-    // scratch run of this wave: fills <= resting makers + 2 * records
-    const unsigned long long need = (unsigned long long)(uint32_t)c.resting + 2ull * (hi - lo);
-    unsigned long long w0 = 0;
-    if (lane == 0) w0 = atomicAdd(bt.scratch_top, need);
-    w0 = rl64(w0, 0);
-    if (w0 + need > bt.scratch_cap) {
-      reg_err(c, ERR_SCRATCH_OOM);
-      return;
-    }
-    c.wptr = (uint32_t)w0;
-  }
+  c.wptr = s * bt.slab;
+  c.wend = c.wptr + bt.slab;
+  STAMP_ADD(c, PH_PROLOGUE);
   const long long Lw = (long long)L;
   for (uint32_t blk = lo; blk < hi; blk += 64) {
-    // ---- 64 records in vector form
+    // ---- 64 records in vector form (two dependent round trips: permutation, then the records)
     const uint32_t j = blk + (uint32_t)lane;
     const bool v = j < hi;
-    const uint32_t oi = v ? bt.perm[j] : 0u;
-    const unsigned long long oseq = v ? bt.seq[oi] : 0ull;
-    const long long opx = v ? bt.px[oi] : 0ll;
-    const int oq = v ? bt.qty[oi] : 0;
-    const uint32_t kd = v ? (uint32_t)bt.kind[oi] : 0u;
+    const uint32_t oi = bt.perm[v ? j : hi - 1u];
+    const unsigned long long oseq_ = bt.seq[oi];
+    const long long opx_ = bt.px[oi];
+    const int oq_ = bt.qty[oi];
+    const uint32_t kd_ = bt.kind[oi];
+    const unsigned long long oseq = v ? oseq_ : 0ull;
+    const long long opx = v ? opx_ : 0ll;
+    const int oq = v ? oq_ : 0;
+    const uint32_t kd = v ? kd_ : 0u;
     const uint32_t side = kd & 3u;
     const bool market = (kd >> 2) & 1u, cancel = (kd >> 3) & 1u;
     const bool buy = side == ME_SIDE_BUY;
@@ -518,22 +572,33 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
     unsigned long long work = __ballot(v && rj == ME_RJ_NONE);
     const uint32_t cnt = min(64u, hi - blk);
     uint32_t stop = cnt;  // records [0, stop) of the block get results
-    uint32_t out_q = 0, out_n = 0;
-    const uint32_t w_blk = c.wptr;
+    uint32_t out_q = 0, out_n = 0, out_w = 0;
+#ifdef ME_STAMPS
+    __builtin_amdgcn_s_waitcnt(0);
+#endif
+    STAMP_ADD(c, PH_FETCH);
     // ---- the serial chain: records that touch the book, in seq order
     while (work) {
       const int k = __builtin_ctzll(work);
       work &= work - 1ull;
       const uint32_t ctl = rl32(cw, k);
-      const uint32_t w_in = c.wptr;
       c.recs_left = hi - (blk + (uint32_t)k);
       uint32_t outq;
+      COUNT(c, CT_FAST);
+      STAMP_ADD(c, PH_SWEEP);
       if (ctl & CW_CXL) {
         outq = reg_cancel(c, (unsigned long long)rli64(opx, k));
+        STAMP_ADD(c, PH_CANCEL);
       } else {
+        if (c.wptr + (uint32_t)c.resting > c.wend &&
+            !reg_reserve_overflow(c, bt.scratch_top, bt.ovf_base, bt.scratch_cap)) {
+          stop = (uint32_t)k;
+          break;
+        }
         const unsigned long long seq = rl64(oseq, k);
         const uint32_t q = (uint32_t)rli32(oq, k);
         const int lm = (int)(ctl & 0xFFu);
+        const uint32_t w_in = c.wptr;
         uint32_t rem = q;
         if (ctl & CW_BUY) {
           while (rem != 0u && c.ba <= lm) {
@@ -549,17 +614,19 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
           }
         }
         outq = q - rem;
+        STAMP_ADD(c, PH_WALK);
+        const bool me_ = lane == k;
+        out_n = me_ ? c.wptr - w_in : out_n;
+        out_w = me_ ? w_in : out_w;
         if (!(ctl & CW_MKT) && rem != 0u && !reg_rest(c, lm, seq, rem, (ctl & CW_BUY) != 0u)) {
           stop = (uint32_t)k;  // chunk pool exhausted: the batch fails (sticky error word)
           break;
         }
+        STAMP_ADD(c, PH_REST);
       }
-      const bool me_ = lane == k;
-      out_q = me_ ? outq : out_q;
-      out_n = me_ ? c.wptr - w_in : out_n;
+      out_q = lane == k ? outq : out_q;
     }
     // ---- results of the block in vector form
-    const uint32_t ex = wave_excl_scan32(out_n);  // fills of the block's earlier records
     if (v && (uint32_t)lane < stop) {
       me_order_result r;
       r.tape_offset = 0;
@@ -585,9 +652,10 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
                             : ME_ST_NEW;
       }
       bt.res[oi] = r;
-      bt.fstart[oi] = w_blk + ex;
+      bt.fstart[oi] = out_w;
       if (out_n) atomicAdd(&bt.tile_sum[oi / TILE_TAPE], out_n);
     }
+    STAMP_ADD(c, PH_RESULT);
     if (stop < cnt) break;
   }
   // ---- write the symbol back
@@ -605,7 +673,6 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
       }
     }
   }
-  wave_mem_order();
   Level o;
   o.total = c.M->tot[lane];
   o.head = c.hd.r0;
@@ -619,6 +686,7 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
     g_lv[64 + lane] = o;
     g_tend[64 + lane] = (uint8_t)c.te.r1;
   }
+  bk.fcache[(size_t)s * FSTK + lane] = c.fstk;
   unsigned long long* g_occ = bk.occ + (size_t)s * bk.Lwords;  // for the host-side book dump
   if (lane == 0) {
     g_occ[0] = c.occ.w0;
@@ -629,13 +697,20 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
     so.best_ask = c.ba >= (int)L ? (int)L : c.ba;
     so.free_head = c.free_head;
     so.resting = (uint32_t)c.resting;
-    so.pad[0] = so.pad[1] = 0;
+    so.nfree = c.nfs;
+    so.pad = 0;
     bk.sym[s] = so;
   }
+#ifdef ME_STAMPS
+  __builtin_amdgcn_s_waitcnt(0);
+  STAMP_ADD(c, PH_EPILOGUE);
+  if (lane == 0 && bk.dbg)
+    for (int p = 0; p < PH_N; ++p) bk.dbg[(size_t)s * 24 + p] = c.st[p];
+#endif
 }
 
 hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev& bt) {
-  if (bk.L > (uint32_t)RL || bk.L < 64u) return hipErrorInvalidValue;
+  if (bk.L > (uint32_t)RL || bk.L < 64u || !bk.fcache || !bk.gsym) return hipErrorInvalidValue;
   const uint32_t waves = bk.S + 1;
   hipLaunchKernelGGL(k_match_reg, dim3((waves + REG_WAVES - 1) / REG_WAVES), dim3(64 * REG_WAVES), 0, st, bk, bt);
   return hipGetLastError();

@@ -22,6 +22,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--batches", type=int, default=30)
+    ap.add_argument("--skip", type=int, default=5, help="warm batches not measured")
     ap.add_argument("--symbols", type=int, default=0)
     a = ap.parse_args()
     assert "stamps" in me._abi.LIB_PATH, "set ME_ENGINE_LIB to the stamps build"
@@ -31,7 +32,7 @@ def main():
     base = st.base_prices()
     lib = me._abi.load()
     lib.me_debug_stamps.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t]
-    eng = me.Engine(sc.num_symbols, sc.levels, base, max_batch=sc.batch, max_resting=1 << 22, max_seq=1 << 30)
+    eng = me.Engine(sc.num_symbols, sc.levels, base, max_batch=sc.batch, max_resting=1 << 23, max_seq=1 << 30)
     buf = np.zeros(sc.num_symbols * 24, dtype=np.uint64)
     tot = np.zeros(24, dtype=np.float64)
     maxwave = []
@@ -39,7 +40,7 @@ def main():
     for k in range(a.batches):
         b = st.next(sc.batch)
         eng.submit_batch(b, want_fills=False)
-        if k < 5:
+        if k < a.skip:
             continue  # warm
         lib.me_debug_stamps(eng.h, buf.ctypes.data, buf.size)
         m = buf.reshape(-1, 24).astype(np.float64)
