@@ -183,9 +183,13 @@ int me_book_dump(me_engine* e, uint32_t symbol, me_book_entry* out, size_t cap, 
 /* Resting orders over all symbols (device counter). */
 int me_resting_count(me_engine* e, uint64_t* n);
 
-/* Kernel timing: when enabled, HIP events bracket every match-kernel launch on the engine stream. */
-int me_timing_enable(me_engine* e, int enable);
-/* Sum (ms) and count of match-kernel durations since enable, plus the whole-pipeline sum. */
+/* Kernel timing. period >= 1: every period-th match-kernel launch records its own start and end
+ * (hipExtLaunchKernelGGL events: no marker packets, though each timed launch still costs the
+ * stream a few microseconds, hence the sampling); period <= 0: off. Resets the counters below. */
+int me_timing_enable(me_engine* e, int period);
+/* match_ms / launches: sum and count of the timed match-kernel durations; orders: records of the
+ * timed launches; fills: fills of ALL batches since enable; pipeline_ms: device time per batch,
+ * start-to-start from the first to the last timed launch (0 with fewer than two). */
 int me_timing_read(me_engine* e, double* match_ms, double* pipeline_ms, uint64_t* launches,
                    uint64_t* fills, uint64_t* orders);
 

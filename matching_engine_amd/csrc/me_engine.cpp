@@ -19,10 +19,10 @@ static_assert(sizeof(me_order_result) == 20, "me_order_result must be 20 B");
 
 namespace me {
 hipError_t launch_sort_pass(hipStream_t st, const uint32_t* keys_in, const uint32_t* idx_in, uint32_t n,
-                            uint32_t clamp_key, int shift, int dbits, uint32_t* hist, uint32_t* keys_out,
-                            uint32_t* idx_out, uint32_t* zero_buf, uint32_t zero_words,
-                            unsigned long long* scratch_top);
-hipError_t launch_match(hipStream_t st, const BookDev& bk, const BatchDev& bt);
+                            uint32_t clamp_key, int shift, int dbits, uint32_t* hist, uint32_t* tot,
+                            uint32_t* keys_out, uint32_t* idx_out, uint32_t* zero_buf,
+                            uint32_t zero_words, unsigned long long* scratch_top, uint32_t* bin_start);
+hipError_t launch_match(hipStream_t st, const BookDev& bk, const BatchDev& bt, hipEvent_t ev0, hipEvent_t ev1);
 uint32_t sort_tile(uint32_t n);
 hipError_t launch_tape(hipStream_t st, const BatchDev& bt, me_fill* tape, unsigned long long tape_cap,
                        unsigned long long* tape_count, unsigned long long* fills_acc, uint32_t* err);
@@ -36,8 +36,9 @@ std::mutex g_err_mu;
 std::string g_create_err;
 
 struct TimedLaunch {
-  hipEvent_t p0, m0, m1, p1;
+  hipEvent_t m0, m1;  // start / end of one match-kernel launch (recorded by the launch itself)
   uint64_t orders;
+  uint64_t idx;       // launch number since timing was enabled
 };
 }  // namespace
 
@@ -57,14 +58,20 @@ struct me_engine {
   int32_t* d_qty = nullptr;
   uint32_t* d_sym = nullptr;
   uint8_t* d_kind = nullptr;
-  uint32_t* d_keys[2] = {nullptr, nullptr};
-  uint32_t* d_idx[2] = {nullptr, nullptr};
-  uint32_t* d_hist = nullptr;
+  // Everything the grouping sort of a batch writes: sorted keys, permutation, histogram, run
+  // table, and the per-batch counters it zeroes.
+  struct SortBufs {
+    uint32_t* keys[2] = {nullptr, nullptr};
+    uint32_t* idx[2] = {nullptr, nullptr};
+    uint32_t* hist = nullptr;
+    uint32_t* tot = nullptr;        // [2 passes][2048] bin totals
+    uint32_t* bin_start = nullptr;  // [2049] run table of the single-pass sort
+    uint32_t* tile_sum = nullptr;
+    unsigned long long* scratch_top = nullptr;
+  } sb;
   me_order_result* d_res = nullptr;
   uint32_t* d_fstart = nullptr;
-  uint32_t* d_tile_sum = nullptr;
   me_fill* d_scratch = nullptr;
-  unsigned long long* d_scratch_top = nullptr;
   me_fill* d_tape = nullptr;
   unsigned long long* d_tape_count = nullptr;
   unsigned long long* d_fills_acc = nullptr;  // fills since timing was (re)enabled
@@ -79,8 +86,11 @@ struct me_engine {
   bool failed = false;
   std::string err;
   // timing
-  bool timing = false;
-  std::vector<TimedLaunch> timed;
+  int timing = 0;           // 0: off; k >= 1: time every k-th match launch
+  uint64_t nlaunch = 0;     // match launches since timing was enabled
+  std::vector<TimedLaunch> timed;  // launches since timing was enabled
+  std::vector<hipEvent_t> ev_pool;  // events reused across enable cycles (no create per launch)
+  size_t ev_used = 0;
   std::vector<void*> user_allocs;
 
   int fail(int code, const std::string& msg) {
@@ -109,20 +119,22 @@ static void free_all(me_engine* e) {
   void* ptrs[] = {e->bk.levels,   e->bk.occ,      e->bk.sym,      e->bk.chdr,       e->bk.cseq, e->bk.owner, e->bk.tend,
                   e->bk.cqty,     e->bk.loc,      e->bk.chunk_top, e->bk.err,       (void*)e->bk.gsym,
                   e->d_seq,       e->d_px,        e->d_qty,       e->d_sym,         e->d_kind,
-                  e->d_keys[0],   e->d_keys[1],   e->d_idx[0],    e->d_idx[1],      e->d_hist,
-                  e->d_res,       e->d_fstart,    e->d_tile_sum,  e->d_scratch,     e->d_scratch_top,
+                  e->d_res,       e->d_fstart,    e->d_scratch,
                   e->d_tape,      e->d_tape_count, e->d_fills_acc, e->bk.dbg,      e->bk.fcache};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
+  {
+    auto& sl = e->sb;
+    void* sp[] = {sl.keys[0], sl.keys[1], sl.idx[0], sl.idx[1], sl.hist, sl.tile_sum, sl.scratch_top,
+                  sl.tot, sl.bin_start};
+    for (void* p : sp)
+      if (p) (void)hipFree(p);
+  }
   for (void* p : e->user_allocs) (void)hipFree(p);
   e->user_allocs.clear();
   if (e->h_pin) (void)hipHostFree(e->h_pin);
-  for (auto& t : e->timed) {
-    (void)hipEventDestroy(t.p0);
-    (void)hipEventDestroy(t.m0);
-    (void)hipEventDestroy(t.m1);
-    (void)hipEventDestroy(t.p1);
-  }
+  for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
+  e->ev_pool.clear();
   e->timed.clear();
   if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
 }
@@ -273,17 +285,22 @@ extern "C" me_engine* me_create(const me_config* cfg) {
   ALLOC(e->d_qty, n);
   ALLOC(e->d_sym, n);
   ALLOC(e->d_kind, n);
-  for (int k = 0; k < 2; ++k) {
-    ALLOC(e->d_keys[k], n);
-    ALLOC(e->d_idx[k], n);
+  {
+    auto& sl = e->sb;
+    for (int k = 0; k < 2; ++k) {
+      ALLOC(sl.keys[k], n);
+      ALLOC(sl.idx[k], n);
+    }
+    ALLOC(sl.hist, (size_t)(1u << MAX_DIGIT_BITS) * ntiles_sort);
+    ALLOC(sl.tot, 2u << MAX_DIGIT_BITS);
+    ALLOC(sl.bin_start, (1u << MAX_DIGIT_BITS) + 1);
+    ALLOC(sl.tile_sum, ntiles_tape);
+    ALLOC(sl.scratch_top, 1);
   }
-  ALLOC(e->d_hist, (size_t)(1u << MAX_DIGIT_BITS) * ntiles_sort);
   ALLOC(e->d_res, n);
   ALLOC(e->d_fstart, n);
-  ALLOC(e->d_tile_sum, ntiles_tape);
   ALLOC(e->d_scratch, ovf_base + scap);
   ALLOC(bk.fcache, S * 64);
-  ALLOC(e->d_scratch_top, 1);
   ALLOC(e->d_tape, scap);
   ALLOC(e->d_tape_count, 1);
   ALLOC(e->d_fills_acc, 1);
@@ -347,14 +364,19 @@ extern "C" uint64_t me_fill_bound(const me_engine* e, size_t n) {
 static int enqueue_batch(me_engine* e, const uint64_t* seq, const int64_t* px, const int32_t* qty,
                          const uint32_t* sym, const uint8_t* kind, uint32_t n) {
   hipStream_t st = e->stream;
+  auto& sl = e->sb;
   TimedLaunch tl{};
-  if (e->timing) {
-    HIP_TRY(hipEventCreate(&tl.p0), "hipEventCreate");
-    HIP_TRY(hipEventCreate(&tl.m0), "hipEventCreate");
-    HIP_TRY(hipEventCreate(&tl.m1), "hipEventCreate");
-    HIP_TRY(hipEventCreate(&tl.p1), "hipEventCreate");
+  const bool timed = e->timing > 0 && e->nlaunch % (uint64_t)e->timing == 0;
+  tl.idx = e->nlaunch++;
+  if (timed) {
+    while (e->ev_pool.size() < e->ev_used + 2) {
+      hipEvent_t ev;
+      HIP_TRY(hipEventCreate(&ev), "hipEventCreate");
+      e->ev_pool.push_back(ev);
+    }
+    tl.m0 = e->ev_pool[e->ev_used++];
+    tl.m1 = e->ev_pool[e->ev_used++];
     tl.orders = n;
-    HIP_TRY(hipEventRecord(tl.p0, st), "hipEventRecord");
   }
   const uint32_t S = e->bk.S;
   const uint32_t ntiles_tape = (n + TILE_TAPE - 1) / TILE_TAPE;
@@ -362,13 +384,15 @@ static int enqueue_batch(me_engine* e, const uint64_t* seq, const int64_t* px, c
   const uint32_t* kin = sym;
   const uint32_t* iin = nullptr;
   int shift = 0;
+  uint32_t* run_table = e->passes == 1 ? sl.bin_start : nullptr;
   for (int p = 0; p < e->passes; ++p) {
-    hipError_t he = launch_sort_pass(st, kin, iin, n, S, shift, e->dbits[p], e->d_hist, e->d_keys[p], e->d_idx[p],
-                                     p == 0 ? e->d_tile_sum : nullptr, p == 0 ? ntiles_tape : 0,
-                                     e->d_scratch_top);
+    hipError_t he = launch_sort_pass(st, kin, iin, n, S, shift, e->dbits[p], sl.hist,
+                                     sl.tot + ((size_t)p << MAX_DIGIT_BITS), sl.keys[p], sl.idx[p],
+                                     p == 0 ? sl.tile_sum : nullptr, p == 0 ? ntiles_tape : 0, sl.scratch_top,
+                                     p == e->passes - 1 ? run_table : nullptr);
     if (he != hipSuccess) return e->hip_fail(he, "grouping sort launch");
-    kin = e->d_keys[p];
-    iin = e->d_idx[p];
+    kin = sl.keys[p];
+    iin = sl.idx[p];
     shift += e->dbits[p];
   }
   BatchDev bt{};
@@ -382,27 +406,19 @@ static int enqueue_batch(me_engine* e, const uint64_t* seq, const int64_t* px, c
   bt.perm = iin;
   bt.res = e->d_res;
   bt.fstart = e->d_fstart;
-  bt.tile_sum = e->d_tile_sum;
+  bt.tile_sum = sl.tile_sum;
   bt.scratch = e->d_scratch;
   bt.scratch_cap = e->scratch_cap;
-  bt.scratch_top = e->d_scratch_top;
+  bt.scratch_top = sl.scratch_top;
   bt.slab = e->slab;
   bt.ovf_base = (unsigned long long)(S + 1) * e->slab;
-  if (e->passes == 1) {  // bins are symbols: the scanned histogram is the run table
-    bt.bin_start = e->d_hist;
-    bt.bin_stride = (n + sort_tile(n) - 1) / sort_tile(n);
-    bt.nbins = S + 1;
-  }
-  if (e->timing) HIP_TRY(hipEventRecord(tl.m0, st), "hipEventRecord");
-  hipError_t he = launch_match(st, e->bk, bt);
+  bt.bin_start = run_table;  // bins are symbols: the run table
+  // timing: the launch itself records start/end (hipExtLaunchKernelGGL), no marker packets
+  hipError_t he = launch_match(st, e->bk, bt, tl.m0, tl.m1);
   if (he != hipSuccess) return e->hip_fail(he, "match launch");
-  if (e->timing) HIP_TRY(hipEventRecord(tl.m1, st), "hipEventRecord");
   he = launch_tape(st, bt, e->d_tape, e->tape_cap, e->d_tape_count, e->d_fills_acc, e->bk.err);
   if (he != hipSuccess) return e->hip_fail(he, "tape launch");
-  if (e->timing) {
-    HIP_TRY(hipEventRecord(tl.p1, st), "hipEventRecord");
-    e->timed.push_back(tl);
-  }
+  if (timed) e->timed.push_back(tl);
   e->last_n = n;
   return ME_OK;
 }
@@ -655,16 +671,12 @@ extern "C" int me_resting_count(me_engine* e, uint64_t* n) {
 extern "C" int me_timing_enable(me_engine* e, int enable) {
   if (!e) return ME_E_INVALID;
   HIP_TRY(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
-  for (auto& t : e->timed) {
-    (void)hipEventDestroy(t.p0);
-    (void)hipEventDestroy(t.m0);
-    (void)hipEventDestroy(t.m1);
-    (void)hipEventDestroy(t.p1);
-  }
   e->timed.clear();
+  e->ev_used = 0;
+  e->nlaunch = 0;
   HIP_TRY(hipMemsetAsync(e->d_fills_acc, 0, 8, e->stream), "reset fill counter");
   HIP_TRY(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
-  e->timing = enable != 0;
+  e->timing = enable > 0 ? enable : 0;
   return ME_OK;
 }
 
@@ -675,12 +687,15 @@ extern "C" int me_timing_read(me_engine* e, double* match_ms, double* pipeline_m
   double m = 0, p = 0;
   uint64_t o = 0;
   for (auto& t : e->timed) {
-    float a = 0, b = 0;
+    float a = 0;
     HIP_TRY(hipEventElapsedTime(&a, t.m0, t.m1), "hipEventElapsedTime");
-    HIP_TRY(hipEventElapsedTime(&b, t.p0, t.p1), "hipEventElapsedTime");
     m += a;
-    p += b;
     o += t.orders;
+  }
+  if (e->timed.size() >= 2) {  // device time per batch: start-to-start of the first and last timed launches
+    float b = 0;
+    HIP_TRY(hipEventElapsedTime(&b, e->timed.front().m0, e->timed.back().m0), "hipEventElapsedTime");
+    p = b / (double)(e->timed.back().idx - e->timed.front().idx);
   }
   if (match_ms) *match_ms = m;
   if (pipeline_ms) *pipeline_ms = p;

@@ -1,7 +1,7 @@
 // me_kernels.hip — gfx950 kernels of the batched matching core.
 //
 // One batch (n records, ascending seq) goes through:
-//   1. k_sort_hist / k_sort_offsets / k_sort_scatter
+//   1. k_sort_hist / k_sort_colscan / k_sort_scatter
 //                                    stable LSD counting sort of the records by symbol
 //                                    (1 pass for <= 2047 symbols, 2 passes up to 4M): groups
 //                                    every symbol's records contiguously, seq order kept.
@@ -14,6 +14,7 @@
 //
 // Matching semantics are pinned by oracle/oracle_book.cpp; there is no
 // reference matcher (include/engine/model.hpp is empty in julien-mrty/Matching_Engine).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include "me_layout.hpp"
@@ -25,8 +26,13 @@ namespace me {
 // ------------------------------------------------------------------ grouping sort
 // One pass of a stable LSD counting sort of the batch by symbol id. digit(key) =
 // (min(key, clamp) >> shift) & mask over nbins <= 2048 bins (the last pass uses only the bins that
-// occur). Three launches: per-tile histograms -> one-workgroup exclusive scan of the histogram
-// matrix in bin-major order (= global start of every (bin, tile) run) -> stable scatter.
+// occur). Three launches, none of them a single-workgroup stage:
+//   k_sort_hist     per-tile histograms (tile-major rows [tile][bin]);
+//   k_sort_colscan  one lane per bin: exclusive scan down its column (all tile loads in flight at
+//                   once) -> start of every (tile, bin) run within the bin, plus the bin total;
+//   k_sort_scatter  every tile adds the exclusive scan of the bin totals (LDS) and scatters its
+//                   records stably (ballot multisplit). The final pass also publishes the run
+//                   table bin_start[0..nbins] (single pass: bins are symbols).
 struct SortPass {
   uint32_t shift, mask, nbins, tile, ntiles, clamp;
 };
@@ -36,7 +42,7 @@ __device__ __forceinline__ uint32_t sort_digit(uint32_t k, const SortPass& p) {
   return (k >> p.shift) & p.mask;
 }
 
-// Per-tile histograms, bin-major [bin][tile].
+// Per-tile histograms, tile-major [tile][bin].
 __global__ __launch_bounds__(256) void k_sort_hist(const uint32_t* __restrict__ keys_in, uint32_t n, SortPass p,
                                                    uint32_t* __restrict__ hist, uint32_t* zero_buf,
                                                    uint32_t zero_words, unsigned long long* scratch_top) {
@@ -47,13 +53,34 @@ __global__ __launch_bounds__(256) void k_sort_hist(const uint32_t* __restrict__ 
   const uint32_t t1 = min(n, t0 + p.tile);
   for (uint32_t i = t0 + threadIdx.x; i < t1; i += blockDim.x) atomicAdd(&h[sort_digit(keys_in[i], p)], 1u);
   __syncthreads();
-  for (uint32_t b = threadIdx.x; b < p.nbins; b += blockDim.x) hist[(size_t)b * p.ntiles + blockIdx.x] = h[b];
+  for (uint32_t b = threadIdx.x; b < p.nbins; b += blockDim.x) hist[(size_t)blockIdx.x * p.nbins + b] = h[b];
   // Per-batch resets folded into the first kernel of the batch.
   if (zero_buf) {
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < zero_words; i += gridDim.x * blockDim.x)
       zero_buf[i] = 0;
     if (blockIdx.x == 0 && threadIdx.x == 0) *scratch_top = 0ull;
   }
+}
+
+// In place: hist[t][b] <- sum of hist[t'][b] over t' < t; tot[b] <- column total. One lane per bin;
+// the column's loads are all issued before the first add (ntiles <= MAX_SORT_TILES).
+__global__ __launch_bounds__(64) void k_sort_colscan(uint32_t* __restrict__ hist, uint32_t* __restrict__ tot,
+                                                     uint32_t nbins, uint32_t ntiles) {
+  const uint32_t b = blockIdx.x * 64 + threadIdx.x;
+  if (b >= nbins) return;
+  uint32_t run = 0;
+  for (uint32_t t0 = 0; t0 < ntiles; t0 += 32) {
+    uint32_t v[32];
+#pragma unroll
+    for (int u = 0; u < 32; ++u) v[u] = hist[(size_t)min(t0 + u, ntiles - 1) * nbins + b];
+#pragma unroll
+    for (int u = 0; u < 32; ++u)
+      if (t0 + u < ntiles) {
+        hist[(size_t)(t0 + u) * nbins + b] = run;
+        run += v[u];
+      }
+  }
+  tot[b] = run;
 }
 
 // Block-wide exclusive scan of LDS array a[0..cnt) (cnt <= 2048) with 256 threads; returns total.
@@ -86,67 +113,40 @@ __device__ uint32_t block_excl_scan_lds(uint32_t* a, uint32_t cnt, uint32_t* wsu
   return total;
 }
 
-// In-place exclusive scan of the histogram matrix (count = nbins * ntiles), one workgroup of
-// 1024 threads: each thread owns a contiguous run, runs are combined by a wave + LDS scan.
-__global__ __launch_bounds__(1024) void k_sort_offsets(uint32_t* __restrict__ hist, uint32_t count) {
-  // 16 waves; wave w owns the contiguous segment [w*seg, (w+1)*seg), read 64 consecutive words per
-  // wave-load (coalesced: one CU's address path handles whole lines, not 64 scattered ones).
-  __shared__ uint32_t wsum[16];
-  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const uint32_t seg = ((count + 16 * 64 - 1) / (16 * 64)) * 64;
-  const uint32_t s0 = min(count, w * seg), s1 = min(count, s0 + seg);
-  uint32_t local = 0;
-  for (uint32_t j = s0; j < s1; j += 8 * 64) {
-    uint32_t v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const uint32_t i = j + u * 64 + lane;
-      v[u] = hist[min(i, count - 1)];  // clamp the index, never branch around a load
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) local += (j + u * 64 + lane < s1) ? v[u] : 0u;
-  }
-  for (int d = 32; d >= 1; d >>= 1) local += __shfl_xor(local, d, 64);
-  if (lane == 0) wsum[w] = local;
-  __syncthreads();
-  uint32_t carry = 0;
-  for (uint32_t k = 0; k < w; ++k) carry += wsum[k];
-  for (uint32_t j = s0; j < s1; j += 8 * 64) {
-    uint32_t v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = hist[min(j + u * 64 + lane, count - 1)];  // 8 loads in flight
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const uint32_t i = j + u * 64 + lane;
-      const uint32_t x = i < s1 ? v[u] : 0u;
-      const uint32_t inc = (uint32_t)wave_incl_scan((long long)x);
-      if (i < s1) hist[i] = carry + inc - x;
-      carry += rl32(inc, 63);
-    }
-  }
-}
-
-// Stable scatter of one tile: dest = start of this tile's run of its digit (k_sort_offsets) +
-// rank among equal digits earlier in the tile. Each wave owns a quarter of the tile and ranks
-// 64 records at a time with a ballot multisplit (one ballot per digit bit).
+// Stable scatter of one tile: dest = start of this tile's run of its digit + rank among equal
+// digits earlier in the tile. Each wave owns a quarter of the tile and ranks 64 records at a time
+// with a ballot multisplit (one ballot per digit bit).
 __global__ __launch_bounds__(256) void k_sort_scatter(const uint32_t* __restrict__ keys_in,
                                                       const uint32_t* __restrict__ idx_in, uint32_t n, SortPass p,
-                                                      uint32_t dbits, const uint32_t* __restrict__ offsets,
+                                                      uint32_t dbits, const uint32_t* __restrict__ colpre,
+                                                      const uint32_t* __restrict__ tot,
                                                       uint32_t* __restrict__ keys_out,
-                                                      uint32_t* __restrict__ idx_out) {
+                                                      uint32_t* __restrict__ idx_out, uint32_t* bin_start) {
+  __shared__ uint32_t base[1u << MAX_DIGIT_BITS];
   __shared__ uint32_t wcnt[4][1u << MAX_DIGIT_BITS];
+  __shared__ uint32_t wsum[4];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const uint32_t tile = blockIdx.x;
-  for (uint32_t b = tid; b < p.nbins; b += 256) wcnt[0][b] = wcnt[1][b] = wcnt[2][b] = wcnt[3][b] = 0;
+  for (uint32_t b = tid; b < p.nbins; b += 256) {
+    base[b] = tot[b];
+    wcnt[0][b] = wcnt[1][b] = wcnt[2][b] = wcnt[3][b] = 0;
+  }
   __syncthreads();
+  block_excl_scan_lds(base, p.nbins, wsum);  // global start of every bin
   const uint32_t t0 = tile * p.tile, t1 = min(n, t0 + p.tile);
   const uint32_t q = p.tile / 4;
   const uint32_t w0 = min(t1, t0 + w * q), w1 = min(t1, w0 + q);
   for (uint32_t i = w0 + lane; i < w1; i += 64) atomicAdd(&wcnt[w][sort_digit(keys_in[i], p)], 1u);
   __syncthreads();
-  // per-bin start of each wave's quarter
-  for (uint32_t b = tid; b < p.nbins; b += 256) {
-    uint32_t run = offsets[(size_t)b * p.ntiles + tile];
+  if (tile == 0 && bin_start) {
+    for (uint32_t b = tid; b < p.nbins; b += 256) bin_start[b] = base[b];
+    if (tid == 0) bin_start[p.nbins] = n;
+  }
+  // this tile's run start of every bin: + records of the bin in earlier tiles (k_sort_colscan)
+  for (uint32_t b = tid; b < p.nbins; b += 256) base[b] += colpre[(size_t)tile * p.nbins + b];
+  __syncthreads();
+  for (uint32_t b = tid; b < p.nbins; b += 256) {  // per-bin start of each wave's quarter
+    uint32_t run = base[b];
     for (int k = 0; k < 4; ++k) {
       const uint32_t c = wcnt[k][b];
       wcnt[k][b] = run;
@@ -157,9 +157,10 @@ __global__ __launch_bounds__(256) void k_sort_scatter(const uint32_t* __restrict
   for (uint32_t c0 = w0; c0 < w1; c0 += 64) {
     const uint32_t i = c0 + lane;
     const bool v = i < w1;
-    uint32_t k = v ? keys_in[i] : 0u;
+    const uint32_t ic = v ? i : w0;  // clamp: never branch around a load
+    uint32_t k = keys_in[ic];
     if (k > p.clamp) k = p.clamp;
-    const uint32_t val = v ? (idx_in ? idx_in[i] : i) : 0u;
+    const uint32_t val = idx_in ? idx_in[ic] : ic;
     const uint32_t d = (k >> p.shift) & p.mask;
     unsigned long long peers = __ballot(v);
     for (uint32_t bit = 0; bit < dbits; ++bit) {
@@ -168,7 +169,7 @@ __global__ __launch_bounds__(256) void k_sort_scatter(const uint32_t* __restrict
     }
     const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
     const uint32_t cnt = (uint32_t)__popcll(peers);
-    const uint32_t start = v ? wcnt[w][d] : 0u;
+    const uint32_t start = wcnt[w][d];
     if (v) {
       keys_out[start + rank] = k;
       idx_out[start + rank] = val;
@@ -1329,9 +1330,9 @@ uint32_t sort_tile(uint32_t n) {
 }
 
 hipError_t launch_sort_pass(hipStream_t st, const uint32_t* keys_in, const uint32_t* idx_in, uint32_t n,
-                            uint32_t clamp_key, int shift, int dbits, uint32_t* hist, uint32_t* keys_out,
-                            uint32_t* idx_out, uint32_t* zero_buf, uint32_t zero_words,
-                            unsigned long long* scratch_top) {
+                            uint32_t clamp_key, int shift, int dbits, uint32_t* hist, uint32_t* tot,
+                            uint32_t* keys_out, uint32_t* idx_out, uint32_t* zero_buf,
+                            uint32_t zero_words, unsigned long long* scratch_top, uint32_t* bin_start) {
   SortPass p;
   p.shift = (uint32_t)shift;
   p.mask = (1u << dbits) - 1u;
@@ -1341,23 +1342,25 @@ hipError_t launch_sort_pass(hipStream_t st, const uint32_t* keys_in, const uint3
   p.clamp = clamp_key;
   hipLaunchKernelGGL(k_sort_hist, dim3(p.ntiles), dim3(256), 0, st, keys_in, n, p, hist, zero_buf, zero_words,
                      scratch_top);
-  hipLaunchKernelGGL(k_sort_offsets, dim3(1), dim3(1024), 0, st, hist, p.nbins * p.ntiles);
+  hipLaunchKernelGGL(k_sort_colscan, dim3((p.nbins + 63) / 64), dim3(64), 0, st, hist, tot, p.nbins, p.ntiles);
   hipLaunchKernelGGL(k_sort_scatter, dim3(p.ntiles), dim3(256), 0, st, keys_in, idx_in, n, p, (uint32_t)dbits, hist,
-                     keys_out, idx_out);
+                     tot, keys_out, idx_out, bin_start);
   return hipGetLastError();
 }
 
-hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev& bt);
+hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev& bt, hipEvent_t ev0, hipEvent_t ev1);
 
-hipError_t launch_match(hipStream_t st, const BookDev& bk, const BatchDev& bt) {
+// ev0 / ev1 (optional, timing): the launch records the kernel's own start and end
+// (hipExtLaunchKernelGGL), so timing adds no marker packet — and no gap — to the stream.
+hipError_t launch_match(hipStream_t st, const BookDev& bk, const BatchDev& bt, hipEvent_t ev0, hipEvent_t ev1) {
   const uint32_t waves = bk.S + 1;
   const dim3 grid((waves + 3) / 4), block(256);
   if (bk.L <= 128) {
-    return launch_match_reg(st, bk, bt);
+    return launch_match_reg(st, bk, bt, ev0, ev1);
   } else if (bk.L <= LDS_MAX_LEVELS) {
-    hipLaunchKernelGGL(k_match<LAD_LDS>, grid, block, 4 * lds_wave_bytes(bk.L), st, bk, bt);
+    hipExtLaunchKernelGGL(k_match<LAD_LDS>, grid, block, 4 * lds_wave_bytes(bk.L), st, ev0, ev1, 0, bk, bt);
   } else {
-    hipLaunchKernelGGL(k_match<LAD_HBM>, grid, block, 0, st, bk, bt);
+    hipExtLaunchKernelGGL(k_match<LAD_HBM>, grid, block, 0, st, ev0, ev1, 0, bk, bt);
   }
   return hipGetLastError();
 }

@@ -103,11 +103,8 @@ struct BatchDev {
   // fills may outgrow it reserves the rest of its batch bound at ovf_base + atomicAdd(scratch_top).
   uint32_t slab;
   unsigned long long ovf_base;
-  // Single-pass grouping sort: the scanned histogram gives every symbol's run directly,
-  // run(s) = [bin_start[s * bin_stride], bin_start[(s + 1) * bin_stride]) (n for the last bin).
+  // Single-pass grouping sort (bins are symbols): run(s) = [bin_start[s], bin_start[s + 1]).
   const uint32_t* bin_start;
-  uint32_t bin_stride;
-  uint32_t nbins;
 };
 
 }  // namespace me

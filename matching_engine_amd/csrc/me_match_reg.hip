@@ -24,6 +24,7 @@
 // chunk into LDS and the walk then reads LDS only; free chunk ids live in a VGPR stack (never a
 // prefetched list pointer); every symbol owns a scratch slab (no per-wave atomic reservation);
 // global loads are never predicated (clamped indices + selects, no branch around a load).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include "me_layout.hpp"
@@ -468,9 +469,9 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
   unsigned long long st_t0 = stamp_now();
 #endif
   uint32_t lo, hi;
-  if (bt.bin_start) {  // single-pass sort: the scanned histogram is the run table
-    lo = bt.bin_start[(size_t)s * bt.bin_stride];
-    hi = s + 1 < bt.nbins ? bt.bin_start[(size_t)(s + 1) * bt.bin_stride] : bt.n;
+  if (bt.bin_start) {  // single-pass sort: the run table
+    lo = bt.bin_start[s];
+    hi = bt.bin_start[s + 1];
   } else {
     lo = wave_lower_bound(bt.skeys, bt.n, s);
     hi = wave_lower_bound(bt.skeys, bt.n, s + 1);
@@ -543,7 +544,7 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
     // ---- 64 records in vector form (two dependent round trips: permutation, then the records)
     const uint32_t j = blk + (uint32_t)lane;
     const bool v = j < hi;
-    const uint32_t oi = bt.perm[v ? j : hi - 1u];
+    const uint32_t oi = bt.perm[v ? j : hi - 1u];  // clamp: never branch around a load
     const unsigned long long oseq_ = bt.seq[oi];
     const long long opx_ = bt.px[oi];
     const int oq_ = bt.qty[oi];
@@ -709,10 +710,11 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
 #endif
 }
 
-hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev& bt) {
+hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev& bt, hipEvent_t ev0, hipEvent_t ev1) {
   if (bk.L > (uint32_t)RL || bk.L < 64u || !bk.fcache || !bk.gsym) return hipErrorInvalidValue;
   const uint32_t waves = bk.S + 1;
-  hipLaunchKernelGGL(k_match_reg, dim3((waves + REG_WAVES - 1) / REG_WAVES), dim3(64 * REG_WAVES), 0, st, bk, bt);
+  hipExtLaunchKernelGGL(k_match_reg, dim3((waves + REG_WAVES - 1) / REG_WAVES), dim3(64 * REG_WAVES), 0, st, ev0,
+                        ev1, 0, bk, bt);
   return hipGetLastError();
 }
 

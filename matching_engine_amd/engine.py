@@ -209,8 +209,9 @@ class Engine:
         return v.value
 
     # -- timing
-    def timing_enable(self, on: bool = True):
-        _check(self.lib, self.h, self.lib.me_timing_enable(self.h, 1 if on else 0))
+    def timing_enable(self, period: int = 1):
+        """HIP events on every `period`-th match launch (True = every launch, 0/False = off)."""
+        _check(self.lib, self.h, self.lib.me_timing_enable(self.h, int(period)))
 
     def timing_read(self):
         m, p = C.c_double(0), C.c_double(0)

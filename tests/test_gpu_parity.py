@@ -239,3 +239,32 @@ def test_full_size_config2_bitexact(me, orc):
             assert np.all(f["maker_seq"] < f["taker_seq"])
         assert_books_equal(eng, ob, range(0, sc.num_symbols, 7), "full c2")
         assert eng.resting_count() == ob.resting()
+
+
+
+def test_back_to_back_device_batches(me, orc):
+    """Device batches submitted back to back without a sync (the bench's pattern): the final books,
+    the resting count, the fill total and the last batch's results/tape equal the oracle's."""
+    sc = me.preset(2)
+    st = me.Stream(sc)
+    base = st.base_prices()
+    batches = [st.next(sc.batch) for _ in range(12)]
+    ob = orc.OracleBook(sc.num_symbols, sc.levels, base, 1 << 22)
+    with engine_for(me, sc.num_symbols, sc.levels, base, sc.batch, 1 << 20, 1 << 22) as eng:
+        dbs = [eng.upload(b) for b in batches]
+        eng.timing_enable(True)
+        for db in dbs:
+            eng.submit_device(db)
+        r, f = eng.fetch_outputs(len(batches[-1]))
+        nfo = 0
+        for b in batches:
+            ro, fo = ob.submit(b)
+            nfo += len(fo)
+        assert_results_equal(r, ro, "back-to-back last batch")
+        assert_fills_equal(f, fo, "back-to-back last batch")
+        tm = eng.timing_read()
+        assert tm["fills"] == nfo and tm["launches"] == len(batches) and tm["match_ms"] > 0
+        assert_books_equal(eng, ob, range(0, sc.num_symbols, 5), "back-to-back")
+        assert eng.resting_count() == ob.resting()
+        for db in dbs:
+            db.free()
