@@ -27,6 +27,7 @@ uint32_t sort_tile(uint32_t n);
 hipError_t launch_tape(hipStream_t st, const BatchDev& bt, me_fill* tape, unsigned long long tape_cap,
                        unsigned long long* tape_count, unsigned long long* fills_acc, uint32_t* err);
 hipError_t launch_init_levels(hipStream_t st, Level* levels, size_t count);
+hipError_t launch_init_chunks(hipStream_t st, Chunk* chunks, size_t count);
 }  // namespace me
 
 using namespace me;
@@ -116,8 +117,8 @@ static int set_create_err(const std::string& s) {
 }
 
 static void free_all(me_engine* e) {
-  void* ptrs[] = {e->bk.levels,   e->bk.occ,      e->bk.sym,      e->bk.chdr,       e->bk.cseq, e->bk.owner, e->bk.tend,
-                  e->bk.cqty,     e->bk.loc,      e->bk.chunk_top, e->bk.err,       (void*)e->bk.gsym,
+  void* ptrs[] = {e->bk.levels,   e->bk.occ,      e->bk.sym,      e->bk.chunks,     e->bk.tend,
+                  e->bk.loc,      e->bk.chunk_top, e->bk.err,       (void*)e->bk.gsym,
                   e->d_seq,       e->d_px,        e->d_qty,       e->d_sym,         e->d_kind,
                   e->d_res,       e->d_fstart,    e->d_scratch,
                   e->d_tape,      e->d_tape_count, e->d_fills_acc, e->bk.dbg,      e->bk.fcache};
@@ -270,10 +271,7 @@ extern "C" me_engine* me_create(const me_config* cfg) {
   ALLOC(bk.occ, S * (L / 64));
   ALLOC(bk.tend, S * L);
   ALLOC(bk.sym, S);
-  ALLOC(bk.chdr, nchunks);
-  ALLOC(bk.owner, nchunks);
-  ALLOC(bk.cseq, nchunks * ME_C);
-  ALLOC(bk.cqty, nchunks * ME_C);
+  ALLOC(bk.chunks, nchunks);
   ALLOC(bk.loc, cfg->max_seq);
   ALLOC(bk.chunk_top, 1);
   ALLOC(bk.err, 1);
@@ -330,9 +328,7 @@ extern "C" me_engine* me_create(const me_config* cfg) {
   bool ok = launch_init_levels(st, bk.levels, S * L) == hipSuccess &&
             hipMemsetAsync(bk.occ, 0, S * (L / 64) * 8, st) == hipSuccess &&
             hipMemsetAsync(bk.tend, 0, S * L, st) == hipSuccess &&
-            hipMemsetAsync(bk.chdr, 0xFF, nchunks * sizeof(ChunkHdr), st) == hipSuccess &&
-            hipMemsetAsync(bk.owner, 0xFF, nchunks * sizeof(uint32_t), st) == hipSuccess &&
-            hipMemsetAsync(bk.cqty, 0, nchunks * ME_C * sizeof(int), st) == hipSuccess &&
+            launch_init_chunks(st, bk.chunks, nchunks) == hipSuccess &&
             hipMemsetAsync(bk.loc, 0xFF, cfg->max_seq * sizeof(uint32_t), st) == hipSuccess &&
             hipMemsetAsync(bk.fcache, 0xFF, S * 64 * sizeof(uint32_t), st) == hipSuccess &&
             hipMemsetAsync(bk.chunk_top, 0, 4, st) == hipSuccess && hipMemsetAsync(bk.err, 0, 4, st) == hipSuccess &&
@@ -583,16 +579,12 @@ static int walk_fifo(me_engine* e, const Level& lv, std::vector<std::pair<uint64
   uint64_t guard = 0;
   while (ch != NIL) {
     if (ch >= e->bk.nchunks || ++guard > e->bk.nchunks) return e->fail(ME_E_STATE, "corrupt FIFO chain");
-    ChunkHdr h;
-    uint64_t seqs[ME_C];
-    int32_t qs[ME_C];
-    HIP_TRY(hipMemcpy(&h, e->bk.chdr + ch, sizeof(h), hipMemcpyDeviceToHost), "D2H chunk");
-    HIP_TRY(hipMemcpy(seqs, e->bk.cseq + (size_t)ch * ME_C, sizeof(seqs), hipMemcpyDeviceToHost), "D2H chunk");
-    HIP_TRY(hipMemcpy(qs, e->bk.cqty + (size_t)ch * ME_C, sizeof(qs), hipMemcpyDeviceToHost), "D2H chunk");
+    Chunk c;
+    HIP_TRY(hipMemcpy(&c, e->bk.chunks + ch, sizeof(c), hipMemcpyDeviceToHost), "D2H chunk");
     for (uint32_t k = 0; k < (uint32_t)ME_C; ++k)  // a slot is live iff qty > 0; slot order = time order
-      if (qs[k] > 0) out.emplace_back(seqs[k], qs[k]);
+      if (c.qty[k] > 0) out.emplace_back(c.seq[k], c.qty[k]);
     if (ch == lv.tail) break;
-    ch = h.next;
+    ch = c.hdr.next;
   }
   return ME_OK;
 }

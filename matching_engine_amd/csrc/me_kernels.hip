@@ -435,8 +435,8 @@ __device__ __forceinline__ void cache_writeback(const C& c, int lvl, CacheEntry*
   const int lane = lane_id();
   if (lane < ME_C) {
     const size_t g = (size_t)cid * ME_C + lane;
-    c.bk.cqty[g] = E->qty[lane];
-    c.bk.cseq[g] = E->seq[lane];
+    cq_at(c.bk.chunks, g) = E->qty[lane];
+    cs_at(c.bk.chunks, g) = E->seq[lane];
   }
 }
 
@@ -471,9 +471,9 @@ __device__ __forceinline__ CacheEntry* cache_get(C& c, int lvl, uint32_t ch) {
   const int lane = lane_id();
   const bool act = lane < ME_C;
   const size_t g = (size_t)ch * ME_C + (act ? lane : 0);
-  const int q = act ? c.bk.cqty[g] : 0;
-  const unsigned long long sq = act ? c.bk.cseq[g] : 0ull;
-  const uint32_t nx = c.bk.chdr[ch].next;
+  const int q = act ? cq_at(c.bk.chunks, g) : 0;
+  const unsigned long long sq = act ? cs_at(c.bk.chunks, g) : 0ull;
+  const uint32_t nx = c.bk.chunks[ch].hdr.next;
   if (act) {
     E->qty[lane] = q;
     E->seq[lane] = sq;
@@ -523,7 +523,7 @@ template <class C>
 __device__ __forceinline__ void set_next(C& c, int lvl, uint32_t ch, uint32_t v) {
   const bool mirror = c.cache && cache_holds(c, lvl, ch);
   if (lane_id() == 0) {
-    c.bk.chdr[ch].next = v;
+    c.bk.chunks[ch].hdr.next = v;
     if (mirror) centry(c, lvl)->next = v;
   }
 }
@@ -532,7 +532,7 @@ __device__ __forceinline__ void set_next(C& c, int lvl, uint32_t ch, uint32_t v)
 // Free-list push: the popped-next is known without a load.
 template <class C>
 __device__ __forceinline__ void free_chunk(C& c, uint32_t ch) {
-  if (lane_id() == 0) c.bk.chdr[ch].next = c.free_head;
+  if (lane_id() == 0) c.bk.chunks[ch].hdr.next = c.free_head;
   c.free_next = c.free_head;
   c.free_head = ch;
 }
@@ -542,7 +542,7 @@ __device__ __forceinline__ void free_chunk(C& c, uint32_t ch) {
 template <class C>
 __device__ __forceinline__ void prefetch_free_next(C& c) {
   const bool ok = c.free_head < c.bk.nchunks;
-  const uint32_t v = c.bk.chdr[ok ? c.free_head : 0].next;
+  const uint32_t v = c.bk.chunks[ok ? c.free_head : 0].hdr.next;
   c.free_next = ok ? v : NIL;
 }
 
@@ -625,9 +625,9 @@ __device__ __forceinline__ uint32_t walk_level(C& c, int lvl, long long take, ui
       sv = act ? E->seq[lane] : 0ull;
       nxt_v = E->next;
     } else {
-      nxt_v = bk.chdr[ch].next;  // issue every load of the chunk before the first use
-      qv = act ? bk.cqty[g] : 0;
-      sv = act ? bk.cseq[g] : 0ull;
+      nxt_v = bk.chunks[ch].hdr.next;  // issue every load of the chunk before the first use
+      qv = act ? cq_at(bk.chunks, g) : 0;
+      sv = act ? cs_at(bk.chunks, g) : 0ull;
     }
     const long long inc = wave_incl_scan((long long)qv);
     const long long ex = inc - qv;
@@ -641,7 +641,7 @@ __device__ __forceinline__ uint32_t walk_level(C& c, int lvl, long long take, ui
       if (fe) E->qty[lane] = qv - (int)f;
       cache_mark_dirty(c, lvl);
     } else if (fe) {
-      bk.cqty[g] = qv - (int)f;
+      cq_at(bk.chunks, g) = qv - (int)f;
     }
     c.resting_delta -= __popcll(__ballot(fe && f == qv));  // makers filled completely leave the book
     const long long live = rli64(inc, 63);
@@ -663,7 +663,7 @@ __device__ __forceinline__ uint32_t walk_level(C& c, int lvl, long long take, ui
       return ch;
     }
   }
-  if (ch != head && ch < bk.nchunks && lane == 0) bk.chdr[ch].prev = NIL;  // new FIFO head
+  if (ch != head && ch < bk.nchunks && lane == 0) bk.chunks[ch].hdr.prev = NIL;  // new FIFO head
   return ch;
 }
 
@@ -807,9 +807,8 @@ __device__ __forceinline__ bool rest_order(C& c, int lvl, unsigned long long seq
       h.next = NIL;
       h.prev = L.tail;
       h.level = (uint32_t)lvl;
-      h.pad = 0;
-      bk.chdr[ch] = h;
-      bk.owner[ch] = c.s;
+      h.owner = c.s;
+      bk.chunks[ch].hdr = h;
     }
     if (L.tail != NIL) set_next(c, lvl, L.tail, ch);
     if (L.tail == NIL) {
@@ -835,8 +834,8 @@ __device__ __forceinline__ bool rest_order(C& c, int lvl, unsigned long long seq
       E->seq[slot] = seq;
       E->qty[slot] = qty;
     } else {
-      bk.cseq[g] = seq;
-      bk.cqty[g] = qty;
+      cs_at(bk.chunks, g) = seq;
+      cq_at(bk.chunks, g) = qty;
     }
     if (seq < bk.max_seq) bk.loc[seq] = (uint32_t)g;
   }
@@ -866,11 +865,11 @@ __device__ __forceinline__ int cancel_order(C& c, unsigned long long tgt) {
   const uint32_t ch = g / ME_C, slot = g % ME_C;
   if (ch >= bk.nchunks) return 0;
   // one round trip: owner, header, the whole chunk's quantities and the target seq
-  const uint32_t owner = rl32(bk.owner[ch], 0);
-  const ChunkHdr hd = bk.chdr[ch];
+  const uint32_t owner = rl32(bk.chunks[ch].hdr.owner, 0);
+  const ChunkHdr hd = bk.chunks[ch].hdr;
   const bool act = lane < ME_C;
-  int qv = act ? bk.cqty[(size_t)ch * ME_C + lane] : 0;
-  unsigned long long sq = rl64(bk.cseq[g], 0);
+  int qv = act ? cq_at(bk.chunks, (size_t)ch * ME_C + lane) : 0;
+  unsigned long long sq = rl64(cs_at(bk.chunks, g), 0);
   if (owner != c.s) return 0;  // another symbol's order: never touch its book
   const int lvl = (int)rl32(hd.level, 0);
   if (lvl < 0 || lvl >= (int)bk.L) {
@@ -897,14 +896,14 @@ __device__ __forceinline__ int cancel_order(C& c, unsigned long long tgt) {
     if (E) {
       E->qty[slot] = 0;
     } else {
-      bk.cqty[g] = 0;
+      cq_at(bk.chunks, g) = 0;
     }
   }
   wave_mem_order();
   if (L.total == 0) {
     // splice the whole (now dead) FIFO onto the free list
     cache_drop(c, lvl, L.head);
-    if (lane == 0) bk.chdr[L.tail].next = c.free_head;
+    if (lane == 0) bk.chunks[L.tail].hdr.next = c.free_head;
     c.free_next = (L.head == L.tail) ? c.free_head : NIL;
     c.free_head = L.head;
     if (L.head != L.tail) prefetch_free_next(c);
@@ -919,14 +918,14 @@ __device__ __forceinline__ int cancel_order(C& c, unsigned long long tgt) {
     uint32_t nh = L.head, nt = L.tail;
     if (ch == L.head) {
       nh = nxt;
-      if (lane == 0) bk.chdr[nxt].prev = NIL;
+      if (lane == 0) bk.chunks[nxt].hdr.prev = NIL;
     } else if (ch == L.tail) {
       nt = prv;
       set_next(c, lvl, prv, NIL);
       c.lad.set_te(lvl, ME_C);  // a non-tail chunk is always full
     } else {
       set_next(c, lvl, prv, nxt);
-      if (lane == 0) bk.chdr[nxt].prev = prv;
+      if (lane == 0) bk.chunks[nxt].hdr.prev = prv;
     }
     if (ch == L.head) cache_drop(c, lvl, ch);  // the cache only ever holds a level's head
     L.head = nh;
@@ -1082,8 +1081,8 @@ __device__ __forceinline__ void cache_flush_all(C& c, uint32_t entries) {
     const CacheEntry* E = c.cache + e;
     const uint32_t cid = E->cid;
     if (cid != NIL && E->dirty) {
-      c.bk.cqty[(size_t)cid * ME_C + sl] = E->qty[sl];
-      c.bk.cseq[(size_t)cid * ME_C + sl] = E->seq[sl];
+      cq_at(c.bk.chunks, (size_t)cid * ME_C + sl) = E->qty[sl];
+      cs_at(c.bk.chunks, (size_t)cid * ME_C + sl) = E->seq[sl];
     }
   }
 }
@@ -1194,8 +1193,8 @@ __global__ __launch_bounds__(256) void k_match(BookDev bk, BatchDev bt) {
         const uint32_t cid = row ? rl32(c.lad.h1, j) : rl32(c.lad.h0, j);
         const CacheEntry* E = c.cache + row * 64 + j;
         if (lane < ME_C) {
-          c.bk.cqty[(size_t)cid * ME_C + lane] = E->qty[lane];
-          c.bk.cseq[(size_t)cid * ME_C + lane] = E->seq[lane];
+          cq_at(c.bk.chunks, (size_t)cid * ME_C + lane) = E->qty[lane];
+          cs_at(c.bk.chunks, (size_t)cid * ME_C + lane) = E->seq[lane];
         }
       }
     }
@@ -1370,6 +1369,20 @@ hipError_t launch_tape(hipStream_t st, const BatchDev& bt, me_fill* tape, unsign
   const uint32_t ntiles = (bt.n + TILE_TAPE - 1) / TILE_TAPE;
   hipLaunchKernelGGL(k_tape_compact, dim3(ntiles), dim3(256), 0, st, bt.tile_sum, ntiles, bt.res, bt.fstart,
                      bt.n, bt.scratch, tape, tape_cap, tape_count, fills_acc, err);
+  return hipGetLastError();
+}
+
+__global__ void k_init_chunks(Chunk* ch, size_t count) {
+  // one thread per 16-B piece of the 256-B blocks: header all-NIL, everything else zero
+  const size_t pieces = count * (sizeof(Chunk) / 16);
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < pieces; i += (size_t)gridDim.x * blockDim.x) {
+    uint4 v = (i % (sizeof(Chunk) / 16)) == 0 ? make_uint4(NIL, NIL, NIL, NIL) : make_uint4(0, 0, 0, 0);
+    reinterpret_cast<uint4*>(ch)[i] = v;
+  }
+}
+
+hipError_t launch_init_chunks(hipStream_t st, Chunk* chunks, size_t count) {
+  hipLaunchKernelGGL(k_init_chunks, dim3(8192), dim3(256), 0, st, chunks, count);
   return hipGetLastError();
 }
 

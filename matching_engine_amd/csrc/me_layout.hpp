@@ -10,8 +10,8 @@
 //   occ    [S][L/64] occupancy bitmap of the ladder (bit set <=> total > 0).
 //   sym    [S]      32 B per-symbol scalars (window base, best bid/ask level, chunk free list).
 //   tend   [S][L]   slots written in each level's tail chunk (appends need no chunk read).
-//   chunks [NC]     FIFO storage: a level's queue is a doubly linked list of chunks of ME_C
-//                   slots {seq u64, qty i32} (SoA: cseq / cqty); a wave reads one chunk per load.
+//   chunks [NC]     FIFO storage: a level's queue is a doubly linked list of 256-B chunk blocks of
+//                   ME_C slots {seq u64, qty i32} (SoA inside the block); a wave reads one chunk per load.
 //                   A slot is live iff qty > 0. Every linked chunk holds >= 1 live order (a chunk
 //                   emptied by cancels is unlinked at once), so chunks in use <= resting orders.
 //   loc    [max_seq] seq -> global slot (chunk * ME_C + slot) for cancels.
@@ -49,8 +49,21 @@ struct alignas(16) ChunkHdr {
   uint32_t next;   // next chunk of the level FIFO, or of the symbol free list
   uint32_t prev;   // previous chunk of the level FIFO (NIL at the head)
   uint32_t level;  // level index the chunk belongs to
-  uint32_t pad;
+  uint32_t owner;  // symbol that allocated the chunk (chunks never change symbol)
 };
+
+// One FIFO chunk, 256 B: header, then the 16 slot quantities (one 64-B segment), then the 16 slot
+// seqs (two 64-B segments). One pointer reaches all of it; slot id g = chunk * ME_C + slot.
+struct alignas(256) Chunk {
+  ChunkHdr hdr;
+  uint32_t pad[12];
+  int qty[ME_C];
+  unsigned long long seq[ME_C];
+};
+static_assert(sizeof(Chunk) == 256, "chunk block must be 256 B");
+
+__host__ __device__ __forceinline__ int& cq_at(Chunk* c, size_t g) { return c[g / ME_C].qty[g % ME_C]; }
+__host__ __device__ __forceinline__ unsigned long long& cs_at(Chunk* c, size_t g) { return c[g / ME_C].seq[g % ME_C]; }
 
 struct alignas(32) SymState {
   long long base;      // price_q4 of level 0
@@ -67,10 +80,7 @@ struct BookDev {
   unsigned long long* occ;
   uint8_t* tend;          // [S][L] slots written in the level's tail chunk (valid when tail != NIL)
   SymState* sym;
-  ChunkHdr* chdr;
-  uint32_t* owner;        // [NC] symbol that allocated the chunk (chunks never change symbol)
-  unsigned long long* cseq;
-  int* cqty;
+  Chunk* chunks;          // [NC] FIFO chunk blocks
   uint32_t* loc;
   uint32_t* chunk_top;
   uint32_t* fcache;       // [S][64] free chunk ids parked between launches (register-ladder kernel)

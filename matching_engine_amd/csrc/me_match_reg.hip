@@ -6,17 +6,23 @@
 //
 //   * the ladder's FIFO ends (head chunk, tail chunk, tail fill) live in VGPRs — level l is lane
 //     l & 63 of row l >> 6 — so reading one is a v_readlane and writing one a lane select;
-//   * occupancy and the head-chunk cache's valid / dirty state are 128-bit SGPR masks, so the
-//     next best price is a bit scan and a cache lookup a bit test;
+//   * occupancy and the head-chunk cache's valid state are 128-bit SGPR masks, so the next best
+//     price is a bit scan and a cache lookup a bit test;
 //   * the head chunk of every level can sit in LDS (16 slots of qty + seq: 26 KB per wave, no
-//     evictions); fills, appends and cancels of a cached head never touch HBM, and it is written
-//     back once at the end of the launch;
+//     evictions); fills, appends and cancels of a cached head never touch HBM, and every valid
+//     entry is written back once at the end of the launch;
 //   * level totals are only ever added to on the hot path: fire-and-forget LDS atomics;
 //   * a chunk's 16 slots are ranked with a 4-step DPP scan of 32-bit saturating adds (one DPP row;
 //     saturation keeps the comparison with the remaining taker quantity exact);
 //   * reject reasons, prices -> levels and the per-record result records are computed for 64
 //     records at a time in vector form; the serial loop visits only records that touch the book
 //     and hands back three numbers per record (quantity, fill count, first scratch fill).
+//
+// Scalar discipline: the wave index goes through readfirstlane, so the divergence analysis sees
+// every per-symbol value and branch as wave-uniform (scalar branches, no exec-mask juggling). The
+// scalar file (102 SGPRs) then holds only the hot state: launch arguments live in LDS and are read
+// where used (ldsu), rarely used cursors live in the wave's LDS, and the pointers / constants that
+// only feed vector memory operations and vector arithmetic are kept in VGPRs (vreg).
 //
 // Memory-counter discipline (gfx950 counts loads AND stores in vmcnt, in issue order): a wait for a
 // load also waits for every store issued before it, i.e. a full HBM write round trip. So the serial
@@ -40,7 +46,10 @@ struct RegLds {
   int cq[RL][ME_C];
   unsigned long long cs[RL][ME_C];
   long long tot[RL];
-  uint32_t cnext[RL];  // chdr[head].next of the cached head (kept in step with HBM)
+  uint32_t cnext[RL];  // chunks[head].hdr.next of the cached head (kept in step with HBM)
+  uint32_t free_head;  // overflow free list in HBM (hdr.next links), NIL if empty
+  uint32_t bump_cur, bump_end;  // chunk ids reserved from the global bump allocator
+  uint32_t pad;
 };
 constexpr int REG_WAVES = 4;  // waves (symbols) per workgroup
 constexpr int VMCNT0 = 0x0F70;  // s_waitcnt immediate: vmcnt(0), expcnt / lgkmcnt untouched (gfx9 encoding)
@@ -94,27 +103,72 @@ struct Mask2 {
   }
 };
 
+// The launch arguments, copied to LDS once per workgroup. Everything the serial loop does not
+// touch on its common paths is read back from here where it is used (ldsu), so those values hold
+// no SGPRs across the loop — the hot state (masks, best prices, cursors) keeps the scalar file.
+struct ColdArgs {
+  BookDev bk;
+  BatchDev bt;
+};
+
+// A wave-uniform value read from LDS at the point of use. A relaxed atomic load is never hoisted out
+// of a loop (a plain load would be, pinning the value in SGPRs for the whole loop) and, unlike a
+// volatile one, keeps its LDS address space (ds_read, not flat); readfirstlane makes it scalar.
+template <class T>
+__device__ __forceinline__ T ldsu(const T& f) {
+  static_assert(sizeof(T) == 8 || sizeof(T) == 4, "ldsu: 4- or 8-byte values");
+  if constexpr (sizeof(T) == 8) {
+    const unsigned long long v = __hip_atomic_load((const unsigned long long*)&f, __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+    // readfirstlane (first ACTIVE lane): readlane 0 may read an inactive lane in a divergent branch
+    const unsigned long long r =
+        ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((int)(v >> 32)) << 32) |
+        (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    return __builtin_bit_cast(T, r);
+  } else {
+    const uint32_t v = __hip_atomic_load((const uint32_t*)&f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return __builtin_bit_cast(T, (uint32_t)__builtin_amdgcn_readfirstlane((int)v));
+  }
+}
+
+// Store a wave-uniform 32-bit value into the wave's LDS (lane 0; read back with ldsu).
+__device__ __forceinline__ void ldsw(uint32_t& f, uint32_t v) {
+  if (lane_id() == 0) __hip_atomic_store(&f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// Keep a wave-uniform value in VGPRs: the empty asm makes it opaque (hence "divergent") to the
+// compiler, so it never takes an SGPR. For pointers and constants that only feed vector memory
+// operations and vector arithmetic.
+__device__ __forceinline__ uint32_t vreg(uint32_t x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+__device__ __forceinline__ unsigned long long vreg64(unsigned long long x) {
+  uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  asm volatile("" : "+v"(lo), "+v"(hi));
+  return ((unsigned long long)hi << 32) | lo;
+}
+template <class T>
+__device__ __forceinline__ T* vptr(T* p) {
+  return (T*)vreg64((unsigned long long)p);
+}
+
 struct RegCtx {
-  ChunkHdr* chdr;
-  uint32_t* owner;
-  unsigned long long* cseq;
-  int* cqty;
-  uint32_t* loc;
-  uint32_t* chunk_top;
-  uint32_t* err;
-  me_fill* scratch;
+  Chunk* chunks;       // VGPR
+  uint32_t* loc;       // VGPR
+  me_fill* scratch;    // VGPR
   RegLds* M;
-  unsigned long long max_seq;
-  long long base;
-  uint32_t nchunks, L;
-  uint32_t s, gs;
+  const ColdArgs* G;
+  long long base;      // VGPR (price of level 0: vector uses only)
+  uint32_t gs;         // VGPR (symbol id written into fills)
+  uint32_t nchunks;
+  uint32_t s;
   Row2 hd, tl, te;     // head chunk, tail chunk, slots written in the tail chunk
-  Mask2 occ, cv, cd;   // occupied levels, cache entry valid (holds the head), cache entry dirty
+  Mask2 occ, cv;       // occupied levels, cache entry valid (holds the level's current head chunk)
   int bb, ba;          // best bid level (-1: none), best ask level (RL: none)
   uint32_t fstk;       // VGPR stack of free chunk ids: lane i holds entry i ...
   uint32_t nfs;        // ... entries [0, nfs) are valid
-  uint32_t free_head;  // overflow free list in HBM (chdr[].next links), NIL if empty
-  uint32_t bump_cur, bump_end, recs_left;
+  uint32_t recs_left;  // records of this wave not yet processed (>= chunks it can still need)
   int resting;
   uint32_t wptr, wend; // next scratch fill of this wave and the end of its reservation
 #ifdef ME_STAMPS
@@ -124,7 +178,7 @@ struct RegCtx {
 };
 
 __device__ __forceinline__ void reg_err(const RegCtx& c, uint32_t bits) {
-  if (lane_id() == 0) atomicOr(c.err, bits);
+  if (lane_id() == 0) atomicOr(ldsu(c.G->bk.err), bits);
 }
 
 // Inclusive scan of a 16-lane row (each DPP row scans on its own), saturating at 2^32 - 1.
@@ -148,9 +202,40 @@ __device__ __forceinline__ void reg_free(RegCtx& c, uint32_t ch) {
     c.fstk = lane_id() == (int)c.nfs ? ch : c.fstk;
     c.nfs += 1;
   } else {
-    if (lane_id() == 0) c.chdr[ch].next = c.free_head;
-    c.free_head = ch;
+    const uint32_t fh = ldsu(c.M->free_head);
+    if (lane_id() == 0) c.chunks[ch].hdr.next = fh;
+    ldsw(c.M->free_head, ch);
   }
+}
+
+// Stack ran dry: pop the HBM overflow list (one dependent load) or take a reserved / freshly
+// reserved id of the global bump allocator. Cursors live in the wave's LDS (rare path).
+__device__ __forceinline__ uint32_t reg_alloc_slow(RegCtx& c) {
+  const uint32_t fh = ldsu(c.M->free_head);
+  if (fh != NIL) {
+    if (fh >= c.nchunks) {
+      reg_err(c, ERR_INCONSISTENT);
+      return NIL;
+    }
+    ldsw(c.M->free_head, rl32(c.chunks[fh].hdr.next, 0));
+    return fh;
+  }
+  uint32_t cur = ldsu(c.M->bump_cur);
+  if (cur >= ldsu(c.M->bump_end)) {
+    // each record needs at most one new chunk: never reserve more than the records left
+    const uint32_t blk = min(16u, max(c.recs_left, 1u));
+    uint32_t got = 0;
+    if (lane_id() == 0) got = atomicAdd(ldsu(c.G->bk.chunk_top), blk);
+    got = rl32(got, 0);
+    if (got >= c.nchunks) {
+      reg_err(c, ERR_CHUNK_OOM);
+      return NIL;
+    }
+    cur = got;
+    ldsw(c.M->bump_end, min(got + blk, c.nchunks));
+  }
+  ldsw(c.M->bump_cur, cur + 1);
+  return cur;
 }
 
 __device__ __forceinline__ uint32_t reg_alloc(RegCtx& c) {
@@ -158,29 +243,7 @@ __device__ __forceinline__ uint32_t reg_alloc(RegCtx& c) {
     c.nfs -= 1;
     return rl32(c.fstk, (int)c.nfs);
   }
-  if (c.free_head != NIL) {  // overflow list: one dependent load (rare: the stack ran dry)
-    const uint32_t ch = c.free_head;
-    if (ch >= c.nchunks) {
-      reg_err(c, ERR_INCONSISTENT);
-      return NIL;
-    }
-    c.free_head = rl32(c.chdr[ch].next, 0);
-    return ch;
-  }
-  if (c.bump_cur >= c.bump_end) {
-    // each record needs at most one new chunk: never reserve more than the records left
-    const uint32_t blk = min(16u, max(c.recs_left, 1u));
-    uint32_t got = 0;
-    if (lane_id() == 0) got = atomicAdd(c.chunk_top, blk);
-    got = rl32(got, 0);
-    if (got >= c.nchunks) {
-      reg_err(c, ERR_CHUNK_OOM);
-      return NIL;
-    }
-    c.bump_cur = got;
-    c.bump_end = min(got + blk, c.nchunks);
-  }
-  return c.bump_cur++;
+  return reg_alloc_slow(c);
 }
 
 // ---- head-chunk cache ------------------------------------------------------------------------
@@ -194,9 +257,9 @@ __device__ __forceinline__ bool reg_fill_entry(RegCtx& c, int lvl, uint32_t ch) 
   const int lane = lane_id();
   const int sl = lane & (ME_C - 1);
   const size_t g = (size_t)ch * ME_C + sl;
-  const uint32_t nx = c.chdr[ch].next;
-  const int qv = c.cqty[g];
-  const unsigned long long sv = c.cseq[g];
+  const uint32_t nx = c.chunks[ch].hdr.next;
+  const int qv = cq_at(c.chunks, g);
+  const unsigned long long sv = cs_at(c.chunks, g);
   // Resolve the loads on every path here (vmcnt(0)): a load left pending behind the lane-masked
   // LDS writes below would make the compiler wait for it (and all later stores) in the hit path.
   __builtin_amdgcn_s_waitcnt(VMCNT0);
@@ -226,12 +289,10 @@ __device__ __forceinline__ bool reg_walk(RegCtx& c, int lvl, uint32_t& rem, unsi
       STAMP_ADD(c, PH_WALK);
       if (!reg_fill_entry(c, lvl, ch)) return false;
       c.cv.set(lvl);
-      c.cd.clr(lvl);
       STAMP_ADD(c, WK_GET);
     }
     COUNT(c, CT_WALK);
     const int q_ = c.M->cq[lvl][sl];
-    const unsigned long long sv = c.M->cs[lvl][sl];
     const uint32_t nx = c.M->cnext[lvl];
     const uint32_t uq = act ? (uint32_t)q_ : 0u;
     const uint32_t inc = scan16_sat(uq);
@@ -243,16 +304,15 @@ __device__ __forceinline__ bool reg_walk(RegCtx& c, int lvl, uint32_t& rem, unsi
     if (fe) {
       me_fill F;
       F.taker_seq = taker;
-      F.maker_seq = sv;
+      F.maker_seq = c.M->cs[lvl][sl];
       F.price_q4 = price;
       F.qty = (int)f;
       F.symbol = c.gs;
-      c.scratch[c.wptr + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32),
-                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u))] = F;
+      // fills only ever come from lanes 0..15: mbcnt_lo alone ranks them
+      c.scratch[c.wptr + (uint32_t)__builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u)] = F;
       c.M->cq[lvl][sl] = (int)(uq - f);
     }
     c.wptr += (uint32_t)__popcll(fm);
-    c.cd.set(lvl);
     c.resting -= __popcll(__ballot(fe && f == uq));  // makers filled completely leave the book
     const uint32_t live = rl32(inc, 15);
     const uint32_t t = rem < live ? rem : live;
@@ -260,9 +320,8 @@ __device__ __forceinline__ bool reg_walk(RegCtx& c, int lvl, uint32_t& rem, unsi
     taken += t;
     if (__ballot(act && uq > f)) break;  // a live slot remains: the taker is done
     // chunk exhausted: its HBM copy must read all-zero before the chunk is reused
-    if (act) c.cqty[(size_t)ch * ME_C + sl] = 0;
+    if (act) cq_at(c.chunks, (size_t)ch * ME_C + sl) = 0;
     c.cv.clr(lvl);
-    c.cd.clr(lvl);
     reg_free(c, ch);
     if (ch == tail) {
       c.hd.put(lvl, NIL);
@@ -277,7 +336,7 @@ __device__ __forceinline__ bool reg_walk(RegCtx& c, int lvl, uint32_t& rem, unsi
   tot_add(c, lvl, -(long long)taken);
   if (ch != head) {
     c.hd.put(lvl, ch);
-    if (lane == 0 && ch < c.nchunks) c.chdr[ch].prev = NIL;  // new FIFO head
+    if (lane == 0 && ch < c.nchunks) c.chunks[ch].hdr.prev = NIL;  // new FIFO head
   }
   return false;
 }
@@ -299,9 +358,8 @@ __device__ __forceinline__ bool reg_rest(RegCtx& c, int lvl, unsigned long long 
       h.next = NIL;
       h.prev = tl;
       h.level = (uint32_t)lvl;
-      h.pad = 0;
-      c.chdr[ch] = h;
-      c.owner[ch] = c.s;
+      h.owner = c.s;
+      c.chunks[ch].hdr = h;
     }
     if (tl == NIL) {  // empty level: the new chunk is its head, installed in the cache zeroed
       c.hd.put(lvl, ch);
@@ -312,7 +370,7 @@ __device__ __forceinline__ bool reg_rest(RegCtx& c, int lvl, unsigned long long 
     } else {
       const bool tl_cached = c.cv.bit(lvl) && c.hd.get(lvl) == tl;
       if (lane == 0) {
-        if (tl < c.nchunks) c.chdr[tl].next = ch;
+        if (tl < c.nchunks) c.chunks[tl].hdr.next = ch;
         if (tl_cached) c.M->cnext[lvl] = ch;
       }
       in_cache = false;
@@ -333,13 +391,12 @@ __device__ __forceinline__ bool reg_rest(RegCtx& c, int lvl, unsigned long long 
       c.M->cq[lvl][slot] = (int)qty;
       c.M->cs[lvl][slot] = seq;
     } else {
-      c.cqty[g] = (int)qty;
-      c.cseq[g] = seq;
+      cq_at(c.chunks, g) = (int)qty;
+      cs_at(c.chunks, g) = seq;
     }
     c.loc[seq] = g;
   }
   tot_add(c, lvl, (long long)qty);
-  if (in_cache) c.cd.set(lvl);
   c.te.put(lvl, slot + 1);
   c.occ.set(lvl);
   if (buy) {
@@ -357,7 +414,7 @@ __device__ __forceinline__ bool reg_rest(RegCtx& c, int lvl, unsigned long long 
 __device__ __forceinline__ uint32_t reg_cancel(RegCtx& c, unsigned long long tgt) {
   const int lane = lane_id();
   const bool act = lane < ME_C;
-  if (tgt == 0ull || tgt >= c.max_seq) return 0;
+  if (tgt == 0ull || tgt >= ldsu(c.G->bk.max_seq)) return 0;
   wave_mem_order();
   const uint32_t g = rl32(c.loc[tgt], 0);
   __builtin_amdgcn_s_waitcnt(VMCNT0);
@@ -365,15 +422,15 @@ __device__ __forceinline__ uint32_t reg_cancel(RegCtx& c, unsigned long long tgt
   const uint32_t ch = g / ME_C, slot = g % ME_C;
   if (ch >= c.nchunks) return 0;
   // one round trip: owner, header, the chunk's quantities and the target seq
-  const uint32_t own = rl32(c.owner[ch], 0);
-  const ChunkHdr hdr = c.chdr[ch];
-  const int qg = c.cqty[(size_t)ch * ME_C + (lane & (ME_C - 1))];
-  unsigned long long sq = rl64(c.cseq[g], 0);
+  const uint32_t own = rl32(c.chunks[ch].hdr.owner, 0);
+  const ChunkHdr hdr = c.chunks[ch].hdr;
+  const int qg = cq_at(c.chunks, (size_t)ch * ME_C + (lane & (ME_C - 1)));
+  unsigned long long sq = rl64(cs_at(c.chunks, g), 0);
   __builtin_amdgcn_s_waitcnt(VMCNT0);  // resolved on every path (see reg_fill_entry)
   int qv = act ? qg : 0;
   if (own != c.s) return 0;  // another symbol's order: never touch its book
   const int lvl = (int)rl32(hdr.level, 0);
-  if (lvl < 0 || lvl >= (int)c.L) {
+  if (lvl < 0 || lvl >= RL) {
     reg_err(c, ERR_INCONSISTENT);
     return 0;
   }
@@ -391,19 +448,17 @@ __device__ __forceinline__ uint32_t reg_cancel(RegCtx& c, unsigned long long tgt
     if (in_cache)
       c.M->cq[lvl][slot] = 0;
     else
-      c.cqty[g] = 0;
+      cq_at(c.chunks, g) = 0;
   }
   tot_add(c, lvl, -(long long)q);
-  if (in_cache) c.cd.set(lvl);
   if (live_after == 0u) {
     if (h >= c.nchunks || t >= c.nchunks) {
       reg_err(c, ERR_INCONSISTENT);
       return (uint32_t)q;
     }
     if (in_cache) {  // the chunk leaves the cache; its HBM copy must read all-zero
-      if (act) c.cqty[(size_t)ch * ME_C + lane] = 0;
+      if (act) cq_at(c.chunks, (size_t)ch * ME_C + lane) = 0;
       c.cv.clr(lvl);
-      c.cd.clr(lvl);
     }
     const uint32_t nxt = rl32(hdr.next, 0), prv = rl32(hdr.prev, 0);
     const bool mirror = c.cv.bit(lvl) && h == prv;  // the cached head is ch's predecessor
@@ -415,18 +470,18 @@ __device__ __forceinline__ uint32_t reg_cancel(RegCtx& c, unsigned long long tgt
       if (lvl == c.ba) c.ba = c.occ.next(lvl);
     } else if (ch == h) {
       c.hd.put(lvl, nxt);
-      if (lane == 0) c.chdr[nxt].prev = NIL;
+      if (lane == 0) c.chunks[nxt].hdr.prev = NIL;
     } else if (ch == t) {
       c.tl.put(lvl, prv);
       c.te.put(lvl, ME_C);  // a non-tail chunk is always full
       if (lane == 0) {
-        c.chdr[prv].next = NIL;
+        c.chunks[prv].hdr.next = NIL;
         if (mirror) c.M->cnext[lvl] = NIL;
       }
     } else {
       if (lane == 0) {
-        c.chdr[prv].next = nxt;
-        c.chdr[nxt].prev = prv;
+        c.chunks[prv].hdr.next = nxt;
+        c.chunks[nxt].hdr.prev = prv;
         if (mirror) c.M->cnext[lvl] = nxt;
       }
     }
@@ -440,8 +495,9 @@ __device__ __forceinline__ uint32_t reg_cancel(RegCtx& c, unsigned long long tgt
 // The taker about to run may emit up to `resting` fills. If they might not fit the wave's slab,
 // reserve the batch bound of everything left (resting + 2 * records left) in the
 // shared overflow region once; after that no further check can fail.
-__device__ __forceinline__ bool reg_reserve_overflow(RegCtx& c, unsigned long long* top, unsigned long long base,
-                                                  unsigned long long cap) {
+__device__ __forceinline__ bool reg_reserve_overflow(RegCtx& c) {
+  unsigned long long* top = ldsu(c.G->bt.scratch_top);
+  const unsigned long long base = ldsu(c.G->bt.ovf_base), cap = ldsu(c.G->bt.scratch_cap);
   const unsigned long long need = (unsigned long long)(uint32_t)c.resting + 2ull * c.recs_left;
   unsigned long long w0 = 0;
   if (lane_id() == 0) w0 = atomicAdd(top, need);
@@ -461,8 +517,19 @@ constexpr uint32_t CW_BUY = 1u << 8, CW_MKT = 1u << 9, CW_CXL = 1u << 10;
 
 __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
   __shared__ RegLds lds[REG_WAVES];
+  __shared__ ColdArgs G;
+  static_assert(sizeof(ColdArgs) % 8 == 0 && sizeof(ColdArgs) <= 8 * 256, "ColdArgs copy");
+  {
+    const ColdArgs a{bk, bt};
+    if (threadIdx.x < sizeof(ColdArgs) / 8)
+      reinterpret_cast<unsigned long long*>(&G)[threadIdx.x] =
+          reinterpret_cast<const unsigned long long*>(&a)[threadIdx.x];
+    __syncthreads();
+  }
   const int lane = lane_id();
-  const uint32_t wv = threadIdx.x >> 6;
+  // wave index: readfirstlane tells the divergence analysis it is wave-uniform (threadIdx.x >> 6 is
+  // not recognised as such), so every per-symbol value and branch below is scalar
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t s = blockIdx.x * REG_WAVES + wv;
   if (s > bk.S) return;
 #ifdef ME_STAMPS
@@ -482,34 +549,28 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
     return;
   }
   const uint32_t L = bk.L;
-  Level* g_lv = bk.levels + (size_t)s * L;
-  uint8_t* g_tend = bk.tend + (size_t)s * L;
+  const Level* p_lv = bk.levels + (size_t)s * L;
+  const uint8_t* p_tend = bk.tend + (size_t)s * L;
   // one round trip: ladder rows, tail fills, symbol scalars, parked free chunks (no predicated
   // loads: row 1 of a 64-level ladder re-reads row 0 and is then discarded)
   const bool in1 = 64u + (uint32_t)lane < L;
   const uint32_t l1 = in1 ? 64u + (uint32_t)lane : (uint32_t)lane;
-  const Level a = g_lv[lane];
-  const Level b = g_lv[l1];
-  const uint32_t te0 = g_tend[lane];
-  const uint32_t te1 = g_tend[l1];
+  const Level a = p_lv[lane];
+  const Level b = p_lv[l1];
+  const uint32_t te0 = p_tend[lane];
+  const uint32_t te1 = p_tend[l1];
   const SymState st = bk.sym[s];
   const uint32_t fst = bk.fcache[(size_t)s * FSTK + lane];
   const uint32_t gsv = bk.gsym[s];
   RegCtx c;
-  c.chdr = bk.chdr;
-  c.owner = bk.owner;
-  c.cseq = bk.cseq;
-  c.cqty = bk.cqty;
-  c.loc = bk.loc;
-  c.chunk_top = bk.chunk_top;
-  c.err = bk.err;
-  c.scratch = bt.scratch;
+  c.chunks = vptr(bk.chunks);
+  c.loc = vptr(bk.loc);
+  c.scratch = vptr(bt.scratch);
+  c.G = &G;
   c.M = &lds[wv];
-  c.max_seq = bk.max_seq;
   c.nchunks = bk.nchunks;
-  c.L = L;
   c.s = s;
-  c.gs = rl32(gsv, 0);
+  c.gs = vreg(gsv);
 #ifdef ME_STAMPS
   for (int p = 0; p < PH_N; ++p) c.st[p] = 0;
   c.st_t = st_t0;
@@ -526,51 +587,61 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
   c.M->tot[64 + lane] = tb;
   c.occ.w0 = __ballot(a.total > 0);
   c.occ.w1 = __ballot(tb > 0);
-  c.cv.w0 = c.cv.w1 = c.cd.w0 = c.cd.w1 = 0ull;
-  c.base = rli64(st.base, 0);
+  c.cv.w0 = c.cv.w1 = 0ull;
+  c.base = (long long)vreg64((unsigned long long)st.base);
   c.bb = rli32(st.best_bid, 0);
   c.ba = rli32(st.best_ask, 0);
   if (c.ba > RL) c.ba = RL;
-  c.free_head = rl32(st.free_head, 0);
+  if (lane == 0) {
+    c.M->free_head = st.free_head;
+    c.M->bump_cur = 0;
+    c.M->bump_end = 0;
+  }
   c.nfs = min(rl32(st.nfree, 0), (uint32_t)FSTK);
   c.fstk = fst;
-  c.bump_cur = c.bump_end = 0;
   c.resting = (int)rl32(st.resting, 0);
   c.wptr = s * bt.slab;
   c.wend = c.wptr + bt.slab;
+  c.recs_left = hi - lo;
   STAMP_ADD(c, PH_PROLOGUE);
-  const long long Lw = (long long)L;
   for (uint32_t blk = lo; blk < hi; blk += 64) {
     // ---- 64 records in vector form (two dependent round trips: permutation, then the records)
     const uint32_t j = blk + (uint32_t)lane;
-    const bool v = j < hi;
-    const uint32_t oi = bt.perm[v ? j : hi - 1u];  // clamp: never branch around a load
-    const unsigned long long oseq_ = bt.seq[oi];
-    const long long opx_ = bt.px[oi];
-    const int oq_ = bt.qty[oi];
-    const uint32_t kd_ = bt.kind[oi];
-    const unsigned long long oseq = v ? oseq_ : 0ull;
-    const long long opx = v ? opx_ : 0ll;
-    const int oq = v ? oq_ : 0;
-    const uint32_t kd = v ? kd_ : 0u;
-    const uint32_t side = kd & 3u;
-    const bool market = (kd >> 2) & 1u, cancel = (kd >> 3) & 1u;
-    const bool buy = side == ME_SIDE_BUY;
-    const bool oow = opx < c.base || (unsigned long long)(opx - c.base) >= (unsigned long long)Lw;
-    uint32_t rj = ME_RJ_NONE;
-    if (!cancel) {
-      if (oq <= 0)
-        rj = ME_RJ_BAD_QTY;
-      else if (side != ME_SIDE_BUY && side != ME_SIDE_SELL)
-        rj = ME_RJ_BAD_SIDE;
-      else if (!market && oow)
-        rj = ME_RJ_OUT_OF_WINDOW;
-      else if (oseq == 0ull || oseq >= c.max_seq)
-        rj = ME_RJ_BAD_SEQ;
+    const uint32_t oi = ldsu(G.bt.perm)[j < hi ? j : hi - 1u];  // clamp: never branch around a load
+    const unsigned long long oseq_ = ldsu(G.bt.seq)[oi];
+    const long long opx_ = ldsu(G.bt.px)[oi];
+    const int oq_ = ldsu(G.bt.qty)[oi];
+    const uint32_t kd_ = ldsu(G.bt.kind)[oi];
+    const unsigned long long max_seq = ldsu(G.bk.max_seq);
+    const long long lbase = c.base;
+    // validation in vector form; only the packed control word and the reject code stay live
+    uint32_t cw, rj;
+    {
+      const bool v = j < hi;
+      const unsigned long long oseq = v ? oseq_ : 0ull;
+      const long long opx = v ? opx_ : 0ll;
+      const int oq = v ? oq_ : 0;
+      const uint32_t kd = v ? kd_ : 0u;
+      const uint32_t side = kd & 3u;
+      const bool market = (kd >> 2) & 1u, cancel = (kd >> 3) & 1u;
+      const bool buy = side == ME_SIDE_BUY;
+      const bool oow = opx < lbase || (unsigned long long)(opx - lbase) >= (unsigned long long)L;
+      rj = ME_RJ_NONE;
+      if (!cancel) {
+        if (oq <= 0)
+          rj = ME_RJ_BAD_QTY;
+        else if (side != ME_SIDE_BUY && side != ME_SIDE_SELL)
+          rj = ME_RJ_BAD_SIDE;
+        else if (!market && oow)
+          rj = ME_RJ_OUT_OF_WINDOW;
+        else if (oseq == 0ull || oseq >= max_seq)
+          rj = ME_RJ_BAD_SEQ;
+      }
+      const uint32_t lim = market ? (buy ? L - 1u : 0u) : (oow ? 0u : (uint32_t)(opx - lbase));
+      cw = lim | (buy ? CW_BUY : 0u) | (market ? CW_MKT : 0u) | (cancel ? CW_CXL : 0u);
+      if (!v) rj = 0xFFu;  // lanes past the run: no record
     }
-    const uint32_t lim = market ? (buy ? L - 1u : 0u) : (oow ? 0u : (uint32_t)(opx - c.base));
-    const uint32_t cw = lim | (buy ? CW_BUY : 0u) | (market ? CW_MKT : 0u) | (cancel ? CW_CXL : 0u);
-    unsigned long long work = __ballot(v && rj == ME_RJ_NONE);
+    unsigned long long work = __ballot(rj == ME_RJ_NONE);
     const uint32_t cnt = min(64u, hi - blk);
     uint32_t stop = cnt;  // records [0, stop) of the block get results
     uint32_t out_q = 0, out_n = 0, out_w = 0;
@@ -588,16 +659,15 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
       COUNT(c, CT_FAST);
       STAMP_ADD(c, PH_SWEEP);
       if (ctl & CW_CXL) {
-        outq = reg_cancel(c, (unsigned long long)rli64(opx, k));
+        outq = reg_cancel(c, (unsigned long long)rli64(opx_, k));
         STAMP_ADD(c, PH_CANCEL);
       } else {
-        if (c.wptr + (uint32_t)c.resting > c.wend &&
-            !reg_reserve_overflow(c, bt.scratch_top, bt.ovf_base, bt.scratch_cap)) {
+        if (c.wptr + (uint32_t)c.resting > c.wend && !reg_reserve_overflow(c)) {
           stop = (uint32_t)k;
           break;
         }
-        const unsigned long long seq = rl64(oseq, k);
-        const uint32_t q = (uint32_t)rli32(oq, k);
+        const unsigned long long seq = rl64(oseq_, k);
+        const uint32_t q = (uint32_t)rli32(oq_, k);
         const int lm = (int)(ctl & 0xFFu);
         const uint32_t w_in = c.wptr;
         uint32_t rem = q;
@@ -628,7 +698,11 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
       out_q = lane == k ? outq : out_q;
     }
     // ---- results of the block in vector form
-    if (v && (uint32_t)lane < stop) {
+    me_order_result* res = ldsu(G.bt.res);
+    uint32_t* fstart = ldsu(G.bt.fstart);
+    uint32_t* tile_sum = ldsu(G.bt.tile_sum);
+    if (rj != 0xFFu && (uint32_t)lane < stop) {
+      const bool market = (kd_ >> 2) & 1u, cancel = (kd_ >> 3) & 1u;
       me_order_result r;
       r.tape_offset = 0;
       r.pad[0] = r.pad[1] = 0;
@@ -636,7 +710,7 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
       r.reason = (uint8_t)rj;
       if (rj != ME_RJ_NONE) {
         r.filled_qty = 0;
-        r.remaining_qty = rj == ME_RJ_BAD_QTY ? 0 : oq;
+        r.remaining_qty = rj == ME_RJ_BAD_QTY ? 0 : oq_;
         r.status = ME_ST_REJECTED;
       } else if (cancel) {
         r.filled_qty = 0;
@@ -644,7 +718,7 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
         r.status = out_q ? ME_ST_CANCELED : ME_ST_REJECTED;
         r.reason = out_q ? ME_RJ_NONE : ME_RJ_UNKNOWN_ORDER;
       } else {
-        const int rem = oq - (int)out_q;
+        const int rem = oq_ - (int)out_q;
         r.filled_qty = (int)out_q;
         r.remaining_qty = rem;
         r.status = rem == 0 ? ME_ST_FILLED
@@ -652,28 +726,34 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
                  : out_q    ? ME_ST_PARTIALLY_FILLED
                             : ME_ST_NEW;
       }
-      bt.res[oi] = r;
-      bt.fstart[oi] = out_w;
-      if (out_n) atomicAdd(&bt.tile_sum[oi / TILE_TAPE], out_n);
+      res[oi] = r;
+      fstart[oi] = out_w;
+      if (out_n) atomicAdd(&tile_sum[oi / TILE_TAPE], out_n);
     }
     STAMP_ADD(c, PH_RESULT);
     if (stop < cnt) break;
   }
   // ---- write the symbol back
-  while (c.bump_cur < c.bump_end) reg_free(c, c.bump_cur++);  // unused reserved chunks
-  for (int row = 0; row < 2; ++row) {  // dirty cached heads (valid entry l holds the head of l)
-    unsigned long long d = row ? (c.cd.w1 & c.cv.w1) : (c.cd.w0 & c.cv.w0);
+  {  // unused reserved chunks
+    uint32_t cur = ldsu(c.M->bump_cur);
+    const uint32_t end = ldsu(c.M->bump_end);
+    while (cur < end) reg_free(c, cur++);
+  }
+  for (int row = 0; row < 2; ++row) {  // every valid cached head back to HBM (entry l holds the head of l)
+    unsigned long long d = row ? c.cv.w1 : c.cv.w0;
     while (d) {
       const int jj = __builtin_ctzll(d);
       d &= d - 1ull;
       const uint32_t cid = rl32(row ? c.hd.r1 : c.hd.r0, jj);
       const int e = row * 64 + jj;
       if (lane < ME_C) {
-        c.cqty[(size_t)cid * ME_C + lane] = c.M->cq[e][lane];
-        c.cseq[(size_t)cid * ME_C + lane] = c.M->cs[e][lane];
+        cq_at(c.chunks, (size_t)cid * ME_C + lane) = c.M->cq[e][lane];
+        cs_at(c.chunks, (size_t)cid * ME_C + lane) = c.M->cs[e][lane];
       }
     }
   }
+  Level* g_lv = ldsu(G.bk.levels) + (size_t)s * L;
+  uint8_t* g_tend = ldsu(G.bk.tend) + (size_t)s * L;
   Level o;
   o.total = c.M->tot[lane];
   o.head = c.hd.r0;
@@ -687,26 +767,29 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
     g_lv[64 + lane] = o;
     g_tend[64 + lane] = (uint8_t)c.te.r1;
   }
-  bk.fcache[(size_t)s * FSTK + lane] = c.fstk;
-  unsigned long long* g_occ = bk.occ + (size_t)s * bk.Lwords;  // for the host-side book dump
+  ldsu(G.bk.fcache)[(size_t)s * FSTK + lane] = c.fstk;
+  const uint32_t Lwords = ldsu(G.bk.Lwords);
+  unsigned long long* g_occ = ldsu(G.bk.occ) + (size_t)s * Lwords;  // for the host-side book dump
+  const uint32_t fh = ldsu(c.M->free_head);
   if (lane == 0) {
     g_occ[0] = c.occ.w0;
-    if (bk.Lwords > 1) g_occ[1] = c.occ.w1;
+    if (Lwords > 1) g_occ[1] = c.occ.w1;
     SymState so;
     so.base = c.base;
     so.best_bid = c.bb;
     so.best_ask = c.ba >= (int)L ? (int)L : c.ba;
-    so.free_head = c.free_head;
+    so.free_head = fh;
     so.resting = (uint32_t)c.resting;
     so.nfree = c.nfs;
     so.pad = 0;
-    bk.sym[s] = so;
+    ldsu(G.bk.sym)[s] = so;
   }
 #ifdef ME_STAMPS
   __builtin_amdgcn_s_waitcnt(0);
   STAMP_ADD(c, PH_EPILOGUE);
-  if (lane == 0 && bk.dbg)
-    for (int p = 0; p < PH_N; ++p) bk.dbg[(size_t)s * 24 + p] = c.st[p];
+  unsigned long long* dbg = ldsu(G.bk.dbg);
+  if (lane == 0 && dbg)
+    for (int p = 0; p < PH_N; ++p) dbg[(size_t)s * 24 + p] = c.st[p];
 #endif
 }
 
