@@ -272,55 +272,64 @@ __device__ __forceinline__ bool reg_fill_entry(RegCtx& c, int lvl, uint32_t ch) 
 }
 
 // ---- taking liquidity ----------------------------------------------------------------------
-// Consume up to `rem` from the FIFO of level lvl, oldest first, emitting one fill per maker slot
-// touched. Returns true if the level emptied. A slot is live iff its qty > 0.
-__device__ __forceinline__ bool reg_walk(RegCtx& c, int lvl, uint32_t& rem, unsigned long long taker) {
+// Consume up to `rem` from the chunk held by cache entry lvl (the head of level lvl), oldest slot
+// first, one fill per maker slot touched. Returns true if every slot of the chunk is consumed.
+// A slot is live iff its qty > 0.
+__device__ __forceinline__ bool reg_take_chunk(RegCtx& c, int lvl, uint32_t& rem, uint32_t& taken,
+                                               unsigned long long taker, long long price) {
   const int lane = lane_id();
   const bool act = lane < ME_C;
   const int sl = lane & (ME_C - 1);
+  COUNT(c, CT_WALK);
+  const int q_ = c.M->cq[lvl][sl];
+  const uint32_t uq = act ? (uint32_t)q_ : 0u;
+  const uint32_t inc = scan16_sat(uq);
+  const uint32_t ex = inc - uq;
+  uint32_t f = rem > ex ? rem - ex : 0u;
+  f = f < uq ? f : uq;
+  const bool fe = f != 0u;
+  const unsigned long long fm = __ballot(fe);
+  if (fe) {
+    me_fill F;
+    F.taker_seq = taker;
+    F.maker_seq = c.M->cs[lvl][sl];
+    F.price_q4 = price;
+    F.qty = (int)f;
+    F.symbol = c.gs;
+    // fills only ever come from lanes 0..15: mbcnt_lo alone ranks them
+    c.scratch[c.wptr + (uint32_t)__builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u)] = F;
+    c.M->cq[lvl][sl] = (int)(uq - f);
+  }
+  c.wptr += (uint32_t)__popcll(fm);
+  c.resting -= __popcll(__ballot(fe && f == uq));  // makers filled completely leave the book
+  const uint32_t live = rl32(inc, 15);
+  const uint32_t t = rem < live ? rem : live;
+  rem -= t;
+  taken += t;
+  return __ballot(act && uq > f) == 0ull;  // no live slot left
+}
+
+// Taker against level lvl. The common case is straight-line: the cached head chunk keeps live
+// slots once the taker is done. Returns true if the level emptied.
+__device__ __forceinline__ bool reg_walk(RegCtx& c, int lvl, uint32_t& rem, unsigned long long taker) {
+  const int lane = lane_id();
   const long long price = c.base + lvl;
-  const uint32_t head = c.hd.get(lvl);
-  const uint32_t tail = c.tl.get(lvl);
-  uint32_t ch = head;
+  uint32_t ch = c.hd.get(lvl);
+  if (!c.cv.bit(lvl)) {
+    COUNT(c, CT_MISS);
+    if (!reg_fill_entry(c, lvl, ch)) return false;
+    c.cv.set(lvl);
+  }
   uint32_t taken = 0;
+  if (!reg_take_chunk(c, lvl, rem, taken, taker, price)) {
+    tot_add(c, lvl, -(long long)taken);
+    return false;
+  }
+  // the head chunk is exhausted: free it and continue down the FIFO (each next chunk is a miss)
+  const uint32_t tail = c.tl.get(lvl);
   for (;;) {
-    if (!c.cv.bit(lvl)) {
-      COUNT(c, CT_MISS);
-      STAMP_ADD(c, PH_WALK);
-      if (!reg_fill_entry(c, lvl, ch)) return false;
-      c.cv.set(lvl);
-      STAMP_ADD(c, WK_GET);
-    }
-    COUNT(c, CT_WALK);
-    const int q_ = c.M->cq[lvl][sl];
-    const uint32_t nx = c.M->cnext[lvl];
-    const uint32_t uq = act ? (uint32_t)q_ : 0u;
-    const uint32_t inc = scan16_sat(uq);
-    const uint32_t ex = inc - uq;
-    uint32_t f = rem > ex ? rem - ex : 0u;
-    f = f < uq ? f : uq;
-    const bool fe = f != 0u;
-    const unsigned long long fm = __ballot(fe);
-    if (fe) {
-      me_fill F;
-      F.taker_seq = taker;
-      F.maker_seq = c.M->cs[lvl][sl];
-      F.price_q4 = price;
-      F.qty = (int)f;
-      F.symbol = c.gs;
-      // fills only ever come from lanes 0..15: mbcnt_lo alone ranks them
-      c.scratch[c.wptr + (uint32_t)__builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u)] = F;
-      c.M->cq[lvl][sl] = (int)(uq - f);
-    }
-    c.wptr += (uint32_t)__popcll(fm);
-    c.resting -= __popcll(__ballot(fe && f == uq));  // makers filled completely leave the book
-    const uint32_t live = rl32(inc, 15);
-    const uint32_t t = rem < live ? rem : live;
-    rem -= t;
-    taken += t;
-    if (__ballot(act && uq > f)) break;  // a live slot remains: the taker is done
-    // chunk exhausted: its HBM copy must read all-zero before the chunk is reused
-    if (act) cq_at(c.chunks, (size_t)ch * ME_C + sl) = 0;
+    const uint32_t nx = rl32(c.M->cnext[lvl], 0);
+    if (lane < ME_C) c.chunks[ch].qty[lane] = 0;  // a freed chunk must read all-zero in HBM
     c.cv.clr(lvl);
     reg_free(c, ch);
     if (ch == tail) {
@@ -330,80 +339,88 @@ __device__ __forceinline__ bool reg_walk(RegCtx& c, int lvl, uint32_t& rem, unsi
       tot_add(c, lvl, -(long long)taken);
       return true;
     }
-    ch = rl32(nx, 0);
+    ch = nx;
     if (rem == 0u) break;
+    COUNT(c, CT_MISS);
+    if (!reg_fill_entry(c, lvl, ch)) return false;
+    c.cv.set(lvl);
+    if (!reg_take_chunk(c, lvl, rem, taken, taker, price)) break;
   }
   tot_add(c, lvl, -(long long)taken);
-  if (ch != head) {
-    c.hd.put(lvl, ch);
-    if (lane == 0 && ch < c.nchunks) c.chunks[ch].hdr.prev = NIL;  // new FIFO head
-  }
+  c.hd.put(lvl, ch);
+  if (lane == 0 && ch < c.nchunks) c.chunks[ch].hdr.prev = NIL;  // new FIFO head
   return false;
 }
 
 // ---- resting -------------------------------------------------------------------------------
-// Append (seq, qty) at the tail of level lvl. A tail that is the cached head is written on chip.
+// Append (seq, qty) at the tail of level lvl. Common case first: a free slot in the tail chunk
+// (written on chip when the tail is the cached head). The new-chunk path is out of line.
+__device__ __forceinline__ bool reg_rest_new_chunk(RegCtx& c, int lvl, unsigned long long seq, uint32_t qty,
+                                                   uint32_t tl) {
+  const int lane = lane_id();
+  const uint32_t ch = reg_alloc(c);
+  if (ch == NIL) return false;
+  if (lane == 0) {
+    ChunkHdr h;
+    h.next = NIL;
+    h.prev = tl;
+    h.level = (uint32_t)lvl;
+    h.owner = c.s;
+    c.chunks[ch].hdr = h;
+    c.loc[seq] = ch * ME_C;
+  }
+  if (tl == NIL) {  // empty level: the new chunk is its head, installed in the cache
+    c.hd.put(lvl, ch);
+    if (lane < ME_C) c.M->cq[lvl][lane] = lane == 0 ? (int)qty : 0;
+    if (lane == 0) {
+      c.M->cs[lvl][0] = seq;
+      c.M->cnext[lvl] = NIL;
+    }
+    c.cv.set(lvl);
+    c.occ.set(lvl);
+  } else {
+    const bool tl_cached = c.cv.bit(lvl) && c.hd.get(lvl) == tl;
+    if (lane == 0) {
+      if (tl < c.nchunks) c.chunks[tl].hdr.next = ch;
+      if (tl_cached) c.M->cnext[lvl] = ch;
+      c.chunks[ch].qty[0] = (int)qty;
+      c.chunks[ch].seq[0] = seq;
+    }
+  }
+  c.tl.put(lvl, ch);
+  c.te.put(lvl, 1u);
+  return true;
+}
+
 __device__ __forceinline__ bool reg_rest(RegCtx& c, int lvl, unsigned long long seq, uint32_t qty, bool buy) {
   const int lane = lane_id();
   const uint32_t tl = c.tl.get(lvl);
   const uint32_t te = c.te.get(lvl);
-  uint32_t ch, slot;
-  bool in_cache;
-  if (tl == NIL || te >= (uint32_t)ME_C) {
-    ch = reg_alloc(c);
-    if (ch == NIL) return false;
-    slot = 0;
-    if (lane == 0) {
-      ChunkHdr h;
-      h.next = NIL;
-      h.prev = tl;
-      h.level = (uint32_t)lvl;
-      h.owner = c.s;
-      c.chunks[ch].hdr = h;
-    }
-    if (tl == NIL) {  // empty level: the new chunk is its head, installed in the cache zeroed
-      c.hd.put(lvl, ch);
-      if (lane < ME_C) c.M->cq[lvl][lane] = 0;
-      if (lane == 0) c.M->cnext[lvl] = NIL;
-      c.cv.set(lvl);
-      in_cache = true;
-    } else {
-      const bool tl_cached = c.cv.bit(lvl) && c.hd.get(lvl) == tl;
-      if (lane == 0) {
-        if (tl < c.nchunks) c.chunks[tl].hdr.next = ch;
-        if (tl_cached) c.M->cnext[lvl] = ch;
-      }
-      in_cache = false;
-    }
-    c.tl.put(lvl, ch);
-  } else {
+  if (tl != NIL && te < (uint32_t)ME_C) {
     if (tl >= c.nchunks) {
       reg_err(c, ERR_INCONSISTENT);
       return false;
     }
-    ch = tl;
-    slot = te;
-    in_cache = c.cv.bit(lvl) && c.hd.get(lvl) == tl;
-  }
-  const uint32_t g = ch * ME_C + slot;
-  if (lane == 0) {
-    if (in_cache) {
-      c.M->cq[lvl][slot] = (int)qty;
-      c.M->cs[lvl][slot] = seq;
-    } else {
-      cq_at(c.chunks, g) = (int)qty;
-      cs_at(c.chunks, g) = seq;
+    const bool in_cache = c.cv.bit(lvl) && c.hd.get(lvl) == tl;
+    if (lane == 0) {
+      if (in_cache) {
+        c.M->cq[lvl][te] = (int)qty;
+        c.M->cs[lvl][te] = seq;
+      } else {
+        c.chunks[tl].qty[te] = (int)qty;
+        c.chunks[tl].seq[te] = seq;
+      }
+      c.loc[seq] = tl * ME_C + te;
     }
-    c.loc[seq] = g;
+    c.te.put(lvl, te + 1u);
+  } else if (!reg_rest_new_chunk(c, lvl, seq, qty, tl)) {
+    return false;
   }
   tot_add(c, lvl, (long long)qty);
-  c.te.put(lvl, slot + 1);
-  c.occ.set(lvl);
-  if (buy) {
-    if (lvl > c.bb) c.bb = lvl;
-  } else {
-    if (lvl < c.ba) c.ba = lvl;
-  }
+  if (buy)
+    c.bb = lvl > c.bb ? lvl : c.bb;
+  else
+    c.ba = lvl < c.ba ? lvl : c.ba;
   c.resting += 1;
   return true;
 }
