@@ -46,6 +46,7 @@ struct RegLds {
   int cq[RL][ME_C];
   unsigned long long cs[RL][ME_C];
   long long tot[RL];
+  long long tdummy[64];  // tot_add: the slots of lanes 1..63
   uint32_t cnext[RL];  // chunks[head].hdr.next of the cached head (kept in step with HBM)
   uint32_t free_head;  // overflow free list in HBM (hdr.next links), NIL if empty
   uint32_t bump_cur, bump_end;  // chunk ids reserved from the global bump allocator
@@ -111,6 +112,17 @@ struct ColdArgs {
   BatchDev bt;
 };
 
+// Global-address-space (1) pointers: an opaque round trip (vreg64, ldsu) would otherwise leave a
+// generic pointer, and vector memory ops on it would be flat_* (counted in both vmcnt and lgkmcnt)
+// instead of global_*.
+#if defined(__HIP_DEVICE_COMPILE__)
+template <class T>
+using gptr = T __attribute__((address_space(1)))*;
+#else  // host pass of the single-source compile: the kernel body is never run there
+template <class T>
+using gptr = T*;
+#endif
+
 // A wave-uniform value read from LDS at the point of use. A relaxed atomic load is never hoisted out
 // of a loop (a plain load would be, pinning the value in SGPRs for the whole loop) and, unlike a
 // volatile one, keeps its LDS address space (ds_read, not flat); readfirstlane makes it scalar.
@@ -131,6 +143,12 @@ __device__ __forceinline__ T ldsu(const T& f) {
   }
 }
 
+// A pointer launch argument read from LDS, as a global-address-space pointer (global_* ops).
+template <class T>
+__device__ __forceinline__ gptr<T> ldsg(T* const& f) {
+  return (gptr<T>)ldsu(reinterpret_cast<const unsigned long long&>(f));
+}
+
 // Store a wave-uniform 32-bit value into the wave's LDS (lane 0; read back with ldsu).
 __device__ __forceinline__ void ldsw(uint32_t& f, uint32_t v) {
   if (lane_id() == 0) __hip_atomic_store(&f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -149,14 +167,14 @@ __device__ __forceinline__ unsigned long long vreg64(unsigned long long x) {
   return ((unsigned long long)hi << 32) | lo;
 }
 template <class T>
-__device__ __forceinline__ T* vptr(T* p) {
-  return (T*)vreg64((unsigned long long)p);
+__device__ __forceinline__ gptr<T> vptr(T* p) {
+  return (gptr<T>)vreg64((unsigned long long)p);
 }
 
 struct RegCtx {
-  Chunk* chunks;       // VGPR
-  uint32_t* loc;       // VGPR
-  me_fill* scratch;    // VGPR
+  gptr<Chunk> chunks;    // VGPR
+  gptr<uint32_t> loc;    // VGPR
+  gptr<me_fill> scratch; // VGPR
   RegLds* M;
   const ColdArgs* G;
   long long base;      // VGPR (price of level 0: vector uses only)
@@ -178,7 +196,7 @@ struct RegCtx {
 };
 
 __device__ __forceinline__ void reg_err(const RegCtx& c, uint32_t bits) {
-  if (lane_id() == 0) atomicOr(ldsu(c.G->bk.err), bits);
+  if (lane_id() == 0) atomicOr(ldsg(c.G->bk.err), bits);
 }
 
 // Inclusive scan of a 16-lane row (each DPP row scans on its own), saturating at 2^32 - 1.
@@ -190,8 +208,12 @@ __device__ __forceinline__ uint32_t scan16_sat(uint32_t x) {
   return x;
 }
 
+// Level totals only ever change by adds. Every lane issues the atomic — lane 0 into the level's
+// total, lanes 1..63 into their own dummy slot — so a one-lane update needs no exec-mask dance.
 __device__ __forceinline__ void tot_add(RegCtx& c, int lvl, long long d) {
-  if (lane_id() == 0) __hip_atomic_fetch_add(&c.M->tot[lvl], d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  const int lane = lane_id();
+  long long* p = lane == 0 ? &c.M->tot[lvl] : &c.M->tdummy[lane];
+  __hip_atomic_fetch_add(p, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 // ---- chunk pool ----------------------------------------------------------------------------
@@ -225,7 +247,7 @@ __device__ __forceinline__ uint32_t reg_alloc_slow(RegCtx& c) {
     // each record needs at most one new chunk: never reserve more than the records left
     const uint32_t blk = min(16u, max(c.recs_left, 1u));
     uint32_t got = 0;
-    if (lane_id() == 0) got = atomicAdd(ldsu(c.G->bk.chunk_top), blk);
+    if (lane_id() == 0) got = atomicAdd(ldsg(c.G->bk.chunk_top), blk);
     got = rl32(got, 0);
     if (got >= c.nchunks) {
       reg_err(c, ERR_CHUNK_OOM);
@@ -256,10 +278,9 @@ __device__ __forceinline__ bool reg_fill_entry(RegCtx& c, int lvl, uint32_t ch) 
   }
   const int lane = lane_id();
   const int sl = lane & (ME_C - 1);
-  const size_t g = (size_t)ch * ME_C + sl;
   const uint32_t nx = c.chunks[ch].hdr.next;
-  const int qv = cq_at(c.chunks, g);
-  const unsigned long long sv = cs_at(c.chunks, g);
+  const int qv = c.chunks[ch].qty[sl];
+  const unsigned long long sv = c.chunks[ch].seq[sl];
   // Resolve the loads on every path here (vmcnt(0)): a load left pending behind the lane-masked
   // LDS writes below would make the compiler wait for it (and all later stores) in the hit path.
   __builtin_amdgcn_s_waitcnt(VMCNT0);
@@ -441,8 +462,8 @@ __device__ __forceinline__ uint32_t reg_cancel(RegCtx& c, unsigned long long tgt
   // one round trip: owner, header, the chunk's quantities and the target seq
   const uint32_t own = rl32(c.chunks[ch].hdr.owner, 0);
   const ChunkHdr hdr = c.chunks[ch].hdr;
-  const int qg = cq_at(c.chunks, (size_t)ch * ME_C + (lane & (ME_C - 1)));
-  unsigned long long sq = rl64(cs_at(c.chunks, g), 0);
+  const int qg = c.chunks[ch].qty[lane & (ME_C - 1)];
+  unsigned long long sq = rl64(c.chunks[ch].seq[slot], 0);
   __builtin_amdgcn_s_waitcnt(VMCNT0);  // resolved on every path (see reg_fill_entry)
   int qv = act ? qg : 0;
   if (own != c.s) return 0;  // another symbol's order: never touch its book
@@ -465,7 +486,7 @@ __device__ __forceinline__ uint32_t reg_cancel(RegCtx& c, unsigned long long tgt
     if (in_cache)
       c.M->cq[lvl][slot] = 0;
     else
-      cq_at(c.chunks, g) = 0;
+      c.chunks[ch].qty[slot] = 0;
   }
   tot_add(c, lvl, -(long long)q);
   if (live_after == 0u) {
@@ -474,7 +495,7 @@ __device__ __forceinline__ uint32_t reg_cancel(RegCtx& c, unsigned long long tgt
       return (uint32_t)q;
     }
     if (in_cache) {  // the chunk leaves the cache; its HBM copy must read all-zero
-      if (act) cq_at(c.chunks, (size_t)ch * ME_C + lane) = 0;
+      if (act) c.chunks[ch].qty[lane] = 0;
       c.cv.clr(lvl);
     }
     const uint32_t nxt = rl32(hdr.next, 0), prv = rl32(hdr.prev, 0);
@@ -513,7 +534,7 @@ __device__ __forceinline__ uint32_t reg_cancel(RegCtx& c, unsigned long long tgt
 // reserve the batch bound of everything left (resting + 2 * records left) in the
 // shared overflow region once; after that no further check can fail.
 __device__ __forceinline__ bool reg_reserve_overflow(RegCtx& c) {
-  unsigned long long* top = ldsu(c.G->bt.scratch_top);
+  unsigned long long* top = ldsg(c.G->bt.scratch_top);
   const unsigned long long base = ldsu(c.G->bt.ovf_base), cap = ldsu(c.G->bt.scratch_cap);
   const unsigned long long need = (unsigned long long)(uint32_t)c.resting + 2ull * c.recs_left;
   unsigned long long w0 = 0;
@@ -624,11 +645,11 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
   for (uint32_t blk = lo; blk < hi; blk += 64) {
     // ---- 64 records in vector form (two dependent round trips: permutation, then the records)
     const uint32_t j = blk + (uint32_t)lane;
-    const uint32_t oi = ldsu(G.bt.perm)[j < hi ? j : hi - 1u];  // clamp: never branch around a load
-    const unsigned long long oseq_ = ldsu(G.bt.seq)[oi];
-    const long long opx_ = ldsu(G.bt.px)[oi];
-    const int oq_ = ldsu(G.bt.qty)[oi];
-    const uint32_t kd_ = ldsu(G.bt.kind)[oi];
+    const uint32_t oi = ldsg(G.bt.perm)[j < hi ? j : hi - 1u];  // clamp: never branch around a load
+    const unsigned long long oseq_ = ldsg(G.bt.seq)[oi];
+    const long long opx_ = ldsg(G.bt.px)[oi];
+    const int oq_ = ldsg(G.bt.qty)[oi];
+    const uint32_t kd_ = ldsg(G.bt.kind)[oi];
     const unsigned long long max_seq = ldsu(G.bk.max_seq);
     const long long lbase = c.base;
     // validation in vector form; only the packed control word and the reject code stay live
@@ -715,9 +736,9 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
       out_q = lane == k ? outq : out_q;
     }
     // ---- results of the block in vector form
-    me_order_result* res = ldsu(G.bt.res);
-    uint32_t* fstart = ldsu(G.bt.fstart);
-    uint32_t* tile_sum = ldsu(G.bt.tile_sum);
+    me_order_result* res = ldsg(G.bt.res);
+    uint32_t* fstart = ldsg(G.bt.fstart);
+    uint32_t* tile_sum = ldsg(G.bt.tile_sum);
     if (rj != 0xFFu && (uint32_t)lane < stop) {
       const bool market = (kd_ >> 2) & 1u, cancel = (kd_ >> 3) & 1u;
       me_order_result r;
@@ -764,13 +785,13 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
       const uint32_t cid = rl32(row ? c.hd.r1 : c.hd.r0, jj);
       const int e = row * 64 + jj;
       if (lane < ME_C) {
-        cq_at(c.chunks, (size_t)cid * ME_C + lane) = c.M->cq[e][lane];
-        cs_at(c.chunks, (size_t)cid * ME_C + lane) = c.M->cs[e][lane];
+        c.chunks[cid].qty[lane] = c.M->cq[e][lane];
+        c.chunks[cid].seq[lane] = c.M->cs[e][lane];
       }
     }
   }
-  Level* g_lv = ldsu(G.bk.levels) + (size_t)s * L;
-  uint8_t* g_tend = ldsu(G.bk.tend) + (size_t)s * L;
+  Level* g_lv = ldsg(G.bk.levels) + (size_t)s * L;
+  uint8_t* g_tend = ldsg(G.bk.tend) + (size_t)s * L;
   Level o;
   o.total = c.M->tot[lane];
   o.head = c.hd.r0;
@@ -784,9 +805,9 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
     g_lv[64 + lane] = o;
     g_tend[64 + lane] = (uint8_t)c.te.r1;
   }
-  ldsu(G.bk.fcache)[(size_t)s * FSTK + lane] = c.fstk;
+  ldsg(G.bk.fcache)[(size_t)s * FSTK + lane] = c.fstk;
   const uint32_t Lwords = ldsu(G.bk.Lwords);
-  unsigned long long* g_occ = ldsu(G.bk.occ) + (size_t)s * Lwords;  // for the host-side book dump
+  unsigned long long* g_occ = ldsg(G.bk.occ) + (size_t)s * Lwords;  // for the host-side book dump
   const uint32_t fh = ldsu(c.M->free_head);
   if (lane == 0) {
     g_occ[0] = c.occ.w0;
@@ -799,12 +820,12 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
     so.resting = (uint32_t)c.resting;
     so.nfree = c.nfs;
     so.pad = 0;
-    ldsu(G.bk.sym)[s] = so;
+    ldsg(G.bk.sym)[s] = so;
   }
 #ifdef ME_STAMPS
   __builtin_amdgcn_s_waitcnt(0);
   STAMP_ADD(c, PH_EPILOGUE);
-  unsigned long long* dbg = ldsu(G.bk.dbg);
+  unsigned long long* dbg = ldsg(G.bk.dbg);
   if (lane == 0 && dbg)
     for (int p = 0; p < PH_N; ++p) dbg[(size_t)s * 24 + p] = c.st[p];
 #endif
