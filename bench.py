@@ -46,6 +46,11 @@ def parse():
     ap.add_argument("--timing-every", type=int, default=8,
                     help="HIP events on every k-th match launch of the timed loop (each timed launch costs "
                          "the stream a few us; 1 = every launch, 0 = off)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (RCCL, one rank per GPU: the real run); gloo only to rehearse N>1 on one GPU")
+    ap.add_argument("--gather-steps", type=int, default=10,
+                    help="N>1: batches run after the timed loop with the RCCL tape/result gather to rank 0 "
+                         "(reported beside value, never in it)")
     ap.add_argument("--traffic-from", default=None,
                     help="JSON {bytes_per_launch: ...} from tools/pmc_traffic.py for roofline.traffic")
     return ap.parse_args()
@@ -60,8 +65,13 @@ def dist_setup(args):
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "gloo":  # rehearsal of the N>1 path with ranks sharing one GPU
+            local = local % max(torch.cuda.device_count(), 1)
+            torch.cuda.set_device(local)
+            dist.init_process_group("gloo")
+        else:  # one rank per GPU over RCCL
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     return world, rank, local
 
 
@@ -82,27 +92,30 @@ def allreduce(v, world, op, local):
     import torch
     import torch.distributed as dist
 
-    t = torch.tensor([v], dtype=torch.float64, device=f"cuda:{local}")
+    dev = "cpu" if dist.get_backend() == "gloo" else f"cuda:{local}"
+    t = torch.tensor([v], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=op)
     return float(t.item())
 
 
 def build_rank_batches(args, world, rank, nbatches):
-    """Global stream, hash-sharded; this rank's batches with local symbol ids."""
+    """Global stream, hash-sharded; this rank's batches with local symbol ids (and, per batch, the
+    positions of its records in the global batch)."""
     S = args.symbols_per_gpu * world
     sc = me.preset(2, num_symbols=S, batch=args.batch_per_gpu * world)
     st = me.Stream(sc)
     base = st.base_prices()
     shard, local, members = me.shard_table(S, world)
     ids = members[rank]
-    out = []
+    out, pos = [], []
     for _ in range(nbatches):
         b = st.next(sc.batch)
         sel = np.nonzero(shard[b.symbol] == rank)[0]
         lb = b.take(sel)
         lb.symbol = np.ascontiguousarray(local[lb.symbol], dtype=np.uint32)
         out.append(lb)
-    return sc, base[ids], ids, out, sc.batch * nbatches
+        pos.append(sel)
+    return sc, base[ids], ids, out, pos, sc.batch * nbatches
 
 
 def cpu_baseline(args):
@@ -132,11 +145,14 @@ def main():
     import torch
 
     nb = args.warmup + args.steps
-    sc, base, ids, batches, global_orders = build_rank_batches(args, world, rank, nb + (0 if args.no_e2e else 10))
-    e2e_batches = batches[nb:]
+    n_gather = args.gather_steps if world > 1 else 0
+    n_e2e = 0 if args.no_e2e else 10
+    sc, base, ids, batches, positions, global_orders = build_rank_batches(args, world, rank, nb + n_gather + n_e2e)
+    gather_batches, gather_pos = batches[nb:nb + n_gather], positions[nb:nb + n_gather]
+    e2e_batches = batches[nb + n_gather:]
     batches = batches[:nb]
-    total_local = sum(len(b) for b in batches)
-    eng = me.Engine(len(ids), sc.levels, base, max_batch=max(len(b) for b in batches) + 1,
+    total_local = sum(len(b) for b in batches + gather_batches + e2e_batches)
+    eng = me.Engine(len(ids), sc.levels, base, max_batch=max(len(b) for b in batches + gather_batches + e2e_batches) + 1,
                     max_resting=total_local // 3 + 65536, max_seq=global_orders + 16, device=local,
                     symbol_ids=ids)
     dbs = [eng.upload(b) for b in batches]
@@ -172,6 +188,34 @@ def main():
     traffic = None
     if args.traffic_from and os.path.exists(args.traffic_from):
         traffic = json.load(open(args.traffic_from)).get("bytes_per_launch")
+
+    # N > 1: the persistence path — every batch's tape and results gathered to rank 0 over RCCL
+    # (matching_engine_amd/gather.py), timed separately; informational, never part of value
+    rccl = None
+    if gather_batches:
+        from matching_engine_amd.gather import EngineGather
+
+        dev = torch.device("cuda", local)
+        gat = EngineGather(eng, dev, max(len(b) for b in gather_batches))
+        gdbs = [eng.upload(b) for b in gather_batches]
+        gpos = [torch.from_numpy(p.astype(np.int64)).to(dev) for p in gather_pos]
+        barrier_sync(world, local)
+        tg0 = time.perf_counter()
+        gfills = 0
+        for db, p in zip(gdbs, gpos):
+            eng.submit_device(db)
+            tape, _ = gat.gather(db.n, p, sc.batch)
+            if tape is not None:
+                gfills += len(tape)
+        barrier_sync(world, local)
+        tg = allreduce(time.perf_counter() - tg0, world, MAX, local)
+        for db in gdbs:
+            db.free()
+        rccl = {"backend": tdist.get_backend(), "steps": len(gather_batches), "ms_per_step": tg / len(gather_batches) * 1e3,
+                "orders_per_s_incl_gather": sc.batch * len(gather_batches) / tg,
+                "tape_bytes_per_step_to_root": 32.0 * gfills / len(gather_batches),
+                "what": "submit + device tape/result copy + RCCL all_gather(sizes) + gather(tape, results) to "
+                        "rank 0 + stable merge by taker seq on rank 0's GPU + D2H of the merged tape"}
 
     # PCIe-inclusive host path (me_submit_batch: H2D + pipeline + D2H of results and tape), informational
     e2e = None
@@ -213,6 +257,7 @@ def main():
             "device_ms_per_step": tm["pipeline_ms"],
             "host_enqueue_ms_per_step_rank0": t_enq / args.steps * 1e3,
             "e2e_host_path_orders_per_s_rank0": e2e,
+            "rccl_tape_gather": rccl,
             "roofline": {
                 "bound": "hbm",
                 "achieved": achieved,

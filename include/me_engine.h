@@ -167,6 +167,10 @@ int me_fetch_outputs(me_engine* e, me_fill* out_fills, size_t fills_cap, size_t*
 /* Device-to-device copy of the last batch's tape into dst (HBM), on the engine stream;
  * *n_fills is the synchronous tape length. */
 int me_copy_tape_device(me_engine* e, void* dst, size_t cap_fills, size_t* n_fills);
+/* Device-to-device copy of the last batch's n_results per-record results (batch order) into dst
+ * (HBM), on the engine stream. With me_copy_tape_device: the per-GPU payload of the RCCL gather to
+ * the persistence root (matching_engine_amd/gather.py). */
+int me_copy_results_device(me_engine* e, void* dst, size_t n_results);
 
 /* Device memory helpers so a C/Python caller can keep batches resident without torch. */
 int me_device_alloc(me_engine* e, size_t bytes, void** dptr);

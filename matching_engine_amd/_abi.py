@@ -103,6 +103,7 @@ PROTOTYPES = {
     "me_sync": (C.c_int, [_P]),
     "me_fetch_outputs": (C.c_int, [_P, _P, _SZ, C.POINTER(_SZ), _P, _SZ]),
     "me_copy_tape_device": (C.c_int, [_P, _P, _SZ, C.POINTER(_SZ)]),
+    "me_copy_results_device": (C.c_int, [_P, _P, _SZ]),
     "me_device_alloc": (C.c_int, [_P, _SZ, C.POINTER(_P)]),
     "me_device_free": (C.c_int, [_P, _P]),
     "me_memcpy_h2d": (C.c_int, [_P, _P, _P, _SZ]),

@@ -522,6 +522,18 @@ extern "C" int me_copy_tape_device(me_engine* e, void* dst, size_t cap_fills, si
   return ME_OK;
 }
 
+extern "C" int me_copy_results_device(me_engine* e, void* dst, size_t n_results) {
+  if (!e) return ME_E_INVALID;
+  if (e->failed) return ME_E_STATE;
+  if (n_results > e->last_n) return e->fail(ME_E_INVALID, "n_results exceeds last batch size");
+  if (n_results && !dst) return e->fail(ME_E_INVALID, "null destination");
+  HIP_TRY(hipSetDevice(e->dev), "hipSetDevice");
+  if (n_results)
+    HIP_TRY(hipMemcpyAsync(dst, e->d_res, n_results * sizeof(me_order_result), hipMemcpyDeviceToDevice, e->stream),
+            "D2D results");
+  return ME_OK;
+}
+
 extern "C" int me_device_alloc(me_engine* e, size_t bytes, void** dptr) {
   if (!e || !dptr) return ME_E_INVALID;
   HIP_TRY(hipSetDevice(e->dev), "hipSetDevice");

@@ -184,6 +184,16 @@ class Engine:
         _check(self.lib, self.h, self.lib.me_fetch_outputs(self.h, ptr(fills), nf.value, C.byref(nf), None, 0))
         return res, fills
 
+    def copy_tape_device(self, dst_ptr: int, cap_fills: int) -> int:
+        """Last batch's tape -> device buffer at dst_ptr (engine stream); returns its length."""
+        nf = C.c_size_t(0)
+        _check(self.lib, self.h, self.lib.me_copy_tape_device(self.h, dst_ptr, cap_fills, C.byref(nf)))
+        return nf.value
+
+    def copy_results_device(self, dst_ptr: int, n: int):
+        """Last batch's n per-record results -> device buffer at dst_ptr (engine stream)."""
+        _check(self.lib, self.h, self.lib.me_copy_results_device(self.h, dst_ptr, n))
+
     def set_stream(self, stream_handle: int | None):
         _check(self.lib, self.h, self.lib.me_set_stream(self.h, stream_handle))
 

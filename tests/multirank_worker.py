@@ -4,9 +4,14 @@ Each rank owns the symbols splitmix64(symbol) % world == rank, runs its shard of
 stream through a per-shard book, and the per-shard tapes/results are gathered to rank 0
 (torch.distributed, gloo) and merged; rank 0 compares with ONE book over the whole stream.
 
-env: RANK, WORLD_SIZE, MASTER_ADDR, MASTER_PORT; argv: ENGINE(oracle|gpu) OUT_JSON
-  oracle: the per-shard book is the CPU oracle (CPU test of the split/gather/merge host logic)
-  gpu:    the per-shard book is the HIP engine on cuda:0 (all ranks share the box's one GPU)
+env: RANK, WORLD_SIZE, MASTER_ADDR, MASTER_PORT; argv: ENGINE(oracle|gpu|gather|gpu_gather) OUT_JSON
+  oracle:     the per-shard book is the CPU oracle (CPU test of the split/gather/merge host logic)
+  gpu:        the per-shard book is the HIP engine on cuda:0 (all ranks share the box's one GPU)
+  gather:     oracle shards, outputs moved by matching_engine_amd.gather.gather_batch (the RCCL
+              tape/result gather) over gloo with CPU tensors
+  gpu_gather: HIP engine shards, outputs staged device-to-device (EngineGather) and gathered with
+              gather_batch (gloo stages the device tensors through the host; one GPU cannot host
+              two RCCL ranks)
 """
 import json
 import os
@@ -35,10 +40,17 @@ def main():
     plan = ShardPlan(S, world)
     ids = plan.members[rank]
     max_seq = 1 << 20
-    if engine_kind == "gpu":
+    gath = None
+    if engine_kind in ("gpu", "gpu_gather"):
         book = me.Engine(len(ids), sc.levels, base[ids], max_batch=sc.batch, max_resting=1 << 16, max_seq=max_seq,
                          symbol_ids=ids)
         submit = book.submit_batch
+        if engine_kind == "gpu_gather":
+            import torch
+
+            from matching_engine_amd.gather import EngineGather
+
+            gath = EngineGather(book, torch.device("cuda", 0), sc.batch)
     else:
         book = OracleBook(len(ids), sc.levels, base[ids], max_seq, symbol_ids=ids)
         submit = book.submit
@@ -52,20 +64,32 @@ def main():
             b.symbol[::997] = S + 5
         lb, pos = plan.split(b)[rank]
         r, f = submit(lb)
-        got = [None] * world
-        dist.all_gather_object(got, (r, pos, f))
+        if engine_kind in ("gather", "gpu_gather"):
+            import torch
+
+            from matching_engine_amd.gather import gather_batch
+
+            post = torch.from_numpy(pos.astype(np.int64))
+            if gath is not None:  # device staging of the engine's own outputs
+                tape, res = gath.gather(len(lb), post, len(b))
+            else:
+                tape, res = gather_batch(torch.from_numpy(f.view(np.uint8).copy()), len(f),
+                                         torch.from_numpy(r.view(np.uint8).copy()), post, len(lb), len(b))
+        else:
+            got = [None] * world
+            dist.all_gather_object(got, (r, pos, f))
+            if rank == 0:
+                tape = merge_tapes([g[2] for g in got])
+                res = merge_results(len(b), [(g[0], g[1]) for g in got])
         if rank == 0:
-            tape = merge_tapes([g[2] for g in got])
-            res = merge_results(len(b), [(g[0], g[1]) for g in got])
             ro, fo = ref.submit(b)
             fills_total += len(fo)
             same_t = len(tape) == len(fo) and bool(np.all(tape == fo))
             same_r = all(np.array_equal(res[x], ro[x]) for x in
                          ("filled_qty", "remaining_qty", "fill_count", "tape_offset", "status", "reason"))
-            if not (same_t and same_r):
+            if ok and not (same_t and same_r):  # keep going: every rank must reach every collective
                 ok = False
                 msg = f"batch {k}: tape equal {same_t}, results equal {same_r}"
-                break
     if rank == 0:
         json.dump({"ok": ok, "msg": msg, "fills": fills_total, "world": world}, open(out_path, "w"))
     dist.barrier()

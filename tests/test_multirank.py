@@ -53,3 +53,19 @@ def test_two_rank_sharding_gpu_engines(built, tmp_path):
     r = _run("gpu", 2, tmp_path)
     assert r["ok"], r["msg"]
     assert r["fills"] > 0
+
+
+def test_two_rank_tape_gather_gloo_cpu(built, tmp_path):
+    """matching_engine_amd.gather.gather_batch (the RCCL tape/result gather) over gloo: per-shard
+    tapes/results gathered to rank 0 equal one oracle book over the whole stream."""
+    r = _run("gather", 2, tmp_path)
+    assert r["ok"], r["msg"]
+    assert r["fills"] > 0
+
+
+@pytest.mark.gpu
+def test_two_rank_tape_gather_gpu_engines(built, tmp_path):
+    r = _run("gpu_gather", 2, tmp_path)
+    assert r["ok"], r["msg"]
+    assert r["fills"] > 0
+
