@@ -51,7 +51,7 @@ def parse():
     ap.add_argument("--gather-steps", type=int, default=10,
                     help="N>1: batches run after the timed loop with the RCCL tape/result gather to rank 0 "
                          "(reported beside value, never in it)")
-    ap.add_argument("--traffic-from", default=None,
+    ap.add_argument("--traffic-from", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="JSON {bytes_per_launch: ...} from tools/pmc_traffic.py for roofline.traffic")
     return ap.parse_args()
 
