@@ -23,6 +23,8 @@ hipError_t launch_sort_pass(hipStream_t st, const uint32_t* keys_in, const uint3
                             uint32_t* keys_out, uint32_t* idx_out, uint32_t* zero_buf,
                             uint32_t zero_words, unsigned long long* scratch_top, uint32_t* bin_start);
 hipError_t launch_match(hipStream_t st, const BookDev& bk, const BatchDev& bt, hipEvent_t ev0, hipEvent_t ev1);
+hipError_t launch_bucket(hipStream_t st, const BatchDev& bt, uint32_t S, uint32_t* zero_buf, uint32_t zero_words,
+                         unsigned long long* scratch_top);
 uint32_t sort_tile(uint32_t n);
 hipError_t launch_tape(hipStream_t st, const BatchDev& bt, me_fill* tape, unsigned long long tape_cap,
                        unsigned long long* tape_count, unsigned long long* fills_acc, uint32_t* err);
@@ -70,6 +72,15 @@ struct me_engine {
     uint32_t* tile_sum = nullptr;
     unsigned long long* scratch_top = nullptr;
   } sb;
+  // Bucketed grouping (register-ladder kernel): per-bin counts and BK_CAP-record buckets.
+  struct BucketBufs {
+    uint32_t* cnt = nullptr;
+    uint64_t* seq = nullptr;
+    int64_t* px = nullptr;
+    int32_t* qty = nullptr;
+    uint32_t* ok = nullptr;
+  } bu;
+  bool bucketed = false;
   me_order_result* d_res = nullptr;
   uint32_t* d_fstart = nullptr;
   me_fill* d_scratch = nullptr;
@@ -127,7 +138,7 @@ static void free_all(me_engine* e) {
   {
     auto& sl = e->sb;
     void* sp[] = {sl.keys[0], sl.keys[1], sl.idx[0], sl.idx[1], sl.hist, sl.tile_sum, sl.scratch_top,
-                  sl.tot, sl.bin_start};
+                  sl.tot, sl.bin_start, e->bu.cnt, e->bu.seq, e->bu.px, e->bu.qty, e->bu.ok};
     for (void* p : sp)
       if (p) (void)hipFree(p);
   }
@@ -295,6 +306,16 @@ extern "C" me_engine* me_create(const me_config* cfg) {
     ALLOC(sl.tile_sum, ntiles_tape);
     ALLOC(sl.scratch_top, 1);
   }
+  // Register-ladder kernel: bucketed grouping when the sort key (index << 7 | slot) fits 32 bits.
+  e->bucketed = L <= 128 && n < BK_MAX_BATCH;
+  if (e->bucketed) {
+    const size_t nb = (S + 1) * (size_t)BK_CAP;
+    ALLOC(e->bu.cnt, (S + 1) * BK_CNT_STRIDE);
+    ALLOC(e->bu.seq, nb);
+    ALLOC(e->bu.px, nb);
+    ALLOC(e->bu.qty, nb);
+    ALLOC(e->bu.ok, nb);
+  }
   ALLOC(e->d_res, n);
   ALLOC(e->d_fstart, n);
   ALLOC(e->d_scratch, ovf_base + scap);
@@ -326,6 +347,7 @@ extern "C" me_engine* me_create(const me_config* cfg) {
     gs[i] = cfg->symbol_ids ? cfg->symbol_ids[i] : (uint32_t)i;
   }
   bool ok = launch_init_levels(st, bk.levels, S * L) == hipSuccess &&
+            (!e->bucketed || hipMemsetAsync(e->bu.cnt, 0, (S + 1) * BK_CNT_STRIDE * 4, st) == hipSuccess) &&
             hipMemsetAsync(bk.occ, 0, S * (L / 64) * 8, st) == hipSuccess &&
             hipMemsetAsync(bk.tend, 0, S * L, st) == hipSuccess &&
             launch_init_chunks(st, bk.chunks, nchunks) == hipSuccess &&
@@ -376,20 +398,22 @@ static int enqueue_batch(me_engine* e, const uint64_t* seq, const int64_t* px, c
   }
   const uint32_t S = e->bk.S;
   const uint32_t ntiles_tape = (n + TILE_TAPE - 1) / TILE_TAPE;
-  // grouping sort
+  // grouping: buckets (register-ladder kernel) or the counting sort
   const uint32_t* kin = sym;
   const uint32_t* iin = nullptr;
-  int shift = 0;
   uint32_t* run_table = e->passes == 1 ? sl.bin_start : nullptr;
-  for (int p = 0; p < e->passes; ++p) {
-    hipError_t he = launch_sort_pass(st, kin, iin, n, S, shift, e->dbits[p], sl.hist,
-                                     sl.tot + ((size_t)p << MAX_DIGIT_BITS), sl.keys[p], sl.idx[p],
-                                     p == 0 ? sl.tile_sum : nullptr, p == 0 ? ntiles_tape : 0, sl.scratch_top,
-                                     p == e->passes - 1 ? run_table : nullptr);
-    if (he != hipSuccess) return e->hip_fail(he, "grouping sort launch");
-    kin = sl.keys[p];
-    iin = sl.idx[p];
-    shift += e->dbits[p];
+  if (!e->bucketed) {
+    int shift = 0;
+    for (int p = 0; p < e->passes; ++p) {
+      hipError_t he = launch_sort_pass(st, kin, iin, n, S, shift, e->dbits[p], sl.hist,
+                                       sl.tot + ((size_t)p << MAX_DIGIT_BITS), sl.keys[p], sl.idx[p],
+                                       p == 0 ? sl.tile_sum : nullptr, p == 0 ? ntiles_tape : 0, sl.scratch_top,
+                                       p == e->passes - 1 ? run_table : nullptr);
+      if (he != hipSuccess) return e->hip_fail(he, "grouping sort launch");
+      kin = sl.keys[p];
+      iin = sl.idx[p];
+      shift += e->dbits[p];
+    }
   }
   BatchDev bt{};
   bt.seq = seq;
@@ -409,6 +433,19 @@ static int enqueue_batch(me_engine* e, const uint64_t* seq, const int64_t* px, c
   bt.slab = e->slab;
   bt.ovf_base = (unsigned long long)(S + 1) * e->slab;
   bt.bin_start = run_table;  // bins are symbols: the run table
+  if (e->bucketed) {
+    bt.skeys = nullptr;
+    bt.perm = nullptr;
+    bt.bin_start = nullptr;
+    bt.bcnt = e->bu.cnt;
+    bt.b_seq = e->bu.seq;
+    bt.b_px = e->bu.px;
+    bt.b_qty = e->bu.qty;
+    bt.b_ok = e->bu.ok;
+    bt.bcap = BK_CAP;
+    hipError_t he = launch_bucket(st, bt, S, sl.tile_sum, ntiles_tape, sl.scratch_top);
+    if (he != hipSuccess) return e->hip_fail(he, "bucket launch");
+  }
   // timing: the launch itself records start/end (hipExtLaunchKernelGGL), no marker packets
   hipError_t he = launch_match(st, e->bk, bt, tl.m0, tl.m1);
   if (he != hipSuccess) return e->hip_fail(he, "match launch");

@@ -115,6 +115,23 @@ struct BatchDev {
   unsigned long long ovf_base;
   // Single-pass grouping sort (bins are symbols): run(s) = [bin_start[s], bin_start[s + 1]).
   const uint32_t* bin_start;
+  // Bucketed grouping (register-ladder kernel, replaces the sort): k_bucket appends every record
+  // to the bucket of its bin (symbol, S = bad symbol) in arbitrary order; bucket b holds its first
+  // bcap records at [b * bcap, (b + 1) * bcap) and bcnt[b] counts all of them. k_match_reg orders
+  // a bucket by batch index on chip and resets bcnt; a bin with more than bcap records rescans the
+  // batch in order instead. Null bcnt: the sort path.
+  uint32_t* bcnt;        // [(S + 1) * BK_CNT_STRIDE]
+  const uint64_t* b_seq;
+  const int64_t* b_px;
+  const int32_t* b_qty;
+  const uint32_t* b_ok;  // batch index | (kind & 15) << BK_KIND_SHIFT
+  uint32_t bcap;
 };
+constexpr int BK_CAP = 128;          // records per bucket (two 64-record blocks)
+constexpr int BK_KIND_SHIFT = 28;    // b_ok: kind bits above the batch index
+constexpr uint32_t BK_IDX_MASK = (1u << BK_KIND_SHIFT) - 1u;
+constexpr uint32_t BK_MAX_BATCH = 1u << 25;  // sort key (index << 7 | bucket slot) fits 32 bits
+constexpr int BK_CNT_STRIDE = 32;    // bcnt[b * stride]: one 128-B line per counter (atomics on one
+                                     // line serialise: packed counters made k_bucket 6x slower)
 
 }  // namespace me

@@ -51,6 +51,19 @@ struct RegLds {
   uint32_t free_head;  // overflow free list in HBM (hdr.next links), NIL if empty
   uint32_t bump_cur, bump_end;  // chunk ids reserved from the global bump allocator
   uint32_t pad;
+  uint32_t scan_cur, scan_cnt, scan_pos;  // rescan of an overfull bucket: next batch index, list fill, list read
+  uint32_t mode;  // record source: 0 bucket, 1 rescan, 2 sort path (perm run [run_lo, run_lo + run_n))
+  uint32_t run_lo, run_n;
+  uint32_t pad2[2];
+  union {
+    struct {  // the symbol's bucket, staged for the batch-order gather
+      unsigned long long seq[BK_CAP];
+      long long px[BK_CAP];
+      int qty[BK_CAP];
+      uint32_t ok[BK_CAP];
+    } b;
+    uint32_t lst[1024];  // rescan: batch indices of the symbol's records in one 1024-record window
+  } in;
 };
 constexpr int REG_WAVES = 4;  // waves (symbols) per workgroup
 constexpr int VMCNT0 = 0x0F70;  // s_waitcnt immediate: vmcnt(0), expcnt / lgkmcnt untouched (gfx9 encoding)
@@ -549,6 +562,117 @@ __device__ __forceinline__ bool reg_reserve_overflow(RegCtx& c) {
   return true;
 }
 
+// ---- batch order of a bucket -----------------------------------------------------------------
+// Bitonic sort of 64 (one register) or 128 (two registers: element 64 + lane in b) distinct 32-bit
+// keys across the wave, ascending. Partners at lane distance 1 and 2 come over DPP, the rest
+// through ds_bpermute.
+template <int J>
+__device__ __forceinline__ uint32_t xor_lane(uint32_t v) {
+  if constexpr (J == 1)
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+  else if constexpr (J == 2)
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+  else
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((lane_id() ^ J) << 2, (int)v);
+}
+template <int J>
+__device__ __forceinline__ uint32_t bitonic_step(uint32_t v, bool asc) {
+  const uint32_t p = xor_lane<J>(v);
+  const bool lower = (lane_id() & J) == 0;
+  return (lower == asc) ? min(v, p) : max(v, p);
+}
+template <int K>
+__device__ __forceinline__ uint32_t bitonic_merge(uint32_t v, bool asc) {
+  if constexpr (K >= 64) v = bitonic_step<32>(v, asc);
+  if constexpr (K >= 32) v = bitonic_step<16>(v, asc);
+  if constexpr (K >= 16) v = bitonic_step<8>(v, asc);
+  if constexpr (K >= 8) v = bitonic_step<4>(v, asc);
+  if constexpr (K >= 4) v = bitonic_step<2>(v, asc);
+  v = bitonic_step<1>(v, asc);
+  return v;
+}
+// stages 2..64 of one register; dir1: direction of the 64-run (element 64 + lane sorts descending)
+__device__ __forceinline__ uint32_t sort64(uint32_t v, bool desc64) {
+  const int lane = lane_id();
+  v = bitonic_merge<2>(v, (lane & 2) == 0);
+  v = bitonic_merge<4>(v, (lane & 4) == 0);
+  v = bitonic_merge<8>(v, (lane & 8) == 0);
+  v = bitonic_merge<16>(v, (lane & 16) == 0);
+  v = bitonic_merge<32>(v, (lane & 32) == 0);
+  v = bitonic_merge<64>(v, !desc64);
+  return v;
+}
+__device__ __forceinline__ void sort128(uint32_t& a, uint32_t& b) {
+  a = sort64(a, false);
+  b = sort64(b, true);
+  const uint32_t lo = min(a, b), hi = max(a, b);
+  a = bitonic_merge<64>(lo, true);
+  b = bitonic_merge<64>(hi, true);
+}
+
+// Rescan of an overfull bucket: the next 1024-record window of the batch that holds records of
+// bin s, as a list of batch indices in LDS (batch order). Returns false when the batch is done.
+__device__ __forceinline__ bool rescan_window(RegLds* M, const ColdArgs& G, uint32_t s) {
+  const int lane = lane_id();
+  const uint32_t n = ldsu(G.bt.n), S = ldsu(G.bk.S);
+  const gptr<const uint32_t> sym = ldsg(G.bt.sym);
+  uint32_t cur = ldsu(M->scan_cur);
+  while (cur < n) {
+    uint32_t sy[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) sy[u] = sym[min(cur + 64u * u + (uint32_t)lane, n - 1u)];
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const uint32_t idx = cur + 64u * u + (uint32_t)lane;
+      const bool m = idx < n && min(sy[u], S) == s;
+      const unsigned long long bm = __ballot(m);
+      if (m) M->in.lst[cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u))] = idx;
+      cnt += (uint32_t)__popcll(bm);
+    }
+    cur += 1024u;
+    if (cnt) {
+      ldsw(M->scan_cur, cur);
+      ldsw(M->scan_cnt, cnt);
+      ldsw(M->scan_pos, 0u);
+      return true;
+    }
+  }
+  ldsw(M->scan_cur, cur);
+  return false;
+}
+
+__device__ __forceinline__ void reject_bad(const ColdArgs& G, uint32_t i, bool v) {
+  if (!v) return;
+  me_order_result r;
+  r.filled_qty = 0;
+  r.remaining_qty = 0;
+  r.fill_count = 0;
+  r.tape_offset = 0;
+  r.status = ME_ST_REJECTED;
+  r.reason = ME_RJ_BAD_SYMBOL;
+  r.pad[0] = r.pad[1] = 0;
+  ldsg(G.bt.res)[i] = r;
+  ldsg(G.bt.fstart)[i] = 0;
+}
+
+// The bad-symbol bin: every record rejected (order irrelevant).
+__device__ __forceinline__ void reject_bad_bucket(RegLds* M, const ColdArgs& G, uint32_t s, uint32_t ns,
+                                                  uint32_t bo0, uint32_t bo1) {
+  const int lane = lane_id();
+  const uint32_t cap = ldsu(G.bt.bcap);
+  if (ns <= cap) {
+    reject_bad(G, bo0 & BK_IDX_MASK, (uint32_t)lane < ns);
+    reject_bad(G, bo1 & BK_IDX_MASK, 64u + (uint32_t)lane < ns);
+    return;
+  }
+  if (lane == 0) M->scan_cur = 0;
+  while (rescan_window(M, G, s)) {
+    const uint32_t cnt = ldsu(M->scan_cnt);
+    for (uint32_t j = 0; j < cnt; j += 64) reject_bad(G, M->in.lst[min(j + lane, cnt - 1u)], j + lane < cnt);
+  }
+}
+
 // ---- the kernel ----------------------------------------------------------------------------
 // Per-record control word built in vector form: lim level | BUY | MARKET | CANCEL.
 constexpr uint32_t CW_BUY = 1u << 8, CW_MKT = 1u << 9, CW_CXL = 1u << 10;
@@ -573,33 +697,55 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
 #ifdef ME_STAMPS
   unsigned long long st_t0 = stamp_now();
 #endif
-  uint32_t lo, hi;
-  if (bt.bin_start) {  // single-pass sort: the run table
+  const bool bucketed = bt.bcnt != nullptr;
+  const uint32_t L = bk.L;
+  const uint32_t sl = s < bk.S ? s : bk.S - 1u;  // the bad-symbol wave's ladder loads are discarded
+  // ---- one round trip: the bin's record count and bucket, ladder rows, tail fills, symbol scalars,
+  // parked free chunks (no predicated loads: row 1 of a 64-level ladder re-reads row 0 and is then
+  // discarded; bucket slots past the count are never used)
+  uint32_t lo = 0, ns;
+  unsigned long long bq0 = 0, bq1 = 0;
+  long long bp0 = 0, bp1 = 0;
+  int bn0 = 0, bn1 = 0;
+  uint32_t bo0 = 0, bo1 = 0;
+  if (bucketed) {
+    const size_t bb = (size_t)s * BK_CAP;
+    ns = bt.bcnt[(size_t)s * BK_CNT_STRIDE];
+    bq0 = bt.b_seq[bb + lane];
+    bq1 = bt.b_seq[bb + 64 + lane];
+    bp0 = bt.b_px[bb + lane];
+    bp1 = bt.b_px[bb + 64 + lane];
+    bn0 = bt.b_qty[bb + lane];
+    bn1 = bt.b_qty[bb + 64 + lane];
+    bo0 = bt.b_ok[bb + lane];
+    bo1 = bt.b_ok[bb + 64 + lane];
+  } else if (bt.bin_start) {  // single-pass sort: the run table
     lo = bt.bin_start[s];
-    hi = bt.bin_start[s + 1];
+    ns = bt.bin_start[s + 1] - lo;
   } else {
     lo = wave_lower_bound(bt.skeys, bt.n, s);
-    hi = wave_lower_bound(bt.skeys, bt.n, s + 1);
+    ns = wave_lower_bound(bt.skeys, bt.n, s + 1) - lo;
   }
-  if (lo >= hi) return;
-  if (s == bk.S) {
-    reject_bad_symbols(bt, lo, hi);
-    return;
-  }
-  const uint32_t L = bk.L;
-  const Level* p_lv = bk.levels + (size_t)s * L;
-  const uint8_t* p_tend = bk.tend + (size_t)s * L;
-  // one round trip: ladder rows, tail fills, symbol scalars, parked free chunks (no predicated
-  // loads: row 1 of a 64-level ladder re-reads row 0 and is then discarded)
+  const Level* p_lv = bk.levels + (size_t)sl * L;
+  const uint8_t* p_tend = bk.tend + (size_t)sl * L;
   const bool in1 = 64u + (uint32_t)lane < L;
   const uint32_t l1 = in1 ? 64u + (uint32_t)lane : (uint32_t)lane;
   const Level a = p_lv[lane];
   const Level b = p_lv[l1];
   const uint32_t te0 = p_tend[lane];
   const uint32_t te1 = p_tend[l1];
-  const SymState st = bk.sym[s];
-  const uint32_t fst = bk.fcache[(size_t)s * FSTK + lane];
-  const uint32_t gsv = bk.gsym[s];
+  const SymState st = bk.sym[sl];
+  const uint32_t fst = bk.fcache[(size_t)sl * FSTK + lane];
+  const uint32_t gsv = bk.gsym[sl];
+  if (ns == 0u) return;
+  if (bucketed && lane == 0) bt.bcnt[(size_t)s * BK_CNT_STRIDE] = 0u;  // ready for the next batch's k_bucket
+  if (s == bk.S) {
+    if (bucketed)
+      reject_bad_bucket(&lds[wv], G, s, ns, bo0, bo1);
+    else
+      reject_bad_symbols(bt, lo, lo + ns);
+    return;
+  }
   RegCtx c;
   c.chunks = vptr(bk.chunks);
   c.loc = vptr(bk.loc);
@@ -634,22 +780,83 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
     c.M->free_head = st.free_head;
     c.M->bump_cur = 0;
     c.M->bump_end = 0;
+    c.M->scan_cur = 0;
+    c.M->scan_cnt = 0;
+    c.M->scan_pos = 0;
   }
   c.nfs = min(rl32(st.nfree, 0), (uint32_t)FSTK);
   c.fstk = fst;
   c.resting = (int)rl32(st.resting, 0);
   c.wptr = s * bt.slab;
   c.wend = c.wptr + bt.slab;
-  c.recs_left = hi - lo;
+  c.recs_left = ns;
+  // ---- batch order. A bucket (<= BK_CAP records, arbitrary order) is staged in LDS and its keys
+  // (batch index << 7 | bucket slot) sorted across the wave; an overfull bucket is replaced by a
+  // rescan of the batch (1024-record windows, batch order by construction).
+  // 0: bucket, 1: rescan, 2: sort path (perm)
+  const uint32_t mode = bucketed ? (ns <= (uint32_t)BK_CAP ? 0u : 1u) : 2u;
+  uint32_t k0 = ~0u, k1 = ~0u;
+  if (mode == 0u) {
+    c.M->in.b.seq[lane] = bq0;
+    c.M->in.b.seq[64 + lane] = bq1;
+    c.M->in.b.px[lane] = bp0;
+    c.M->in.b.px[64 + lane] = bp1;
+    c.M->in.b.qty[lane] = bn0;
+    c.M->in.b.qty[64 + lane] = bn1;
+    c.M->in.b.ok[lane] = bo0;
+    c.M->in.b.ok[64 + lane] = bo1;
+    k0 = (uint32_t)lane < ns ? ((bo0 & BK_IDX_MASK) << 7) | (uint32_t)lane : ~0u;
+    k1 = 64u + (uint32_t)lane < ns ? ((bo1 & BK_IDX_MASK) << 7) | (64u + (uint32_t)lane) : ~0u;
+    if (ns > 64u)
+      sort128(k0, k1);
+    else
+      k0 = sort64(k0, false);
+  }
+  if (lane == 0) {  // read back where used: nothing of this holds an SGPR across the serial loop
+    c.M->mode = mode;
+    c.M->run_lo = lo;
+    c.M->run_n = ns;
+  }
   STAMP_ADD(c, PH_PROLOGUE);
-  for (uint32_t blk = lo; blk < hi; blk += 64) {
-    // ---- 64 records in vector form (two dependent round trips: permutation, then the records)
-    const uint32_t j = blk + (uint32_t)lane;
-    const uint32_t oi = ldsg(G.bt.perm)[j < hi ? j : hi - 1u];  // clamp: never branch around a load
-    const unsigned long long oseq_ = ldsg(G.bt.seq)[oi];
-    const long long opx_ = ldsg(G.bt.px)[oi];
-    const int oq_ = ldsg(G.bt.qty)[oi];
-    const uint32_t kd_ = ldsg(G.bt.kind)[oi];
+  // left: records of the symbol not yet visited (its count; the rescan keeps its own cursors)
+  for (uint32_t left = ns;;) {
+    // ---- up to 64 records in vector form, batch order
+    uint32_t oi, cnt;
+    unsigned long long oseq_;
+    long long opx_;
+    int oq_;
+    uint32_t kd_;
+    const uint32_t md = ldsu(c.M->mode);
+    if (md == 0u) {
+      if (left == 0u) break;
+      cnt = min(64u, left);
+      const uint32_t pos = k0 & (BK_CAP - 1);  // past the count: key ~0, slot 127 (discarded)
+      oi = k0 >> 7;
+      k0 = k1;  // the second block, if any
+      oseq_ = c.M->in.b.seq[pos];
+      opx_ = c.M->in.b.px[pos];
+      oq_ = c.M->in.b.qty[pos];
+      kd_ = c.M->in.b.ok[pos] >> BK_KIND_SHIFT;
+    } else {
+      if (md == 1u) {
+        if (ldsu(c.M->scan_pos) >= ldsu(c.M->scan_cnt) && !rescan_window(c.M, G, s)) break;
+        const uint32_t p0 = ldsu(c.M->scan_pos), lc = ldsu(c.M->scan_cnt);
+        cnt = min(64u, lc - p0);
+        oi = c.M->in.lst[p0 + min((uint32_t)lane, cnt - 1u)];
+        ldsw(c.M->scan_pos, p0 + cnt);
+      } else {
+        if (left == 0u) break;
+        cnt = min(64u, left);
+        const uint32_t at = ldsu(c.M->run_lo) + (ldsu(c.M->run_n) - left);
+        oi = ldsg(G.bt.perm)[at + min((uint32_t)lane, cnt - 1u)];  // clamp: never branch around a load
+      }
+      oseq_ = ldsg(G.bt.seq)[oi];
+      opx_ = ldsg(G.bt.px)[oi];
+      oq_ = ldsg(G.bt.qty)[oi];
+      kd_ = ldsg(G.bt.kind)[oi];
+    }
+    const uint32_t j = (uint32_t)lane;  // record j of the block
+    const uint32_t hi = cnt;
     const unsigned long long max_seq = ldsu(G.bk.max_seq);
     const long long lbase = c.base;
     // validation in vector form; only the packed control word and the reject code stay live
@@ -680,7 +887,6 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
       if (!v) rj = 0xFFu;  // lanes past the run: no record
     }
     unsigned long long work = __ballot(rj == ME_RJ_NONE);
-    const uint32_t cnt = min(64u, hi - blk);
     uint32_t stop = cnt;  // records [0, stop) of the block get results
     uint32_t out_q = 0, out_n = 0, out_w = 0;
 #ifdef ME_STAMPS
@@ -692,7 +898,7 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
       const int k = __builtin_ctzll(work);
       work &= work - 1ull;
       const uint32_t ctl = rl32(cw, k);
-      c.recs_left = hi - (blk + (uint32_t)k);
+      c.recs_left = left - (uint32_t)k;
       uint32_t outq;
       COUNT(c, CT_FAST);
       STAMP_ADD(c, PH_SWEEP);
@@ -769,6 +975,7 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
       if (out_n) atomicAdd(&tile_sum[oi / TILE_TAPE], out_n);
     }
     STAMP_ADD(c, PH_RESULT);
+    left -= cnt;
     if (stop < cnt) break;
   }
   // ---- write the symbol back

@@ -151,6 +151,37 @@ def test_edge_one_symbol_whole_batch_and_tile_boundaries(me, orc):
         run_both(eng, ob, batches, ctx="tiles")
 
 
+def test_edge_bucket_boundaries(me, orc):
+    """Register-ladder grouping: per-symbol record counts on both sides of one block (64) and of the
+    bucket capacity (128; more records take the batch rescan), and more bad-symbol records than a
+    bucket holds — interleaved at random, several batches so the bucket counters are reused."""
+    B, S, L, M = me.SIDE_BUY, me.SIDE_SELL, me.TYPE_LIMIT, me.TYPE_MARKET
+    rng = np.random.default_rng(11)
+    counts = [1, 63, 64, 65, 127, 128, 129, 300]
+    bad = 200
+    nsym = len(counts)
+    base = [10_000 + 1000 * k for k in range(nsym)]
+    batches, seq = [], 1
+    for _ in range(3):
+        syms = np.concatenate([np.full(c, k) for k, c in enumerate(counts)] +
+                              [rng.integers(nsym, nsym + 50, bad)])
+        rng.shuffle(syms)
+        rows = []
+        for sy in syms:
+            sy = int(sy)
+            side = B if rng.random() < 0.5 else S
+            if rng.random() < 0.2:
+                rows.append((sy, side, M, 0, 0, int(rng.integers(1, 60))))
+            else:
+                px = (base[sy] if sy < nsym else 10_000) + 64 + int(rng.integers(-20, 21))
+                rows.append((sy, side, L, 0, px, int(rng.integers(1, 60))))
+        batches.append(_rows(me, rows, start_seq=seq))
+        seq += len(rows)
+    ob = orc.OracleBook(nsym, 128, base, 1 << 16)
+    with engine_for(me, nsym, 128, base, 4096, 1 << 14, 1 << 16) as eng:
+        run_both(eng, ob, batches, ctx="buckets")
+
+
 def test_edge_symbol_count_sort_plans(me, orc):
     """1-pass sort up to 2047 symbols, 2-pass from 2048: exercise both sides of the switch."""
     for S in (1, 2, 2047, 2048, 70_000):
