@@ -39,6 +39,9 @@
 namespace me {
 
 constexpr int RL = 128;  // levels covered by this kernel
+// Block placement: rare paths out of line, so the common path runs without taken branches.
+#define ME_LIKELY(x) __builtin_expect(!!(x), 1)
+#define ME_UNLIKELY(x) __builtin_expect(!!(x), 0)
 constexpr int FSTK = 64; // free chunk ids a wave keeps in its VGPR stack (= fcache row length)
 
 // One wave's LDS: the head-chunk cache (entry l = head chunk of level l) and the level totals.
@@ -212,12 +215,17 @@ __device__ __forceinline__ void reg_err(const RegCtx& c, uint32_t bits) {
   if (lane_id() == 0) atomicOr(ldsg(c.G->bk.err), bits);
 }
 
-// Inclusive scan of a 16-lane row (each DPP row scans on its own), saturating at 2^32 - 1.
+// Inclusive scan of a 16-lane row (each DPP row scans on its own), saturating at 2^32 - 1. The row
+// shifts use bound_ctrl (a lane with no source reads 0), so no "old" value is materialised.
+template <int kCtrl>
+__device__ __forceinline__ uint32_t shr_row(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kCtrl, 0xF, 0xF, true);
+}
 __device__ __forceinline__ uint32_t scan16_sat(uint32_t x) {
-  x = __builtin_elementwise_add_sat(x, dpp32<0x111, 0xF>(x));  // row_shr:1
-  x = __builtin_elementwise_add_sat(x, dpp32<0x112, 0xF>(x));  // row_shr:2
-  x = __builtin_elementwise_add_sat(x, dpp32<0x114, 0xF>(x));  // row_shr:4
-  x = __builtin_elementwise_add_sat(x, dpp32<0x118, 0xF>(x));  // row_shr:8
+  x = __builtin_elementwise_add_sat(x, shr_row<0x111>(x));  // row_shr:1
+  x = __builtin_elementwise_add_sat(x, shr_row<0x112>(x));  // row_shr:2
+  x = __builtin_elementwise_add_sat(x, shr_row<0x114>(x));  // row_shr:4
+  x = __builtin_elementwise_add_sat(x, shr_row<0x118>(x));  // row_shr:8
   return x;
 }
 
@@ -233,7 +241,7 @@ __device__ __forceinline__ void tot_add(RegCtx& c, int lvl, long long d) {
 // Free-list push of a chunk whose HBM quantities are all zero: onto the VGPR stack, or (stack
 // full) onto the HBM overflow list — a store, never a load.
 __device__ __forceinline__ void reg_free(RegCtx& c, uint32_t ch) {
-  if (c.nfs < (uint32_t)FSTK) {
+  if (ME_LIKELY(c.nfs < (uint32_t)FSTK)) {
     c.fstk = lane_id() == (int)c.nfs ? ch : c.fstk;
     c.nfs += 1;
   } else {
@@ -274,7 +282,7 @@ __device__ __forceinline__ uint32_t reg_alloc_slow(RegCtx& c) {
 }
 
 __device__ __forceinline__ uint32_t reg_alloc(RegCtx& c) {
-  if (c.nfs) {
+  if (ME_LIKELY(c.nfs != 0u)) {
     c.nfs -= 1;
     return rl32(c.fstk, (int)c.nfs);
   }
@@ -285,7 +293,7 @@ __device__ __forceinline__ uint32_t reg_alloc(RegCtx& c) {
 // Miss: copy chunk ch (the head of level lvl) into cache entry lvl. The only global load of a walk;
 // its registers die at the LDS writes, so no wait on it leaks into the hit path.
 __device__ __forceinline__ bool reg_fill_entry(RegCtx& c, int lvl, uint32_t ch) {
-  if (ch >= c.nchunks) {  // NIL or corrupt: never index with it
+  if (ME_UNLIKELY(ch >= c.nchunks)) {  // NIL or corrupt: never index with it
     reg_err(c, ERR_INCONSISTENT);
     return false;
   }
@@ -316,6 +324,9 @@ __device__ __forceinline__ bool reg_take_chunk(RegCtx& c, int lvl, uint32_t& rem
   const int sl = lane & (ME_C - 1);
   COUNT(c, CT_WALK);
   const int q_ = c.M->cq[lvl][sl];
+  // read with the quantities (one LDS round trip); the opaque use keeps it from sinking into the
+  // fill branch, where it would be a second round trip
+  const unsigned long long mseq = vreg64(c.M->cs[lvl][sl]);
   const uint32_t uq = act ? (uint32_t)q_ : 0u;
   const uint32_t inc = scan16_sat(uq);
   const uint32_t ex = inc - uq;
@@ -326,7 +337,7 @@ __device__ __forceinline__ bool reg_take_chunk(RegCtx& c, int lvl, uint32_t& rem
   if (fe) {
     me_fill F;
     F.taker_seq = taker;
-    F.maker_seq = c.M->cs[lvl][sl];
+    F.maker_seq = mseq;
     F.price_q4 = price;
     F.qty = (int)f;
     F.symbol = c.gs;
@@ -335,12 +346,12 @@ __device__ __forceinline__ bool reg_take_chunk(RegCtx& c, int lvl, uint32_t& rem
     c.M->cq[lvl][sl] = (int)(uq - f);
   }
   c.wptr += (uint32_t)__popcll(fm);
-  c.resting -= __popcll(__ballot(fe && f == uq));  // makers filled completely leave the book
+  c.resting -= __popcll(__ballot(f == uq) & fm);  // makers filled completely leave the book
   const uint32_t live = rl32(inc, 15);
   const uint32_t t = rem < live ? rem : live;
   rem -= t;
   taken += t;
-  return __ballot(act && uq > f) == 0ull;  // no live slot left
+  return (__ballot(uq > f) & 0xFFFFull) == 0ull;  // no live slot left (slots are lanes 0..15)
 }
 
 // Taker against level lvl. The common case is straight-line: the cached head chunk keeps live
@@ -349,13 +360,13 @@ __device__ __forceinline__ bool reg_walk(RegCtx& c, int lvl, uint32_t& rem, unsi
   const int lane = lane_id();
   const long long price = c.base + lvl;
   uint32_t ch = c.hd.get(lvl);
-  if (!c.cv.bit(lvl)) {
+  if (ME_UNLIKELY(!c.cv.bit(lvl))) {
     COUNT(c, CT_MISS);
     if (!reg_fill_entry(c, lvl, ch)) return false;
     c.cv.set(lvl);
   }
   uint32_t taken = 0;
-  if (!reg_take_chunk(c, lvl, rem, taken, taker, price)) {
+  if (ME_LIKELY(!reg_take_chunk(c, lvl, rem, taken, taker, price))) {
     tot_add(c, lvl, -(long long)taken);
     return false;
   }
@@ -430,8 +441,8 @@ __device__ __forceinline__ bool reg_rest(RegCtx& c, int lvl, unsigned long long 
   const int lane = lane_id();
   const uint32_t tl = c.tl.get(lvl);
   const uint32_t te = c.te.get(lvl);
-  if (tl != NIL && te < (uint32_t)ME_C) {
-    if (tl >= c.nchunks) {
+  if (ME_LIKELY(tl != NIL && te < (uint32_t)ME_C)) {
+    if (ME_UNLIKELY(tl >= c.nchunks)) {
       reg_err(c, ERR_INCONSISTENT);
       return false;
     }
@@ -902,11 +913,11 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
       uint32_t outq;
       COUNT(c, CT_FAST);
       STAMP_ADD(c, PH_SWEEP);
-      if (ctl & CW_CXL) {
+      if (ME_UNLIKELY(ctl & CW_CXL)) {
         outq = reg_cancel(c, (unsigned long long)rli64(opx_, k));
         STAMP_ADD(c, PH_CANCEL);
       } else {
-        if (c.wptr + (uint32_t)c.resting > c.wend && !reg_reserve_overflow(c)) {
+        if (ME_UNLIKELY(c.wptr + (uint32_t)c.resting > c.wend) && !reg_reserve_overflow(c)) {
           stop = (uint32_t)k;
           break;
         }
@@ -918,13 +929,13 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
         if (ctl & CW_BUY) {
           while (rem != 0u && c.ba <= lm) {
             const int lvl = c.ba;
-            if (!reg_walk(c, lvl, rem, seq)) break;
+            if (ME_LIKELY(!reg_walk(c, lvl, rem, seq))) break;
             c.ba = c.occ.next(lvl + 1);
           }
         } else {
           while (rem != 0u && c.bb >= lm) {
             const int lvl = c.bb;
-            if (!reg_walk(c, lvl, rem, seq)) break;
+            if (ME_LIKELY(!reg_walk(c, lvl, rem, seq))) break;
             c.bb = c.occ.prev(lvl - 1);
           }
         }
@@ -933,7 +944,7 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
         const bool me_ = lane == k;
         out_n = me_ ? c.wptr - w_in : out_n;
         out_w = me_ ? w_in : out_w;
-        if (!(ctl & CW_MKT) && rem != 0u && !reg_rest(c, lm, seq, rem, (ctl & CW_BUY) != 0u)) {
+        if (!(ctl & CW_MKT) && rem != 0u && ME_UNLIKELY(!reg_rest(c, lm, seq, rem, (ctl & CW_BUY) != 0u))) {
           stop = (uint32_t)k;  // chunk pool exhausted: the batch fails (sticky error word)
           break;
         }
