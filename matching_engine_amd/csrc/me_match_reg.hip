@@ -6,8 +6,8 @@
 //
 //   * the ladder's FIFO ends (head chunk, tail chunk, tail fill) live in VGPRs — level l is lane
 //     l & 63 of row l >> 6 — so reading one is a v_readlane and writing one a lane select;
-//   * occupancy and the head-chunk cache's valid state are 128-bit SGPR masks, so the next best
-//     price is a bit scan and a cache lookup a bit test;
+//   * occupancy is a 128-bit SGPR mask, so the next best price is a bit scan; whether the head
+//     chunk sits in the cache is the top bit of the head row (read with the head id itself);
 //   * the head chunk of every level can sit in LDS (16 slots of qty + seq: 26 KB per wave, no
 //     evictions); fills, appends and cancels of a cached head never touch HBM, and every valid
 //     entry is written back once at the end of the launch;
@@ -43,6 +43,9 @@ constexpr int RL = 128;  // levels covered by this kernel
 #define ME_LIKELY(x) __builtin_expect(!!(x), 1)
 #define ME_UNLIKELY(x) __builtin_expect(!!(x), 0)
 constexpr int FSTK = 64; // free chunk ids a wave keeps in its VGPR stack (= fcache row length)
+// Head-row flag: set unless cache entry l holds level l's head chunk (chunk ids stay below 2^31;
+// NIL, an empty level, reads as not cached).
+constexpr uint32_t HC = 0x80000000u;
 
 // One wave's LDS: the head-chunk cache (entry l = head chunk of level l) and the level totals.
 struct RegLds {
@@ -57,7 +60,8 @@ struct RegLds {
   uint32_t scan_cur, scan_cnt, scan_pos;  // rescan of an overfull bucket: next batch index, list fill, list read
   uint32_t mode;  // record source: 0 bucket, 1 rescan, 2 sort path (perm run [run_lo, run_lo + run_n))
   uint32_t run_lo, run_n;
-  uint32_t pad2[2];
+  int dq;                 // reg_rest: LDS target of an append to an uncached tail
+  unsigned long long dsq;
   union {
     struct {  // the symbol's bucket, staged for the batch-order gather
       unsigned long long seq[BK_CAP];
@@ -197,8 +201,8 @@ struct RegCtx {
   uint32_t gs;         // VGPR (symbol id written into fills)
   uint32_t nchunks;
   uint32_t s;
-  Row2 hd, tl, te;     // head chunk, tail chunk, slots written in the tail chunk
-  Mask2 occ, cv;       // occupied levels, cache entry valid (holds the level's current head chunk)
+  Row2 hd, tl, te;     // head chunk (| HC unless cached), tail chunk, slots written in the tail chunk
+  Mask2 occ;           // occupied levels
   int bb, ba;          // best bid level (-1: none), best ask level (RL: none)
   uint32_t fstk;       // VGPR stack of free chunk ids: lane i holds entry i ...
   uint32_t nfs;        // ... entries [0, nfs) are valid
@@ -359,11 +363,12 @@ __device__ __forceinline__ bool reg_take_chunk(RegCtx& c, int lvl, uint32_t& rem
 __device__ __forceinline__ bool reg_walk(RegCtx& c, int lvl, uint32_t& rem, unsigned long long taker) {
   const int lane = lane_id();
   const long long price = c.base + lvl;
-  uint32_t ch = c.hd.get(lvl);
-  if (ME_UNLIKELY(!c.cv.bit(lvl))) {
+  const uint32_t hv = c.hd.get(lvl);
+  uint32_t ch = hv & ~HC;  // an occupied level: a real chunk id
+  if (ME_UNLIKELY(hv & HC)) {
     COUNT(c, CT_MISS);
     if (!reg_fill_entry(c, lvl, ch)) return false;
-    c.cv.set(lvl);
+    c.hd.put(lvl, ch);  // now cached
   }
   uint32_t taken = 0;
   if (ME_LIKELY(!reg_take_chunk(c, lvl, rem, taken, taker, price))) {
@@ -372,10 +377,10 @@ __device__ __forceinline__ bool reg_walk(RegCtx& c, int lvl, uint32_t& rem, unsi
   }
   // the head chunk is exhausted: free it and continue down the FIFO (each next chunk is a miss)
   const uint32_t tail = c.tl.get(lvl);
+  bool cached = false;  // whether the level's new head ends up in the cache
   for (;;) {
     const uint32_t nx = rl32(c.M->cnext[lvl], 0);
     if (lane < ME_C) c.chunks[ch].qty[lane] = 0;  // a freed chunk must read all-zero in HBM
-    c.cv.clr(lvl);
     reg_free(c, ch);
     if (ch == tail) {
       c.hd.put(lvl, NIL);
@@ -387,12 +392,17 @@ __device__ __forceinline__ bool reg_walk(RegCtx& c, int lvl, uint32_t& rem, unsi
     ch = nx;
     if (rem == 0u) break;
     COUNT(c, CT_MISS);
-    if (!reg_fill_entry(c, lvl, ch)) return false;
-    c.cv.set(lvl);
-    if (!reg_take_chunk(c, lvl, rem, taken, taker, price)) break;
+    if (!reg_fill_entry(c, lvl, ch)) {
+      c.hd.put(lvl, ch | HC);
+      return false;
+    }
+    if (!reg_take_chunk(c, lvl, rem, taken, taker, price)) {
+      cached = true;
+      break;
+    }
   }
   tot_add(c, lvl, -(long long)taken);
-  c.hd.put(lvl, ch);
+  c.hd.put(lvl, cached ? ch : (ch | HC));
   if (lane == 0 && ch < c.nchunks) c.chunks[ch].hdr.prev = NIL;  // new FIFO head
   return false;
 }
@@ -415,16 +425,15 @@ __device__ __forceinline__ bool reg_rest_new_chunk(RegCtx& c, int lvl, unsigned 
     c.loc[seq] = ch * ME_C;
   }
   if (tl == NIL) {  // empty level: the new chunk is its head, installed in the cache
-    c.hd.put(lvl, ch);
+    c.hd.put(lvl, ch);  // cached
     if (lane < ME_C) c.M->cq[lvl][lane] = lane == 0 ? (int)qty : 0;
     if (lane == 0) {
       c.M->cs[lvl][0] = seq;
       c.M->cnext[lvl] = NIL;
     }
-    c.cv.set(lvl);
     c.occ.set(lvl);
   } else {
-    const bool tl_cached = c.cv.bit(lvl) && c.hd.get(lvl) == tl;
+    const bool tl_cached = c.hd.get(lvl) == tl;  // the tail is the cached head
     if (lane == 0) {
       if (tl < c.nchunks) c.chunks[tl].hdr.next = ch;
       if (tl_cached) c.M->cnext[lvl] = ch;
@@ -446,15 +455,16 @@ __device__ __forceinline__ bool reg_rest(RegCtx& c, int lvl, unsigned long long 
       reg_err(c, ERR_INCONSISTENT);
       return false;
     }
-    const bool in_cache = c.cv.bit(lvl) && c.hd.get(lvl) == tl;
+    const bool in_cache = c.hd.get(lvl) == tl;  // the tail is the cached head
     if (lane == 0) {
-      if (in_cache) {
-        c.M->cq[lvl][te] = (int)qty;
-        c.M->cs[lvl][te] = seq;
-      } else {
-        c.chunks[tl].qty[te] = (int)qty;
-        c.chunks[tl].seq[te] = seq;
-      }
+      // no branch on in_cache: the HBM slot is written either way (a cached tail is written back
+      // from LDS at the end anyway) and the LDS copy goes to the entry or to a dummy slot
+      int* lq = in_cache ? &c.M->cq[lvl][te] : &c.M->dq;
+      unsigned long long* ls = in_cache ? &c.M->cs[lvl][te] : &c.M->dsq;
+      *lq = (int)qty;
+      *ls = seq;
+      c.chunks[tl].qty[te] = (int)qty;
+      c.chunks[tl].seq[te] = seq;
       c.loc[seq] = tl * ME_C + te;
     }
     c.te.put(lvl, te + 1u);
@@ -496,8 +506,9 @@ __device__ __forceinline__ uint32_t reg_cancel(RegCtx& c, unsigned long long tgt
     reg_err(c, ERR_INCONSISTENT);
     return 0;
   }
-  const uint32_t h = c.hd.get(lvl), t = c.tl.get(lvl);
-  const bool in_cache = c.cv.bit(lvl) && h == ch;  // the on-chip copy is authoritative
+  const uint32_t hv = c.hd.get(lvl), t = c.tl.get(lvl);
+  const uint32_t h = hv == NIL ? NIL : (hv & ~HC);
+  const bool in_cache = hv == ch;  // ch is the cached head: the on-chip copy is authoritative
   if (in_cache) {
     const int qc = c.M->cq[lvl][lane & (ME_C - 1)];
     qv = act ? qc : 0;
@@ -520,10 +531,9 @@ __device__ __forceinline__ uint32_t reg_cancel(RegCtx& c, unsigned long long tgt
     }
     if (in_cache) {  // the chunk leaves the cache; its HBM copy must read all-zero
       if (act) c.chunks[ch].qty[lane] = 0;
-      c.cv.clr(lvl);
     }
     const uint32_t nxt = rl32(hdr.next, 0), prv = rl32(hdr.prev, 0);
-    const bool mirror = c.cv.bit(lvl) && h == prv;  // the cached head is ch's predecessor
+    const bool mirror = hv == prv;  // the cached head is ch's predecessor
     if (h == t) {  // ch was the level's only chunk: the level empties
       c.hd.put(lvl, NIL);
       c.tl.put(lvl, NIL);
@@ -531,7 +541,7 @@ __device__ __forceinline__ uint32_t reg_cancel(RegCtx& c, unsigned long long tgt
       if (lvl == c.bb) c.bb = c.occ.prev(lvl);
       if (lvl == c.ba) c.ba = c.occ.next(lvl);
     } else if (ch == h) {
-      c.hd.put(lvl, nxt);
+      c.hd.put(lvl, nxt | HC);  // the new head is not cached
       if (lane == 0) c.chunks[nxt].hdr.prev = NIL;
     } else if (ch == t) {
       c.tl.put(lvl, prv);
@@ -771,8 +781,8 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
   c.st_t = st_t0;
   STAMP_ADD(c, PH_SW_WINDOW);  // run bounds
 #endif
-  c.hd.r0 = a.head;
-  c.hd.r1 = in1 ? b.head : NIL;
+  c.hd.r0 = a.head | HC;  // nothing cached yet (NIL stays NIL)
+  c.hd.r1 = in1 ? (b.head | HC) : NIL;
   c.tl.r0 = a.tail;
   c.tl.r1 = in1 ? b.tail : NIL;
   c.te.r0 = te0;
@@ -782,7 +792,6 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
   c.M->tot[64 + lane] = tb;
   c.occ.w0 = __ballot(a.total > 0);
   c.occ.w1 = __ballot(tb > 0);
-  c.cv.w0 = c.cv.w1 = 0ull;
   c.base = (long long)vreg64((unsigned long long)st.base);
   c.bb = rli32(st.best_bid, 0);
   c.ba = rli32(st.best_ask, 0);
@@ -926,19 +935,18 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
         const int lm = (int)(ctl & 0xFFu);
         const uint32_t w_in = c.wptr;
         uint32_t rem = q;
-        if (ctl & CW_BUY) {
-          while (rem != 0u && c.ba <= lm) {
-            const int lvl = c.ba;
-            if (ME_LIKELY(!reg_walk(c, lvl, rem, seq))) break;
-            c.ba = c.occ.next(lvl + 1);
-          }
-        } else {
-          while (rem != 0u && c.bb >= lm) {
-            const int lvl = c.bb;
-            if (ME_LIKELY(!reg_walk(c, lvl, rem, seq))) break;
-            c.bb = c.occ.prev(lvl - 1);
-          }
+        // one walk loop for both sides (one copy of the walk): the opposite best moves away from
+        // the taker's limit as levels empty
+        const bool buy = (ctl & CW_BUY) != 0u;
+        int lvl = buy ? c.ba : c.bb;
+        while (rem != 0u && (buy ? lvl <= lm : lvl >= lm)) {
+          if (ME_LIKELY(!reg_walk(c, lvl, rem, seq))) break;
+          lvl = buy ? c.occ.next(lvl + 1) : c.occ.prev(lvl - 1);
         }
+        if (buy)
+          c.ba = lvl;
+        else
+          c.bb = lvl;
         outq = q - rem;
         STAMP_ADD(c, PH_WALK);
         const bool me_ = lane == k;
@@ -996,7 +1004,7 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
     while (cur < end) reg_free(c, cur++);
   }
   for (int row = 0; row < 2; ++row) {  // every valid cached head back to HBM (entry l holds the head of l)
-    unsigned long long d = row ? c.cv.w1 : c.cv.w0;
+    unsigned long long d = __ballot(((row ? c.hd.r1 : c.hd.r0) & HC) == 0u);  // cached heads
     while (d) {
       const int jj = __builtin_ctzll(d);
       d &= d - 1ull;
@@ -1012,13 +1020,13 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
   uint8_t* g_tend = ldsg(G.bk.tend) + (size_t)s * L;
   Level o;
   o.total = c.M->tot[lane];
-  o.head = c.hd.r0;
+  o.head = c.hd.r0 == NIL ? NIL : (c.hd.r0 & ~HC);
   o.tail = c.tl.r0;
   g_lv[lane] = o;
   g_tend[lane] = (uint8_t)c.te.r0;
   if (in1) {
     o.total = c.M->tot[64 + lane];
-    o.head = c.hd.r1;
+    o.head = c.hd.r1 == NIL ? NIL : (c.hd.r1 & ~HC);
     o.tail = c.tl.r1;
     g_lv[64 + lane] = o;
     g_tend[64 + lane] = (uint8_t)c.te.r1;
