@@ -939,7 +939,9 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
         // the taker's limit as levels empty
         const bool buy = (ctl & CW_BUY) != 0u;
         int lvl = buy ? c.ba : c.bb;
-        while (rem != 0u && (buy ? lvl <= lm : lvl >= lm)) {
+        for (;;) {
+          const int gap = buy ? lm - lvl : lvl - lm;  // >= 0: the level crosses the limit (int select, scalar)
+          if (rem == 0u || gap < 0) break;
           if (ME_LIKELY(!reg_walk(c, lvl, rem, seq))) break;
           lvl = buy ? c.occ.next(lvl + 1) : c.occ.prev(lvl - 1);
         }
