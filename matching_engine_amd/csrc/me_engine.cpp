@@ -23,8 +23,8 @@ hipError_t launch_sort_pass(hipStream_t st, const uint32_t* keys_in, const uint3
                             uint32_t* keys_out, uint32_t* idx_out, uint32_t* zero_buf,
                             uint32_t zero_words, unsigned long long* scratch_top, uint32_t* bin_start);
 hipError_t launch_match(hipStream_t st, const BookDev& bk, const BatchDev& bt, hipEvent_t ev0, hipEvent_t ev1);
-hipError_t launch_bucket(hipStream_t st, const BatchDev& bt, uint32_t S, uint32_t* zero_buf, uint32_t zero_words,
-                         unsigned long long* scratch_top);
+hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev& bt, const AuxDev& ax, hipEvent_t ev0,
+                            hipEvent_t ev1);
 uint32_t sort_tile(uint32_t n);
 hipError_t launch_tape(hipStream_t st, const BatchDev& bt, me_fill* tape, unsigned long long tape_cap,
                        unsigned long long* tape_count, unsigned long long* fills_acc, uint32_t* err);
@@ -69,9 +69,18 @@ struct me_engine {
     uint32_t* hist = nullptr;
     uint32_t* tot = nullptr;        // [2 passes][2048] bin totals
     uint32_t* bin_start = nullptr;  // [2049] run table of the single-pass sort
-    uint32_t* tile_sum = nullptr;
-    unsigned long long* scratch_top = nullptr;
   } sb;
+  // Per-batch outputs. The pipelined register-ladder path rotates three sets (batch b is bucketed
+  // while b-1 is matched and b-2's tape is compacted); the other paths use set 0.
+  struct OutSet {
+    me_order_result* res = nullptr;
+    uint32_t* fstart = nullptr;
+    uint32_t* tile_sum = nullptr;
+    me_fill* scratch = nullptr;
+    unsigned long long* top = nullptr;
+  } os[3];
+  int nsets = 1;
+  int last_set = 0;  // output set of the most recent batch
   // Bucketed grouping (register-ladder kernel): per-bin counts and BK_CAP-record buckets.
   struct BucketBufs {
     uint32_t* cnt = nullptr;
@@ -79,11 +88,22 @@ struct me_engine {
     int64_t* px = nullptr;
     int32_t* qty = nullptr;
     uint32_t* ok = nullptr;
-  } bu;
+  } bu[2];
   bool bucketed = false;
-  me_order_result* d_res = nullptr;
-  uint32_t* d_fstart = nullptr;
-  me_fill* d_scratch = nullptr;
+  // Pipelined path: batches launched but not finished. A batch is bucketed in the launch of its
+  // own submit, matched in the next launch, its tape compacted in the one after; me_sync (and
+  // everything that reads outputs or the book) flushes.
+  struct Pend {
+    bool valid = false;
+    const uint64_t* seq = nullptr;
+    const int64_t* px = nullptr;
+    const int32_t* qty = nullptr;
+    const uint32_t* sym = nullptr;
+    const uint8_t* kind = nullptr;
+    uint32_t n = 0;
+    int oset = 0, bset = 0;
+  } p_match, p_tape;
+  uint64_t nbatch = 0;
   me_fill* d_tape = nullptr;
   unsigned long long* d_tape_count = nullptr;
   unsigned long long* d_fills_acc = nullptr;  // fills since timing was (re)enabled
@@ -131,16 +151,24 @@ static void free_all(me_engine* e) {
   void* ptrs[] = {e->bk.levels,   e->bk.occ,      e->bk.sym,      e->bk.chunks,     e->bk.tend,
                   e->bk.loc,      e->bk.chunk_top, e->bk.err,       (void*)e->bk.gsym,
                   e->d_seq,       e->d_px,        e->d_qty,       e->d_sym,         e->d_kind,
-                  e->d_res,       e->d_fstart,    e->d_scratch,
                   e->d_tape,      e->d_tape_count, e->d_fills_acc, e->bk.dbg,      e->bk.fcache};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   {
     auto& sl = e->sb;
-    void* sp[] = {sl.keys[0], sl.keys[1], sl.idx[0], sl.idx[1], sl.hist, sl.tile_sum, sl.scratch_top,
-                  sl.tot, sl.bin_start, e->bu.cnt, e->bu.seq, e->bu.px, e->bu.qty, e->bu.ok};
+    void* sp[] = {sl.keys[0], sl.keys[1], sl.idx[0], sl.idx[1], sl.hist, sl.tot, sl.bin_start};
     for (void* p : sp)
       if (p) (void)hipFree(p);
+    for (auto& b : e->bu) {
+      void* bp[] = {b.cnt, b.seq, b.px, b.qty, b.ok};
+      for (void* p : bp)
+        if (p) (void)hipFree(p);
+    }
+    for (auto& o : e->os) {
+      void* op[] = {o.res, o.fstart, o.tile_sum, o.scratch, o.top};
+      for (void* p : op)
+        if (p) (void)hipFree(p);
+    }
   }
   for (void* p : e->user_allocs) (void)hipFree(p);
   e->user_allocs.clear();
@@ -303,22 +331,28 @@ extern "C" me_engine* me_create(const me_config* cfg) {
     ALLOC(sl.hist, (size_t)(1u << MAX_DIGIT_BITS) * ntiles_sort);
     ALLOC(sl.tot, 2u << MAX_DIGIT_BITS);
     ALLOC(sl.bin_start, (1u << MAX_DIGIT_BITS) + 1);
-    ALLOC(sl.tile_sum, ntiles_tape);
-    ALLOC(sl.scratch_top, 1);
   }
   // Register-ladder kernel: bucketed grouping when the sort key (index << 7 | slot) fits 32 bits.
   e->bucketed = L <= 128 && n < BK_MAX_BATCH;
   if (e->bucketed) {
     const size_t nb = (S + 1) * (size_t)BK_CAP;
-    ALLOC(e->bu.cnt, (S + 1) * BK_CNT_STRIDE);
-    ALLOC(e->bu.seq, nb);
-    ALLOC(e->bu.px, nb);
-    ALLOC(e->bu.qty, nb);
-    ALLOC(e->bu.ok, nb);
+    for (auto& b : e->bu) {
+      ALLOC(b.cnt, (S + 1) * BK_CNT_STRIDE);
+      ALLOC(b.seq, nb);
+      ALLOC(b.px, nb);
+      ALLOC(b.qty, nb);
+      ALLOC(b.ok, nb);
+    }
   }
-  ALLOC(e->d_res, n);
-  ALLOC(e->d_fstart, n);
-  ALLOC(e->d_scratch, ovf_base + scap);
+  e->nsets = e->bucketed ? 3 : 1;
+  for (int k = 0; k < e->nsets; ++k) {
+    auto& o = e->os[k];
+    ALLOC(o.res, n);
+    ALLOC(o.fstart, n);
+    ALLOC(o.tile_sum, ntiles_tape);
+    ALLOC(o.scratch, ovf_base + scap);
+    ALLOC(o.top, 1);
+  }
   ALLOC(bk.fcache, S * 64);
   ALLOC(e->d_tape, scap);
   ALLOC(e->d_tape_count, 1);
@@ -347,7 +381,8 @@ extern "C" me_engine* me_create(const me_config* cfg) {
     gs[i] = cfg->symbol_ids ? cfg->symbol_ids[i] : (uint32_t)i;
   }
   bool ok = launch_init_levels(st, bk.levels, S * L) == hipSuccess &&
-            (!e->bucketed || hipMemsetAsync(e->bu.cnt, 0, (S + 1) * BK_CNT_STRIDE * 4, st) == hipSuccess) &&
+            (!e->bucketed || (hipMemsetAsync(e->bu[0].cnt, 0, (S + 1) * BK_CNT_STRIDE * 4, st) == hipSuccess &&
+                              hipMemsetAsync(e->bu[1].cnt, 0, (S + 1) * BK_CNT_STRIDE * 4, st) == hipSuccess)) &&
             hipMemsetAsync(bk.occ, 0, S * (L / 64) * 8, st) == hipSuccess &&
             hipMemsetAsync(bk.tend, 0, S * L, st) == hipSuccess &&
             launch_init_chunks(st, bk.chunks, nchunks) == hipSuccess &&
@@ -378,13 +413,10 @@ extern "C" uint64_t me_fill_bound(const me_engine* e, size_t n) {
   return e ? (uint64_t)e->cfg.max_resting + 2ull * n : 0;
 }
 
-// Enqueue the whole pipeline for a device-resident batch.
-static int enqueue_batch(me_engine* e, const uint64_t* seq, const int64_t* px, const int32_t* qty,
-                         const uint32_t* sym, const uint8_t* kind, uint32_t n) {
-  hipStream_t st = e->stream;
-  auto& sl = e->sb;
-  TimedLaunch tl{};
-  const bool timed = e->timing > 0 && e->nlaunch % (uint64_t)e->timing == 0;
+// Timing bookkeeping for one match launch (every e->timing-th launch records its own start / end).
+static int timing_slot(me_engine* e, uint32_t orders, TimedLaunch& tl, bool& timed) {
+  timed = e->timing > 0 && e->nlaunch % (uint64_t)e->timing == 0;
+  tl = TimedLaunch{};
   tl.idx = e->nlaunch++;
   if (timed) {
     while (e->ev_pool.size() < e->ev_used + 2) {
@@ -394,27 +426,14 @@ static int enqueue_batch(me_engine* e, const uint64_t* seq, const int64_t* px, c
     }
     tl.m0 = e->ev_pool[e->ev_used++];
     tl.m1 = e->ev_pool[e->ev_used++];
-    tl.orders = n;
+    tl.orders = orders;
   }
-  const uint32_t S = e->bk.S;
-  const uint32_t ntiles_tape = (n + TILE_TAPE - 1) / TILE_TAPE;
-  // grouping: buckets (register-ladder kernel) or the counting sort
-  const uint32_t* kin = sym;
-  const uint32_t* iin = nullptr;
-  uint32_t* run_table = e->passes == 1 ? sl.bin_start : nullptr;
-  if (!e->bucketed) {
-    int shift = 0;
-    for (int p = 0; p < e->passes; ++p) {
-      hipError_t he = launch_sort_pass(st, kin, iin, n, S, shift, e->dbits[p], sl.hist,
-                                       sl.tot + ((size_t)p << MAX_DIGIT_BITS), sl.keys[p], sl.idx[p],
-                                       p == 0 ? sl.tile_sum : nullptr, p == 0 ? ntiles_tape : 0, sl.scratch_top,
-                                       p == e->passes - 1 ? run_table : nullptr);
-      if (he != hipSuccess) return e->hip_fail(he, "grouping sort launch");
-      kin = sl.keys[p];
-      iin = sl.idx[p];
-      shift += e->dbits[p];
-    }
-  }
+  return ME_OK;
+}
+
+static BatchDev batch_dev(me_engine* e, const uint64_t* seq, const int64_t* px, const int32_t* qty,
+                          const uint32_t* sym, const uint8_t* kind, uint32_t n, int oset) {
+  const auto& o = e->os[oset];
   BatchDev bt{};
   bt.seq = seq;
   bt.px = px;
@@ -422,36 +441,144 @@ static int enqueue_batch(me_engine* e, const uint64_t* seq, const int64_t* px, c
   bt.sym = sym;
   bt.kind = kind;
   bt.n = n;
+  bt.res = o.res;
+  bt.fstart = o.fstart;
+  bt.tile_sum = o.tile_sum;
+  bt.scratch = o.scratch;
+  bt.scratch_cap = e->scratch_cap;
+  bt.scratch_top = o.top;
+  bt.slab = e->slab;
+  bt.ovf_base = (unsigned long long)(e->bk.S + 1) * e->slab;
+  return bt;
+}
+
+// One launch of the pipelined register-ladder path: match p_match (if any), bucket nb (if any)
+// and clear its counters, compact p_tape's tape (if any) — then the pipeline shifts by one.
+static int pipe_launch(me_engine* e, const me_engine::Pend* nb) {
+  BatchDev bt{};
+  AuxDev ax{};
+  const auto& pm = e->p_match;
+  const auto& pt = e->p_tape;
+  if (pm.valid) {
+    bt = batch_dev(e, pm.seq, pm.px, pm.qty, pm.sym, pm.kind, pm.n, pm.oset);
+    const auto& b = e->bu[pm.bset];
+    bt.bcnt = b.cnt;
+    bt.b_seq = b.seq;
+    bt.b_px = b.px;
+    bt.b_qty = b.qty;
+    bt.b_ok = b.ok;
+    bt.bcap = BK_CAP;
+  }
+  if (nb) {
+    const auto& b = e->bu[nb->bset];
+    const auto& o = e->os[nb->oset];
+    ax.sym = nb->sym;
+    ax.seq = nb->seq;
+    ax.px = nb->px;
+    ax.qty = nb->qty;
+    ax.kind = nb->kind;
+    ax.n = nb->n;
+    ax.S = e->bk.S;
+    ax.bcnt = b.cnt;
+    ax.b_seq = b.seq;
+    ax.b_px = b.px;
+    ax.b_qty = b.qty;
+    ax.b_ok = b.ok;
+    ax.zero_tile_sum = o.tile_sum;
+    ax.zero_tiles = (nb->n + TILE_TAPE - 1) / TILE_TAPE;
+    ax.zero_top = o.top;
+  }
+  if (pt.valid) {
+    const auto& o = e->os[pt.oset];
+    ax.tn = pt.n;
+    ax.tile_sum = o.tile_sum;
+    ax.res = o.res;
+    ax.fstart = o.fstart;
+    ax.scratch = o.scratch;
+    ax.tape = e->d_tape;
+    ax.tape_cap = e->tape_cap;
+    ax.tape_count = e->d_tape_count;
+    ax.fills_acc = e->d_fills_acc;
+  }
+  TimedLaunch tl{};
+  bool timed = false;
+  if (pm.valid) {
+    int rc = timing_slot(e, pm.n, tl, timed);
+    if (rc) return rc;
+  }
+  hipError_t he = launch_match_reg(e->stream, e->bk, bt, ax, tl.m0, tl.m1);
+  if (he != hipSuccess) return e->hip_fail(he, "pipelined match launch");
+  if (timed) e->timed.push_back(tl);
+  e->p_tape = e->p_match;
+  e->p_match = nb ? *nb : me_engine::Pend{};
+  return ME_OK;
+}
+
+// Finish every launched batch (the last one's outputs are then final).
+static int flush_pipeline(me_engine* e) {
+  while (e->p_match.valid || e->p_tape.valid) {
+    int rc = pipe_launch(e, nullptr);
+    if (rc) return rc;
+  }
+  return ME_OK;
+}
+
+// Enqueue a device-resident batch.
+static int enqueue_batch(me_engine* e, const uint64_t* seq, const int64_t* px, const int32_t* qty,
+                         const uint32_t* sym, const uint8_t* kind, uint32_t n) {
+  if (e->bucketed) {
+    me_engine::Pend nb;
+    nb.valid = true;
+    nb.seq = seq;
+    nb.px = px;
+    nb.qty = qty;
+    nb.sym = sym;
+    nb.kind = kind;
+    nb.n = n;
+    nb.oset = (int)(e->nbatch % 3);
+    nb.bset = (int)(e->nbatch % 2);
+    e->nbatch++;
+    int rc = pipe_launch(e, &nb);
+    if (rc) return rc;
+    e->last_set = nb.oset;
+    e->last_n = n;
+    return ME_OK;
+  }
+  hipStream_t st = e->stream;
+  auto& sl = e->sb;
+  const auto& o = e->os[0];
+  TimedLaunch tl{};
+  bool timed = false;
+  int rc = timing_slot(e, n, tl, timed);
+  if (rc) return rc;
+  const uint32_t S = e->bk.S;
+  const uint32_t ntiles_tape = (n + TILE_TAPE - 1) / TILE_TAPE;
+  // grouping: the stable counting sort by symbol
+  const uint32_t* kin = sym;
+  const uint32_t* iin = nullptr;
+  uint32_t* run_table = e->passes == 1 ? sl.bin_start : nullptr;
+  int shift = 0;
+  for (int p = 0; p < e->passes; ++p) {
+    hipError_t he = launch_sort_pass(st, kin, iin, n, S, shift, e->dbits[p], sl.hist,
+                                     sl.tot + ((size_t)p << MAX_DIGIT_BITS), sl.keys[p], sl.idx[p],
+                                     p == 0 ? o.tile_sum : nullptr, p == 0 ? ntiles_tape : 0, o.top,
+                                     p == e->passes - 1 ? run_table : nullptr);
+    if (he != hipSuccess) return e->hip_fail(he, "grouping sort launch");
+    kin = sl.keys[p];
+    iin = sl.idx[p];
+    shift += e->dbits[p];
+  }
+  BatchDev bt = batch_dev(e, seq, px, qty, sym, kind, n, 0);
   bt.skeys = kin;
   bt.perm = iin;
-  bt.res = e->d_res;
-  bt.fstart = e->d_fstart;
-  bt.tile_sum = sl.tile_sum;
-  bt.scratch = e->d_scratch;
-  bt.scratch_cap = e->scratch_cap;
-  bt.scratch_top = sl.scratch_top;
-  bt.slab = e->slab;
-  bt.ovf_base = (unsigned long long)(S + 1) * e->slab;
   bt.bin_start = run_table;  // bins are symbols: the run table
-  if (e->bucketed) {
-    bt.skeys = nullptr;
-    bt.perm = nullptr;
-    bt.bin_start = nullptr;
-    bt.bcnt = e->bu.cnt;
-    bt.b_seq = e->bu.seq;
-    bt.b_px = e->bu.px;
-    bt.b_qty = e->bu.qty;
-    bt.b_ok = e->bu.ok;
-    bt.bcap = BK_CAP;
-    hipError_t he = launch_bucket(st, bt, S, sl.tile_sum, ntiles_tape, sl.scratch_top);
-    if (he != hipSuccess) return e->hip_fail(he, "bucket launch");
-  }
   // timing: the launch itself records start/end (hipExtLaunchKernelGGL), no marker packets
   hipError_t he = launch_match(st, e->bk, bt, tl.m0, tl.m1);
   if (he != hipSuccess) return e->hip_fail(he, "match launch");
   he = launch_tape(st, bt, e->d_tape, e->tape_cap, e->d_tape_count, e->d_fills_acc, e->bk.err);
   if (he != hipSuccess) return e->hip_fail(he, "tape launch");
   if (timed) e->timed.push_back(tl);
+  e->last_set = 0;
   e->last_n = n;
   return ME_OK;
 }
@@ -485,6 +612,10 @@ extern "C" int me_submit_batch_device(me_engine* e, const me_order_soa* b, size_
 extern "C" int me_sync(me_engine* e) {
   if (!e) return ME_E_INVALID;
   HIP_TRY(hipSetDevice(e->dev), "hipSetDevice");
+  if (!e->failed) {
+    int rc = flush_pipeline(e);
+    if (rc) return rc;
+  }
   HIP_TRY(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
   if (e->failed) return ME_E_STATE;
   return check_err_word(e);
@@ -500,7 +631,7 @@ extern "C" int me_fetch_outputs(me_engine* e, me_fill* out_fills, size_t fills_c
   if (n_fills) *n_fills = (size_t)cnt;
   if (out_results && n_results) {
     if (n_results > e->last_n) return e->fail(ME_E_INVALID, "n_results exceeds last batch size");
-    HIP_TRY(hipMemcpy(out_results, e->d_res, n_results * sizeof(me_order_result), hipMemcpyDeviceToHost),
+    HIP_TRY(hipMemcpy(out_results, e->os[e->last_set].res, n_results * sizeof(me_order_result), hipMemcpyDeviceToHost),
             "D2H results");
   }
   if (out_fills && cnt) {
@@ -522,7 +653,10 @@ extern "C" int me_submit_batch(me_engine* e, const me_order_soa* b, size_t n, me
   if (!b || !b->seq || !b->price_q4 || !b->qty || !b->symbol || !b->kind) return e->fail(ME_E_INVALID, "null batch");
   if (n > e->cfg.max_batch) return e->fail(ME_E_INVALID, "batch larger than max_batch");
   HIP_TRY(hipSetDevice(e->dev), "hipSetDevice");
-  HIP_TRY(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
+  {  // nothing launched may still read the staging buffers
+    int rc = me_sync(e);
+    if (rc) return rc;
+  }
   // stage into pinned memory, one H2D per column
   char* p = (char*)e->h_pin;
   uint64_t* hs = (uint64_t*)p;
@@ -565,8 +699,13 @@ extern "C" int me_copy_results_device(me_engine* e, void* dst, size_t n_results)
   if (n_results > e->last_n) return e->fail(ME_E_INVALID, "n_results exceeds last batch size");
   if (n_results && !dst) return e->fail(ME_E_INVALID, "null destination");
   HIP_TRY(hipSetDevice(e->dev), "hipSetDevice");
+  {
+    int rc = flush_pipeline(e);
+    if (rc) return rc;
+  }
   if (n_results)
-    HIP_TRY(hipMemcpyAsync(dst, e->d_res, n_results * sizeof(me_order_result), hipMemcpyDeviceToDevice, e->stream),
+    HIP_TRY(hipMemcpyAsync(dst, e->os[e->last_set].res, n_results * sizeof(me_order_result), hipMemcpyDeviceToDevice,
+                           e->stream),
             "D2D results");
   return ME_OK;
 }
@@ -599,6 +738,10 @@ extern "C" int me_memcpy_h2d(me_engine* e, void* dst, const void* src, size_t by
 
 extern "C" int me_set_stream(me_engine* e, void* s) {
   if (!e) return ME_E_INVALID;
+  if (!e->failed) {
+    int rc = flush_pipeline(e);
+    if (rc) return rc;
+  }
   HIP_TRY(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
   e->stream = s ? (hipStream_t)s : e->own_stream;
   return ME_OK;
@@ -711,6 +854,10 @@ extern "C" int me_resting_count(me_engine* e, uint64_t* n) {
 
 extern "C" int me_timing_enable(me_engine* e, int enable) {
   if (!e) return ME_E_INVALID;
+  if (!e->failed) {
+    int rc = flush_pipeline(e);
+    if (rc) return rc;
+  }
   HIP_TRY(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
   e->timed.clear();
   e->ev_used = 0;
@@ -724,6 +871,10 @@ extern "C" int me_timing_enable(me_engine* e, int enable) {
 extern "C" int me_timing_read(me_engine* e, double* match_ms, double* pipeline_ms, uint64_t* launches,
                               uint64_t* fills, uint64_t* orders) {
   if (!e) return ME_E_INVALID;
+  if (!e->failed) {
+    int rc = flush_pipeline(e);
+    if (rc) return rc;
+  }
   HIP_TRY(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
   double m = 0, p = 0;
   uint64_t o = 0;

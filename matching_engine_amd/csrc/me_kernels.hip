@@ -1347,48 +1347,8 @@ hipError_t launch_sort_pass(hipStream_t st, const uint32_t* keys_in, const uint3
   return hipGetLastError();
 }
 
-// Bucketed grouping (register-ladder path): one record per thread, one returning atomic on its
-// bin's counter gives it a bucket slot (arbitrary order — k_match_reg restores batch order on
-// chip), and the record is copied into the bucket so the matching kernel reads its symbol's
-// records contiguously with no permutation round trip. Also the per-batch resets.
-__global__ __launch_bounds__(256) void k_bucket(const uint32_t* __restrict__ sym, const uint64_t* __restrict__ seq,
-                                                const int64_t* __restrict__ px, const int32_t* __restrict__ qty,
-                                                const uint8_t* __restrict__ kind, uint32_t n, uint32_t S,
-                                                uint32_t cap, uint32_t* bcnt, uint64_t* __restrict__ b_seq,
-                                                int64_t* __restrict__ b_px, int32_t* __restrict__ b_qty,
-                                                uint32_t* __restrict__ b_ok, uint32_t* zero_buf, uint32_t zero_words,
-                                                unsigned long long* scratch_top) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < zero_words) zero_buf[i] = 0;
-  if (i == 0) *scratch_top = 0ull;
-  if (i >= n) return;
-  const uint32_t b = min(sym[i], S);
-  // the payload loads are in flight while the atomic returns
-  const uint64_t sq = seq[i];
-  const int64_t p = px[i];
-  const int32_t q = qty[i];
-  const uint32_t k = kind[i];
-  const uint32_t r = atomicAdd(&bcnt[(size_t)b * BK_CNT_STRIDE], 1u);
-  if (r < cap) {
-    const size_t d = (size_t)b * cap + r;
-    b_seq[d] = sq;
-    b_px[d] = p;
-    b_qty[d] = q;
-    b_ok[d] = i | ((k & 15u) << BK_KIND_SHIFT);
-  }
-}
-
-hipError_t launch_bucket(hipStream_t st, const BatchDev& bt, uint32_t S, uint32_t* zero_buf, uint32_t zero_words,
-                         unsigned long long* scratch_top) {
-  const uint32_t work = max(bt.n, max(zero_words, 1u));
-  hipLaunchKernelGGL(k_bucket, dim3((work + 255) / 256), dim3(256), 0, st, bt.sym, bt.seq, bt.px, bt.qty, bt.kind,
-                     bt.n, S, bt.bcap, bt.bcnt, const_cast<uint64_t*>(bt.b_seq), const_cast<int64_t*>(bt.b_px),
-                     const_cast<int32_t*>(bt.b_qty), const_cast<uint32_t*>(bt.b_ok), zero_buf, zero_words,
-                     scratch_top);
-  return hipGetLastError();
-}
-
-hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev& bt, hipEvent_t ev0, hipEvent_t ev1);
+hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev& bt, const AuxDev& ax, hipEvent_t ev0,
+                            hipEvent_t ev1);
 
 // ev0 / ev1 (optional, timing): the launch records the kernel's own start and end
 // (hipExtLaunchKernelGGL), so timing adds no marker packet — and no gap — to the stream.
@@ -1396,7 +1356,7 @@ hipError_t launch_match(hipStream_t st, const BookDev& bk, const BatchDev& bt, h
   const uint32_t waves = bk.S + 1;
   const dim3 grid((waves + 3) / 4), block(256);
   if (bk.L <= 128) {
-    return launch_match_reg(st, bk, bt, ev0, ev1);
+    return launch_match_reg(st, bk, bt, AuxDev{}, ev0, ev1);
   } else if (bk.L <= LDS_MAX_LEVELS) {
     hipExtLaunchKernelGGL(k_match<LAD_LDS>, grid, block, 4 * lds_wave_bytes(bk.L), st, ev0, ev1, 0, bk, bt);
   } else {

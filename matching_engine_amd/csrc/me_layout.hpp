@@ -127,6 +127,39 @@ struct BatchDev {
   const uint32_t* b_ok;  // batch index | (kind & 15) << BK_KIND_SHIFT
   uint32_t bcap;
 };
+// Side jobs of one pipelined register-ladder launch (me_match_reg.hip), run by each workgroup's
+// extra waves while its matching waves work on batch b-1: group batch b into its buckets, clear
+// the counters batch b will use, compact the tape of batch b-2. A job with zero records is off.
+struct AuxDev {
+  // bucket job: batch b
+  const uint32_t* sym;
+  const uint64_t* seq;
+  const int64_t* px;
+  const int32_t* qty;
+  const uint8_t* kind;
+  uint32_t n;
+  uint32_t S;
+  uint32_t* bcnt;
+  uint64_t* b_seq;
+  int64_t* b_px;
+  int32_t* b_qty;
+  uint32_t* b_ok;
+  // clear job: the output set batch b will use
+  uint32_t* zero_tile_sum;
+  uint32_t zero_tiles;
+  unsigned long long* zero_top;
+  // tape job: batch b-2
+  uint32_t tn;
+  const uint32_t* tile_sum;
+  me_order_result* res;
+  const uint32_t* fstart;
+  const me_fill* scratch;
+  me_fill* tape;
+  unsigned long long tape_cap;
+  unsigned long long* tape_count;
+  unsigned long long* fills_acc;
+};
+
 constexpr int BK_CAP = 128;          // records per bucket (two 64-record blocks)
 constexpr int BK_KIND_SHIFT = 28;    // b_ok: kind bits above the batch index
 constexpr uint32_t BK_IDX_MASK = (1u << BK_KIND_SHIFT) - 1u;

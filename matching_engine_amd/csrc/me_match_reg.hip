@@ -72,7 +72,7 @@ struct RegLds {
     uint32_t lst[1024];  // rescan: batch indices of the symbol's records in one 1024-record window
   } in;
 };
-constexpr int REG_WAVES = 4;  // waves (symbols) per workgroup
+constexpr int REG_WAVES = 4;  // matching waves (symbols) per workgroup; as many side-job waves follow
 constexpr int VMCNT0 = 0x0F70;  // s_waitcnt immediate: vmcnt(0), expcnt / lgkmcnt untouched (gfx9 encoding)
 
 // One 32-bit field of the 128-level ladder: level l is lane (l & 63) of row (l >> 6).
@@ -130,6 +130,7 @@ struct Mask2 {
 struct ColdArgs {
   BookDev bk;
   BatchDev bt;
+  AuxDev ax;
 };
 
 // Global-address-space (1) pointers: an opaque round trip (vreg64, ldsu) would otherwise leave a
@@ -694,16 +695,134 @@ __device__ __forceinline__ void reject_bad_bucket(RegLds* M, const ColdArgs& G, 
   }
 }
 
+// ---- side jobs of a pipelined launch (the workgroup's waves REG_WAVES .. 2*REG_WAVES-1) -------
+// Memory-latency work with few instructions, so sharing the SIMDs with the matching waves costs
+// them little; what it saves is two launches per batch.
+
+// Bucket job: records [r0, r1) of batch b, one returning atomic per record on its bin's counter.
+__device__ __forceinline__ void aux_bucket(const ColdArgs& G, uint32_t r0, uint32_t r1) {
+  const int lane = lane_id();
+  const gptr<const uint32_t> sym = ldsg(G.ax.sym);
+  const gptr<const uint64_t> seq = ldsg(G.ax.seq);
+  const gptr<const int64_t> px = ldsg(G.ax.px);
+  const gptr<const int32_t> qty = ldsg(G.ax.qty);
+  const gptr<const uint8_t> kind = ldsg(G.ax.kind);
+  const gptr<uint32_t> bcnt = ldsg(G.ax.bcnt);
+  const gptr<uint64_t> bseq = ldsg(G.ax.b_seq);
+  const gptr<int64_t> bpx = ldsg(G.ax.b_px);
+  const gptr<int32_t> bqty = ldsg(G.ax.b_qty);
+  const gptr<uint32_t> bok = ldsg(G.ax.b_ok);
+  const uint32_t S = ldsu(G.ax.S);
+  for (uint32_t i0 = r0; i0 < r1; i0 += 64) {
+    const uint32_t i = i0 + (uint32_t)lane;
+    if (i < r1) {
+      const uint32_t b = min(sym[i], S);
+      const uint64_t sq = seq[i];  // the payload loads are in flight while the atomic returns
+      const int64_t p = px[i];
+      const int32_t q = qty[i];
+      const uint32_t k = kind[i];
+      const uint32_t r = atomicAdd(&bcnt[(size_t)b * BK_CNT_STRIDE], 1u);
+      if (r < (uint32_t)BK_CAP) {
+        const size_t d = (size_t)b * BK_CAP + r;
+        bseq[d] = sq;
+        bpx[d] = p;
+        bqty[d] = q;
+        bok[d] = i | ((k & 15u) << BK_KIND_SHIFT);
+      }
+    }
+  }
+}
+
+// Tape job, one TILE_TAPE-record tile of batch b-2 per wave: tape offsets of its records and the
+// copy of their fills from scratch into the tape (ordered by taker seq).
+__device__ __forceinline__ void aux_tape_tile(const ColdArgs& G, uint32_t* off, uint32_t t, uint32_t ntiles,
+                                              uint32_t tn) {
+  const int lane = lane_id();
+  const gptr<const uint32_t> tile_sum = ldsg(G.ax.tile_sum);
+  const gptr<me_order_result> res = ldsg(G.ax.res);
+  const gptr<const uint32_t> fstart = ldsg(G.ax.fstart);
+  const gptr<const me_fill> scratch = ldsg(G.ax.scratch);
+  const gptr<me_fill> tape = ldsg(G.ax.tape);
+  long long acc = 0;  // fills of the earlier tiles
+  for (uint32_t u = (uint32_t)lane; u < t; u += 64) acc += tile_sum[u];
+  for (int d = 32; d >= 1; d >>= 1) acc += __shfl_xor(acc, d, 64);
+  const unsigned long long base = (unsigned long long)rli64(acc, 0);
+  const uint32_t r0 = t * TILE_TAPE;
+  const uint32_t cnt = min((uint32_t)TILE_TAPE, tn - r0);
+  uint32_t c[TILE_TAPE / 64];
+  long long loc = 0;
+#pragma unroll
+  for (int k = 0; k < TILE_TAPE / 64; ++k) {  // lane holds records 4*lane .. 4*lane+3 of the tile
+    const uint32_t j = (uint32_t)(lane * (TILE_TAPE / 64) + k);
+    c[k] = j < cnt ? res[r0 + j].fill_count : 0u;
+    loc += c[k];
+  }
+  const long long incl = wave_incl_scan(loc);
+  const uint32_t total = (uint32_t)rli64(incl, 63);
+  uint32_t o = (uint32_t)(incl - loc);
+#pragma unroll
+  for (int k = 0; k < TILE_TAPE / 64; ++k) {
+    const uint32_t j = (uint32_t)(lane * (TILE_TAPE / 64) + k);
+    off[j] = j < cnt ? o : total;
+    if (j < cnt) res[r0 + j].tape_offset = (uint32_t)(base + o);
+    o += c[k];
+  }
+  if (lane == 0) off[TILE_TAPE] = total;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  if (base + total > ldsu(G.ax.tape_cap)) {
+    if (lane == 0) atomicOr(ldsg(G.bk.err), ERR_SCRATCH_OOM);
+    return;
+  }
+  for (uint32_t f = (uint32_t)lane; f < total; f += 64) {
+    uint32_t lo = 0, hi = cnt;  // last k with off[k] <= f: off[lo] <= f < off[hi]
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (off[mid] <= f)
+        lo = mid;
+      else
+        hi = mid;
+    }
+    tape[base + f] = scratch[fstart[r0 + lo] + (f - off[lo])];
+  }
+  if (t == ntiles - 1 && lane == 0) {
+    *ldsg(G.ax.tape_count) = base + total;
+    atomicAdd(ldsg(G.ax.fills_acc), base + total);
+  }
+}
+
+__device__ __forceinline__ void aux_jobs(const ColdArgs& G, uint32_t* off, uint32_t a, uint32_t A) {
+  const int lane = lane_id();
+  const uint32_t zt = ldsu(G.ax.zero_tiles);
+  if (zt) {
+    const gptr<uint32_t> z = ldsg(G.ax.zero_tile_sum);
+    for (uint32_t i = a * 64u + (uint32_t)lane; i < zt; i += A * 64u) z[i] = 0u;
+    if (a == 0 && lane == 0) *ldsg(G.ax.zero_top) = 0ull;
+  }
+  const uint32_t n = ldsu(G.ax.n);
+  if (n) {
+    const uint32_t per = (((n + A - 1u) / A) + 63u) & ~63u;
+    const uint32_t r0 = min(n, a * per);
+    aux_bucket(G, r0, min(n, r0 + per));
+  }
+  const uint32_t tn = ldsu(G.ax.tn);
+  if (tn) {
+    const uint32_t ntiles = (tn + TILE_TAPE - 1) / TILE_TAPE;
+    for (uint32_t t = a; t < ntiles; t += A) aux_tape_tile(G, off, t, ntiles, tn);
+  }
+}
+
 // ---- the kernel ----------------------------------------------------------------------------
 // Per-record control word built in vector form: lim level | BUY | MARKET | CANCEL.
 constexpr uint32_t CW_BUY = 1u << 8, CW_MKT = 1u << 9, CW_CXL = 1u << 10;
 
-__global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
+__global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(BookDev bk, BatchDev bt, AuxDev ax) {
   __shared__ RegLds lds[REG_WAVES];
+  __shared__ uint32_t aux_off[REG_WAVES][TILE_TAPE + 1];
   __shared__ ColdArgs G;
-  static_assert(sizeof(ColdArgs) % 8 == 0 && sizeof(ColdArgs) <= 8 * 256, "ColdArgs copy");
+  static_assert(sizeof(ColdArgs) % 8 == 0 && sizeof(ColdArgs) <= 8 * 64 * REG_WAVES, "ColdArgs copy");
   {
-    const ColdArgs a{bk, bt};
+    const ColdArgs a{bk, bt, ax};
     if (threadIdx.x < sizeof(ColdArgs) / 8)
       reinterpret_cast<unsigned long long*>(&G)[threadIdx.x] =
           reinterpret_cast<const unsigned long long*>(&a)[threadIdx.x];
@@ -713,8 +832,13 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
   // wave index: readfirstlane tells the divergence analysis it is wave-uniform (threadIdx.x >> 6 is
   // not recognised as such), so every per-symbol value and branch below is scalar
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (wv >= (uint32_t)REG_WAVES) {  // side-job wave
+    const uint32_t k = wv - REG_WAVES;
+    aux_jobs(G, aux_off[k], blockIdx.x * REG_WAVES + k, gridDim.x * REG_WAVES);
+    return;
+  }
   const uint32_t s = blockIdx.x * REG_WAVES + wv;
-  if (s > bk.S) return;
+  if (bt.n == 0u || s > bk.S) return;  // no match job in this launch / no symbol
 #ifdef ME_STAMPS
   unsigned long long st_t0 = stamp_now();
 #endif
@@ -1059,11 +1183,16 @@ __global__ __launch_bounds__(256) void k_match_reg(BookDev bk, BatchDev bt) {
 #endif
 }
 
-hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev& bt, hipEvent_t ev0, hipEvent_t ev1) {
+// One launch: the match job of bt (bt.n == 0: none) on (S + 1) / REG_WAVES workgroups and the side
+// jobs of ax on every workgroup's extra waves (at least ~256 side-job records per wave).
+hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev& bt, const AuxDev& ax, hipEvent_t ev0,
+                            hipEvent_t ev1) {
   if (bk.L > (uint32_t)RL || bk.L < 64u || !bk.fcache || !bk.gsym) return hipErrorInvalidValue;
-  const uint32_t waves = bk.S + 1;
-  hipExtLaunchKernelGGL(k_match_reg, dim3((waves + REG_WAVES - 1) / REG_WAVES), dim3(64 * REG_WAVES), 0, st, ev0,
-                        ev1, 0, bk, bt);
+  const uint32_t match_wgs = bt.n ? (bk.S + 1 + REG_WAVES - 1) / REG_WAVES : 0u;
+  const uint32_t work = max(ax.n, ax.tn);
+  const uint32_t aux_wgs = (work + 256u * REG_WAVES - 1) / (256u * REG_WAVES);
+  const uint32_t grid = max(max(match_wgs, aux_wgs), 1u);
+  hipExtLaunchKernelGGL(k_match_reg, dim3(grid), dim3(128 * REG_WAVES), 0, st, ev0, ev1, 0, bk, bt, ax);
   return hipGetLastError();
 }
 
