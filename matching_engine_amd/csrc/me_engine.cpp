@@ -104,6 +104,7 @@ struct me_engine {
     int oset = 0, bset = 0;
   } p_match, p_tape;
   uint64_t nbatch = 0;
+  uint32_t ncu = 0;  // compute units: workgroups of one dispatch round host the side jobs
   me_fill* d_tape = nullptr;
   unsigned long long* d_tape_count = nullptr;
   unsigned long long* d_fills_acc = nullptr;  // fills since timing was (re)enabled
@@ -290,6 +291,12 @@ extern "C" me_engine* me_create(const me_config* cfg) {
   if (n >= 0x7FFFFFFFull) return bail("me_create: max_batch too large");
   he = hipSetDevice(e->dev);
   if (he != hipSuccess) return bail(std::string("hipSetDevice: ") + hipGetErrorString(he));
+  {
+    int ncu = 0;
+    he = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, e->dev);
+    if (he != hipSuccess) return bail(std::string("hipDeviceGetAttribute: ") + hipGetErrorString(he));
+    e->ncu = (uint32_t)(ncu > 0 ? ncu : 1);
+  }
   he = hipStreamCreateWithFlags(&e->own_stream, hipStreamNonBlocking);
   if (he != hipSuccess) return bail(std::string("hipStreamCreate: ") + hipGetErrorString(he));
   e->stream = e->own_stream;
@@ -484,6 +491,8 @@ static int pipe_launch(me_engine* e, const me_engine::Pend* nb) {
     ax.b_px = b.px;
     ax.b_qty = b.qty;
     ax.b_ok = b.ok;
+    ax.bres = o.res;
+    ax.bfstart = o.fstart;
     ax.zero_tile_sum = o.tile_sum;
     ax.zero_tiles = (nb->n + TILE_TAPE - 1) / TILE_TAPE;
     ax.zero_top = o.top;
@@ -500,6 +509,7 @@ static int pipe_launch(me_engine* e, const me_engine::Pend* nb) {
     ax.tape_count = e->d_tape_count;
     ax.fills_acc = e->d_fills_acc;
   }
+  ax.nwg = e->ncu;
   TimedLaunch tl{};
   bool timed = false;
   if (pm.valid) {

@@ -28,7 +28,7 @@ namespace me {
 constexpr int ME_C = 16;                 // slots per chunk (one wave-load of qty + seq)
 constexpr uint32_t NIL = 0xFFFFFFFFu;
 constexpr int MAX_SORT_TILES = 256;      // sort tiles per pass (tile = records / workgroup >= 1024)
-constexpr int TILE_TAPE = 256;           // records per workgroup in the tape compaction
+constexpr int TILE_TAPE = 64;            // records per tape tile (one side-job wave, or one k_tape_compact workgroup)
 constexpr int MAX_DIGIT_BITS = 11;       // radix digit width (LDS histogram of 2048 bins)
 constexpr uint32_t LDS_MAX_LEVELS = 1024; // ladders up to this depth are staged in LDS (17.5 KB/wave)
 
@@ -144,6 +144,9 @@ struct AuxDev {
   int64_t* b_px;
   int32_t* b_qty;
   uint32_t* b_ok;
+  me_order_result* bres;  // batch b's results: unknown-symbol records are rejected by the bucket job
+  uint32_t* bfstart;
+  uint32_t nwg;           // workgroups that run side jobs (those of the first dispatch round)
   // clear job: the output set batch b will use
   uint32_t* zero_tile_sum;
   uint32_t zero_tiles;

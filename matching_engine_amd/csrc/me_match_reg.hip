@@ -664,6 +664,18 @@ __device__ __forceinline__ bool rescan_window(RegLds* M, const ColdArgs& G, uint
   return false;
 }
 
+__device__ __forceinline__ void reject_bad_at(gptr<me_order_result> res, gptr<uint32_t> fstart, uint32_t i) {
+  me_order_result r;
+  r.filled_qty = 0;
+  r.remaining_qty = 0;
+  r.fill_count = 0;
+  r.tape_offset = 0;
+  r.status = ME_ST_REJECTED;
+  r.reason = ME_RJ_BAD_SYMBOL;
+  r.pad[0] = r.pad[1] = 0;
+  res[i] = r;
+  fstart[i] = 0;
+}
 __device__ __forceinline__ void reject_bad(const ColdArgs& G, uint32_t i, bool v) {
   if (!v) return;
   me_order_result r;
@@ -713,10 +725,16 @@ __device__ __forceinline__ void aux_bucket(const ColdArgs& G, uint32_t r0, uint3
   const gptr<int32_t> bqty = ldsg(G.ax.b_qty);
   const gptr<uint32_t> bok = ldsg(G.ax.b_ok);
   const uint32_t S = ldsu(G.ax.S);
+  const gptr<me_order_result> bres = ldsg(G.ax.bres);
+  const gptr<uint32_t> bfst = ldsg(G.ax.bfstart);
   for (uint32_t i0 = r0; i0 < r1; i0 += 64) {
     const uint32_t i = i0 + (uint32_t)lane;
     if (i < r1) {
       const uint32_t b = min(sym[i], S);
+      if (b == S) {  // unknown symbol: rejected here, never bucketed (batch b's result set is free)
+        reject_bad_at(bres, bfst, i);
+        continue;
+      }
       const uint64_t sq = seq[i];  // the payload loads are in flight while the atomic returns
       const int64_t p = px[i];
       const int32_t q = qty[i];
@@ -735,8 +753,7 @@ __device__ __forceinline__ void aux_bucket(const ColdArgs& G, uint32_t r0, uint3
 
 // Tape job, one TILE_TAPE-record tile of batch b-2 per wave: tape offsets of its records and the
 // copy of their fills from scratch into the tape (ordered by taker seq).
-__device__ __forceinline__ void aux_tape_tile(const ColdArgs& G, uint32_t* off, uint32_t t, uint32_t ntiles,
-                                              uint32_t tn) {
+__device__ __forceinline__ void aux_tape_tile(const ColdArgs& G, uint32_t t, uint32_t ntiles, uint32_t tn) {
   const int lane = lane_id();
   const gptr<const uint32_t> tile_sum = ldsg(G.ax.tile_sum);
   const gptr<me_order_result> res = ldsg(G.ax.res);
@@ -763,27 +780,23 @@ __device__ __forceinline__ void aux_tape_tile(const ColdArgs& G, uint32_t* off, 
 #pragma unroll
   for (int k = 0; k < TILE_TAPE / 64; ++k) {
     const uint32_t j = (uint32_t)(lane * (TILE_TAPE / 64) + k);
-    off[j] = j < cnt ? o : total;
     if (j < cnt) res[r0 + j].tape_offset = (uint32_t)(base + o);
     o += c[k];
   }
-  if (lane == 0) off[TILE_TAPE] = total;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
   if (base + total > ldsu(G.ax.tape_cap)) {
     if (lane == 0) atomicOr(ldsg(G.bk.err), ERR_SCRATCH_OOM);
     return;
   }
-  for (uint32_t f = (uint32_t)lane; f < total; f += 64) {
-    uint32_t lo = 0, hi = cnt;  // last k with off[k] <= f: off[lo] <= f < off[hi]
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (off[mid] <= f)
-        lo = mid;
-      else
-        hi = mid;
+  // each lane copies the fills of its own records (scratch runs are contiguous per record)
+  uint32_t o2 = (uint32_t)(incl - loc);
+#pragma unroll
+  for (int k = 0; k < TILE_TAPE / 64; ++k) {
+    const uint32_t j = (uint32_t)(lane * (TILE_TAPE / 64) + k);
+    if (c[k]) {
+      const uint32_t src = fstart[r0 + j];
+      for (uint32_t q = 0; q < c[k]; ++q) tape[base + o2 + q] = scratch[src + q];
     }
-    tape[base + f] = scratch[fstart[r0 + lo] + (f - off[lo])];
+    o2 += c[k];
   }
   if (t == ntiles - 1 && lane == 0) {
     *ldsg(G.ax.tape_count) = base + total;
@@ -791,7 +804,7 @@ __device__ __forceinline__ void aux_tape_tile(const ColdArgs& G, uint32_t* off, 
   }
 }
 
-__device__ __forceinline__ void aux_jobs(const ColdArgs& G, uint32_t* off, uint32_t a, uint32_t A) {
+__device__ __forceinline__ void aux_jobs(const ColdArgs& G, uint32_t a, uint32_t A) {
   const int lane = lane_id();
   const uint32_t zt = ldsu(G.ax.zero_tiles);
   if (zt) {
@@ -808,7 +821,7 @@ __device__ __forceinline__ void aux_jobs(const ColdArgs& G, uint32_t* off, uint3
   const uint32_t tn = ldsu(G.ax.tn);
   if (tn) {
     const uint32_t ntiles = (tn + TILE_TAPE - 1) / TILE_TAPE;
-    for (uint32_t t = a; t < ntiles; t += A) aux_tape_tile(G, off, t, ntiles, tn);
+    for (uint32_t t = a; t < ntiles; t += A) aux_tape_tile(G, t, ntiles, tn);
   }
 }
 
@@ -818,7 +831,6 @@ constexpr uint32_t CW_BUY = 1u << 8, CW_MKT = 1u << 9, CW_CXL = 1u << 10;
 
 __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(BookDev bk, BatchDev bt, AuxDev ax) {
   __shared__ RegLds lds[REG_WAVES];
-  __shared__ uint32_t aux_off[REG_WAVES][TILE_TAPE + 1];
   __shared__ ColdArgs G;
   static_assert(sizeof(ColdArgs) % 8 == 0 && sizeof(ColdArgs) <= 8 * 64 * REG_WAVES, "ColdArgs copy");
   {
@@ -832,9 +844,9 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(BookDev bk, Batch
   // wave index: readfirstlane tells the divergence analysis it is wave-uniform (threadIdx.x >> 6 is
   // not recognised as such), so every per-symbol value and branch below is scalar
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (wv >= (uint32_t)REG_WAVES) {  // side-job wave
-    const uint32_t k = wv - REG_WAVES;
-    aux_jobs(G, aux_off[k], blockIdx.x * REG_WAVES + k, gridDim.x * REG_WAVES);
+  if (wv >= (uint32_t)REG_WAVES) {  // side-job wave (only in the workgroups of the first dispatch round)
+    const uint32_t k = wv - REG_WAVES, nwg = max(min(ax.nwg, gridDim.x), 1u);
+    if (blockIdx.x < nwg) aux_jobs(G, blockIdx.x * REG_WAVES + k, nwg * REG_WAVES);
     return;
   }
   const uint32_t s = blockIdx.x * REG_WAVES + wv;
@@ -1188,7 +1200,9 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(BookDev bk, Batch
 hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev& bt, const AuxDev& ax, hipEvent_t ev0,
                             hipEvent_t ev1) {
   if (bk.L > (uint32_t)RL || bk.L < 64u || !bk.fcache || !bk.gsym) return hipErrorInvalidValue;
-  const uint32_t match_wgs = bt.n ? (bk.S + 1 + REG_WAVES - 1) / REG_WAVES : 0u;
+  // bucketed batches carry no bad-symbol bin (the bucket job rejects those records)
+  const uint32_t waves = bt.bcnt ? bk.S : bk.S + 1;
+  const uint32_t match_wgs = bt.n ? (waves + REG_WAVES - 1) / REG_WAVES : 0u;
   const uint32_t work = max(ax.n, ax.tn);
   const uint32_t aux_wgs = (work + 256u * REG_WAVES - 1) / (256u * REG_WAVES);
   const uint32_t grid = max(max(match_wgs, aux_wgs), 1u);
