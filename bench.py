@@ -6,11 +6,12 @@ synthetic stream (80% LIMIT at mid +-32 ticks / 20% MARKET, qty U[1,100]), 65,53
 per GPU. With N GPUs the global stream has 1,024*N symbols and 65,536*N-order batches,
 hash-sharded by symbol (splitmix64(symbol) % N) with no cross-GPU matching: weak scaling.
 
-One step = one batch through the whole device pipeline (group-by-symbol sort -> match ->
-tape compaction) with the batch already resident in HBM. W warmup steps, then K timed steps
-bracketed by barrier + device sync; the max over ranks is the job time.
+One step = one batch through the whole device pipeline (bucket by symbol -> match -> tape
+compaction; L > 128: sort -> match -> compaction) with the batch already resident in HBM. W warmup
+steps, then K timed steps bracketed by barrier + device sync; the max over ranks is the job time.
+--workload c3|c4|c5 runs the other BASELINE configs as secondary lines (same JSON shape).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c4|c5]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 """
 from __future__ import annotations
@@ -33,13 +34,37 @@ BYTES_PER_ORDER = 48   # 32 B record read + 16 B resting insert / cancel (SURVEY
 BYTES_PER_FILL = 48    # 32 B tape record + 16 B maker-slot RMW
 
 
+# Per-workload shape. Weak scaling: symbols and batch grow with N, except config 4
+# whose 100k Zipf symbols are global (symbol 0 alone draws ~13 % of the stream at every N).
+WORKLOADS = {
+    "c2": dict(preset=2, symbols_per_gpu=1024, batch_per_gpu=65536,
+               text="BASELINE configs[1]: 1,024 symbols/GPU x uniform stream, 65,536-order batches/GPU, "
+                    "80% LIMIT +-32 ticks / 20% MARKET, qty U[1,100]"),
+    "c3": dict(preset=3, symbols_per_gpu=12500, batch_per_gpu=131072,
+               text="BASELINE configs[2] per-GPU share: 12,500 symbols/GPU (100k at N=8), 131,072-order "
+                    "batches/GPU (1M at N=8), uniform stream, hash-sharded"),
+    "c4": dict(preset=4, symbols=100_000, batch_per_gpu=65536, seeded=1000, per_side=10_000,
+               text="BASELINE configs[3]: Zipf(1.1) popularity over 100k symbols, L=32,768-level windows, "
+                    "LIMIT +-5,000 ticks; the 1,000 most popular books pre-seeded to 10,000 levels/side "
+                    "(20M resting orders) before warmup"),
+    "c5": dict(preset=5, symbols_per_gpu=1024, batch_per_gpu=65536,
+               text="BASELINE configs[4]: 1,024 symbols/GPU, 60% cancels of live orders, 25% LIMIT, "
+                    "15% MARKET sweeping U[1,20] x 100 qty"),
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--symbols-per-gpu", type=int, default=1024)
-    ap.add_argument("--batch-per-gpu", type=int, default=65536)
+    ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS),
+                    help="c2 (default) = BASELINE configs[1], the metric's workload; c3/c4/c5 = the other "
+                         "BASELINE configs as secondary lines (DESIGN.md §7)")
+    ap.add_argument("--symbols-per-gpu", type=int, default=None)
+    ap.add_argument("--batch-per-gpu", type=int, default=None)
+    ap.add_argument("--batches-per-launch", type=int, default=0,
+                    help="batches matched per kernel launch (me_config.batches_per_launch; 0 = engine default 8)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
@@ -53,7 +78,18 @@ def parse():
                          "(reported beside value, never in it)")
     ap.add_argument("--traffic-from", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="JSON {bytes_per_launch: ...} from tools/pmc_traffic.py for roofline.traffic")
-    return ap.parse_args()
+    args = ap.parse_args()
+    w = WORKLOADS[args.workload]
+    if args.symbols_per_gpu is None:
+        args.symbols_per_gpu = w.get("symbols_per_gpu", 0)
+    if args.batch_per_gpu is None:
+        args.batch_per_gpu = w["batch_per_gpu"]
+    return args
+
+
+def global_symbols(args, world):
+    w = WORKLOADS[args.workload]
+    return w["symbols"] if "symbols" in w else args.symbols_per_gpu * world
 
 
 def dist_setup(args):
@@ -101,12 +137,21 @@ def allreduce(v, world, op, local):
 def build_rank_batches(args, world, rank, nbatches):
     """Global stream, hash-sharded; this rank's batches with local symbol ids (and, per batch, the
     positions of its records in the global batch)."""
-    S = args.symbols_per_gpu * world
-    sc = me.preset(2, num_symbols=S, batch=args.batch_per_gpu * world)
+    w = WORKLOADS[args.workload]
+    S = global_symbols(args, world)
+    sc = me.preset(w["preset"], num_symbols=S, batch=args.batch_per_gpu * world)
     st = me.Stream(sc)
     base = st.base_prices()
     shard, local, members = me.shard_table(S, world)
     ids = members[rank]
+    seeds = []
+    if w.get("seeded"):  # config 4: deep pre-seeded books of the most popular symbols (not timed)
+        sb = st.seed_books(range(w["seeded"]), w["per_side"])
+        sel = np.nonzero(shard[sb.symbol] == rank)[0]
+        sb = sb.take(sel)
+        sb.symbol = np.ascontiguousarray(local[sb.symbol], dtype=np.uint32)
+        step = 1 << 20
+        seeds = [sb.take(slice(i, i + step)) for i in range(0, len(sb), step)]
     out, pos = [], []
     for _ in range(nbatches):
         b = st.next(sc.batch)
@@ -115,7 +160,7 @@ def build_rank_batches(args, world, rank, nbatches):
         lb.symbol = np.ascontiguousarray(local[lb.symbol], dtype=np.uint32)
         out.append(lb)
         pos.append(sel)
-    return sc, base[ids], ids, out, pos, sc.batch * nbatches
+    return sc, base[ids], ids, out, pos, sc.batch * nbatches, seeds
 
 
 def cpu_baseline(args):
@@ -123,7 +168,8 @@ def cpu_baseline(args):
     itself has no matcher) on a bounded prefix of the same N=1 stream, 1 thread."""
     from oracle.oracle import OracleBook
 
-    sc = me.preset(2, num_symbols=args.symbols_per_gpu, batch=args.batch_per_gpu)
+    w = WORKLOADS[args.workload]
+    sc = me.preset(w["preset"], num_symbols=global_symbols(args, 1), batch=args.batch_per_gpu)
     st = me.Stream(sc)
     ob = OracleBook(sc.num_symbols, sc.levels, st.base_prices(), 1 << 40)
     done, t_cpu, k = 0, 0.0, 0
@@ -135,7 +181,7 @@ def cpu_baseline(args):
         done += len(b)
         k += 1
     return {"value": done / t_cpu, "unit": "orders/s", "cores": 1, "kind": "port",
-            "sample": f"first {k} batches ({done} orders) of the config-2 stream, oracle/oracle_book.cpp "
+            "sample": f"first {k} batches ({done} orders) of the {args.workload} stream, oracle/oracle_book.cpp "
                       f"scalar price-time book, {t_cpu:.1f}s"}
 
 
@@ -147,14 +193,19 @@ def main():
     nb = args.warmup + args.steps
     n_gather = args.gather_steps if world > 1 else 0
     n_e2e = 0 if args.no_e2e else 10
-    sc, base, ids, batches, positions, global_orders = build_rank_batches(args, world, rank, nb + n_gather + n_e2e)
+    sc, base, ids, batches, positions, global_orders, seeds = build_rank_batches(args, world, rank,
+                                                                                 nb + n_gather + n_e2e)
     gather_batches, gather_pos = batches[nb:nb + n_gather], positions[nb:nb + n_gather]
     e2e_batches = batches[nb + n_gather:]
     batches = batches[:nb]
     total_local = sum(len(b) for b in batches + gather_batches + e2e_batches)
-    eng = me.Engine(len(ids), sc.levels, base, max_batch=max(len(b) for b in batches + gather_batches + e2e_batches) + 1,
-                    max_resting=total_local // 3 + 65536, max_seq=global_orders + 16, device=local,
-                    symbol_ids=ids)
+    n_seed = sum(len(b) for b in seeds)
+    eng = me.Engine(len(ids), sc.levels, base,
+                    max_batch=max(len(b) for b in batches + gather_batches + e2e_batches + seeds) + 1,
+                    max_resting=total_local // 3 + n_seed + 65536, max_seq=global_orders + n_seed + 16,
+                    device=local, symbol_ids=ids, batches_per_launch=args.batches_per_launch)
+    for b in seeds:
+        eng.submit_batch(b, want_fills=False)
     dbs = [eng.upload(b) for b in batches]
     for db in dbs[: args.warmup]:
         eng.submit_device(db)
@@ -180,10 +231,12 @@ def main():
     fills_all = allreduce(float(tm["fills"]), world, SUM, local)
 
     # roofline of the dominant kernel (k_match) on this rank, from HIP events on its stream
-    # (HIP events on every --timing-every-th launch of the timed loop; bytes per launch over all K)
+    # (HIP events on every --timing-every-th launch of the timed loop; one launch matches a group of
+    # batches_per_launch batches, so its algorithmic bytes are the timed orders' share of all bytes)
     timed = max(tm["launches"], 1)
     avg_match_s = tm["match_ms"] / 1e3 / timed
-    bytes_per_launch = (BYTES_PER_ORDER * orders_local + BYTES_PER_FILL * tm["fills"]) / args.steps
+    bytes_per_order = (BYTES_PER_ORDER * orders_local + BYTES_PER_FILL * tm["fills"]) / max(orders_local, 1)
+    bytes_per_launch = bytes_per_order * tm["orders"] / timed
     achieved = bytes_per_launch / avg_match_s / 1e9
     traffic = None
     if args.traffic_from and os.path.exists(args.traffic_from):
@@ -229,7 +282,8 @@ def main():
         e2e = n2 / (time.perf_counter() - t2)
 
     if rank == 0:
-        cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args)
+        # config 4's 100k x 32,768-level oracle book (~50 GB of host arrays) is not run on the host
+        cpu = None if (args.no_cpu_baseline or world > 1 or args.workload == "c4") else cpu_baseline(args)
         line = {
             "metric": "orders matched/sec (whole node); fills bit-exact vs CPU oracle",
             "value": orders_all / job_time,
@@ -242,11 +296,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int64",
-            "data": "synthetic (me_gen config 2 stream, seed 2)",
+            "data": f"synthetic (me_gen config {sc.config} stream, seed {sc.seed})",
             "config": {
-                "workload": "BASELINE configs[1]: 1,024 symbols/GPU x uniform stream, 65,536-order batches/GPU, "
-                            "80% LIMIT +-32 ticks / 20% MARKET, qty U[1,100]",
-                "symbols": args.symbols_per_gpu * world,
+                "workload": WORKLOADS[args.workload]["text"],
+                "symbols": global_symbols(args, world),
                 "global_batch": args.batch_per_gpu * world,
                 "levels": sc.levels,
                 "parallelism": f"symbol-hash shards x{world} (no cross-GPU matching)",
@@ -254,6 +307,7 @@ def main():
             "fills_per_order": fills_all / max(orders_all, 1),
             "kernel_match_ms_avg": tm["match_ms"] / timed,
             "kernel_match_launches_timed": tm["launches"],
+            "batches_per_launch": args.batches_per_launch or (8 if sc.levels <= 128 else 1),
             "device_ms_per_step": tm["pipeline_ms"],
             "host_enqueue_ms_per_step_rank0": t_enq / args.steps * 1e3,
             "e2e_host_path_orders_per_s_rank0": e2e,

@@ -95,6 +95,8 @@ typedef struct me_config {
   uint64_t max_seq;            /* locator capacity: accepted seqs are 1 <= seq < max_seq */
   const int64_t* base_price;   /* [num_symbols] price_q4 of level 0 of each symbol's window */
   const uint32_t* symbol_ids;  /* optional [num_symbols] ids written to me_fill.symbol (NULL = local id) */
+  uint32_t batches_per_launch; /* L <= 128: device batches matched per kernel launch, 1..8 (0 = 8). Back-to-back
+                                  me_submit_batch_device calls fill a group; me_sync flushes a partial one */
 } me_config;
 
 /* One batch in structure-of-arrays form, ascending seq (= numeric OID). */
@@ -156,7 +158,8 @@ int me_submit_batch(me_engine* e, const me_order_soa* batch, size_t n, me_fill* 
 /* Upper bound on the tape length of one batch of n records (resting capacity + 2n). */
 uint64_t me_fill_bound(const me_engine* e, size_t n);
 
-/* Device-resident batch (pointers in HBM), enqueued on the engine stream, asynchronous.
+/* Device-resident batch (pointers in HBM), enqueued on the engine stream, asynchronous. The batch
+ * buffers must stay valid until the next me_sync (or any call that reads outputs or the book).
  * Outputs stay on the device until me_fetch_outputs. */
 int me_submit_batch_device(me_engine* e, const me_order_soa* dev_batch, size_t n);
 /* Wait for all enqueued work; returns ME_E_CAPACITY if a pool overflowed in any batch. */

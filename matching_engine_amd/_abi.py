@@ -41,6 +41,7 @@ class MeConfig(C.Structure):
         ("max_seq", C.c_uint64),
         ("base_price", C.POINTER(C.c_int64)),
         ("symbol_ids", C.POINTER(C.c_uint32)),
+        ("batches_per_launch", C.c_uint32),
     ]
 
 

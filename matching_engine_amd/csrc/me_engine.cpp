@@ -23,7 +23,7 @@ hipError_t launch_sort_pass(hipStream_t st, const uint32_t* keys_in, const uint3
                             uint32_t* keys_out, uint32_t* idx_out, uint32_t* zero_buf,
                             uint32_t zero_words, unsigned long long* scratch_top, uint32_t* bin_start);
 hipError_t launch_match(hipStream_t st, const BookDev& bk, const BatchDev& bt, hipEvent_t ev0, hipEvent_t ev1);
-hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev& bt, const AuxDev& ax, hipEvent_t ev0,
+hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* bt, uint32_t ng, const AuxDev& ax, hipEvent_t ev0,
                             hipEvent_t ev1);
 uint32_t sort_tile(uint32_t n);
 hipError_t launch_tape(hipStream_t st, const BatchDev& bt, me_fill* tape, unsigned long long tape_cap,
@@ -41,7 +41,7 @@ std::string g_create_err;
 struct TimedLaunch {
   hipEvent_t m0, m1;  // start / end of one match-kernel launch (recorded by the launch itself)
   uint64_t orders;
-  uint64_t idx;       // launch number since timing was enabled
+  uint64_t idx;       // batches matched (since timing was enabled) before this launch
 };
 }  // namespace
 
@@ -70,15 +70,16 @@ struct me_engine {
     uint32_t* tot = nullptr;        // [2 passes][2048] bin totals
     uint32_t* bin_start = nullptr;  // [2049] run table of the single-pass sort
   } sb;
-  // Per-batch outputs. The pipelined register-ladder path rotates three sets (batch b is bucketed
-  // while b-1 is matched and b-2's tape is compacted); the other paths use set 0.
+  // Per-batch outputs. The pipelined register-ladder path rotates three groups of `group` sets
+  // (group J is bucketed while J-1 is matched and J-2's tapes are compacted); the
+  // other paths use set 0.
   struct OutSet {
     me_order_result* res = nullptr;
     uint32_t* fstart = nullptr;
     uint32_t* tile_sum = nullptr;
     me_fill* scratch = nullptr;
     unsigned long long* top = nullptr;
-  } os[3];
+  } os[3 * ME_GMAX];
   int nsets = 1;
   int last_set = 0;  // output set of the most recent batch
   // Bucketed grouping (register-ladder kernel): per-bin counts and BK_CAP-record buckets.
@@ -88,11 +89,11 @@ struct me_engine {
     int64_t* px = nullptr;
     int32_t* qty = nullptr;
     uint32_t* ok = nullptr;
-  } bu[2];
+  } bu[2 * ME_GMAX];
   bool bucketed = false;
-  // Pipelined path: batches launched but not finished. A batch is bucketed in the launch of its
-  // own submit, matched in the next launch, its tape compacted in the one after; me_sync (and
-  // everything that reads outputs or the book) flushes.
+  // Pipelined path: batches submitted but not finished. Submits fill a group of up to `group`
+  // batches; a full group is bucketed in one launch, matched in the next, its tapes compacted in the
+  // one after; me_sync (and everything that reads outputs or the book) flushes.
   struct Pend {
     bool valid = false;
     const uint64_t* seq = nullptr;
@@ -102,11 +103,17 @@ struct me_engine {
     const uint8_t* kind = nullptr;
     uint32_t n = 0;
     int oset = 0, bset = 0;
-  } p_match, p_tape;
-  uint64_t nbatch = 0;
+  };
+  struct Group {
+    Pend b[ME_GMAX];
+    uint32_t n = 0;
+  } g_fill, g_match, g_tape;
+  uint32_t group = 1;     // batches per launch (me_config.batches_per_launch)
+  uint64_t ngroup = 0;    // groups launched
+  int last_tape = 0;      // tape buffer (position in its group) of the most recent batch
   uint32_t ncu = 0;  // compute units: workgroups of one dispatch round host the side jobs
-  me_fill* d_tape = nullptr;
-  unsigned long long* d_tape_count = nullptr;
+  me_fill* d_tape = nullptr;                   // [group][tape_cap]: one tape per position in a group
+  unsigned long long* d_tape_count = nullptr;  // [ME_GMAX]
   unsigned long long* d_fills_acc = nullptr;  // fills since timing was (re)enabled
   unsigned long long scratch_cap = 0;  // fill scratch: per-symbol slabs + overflow region
   unsigned long long tape_cap = 0;     // tape bound of one batch (max_resting + 2 * max_batch)
@@ -121,6 +128,7 @@ struct me_engine {
   // timing
   int timing = 0;           // 0: off; k >= 1: time every k-th match launch
   uint64_t nlaunch = 0;     // match launches since timing was enabled
+  uint64_t nbat = 0;        // batches those launches matched
   std::vector<TimedLaunch> timed;  // launches since timing was enabled
   std::vector<hipEvent_t> ev_pool;  // events reused across enable cycles (no create per launch)
   size_t ev_used = 0;
@@ -222,6 +230,13 @@ extern "C" int me_normalize_to_q4(int64_t price, int32_t scale, int64_t* out) {
 template <class T>
 static hipError_t dalloc(T** p, size_t count) {
   return hipMalloc((void**)p, std::max<size_t>(count, 1) * sizeof(T));
+}
+
+static bool zero_bucket_counts(me_engine* e, hipStream_t st) {
+  if (!e->bucketed) return true;
+  for (uint32_t k = 0; k < 2 * e->group; ++k)
+    if (hipMemsetAsync(e->bu[k].cnt, 0, (e->bk.S + 1) * (size_t)BK_CNT_STRIDE * 4, st) != hipSuccess) return false;
+  return true;
 }
 
 extern "C" me_engine* me_create(const me_config* cfg) {
@@ -341,9 +356,12 @@ extern "C" me_engine* me_create(const me_config* cfg) {
   }
   // Register-ladder kernel: bucketed grouping when the sort key (index << 7 | slot) fits 32 bits.
   e->bucketed = L <= 128 && n < BK_MAX_BATCH;
+  e->group = e->bucketed ? (cfg->batches_per_launch ? cfg->batches_per_launch : ME_DEFAULT_GROUP) : 1u;
+  if (e->group > (uint32_t)ME_GMAX) return bail("me_create: batches_per_launch exceeds " + std::to_string(ME_GMAX));
   if (e->bucketed) {
     const size_t nb = (S + 1) * (size_t)BK_CAP;
-    for (auto& b : e->bu) {
+    for (uint32_t k = 0; k < 2 * e->group; ++k) {
+      auto& b = e->bu[k];
       ALLOC(b.cnt, (S + 1) * BK_CNT_STRIDE);
       ALLOC(b.seq, nb);
       ALLOC(b.px, nb);
@@ -351,7 +369,7 @@ extern "C" me_engine* me_create(const me_config* cfg) {
       ALLOC(b.ok, nb);
     }
   }
-  e->nsets = e->bucketed ? 3 : 1;
+  e->nsets = e->bucketed ? 3 * (int)e->group : 1;
   for (int k = 0; k < e->nsets; ++k) {
     auto& o = e->os[k];
     ALLOC(o.res, n);
@@ -361,8 +379,8 @@ extern "C" me_engine* me_create(const me_config* cfg) {
     ALLOC(o.top, 1);
   }
   ALLOC(bk.fcache, S * 64);
-  ALLOC(e->d_tape, scap);
-  ALLOC(e->d_tape_count, 1);
+  ALLOC(e->d_tape, scap * e->group);
+  ALLOC(e->d_tape_count, ME_GMAX);
   ALLOC(e->d_fills_acc, 1);
 #ifdef ME_STAMPS
   ALLOC(bk.dbg, S * 24);
@@ -388,8 +406,7 @@ extern "C" me_engine* me_create(const me_config* cfg) {
     gs[i] = cfg->symbol_ids ? cfg->symbol_ids[i] : (uint32_t)i;
   }
   bool ok = launch_init_levels(st, bk.levels, S * L) == hipSuccess &&
-            (!e->bucketed || (hipMemsetAsync(e->bu[0].cnt, 0, (S + 1) * BK_CNT_STRIDE * 4, st) == hipSuccess &&
-                              hipMemsetAsync(e->bu[1].cnt, 0, (S + 1) * BK_CNT_STRIDE * 4, st) == hipSuccess)) &&
+            zero_bucket_counts(e, st) &&
             hipMemsetAsync(bk.occ, 0, S * (L / 64) * 8, st) == hipSuccess &&
             hipMemsetAsync(bk.tend, 0, S * L, st) == hipSuccess &&
             launch_init_chunks(st, bk.chunks, nchunks) == hipSuccess &&
@@ -398,7 +415,7 @@ extern "C" me_engine* me_create(const me_config* cfg) {
             hipMemsetAsync(bk.chunk_top, 0, 4, st) == hipSuccess && hipMemsetAsync(bk.err, 0, 4, st) == hipSuccess &&
             hipMemcpyAsync(bk.sym, ss.data(), S * sizeof(SymState), hipMemcpyHostToDevice, st) == hipSuccess &&
             hipMemcpyAsync(gsym, gs.data(), S * 4, hipMemcpyHostToDevice, st) == hipSuccess &&
-            hipMemsetAsync(e->d_tape_count, 0, 8, st) == hipSuccess &&
+            hipMemsetAsync(e->d_tape_count, 0, 8 * ME_GMAX, st) == hipSuccess &&
             hipMemsetAsync(e->d_fills_acc, 0, 8, st) == hipSuccess &&
             hipStreamSynchronize(st) == hipSuccess;
   if (!ok) return bail(std::string("me_create: book init failed: ") + hipGetErrorString(hipGetLastError()));
@@ -421,10 +438,12 @@ extern "C" uint64_t me_fill_bound(const me_engine* e, size_t n) {
 }
 
 // Timing bookkeeping for one match launch (every e->timing-th launch records its own start / end).
-static int timing_slot(me_engine* e, uint32_t orders, TimedLaunch& tl, bool& timed) {
+static int timing_slot(me_engine* e, uint32_t orders, uint32_t batches, TimedLaunch& tl, bool& timed) {
   timed = e->timing > 0 && e->nlaunch % (uint64_t)e->timing == 0;
   tl = TimedLaunch{};
-  tl.idx = e->nlaunch++;
+  e->nlaunch++;
+  tl.idx = e->nbat;  // batches matched before this launch
+  e->nbat += batches;
   if (timed) {
     while (e->ev_pool.size() < e->ev_used + 2) {
       hipEvent_t ev;
@@ -459,74 +478,95 @@ static BatchDev batch_dev(me_engine* e, const uint64_t* seq, const int64_t* px, 
   return bt;
 }
 
-// One launch of the pipelined register-ladder path: match p_match (if any), bucket nb (if any)
-// and clear its counters, compact p_tape's tape (if any) — then the pipeline shifts by one.
-static int pipe_launch(me_engine* e, const me_engine::Pend* nb) {
-  BatchDev bt{};
+// One launch of the pipelined register-ladder path: match group g_match (if any), bucket group nb
+// (if any) and clear the counters its batches will use, compact g_tape's tapes (if any) — then the
+// pipeline shifts by one group.
+static int pipe_launch(me_engine* e, const me_engine::Group* nb) {
+  BatchDev bt[ME_GMAX] = {};
   AuxDev ax{};
-  const auto& pm = e->p_match;
-  const auto& pt = e->p_tape;
-  if (pm.valid) {
-    bt = batch_dev(e, pm.seq, pm.px, pm.qty, pm.sym, pm.kind, pm.n, pm.oset);
+  const auto& gm = e->g_match;
+  const auto& gt = e->g_tape;
+  uint32_t orders = 0;
+  for (uint32_t g = 0; g < gm.n; ++g) {
+    const auto& pm = gm.b[g];
+    bt[g] = batch_dev(e, pm.seq, pm.px, pm.qty, pm.sym, pm.kind, pm.n, pm.oset);
     const auto& b = e->bu[pm.bset];
-    bt.bcnt = b.cnt;
-    bt.b_seq = b.seq;
-    bt.b_px = b.px;
-    bt.b_qty = b.qty;
-    bt.b_ok = b.ok;
-    bt.bcap = BK_CAP;
+    bt[g].bcnt = b.cnt;
+    bt[g].b_seq = b.seq;
+    bt[g].b_px = b.px;
+    bt[g].b_qty = b.qty;
+    bt[g].b_ok = b.ok;
+    bt[g].bcap = BK_CAP;
+    orders += pm.n;
   }
-  if (nb) {
-    const auto& b = e->bu[nb->bset];
-    const auto& o = e->os[nb->oset];
-    ax.sym = nb->sym;
-    ax.seq = nb->seq;
-    ax.px = nb->px;
-    ax.qty = nb->qty;
-    ax.kind = nb->kind;
-    ax.n = nb->n;
-    ax.S = e->bk.S;
-    ax.bcnt = b.cnt;
-    ax.b_seq = b.seq;
-    ax.b_px = b.px;
-    ax.b_qty = b.qty;
-    ax.b_ok = b.ok;
-    ax.bres = o.res;
-    ax.bfstart = o.fstart;
-    ax.zero_tile_sum = o.tile_sum;
-    ax.zero_tiles = (nb->n + TILE_TAPE - 1) / TILE_TAPE;
-    ax.zero_top = o.top;
-  }
-  if (pt.valid) {
-    const auto& o = e->os[pt.oset];
-    ax.tn = pt.n;
-    ax.tile_sum = o.tile_sum;
-    ax.res = o.res;
-    ax.fstart = o.fstart;
-    ax.scratch = o.scratch;
-    ax.tape = e->d_tape;
-    ax.tape_cap = e->tape_cap;
-    ax.tape_count = e->d_tape_count;
-    ax.fills_acc = e->d_fills_acc;
-  }
+  ax.S = e->bk.S;
   ax.nwg = e->ncu;
+  if (nb) {
+    ax.nb = nb->n;
+    for (uint32_t j = 0; j < nb->n; ++j) {
+      const auto& p = nb->b[j];
+      const auto& b = e->bu[p.bset];
+      const auto& o = e->os[p.oset];
+      AuxBucket& J = ax.b[j];
+      J.sym = p.sym;
+      J.seq = p.seq;
+      J.px = p.px;
+      J.qty = p.qty;
+      J.kind = p.kind;
+      J.n = p.n;
+      J.bcnt = b.cnt;
+      J.b_seq = b.seq;
+      J.b_px = b.px;
+      J.b_qty = b.qty;
+      J.b_ok = b.ok;
+      J.bres = o.res;
+      J.bfstart = o.fstart;
+      J.zero_tile_sum = o.tile_sum;
+      J.zero_tiles = (p.n + TILE_TAPE - 1) / TILE_TAPE;
+      J.zero_top = o.top;
+    }
+  }
+  ax.nt = gt.n;
+  ax.tape_cap = e->tape_cap;
+  ax.fills_acc = e->d_fills_acc;
+  for (uint32_t j = 0; j < gt.n; ++j) {
+    const auto& o = e->os[gt.b[j].oset];
+    AuxTape& J = ax.t[j];
+    J.tn = gt.b[j].n;
+    J.tile_sum = o.tile_sum;
+    J.res = o.res;
+    J.fstart = o.fstart;
+    J.scratch = o.scratch;
+    J.tape = e->d_tape + (size_t)j * e->tape_cap;
+    J.tape_count = e->d_tape_count + j;
+  }
   TimedLaunch tl{};
   bool timed = false;
-  if (pm.valid) {
-    int rc = timing_slot(e, pm.n, tl, timed);
+  if (gm.n) {
+    int rc = timing_slot(e, orders, gm.n, tl, timed);
     if (rc) return rc;
   }
-  hipError_t he = launch_match_reg(e->stream, e->bk, bt, ax, tl.m0, tl.m1);
+  hipError_t he = launch_match_reg(e->stream, e->bk, bt, gm.n, ax, tl.m0, tl.m1);
   if (he != hipSuccess) return e->hip_fail(he, "pipelined match launch");
   if (timed) e->timed.push_back(tl);
-  e->p_tape = e->p_match;
-  e->p_match = nb ? *nb : me_engine::Pend{};
+  e->g_tape = e->g_match;
+  if (nb) {
+    e->g_match = *nb;
+    e->ngroup++;
+  } else {
+    e->g_match = me_engine::Group{};
+  }
   return ME_OK;
 }
 
-// Finish every launched batch (the last one's outputs are then final).
+// Finish every submitted batch (the last one's outputs are then final).
 static int flush_pipeline(me_engine* e) {
-  while (e->p_match.valid || e->p_tape.valid) {
+  if (e->g_fill.n) {  // a partial group goes out as it is
+    int rc = pipe_launch(e, &e->g_fill);
+    e->g_fill = me_engine::Group{};
+    if (rc) return rc;
+  }
+  while (e->g_match.n || e->g_tape.n) {
     int rc = pipe_launch(e, nullptr);
     if (rc) return rc;
   }
@@ -537,7 +577,9 @@ static int flush_pipeline(me_engine* e) {
 static int enqueue_batch(me_engine* e, const uint64_t* seq, const int64_t* px, const int32_t* qty,
                          const uint32_t* sym, const uint8_t* kind, uint32_t n) {
   if (e->bucketed) {
-    me_engine::Pend nb;
+    auto& gf = e->g_fill;
+    const uint32_t pos = gf.n;
+    me_engine::Pend& nb = gf.b[pos];
     nb.valid = true;
     nb.seq = seq;
     nb.px = px;
@@ -545,13 +587,17 @@ static int enqueue_batch(me_engine* e, const uint64_t* seq, const int64_t* px, c
     nb.sym = sym;
     nb.kind = kind;
     nb.n = n;
-    nb.oset = (int)(e->nbatch % 3);
-    nb.bset = (int)(e->nbatch % 2);
-    e->nbatch++;
-    int rc = pipe_launch(e, &nb);
-    if (rc) return rc;
+    nb.oset = (int)((e->ngroup % 3) * e->group + pos);
+    nb.bset = (int)((e->ngroup % 2) * e->group + pos);
+    gf.n = pos + 1;
     e->last_set = nb.oset;
+    e->last_tape = (int)pos;
     e->last_n = n;
+    if (gf.n == e->group) {
+      int rc = pipe_launch(e, &gf);
+      gf = me_engine::Group{};
+      if (rc) return rc;
+    }
     return ME_OK;
   }
   hipStream_t st = e->stream;
@@ -559,7 +605,7 @@ static int enqueue_batch(me_engine* e, const uint64_t* seq, const int64_t* px, c
   const auto& o = e->os[0];
   TimedLaunch tl{};
   bool timed = false;
-  int rc = timing_slot(e, n, tl, timed);
+  int rc = timing_slot(e, n, 1u, tl, timed);
   if (rc) return rc;
   const uint32_t S = e->bk.S;
   const uint32_t ntiles_tape = (n + TILE_TAPE - 1) / TILE_TAPE;
@@ -589,6 +635,7 @@ static int enqueue_batch(me_engine* e, const uint64_t* seq, const int64_t* px, c
   if (he != hipSuccess) return e->hip_fail(he, "tape launch");
   if (timed) e->timed.push_back(tl);
   e->last_set = 0;
+  e->last_tape = 0;
   e->last_n = n;
   return ME_OK;
 }
@@ -637,7 +684,8 @@ extern "C" int me_fetch_outputs(me_engine* e, me_fill* out_fills, size_t fills_c
   int rc = me_sync(e);
   if (rc) return rc;
   unsigned long long cnt = 0;
-  if (e->last_n) HIP_TRY(hipMemcpy(&cnt, e->d_tape_count, 8, hipMemcpyDeviceToHost), "read tape count");
+  if (e->last_n)
+    HIP_TRY(hipMemcpy(&cnt, e->d_tape_count + e->last_tape, 8, hipMemcpyDeviceToHost), "read tape count");
   if (n_fills) *n_fills = (size_t)cnt;
   if (out_results && n_results) {
     if (n_results > e->last_n) return e->fail(ME_E_INVALID, "n_results exceeds last batch size");
@@ -646,7 +694,8 @@ extern "C" int me_fetch_outputs(me_engine* e, me_fill* out_fills, size_t fills_c
   }
   if (out_fills && cnt) {
     if (cnt > fills_cap) return e->fail(ME_E_INVALID, "fills_cap smaller than the tape");
-    HIP_TRY(hipMemcpy(out_fills, e->d_tape, cnt * sizeof(me_fill), hipMemcpyDeviceToHost), "D2H tape");
+    HIP_TRY(hipMemcpy(out_fills, e->d_tape + (size_t)e->last_tape * e->tape_cap, cnt * sizeof(me_fill),
+                      hipMemcpyDeviceToHost), "D2H tape");
   }
   return ME_OK;
 }
@@ -695,10 +744,12 @@ extern "C" int me_copy_tape_device(me_engine* e, void* dst, size_t cap_fills, si
   int rc = me_sync(e);
   if (rc) return rc;
   unsigned long long cnt = 0;
-  if (e->last_n) HIP_TRY(hipMemcpy(&cnt, e->d_tape_count, 8, hipMemcpyDeviceToHost), "read tape count");
+  if (e->last_n)
+    HIP_TRY(hipMemcpy(&cnt, e->d_tape_count + e->last_tape, 8, hipMemcpyDeviceToHost), "read tape count");
   if (n_fills) *n_fills = (size_t)cnt;
   if (cnt > cap_fills) return e->fail(ME_E_INVALID, "cap_fills smaller than the tape");
-  if (cnt) HIP_TRY(hipMemcpyAsync(dst, e->d_tape, cnt * sizeof(me_fill), hipMemcpyDeviceToDevice, e->stream),
+  if (cnt) HIP_TRY(hipMemcpyAsync(dst, e->d_tape + (size_t)e->last_tape * e->tape_cap, cnt * sizeof(me_fill),
+                                  hipMemcpyDeviceToDevice, e->stream),
                    "D2D tape");
   return ME_OK;
 }
@@ -734,6 +785,10 @@ extern "C" int me_device_free(me_engine* e, void* dptr) {
   if (it == e->user_allocs.end()) return e->fail(ME_E_INVALID, "pointer not allocated by me_device_alloc");
   e->user_allocs.erase(it);
   HIP_TRY(hipSetDevice(e->dev), "hipSetDevice");
+  if (!e->failed) {  // a submitted batch may still live in this buffer: finish it first
+    int rc = flush_pipeline(e);
+    if (rc) return rc;
+  }
   HIP_TRY(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
   HIP_TRY(hipFree(dptr), "hipFree");
   return ME_OK;
@@ -872,6 +927,7 @@ extern "C" int me_timing_enable(me_engine* e, int enable) {
   e->timed.clear();
   e->ev_used = 0;
   e->nlaunch = 0;
+  e->nbat = 0;
   HIP_TRY(hipMemsetAsync(e->d_fills_acc, 0, 8, e->stream), "reset fill counter");
   HIP_TRY(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
   e->timing = enable > 0 ? enable : 0;
@@ -894,7 +950,8 @@ extern "C" int me_timing_read(me_engine* e, double* match_ms, double* pipeline_m
     m += a;
     o += t.orders;
   }
-  if (e->timed.size() >= 2) {  // device time per batch: start-to-start of the first and last timed launches
+  if (e->timed.size() >= 2 && e->timed.back().idx > e->timed.front().idx) {
+    // device time per batch: start-to-start of the first and last timed launches over the batches between
     float b = 0;
     HIP_TRY(hipEventElapsedTime(&b, e->timed.front().m0, e->timed.back().m0), "hipEventElapsedTime");
     p = b / (double)(e->timed.back().idx - e->timed.front().idx);

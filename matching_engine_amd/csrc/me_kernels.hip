@@ -1347,8 +1347,8 @@ hipError_t launch_sort_pass(hipStream_t st, const uint32_t* keys_in, const uint3
   return hipGetLastError();
 }
 
-hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev& bt, const AuxDev& ax, hipEvent_t ev0,
-                            hipEvent_t ev1);
+hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* bt, uint32_t ng, const AuxDev& ax,
+                            hipEvent_t ev0, hipEvent_t ev1);
 
 // ev0 / ev1 (optional, timing): the launch records the kernel's own start and end
 // (hipExtLaunchKernelGGL), so timing adds no marker packet — and no gap — to the stream.
@@ -1356,7 +1356,7 @@ hipError_t launch_match(hipStream_t st, const BookDev& bk, const BatchDev& bt, h
   const uint32_t waves = bk.S + 1;
   const dim3 grid((waves + 3) / 4), block(256);
   if (bk.L <= 128) {
-    return launch_match_reg(st, bk, bt, AuxDev{}, ev0, ev1);
+    return launch_match_reg(st, bk, &bt, 1u, AuxDev{}, ev0, ev1);
   } else if (bk.L <= LDS_MAX_LEVELS) {
     hipExtLaunchKernelGGL(k_match<LAD_LDS>, grid, block, 4 * lds_wave_bytes(bk.L), st, ev0, ev1, 0, bk, bt);
   } else {

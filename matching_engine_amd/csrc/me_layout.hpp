@@ -127,40 +127,53 @@ struct BatchDev {
   const uint32_t* b_ok;  // batch index | (kind & 15) << BK_KIND_SHIFT
   uint32_t bcap;
 };
+// Batches per register-ladder launch at most (me_config.batches_per_launch). One launch matches a
+// group of up to ME_GMAX batches: every symbol's wave runs through its records of all of them in
+// order, so a launch costs the heaviest symbol's share of the whole group rather than the sum of
+// each batch's heaviest share.
+constexpr int ME_GMAX = 8;
+constexpr uint32_t ME_DEFAULT_GROUP = 8;
+
 // Side jobs of one pipelined register-ladder launch (me_match_reg.hip), run by each workgroup's
-// extra waves while its matching waves work on batch b-1: group batch b into its buckets, clear
-// the counters batch b will use, compact the tape of batch b-2. A job with zero records is off.
-struct AuxDev {
-  // bucket job: batch b
+// extra waves while its matching waves work on group J-1: group the batches of group J into their
+// buckets (and clear the output counters they will use), compact the tapes of group J-2.
+struct AuxBucket {  // bucket + clear job of one batch
   const uint32_t* sym;
   const uint64_t* seq;
   const int64_t* px;
   const int32_t* qty;
   const uint8_t* kind;
   uint32_t n;
-  uint32_t S;
+  uint32_t zero_tiles;
   uint32_t* bcnt;
   uint64_t* b_seq;
   int64_t* b_px;
   int32_t* b_qty;
   uint32_t* b_ok;
-  me_order_result* bres;  // batch b's results: unknown-symbol records are rejected by the bucket job
+  me_order_result* bres;  // the batch's results: unknown-symbol records are rejected by the bucket job
   uint32_t* bfstart;
-  uint32_t nwg;           // workgroups that run side jobs (those of the first dispatch round)
-  // clear job: the output set batch b will use
   uint32_t* zero_tile_sum;
-  uint32_t zero_tiles;
   unsigned long long* zero_top;
-  // tape job: batch b-2
-  uint32_t tn;
+};
+struct AuxTape {  // tape job of one batch
   const uint32_t* tile_sum;
   me_order_result* res;
   const uint32_t* fstart;
   const me_fill* scratch;
   me_fill* tape;
-  unsigned long long tape_cap;
   unsigned long long* tape_count;
+  uint32_t tn;
+  uint32_t pad;
+};
+struct AuxDev {
+  uint32_t S;
+  uint32_t nwg;  // workgroups that run side jobs (those of the first dispatch round)
+  uint32_t nb;   // bucket jobs (batches of group J)
+  uint32_t nt;   // tape jobs (batches of group J-2)
+  unsigned long long tape_cap;
   unsigned long long* fills_acc;
+  AuxBucket b[ME_GMAX];
+  AuxTape t[ME_GMAX];
 };
 
 constexpr int BK_CAP = 128;          // records per bucket (two 64-record blocks)

@@ -59,6 +59,7 @@ struct RegLds {
   uint32_t pad;
   uint32_t scan_cur, scan_cnt, scan_pos;  // rescan of an overfull bucket: next batch index, list fill, list read
   uint32_t mode;  // record source: 0 bucket, 1 rescan, 2 sort path (perm run [run_lo, run_lo + run_n))
+  uint32_t g_cur, g_next;  // batch of the group being matched (its outputs: G.bt[g_cur]), the next one
   uint32_t run_lo, run_n;
   int dq;                 // reg_rest: LDS target of an append to an uncached tail
   unsigned long long dsq;
@@ -129,8 +130,10 @@ struct Mask2 {
 // no SGPRs across the loop — the hot state (masks, best prices, cursors) keeps the scalar file.
 struct ColdArgs {
   BookDev bk;
-  BatchDev bt;
+  BatchDev bt[ME_GMAX];  // the match job: batches [0, ng) of group J-1, in stream order
   AuxDev ax;
+  uint32_t ng;
+  uint32_t pad;
 };
 
 // Global-address-space (1) pointers: an opaque round trip (vreg64, ldsu) would otherwise leave a
@@ -569,8 +572,9 @@ __device__ __forceinline__ uint32_t reg_cancel(RegCtx& c, unsigned long long tgt
 // reserve the batch bound of everything left (resting + 2 * records left) in the
 // shared overflow region once; after that no further check can fail.
 __device__ __forceinline__ bool reg_reserve_overflow(RegCtx& c) {
-  unsigned long long* top = ldsg(c.G->bt.scratch_top);
-  const unsigned long long base = ldsu(c.G->bt.ovf_base), cap = ldsu(c.G->bt.scratch_cap);
+  const BatchDev& B = c.G->bt[ldsu(c.M->g_cur)];
+  unsigned long long* top = ldsg(B.scratch_top);
+  const unsigned long long base = ldsu(B.ovf_base), cap = ldsu(B.scratch_cap);
   const unsigned long long need = (unsigned long long)(uint32_t)c.resting + 2ull * c.recs_left;
   unsigned long long w0 = 0;
   if (lane_id() == 0) w0 = atomicAdd(top, need);
@@ -600,7 +604,9 @@ __device__ __forceinline__ uint32_t xor_lane(uint32_t v) {
 template <int J>
 __device__ __forceinline__ uint32_t bitonic_step(uint32_t v, bool asc) {
   const uint32_t p = xor_lane<J>(v);
-  const bool lower = (lane_id() & J) == 0;
+  // (opaque lane id: the per-lane masks are rebuilt per sort, not hoisted out of the batch loop,
+  // where they would be live SGPR pairs across the serial loop)
+  const bool lower = ((int)vreg((uint32_t)lane_id()) & J) == 0;
   return (lower == asc) ? min(v, p) : max(v, p);
 }
 template <int K>
@@ -615,7 +621,7 @@ __device__ __forceinline__ uint32_t bitonic_merge(uint32_t v, bool asc) {
 }
 // stages 2..64 of one register; dir1: direction of the 64-run (element 64 + lane sorts descending)
 __device__ __forceinline__ uint32_t sort64(uint32_t v, bool desc64) {
-  const int lane = lane_id();
+  const int lane = (int)vreg((uint32_t)lane_id());
   v = bitonic_merge<2>(v, (lane & 2) == 0);
   v = bitonic_merge<4>(v, (lane & 4) == 0);
   v = bitonic_merge<8>(v, (lane & 8) == 0);
@@ -634,10 +640,10 @@ __device__ __forceinline__ void sort128(uint32_t& a, uint32_t& b) {
 
 // Rescan of an overfull bucket: the next 1024-record window of the batch that holds records of
 // bin s, as a list of batch indices in LDS (batch order). Returns false when the batch is done.
-__device__ __forceinline__ bool rescan_window(RegLds* M, const ColdArgs& G, uint32_t s) {
+__device__ __forceinline__ bool rescan_window(RegLds* M, const ColdArgs& G, uint32_t g, uint32_t s) {
   const int lane = lane_id();
-  const uint32_t n = ldsu(G.bt.n), S = ldsu(G.bk.S);
-  const gptr<const uint32_t> sym = ldsg(G.bt.sym);
+  const uint32_t n = ldsu(G.bt[g].n), S = ldsu(G.bk.S);
+  const gptr<const uint32_t> sym = ldsg(G.bt[g].sym);
   uint32_t cur = ldsu(M->scan_cur);
   while (cur < n) {
     uint32_t sy[16];
@@ -676,7 +682,7 @@ __device__ __forceinline__ void reject_bad_at(gptr<me_order_result> res, gptr<ui
   res[i] = r;
   fstart[i] = 0;
 }
-__device__ __forceinline__ void reject_bad(const ColdArgs& G, uint32_t i, bool v) {
+__device__ __forceinline__ void reject_bad(const ColdArgs& G, uint32_t g, uint32_t i, bool v) {
   if (!v) return;
   me_order_result r;
   r.filled_qty = 0;
@@ -686,52 +692,42 @@ __device__ __forceinline__ void reject_bad(const ColdArgs& G, uint32_t i, bool v
   r.status = ME_ST_REJECTED;
   r.reason = ME_RJ_BAD_SYMBOL;
   r.pad[0] = r.pad[1] = 0;
-  ldsg(G.bt.res)[i] = r;
-  ldsg(G.bt.fstart)[i] = 0;
+  ldsg(G.bt[g].res)[i] = r;
+  ldsg(G.bt[g].fstart)[i] = 0;
 }
 
-// The bad-symbol bin: every record rejected (order irrelevant).
-__device__ __forceinline__ void reject_bad_bucket(RegLds* M, const ColdArgs& G, uint32_t s, uint32_t ns,
-                                                  uint32_t bo0, uint32_t bo1) {
-  const int lane = lane_id();
-  const uint32_t cap = ldsu(G.bt.bcap);
-  if (ns <= cap) {
-    reject_bad(G, bo0 & BK_IDX_MASK, (uint32_t)lane < ns);
-    reject_bad(G, bo1 & BK_IDX_MASK, 64u + (uint32_t)lane < ns);
-    return;
-  }
-  if (lane == 0) M->scan_cur = 0;
-  while (rescan_window(M, G, s)) {
-    const uint32_t cnt = ldsu(M->scan_cnt);
-    for (uint32_t j = 0; j < cnt; j += 64) reject_bad(G, M->in.lst[min(j + lane, cnt - 1u)], j + lane < cnt);
-  }
+// The bad-symbol bin of the sort path (one batch): every record rejected (order irrelevant).
+__device__ __forceinline__ void reject_bad_run(const ColdArgs& G, uint32_t lo, uint32_t hi) {
+  const gptr<const uint32_t> perm = ldsg(G.bt[0].perm);
+  for (uint32_t i = lo + (uint32_t)lane_id(); i < hi; i += 64) reject_bad(G, 0, perm[i], true);
 }
 
 // ---- side jobs of a pipelined launch (the workgroup's waves REG_WAVES .. 2*REG_WAVES-1) -------
 // Memory-latency work with few instructions, so sharing the SIMDs with the matching waves costs
 // them little; what it saves is two launches per batch.
 
-// Bucket job: records [r0, r1) of batch b, one returning atomic per record on its bin's counter.
-__device__ __forceinline__ void aux_bucket(const ColdArgs& G, uint32_t r0, uint32_t r1) {
+// Bucket job: records [r0, r1) of bucket job j, one returning atomic per record on its bin's counter.
+__device__ __forceinline__ void aux_bucket(const ColdArgs& G, uint32_t j, uint32_t r0, uint32_t r1) {
   const int lane = lane_id();
-  const gptr<const uint32_t> sym = ldsg(G.ax.sym);
-  const gptr<const uint64_t> seq = ldsg(G.ax.seq);
-  const gptr<const int64_t> px = ldsg(G.ax.px);
-  const gptr<const int32_t> qty = ldsg(G.ax.qty);
-  const gptr<const uint8_t> kind = ldsg(G.ax.kind);
-  const gptr<uint32_t> bcnt = ldsg(G.ax.bcnt);
-  const gptr<uint64_t> bseq = ldsg(G.ax.b_seq);
-  const gptr<int64_t> bpx = ldsg(G.ax.b_px);
-  const gptr<int32_t> bqty = ldsg(G.ax.b_qty);
-  const gptr<uint32_t> bok = ldsg(G.ax.b_ok);
+  const AuxBucket& J = G.ax.b[j];
+  const gptr<const uint32_t> sym = ldsg(J.sym);
+  const gptr<const uint64_t> seq = ldsg(J.seq);
+  const gptr<const int64_t> px = ldsg(J.px);
+  const gptr<const int32_t> qty = ldsg(J.qty);
+  const gptr<const uint8_t> kind = ldsg(J.kind);
+  const gptr<uint32_t> bcnt = ldsg(J.bcnt);
+  const gptr<uint64_t> bseq = ldsg(J.b_seq);
+  const gptr<int64_t> bpx = ldsg(J.b_px);
+  const gptr<int32_t> bqty = ldsg(J.b_qty);
+  const gptr<uint32_t> bok = ldsg(J.b_ok);
   const uint32_t S = ldsu(G.ax.S);
-  const gptr<me_order_result> bres = ldsg(G.ax.bres);
-  const gptr<uint32_t> bfst = ldsg(G.ax.bfstart);
+  const gptr<me_order_result> bres = ldsg(J.bres);
+  const gptr<uint32_t> bfst = ldsg(J.bfstart);
   for (uint32_t i0 = r0; i0 < r1; i0 += 64) {
     const uint32_t i = i0 + (uint32_t)lane;
     if (i < r1) {
       const uint32_t b = min(sym[i], S);
-      if (b == S) {  // unknown symbol: rejected here, never bucketed (batch b's result set is free)
+      if (b == S) {  // unknown symbol: rejected here, never bucketed (the batch's result set is free)
         reject_bad_at(bres, bfst, i);
         continue;
       }
@@ -751,15 +747,17 @@ __device__ __forceinline__ void aux_bucket(const ColdArgs& G, uint32_t r0, uint3
   }
 }
 
-// Tape job, one TILE_TAPE-record tile of batch b-2 per wave: tape offsets of its records and the
-// copy of their fills from scratch into the tape (ordered by taker seq).
-__device__ __forceinline__ void aux_tape_tile(const ColdArgs& G, uint32_t t, uint32_t ntiles, uint32_t tn) {
+// Tape job j, one TILE_TAPE-record tile per wave: tape offsets of its records and the copy of their
+// fills from scratch into the batch's tape (ordered by taker seq).
+__device__ __forceinline__ void aux_tape_tile(const ColdArgs& G, uint32_t jb, uint32_t t, uint32_t ntiles,
+                                              uint32_t tn) {
   const int lane = lane_id();
-  const gptr<const uint32_t> tile_sum = ldsg(G.ax.tile_sum);
-  const gptr<me_order_result> res = ldsg(G.ax.res);
-  const gptr<const uint32_t> fstart = ldsg(G.ax.fstart);
-  const gptr<const me_fill> scratch = ldsg(G.ax.scratch);
-  const gptr<me_fill> tape = ldsg(G.ax.tape);
+  const AuxTape& J = G.ax.t[jb];
+  const gptr<const uint32_t> tile_sum = ldsg(J.tile_sum);
+  const gptr<me_order_result> res = ldsg(J.res);
+  const gptr<const uint32_t> fstart = ldsg(J.fstart);
+  const gptr<const me_fill> scratch = ldsg(J.scratch);
+  const gptr<me_fill> tape = ldsg(J.tape);
   long long acc = 0;  // fills of the earlier tiles
   for (uint32_t u = (uint32_t)lane; u < t; u += 64) acc += tile_sum[u];
   for (int d = 32; d >= 1; d >>= 1) acc += __shfl_xor(acc, d, 64);
@@ -799,29 +797,31 @@ __device__ __forceinline__ void aux_tape_tile(const ColdArgs& G, uint32_t t, uin
     o2 += c[k];
   }
   if (t == ntiles - 1 && lane == 0) {
-    *ldsg(G.ax.tape_count) = base + total;
+    *ldsg(J.tape_count) = base + total;
     atomicAdd(ldsg(G.ax.fills_acc), base + total);
   }
 }
 
+// Side-job wave a of A: its share of every bucket / clear job of group J and every tape job of J-2.
 __device__ __forceinline__ void aux_jobs(const ColdArgs& G, uint32_t a, uint32_t A) {
   const int lane = lane_id();
-  const uint32_t zt = ldsu(G.ax.zero_tiles);
-  if (zt) {
-    const gptr<uint32_t> z = ldsg(G.ax.zero_tile_sum);
+  const uint32_t nb = ldsu(G.ax.nb);
+  for (uint32_t j = 0; j < nb; ++j) {
+    const AuxBucket& J = G.ax.b[j];
+    const uint32_t zt = ldsu(J.zero_tiles);
+    const gptr<uint32_t> z = ldsg(J.zero_tile_sum);
     for (uint32_t i = a * 64u + (uint32_t)lane; i < zt; i += A * 64u) z[i] = 0u;
-    if (a == 0 && lane == 0) *ldsg(G.ax.zero_top) = 0ull;
-  }
-  const uint32_t n = ldsu(G.ax.n);
-  if (n) {
+    if (a == 0 && lane == 0) *ldsg(J.zero_top) = 0ull;
+    const uint32_t n = ldsu(J.n);
     const uint32_t per = (((n + A - 1u) / A) + 63u) & ~63u;
     const uint32_t r0 = min(n, a * per);
-    aux_bucket(G, r0, min(n, r0 + per));
+    aux_bucket(G, j, r0, min(n, r0 + per));
   }
-  const uint32_t tn = ldsu(G.ax.tn);
-  if (tn) {
+  const uint32_t nt = ldsu(G.ax.nt);
+  for (uint32_t j = 0; j < nt; ++j) {
+    const uint32_t tn = ldsu(G.ax.t[j].tn);
     const uint32_t ntiles = (tn + TILE_TAPE - 1) / TILE_TAPE;
-    for (uint32_t t = a; t < ntiles; t += A) aux_tape_tile(G, t, ntiles, tn);
+    for (uint32_t t = a; t < ntiles; t += A) aux_tape_tile(G, j, t, ntiles, tn);
   }
 }
 
@@ -829,59 +829,50 @@ __device__ __forceinline__ void aux_jobs(const ColdArgs& G, uint32_t a, uint32_t
 // Per-record control word built in vector form: lim level | BUY | MARKET | CANCEL.
 constexpr uint32_t CW_BUY = 1u << 8, CW_MKT = 1u << 9, CW_CXL = 1u << 10;
 
-__global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(BookDev bk, BatchDev bt, AuxDev ax) {
+__global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
   __shared__ RegLds lds[REG_WAVES];
   __shared__ ColdArgs G;
-  static_assert(sizeof(ColdArgs) % 8 == 0 && sizeof(ColdArgs) <= 8 * 64 * REG_WAVES, "ColdArgs copy");
+  static_assert(sizeof(ColdArgs) % 8 == 0 && sizeof(ColdArgs) <= 8 * 128 * REG_WAVES, "ColdArgs copy");
   {
-    const ColdArgs a{bk, bt, ax};
     if (threadIdx.x < sizeof(ColdArgs) / 8)
       reinterpret_cast<unsigned long long*>(&G)[threadIdx.x] =
-          reinterpret_cast<const unsigned long long*>(&a)[threadIdx.x];
+          reinterpret_cast<const unsigned long long*>(&args)[threadIdx.x];
     __syncthreads();
   }
+  const BookDev& bk = args.bk;
   const int lane = lane_id();
   // wave index: readfirstlane tells the divergence analysis it is wave-uniform (threadIdx.x >> 6 is
   // not recognised as such), so every per-symbol value and branch below is scalar
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (wv >= (uint32_t)REG_WAVES) {  // side-job wave (only in the workgroups of the first dispatch round)
-    const uint32_t k = wv - REG_WAVES, nwg = max(min(ax.nwg, gridDim.x), 1u);
+    const uint32_t k = wv - REG_WAVES, nwg = max(min(args.ax.nwg, gridDim.x), 1u);
     if (blockIdx.x < nwg) aux_jobs(G, blockIdx.x * REG_WAVES + k, nwg * REG_WAVES);
     return;
   }
   const uint32_t s = blockIdx.x * REG_WAVES + wv;
-  if (bt.n == 0u || s > bk.S) return;  // no match job in this launch / no symbol
+  const uint32_t ng = args.ng;
+  if (ng == 0u || s > bk.S) return;  // no match job in this launch / no symbol
 #ifdef ME_STAMPS
   unsigned long long st_t0 = stamp_now();
 #endif
-  const bool bucketed = bt.bcnt != nullptr;
+  const bool bucketed = args.bt[0].bcnt != nullptr;
   const uint32_t L = bk.L;
   const uint32_t sl = s < bk.S ? s : bk.S - 1u;  // the bad-symbol wave's ladder loads are discarded
-  // ---- one round trip: the bin's record count and bucket, ladder rows, tail fills, symbol scalars,
-  // parked free chunks (no predicated loads: row 1 of a 64-level ladder re-reads row 0 and is then
-  // discarded; bucket slots past the count are never used)
-  uint32_t lo = 0, ns;
-  unsigned long long bq0 = 0, bq1 = 0;
-  long long bp0 = 0, bp1 = 0;
-  int bn0 = 0, bn1 = 0;
-  uint32_t bo0 = 0, bo1 = 0;
-  if (bucketed) {
-    const size_t bb = (size_t)s * BK_CAP;
-    ns = bt.bcnt[(size_t)s * BK_CNT_STRIDE];
-    bq0 = bt.b_seq[bb + lane];
-    bq1 = bt.b_seq[bb + 64 + lane];
-    bp0 = bt.b_px[bb + lane];
-    bp1 = bt.b_px[bb + 64 + lane];
-    bn0 = bt.b_qty[bb + lane];
-    bn1 = bt.b_qty[bb + 64 + lane];
-    bo0 = bt.b_ok[bb + lane];
-    bo1 = bt.b_ok[bb + 64 + lane];
-  } else if (bt.bin_start) {  // single-pass sort: the run table
-    lo = bt.bin_start[s];
-    ns = bt.bin_start[s + 1] - lo;
+  // ---- one round trip: the symbol's record count in every batch of the group, ladder rows, tail
+  // fills, symbol scalars, parked free chunks (no predicated loads: row 1 of a 64-level ladder
+  // re-reads row 0 and is then discarded)
+  uint32_t lo = 0, nsv = 0, ns;
+  if (bucketed) {  // lane g < ng: the symbol's count in batch g
+    const uint32_t gl = min((uint32_t)lane, ng - 1u);
+    const uint32_t* cp = G.bt[gl].bcnt;
+    nsv = (uint32_t)lane < ng ? cp[(size_t)s * BK_CNT_STRIDE] : 0u;
+    ns = 0;
+  } else if (args.bt[0].bin_start) {  // single-pass sort: the run table
+    lo = args.bt[0].bin_start[s];
+    ns = args.bt[0].bin_start[s + 1] - lo;
   } else {
-    lo = wave_lower_bound(bt.skeys, bt.n, s);
-    ns = wave_lower_bound(bt.skeys, bt.n, s + 1) - lo;
+    lo = wave_lower_bound(args.bt[0].skeys, args.bt[0].n, s);
+    ns = wave_lower_bound(args.bt[0].skeys, args.bt[0].n, s + 1) - lo;
   }
   const Level* p_lv = bk.levels + (size_t)sl * L;
   const uint8_t* p_tend = bk.tend + (size_t)sl * L;
@@ -894,19 +885,20 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(BookDev bk, Batch
   const SymState st = bk.sym[sl];
   const uint32_t fst = bk.fcache[(size_t)sl * FSTK + lane];
   const uint32_t gsv = bk.gsym[sl];
+  if (bucketed) {
+    // a count above the bucket keeps its bit in the rescan mask (rare; at most ME_GMAX lanes)
+    long long t = (long long)nsv;
+    for (int d = 1; d < 8; d <<= 1) t += __shfl_xor(t, d, 64);
+    ns = (uint32_t)rli64(t, 0);
+  }
   if (ns == 0u) return;
-  if (bucketed && lane == 0) bt.bcnt[(size_t)s * BK_CNT_STRIDE] = 0u;  // ready for the next batch's k_bucket
-  if (s == bk.S) {
-    if (bucketed)
-      reject_bad_bucket(&lds[wv], G, s, ns, bo0, bo1);
-    else
-      reject_bad_symbols(bt, lo, lo + ns);
+  if (s == bk.S) {  // the sort path's bad-symbol bin (bucketed batches carry none)
+    reject_bad_run(G, lo, lo + ns);
     return;
   }
   RegCtx c;
   c.chunks = vptr(bk.chunks);
   c.loc = vptr(bk.loc);
-  c.scratch = vptr(bt.scratch);
   c.G = &G;
   c.M = &lds[wv];
   c.nchunks = bk.nchunks;
@@ -936,204 +928,236 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(BookDev bk, Batch
     c.M->free_head = st.free_head;
     c.M->bump_cur = 0;
     c.M->bump_end = 0;
-    c.M->scan_cur = 0;
-    c.M->scan_cnt = 0;
-    c.M->scan_pos = 0;
   }
   c.nfs = min(rl32(st.nfree, 0), (uint32_t)FSTK);
   c.fstk = fst;
   c.resting = (int)rl32(st.resting, 0);
-  c.wptr = s * bt.slab;
-  c.wend = c.wptr + bt.slab;
+  c.wptr = 0;
+  c.wend = 0;
   c.recs_left = ns;
-  // ---- batch order. A bucket (<= BK_CAP records, arbitrary order) is staged in LDS and its keys
-  // (batch index << 7 | bucket slot) sorted across the wave; an overfull bucket is replaced by a
-  // rescan of the batch (1024-record windows, batch order by construction).
-  // 0: bucket, 1: rescan, 2: sort path (perm)
-  const uint32_t mode = bucketed ? (ns <= (uint32_t)BK_CAP ? 0u : 1u) : 2u;
-  uint32_t k0 = ~0u, k1 = ~0u;
-  if (mode == 0u) {
-    c.M->in.b.seq[lane] = bq0;
-    c.M->in.b.seq[64 + lane] = bq1;
-    c.M->in.b.px[lane] = bp0;
-    c.M->in.b.px[64 + lane] = bp1;
-    c.M->in.b.qty[lane] = bn0;
-    c.M->in.b.qty[64 + lane] = bn1;
-    c.M->in.b.ok[lane] = bo0;
-    c.M->in.b.ok[64 + lane] = bo1;
-    k0 = (uint32_t)lane < ns ? ((bo0 & BK_IDX_MASK) << 7) | (uint32_t)lane : ~0u;
-    k1 = 64u + (uint32_t)lane < ns ? ((bo1 & BK_IDX_MASK) << 7) | (64u + (uint32_t)lane) : ~0u;
-    if (ns > 64u)
-      sort128(k0, k1);
-    else
-      k0 = sort64(k0, false);
-  }
-  if (lane == 0) {  // read back where used: nothing of this holds an SGPR across the serial loop
-    c.M->mode = mode;
-    c.M->run_lo = lo;
-    c.M->run_n = ns;
-  }
-  STAMP_ADD(c, PH_PROLOGUE);
-  // left: records of the symbol not yet visited (its count; the rescan keeps its own cursors)
-  for (uint32_t left = ns;;) {
-    // ---- up to 64 records in vector form, batch order
-    uint32_t oi, cnt;
-    unsigned long long oseq_;
-    long long opx_;
-    int oq_;
-    uint32_t kd_;
-    const uint32_t md = ldsu(c.M->mode);
-    if (md == 0u) {
-      if (left == 0u) break;
-      cnt = min(64u, left);
-      const uint32_t pos = k0 & (BK_CAP - 1);  // past the count: key ~0, slot 127 (discarded)
-      oi = k0 >> 7;
-      k0 = k1;  // the second block, if any
-      oseq_ = c.M->in.b.seq[pos];
-      opx_ = c.M->in.b.px[pos];
-      oq_ = c.M->in.b.qty[pos];
-      kd_ = c.M->in.b.ok[pos] >> BK_KIND_SHIFT;
-    } else {
-      if (md == 1u) {
-        if (ldsu(c.M->scan_pos) >= ldsu(c.M->scan_cnt) && !rescan_window(c.M, G, s)) break;
-        const uint32_t p0 = ldsu(c.M->scan_pos), lc = ldsu(c.M->scan_cnt);
-        cnt = min(64u, lc - p0);
-        oi = c.M->in.lst[p0 + min((uint32_t)lane, cnt - 1u)];
-        ldsw(c.M->scan_pos, p0 + cnt);
-      } else {
+  // ---- the batches of the group, in stream order; the book stays on chip between them
+  ldsw(c.M->g_next, 0u);
+  ldsw(c.M->run_lo, lo);  // the sort path's run (one batch)
+  ldsw(c.M->run_n, ns);
+  for (;;) {  // the batch cursor lives in LDS: no SGPR of it is live across the serial loop
+    const uint32_t g = ldsu(c.M->g_next);
+    if (g >= ldsu(G.ng)) break;
+    ldsw(c.M->g_next, g + 1u);
+    ldsw(c.M->g_cur, g);
+    uint32_t nsg = ldsu(c.M->run_n);
+    uint32_t k0 = ~0u, k1 = ~0u;
+    uint32_t mode = 2u;  // 0: bucket, 1: rescan, 2: sort path (perm)
+    if (ldsu(G.bt[0].bcnt) != nullptr) {
+      nsg = rl32(nsv, (int)g);
+      if (nsg == 0u) continue;
+      const BatchDev& B = G.bt[g];
+      const size_t bb = (size_t)s * BK_CAP;
+      const gptr<const uint64_t> pseq = ldsg(B.b_seq);
+      const gptr<const int64_t> ppx = ldsg(B.b_px);
+      const gptr<const int32_t> pqty = ldsg(B.b_qty);
+      const gptr<const uint32_t> pok = ldsg(B.b_ok);
+      const unsigned long long bq0 = pseq[bb + lane], bq1 = pseq[bb + 64 + lane];
+      const long long bp0 = ppx[bb + lane], bp1 = ppx[bb + 64 + lane];
+      const int bn0 = pqty[bb + lane], bn1 = pqty[bb + 64 + lane];
+      const uint32_t bo0 = pok[bb + lane], bo1 = pok[bb + 64 + lane];
+      if (lane == 0) ldsg(B.bcnt)[(size_t)s * BK_CNT_STRIDE] = 0u;  // ready for a later group's bucket job
+      // ---- batch order. A bucket (<= BK_CAP records, arbitrary order) is staged in LDS and its keys
+      // (batch index << 7 | bucket slot) sorted across the wave; an overfull bucket is replaced by a
+      // rescan of the batch (1024-record windows, batch order by construction).
+      mode = nsg <= (uint32_t)BK_CAP ? 0u : 1u;
+      if (mode == 0u) {
+        c.M->in.b.seq[lane] = bq0;
+        c.M->in.b.seq[64 + lane] = bq1;
+        c.M->in.b.px[lane] = bp0;
+        c.M->in.b.px[64 + lane] = bp1;
+        c.M->in.b.qty[lane] = bn0;
+        c.M->in.b.qty[64 + lane] = bn1;
+        c.M->in.b.ok[lane] = bo0;
+        c.M->in.b.ok[64 + lane] = bo1;
+        k0 = (uint32_t)lane < nsg ? ((bo0 & BK_IDX_MASK) << 7) | (uint32_t)lane : ~0u;
+        k1 = 64u + (uint32_t)lane < nsg ? ((bo1 & BK_IDX_MASK) << 7) | (64u + (uint32_t)lane) : ~0u;
+        if (nsg > 64u)
+          sort128(k0, k1);
+        else
+          k0 = sort64(k0, false);
+      }
+    }
+    c.scratch = vptr(ldsu(G.bt[g].scratch));
+    c.wptr = s * ldsu(G.bt[g].slab);
+    c.wend = c.wptr + ldsu(G.bt[g].slab);
+    c.recs_left = nsg;
+    if (lane == 0) {  // read back where used: nothing of this holds an SGPR across the serial loop
+      c.M->mode = mode;
+      c.M->scan_cur = 0;
+      c.M->scan_cnt = 0;
+      c.M->scan_pos = 0;
+    }
+    STAMP_ADD(c, PH_PROLOGUE);
+    // left: records of the symbol not yet visited (its count; the rescan keeps its own cursors)
+    for (uint32_t left = nsg;;) {
+      // ---- up to 64 records in vector form, batch order
+      uint32_t oi, cnt;
+      unsigned long long oseq_;
+      long long opx_;
+      int oq_;
+      uint32_t kd_;
+      const uint32_t md = ldsu(c.M->mode);
+      if (md == 0u) {
         if (left == 0u) break;
         cnt = min(64u, left);
-        const uint32_t at = ldsu(c.M->run_lo) + (ldsu(c.M->run_n) - left);
-        oi = ldsg(G.bt.perm)[at + min((uint32_t)lane, cnt - 1u)];  // clamp: never branch around a load
-      }
-      oseq_ = ldsg(G.bt.seq)[oi];
-      opx_ = ldsg(G.bt.px)[oi];
-      oq_ = ldsg(G.bt.qty)[oi];
-      kd_ = ldsg(G.bt.kind)[oi];
-    }
-    const uint32_t j = (uint32_t)lane;  // record j of the block
-    const uint32_t hi = cnt;
-    const unsigned long long max_seq = ldsu(G.bk.max_seq);
-    const long long lbase = c.base;
-    // validation in vector form; only the packed control word and the reject code stay live
-    uint32_t cw, rj;
-    {
-      const bool v = j < hi;
-      const unsigned long long oseq = v ? oseq_ : 0ull;
-      const long long opx = v ? opx_ : 0ll;
-      const int oq = v ? oq_ : 0;
-      const uint32_t kd = v ? kd_ : 0u;
-      const uint32_t side = kd & 3u;
-      const bool market = (kd >> 2) & 1u, cancel = (kd >> 3) & 1u;
-      const bool buy = side == ME_SIDE_BUY;
-      const bool oow = opx < lbase || (unsigned long long)(opx - lbase) >= (unsigned long long)L;
-      rj = ME_RJ_NONE;
-      if (!cancel) {
-        if (oq <= 0)
-          rj = ME_RJ_BAD_QTY;
-        else if (side != ME_SIDE_BUY && side != ME_SIDE_SELL)
-          rj = ME_RJ_BAD_SIDE;
-        else if (!market && oow)
-          rj = ME_RJ_OUT_OF_WINDOW;
-        else if (oseq == 0ull || oseq >= max_seq)
-          rj = ME_RJ_BAD_SEQ;
-      }
-      const uint32_t lim = market ? (buy ? L - 1u : 0u) : (oow ? 0u : (uint32_t)(opx - lbase));
-      cw = lim | (buy ? CW_BUY : 0u) | (market ? CW_MKT : 0u) | (cancel ? CW_CXL : 0u);
-      if (!v) rj = 0xFFu;  // lanes past the run: no record
-    }
-    unsigned long long work = __ballot(rj == ME_RJ_NONE);
-    uint32_t stop = cnt;  // records [0, stop) of the block get results
-    uint32_t out_q = 0, out_n = 0, out_w = 0;
-#ifdef ME_STAMPS
-    __builtin_amdgcn_s_waitcnt(0);
-#endif
-    STAMP_ADD(c, PH_FETCH);
-    // ---- the serial chain: records that touch the book, in seq order
-    while (work) {
-      const int k = __builtin_ctzll(work);
-      work &= work - 1ull;
-      const uint32_t ctl = rl32(cw, k);
-      c.recs_left = left - (uint32_t)k;
-      uint32_t outq;
-      COUNT(c, CT_FAST);
-      STAMP_ADD(c, PH_SWEEP);
-      if (ME_UNLIKELY(ctl & CW_CXL)) {
-        outq = reg_cancel(c, (unsigned long long)rli64(opx_, k));
-        STAMP_ADD(c, PH_CANCEL);
+        const uint32_t pos = k0 & (BK_CAP - 1);  // past the count: key ~0, slot 127 (discarded)
+        oi = k0 >> 7;
+        k0 = k1;  // the second block, if any
+        oseq_ = c.M->in.b.seq[pos];
+        opx_ = c.M->in.b.px[pos];
+        oq_ = c.M->in.b.qty[pos];
+        kd_ = c.M->in.b.ok[pos] >> BK_KIND_SHIFT;
       } else {
-        if (ME_UNLIKELY(c.wptr + (uint32_t)c.resting > c.wend) && !reg_reserve_overflow(c)) {
-          stop = (uint32_t)k;
-          break;
+        if (md == 1u) {
+          if (ldsu(c.M->scan_pos) >= ldsu(c.M->scan_cnt) && !rescan_window(c.M, G, ldsu(c.M->g_cur), s)) break;
+          const uint32_t p0 = ldsu(c.M->scan_pos), lc = ldsu(c.M->scan_cnt);
+          cnt = min(64u, lc - p0);
+          oi = c.M->in.lst[p0 + min((uint32_t)lane, cnt - 1u)];
+          ldsw(c.M->scan_pos, p0 + cnt);
+        } else {
+          if (left == 0u) break;
+          cnt = min(64u, left);
+          const uint32_t at = ldsu(c.M->run_lo) + (ldsu(c.M->run_n) - left);
+          oi = ldsg(G.bt[0].perm)[at + min((uint32_t)lane, cnt - 1u)];  // clamp: never branch around a load
         }
-        const unsigned long long seq = rl64(oseq_, k);
-        const uint32_t q = (uint32_t)rli32(oq_, k);
-        const int lm = (int)(ctl & 0xFFu);
-        const uint32_t w_in = c.wptr;
-        uint32_t rem = q;
-        // one walk loop for both sides (one copy of the walk): the opposite best moves away from
-        // the taker's limit as levels empty
-        const bool buy = (ctl & CW_BUY) != 0u;
-        int lvl = buy ? c.ba : c.bb;
-        for (;;) {
-          const int gap = buy ? lm - lvl : lvl - lm;  // >= 0: the level crosses the limit (int select, scalar)
-          if (rem == 0u || gap < 0) break;
-          if (ME_LIKELY(!reg_walk(c, lvl, rem, seq))) break;
-          lvl = buy ? c.occ.next(lvl + 1) : c.occ.prev(lvl - 1);
-        }
-        if (buy)
-          c.ba = lvl;
-        else
-          c.bb = lvl;
-        outq = q - rem;
-        STAMP_ADD(c, PH_WALK);
-        const bool me_ = lane == k;
-        out_n = me_ ? c.wptr - w_in : out_n;
-        out_w = me_ ? w_in : out_w;
-        if (!(ctl & CW_MKT) && rem != 0u && ME_UNLIKELY(!reg_rest(c, lm, seq, rem, (ctl & CW_BUY) != 0u))) {
-          stop = (uint32_t)k;  // chunk pool exhausted: the batch fails (sticky error word)
-          break;
-        }
-        STAMP_ADD(c, PH_REST);
+        const BatchDev& B = G.bt[ldsu(c.M->g_cur)];
+        oseq_ = ldsg(B.seq)[oi];
+        opx_ = ldsg(B.px)[oi];
+        oq_ = ldsg(B.qty)[oi];
+        kd_ = ldsg(B.kind)[oi];
       }
-      out_q = lane == k ? outq : out_q;
-    }
-    // ---- results of the block in vector form
-    me_order_result* res = ldsg(G.bt.res);
-    uint32_t* fstart = ldsg(G.bt.fstart);
-    uint32_t* tile_sum = ldsg(G.bt.tile_sum);
-    if (rj != 0xFFu && (uint32_t)lane < stop) {
-      const bool market = (kd_ >> 2) & 1u, cancel = (kd_ >> 3) & 1u;
-      me_order_result r;
-      r.tape_offset = 0;
-      r.pad[0] = r.pad[1] = 0;
-      r.fill_count = out_n;
-      r.reason = (uint8_t)rj;
-      if (rj != ME_RJ_NONE) {
-        r.filled_qty = 0;
-        r.remaining_qty = rj == ME_RJ_BAD_QTY ? 0 : oq_;
-        r.status = ME_ST_REJECTED;
-      } else if (cancel) {
-        r.filled_qty = 0;
-        r.remaining_qty = (int)out_q;
-        r.status = out_q ? ME_ST_CANCELED : ME_ST_REJECTED;
-        r.reason = out_q ? ME_RJ_NONE : ME_RJ_UNKNOWN_ORDER;
-      } else {
-        const int rem = oq_ - (int)out_q;
-        r.filled_qty = (int)out_q;
-        r.remaining_qty = rem;
-        r.status = rem == 0 ? ME_ST_FILLED
-                 : market   ? ME_ST_CANCELED
-                 : out_q    ? ME_ST_PARTIALLY_FILLED
-                            : ME_ST_NEW;
+      const uint32_t j = (uint32_t)lane;  // record j of the block
+      const uint32_t hi = cnt;
+      const unsigned long long max_seq = ldsu(G.bk.max_seq);
+      const long long lbase = c.base;
+      // validation in vector form; only the packed control word and the reject code stay live
+      uint32_t cw, rj;
+      {
+        const bool v = j < hi;
+        const unsigned long long oseq = v ? oseq_ : 0ull;
+        const long long opx = v ? opx_ : 0ll;
+        const int oq = v ? oq_ : 0;
+        const uint32_t kd = v ? kd_ : 0u;
+        const uint32_t side = kd & 3u;
+        const bool market = (kd >> 2) & 1u, cancel = (kd >> 3) & 1u;
+        const bool buy = side == ME_SIDE_BUY;
+        const bool oow = opx < lbase || (unsigned long long)(opx - lbase) >= (unsigned long long)L;
+        rj = ME_RJ_NONE;
+        if (!cancel) {
+          if (oq <= 0)
+            rj = ME_RJ_BAD_QTY;
+          else if (side != ME_SIDE_BUY && side != ME_SIDE_SELL)
+            rj = ME_RJ_BAD_SIDE;
+          else if (!market && oow)
+            rj = ME_RJ_OUT_OF_WINDOW;
+          else if (oseq == 0ull || oseq >= max_seq)
+            rj = ME_RJ_BAD_SEQ;
+        }
+        const uint32_t lim = market ? (buy ? L - 1u : 0u) : (oow ? 0u : (uint32_t)(opx - lbase));
+        cw = lim | (buy ? CW_BUY : 0u) | (market ? CW_MKT : 0u) | (cancel ? CW_CXL : 0u);
+        if (!v) rj = 0xFFu;  // lanes past the run: no record
       }
-      res[oi] = r;
-      fstart[oi] = out_w;
-      if (out_n) atomicAdd(&tile_sum[oi / TILE_TAPE], out_n);
+      unsigned long long work = __ballot(rj == ME_RJ_NONE);
+      uint32_t stop = cnt;  // records [0, stop) of the block get results
+      uint32_t out_q = 0, out_n = 0, out_w = 0;
+  #ifdef ME_STAMPS
+      __builtin_amdgcn_s_waitcnt(0);
+  #endif
+      STAMP_ADD(c, PH_FETCH);
+      // ---- the serial chain: records that touch the book, in seq order
+      while (work) {
+        const int k = __builtin_ctzll(work);
+        work &= work - 1ull;
+        const uint32_t ctl = rl32(cw, k);
+        c.recs_left = left - (uint32_t)k;
+        uint32_t outq;
+        COUNT(c, CT_FAST);
+        STAMP_ADD(c, PH_SWEEP);
+        if (ME_UNLIKELY(ctl & CW_CXL)) {
+          outq = reg_cancel(c, (unsigned long long)rli64(opx_, k));
+          STAMP_ADD(c, PH_CANCEL);
+        } else {
+          if (ME_UNLIKELY(c.wptr + (uint32_t)c.resting > c.wend) && !reg_reserve_overflow(c)) {
+            stop = (uint32_t)k;
+            break;
+          }
+          const unsigned long long seq = rl64(oseq_, k);
+          const uint32_t q = (uint32_t)rli32(oq_, k);
+          const int lm = (int)(ctl & 0xFFu);
+          const uint32_t w_in = c.wptr;
+          uint32_t rem = q;
+          // one walk loop for both sides (one copy of the walk): the opposite best moves away from
+          // the taker's limit as levels empty
+          const bool buy = (ctl & CW_BUY) != 0u;
+          int lvl = buy ? c.ba : c.bb;
+          for (;;) {
+            const int gap = buy ? lm - lvl : lvl - lm;  // >= 0: the level crosses the limit (int select, scalar)
+            if (rem == 0u || gap < 0) break;
+            if (ME_LIKELY(!reg_walk(c, lvl, rem, seq))) break;
+            lvl = buy ? c.occ.next(lvl + 1) : c.occ.prev(lvl - 1);
+          }
+          if (buy)
+            c.ba = lvl;
+          else
+            c.bb = lvl;
+          outq = q - rem;
+          STAMP_ADD(c, PH_WALK);
+          const bool me_ = lane == k;
+          out_n = me_ ? c.wptr - w_in : out_n;
+          out_w = me_ ? w_in : out_w;
+          if (!(ctl & CW_MKT) && rem != 0u && ME_UNLIKELY(!reg_rest(c, lm, seq, rem, (ctl & CW_BUY) != 0u))) {
+            stop = (uint32_t)k;  // chunk pool exhausted: the batch fails (sticky error word)
+            break;
+          }
+          STAMP_ADD(c, PH_REST);
+        }
+        out_q = lane == k ? outq : out_q;
+      }
+      // ---- results of the block in vector form
+      me_order_result* res = ldsg(G.bt[ldsu(c.M->g_cur)].res);
+      uint32_t* fstart = ldsg(G.bt[ldsu(c.M->g_cur)].fstart);
+      uint32_t* tile_sum = ldsg(G.bt[ldsu(c.M->g_cur)].tile_sum);
+      if (rj != 0xFFu && (uint32_t)lane < stop) {
+        const bool market = (kd_ >> 2) & 1u, cancel = (kd_ >> 3) & 1u;
+        me_order_result r;
+        r.tape_offset = 0;
+        r.pad[0] = r.pad[1] = 0;
+        r.fill_count = out_n;
+        r.reason = (uint8_t)rj;
+        if (rj != ME_RJ_NONE) {
+          r.filled_qty = 0;
+          r.remaining_qty = rj == ME_RJ_BAD_QTY ? 0 : oq_;
+          r.status = ME_ST_REJECTED;
+        } else if (cancel) {
+          r.filled_qty = 0;
+          r.remaining_qty = (int)out_q;
+          r.status = out_q ? ME_ST_CANCELED : ME_ST_REJECTED;
+          r.reason = out_q ? ME_RJ_NONE : ME_RJ_UNKNOWN_ORDER;
+        } else {
+          const int rem = oq_ - (int)out_q;
+          r.filled_qty = (int)out_q;
+          r.remaining_qty = rem;
+          r.status = rem == 0 ? ME_ST_FILLED
+                   : market   ? ME_ST_CANCELED
+                   : out_q    ? ME_ST_PARTIALLY_FILLED
+                              : ME_ST_NEW;
+        }
+        res[oi] = r;
+        fstart[oi] = out_w;
+        if (out_n) atomicAdd(&tile_sum[oi / TILE_TAPE], out_n);
+      }
+      STAMP_ADD(c, PH_RESULT);
+      left -= cnt;
+      if (stop < cnt) {  // capacity failure: the sticky error word fails the launch
+        ldsw(c.M->g_next, ME_GMAX);
+        break;
+      }
     }
-    STAMP_ADD(c, PH_RESULT);
-    left -= cnt;
-    if (stop < cnt) break;
   }
   // ---- write the symbol back
   {  // unused reserved chunks
@@ -1195,18 +1219,30 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(BookDev bk, Batch
 #endif
 }
 
-// One launch: the match job of bt (bt.n == 0: none) on (S + 1) / REG_WAVES workgroups and the side
-// jobs of ax on every workgroup's extra waves (at least ~256 side-job records per wave).
-hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev& bt, const AuxDev& ax, hipEvent_t ev0,
-                            hipEvent_t ev1) {
+// One launch: the match job of bt[0, ng) (ng == 0: none) on S / REG_WAVES workgroups (S + 1 for the
+// sort path's bad-symbol bin) and the side jobs of ax on the first dispatch round's extra waves.
+hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* bt, uint32_t ng, const AuxDev& ax,
+                            hipEvent_t ev0, hipEvent_t ev1) {
   if (bk.L > (uint32_t)RL || bk.L < 64u || !bk.fcache || !bk.gsym) return hipErrorInvalidValue;
+  if (ng > (uint32_t)ME_GMAX || ax.nb > (uint32_t)ME_GMAX || ax.nt > (uint32_t)ME_GMAX) return hipErrorInvalidValue;
+  ColdArgs A{};
+  A.bk = bk;
+  A.ax = ax;
+  A.ng = ng;
+  for (uint32_t g = 0; g < ng; ++g) {
+    // the group's batches are all bucketed, or it is one sort-path batch
+    if (bt[g].n == 0u || (g > 0 && (!bt[g].bcnt || !bt[0].bcnt))) return hipErrorInvalidValue;
+    A.bt[g] = bt[g];
+  }
   // bucketed batches carry no bad-symbol bin (the bucket job rejects those records)
-  const uint32_t waves = bt.bcnt ? bk.S : bk.S + 1;
-  const uint32_t match_wgs = bt.n ? (waves + REG_WAVES - 1) / REG_WAVES : 0u;
-  const uint32_t work = max(ax.n, ax.tn);
-  const uint32_t aux_wgs = (work + 256u * REG_WAVES - 1) / (256u * REG_WAVES);
+  const uint32_t waves = ng && A.bt[0].bcnt ? bk.S : bk.S + 1;
+  const uint32_t match_wgs = ng ? (waves + REG_WAVES - 1) / REG_WAVES : 0u;
+  uint32_t nbr = 0, ntr = 0;
+  for (uint32_t j = 0; j < ax.nb; ++j) nbr += ax.b[j].n;
+  for (uint32_t j = 0; j < ax.nt; ++j) ntr += ax.t[j].tn;
+  const uint32_t aux_wgs = min((max(nbr, ntr) + 256u * REG_WAVES - 1) / (256u * REG_WAVES), max(ax.nwg, 1u));
   const uint32_t grid = max(max(match_wgs, aux_wgs), 1u);
-  hipExtLaunchKernelGGL(k_match_reg, dim3(grid), dim3(128 * REG_WAVES), 0, st, ev0, ev1, 0, bk, bt, ax);
+  hipExtLaunchKernelGGL(k_match_reg, dim3(grid), dim3(128 * REG_WAVES), 0, st, ev0, ev1, 0, A);
   return hipGetLastError();
 }
 

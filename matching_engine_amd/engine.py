@@ -105,6 +105,7 @@ class Engine:
         max_chunks: int = 0,
         device: int = 0,
         symbol_ids=None,
+        batches_per_launch: int = 0,
     ):
         self.lib = _abi.load()
         self.num_symbols = int(num_symbols)
@@ -122,6 +123,7 @@ class Engine:
             max_seq,
             self._base.ctypes.data_as(C.POINTER(C.c_int64)),
             None if self._ids is None else self._ids.ctypes.data_as(C.POINTER(C.c_uint32)),
+            batches_per_launch,
         )
         self.max_batch = int(max_batch)
         h = self.lib.me_create(C.byref(cfg))

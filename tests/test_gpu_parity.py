@@ -273,15 +273,24 @@ def test_full_size_config2_bitexact(me, orc):
 
 
 
-def test_back_to_back_device_batches(me, orc):
-    """Device batches submitted back to back without a sync (the bench's pattern): the final books,
-    the resting count, the fill total and the last batch's results/tape equal the oracle's."""
-    sc = me.preset(2)
+@pytest.mark.parametrize("group", [1, 3, 8])
+@pytest.mark.parametrize("stream", ["uniform", "skewed"])
+def test_back_to_back_device_batches(me, orc, group, stream):
+    """Device batches submitted back to back without a sync (the bench's pattern), matched
+    `group` batches per launch: the final books, the resting count, the fill total and the last
+    batch's results/tape equal the oracle's. The skewed stream (Zipf symbols) overfills buckets
+    (the rescan path) and carries unknown-symbol records (rejected by the bucket job)."""
+    over = {} if stream == "uniform" else dict(zipf_s=1.2)
+    sc = me.preset(2, **over)
     st = me.Stream(sc)
     base = st.base_prices()
     batches = [st.next(sc.batch) for _ in range(12)]
+    if stream == "skewed":
+        for k, b in enumerate(batches):
+            b.symbol[k * 97 % len(b)::4099] = sc.num_symbols + 3  # unknown symbols
     ob = orc.OracleBook(sc.num_symbols, sc.levels, base, 1 << 22)
-    with engine_for(me, sc.num_symbols, sc.levels, base, sc.batch, 1 << 20, 1 << 22) as eng:
+    with engine_for(me, sc.num_symbols, sc.levels, base, sc.batch, 1 << 20, 1 << 22,
+                    batches_per_launch=group) as eng:
         dbs = [eng.upload(b) for b in batches]
         eng.timing_enable(True)
         for db in dbs:
@@ -294,8 +303,32 @@ def test_back_to_back_device_batches(me, orc):
         assert_results_equal(r, ro, "back-to-back last batch")
         assert_fills_equal(f, fo, "back-to-back last batch")
         tm = eng.timing_read()
-        assert tm["fills"] == nfo and tm["launches"] == len(batches) and tm["match_ms"] > 0
+        assert tm["fills"] == nfo and tm["launches"] == -(-len(batches) // group) and tm["match_ms"] > 0
         assert_books_equal(eng, ob, range(0, sc.num_symbols, 5), "back-to-back")
         assert eng.resting_count() == ob.resting()
         for db in dbs:
             db.free()
+
+
+def test_partial_groups_between_fetches(me, orc):
+    """Runs of 1..7 device batches between fetches: every fetch flushes a partial group, and the
+    next group starts over; every fetched batch equals the oracle's."""
+    sc = me.preset(2, num_symbols=512, batch=8192)
+    st = me.Stream(sc)
+    base = st.base_prices()
+    ob = orc.OracleBook(sc.num_symbols, sc.levels, base, 1 << 22)
+    with engine_for(me, sc.num_symbols, sc.levels, base, sc.batch, 1 << 18, 1 << 22) as eng:
+        for run in (1, 7, 2, 8, 5, 3):
+            batches = [st.next(sc.batch) for _ in range(run)]
+            dbs = [eng.upload(b) for b in batches]
+            for db in dbs:
+                eng.submit_device(db)
+            r, f = eng.fetch_outputs(len(batches[-1]))
+            for b in batches:
+                ro, fo = ob.submit(b)
+            assert_results_equal(r, ro, f"run {run}")
+            assert_fills_equal(f, fo, f"run {run}")
+            for db in dbs:
+                db.free()
+        assert_books_equal(eng, ob, range(0, sc.num_symbols, 3), "partial groups")
+        assert eng.resting_count() == ob.resting()
