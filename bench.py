@@ -68,7 +68,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
-    ap.add_argument("--timing-every", type=int, default=8,
+    ap.add_argument("--timing-every", type=int, default=4,
                     help="HIP events on every k-th match launch of the timed loop (each timed launch costs "
                          "the stream a few us; 1 = every launch, 0 = off)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
