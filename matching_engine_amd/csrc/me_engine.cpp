@@ -3,6 +3,7 @@
 // C-ABI of include/me_engine.h. No CPU matching path exists here: without a HIP device
 // me_create fails and every call reports it.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -30,6 +31,7 @@ hipError_t launch_tape(hipStream_t st, const BatchDev& bt, me_fill* tape, unsign
                        unsigned long long* tape_count, unsigned long long* fills_acc, uint32_t* err);
 hipError_t launch_init_levels(hipStream_t st, Level* levels, size_t count);
 hipError_t launch_init_chunks(hipStream_t st, Chunk* chunks, size_t count);
+hipError_t prepare_hot(const BookDev& bk);
 }  // namespace me
 
 using namespace me;
@@ -59,6 +61,10 @@ struct me_engine {
   uint64_t* d_seq = nullptr;
   int64_t* d_px = nullptr;
   int32_t* d_qty = nullptr;
+  // Deep windows (L > LDS_MAX_LEVELS): hand-off list of busy symbols to k_match_hot
+  // ([0] = count, then symbol ids) and the record count that makes a symbol busy (0 = off).
+  uint32_t* d_hot = nullptr;
+  uint32_t hot_min = 0;
   uint32_t* d_sym = nullptr;
   uint8_t* d_kind = nullptr;
   // Everything the grouping sort of a batch writes: sorted keys, permutation, histogram, run
@@ -160,7 +166,8 @@ static void free_all(me_engine* e) {
   void* ptrs[] = {e->bk.levels,   e->bk.occ,      e->bk.sym,      e->bk.chunks,     e->bk.tend,
                   e->bk.loc,      e->bk.chunk_top, e->bk.err,       (void*)e->bk.gsym,
                   e->d_seq,       e->d_px,        e->d_qty,       e->d_sym,         e->d_kind,
-                  e->d_tape,      e->d_tape_count, e->d_fills_acc, e->bk.dbg,      e->bk.fcache};
+                  e->d_tape,      e->d_tape_count, e->d_fills_acc, e->bk.dbg,      e->bk.fcache,
+                  e->d_hot};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   {
@@ -382,6 +389,18 @@ extern "C" me_engine* me_create(const me_config* cfg) {
   ALLOC(e->d_tape, scap * e->group);
   ALLOC(e->d_tape_count, ME_GMAX);
   ALLOC(e->d_fills_acc, 1);
+  if (L > LDS_MAX_LEVELS) {
+    // ME_HOT_MIN=n (opt-in, A/B runs): symbols with >= n records in a batch get an LDS-resident
+    // ladder window (k_match_hot). Off by default: measured slower than the HBM ladder on config 4
+    // (DESIGN.md §8 — the hot wave is bound by dependent chunk loads and issue, not level reads).
+    e->hot_min = 0;
+    if (const char* v = getenv("ME_HOT_MIN")) e->hot_min = (uint32_t)strtoul(v, nullptr, 10);
+    if (e->hot_min) {
+      ALLOC(e->d_hot, 1 + HOT_MAX);
+      hipError_t he = prepare_hot(bk);
+      if (he != hipSuccess) return bail(std::string("k_match_hot LDS window: ") + hipGetErrorString(he));
+    }
+  }
 #ifdef ME_STAMPS
   ALLOC(bk.dbg, S * 24);
   (void)hipMemset(bk.dbg, 0, S * 24 * 8);
@@ -628,6 +647,8 @@ static int enqueue_batch(me_engine* e, const uint64_t* seq, const int64_t* px, c
   bt.skeys = kin;
   bt.perm = iin;
   bt.bin_start = run_table;  // bins are symbols: the run table
+  bt.hot = e->d_hot;
+  bt.hot_min = e->hot_min;
   // timing: the launch itself records start/end (hipExtLaunchKernelGGL), no marker packets
   hipError_t he = launch_match(st, e->bk, bt, tl.m0, tl.m1);
   if (he != hipSuccess) return e->hip_fail(he, "match launch");

@@ -215,6 +215,13 @@ struct LadderMem {
   __device__ __forceinline__ void set(int l, const Level& x) {
     if (lane_id() == 0) lv[l] = x;
   }
+  __device__ __forceinline__ uint32_t head(int l) const { return rl32(lv[l].head, 0); }
+  // per-lane level read (the sweep's 64-level windows); lanes with !valid read nothing
+  __device__ __forceinline__ Level lane_get(int l, bool valid) const {
+    Level x{0, NIL, NIL};
+    if (valid) x = lv[l];
+    return x;
+  }
   __device__ __forceinline__ uint32_t get_te(int l) const { return rl32((uint32_t)tend[l], 0); }
   __device__ __forceinline__ void set_te(int l, uint32_t v) {
     if (lane_id() == 0) tend[l] = (uint8_t)v;
@@ -359,6 +366,138 @@ struct LadderReg {
   }
 };
 
+
+// LadderWin (k_match_hot, deep windows): one workgroup per hot symbol. The whole occupancy bitmap
+// and a window [wlo, wlo + W) of the ladder (levels + tail fills) around the best prices live in
+// LDS for the launch; levels outside the window stay in HBM. Every accessor branches on the
+// (wave-uniform) level, so top-of-book work never leaves the CU and deep rests cost one HBM
+// round trip as before. LDS pointers are address-space-3 (ds_* instructions: an LDS access never
+// waits on the wave's outstanding global stores, as a flat one would).
+template <class T>
+using lptr = T __attribute__((address_space(3)))*;
+template <class T>
+using gptr1 = T __attribute__((address_space(1)))*;
+
+// Level copies across address spaces go field by field (one 16-B access after merging).
+template <class P>
+__device__ __forceinline__ Level ld_level(P p) {
+  Level x;
+  x.total = p->total;
+  x.head = p->head;
+  x.tail = p->tail;
+  return x;
+}
+template <class P>
+__device__ __forceinline__ void st_level(P p, const Level& x) {
+  p->total = x.total;
+  p->head = x.head;
+  p->tail = x.tail;
+}
+
+struct LadderWin {
+  lptr<Level> wl;                 // LDS levels of the window
+  lptr<uint8_t> wt;               // LDS tail fills of the window
+  lptr<unsigned long long> occ;   // LDS occupancy of the whole ladder
+  gptr1<Level> glv;               // HBM ladder (authoritative outside the window)
+  gptr1<uint8_t> gtend;
+  uint32_t L, Lwords;
+  int wlo;
+  uint32_t W;
+
+  __device__ __forceinline__ bool inw(int l) const { return (uint32_t)(l - wlo) < W; }
+  __device__ __forceinline__ Level get(int l) const {
+    Level x;
+    if (inw(l)) {
+      x = ld_level(wl + (l - wlo));
+    } else {
+      x = ld_level(glv + l);
+    }
+    x.total = rli64(x.total, 0);
+    x.head = rl32(x.head, 0);
+    x.tail = rl32(x.tail, 0);
+    return x;
+  }
+  __device__ __forceinline__ uint32_t head(int l) const { return get(l).head; }
+  __device__ __forceinline__ void set(int l, const Level& x) {
+    if (lane_id() == 0) {
+      if (inw(l))
+        st_level(wl + (l - wlo), x);
+      else
+        st_level(glv + l, x);
+    }
+  }
+  __device__ __forceinline__ Level lane_get(int l, bool valid) const {
+    Level x{0, NIL, NIL};
+    if (valid) {
+      if (inw(l))
+        x = ld_level(wl + (l - wlo));
+      else
+        x = ld_level(glv + l);
+    }
+    return x;
+  }
+  __device__ __forceinline__ uint32_t get_te(int l) const {
+    if (inw(l)) return rl32((uint32_t)wt[l - wlo], 0);
+    return rl32((uint32_t)gtend[l], 0);
+  }
+  __device__ __forceinline__ void set_te(int l, uint32_t v) {
+    if (lane_id() == 0) {
+      if (inw(l))
+        wt[l - wlo] = (uint8_t)v;
+      else
+        gtend[l] = (uint8_t)v;
+    }
+  }
+  __device__ __forceinline__ void occ_set(int l) {
+    if (lane_id() == 0) occ[l >> 6] |= (1ull << (l & 63));
+  }
+  __device__ __forceinline__ void occ_clear(int l) {
+    if (lane_id() == 0) occ[l >> 6] &= ~(1ull << (l & 63));
+  }
+  // Smallest occupied level >= x, or L (64 bitmap words per step from LDS).
+  __device__ int next_occ(int x) const {
+    const int Li = (int)L;
+    if (x >= Li) return Li;
+    if (x < 0) x = 0;
+    const int w = x >> 6;
+    const unsigned long long word = occ[w] & (~0ull << (x & 63));
+    if (word) return (w << 6) + __builtin_ctzll(word);
+    const int lane = lane_id();
+    const int nw = (int)Lwords;
+    for (int b = w + 1; b < nw; b += 64) {
+      const int idx = b + lane;
+      const unsigned long long v = idx < nw ? occ[idx] : 0ull;
+      const unsigned long long m = __ballot(v != 0ull);
+      if (m) {
+        const int t = __builtin_ctzll(m);
+        return ((b + t) << 6) + __builtin_ctzll(rl64(v, t));
+      }
+    }
+    return Li;
+  }
+  // Largest occupied level <= x, or -1.
+  __device__ int prev_occ(int x) const {
+    if (x < 0) return -1;
+    if (x >= (int)L) x = (int)L - 1;
+    const int w = x >> 6;
+    const int r = x & 63;
+    const unsigned long long keep = (r == 63) ? ~0ull : ((1ull << (r + 1)) - 1ull);
+    const unsigned long long word = occ[w] & keep;
+    if (word) return (w << 6) + 63 - __builtin_clzll(word);
+    const int lane = lane_id();
+    for (int t0 = w - 1; t0 >= 0; t0 -= 64) {
+      const int idx = t0 - lane;
+      const unsigned long long v = idx >= 0 ? occ[idx] : 0ull;
+      const unsigned long long m = __ballot(v != 0ull);
+      if (m) {
+        const int t = __builtin_ctzll(m);
+        return ((t0 - t) << 6) + 63 - __builtin_clzll(rl64(v, t));
+      }
+    }
+    return -1;
+  }
+};
+
 template <class Lad>
 struct WaveCtx {
   BookDev bk;
@@ -401,7 +540,7 @@ __device__ __forceinline__ uint32_t head_of(const C& c, int lvl) {
   if constexpr (kRegLadder<C>)
     return lvl < 64 ? rl32(c.lad.h0, lvl & 63) : rl32(c.lad.h1, lvl & 63);
   else
-    return rl32(c.lad.lv[lvl].head, 0);
+    return c.lad.head(lvl);
 }
 
 template <class C>
@@ -738,11 +877,7 @@ __device__ __forceinline__ long long sweep(C& c, int dir, int lim, long long wan
       if (dir > 0 ? (cur > lim || cur >= L) : (cur < lim || cur < 0)) break;
       const int lv = cur + dir * lane;
       const bool valid = (dir > 0) ? (lv <= lim && lv < L) : (lv >= lim && lv >= 0);
-      Level W;
-      W.total = 0;
-      W.head = NIL;
-      W.tail = NIL;
-      if (valid) W = c.lad.lv[lv];
+      const Level W = c.lad.lane_get(lv, valid);
       const long long tot = W.total;
       const long long inc = wave_incl_scan(tot);
       const long long ex = inc - tot;
@@ -1151,6 +1286,18 @@ __global__ __launch_bounds__(256) void k_match(BookDev bk, BatchDev bt) {
     reject_bad_symbols(bt, lo, hi);
     return;
   }
+  if constexpr (kLad == LAD_HBM) {
+    // a busy symbol goes to k_match_hot (LDS window of its ladder), launched right after this
+    if (bt.hot_min && hi - lo >= bt.hot_min) {
+      uint32_t idx = 0;
+      if (lane == 0) idx = atomicAdd(bt.hot, 1u);
+      idx = rl32(idx, 0);
+      if (idx < HOT_MAX) {
+        if (lane == 0) bt.hot[1 + idx] = s;
+        return;
+      }
+    }
+  }
   const uint32_t L = bk.L;
   Level* g_lv = bk.levels + (size_t)s * L;
   unsigned long long* g_occ = bk.occ + (size_t)s * bk.Lwords;
@@ -1255,6 +1402,113 @@ __global__ __launch_bounds__(256) void k_match(BookDev bk, BatchDev bt) {
   }
 }
 
+
+// ---- hot symbols of deep windows (L > LDS_MAX_LEVELS) --------------------------------------
+// LDS of one k_match_hot workgroup: occupancy words | window levels | window tail fills | cache.
+struct HotLds {
+  uint32_t W, occ_off, lv_off, te_off, ck_off, bytes;
+  uint32_t cache;  // head-chunk cache on (ME_HOT_CACHE=0 turns it off: A/B runs)
+};
+__host__ __device__ inline HotLds hot_lds(uint32_t L, uint32_t Lwords, uint32_t budget) {
+  HotLds h{};
+  h.occ_off = 0;
+  const uint32_t fixed = Lwords * 8u + CK_MEM * (uint32_t)sizeof(CacheEntry) + 64u;
+  uint32_t W = budget > fixed ? (budget - fixed) / ((uint32_t)sizeof(Level) + 1u) : 0u;
+  W &= ~63u;
+  if (W > L) W = L;
+  h.W = W;
+  h.lv_off = (Lwords * 8u + 15u) & ~15u;
+  h.te_off = h.lv_off + W * (uint32_t)sizeof(Level);
+  h.ck_off = (h.te_off + W + 15u) & ~15u;
+  h.bytes = h.ck_off + CK_MEM * (uint32_t)sizeof(CacheEntry);
+  h.cache = 1;
+  return h;
+}
+
+// One workgroup (one wave) per hot symbol, the symbols k_match<LAD_HBM> handed over in bt.hot.
+// Same record loop as k_match; the ladder window sits around the symbol's best prices.
+__global__ __launch_bounds__(64) void k_match_hot(BookDev bk, BatchDev bt, HotLds hl) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int lane = lane_id();
+  const uint32_t cnt = min(rl32(bt.hot[0], 0), HOT_MAX);
+  const uint32_t L = bk.L, W = hl.W;
+  for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
+    const uint32_t s = rl32(bt.hot[1 + i], 0);
+    const uint32_t lo = bt.bin_start ? bt.bin_start[s] : wave_lower_bound(bt.skeys, bt.n, s);
+    const uint32_t hi = bt.bin_start ? bt.bin_start[s + 1] : wave_lower_bound(bt.skeys, bt.n, s + 1);
+    gptr1<Level> g_lv = (gptr1<Level>)(bk.levels + (size_t)s * L);
+    gptr1<unsigned long long> g_occ = (gptr1<unsigned long long>)(bk.occ + (size_t)s * bk.Lwords);
+    gptr1<uint8_t> g_tend = (gptr1<uint8_t>)(bk.tend + (size_t)s * L);
+    WaveCtx<LadderWin> c;
+#ifdef ME_STAMPS
+    for (int p = 0; p < PH_N; ++p) c.st[p] = 0;
+    STAMP_MARK(c);
+#endif
+    const SymState st = bk.sym[s];
+    const int bb = rli32(st.best_bid, 0), ba = rli32(st.best_ask, 0);
+    int center = (int)L / 2;
+    if (bb >= 0 && ba < (int)L)
+      center = (bb + ba) / 2;
+    else if (bb >= 0)
+      center = bb;
+    else if (ba < (int)L)
+      center = ba;
+    int wlo = center - (int)(W / 2);
+    if (wlo > (int)(L - W)) wlo = (int)(L - W);
+    if (wlo < 0) wlo = 0;
+    wlo &= ~63;
+    c.lad.wl = (lptr<Level>)(smem + hl.lv_off);
+    c.lad.wt = (lptr<uint8_t>)(smem + hl.te_off);
+    c.lad.occ = (lptr<unsigned long long>)(smem + hl.occ_off);
+    c.lad.glv = g_lv;
+    c.lad.gtend = g_tend;
+    c.lad.L = L;
+    c.lad.Lwords = bk.Lwords;
+    c.lad.wlo = wlo;
+    c.lad.W = W;
+    c.cache = hl.cache ? (CacheEntry*)(smem + hl.ck_off) : nullptr;
+    c.cmask = hl.cache ? CK_MEM - 1 : 0;
+    // stage the window: 8 level loads per lane in flight per step
+    for (uint32_t b = 0; b < W; b += 64 * 8) {
+      Level r[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t j = b + (uint32_t)k * 64 + (uint32_t)lane;
+        r[k] = Level{0, NIL, NIL};
+        if (j < W) r[k] = ld_level(g_lv + (wlo + j));
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t j = b + (uint32_t)k * 64 + (uint32_t)lane;
+        if (j < W) st_level(c.lad.wl + j, r[k]);
+      }
+    }
+    {
+      gptr1<uint32_t> gt4 = (gptr1<uint32_t>)(g_tend + wlo);  // wlo, W multiples of 64
+      lptr<uint32_t> wt4 = (lptr<uint32_t>)c.lad.wt;
+      for (uint32_t j = lane; j < W / 4; j += 64) wt4[j] = gt4[j];
+      for (uint32_t j = lane; j < bk.Lwords; j += 64) c.lad.occ[j] = g_occ[j];
+      if (c.cache)
+        for (uint32_t j = lane; j < (uint32_t)CK_MEM; j += 64) c.cache[j].cid = NIL;
+    }
+    wave_mem_order();
+    if (!wave_begin(c, bk, bt, s, lo, hi)) return;
+    STAMP_ADD(c, PH_PROLOGUE);
+    match_records(c, bt, lo, hi);
+    if (c.cache) cache_flush_all(c, CK_MEM);
+    wave_mem_order();
+    for (uint32_t j = lane; j < W; j += 64) st_level(g_lv + (wlo + j), ld_level(c.lad.wl + j));
+    {
+      gptr1<uint32_t> gt4 = (gptr1<uint32_t>)(g_tend + wlo);
+      lptr<uint32_t> wt4 = (lptr<uint32_t>)c.lad.wt;
+      for (uint32_t j = lane; j < W / 4; j += 64) gt4[j] = wt4[j];
+      for (uint32_t j = lane; j < bk.Lwords; j += 64) g_occ[j] = c.lad.occ[j];
+    }
+    wave_end(c);
+    wave_mem_order();
+  }
+}
+
 // ------------------------------------------------------------------ tape compaction
 // Block b owns records [b*1024, +1024). Tape offset of record i = sum of fills of records < i
 // (batch order == seq order). Fills are then copied scratch -> tape with consecutive threads
@@ -1350,6 +1604,18 @@ hipError_t launch_sort_pass(hipStream_t st, const uint32_t* keys_in, const uint3
 hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* bt, uint32_t ng, const AuxDev& ax,
                             hipEvent_t ev0, hipEvent_t ev1);
 
+// LDS one k_match_hot workgroup may use (the CU's 160 KB, less a margin).
+uint32_t hot_lds_budget() { return 160u * 1024u - 1024u; }
+static uint32_t g_hot_cache = 1;
+
+// Opt k_match_hot into the large dynamic LDS allocation once per process.
+hipError_t prepare_hot(const BookDev& bk) {
+  const HotLds hl = hot_lds(bk.L, bk.Lwords, hot_lds_budget());
+  if (hl.W < 64) return hipErrorInvalidValue;
+  if (const char* v = getenv("ME_HOT_CACHE")) g_hot_cache = (uint32_t)atoi(v);
+  return hipFuncSetAttribute((const void*)k_match_hot, hipFuncAttributeMaxDynamicSharedMemorySize, (int)hl.bytes);
+}
+
 // ev0 / ev1 (optional, timing): the launch records the kernel's own start and end
 // (hipExtLaunchKernelGGL), so timing adds no marker packet — and no gap — to the stream.
 hipError_t launch_match(hipStream_t st, const BookDev& bk, const BatchDev& bt, hipEvent_t ev0, hipEvent_t ev1) {
@@ -1359,8 +1625,17 @@ hipError_t launch_match(hipStream_t st, const BookDev& bk, const BatchDev& bt, h
     return launch_match_reg(st, bk, &bt, 1u, AuxDev{}, ev0, ev1);
   } else if (bk.L <= LDS_MAX_LEVELS) {
     hipExtLaunchKernelGGL(k_match<LAD_LDS>, grid, block, 4 * lds_wave_bytes(bk.L), st, ev0, ev1, 0, bk, bt);
-  } else {
+  } else if (!bt.hot_min || !bt.hot) {
     hipExtLaunchKernelGGL(k_match<LAD_HBM>, grid, block, 0, st, ev0, ev1, 0, bk, bt);
+  } else {
+    // deep windows: cold symbols match against the HBM ladder; busy ones are handed to
+    // k_match_hot, one workgroup each with an LDS window of the ladder
+    HotLds hl = hot_lds(bk.L, bk.Lwords, hot_lds_budget());
+    hl.cache = g_hot_cache;
+    hipError_t he = hipMemsetAsync(bt.hot, 0, 4, st);
+    if (he != hipSuccess) return he;
+    hipExtLaunchKernelGGL(k_match<LAD_HBM>, grid, block, 0, st, ev0, nullptr, 0, bk, bt);
+    hipExtLaunchKernelGGL(k_match_hot, dim3(HOT_GRID), dim3(64), hl.bytes, st, nullptr, ev1, 0, bk, bt, hl);
   }
   return hipGetLastError();
 }

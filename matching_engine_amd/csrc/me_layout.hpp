@@ -126,7 +126,15 @@ struct BatchDev {
   const int32_t* b_qty;
   const uint32_t* b_ok;  // batch index | (kind & 15) << BK_KIND_SHIFT
   uint32_t bcap;
+  // Deep-window path (L > LDS_MAX_LEVELS): a symbol with >= hot_min records in the batch is handed
+  // from k_match<LAD_HBM> to k_match_hot (one workgroup, LDS-resident ladder window) through
+  // hot[1 + i], i < hot[0] (the count; zeroed before each match launch). hot_min 0: no hand-off.
+  uint32_t* hot;
+  uint32_t hot_min;
 };
+constexpr uint32_t HOT_MAX = 1024;   // hot symbols per batch (more are matched in place)
+constexpr uint32_t HOT_GRID = 256;   // k_match_hot workgroups: one per CU (the LDS window fills it)
+constexpr uint32_t HOT_MIN_RECORDS = 64;  // threshold the tests use (ME_HOT_MIN, opt-in)
 // Batches per register-ladder launch at most (me_config.batches_per_launch). One launch matches a
 // group of up to ME_GMAX batches: every symbol's wave runs through its records of all of them in
 // order, so a launch costs the heaviest symbol's share of the whole group rather than the sum of

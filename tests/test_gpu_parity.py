@@ -81,6 +81,26 @@ def test_config4_zipf_deep_books(me, orc):
     assert nf > 0
 
 
+def test_config4_hot_symbols_ladder_window(me, orc, monkeypatch):
+    """Config 4 at its real window depth (L = 32,768): busy symbols go to k_match_hot, whose LDS
+    window (~8.5k levels around the best prices) is smaller than the ladder, so rests and sweeps
+    hit levels on both sides of the window edge. (The hand-off is opt-in: ME_HOT_MIN.)"""
+    monkeypatch.setenv("ME_HOT_MIN", "64")
+    nf, total = _stream_run(me, orc, 4, 3, seed_per_side=6000, num_symbols=40, levels=32768,
+                            spread_ticks=5000)
+    assert nf > 0
+
+
+@pytest.mark.parametrize("hot_min", ["0", "64"])
+def test_deep_window_hot_list_overflow(me, orc, monkeypatch, hot_min):
+    """More busy symbols than k_match_hot workgroups (each loops over several) and than the hand-off
+    list holds (the rest are matched in place by k_match<LAD_HBM>); the same stream without it."""
+    monkeypatch.setenv("ME_HOT_MIN", hot_min)
+    nf, total = _stream_run(me, orc, 2, 2, num_symbols=1100, levels=2048, batch=1100 * 80,
+                            book_symbols=range(0, 1100, 7))
+    assert nf > 0
+
+
 def test_config5_cancel_heavy_sweeps(me, orc):
     nf, total = _stream_run(me, orc, 5, 8)
     assert nf > 0
