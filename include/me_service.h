@@ -15,6 +15,10 @@
  *                             writes them, final status/remaining from the match, fills rows, maker
  *                             status updates) — the batched rewrite of storage.cpp:78-208.
  *   me_service_book           GetOrderBook (matching_engine_service.cpp:123-129) from the GPU book.
+ *   me_service_cancel_order   CancelOrder — a build extension (the reference has no cancel RPC; SURVEY
+ *                             §8(f) row 4): queues a cancel record for a resting order into the slice.
+ *   me_service_updates        StreamOrderUpdates (proto/matching_engine.proto:34,71-91): drains the
+ *                             OrderUpdate events the flushes produced, optionally for one client_id.
  */
 #ifndef ME_SERVICE_H
 #define ME_SERVICE_H
@@ -69,6 +73,39 @@ int me_service_flush(me_service* s, me_fill* out_fills, size_t fills_cap, size_t
 /* GetOrderBook for a symbol string (top depth levels per side). */
 int me_service_book(me_service* s, const char* symbol, me_level* bids, me_level* asks, size_t depth,
                     size_t* n_bids, size_t* n_asks);
+
+/* CancelOrder request (build extension, mirrors OrderRequest's conventions). */
+typedef struct me_cancel_request {
+  const char* client_id;
+  const char* symbol;
+  const char* order_id; /* "OID-<n>" of the order to cancel */
+} me_cancel_request;
+
+/* Validation (first failing check wins, in-band like SubmitOrder :66-83): "symbol is required",
+ * "order_id is invalid" (not "OID-<n>", n >= 1). An accepted cancel consumes the next OID number as
+ * its stream position (like any request reaching :85) and answers success=1 with order_id = the
+ * TARGET's id; whether it removed anything arrives as an OrderUpdate after the flush (CANCELED with
+ * the removed quantity, or REJECTED when the target was not resting on that symbol). */
+int me_service_cancel_order(me_service* s, const me_cancel_request* req, me_order_response* resp);
+
+/* OrderUpdate (proto:71-91). Events per flushed record, in slice order: for each fill the maker's
+ * update then the taker's (fill price/qty, remaining after the fill, PARTIALLY_FILLED / FILLED);
+ * then a closing taker update when no fill closed it (NEW resting, CANCELED market remainder,
+ * REJECTED); a cancel record emits CANCELED (remaining = removed qty) or REJECTED for its target. */
+typedef struct me_order_update {
+  char order_id[32];
+  char client_id[64];
+  char symbol[32];
+  int32_t status;            /* ME_ST_* */
+  int32_t scale;             /* 4: prices are Q4 */
+  int64_t fill_price;        /* Q4, 0 without a fill */
+  int32_t fill_quantity;
+  int32_t remaining_quantity;
+} me_order_update;
+
+/* Drain up to cap queued updates (client_id NULL or "": every client; else only that client's,
+ * leaving the others queued). *n = updates written; returns ME_OK. */
+int me_service_updates(me_service* s, const char* client_id, me_order_update* out, size_t cap, size_t* n);
 
 int me_service_last_error(const me_service* s, char* buf, size_t cap);
 

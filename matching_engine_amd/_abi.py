@@ -182,7 +182,32 @@ class MeOrderResponse(C.Structure):
     ]
 
 
+class MeCancelRequest(C.Structure):
+    _fields_ = [
+        ("client_id", C.c_char_p),
+        ("symbol", C.c_char_p),
+        ("order_id", C.c_char_p),
+    ]
+
+
+class MeOrderUpdate(C.Structure):
+    _fields_ = [
+        ("order_id", C.c_char * 32),
+        ("client_id", C.c_char * 64),
+        ("symbol", C.c_char * 32),
+        ("status", C.c_int32),
+        ("scale", C.c_int32),
+        ("fill_price", C.c_int64),
+        ("fill_quantity", C.c_int32),
+        ("remaining_quantity", C.c_int32),
+    ]
+
+
+assert C.sizeof(MeOrderUpdate) == 152, "me_order_update layout"
+
 PROTOTYPES.update({
+    "me_service_cancel_order": (C.c_int, [_P, C.POINTER(MeCancelRequest), C.POINTER(MeOrderResponse)]),
+    "me_service_updates": (C.c_int, [_P, C.c_char_p, C.POINTER(MeOrderUpdate), _SZ, C.POINTER(_SZ)]),
     "me_service_create": (_P, [_P, C.POINTER(C.c_char_p), C.c_uint32, C.c_char_p]),
     "me_service_destroy": (None, [_P]),
     "me_service_submit_order": (C.c_int, [_P, C.POINTER(MeOrderRequest), C.POINTER(MeOrderResponse)]),

@@ -15,6 +15,7 @@
 #include <string.h>
 
 #include <chrono>
+#include <deque>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -107,7 +108,18 @@ struct Pending {
   uint32_t symbol_id;
   std::string symbol;
   int32_t side;
+  bool cancel;      // CancelOrder record (build extension): target = the order it removes
+  uint64_t target;
 };
+
+// A resting order the OrderUpdate stream still reports on (owner + unfilled quantity).
+struct Live {
+  std::string client;
+  std::string symbol;
+  int32_t remaining;
+};
+
+constexpr size_t kMaxQueuedUpdates = size_t(1) << 24;  // oldest events are dropped beyond this
 
 }  // namespace
 
@@ -124,6 +136,10 @@ struct me_service {
   std::vector<uint32_t> sid;
   std::vector<uint8_t> kind;
   std::vector<Pending> meta;
+  // StreamOrderUpdates: resting orders by seq, and the undrained events
+  std::unordered_map<uint64_t, Live> live;
+  std::deque<me_order_update> updates;
+  uint64_t updates_dropped = 0;
   // persistence
   sqlite3* db = nullptr;
   sqlite3_stmt* st_ins = nullptr;
@@ -264,7 +280,45 @@ extern "C" int me_service_submit_order(me_service* s, const me_order_request* r,
   s->qty.push_back(r->quantity);
   s->sid.push_back(sid);
   s->kind.push_back(ME_KIND(r->side, r->order_type == ME_TYPE_LIMIT ? ME_TYPE_LIMIT : ME_TYPE_MARKET, ME_OP_NEW));
-  s->meta.push_back(Pending{r->client_id ? r->client_id : "", sid, symbol, r->side});
+  s->meta.push_back(Pending{r->client_id ? r->client_id : "", sid, symbol, r->side, false, 0});
+  return 0;
+}
+
+// "OID-<n>", n >= 1 with no trailing characters -> n; else 0.
+static uint64_t parse_oid(const char* s) {
+  if (!s || strncmp(s, "OID-", 4) != 0 || !s[4]) return 0;
+  uint64_t v = 0;
+  for (const char* p = s + 4; *p; ++p) {
+    if (*p < '0' || *p > '9' || v > (UINT64_MAX - 9) / 10) return 0;
+    v = v * 10 + (uint64_t)(*p - '0');
+  }
+  return v;
+}
+
+extern "C" int me_service_cancel_order(me_service* s, const me_cancel_request* r, me_order_response* resp) {
+  memset(resp, 0, sizeof(*resp));
+  const char* symbol = r->symbol ? r->symbol : "";
+  if (!symbol[0]) {
+    put(resp->error_message, sizeof resp->error_message, "symbol is required");
+    return 0;
+  }
+  const uint64_t target = parse_oid(r->order_id);
+  if (!target) {
+    put(resp->error_message, sizeof resp->error_message, "order_id is invalid");
+    return 0;
+  }
+  std::lock_guard<std::mutex> lk(s->mu);
+  const uint64_t id = s->next_id++;  // the cancel's stream position (batch order == seq order)
+  put(resp->order_id, sizeof resp->order_id, "OID-" + std::to_string(target));
+  resp->success = 1;
+  auto it = s->sym.find(symbol);
+  const uint32_t sid = it == s->sym.end() ? (uint32_t)s->names.size() : it->second;
+  s->seq.push_back(id);
+  s->px.push_back((int64_t)target);
+  s->qty.push_back(0);
+  s->sid.push_back(sid);
+  s->kind.push_back(ME_KIND(ME_SIDE_BUY, ME_TYPE_LIMIT, ME_OP_CANCEL));
+  s->meta.push_back(Pending{r->client_id ? r->client_id : "", sid, symbol, 0, true, target});
   return 0;
 }
 
@@ -278,6 +332,92 @@ extern "C" uint64_t me_service_next_oid(const me_service* s) {
   return s->next_id;
 }
 
+static void push_update(me_service* s, uint64_t oid, const std::string& client, const std::string& symbol,
+                        int status, int64_t price, int32_t fq, int32_t remaining) {
+  me_order_update u;
+  memset(&u, 0, sizeof u);
+  put(u.order_id, sizeof u.order_id, "OID-" + std::to_string(oid));
+  put(u.client_id, sizeof u.client_id, client);
+  put(u.symbol, sizeof u.symbol, symbol);
+  u.status = status;
+  u.scale = 4;
+  u.fill_price = price;
+  u.fill_quantity = fq;
+  u.remaining_quantity = remaining;
+  if (s->updates.size() >= kMaxQueuedUpdates) {
+    s->updates.pop_front();
+    s->updates_dropped++;
+  }
+  s->updates.push_back(u);
+}
+
+// OrderUpdate events of one matched slice (order documented in me_service.h), and the live-order
+// table they are computed from (owner and unfilled quantity of every resting order).
+static void emit_updates(me_service* s, size_t n, const me_order_result* res, const me_fill* tape) {
+  for (size_t i = 0; i < n; ++i) {
+    const Pending& m = s->meta[i];
+    const me_order_result& r = res[i];
+    if (m.cancel) {
+      auto it = s->live.find(m.target);
+      if (r.status == ME_ST_CANCELED && it != s->live.end()) {
+        push_update(s, m.target, it->second.client, it->second.symbol, ME_ST_CANCELED, 0, 0, r.remaining_qty);
+        s->live.erase(it);
+      } else {
+        push_update(s, m.target, m.client, m.symbol, r.status == ME_ST_CANCELED ? ME_ST_CANCELED : ME_ST_REJECTED,
+                    0, 0, r.remaining_qty);
+      }
+      continue;
+    }
+    const uint64_t oid = s->seq[i];
+    int32_t rem = s->qty[i];
+    for (uint32_t f = 0; f < r.fill_count; ++f) {
+      const me_fill& fl = tape[r.tape_offset + f];
+      auto it = s->live.find(fl.maker_seq);
+      if (it != s->live.end()) {
+        Live& mk = it->second;
+        mk.remaining -= fl.qty;
+        push_update(s, fl.maker_seq, mk.client, mk.symbol,
+                    mk.remaining > 0 ? ME_ST_PARTIALLY_FILLED : ME_ST_FILLED, fl.price_q4, fl.qty, mk.remaining);
+        if (mk.remaining <= 0) s->live.erase(it);
+      }
+      rem -= fl.qty;
+      push_update(s, oid, m.client, m.symbol, rem > 0 ? ME_ST_PARTIALLY_FILLED : ME_ST_FILLED, fl.price_q4,
+                  fl.qty, rem);
+    }
+    const bool market = ((s->kind[i] >> 2) & 1u) != 0;
+    if (r.status == ME_ST_REJECTED || r.status == ME_ST_CANCELED || (r.fill_count == 0 && r.status == ME_ST_NEW))
+      push_update(s, oid, m.client, m.symbol, r.status, 0, 0, r.remaining_qty);
+    if (!market && r.remaining_qty > 0 && (r.status == ME_ST_NEW || r.status == ME_ST_PARTIALLY_FILLED))
+      s->live[oid] = Live{m.client, m.symbol, r.remaining_qty};
+  }
+}
+
+extern "C" int me_service_updates(me_service* s, const char* client_id, me_order_update* out, size_t cap,
+                                  size_t* n) {
+  std::lock_guard<std::mutex> lk(s->mu);
+  size_t k = 0;
+  const bool all = !client_id || !client_id[0];
+  if (all) {
+    for (; k < cap && !s->updates.empty(); ++k) {
+      if (out) out[k] = s->updates.front();
+      s->updates.pop_front();
+    }
+  } else {  // one pass: this client's events out (up to cap), every other event kept in order
+    std::deque<me_order_update> keep;
+    for (auto& u : s->updates) {
+      if (k < cap && strncmp(u.client_id, client_id, sizeof u.client_id) == 0) {
+        if (out) out[k] = u;
+        ++k;
+      } else {
+        keep.push_back(u);
+      }
+    }
+    s->updates.swap(keep);
+  }
+  if (n) *n = k;
+  return ME_OK;
+}
+
 static bool persist(me_service* s, size_t n, const me_order_result* res, const me_fill* tape, size_t nf) {
   if (!s->db) return true;
   const int64_t ts = now_ms();
@@ -289,8 +429,20 @@ static bool persist(me_service* s, size_t n, const me_order_result* res, const m
   if (!s->sql_ok(g_sql.exec(s->db, "BEGIN", nullptr, nullptr, nullptr), "begin")) return false;
   bool ok = true;
   for (size_t i = 0; i < n && ok; ++i) {
-    const std::string oid = "OID-" + std::to_string(s->seq[i]);
     const Pending& m = s->meta[i];
+    if (m.cancel) {  // no row of its own: the target's row becomes CANCELED
+      if (res[i].status == ME_ST_CANCELED) {
+        const std::string toid = "OID-" + std::to_string(m.target);
+        sqlite3_stmt* up = s->st_upd;
+        g_sql.bind_int64(up, 1, ME_ST_CANCELED);
+        g_sql.bind_int64(up, 2, res[i].remaining_qty);  // the quantity the cancel removed
+        g_sql.bind_int64(up, 3, ts);
+        g_sql.bind_text(up, 4, toid.c_str(), -1, SQLITE_TRANSIENT);
+        ok = step(up, "cancel order");
+      }
+      continue;
+    }
+    const std::string oid = "OID-" + std::to_string(s->seq[i]);
     sqlite3_stmt* st = s->st_ins;  // insert_new_order's row (storage.cpp:102-112)
     g_sql.bind_text(st, 1, oid.c_str(), -1, SQLITE_TRANSIENT);
     g_sql.bind_text(st, 2, m.client.c_str(), -1, SQLITE_TRANSIENT);
@@ -361,6 +513,7 @@ extern "C" int me_service_flush(me_service* s, me_fill* out_fills, size_t fills_
     return s->fail(rc, std::string("engine: ") + e);
   }
   if (!persist(s, n, res.data(), tape.data(), nf)) return s->fail(ME_E_SQLITE, s->err);
+  emit_updates(s, n, res.data(), tape.data());
   if (n_fills) *n_fills = nf;
   if (out_fills) {
     if (nf > fills_cap) return s->fail(ME_E_INVALID, "fills_cap smaller than the tape");

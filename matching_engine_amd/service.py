@@ -7,7 +7,8 @@ import ctypes as C
 import numpy as np
 
 from . import _abi
-from ._abi import FILL_DTYPE, LEVEL_DTYPE, RESULT_DTYPE, MeOrderRequest, MeOrderResponse, ptr
+from ._abi import (FILL_DTYPE, LEVEL_DTYPE, RESULT_DTYPE, MeCancelRequest, MeOrderRequest, MeOrderResponse,
+                   MeOrderUpdate, ptr)
 
 
 class ServiceError(RuntimeError):
@@ -52,6 +53,30 @@ class MatchingEngineService:
         self.lib.me_service_submit_order(self.h, C.byref(req), C.byref(resp))
         return {"order_id": resp.order_id.decode(), "success": bool(resp.success),
                 "error_message": resp.error_message.decode(), "grpc_status": resp.grpc_status}
+
+    def cancel_order(self, client_id, symbol, order_id) -> dict:
+        """CancelOrder (build extension, me_service.h): queue a cancel of a resting order; the outcome
+        arrives as an OrderUpdate after the flush."""
+        req = MeCancelRequest(client_id.encode(), symbol.encode(), order_id.encode())
+        resp = MeOrderResponse()
+        self.lib.me_service_cancel_order(self.h, C.byref(req), C.byref(resp))
+        return {"order_id": resp.order_id.decode(), "success": bool(resp.success),
+                "error_message": resp.error_message.decode(), "grpc_status": resp.grpc_status}
+
+    def order_updates(self, client_id=None, cap=1 << 16) -> list:
+        """StreamOrderUpdates (proto:34,71-91): drain the queued OrderUpdate events (one client, or all)."""
+        out = []
+        buf = (MeOrderUpdate * cap)()
+        while True:
+            n = C.c_size_t(0)
+            self.lib.me_service_updates(self.h, client_id.encode() if client_id else None, buf, cap, C.byref(n))
+            for u in buf[: n.value]:
+                out.append({"order_id": u.order_id.decode(), "client_id": u.client_id.decode(),
+                            "symbol": u.symbol.decode(), "status": u.status, "fill_price": u.fill_price,
+                            "scale": u.scale, "fill_quantity": u.fill_quantity,
+                            "remaining_quantity": u.remaining_quantity})
+            if n.value < cap:
+                return out
 
     @property
     def pending(self) -> int:

@@ -156,3 +156,102 @@ def test_submitorder_stream_matches_oracle_and_db(me, tmp_path):
     assert np.array_equal(bids, obids) and np.array_equal(asks, oasks)
     svc.close()
     eng.close()
+
+
+def test_cancel_request_validation(me):
+    """CancelOrder (build extension): in-band rejects in SubmitOrder's style, no OID consumed on a
+    reject; an accepted cancel answers with the target's id and takes the next stream position."""
+    svc = me.MatchingEngineService(None, ["SYM"])
+    assert svc.cancel_order("C", "", "OID-1")["error_message"] == "symbol is required"
+    for bad in ("OID-", "OID-0", "OID-x1", "X-3", "OID-3a", ""):
+        r = svc.cancel_order("C", "SYM", bad)
+        assert r == {"order_id": "", "success": False, "error_message": "order_id is invalid", "grpc_status": 0}
+    assert svc.next_oid == 1 and svc.pending == 0
+    assert svc.submit_order("C", "SYM", 0, 1, 100, 4, 5)["order_id"] == "OID-1"
+    r = svc.cancel_order("C", "SYM", "OID-1")
+    assert r == {"order_id": "OID-1", "success": True, "error_message": "", "grpc_status": 0}
+    assert svc.next_oid == 3 and svc.pending == 2
+    assert svc.order_updates() == []  # nothing matched yet
+
+
+@pytest.mark.gpu
+def test_cancels_and_order_update_stream(me, tmp_path):
+    """SubmitOrder + CancelOrder slices: results/tapes equal the oracle fed the same records (cancels
+    as cancel records), every fill appears as a maker and a taker OrderUpdate, every cancel as one
+    CANCELED / REJECTED update, per-client drains partition the stream, and each order's last update
+    carries the remaining quantity its DB row holds."""
+    from oracle.oracle import OracleBook
+
+    rng = np.random.default_rng(11)
+    syms = [f"S{i}" for i in range(8)]
+    mids = {s: 1_000_000 + 1000 * i for i, s in enumerate(syms)}
+    base = np.array([mids[s] - 64 for s in syms], dtype=np.int64)
+    db = str(tmp_path / "cancel.sqlite")
+    eng = me.Engine(len(syms), 128, base, max_batch=4096, max_resting=1 << 14, max_seq=1 << 20)
+    svc = me.MatchingEngineService(eng, syms, db_path=db)
+    ob = OracleBook(len(syms), 128, base, 1 << 20)
+    accepted = []  # (oid, symbol) of LIMIT orders
+    events = []
+    for slice_no in range(4):
+        seqs, px, qty, sid, kinds = [], [], [], [], []
+        nf_expect = 0
+        for _ in range(1200):
+            if accepted and rng.random() < 0.3:
+                oid, s = accepted[int(rng.integers(len(accepted)))]
+                if rng.random() < 0.1:
+                    s = syms[(syms.index(s) + 1) % len(syms)]  # wrong symbol -> REJECTED
+                r = svc.cancel_order(f"C{oid % 3}", s, f"OID-{oid}")
+                assert r["success"] and r["order_id"] == f"OID-{oid}"
+                seqs.append(svc.next_oid - 1)
+                px.append(oid)
+                qty.append(0)
+                sid.append(syms.index(s))
+                kinds.append(me.kind(me.SIDE_BUY, me.TYPE_LIMIT, 1))
+                continue
+            s = syms[int(rng.integers(len(syms)))]
+            otype = 1 if rng.random() < 0.2 else 0
+            side = int(rng.choice([1, 2]))
+            q4 = mids[s] + int(rng.integers(-30, 31))
+            qn = int(rng.integers(1, 60))
+            r = svc.submit_order(f"C{svc.next_oid % 3}", s, otype, side, 0 if otype else q4, 4, qn)
+            oid = int(r["order_id"][4:])
+            if otype == 0:
+                accepted.append((oid, s))
+            seqs.append(oid)
+            px.append(0 if otype else q4)
+            qty.append(qn)
+            sid.append(syms.index(s))
+            kinds.append(me.kind(side, otype))
+        seq, res, fills = svc.flush()
+        ro, fo = ob.submit(me.Batch(seqs, px, qty, sid, kinds))
+        assert np.array_equal(seq, np.array(seqs, dtype=np.uint64))
+        assert_results_equal(res, ro, f"slice {slice_no}")
+        assert_fills_equal(fills, fo, f"slice {slice_no}")
+        # drain per client: the three drains partition the slice's events
+        ev = svc.order_updates("C0") + svc.order_updates("C1") + svc.order_updates("C2")
+        assert svc.order_updates() == []
+        cancels = int(np.sum((np.array(kinds) >> 3) & 1))
+        nclose = sum(1 for k, r_ in zip(kinds, ro) if not (k >> 3) & 1 and
+                     (r_["status"] in (3, 4) or (r_["fill_count"] == 0 and r_["status"] == 0)))
+        assert len(ev) == 2 * len(fo) + cancels + nclose
+        assert sum(e["fill_quantity"] for e in ev) == 2 * int(fo["qty"].sum())
+        ncanceled = sum(1 for k, r_ in zip(kinds, ro) if (k >> 3) & 1 and r_["status"] == 3)
+        assert sum(1 for e in ev if e["status"] == 3 and e["fill_quantity"] == 0
+                   and e["remaining_quantity"] > 0) >= ncanceled
+        events += ev
+    last = {}
+    for e in events:
+        last[e["order_id"]] = e
+    con = sqlite3.connect(db)
+    checked = 0
+    for oid, e in last.items():
+        row = con.execute("SELECT status, remaining_quantity FROM orders WHERE order_id=?", (oid,)).fetchone()
+        assert row is not None, oid
+        if e["status"] in (0, 1, 2, 3):
+            assert row[1] == e["remaining_quantity"], (oid, row, e)
+            checked += 1
+        if e["status"] == 3:
+            assert row[0] == 3
+    assert checked > 1000
+    svc.close()
+    eng.close()
