@@ -17,6 +17,7 @@
  *   me_service_book           GetOrderBook (matching_engine_service.cpp:123-129) from the GPU book.
  *   me_service_cancel_order   CancelOrder — a build extension (the reference has no cancel RPC; SURVEY
  *                             §8(f) row 4): queues a cancel record for a resting order into the slice.
+ *   me_service_market_data    StreamMarketData's MarketDataUpdate (proto:60-67) from the GPU book.
  *   me_service_updates        StreamOrderUpdates (proto/matching_engine.proto:34,71-91): drains the
  *                             OrderUpdate events the flushes produced, optionally for one client_id.
  */
@@ -106,6 +107,24 @@ typedef struct me_order_update {
 /* Drain up to cap queued updates (client_id NULL or "": every client; else only that client's,
  * leaving the others queued). *n = updates written; returns ME_OK. */
 int me_service_updates(me_service* s, const char* client_id, me_order_update* out, size_t cap, size_t* n);
+
+/* MarketDataUpdate (proto:60-67) for StreamMarketData, from the GPU book: best bid / ask (Q4,
+ * scale 4) and the total quantity resting there (saturated to int32). The reference's
+ * Storage::best_bid / best_ask SQL (storage.cpp:212-252) query side=0 / side=1, which the schema's
+ * CHECK side IN (1,2) never admits, so they always return nullopt; here a missing side reads 0
+ * with has_bid / has_ask = 0 (proto3 default). Unknown symbol: both sides missing. */
+typedef struct me_market_data {
+  int64_t best_bid;
+  int64_t best_ask;
+  int32_t scale;
+  int32_t bid_size;
+  int32_t ask_size;
+  int32_t has_bid;
+  int32_t has_ask;
+  int32_t pad;
+} me_market_data;
+
+int me_service_market_data(me_service* s, const char* symbol, me_market_data* out);
 
 int me_service_last_error(const me_service* s, char* buf, size_t cap);
 

@@ -205,8 +205,22 @@ class MeOrderUpdate(C.Structure):
 
 assert C.sizeof(MeOrderUpdate) == 152, "me_order_update layout"
 
+
+class MeMarketData(C.Structure):
+    _fields_ = [
+        ("best_bid", C.c_int64),
+        ("best_ask", C.c_int64),
+        ("scale", C.c_int32),
+        ("bid_size", C.c_int32),
+        ("ask_size", C.c_int32),
+        ("has_bid", C.c_int32),
+        ("has_ask", C.c_int32),
+        ("pad", C.c_int32),
+    ]
+
 PROTOTYPES.update({
     "me_service_cancel_order": (C.c_int, [_P, C.POINTER(MeCancelRequest), C.POINTER(MeOrderResponse)]),
+    "me_service_market_data": (C.c_int, [_P, C.c_char_p, C.POINTER(MeMarketData)]),
     "me_service_updates": (C.c_int, [_P, C.c_char_p, C.POINTER(MeOrderUpdate), _SZ, C.POINTER(_SZ)]),
     "me_service_create": (_P, [_P, C.POINTER(C.c_char_p), C.c_uint32, C.c_char_p]),
     "me_service_destroy": (None, [_P]),

@@ -543,6 +543,30 @@ extern "C" int me_service_book(me_service* s, const char* symbol, me_level* bids
   return me_book_snapshot(s->eng, it->second, bids, asks, depth, n_bids, n_asks);
 }
 
+extern "C" int me_service_market_data(me_service* s, const char* symbol, me_market_data* out) {
+  memset(out, 0, sizeof(*out));
+  out->scale = 4;
+  auto it = s->sym.find(symbol ? symbol : "");
+  if (it == s->sym.end()) return ME_OK;
+  if (!s->eng) return s->fail(ME_E_STATE, "no engine");
+  me_level b{}, a{};
+  size_t nb = 0, na = 0;
+  const int rc = me_book_snapshot(s->eng, it->second, &b, &a, 1, &nb, &na);
+  if (rc != ME_OK) return rc;
+  auto sat = [](int64_t v) { return (int32_t)(v > INT32_MAX ? INT32_MAX : v); };
+  if (nb) {
+    out->has_bid = 1;
+    out->best_bid = b.price_q4;
+    out->bid_size = sat(b.total_qty);
+  }
+  if (na) {
+    out->has_ask = 1;
+    out->best_ask = a.price_q4;
+    out->ask_size = sat(a.total_qty);
+  }
+  return ME_OK;
+}
+
 extern "C" int me_service_last_error(const me_service* s, char* buf, size_t cap) {
   if (buf && cap) put(buf, cap, s->err);
   return (int)s->err.size();

@@ -8,7 +8,7 @@ import numpy as np
 
 from . import _abi
 from ._abi import (FILL_DTYPE, LEVEL_DTYPE, RESULT_DTYPE, MeCancelRequest, MeOrderRequest, MeOrderResponse,
-                   MeOrderUpdate, ptr)
+                   MeMarketData, MeOrderUpdate, ptr)
 
 
 class ServiceError(RuntimeError):
@@ -99,6 +99,16 @@ class MatchingEngineService:
         if rc != 0:
             raise ServiceError(f"flush failed ({rc}): {self.last_error()}")
         return seq[: nr.value].copy(), res[: nr.value].copy(), fills[: nf.value].copy()
+
+    def market_data(self, symbol) -> dict:
+        """MarketDataUpdate (proto:60-67) from the GPU book; a missing side has has_* False and 0s."""
+        m = MeMarketData()
+        rc = self.lib.me_service_market_data(self.h, symbol.encode(), C.byref(m))
+        if rc != 0:
+            raise ServiceError(self.last_error())
+        return {"symbol": symbol, "best_bid": m.best_bid, "best_ask": m.best_ask, "scale": m.scale,
+                "bid_size": m.bid_size, "ask_size": m.ask_size, "has_bid": bool(m.has_bid),
+                "has_ask": bool(m.has_ask)}
 
     def get_order_book(self, symbol, depth=10):
         bids = np.zeros(depth, dtype=LEVEL_DTYPE)

@@ -154,6 +154,18 @@ def test_submitorder_stream_matches_oracle_and_db(me, tmp_path):
     bids, asks = svc.get_order_book("S3", 5)
     obids, oasks = ob.snapshot(3, 5)
     assert np.array_equal(bids, obids) and np.array_equal(asks, oasks)
+    # StreamMarketData's MarketDataUpdate: the top level of each side
+    for s in syms[:4]:
+        md = svc.market_data(s)
+        ob1, oa1 = ob.snapshot(syms.index(s), 1)
+        assert md["has_bid"] == (len(ob1) == 1) and md["has_ask"] == (len(oa1) == 1)
+        if len(ob1):
+            assert (md["best_bid"], md["bid_size"]) == (int(ob1[0]["price_q4"]), int(ob1[0]["total_qty"]))
+        if len(oa1):
+            assert (md["best_ask"], md["ask_size"]) == (int(oa1[0]["price_q4"]), int(oa1[0]["total_qty"]))
+        assert md["scale"] == 4
+    assert svc.market_data("NOPE") == {"symbol": "NOPE", "best_bid": 0, "best_ask": 0, "scale": 4,
+                                       "bid_size": 0, "ask_size": 0, "has_bid": False, "has_ask": False}
     svc.close()
     eng.close()
 
