@@ -56,15 +56,15 @@ WORKLOADS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=320)
+    ap.add_argument("--warmup", type=int, default=32)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS),
                     help="c2 (default) = BASELINE configs[1], the metric's workload; c3/c4/c5 = the other "
                          "BASELINE configs as secondary lines (DESIGN.md §7)")
     ap.add_argument("--symbols-per-gpu", type=int, default=None)
     ap.add_argument("--batch-per-gpu", type=int, default=None)
     ap.add_argument("--batches-per-launch", type=int, default=0,
-                    help="batches matched per kernel launch (me_config.batches_per_launch; 0 = engine default 8)")
+                    help="batches matched per kernel launch (me_config.batches_per_launch; 0 = engine default 32)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
@@ -288,7 +288,6 @@ def main():
         e2e = n2 / (time.perf_counter() - t2)
 
     if rank == 0:
-        # config 4's 100k x 32,768-level oracle book (~50 GB of host arrays) is not run on the host
         cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args)
         line = {
             "metric": "orders matched/sec (whole node); fills bit-exact vs CPU oracle",
@@ -313,7 +312,7 @@ def main():
             "fills_per_order": fills_all / max(orders_all, 1),
             "kernel_match_ms_avg": tm["match_ms"] / timed,
             "kernel_match_launches_timed": tm["launches"],
-            "batches_per_launch": args.batches_per_launch or (8 if sc.levels <= 128 else 1),
+            "batches_per_launch": args.batches_per_launch or (32 if sc.levels <= 128 else 1),
             "device_ms_per_step": tm["pipeline_ms"],
             "host_enqueue_ms_per_step_rank0": t_enq / args.steps * 1e3,
             "e2e_host_path_orders_per_s_rank0": e2e,

@@ -832,11 +832,10 @@ constexpr uint32_t CW_BUY = 1u << 8, CW_MKT = 1u << 9, CW_CXL = 1u << 10;
 __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
   __shared__ RegLds lds[REG_WAVES];
   __shared__ ColdArgs G;
-  static_assert(sizeof(ColdArgs) % 8 == 0 && sizeof(ColdArgs) <= 8 * 128 * REG_WAVES, "ColdArgs copy");
+  static_assert(sizeof(ColdArgs) % 8 == 0, "ColdArgs copy");
   {
-    if (threadIdx.x < sizeof(ColdArgs) / 8)
-      reinterpret_cast<unsigned long long*>(&G)[threadIdx.x] =
-          reinterpret_cast<const unsigned long long*>(&args)[threadIdx.x];
+    for (uint32_t i = threadIdx.x; i < sizeof(ColdArgs) / 8; i += 128 * REG_WAVES)
+      reinterpret_cast<unsigned long long*>(&G)[i] = reinterpret_cast<const unsigned long long*>(&args)[i];
     __syncthreads();
   }
   const BookDev& bk = args.bk;

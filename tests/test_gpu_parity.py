@@ -293,7 +293,7 @@ def test_full_size_config2_bitexact(me, orc):
 
 
 
-@pytest.mark.parametrize("group", [1, 3, 8])
+@pytest.mark.parametrize("group", [1, 3, 8, 32])
 @pytest.mark.parametrize("stream", ["uniform", "skewed"])
 def test_back_to_back_device_batches(me, orc, group, stream):
     """Device batches submitted back to back without a sync (the bench's pattern), matched

@@ -17,7 +17,7 @@ if [ "$2" != "skip-tests" ]; then
 fi
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo SMOKE_FAIL; tail -20 $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log
-B="python3 $R/bench.py --steps 50 --warmup 10 --no-cpu-baseline --no-e2e"
+B="python3 $R/bench.py --steps 320 --warmup 32 --no-cpu-baseline --no-e2e"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d $O/prof_kt -o kt -- $B > $O/prof_kt.log 2>&1 || { echo PROF_FAIL; tail -20 $O/prof_kt.log; exit 1; }
 python3 $R/tools/trace_gaps.py $O/prof_kt > $O/trace_gaps.txt && cat $O/trace_gaps.txt
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_match --output-format csv -d $O/fetch -o pmc -- $B > $O/fetch.log 2>&1 || { echo PMC_FAIL fetch; tail -5 $O/fetch.log; exit 1; }
