@@ -95,7 +95,7 @@ typedef struct me_config {
   uint64_t max_seq;            /* locator capacity: accepted seqs are 1 <= seq < max_seq */
   const int64_t* base_price;   /* [num_symbols] price_q4 of level 0 of each symbol's window */
   const uint32_t* symbol_ids;  /* optional [num_symbols] ids written to me_fill.symbol (NULL = local id) */
-  uint32_t batches_per_launch; /* L <= 128: device batches matched per kernel launch, 1..32 (0 = 32). Back-to-back
+  uint32_t batches_per_launch; /* L <= 128: device batches matched per kernel launch, 1..64 (0 = 32). Back-to-back
                                   me_submit_batch_device calls fill a group; me_sync flushes a partial one */
 } me_config;
 

@@ -293,7 +293,7 @@ def test_full_size_config2_bitexact(me, orc):
 
 
 
-@pytest.mark.parametrize("group", [1, 3, 8, 32])
+@pytest.mark.parametrize("group", [1, 3, 8, 32, 64])
 @pytest.mark.parametrize("stream", ["uniform", "skewed"])
 def test_back_to_back_device_batches(me, orc, group, stream):
     """Device batches submitted back to back without a sync (the bench's pattern), matched
@@ -304,7 +304,7 @@ def test_back_to_back_device_batches(me, orc, group, stream):
     sc = me.preset(2, **over)
     st = me.Stream(sc)
     base = st.base_prices()
-    batches = [st.next(sc.batch) for _ in range(12)]
+    batches = [st.next(sc.batch) for _ in range(max(12, group + 5))]  # >= one full group + a partial one
     if stream == "skewed":
         for k, b in enumerate(batches):
             b.symbol[k * 97 % len(b)::4099] = sc.num_symbols + 3  # unknown symbols
