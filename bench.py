@@ -66,6 +66,8 @@ def parse():
     ap.add_argument("--batches-per-launch", type=int, default=0,
                     help="batches matched per kernel launch (me_config.batches_per_launch; 0 = engine default 32)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1),
+                    help="threads of the sharded CPU baseline (the GPU box's CPU share is 16); 1 = scalar only")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--timing-every", type=int, default=4,
@@ -164,20 +166,32 @@ def build_rank_batches(args, world, rank, nbatches):
 
 
 def cpu_baseline(args):
-    """Scalar CPU oracle (oracle/, a port of the build-defined matching semantics; the reference
-    itself has no matcher) on a bounded prefix of the same N=1 stream, 1 thread."""
+    """CPU oracle (oracle/, the scalar price-time book of the build-defined semantics; the reference
+    itself has no matcher) on a bounded prefix of the same N=1 stream: 1 thread, and `--cpu-threads`
+    threads with the symbols hash-sharded across them exactly as across GPUs (one book per thread,
+    no shared state; ctypes drops the GIL inside orc_submit). Batches are split per thread before
+    the clock starts, like the GPU's HBM-resident inputs."""
+    import threading
+
     from oracle.oracle import OracleBook
 
     w = WORKLOADS[args.workload]
-    sc = me.preset(w["preset"], num_symbols=global_symbols(args, 1), batch=args.batch_per_gpu)
-    st = me.Stream(sc)
-    ob = OracleBook(sc.num_symbols, sc.levels, st.base_prices(), 1 << 40)
+    S = global_symbols(args, 1)
+    sc = me.preset(w["preset"], num_symbols=S, batch=args.batch_per_gpu)
+
+    def seeded_stream():
+        st = me.Stream(sc)
+        seeds = st.seed_books(range(w["seeded"]), w["per_side"]) if w.get("seeded") else None
+        return st, seeds
+
+    # ---- 1 thread
+    st, seeds = seeded_stream()
+    ob = OracleBook(S, sc.levels, st.base_prices(), 1 << 40)
     seeded = ""
-    if w.get("seeded"):  # config 4: the same pre-seeded deep books as the GPU run (untimed)
-        sb = st.seed_books(range(w["seeded"]), w["per_side"])
-        for i in range(0, len(sb), 1 << 20):
-            ob.submit(sb.take(slice(i, i + (1 << 20))))
-        seeded = f" after seeding {len(sb)} resting orders (untimed)"
+    if seeds is not None:  # config 4: the same pre-seeded deep books as the GPU run (untimed)
+        for i in range(0, len(seeds), 1 << 20):
+            ob.submit(seeds.take(slice(i, i + (1 << 20))))
+        seeded = f" after seeding {len(seeds)} resting orders (untimed)"
     done, t_cpu, k = 0, 0.0, 0
     while t_cpu < args.cpu_seconds:
         b = st.next(sc.batch)
@@ -186,9 +200,47 @@ def cpu_baseline(args):
         t_cpu += time.perf_counter() - t0
         done += len(b)
         k += 1
-    return {"value": done / t_cpu, "unit": "orders/s", "cores": 1, "kind": "port",
-            "sample": f"first {k} batches ({done} orders) of the {args.workload} stream, oracle/oracle_book.cpp "
-                      f"scalar price-time book, {t_cpu:.1f}s{seeded}"}
+    ob.close()
+    one = done / t_cpu
+    out = {"value": one, "unit": "orders/s", "cores": 1, "kind": "port",
+           "sample": f"first {k} batches ({done} orders) of the {args.workload} stream, oracle/oracle_book.cpp "
+                     f"scalar price-time book, {t_cpu:.1f}s{seeded}"}
+    T = args.cpu_threads
+    if T <= 1:
+        return out
+    # ---- T threads, symbols hash-sharded (the same prefix length as the 1-thread sample)
+    st, seeds = seeded_stream()
+    from matching_engine_amd.sharding import ShardPlan
+
+    plan = ShardPlan(S, T)
+    base = st.base_prices()
+    books = [OracleBook(len(plan.members[r]), sc.levels, base[plan.members[r]], 1 << 40) for r in range(T)]
+    if seeds is not None:
+        for i in range(0, len(seeds), 1 << 20):
+            for r, (lb, _) in enumerate(plan.split(seeds.take(slice(i, i + (1 << 20))))):
+                books[r].submit(lb)
+    parts = [[] for _ in range(T)]
+    for _ in range(k):
+        for r, (lb, _) in enumerate(plan.split(st.next(sc.batch))):
+            parts[r].append(lb)
+
+    def run(r):
+        for lb in parts[r]:
+            books[r].submit(lb)
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(T)]
+    t0 = time.perf_counter()
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    tw = time.perf_counter() - t0
+    for bk in books:
+        bk.close()
+    out.update({"value": done / tw, "cores": T, "single_core_value": one,
+                "sample": out["sample"] + f"; then the same {k} batches on {T} threads, symbols hash-sharded "
+                          f"(one book per thread), {tw:.1f}s wall"})
+    return out
 
 
 def main():
