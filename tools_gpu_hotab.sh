@@ -8,7 +8,8 @@ O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd $R
 B="python bench.py --workload c4 --steps 12 --warmup 3 --no-e2e --no-cpu-baseline --traffic-from ''"
-for V in "ME_HOT_MIN=0" "ME_HOT_CACHE=1" "ME_HOT_CACHE=0"; do
-  env $V timeout -k 10 300 $B > $O/$V.json 2> $O/$V.err || { echo BENCH_FAIL $V; tail -5 $O/$V.err; exit 1; }
-  python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], round(d['value']/1e6,3), 'M orders/s', round(d['kernel_match_ms_avg'],3), 'ms')" $O/$V.json $V
+for V in "ME_HOT_MIN=0" "ME_HOT_MIN=64 ME_HOT_CACHE=1" "ME_HOT_MIN=64 ME_HOT_CACHE=0"; do
+  F=$(echo $V | tr " =" "__")
+  env $V timeout -k 10 300 $B > $O/$F.json 2> $O/$F.err || { echo BENCH_FAIL $V; tail -5 $O/$F.err; exit 1; }
+  python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], round(d['value']/1e6,3), 'M orders/s', round(d['kernel_match_ms_avg'],3), 'ms')" $O/$F.json "$V"
 done
