@@ -139,7 +139,10 @@ constexpr uint32_t HOT_MIN_RECORDS = 64;  // threshold the tests use (ME_HOT_MIN
 // group of up to ME_GMAX batches: every symbol's wave runs through its records of all of them in
 // order, so a launch costs the heaviest symbol's share of the whole group rather than the sum of
 // each batch's heaviest share.
-constexpr int ME_GMAX = 64;
+#ifndef ME_GROUP_MAX
+#define ME_GROUP_MAX 64
+#endif
+constexpr int ME_GMAX = ME_GROUP_MAX;
 constexpr uint32_t ME_DEFAULT_GROUP = 32;
 
 // Side jobs of one pipelined register-ladder launch (me_match_reg.hip), run by each workgroup's

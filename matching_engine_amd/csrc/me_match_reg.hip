@@ -73,7 +73,10 @@ struct RegLds {
     uint32_t lst[1024];  // rescan: batch indices of the symbol's records in one 1024-record window
   } in;
 };
-constexpr int REG_WAVES = 4;  // matching waves (symbols) per workgroup; as many side-job waves follow
+#ifndef ME_REG_WAVES
+#define ME_REG_WAVES 4
+#endif
+constexpr int REG_WAVES = ME_REG_WAVES;  // matching waves (symbols) per workgroup; as many side-job waves follow
 constexpr int VMCNT0 = 0x0F70;  // s_waitcnt immediate: vmcnt(0), expcnt / lgkmcnt untouched (gfx9 encoding)
 
 // One 32-bit field of the 128-level ladder: level l is lane (l & 63) of row (l >> 6).
@@ -848,6 +851,11 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
     if (blockIdx.x < nwg) aux_jobs(G, blockIdx.x * REG_WAVES + k, nwg * REG_WAVES);
     return;
   }
+#ifndef ME_NO_SETPRIO
+  // the serial record loop outranks the side jobs sharing its SIMD at the issue arbiter (the side
+  // jobs are latency work with slack until the next launch)
+  __builtin_amdgcn_s_setprio(3);
+#endif
   const uint32_t s = blockIdx.x * REG_WAVES + wv;
   const uint32_t ng = args.ng;
   if (ng == 0u || s > bk.S) return;  // no match job in this launch / no symbol
