@@ -56,7 +56,7 @@ WORKLOADS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=320)
+    ap.add_argument("--steps", type=int, default=640)
     ap.add_argument("--warmup", type=int, default=32)
     ap.add_argument("--workload", default="c2", choices=sorted(WORKLOADS),
                     help="c2 (default) = BASELINE configs[1], the metric's workload; c3/c4/c5 = the other "
