@@ -91,10 +91,7 @@ struct me_engine {
   // Bucketed grouping (register-ladder kernel): per-bin counts and BK_CAP-record buckets.
   struct BucketBufs {
     uint32_t* cnt = nullptr;
-    uint64_t* seq = nullptr;
-    int64_t* px = nullptr;
-    int32_t* qty = nullptr;
-    uint32_t* ok = nullptr;
+    BkRec* rec = nullptr;
   } bu[2 * ME_GMAX];
   bool bucketed = false;
   // Pipelined path: batches submitted but not finished. Submits fill a group of up to `group`
@@ -176,7 +173,7 @@ static void free_all(me_engine* e) {
     for (void* p : sp)
       if (p) (void)hipFree(p);
     for (auto& b : e->bu) {
-      void* bp[] = {b.cnt, b.seq, b.px, b.qty, b.ok};
+      void* bp[] = {b.cnt, b.rec};
       for (void* p : bp)
         if (p) (void)hipFree(p);
     }
@@ -370,10 +367,7 @@ extern "C" me_engine* me_create(const me_config* cfg) {
     for (uint32_t k = 0; k < 2 * e->group; ++k) {
       auto& b = e->bu[k];
       ALLOC(b.cnt, (S + 1) * BK_CNT_STRIDE);
-      ALLOC(b.seq, nb);
-      ALLOC(b.px, nb);
-      ALLOC(b.qty, nb);
-      ALLOC(b.ok, nb);
+      ALLOC(b.rec, nb);
     }
   }
   e->nsets = e->bucketed ? 3 * (int)e->group : 1;
@@ -511,10 +505,7 @@ static int pipe_launch(me_engine* e, const me_engine::Group* nb) {
     bt[g] = batch_dev(e, pm.seq, pm.px, pm.qty, pm.sym, pm.kind, pm.n, pm.oset);
     const auto& b = e->bu[pm.bset];
     bt[g].bcnt = b.cnt;
-    bt[g].b_seq = b.seq;
-    bt[g].b_px = b.px;
-    bt[g].b_qty = b.qty;
-    bt[g].b_ok = b.ok;
+    bt[g].b_rec = b.rec;
     bt[g].bcap = BK_CAP;
     orders += pm.n;
   }
@@ -534,10 +525,7 @@ static int pipe_launch(me_engine* e, const me_engine::Group* nb) {
       J.kind = p.kind;
       J.n = p.n;
       J.bcnt = b.cnt;
-      J.b_seq = b.seq;
-      J.b_px = b.px;
-      J.b_qty = b.qty;
-      J.b_ok = b.ok;
+      J.b_rec = b.rec;
       J.bres = o.res;
       J.bfstart = o.fstart;
       J.zero_tile_sum = o.tile_sum;

@@ -75,6 +75,15 @@ struct alignas(32) SymState {
   uint32_t pad;
 };
 
+// One bucketed record (24 B, AoS): the bucket job writes it as one unit, so a record's bytes land
+// in one or two lines instead of four SoA arrays' lines (fewer partially written lines per XCD).
+struct alignas(8) BkRec {
+  uint64_t seq;
+  int64_t px;
+  int32_t qty;
+  uint32_t ok;  // batch index | (kind & 15) << BK_KIND_SHIFT
+};
+
 struct BookDev {
   Level* levels;
   unsigned long long* occ;
@@ -121,10 +130,7 @@ struct BatchDev {
   // a bucket by batch index on chip and resets bcnt; a bin with more than bcap records rescans the
   // batch in order instead. Null bcnt: the sort path.
   uint32_t* bcnt;        // [(S + 1) * BK_CNT_STRIDE]
-  const uint64_t* b_seq;
-  const int64_t* b_px;
-  const int32_t* b_qty;
-  const uint32_t* b_ok;  // batch index | (kind & 15) << BK_KIND_SHIFT
+  const struct BkRec* b_rec;  // [(S + 1) * bcap] bucketed records
   uint32_t bcap;
   // Deep-window path (L > LDS_MAX_LEVELS): a symbol with >= hot_min records in the batch is handed
   // from k_match<LAD_HBM> to k_match_hot (one workgroup, LDS-resident ladder window) through
@@ -157,10 +163,7 @@ struct AuxBucket {  // bucket + clear job of one batch
   uint32_t n;
   uint32_t zero_tiles;
   uint32_t* bcnt;
-  uint64_t* b_seq;
-  int64_t* b_px;
-  int32_t* b_qty;
-  uint32_t* b_ok;
+  struct BkRec* b_rec;
   me_order_result* bres;  // the batch's results: unknown-symbol records are rejected by the bucket job
   uint32_t* bfstart;
   uint32_t* zero_tile_sum;
@@ -188,7 +191,7 @@ struct AuxDev {
 };
 
 constexpr int BK_CAP = 128;          // records per bucket (two 64-record blocks)
-constexpr int BK_KIND_SHIFT = 28;    // b_ok: kind bits above the batch index
+constexpr int BK_KIND_SHIFT = 28;    // BkRec::ok: kind bits above the batch index
 constexpr uint32_t BK_IDX_MASK = (1u << BK_KIND_SHIFT) - 1u;
 constexpr uint32_t BK_MAX_BATCH = 1u << 25;  // sort key (index << 7 | bucket slot) fits 32 bits
 constexpr int BK_CNT_STRIDE = 32;    // bcnt[b * stride]: one 128-B line per counter (atomics on one

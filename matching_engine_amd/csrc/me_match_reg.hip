@@ -719,10 +719,7 @@ __device__ __forceinline__ void aux_bucket(const ColdArgs& G, uint32_t j, uint32
   const gptr<const int32_t> qty = ldsg(J.qty);
   const gptr<const uint8_t> kind = ldsg(J.kind);
   const gptr<uint32_t> bcnt = ldsg(J.bcnt);
-  const gptr<uint64_t> bseq = ldsg(J.b_seq);
-  const gptr<int64_t> bpx = ldsg(J.b_px);
-  const gptr<int32_t> bqty = ldsg(J.b_qty);
-  const gptr<uint32_t> bok = ldsg(J.b_ok);
+  const gptr<BkRec> brec = ldsg(J.b_rec);
   const uint32_t S = ldsu(G.ax.S);
   const gptr<me_order_result> bres = ldsg(J.bres);
   const gptr<uint32_t> bfst = ldsg(J.bfstart);
@@ -741,10 +738,10 @@ __device__ __forceinline__ void aux_bucket(const ColdArgs& G, uint32_t j, uint32
       const uint32_t r = atomicAdd(&bcnt[(size_t)b * BK_CNT_STRIDE], 1u);
       if (r < (uint32_t)BK_CAP) {
         const size_t d = (size_t)b * BK_CAP + r;
-        bseq[d] = sq;
-        bpx[d] = p;
-        bqty[d] = q;
-        bok[d] = i | ((k & 15u) << BK_KIND_SHIFT);
+        brec[d].seq = sq;
+        brec[d].px = p;
+        brec[d].qty = q;
+        brec[d].ok = i | ((k & 15u) << BK_KIND_SHIFT);
       }
     }
   }
@@ -959,14 +956,11 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
       if (nsg == 0u) continue;
       const BatchDev& B = G.bt[g];
       const size_t bb = (size_t)s * BK_CAP;
-      const gptr<const uint64_t> pseq = ldsg(B.b_seq);
-      const gptr<const int64_t> ppx = ldsg(B.b_px);
-      const gptr<const int32_t> pqty = ldsg(B.b_qty);
-      const gptr<const uint32_t> pok = ldsg(B.b_ok);
-      const unsigned long long bq0 = pseq[bb + lane], bq1 = pseq[bb + 64 + lane];
-      const long long bp0 = ppx[bb + lane], bp1 = ppx[bb + 64 + lane];
-      const int bn0 = pqty[bb + lane], bn1 = pqty[bb + 64 + lane];
-      const uint32_t bo0 = pok[bb + lane], bo1 = pok[bb + 64 + lane];
+      const gptr<const BkRec> prec = ldsg(B.b_rec);
+      const unsigned long long bq0 = prec[bb + lane].seq, bq1 = prec[bb + 64 + lane].seq;
+      const long long bp0 = prec[bb + lane].px, bp1 = prec[bb + 64 + lane].px;
+      const int bn0 = prec[bb + lane].qty, bn1 = prec[bb + 64 + lane].qty;
+      const uint32_t bo0 = prec[bb + lane].ok, bo1 = prec[bb + 64 + lane].ok;
       if (lane == 0) ldsg(B.bcnt)[(size_t)s * BK_CNT_STRIDE] = 0u;  // ready for a later group's bucket job
       // ---- batch order. A bucket (<= BK_CAP records, arbitrary order) is staged in LDS and its keys
       // (batch index << 7 | bucket slot) sorted across the wave; an overfull bucket is replaced by a
