@@ -673,7 +673,9 @@ __device__ __forceinline__ bool rescan_window(RegLds* M, const ColdArgs& G, uint
   return false;
 }
 
-__device__ __forceinline__ void reject_bad_at(gptr<me_order_result> res, gptr<uint32_t> fstart, uint32_t i) {
+// (pipelined path: no fill start of its own — the tape job reads a record's scratch start from its
+// result's tape_offset, see aux_tape_tile)
+__device__ __forceinline__ void reject_bad_at(gptr<me_order_result> res, uint32_t i) {
   me_order_result r;
   r.filled_qty = 0;
   r.remaining_qty = 0;
@@ -683,7 +685,6 @@ __device__ __forceinline__ void reject_bad_at(gptr<me_order_result> res, gptr<ui
   r.reason = ME_RJ_BAD_SYMBOL;
   r.pad[0] = r.pad[1] = 0;
   res[i] = r;
-  fstart[i] = 0;
 }
 __device__ __forceinline__ void reject_bad(const ColdArgs& G, uint32_t g, uint32_t i, bool v) {
   if (!v) return;
@@ -722,13 +723,12 @@ __device__ __forceinline__ void aux_bucket(const ColdArgs& G, uint32_t j, uint32
   const gptr<BkRec> brec = ldsg(J.b_rec);
   const uint32_t S = ldsu(G.ax.S);
   const gptr<me_order_result> bres = ldsg(J.bres);
-  const gptr<uint32_t> bfst = ldsg(J.bfstart);
   for (uint32_t i0 = r0; i0 < r1; i0 += 64) {
     const uint32_t i = i0 + (uint32_t)lane;
     if (i < r1) {
       const uint32_t b = min(sym[i], S);
       if (b == S) {  // unknown symbol: rejected here, never bucketed (the batch's result set is free)
-        reject_bad_at(bres, bfst, i);
+        reject_bad_at(bres, i);
         continue;
       }
       const uint64_t sq = seq[i];  // the payload loads are in flight while the atomic returns
@@ -755,7 +755,6 @@ __device__ __forceinline__ void aux_tape_tile(const ColdArgs& G, uint32_t jb, ui
   const AuxTape& J = G.ax.t[jb];
   const gptr<const uint32_t> tile_sum = ldsg(J.tile_sum);
   const gptr<me_order_result> res = ldsg(J.res);
-  const gptr<const uint32_t> fstart = ldsg(J.fstart);
   const gptr<const me_fill> scratch = ldsg(J.scratch);
   const gptr<me_fill> tape = ldsg(J.tape);
   long long acc = 0;  // fills of the earlier tiles
@@ -764,12 +763,14 @@ __device__ __forceinline__ void aux_tape_tile(const ColdArgs& G, uint32_t jb, ui
   const unsigned long long base = (unsigned long long)rli64(acc, 0);
   const uint32_t r0 = t * TILE_TAPE;
   const uint32_t cnt = min((uint32_t)TILE_TAPE, tn - r0);
-  uint32_t c[TILE_TAPE / 64];
+  uint32_t c[TILE_TAPE / 64], src[TILE_TAPE / 64];
   long long loc = 0;
 #pragma unroll
   for (int k = 0; k < TILE_TAPE / 64; ++k) {  // lane holds records 4*lane .. 4*lane+3 of the tile
     const uint32_t j = (uint32_t)(lane * (TILE_TAPE / 64) + k);
+    // the match job left the record's scratch start in tape_offset (same line as fill_count)
     c[k] = j < cnt ? res[r0 + j].fill_count : 0u;
+    src[k] = j < cnt ? res[r0 + j].tape_offset : 0u;
     loc += c[k];
   }
   const long long incl = wave_incl_scan(loc);
@@ -789,11 +790,8 @@ __device__ __forceinline__ void aux_tape_tile(const ColdArgs& G, uint32_t jb, ui
   uint32_t o2 = (uint32_t)(incl - loc);
 #pragma unroll
   for (int k = 0; k < TILE_TAPE / 64; ++k) {
-    const uint32_t j = (uint32_t)(lane * (TILE_TAPE / 64) + k);
-    if (c[k]) {
-      const uint32_t src = fstart[r0 + j];
-      for (uint32_t q = 0; q < c[k]; ++q) tape[base + o2 + q] = scratch[src + q];
-    }
+    if (c[k])
+      for (uint32_t q = 0; q < c[k]; ++q) tape[base + o2 + q] = scratch[src[k] + q];
     o2 += c[k];
   }
   if (t == ntiles - 1 && lane == 0) {
@@ -1122,11 +1120,12 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
       // ---- results of the block in vector form
       me_order_result* res = ldsg(G.bt[ldsu(c.M->g_cur)].res);
       uint32_t* fstart = ldsg(G.bt[ldsu(c.M->g_cur)].fstart);
+      const bool sortp = ldsu(G.bt[0].bcnt) == nullptr;
       uint32_t* tile_sum = ldsg(G.bt[ldsu(c.M->g_cur)].tile_sum);
       if (rj != 0xFFu && (uint32_t)lane < stop) {
         const bool market = (kd_ >> 2) & 1u, cancel = (kd_ >> 3) & 1u;
         me_order_result r;
-        r.tape_offset = 0;
+        r.tape_offset = out_w;  // scratch start until the tape job writes the tape offset
         r.pad[0] = r.pad[1] = 0;
         r.fill_count = out_n;
         r.reason = (uint8_t)rj;
@@ -1149,7 +1148,7 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
                               : ME_ST_NEW;
         }
         res[oi] = r;
-        fstart[oi] = out_w;
+        if (sortp) fstart[oi] = out_w;  // k_tape_compact (sort path) reads the fill starts array
         if (out_n) atomicAdd(&tile_sum[oi / TILE_TAPE], out_n);
       }
       STAMP_ADD(c, PH_RESULT);
