@@ -186,7 +186,7 @@ def cpu_baseline(args):
 
     # ---- 1 thread
     st, seeds = seeded_stream()
-    ob = OracleBook(S, sc.levels, st.base_prices(), 1 << 40)
+    ob = OracleBook(S)
     seeded = ""
     if seeds is not None:  # config 4: the same pre-seeded deep books as the GPU run (untimed)
         for i in range(0, len(seeds), 1 << 20):
@@ -214,7 +214,7 @@ def cpu_baseline(args):
 
     plan = ShardPlan(S, T)
     base = st.base_prices()
-    books = [OracleBook(len(plan.members[r]), sc.levels, base[plan.members[r]], 1 << 40) for r in range(T)]
+    books = [OracleBook(len(plan.members[r])) for r in range(T)]
     if seeds is not None:
         for i in range(0, len(seeds), 1 << 20):
             for r, (lb, _) in enumerate(plan.split(seeds.take(slice(i, i + (1 << 20))))):
@@ -260,7 +260,7 @@ def main():
     n_seed = sum(len(b) for b in seeds)
     eng = me.Engine(len(ids), sc.levels, base,
                     max_batch=max(len(b) for b in batches + gather_batches + e2e_batches + seeds) + 1,
-                    max_resting=total_local // 3 + n_seed + 65536, max_seq=global_orders + n_seed + 16,
+                    max_resting=total_local // 3 + n_seed + 65536,
                     device=local, symbol_ids=ids, batches_per_launch=args.batches_per_launch)
     for b in seeds:
         eng.submit_batch(b, want_fills=False)

@@ -54,10 +54,10 @@ enum {
   ME_RJ_NONE = 0,
   ME_RJ_BAD_QTY = 1,       /* qty <= 0 (the service rejects these before they reach a batch) */
   ME_RJ_BAD_SIDE = 2,      /* side not BUY/SELL (reference: CHECK side IN (1,2) -> "DB insert failed") */
-  ME_RJ_OUT_OF_WINDOW = 3, /* LIMIT price outside the symbol's fixed-depth level window */
+  ME_RJ_OUT_OF_WINDOW = 3, /* retired: every int64 price is accepted (never produced) */
   ME_RJ_BAD_SYMBOL = 4,    /* symbol id >= num_symbols */
   ME_RJ_UNKNOWN_ORDER = 5, /* CANCEL target is not a live resting order of this symbol */
-  ME_RJ_BAD_SEQ = 6        /* seq outside [1, max_seq) (locator capacity) */
+  ME_RJ_BAD_SEQ = 6        /* seq == 0 (no OID is 0: the counter starts at 1, storage.cpp:254-267) */
 };
 
 /* kind byte of a batch record: bits 0-1 side, bit 2 type (1 = MARKET), bit 3 op (1 = CANCEL). */
@@ -88,18 +88,25 @@ typedef struct me_engine me_engine;
 typedef struct me_config {
   int32_t device;              /* HIP device ordinal */
   uint32_t num_symbols;        /* local symbols of this shard, ids 0..num_symbols-1 */
-  uint32_t levels;             /* L: fixed-depth price levels per symbol (power of two, 64..2^20) */
+  uint32_t levels;             /* L: price levels of each symbol's on-chip WINDOW (power of two, 64..2^20).
+                                  Prices are not limited to it: levels outside live in far arrays and the
+                                  window re-centres as the market moves */
   uint32_t max_batch;          /* largest n accepted by me_submit_batch* */
   uint64_t max_resting;        /* resting orders the scratch/tape bound is sized for */
   uint64_t max_chunks;         /* FIFO chunk pool (ME_CHUNK_SLOTS slots each); 0 = max_resting + 2*S */
-  uint64_t max_seq;            /* locator capacity: accepted seqs are 1 <= seq < max_seq */
-  const int64_t* base_price;   /* [num_symbols] price_q4 of level 0 of each symbol's window */
+  uint64_t seq_ring;           /* seq-ring entries for cancels (power of two, 0 = 2^28). Any u64 seq is
+                                  accepted; one launch group (batches_per_launch batches) must span fewer
+                                  than seq_ring seqs */
+  const int64_t* base_price;   /* [num_symbols] initial window base (price_q4 of level 0) per symbol */
   const uint32_t* symbol_ids;  /* optional [num_symbols] ids written to me_fill.symbol (NULL = local id) */
   uint32_t batches_per_launch; /* L <= 128: device batches matched per kernel launch, 1..64 (0 = 32). Back-to-back
                                   me_submit_batch_device calls fill a group; me_sync flushes a partial one */
+  uint32_t far_levels;         /* capacity per symbol and side of the far arrays (price levels outside the
+                                  window), 0 = 1024 */
 } me_config;
 
-/* One batch in structure-of-arrays form, ascending seq (= numeric OID). */
+/* One batch in structure-of-arrays form. Seqs (= numeric OIDs) strictly ascend across the whole
+ * stream of an engine (checked on the device: a violation fails the batch with ME_E_INVALID). */
 typedef struct me_order_soa {
   const uint64_t* seq;      /* numeric OID of the record */
   const int64_t* price_q4;  /* NEW: normalized Q4 price (ignored for MARKET); CANCEL: target seq */
@@ -167,6 +174,11 @@ int me_sync(me_engine* e);
 /* Copy the last batch's tape/results to host memory (synchronous). */
 int me_fetch_outputs(me_engine* e, me_fill* out_fills, size_t fills_cap, size_t* n_fills,
                      me_order_result* out_results, size_t n_results);
+/* Batches of the most recent launch group (1..batches_per_launch; the last batch is the last one of
+ * it) and the outputs of its k-th batch (synchronous, like me_fetch_outputs). */
+uint32_t me_last_group_size(const me_engine* e);
+int me_fetch_group_outputs(me_engine* e, uint32_t k, me_fill* out_fills, size_t fills_cap, size_t* n_fills,
+                           me_order_result* out_results, size_t n_results);
 /* Device-to-device copy of the last batch's tape into dst (HBM), on the engine stream;
  * *n_fills is the synchronous tape length. */
 int me_copy_tape_device(me_engine* e, void* dst, size_t cap_fills, size_t* n_fills);
@@ -215,6 +227,10 @@ typedef struct me_gen_params {
   uint32_t cancel_pct;      /* % CANCEL among records */
   double zipf_s;            /* > 0: Zipf(s) symbol popularity, 0 = uniform */
   int32_t market_qty_mult;  /* > 0: MARKET qty = U[1, market_qty_mult] * max_qty (sweeps) */
+  uint64_t seq_start;       /* first seq of the stream (0 = 1) */
+  int32_t drift_step;       /* > 0: a symbol's mid moves drift_step ticks (in its own fixed direction) ... */
+  uint32_t drift_every;     /* ... every drift_every records of that symbol */
+  uint32_t far_pct;         /* % of LIMITs priced far away: mid +- U[levels, 64 * levels] ticks */
 } me_gen_params;
 
 typedef struct me_gen me_gen;

@@ -38,10 +38,11 @@ class MeConfig(C.Structure):
         ("max_batch", C.c_uint32),
         ("max_resting", C.c_uint64),
         ("max_chunks", C.c_uint64),
-        ("max_seq", C.c_uint64),
+        ("seq_ring", C.c_uint64),
         ("base_price", C.POINTER(C.c_int64)),
         ("symbol_ids", C.POINTER(C.c_uint32)),
         ("batches_per_launch", C.c_uint32),
+        ("far_levels", C.c_uint32),
     ]
 
 
@@ -67,6 +68,10 @@ class MeGenParams(C.Structure):
         ("cancel_pct", C.c_uint32),
         ("zipf_s", C.c_double),
         ("market_qty_mult", C.c_int32),
+        ("seq_start", C.c_uint64),
+        ("drift_step", C.c_int32),
+        ("drift_every", C.c_uint32),
+        ("far_pct", C.c_uint32),
     ]
 
 
@@ -103,6 +108,8 @@ PROTOTYPES = {
     "me_submit_batch_device": (C.c_int, [_P, C.POINTER(MeOrderSoa), _SZ]),
     "me_sync": (C.c_int, [_P]),
     "me_fetch_outputs": (C.c_int, [_P, _P, _SZ, C.POINTER(_SZ), _P, _SZ]),
+    "me_last_group_size": (C.c_uint32, [_P]),
+    "me_fetch_group_outputs": (C.c_int, [_P, C.c_uint32, _P, _SZ, C.POINTER(_SZ), _P, _SZ]),
     "me_copy_tape_device": (C.c_int, [_P, _P, _SZ, C.POINTER(_SZ)]),
     "me_copy_results_device": (C.c_int, [_P, _P, _SZ]),
     "me_device_alloc": (C.c_int, [_P, _SZ, C.POINTER(_P)]),

@@ -22,7 +22,10 @@ namespace me {
 hipError_t launch_sort_pass(hipStream_t st, const uint32_t* keys_in, const uint32_t* idx_in, uint32_t n,
                             uint32_t clamp_key, int shift, int dbits, uint32_t* hist, uint32_t* tot,
                             uint32_t* keys_out, uint32_t* idx_out, uint32_t* zero_buf,
-                            uint32_t zero_words, unsigned long long* scratch_top, uint32_t* bin_start);
+                            uint32_t zero_words, unsigned long long* scratch_top, uint32_t* bin_start,
+                            const uint64_t* seq, uint32_t* err);
+hipError_t launch_seq_sweep(hipStream_t st, const BookDev& bk, const uint64_t* const* seq, const uint32_t* n,
+                            uint32_t ng, uint32_t in_idx, uint32_t grid);
 hipError_t launch_match(hipStream_t st, const BookDev& bk, const BatchDev& bt, hipEvent_t ev0, hipEvent_t ev1);
 hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* bt, uint32_t ng, const AuxDev& ax, hipEvent_t ev0,
                             hipEvent_t ev1);
@@ -31,7 +34,6 @@ hipError_t launch_tape(hipStream_t st, const BatchDev& bt, me_fill* tape, unsign
                        unsigned long long* tape_count, unsigned long long* fills_acc, uint32_t* err);
 hipError_t launch_init_levels(hipStream_t st, Level* levels, size_t count);
 hipError_t launch_init_chunks(hipStream_t st, Chunk* chunks, size_t count);
-hipError_t prepare_hot(const BookDev& bk);
 }  // namespace me
 
 using namespace me;
@@ -61,10 +63,6 @@ struct me_engine {
   uint64_t* d_seq = nullptr;
   int64_t* d_px = nullptr;
   int32_t* d_qty = nullptr;
-  // Deep windows (L > LDS_MAX_LEVELS): hand-off list of busy symbols to k_match_hot
-  // ([0] = count, then symbol ids) and the record count that makes a symbol busy (0 = off).
-  uint32_t* d_hot = nullptr;
-  uint32_t hot_min = 0;
   uint32_t* d_sym = nullptr;
   uint8_t* d_kind = nullptr;
   // Everything the grouping sort of a batch writes: sorted keys, permutation, histogram, run
@@ -126,6 +124,13 @@ struct me_engine {
   void* h_pin = nullptr;
   size_t h_pin_bytes = 0;
   uint32_t last_n = 0;
+  uint32_t sq_idx = 0;  // seq-ring state the next k_seq_sweep reads (it writes the other one)
+  struct LastGroup {    // the launch group holding the most recent batch: where its outputs live
+    uint32_t n = 0;
+    int oset[ME_GMAX];
+    int tape[ME_GMAX];
+    uint32_t bn[ME_GMAX];
+  } lastg;
   bool failed = false;
   std::string err;
   // timing
@@ -164,7 +169,7 @@ static void free_all(me_engine* e) {
                   e->bk.loc,      e->bk.chunk_top, e->bk.err,       (void*)e->bk.gsym,
                   e->d_seq,       e->d_px,        e->d_qty,       e->d_sym,         e->d_kind,
                   e->d_tape,      e->d_tape_count, e->d_fills_acc, e->bk.dbg,      e->bk.fcache,
-                  e->d_hot};
+                  e->bk.far,      e->bk.old,       e->bk.sq};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   {
@@ -245,9 +250,10 @@ static bool zero_bucket_counts(me_engine* e, hipStream_t st) {
 
 extern "C" me_engine* me_create(const me_config* cfg) {
   if (!cfg || cfg->num_symbols == 0 || cfg->levels < 64 || (cfg->levels & (cfg->levels - 1)) ||
-      cfg->levels > (1u << 20) || cfg->max_batch == 0 || !cfg->base_price || cfg->max_seq < 2) {
+      cfg->levels > (1u << 20) || cfg->max_batch == 0 || !cfg->base_price ||
+      (cfg->seq_ring && (cfg->seq_ring < 64 || (cfg->seq_ring & (cfg->seq_ring - 1)) || cfg->seq_ring > (1ull << 34)))) {
     set_create_err("me_create: invalid config (num_symbols>0, levels power of two in [64,2^20], "
-                   "max_batch>0, base_price, max_seq>=2)");
+                   "max_batch>0, base_price, seq_ring 0 or a power of two in [64, 2^34])");
     return nullptr;
   }
   const uint64_t S = cfg->num_symbols;
@@ -324,7 +330,13 @@ extern "C" me_engine* me_create(const me_config* cfg) {
   bk.L = (uint32_t)L;
   bk.Lwords = (uint32_t)(L / 64);
   bk.nchunks = (uint32_t)nchunks;
-  bk.max_seq = cfg->max_seq;
+  const uint64_t ring = cfg->seq_ring ? cfg->seq_ring : (1ull << 28);
+  bk.ring_mask = ring - 1;
+  bk.fcap = cfg->far_levels ? cfg->far_levels : 1024u;
+  // old-order table: live orders <= resting, at load <= 1/2
+  uint64_t oldn = 1024;
+  while (oldn < 2 * (cfg->max_resting + 64)) oldn <<= 1;
+  bk.old_mask = oldn - 1;
   const uint32_t ntiles_sort = MAX_SORT_TILES;
   const uint32_t ntiles_tape = (uint32_t)((n + TILE_TAPE - 1) / TILE_TAPE);
 #define ALLOC(p, cnt)                                                              \
@@ -337,7 +349,10 @@ extern "C" me_engine* me_create(const me_config* cfg) {
   ALLOC(bk.tend, S * L);
   ALLOC(bk.sym, S);
   ALLOC(bk.chunks, nchunks);
-  ALLOC(bk.loc, cfg->max_seq);
+  ALLOC(bk.loc, ring);
+  ALLOC(bk.far, S * 2 * (uint64_t)bk.fcap);
+  ALLOC(bk.old, oldn);
+  ALLOC(bk.sq, 2);
   ALLOC(bk.chunk_top, 1);
   ALLOC(bk.err, 1);
   uint32_t* gsym = nullptr;
@@ -383,18 +398,6 @@ extern "C" me_engine* me_create(const me_config* cfg) {
   ALLOC(e->d_tape, scap * e->group);
   ALLOC(e->d_tape_count, ME_GMAX);
   ALLOC(e->d_fills_acc, 1);
-  if (L > LDS_MAX_LEVELS) {
-    // ME_HOT_MIN=n (opt-in, A/B runs): symbols with >= n records in a batch get an LDS-resident
-    // ladder window (k_match_hot). Off by default: measured slower than the HBM ladder on config 4
-    // (DESIGN.md §8 — the hot wave is bound by dependent chunk loads and issue, not level reads).
-    e->hot_min = 0;
-    if (const char* v = getenv("ME_HOT_MIN")) e->hot_min = (uint32_t)strtoul(v, nullptr, 10);
-    if (e->hot_min) {
-      ALLOC(e->d_hot, 1 + HOT_MAX);
-      hipError_t he = prepare_hot(bk);
-      if (he != hipSuccess) return bail(std::string("k_match_hot LDS window: ") + hipGetErrorString(he));
-    }
-  }
 #ifdef ME_STAMPS
   ALLOC(bk.dbg, S * 24);
   (void)hipMemset(bk.dbg, 0, S * 24 * 8);
@@ -408,22 +411,26 @@ extern "C" me_engine* me_create(const me_config* cfg) {
   std::vector<SymState> ss(S);
   std::vector<uint32_t> gs(S);
   e->base_host.assign(cfg->base_price, cfg->base_price + S);
+  const int64_t base_max = INT64_MAX - (int64_t)L + 1;  // base + L never overflows
   for (uint64_t i = 0; i < S; ++i) {
-    ss[i].base = cfg->base_price[i];
+    memset(&ss[i], 0, sizeof(SymState));
+    ss[i].base = cfg->base_price[i] > base_max ? base_max : cfg->base_price[i];
     ss[i].best_bid = -1;
     ss[i].best_ask = (int)L;
     ss[i].free_head = NIL;
-    ss[i].resting = 0;
-    ss[i].nfree = 0;
-    ss[i].pad = 0;
     gs[i] = cfg->symbol_ids ? cfg->symbol_ids[i] : (uint32_t)i;
   }
+  SeqState sq0[2];
+  memset(sq0, 0, sizeof sq0);
+  sq0[0].epoch = sq0[1].epoch = 1;  // old-order entries of epoch 0 (the zeroed table) read as empty
   bool ok = launch_init_levels(st, bk.levels, S * L) == hipSuccess &&
             zero_bucket_counts(e, st) &&
             hipMemsetAsync(bk.occ, 0, S * (L / 64) * 8, st) == hipSuccess &&
             hipMemsetAsync(bk.tend, 0, S * L, st) == hipSuccess &&
             launch_init_chunks(st, bk.chunks, nchunks) == hipSuccess &&
-            hipMemsetAsync(bk.loc, 0xFF, cfg->max_seq * sizeof(uint32_t), st) == hipSuccess &&
+            hipMemsetAsync(bk.loc, 0xFF, ring * sizeof(uint32_t), st) == hipSuccess &&
+            hipMemsetAsync(bk.old, 0, oldn * sizeof(OldEnt), st) == hipSuccess &&
+            hipMemcpyAsync(bk.sq, sq0, sizeof sq0, hipMemcpyHostToDevice, st) == hipSuccess &&
             hipMemsetAsync(bk.fcache, 0xFF, S * 64 * sizeof(uint32_t), st) == hipSuccess &&
             hipMemsetAsync(bk.chunk_top, 0, 4, st) == hipSuccess && hipMemsetAsync(bk.err, 0, 4, st) == hipSuccess &&
             hipMemcpyAsync(bk.sym, ss.data(), S * sizeof(SymState), hipMemcpyHostToDevice, st) == hipSuccess &&
@@ -491,6 +498,22 @@ static BatchDev batch_dev(me_engine* e, const uint64_t* seq, const int64_t* px, 
   return bt;
 }
 
+// The seq-ring horizon check ahead of the match launch of a group (k_seq_sweep): flips the state
+// index the match launches read.
+static int seq_sweep(me_engine* e, const me_engine::Group& g) {
+  const uint64_t* seq[ME_GMAX];
+  uint32_t n[ME_GMAX];
+  for (uint32_t k = 0; k < g.n; ++k) {
+    seq[k] = g.b[k].seq;
+    n[k] = g.b[k].n;
+  }
+  hipError_t he = launch_seq_sweep(e->stream, e->bk, seq, n, g.n, e->sq_idx, 4 * e->ncu);
+  if (he != hipSuccess) return e->hip_fail(he, "seq sweep launch");
+  e->sq_idx ^= 1u;
+  e->bk.sq_idx = e->sq_idx;
+  return ME_OK;
+}
+
 // One launch of the pipelined register-ladder path: match group g_match (if any), bucket group nb
 // (if any) and clear the counters its batches will use, compact g_tape's tapes (if any) — then the
 // pipeline shifts by one group.
@@ -550,7 +573,9 @@ static int pipe_launch(me_engine* e, const me_engine::Group* nb) {
   TimedLaunch tl{};
   bool timed = false;
   if (gm.n) {
-    int rc = timing_slot(e, orders, gm.n, tl, timed);
+    int rc = seq_sweep(e, gm);
+    if (rc) return rc;
+    rc = timing_slot(e, orders, gm.n, tl, timed);
     if (rc) return rc;
   }
   hipError_t he = launch_match_reg(e->stream, e->bk, bt, gm.n, ax, tl.m0, tl.m1);
@@ -600,6 +625,10 @@ static int enqueue_batch(me_engine* e, const uint64_t* seq, const int64_t* px, c
     e->last_set = nb.oset;
     e->last_tape = (int)pos;
     e->last_n = n;
+    e->lastg.n = pos + 1;
+    e->lastg.oset[pos] = nb.oset;
+    e->lastg.tape[pos] = (int)pos;
+    e->lastg.bn[pos] = n;
     if (gf.n == e->group) {
       int rc = pipe_launch(e, &gf);
       gf = me_engine::Group{};
@@ -621,11 +650,19 @@ static int enqueue_batch(me_engine* e, const uint64_t* seq, const int64_t* px, c
   const uint32_t* iin = nullptr;
   uint32_t* run_table = e->passes == 1 ? sl.bin_start : nullptr;
   int shift = 0;
+  {
+    me_engine::Group g1;
+    g1.n = 1;
+    g1.b[0].seq = seq;
+    g1.b[0].n = n;
+    int rc2 = seq_sweep(e, g1);
+    if (rc2) return rc2;
+  }
   for (int p = 0; p < e->passes; ++p) {
     hipError_t he = launch_sort_pass(st, kin, iin, n, S, shift, e->dbits[p], sl.hist,
                                      sl.tot + ((size_t)p << MAX_DIGIT_BITS), sl.keys[p], sl.idx[p],
                                      p == 0 ? o.tile_sum : nullptr, p == 0 ? ntiles_tape : 0, o.top,
-                                     p == e->passes - 1 ? run_table : nullptr);
+                                     p == e->passes - 1 ? run_table : nullptr, p == 0 ? seq : nullptr, e->bk.err);
     if (he != hipSuccess) return e->hip_fail(he, "grouping sort launch");
     kin = sl.keys[p];
     iin = sl.idx[p];
@@ -635,8 +672,6 @@ static int enqueue_batch(me_engine* e, const uint64_t* seq, const int64_t* px, c
   bt.skeys = kin;
   bt.perm = iin;
   bt.bin_start = run_table;  // bins are symbols: the run table
-  bt.hot = e->d_hot;
-  bt.hot_min = e->hot_min;
   // timing: the launch itself records start/end (hipExtLaunchKernelGGL), no marker packets
   hipError_t he = launch_match(st, e->bk, bt, tl.m0, tl.m1);
   if (he != hipSuccess) return e->hip_fail(he, "match launch");
@@ -646,6 +681,10 @@ static int enqueue_batch(me_engine* e, const uint64_t* seq, const int64_t* px, c
   e->last_set = 0;
   e->last_tape = 0;
   e->last_n = n;
+  e->lastg.n = 1;
+  e->lastg.oset[0] = 0;
+  e->lastg.tape[0] = 0;
+  e->lastg.bn[0] = n;
   return ME_OK;
 }
 
@@ -657,7 +696,15 @@ static int check_err_word(me_engine* e) {
     if (w & ERR_CHUNK_OOM) m += " chunk pool exhausted (raise max_chunks);";
     if (w & ERR_SCRATCH_OOM) m += " fill scratch/tape bound exceeded (raise max_resting);";
     if (w & ERR_INCONSISTENT) m += " book inconsistency;";
-    return e->fail(ME_E_CAPACITY, m);
+    if (w & ERR_FAR_OOM) m += " far-level array full (raise far_levels);";
+    if (w & ERR_OLD_OOM) m += " old-order table full (raise max_resting);";
+    if (w & ERR_SEQ_ORDER) m += " seqs not strictly ascending (API precondition);";
+    if (w & ERR_SEQ_SPAN) m += " one launch group spans the whole seq ring (raise seq_ring);";
+    const int code = (w & (ERR_SEQ_ORDER | ERR_SEQ_SPAN)) && !(w & ~(ERR_SEQ_ORDER | ERR_SEQ_SPAN)) ? ME_E_INVALID
+                                                                                                    : ME_E_CAPACITY;
+    e->fail(code, m);
+    e->failed = true;  // sticky: the books may no longer be what the stream says
+    return code;
   }
   return ME_OK;
 }
@@ -705,6 +752,32 @@ extern "C" int me_fetch_outputs(me_engine* e, me_fill* out_fills, size_t fills_c
     if (cnt > fills_cap) return e->fail(ME_E_INVALID, "fills_cap smaller than the tape");
     HIP_TRY(hipMemcpy(out_fills, e->d_tape + (size_t)e->last_tape * e->tape_cap, cnt * sizeof(me_fill),
                       hipMemcpyDeviceToHost), "D2H tape");
+  }
+  return ME_OK;
+}
+
+extern "C" uint32_t me_last_group_size(const me_engine* e) { return e ? e->lastg.n : 0u; }
+
+extern "C" int me_fetch_group_outputs(me_engine* e, uint32_t k, me_fill* out_fills, size_t fills_cap, size_t* n_fills,
+                                      me_order_result* out_results, size_t n_results) {
+  if (!e) return ME_E_INVALID;
+  int rc = me_sync(e);
+  if (rc) return rc;
+  if (k >= e->lastg.n) return e->fail(ME_E_INVALID, "batch index outside the last launch group");
+  unsigned long long cnt = 0;
+  HIP_TRY(hipMemcpy(&cnt, e->d_tape_count + e->lastg.tape[k], 8, hipMemcpyDeviceToHost), "read tape count");
+  if (n_fills) *n_fills = (size_t)cnt;
+  if (out_results && n_results) {
+    if (n_results > e->lastg.bn[k]) return e->fail(ME_E_INVALID, "n_results exceeds the batch size");
+    HIP_TRY(hipMemcpy(out_results, e->os[e->lastg.oset[k]].res, n_results * sizeof(me_order_result),
+                      hipMemcpyDeviceToHost),
+            "D2H results");
+  }
+  if (out_fills && cnt) {
+    if (cnt > fills_cap) return e->fail(ME_E_INVALID, "fills_cap smaller than the tape");
+    HIP_TRY(hipMemcpy(out_fills, e->d_tape + (size_t)e->lastg.tape[k] * e->tape_cap, cnt * sizeof(me_fill),
+                      hipMemcpyDeviceToHost),
+            "D2H tape");
   }
   return ME_OK;
 }
@@ -826,6 +899,12 @@ namespace {
 struct HostLevelView {
   std::vector<Level> levels;
   SymState st;
+  std::vector<FarLevel> far[2];  // as stored: best last
+};
+// One price level in priority order (best first) of one side: window levels, then far levels.
+struct SideLevel {
+  int64_t price;
+  Level lv;
 };
 }  // namespace
 
@@ -835,7 +914,32 @@ static int load_symbol(me_engine* e, uint32_t s, HostLevelView& v) {
   HIP_TRY(hipMemcpy(v.levels.data(), e->bk.levels + (size_t)s * L, L * sizeof(Level), hipMemcpyDeviceToHost),
           "D2H levels");
   HIP_TRY(hipMemcpy(&v.st, e->bk.sym + s, sizeof(SymState), hipMemcpyDeviceToHost), "D2H symbol");
+  for (uint32_t k = 0; k < 2; ++k) {
+    const uint32_t n = std::min(v.st.nfar[k], e->bk.fcap);
+    v.far[k].resize(n);
+    if (n)
+      HIP_TRY(hipMemcpy(v.far[k].data(), far_of(e->bk, s, k), n * sizeof(FarLevel), hipMemcpyDeviceToHost),
+              "D2H far levels");
+  }
   return ME_OK;
+}
+
+// Bids (side 0) or asks (side 1) of a symbol, best first.
+static std::vector<SideLevel> side_levels(const me_engine* e, const HostLevelView& v, int side) {
+  std::vector<SideLevel> out;
+  const int L = (int)e->bk.L;
+  if (side == 0) {
+    for (int l = std::min(v.st.best_bid, L - 1); l >= 0; --l)
+      if (v.levels[l].total > 0) out.push_back({v.st.base + l, v.levels[l]});
+  } else {
+    for (int l = std::max(v.st.best_ask, 0); l < L; ++l)
+      if (v.levels[l].total > 0) out.push_back({v.st.base + l, v.levels[l]});
+  }
+  for (size_t i = v.far[side].size(); i-- > 0;) {
+    const FarLevel& f = v.far[side][i];
+    out.push_back({f.price, Level{f.total, f.head, f.tail}});
+  }
+  return out;
 }
 
 // Live (seq, qty) of a level FIFO in priority order.
@@ -864,21 +968,18 @@ extern "C" int me_book_snapshot(me_engine* e, uint32_t symbol, me_level* bids, m
   HostLevelView v;
   if ((rc = load_symbol(e, symbol, v))) return rc;
   std::vector<std::pair<uint64_t, int32_t>> fifo;
-  size_t nb = 0, na = 0;
-  for (int l = v.st.best_bid; l >= 0 && nb < depth; --l) {
-    if (v.levels[l].total <= 0) continue;
-    if ((rc = walk_fifo(e, v.levels[l], fifo))) return rc;
-    if (bids) bids[nb] = me_level{v.st.base + l, v.levels[l].total, (uint32_t)fifo.size(), 0};
-    ++nb;
+  for (int side = 0; side < 2; ++side) {
+    me_level* out = side ? asks : bids;
+    size_t k = 0;
+    for (const SideLevel& sl : side_levels(e, v, side)) {
+      if (k >= depth) break;
+      if ((rc = walk_fifo(e, sl.lv, fifo))) return rc;
+      if (out) out[k] = me_level{sl.price, sl.lv.total, (uint32_t)fifo.size(), 0};
+      ++k;
+    }
+    if (side == 0 && n_bids) *n_bids = k;
+    if (side == 1 && n_asks) *n_asks = k;
   }
-  for (int l = v.st.best_ask; l < (int)e->bk.L && na < depth; ++l) {
-    if (v.levels[l].total <= 0) continue;
-    if ((rc = walk_fifo(e, v.levels[l], fifo))) return rc;
-    if (asks) asks[na] = me_level{v.st.base + l, v.levels[l].total, (uint32_t)fifo.size(), 0};
-    ++na;
-  }
-  if (n_bids) *n_bids = nb;
-  if (n_asks) *n_asks = na;
   return ME_OK;
 }
 
@@ -891,19 +992,16 @@ extern "C" int me_book_dump(me_engine* e, uint32_t symbol, me_book_entry* out, s
   if ((rc = load_symbol(e, symbol, v))) return rc;
   std::vector<std::pair<uint64_t, int32_t>> fifo;
   size_t k = 0;
-  for (int pass = 0; pass < 2; ++pass) {
-    const bool bid = pass == 0;
-    int l = bid ? v.st.best_bid : v.st.best_ask;
-    for (; bid ? l >= 0 : l < (int)e->bk.L; l += bid ? -1 : 1) {
-      if (v.levels[l].total <= 0) continue;
-      if ((rc = walk_fifo(e, v.levels[l], fifo))) return rc;
+  for (int side = 0; side < 2; ++side) {
+    for (const SideLevel& sl : side_levels(e, v, side)) {
+      if ((rc = walk_fifo(e, sl.lv, fifo))) return rc;
       for (auto& pr : fifo) {
         if (out && k < cap) {
           me_book_entry be{};
           be.seq = pr.first;
-          be.price_q4 = v.st.base + l;
+          be.price_q4 = sl.price;
           be.qty = pr.second;
-          be.side = bid ? ME_SIDE_BUY : ME_SIDE_SELL;
+          be.side = side ? ME_SIDE_SELL : ME_SIDE_BUY;
           out[k] = be;
         }
         ++k;

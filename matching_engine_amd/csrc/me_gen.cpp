@@ -60,6 +60,8 @@ struct me_gen {
   Rng rng;
   uint64_t next_seq = 1;
   std::vector<int64_t> mid;
+  std::vector<int8_t> dir;          // drift direction of each symbol
+  std::vector<uint32_t> since;      // records of each symbol since its mid last moved
   std::vector<double> zipf_cdf;
   std::vector<std::vector<uint64_t>> cancel_pool;  // per symbol: LIMIT seqs not yet targeted
   explicit me_gen(const me_gen_params& pp) : p(pp), rng(pp.seed) {}
@@ -67,14 +69,19 @@ struct me_gen {
 
 extern "C" me_gen* me_gen_create(const me_gen_params* p) {
   if (!p || p->num_symbols == 0 || p->levels < 64 || p->max_qty <= 0 || p->spread_ticks < 0 ||
-      (int64_t)p->spread_ticks * 2 + 1 > (int64_t)p->levels || p->market_pct + p->cancel_pct > 100)
+      (int64_t)p->spread_ticks * 2 + 1 > (int64_t)p->levels || p->market_pct + p->cancel_pct > 100 ||
+      p->far_pct > 100 || p->drift_step < 0 || (p->drift_step > 0 && p->drift_every == 0))
     return nullptr;
   me_gen* g = new me_gen(*p);
+  g->next_seq = p->seq_start ? p->seq_start : 1;
   g->mid.resize(p->num_symbols);
+  g->dir.resize(p->num_symbols);
+  g->since.assign(p->num_symbols, 0);
   for (uint32_t s = 0; s < p->num_symbols; ++s) {
     // per-symbol mid: 100.0000 +- 10.0000 in Q4, fixed by (seed, symbol)
     const uint64_t h = splitmix64(p->seed * 0x100000001B3ull ^ (uint64_t)s);
     g->mid[s] = 1000000 + (int64_t)(h % 200001) - 100000;
+    g->dir[s] = (h >> 40) & 1 ? 1 : -1;
   }
   if (p->zipf_s > 0) {
     g->zipf_cdf.resize(p->num_symbols);
@@ -112,6 +119,10 @@ extern "C" int me_gen_next(me_gen* g, size_t n, uint64_t* seq, int64_t* price_q4
   for (size_t i = 0; i < n; ++i) {
     const uint64_t sq = g->next_seq++;
     const uint32_t s = pick_symbol(g);
+    if (p.drift_step > 0 && ++g->since[s] >= p.drift_every) {  // the symbol's market moves
+      g->since[s] = 0;
+      g->mid[s] += g->dir[s] * (int64_t)p.drift_step;
+    }
     const uint32_t r = (uint32_t)g->rng.below(100);
     uint8_t k;
     int64_t px = 0;
@@ -136,8 +147,13 @@ extern "C" int me_gen_next(me_gen* g, size_t n, uint64_t* seq, int64_t* price_q4
         if (p.market_qty_mult > 0) q = (int32_t)(1 + g->rng.below((uint64_t)p.market_qty_mult)) * p.max_qty;
         k = ME_KIND(side, ME_TYPE_MARKET, ME_OP_NEW);
       } else {
-        const int64_t off = (int64_t)g->rng.below(2 * (uint64_t)p.spread_ticks + 1) - p.spread_ticks;
+        int64_t off = (int64_t)g->rng.below(2 * (uint64_t)p.spread_ticks + 1) - p.spread_ticks;
+        if (p.far_pct && g->rng.below(100) < p.far_pct) {  // far away from the window, either side
+          off = (int64_t)p.levels + (int64_t)g->rng.below(63 * (uint64_t)p.levels + 1);
+          if (g->rng.next() >> 63) off = -off;
+        }
         px = g->mid[s] + off;
+        if (px < 1) px = 1;
         q = (int32_t)(1 + g->rng.below((uint64_t)p.max_qty));
         k = ME_KIND(side, ME_TYPE_LIMIT, ME_OP_NEW);
         if (p.cancel_pct) g->cancel_pool[s].push_back(sq);

@@ -8,7 +8,8 @@
 //   2. k_match                       one wavefront per symbol walks its records in seq order
 //                                    against the HBM-resident book (price-time priority), using
 //                                    ballot + 64-lane prefix scans over levels and FIFO chunks;
-//                                    fills go to a per-wave scratch run.
+//                                    fills go to a per-wave scratch run. (Windows of <= 128
+//                                    levels use k_match_reg, me_match_reg.hip.)
 //   3. k_tape_compact                exclusive scan of per-record fill counts (batch order) and
 //                                    a coalesced copy scratch -> tape ordered (taker_seq, fill#).
 //
@@ -17,6 +18,7 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
+#include "me_far.hpp"
 #include "me_layout.hpp"
 #include "me_wave.hpp"
 
@@ -43,15 +45,22 @@ __device__ __forceinline__ uint32_t sort_digit(uint32_t k, const SortPass& p) {
 }
 
 // Per-tile histograms, tile-major [tile][bin].
+// The first pass also checks the API precondition the seq ring relies on (seqs strictly ascending).
 __global__ __launch_bounds__(256) void k_sort_hist(const uint32_t* __restrict__ keys_in, uint32_t n, SortPass p,
                                                    uint32_t* __restrict__ hist, uint32_t* zero_buf,
-                                                   uint32_t zero_words, unsigned long long* scratch_top) {
+                                                   uint32_t zero_words, unsigned long long* scratch_top,
+                                                   const uint64_t* __restrict__ seq, uint32_t* err) {
   __shared__ uint32_t h[1u << MAX_DIGIT_BITS];
   for (uint32_t b = threadIdx.x; b < p.nbins; b += blockDim.x) h[b] = 0;
   __syncthreads();
   const uint32_t t0 = blockIdx.x * p.tile;
   const uint32_t t1 = min(n, t0 + p.tile);
-  for (uint32_t i = t0 + threadIdx.x; i < t1; i += blockDim.x) atomicAdd(&h[sort_digit(keys_in[i], p)], 1u);
+  bool order_ok = true;
+  for (uint32_t i = t0 + threadIdx.x; i < t1; i += blockDim.x) {
+    atomicAdd(&h[sort_digit(keys_in[i], p)], 1u);
+    if (seq && i > 0) order_ok &= seq[i] > seq[i - 1];
+  }
+  if (!order_ok) atomicOr(err, ERR_SEQ_ORDER);
   __syncthreads();
   for (uint32_t b = threadIdx.x; b < p.nbins; b += blockDim.x) hist[(size_t)blockIdx.x * p.nbins + b] = h[b];
   // Per-batch resets folded into the first kernel of the batch.
@@ -181,13 +190,15 @@ __global__ __launch_bounds__(256) void k_sort_scatter(const uint32_t* __restrict
 }
 
 // ------------------------------------------------------------------ matching
-// Head-chunk cache (LDS): entry (lvl & cmask) holds the FIFO head chunk of one level — its 16
-// slot quantities/seqs and its next pointer — so walks and appends on top-of-book levels stay
-// on chip. The HBM copy is stale while an entry is dirty; write-back on eviction, on free
-// (freed chunks must hold qty 0 in HBM) and at kernel end. With the register ladder (L <= 128)
-// every level has its own entry (no evictions).
-constexpr int CK_MEM = 64;  // entries with the LDS ladder (direct-mapped by level)
-constexpr int CK_REG = 128;
+// Deep windows (L > 128): one wavefront per symbol walks its records in seq order against the
+// ladder (levels / occupancy / tail fills in LDS for L <= LDS_MAX_LEVELS, else in HBM) and the far
+// levels outside the window (me_far.hpp).
+//
+// Head-chunk cache (LDS, ladders in LDS only): entry (lvl & cmask) holds the FIFO head chunk of one
+// level — its 16 slot quantities/seqs and its next pointer — so walks and appends on top-of-book
+// levels stay on chip. The HBM copy is stale while an entry is dirty; write-back on eviction, on free
+// (freed chunks must hold qty 0 in HBM), before a re-centre and at kernel end.
+constexpr int CK_MEM = 64;  // entries (direct-mapped by level)
 struct alignas(16) CacheEntry {
   uint32_t cid;    // cached chunk id, NIL = empty
   uint32_t dirty;  // slots differ from HBM
@@ -197,8 +208,7 @@ struct alignas(16) CacheEntry {
   unsigned long long seq[ME_C];
 };
 
-// ---- ladders: where a wave keeps its symbol's price levels ---------------------------------
-// LadderMem: levels / occupancy / tail-fill arrays behind pointers (LDS for L <= 1024, else HBM).
+// Where a wave keeps its symbol's window: levels / occupancy / tail-fill arrays behind pointers.
 struct LadderMem {
   Level* lv;
   unsigned long long* occ;
@@ -280,234 +290,23 @@ struct LadderMem {
   }
 };
 
-// LadderReg (L <= 128): level l lives in lane (l & 63) of register row (l >> 6). Reads are
-// readlanes, writes are per-lane selects; occupancy is a 128-bit mask in SGPRs (best-price search
-// = one bit scan). The head-chunk cache entry of level l is l itself (no evictions) and its
-// valid / dirty state are SGPR masks too: no memory round trip for any ladder bookkeeping.
-struct LadderReg {
-  long long t0, t1;  // total
-  uint32_t h0, h1;   // head chunk
-  uint32_t l0, l1;   // tail chunk
-  uint32_t e0, e1;   // slots written in the tail chunk
-  uint32_t L;
-  unsigned long long occ0, occ1;  // occupancy (wave-uniform)
-  unsigned long long cv0, cv1;    // cache entry l holds the head chunk of l
-  unsigned long long cd0, cd1;    // cache entry l is dirty
+struct WaveCtx;
+__device__ __forceinline__ uint32_t alloc_chunk(WaveCtx& c);
+__device__ __forceinline__ void free_chunk(WaveCtx& c, uint32_t ch);
 
-  __device__ __forceinline__ Level get(int l) const {
-    const int j = l & 63;
-    Level x;
-    if (l < 64) {
-      x.total = rli64(t0, j);
-      x.head = rl32(h0, j);
-      x.tail = rl32(l0, j);
-    } else {
-      x.total = rli64(t1, j);
-      x.head = rl32(h1, j);
-      x.tail = rl32(l1, j);
-    }
-    return x;
-  }
-  // (branch-free on purpose: a row-dependent if/else over members turns into a pointer select
-  // that keeps the whole context in scratch memory)
-  __device__ __forceinline__ void set(int l, const Level& x) {
-    const bool me = lane_id() == (l & 63);
-    const bool m0 = me && l < 64, m1 = me && l >= 64;
-    t0 = m0 ? x.total : t0;
-    h0 = m0 ? x.head : h0;
-    l0 = m0 ? x.tail : l0;
-    t1 = m1 ? x.total : t1;
-    h1 = m1 ? x.head : h1;
-    l1 = m1 ? x.tail : l1;
-  }
-  __device__ __forceinline__ uint32_t get_te(int l) const { return l < 64 ? rl32(e0, l & 63) : rl32(e1, l & 63); }
-  __device__ __forceinline__ void set_te(int l, uint32_t v) {
-    const bool me = lane_id() == (l & 63);
-    e0 = (me && l < 64) ? v : e0;
-    e1 = (me && l >= 64) ? v : e1;
-  }
-  static __device__ __forceinline__ unsigned long long lo_bit(int l) { return l < 64 ? (1ull << (l & 63)) : 0ull; }
-  static __device__ __forceinline__ unsigned long long hi_bit(int l) { return l >= 64 ? (1ull << (l & 63)) : 0ull; }
-  static __device__ __forceinline__ void bit_set(unsigned long long& a, unsigned long long& b, int l) {
-    a |= lo_bit(l);
-    b |= hi_bit(l);
-  }
-  static __device__ __forceinline__ void bit_clr(unsigned long long& a, unsigned long long& b, int l) {
-    a &= ~lo_bit(l);
-    b &= ~hi_bit(l);
-  }
-  static __device__ __forceinline__ bool bit_get(unsigned long long a, unsigned long long b, int l) {
-    return l < 64 ? ((a >> l) & 1ull) : ((b >> (l - 64)) & 1ull);
-  }
-  __device__ __forceinline__ void occ_set(int l) { bit_set(occ0, occ1, l); }
-  __device__ __forceinline__ void occ_clear(int l) { bit_clr(occ0, occ1, l); }
-  __device__ __forceinline__ int next_occ(int x) const {
-    if (x >= (int)L) return (int)L;
-    if (x < 0) x = 0;
-    if (x < 64) {
-      const unsigned long long w = occ0 & (~0ull << x);
-      if (w) return __builtin_ctzll(w);
-      return occ1 ? 64 + __builtin_ctzll(occ1) : (int)L;
-    }
-    const unsigned long long w = occ1 & (~0ull << (x - 64));
-    return w ? 64 + __builtin_ctzll(w) : (int)L;
-  }
-  __device__ __forceinline__ int prev_occ(int x) const {
-    if (x < 0) return -1;
-    if (x >= (int)L) x = (int)L - 1;
-    if (x >= 64) {
-      const int r = x - 64;
-      const unsigned long long w = occ1 & ((r == 63) ? ~0ull : ((1ull << (r + 1)) - 1ull));
-      if (w) return 64 + 63 - __builtin_clzll(w);
-      return occ0 ? 63 - __builtin_clzll(occ0) : -1;
-    }
-    const unsigned long long w = occ0 & ((x == 63) ? ~0ull : ((1ull << (x + 1)) - 1ull));
-    return w ? 63 - __builtin_clzll(w) : -1;
-  }
-};
-
-
-// LadderWin (k_match_hot, deep windows): one workgroup per hot symbol. The whole occupancy bitmap
-// and a window [wlo, wlo + W) of the ladder (levels + tail fills) around the best prices live in
-// LDS for the launch; levels outside the window stay in HBM. Every accessor branches on the
-// (wave-uniform) level, so top-of-book work never leaves the CU and deep rests cost one HBM
-// round trip as before. LDS pointers are address-space-3 (ds_* instructions: an LDS access never
-// waits on the wave's outstanding global stores, as a flat one would).
-template <class T>
-using lptr = T __attribute__((address_space(3)))*;
-template <class T>
-using gptr1 = T __attribute__((address_space(1)))*;
-
-// Level copies across address spaces go field by field (one 16-B access after merging).
-template <class P>
-__device__ __forceinline__ Level ld_level(P p) {
-  Level x;
-  x.total = p->total;
-  x.head = p->head;
-  x.tail = p->tail;
-  return x;
-}
-template <class P>
-__device__ __forceinline__ void st_level(P p, const Level& x) {
-  p->total = x.total;
-  p->head = x.head;
-  p->tail = x.tail;
+__device__ __forceinline__ void set_err(const BookDev& bk, uint32_t bits) {
+  if (lane_id() == 0) atomicOr(bk.err, bits);
 }
 
-struct LadderWin {
-  lptr<Level> wl;                 // LDS levels of the window
-  lptr<uint8_t> wt;               // LDS tail fills of the window
-  lptr<unsigned long long> occ;   // LDS occupancy of the whole ladder
-  gptr1<Level> glv;               // HBM ladder (authoritative outside the window)
-  gptr1<uint8_t> gtend;
-  uint32_t L, Lwords;
-  int wlo;
-  uint32_t W;
-
-  __device__ __forceinline__ bool inw(int l) const { return (uint32_t)(l - wlo) < W; }
-  __device__ __forceinline__ Level get(int l) const {
-    Level x;
-    if (inw(l)) {
-      x = ld_level(wl + (l - wlo));
-    } else {
-      x = ld_level(glv + l);
-    }
-    x.total = rli64(x.total, 0);
-    x.head = rl32(x.head, 0);
-    x.tail = rl32(x.tail, 0);
-    return x;
-  }
-  __device__ __forceinline__ uint32_t head(int l) const { return get(l).head; }
-  __device__ __forceinline__ void set(int l, const Level& x) {
-    if (lane_id() == 0) {
-      if (inw(l))
-        st_level(wl + (l - wlo), x);
-      else
-        st_level(glv + l, x);
-    }
-  }
-  __device__ __forceinline__ Level lane_get(int l, bool valid) const {
-    Level x{0, NIL, NIL};
-    if (valid) {
-      if (inw(l))
-        x = ld_level(wl + (l - wlo));
-      else
-        x = ld_level(glv + l);
-    }
-    return x;
-  }
-  __device__ __forceinline__ uint32_t get_te(int l) const {
-    if (inw(l)) return rl32((uint32_t)wt[l - wlo], 0);
-    return rl32((uint32_t)gtend[l], 0);
-  }
-  __device__ __forceinline__ void set_te(int l, uint32_t v) {
-    if (lane_id() == 0) {
-      if (inw(l))
-        wt[l - wlo] = (uint8_t)v;
-      else
-        gtend[l] = (uint8_t)v;
-    }
-  }
-  __device__ __forceinline__ void occ_set(int l) {
-    if (lane_id() == 0) occ[l >> 6] |= (1ull << (l & 63));
-  }
-  __device__ __forceinline__ void occ_clear(int l) {
-    if (lane_id() == 0) occ[l >> 6] &= ~(1ull << (l & 63));
-  }
-  // Smallest occupied level >= x, or L (64 bitmap words per step from LDS).
-  __device__ int next_occ(int x) const {
-    const int Li = (int)L;
-    if (x >= Li) return Li;
-    if (x < 0) x = 0;
-    const int w = x >> 6;
-    const unsigned long long word = occ[w] & (~0ull << (x & 63));
-    if (word) return (w << 6) + __builtin_ctzll(word);
-    const int lane = lane_id();
-    const int nw = (int)Lwords;
-    for (int b = w + 1; b < nw; b += 64) {
-      const int idx = b + lane;
-      const unsigned long long v = idx < nw ? occ[idx] : 0ull;
-      const unsigned long long m = __ballot(v != 0ull);
-      if (m) {
-        const int t = __builtin_ctzll(m);
-        return ((b + t) << 6) + __builtin_ctzll(rl64(v, t));
-      }
-    }
-    return Li;
-  }
-  // Largest occupied level <= x, or -1.
-  __device__ int prev_occ(int x) const {
-    if (x < 0) return -1;
-    if (x >= (int)L) x = (int)L - 1;
-    const int w = x >> 6;
-    const int r = x & 63;
-    const unsigned long long keep = (r == 63) ? ~0ull : ((1ull << (r + 1)) - 1ull);
-    const unsigned long long word = occ[w] & keep;
-    if (word) return (w << 6) + 63 - __builtin_clzll(word);
-    const int lane = lane_id();
-    for (int t0 = w - 1; t0 >= 0; t0 -= 64) {
-      const int idx = t0 - lane;
-      const unsigned long long v = idx >= 0 ? occ[idx] : 0ull;
-      const unsigned long long m = __ballot(v != 0ull);
-      if (m) {
-        const int t = __builtin_ctzll(m);
-        return ((t0 - t) << 6) + 63 - __builtin_clzll(rl64(v, t));
-      }
-    }
-    return -1;
-  }
-};
-
-template <class Lad>
 struct WaveCtx {
   BookDev bk;
-  Lad lad;
+  LadderMem lad;
   CacheEntry* cache;         // head-chunk cache in LDS, or nullptr (HBM ladder)
   uint32_t cmask;            // cache entry of level l = l & cmask
   uint32_t s;                // local symbol
   uint32_t gs;               // symbol id written in fills
   long long base;
-  int bb, ba;                // best bid / best ask level
+  int bb, ba;                // best bid / best ask level of the window
   uint32_t free_head;        // chunk free list of this symbol ...
   uint32_t free_next;        // ... and chdr[free_head].next, loaded ahead of the pop that needs it
   uint32_t bump_cur, bump_end;  // chunk ids reserved from the global bump allocator
@@ -515,62 +314,55 @@ struct WaveCtx {
   int resting_delta;
   unsigned long long wptr;   // next scratch slot of this wave
   me_fill* scratch;
+  uint32_t nfar0, nfar1;     // far-level counts (me_far.hpp)
+  unsigned long long horizon;  // seq-ring horizon of this launch
+  uint32_t epoch;            // old-order table epoch of this launch
 #ifdef ME_STAMPS
   unsigned long long st[PH_N];
   unsigned long long st_t;
 #endif
+  // far-level interface (me_far.hpp)
+  __device__ __forceinline__ gptr<Chunk> fchunks() const { return (gptr<Chunk>)bk.chunks; }
+  __device__ __forceinline__ uint32_t fnchunks() const { return bk.nchunks; }
+  __device__ __forceinline__ uint32_t fsym() const { return s; }
+  __device__ __forceinline__ uint32_t fgsym() const { return gs; }
+  __device__ __forceinline__ uint32_t fcap() const { return bk.fcap; }
+  __device__ __forceinline__ gptr<FarLevel> farr(uint32_t k) const { return (gptr<FarLevel>)far_of(bk, s, k); }
+  __device__ __forceinline__ uint32_t fcount(uint32_t k) const { return k ? nfar1 : nfar0; }
+  __device__ __forceinline__ void fset_count(uint32_t k, uint32_t n) {
+    if (k)
+      nfar1 = n;
+    else
+      nfar0 = n;
+  }
+  __device__ __forceinline__ void femit(bool fe, unsigned long long fm, const me_fill& F) {
+    if (fe) scratch[wptr + (unsigned long long)__popcll(fm & lanemask_lt())] = F;
+    wptr += (unsigned long long)__popcll(fm);
+  }
+  __device__ __forceinline__ void fresting(int d) { resting_delta += d; }
+  __device__ __forceinline__ void ferr(uint32_t bits) { set_err(bk, bits); }
+  __device__ __forceinline__ void floc(unsigned long long seq, uint32_t g) {
+    if (lane_id() == 0) bk.loc[seq & bk.ring_mask] = g;
+  }
+  __device__ __forceinline__ uint32_t falloc() { return alloc_chunk(*this); }
+  __device__ __forceinline__ void ffree(uint32_t ch) { free_chunk(*this, ch); }
 };
 
-__device__ __forceinline__ void set_err(const BookDev& bk, uint32_t bits) {
-  if (lane_id() == 0) atomicOr(bk.err, bits);
-}
-
 // ---- head-chunk cache -------------------------------------------------------------------
-// Generic ladders keep the entry's chunk id and dirty flag in LDS; the register ladder keeps
-// them as SGPR masks (valid bit l <=> entry l holds the current head chunk of level l), so a
-// lookup there is a bit test, never an LDS round trip.
-template <class C>
-constexpr bool kRegLadder = __is_same(decltype(C::lad), LadderReg);
+__device__ __forceinline__ CacheEntry* centry(const WaveCtx& c, int lvl) { return c.cache + ((uint32_t)lvl & c.cmask); }
 
-template <class C>
-__device__ __forceinline__ CacheEntry* centry(const C& c, int lvl) { return c.cache + ((uint32_t)lvl & c.cmask); }
-
-template <class C>
-__device__ __forceinline__ uint32_t head_of(const C& c, int lvl) {
-  if constexpr (kRegLadder<C>)
-    return lvl < 64 ? rl32(c.lad.h0, lvl & 63) : rl32(c.lad.h1, lvl & 63);
-  else
-    return c.lad.head(lvl);
+__device__ __forceinline__ bool cache_holds(const WaveCtx& c, int lvl, uint32_t ch) {
+  return c.cache && rl32(centry(c, lvl)->cid, 0) == ch;
 }
 
-template <class C>
-__device__ __forceinline__ bool cache_holds(const C& c, int lvl, uint32_t ch) {
-  if constexpr (kRegLadder<C>)
-    return LadderReg::bit_get(c.lad.cv0, c.lad.cv1, lvl) && head_of(c, lvl) == ch;
-  else
-    return c.cache && rl32(centry(c, lvl)->cid, 0) == ch;
+__device__ __forceinline__ void cache_mark_dirty(WaveCtx& c, int lvl) {
+  if (lane_id() == 0) centry(c, lvl)->dirty = 1;
 }
 
-template <class C>
-__device__ __forceinline__ void cache_mark_dirty(C& c, int lvl) {
-  if constexpr (kRegLadder<C>)
-    LadderReg::bit_set(c.lad.cd0, c.lad.cd1, lvl);
-  else if (lane_id() == 0)
-    centry(c, lvl)->dirty = 1;
-}
-
-// Write entry E of level lvl back to HBM if dirty. Register ladder: the caller passes the chunk
-// the (valid) entry holds; generic ladders read it from the entry.
-template <class C>
-__device__ __forceinline__ void cache_writeback(const C& c, int lvl, CacheEntry* E, uint32_t held = NIL) {
-  uint32_t cid;
-  if constexpr (kRegLadder<C>) {
-    if (!LadderReg::bit_get(c.lad.cv0, c.lad.cv1, lvl) || !LadderReg::bit_get(c.lad.cd0, c.lad.cd1, lvl)) return;
-    cid = held;
-  } else {
-    cid = rl32(E->cid, 0);
-    if (cid == NIL || !rl32(E->dirty, 0)) return;
-  }
+// Write entry E back to HBM if dirty.
+__device__ __forceinline__ void cache_writeback(const WaveCtx& c, CacheEntry* E) {
+  const uint32_t cid = rl32(E->cid, 0);
+  if (cid == NIL || !rl32(E->dirty, 0)) return;
   const int lane = lane_id();
   if (lane < ME_C) {
     const size_t g = (size_t)cid * ME_C + lane;
@@ -579,33 +371,20 @@ __device__ __forceinline__ void cache_writeback(const C& c, int lvl, CacheEntry*
   }
 }
 
-template <class C>
-__device__ __forceinline__ void cache_set_state(C& c, int lvl, CacheEntry* E, uint32_t ch, bool dirty) {
-  if constexpr (kRegLadder<C>) {
-    LadderReg::bit_set(c.lad.cv0, c.lad.cv1, lvl);
-    if (dirty)
-      LadderReg::bit_set(c.lad.cd0, c.lad.cd1, lvl);
-    else
-      LadderReg::bit_clr(c.lad.cd0, c.lad.cd1, lvl);
-    if (lane_id() == 0) E->cid = ch;
-  } else if (lane_id() == 0) {
+__device__ __forceinline__ void cache_set_state(WaveCtx& c, CacheEntry* E, uint32_t ch, bool dirty) {
+  if (lane_id() == 0) {
     E->cid = ch;
     E->dirty = dirty ? 1u : 0u;
   }
 }
 
 // Make `ch` (the head chunk of level lvl) the cached chunk of its entry; returns the entry.
-template <class C>
-__device__ __forceinline__ CacheEntry* cache_get(C& c, int lvl, uint32_t ch) {
+__device__ __forceinline__ CacheEntry* cache_get(WaveCtx& c, int lvl, uint32_t ch) {
   CacheEntry* E = centry(c, lvl);
-  if constexpr (kRegLadder<C>) {
-    if (LadderReg::bit_get(c.lad.cv0, c.lad.cv1, lvl)) return E;  // valid => holds the head
-  } else {
-    const uint32_t cur = rl32(E->cid, 0);
-    if (cur == ch) return E;
-    if (cur != NIL) COUNT(c, CT_EVICT);
-    cache_writeback(c, lvl, E);
-  }
+  const uint32_t cur = rl32(E->cid, 0);
+  if (cur == ch) return E;
+  if (cur != NIL) COUNT(c, CT_EVICT);
+  cache_writeback(c, E);
   COUNT(c, CT_MISS);
   const int lane = lane_id();
   const bool act = lane < ME_C;
@@ -618,75 +397,74 @@ __device__ __forceinline__ CacheEntry* cache_get(C& c, int lvl, uint32_t ch) {
     E->seq[lane] = sq;
   }
   if (lane == 0) E->next = nx;
-  cache_set_state(c, lvl, E, ch, false);
+  cache_set_state(c, E, ch, false);
   return E;
 }
 
 // A brand-new (all-empty) chunk becomes the head of an empty level: install it without a load.
-template <class C>
-__device__ __forceinline__ void cache_install_new(C& c, int lvl, uint32_t ch) {
+__device__ __forceinline__ void cache_install_new(WaveCtx& c, int lvl, uint32_t ch) {
   CacheEntry* E = centry(c, lvl);
-  if constexpr (!kRegLadder<C>) cache_writeback(c, lvl, E);  // register ladder: entry of an empty level is invalid
+  cache_writeback(c, E);
   const int lane = lane_id();
   if (lane < ME_C) {
     E->qty[lane] = 0;
     E->seq[lane] = 0ull;
   }
   if (lane == 0) E->next = NIL;
-  cache_set_state(c, lvl, E, ch, true);
+  cache_set_state(c, E, ch, true);
 }
 
 // The cached chunk ch of lvl is being freed or unlinked: HBM must hold its final (all-zero)
-// quantities before the chunk is reused. Callers pass the chunk the entry holds (the level's
-// head, or the chunk a walk just loaded); generic ladders double-check the id.
-template <class C>
-__device__ __forceinline__ void cache_drop(C& c, int lvl, uint32_t ch) {
+// quantities before the chunk is reused.
+__device__ __forceinline__ void cache_drop(WaveCtx& c, int lvl, uint32_t ch) {
   if (!c.cache) return;
   CacheEntry* E = centry(c, lvl);
-  if constexpr (kRegLadder<C>) {
-    if (!LadderReg::bit_get(c.lad.cv0, c.lad.cv1, lvl)) return;
-  } else {
-    if (rl32(E->cid, 0) != ch) return;
-  }
-  cache_writeback(c, lvl, E, ch);
-  if constexpr (kRegLadder<C>) {
-    LadderReg::bit_clr(c.lad.cv0, c.lad.cv1, lvl);
-    LadderReg::bit_clr(c.lad.cd0, c.lad.cd1, lvl);
-  } else if (lane_id() == 0) {
-    E->cid = NIL;
-  }
+  if (rl32(E->cid, 0) != ch) return;
+  cache_writeback(c, E);
+  if (lane_id() == 0) E->cid = NIL;
 }
 
 // chdr[ch].next = v, mirrored into the cache entry of lvl when it holds ch.
-template <class C>
-__device__ __forceinline__ void set_next(C& c, int lvl, uint32_t ch, uint32_t v) {
-  const bool mirror = c.cache && cache_holds(c, lvl, ch);
+__device__ __forceinline__ void set_next(WaveCtx& c, int lvl, uint32_t ch, uint32_t v) {
+  const bool mirror = cache_holds(c, lvl, ch);
   if (lane_id() == 0) {
     c.bk.chunks[ch].hdr.next = v;
     if (mirror) centry(c, lvl)->next = v;
   }
 }
 
-// ---- chunk allocation -------------------------------------------------------------------
-// Free-list push: the popped-next is known without a load.
-template <class C>
-__device__ __forceinline__ void free_chunk(C& c, uint32_t ch) {
-  if (lane_id() == 0) c.bk.chunks[ch].hdr.next = c.free_head;
-  c.free_next = c.free_head;
-  c.free_head = ch;
+// Dirty cached head chunks back to HBM: lane = (entry, slot) pairs, 4 entries per pass.
+__device__ __forceinline__ void cache_flush_all(WaveCtx& c, uint32_t entries) {
+  const int lane = lane_id();
+  wave_mem_order();
+  for (uint32_t e0 = 0; e0 < entries; e0 += 64 / ME_C) {
+    const uint32_t e = e0 + lane / ME_C, sl = lane % ME_C;
+    const CacheEntry* E = c.cache + e;
+    const uint32_t cid = E->cid;
+    if (cid != NIL && E->dirty) {
+      cq_at(c.bk.chunks, (size_t)cid * ME_C + sl) = E->qty[sl];
+      cs_at(c.bk.chunks, (size_t)cid * ME_C + sl) = E->seq[sl];
+    }
+  }
 }
 
+// ---- chunk allocation -------------------------------------------------------------------
 // Issue the load of chdr[free_head].next without waiting for it: the value stays in a VGPR and is
 // only read (readlane -> s_waitcnt) by the next pop, usually many records later.
-template <class C>
-__device__ __forceinline__ void prefetch_free_next(C& c) {
+__device__ __forceinline__ void prefetch_free_next(WaveCtx& c) {
   const bool ok = c.free_head < c.bk.nchunks;
   const uint32_t v = c.bk.chunks[ok ? c.free_head : 0].hdr.next;
   c.free_next = ok ? v : NIL;
 }
 
-template <class C>
-__device__ __forceinline__ uint32_t alloc_chunk(C& c) {
+// Free-list push: the popped-next is known without a load.
+__device__ __forceinline__ void free_chunk(WaveCtx& c, uint32_t ch) {
+  if (lane_id() == 0) c.bk.chunks[ch].hdr.next = c.free_head;
+  c.free_next = c.free_head;
+  c.free_head = ch;
+}
+
+__device__ __forceinline__ uint32_t alloc_chunk(WaveCtx& c) {
   if (c.free_head != NIL) {
     const uint32_t ch = c.free_head;
     if (ch >= c.bk.nchunks) {
@@ -714,8 +492,7 @@ __device__ __forceinline__ uint32_t alloc_chunk(C& c) {
 }
 
 // Append one fill per lane where e holds, in lane order, to the wave's scratch run.
-template <class C>
-__device__ __forceinline__ void emit_fills(C& c, bool e, unsigned long long taker, unsigned long long maker,
+__device__ __forceinline__ void emit_fills(WaveCtx& c, bool e, unsigned long long taker, unsigned long long maker,
                                            long long price, int qty) {
   unsigned long long m = __ballot(e);
   if (e) {
@@ -731,14 +508,13 @@ __device__ __forceinline__ void emit_fills(C& c, bool e, unsigned long long take
   c.wptr += (unsigned long long)__popcll(m);
 }
 
-// Consume `take` (> 0, <= level total) from the FIFO of level `lvl`, oldest first. A slot is
+// Consume `take` (> 0, <= level total) from the FIFO of window level `lvl`, oldest first. A slot is
 // live iff its qty > 0 (consumed, cancelled and unwritten slots hold 0). A chunk's 16 slots are
 // ranked with one wave prefix scan; with the cache they come from LDS, otherwise one HBM round
 // trip loads header and slots together. Exhausted chunks go back to the free list. Returns the
 // new head chunk (NIL: level emptied).
-template <class C>
-__device__ __forceinline__ uint32_t walk_level(C& c, int lvl, long long take, uint32_t head, uint32_t tail,
-                               unsigned long long taker) {
+__device__ __forceinline__ uint32_t walk_level(WaveCtx& c, int lvl, long long take, uint32_t head, uint32_t tail,
+                                               unsigned long long taker) {
   const int lane = lane_id();
   const BookDev& bk = c.bk;
   const long long price = c.base + lvl;
@@ -807,8 +583,7 @@ __device__ __forceinline__ uint32_t walk_level(C& c, int lvl, long long take, ui
 }
 
 // Write back level lvl after `take` was consumed from it.
-template <class C>
-__device__ __forceinline__ void level_after_take(C& c, int lvl, long long ntot, uint32_t nh, uint32_t tail) {
+__device__ __forceinline__ void level_after_take(WaveCtx& c, int lvl, long long ntot, uint32_t nh, uint32_t tail) {
   Level o;
   o.total = ntot;
   o.head = ntot ? nh : NIL;
@@ -818,8 +593,7 @@ __device__ __forceinline__ void level_after_take(C& c, int lvl, long long ntot, 
 }
 
 // Consume `take` at level lvl whose header is (tot, head, tail); returns true if it emptied.
-template <class C>
-__device__ __forceinline__ bool take_level(C& c, int lvl, long long tot, long long take, uint32_t head,
+__device__ __forceinline__ bool take_level(WaveCtx& c, int lvl, long long tot, long long take, uint32_t head,
                                            uint32_t tail, unsigned long long taker) {
   STAMP_ADD(c, PH_SWEEP);
   const uint32_t nh = walk_level(c, lvl, take, head, tail, taker);
@@ -829,19 +603,16 @@ __device__ __forceinline__ bool take_level(C& c, int lvl, long long tot, long lo
   return tot == take;
 }
 
-// Sweep the opposite side for a taker. dir = +1 (BUY: asks upward from best_ask) or -1 (SELL:
-// bids downward from best_bid); lim = last level the taker may trade at. Returns qty filled.
-// LadderMem: 64-level windows — lanes load consecutive levels, an inclusive scan of their totals
-// says how far the taker reaches. LadderReg: one masked scan over the register-resident ladder.
-template <class C>
-__device__ __forceinline__ long long sweep(C& c, int dir, int lim, long long want, unsigned long long taker, uint32_t& nfill) {
+// Sweep the opposite side of the window for a taker. dir = +1 (BUY: asks upward from best_ask) or
+// -1 (SELL: bids downward from best_bid); lim = last window level the taker may trade at (-1 / L:
+// none). 64-level windows: lanes load consecutive levels, an inclusive scan of their totals says how
+// far the taker reaches. Returns qty filled.
+__device__ __forceinline__ long long sweep(WaveCtx& c, int dir, int lim, long long want, unsigned long long taker) {
   const int lane = lane_id();
   const int L = (int)c.bk.L;
   long long rem = want;
   int cur = (dir > 0) ? c.ba : c.bb;
   bool emptied = false;
-  const unsigned long long w_start = c.wptr;
-  nfill = 0;
   if (dir > 0 ? (cur > lim || cur >= L) : (cur < lim || cur < 0)) return 0;  // does not cross
   // fast path: the best level alone fills the taker (no scan)
   {
@@ -855,58 +626,42 @@ __device__ __forceinline__ long long sweep(C& c, int dir, int lim, long long wan
           c.bb = c.lad.prev_occ(cur - 1);
         STAMP_ADD(c, PH_SW_BEST);
       }
-      nfill = (uint32_t)(c.wptr - w_start);
       return want;
     }
   }
-  if constexpr (kRegLadder<C>) {
-    // level by level from the best: the occupancy bit scan finds the next level in SALU, the
-    // level header is a readlane — no scan, no memory round trip
-    while (rem > 0 && (dir > 0 ? (cur <= lim && cur < L) : (cur >= lim && cur >= 0))) {
-      const Level B = c.lad.get(cur);
-      const long long take = B.total < rem ? B.total : rem;
-      const bool gone = take_level(c, cur, B.total, take, B.head, B.tail, taker);
+  while (rem > 0) {
+    if (dir > 0 ? (cur > lim || cur >= L) : (cur < lim || cur < 0)) break;
+    const int lv = cur + dir * lane;
+    const bool valid = (dir > 0) ? (lv <= lim && lv < L) : (lv >= lim && lv >= 0);
+    const Level W = c.lad.lane_get(lv, valid);
+    const long long tot = W.total;
+    const long long inc = wave_incl_scan(tot);
+    const long long ex = inc - tot;
+    const long long rem0 = rem;
+    unsigned long long tm = __ballot(valid && tot > 0 && ex < rem0);
+    STAMP_ADD(c, PH_SW_WINDOW);
+    while (tm) {
+      const int t = __builtin_ctzll(tm);
+      tm &= tm - 1;
+      const int lvl = cur + dir * t;
+      const long long ltot = rli64(tot, t);
+      const long long lex = rli64(ex, t);
+      long long take = rem0 - lex;
+      if (take > ltot) take = ltot;
+      emptied |= take_level(c, lvl, ltot, take, rl32(W.head, t), rl32(W.tail, t), taker);
       rem -= take;
-      if (!gone) break;  // partially consumed: the taker is done
-      emptied = true;
-      cur = dir > 0 ? c.lad.next_occ(cur + 1) : c.lad.prev_occ(cur - 1);
-      STAMP_ADD(c, PH_SW_JUMP);
     }
-  } else {
-    while (rem > 0) {
-      if (dir > 0 ? (cur > lim || cur >= L) : (cur < lim || cur < 0)) break;
-      const int lv = cur + dir * lane;
-      const bool valid = (dir > 0) ? (lv <= lim && lv < L) : (lv >= lim && lv >= 0);
-      const Level W = c.lad.lane_get(lv, valid);
-      const long long tot = W.total;
-      const long long inc = wave_incl_scan(tot);
-      const long long ex = inc - tot;
-      const long long rem0 = rem;
-      unsigned long long tm = __ballot(valid && tot > 0 && ex < rem0);
-      STAMP_ADD(c, PH_SW_WINDOW);
-      while (tm) {
-        const int t = __builtin_ctzll(tm);
-        tm &= tm - 1;
-        const int lvl = cur + dir * t;
-        const long long ltot = rli64(tot, t);
-        const long long lex = rli64(ex, t);
-        long long take = rem0 - lex;
-        if (take > ltot) take = ltot;
-        emptied |= take_level(c, lvl, ltot, take, rl32(W.head, t), rl32(W.tail, t), taker);
-        rem -= take;
-      }
-      if (rem == 0) break;
-      // every valid level of this window is now empty; jump to the next occupied one
-      const int nxt = cur + dir * 64;
-      if (dir > 0) {
-        if (nxt > lim) break;
-        cur = c.lad.next_occ(nxt);
-      } else {
-        if (nxt < lim) break;
-        cur = c.lad.prev_occ(nxt);
-      }
-      STAMP_ADD(c, PH_SW_JUMP);
+    if (rem == 0) break;
+    // every valid level of this window is now empty; jump to the next occupied one
+    const int nxt = cur + dir * 64;
+    if (dir > 0) {
+      if (nxt > lim) break;
+      cur = c.lad.next_occ(nxt);
+    } else {
+      if (nxt < lim) break;
+      cur = c.lad.prev_occ(nxt);
     }
+    STAMP_ADD(c, PH_SW_JUMP);
   }
   if (emptied) {
     if (dir > 0)
@@ -915,14 +670,12 @@ __device__ __forceinline__ long long sweep(C& c, int dir, int lim, long long wan
       c.bb = c.lad.prev_occ(c.bb);
     STAMP_ADD(c, PH_SW_BEST);
   }
-  nfill = (uint32_t)(c.wptr - w_start);
   return want - rem;
 }
 
-// Append a resting order at the tail of level lvl's FIFO. The tail fill count lives beside the
-// level, so the common case issues no HBM load; a tail that is the cached head is written on chip.
-template <class C>
-__device__ __forceinline__ bool rest_order(C& c, int lvl, unsigned long long seq, int qty, bool buy) {
+// Append a resting order at the tail of window level lvl's FIFO. The tail fill count lives beside
+// the level, so the common case issues no HBM load; a tail that is the cached head is written on chip.
+__device__ __forceinline__ bool rest_order(WaveCtx& c, int lvl, unsigned long long seq, int qty, bool buy) {
   const int lane = lane_id();
   const BookDev& bk = c.bk;
   Level L = c.lad.get(lvl);
@@ -941,9 +694,10 @@ __device__ __forceinline__ bool rest_order(C& c, int lvl, unsigned long long seq
       ChunkHdr h;
       h.next = NIL;
       h.prev = L.tail;
-      h.level = (uint32_t)lvl;
       h.owner = c.s;
+      h.pad = 0;
       bk.chunks[ch].hdr = h;
+      bk.chunks[ch].price = c.base + lvl;
     }
     if (L.tail != NIL) set_next(c, lvl, L.tail, ch);
     if (L.tail == NIL) {
@@ -972,8 +726,8 @@ __device__ __forceinline__ bool rest_order(C& c, int lvl, unsigned long long seq
       cs_at(bk.chunks, g) = seq;
       cq_at(bk.chunks, g) = qty;
     }
-    if (seq < bk.max_seq) bk.loc[seq] = (uint32_t)g;
   }
+  c.floc(seq, (uint32_t)g);
   c.lad.set(lvl, L);
   c.lad.set_te(lvl, slot + 1);
   if (was_empty) c.lad.occ_set(lvl);
@@ -986,53 +740,27 @@ __device__ __forceinline__ bool rest_order(C& c, int lvl, unsigned long long seq
   return true;
 }
 
-// Cancel the live resting order `tgt` of this symbol. Returns the removed qty, 0 if not live.
-// A chunk left without live orders is unlinked from its FIFO at once (so chunks in use never
-// exceed resting orders); a level left empty returns its whole FIFO to the free list.
-template <class C>
-__device__ __forceinline__ int cancel_order(C& c, unsigned long long tgt) {
+// Cancel the window order in slot `slot` of chunk ch (level lvl, quantity q, the chunk's live
+// quantities qv, FIFO links nxt / prv). A chunk left without live orders is unlinked from its FIFO
+// at once (so chunks in use never exceed resting orders); a level left empty returns its whole FIFO
+// to the free list.
+__device__ __forceinline__ void cancel_window(WaveCtx& c, int lvl, uint32_t ch, uint32_t slot, int q, int qv,
+                                              uint32_t nxt, uint32_t prv, CacheEntry* E) {
   const BookDev& bk = c.bk;
   const int lane = lane_id();
-  if (tgt == 0ull || tgt >= bk.max_seq) return 0;
-  wave_mem_order();
-  const uint32_t g = rl32(bk.loc[tgt], 0);
-  if (g == NIL) return 0;
-  const uint32_t ch = g / ME_C, slot = g % ME_C;
-  if (ch >= bk.nchunks) return 0;
-  // one round trip: owner, header, the whole chunk's quantities and the target seq
-  const uint32_t owner = rl32(bk.chunks[ch].hdr.owner, 0);
-  const ChunkHdr hd = bk.chunks[ch].hdr;
-  const bool act = lane < ME_C;
-  int qv = act ? cq_at(bk.chunks, (size_t)ch * ME_C + lane) : 0;
-  unsigned long long sq = rl64(cs_at(bk.chunks, g), 0);
-  if (owner != c.s) return 0;  // another symbol's order: never touch its book
-  const int lvl = (int)rl32(hd.level, 0);
-  if (lvl < 0 || lvl >= (int)bk.L) {
-    set_err(bk, ERR_INCONSISTENT);
-    return 0;
-  }
-  CacheEntry* E = cache_holds(c, lvl, ch) ? centry(c, lvl) : nullptr;
-  if (E) {  // the on-chip copy is authoritative
-    qv = act ? E->qty[lane] : 0;
-    sq = rl64(E->seq[slot], 0);
-  }
-  const int q = rli32(qv, (int)slot);
-  if (sq != tgt || q <= 0) return 0;
-  const uint32_t nxt = rl32(hd.next, 0), prv = rl32(hd.prev, 0);
   const uint32_t live_after = (uint32_t)__popcll(__ballot(qv > 0)) - 1;
   Level L = c.lad.get(lvl);
   L.total -= q;
   if (L.tail >= bk.nchunks || L.head >= bk.nchunks) {
     set_err(bk, ERR_INCONSISTENT);
-    return q;
+    return;
   }
   if (E) cache_mark_dirty(c, lvl);
   if (lane == 0) {
-    if (E) {
+    if (E)
       E->qty[slot] = 0;
-    } else {
-      cq_at(bk.chunks, g) = 0;
-    }
+    else
+      cq_at(bk.chunks, (size_t)ch * ME_C + slot) = 0;
   }
   wave_mem_order();
   if (L.total == 0) {
@@ -1071,7 +799,183 @@ __device__ __forceinline__ int cancel_order(C& c, unsigned long long tgt) {
     c.lad.set(lvl, L);
   }
   c.resting_delta -= 1;
-  return q;
+}
+
+// Cancel the live resting order `tgt` of this symbol. Returns the removed qty, 0 if not live. The
+// seq ring names its slot unless a later seq overwrote the entry, in which case an order older than
+// the horizon is in the old-order table; every candidate slot is verified (owner, seq, qty > 0).
+__device__ __forceinline__ int cancel_order(WaveCtx& c, unsigned long long tgt) {
+  const BookDev& bk = c.bk;
+  const int lane = lane_id();
+  const bool act = lane < ME_C;
+  if (tgt == 0ull) return 0;
+  wave_mem_order();
+  uint32_t g = rl32(bk.loc[tgt & bk.ring_mask], 0);
+  for (int pass = 0;; ++pass) {
+    if (g != NIL && g / ME_C < bk.nchunks) {
+      const uint32_t ch = g / ME_C, slot = g % ME_C;
+      // one round trip: header, price, the whole chunk's quantities and the target seq
+      const ChunkHdr hd = bk.chunks[ch].hdr;
+      const long long price = rli64(bk.chunks[ch].price, 0);
+      int qv = act ? cq_at(bk.chunks, (size_t)ch * ME_C + lane) : 0;
+      unsigned long long sq = rl64(cs_at(bk.chunks, g), 0);
+      const uint32_t owner = rl32(hd.owner, 0);
+      const long long lv64 = price - c.base;
+      const bool inw = owner == c.s && (unsigned long long)lv64 < (unsigned long long)bk.L;
+      const int lvl = inw ? (int)lv64 : 0;
+      CacheEntry* E = inw && cache_holds(c, lvl, ch) ? centry(c, lvl) : nullptr;
+      if (E) {  // the on-chip copy is authoritative
+        qv = act ? E->qty[lane] : 0;
+        sq = rl64(E->seq[slot], 0);
+      }
+      if (owner == c.s && sq == tgt) {  // the order's slot: live or dead, it never moves
+        const int q = rli32(qv, (int)slot);
+        if (q <= 0) return 0;
+        const uint32_t nxt = rl32(hd.next, 0), prv = rl32(hd.prev, 0);
+        if (!inw) return (int)far_cancel(c, price < c.base ? 0u : 1u, price, ch, slot, q, qv, nxt, prv);
+        cancel_window(c, lvl, ch, slot, q, qv, nxt, prv, E);
+        return q;
+      }
+    }
+    // the ring entry is someone else's: only an order older than the horizon can still be live
+    if (pass != 0 || tgt >= c.horizon) return 0;
+    g = old_lookup((gptr<const OldEnt>)bk.old, bk.old_mask, c.epoch, tgt);
+    if (g == NIL) return 0;
+  }
+}
+
+// ---- re-centring the window (rare) ---------------------------------------------------------
+// Shift the window arrays by d (level j <- level j + d, empty outside), one 64-level block per step;
+// every block is exactly one occupancy word, rebuilt from the shifted totals. Ascending blocks for
+// d > 0 and descending for d < 0, so no block reads what an earlier one wrote.
+__device__ __forceinline__ void lad_shift(WaveCtx& c, int d) {
+  const int lane = lane_id();
+  const int L = (int)c.lad.L;
+  wave_mem_order();
+  for (int k = 0; k < L; k += 64) {
+    const int j0 = d > 0 ? k : L - 64 - k;
+    const int j = j0 + lane, src = j + d;
+    const bool in = src >= 0 && src < L;
+    Level v{0, NIL, NIL};
+    uint32_t t = 0;
+    if (in) {
+      v = c.lad.lv[src];
+      t = c.lad.tend[src];
+    }
+    const unsigned long long w = __ballot(v.total > 0);
+    c.lad.lv[j] = v;
+    c.lad.tend[j] = (uint8_t)t;
+    if (lane == 0) c.lad.occ[j0 >> 6] = w;
+  }
+  wave_mem_order();
+}
+
+// Move the window so that it is centred on `target` as far as invariant I allows (me_far.hpp):
+// cached heads go back to HBM and the cache is cleared (it is indexed by level), levels leaving the
+// window become far levels at the best end of their side, the window arrays shift, and far levels
+// now inside it are installed. Chunks name their level by price, so none of them changes.
+__device__ void lad_recentre(WaveCtx& c, long long target) {
+  const int lane = lane_id();
+  const uint32_t L = c.lad.L;
+  const long long base = c.base;
+  const bool wb = c.bb >= 0, wa = c.ba < (int)L;
+  long long bbp = 0, bap = 0;
+  if (wb)
+    bbp = base + c.bb;
+  else if (c.nfar0)
+    bbp = far_get(c.farr(0), c.nfar0 - 1u).price;
+  if (wa)
+    bap = base + c.ba;
+  else if (c.nfar1)
+    bap = far_get(c.farr(1), c.nfar1 - 1u).price;
+  const long long nb = recentre_base(target, L, wb || c.nfar0 != 0u, bbp, wa || c.nfar1 != 0u, bap);
+  if (nb == base) return;
+  const bool up = nb > base;
+  const unsigned long long dist =
+      up ? (unsigned long long)nb - (unsigned long long)base : (unsigned long long)base - (unsigned long long)nb;
+  const int dm = dist >= L ? (int)L : (int)dist;
+  const int d = up ? dm : -dm;
+  if (c.cache) {
+    cache_flush_all(c, CK_MEM);
+    for (uint32_t i = lane; i < (uint32_t)CK_MEM; i += 64) c.cache[i].cid = NIL;
+    wave_mem_order();
+  }
+  if (d > 0) {  // bids leave at the bottom
+    for (int l = c.lad.next_occ(0); l < d; l = c.lad.next_occ(l + 1)) {
+      if (l > c.bb) set_err(c.bk, ERR_INCONSISTENT);
+      const Level x = c.lad.get(l);
+      FarLevel e;
+      e.price = base + l;
+      e.total = x.total;
+      e.head = x.head;
+      e.tail = x.tail;
+      e.tend = c.lad.get_te(l);
+      e.pad = 0;
+      far_push(c, 0u, e);
+    }
+  } else {  // asks leave at the top
+    for (int l = c.lad.prev_occ((int)L - 1); l >= (int)L + d; l = c.lad.prev_occ(l - 1)) {
+      if (l < c.ba) set_err(c.bk, ERR_INCONSISTENT);
+      const Level x = c.lad.get(l);
+      FarLevel e;
+      e.price = base + l;
+      e.total = x.total;
+      e.head = x.head;
+      e.tail = x.tail;
+      e.tend = c.lad.get_te(l);
+      e.pad = 0;
+      far_push(c, 1u, e);
+    }
+  }
+  lad_shift(c, d);
+  int nbb = (c.bb >= 0 && c.bb - d >= 0) ? c.bb - d : -1;
+  int nba = (c.ba < (int)L && c.ba - d < (int)L) ? c.ba - d : (int)L;
+  c.base = nb;
+  const uint32_t k = d < 0 ? 0u : 1u;  // the side whose far levels may now be inside the window
+  const gptr<FarLevel> a = c.farr(k);
+  uint32_t n = c.fcount(k);
+  while (n) {
+    const FarLevel e = far_get(a, n - 1u);
+    const unsigned long long off = (unsigned long long)e.price - (unsigned long long)nb;
+    if (k == 0 ? e.price < nb : off >= L) break;
+    if (off >= L) {  // impossible by recentre_base: never write outside the window
+      set_err(c.bk, ERR_INCONSISTENT);
+      break;
+    }
+    const int j = (int)off;
+    Level x;
+    x.total = e.total;
+    x.head = e.head;
+    x.tail = e.tail;
+    c.lad.set(j, x);
+    c.lad.set_te(j, e.tend);
+    c.lad.occ_set(j);
+    if (k == 0)
+      nbb = j > nbb ? j : nbb;
+    else
+      nba = j < nba ? j : nba;
+    --n;
+  }
+  c.fset_count(k, n);
+  c.bb = nbb;
+  c.ba = nba;
+  wave_mem_order();
+}
+
+// Rest (seq, qty) at price p outside the window: re-centre first when the rest would put a bid above
+// the window or an ask below it (invariant I) or when the window is empty; then a window or far rest.
+__device__ bool far_or_window_rest(WaveCtx& c, long long p, unsigned long long seq, int qty, bool buy) {
+  const uint32_t L = c.lad.L;
+  const bool above = p > c.base;  // p is outside [base, base + L)
+  const bool mandatory = buy == above;
+  if (mandatory || (c.bb < 0 && c.ba >= (int)L)) lad_recentre(c, p);
+  const unsigned long long off = (unsigned long long)p - (unsigned long long)c.base;
+  if (off < L) return rest_order(c, (int)off, seq, qty, buy);
+  if (mandatory) {
+    set_err(c.bk, ERR_INCONSISTENT);
+    return false;
+  }
+  return far_rest(c, p < c.base ? 0u : 1u, p, seq, (uint32_t)qty);
 }
 
 // Per-record results are collected in lane k for record k of the current 64-record block and
@@ -1113,17 +1017,14 @@ __host__ __device__ constexpr size_t lds_ladder_bytes(uint32_t L) {
 __host__ __device__ constexpr size_t lds_wave_bytes(uint32_t L) {
   return lds_ladder_bytes(L) + CK_MEM * sizeof(CacheEntry);
 }
-__host__ __device__ constexpr size_t lds_wave_bytes_reg() { return CK_REG * sizeof(CacheEntry); }
 
-// Ladder placement of a k_match instantiation.
-enum LadderKind { LAD_HBM = 0, LAD_LDS = 1, LAD_REG = 2 };
+// Window placement of a k_match instantiation.
+enum LadderKind { LAD_HBM = 0, LAD_LDS = 1 };
 
-// The per-record loop of one symbol, shared by every ladder kind.
-template <class C>
-__device__ __forceinline__ void match_records(C& c, const BatchDev& bt, uint32_t lo, uint32_t hi) {
+// The per-record loop of one symbol.
+__device__ __forceinline__ void match_records(WaveCtx& c, const BatchDev& bt, uint32_t lo, uint32_t hi) {
   const int lane = lane_id();
-  const BookDev& bk = c.bk;
-  const long long Lw = (long long)bk.L;
+  const uint32_t Lw = c.bk.L;
   bool ok = true;
   for (uint32_t blk = lo; blk < hi && ok; blk += 64) {
     const uint32_t j = blk + (uint32_t)lane;
@@ -1166,33 +1067,36 @@ __device__ __forceinline__ void match_records(C& c, const BatchDev& bt, uint32_t
         put_result(R, k, 0, q, 0, ME_ST_REJECTED, ME_RJ_BAD_SIDE, fstart);
         continue;
       }
-      int li = 0;
-      if (!market) {
-        if (px < c.base || (unsigned long long)px - (unsigned long long)c.base >= (unsigned long long)Lw) {
-          put_result(R, k, 0, q, 0, ME_ST_REJECTED, ME_RJ_OUT_OF_WINDOW, fstart);
-          continue;
-        }
-        li = (int)(px - c.base);
-      }
-      if (seq == 0ull || seq >= bk.max_seq) {
+      if (seq == 0ull) {  // no OID is 0 (the counter starts at 1, storage.cpp:254-267)
         put_result(R, k, 0, q, 0, ME_ST_REJECTED, ME_RJ_BAD_SEQ, fstart);
         continue;
       }
       const bool buy = side == ME_SIDE_BUY;
-      const int lim = market ? (buy ? (int)Lw - 1 : 0) : li;
-      uint32_t nfill = 0;
-      const long long got = sweep(c, buy ? 1 : -1, lim, (long long)q, seq, nfill);
+      const unsigned long long off = (unsigned long long)px - (unsigned long long)c.base;
+      const bool inw = off < (unsigned long long)Lw;
+      const bool above = !inw && px > c.base;
+      // last window level the taker may trade at (-1 / L: none) and whether it reaches past the window
+      const int lim = market ? (buy ? (int)Lw - 1 : 0)
+                    : inw    ? (int)off
+                    : buy    ? (above ? (int)Lw - 1 : -1)
+                             : (above ? (int)Lw : 0);
+      const bool far = market || (buy ? above : (!inw && !above));
+      long long got = sweep(c, buy ? 1 : -1, lim, (long long)q, seq);
+      if (got < q && far && c.fcount(buy ? 1u : 0u) != 0u)
+        got += far_take(c, buy, market, px, (uint32_t)(q - got), seq);
       STAMP_ADD(c, PH_SWEEP);
+      const uint32_t nfill = (uint32_t)(c.wptr - fstart);
       const int filled = (int)got;
       const int rem = q - filled;
       uint8_t stt;
       if (market) {
         stt = rem == 0 ? ME_ST_FILLED : ME_ST_CANCELED;
       } else {
-        const bool failed = rem > 0 && !rest_order(c, li, seq, rem, buy);
+        const bool failed = rem > 0 && !(inw ? rest_order(c, (int)off, seq, rem, buy)
+                                             : far_or_window_rest(c, px, seq, rem, buy));
         STAMP_ADD(c, PH_REST);
         if (failed) {
-          ok = false;  // chunk pool exhausted: the batch fails (sticky error word)
+          ok = false;  // a pool is exhausted: the batch fails (sticky error word)
           break;
         }
         stt = rem == 0 ? ME_ST_FILLED : (filled > 0 ? ME_ST_PARTIALLY_FILLED : ME_ST_NEW);
@@ -1206,33 +1110,22 @@ __device__ __forceinline__ void match_records(C& c, const BatchDev& bt, uint32_t
   while (c.bump_cur < c.bump_end) free_chunk(c, c.bump_cur++);
 }
 
-// Dirty cached head chunks back to HBM: lane = (entry, slot) pairs, 4 entries per pass.
-template <class C>
-__device__ __forceinline__ void cache_flush_all(C& c, uint32_t entries) {
-  const int lane = lane_id();
-  wave_mem_order();
-  for (uint32_t e0 = 0; e0 < entries; e0 += 64 / ME_C) {
-    const uint32_t e = e0 + lane / ME_C, sl = lane % ME_C;
-    const CacheEntry* E = c.cache + e;
-    const uint32_t cid = E->cid;
-    if (cid != NIL && E->dirty) {
-      cq_at(c.bk.chunks, (size_t)cid * ME_C + sl) = E->qty[sl];
-      cs_at(c.bk.chunks, (size_t)cid * ME_C + sl) = E->seq[sl];
-    }
-  }
-}
-
-template <class C>
-__device__ __forceinline__ bool wave_begin(C& c, const BookDev& bk, const BatchDev& bt, uint32_t s, uint32_t lo, uint32_t hi) {
+__device__ __forceinline__ bool wave_begin(WaveCtx& c, const BookDev& bk, const BatchDev& bt, uint32_t s, uint32_t lo,
+                                           uint32_t hi) {
   const int lane = lane_id();
   c.bk = bk;
   c.s = s;
   c.gs = bk.gsym ? bk.gsym[s] : s;
   const SymState st = bk.sym[s];
+  const SeqState sqs = bk.sq[bk.sq_idx];
   c.base = rli64(st.base, 0);
   c.bb = rli32(st.best_bid, 0);
   c.ba = rli32(st.best_ask, 0);
   c.free_head = rl32(st.free_head, 0);
+  c.nfar0 = rl32(st.nfar[0], 0);
+  c.nfar1 = rl32(st.nfar[1], 0);
+  c.horizon = rl64(sqs.horizon, 0);
+  c.epoch = rl32(sqs.epoch, 0);
   prefetch_free_next(c);
   c.bump_cur = c.bump_end = 0;
   c.resting_delta = (int)rl32(st.resting, 0);  // becomes the new resting count
@@ -1250,8 +1143,7 @@ __device__ __forceinline__ bool wave_begin(C& c, const BookDev& bk, const BatchD
   return true;
 }
 
-template <class C>
-__device__ __forceinline__ void wave_end(C& c) {
+__device__ __forceinline__ void wave_end(WaveCtx& c) {
   if (lane_id() == 0) {
     SymState o;
     o.base = c.base;
@@ -1260,7 +1152,9 @@ __device__ __forceinline__ void wave_end(C& c) {
     o.free_head = c.free_head;
     o.resting = (uint32_t)c.resting_delta;
     o.nfree = 0;
-    o.pad = 0;
+    o.nfar[0] = c.nfar0;
+    o.nfar[1] = c.nfar1;
+    for (int k = 0; k < 5; ++k) o.pad[k] = 0;
     c.bk.sym[c.s] = o;
   }
 #ifdef ME_STAMPS
@@ -1279,233 +1173,118 @@ __global__ __launch_bounds__(256) void k_match(BookDev bk, BatchDev bt) {
   const uint32_t wv = threadIdx.x >> 6;
   const uint32_t s = blockIdx.x * 4u + wv;
   if (s > bk.S) return;
-  const uint32_t lo = wave_lower_bound(bt.skeys, bt.n, s);
-  const uint32_t hi = wave_lower_bound(bt.skeys, bt.n, s + 1);
+  const uint32_t lo = bt.bin_start ? bt.bin_start[s] : wave_lower_bound(bt.skeys, bt.n, s);
+  const uint32_t hi = bt.bin_start ? bt.bin_start[s + 1] : wave_lower_bound(bt.skeys, bt.n, s + 1);
   if (lo >= hi) return;
   if (s == bk.S) {
     reject_bad_symbols(bt, lo, hi);
     return;
   }
-  if constexpr (kLad == LAD_HBM) {
-    // a busy symbol goes to k_match_hot (LDS window of its ladder), launched right after this
-    if (bt.hot_min && hi - lo >= bt.hot_min) {
-      uint32_t idx = 0;
-      if (lane == 0) idx = atomicAdd(bt.hot, 1u);
-      idx = rl32(idx, 0);
-      if (idx < HOT_MAX) {
-        if (lane == 0) bt.hot[1 + idx] = s;
-        return;
-      }
-    }
-  }
   const uint32_t L = bk.L;
   Level* g_lv = bk.levels + (size_t)s * L;
   unsigned long long* g_occ = bk.occ + (size_t)s * bk.Lwords;
   uint8_t* g_tend = bk.tend + (size_t)s * L;
-  if constexpr (kLad == LAD_REG) {
-    WaveCtx<LadderReg> c;
+  WaveCtx c;
 #ifdef ME_STAMPS
-    for (int p = 0; p < PH_N; ++p) c.st[p] = 0;
-    STAMP_MARK(c);
+  for (int p = 0; p < PH_N; ++p) c.st[p] = 0;
+  STAMP_MARK(c);
 #endif
-    // levels lane and 64 + lane; the occupancy bitmap is implied by the totals
-    Level a = g_lv[lane];
-    Level b;
-    b.total = 0;
-    b.head = b.tail = NIL;
-    if (64 + (uint32_t)lane < L) b = g_lv[64 + lane];
-    c.lad.t0 = a.total;
-    c.lad.h0 = a.head;
-    c.lad.l0 = a.tail;
-    c.lad.t1 = b.total;
-    c.lad.h1 = b.head;
-    c.lad.l1 = b.tail;
-    c.lad.e0 = g_tend[lane];
-    c.lad.e1 = (64 + (uint32_t)lane < L) ? g_tend[64 + lane] : 0u;
-    c.lad.L = L;
-    c.lad.occ0 = __ballot(a.total > 0);
-    c.lad.occ1 = __ballot(b.total > 0);
-    c.lad.cv0 = c.lad.cv1 = c.lad.cd0 = c.lad.cd1 = 0ull;
-    c.cache = (CacheEntry*)(smem + (size_t)wv * lds_wave_bytes_reg());
-    c.cmask = CK_REG - 1;
-    if (!wave_begin(c, bk, bt, s, lo, hi)) return;
-    STAMP_ADD(c, PH_PROLOGUE);
-    match_records(c, bt, lo, hi);
-    // dirty cached heads back to HBM (valid entry l holds the head of level l)
-    for (int row = 0; row < 2; ++row) {
-      unsigned long long d = row ? (c.lad.cd1 & c.lad.cv1) : (c.lad.cd0 & c.lad.cv0);
-      while (d) {
-        const int j = __builtin_ctzll(d);
-        d &= d - 1;
-        const uint32_t cid = row ? rl32(c.lad.h1, j) : rl32(c.lad.h0, j);
-        const CacheEntry* E = c.cache + row * 64 + j;
-        if (lane < ME_C) {
-          cq_at(c.bk.chunks, (size_t)cid * ME_C + lane) = E->qty[lane];
-          cs_at(c.bk.chunks, (size_t)cid * ME_C + lane) = E->seq[lane];
-        }
-      }
+  c.lad.L = L;
+  c.lad.Lwords = bk.Lwords;
+  if constexpr (kLad == LAD_LDS) {
+    unsigned char* base = smem + (size_t)wv * lds_wave_bytes(L);
+    c.lad.lv = (Level*)base;
+    c.lad.occ = (unsigned long long*)(base + (size_t)L * sizeof(Level));
+    c.lad.tend = base + (size_t)L * sizeof(Level) + (size_t)(L / 64) * 8;
+    c.cache = (CacheEntry*)(base + lds_ladder_bytes(L));
+    c.cmask = CK_MEM - 1;
+    for (uint32_t i = lane; i < L; i += 64) {
+      c.lad.lv[i] = g_lv[i];
+      c.lad.tend[i] = g_tend[i];
     }
-    g_lv[lane] = Level{c.lad.t0, c.lad.h0, c.lad.l0};
-    g_tend[lane] = (uint8_t)c.lad.e0;
-    if (64 + (uint32_t)lane < L) {
-      g_lv[64 + lane] = Level{c.lad.t1, c.lad.h1, c.lad.l1};
-      g_tend[64 + lane] = (uint8_t)c.lad.e1;
-    }
-    // keep the HBM occupancy bitmap valid for the host-side book dump
-    const unsigned long long m0 = __ballot(c.lad.t0 > 0), m1 = __ballot(c.lad.t1 > 0);
-    if (lane == 0) {
-      g_occ[0] = m0;
-      if (bk.Lwords > 1) g_occ[1] = m1;
-    }
-    wave_end(c);
+    for (uint32_t i = lane; i < bk.Lwords; i += 64) c.lad.occ[i] = g_occ[i];
+    for (uint32_t i = lane; i < (uint32_t)CK_MEM; i += 64) c.cache[i].cid = NIL;
+    wave_mem_order();
   } else {
-    WaveCtx<LadderMem> c;
-#ifdef ME_STAMPS
-    for (int p = 0; p < PH_N; ++p) c.st[p] = 0;
-    STAMP_MARK(c);
-#endif
-    c.lad.L = L;
-    c.lad.Lwords = bk.Lwords;
-    if constexpr (kLad == LAD_LDS) {
-      unsigned char* base = smem + (size_t)wv * lds_wave_bytes(L);
-      c.lad.lv = (Level*)base;
-      c.lad.occ = (unsigned long long*)(base + (size_t)L * sizeof(Level));
-      c.lad.tend = base + (size_t)L * sizeof(Level) + (size_t)(L / 64) * 8;
-      c.cache = (CacheEntry*)(base + lds_ladder_bytes(L));
-      c.cmask = CK_MEM - 1;
-      for (uint32_t i = lane; i < L; i += 64) {
-        c.lad.lv[i] = g_lv[i];
-        c.lad.tend[i] = g_tend[i];
-      }
-      for (uint32_t i = lane; i < bk.Lwords; i += 64) c.lad.occ[i] = g_occ[i];
-      for (uint32_t i = lane; i < (uint32_t)CK_MEM; i += 64) c.cache[i].cid = NIL;
-      wave_mem_order();
-    } else {
-      c.lad.lv = g_lv;
-      c.lad.occ = g_occ;
-      c.lad.tend = g_tend;
-      c.cache = nullptr;
-      c.cmask = 0;
-    }
-    if (!wave_begin(c, bk, bt, s, lo, hi)) return;
-    STAMP_ADD(c, PH_PROLOGUE);
-    match_records(c, bt, lo, hi);
-    if constexpr (kLad == LAD_LDS) {
-      cache_flush_all(c, CK_MEM);
-      for (uint32_t i = lane; i < L; i += 64) {
-        g_lv[i] = c.lad.lv[i];
-        g_tend[i] = c.lad.tend[i];
-      }
-      for (uint32_t i = lane; i < bk.Lwords; i += 64) g_occ[i] = c.lad.occ[i];
-    }
-    wave_end(c);
+    c.lad.lv = g_lv;
+    c.lad.occ = g_occ;
+    c.lad.tend = g_tend;
+    c.cache = nullptr;
+    c.cmask = 0;
   }
+  if (!wave_begin(c, bk, bt, s, lo, hi)) return;
+  STAMP_ADD(c, PH_PROLOGUE);
+  match_records(c, bt, lo, hi);
+  if constexpr (kLad == LAD_LDS) {
+    cache_flush_all(c, CK_MEM);
+    for (uint32_t i = lane; i < L; i += 64) {
+      g_lv[i] = c.lad.lv[i];
+      g_tend[i] = c.lad.tend[i];
+    }
+    for (uint32_t i = lane; i < bk.Lwords; i += 64) g_occ[i] = c.lad.occ[i];
+  }
+  wave_end(c);
 }
 
-
-// ---- hot symbols of deep windows (L > LDS_MAX_LEVELS) --------------------------------------
-// LDS of one k_match_hot workgroup: occupancy words | window levels | window tail fills | cache.
-struct HotLds {
-  uint32_t W, occ_off, lv_off, te_off, ck_off, bytes;
-  uint32_t cache;  // head-chunk cache on (ME_HOT_CACHE=0 turns it off: A/B runs)
+// ---- seq ring horizon ---------------------------------------------------------
+// Runs before every match launch. The ring holds loc[seq & (R - 1)]; a rest of seq y overwrites the
+// entry of y - R. Every live order at or above the horizon has its entry, every older live order is
+// in the old-order table, so the ring is safe while every seq matched stays below horizon + R. When
+// the next group's largest seq would reach that, this kernel moves the horizon to the group's first
+// seq and rebuilds the old-order table from the chunk pool (all live orders, which are older than
+// the group since seqs ascend), in a new epoch: entries of earlier epochs read as empty. Every
+// workgroup makes the same decision from state[in] and the group's first / last seqs.
+struct SeqGroup {
+  const uint64_t* seq[ME_GMAX];
+  uint32_t n[ME_GMAX];
+  uint32_t ng;
+  uint32_t in;  // state index read; the kernel writes state[in ^ 1]
 };
-__host__ __device__ inline HotLds hot_lds(uint32_t L, uint32_t Lwords, uint32_t budget) {
-  HotLds h{};
-  h.occ_off = 0;
-  const uint32_t fixed = Lwords * 8u + CK_MEM * (uint32_t)sizeof(CacheEntry) + 64u;
-  uint32_t W = budget > fixed ? (budget - fixed) / ((uint32_t)sizeof(Level) + 1u) : 0u;
-  W &= ~63u;
-  if (W > L) W = L;
-  h.W = W;
-  h.lv_off = (Lwords * 8u + 15u) & ~15u;
-  h.te_off = h.lv_off + W * (uint32_t)sizeof(Level);
-  h.ck_off = (h.te_off + W + 15u) & ~15u;
-  h.bytes = h.ck_off + CK_MEM * (uint32_t)sizeof(CacheEntry);
-  h.cache = 1;
-  return h;
-}
 
-// One workgroup (one wave) per hot symbol, the symbols k_match<LAD_HBM> handed over in bt.hot.
-// Same record loop as k_match; the ladder window sits around the symbol's best prices.
-__global__ __launch_bounds__(64) void k_match_hot(BookDev bk, BatchDev bt, HotLds hl) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int lane = lane_id();
-  const uint32_t cnt = min(rl32(bt.hot[0], 0), HOT_MAX);
-  const uint32_t L = bk.L, W = hl.W;
-  for (uint32_t i = blockIdx.x; i < cnt; i += gridDim.x) {
-    const uint32_t s = rl32(bt.hot[1 + i], 0);
-    const uint32_t lo = bt.bin_start ? bt.bin_start[s] : wave_lower_bound(bt.skeys, bt.n, s);
-    const uint32_t hi = bt.bin_start ? bt.bin_start[s + 1] : wave_lower_bound(bt.skeys, bt.n, s + 1);
-    gptr1<Level> g_lv = (gptr1<Level>)(bk.levels + (size_t)s * L);
-    gptr1<unsigned long long> g_occ = (gptr1<unsigned long long>)(bk.occ + (size_t)s * bk.Lwords);
-    gptr1<uint8_t> g_tend = (gptr1<uint8_t>)(bk.tend + (size_t)s * L);
-    WaveCtx<LadderWin> c;
-#ifdef ME_STAMPS
-    for (int p = 0; p < PH_N; ++p) c.st[p] = 0;
-    STAMP_MARK(c);
-#endif
-    const SymState st = bk.sym[s];
-    const int bb = rli32(st.best_bid, 0), ba = rli32(st.best_ask, 0);
-    int center = (int)L / 2;
-    if (bb >= 0 && ba < (int)L)
-      center = (bb + ba) / 2;
-    else if (bb >= 0)
-      center = bb;
-    else if (ba < (int)L)
-      center = ba;
-    int wlo = center - (int)(W / 2);
-    if (wlo > (int)(L - W)) wlo = (int)(L - W);
-    if (wlo < 0) wlo = 0;
-    wlo &= ~63;
-    c.lad.wl = (lptr<Level>)(smem + hl.lv_off);
-    c.lad.wt = (lptr<uint8_t>)(smem + hl.te_off);
-    c.lad.occ = (lptr<unsigned long long>)(smem + hl.occ_off);
-    c.lad.glv = g_lv;
-    c.lad.gtend = g_tend;
-    c.lad.L = L;
-    c.lad.Lwords = bk.Lwords;
-    c.lad.wlo = wlo;
-    c.lad.W = W;
-    c.cache = hl.cache ? (CacheEntry*)(smem + hl.ck_off) : nullptr;
-    c.cmask = hl.cache ? CK_MEM - 1 : 0;
-    // stage the window: 8 level loads per lane in flight per step
-    for (uint32_t b = 0; b < W; b += 64 * 8) {
-      Level r[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const uint32_t j = b + (uint32_t)k * 64 + (uint32_t)lane;
-        r[k] = Level{0, NIL, NIL};
-        if (j < W) r[k] = ld_level(g_lv + (wlo + j));
-      }
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const uint32_t j = b + (uint32_t)k * 64 + (uint32_t)lane;
-        if (j < W) st_level(c.lad.wl + j, r[k]);
+__global__ __launch_bounds__(256) void k_seq_sweep(BookDev bk, SeqGroup sg) {
+  const SeqState st = bk.sq[sg.in];
+  const unsigned long long gmin = sg.seq[0][0];
+  const unsigned long long gmax = sg.seq[sg.ng - 1][sg.n[sg.ng - 1] - 1];
+  const unsigned long long R = bk.ring_mask + 1ull;
+  const bool need = gmax - st.horizon >= R;
+  const uint32_t epoch = need ? st.epoch + 1u : st.epoch;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    bool order_ok = st.last == 0ull || gmin > st.last;
+    for (uint32_t g = 0; g + 1 < sg.ng; ++g) order_ok &= sg.seq[g][sg.n[g] - 1] < sg.seq[g + 1][0];
+    uint32_t bits = 0;
+    if (!order_ok) bits |= ERR_SEQ_ORDER;
+    if (gmax - gmin >= R) bits |= ERR_SEQ_SPAN;
+    if (bits) atomicOr(bk.err, bits);
+    SeqState o;
+    o.horizon = need ? gmin : st.horizon;
+    o.last = gmax > st.last ? gmax : st.last;
+    o.epoch = epoch;
+    o.pad[0] = o.pad[1] = o.pad[2] = 0;
+    bk.sq[sg.in ^ 1u] = o;
+  }
+  if (!need) return;
+  const uint32_t top = min(*bk.chunk_top, bk.nchunks);
+  const size_t slots = (size_t)top * ME_C;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < slots; i += (size_t)gridDim.x * blockDim.x) {
+    if (cq_at(bk.chunks, i) <= 0) continue;
+    const unsigned long long q = cs_at(bk.chunks, i);
+    const unsigned long long want = ((unsigned long long)i << 32) | epoch;  // {epoch, slot}
+    unsigned long long h = old_hash(q) & bk.old_mask;
+    bool placed = false;
+    for (unsigned long long p = 0; p <= bk.old_mask && !placed; ++p, h = (h + 1) & bk.old_mask) {
+      unsigned long long* w = reinterpret_cast<unsigned long long*>(&bk.old[h]);
+      unsigned long long cur = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      while ((uint32_t)cur != epoch) {  // empty in this epoch: claim it
+        const unsigned long long prev = atomicCAS(w, cur, want);
+        if (prev == cur) {
+          bk.old[h].seq = q;
+          placed = true;
+          break;
+        }
+        cur = prev;
       }
     }
-    {
-      gptr1<uint32_t> gt4 = (gptr1<uint32_t>)(g_tend + wlo);  // wlo, W multiples of 64
-      lptr<uint32_t> wt4 = (lptr<uint32_t>)c.lad.wt;
-      for (uint32_t j = lane; j < W / 4; j += 64) wt4[j] = gt4[j];
-      for (uint32_t j = lane; j < bk.Lwords; j += 64) c.lad.occ[j] = g_occ[j];
-      if (c.cache)
-        for (uint32_t j = lane; j < (uint32_t)CK_MEM; j += 64) c.cache[j].cid = NIL;
-    }
-    wave_mem_order();
-    if (!wave_begin(c, bk, bt, s, lo, hi)) return;
-    STAMP_ADD(c, PH_PROLOGUE);
-    match_records(c, bt, lo, hi);
-    if (c.cache) cache_flush_all(c, CK_MEM);
-    wave_mem_order();
-    for (uint32_t j = lane; j < W; j += 64) st_level(g_lv + (wlo + j), ld_level(c.lad.wl + j));
-    {
-      gptr1<uint32_t> gt4 = (gptr1<uint32_t>)(g_tend + wlo);
-      lptr<uint32_t> wt4 = (lptr<uint32_t>)c.lad.wt;
-      for (uint32_t j = lane; j < W / 4; j += 64) gt4[j] = wt4[j];
-      for (uint32_t j = lane; j < bk.Lwords; j += 64) g_occ[j] = c.lad.occ[j];
-    }
-    wave_end(c);
-    wave_mem_order();
+    if (!placed) atomicOr(bk.err, ERR_OLD_OOM);
   }
 }
 
@@ -1585,7 +1364,8 @@ uint32_t sort_tile(uint32_t n) {
 hipError_t launch_sort_pass(hipStream_t st, const uint32_t* keys_in, const uint32_t* idx_in, uint32_t n,
                             uint32_t clamp_key, int shift, int dbits, uint32_t* hist, uint32_t* tot,
                             uint32_t* keys_out, uint32_t* idx_out, uint32_t* zero_buf,
-                            uint32_t zero_words, unsigned long long* scratch_top, uint32_t* bin_start) {
+                            uint32_t zero_words, unsigned long long* scratch_top, uint32_t* bin_start,
+                            const uint64_t* seq, uint32_t* err) {
   SortPass p;
   p.shift = (uint32_t)shift;
   p.mask = (1u << dbits) - 1u;
@@ -1594,7 +1374,7 @@ hipError_t launch_sort_pass(hipStream_t st, const uint32_t* keys_in, const uint3
   p.ntiles = (n + p.tile - 1) / p.tile;
   p.clamp = clamp_key;
   hipLaunchKernelGGL(k_sort_hist, dim3(p.ntiles), dim3(256), 0, st, keys_in, n, p, hist, zero_buf, zero_words,
-                     scratch_top);
+                     scratch_top, seq, err);
   hipLaunchKernelGGL(k_sort_colscan, dim3((p.nbins + 63) / 64), dim3(64), 0, st, hist, tot, p.nbins, p.ntiles);
   hipLaunchKernelGGL(k_sort_scatter, dim3(p.ntiles), dim3(256), 0, st, keys_in, idx_in, n, p, (uint32_t)dbits, hist,
                      tot, keys_out, idx_out, bin_start);
@@ -1603,18 +1383,6 @@ hipError_t launch_sort_pass(hipStream_t st, const uint32_t* keys_in, const uint3
 
 hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* bt, uint32_t ng, const AuxDev& ax,
                             hipEvent_t ev0, hipEvent_t ev1);
-
-// LDS one k_match_hot workgroup may use (the CU's 160 KB, less a margin).
-uint32_t hot_lds_budget() { return 160u * 1024u - 1024u; }
-static uint32_t g_hot_cache = 1;
-
-// Opt k_match_hot into the large dynamic LDS allocation once per process.
-hipError_t prepare_hot(const BookDev& bk) {
-  const HotLds hl = hot_lds(bk.L, bk.Lwords, hot_lds_budget());
-  if (hl.W < 64) return hipErrorInvalidValue;
-  if (const char* v = getenv("ME_HOT_CACHE")) g_hot_cache = (uint32_t)atoi(v);
-  return hipFuncSetAttribute((const void*)k_match_hot, hipFuncAttributeMaxDynamicSharedMemorySize, (int)hl.bytes);
-}
 
 // ev0 / ev1 (optional, timing): the launch records the kernel's own start and end
 // (hipExtLaunchKernelGGL), so timing adds no marker packet — and no gap — to the stream.
@@ -1625,18 +1393,26 @@ hipError_t launch_match(hipStream_t st, const BookDev& bk, const BatchDev& bt, h
     return launch_match_reg(st, bk, &bt, 1u, AuxDev{}, ev0, ev1);
   } else if (bk.L <= LDS_MAX_LEVELS) {
     hipExtLaunchKernelGGL(k_match<LAD_LDS>, grid, block, 4 * lds_wave_bytes(bk.L), st, ev0, ev1, 0, bk, bt);
-  } else if (!bt.hot_min || !bt.hot) {
-    hipExtLaunchKernelGGL(k_match<LAD_HBM>, grid, block, 0, st, ev0, ev1, 0, bk, bt);
   } else {
-    // deep windows: cold symbols match against the HBM ladder; busy ones are handed to
-    // k_match_hot, one workgroup each with an LDS window of the ladder
-    HotLds hl = hot_lds(bk.L, bk.Lwords, hot_lds_budget());
-    hl.cache = g_hot_cache;
-    hipError_t he = hipMemsetAsync(bt.hot, 0, 4, st);
-    if (he != hipSuccess) return he;
-    hipExtLaunchKernelGGL(k_match<LAD_HBM>, grid, block, 0, st, ev0, nullptr, 0, bk, bt);
-    hipExtLaunchKernelGGL(k_match_hot, dim3(HOT_GRID), dim3(64), hl.bytes, st, nullptr, ev1, 0, bk, bt, hl);
+    hipExtLaunchKernelGGL(k_match<LAD_HBM>, grid, block, 0, st, ev0, ev1, 0, bk, bt);
   }
+  return hipGetLastError();
+}
+
+// The seq-ring horizon check (and, when due, the old-order table rebuild) ahead of a match launch
+// over batches seq[0..ng) (n[g] > 0 each). Reads state in_idx, writes state in_idx ^ 1.
+hipError_t launch_seq_sweep(hipStream_t st, const BookDev& bk, const uint64_t* const* seq, const uint32_t* n,
+                            uint32_t ng, uint32_t in_idx, uint32_t grid) {
+  if (ng == 0 || ng > (uint32_t)ME_GMAX) return hipErrorInvalidValue;
+  SeqGroup sg{};
+  for (uint32_t g = 0; g < ng; ++g) {
+    if (!n[g]) return hipErrorInvalidValue;
+    sg.seq[g] = seq[g];
+    sg.n[g] = n[g];
+  }
+  sg.ng = ng;
+  sg.in = in_idx;
+  hipLaunchKernelGGL(k_seq_sweep, dim3(grid ? grid : 1), dim3(256), 0, st, bk, sg);
   return hipGetLastError();
 }
 

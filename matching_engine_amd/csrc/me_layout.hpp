@@ -1,21 +1,31 @@
 // me_layout.hpp — HBM layout of the resident books and of one in-flight batch.
 //
-// Shared by the gfx950 kernels (me_kernels.hip) and the host engine (me_engine.cpp).
-// Everything is plain-old-data; the host allocates, the kernels own the contents.
+// Shared by the gfx950 kernels (me_kernels.hip, me_match_reg.hip) and the host engine
+// (me_engine.cpp). Everything is plain-old-data; the host allocates, the kernels own the contents.
 //
-// Book of one shard:
-//   levels [S][L]   16 B {total, head chunk, tail chunk}: the fixed-depth price ladder. Bids and
-//                   asks share one ladder per symbol: after every order best_bid < best_ask, so
-//                   a level's side is implied by its position.
-//   occ    [S][L/64] occupancy bitmap of the ladder (bit set <=> total > 0).
-//   sym    [S]      32 B per-symbol scalars (window base, best bid/ask level, chunk free list).
+// Book of one shard. Prices are unbounded int64 Q4 (include/domain/price.hpp:6):
+//   levels [S][L]   16 B {total, head chunk, tail chunk}: the fixed-depth WINDOW of price levels
+//                   [base, base + L). Bids and asks share it: after every order best_bid < best_ask,
+//                   so a level's side is implied by its position.
+//   far    [S][2][F] 32 B {price, total, head, tail, tend}: levels OUTSIDE the window. Side 0 holds
+//                   bids below the window (ascending price, best last), side 1 asks above it
+//                   (descending price, best last). Invariant: no bid rests above the window and no
+//                   ask below it; a rest that would break this re-centres the window first.
+//   occ    [S][L/64] occupancy bitmap of the window (bit set <=> total > 0).
+//   sym    [S]      64 B per-symbol scalars (window base, best bid/ask level, chunk free list,
+//                   far-level counts).
 //   tend   [S][L]   slots written in each level's tail chunk (appends need no chunk read).
 //   chunks [NC]     FIFO storage: a level's queue is a doubly linked list of 256-B chunk blocks of
-//                   ME_C slots {seq u64, qty i32} (SoA inside the block); a wave reads one chunk per load.
-//                   A slot is live iff qty > 0. Every linked chunk holds >= 1 live order (a chunk
-//                   emptied by cancels is unlinked at once), so chunks in use <= resting orders.
-//   loc    [max_seq] seq -> global slot (chunk * ME_C + slot) for cancels.
-//   fcache [S][64]  free chunk ids a symbol keeps between launches (the register-ladder kernel
+//                   ME_C slots {seq u64, qty i32} (SoA inside the block) plus the level's price; a
+//                   wave reads one chunk per load. A slot is live iff qty > 0. Every linked chunk
+//                   holds >= 1 live order (a chunk emptied by cancels is unlinked at once), so
+//                   chunks in use <= resting orders.
+//   loc    [R]      seq ring: loc[seq & (R - 1)] = global slot (chunk * ME_C + slot) of the order
+//                   that rested with that seq. Never deleted; a lookup verifies the slot still
+//                   holds the seq. Entries of orders older than the ring horizon are copied into
+//                   the old-order table by k_seq_sweep before anything could overwrite them.
+//   old    [H]      old-order table (open addressing by seq): rebuilt by k_seq_sweep.
+//   fcache [S][64]  free chunk ids a symbol keeps between launches (the register-window kernel
 //                   holds them in one VGPR: pops and pushes never touch memory).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -37,6 +47,10 @@ enum : uint32_t {
   ERR_CHUNK_OOM = 1u,
   ERR_SCRATCH_OOM = 2u,
   ERR_INCONSISTENT = 4u,
+  ERR_FAR_OOM = 8u,      // a symbol's far-level array is full (me_config.far_levels)
+  ERR_OLD_OOM = 16u,     // the old-order table overflowed (sized from max_resting)
+  ERR_SEQ_ORDER = 32u,   // seqs not strictly ascending across the stream (API precondition)
+  ERR_SEQ_SPAN = 64u,    // one launch group spans >= the seq ring (raise me_config.seq_ring)
 };
 
 struct alignas(16) Level {
@@ -48,15 +62,18 @@ struct alignas(16) Level {
 struct alignas(16) ChunkHdr {
   uint32_t next;   // next chunk of the level FIFO, or of the symbol free list
   uint32_t prev;   // previous chunk of the level FIFO (NIL at the head)
-  uint32_t level;  // level index the chunk belongs to
   uint32_t owner;  // symbol that allocated the chunk (chunks never change symbol)
+  uint32_t pad;
 };
 
-// One FIFO chunk, 256 B: header, then the 16 slot quantities (one 64-B segment), then the 16 slot
-// seqs (two 64-B segments). One pointer reaches all of it; slot id g = chunk * ME_C + slot.
+// One FIFO chunk, 256 B: header and the level's price (one 64-B segment with the header), then
+// the 16 slot quantities (one 64-B segment), then the 16 slot seqs (two 64-B segments). One pointer
+// reaches all of it; slot id g = chunk * ME_C + slot. The price (not a window index) names the
+// level, so re-centring a window never touches chunks.
 struct alignas(256) Chunk {
   ChunkHdr hdr;
-  uint32_t pad[12];
+  long long price;
+  uint32_t pad[10];
   int qty[ME_C];
   unsigned long long seq[ME_C];
 };
@@ -65,14 +82,44 @@ static_assert(sizeof(Chunk) == 256, "chunk block must be 256 B");
 __host__ __device__ __forceinline__ int& cq_at(Chunk* c, size_t g) { return c[g / ME_C].qty[g % ME_C]; }
 __host__ __device__ __forceinline__ unsigned long long& cs_at(Chunk* c, size_t g) { return c[g / ME_C].seq[g % ME_C]; }
 
-struct alignas(32) SymState {
-  long long base;      // price_q4 of level 0
-  int best_bid;        // highest occupied bid level, -1 if none
-  int best_ask;        // lowest occupied ask level, L if none
+struct alignas(64) SymState {
+  long long base;      // price_q4 of level 0 of the window
+  int best_bid;        // highest occupied bid level of the window, -1 if none
+  int best_ask;        // lowest occupied ask level of the window, L if none
   uint32_t free_head;  // chunk free list of this symbol
-  uint32_t resting;    // live resting orders
-  uint32_t nfree;      // free chunk ids parked in fcache[sym][0..nfree) (register-ladder kernel)
+  uint32_t resting;    // live resting orders (window and far levels)
+  uint32_t nfree;      // free chunk ids parked in fcache[sym][0..nfree) (register-window kernel)
+  uint32_t nfar[2];    // far levels: [0] bids below the window, [1] asks above it
+  uint32_t pad[5];
+};
+static_assert(sizeof(SymState) == 64, "SymState is one 64-B segment");
+
+// A price level outside its symbol's window (BookDev::far). Same FIFO chunks as window levels.
+struct alignas(32) FarLevel {
+  long long price;
+  long long total;
+  uint32_t head, tail;
+  uint32_t tend;  // slots written in the tail chunk
   uint32_t pad;
+};
+static_assert(sizeof(FarLevel) == 32, "FarLevel is 32 B");
+
+// Old-order table entry: the claim word {epoch, slot} is CAS'd by k_seq_sweep; an entry is empty
+// unless its epoch is the current one (no clearing pass).
+struct alignas(16) OldEnt {
+  uint32_t epoch;
+  uint32_t slot;
+  unsigned long long seq;
+};
+
+// Seq-ring horizon, double-buffered: k_seq_sweep reads state[p] and writes state[p ^ 1]; the match
+// launches after it read state[p ^ 1] (BookDev::sq_idx). Every live order with seq >= horizon has
+// an intact ring entry; every older live order is in the old-order table of `epoch`.
+struct alignas(32) SeqState {
+  unsigned long long horizon;
+  unsigned long long last;   // largest seq of the stream so far (0 = none)
+  uint32_t epoch;
+  uint32_t pad[3];
 };
 
 // One bucketed record (24 B, AoS): the bucket job writes it as one unit, so a record's bytes land
@@ -90,18 +137,36 @@ struct BookDev {
   uint8_t* tend;          // [S][L] slots written in the level's tail chunk (valid when tail != NIL)
   SymState* sym;
   Chunk* chunks;          // [NC] FIFO chunk blocks
-  uint32_t* loc;
+  uint32_t* loc;          // [ring_mask + 1] seq ring
   uint32_t* chunk_top;
-  uint32_t* fcache;       // [S][64] free chunk ids parked between launches (register-ladder kernel)
+  uint32_t* fcache;       // [S][64] free chunk ids parked between launches (register-window kernel)
   uint32_t* err;
   const uint32_t* gsym;  // [S] id written into me_fill.symbol
   unsigned long long* dbg;  // [S][8] phase cycles, diagnostic (-DME_STAMPS) builds only
-  unsigned long long max_seq;
+  FarLevel* far;          // [S][2][fcap]
+  OldEnt* old;            // [old_mask + 1]
+  SeqState* sq;           // [2]
+  unsigned long long ring_mask;
+  unsigned long long old_mask;
+  uint32_t fcap;
+  uint32_t sq_idx;        // state the match launches read (k_seq_sweep wrote it)
   uint32_t nchunks;
   uint32_t S;
   uint32_t L;
   uint32_t Lwords;
 };
+
+// Far array of (symbol s, side k): k = 0 bids below the window, 1 asks above it.
+__host__ __device__ __forceinline__ FarLevel* far_of(const BookDev& bk, uint32_t s, uint32_t k) {
+  return bk.far + ((size_t)s * 2u + k) * bk.fcap;
+}
+// Hash of a seq into the old-order table.
+__host__ __device__ __forceinline__ unsigned long long old_hash(unsigned long long q) {
+  q ^= q >> 33;
+  q *= 0xff51afd7ed558ccdull;
+  q ^= q >> 33;
+  return q;
+}
 
 struct BatchDev {
   const uint64_t* seq;
@@ -132,15 +197,7 @@ struct BatchDev {
   uint32_t* bcnt;        // [(S + 1) * BK_CNT_STRIDE]
   const struct BkRec* b_rec;  // [(S + 1) * bcap] bucketed records
   uint32_t bcap;
-  // Deep-window path (L > LDS_MAX_LEVELS): a symbol with >= hot_min records in the batch is handed
-  // from k_match<LAD_HBM> to k_match_hot (one workgroup, LDS-resident ladder window) through
-  // hot[1 + i], i < hot[0] (the count; zeroed before each match launch). hot_min 0: no hand-off.
-  uint32_t* hot;
-  uint32_t hot_min;
 };
-constexpr uint32_t HOT_MAX = 1024;   // hot symbols per batch (more are matched in place)
-constexpr uint32_t HOT_GRID = 256;   // k_match_hot workgroups: one per CU (the LDS window fills it)
-constexpr uint32_t HOT_MIN_RECORDS = 64;  // threshold the tests use (ME_HOT_MIN, opt-in)
 // Batches per register-ladder launch at most (me_config.batches_per_launch). One launch matches a
 // group of up to ME_GMAX batches: every symbol's wave runs through its records of all of them in
 // order, so a launch costs the heaviest symbol's share of the whole group rather than the sum of

@@ -33,6 +33,7 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
+#include "me_far.hpp"
 #include "me_layout.hpp"
 #include "me_wave.hpp"
 
@@ -63,6 +64,10 @@ struct RegLds {
   uint32_t run_lo, run_n;
   int dq;                 // reg_rest: LDS target of an append to an uncached tail
   unsigned long long dsq;
+  uint32_t nfar[2];       // far-level counts of the symbol (me_far.hpp), rare-path state
+  uint32_t epoch;         // old-order table epoch of this launch
+  uint32_t pad2;
+  unsigned long long horizon;  // seqs below it may live in the old-order table instead of the ring
   union {
     struct {  // the symbol's bucket, staged for the batch-order gather
       unsigned long long seq[BK_CAP];
@@ -139,17 +144,6 @@ struct ColdArgs {
   uint32_t pad;
 };
 
-// Global-address-space (1) pointers: an opaque round trip (vreg64, ldsu) would otherwise leave a
-// generic pointer, and vector memory ops on it would be flat_* (counted in both vmcnt and lgkmcnt)
-// instead of global_*.
-#if defined(__HIP_DEVICE_COMPILE__)
-template <class T>
-using gptr = T __attribute__((address_space(1)))*;
-#else  // host pass of the single-source compile: the kernel body is never run there
-template <class T>
-using gptr = T*;
-#endif
-
 // A wave-uniform value read from LDS at the point of use. A relaxed atomic load is never hoisted out
 // of a loop (a plain load would be, pinning the value in SGPRs for the whole loop) and, unlike a
 // volatile one, keeps its LDS address space (ds_read, not flat); readfirstlane makes it scalar.
@@ -201,6 +195,7 @@ __device__ __forceinline__ gptr<T> vptr(T* p) {
 struct RegCtx {
   gptr<Chunk> chunks;    // VGPR
   gptr<uint32_t> loc;    // VGPR
+  unsigned long long rmask;  // VGPR: seq ring mask
   gptr<me_fill> scratch; // VGPR
   RegLds* M;
   const ColdArgs* G;
@@ -220,25 +215,36 @@ struct RegCtx {
   unsigned long long st[PH_N];
   unsigned long long st_t;
 #endif
+  // far-level interface (me_far.hpp): all rare-path, state read back from LDS where used
+  __device__ __forceinline__ gptr<Chunk> fchunks() const { return chunks; }
+  __device__ __forceinline__ uint32_t fnchunks() const { return nchunks; }
+  __device__ __forceinline__ uint32_t fsym() const { return s; }
+  __device__ __forceinline__ uint32_t fgsym() const { return gs; }
+  __device__ __forceinline__ uint32_t fcap() const { return ldsu(G->bk.fcap); }
+  __device__ __forceinline__ gptr<FarLevel> farr(uint32_t k) const {
+    return ldsg(G->bk.far) + ((size_t)s * 2u + k) * (size_t)fcap();
+  }
+  __device__ __forceinline__ uint32_t fcount(uint32_t k) const { return ldsu(M->nfar[k]); }
+  __device__ __forceinline__ void fset_count(uint32_t k, uint32_t n) {
+    if (lane_id() == 0) __hip_atomic_store(&M->nfar[k], n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  __device__ __forceinline__ void femit(bool fe, unsigned long long fm, const me_fill& F) {
+    if (fe) scratch[wptr + (uint32_t)__builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u)] = F;  // lanes 0..15
+    wptr += (uint32_t)__popcll(fm);
+  }
+  __device__ __forceinline__ void fresting(int d) { resting += d; }
+  __device__ __forceinline__ void floc(unsigned long long seq, uint32_t g) {
+    if (lane_id() == 0) loc[seq & rmask] = g;
+  }
+  __device__ __forceinline__ void ferr(uint32_t bits);
+  __device__ __forceinline__ uint32_t falloc();
+  __device__ __forceinline__ void ffree(uint32_t ch);
 };
 
 __device__ __forceinline__ void reg_err(const RegCtx& c, uint32_t bits) {
   if (lane_id() == 0) atomicOr(ldsg(c.G->bk.err), bits);
 }
-
-// Inclusive scan of a 16-lane row (each DPP row scans on its own), saturating at 2^32 - 1. The row
-// shifts use bound_ctrl (a lane with no source reads 0), so no "old" value is materialised.
-template <int kCtrl>
-__device__ __forceinline__ uint32_t shr_row(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kCtrl, 0xF, 0xF, true);
-}
-__device__ __forceinline__ uint32_t scan16_sat(uint32_t x) {
-  x = __builtin_elementwise_add_sat(x, shr_row<0x111>(x));  // row_shr:1
-  x = __builtin_elementwise_add_sat(x, shr_row<0x112>(x));  // row_shr:2
-  x = __builtin_elementwise_add_sat(x, shr_row<0x114>(x));  // row_shr:4
-  x = __builtin_elementwise_add_sat(x, shr_row<0x118>(x));  // row_shr:8
-  return x;
-}
+__device__ __forceinline__ void RegCtx::ferr(uint32_t bits) { reg_err(*this, bits); }
 
 // Level totals only ever change by adds. Every lane issues the atomic — lane 0 into the level's
 // total, lanes 1..63 into their own dummy slot — so a one-lane update needs no exec-mask dance.
@@ -299,6 +305,8 @@ __device__ __forceinline__ uint32_t reg_alloc(RegCtx& c) {
   }
   return reg_alloc_slow(c);
 }
+__device__ __forceinline__ uint32_t RegCtx::falloc() { return reg_alloc(*this); }
+__device__ __forceinline__ void RegCtx::ffree(uint32_t ch) { reg_free(*this, ch); }
 
 // ---- head-chunk cache ------------------------------------------------------------------------
 // Miss: copy chunk ch (the head of level lvl) into cache entry lvl. The only global load of a walk;
@@ -426,10 +434,11 @@ __device__ __forceinline__ bool reg_rest_new_chunk(RegCtx& c, int lvl, unsigned 
     ChunkHdr h;
     h.next = NIL;
     h.prev = tl;
-    h.level = (uint32_t)lvl;
     h.owner = c.s;
+    h.pad = 0;
     c.chunks[ch].hdr = h;
-    c.loc[seq] = ch * ME_C;
+    c.chunks[ch].price = c.base + lvl;
+    c.loc[seq & c.rmask] = ch * ME_C;
   }
   if (tl == NIL) {  // empty level: the new chunk is its head, installed in the cache
     c.hd.put(lvl, ch);  // cached
@@ -472,7 +481,7 @@ __device__ __forceinline__ bool reg_rest(RegCtx& c, int lvl, unsigned long long 
       *ls = seq;
       c.chunks[tl].qty[te] = (int)qty;
       c.chunks[tl].seq[te] = seq;
-      c.loc[seq] = tl * ME_C + te;
+      c.loc[seq & c.rmask] = tl * ME_C + te;
     }
     c.te.put(lvl, te + 1u);
   } else if (!reg_rest_new_chunk(c, lvl, seq, qty, tl)) {
@@ -488,86 +497,270 @@ __device__ __forceinline__ bool reg_rest(RegCtx& c, int lvl, unsigned long long 
 }
 
 // ---- cancelling ----------------------------------------------------------------------------
-// Remove the live resting order `tgt` of this symbol; returns its qty, 0 if not live. A chunk
+// Remove the live resting order `tgt` of this symbol; returns its qty, 0 if not live. The seq ring
+// names its slot unless a later seq overwrote the entry, in which case an order older than the
+// horizon is in the old-order table; every candidate slot is verified (owner, seq, qty > 0). A chunk
 // left without live orders is unlinked at once (chunks in use never exceed resting orders).
 __device__ __forceinline__ uint32_t reg_cancel(RegCtx& c, unsigned long long tgt) {
   const int lane = lane_id();
   const bool act = lane < ME_C;
-  if (tgt == 0ull || tgt >= ldsu(c.G->bk.max_seq)) return 0;
+  if (tgt == 0ull) return 0;
   wave_mem_order();
-  const uint32_t g = rl32(c.loc[tgt], 0);
+  uint32_t g = rl32(c.loc[tgt & c.rmask], 0);
   __builtin_amdgcn_s_waitcnt(VMCNT0);
-  if (g == NIL) return 0;
-  const uint32_t ch = g / ME_C, slot = g % ME_C;
-  if (ch >= c.nchunks) return 0;
-  // one round trip: owner, header, the chunk's quantities and the target seq
-  const uint32_t own = rl32(c.chunks[ch].hdr.owner, 0);
-  const ChunkHdr hdr = c.chunks[ch].hdr;
-  const int qg = c.chunks[ch].qty[lane & (ME_C - 1)];
-  unsigned long long sq = rl64(c.chunks[ch].seq[slot], 0);
-  __builtin_amdgcn_s_waitcnt(VMCNT0);  // resolved on every path (see reg_fill_entry)
-  int qv = act ? qg : 0;
-  if (own != c.s) return 0;  // another symbol's order: never touch its book
-  const int lvl = (int)rl32(hdr.level, 0);
-  if (lvl < 0 || lvl >= RL) {
+  for (int pass = 0;; ++pass) {
+    if (g != NIL && g / ME_C < c.nchunks) {
+      const uint32_t ch = g / ME_C, slot = g % ME_C;
+      // one round trip: header, price, the chunk's quantities and the target seq
+      const ChunkHdr hdr = c.chunks[ch].hdr;
+      const long long price = c.chunks[ch].price;
+      const int qg = c.chunks[ch].qty[lane & (ME_C - 1)];
+      unsigned long long sq = rl64(c.chunks[ch].seq[slot], 0);
+      __builtin_amdgcn_s_waitcnt(VMCNT0);  // resolved on every path (see reg_fill_entry)
+      int qv = act ? qg : 0;
+      const uint32_t own = rl32(hdr.owner, 0);
+      const long long prc = rli64(price, 0);
+      const long long lv64 = prc - rli64(c.base, 0);
+      const bool inw = own == c.s && (unsigned long long)lv64 < (unsigned long long)RL;
+      const int lvl = inw ? (int)lv64 : 0;
+      const uint32_t hv = c.hd.get(lvl);
+      const bool in_cache = inw && hv == ch;  // ch is the cached head: the on-chip copy is authoritative
+      if (in_cache) {
+        const int qc = c.M->cq[lvl][lane & (ME_C - 1)];
+        qv = act ? qc : 0;
+        sq = rl64(c.M->cs[lvl][slot], 0);
+      }
+      if (own == c.s && sq == tgt) {  // the order's slot: live or dead, it never moves
+        const int q = rli32(qv, (int)slot);
+        if (q <= 0) return 0;
+        const uint32_t nxt = rl32(hdr.next, 0), prv = rl32(hdr.prev, 0);
+        if (ME_UNLIKELY(!inw)) {  // a far level (me_far.hpp)
+          return far_cancel(c, prc < rli64(c.base, 0) ? 0u : 1u, prc, ch, slot, q, qv, nxt, prv);
+        }
+        const uint32_t t = c.tl.get(lvl);
+        const uint32_t h = hv == NIL ? NIL : (hv & ~HC);
+        const uint32_t live_after = (uint32_t)__popcll(__ballot(qv > 0)) - 1u;
+        if (lane == 0) {
+          if (in_cache)
+            c.M->cq[lvl][slot] = 0;
+          else
+            c.chunks[ch].qty[slot] = 0;
+        }
+        tot_add(c, lvl, -(long long)q);
+        if (live_after == 0u) {
+          if (h >= c.nchunks || t >= c.nchunks) {
+            reg_err(c, ERR_INCONSISTENT);
+            return (uint32_t)q;
+          }
+          if (in_cache) {  // the chunk leaves the cache; its HBM copy must read all-zero
+            if (act) c.chunks[ch].qty[lane] = 0;
+          }
+          const bool mirror = hv == prv;  // the cached head is ch's predecessor
+          if (h == t) {  // ch was the level's only chunk: the level empties
+            c.hd.put(lvl, NIL);
+            c.tl.put(lvl, NIL);
+            c.occ.clr(lvl);
+            if (lvl == c.bb) c.bb = c.occ.prev(lvl);
+            if (lvl == c.ba) c.ba = c.occ.next(lvl);
+          } else if (ch == h) {
+            c.hd.put(lvl, nxt | HC);  // the new head is not cached
+            if (lane == 0) c.chunks[nxt].hdr.prev = NIL;
+          } else if (ch == t) {
+            c.tl.put(lvl, prv);
+            c.te.put(lvl, ME_C);  // a non-tail chunk is always full
+            if (lane == 0) {
+              c.chunks[prv].hdr.next = NIL;
+              if (mirror) c.M->cnext[lvl] = NIL;
+            }
+          } else {
+            if (lane == 0) {
+              c.chunks[prv].hdr.next = nxt;
+              c.chunks[nxt].hdr.prev = prv;
+              if (mirror) c.M->cnext[lvl] = nxt;
+            }
+          }
+          reg_free(c, ch);
+        }
+        c.resting -= 1;
+        return (uint32_t)q;
+      }
+    }
+    // the ring entry is someone else's: only an order older than the horizon can still be live
+    if (pass != 0 || tgt >= ldsu(c.M->horizon)) return 0;
+    g = old_lookup(ldsg(c.G->bk.old), ldsu(c.G->bk.old_mask), ldsu(c.M->epoch), tgt);
+    if (g == NIL) return 0;
+  }
+}
+
+// ---- re-centring the window (rare) ----------------------------------------------------------
+// Level j of a 128-lane row pair after a shift by d: old level j + d, or `fill` outside [0, L).
+__device__ __forceinline__ uint32_t row_pick(uint32_t o0, uint32_t o1, int src, uint32_t L, uint32_t fill) {
+  const int a = (src & 63) << 2;
+  const uint32_t v0 = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)o0);
+  const uint32_t v1 = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)o1);
+  return (src >= 0 && src < (int)L) ? (src < 64 ? v0 : v1) : fill;
+}
+__device__ __forceinline__ void row_shift(Row2& r, int d, uint32_t L, uint32_t fill) {
+  const int lane = lane_id();
+  const uint32_t o0 = r.r0, o1 = r.r1;
+  r.r0 = row_pick(o0, o1, lane + d, L, fill);
+  const uint32_t n1 = row_pick(o0, o1, 64 + lane + d, L, fill);
+  r.r1 = 64u + (uint32_t)lane < L ? n1 : fill;
+}
+
+// Install far level e as window level j (its head chunk is not cached).
+__device__ __forceinline__ void reg_install(RegCtx& c, int j, const FarLevel& e) {
+  c.hd.put(j, e.head | HC);
+  c.tl.put(j, e.tail);
+  c.te.put(j, e.tend);
+  if (lane_id() == 0) c.M->tot[j] = e.total;
+}
+
+// Move the window so that it is centred on `target` as far as invariant I allows (me_far.hpp
+// recentre_base): cached heads go back to HBM (the cache is indexed by window level), levels leaving
+// the window become far levels at the best end of their side, the ladder rows and totals shift, and
+// far levels now inside the window are popped into it. Chunks name their level by price, so none
+// of them changes.
+__device__ __forceinline__ void reg_recentre(RegCtx& c, long long target) {
+  const int lane = lane_id();
+  const uint32_t L = ldsu(c.G->bk.L);
+  const long long base = rli64(c.base, 0);
+  const uint32_t n0 = c.fcount(0), n1 = c.fcount(1);
+  const bool wb = c.bb >= 0, wa = c.ba < (int)L;
+  long long bbp = 0, bap = 0;
+  if (wb)
+    bbp = base + c.bb;
+  else if (n0)
+    bbp = far_get(c.farr(0), n0 - 1u).price;
+  if (wa)
+    bap = base + c.ba;
+  else if (n1)
+    bap = far_get(c.farr(1), n1 - 1u).price;
+  const long long nb = recentre_base(target, L, wb || n0 != 0u, bbp, wa || n1 != 0u, bap);
+  if (nb == base) return;
+  const bool up = nb > base;
+  const unsigned long long dist =
+      up ? (unsigned long long)nb - (unsigned long long)base : (unsigned long long)base - (unsigned long long)nb;
+  const int dm = dist >= L ? (int)L : (int)dist;
+  const int d = up ? dm : -dm;
+  // 1. cached heads back to HBM
+  for (int row = 0; row < 2; ++row) {
+    unsigned long long cm = __ballot(((row ? c.hd.r1 : c.hd.r0) & HC) == 0u);
+    while (cm) {
+      const int jj = __builtin_ctzll(cm);
+      cm &= cm - 1ull;
+      const uint32_t cid = rl32(row ? c.hd.r1 : c.hd.r0, jj);
+      const int e = row * 64 + jj;
+      if (lane < ME_C) {
+        c.chunks[cid].qty[lane] = c.M->cq[e][lane];
+        c.chunks[cid].seq[lane] = c.M->cs[e][lane];
+      }
+    }
+  }
+  c.hd.r0 |= HC;
+  c.hd.r1 |= HC;
+  // 2. levels leaving the window: bids at the bottom (moving up), asks at the top (moving down)
+  if (d > 0) {
+    for (int l = c.occ.next(0); l < d; l = c.occ.next(l + 1)) {
+      if (l > c.bb) reg_err(c, ERR_INCONSISTENT);
+      FarLevel e;
+      e.price = base + l;
+      e.total = ldsu(c.M->tot[l]);
+      e.head = c.hd.get(l) & ~HC;
+      e.tail = c.tl.get(l);
+      e.tend = c.te.get(l);
+      e.pad = 0;
+      far_push(c, 0u, e);
+    }
+  } else {
+    for (int l = c.occ.prev((int)L - 1); l >= (int)L + d; l = c.occ.prev(l - 1)) {
+      if (l < c.ba) reg_err(c, ERR_INCONSISTENT);
+      FarLevel e;
+      e.price = base + l;
+      e.total = ldsu(c.M->tot[l]);
+      e.head = c.hd.get(l) & ~HC;
+      e.tail = c.tl.get(l);
+      e.tend = c.te.get(l);
+      e.pad = 0;
+      far_push(c, 1u, e);
+    }
+  }
+  // 3. shift the window
+  row_shift(c.hd, d, L, NIL);
+  row_shift(c.tl, d, L, NIL);
+  row_shift(c.te, d, L, 0u);
+  {
+    const long long t0 = c.M->tot[lane], t1 = c.M->tot[64 + lane];
+    const uint32_t l0 = row_pick((uint32_t)t0, (uint32_t)t1, lane + d, L, 0u);
+    const uint32_t h0 = row_pick((uint32_t)(t0 >> 32), (uint32_t)(t1 >> 32), lane + d, L, 0u);
+    const uint32_t l1 = row_pick((uint32_t)t0, (uint32_t)t1, 64 + lane + d, L, 0u);
+    const uint32_t h1 = row_pick((uint32_t)(t0 >> 32), (uint32_t)(t1 >> 32), 64 + lane + d, L, 0u);
+    c.M->tot[lane] = (long long)(((unsigned long long)h0 << 32) | l0);
+    c.M->tot[64 + lane] = 64u + (uint32_t)lane < L ? (long long)(((unsigned long long)h1 << 32) | l1) : 0ll;
+  }
+  int nbb = (c.bb >= 0 && c.bb - d >= 0) ? c.bb - d : -1;
+  int nba = (c.ba < (int)L && c.ba - d < (int)L) ? c.ba - d : RL;
+  c.base = (long long)vreg64((unsigned long long)nb);
+  // 4. far levels now inside the window
+  if (d < 0) {
+    const gptr<FarLevel> a = c.farr(0);
+    uint32_t n = c.fcount(0);
+    while (n) {
+      const FarLevel e = far_get(a, n - 1u);
+      if (e.price < nb) break;
+      const unsigned long long off = (unsigned long long)e.price - (unsigned long long)nb;
+      if (off >= L) {  // impossible by recentre_base (every bid is below nb + L)
+        reg_err(c, ERR_INCONSISTENT);
+        break;
+      }
+      const int j = (int)off;
+      reg_install(c, j, e);
+      nbb = j > nbb ? j : nbb;
+      --n;
+    }
+    c.fset_count(0, n);
+  } else {
+    const gptr<FarLevel> a = c.farr(1);
+    uint32_t n = c.fcount(1);
+    while (n) {
+      const FarLevel e = far_get(a, n - 1u);
+      const unsigned long long off = (unsigned long long)e.price - (unsigned long long)nb;  // asks >= nb
+      if (off >= L) break;
+      const int j = (int)off;
+      reg_install(c, j, e);
+      nba = j < nba ? j : nba;
+      --n;
+    }
+    c.fset_count(1, n);
+  }
+  c.bb = nbb;
+  c.ba = nba;
+  c.occ.w0 = __ballot(c.M->tot[lane] > 0);
+  c.occ.w1 = __ballot(c.M->tot[64 + lane] > 0);
+}
+
+// Rest (seq, qty) at price p outside the window. Re-centre first when the rest would put a bid above
+// the window or an ask below it (invariant I) or when the window is empty; then rest in the window
+// or on the far side. Returns -1 on a capacity failure, 1 when the window moved (the block's control
+// words must be rebuilt), 0 otherwise.
+__device__ __forceinline__ int reg_far_rest(RegCtx& c, long long p, unsigned long long seq, uint32_t qty, bool buy) {
+  const uint32_t L = ldsu(c.G->bk.L);
+  long long base = rli64(c.base, 0);
+  const bool above = p > base;  // p is outside [base, base + L)
+  const bool mandatory = buy == above;
+  int moved = 0;
+  if (mandatory || (c.occ.w0 | c.occ.w1) == 0ull) {
+    reg_recentre(c, p);
+    moved = 1;
+    base = rli64(c.base, 0);
+  }
+  const unsigned long long off = (unsigned long long)p - (unsigned long long)base;
+  if (off < L) return reg_rest(c, (int)off, seq, qty, buy) ? moved : -1;
+  if (mandatory) {
     reg_err(c, ERR_INCONSISTENT);
-    return 0;
+    return -1;
   }
-  const uint32_t hv = c.hd.get(lvl), t = c.tl.get(lvl);
-  const uint32_t h = hv == NIL ? NIL : (hv & ~HC);
-  const bool in_cache = hv == ch;  // ch is the cached head: the on-chip copy is authoritative
-  if (in_cache) {
-    const int qc = c.M->cq[lvl][lane & (ME_C - 1)];
-    qv = act ? qc : 0;
-    sq = rl64(c.M->cs[lvl][slot], 0);
-  }
-  const int q = rli32(qv, (int)slot);
-  if (sq != tgt || q <= 0) return 0;
-  const uint32_t live_after = (uint32_t)__popcll(__ballot(qv > 0)) - 1u;
-  if (lane == 0) {
-    if (in_cache)
-      c.M->cq[lvl][slot] = 0;
-    else
-      c.chunks[ch].qty[slot] = 0;
-  }
-  tot_add(c, lvl, -(long long)q);
-  if (live_after == 0u) {
-    if (h >= c.nchunks || t >= c.nchunks) {
-      reg_err(c, ERR_INCONSISTENT);
-      return (uint32_t)q;
-    }
-    if (in_cache) {  // the chunk leaves the cache; its HBM copy must read all-zero
-      if (act) c.chunks[ch].qty[lane] = 0;
-    }
-    const uint32_t nxt = rl32(hdr.next, 0), prv = rl32(hdr.prev, 0);
-    const bool mirror = hv == prv;  // the cached head is ch's predecessor
-    if (h == t) {  // ch was the level's only chunk: the level empties
-      c.hd.put(lvl, NIL);
-      c.tl.put(lvl, NIL);
-      c.occ.clr(lvl);
-      if (lvl == c.bb) c.bb = c.occ.prev(lvl);
-      if (lvl == c.ba) c.ba = c.occ.next(lvl);
-    } else if (ch == h) {
-      c.hd.put(lvl, nxt | HC);  // the new head is not cached
-      if (lane == 0) c.chunks[nxt].hdr.prev = NIL;
-    } else if (ch == t) {
-      c.tl.put(lvl, prv);
-      c.te.put(lvl, ME_C);  // a non-tail chunk is always full
-      if (lane == 0) {
-        c.chunks[prv].hdr.next = NIL;
-        if (mirror) c.M->cnext[lvl] = NIL;
-      }
-    } else {
-      if (lane == 0) {
-        c.chunks[prv].hdr.next = nxt;
-        c.chunks[nxt].hdr.prev = prv;
-        if (mirror) c.M->cnext[lvl] = nxt;
-      }
-    }
-    reg_free(c, ch);
-  }
-  c.resting -= 1;
-  return (uint32_t)q;
+  return far_rest(c, p < base ? 0u : 1u, p, seq, qty) ? moved : -1;
 }
 
 // ---- scratch ---------------------------------------------------------------------------------
@@ -723,9 +916,12 @@ __device__ __forceinline__ void aux_bucket(const ColdArgs& G, uint32_t j, uint32
   const gptr<BkRec> brec = ldsg(J.b_rec);
   const uint32_t S = ldsu(G.ax.S);
   const gptr<me_order_result> bres = ldsg(J.bres);
+  bool order_ok = true;
   for (uint32_t i0 = r0; i0 < r1; i0 += 64) {
     const uint32_t i = i0 + (uint32_t)lane;
     if (i < r1) {
+      // API precondition (the seq ring relies on it): seqs strictly ascending through the batch
+      if (i > 0) order_ok &= seq[i] > seq[i - 1];
       const uint32_t b = min(sym[i], S);
       if (b == S) {  // unknown symbol: rejected here, never bucketed (the batch's result set is free)
         reject_bad_at(bres, i);
@@ -745,6 +941,7 @@ __device__ __forceinline__ void aux_bucket(const ColdArgs& G, uint32_t j, uint32
       }
     }
   }
+  if (__ballot(!order_ok) && lane == 0) atomicOr(ldsg(G.bk.err), ERR_SEQ_ORDER);
 }
 
 // Tape job j, one TILE_TAPE-record tile per wave: tape offsets of its records and the copy of their
@@ -824,8 +1021,27 @@ __device__ __forceinline__ void aux_jobs(const ColdArgs& G, uint32_t a, uint32_t
 }
 
 // ---- the kernel ----------------------------------------------------------------------------
-// Per-record control word built in vector form: lim level | BUY | MARKET | CANCEL.
-constexpr uint32_t CW_BUY = 1u << 8, CW_MKT = 1u << 9, CW_CXL = 1u << 10;
+// Per-record control word built in vector form: (window limit level + 1) | BUY | MARKET | CANCEL |
+// FAR (the limit reaches past the window on the side the taker crosses: MARKET, a BUY above the
+// window, a SELL below it) | OUT (a LIMIT priced outside the window: its rest takes the far path).
+constexpr uint32_t CW_BUY = 1u << 8, CW_MKT = 1u << 9, CW_CXL = 1u << 10, CW_FAR = 1u << 11, CW_OUT = 1u << 12;
+
+__device__ __forceinline__ uint32_t make_cw(long long opx, uint32_t kd, long long base, uint32_t L) {
+  const uint32_t side = kd & 3u;
+  const bool market = (kd >> 2) & 1u, cancel = (kd >> 3) & 1u;
+  const bool buy = side == ME_SIDE_BUY;
+  const unsigned long long off = (unsigned long long)opx - (unsigned long long)base;
+  const bool inw = off < (unsigned long long)L;
+  const bool above = !inw && opx > base;
+  // the last window level the taker may trade at, -1 .. L (none below / above the window)
+  const int lim = market ? (buy ? (int)L - 1 : 0)
+                : inw    ? (int)off
+                : buy    ? (above ? (int)L - 1 : -1)
+                         : (above ? (int)L : 0);
+  const bool far = market || (buy ? above : (!inw && !above));
+  return (uint32_t)(lim + 1) | (buy ? CW_BUY : 0u) | (market ? CW_MKT : 0u) | (cancel ? CW_CXL : 0u) |
+         (far ? CW_FAR : 0u) | (!market && !inw ? CW_OUT : 0u);
+}
 
 __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
   __shared__ RegLds lds[REG_WAVES];
@@ -901,6 +1117,7 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
   RegCtx c;
   c.chunks = vptr(bk.chunks);
   c.loc = vptr(bk.loc);
+  c.rmask = vreg64(bk.ring_mask);
   c.G = &G;
   c.M = &lds[wv];
   c.nchunks = bk.nchunks;
@@ -926,10 +1143,17 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
   c.bb = rli32(st.best_bid, 0);
   c.ba = rli32(st.best_ask, 0);
   if (c.ba > RL) c.ba = RL;
-  if (lane == 0) {
-    c.M->free_head = st.free_head;
-    c.M->bump_cur = 0;
-    c.M->bump_end = 0;
+  {
+    const SeqState sqs = bk.sq[bk.sq_idx];
+    if (lane == 0) {
+      c.M->free_head = st.free_head;
+      c.M->bump_cur = 0;
+      c.M->bump_end = 0;
+      c.M->nfar[0] = st.nfar[0];
+      c.M->nfar[1] = st.nfar[1];
+      c.M->horizon = sqs.horizon;
+      c.M->epoch = sqs.epoch;
+    }
   }
   c.nfs = min(rl32(st.nfree, 0), (uint32_t)FSTK);
   c.fstk = fst;
@@ -1032,33 +1256,25 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
       }
       const uint32_t j = (uint32_t)lane;  // record j of the block
       const uint32_t hi = cnt;
-      const unsigned long long max_seq = ldsu(G.bk.max_seq);
-      const long long lbase = c.base;
       // validation in vector form; only the packed control word and the reject code stay live
       uint32_t cw, rj;
       {
         const bool v = j < hi;
         const unsigned long long oseq = v ? oseq_ : 0ull;
-        const long long opx = v ? opx_ : 0ll;
         const int oq = v ? oq_ : 0;
         const uint32_t kd = v ? kd_ : 0u;
         const uint32_t side = kd & 3u;
-        const bool market = (kd >> 2) & 1u, cancel = (kd >> 3) & 1u;
-        const bool buy = side == ME_SIDE_BUY;
-        const bool oow = opx < lbase || (unsigned long long)(opx - lbase) >= (unsigned long long)L;
+        const bool cancel = (kd >> 3) & 1u;
         rj = ME_RJ_NONE;
         if (!cancel) {
           if (oq <= 0)
             rj = ME_RJ_BAD_QTY;
           else if (side != ME_SIDE_BUY && side != ME_SIDE_SELL)
             rj = ME_RJ_BAD_SIDE;
-          else if (!market && oow)
-            rj = ME_RJ_OUT_OF_WINDOW;
-          else if (oseq == 0ull || oseq >= max_seq)
-            rj = ME_RJ_BAD_SEQ;
+          else if (oseq == 0ull)
+            rj = ME_RJ_BAD_SEQ;  // no OID is 0 (the counter starts at 1, storage.cpp:254-267)
         }
-        const uint32_t lim = market ? (buy ? L - 1u : 0u) : (oow ? 0u : (uint32_t)(opx - lbase));
-        cw = lim | (buy ? CW_BUY : 0u) | (market ? CW_MKT : 0u) | (cancel ? CW_CXL : 0u);
+        cw = make_cw(v ? opx_ : 0ll, kd, c.base, L);
         if (!v) rj = 0xFFu;  // lanes past the run: no record
       }
       unsigned long long work = __ballot(rj == ME_RJ_NONE);
@@ -1087,7 +1303,7 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
           }
           const unsigned long long seq = rl64(oseq_, k);
           const uint32_t q = (uint32_t)rli32(oq_, k);
-          const int lm = (int)(ctl & 0xFFu);
+          const int lm = (int)(ctl & 0xFFu) - 1;
           const uint32_t w_in = c.wptr;
           uint32_t rem = q;
           // one walk loop for both sides (one copy of the walk): the opposite best moves away from
@@ -1104,14 +1320,26 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
             c.ba = lvl;
           else
             c.bb = lvl;
+          // the window side is exhausted and the limit reaches further: far levels (rare)
+          if (ME_UNLIKELY(rem != 0u && (ctl & CW_FAR)) && c.fcount(buy ? 1u : 0u) != 0u)
+            rem -= far_take(c, buy, (ctl & CW_MKT) != 0u, (long long)rl64((unsigned long long)opx_, k), rem, seq);
           outq = q - rem;
           STAMP_ADD(c, PH_WALK);
           const bool me_ = lane == k;
           out_n = me_ ? c.wptr - w_in : out_n;
           out_w = me_ ? w_in : out_w;
-          if (!(ctl & CW_MKT) && rem != 0u && ME_UNLIKELY(!reg_rest(c, lm, seq, rem, (ctl & CW_BUY) != 0u))) {
-            stop = (uint32_t)k;  // chunk pool exhausted: the batch fails (sticky error word)
-            break;
+          if (!(ctl & CW_MKT) && rem != 0u) {
+            if (ME_UNLIKELY(ctl & CW_OUT)) {  // priced outside the window
+              const int rr = reg_far_rest(c, (long long)rl64((unsigned long long)opx_, k), seq, rem, buy);
+              if (rr < 0) {
+                stop = (uint32_t)k;
+                break;
+              }
+              if (rr > 0) cw = make_cw(j < hi ? opx_ : 0ll, j < hi ? kd_ : 0u, c.base, L);  // the window moved
+            } else if (ME_UNLIKELY(!reg_rest(c, lm, seq, rem, buy))) {
+              stop = (uint32_t)k;  // chunk pool exhausted: the batch fails (sticky error word)
+              break;
+            }
           }
           STAMP_ADD(c, PH_REST);
         }
@@ -1197,6 +1425,7 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
   const uint32_t Lwords = ldsu(G.bk.Lwords);
   unsigned long long* g_occ = ldsg(G.bk.occ) + (size_t)s * Lwords;  // for the host-side book dump
   const uint32_t fh = ldsu(c.M->free_head);
+  const uint32_t nf0 = c.fcount(0), nf1 = c.fcount(1);
   if (lane == 0) {
     g_occ[0] = c.occ.w0;
     if (Lwords > 1) g_occ[1] = c.occ.w1;
@@ -1207,7 +1436,9 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
     so.free_head = fh;
     so.resting = (uint32_t)c.resting;
     so.nfree = c.nfs;
-    so.pad = 0;
+    so.nfar[0] = nf0;
+    so.nfar[1] = nf1;
+    for (int k = 0; k < 5; ++k) so.pad[k] = 0;
     ldsg(G.bk.sym)[s] = so;
   }
 #ifdef ME_STAMPS

@@ -46,6 +46,31 @@ __device__ __forceinline__ long long wave_incl_scan(long long x) {
   x += dpp64<0x143, 0xC>(x);  // row_bcast:31 into rows 2, 3
   return x;
 }
+// Inclusive scan of a 16-lane row (each DPP row scans on its own), saturating at 2^32 - 1. The row
+// shifts use bound_ctrl (a lane with no source reads 0), so no "old" value is materialised.
+template <int kCtrl>
+__device__ __forceinline__ uint32_t shr_row(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, kCtrl, 0xF, 0xF, true);
+}
+__device__ __forceinline__ uint32_t scan16_sat(uint32_t x) {
+  x = __builtin_elementwise_add_sat(x, shr_row<0x111>(x));  // row_shr:1
+  x = __builtin_elementwise_add_sat(x, shr_row<0x112>(x));  // row_shr:2
+  x = __builtin_elementwise_add_sat(x, shr_row<0x114>(x));  // row_shr:4
+  x = __builtin_elementwise_add_sat(x, shr_row<0x118>(x));  // row_shr:8
+  return x;
+}
+
+// Global-address-space (1) pointers: an opaque round trip (vreg64, ldsu) would otherwise leave a
+// generic pointer, and vector memory ops on it would be flat_* (counted in both vmcnt and lgkmcnt)
+// instead of global_*.
+#if defined(__HIP_DEVICE_COMPILE__)
+template <class T>
+using gptr = T __attribute__((address_space(1)))*;
+#else  // host pass of the single-source compile: the kernel body is never run there
+template <class T>
+using gptr = T*;
+#endif
+
 // Orders the wave's own global stores before its later loads of the same lines (another lane
 // may read what this lane wrote). Same-CU ordering: no cache maintenance, a compiler barrier.
 __device__ __forceinline__ void wave_mem_order() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }

@@ -92,7 +92,11 @@ class DeviceBatch:
 
 
 class Engine:
-    """One shard of HBM-resident books (include/me_engine.h me_create ... me_destroy)."""
+    """One shard of HBM-resident books (include/me_engine.h me_create ... me_destroy).
+
+    `levels` is the depth of each symbol's on-chip window; `base_prices` only its initial position:
+    any int64 price is accepted (far levels + re-centring) and any u64 seq (the seq ring, `seq_ring`
+    entries, 0 = 2^28)."""
 
     def __init__(
         self,
@@ -101,11 +105,12 @@ class Engine:
         base_prices,
         max_batch: int,
         max_resting: int,
-        max_seq: int,
+        seq_ring: int = 0,
         max_chunks: int = 0,
         device: int = 0,
         symbol_ids=None,
         batches_per_launch: int = 0,
+        far_levels: int = 0,
     ):
         self.lib = _abi.load()
         self.num_symbols = int(num_symbols)
@@ -120,10 +125,11 @@ class Engine:
             max_batch,
             max_resting,
             max_chunks,
-            max_seq,
+            seq_ring,
             self._base.ctypes.data_as(C.POINTER(C.c_int64)),
             None if self._ids is None else self._ids.ctypes.data_as(C.POINTER(C.c_uint32)),
             batches_per_launch,
+            far_levels,
         )
         self.max_batch = int(max_batch)
         h = self.lib.me_create(C.byref(cfg))
@@ -184,6 +190,19 @@ class Engine:
         _check(self.lib, self.h, self.lib.me_fetch_outputs(self.h, None, 0, C.byref(nf), ptr(res), n))
         fills = np.zeros(nf.value, dtype=FILL_DTYPE)
         _check(self.lib, self.h, self.lib.me_fetch_outputs(self.h, ptr(fills), nf.value, C.byref(nf), None, 0))
+        return res, fills
+
+    def last_group_size(self) -> int:
+        return int(self.lib.me_last_group_size(self.h))
+
+    def fetch_group_outputs(self, k: int, n: int):
+        """Outputs of the k-th batch (n records) of the most recent launch group."""
+        res = np.zeros(n, dtype=RESULT_DTYPE)
+        nf = C.c_size_t(0)
+        _check(self.lib, self.h, self.lib.me_fetch_group_outputs(self.h, k, None, 0, C.byref(nf), ptr(res), n))
+        fills = np.zeros(nf.value, dtype=FILL_DTYPE)
+        _check(self.lib, self.h, self.lib.me_fetch_group_outputs(self.h, k, ptr(fills), nf.value, C.byref(nf),
+                                                                 None, 0))
         return res, fills
 
     def copy_tape_device(self, dst_ptr: int, cap_fills: int) -> int:
@@ -251,6 +270,10 @@ class StreamConfig:
     batch: int = 65536
     batches: int = 1024
     seed_levels_per_side: int = 0
+    seq_start: int = 0       # first seq (0 = 1); > 2^33 exercises OIDs far beyond any fixed table
+    drift_step: int = 0      # > 0: each symbol's mid trends drift_step ticks every drift_every records
+    drift_every: int = 0
+    far_pct: int = 0         # % of LIMITs priced U[L, 64L] ticks away from the mid (outside the window)
 
 
 def preset(config: int, **over) -> StreamConfig:
@@ -275,7 +298,8 @@ class Stream:
         self.lib = _abi.load()
         self.sc = sc
         p = MeGenParams(sc.config, sc.seed, sc.num_symbols, sc.levels, sc.spread_ticks, sc.max_qty,
-                        sc.market_pct, sc.cancel_pct, float(sc.zipf_s), sc.market_qty_mult)
+                        sc.market_pct, sc.cancel_pct, float(sc.zipf_s), sc.market_qty_mult, sc.seq_start,
+                        sc.drift_step, sc.drift_every, sc.far_pct)
         self.g = self.lib.me_gen_create(C.byref(p))
         if not self.g:
             raise ValueError(f"invalid stream config {sc}")

@@ -32,7 +32,7 @@ def load():
         lib = C.CDLL(LIB)
         P, SZ = C.c_void_p, C.c_size_t
         lib.orc_create.restype = P
-        lib.orc_create.argtypes = [C.c_uint32, C.c_uint32, P, C.c_uint64]
+        lib.orc_create.argtypes = [C.c_uint32]
         lib.orc_destroy.argtypes = [P]
         lib.orc_resting.restype = C.c_uint64
         lib.orc_resting.argtypes = [P]
@@ -60,13 +60,13 @@ def _p(a):
 
 
 class OracleBook:
-    """Scalar price-time books for num_symbols symbols (same admission rules as the engine)."""
+    """Unbounded scalar price-time books for num_symbols symbols: no price window, no seq cap (the
+    engine's fixed-depth windows and seq ring are implementation details it must hide)."""
 
-    def __init__(self, num_symbols, levels, base_prices, max_seq, symbol_ids=None):
+    def __init__(self, num_symbols, symbol_ids=None):
         self.lib = load()
-        self.base = np.ascontiguousarray(base_prices, dtype=np.int64)
         self.ids = None if symbol_ids is None else np.ascontiguousarray(symbol_ids, dtype=np.uint32)
-        self.h = self.lib.orc_create(num_symbols, levels, _p(self.base), max_seq)
+        self.h = self.lib.orc_create(num_symbols)
 
     def close(self):
         if self.h:

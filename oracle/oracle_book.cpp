@@ -13,8 +13,11 @@
 //      bytes), so fills are "parity unpinned" by the reference; this scalar price-time book is the
 //      golden model defined in DESIGN.md §2 (derived from the declared-but-unimplemented contract:
 //      OrderUpdate.Status proto/matching_engine.proto:79-85, FillRow include/storage/storage.hpp:11-17).
-//      It deliberately shares no data structure with the GPU design: std::map price levels and
-//      std::deque FIFOs, unbounded prices except for the same level-window admission rule.
+//      It deliberately shares no data structure and no limit with the GPU design: std::map price
+//      levels over the whole int64 Q4 range (include/domain/price.hpp:6), std::deque FIFOs, and an
+//      unbounded seq -> order map (OIDs are an unbounded u64, matching_engine_service.cpp:29-32).
+//      The only admission rules are the domain's: BAD_QTY, BAD_SIDE (storage.cpp:32 CHECK),
+//      BAD_SYMBOL, and seq 0 (no OID is ever 0: the counter starts at 1, storage.cpp:254-267).
 #include <stdint.h>
 #include <string.h>
 
@@ -55,20 +58,14 @@ struct Where {
 
 struct orc {
   uint32_t S;
-  uint32_t L;
-  uint64_t max_seq;
-  std::vector<int64_t> base;
   std::vector<Book> books;
   std::unordered_map<uint64_t, Where> where;  // live resting orders only
   uint64_t resting = 0;
 };
 
-extern "C" orc* orc_create(uint32_t S, uint32_t L, const int64_t* base, uint64_t max_seq) {
+extern "C" orc* orc_create(uint32_t S) {
   orc* o = new orc();
   o->S = S;
-  o->L = L;
-  o->max_seq = max_seq;
-  o->base.assign(base, base + S);
   o->books.resize(S);
   o->where.reserve(1 << 20);
   return o;
@@ -171,14 +168,7 @@ extern "C" int orc_submit(orc* o, size_t n, const uint64_t* seq, const int64_t* 
       res_out[i] = r;
       continue;
     }
-    const int64_t base = o->base[s];
-    if (!market && (px[i] < base || (uint64_t)px[i] - (uint64_t)base >= (uint64_t)o->L)) {
-      r.status = ME_ST_REJECTED;
-      r.reason = ME_RJ_OUT_OF_WINDOW;
-      res_out[i] = r;
-      continue;
-    }
-    if (seq[i] == 0 || seq[i] >= o->max_seq) {
+    if (seq[i] == 0) {
       r.status = ME_ST_REJECTED;
       r.reason = ME_RJ_BAD_SEQ;
       res_out[i] = r;

@@ -79,5 +79,5 @@ def load_fixture(cid):
         fills.append(np.ascontiguousarray(z[f"b{k}_fills"]).view(FILL_DTYPE).reshape(-1))
     book = np.ascontiguousarray(z["book"]).view(BOOK_ENTRY_DTYPE).reshape(-1)
     meta = dict(num_symbols=int(z["num_symbols"][0]), levels=int(z["levels"][0]), base=z["base"],
-                max_seq=int(z["max_seq"][0]), book_counts=z["book_counts"])
+                book_counts=z["book_counts"])
     return meta, batches, res, fills, book

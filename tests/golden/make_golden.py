@@ -6,10 +6,12 @@
 2. submit_contract.json — SubmitOrder request -> response/persisted-row cases. The reference
    server cannot be built here (gRPC/protobuf/SQLiteCpp absent), so expected
    values are restated from its source (cited per case); the Q4 prices inside come from (1).
-3. match_c{1..5}.npz — small seeded streams of the five configurations run through the CPU
-   oracle: per-batch results + tapes + final resting books. The reference has no matcher, so
-   these are "parity unpinned" w.r.t. the reference: they pin the oracle against regressions and
-   are the GPU engine's bit-exact target.
+3. match_c{1..6}.npz — small seeded streams of the five configurations, plus (6) a drifting,
+   cancel-heavy stream with far-away LIMITs and OIDs above 2^33, run through the CPU oracle (an
+   unbounded price-time book): per-batch results + tapes + final resting books. The reference has
+   no matcher, so these are "parity unpinned" w.r.t. the reference: they pin the oracle against
+   regressions and are the GPU engine's bit-exact target (its 128-level windows must re-centre and
+   spill to far levels to reproduce them).
 
 usage: python tests/golden/make_golden.py [--only price|contract|match]
 """
@@ -132,12 +134,17 @@ def make_contract():
 
 # Small versions of the five configurations; shared with tests/test_gpu_parity.py.
 FIXTURES = {
-    1: dict(preset=1, over=dict(batch=2048), batches=4, max_seq=1 << 20),
-    2: dict(preset=2, over=dict(num_symbols=64, batch=4096), batches=4, max_seq=1 << 20),
-    3: dict(preset=3, over=dict(num_symbols=5000, batch=8192), batches=3, max_seq=1 << 20),
+    1: dict(preset=1, over=dict(batch=2048), batches=4),
+    2: dict(preset=2, over=dict(num_symbols=64, batch=4096), batches=4),
+    3: dict(preset=3, over=dict(num_symbols=5000, batch=8192), batches=3),
     4: dict(preset=4, over=dict(num_symbols=40, levels=1024, spread_ticks=250, seed_levels_per_side=300,
-                                batch=4096), batches=3, max_seq=1 << 20),
-    5: dict(preset=5, over=dict(num_symbols=64, batch=4096), batches=4, max_seq=1 << 20),
+                                batch=4096), batches=3),
+    5: dict(preset=5, over=dict(num_symbols=64, batch=4096), batches=4),
+    # mids trend 3 ticks every 4 records of a symbol (~3 windows over the stream), 2 % of LIMITs
+    # priced L..64L away, 20 % cancels, sweeping MARKETs, OIDs from 2^33 + 12345
+    6: dict(preset=5, over=dict(num_symbols=32, batch=2048, cancel_pct=20, market_pct=15, market_qty_mult=4,
+                                drift_step=3, drift_every=4, far_pct=2, seq_start=(1 << 33) + 12345),
+            batches=8),
 }
 
 
@@ -161,9 +168,9 @@ def make_match():
 
     for cid, fx in FIXTURES.items():
         sc, base, batches = fixture_stream(cid)
-        ob = OracleBook(sc.num_symbols, sc.levels, base, fx["max_seq"])
+        ob = OracleBook(sc.num_symbols)
         out = {"base": base, "levels": np.array([sc.levels]), "num_symbols": np.array([sc.num_symbols]),
-               "max_seq": np.array([fx["max_seq"]], dtype=np.uint64), "nbatches": np.array([len(batches)])}
+               "nbatches": np.array([len(batches)])}
         for k, b in enumerate(batches):
             res, fills = ob.submit(b)
             for f in ("seq", "price_q4", "qty", "symbol", "kind"):

@@ -39,10 +39,9 @@ def main():
     base = st.base_prices()
     plan = ShardPlan(S, world)
     ids = plan.members[rank]
-    max_seq = 1 << 20
     gath = None
     if engine_kind in ("gpu", "gpu_gather"):
-        book = me.Engine(len(ids), sc.levels, base[ids], max_batch=sc.batch, max_resting=1 << 16, max_seq=max_seq,
+        book = me.Engine(len(ids), sc.levels, base[ids], max_batch=sc.batch, max_resting=1 << 16,
                          symbol_ids=ids)
         submit = book.submit_batch
         if engine_kind == "gpu_gather":
@@ -52,9 +51,9 @@ def main():
 
             gath = EngineGather(book, torch.device("cuda", 0), sc.batch)
     else:
-        book = OracleBook(len(ids), sc.levels, base[ids], max_seq, symbol_ids=ids)
+        book = OracleBook(len(ids), symbol_ids=ids)
         submit = book.submit
-    ref = OracleBook(S, sc.levels, base, max_seq) if rank == 0 else None
+    ref = OracleBook(S) if rank == 0 else None
     ok, fills_total = True, 0
     msg = ""
     for k in range(nb):

@@ -83,10 +83,10 @@ def test_submit_contract_oid_sequence(orc):
 
 
 # ---------------------------------------------------------------- oracle matching fixtures
-@pytest.mark.parametrize("cid", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("cid", [1, 2, 3, 4, 5, 6])
 def test_oracle_replays_golden_fixture(orc, cid):
     meta, batches, res, fills, book = load_fixture(cid)
-    ob = orc.OracleBook(meta["num_symbols"], meta["levels"], meta["base"], meta["max_seq"])
+    ob = orc.OracleBook(meta["num_symbols"])
     for k, b in enumerate(batches):
         r, f = ob.submit(b)
         assert_results_equal(r, res[k], f"c{cid} b{k}")
@@ -117,7 +117,7 @@ def _batch(me, rows, start_seq=1):
 
 def test_semantics_price_time_priority(me, orc):
     B, S, L, M = me.SIDE_BUY, me.SIDE_SELL, me.TYPE_LIMIT, me.TYPE_MARKET
-    ob = orc.OracleBook(1, 128, [900], 1 << 20)
+    ob = orc.OracleBook(1)
     rows = [
         (0, S, L, 0, 1010, 5),   # 1 ask 1010
         (0, S, L, 0, 1005, 3),   # 2 ask 1005 (better)
@@ -141,11 +141,11 @@ def test_semantics_price_time_priority(me, orc):
 
 def test_semantics_rejects_and_cancel(me, orc):
     B, S, L, M = me.SIDE_BUY, me.SIDE_SELL, me.TYPE_LIMIT, me.TYPE_MARKET
-    ob = orc.OracleBook(2, 128, [1000, 5000], 1 << 10)
+    ob = orc.OracleBook(2)
     rows = [
-        (0, B, L, 0, 1000, 5),        # 1 rests at level 0
-        (0, B, L, 0, 999, 5),         # 2 below window -> REJECTED out of window
-        (0, B, L, 0, 1128, 5),        # 3 above window -> REJECTED
+        (0, B, L, 0, 1000, 5),        # 1 rests
+        (0, B, L, 0, 999, 5),         # 2 rests (any price: the book is unbounded)
+        (0, B, L, 0, 1128, 5),        # 3 rests, best bid
         (1, 0, L, 0, 5001, 5),        # 4 side 0 -> REJECTED bad side
         (0, B, L, 0, 1001, 0),        # 5 qty 0 -> REJECTED bad qty
         (7, B, L, 0, 1001, 1),        # 6 symbol out of range -> REJECTED bad symbol
@@ -153,26 +153,56 @@ def test_semantics_rejects_and_cancel(me, orc):
         (0, S, L, 1, 1, 0),           # 8 cancel #1 -> CANCELED, remaining 5
         (0, S, L, 1, 1, 0),           # 9 cancel again -> REJECTED unknown
         (0, S, L, 1, 12, 0),          # 10 cancel a future seq -> REJECTED
-        (0, B, M, 0, 0, 3),           # 11 market into empty book -> CANCELED, remaining 3
+        (0, S, M, 0, 0, 3),           # 11 market sell: 3 from #3 @1128 -> FILLED
     ]
     r, f = ob.submit(_batch(me, rows))
-    assert len(f) == 0
+    assert [(int(x["taker_seq"]), int(x["maker_seq"]), int(x["price_q4"]), int(x["qty"])) for x in f] == [
+        (11, 3, 1128, 3)]
     st = [(int(x["status"]), int(x["reason"]), int(x["remaining_qty"])) for x in r]
     assert st == [
-        (me.ST_NEW, 0, 5), (me.ST_REJECTED, me.RJ_OUT_OF_WINDOW, 5), (me.ST_REJECTED, me.RJ_OUT_OF_WINDOW, 5),
+        (me.ST_NEW, 0, 5), (me.ST_NEW, 0, 5), (me.ST_NEW, 0, 5),
         (me.ST_REJECTED, me.RJ_BAD_SIDE, 5), (me.ST_REJECTED, me.RJ_BAD_QTY, 0),
         (me.ST_REJECTED, me.RJ_BAD_SYMBOL, 0), (me.ST_REJECTED, me.RJ_UNKNOWN_ORDER, 0),
         (me.ST_CANCELED, 0, 5), (me.ST_REJECTED, me.RJ_UNKNOWN_ORDER, 0), (me.ST_REJECTED, me.RJ_UNKNOWN_ORDER, 0),
-        (me.ST_CANCELED, 0, 3)]
-    assert ob.resting() == 0
-    # seq beyond the locator capacity
-    r, _ = ob.submit(_batch(me, [(0, B, L, 0, 1000, 1)], start_seq=1 << 10))
+        (me.ST_FILLED, 0, 0)]
+    assert ob.resting() == 2
+    # no OID is 0 (the reference's counter starts at 1); every other u64 seq is accepted
+    r, _ = ob.submit(_batch(me, [(0, B, L, 0, 1000, 1)], start_seq=0))
     assert (r["status"][0], r["reason"][0]) == (me.ST_REJECTED, me.RJ_BAD_SEQ)
+
+
+def test_semantics_unbounded_prices_and_seqs(me, orc):
+    """The reference accepts any LIMIT with a positive raw price at any int64 Q4
+    (matching_engine_service.cpp:78-83, price.hpp:15-29) and OIDs are an unbounded u64 (:29-32):
+    no admission rule beyond the domain's, prices sort as int64, cancels find seqs above 2^33."""
+    B, S, L, M = me.SIDE_BUY, me.SIDE_SELL, me.TYPE_LIMIT, me.TYPE_MARKET
+    I64 = (1 << 63) - 1
+    ob = orc.OracleBook(1)
+    start = (1 << 33) + 17
+    rows = [
+        (0, S, L, 0, I64, 2),          # ask at the top of the int64 range
+        (0, S, L, 0, 10 ** 15, 3),     # ask far below it
+        (0, B, L, 0, -(1 << 62), 4),   # bid deep in the negative range
+        (0, B, L, 0, 5, 1),            # best bid
+        (0, B, M, 0, 0, 4),            # market buy: 3 @1e15 then 1 @I64
+        (0, S, L, 0, -(1 << 63), 6),   # sell at INT64_MIN: crosses both bids (1 @5, 4 @-2^62), rests 1
+        (0, S, L, 1, start + 2, 0),    # cancel the -2^62 bid: already filled -> REJECTED
+        (0, S, L, 1, start, 0),        # cancel the I64 ask: 1 left -> CANCELED 1
+    ]
+    r, f = ob.submit(_batch(me, rows, start_seq=start))
+    got = [(int(x["taker_seq"]) - start, int(x["maker_seq"]) - start, int(x["price_q4"]), int(x["qty"])) for x in f]
+    assert got == [(4, 1, 10 ** 15, 3), (4, 0, I64, 1), (5, 3, 5, 1), (5, 2, -(1 << 62), 4)]
+    assert [int(x) for x in r["status"]] == [me.ST_NEW, me.ST_NEW, me.ST_NEW, me.ST_NEW, me.ST_FILLED,
+                                             me.ST_PARTIALLY_FILLED, me.ST_REJECTED, me.ST_CANCELED]
+    assert int(r["remaining_qty"][7]) == 1
+    d = ob.dump(0)
+    assert [(int(x["seq"]) - start, int(x["price_q4"]), int(x["qty"]), int(x["side"])) for x in d] == [
+        (5, -(1 << 63), 1, S)]
 
 
 def test_semantics_cancel_frees_level_and_best_moves(me, orc):
     B, S, L, M = me.SIDE_BUY, me.SIDE_SELL, me.TYPE_LIMIT, me.TYPE_MARKET
-    ob = orc.OracleBook(1, 128, [1000], 1 << 20)
+    ob = orc.OracleBook(1)
     rows = [(0, S, L, 0, 1010, 5), (0, S, L, 0, 1020, 5), (0, S, L, 1, 1, 0), (0, B, L, 0, 1015, 9)]
     r, f = ob.submit(_batch(me, rows))
     assert len(f) == 0 and r["status"][3] == me.ST_NEW  # 1010 cancelled: best ask is now 1020 > 1015

@@ -1,5 +1,6 @@
-"""GPU parity: the HIP engine (through the C-ABI) against the CPU oracle and the committed golden
-fixtures — bit-exact per-record results, trade tapes and resting books. Needs an MI355X."""
+"""GPU parity: the HIP engine (through the C-ABI) against the CPU oracle — an unbounded price-time
+book — and the committed golden fixtures: bit-exact per-record results, trade tapes and resting
+books. Needs an MI355X."""
 import numpy as np
 import pytest
 
@@ -23,18 +24,30 @@ def orc(built):
     return oracle
 
 
-def engine_for(me, S, L, base, max_batch, max_resting, max_seq=1 << 22, **kw):
-    return me.Engine(S, L, base, max_batch=max_batch, max_resting=max_resting, max_seq=max_seq, **kw)
+def engine_for(me, S, L, base, max_batch, max_resting, **kw):
+    kw.setdefault("seq_ring", 1 << 22)
+    return me.Engine(S, L, base, max_batch=max_batch, max_resting=max_resting, **kw)
+
+
+def no_window_rejects(res, ctx=""):
+    """The engine's window and seq ring are invisible: never OUT_OF_WINDOW, BAD_SEQ only for seq 0."""
+    assert not np.any(res["reason"] == 3), f"{ctx}: OUT_OF_WINDOW reject"
+    assert not np.any(res["reason"] == 6), f"{ctx}: BAD_SEQ reject"
+
+
+def _rows(me, rows, start_seq=1):
+    n = len(rows)
+    return me.Batch(np.arange(start_seq, start_seq + n, dtype=np.uint64), [r[4] for r in rows],
+                    [r[5] for r in rows], [r[0] for r in rows], [me.kind(r[1], r[2], r[3]) for r in rows])
 
 
 # ---------------------------------------------------------------- committed fixtures
-@pytest.mark.parametrize("cid", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("cid", [1, 2, 3, 4, 5, 6])
 def test_golden_fixture_on_gpu(me, cid):
     meta, batches, res, fills, book = load_fixture(cid)
     mb = max(len(b) for b in batches)
     # deep sparse books (config 4) keep ~one chunk per resting order: size the pool for that
-    with engine_for(me, meta["num_symbols"], meta["levels"], meta["base"], mb, 1 << 18, meta["max_seq"],
-                    max_chunks=1 << 17) as eng:
+    with engine_for(me, meta["num_symbols"], meta["levels"], meta["base"], mb, 1 << 18, max_chunks=1 << 17) as eng:
         for k, b in enumerate(batches):
             r, f = eng.submit_batch(b)
             assert_results_equal(r, res[k], f"fixture c{cid} b{k}")
@@ -44,7 +57,7 @@ def test_golden_fixture_on_gpu(me, cid):
 
 
 # ---------------------------------------------------------------- live differential runs
-def _stream_run(me, orc, cfg, nbatches, seed_per_side=0, max_seq=1 << 26, book_symbols=None, **over):
+def _stream_run(me, orc, cfg, nbatches, seed_per_side=0, book_symbols=None, eng_kw=None, **over):
     sc = me.preset(cfg, **over)
     st = me.Stream(sc)
     base = st.base_prices()
@@ -54,9 +67,9 @@ def _stream_run(me, orc, cfg, nbatches, seed_per_side=0, max_seq=1 << 26, book_s
     batches += [st.next(sc.batch) for _ in range(nbatches)]
     mb = max(len(b) for b in batches)
     total = sum(len(b) for b in batches)
-    ob = orc.OracleBook(sc.num_symbols, sc.levels, base, max_seq)
-    with engine_for(me, sc.num_symbols, sc.levels, base, mb, total + 1024, max_seq,
-                    max_chunks=total + 2 * sc.num_symbols) as eng:
+    ob = orc.OracleBook(sc.num_symbols)
+    with engine_for(me, sc.num_symbols, sc.levels, base, mb, total + 1024, max_chunks=total + 2 * sc.num_symbols,
+                    **(eng_kw or {})) as eng:
         nf = run_both(eng, ob, batches, book_symbols=book_symbols, ctx=f"config {cfg}")
     return nf, total
 
@@ -81,21 +94,24 @@ def test_config4_zipf_deep_books(me, orc):
     assert nf > 0
 
 
-def test_config4_hot_symbols_ladder_window(me, orc, monkeypatch):
-    """Config 4 at its real window depth (L = 32,768): busy symbols go to k_match_hot, whose LDS
-    window (~8.5k levels around the best prices) is smaller than the ladder, so rests and sweeps
-    hit levels on both sides of the window edge. (The hand-off is opt-in: ME_HOT_MIN.)"""
-    monkeypatch.setenv("ME_HOT_MIN", "64")
-    nf, total = _stream_run(me, orc, 4, 3, seed_per_side=6000, num_symbols=40, levels=32768,
-                            spread_ticks=5000)
+def test_config4_bench_shape(me, orc):
+    """Config 4 at the bench's shape: L = 32,768-level windows (the HBM-window kernel), the most
+    popular books seeded to 10,000 levels per side, Zipf(1.1) symbols, LIMITs +-5,000 ticks."""
+    sc = me.preset(4, num_symbols=2000, batch=65536)
+    st = me.Stream(sc)
+    base = st.base_prices()
+    seeds = st.seed_books(range(24), 10_000)
+    batches = [seeds.take(slice(i, i + 65536)) for i in range(0, len(seeds), 65536)]
+    batches += [st.next(sc.batch) for _ in range(3)]
+    total = sum(len(b) for b in batches)
+    ob = orc.OracleBook(sc.num_symbols)
+    with engine_for(me, sc.num_symbols, sc.levels, base, 65536, total + 1024, max_chunks=total + 4096) as eng:
+        nf = run_both(eng, ob, batches, book_symbols=list(range(24)) + list(range(24, 2000, 61)), ctx="c4 bench")
     assert nf > 0
 
 
-@pytest.mark.parametrize("hot_min", ["0", "64"])
-def test_deep_window_hot_list_overflow(me, orc, monkeypatch, hot_min):
-    """More busy symbols than k_match_hot workgroups (each loops over several) and than the hand-off
-    list holds (the rest are matched in place by k_match<LAD_HBM>); the same stream without it."""
-    monkeypatch.setenv("ME_HOT_MIN", hot_min)
+def test_deep_window_many_symbols(me, orc):
+    """More symbols than one dispatch round of deep-window workgroups, busy and idle alike."""
     nf, total = _stream_run(me, orc, 2, 2, num_symbols=1100, levels=2048, batch=1100 * 80,
                             book_symbols=range(0, 1100, 7))
     assert nf > 0
@@ -106,33 +122,139 @@ def test_config5_cancel_heavy_sweeps(me, orc):
     assert nf > 0
 
 
+# ---------------------------------------------------------------- unbounded prices and seqs
+def _drift_stream(me, levels, num_symbols, batch, nbatches, drift_every, drift_step=1, far_pct=1, cancel_pct=10,
+                  market_qty_mult=3, seq_start=(1 << 33) + 777):
+    sc = me.preset(5, num_symbols=num_symbols, levels=levels, batch=batch, cancel_pct=cancel_pct, market_pct=15,
+                   market_qty_mult=market_qty_mult, drift_step=drift_step, drift_every=drift_every,
+                   far_pct=far_pct, seq_start=seq_start)
+    st = me.Stream(sc)
+    return sc, st.base_prices(), [st.next(batch) for _ in range(nbatches)]
+
+
+def test_drifting_mids_far_limits_big_oids(me, orc):
+    """Every symbol's mid trends 10 x L over 200 batches (1 tick every 5 of its records, 32 records
+    per symbol per batch), 1 % of LIMITs are priced L..64L away, 10 % cancels, sweeping MARKETs, OIDs
+    above 2^33: the 128-level windows re-centre and spill to far levels, and every batch is bit-exact
+    against the window-free oracle with no OUT_OF_WINDOW / BAD_SEQ reject."""
+    sc, base, batches = _drift_stream(me, 128, 256, 8192, 200, drift_every=5)
+    ob = orc.OracleBook(sc.num_symbols)
+    with engine_for(me, sc.num_symbols, sc.levels, base, sc.batch, 1 << 20) as eng:
+        for k, b in enumerate(batches):
+            r, f = eng.submit_batch(b)
+            ro, fo = ob.submit(b)
+            assert_results_equal(r, ro, f"drift b{k}")
+            assert_fills_equal(f, fo, f"drift b{k}")
+            no_window_rejects(r, f"drift b{k}")
+        assert_books_equal(eng, ob, range(sc.num_symbols), "drift")
+        assert eng.resting_count() == ob.resting()
+    # the stream really left the initial windows: LIMIT prices of the last batch moved ~10 windows
+    last = batches[-1]
+    lim = ((last.kind >> 2) & 3) == 0
+    moved = np.abs(last.price_q4[lim] - base[last.symbol[lim]])
+    assert np.median(moved) > 5 * sc.levels
+
+
+@pytest.mark.parametrize("group", [8, 32])
+def test_drifting_stream_device_groups_every_batch(me, orc, group):
+    """The drifting far-price stream through back-to-back device batches, `group` per launch: every
+    batch of every group is compared with the oracle (me_fetch_group_outputs)."""
+    sc, base, batches = _drift_stream(me, 128, 512, 16384, 2 * group, drift_every=3)
+    ob = orc.OracleBook(sc.num_symbols)
+    with engine_for(me, sc.num_symbols, sc.levels, base, sc.batch, 1 << 21, batches_per_launch=group) as eng:
+        for g0 in range(0, len(batches), group):
+            grp = batches[g0:g0 + group]
+            dbs = [eng.upload(b) for b in grp]
+            for db in dbs:
+                eng.submit_device(db)
+            eng.sync()
+            assert eng.last_group_size() == len(grp)
+            for k, b in enumerate(grp):
+                r, f = eng.fetch_group_outputs(k, len(b))
+                ro, fo = ob.submit(b)
+                assert_results_equal(r, ro, f"group {g0 // group} batch {k}")
+                assert_fills_equal(f, fo, f"group {g0 // group} batch {k}")
+                no_window_rejects(r)
+            for db in dbs:
+                db.free()
+        assert_books_equal(eng, ob, range(0, sc.num_symbols, 3), "drift groups")
+        assert eng.resting_count() == ob.resting()
+
+
+@pytest.mark.parametrize("levels", [1024, 4096])
+def test_drifting_mids_deep_windows(me, orc, levels):
+    """The same unbounded semantics on the deep-window kernel (LDS window at 1,024 levels, HBM window
+    at 4,096): mids trend 8 ticks per record of their symbol (several windows over the stream), far
+    LIMITs up to 64 windows away."""
+    sc, base, batches = _drift_stream(me, levels, 64, 4096, 40, drift_every=1, drift_step=8, far_pct=2)
+    ob = orc.OracleBook(sc.num_symbols)
+    with engine_for(me, sc.num_symbols, sc.levels, base, sc.batch, 1 << 18) as eng:
+        for k, b in enumerate(batches):
+            r, f = eng.submit_batch(b)
+            ro, fo = ob.submit(b)
+            assert_results_equal(r, ro, f"deep drift L={levels} b{k}")
+            assert_fills_equal(f, fo, f"deep drift L={levels} b{k}")
+            no_window_rejects(r)
+        assert_books_equal(eng, ob, range(sc.num_symbols), f"deep drift L={levels}")
+        assert eng.resting_count() == ob.resting()
+
+
+@pytest.mark.parametrize("levels", [128, 256])
+def test_seq_ring_sweeps_and_old_order_cancels(me, orc, levels):
+    """A 4,096-entry seq ring under a 60 %-cancel stream of 1,024-record batches: the ring wraps ~20
+    times, k_seq_sweep moves the horizon and rebuilds the old-order table each time, and cancels of
+    orders older than the ring still find them (or correctly miss dead ones)."""
+    sc = me.preset(5, num_symbols=16, levels=levels, batch=1024, seq_start=(1 << 40) + 3)
+    st = me.Stream(sc)
+    base = st.base_prices()
+    batches = [st.next(sc.batch) for _ in range(80)]
+    ob = orc.OracleBook(sc.num_symbols)
+    with engine_for(me, sc.num_symbols, sc.levels, base, sc.batch, 1 << 16, seq_ring=4096,
+                    batches_per_launch=1) as eng:
+        nf = run_both(eng, ob, batches, ctx=f"ring L={levels}")
+    assert nf > 0
+
+
+def test_seq_ring_span_and_order_are_loud(me):
+    B, L = me.SIDE_BUY, me.TYPE_LIMIT
+    with engine_for(me, 1, 128, [1000], 256, 256, seq_ring=1024) as eng:
+        b = _rows(me, [(0, B, L, 0, 1000, 1)] * 2, start_seq=10)
+        b.seq[1] = 10 + 5000  # one batch spans more than the ring
+        with pytest.raises(me.EngineError, match="seq ring"):
+            eng.submit_batch(b)
+    with engine_for(me, 1, 128, [1000], 256, 256) as eng:
+        eng.submit_batch(_rows(me, [(0, B, L, 0, 1000, 1)], start_seq=100))
+        with pytest.raises(me.EngineError, match="ascending"):
+            eng.submit_batch(_rows(me, [(0, B, L, 0, 1000, 1)], start_seq=50))
+
+
 # ---------------------------------------------------------------- edge cases
-def _rows(me, rows, start_seq=1):
-    n = len(rows)
-    return me.Batch(np.arange(start_seq, start_seq + n, dtype=np.uint64), [r[4] for r in rows],
-                    [r[5] for r in rows], [r[0] for r in rows], [me.kind(r[1], r[2], r[3]) for r in rows])
-
-
-def test_edge_semantics_and_rejects(me, orc):
+@pytest.mark.parametrize("levels", [64, 128, 512])
+def test_edge_semantics_and_rejects(me, orc, levels):
     B, S, L, M = me.SIDE_BUY, me.SIDE_SELL, me.TYPE_LIMIT, me.TYPE_MARKET
+    I64 = (1 << 63) - 1
     rows = [
         (0, B, L, 0, 1000, 5), (0, B, L, 0, 999, 5), (0, B, L, 0, 1128, 5), (1, 0, L, 0, 5001, 5),
         (0, B, L, 0, 1001, 0), (7, B, L, 0, 1001, 1), (1, S, L, 1, 1, 0), (0, S, L, 1, 1, 0), (0, S, L, 1, 1, 0),
         (0, S, L, 1, 12, 0), (0, B, M, 0, 0, 3), (1, 3, M, 0, 0, 3), (0, S, L, 1, 1 << 40, 0),
         (1, S, L, 0, 5127, 2), (1, B, M, 0, 123, 5), (1, S, L, 0, 5000, 7), (1, B, L, 0, 5127, 9),
+        # int64 extremes: asks far above, bids far below, then sweeps through all of them
+        (1, S, L, 0, I64, 4), (1, S, L, 0, 10 ** 15, 4), (1, B, L, 0, -(1 << 62), 3), (1, B, L, 0, -(1 << 63), 2),
+        (1, B, M, 0, 0, 20), (1, S, L, 0, -(1 << 63), 9), (1, S, L, 1, 19, 0), (1, B, L, 0, 7, 3),
     ]
     b = _rows(me, rows)
-    ob = orc.OracleBook(2, 128, [1000, 5000], 1 << 10)
-    with engine_for(me, 2, 128, [1000, 5000], 64, 256, 1 << 10) as eng:
+    ob = orc.OracleBook(2)
+    with engine_for(me, 2, levels, [1000, 5000], 64, 256) as eng:
         run_both(eng, ob, [b], ctx="edge")
-        run_both(eng, ob, [_rows(me, [(0, B, L, 0, 1000, 1)], start_seq=1 << 10)], ctx="bad seq")
-        r, f = eng.submit_batch(_rows(me, [], start_seq=2000))
+        run_both(eng, ob, [_rows(me, [(0, B, L, 0, 1000, 1)], start_seq=1 << 44)], ctx="big seq")
+        r, f = eng.submit_batch(_rows(me, [], start_seq=(1 << 44) + 10))
         assert len(r) == 0 and len(f) == 0
 
 
 def test_edge_deep_sweep_multi_window_multi_chunk(me, orc):
     """Sweeps crossing >64 levels (several ballot windows) and levels holding >32 orders (several
-    FIFO chunks), cancels inside chunks, then chunk reuse from the free list."""
+    FIFO chunks), cancels inside chunks, then chunk reuse from the free list; with a deep window
+    and with a 128-level window the 300 ask levels mostly live in far levels."""
     B, S, L, M = me.SIDE_BUY, me.SIDE_SELL, me.TYPE_LIMIT, me.TYPE_MARKET
     rows = []
     for lvl in range(300):                     # 300 ask levels, 1..3 orders each
@@ -149,13 +271,13 @@ def test_edge_deep_sweep_multi_window_multi_chunk(me, orc):
     b3 = _rows(me, sweeps, start_seq=seq)
     seq += len(sweeps)
     refill = _rows(me, [(0, B, L, 0, 9000 + (k % 5), 3) for k in range(200)], start_seq=seq)
-    base = [8000]
-    ob = orc.OracleBook(1, 4096, base, 1 << 20)
-    with engine_for(me, 1, 4096, base, 1024, 4096, 1 << 20, max_chunks=4096) as eng:
-        run_both(eng, ob, [b1, b2, b3, refill], ctx="deep sweep")
-        bids, asks = eng.snapshot(0, 5)
-        obids, oasks = ob.snapshot(0, 5)
-        assert np.array_equal(bids, obids) and np.array_equal(asks, oasks)
+    for levels, base in ((4096, 8000), (128, 9950)):
+        ob = orc.OracleBook(1)
+        with engine_for(me, 1, levels, [base], 1024, 4096, max_chunks=4096) as eng:
+            run_both(eng, ob, [b1, b2, b3, refill], ctx=f"deep sweep L={levels}")
+            bids, asks = eng.snapshot(0, 5)
+            obids, oasks = ob.snapshot(0, 5)
+            assert np.array_equal(bids, obids) and np.array_equal(asks, oasks)
 
 
 def test_edge_one_symbol_whole_batch_and_tile_boundaries(me, orc):
@@ -166,13 +288,13 @@ def test_edge_one_symbol_whole_batch_and_tile_boundaries(me, orc):
     base = st.base_prices()
     sizes = [65536, 4095, 4096, 4097, 1023, 1024, 1025, 1, 63, 64, 65]
     batches = [st.next(n) for n in sizes]
-    ob = orc.OracleBook(1, sc.levels, base, 1 << 22)
-    with engine_for(me, 1, sc.levels, base, 65536, 1 << 18, 1 << 22) as eng:
+    ob = orc.OracleBook(1)
+    with engine_for(me, 1, sc.levels, base, 65536, 1 << 18) as eng:
         run_both(eng, ob, batches, ctx="tiles")
 
 
 def test_edge_bucket_boundaries(me, orc):
-    """Register-ladder grouping: per-symbol record counts on both sides of one block (64) and of the
+    """Register-window grouping: per-symbol record counts on both sides of one block (64) and of the
     bucket capacity (128; more records take the batch rescan), and more bad-symbol records than a
     bucket holds — interleaved at random, several batches so the bucket counters are reused."""
     B, S, L, M = me.SIDE_BUY, me.SIDE_SELL, me.TYPE_LIMIT, me.TYPE_MARKET
@@ -197,8 +319,8 @@ def test_edge_bucket_boundaries(me, orc):
                 rows.append((sy, side, L, 0, px, int(rng.integers(1, 60))))
         batches.append(_rows(me, rows, start_seq=seq))
         seq += len(rows)
-    ob = orc.OracleBook(nsym, 128, base, 1 << 16)
-    with engine_for(me, nsym, 128, base, 4096, 1 << 14, 1 << 16) as eng:
+    ob = orc.OracleBook(nsym)
+    with engine_for(me, nsym, 128, base, 4096, 1 << 14) as eng:
         run_both(eng, ob, batches, ctx="buckets")
 
 
@@ -209,8 +331,8 @@ def test_edge_symbol_count_sort_plans(me, orc):
         st = me.Stream(sc)
         base = st.base_prices()
         batches = [st.next(20000) for _ in range(2)]
-        ob = orc.OracleBook(S, sc.levels, base, 1 << 22)
-        with engine_for(me, S, sc.levels, base, 20000, 1 << 17, 1 << 22) as eng:
+        ob = orc.OracleBook(S)
+        with engine_for(me, S, sc.levels, base, 20000, 1 << 17) as eng:
             run_both(eng, ob, batches, book_symbols=range(0, S, max(1, S // 50)), ctx=f"S={S}")
 
 
@@ -219,9 +341,9 @@ def test_cancelled_chunks_are_unlinked(me, orc):
     (head, middle, tail) must be unlinked and reused, so a 4-chunk pool suffices for 30 rounds."""
     B, S, L, M = me.SIDE_BUY, me.SIDE_SELL, me.TYPE_LIMIT, me.TYPE_MARKET
     C = me._abi.CHUNK_SLOTS
-    ob = orc.OracleBook(1, 128, [1000], 1 << 20)
+    ob = orc.OracleBook(1)
     seq = 1
-    with engine_for(me, 1, 128, [1000], 4 * C, 4 * C, 1 << 20, max_chunks=4) as eng:
+    with engine_for(me, 1, 128, [1000], 4 * C, 4 * C, max_chunks=4) as eng:
         run_both(eng, ob, [_rows(me, [(0, B, L, 0, 1050, 7)], start_seq=seq)], ctx="anchor")
         seq += 1
         for rnd in range(30):
@@ -243,11 +365,16 @@ def test_cancelled_chunks_are_unlinked(me, orc):
 def test_capacity_exhaustion_is_loud(me):
     B, L = me.SIDE_BUY, me.TYPE_LIMIT
     rows = [(0, B, L, 0, 1000 + (k % 64), 1) for k in range(200)]  # 64 levels -> needs >= 64 chunks
-    with engine_for(me, 1, 128, [1000], 256, 16, 1 << 20, max_chunks=8) as eng:
+    with engine_for(me, 1, 128, [1000], 256, 16, max_chunks=8) as eng:
         with pytest.raises(me.EngineError, match="chunk pool"):
             eng.submit_batch(_rows(me, rows))
         with pytest.raises(me.EngineError):
             eng.submit_batch(_rows(me, rows[:1], start_seq=500))  # failed state is sticky
+    # far levels beyond their array: a best bid in the window, then 40 distinct bids far below it
+    rows = [(0, B, L, 0, 5000, 1)] + [(0, B, L, 0, 100 + 3 * k, 1) for k in range(40)]
+    with engine_for(me, 1, 128, [4990], 256, 256, far_levels=16) as eng:
+        with pytest.raises(me.EngineError, match="far-level"):
+            eng.submit_batch(_rows(me, rows))
 
 
 def test_device_resident_path_matches_host_path(me, orc):
@@ -255,8 +382,8 @@ def test_device_resident_path_matches_host_path(me, orc):
     st = me.Stream(sc)
     base = st.base_prices()
     batches = [st.next(sc.batch) for _ in range(6)]
-    ob = orc.OracleBook(sc.num_symbols, sc.levels, base, 1 << 22)
-    with engine_for(me, sc.num_symbols, sc.levels, base, sc.batch, 1 << 18, 1 << 22) as eng:
+    ob = orc.OracleBook(sc.num_symbols)
+    with engine_for(me, sc.num_symbols, sc.levels, base, sc.batch, 1 << 18) as eng:
         dbs = [eng.upload(b) for b in batches]
         for b, db in zip(batches, dbs):
             eng.submit_device(db)
@@ -267,7 +394,7 @@ def test_device_resident_path_matches_host_path(me, orc):
         assert_books_equal(eng, ob, range(sc.num_symbols), "device path")
 
 
-# ---------------------------------------------------------------- BASELINE size (config 2)
+# ---------------------------------------------------------------- BASELINE sizes
 def test_full_size_config2_bitexact(me, orc):
     """BASELINE.json configs[1] at its real size (1,024 symbols, 65,536-record batches): 24
     consecutive batches compared record-for-record and fill-for-fill, plus size-independent
@@ -275,8 +402,8 @@ def test_full_size_config2_bitexact(me, orc):
     sc = me.preset(2)
     st = me.Stream(sc)
     base = st.base_prices()
-    ob = orc.OracleBook(sc.num_symbols, sc.levels, base, 1 << 26)
-    with engine_for(me, sc.num_symbols, sc.levels, base, sc.batch, 1 << 21, 1 << 26) as eng:
+    ob = orc.OracleBook(sc.num_symbols)
+    with engine_for(me, sc.num_symbols, sc.levels, base, sc.batch, 1 << 21, seq_ring=1 << 26) as eng:
         for k in range(24):
             b = st.next(sc.batch)
             r, f = eng.submit_batch(b)
@@ -291,6 +418,59 @@ def test_full_size_config2_bitexact(me, orc):
         assert_books_equal(eng, ob, range(0, sc.num_symbols, 7), "full c2")
         assert eng.resting_count() == ob.resting()
 
+
+@pytest.mark.parametrize("group", [32, 64])
+def test_every_batch_of_full_groups(me, orc, group):
+    """The bench's pattern at full config-2 size — device batches back to back, `group` per launch —
+    with EVERY batch of two full groups compared against the oracle, record for record."""
+    sc = me.preset(2)
+    st = me.Stream(sc)
+    base = st.base_prices()
+    ob = orc.OracleBook(sc.num_symbols)
+    with engine_for(me, sc.num_symbols, sc.levels, base, sc.batch, 1 << 21, seq_ring=1 << 26,
+                    batches_per_launch=group) as eng:
+        for gi in range(2):
+            batches = [st.next(sc.batch) for _ in range(group)]
+            dbs = [eng.upload(b) for b in batches]
+            for db in dbs:
+                eng.submit_device(db)
+            eng.sync()
+            assert eng.last_group_size() == group
+            for k, b in enumerate(batches):
+                r, f = eng.fetch_group_outputs(k, len(b))
+                ro, fo = ob.submit(b)
+                assert_results_equal(r, ro, f"G={group} group {gi} batch {k}")
+                assert_fills_equal(f, fo, f"G={group} group {gi} batch {k}")
+            for db in dbs:
+                db.free()
+        assert_books_equal(eng, ob, range(0, sc.num_symbols, 5), f"G={group}")
+        assert eng.resting_count() == ob.resting()
+
+
+def test_config3_grouped_bench_shape(me, orc):
+    """The bench's config-3 shape per GPU: 12,500 symbols (more than one round of waves), 131,072-
+    record batches, 32 per launch; every batch of the group against the oracle."""
+    sc = me.preset(3, num_symbols=12_500, batch=131_072)
+    st = me.Stream(sc)
+    base = st.base_prices()
+    batches = [st.next(sc.batch) for _ in range(32)]
+    ob = orc.OracleBook(sc.num_symbols)
+    with engine_for(me, sc.num_symbols, sc.levels, base, sc.batch, 1 << 22, seq_ring=1 << 26,
+                    batches_per_launch=32) as eng:
+        dbs = [eng.upload(b) for b in batches]
+        for db in dbs:
+            eng.submit_device(db)
+        eng.sync()
+        assert eng.last_group_size() == 32
+        for k, b in enumerate(batches):
+            r, f = eng.fetch_group_outputs(k, len(b))
+            ro, fo = ob.submit(b)
+            assert_results_equal(r, ro, f"c3 batch {k}")
+            assert_fills_equal(f, fo, f"c3 batch {k}")
+        assert_books_equal(eng, ob, range(0, sc.num_symbols, 97), "c3 grouped")
+        assert eng.resting_count() == ob.resting()
+        for db in dbs:
+            db.free()
 
 
 @pytest.mark.parametrize("group", [1, 3, 8, 32, 64])
@@ -308,9 +488,8 @@ def test_back_to_back_device_batches(me, orc, group, stream):
     if stream == "skewed":
         for k, b in enumerate(batches):
             b.symbol[k * 97 % len(b)::4099] = sc.num_symbols + 3  # unknown symbols
-    ob = orc.OracleBook(sc.num_symbols, sc.levels, base, 1 << 22)
-    with engine_for(me, sc.num_symbols, sc.levels, base, sc.batch, 1 << 20, 1 << 22,
-                    batches_per_launch=group) as eng:
+    ob = orc.OracleBook(sc.num_symbols)
+    with engine_for(me, sc.num_symbols, sc.levels, base, sc.batch, 1 << 20, batches_per_launch=group) as eng:
         dbs = [eng.upload(b) for b in batches]
         eng.timing_enable(True)
         for db in dbs:
@@ -336,8 +515,8 @@ def test_partial_groups_between_fetches(me, orc):
     sc = me.preset(2, num_symbols=512, batch=8192)
     st = me.Stream(sc)
     base = st.base_prices()
-    ob = orc.OracleBook(sc.num_symbols, sc.levels, base, 1 << 22)
-    with engine_for(me, sc.num_symbols, sc.levels, base, sc.batch, 1 << 18, 1 << 22) as eng:
+    ob = orc.OracleBook(sc.num_symbols)
+    with engine_for(me, sc.num_symbols, sc.levels, base, sc.batch, 1 << 18) as eng:
         for run in (1, 7, 2, 8, 5, 3):
             batches = [st.next(sc.batch) for _ in range(run)]
             dbs = [eng.upload(b) for b in batches]

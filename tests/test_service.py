@@ -79,8 +79,10 @@ def test_schema_matches_reference(me, tmp_path):
 def test_persisted_rows_match_reference(me, tmp_path):
     """tests/test_submit_order.cpp:56-79 plus the whole contract: rows as insert_new_order writes them."""
     db = str(tmp_path / "server_test.sqlite")
-    base = [0, 0]  # windows: SYM and ABC levels cover the small test prices
-    with me.Engine(2, 1 << 20, [-100, -100], max_batch=1024, max_resting=1024, max_seq=1 << 20) as eng:
+    # 128-level windows far from the contract's prices (Q4 0 .. 10^9): every order rests through the
+    # far levels and window re-centring, as an unbounded book must
+    base = [5_000_000, 5_000_000]
+    with me.Engine(2, 128, base, max_batch=1024, max_resting=1024) as eng:
         svc = me.MatchingEngineService(eng, ["SYM", "ABC"], db_path=db)
         got = _submit_all(svc, _cases())
         svc.flush()
@@ -110,10 +112,10 @@ def test_submitorder_stream_matches_oracle_and_db(me, tmp_path):
     mids = {s: 1_000_000 + 1000 * i for i, s in enumerate(syms)}
     base = np.array([mids[s] - 64 for s in syms], dtype=np.int64)
     db = str(tmp_path / "flow.sqlite")
-    eng = me.Engine(len(syms), 128, base, max_batch=4096, max_resting=1 << 14, max_seq=1 << 20)
+    eng = me.Engine(len(syms), 128, base, max_batch=4096, max_resting=1 << 14)
     svc = me.MatchingEngineService(eng, syms, db_path=db)
     osvc = OracleService(1)
-    ob = OracleBook(len(syms), 128, base, 1 << 20)
+    ob = OracleBook(len(syms))
     all_fills = 0
     for slice_no in range(4):
         seqs, px, qty, sid, kinds = [], [], [], [], []
@@ -199,9 +201,9 @@ def test_cancels_and_order_update_stream(me, tmp_path):
     mids = {s: 1_000_000 + 1000 * i for i, s in enumerate(syms)}
     base = np.array([mids[s] - 64 for s in syms], dtype=np.int64)
     db = str(tmp_path / "cancel.sqlite")
-    eng = me.Engine(len(syms), 128, base, max_batch=4096, max_resting=1 << 14, max_seq=1 << 20)
+    eng = me.Engine(len(syms), 128, base, max_batch=4096, max_resting=1 << 14)
     svc = me.MatchingEngineService(eng, syms, db_path=db)
-    ob = OracleBook(len(syms), 128, base, 1 << 20)
+    ob = OracleBook(len(syms))
     accepted = []  # (oid, symbol) of LIMIT orders
     events = []
     for slice_no in range(4):

@@ -37,7 +37,7 @@ def main():
     seeds = st.seed_books(range(a.seed_top), a.per_side) if a.seed_top else None
     nseed = len(seeds) if seeds is not None else 0
     eng = me.Engine(sc.num_symbols, sc.levels, base, max_batch=max(sc.batch, min(nseed, 1 << 20)),
-                    max_resting=(1 << 23) + nseed, max_seq=1 << 30)
+                    max_resting=(1 << 23) + nseed)
     for i in range(0, nseed, 1 << 20):
         eng.submit_batch(seeds.take(slice(i, i + (1 << 20))), want_fills=False)
     hot = np.zeros(24, dtype=np.float64)
