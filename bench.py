@@ -63,6 +63,8 @@ def parse():
                          "BASELINE configs as secondary lines (DESIGN.md §7)")
     ap.add_argument("--symbols-per-gpu", type=int, default=None)
     ap.add_argument("--batch-per-gpu", type=int, default=None)
+    ap.add_argument("--seq-ring", type=int, default=1 << 28,
+                    help="me_config.seq_ring (seq-ring entries for cancels; 2^28 is the engine default)")
     ap.add_argument("--batches-per-launch", type=int, default=0,
                     help="batches matched per kernel launch (me_config.batches_per_launch; 0 = engine default 32)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample")
@@ -260,7 +262,7 @@ def main():
     n_seed = sum(len(b) for b in seeds)
     eng = me.Engine(len(ids), sc.levels, base,
                     max_batch=max(len(b) for b in batches + gather_batches + e2e_batches + seeds) + 1,
-                    max_resting=total_local // 3 + n_seed + 65536,
+                    max_resting=total_local // 3 + n_seed + 65536, seq_ring=args.seq_ring,
                     device=local, symbol_ids=ids, batches_per_launch=args.batches_per_launch)
     for b in seeds:
         eng.submit_batch(b, want_fills=False)

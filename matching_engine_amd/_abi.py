@@ -155,7 +155,10 @@ def load() -> C.CDLL:
     except ImportError:
         pass
     lib = C.CDLL(LIB_PATH)
+    variant = bool(os.environ.get("ME_ENGINE_LIB"))  # an older build in an A/B run may lack newer entries
     for name, (res, args) in PROTOTYPES.items():
+        if variant and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -169,7 +169,7 @@ static void free_all(me_engine* e) {
                   e->bk.loc,      e->bk.chunk_top, e->bk.err,       (void*)e->bk.gsym,
                   e->d_seq,       e->d_px,        e->d_qty,       e->d_sym,         e->d_kind,
                   e->d_tape,      e->d_tape_count, e->d_fills_acc, e->bk.dbg,      e->bk.fcache,
-                  e->bk.far,      e->bk.old,       e->bk.sq};
+                  e->bk.far,      e->bk.old,       e->bk.sq,       e->bk.hcount,     e->bk.hand};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   {
@@ -353,6 +353,8 @@ extern "C" me_engine* me_create(const me_config* cfg) {
   ALLOC(bk.far, S * 2 * (uint64_t)bk.fcap);
   ALLOC(bk.old, oldn);
   ALLOC(bk.sq, 2);
+  ALLOC(bk.hcount, 1);
+  ALLOC(bk.hand, S);
   ALLOC(bk.chunk_top, 1);
   ALLOC(bk.err, 1);
   uint32_t* gsym = nullptr;
@@ -430,6 +432,7 @@ extern "C" me_engine* me_create(const me_config* cfg) {
             launch_init_chunks(st, bk.chunks, nchunks) == hipSuccess &&
             hipMemsetAsync(bk.loc, 0xFF, ring * sizeof(uint32_t), st) == hipSuccess &&
             hipMemsetAsync(bk.old, 0, oldn * sizeof(OldEnt), st) == hipSuccess &&
+            hipMemsetAsync(bk.hcount, 0, 4, st) == hipSuccess &&
             hipMemcpyAsync(bk.sq, sq0, sizeof sq0, hipMemcpyHostToDevice, st) == hipSuccess &&
             hipMemsetAsync(bk.fcache, 0xFF, S * 64 * sizeof(uint32_t), st) == hipSuccess &&
             hipMemsetAsync(bk.chunk_top, 0, 4, st) == hipSuccess && hipMemsetAsync(bk.err, 0, 4, st) == hipSuccess &&
@@ -507,7 +510,9 @@ static int seq_sweep(me_engine* e, const me_engine::Group& g) {
     seq[k] = g.b[k].seq;
     n[k] = g.b[k].n;
   }
-  hipError_t he = launch_seq_sweep(e->stream, e->bk, seq, n, g.n, e->sq_idx, 4 * e->ncu);
+  // a small grid: the launch is on the stream before every match launch and usually decides "no
+  // sweep" (a 1,024-workgroup grid cost ~0.7 us per batch at config 2); a due sweep loops over the pool
+  hipError_t he = launch_seq_sweep(e->stream, e->bk, seq, n, g.n, e->sq_idx, 64);
   if (he != hipSuccess) return e->hip_fail(he, "seq sweep launch");
   e->sq_idx ^= 1u;
   e->bk.sq_idx = e->sq_idx;

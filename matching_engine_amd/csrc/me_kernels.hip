@@ -1261,6 +1261,7 @@ __global__ __launch_bounds__(256) void k_seq_sweep(BookDev bk, SeqGroup sg) {
     o.epoch = epoch;
     o.pad[0] = o.pad[1] = o.pad[2] = 0;
     bk.sq[sg.in ^ 1u] = o;
+    *bk.hcount = 0;  // the match launch after this one hands symbols off from 0
   }
   if (!need) return;
   const uint32_t top = min(*bk.chunk_top, bk.nchunks);

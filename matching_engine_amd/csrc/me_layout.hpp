@@ -131,6 +131,15 @@ struct alignas(8) BkRec {
   uint32_t ok;  // batch index | (kind & 15) << BK_KIND_SHIFT
 };
 
+// A symbol the register-window kernel handed to its continuation launch (me_match_reg.hip): its
+// records from position `pos` (in the symbol's batch order) of batch `g` of the group on. Written
+// before the record at `pos` changed anything; wptr / wend: the scratch run of batch g.
+struct Handoff {
+  uint32_t s, g, pos, nsg;
+  uint32_t wptr, wend;
+  uint32_t pad[2];
+};
+
 struct BookDev {
   Level* levels;
   unsigned long long* occ;
@@ -146,6 +155,8 @@ struct BookDev {
   FarLevel* far;          // [S][2][fcap]
   OldEnt* old;            // [old_mask + 1]
   SeqState* sq;           // [2]
+  uint32_t* hcount;       // hand-offs of the current match launch (zeroed by k_seq_sweep)
+  Handoff* hand;          // [S]
   unsigned long long ring_mask;
   unsigned long long old_mask;
   uint32_t fcap;

@@ -501,6 +501,11 @@ __device__ __forceinline__ bool reg_rest(RegCtx& c, int lvl, unsigned long long 
 // names its slot unless a later seq overwrote the entry, in which case an order older than the
 // horizon is in the old-order table; every candidate slot is verified (owner, seq, qty > 0). A chunk
 // left without live orders is unlinked at once (chunks in use never exceed resting orders).
+// kSlow = false (k_match_reg<false>): a window order named by its ring entry is cancelled here; every
+// other case (a far level, a stale ring entry of an order older than the horizon) returns HANDOFF
+// before anything changed, and the continuation launch (kSlow = true) does the whole cancel.
+constexpr uint32_t HANDOFF = 0xFFFFFFFFu;
+template <bool kSlow>
 __device__ __forceinline__ uint32_t reg_cancel(RegCtx& c, unsigned long long tgt) {
   const int lane = lane_id();
   const bool act = lane < ME_C;
@@ -535,7 +540,10 @@ __device__ __forceinline__ uint32_t reg_cancel(RegCtx& c, unsigned long long tgt
         if (q <= 0) return 0;
         const uint32_t nxt = rl32(hdr.next, 0), prv = rl32(hdr.prev, 0);
         if (ME_UNLIKELY(!inw)) {  // a far level (me_far.hpp)
-          return far_cancel(c, prc < rli64(c.base, 0) ? 0u : 1u, prc, ch, slot, q, qv, nxt, prv);
+          if constexpr (kSlow)
+            return far_cancel(c, prc < rli64(c.base, 0) ? 0u : 1u, prc, ch, slot, q, qv, nxt, prv);
+          else
+            return HANDOFF;
         }
         const uint32_t t = c.tl.get(lvl);
         const uint32_t h = hv == NIL ? NIL : (hv & ~HC);
@@ -587,8 +595,12 @@ __device__ __forceinline__ uint32_t reg_cancel(RegCtx& c, unsigned long long tgt
     }
     // the ring entry is someone else's: only an order older than the horizon can still be live
     if (pass != 0 || tgt >= ldsu(c.M->horizon)) return 0;
-    g = old_lookup(ldsg(c.G->bk.old), ldsu(c.G->bk.old_mask), ldsu(c.M->epoch), tgt);
-    if (g == NIL) return 0;
+    if constexpr (kSlow) {
+      g = old_lookup(ldsg(c.G->bk.old), ldsu(c.G->bk.old_mask), ldsu(c.M->epoch), tgt);
+      if (g == NIL) return 0;
+    } else {
+      return HANDOFF;
+    }
   }
 }
 
@@ -998,6 +1010,7 @@ __device__ __forceinline__ void aux_tape_tile(const ColdArgs& G, uint32_t jb, ui
 }
 
 // Side-job wave a of A: its share of every bucket / clear job of group J and every tape job of J-2.
+// Side-job wave a of A: its share of every bucket / clear job of group J and every tape job of J-2.
 __device__ __forceinline__ void aux_jobs(const ColdArgs& G, uint32_t a, uint32_t A) {
   const int lane = lane_id();
   const uint32_t nb = ldsu(G.ax.nb);
@@ -1043,23 +1056,35 @@ __device__ __forceinline__ uint32_t make_cw(long long opx, uint32_t kd, long lon
          (far ? CW_FAR : 0u) | (!market && !inw ? CW_OUT : 0u);
 }
 
+// One wavefront per symbol. kSlow = false: the common launch — every symbol of the group, no far-level
+// code at all (it cost the serial loop 19-27 % through register allocation even when never run,
+// DESIGN.md §8): a record that needs a far level (a LIMIT priced outside the window, a MARKET while the
+// opposite side has far levels, a cancel of a far or old order) hands its symbol off before it changes
+// anything. kSlow = true: the continuation launch right after it — the handed-off symbols only, from
+// their hand-off record to the end of the group, with the far-level code inline.
+template <bool kSlow>
 __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
   __shared__ RegLds lds[REG_WAVES];
   __shared__ ColdArgs G;
   static_assert(sizeof(ColdArgs) % 8 == 0, "ColdArgs copy");
+  const BookDev& bk = args.bk;
+  uint32_t nhand = 0;
+  if constexpr (kSlow) {  // nothing handed off (the usual case): leave before the argument copy
+    nhand = min(*(volatile uint32_t*)bk.hcount, bk.S);
+    if (blockIdx.x * REG_WAVES >= nhand) return;
+  }
   {
     for (uint32_t i = threadIdx.x; i < sizeof(ColdArgs) / 8; i += 128 * REG_WAVES)
       reinterpret_cast<unsigned long long*>(&G)[i] = reinterpret_cast<const unsigned long long*>(&args)[i];
     __syncthreads();
   }
-  const BookDev& bk = args.bk;
   const int lane = lane_id();
   // wave index: readfirstlane tells the divergence analysis it is wave-uniform (threadIdx.x >> 6 is
   // not recognised as such), so every per-symbol value and branch below is scalar
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (wv >= (uint32_t)REG_WAVES) {  // side-job wave (only in the workgroups of the first dispatch round)
     const uint32_t k = wv - REG_WAVES, nwg = max(min(args.ax.nwg, gridDim.x), 1u);
-    if (blockIdx.x < nwg) aux_jobs(G, blockIdx.x * REG_WAVES + k, nwg * REG_WAVES);
+    if (!kSlow && blockIdx.x < nwg) aux_jobs(G, blockIdx.x * REG_WAVES + k, nwg * REG_WAVES);
     return;
   }
 #ifndef ME_NO_SETPRIO
@@ -1067,9 +1092,24 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
   // jobs are latency work with slack until the next launch)
   __builtin_amdgcn_s_setprio(3);
 #endif
-  const uint32_t s = blockIdx.x * REG_WAVES + wv;
   const uint32_t ng = args.ng;
-  if (ng == 0u || s > bk.S) return;  // no match job in this launch / no symbol
+  if (ng == 0u) return;  // no match job in this launch
+  // kSlow: hand-off entries wv, wv + REG_WAVES * gridDim.x, ... of this workgroup's share
+  for (uint32_t hi_ = blockIdx.x * REG_WAVES + wv; !kSlow || hi_ < nhand; hi_ += REG_WAVES * gridDim.x) {
+  Handoff ho{};
+  uint32_t s;
+  if constexpr (kSlow) {
+    ho = bk.hand[hi_];
+    s = rl32(ho.s, 0);
+    ho.g = rl32(ho.g, 0);
+    ho.pos = rl32(ho.pos, 0);
+    ho.nsg = rl32(ho.nsg, 0);
+    ho.wptr = rl32(ho.wptr, 0);
+    ho.wend = rl32(ho.wend, 0);
+  } else {
+    s = blockIdx.x * REG_WAVES + wv;
+    if (s > bk.S) return;  // no symbol
+  }
 #ifdef ME_STAMPS
   unsigned long long st_t0 = stamp_now();
 #endif
@@ -1084,6 +1124,9 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
     const uint32_t gl = min((uint32_t)lane, ng - 1u);
     const uint32_t* cp = G.bt[gl].bcnt;
     nsv = (uint32_t)lane < ng ? cp[(size_t)s * BK_CNT_STRIDE] : 0u;
+    if constexpr (kSlow) {  // batches before the hand-off are done; its own counter is already reset
+      nsv = (uint32_t)lane < ho.g ? 0u : ((uint32_t)lane == ho.g ? ho.nsg : nsv);
+    }
     ns = 0;
   } else if (args.bt[0].bin_start) {  // single-pass sort: the run table
     lo = args.bt[0].bin_start[s];
@@ -1109,8 +1152,11 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
     for (int d = 1; d < 8; d <<= 1) t += __shfl_xor(t, d, 64);
     ns = (uint32_t)rli64(t, 0);
   }
-  if (ns == 0u) return;
-  if (s == bk.S) {  // the sort path's bad-symbol bin (bucketed batches carry none)
+  if (ns == 0u) {
+    if constexpr (kSlow) continue;
+    else return;
+  }
+  if (!kSlow && s == bk.S) {  // the sort path's bad-symbol bin (bucketed batches carry none)
     reject_bad_run(G, lo, lo + ns);
     return;
   }
@@ -1162,7 +1208,7 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
   c.wend = 0;
   c.recs_left = ns;
   // ---- the batches of the group, in stream order; the book stays on chip between them
-  ldsw(c.M->g_next, 0u);
+  ldsw(c.M->g_next, kSlow ? ho.g : 0u);
   ldsw(c.M->run_lo, lo);  // the sort path's run (one batch)
   ldsw(c.M->run_n, ns);
   for (;;) {  // the batch cursor lives in LDS: no SGPR of it is live across the serial loop
@@ -1208,7 +1254,15 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
     c.scratch = vptr(ldsu(G.bt[g].scratch));
     c.wptr = s * ldsu(G.bt[g].slab);
     c.wend = c.wptr + ldsu(G.bt[g].slab);
-    c.recs_left = nsg;
+    uint32_t skip = 0;  // (continuation) records of the hand-off batch the common launch finished
+    if constexpr (kSlow) {
+      if (g == ho.g) {
+        skip = ho.pos;
+        c.wptr = ho.wptr;
+        c.wend = ho.wend;
+      }
+    }
+    c.recs_left = nsg - skip;
     if (lane == 0) {  // read back where used: nothing of this holds an SGPR across the serial loop
       c.M->mode = mode;
       c.M->scan_cur = 0;
@@ -1256,10 +1310,11 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
       }
       const uint32_t j = (uint32_t)lane;  // record j of the block
       const uint32_t hi = cnt;
+      const uint32_t vis = nsg - left;    // records of the batch before this block
       // validation in vector form; only the packed control word and the reject code stay live
       uint32_t cw, rj;
       {
-        const bool v = j < hi;
+        const bool v = j < hi && (!kSlow || vis + j >= skip);
         const unsigned long long oseq = v ? oseq_ : 0ull;
         const int oq = v ? oq_ : 0;
         const uint32_t kd = v ? kd_ : 0u;
@@ -1275,10 +1330,11 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
             rj = ME_RJ_BAD_SEQ;  // no OID is 0 (the counter starts at 1, storage.cpp:254-267)
         }
         cw = make_cw(v ? opx_ : 0ll, kd, c.base, L);
-        if (!v) rj = 0xFFu;  // lanes past the run: no record
+        if (!v) rj = 0xFFu;  // lanes past the run (or before the continuation point): no record
       }
       unsigned long long work = __ballot(rj == ME_RJ_NONE);
       uint32_t stop = cnt;  // records [0, stop) of the block get results
+      bool handoff = false;
       uint32_t out_q = 0, out_n = 0, out_w = 0;
   #ifdef ME_STAMPS
       __builtin_amdgcn_s_waitcnt(0);
@@ -1294,9 +1350,22 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
         COUNT(c, CT_FAST);
         STAMP_ADD(c, PH_SWEEP);
         if (ME_UNLIKELY(ctl & CW_CXL)) {
-          outq = reg_cancel(c, (unsigned long long)rli64(opx_, k));
+          outq = reg_cancel<kSlow>(c, (unsigned long long)rli64(opx_, k));
+          if (!kSlow && ME_UNLIKELY(outq == HANDOFF)) {
+            stop = (uint32_t)k;
+            handoff = true;
+            break;
+          }
           STAMP_ADD(c, PH_CANCEL);
         } else {
+          const bool buy = (ctl & CW_BUY) != 0u;
+          if constexpr (!kSlow) {  // far levels ahead: hand the symbol off before anything changes
+            if (ME_UNLIKELY((ctl & CW_OUT) || ((ctl & CW_MKT) && c.fcount(buy ? 1u : 0u) != 0u))) {
+              stop = (uint32_t)k;
+              handoff = true;
+              break;
+            }
+          }
           if (ME_UNLIKELY(c.wptr + (uint32_t)c.resting > c.wend) && !reg_reserve_overflow(c)) {
             stop = (uint32_t)k;
             break;
@@ -1308,7 +1377,6 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
           uint32_t rem = q;
           // one walk loop for both sides (one copy of the walk): the opposite best moves away from
           // the taker's limit as levels empty
-          const bool buy = (ctl & CW_BUY) != 0u;
           int lvl = buy ? c.ba : c.bb;
           for (;;) {
             const int gap = buy ? lm - lvl : lvl - lm;  // >= 0: the level crosses the limit (int select, scalar)
@@ -1320,26 +1388,30 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
             c.ba = lvl;
           else
             c.bb = lvl;
-          // the window side is exhausted and the limit reaches further: far levels (rare)
-          if (ME_UNLIKELY(rem != 0u && (ctl & CW_FAR)) && c.fcount(buy ? 1u : 0u) != 0u)
-            rem -= far_take(c, buy, (ctl & CW_MKT) != 0u, (long long)rl64((unsigned long long)opx_, k), rem, seq);
+          int rr = 0;
+          if constexpr (kSlow) {
+            // the window side is exhausted and the limit reaches further: far levels
+            if (rem != 0u && (ctl & CW_FAR) && c.fcount(buy ? 1u : 0u) != 0u)
+              rem -= far_take(c, buy, (ctl & CW_MKT) != 0u, (long long)rl64((unsigned long long)opx_, k), rem, seq);
+            // a LIMIT priced outside the window rests through the far path (may re-centre the window)
+            if ((ctl & CW_OUT) && rem != 0u)
+              rr = reg_far_rest(c, (long long)rl64((unsigned long long)opx_, k), seq, rem, buy) < 0 ? -1 : 1;
+          }
           outq = q - rem;
           STAMP_ADD(c, PH_WALK);
           const bool me_ = lane == k;
           out_n = me_ ? c.wptr - w_in : out_n;
           out_w = me_ ? w_in : out_w;
-          if (!(ctl & CW_MKT) && rem != 0u) {
-            if (ME_UNLIKELY(ctl & CW_OUT)) {  // priced outside the window
-              const int rr = reg_far_rest(c, (long long)rl64((unsigned long long)opx_, k), seq, rem, buy);
-              if (rr < 0) {
-                stop = (uint32_t)k;
-                break;
-              }
-              if (rr > 0) cw = make_cw(j < hi ? opx_ : 0ll, j < hi ? kd_ : 0u, c.base, L);  // the window moved
-            } else if (ME_UNLIKELY(!reg_rest(c, lm, seq, rem, buy))) {
-              stop = (uint32_t)k;  // chunk pool exhausted: the batch fails (sticky error word)
+          if (kSlow && rr != 0) {
+            if (rr < 0) {
+              stop = (uint32_t)k;
               break;
             }
+            const bool v = j < hi && vis + j >= skip;
+            cw = make_cw(v ? opx_ : 0ll, v ? kd_ : 0u, c.base, L);  // the window may have moved
+          } else if (!(ctl & (CW_MKT | CW_OUT)) && rem != 0u && ME_UNLIKELY(!reg_rest(c, lm, seq, rem, buy))) {
+            stop = (uint32_t)k;  // chunk pool exhausted: the batch fails (sticky error word)
+            break;
           }
           STAMP_ADD(c, PH_REST);
         }
@@ -1380,8 +1452,24 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
         if (out_n) atomicAdd(&tile_sum[oi / TILE_TAPE], out_n);
       }
       STAMP_ADD(c, PH_RESULT);
+      if (!kSlow && handoff) {  // the rest of the symbol's records go to the continuation launch
+        uint32_t idx = 0;
+        if (lane == 0) idx = atomicAdd(ldsg(G.bk.hcount), 1u);
+        idx = rl32(idx, 0);
+        if (lane == 0) {
+          Handoff h;
+          h.s = s;
+          h.g = ldsu(c.M->g_cur);
+          h.pos = vis + stop;
+          h.nsg = nsg;
+          h.wptr = c.wptr;
+          h.wend = c.wend;
+          h.pad[0] = h.pad[1] = 0;
+          ldsg(G.bk.hand)[idx] = h;
+        }
+      }
       left -= cnt;
-      if (stop < cnt) {  // capacity failure: the sticky error word fails the launch
+      if (stop < cnt) {  // hand-off, or a capacity failure (the sticky error word fails the launch)
         ldsw(c.M->g_next, ME_GMAX);
         break;
       }
@@ -1448,13 +1536,18 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
   if (lane == 0 && dbg)
     for (int p = 0; p < PH_N; ++p) dbg[(size_t)s * 24 + p] = c.st[p];
 #endif
+  if constexpr (!kSlow) break;
+  }
 }
 
 // One launch: the match job of bt[0, ng) (ng == 0: none) on S / REG_WAVES workgroups (S + 1 for the
-// sort path's bad-symbol bin) and the side jobs of ax on the first dispatch round's extra waves.
+// sort path's bad-symbol bin) and the side jobs of ax on the first dispatch round's extra waves; then,
+// when it matched anything, the continuation launch over the symbols it handed off (64 workgroups,
+// which leave at once when there are none). ev0 / ev1 bracket both.
 hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* bt, uint32_t ng, const AuxDev& ax,
                             hipEvent_t ev0, hipEvent_t ev1) {
-  if (bk.L > (uint32_t)RL || bk.L < 64u || !bk.fcache || !bk.gsym) return hipErrorInvalidValue;
+  if (bk.L > (uint32_t)RL || bk.L < 64u || !bk.fcache || !bk.gsym || !bk.hand || !bk.hcount)
+    return hipErrorInvalidValue;
   if (ng > (uint32_t)ME_GMAX || ax.nb > (uint32_t)ME_GMAX || ax.nt > (uint32_t)ME_GMAX) return hipErrorInvalidValue;
   ColdArgs A{};
   A.bk = bk;
@@ -1473,7 +1566,12 @@ hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* b
   for (uint32_t j = 0; j < ax.nt; ++j) ntr += ax.t[j].tn;
   const uint32_t aux_wgs = min((max(nbr, ntr) + 256u * REG_WAVES - 1) / (256u * REG_WAVES), max(ax.nwg, 1u));
   const uint32_t grid = max(max(match_wgs, aux_wgs), 1u);
-  hipExtLaunchKernelGGL(k_match_reg, dim3(grid), dim3(128 * REG_WAVES), 0, st, ev0, ev1, 0, A);
+  hipExtLaunchKernelGGL(k_match_reg<false>, dim3(grid), dim3(128 * REG_WAVES), 0, st, ev0, ng ? nullptr : ev1, 0, A);
+  if (ng) {
+    A.ax = AuxDev{};
+    hipExtLaunchKernelGGL(k_match_reg<true>, dim3(min(64u, match_wgs)), dim3(128 * REG_WAVES), 0, st, nullptr, ev1, 0,
+                          A);
+  }
   return hipGetLastError();
 }
 
