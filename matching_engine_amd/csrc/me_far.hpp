@@ -218,10 +218,8 @@ __device__ bool far_rest(C& c, uint32_t k, long long p, unsigned long long seq, 
       ChunkHdr h;
       h.next = NIL;
       h.prev = e.tail;
-      h.owner = c.fsym();
-      h.pad = 0;
+      h.price = p;
       chunks[ch].hdr = h;
-      chunks[ch].price = p;
       if (e.tail != NIL) chunks[e.tail].hdr.next = ch;
     }
     if (e.tail == NIL) e.head = ch;

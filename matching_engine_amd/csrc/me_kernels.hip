@@ -487,6 +487,8 @@ __device__ __forceinline__ uint32_t alloc_chunk(WaveCtx& c) {
     }
     c.bump_cur = got;
     c.bump_end = min(got + BLK, c.bk.nchunks);
+    // fresh chunks belong to this symbol for good (unused ones join its free list)
+    if ((uint32_t)lane_id() < BLK && got + (uint32_t)lane_id() < c.bk.nchunks) c.bk.chunks[got + lane_id()].owner = c.s;
   }
   return c.bump_cur++;
 }
@@ -694,10 +696,8 @@ __device__ __forceinline__ bool rest_order(WaveCtx& c, int lvl, unsigned long lo
       ChunkHdr h;
       h.next = NIL;
       h.prev = L.tail;
-      h.owner = c.s;
-      h.pad = 0;
+      h.price = c.base + lvl;
       bk.chunks[ch].hdr = h;
-      bk.chunks[ch].price = c.base + lvl;
     }
     if (L.tail != NIL) set_next(c, lvl, L.tail, ch);
     if (L.tail == NIL) {
@@ -816,10 +816,11 @@ __device__ __forceinline__ int cancel_order(WaveCtx& c, unsigned long long tgt) 
       const uint32_t ch = g / ME_C, slot = g % ME_C;
       // one round trip: header, price, the whole chunk's quantities and the target seq
       const ChunkHdr hd = bk.chunks[ch].hdr;
-      const long long price = rli64(bk.chunks[ch].price, 0);
+      const uint32_t owner_v = bk.chunks[ch].owner;
+      const long long price = rli64(hd.price, 0);
       int qv = act ? cq_at(bk.chunks, (size_t)ch * ME_C + lane) : 0;
       unsigned long long sq = rl64(cs_at(bk.chunks, g), 0);
-      const uint32_t owner = rl32(hd.owner, 0);
+      const uint32_t owner = rl32(owner_v, 0);
       const long long lv64 = price - c.base;
       const bool inw = owner == c.s && (unsigned long long)lv64 < (unsigned long long)bk.L;
       const int lvl = inw ? (int)lv64 : 0;

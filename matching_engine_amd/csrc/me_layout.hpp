@@ -59,21 +59,22 @@ struct alignas(16) Level {
   uint32_t tail;     // last chunk (appends go here)
 };
 
+// Written as one 16-B store whenever a chunk joins a level. The price (not a window index) names the
+// level, so re-centring a window never touches chunks.
 struct alignas(16) ChunkHdr {
-  uint32_t next;   // next chunk of the level FIFO, or of the symbol free list
-  uint32_t prev;   // previous chunk of the level FIFO (NIL at the head)
-  uint32_t owner;  // symbol that allocated the chunk (chunks never change symbol)
-  uint32_t pad;
+  uint32_t next;    // next chunk of the level FIFO, or of the symbol free list
+  uint32_t prev;    // previous chunk of the level FIFO (NIL at the head)
+  long long price;  // price_q4 of the level the chunk belongs to
 };
 
-// One FIFO chunk, 256 B: header and the level's price (one 64-B segment with the header), then
-// the 16 slot quantities (one 64-B segment), then the 16 slot seqs (two 64-B segments). One pointer
-// reaches all of it; slot id g = chunk * ME_C + slot. The price (not a window index) names the
-// level, so re-centring a window never touches chunks.
+// One FIFO chunk, 256 B: header and owner (one 64-B segment), then the 16 slot quantities (one 64-B
+// segment), then the 16 slot seqs (two 64-B segments). One pointer reaches all of it; slot id
+// g = chunk * ME_C + slot.
 struct alignas(256) Chunk {
   ChunkHdr hdr;
-  long long price;
-  uint32_t pad[10];
+  uint32_t owner;  // symbol that took the chunk from the global pool (chunks never change symbol:
+                   // written once, when the bump allocator hands the chunk out)
+  uint32_t pad[11];
   int qty[ME_C];
   unsigned long long seq[ME_C];
 };

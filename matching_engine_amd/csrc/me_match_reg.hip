@@ -293,6 +293,8 @@ __device__ __forceinline__ uint32_t reg_alloc_slow(RegCtx& c) {
     }
     cur = got;
     ldsw(c.M->bump_end, min(got + blk, c.nchunks));
+    // fresh chunks belong to this symbol for good (unused ones join its free stack)
+    if ((uint32_t)lane_id() < blk && got + (uint32_t)lane_id() < c.nchunks) c.chunks[got + lane_id()].owner = c.s;
   }
   ldsw(c.M->bump_cur, cur + 1);
   return cur;
@@ -434,10 +436,8 @@ __device__ __forceinline__ bool reg_rest_new_chunk(RegCtx& c, int lvl, unsigned 
     ChunkHdr h;
     h.next = NIL;
     h.prev = tl;
-    h.owner = c.s;
-    h.pad = 0;
+    h.price = c.base + lvl;
     c.chunks[ch].hdr = h;
-    c.chunks[ch].price = c.base + lvl;
     c.loc[seq & c.rmask] = ch * ME_C;
   }
   if (tl == NIL) {  // empty level: the new chunk is its head, installed in the cache
@@ -518,12 +518,13 @@ __device__ __forceinline__ uint32_t reg_cancel(RegCtx& c, unsigned long long tgt
       const uint32_t ch = g / ME_C, slot = g % ME_C;
       // one round trip: header, price, the chunk's quantities and the target seq
       const ChunkHdr hdr = c.chunks[ch].hdr;
-      const long long price = c.chunks[ch].price;
+      const uint32_t owner = c.chunks[ch].owner;
+      const long long price = hdr.price;
       const int qg = c.chunks[ch].qty[lane & (ME_C - 1)];
       unsigned long long sq = rl64(c.chunks[ch].seq[slot], 0);
       __builtin_amdgcn_s_waitcnt(VMCNT0);  // resolved on every path (see reg_fill_entry)
       int qv = act ? qg : 0;
-      const uint32_t own = rl32(hdr.owner, 0);
+      const uint32_t own = rl32(owner, 0);
       const long long prc = rli64(price, 0);
       const long long lv64 = prc - rli64(c.base, 0);
       const bool inw = own == c.s && (unsigned long long)lv64 < (unsigned long long)RL;
@@ -1037,9 +1038,13 @@ __device__ __forceinline__ void aux_jobs(const ColdArgs& G, uint32_t a, uint32_t
 // Per-record control word built in vector form: (window limit level + 1) | BUY | MARKET | CANCEL |
 // FAR (the limit reaches past the window on the side the taker crosses: MARKET, a BUY above the
 // window, a SELL below it) | OUT (a LIMIT priced outside the window: its rest takes the far path).
-constexpr uint32_t CW_BUY = 1u << 8, CW_MKT = 1u << 9, CW_CXL = 1u << 10, CW_FAR = 1u << 11, CW_OUT = 1u << 12;
+// HAND (common launch only): the record needs a far level — OUT, or a MARKET while the side it crosses
+// has far levels (far counts only change in the continuation launch, so they are fixed per launch).
+constexpr uint32_t CW_BUY = 1u << 8, CW_MKT = 1u << 9, CW_CXL = 1u << 10, CW_FAR = 1u << 11, CW_OUT = 1u << 12,
+                   CW_HAND = 1u << 13;
 
-__device__ __forceinline__ uint32_t make_cw(long long opx, uint32_t kd, long long base, uint32_t L) {
+// far: bit 0 = the symbol has far bids (side 0), bit 1 = far asks (side 1)
+__device__ __forceinline__ uint32_t make_cw(long long opx, uint32_t kd, long long base, uint32_t L, uint32_t far_nz) {
   const uint32_t side = kd & 3u;
   const bool market = (kd >> 2) & 1u, cancel = (kd >> 3) & 1u;
   const bool buy = side == ME_SIDE_BUY;
@@ -1052,8 +1057,10 @@ __device__ __forceinline__ uint32_t make_cw(long long opx, uint32_t kd, long lon
                 : buy    ? (above ? (int)L - 1 : -1)
                          : (above ? (int)L : 0);
   const bool far = market || (buy ? above : (!inw && !above));
+  const bool out = !market && !inw;
+  const bool hand = out || (market && ((far_nz >> (buy ? 1 : 0)) & 1u));
   return (uint32_t)(lim + 1) | (buy ? CW_BUY : 0u) | (market ? CW_MKT : 0u) | (cancel ? CW_CXL : 0u) |
-         (far ? CW_FAR : 0u) | (!market && !inw ? CW_OUT : 0u);
+         (far ? CW_FAR : 0u) | (out ? CW_OUT : 0u) | (hand ? CW_HAND : 0u);
 }
 
 // One wavefront per symbol. kSlow = false: the common launch — every symbol of the group, no far-level
@@ -1329,12 +1336,22 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
           else if (oseq == 0ull)
             rj = ME_RJ_BAD_SEQ;  // no OID is 0 (the counter starts at 1, storage.cpp:254-267)
         }
-        cw = make_cw(v ? opx_ : 0ll, kd, c.base, L);
+        const uint32_t fnz = kSlow ? 0u : ((ldsu(c.M->nfar[0]) != 0u) | ((ldsu(c.M->nfar[1]) != 0u) << 1));
+        cw = make_cw(v ? opx_ : 0ll, kd, c.base, L, fnz);
         if (!v) rj = 0xFFu;  // lanes past the run (or before the continuation point): no record
       }
       unsigned long long work = __ballot(rj == ME_RJ_NONE);
       uint32_t stop = cnt;  // records [0, stop) of the block get results
       bool handoff = false;
+      if constexpr (!kSlow) {  // from the first record that needs a far level on: the continuation's
+        const unsigned long long hm = __ballot(rj == ME_RJ_NONE && (cw & CW_HAND));
+        if (ME_UNLIKELY(hm != 0ull)) {
+          const int h = __builtin_ctzll(hm);
+          work &= (1ull << h) - 1ull;
+          stop = (uint32_t)h;
+          handoff = true;
+        }
+      }
       uint32_t out_q = 0, out_n = 0, out_w = 0;
   #ifdef ME_STAMPS
       __builtin_amdgcn_s_waitcnt(0);
@@ -1359,15 +1376,9 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
           STAMP_ADD(c, PH_CANCEL);
         } else {
           const bool buy = (ctl & CW_BUY) != 0u;
-          if constexpr (!kSlow) {  // far levels ahead: hand the symbol off before anything changes
-            if (ME_UNLIKELY((ctl & CW_OUT) || ((ctl & CW_MKT) && c.fcount(buy ? 1u : 0u) != 0u))) {
-              stop = (uint32_t)k;
-              handoff = true;
-              break;
-            }
-          }
           if (ME_UNLIKELY(c.wptr + (uint32_t)c.resting > c.wend) && !reg_reserve_overflow(c)) {
             stop = (uint32_t)k;
+            handoff = false;
             break;
           }
           const unsigned long long seq = rl64(oseq_, k);
@@ -1405,12 +1416,14 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
           if (kSlow && rr != 0) {
             if (rr < 0) {
               stop = (uint32_t)k;
+              handoff = false;
               break;
             }
             const bool v = j < hi && vis + j >= skip;
-            cw = make_cw(v ? opx_ : 0ll, v ? kd_ : 0u, c.base, L);  // the window may have moved
+            cw = make_cw(v ? opx_ : 0ll, v ? kd_ : 0u, c.base, L, 0u);  // the window may have moved
           } else if (!(ctl & (CW_MKT | CW_OUT)) && rem != 0u && ME_UNLIKELY(!reg_rest(c, lm, seq, rem, buy))) {
             stop = (uint32_t)k;  // chunk pool exhausted: the batch fails (sticky error word)
+            handoff = false;
             break;
           }
           STAMP_ADD(c, PH_REST);
