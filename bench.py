@@ -72,6 +72,8 @@ def parse():
                     help="threads of the sharded CPU baseline (the GPU box's CPU share is 16); 1 = scalar only")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--e2e-steps", type=int, default=192,
+                    help="batches through the pipelined host path (me_submit_host/me_collect) after the timed loop")
     ap.add_argument("--timing-every", type=int, default=4,
                     help="HIP events on every k-th match launch of the timed loop (each timed launch costs "
                          "the stream a few us; 1 = every launch, 0 = off)")
@@ -252,7 +254,7 @@ def main():
 
     nb = args.warmup + args.steps
     n_gather = args.gather_steps if world > 1 else 0
-    n_e2e = 0 if args.no_e2e else 10
+    n_e2e = 0 if args.no_e2e else args.e2e_steps
     sc, base, ids, batches, positions, global_orders, seeds = build_rank_batches(args, world, rank,
                                                                                  nb + n_gather + n_e2e)
     gather_batches, gather_pos = batches[nb:nb + n_gather], positions[nb:nb + n_gather]
@@ -330,15 +332,24 @@ def main():
                 "what": "submit + device tape/result copy + RCCL all_gather(sizes) + gather(tape, results) to "
                         "rank 0 + stable merge by taker seq on rank 0's GPU + D2H of the merged tape"}
 
-    # PCIe-inclusive host path (me_submit_batch: H2D + pipeline + D2H of results and tape), informational
+    # PCIe-inclusive host path (me_submit_host / me_collect: staging copy into a pinned slot, H2D on
+    # its own stream, the grouped pipeline, D2H of results + tape into pinned memory), informational.
+    # Each ticket is collected when its slot is needed again (host_slots submissions later).
     e2e = None
     if e2e_batches:
-        torch.cuda.synchronize(local)
+        eng.sync()
+        slots = eng.config()["host_slots"]
         t2 = time.perf_counter()
-        n2 = 0
+        n2, f2, pend = 0, 0, []
         for b in e2e_batches:
-            eng.submit_batch(b)
+            if len(pend) == slots:
+                _, f = eng.collect(pend.pop(0), copy=False)
+                f2 += len(f)
+            pend.append(eng.submit_host(b))
             n2 += len(b)
+        for t in pend:
+            _, f = eng.collect(t, copy=False)
+            f2 += len(f)
         e2e = n2 / (time.perf_counter() - t2)
 
     if rank == 0:

@@ -103,6 +103,11 @@ typedef struct me_config {
                                   me_submit_batch_device calls fill a group; me_sync flushes a partial one */
   uint32_t far_levels;         /* capacity per symbol and side of the far arrays (price levels outside the
                                   window), 0 = 1024 */
+  uint32_t host_slots;         /* pinned slots of the host-batch pipeline (me_submit_host), 0 = enough to keep
+                                  three launch groups in flight (3 * batches_per_launch + 1); allocated on use */
+  uint64_t host_tape_cap;      /* fills a slot holds (0 = 2 * max_batch + 4096). A longer tape is recovered at
+                                  me_collect while its batch's scratch is intact (collected before 3 further
+                                  launch groups were submitted), else that collect fails with ME_E_CAPACITY */
 } me_config;
 
 /* One batch in structure-of-arrays form. Seqs (= numeric OIDs) strictly ascend across the whole
@@ -157,17 +162,44 @@ typedef struct me_book_entry {
 me_engine* me_create(const me_config* cfg);
 void me_destroy(me_engine* e);
 
-/* Host-memory batch: H2D -> group by symbol -> match -> compact tape -> D2H, synchronous.
- * out_fills must hold me_fill_bound(e, n) records (or NULL to skip the tape copy);
+/* Host-memory batch, synchronous: me_submit_host + me_collect + copy-out.
+ * out_fills must hold the tape (me_fill_bound(e, n) records always suffice; NULL skips the copy);
  * out_results holds n records (or NULL). *n_fills receives the tape length. */
 int me_submit_batch(me_engine* e, const me_order_soa* batch, size_t n, me_fill* out_fills,
                     size_t fills_cap, size_t* n_fills, me_order_result* out_results);
 /* Upper bound on the tape length of one batch of n records (resting capacity + 2n). */
 uint64_t me_fill_bound(const me_engine* e, size_t n);
 
+/* ---- pipelined host batches (the time-slice path of SubmitOrder) -----------
+ * me_submit_host stages the batch in the next of the engine's pinned slots (skipped when the batch
+ * already lives there, see me_host_inputs), copies it to HBM on the engine's H2D stream and enqueues
+ * it behind everything submitted before; it returns at once with a ticket (0, 1, 2, ...). The H2D of
+ * batch k+1, the match of batch k and the D2H of batch k-1 (results + tape, on a D2H stream) overlap.
+ * me_collect waits for the ticket's batch (launching a partial group first when it is still waiting
+ * for one) and points into the slot's pinned outputs: valid until the slot is reused by ticket +
+ * host_slots. A slot is reused only after its ticket was collected (else ME_E_STATE). Not
+ * thread-safe, like every other entry point: serialize calls on one engine. */
+int me_submit_host(me_engine* e, const me_order_soa* batch, size_t n, uint64_t* ticket);
+int me_collect(me_engine* e, uint64_t ticket, const me_fill** fills, size_t* n_fills,
+               const me_order_result** results, size_t* n_results);
+/* Writable pinned arrays for the n-record batch the next me_submit_host will take (zero-copy
+ * staging: fill them, then pass the same pointers to me_submit_host). ME_E_STATE while that slot's
+ * previous ticket is uncollected. */
+typedef struct me_order_soa_w {
+  uint64_t* seq;
+  int64_t* price_q4;
+  int32_t* qty;
+  uint32_t* symbol;
+  uint8_t* kind;
+} me_order_soa_w;
+int me_host_inputs(me_engine* e, size_t n, me_order_soa_w* out);
+/* The engine's configuration as created, defaults resolved (base_price / symbol_ids NULL). */
+int me_get_config(const me_engine* e, me_config* out);
+
 /* Device-resident batch (pointers in HBM), enqueued on the engine stream, asynchronous. The batch
  * buffers must stay valid until the next me_sync (or any call that reads outputs or the book).
- * Outputs stay on the device until me_fetch_outputs. */
+ * Outputs stay on the device until me_fetch_outputs (me_fetch_outputs / me_fetch_group_outputs /
+ * me_copy_*_device read the most recent batch and fail with ME_E_INVALID when it was a host batch). */
 int me_submit_batch_device(me_engine* e, const me_order_soa* dev_batch, size_t n);
 /* Wait for all enqueued work; returns ME_E_CAPACITY if a pool overflowed in any batch. */
 int me_sync(me_engine* e);

@@ -10,10 +10,17 @@
  *                             order and strings (:66-83), OID allocation (:85, consumed even when
  *                             normalisation throws), normalize_to_q4 (:89-97), side CHECK -> "DB insert
  *                             failed" with order_id set (:107-111). The order joins the open time slice.
- *   me_service_flush          the time-slice batcher: runs the slice through the engine and ingests the
- *                             whole batch in ONE SQLite transaction (orders rows as insert_new_order
- *                             writes them, final status/remaining from the match, fills rows, maker
- *                             status updates) — the batched rewrite of storage.cpp:78-208.
+ *                             Any non-empty symbol is accepted (:66-71): a new one takes the engine's
+ *                             next unused book; only when all of them are taken is it refused
+ *                             (grpc_status 8 RESOURCE_EXHAUSTED, "symbol capacity exhausted", no OID).
+ *   me_service_flush          the time-slice batcher: matches every slice submitted so far on the engine
+ *                             (me_submit_host / me_collect) and ingests each in ONE SQLite transaction
+ *                             (orders rows as insert_new_order writes them carrying the matched status
+ *                             and remainder, fills rows, maker / cancel-target updates) — the batched
+ *                             rewrite of storage.cpp:78-208. Matching and persistence run outside the
+ *                             submit lock: SubmitOrder never waits for a flush.
+ *   me_service_start          background flusher: a slice closes at slice_orders records or once it is
+ *                             interval_us old, and is flushed without any caller.
  *   me_service_book           GetOrderBook (matching_engine_service.cpp:123-129) from the GPU book.
  *   me_service_cancel_order   CancelOrder — a build extension (the reference has no cancel RPC; SURVEY
  *                             §8(f) row 4): queues a cancel record for a resting order into the slice.
@@ -51,9 +58,11 @@ typedef struct me_order_response {
 
 typedef struct me_service me_service;
 
-/* engine: the shard the slices are matched on (NULL: submit works, flush fails loudly).
- * symbols[num_symbols]: symbol strings of the engine's local ids 0..num_symbols-1.
- * db_path: SQLite file (NULL: no persistence). */
+/* engine: the shard the slices are matched on (NULL: submit works, flush fails loudly). The service
+ * drives it from its own threads: no other caller may use the engine while the service lives.
+ * symbols[num_symbols]: symbol strings pre-assigned to the engine's local ids 0..num_symbols-1; later
+ * symbols take the following ids, up to the engine's num_symbols.
+ * db_path: SQLite file (NULL: no persistence). Destroy does not flush: flush first. */
 me_service* me_service_create(me_engine* engine, const char* const* symbols, uint32_t num_symbols,
                               const char* db_path);
 void me_service_destroy(me_service* s);
@@ -66,10 +75,24 @@ size_t me_service_pending(const me_service* s);
 /* Next OID number the service will allocate. */
 uint64_t me_service_next_oid(const me_service* s);
 
-/* Match the open slice and persist it. Any output may be NULL; *n_results = records matched
- * (order of submission), out_seq[i] their numeric OIDs. */
+/* Match and persist every slice submitted before the call, oldest first. Any output may be NULL;
+ * the outputs cover the records this call matched, in submission order (tape offsets into the
+ * concatenated tape): *n_results records, out_seq[i] their numeric OIDs. The capacities are checked
+ * before anything is matched (results_cap >= me_service_pending, fills_cap >= me_fill_bound of it),
+ * else ME_E_INVALID and nothing happens.
+ * A slice the engine accepted is never matched again. When its transaction fails (e.g. SQLITE_BUSY
+ * past the 5 s busy timeout) the matched slice is kept in memory, later slices still match, and every
+ * later flush first retries the kept ones in order; the call returns ME_E_SQLITE meanwhile
+ * (me_service_unpersisted counts the records waiting). */
 int me_service_flush(me_service* s, me_fill* out_fills, size_t fills_cap, size_t* n_fills,
                      me_order_result* out_results, uint64_t* out_seq, size_t results_cap, size_t* n_results);
+/* Matched records whose SQLite transaction has not committed yet. */
+size_t me_service_unpersisted(const me_service* s);
+/* Background flusher (one thread): a slice closes at slice_orders records (0 or more than the
+ * engine's max_batch: max_batch) or once it is interval_us old (0: 1000), and is flushed at once.
+ * Errors go to me_service_last_error. me_service_stop joins it. */
+int me_service_start(me_service* s, uint32_t interval_us, uint32_t slice_orders);
+int me_service_stop(me_service* s);
 
 /* GetOrderBook for a symbol string (top depth levels per side). */
 int me_service_book(me_service* s, const char* symbol, me_level* bids, me_level* asks, size_t depth,
@@ -83,7 +106,8 @@ typedef struct me_cancel_request {
 } me_cancel_request;
 
 /* Validation (first failing check wins, in-band like SubmitOrder :66-83): "symbol is required",
- * "order_id is invalid" (not "OID-<n>", n >= 1). An accepted cancel consumes the next OID number as
+ * "order_id is invalid" (not "OID-<n>", n >= 1), "order belongs to another client" (the target is a
+ * resting or pending order of a different client_id). An accepted cancel consumes the next OID number as
  * its stream position (like any request reaching :85) and answers success=1 with order_id = the
  * TARGET's id; whether it removed anything arrives as an OrderUpdate after the flush (CANCELED with
  * the removed quantity, or REJECTED when the target was not resting on that symbol). */

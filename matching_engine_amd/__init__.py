@@ -8,6 +8,7 @@ from ._abi import (  # noqa: F401
     SIDE_BUY, SIDE_SELL, SIDE_UNSPECIFIED, TYPE_LIMIT, TYPE_MARKET, OP_NEW, OP_CANCEL,
     ST_NEW, ST_PARTIALLY_FILLED, ST_FILLED, ST_CANCELED, ST_REJECTED,
     RJ_NONE, RJ_BAD_QTY, RJ_BAD_SIDE, RJ_OUT_OF_WINDOW, RJ_BAD_SYMBOL, RJ_UNKNOWN_ORDER, RJ_BAD_SEQ,
+    ME_OK, ME_E_INVALID, ME_E_HIP, ME_E_CAPACITY, ME_E_STATE, ME_E_SQLITE,
 )
 from .engine import (  # noqa: F401
     Batch, DeviceBatch, Engine, EngineError, Stream, StreamConfig, normalize_to_q4, preset, shard_of, shard_table,

@@ -43,10 +43,22 @@ class MeConfig(C.Structure):
         ("symbol_ids", C.POINTER(C.c_uint32)),
         ("batches_per_launch", C.c_uint32),
         ("far_levels", C.c_uint32),
+        ("host_slots", C.c_uint32),
+        ("host_tape_cap", C.c_uint64),
     ]
 
 
 class MeOrderSoa(C.Structure):
+    _fields_ = [
+        ("seq", C.c_void_p),
+        ("price_q4", C.c_void_p),
+        ("qty", C.c_void_p),
+        ("symbol", C.c_void_p),
+        ("kind", C.c_void_p),
+    ]
+
+
+class MeOrderSoaW(C.Structure):
     _fields_ = [
         ("seq", C.c_void_p),
         ("price_q4", C.c_void_p),
@@ -105,6 +117,10 @@ PROTOTYPES = {
     "me_destroy": (None, [_P]),
     "me_submit_batch": (C.c_int, [_P, C.POINTER(MeOrderSoa), _SZ, _P, _SZ, C.POINTER(_SZ), _P]),
     "me_fill_bound": (C.c_uint64, [_P, _SZ]),
+    "me_submit_host": (C.c_int, [_P, C.POINTER(MeOrderSoa), _SZ, C.POINTER(C.c_uint64)]),
+    "me_collect": (C.c_int, [_P, C.c_uint64, C.POINTER(_P), C.POINTER(_SZ), C.POINTER(_P), C.POINTER(_SZ)]),
+    "me_host_inputs": (C.c_int, [_P, _SZ, C.POINTER(MeOrderSoaW)]),
+    "me_get_config": (C.c_int, [_P, C.POINTER(MeConfig)]),
     "me_submit_batch_device": (C.c_int, [_P, C.POINTER(MeOrderSoa), _SZ]),
     "me_sync": (C.c_int, [_P]),
     "me_fetch_outputs": (C.c_int, [_P, _P, _SZ, C.POINTER(_SZ), _P, _SZ]),
@@ -240,4 +256,7 @@ PROTOTYPES.update({
     "me_service_flush": (C.c_int, [_P, _P, _SZ, C.POINTER(_SZ), _P, _P, _SZ, C.POINTER(_SZ)]),
     "me_service_book": (C.c_int, [_P, C.c_char_p, _P, _P, _SZ, C.POINTER(_SZ), C.POINTER(_SZ)]),
     "me_service_last_error": (C.c_int, [_P, C.c_char_p, _SZ]),
+    "me_service_unpersisted": (_SZ, [_P]),
+    "me_service_start": (C.c_int, [_P, C.c_uint32, C.c_uint32]),
+    "me_service_stop": (C.c_int, [_P]),
 })

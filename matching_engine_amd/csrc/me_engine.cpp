@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "me_engine.h"
@@ -31,7 +32,10 @@ hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* b
                             hipEvent_t ev1);
 uint32_t sort_tile(uint32_t n);
 hipError_t launch_tape(hipStream_t st, const BatchDev& bt, me_fill* tape, unsigned long long tape_cap,
-                       unsigned long long* tape_count, unsigned long long* fills_acc, uint32_t* err);
+                       unsigned long long* tape_count, unsigned long long* fills_acc, uint32_t* err,
+                       me_order_result* hres, uint32_t* err_out);
+hipError_t launch_tape_spill(hipStream_t st, const me_order_result* res, const uint32_t* fstart, uint32_t n,
+                             const me_fill* scratch, unsigned long long cap, me_fill* spill);
 hipError_t launch_init_levels(hipStream_t st, Level* levels, size_t count);
 hipError_t launch_init_chunks(hipStream_t st, Chunk* chunks, size_t count);
 }  // namespace me
@@ -47,6 +51,31 @@ struct TimedLaunch {
   uint64_t orders;
   uint64_t idx;       // batches matched (since timing was enabled) before this launch
 };
+
+// Output block of a host slot (same layout in HBM and in pinned memory): SlotMeta, the tape (cap
+// records), the results (max_batch records).
+struct SlotMeta {
+  unsigned long long count;  // the batch's tape length (may exceed the slot's cap)
+  uint32_t err;              // the device error word when the tape job finished
+  uint32_t pad;
+};
+static_assert(sizeof(SlotMeta) == 16, "SlotMeta");
+
+// One slot of the host-batch pipeline (me_submit_host / me_collect).
+struct HostSlot {
+  char* h_in = nullptr;   // pinned staging: the batch packed as seq[n] px[n] qty[n] sym[n] kind[n]
+  char* d_in = nullptr;   // its HBM copy
+  char* h_out = nullptr;  // pinned outputs (SlotMeta | tape | results)
+  char* d_out = nullptr;  // HBM outputs the tape job writes
+  hipEvent_t ev_in = nullptr;    // H2D done (H2D stream)
+  hipEvent_t ev_done = nullptr;  // outputs in pinned memory (D2H stream)
+  uint64_t ticket = 0;
+  uint32_t n = 0;
+  int state = 0;  // 0 free (collected), 1 enqueued, 2 outputs copy enqueued
+  int oset = 0;   // output set (results / scratch starts / scratch) the batch used, and its generation
+  uint64_t oset_gen = 0;
+  std::vector<me_fill> big;  // the whole tape when it outgrew the slot (spilled at me_collect)
+};
 }  // namespace
 
 struct me_engine {
@@ -59,12 +88,6 @@ struct me_engine {
   // grouping sort plan
   int passes = 1;
   int dbits[2] = {0, 0};
-  // batch buffers
-  uint64_t* d_seq = nullptr;
-  int64_t* d_px = nullptr;
-  int32_t* d_qty = nullptr;
-  uint32_t* d_sym = nullptr;
-  uint8_t* d_kind = nullptr;
   // Everything the grouping sort of a batch writes: sorted keys, permutation, histogram, run
   // table, and the per-batch counters it zeroes.
   struct SortBufs {
@@ -104,6 +127,7 @@ struct me_engine {
     const uint8_t* kind = nullptr;
     uint32_t n = 0;
     int oset = 0, bset = 0;
+    int slot = -1;  // host slot (me_submit_host), -1: a device batch
   };
   struct Group {
     Pend b[ME_GMAX];
@@ -120,9 +144,18 @@ struct me_engine {
   unsigned long long tape_cap = 0;     // tape bound of one batch (max_resting + 2 * max_batch)
   uint32_t slab = 0;                   // scratch fills per symbol slab (register-ladder kernel)
   uint32_t ntiles_sort = 0;            // sort tiles of a max_batch batch (histogram row stride)
-  // pinned staging for host batches
-  void* h_pin = nullptr;
-  size_t h_pin_bytes = 0;
+  // host-batch pipeline
+  std::vector<HostSlot> hs;
+  std::vector<int> free_slots;  // LIFO: a synchronous caller keeps reusing one warm slot
+  std::unordered_map<uint64_t, int> by_ticket;  // uncollected tickets -> slot
+  uint64_t hcap = 0;         // tape records per slot
+  uint64_t next_ticket = 0;
+  hipStream_t s_h2d = nullptr, s_d2h = nullptr;
+  hipEvent_t ev_tape = nullptr;  // a launch that compacted host tapes finished (the D2H stream waits on it)
+  std::vector<uint64_t> oset_gen;  // batches assigned to each output set so far
+  me_fill* d_spill = nullptr;
+  size_t spill_cap = 0;
+  bool last_host = false;  // the most recent batch was a host batch (the device-output fetches refuse)
   uint32_t last_n = 0;
   uint32_t sq_idx = 0;  // seq-ring state the next k_seq_sweep reads (it writes the other one)
   struct LastGroup {    // the launch group holding the most recent batch: where its outputs live
@@ -167,7 +200,6 @@ static int set_create_err(const std::string& s) {
 static void free_all(me_engine* e) {
   void* ptrs[] = {e->bk.levels,   e->bk.occ,      e->bk.sym,      e->bk.chunks,     e->bk.tend,
                   e->bk.loc,      e->bk.chunk_top, e->bk.err,       (void*)e->bk.gsym,
-                  e->d_seq,       e->d_px,        e->d_qty,       e->d_sym,         e->d_kind,
                   e->d_tape,      e->d_tape_count, e->d_fills_acc, e->bk.dbg,      e->bk.fcache,
                   e->bk.far,      e->bk.old,       e->bk.sq,       e->bk.hcount,     e->bk.hand};
   for (void* p : ptrs)
@@ -190,7 +222,19 @@ static void free_all(me_engine* e) {
   }
   for (void* p : e->user_allocs) (void)hipFree(p);
   e->user_allocs.clear();
-  if (e->h_pin) (void)hipHostFree(e->h_pin);
+  for (auto& h : e->hs) {
+    if (h.h_in) (void)hipHostFree(h.h_in);
+    if (h.h_out) (void)hipHostFree(h.h_out);
+    if (h.d_in) (void)hipFree(h.d_in);
+    if (h.d_out) (void)hipFree(h.d_out);
+    if (h.ev_in) (void)hipEventDestroy(h.ev_in);
+    if (h.ev_done) (void)hipEventDestroy(h.ev_done);
+  }
+  e->hs.clear();
+  if (e->d_spill) (void)hipFree(e->d_spill);
+  if (e->ev_tape) (void)hipEventDestroy(e->ev_tape);
+  if (e->s_h2d) (void)hipStreamDestroy(e->s_h2d);
+  if (e->s_d2h) (void)hipStreamDestroy(e->s_d2h);
   for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
   e->ev_pool.clear();
   e->timed.clear();
@@ -360,11 +404,6 @@ extern "C" me_engine* me_create(const me_config* cfg) {
   uint32_t* gsym = nullptr;
   ALLOC(gsym, S);
   bk.gsym = gsym;
-  ALLOC(e->d_seq, n);
-  ALLOC(e->d_px, n);
-  ALLOC(e->d_qty, n);
-  ALLOC(e->d_sym, n);
-  ALLOC(e->d_kind, n);
   {
     auto& sl = e->sb;
     for (int k = 0; k < 2; ++k) {
@@ -387,7 +426,8 @@ extern "C" me_engine* me_create(const me_config* cfg) {
       ALLOC(b.rec, nb);
     }
   }
-  e->nsets = e->bucketed ? 3 * (int)e->group : 1;
+  // the sort path rotates three sets too, so a host batch's scratch outlives the next two batches
+  e->nsets = e->bucketed ? 3 * (int)e->group : 3;
   for (int k = 0; k < e->nsets; ++k) {
     auto& o = e->os[k];
     ALLOC(o.res, n);
@@ -442,9 +482,28 @@ extern "C" me_engine* me_create(const me_config* cfg) {
             hipMemsetAsync(e->d_fills_acc, 0, 8, st) == hipSuccess &&
             hipStreamSynchronize(st) == hipSuccess;
   if (!ok) return bail(std::string("me_create: book init failed: ") + hipGetErrorString(hipGetLastError()));
-  e->h_pin_bytes = n * (8 + 8 + 4 + 4 + 1) + 64;
-  he = hipHostMalloc(&e->h_pin, e->h_pin_bytes, hipHostMallocDefault);
-  if (he != hipSuccess) return bail(std::string("hipHostMalloc: ") + hipGetErrorString(he));
+  // host-batch pipeline: slots are allocated on first use
+  {
+    uint64_t H = cfg->host_slots ? cfg->host_slots : 3ull * e->group + 1;
+    if (H > 4096) return bail("me_create: host_slots exceeds 4096");
+    e->hs.resize(H);
+    for (uint64_t k = H; k-- > 0;) e->free_slots.push_back((int)k);
+    e->hcap = cfg->host_tape_cap ? cfg->host_tape_cap : 2 * n + 4096;
+    e->oset_gen.assign(e->nsets, 0);
+    if ((he = hipStreamCreateWithFlags(&e->s_h2d, hipStreamNonBlocking)) != hipSuccess ||
+        (he = hipStreamCreateWithFlags(&e->s_d2h, hipStreamNonBlocking)) != hipSuccess ||
+        (he = hipEventCreateWithFlags(&e->ev_tape, hipEventDisableTiming)) != hipSuccess)
+      return bail(std::string("me_create: host pipeline streams: ") + hipGetErrorString(he));
+  }
+  // the configuration as resolved (me_get_config)
+  e->cfg.max_chunks = nchunks;
+  e->cfg.seq_ring = ring;
+  e->cfg.far_levels = bk.fcap;
+  e->cfg.batches_per_launch = e->group;
+  e->cfg.host_slots = (uint32_t)e->hs.size();
+  e->cfg.host_tape_cap = e->hcap;
+  e->cfg.base_price = nullptr;
+  e->cfg.symbol_ids = nullptr;
   return e;
 }
 
@@ -452,6 +511,8 @@ extern "C" void me_destroy(me_engine* e) {
   if (!e) return;
   (void)hipSetDevice(e->dev);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
+  if (e->s_h2d) (void)hipStreamSynchronize(e->s_h2d);
+  if (e->s_d2h) (void)hipStreamSynchronize(e->s_d2h);
   free_all(e);
   delete e;
 }
@@ -519,6 +580,64 @@ static int seq_sweep(me_engine* e, const me_engine::Group& g) {
   return ME_OK;
 }
 
+// ---- host slots ---------------------------------------------------------------------------
+static size_t slot_in_bytes(uint64_t n) { return (size_t)n * (8 + 8 + 4 + 4 + 1); }
+static size_t slot_res_off(const me_engine* e) { return sizeof(SlotMeta) + (size_t)e->hcap * sizeof(me_fill); }
+static size_t slot_out_bytes(const me_engine* e) {
+  return slot_res_off(e) + (size_t)e->cfg.max_batch * sizeof(me_order_result);
+}
+// The packed SoA of an n-record batch at base p.
+static void slot_soa(char* p, uint64_t n, uint64_t*& seq, int64_t*& px, int32_t*& qty, uint32_t*& sym,
+                     uint8_t*& kind) {
+  seq = (uint64_t*)p;
+  px = (int64_t*)(p + 8 * n);
+  qty = (int32_t*)(p + 16 * n);
+  sym = (uint32_t*)(p + 20 * n);
+  kind = (uint8_t*)(p + 24 * n);
+}
+// Where the tape job of a host batch writes (the slot's HBM output block).
+static void slot_outputs(me_engine* e, HostSlot& h, me_fill*& tape, unsigned long long*& count,
+                         me_order_result*& res, uint32_t*& err) {
+  SlotMeta* m = (SlotMeta*)h.d_out;
+  count = &m->count;
+  err = &m->err;
+  tape = (me_fill*)(h.d_out + sizeof(SlotMeta));
+  res = (me_order_result*)(h.d_out + slot_res_off(e));
+}
+static int slot_alloc(me_engine* e, HostSlot& h) {
+  if (h.h_in) return ME_OK;
+  const size_t in = slot_in_bytes(e->cfg.max_batch) + 64, out = slot_out_bytes(e);
+  HIP_TRY(hipHostMalloc((void**)&h.h_in, in, hipHostMallocDefault), "hipHostMalloc slot inputs");
+  HIP_TRY(hipHostMalloc((void**)&h.h_out, out, hipHostMallocDefault), "hipHostMalloc slot outputs");
+  HIP_TRY(hipMalloc((void**)&h.d_in, in), "hipMalloc slot inputs");
+  HIP_TRY(hipMalloc((void**)&h.d_out, out), "hipMalloc slot outputs");
+  HIP_TRY(hipEventCreateWithFlags(&h.ev_in, hipEventDisableTiming), "hipEventCreate");
+  HIP_TRY(hipEventCreateWithFlags(&h.ev_done, hipEventDisableTiming), "hipEventCreate");
+  return ME_OK;
+}
+// After the launch that wrote the tapes of host slots[0..ns): the D2H stream waits for it and copies
+// each slot's meta + tape head + results into pinned memory. Nothing later on the engine stream
+// writes those HBM blocks before the slot is collected and reused.
+static int enqueue_host_d2h(me_engine* e, const int* slots, int ns) {
+  HIP_TRY(hipEventRecord(e->ev_tape, e->stream), "hipEventRecord");
+  HIP_TRY(hipStreamWaitEvent(e->s_d2h, e->ev_tape, 0), "hipStreamWaitEvent");
+  for (int k = 0; k < ns; ++k) {
+    HostSlot& h = e->hs[slots[k]];
+    // the tape head copied with the results: room for 1.5 fills per record (the rest, when there is
+    // more, is read at me_collect)
+    const uint64_t head = std::min<uint64_t>(e->hcap, (uint64_t)h.n + h.n / 2 + 1024);
+    HIP_TRY(hipMemcpyAsync(h.h_out, h.d_out, sizeof(SlotMeta) + head * sizeof(me_fill), hipMemcpyDeviceToHost,
+                           e->s_d2h),
+            "D2H slot tape");
+    HIP_TRY(hipMemcpyAsync(h.h_out + slot_res_off(e), h.d_out + slot_res_off(e), (size_t)h.n * sizeof(me_order_result),
+                           hipMemcpyDeviceToHost, e->s_d2h),
+            "D2H slot results");
+    HIP_TRY(hipEventRecord(h.ev_done, e->s_d2h), "hipEventRecord");
+    h.state = 2;
+  }
+  return ME_OK;
+}
+
 // One launch of the pipelined register-ladder path: match group g_match (if any), bucket group nb
 // (if any) and clear the counters its batches will use, compact g_tape's tapes (if any) — then the
 // pipeline shifts by one group.
@@ -562,8 +681,8 @@ static int pipe_launch(me_engine* e, const me_engine::Group* nb) {
     }
   }
   ax.nt = gt.n;
-  ax.tape_cap = e->tape_cap;
   ax.fills_acc = e->d_fills_acc;
+  bool host_tapes = false;
   for (uint32_t j = 0; j < gt.n; ++j) {
     const auto& o = e->os[gt.b[j].oset];
     AuxTape& J = ax.t[j];
@@ -572,8 +691,15 @@ static int pipe_launch(me_engine* e, const me_engine::Group* nb) {
     J.res = o.res;
     J.fstart = o.fstart;
     J.scratch = o.scratch;
-    J.tape = e->d_tape + (size_t)j * e->tape_cap;
-    J.tape_count = e->d_tape_count + j;
+    if (gt.b[j].slot >= 0) {
+      host_tapes = true;
+      slot_outputs(e, e->hs[gt.b[j].slot], J.tape, J.tape_count, J.hres, J.err_out);
+      J.cap = e->hcap;
+    } else {
+      J.tape = e->d_tape + (size_t)j * e->tape_cap;
+      J.tape_count = e->d_tape_count + j;
+      J.cap = e->tape_cap;
+    }
   }
   TimedLaunch tl{};
   bool timed = false;
@@ -586,6 +712,13 @@ static int pipe_launch(me_engine* e, const me_engine::Group* nb) {
   hipError_t he = launch_match_reg(e->stream, e->bk, bt, gm.n, ax, tl.m0, tl.m1);
   if (he != hipSuccess) return e->hip_fail(he, "pipelined match launch");
   if (timed) e->timed.push_back(tl);
+  if (host_tapes) {
+    int slots[ME_GMAX], ns = 0;
+    for (uint32_t j = 0; j < gt.n; ++j)
+      if (gt.b[j].slot >= 0) slots[ns++] = gt.b[j].slot;
+    int rc = enqueue_host_d2h(e, slots, ns);
+    if (rc) return rc;
+  }
   e->g_tape = e->g_match;
   if (nb) {
     e->g_match = *nb;
@@ -612,7 +745,8 @@ static int flush_pipeline(me_engine* e) {
 
 // Enqueue a device-resident batch.
 static int enqueue_batch(me_engine* e, const uint64_t* seq, const int64_t* px, const int32_t* qty,
-                         const uint32_t* sym, const uint8_t* kind, uint32_t n) {
+                         const uint32_t* sym, const uint8_t* kind, uint32_t n, int slot = -1) {
+  e->last_host = slot >= 0;
   if (e->bucketed) {
     auto& gf = e->g_fill;
     const uint32_t pos = gf.n;
@@ -626,6 +760,12 @@ static int enqueue_batch(me_engine* e, const uint64_t* seq, const int64_t* px, c
     nb.n = n;
     nb.oset = (int)((e->ngroup % 3) * e->group + pos);
     nb.bset = (int)((e->ngroup % 2) * e->group + pos);
+    nb.slot = slot;
+    const uint64_t gen = ++e->oset_gen[nb.oset];
+    if (slot >= 0) {
+      e->hs[slot].oset = nb.oset;
+      e->hs[slot].oset_gen = gen;
+    }
     gf.n = pos + 1;
     e->last_set = nb.oset;
     e->last_tape = (int)pos;
@@ -643,7 +783,8 @@ static int enqueue_batch(me_engine* e, const uint64_t* seq, const int64_t* px, c
   }
   hipStream_t st = e->stream;
   auto& sl = e->sb;
-  const auto& o = e->os[0];
+  const int oset = (int)(e->ngroup++ % (uint64_t)e->nsets);
+  const auto& o = e->os[oset];
   TimedLaunch tl{};
   bool timed = false;
   int rc = timing_slot(e, n, 1u, tl, timed);
@@ -673,29 +814,44 @@ static int enqueue_batch(me_engine* e, const uint64_t* seq, const int64_t* px, c
     iin = sl.idx[p];
     shift += e->dbits[p];
   }
-  BatchDev bt = batch_dev(e, seq, px, qty, sym, kind, n, 0);
+  BatchDev bt = batch_dev(e, seq, px, qty, sym, kind, n, oset);
   bt.skeys = kin;
   bt.perm = iin;
   bt.bin_start = run_table;  // bins are symbols: the run table
   // timing: the launch itself records start/end (hipExtLaunchKernelGGL), no marker packets
+  const uint64_t gen = ++e->oset_gen[oset];
   hipError_t he = launch_match(st, e->bk, bt, tl.m0, tl.m1);
   if (he != hipSuccess) return e->hip_fail(he, "match launch");
-  he = launch_tape(st, bt, e->d_tape, e->tape_cap, e->d_tape_count, e->d_fills_acc, e->bk.err);
+  if (slot >= 0) {
+    HostSlot& h = e->hs[slot];
+    h.oset = oset;
+    h.oset_gen = gen;
+    me_fill* tape;
+    unsigned long long* cnt;
+    me_order_result* hres;
+    uint32_t* eo;
+    slot_outputs(e, h, tape, cnt, hres, eo);
+    he = launch_tape(st, bt, tape, e->hcap, cnt, e->d_fills_acc, e->bk.err, hres, eo);
+  } else {
+    he = launch_tape(st, bt, e->d_tape, e->tape_cap, e->d_tape_count, e->d_fills_acc, e->bk.err, nullptr, nullptr);
+  }
   if (he != hipSuccess) return e->hip_fail(he, "tape launch");
   if (timed) e->timed.push_back(tl);
-  e->last_set = 0;
+  if (slot >= 0) {
+    rc = enqueue_host_d2h(e, &slot, 1);
+    if (rc) return rc;
+  }
+  e->last_set = oset;
   e->last_tape = 0;
   e->last_n = n;
   e->lastg.n = 1;
-  e->lastg.oset[0] = 0;
+  e->lastg.oset[0] = oset;
   e->lastg.tape[0] = 0;
   e->lastg.bn[0] = n;
   return ME_OK;
 }
 
-static int check_err_word(me_engine* e) {
-  uint32_t w = 0;
-  HIP_TRY(hipMemcpy(&w, e->bk.err, 4, hipMemcpyDeviceToHost), "read error word");
+static int check_err_bits(me_engine* e, uint32_t w) {
   if (w) {
     std::string m = "device pool overflow/inconsistency (bits=" + std::to_string(w) + "):";
     if (w & ERR_CHUNK_OOM) m += " chunk pool exhausted (raise max_chunks);";
@@ -712,6 +868,12 @@ static int check_err_word(me_engine* e) {
     return code;
   }
   return ME_OK;
+}
+
+static int check_err_word(me_engine* e) {
+  uint32_t w = 0;
+  HIP_TRY(hipMemcpy(&w, e->bk.err, 4, hipMemcpyDeviceToHost), "read error word");
+  return check_err_bits(e, w);
 }
 
 extern "C" int me_submit_batch_device(me_engine* e, const me_order_soa* b, size_t n) {
@@ -742,6 +904,7 @@ extern "C" int me_sync(me_engine* e) {
 extern "C" int me_fetch_outputs(me_engine* e, me_fill* out_fills, size_t fills_cap, size_t* n_fills,
                                 me_order_result* out_results, size_t n_results) {
   if (!e) return ME_E_INVALID;
+  if (e->last_host) return e->fail(ME_E_INVALID, "the most recent batch was a host batch: its outputs come from me_collect");
   int rc = me_sync(e);
   if (rc) return rc;
   unsigned long long cnt = 0;
@@ -766,6 +929,7 @@ extern "C" uint32_t me_last_group_size(const me_engine* e) { return e ? e->lastg
 extern "C" int me_fetch_group_outputs(me_engine* e, uint32_t k, me_fill* out_fills, size_t fills_cap, size_t* n_fills,
                                       me_order_result* out_results, size_t n_results) {
   if (!e) return ME_E_INVALID;
+  if (e->last_host) return e->fail(ME_E_INVALID, "the most recent batch was a host batch: its outputs come from me_collect");
   int rc = me_sync(e);
   if (rc) return rc;
   if (k >= e->lastg.n) return e->fail(ME_E_INVALID, "batch index outside the last launch group");
@@ -787,47 +951,168 @@ extern "C" int me_fetch_group_outputs(me_engine* e, uint32_t k, me_fill* out_fil
   return ME_OK;
 }
 
+// ---- host-batch pipeline (include/me_engine.h) ----------------------------------------------
+static int slots_busy(me_engine* e) {
+  uint64_t oldest = UINT64_MAX;
+  for (auto& kv : e->by_ticket) oldest = std::min(oldest, kv.first);
+  return e->fail(ME_E_STATE, "all host slots busy: collect ticket " + std::to_string(oldest) + " first");
+}
+
+extern "C" int me_host_inputs(me_engine* e, size_t n, me_order_soa_w* out) {
+  if (!e || !out) return ME_E_INVALID;
+  if (n == 0 || n > e->cfg.max_batch) return e->fail(ME_E_INVALID, "me_host_inputs: n must be in [1, max_batch]");
+  if (e->free_slots.empty()) return slots_busy(e);
+  HostSlot& h = e->hs[e->free_slots.back()];
+  HIP_TRY(hipSetDevice(e->dev), "hipSetDevice");
+  int rc = slot_alloc(e, h);
+  if (rc) return rc;
+  // the slot's previous H2D may still be reading the staging buffer (its batch was collected, so it
+  // finished long ago, but the event is cheap to wait on)
+  HIP_TRY(hipEventSynchronize(h.ev_in), "hipEventSynchronize");
+  slot_soa(h.h_in, n, out->seq, out->price_q4, out->qty, out->symbol, out->kind);
+  return ME_OK;
+}
+
+extern "C" int me_submit_host(me_engine* e, const me_order_soa* b, size_t n, uint64_t* ticket) {
+  if (!e) return ME_E_INVALID;
+  if (e->failed) return ME_E_STATE;
+  if (!b || !b->seq || !b->price_q4 || !b->qty || !b->symbol || !b->kind) return e->fail(ME_E_INVALID, "null batch");
+  if (n == 0 || n > e->cfg.max_batch) return e->fail(ME_E_INVALID, "host batch size must be in [1, max_batch]");
+  if (e->free_slots.empty()) return slots_busy(e);
+  const int slot = e->free_slots.back();
+  HostSlot& h = e->hs[slot];
+  HIP_TRY(hipSetDevice(e->dev), "hipSetDevice");
+  int rc = slot_alloc(e, h);
+  if (rc) return rc;
+  uint64_t* seq;
+  int64_t* px;
+  int32_t* qty;
+  uint32_t* sym;
+  uint8_t* kind;
+  slot_soa(h.h_in, n, seq, px, qty, sym, kind);
+  if (b->seq != seq || b->price_q4 != px || b->qty != qty || b->symbol != sym || b->kind != kind) {
+    HIP_TRY(hipEventSynchronize(h.ev_in), "hipEventSynchronize");
+    memcpy(seq, b->seq, 8 * n);
+    memcpy(px, b->price_q4, 8 * n);
+    memcpy(qty, b->qty, 4 * n);
+    memcpy(sym, b->symbol, 4 * n);
+    memcpy(kind, b->kind, n);
+  }
+  // one H2D of the packed batch on the H2D stream; the engine stream waits for it before the launch
+  // that buckets (or sorts) the batch
+  HIP_TRY(hipMemcpyAsync(h.d_in, h.h_in, slot_in_bytes(n), hipMemcpyHostToDevice, e->s_h2d), "H2D host batch");
+  HIP_TRY(hipEventRecord(h.ev_in, e->s_h2d), "hipEventRecord");
+  HIP_TRY(hipStreamWaitEvent(e->stream, h.ev_in, 0), "hipStreamWaitEvent");
+  h.ticket = e->next_ticket;
+  h.n = (uint32_t)n;
+  h.state = 1;
+  h.big.clear();
+  slot_soa(h.d_in, n, seq, px, qty, sym, kind);
+  e->free_slots.pop_back();
+  e->by_ticket[h.ticket] = slot;
+  rc = enqueue_batch(e, seq, px, qty, sym, kind, (uint32_t)n, slot);
+  if (rc) return rc;
+  if (ticket) *ticket = e->next_ticket;
+  e->next_ticket++;
+  return ME_OK;
+}
+
+extern "C" int me_collect(me_engine* e, uint64_t ticket, const me_fill** fills, size_t* n_fills,
+                          const me_order_result** results, size_t* n_results) {
+  if (!e) return ME_E_INVALID;
+  auto it = e->by_ticket.find(ticket);
+  if (it == e->by_ticket.end()) return e->fail(ME_E_INVALID, "unknown or already collected ticket");
+  const int slot = it->second;
+  HostSlot& h = e->hs[slot];
+  HIP_TRY(hipSetDevice(e->dev), "hipSetDevice");
+  if (h.state == 1) {  // its group has not reached the tape job yet
+    if (e->failed) return ME_E_STATE;
+    int rc = flush_pipeline(e);
+    if (rc) return rc;
+  }
+  if (h.state != 2) return e->fail(ME_E_STATE, "host batch outputs were never enqueued");
+  HIP_TRY(hipEventSynchronize(h.ev_done), "hipEventSynchronize");
+  h.state = 0;  // collected: the outputs stay readable until the slot is reused
+  e->by_ticket.erase(it);
+  e->free_slots.push_back(slot);
+  const SlotMeta* m = (const SlotMeta*)h.h_out;
+  {
+    int rc = check_err_bits(e, m->err);
+    if (rc) return rc;
+  }
+  const uint64_t cnt = m->count;
+  me_fill* tape = (me_fill*)(h.h_out + sizeof(SlotMeta));
+  const uint64_t head = std::min<uint64_t>(e->hcap, (uint64_t)h.n + h.n / 2 + 1024);
+  if (cnt > head) {  // the rest of the slot's tape, and past its cap the spill from scratch
+    const uint64_t in_slot = std::min<uint64_t>(cnt, e->hcap);
+    HIP_TRY(hipMemcpy(tape + head, h.d_out + sizeof(SlotMeta) + head * sizeof(me_fill),
+                      (in_slot - head) * sizeof(me_fill), hipMemcpyDeviceToHost),
+            "D2H slot tape tail");
+    if (cnt > e->hcap) {
+      if (e->oset_gen[h.oset] != h.oset_gen) {  // this batch's output is lost; the books are intact (not sticky)
+        e->err = "host batch tape (" + std::to_string(cnt) + " fills) outgrew host_tape_cap and its scratch was "
+                 "reused before me_collect: raise host_tape_cap or collect within 3 launch groups";
+        return ME_E_CAPACITY;
+      }
+      const size_t extra = (size_t)(cnt - e->hcap);
+      if (extra > e->spill_cap) {
+        if (e->d_spill) HIP_TRY(hipFree(e->d_spill), "hipFree");
+        e->d_spill = nullptr;
+        e->spill_cap = 0;
+        HIP_TRY(hipMalloc((void**)&e->d_spill, extra * sizeof(me_fill)), "hipMalloc spill");
+        e->spill_cap = extra;
+      }
+      const auto& o = e->os[h.oset];
+      const me_order_result* dres = (const me_order_result*)(h.d_out + slot_res_off(e));
+      hipError_t he = launch_tape_spill(e->stream, dres, o.fstart, h.n, o.scratch, e->hcap, e->d_spill);
+      if (he != hipSuccess) return e->hip_fail(he, "spill launch");
+      HIP_TRY(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
+      h.big.resize(cnt);
+      memcpy(h.big.data(), tape, e->hcap * sizeof(me_fill));
+      HIP_TRY(hipMemcpy(h.big.data() + e->hcap, e->d_spill, extra * sizeof(me_fill), hipMemcpyDeviceToHost),
+              "D2H spill");
+      tape = h.big.data();
+    }
+  }
+  if (fills) *fills = tape;
+  if (n_fills) *n_fills = (size_t)cnt;
+  if (results) *results = (const me_order_result*)(h.h_out + slot_res_off(e));
+  if (n_results) *n_results = h.n;
+  return ME_OK;
+}
+
 extern "C" int me_submit_batch(me_engine* e, const me_order_soa* b, size_t n, me_fill* out_fills,
                                size_t fills_cap, size_t* n_fills, me_order_result* out_results) {
   if (!e) return ME_E_INVALID;
   if (e->failed) return ME_E_STATE;
   if (n_fills) *n_fills = 0;
-  if (n == 0) {
-    e->last_n = 0;
-    return ME_OK;
-  }
-  if (!b || !b->seq || !b->price_q4 || !b->qty || !b->symbol || !b->kind) return e->fail(ME_E_INVALID, "null batch");
-  if (n > e->cfg.max_batch) return e->fail(ME_E_INVALID, "batch larger than max_batch");
-  HIP_TRY(hipSetDevice(e->dev), "hipSetDevice");
-  {  // nothing launched may still read the staging buffers
-    int rc = me_sync(e);
-    if (rc) return rc;
-  }
-  // stage into pinned memory, one H2D per column
-  char* p = (char*)e->h_pin;
-  uint64_t* hs = (uint64_t*)p;
-  int64_t* hp = (int64_t*)(p + 8 * n);
-  int32_t* hq = (int32_t*)(p + 16 * n);
-  uint32_t* hy = (uint32_t*)(p + 20 * n);
-  uint8_t* hk = (uint8_t*)(p + 24 * n);
-  memcpy(hs, b->seq, 8 * n);
-  memcpy(hp, b->price_q4, 8 * n);
-  memcpy(hq, b->qty, 4 * n);
-  memcpy(hy, b->symbol, 4 * n);
-  memcpy(hk, b->kind, n);
-  hipStream_t st = e->stream;
-  HIP_TRY(hipMemcpyAsync(e->d_seq, hs, 8 * n, hipMemcpyHostToDevice, st), "H2D seq");
-  HIP_TRY(hipMemcpyAsync(e->d_px, hp, 8 * n, hipMemcpyHostToDevice, st), "H2D price");
-  HIP_TRY(hipMemcpyAsync(e->d_qty, hq, 4 * n, hipMemcpyHostToDevice, st), "H2D qty");
-  HIP_TRY(hipMemcpyAsync(e->d_sym, hy, 4 * n, hipMemcpyHostToDevice, st), "H2D symbol");
-  HIP_TRY(hipMemcpyAsync(e->d_kind, hk, n, hipMemcpyHostToDevice, st), "H2D kind");
-  int rc = enqueue_batch(e, e->d_seq, e->d_px, e->d_qty, e->d_sym, e->d_kind, (uint32_t)n);
+  if (n == 0) return ME_OK;
+  uint64_t t = 0;
+  int rc = me_submit_host(e, b, n, &t);
   if (rc) return rc;
-  return me_fetch_outputs(e, out_fills, fills_cap, n_fills, out_results, out_results ? n : 0);
+  const me_fill* f = nullptr;
+  const me_order_result* r = nullptr;
+  size_t nf = 0, nr = 0;
+  rc = me_collect(e, t, &f, &nf, &r, &nr);
+  if (rc) return rc;
+  if (n_fills) *n_fills = nf;
+  if (out_results) memcpy(out_results, r, nr * sizeof(me_order_result));
+  if (out_fills && nf) {
+    if (nf > fills_cap) return e->fail(ME_E_INVALID, "fills_cap smaller than the tape");
+    memcpy(out_fills, f, nf * sizeof(me_fill));
+  }
+  return ME_OK;
+}
+
+extern "C" int me_get_config(const me_engine* e, me_config* out) {
+  if (!e || !out) return ME_E_INVALID;
+  *out = e->cfg;
+  return ME_OK;
 }
 
 extern "C" int me_copy_tape_device(me_engine* e, void* dst, size_t cap_fills, size_t* n_fills) {
   if (!e) return ME_E_INVALID;
+  if (e->last_host) return e->fail(ME_E_INVALID, "the most recent batch was a host batch: its outputs come from me_collect");
   int rc = me_sync(e);
   if (rc) return rc;
   unsigned long long cnt = 0;
@@ -843,6 +1128,7 @@ extern "C" int me_copy_tape_device(me_engine* e, void* dst, size_t cap_fills, si
 
 extern "C" int me_copy_results_device(me_engine* e, void* dst, size_t n_results) {
   if (!e) return ME_E_INVALID;
+  if (e->last_host) return e->fail(ME_E_INVALID, "the most recent batch was a host batch: its outputs come from me_collect");
   if (e->failed) return ME_E_STATE;
   if (n_results > e->last_n) return e->fail(ME_E_INVALID, "n_results exceeds last batch size");
   if (n_results && !dst) return e->fail(ME_E_INVALID, "null destination");

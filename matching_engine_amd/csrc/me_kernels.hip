@@ -1299,7 +1299,8 @@ __global__ __launch_bounds__(256) void k_tape_compact(const uint32_t* __restrict
                                                       uint32_t n, const me_fill* __restrict__ scratch,
                                                       me_fill* __restrict__ tape, unsigned long long tape_cap,
                                                       unsigned long long* tape_count, unsigned long long* fills_acc,
-                                                      uint32_t* err) {
+                                                      uint32_t* err, me_order_result* hres, uint32_t* err_out) {
+  // hres != nullptr: a host batch (see AuxTape): tape_cap is soft, final results copied to hres
   __shared__ uint32_t off[TILE_TAPE + 1];
   __shared__ unsigned long long red[4];
   __shared__ uint32_t wsum[4];
@@ -1316,13 +1317,21 @@ __global__ __launch_bounds__(256) void k_tape_compact(const uint32_t* __restrict
   const unsigned long long base = red[0] + red[1] + red[2] + red[3];
   const uint32_t total = block_excl_scan_lds(off, cnt, wsum);
   if (tid == 0) off[cnt] = total;
-  for (uint32_t k = tid; k < cnt; k += 256) res[r0 + k].tape_offset = (uint32_t)(base + off[k]);
+  for (uint32_t k = tid; k < cnt; k += 256) {
+    res[r0 + k].tape_offset = (uint32_t)(base + off[k]);
+    if (hres) {
+      me_order_result r = res[r0 + k];
+      r.tape_offset = (uint32_t)(base + off[k]);
+      hres[r0 + k] = r;
+    }
+  }
   __syncthreads();
-  if (base + total > tape_cap) {
+  if (!hres && base + total > tape_cap) {
     if (tid == 0) atomicOr(err, ERR_SCRATCH_OOM);
     return;
   }
-  for (uint32_t f = tid; f < total; f += 256) {
+  const uint32_t lim = base >= tape_cap ? 0u : (uint32_t)min((unsigned long long)total, tape_cap - base);
+  for (uint32_t f = tid; f < lim; f += 256) {
     // last k with off[k] <= f
     uint32_t lo = 0, hi = cnt;  // off[lo] <= f < off[hi]
     while (hi - lo > 1) {
@@ -1338,6 +1347,23 @@ __global__ __launch_bounds__(256) void k_tape_compact(const uint32_t* __restrict
   if (b == gridDim.x - 1 && tid == 0) {
     *tape_count = base + total;
     atomicAdd(fills_acc, base + total);
+    if (err_out) *err_out = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// The fills of a host batch past its slot's soft tape cap (me_collect): record i's fills sit at
+// scratch[fstart[i] ..) and belong at tape[res[i].tape_offset ..); those at or past `cap` are copied
+// to spill[index - cap].
+__global__ __launch_bounds__(256) void k_tape_spill(const me_order_result* __restrict__ res,
+                                                    const uint32_t* __restrict__ fstart, uint32_t n,
+                                                    const me_fill* __restrict__ scratch, unsigned long long cap,
+                                                    me_fill* __restrict__ spill) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= n) return;
+  const me_order_result r = res[i];
+  for (uint32_t q = 0; q < r.fill_count; ++q) {
+    const unsigned long long t = (unsigned long long)r.tape_offset + q;
+    if (t >= cap) spill[t - cap] = scratch[fstart[i] + q];
   }
 }
 
@@ -1419,10 +1445,18 @@ hipError_t launch_seq_sweep(hipStream_t st, const BookDev& bk, const uint64_t* c
 }
 
 hipError_t launch_tape(hipStream_t st, const BatchDev& bt, me_fill* tape, unsigned long long tape_cap,
-                       unsigned long long* tape_count, unsigned long long* fills_acc, uint32_t* err) {
+                       unsigned long long* tape_count, unsigned long long* fills_acc, uint32_t* err,
+                       me_order_result* hres, uint32_t* err_out) {
   const uint32_t ntiles = (bt.n + TILE_TAPE - 1) / TILE_TAPE;
   hipLaunchKernelGGL(k_tape_compact, dim3(ntiles), dim3(256), 0, st, bt.tile_sum, ntiles, bt.res, bt.fstart,
-                     bt.n, bt.scratch, tape, tape_cap, tape_count, fills_acc, err);
+                     bt.n, bt.scratch, tape, tape_cap, tape_count, fills_acc, err, hres, err_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_tape_spill(hipStream_t st, const me_order_result* res, const uint32_t* fstart, uint32_t n,
+                             const me_fill* scratch, unsigned long long cap, me_fill* spill) {
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(k_tape_spill, dim3((n + 255) / 256), dim3(256), 0, st, res, fstart, n, scratch, cap, spill);
   return hipGetLastError();
 }
 

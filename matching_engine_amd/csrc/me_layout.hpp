@@ -241,10 +241,17 @@ struct AuxBucket {  // bucket + clear job of one batch
 struct AuxTape {  // tape job of one batch
   const uint32_t* tile_sum;
   me_order_result* res;
-  const uint32_t* fstart;
+  uint32_t* fstart;
   const me_fill* scratch;
   me_fill* tape;
   unsigned long long* tape_count;
+  // Host batches (me_submit_host): the tape buffer is the slot's, `cap` records long and SOFT — fills
+  // past it are not copied (me_collect recovers them from scratch) and raise no error; the final
+  // results go to hres, each record's scratch start to fstart, the error word to err_out.
+  // Device batches: hres == nullptr, cap = the tape bound (exceeding it is ERR_SCRATCH_OOM).
+  me_order_result* hres;
+  uint32_t* err_out;
+  unsigned long long cap;
   uint32_t tn;
   uint32_t pad;
 };
@@ -253,7 +260,6 @@ struct AuxDev {
   uint32_t nwg;  // workgroups that run side jobs (those of the first dispatch round)
   uint32_t nb;   // bucket jobs (batches of group J)
   uint32_t nt;   // tape jobs (batches of group J-2)
-  unsigned long long tape_cap;
   unsigned long long* fills_acc;
   AuxBucket b[ME_GMAX];
   AuxTape t[ME_GMAX];

@@ -967,6 +967,9 @@ __device__ __forceinline__ void aux_tape_tile(const ColdArgs& G, uint32_t jb, ui
   const gptr<me_order_result> res = ldsg(J.res);
   const gptr<const me_fill> scratch = ldsg(J.scratch);
   const gptr<me_fill> tape = ldsg(J.tape);
+  const gptr<me_order_result> hres = ldsg(J.hres);
+  const bool host = hres != nullptr;  // a host batch: soft tape cap, results and scratch starts kept
+  const unsigned long long cap = ldsu(J.cap);
   long long acc = 0;  // fills of the earlier tiles
   for (uint32_t u = (uint32_t)lane; u < t; u += 64) acc += tile_sum[u];
   for (int d = 32; d >= 1; d >>= 1) acc += __shfl_xor(acc, d, 64);
@@ -992,7 +995,21 @@ __device__ __forceinline__ void aux_tape_tile(const ColdArgs& G, uint32_t jb, ui
     if (j < cnt) res[r0 + j].tape_offset = (uint32_t)(base + o);
     o += c[k];
   }
-  if (base + total > ldsu(G.ax.tape_cap)) {
+  if (host) {  // the slot's copy of the final results; the scratch starts stay for me_collect's spill
+    const gptr<uint32_t> fst = ldsg(J.fstart);
+    uint32_t o3 = (uint32_t)(incl - loc);
+#pragma unroll
+    for (int k = 0; k < TILE_TAPE / 64; ++k) {
+      const uint32_t j = (uint32_t)(lane * (TILE_TAPE / 64) + k);
+      if (j < cnt) {
+        me_order_result r = res[r0 + j];  // written by the match job of an earlier launch
+        r.tape_offset = (uint32_t)(base + o3);
+        hres[r0 + j] = r;
+        fst[r0 + j] = src[k];
+      }
+      o3 += c[k];
+    }
+  } else if (base + total > cap) {
     if (lane == 0) atomicOr(ldsg(G.bk.err), ERR_SCRATCH_OOM);
     return;
   }
@@ -1001,12 +1018,14 @@ __device__ __forceinline__ void aux_tape_tile(const ColdArgs& G, uint32_t jb, ui
 #pragma unroll
   for (int k = 0; k < TILE_TAPE / 64; ++k) {
     if (c[k])
-      for (uint32_t q = 0; q < c[k]; ++q) tape[base + o2 + q] = scratch[src[k] + q];
+      for (uint32_t q = 0; q < c[k]; ++q)
+        if (base + o2 + q < cap) tape[base + o2 + q] = scratch[src[k] + q];
     o2 += c[k];
   }
   if (t == ntiles - 1 && lane == 0) {
     *ldsg(J.tape_count) = base + total;
     atomicAdd(ldsg(G.ax.fills_acc), base + total);
+    if (host) *ldsg(J.err_out) = __hip_atomic_load(ldsg(G.bk.err), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 

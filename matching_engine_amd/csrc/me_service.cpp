@@ -3,11 +3,22 @@
 // Per order (host, synchronous, the reference's exact contract):
 //   validate (matching_engine_service.cpp:66-83) -> "OID-<n>" (:85, :29-32) -> normalize_to_q4
 //   (:89-97, price.hpp:15-29) -> side CHECK (storage.cpp:32) -> response (:107-114)
-// and the order joins the open time slice (SoA). me_service_flush matches the slice on the GPU
-// engine and persists it in ONE SQLite transaction (the batched rewrite of storage.cpp:78-208):
-// orders rows exactly as insert_new_order writes them (incl. order_type=1, storage.cpp:106),
-// update_order_status-style updates for the matched outcome, and fills rows through the
+// and the order joins the open time slice (SoA). A slice closes when it reaches the slice size or
+// (with the background flusher, me_service_start) when it is older than the interval; closed slices
+// are matched on the engine and persisted, in stream order, OUTSIDE the submit lock — SubmitOrder
+// only ever waits for another SubmitOrder. Persistence is ONE SQLite transaction per slice (the
+// batched rewrite of storage.cpp:78-208): each order's row as insert_new_order writes it (incl.
+// order_type=1, storage.cpp:106) carrying its matched status and remainder in the same INSERT,
+// update_order_status-style updates for makers and cancel targets, and fills rows through the
 // corrected add_fill statement (5 columns, 5 placeholders; the reference's has 6, storage.cpp:190).
+//
+// Locks (always taken in this order, never the other way round):
+//   flush_mu  one flusher at a time: slices are matched and persisted in stream order; owns the DB
+//   eng_mu    every engine call (the engine is single-threaded): flush matching, book reads
+//   mu        the open slice, the closed-slice queue, the symbol table, the OID counter
+//   live_mu   resting orders' owners and remainders (cancel ownership, OrderUpdate bookkeeping)
+//   upd_mu    the OrderUpdate queue
+//   err_mu    the last error text
 //
 // SQLite is loaded at run time (dlopen libsqlite3.so.0) so the library has no build-time
 // dependency on a sqlite3 header.
@@ -15,9 +26,11 @@
 #include <string.h>
 
 #include <chrono>
+#include <condition_variable>
 #include <deque>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -87,6 +100,10 @@ inline int64_t now_ms() {
   using namespace std::chrono;
   return duration_cast<milliseconds>(system_clock::now().time_since_epoch()).count();
 }
+inline int64_t mono_us() {
+  using namespace std::chrono;
+  return duration_cast<microseconds>(steady_clock::now().time_since_epoch()).count();
+}
 
 // storage.cpp:26-69, verbatim schema semantics.
 const char* kSchema =
@@ -105,14 +122,34 @@ const char* kSchema =
 
 struct Pending {
   std::string client;
-  uint32_t symbol_id;
   std::string symbol;
   int32_t side;
   bool cancel;      // CancelOrder record (build extension): target = the order it removes
   uint64_t target;
 };
 
-// A resting order the OrderUpdate stream still reports on (owner + unfilled quantity).
+// One time slice: the SoA handed to the engine + the host-only fields persistence needs.
+struct Slice {
+  std::vector<uint64_t> seq;
+  std::vector<int64_t> px;
+  std::vector<int32_t> qty;
+  std::vector<uint32_t> sid;
+  std::vector<uint8_t> kind;
+  std::vector<Pending> meta;
+  int64_t opened_us = 0;
+  size_t size() const { return seq.size(); }
+};
+
+// A matched slice whose transaction failed: kept, in order, until a later flush commits it.
+struct Unpersisted {
+  Slice sl;
+  std::vector<me_order_result> res;
+  std::vector<me_fill> tape;
+  int64_t ts;
+};
+
+// An order the OrderUpdate stream still reports on, and whose owner may cancel it: every accepted
+// LIMIT order from SubmitOrder until it stops resting.
 struct Live {
   std::string client;
   std::string symbol;
@@ -125,38 +162,50 @@ constexpr size_t kMaxQueuedUpdates = size_t(1) << 24;  // oldest events are drop
 
 struct me_service {
   me_engine* eng = nullptr;
+  uint32_t sym_cap = UINT32_MAX;  // symbols the engine holds (local ids 0 .. sym_cap-1)
+  size_t slice_max = 0;           // records per slice (the engine's max_batch)
+  // --- mu
+  std::mutex mu;
   std::unordered_map<std::string, uint32_t> sym;
   std::vector<std::string> names;
   uint64_t next_id = 1;
-  mutable std::mutex mu;
-  // open time slice (SoA handed to the engine) + the host-only fields persistence needs
-  std::vector<uint64_t> seq;
-  std::vector<int64_t> px;
-  std::vector<int32_t> qty;
-  std::vector<uint32_t> sid;
-  std::vector<uint8_t> kind;
-  std::vector<Pending> meta;
-  // StreamOrderUpdates: resting orders by seq, and the undrained events
+  Slice open;
+  std::deque<Slice> closed;
+  size_t closed_records = 0;
+  // --- flush_mu (persistence + retry queue)
+  std::mutex flush_mu;
+  std::deque<Unpersisted> unpersisted;
+  size_t unpersisted_records = 0;  // read without flush_mu through an atomic-free snapshot under mu
+  // --- eng_mu
+  std::mutex eng_mu;
+  // --- live_mu / upd_mu
+  std::mutex live_mu;
   std::unordered_map<uint64_t, Live> live;
+  std::mutex upd_mu;
   std::deque<me_order_update> updates;
   uint64_t updates_dropped = 0;
-  // persistence
+  // --- background flusher
+  std::thread flusher;
+  std::condition_variable cv;  // with mu
+  bool stop = false;
+  int64_t interval_us = 0;
+  // --- persistence (under flush_mu)
   sqlite3* db = nullptr;
   sqlite3_stmt* st_ins = nullptr;
   sqlite3_stmt* st_upd = nullptr;
   sqlite3_stmt* st_fill = nullptr;
   sqlite3_stmt* st_maker = nullptr;
+  bool failed = false;  // the engine lost a slice it had accepted: nothing more can be matched
+  // --- err_mu
+  mutable std::mutex err_mu;
   std::string err;
 
   int fail(int code, const std::string& m) {
+    std::lock_guard<std::mutex> lk(err_mu);
     err = m;
     return code;
   }
-  bool sql_ok(int rc, const char* what) {
-    if (rc == SQLITE_OK || rc == SQLITE_DONE || rc == SQLITE_ROW) return true;
-    err = std::string(what) + ": " + (db ? g_sql.errmsg(db) : "no db");
-    return false;
-  }
+  std::string sql_err(const char* what) { return std::string(what) + ": " + (db ? g_sql.errmsg(db) : "no db"); }
 };
 
 static void close_db(me_service* s) {
@@ -167,29 +216,35 @@ static void close_db(me_service* s) {
   s->db = nullptr;
 }
 
-static bool open_db(me_service* s, const char* path) {
+static bool sql_ok(int rc) { return rc == SQLITE_OK || rc == SQLITE_DONE || rc == SQLITE_ROW; }
+
+static bool open_db(me_service* s, const char* path, std::string& err) {
   {
     std::lock_guard<std::mutex> lk(g_sql_mu);
-    if (!g_sql.load(s->err)) return false;
+    if (!g_sql.load(err)) return false;
   }
-  if (!s->sql_ok(g_sql.open_v2(path, &s->db, SQLITE_OPEN_READWRITE | SQLITE_OPEN_CREATE | SQLITE_OPEN_FULLMUTEX,
-                               nullptr),
-                 "open"))
+  auto chk = [&](int rc, const char* what) {
+    if (sql_ok(rc)) return true;
+    err = s->sql_err(what);
+    return false;
+  };
+  if (!chk(g_sql.open_v2(path, &s->db, SQLITE_OPEN_READWRITE | SQLITE_OPEN_CREATE | SQLITE_OPEN_FULLMUTEX, nullptr),
+           "open"))
     return false;
   g_sql.busy_timeout(s->db, 5000);  // storage.cpp:14
   // storage.cpp:17-24 pragmas, then the schema
-  if (!s->sql_ok(g_sql.exec(s->db, "PRAGMA journal_mode=WAL;", nullptr, nullptr, nullptr), "pragma") ||
-      !s->sql_ok(g_sql.exec(s->db, "PRAGMA synchronous=NORMAL;", nullptr, nullptr, nullptr), "pragma") ||
-      !s->sql_ok(g_sql.exec(s->db, "PRAGMA foreign_keys=ON;", nullptr, nullptr, nullptr), "pragma") ||
-      !s->sql_ok(g_sql.exec(s->db, kSchema, nullptr, nullptr, nullptr), "schema"))
+  if (!chk(g_sql.exec(s->db, "PRAGMA journal_mode=WAL;", nullptr, nullptr, nullptr), "pragma") ||
+      !chk(g_sql.exec(s->db, "PRAGMA synchronous=NORMAL;", nullptr, nullptr, nullptr), "pragma") ||
+      !chk(g_sql.exec(s->db, "PRAGMA foreign_keys=ON;", nullptr, nullptr, nullptr), "pragma") ||
+      !chk(g_sql.exec(s->db, kSchema, nullptr, nullptr, nullptr), "schema"))
     return false;
   // load_next_oid_seq (storage.cpp:254-267)
   sqlite3_stmt* q = nullptr;
-  if (!s->sql_ok(g_sql.prepare_v2(s->db,
-                                  "SELECT COALESCE(MAX(CAST(SUBSTR(order_id, 5) AS INTEGER)), 0) + 1 "
-                                  "FROM orders WHERE order_id LIKE 'OID-%'",
-                                  -1, &q, nullptr),
-                 "prepare oid"))
+  if (!chk(g_sql.prepare_v2(s->db,
+                            "SELECT COALESCE(MAX(CAST(SUBSTR(order_id, 5) AS INTEGER)), 0) + 1 "
+                            "FROM orders WHERE order_id LIKE 'OID-%'",
+                            -1, &q, nullptr),
+           "prepare oid"))
     return false;
   if (g_sql.step(q) == SQLITE_ROW) s->next_id = (uint64_t)g_sql.column_int64(q, 0);
   g_sql.finalize(q);
@@ -202,38 +257,79 @@ static bool open_db(me_service* s, const char* path) {
   const char* maker =
       "UPDATE orders SET remaining_quantity=remaining_quantity-?, status=CASE WHEN remaining_quantity-?=0 "
       "THEN 2 ELSE 1 END, updated_ts=? WHERE order_id=?";
-  return s->sql_ok(g_sql.prepare_v2(s->db, ins, -1, &s->st_ins, nullptr), "prepare insert") &&
-         s->sql_ok(g_sql.prepare_v2(s->db, upd, -1, &s->st_upd, nullptr), "prepare update") &&
-         s->sql_ok(g_sql.prepare_v2(s->db, fill, -1, &s->st_fill, nullptr), "prepare fill") &&
-         s->sql_ok(g_sql.prepare_v2(s->db, maker, -1, &s->st_maker, nullptr), "prepare maker");
+  return chk(g_sql.prepare_v2(s->db, ins, -1, &s->st_ins, nullptr), "prepare insert") &&
+         chk(g_sql.prepare_v2(s->db, upd, -1, &s->st_upd, nullptr), "prepare update") &&
+         chk(g_sql.prepare_v2(s->db, fill, -1, &s->st_fill, nullptr), "prepare fill") &&
+         chk(g_sql.prepare_v2(s->db, maker, -1, &s->st_maker, nullptr), "prepare maker");
 }
 
 extern "C" me_service* me_service_create(me_engine* engine, const char* const* symbols, uint32_t num_symbols,
                                          const char* db_path) {
   me_service* s = new me_service();
   s->eng = engine;
+  if (engine) {
+    me_config c{};
+    if (me_get_config(engine, &c) == ME_OK) {
+      s->sym_cap = c.num_symbols;
+      s->slice_max = c.max_batch;
+    }
+  }
   for (uint32_t i = 0; i < num_symbols; ++i) {
     s->names.emplace_back(symbols[i]);
     s->sym.emplace(s->names.back(), i);
   }
-  if (db_path && !open_db(s, db_path)) {
+  if (s->names.size() > s->sym_cap) s->fail(ME_E_INVALID, "me_service_create: more symbols than the engine holds");
+  std::string err;
+  if (db_path && !open_db(s, db_path, err)) {
     // keep the object so the caller can read the error; persistence is disabled
     close_db(s);
-    s->err = "me_service_create: " + s->err;
+    s->fail(ME_E_SQLITE, "me_service_create: " + err);
   }
   return s;
-}
-
-extern "C" void me_service_destroy(me_service* s) {
-  if (!s) return;
-  close_db(s);
-  delete s;
 }
 
 static void put(char* dst, size_t cap, const std::string& v) {
   size_t k = v.size() < cap - 1 ? v.size() : cap - 1;
   memcpy(dst, v.data(), k);
   dst[k] = 0;
+}
+
+// Close the open slice (mu held).
+static void close_open(me_service* s) {
+  if (!s->open.size()) return;
+  s->closed_records += s->open.size();
+  s->closed.push_back(std::move(s->open));
+  s->open = Slice{};
+  s->cv.notify_all();
+}
+
+// Append a record to the open slice (mu held); a full slice is closed and handed to the flusher.
+static void append(me_service* s, uint64_t seq, int64_t px, int32_t qty, uint32_t sid, uint8_t kind, Pending&& m) {
+  Slice& o = s->open;
+  if (!o.size()) o.opened_us = mono_us();
+  o.seq.push_back(seq);
+  o.px.push_back(px);
+  o.qty.push_back(qty);
+  o.sid.push_back(sid);
+  o.kind.push_back(kind);
+  o.meta.push_back(std::move(m));
+  if (s->slice_max && o.size() >= s->slice_max) close_open(s);
+}
+
+// Symbol string -> local id, interning a new one while the engine has room (mu held). The reference
+// accepts any non-empty symbol (matching_engine_service.cpp:66-71): a new symbol's book is the
+// engine's next unused local book, its window placed by its first orders.
+static bool intern(me_service* s, const std::string& symbol, uint32_t& sid) {
+  auto it = s->sym.find(symbol);
+  if (it != s->sym.end()) {
+    sid = it->second;
+    return true;
+  }
+  if (s->names.size() >= s->sym_cap) return false;
+  sid = (uint32_t)s->names.size();
+  s->names.push_back(symbol);
+  s->sym.emplace(symbol, sid);
+  return true;
 }
 
 extern "C" int me_service_submit_order(me_service* s, const me_order_request* r, me_order_response* resp) {
@@ -252,7 +348,15 @@ extern "C" int me_service_submit_order(me_service* s, const me_order_request* r,
     put(resp->error_message, sizeof resp->error_message, "price must be > 0 for LIMIT");
     return 0;
   }
+  const std::string sym(symbol);
+  std::string client = r->client_id ? r->client_id : "";
   std::lock_guard<std::mutex> lk(s->mu);
+  uint32_t sid = 0;
+  if (!intern(s, sym, sid)) {  // the engine's books are all taken: RESOURCE_EXHAUSTED, no OID
+    resp->grpc_status = 8;
+    put(resp->error_message, sizeof resp->error_message, "symbol capacity exhausted");
+    return 0;
+  }
   // --- OID (:85), consumed even if normalisation throws below
   const uint64_t id = s->next_id++;
   int64_t q4 = 0;
@@ -272,15 +376,13 @@ extern "C" int me_service_submit_order(me_service* s, const me_order_request* r,
     return 0;
   }
   resp->success = 1;
-  // --- join the open time slice
-  auto it = s->sym.find(symbol);
-  const uint32_t sid = it == s->sym.end() ? (uint32_t)s->names.size() : it->second;  // unknown -> BAD_SYMBOL
-  s->seq.push_back(id);
-  s->px.push_back(q4);
-  s->qty.push_back(r->quantity);
-  s->sid.push_back(sid);
-  s->kind.push_back(ME_KIND(r->side, r->order_type == ME_TYPE_LIMIT ? ME_TYPE_LIMIT : ME_TYPE_MARKET, ME_OP_NEW));
-  s->meta.push_back(Pending{r->client_id ? r->client_id : "", sid, symbol, r->side, false, 0});
+  const bool limit = r->order_type == ME_TYPE_LIMIT;
+  if (limit) {  // its owner, for CancelOrder and the OrderUpdate stream
+    std::lock_guard<std::mutex> lv(s->live_mu);
+    s->live[id] = Live{client, sym, r->quantity};
+  }
+  append(s, id, q4, r->quantity, sid, ME_KIND(r->side, limit ? ME_TYPE_LIMIT : ME_TYPE_MARKET, ME_OP_NEW),
+         Pending{std::move(client), sym, r->side, false, 0});
   return 0;
 }
 
@@ -307,29 +409,47 @@ extern "C" int me_service_cancel_order(me_service* s, const me_cancel_request* r
     put(resp->error_message, sizeof resp->error_message, "order_id is invalid");
     return 0;
   }
+  const std::string client = r->client_id ? r->client_id : "";
+  const std::string sym(symbol);
   std::lock_guard<std::mutex> lk(s->mu);
+  {  // only the order's owner may cancel it
+    std::lock_guard<std::mutex> lv(s->live_mu);
+    auto it = s->live.find(target);
+    if (it != s->live.end() && it->second.client != client) {
+      put(resp->error_message, sizeof resp->error_message, "order belongs to another client");
+      return 0;
+    }
+  }
+  uint32_t sid = 0;
+  if (!intern(s, sym, sid)) {
+    resp->grpc_status = 8;
+    put(resp->error_message, sizeof resp->error_message, "symbol capacity exhausted");
+    return 0;
+  }
   const uint64_t id = s->next_id++;  // the cancel's stream position (batch order == seq order)
   put(resp->order_id, sizeof resp->order_id, "OID-" + std::to_string(target));
   resp->success = 1;
-  auto it = s->sym.find(symbol);
-  const uint32_t sid = it == s->sym.end() ? (uint32_t)s->names.size() : it->second;
-  s->seq.push_back(id);
-  s->px.push_back((int64_t)target);
-  s->qty.push_back(0);
-  s->sid.push_back(sid);
-  s->kind.push_back(ME_KIND(ME_SIDE_BUY, ME_TYPE_LIMIT, ME_OP_CANCEL));
-  s->meta.push_back(Pending{r->client_id ? r->client_id : "", sid, symbol, 0, true, target});
+  append(s, id, (int64_t)target, 0, sid, ME_KIND(ME_SIDE_BUY, ME_TYPE_LIMIT, ME_OP_CANCEL),
+         Pending{client, sym, 0, true, target});
   return 0;
 }
 
 extern "C" size_t me_service_pending(const me_service* s) {
-  std::lock_guard<std::mutex> lk(s->mu);
-  return s->seq.size();
+  me_service* m = const_cast<me_service*>(s);
+  std::lock_guard<std::mutex> lk(m->mu);
+  return m->open.size() + m->closed_records;
 }
 
 extern "C" uint64_t me_service_next_oid(const me_service* s) {
-  std::lock_guard<std::mutex> lk(s->mu);
-  return s->next_id;
+  me_service* m = const_cast<me_service*>(s);
+  std::lock_guard<std::mutex> lk(m->mu);
+  return m->next_id;
+}
+
+extern "C" size_t me_service_unpersisted(const me_service* s) {
+  me_service* m = const_cast<me_service*>(s);
+  std::lock_guard<std::mutex> lk(m->mu);
+  return m->unpersisted_records;
 }
 
 static void push_update(me_service* s, uint64_t oid, const std::string& client, const std::string& symbol,
@@ -352,49 +472,61 @@ static void push_update(me_service* s, uint64_t oid, const std::string& client, 
 }
 
 // OrderUpdate events of one matched slice (order documented in me_service.h), and the live-order
-// table they are computed from (owner and unfilled quantity of every resting order).
-static void emit_updates(me_service* s, size_t n, const me_order_result* res, const me_fill* tape) {
-  for (size_t i = 0; i < n; ++i) {
-    const Pending& m = s->meta[i];
-    const me_order_result& r = res[i];
-    if (m.cancel) {
-      auto it = s->live.find(m.target);
-      if (r.status == ME_ST_CANCELED && it != s->live.end()) {
-        push_update(s, m.target, it->second.client, it->second.symbol, ME_ST_CANCELED, 0, 0, r.remaining_qty);
-        s->live.erase(it);
+// table they are computed from. Locks are taken per block of records so SubmitOrder / CancelOrder
+// (which touch the live table) never wait for a whole slice.
+static void emit_updates(me_service* s, const Slice& sl, const me_order_result* res, const me_fill* tape) {
+  constexpr size_t kBlock = 512;
+  for (size_t i0 = 0; i0 < sl.size(); i0 += kBlock) {
+    std::lock_guard<std::mutex> lv(s->live_mu);
+    std::lock_guard<std::mutex> lu(s->upd_mu);
+    for (size_t i = i0; i < sl.size() && i < i0 + kBlock; ++i) {
+      const Pending& m = sl.meta[i];
+      const me_order_result& r = res[i];
+      if (m.cancel) {
+        auto it = s->live.find(m.target);
+        if (r.status == ME_ST_CANCELED && it != s->live.end()) {
+          push_update(s, m.target, it->second.client, it->second.symbol, ME_ST_CANCELED, 0, 0, r.remaining_qty);
+          s->live.erase(it);
+        } else {
+          push_update(s, m.target, m.client, m.symbol, r.status == ME_ST_CANCELED ? ME_ST_CANCELED : ME_ST_REJECTED,
+                      0, 0, r.remaining_qty);
+        }
+        continue;
+      }
+      const uint64_t oid = sl.seq[i];
+      int32_t rem = sl.qty[i];
+      for (uint32_t f = 0; f < r.fill_count; ++f) {
+        const me_fill& fl = tape[r.tape_offset + f];
+        auto it = s->live.find(fl.maker_seq);
+        if (it != s->live.end()) {
+          Live& mk = it->second;
+          mk.remaining -= fl.qty;
+          push_update(s, fl.maker_seq, mk.client, mk.symbol,
+                      mk.remaining > 0 ? ME_ST_PARTIALLY_FILLED : ME_ST_FILLED, fl.price_q4, fl.qty, mk.remaining);
+          if (mk.remaining <= 0) s->live.erase(it);
+        }
+        rem -= fl.qty;
+        push_update(s, oid, m.client, m.symbol, rem > 0 ? ME_ST_PARTIALLY_FILLED : ME_ST_FILLED, fl.price_q4,
+                    fl.qty, rem);
+      }
+      const bool market = ((sl.kind[i] >> 2) & 1u) != 0;
+      if (r.status == ME_ST_REJECTED || r.status == ME_ST_CANCELED || (r.fill_count == 0 && r.status == ME_ST_NEW))
+        push_update(s, oid, m.client, m.symbol, r.status, 0, 0, r.remaining_qty);
+      if (market) continue;
+      if (r.remaining_qty > 0 && (r.status == ME_ST_NEW || r.status == ME_ST_PARTIALLY_FILLED)) {
+        auto it = s->live.find(oid);
+        if (it != s->live.end()) it->second.remaining = r.remaining_qty;
+        else s->live[oid] = Live{m.client, m.symbol, r.remaining_qty};
       } else {
-        push_update(s, m.target, m.client, m.symbol, r.status == ME_ST_CANCELED ? ME_ST_CANCELED : ME_ST_REJECTED,
-                    0, 0, r.remaining_qty);
+        s->live.erase(oid);
       }
-      continue;
     }
-    const uint64_t oid = s->seq[i];
-    int32_t rem = s->qty[i];
-    for (uint32_t f = 0; f < r.fill_count; ++f) {
-      const me_fill& fl = tape[r.tape_offset + f];
-      auto it = s->live.find(fl.maker_seq);
-      if (it != s->live.end()) {
-        Live& mk = it->second;
-        mk.remaining -= fl.qty;
-        push_update(s, fl.maker_seq, mk.client, mk.symbol,
-                    mk.remaining > 0 ? ME_ST_PARTIALLY_FILLED : ME_ST_FILLED, fl.price_q4, fl.qty, mk.remaining);
-        if (mk.remaining <= 0) s->live.erase(it);
-      }
-      rem -= fl.qty;
-      push_update(s, oid, m.client, m.symbol, rem > 0 ? ME_ST_PARTIALLY_FILLED : ME_ST_FILLED, fl.price_q4,
-                  fl.qty, rem);
-    }
-    const bool market = ((s->kind[i] >> 2) & 1u) != 0;
-    if (r.status == ME_ST_REJECTED || r.status == ME_ST_CANCELED || (r.fill_count == 0 && r.status == ME_ST_NEW))
-      push_update(s, oid, m.client, m.symbol, r.status, 0, 0, r.remaining_qty);
-    if (!market && r.remaining_qty > 0 && (r.status == ME_ST_NEW || r.status == ME_ST_PARTIALLY_FILLED))
-      s->live[oid] = Live{m.client, m.symbol, r.remaining_qty};
   }
 }
 
 extern "C" int me_service_updates(me_service* s, const char* client_id, me_order_update* out, size_t cap,
                                   size_t* n) {
-  std::lock_guard<std::mutex> lk(s->mu);
+  std::lock_guard<std::mutex> lk(s->upd_mu);
   size_t k = 0;
   const bool all = !client_id || !client_id[0];
   if (all) {
@@ -418,18 +550,26 @@ extern "C" int me_service_updates(me_service* s, const char* client_id, me_order
   return ME_OK;
 }
 
-static bool persist(me_service* s, size_t n, const me_order_result* res, const me_fill* tape, size_t nf) {
+// One transaction for one matched slice (flush_mu held).
+static bool persist(me_service* s, const Slice& sl, const me_order_result* res, const me_fill* tape, int64_t ts,
+                    std::string& err) {
   if (!s->db) return true;
-  const int64_t ts = now_ms();
+  bool ok = true;
   auto step = [&](sqlite3_stmt* st, const char* what) {
     const int rc = g_sql.step(st);
     g_sql.reset(st);
-    return s->sql_ok(rc, what);
+    if (!sql_ok(rc)) {
+      err = s->sql_err(what);
+      return false;
+    }
+    return true;
   };
-  if (!s->sql_ok(g_sql.exec(s->db, "BEGIN", nullptr, nullptr, nullptr), "begin")) return false;
-  bool ok = true;
-  for (size_t i = 0; i < n && ok; ++i) {
-    const Pending& m = s->meta[i];
+  if (!sql_ok(g_sql.exec(s->db, "BEGIN", nullptr, nullptr, nullptr))) {
+    err = s->sql_err("begin");
+    return false;
+  }
+  for (size_t i = 0; i < sl.size() && ok; ++i) {
+    const Pending& m = sl.meta[i];
     if (m.cancel) {  // no row of its own: the target's row becomes CANCELED
       if (res[i].status == ME_ST_CANCELED) {
         const std::string toid = "OID-" + std::to_string(m.target);
@@ -442,17 +582,20 @@ static bool persist(me_service* s, size_t n, const me_order_result* res, const m
       }
       continue;
     }
-    const std::string oid = "OID-" + std::to_string(s->seq[i]);
-    sqlite3_stmt* st = s->st_ins;  // insert_new_order's row (storage.cpp:102-112)
+    // insert_new_order's row (storage.cpp:102-112) with the matched outcome in the same INSERT:
+    // status and remaining_quantity are what an insert (NEW, quantity) followed by
+    // update_order_status (storage.cpp:160-181) would leave
+    const std::string oid = "OID-" + std::to_string(sl.seq[i]);
+    sqlite3_stmt* st = s->st_ins;
     g_sql.bind_text(st, 1, oid.c_str(), -1, SQLITE_TRANSIENT);
     g_sql.bind_text(st, 2, m.client.c_str(), -1, SQLITE_TRANSIENT);
     g_sql.bind_text(st, 3, m.symbol.c_str(), -1, SQLITE_TRANSIENT);
     g_sql.bind_int64(st, 4, m.side);
     g_sql.bind_int64(st, 5, 1);  // order_type: the reference binds the constant 1 (storage.cpp:106)
-    g_sql.bind_int64(st, 6, s->px[i]);
-    g_sql.bind_int64(st, 7, s->qty[i]);
-    g_sql.bind_int64(st, 8, 0);
-    g_sql.bind_int64(st, 9, s->qty[i]);
+    g_sql.bind_int64(st, 6, sl.px[i]);
+    g_sql.bind_int64(st, 7, sl.qty[i]);
+    g_sql.bind_int64(st, 8, res[i].status);
+    g_sql.bind_int64(st, 9, res[i].remaining_qty);  // unfilled qty (0 once FILLED)
     g_sql.bind_int64(st, 10, ts);
     g_sql.bind_int64(st, 11, ts);
     ok = step(st, "insert order");
@@ -476,82 +619,255 @@ static bool persist(me_service* s, size_t n, const me_order_result* res, const m
         ok = step(fs, "insert fill");
       }
     }
-    if (ok && (res[i].status != ME_ST_NEW || res[i].remaining_qty != s->qty[i])) {
-      sqlite3_stmt* up = s->st_upd;  // update_order_status (storage.cpp:160-181)
-      g_sql.bind_int64(up, 1, res[i].status);
-      g_sql.bind_int64(up, 2, res[i].remaining_qty);  // unfilled qty (0 once FILLED)
-      g_sql.bind_int64(up, 3, ts);
-      g_sql.bind_text(up, 4, oid.c_str(), -1, SQLITE_TRANSIENT);
-      ok = step(up, "update order");
-    }
   }
-  (void)nf;
   if (!ok) {
     g_sql.exec(s->db, "ROLLBACK", nullptr, nullptr, nullptr);
     return false;
   }
-  return s->sql_ok(g_sql.exec(s->db, "COMMIT", nullptr, nullptr, nullptr), "commit");
+  if (!sql_ok(g_sql.exec(s->db, "COMMIT", nullptr, nullptr, nullptr))) {
+    err = s->sql_err("commit");
+    g_sql.exec(s->db, "ROLLBACK", nullptr, nullptr, nullptr);
+    return false;
+  }
+  return true;
+}
+
+// Commit the queued unpersisted slices, oldest first (flush_mu held). False when one still fails.
+static bool persist_backlog(me_service* s, std::string& err) {
+  while (!s->unpersisted.empty()) {
+    Unpersisted& u = s->unpersisted.front();
+    if (!persist(s, u.sl, u.res.data(), u.tape.data(), u.ts, err)) return false;
+    {
+      std::lock_guard<std::mutex> lk(s->mu);
+      s->unpersisted_records -= u.sl.size();
+    }
+    s->unpersisted.pop_front();
+  }
+  return true;
+}
+
+// Where a flush's caller wants the matched outputs (any pointer may be NULL).
+struct FlushOut {
+  me_fill* fills = nullptr;
+  size_t fills_cap = 0;
+  size_t nf = 0;
+  me_order_result* res = nullptr;
+  uint64_t* seq = nullptr;
+  size_t nr = 0;
+};
+
+// Match + persist one closed slice (flush_mu held, the slice already taken off the queue).
+static int process(me_service* s, Slice&& sl, FlushOut* out) {
+  const size_t n = sl.size();
+  const me_fill* tape = nullptr;
+  const me_order_result* res = nullptr;
+  size_t nf = 0, nr = 0;
+  {
+    std::lock_guard<std::mutex> le(s->eng_mu);
+    me_order_soa b{sl.seq.data(), sl.px.data(), sl.qty.data(), sl.sid.data(), sl.kind.data()};
+    uint64_t t = 0;
+    int rc = me_submit_host(s->eng, &b, n, &t);
+    if (rc != ME_OK) {  // not accepted: the slice goes back to the head of the queue
+      char e[512];
+      me_last_error(s->eng, e, sizeof e);
+      std::lock_guard<std::mutex> lk(s->mu);
+      s->closed_records += n;
+      s->closed.push_front(std::move(sl));
+      return s->fail(rc, std::string("engine: ") + e);
+    }
+    rc = me_collect(s->eng, t, &tape, &nf, &res, &nr);
+    if (rc != ME_OK) {  // accepted and lost: the books may hold the slice, the service cannot go on
+      char e[512];
+      me_last_error(s->eng, e, sizeof e);
+      s->failed = true;
+      return s->fail(rc, std::string("engine lost an accepted slice: ") + e);
+    }
+  }
+  // the slot's pinned outputs stay valid until the next me_submit_host, which only a later
+  // process() (this thread, flush_mu) can issue
+  int rc = ME_OK;
+  std::string err;
+  const int64_t ts = now_ms();
+  if (!persist_backlog(s, err) || !persist(s, sl, res, tape, ts, err)) {
+    Unpersisted u{std::move(sl), std::vector<me_order_result>(res, res + nr), std::vector<me_fill>(tape, tape + nf),
+                  ts};
+    {
+      std::lock_guard<std::mutex> lk(s->mu);
+      s->unpersisted_records += u.sl.size();
+    }
+    s->unpersisted.push_back(std::move(u));
+    rc = s->fail(ME_E_SQLITE, "persistence deferred (" + err + "); the slice is matched and kept for the next flush");
+    const Unpersisted& k = s->unpersisted.back();
+    emit_updates(s, k.sl, k.res.data(), k.tape.data());
+    if (out) {
+      if (out->fills) memcpy(out->fills + out->nf, k.tape.data(), nf * sizeof(me_fill));
+      if (out->res)
+        for (size_t i = 0; i < nr; ++i) {
+          out->res[out->nr + i] = k.res[i];
+          out->res[out->nr + i].tape_offset += (uint32_t)out->nf;
+        }
+      if (out->seq) memcpy(out->seq + out->nr, k.sl.seq.data(), nr * sizeof(uint64_t));
+      out->nf += nf;
+      out->nr += nr;
+    }
+    return rc;
+  }
+  emit_updates(s, sl, res, tape);
+  if (out) {
+    if (out->fills) memcpy(out->fills + out->nf, tape, nf * sizeof(me_fill));
+    if (out->res)
+      for (size_t i = 0; i < nr; ++i) {
+        out->res[out->nr + i] = res[i];
+        out->res[out->nr + i].tape_offset += (uint32_t)out->nf;
+      }
+    if (out->seq) memcpy(out->seq + out->nr, sl.seq.data(), nr * sizeof(uint64_t));
+    out->nf += nf;
+    out->nr += nr;
+  }
+  return rc;
+}
+
+// Flush the closed slices (and the open one when take_open), oldest first. `limit` bounds how many
+// slices are taken (those present when the caller checked its output capacity).
+static int flush_closed(me_service* s, bool take_open, size_t limit, FlushOut* out) {
+  if (s->failed) return s->fail(ME_E_STATE, "service failed: the engine lost an accepted slice");
+  if (!s->eng) {
+    std::lock_guard<std::mutex> lk(s->mu);
+    if (s->open.size() || !s->closed.empty())
+      return s->fail(ME_E_STATE, "me_service_flush: no engine (HIP device required)");
+  }
+  int rc = ME_OK;
+  std::string err;
+  if (!persist_backlog(s, err)) rc = s->fail(ME_E_SQLITE, "persistence deferred (" + err + ")");
+  if (take_open) {
+    std::lock_guard<std::mutex> lk(s->mu);
+    close_open(s);
+  }
+  for (size_t k = 0; k < limit; ++k) {
+    Slice sl;
+    {
+      std::lock_guard<std::mutex> lk(s->mu);
+      if (s->closed.empty()) break;
+      sl = std::move(s->closed.front());
+      s->closed.pop_front();
+      s->closed_records -= sl.size();
+    }
+    const int r = process(s, std::move(sl), out);
+    if (r == ME_E_SQLITE) {
+      rc = r;  // matched and kept: later slices still match (and queue behind it for the DB)
+      continue;
+    }
+    if (r != ME_OK) return r;
+  }
+  return rc;
 }
 
 extern "C" int me_service_flush(me_service* s, me_fill* out_fills, size_t fills_cap, size_t* n_fills,
                                 me_order_result* out_results, uint64_t* out_seq, size_t results_cap,
                                 size_t* n_results) {
-  std::lock_guard<std::mutex> lk(s->mu);
-  const size_t n = s->seq.size();
   if (n_fills) *n_fills = 0;
-  if (n_results) *n_results = n;
-  if (n == 0) return ME_OK;
-  if (!s->eng) return s->fail(ME_E_STATE, "me_service_flush: no engine (HIP device required)");
-  std::vector<me_order_result> res(n);
-  std::vector<me_fill> tape(me_fill_bound(s->eng, n));
-  size_t nf = 0;
-  me_order_soa b{s->seq.data(), s->px.data(), s->qty.data(), s->sid.data(), s->kind.data()};
-  int rc = me_submit_batch(s->eng, &b, n, tape.data(), tape.size(), &nf, res.data());
-  if (rc != ME_OK) {
-    char e[512];
-    me_last_error(s->eng, e, sizeof e);
-    return s->fail(rc, std::string("engine: ") + e);
+  if (n_results) *n_results = 0;
+  std::lock_guard<std::mutex> lf(s->flush_mu);
+  size_t total = 0, nslices = 0;
+  {
+    std::lock_guard<std::mutex> lk(s->mu);
+    total = s->open.size() + s->closed_records;
+    nslices = s->closed.size() + (s->open.size() ? 1 : 0);
   }
-  if (!persist(s, n, res.data(), tape.data(), nf)) return s->fail(ME_E_SQLITE, s->err);
-  emit_updates(s, n, res.data(), tape.data());
-  if (n_fills) *n_fills = nf;
-  if (out_fills) {
-    if (nf > fills_cap) return s->fail(ME_E_INVALID, "fills_cap smaller than the tape");
-    memcpy(out_fills, tape.data(), nf * sizeof(me_fill));
+  // the caller's buffers are checked before anything is matched
+  if ((out_results || out_seq) && total > results_cap)
+    return s->fail(ME_E_INVALID, "results_cap smaller than the pending records");
+  if (out_fills && s->eng && fills_cap < me_fill_bound(s->eng, total))
+    return s->fail(ME_E_INVALID, "fills_cap smaller than me_fill_bound(pending records)");
+  FlushOut out{out_fills, fills_cap, 0, out_results, out_seq, 0};
+  const int rc = flush_closed(s, true, nslices, &out);
+  if (n_fills) *n_fills = out.nf;
+  if (n_results) *n_results = out.nr;
+  return rc;
+}
+
+// The background flusher: closes the open slice once it is interval old (or the submit path closed
+// it at the slice size) and flushes the closed ones.
+static void flusher_main(me_service* s) {
+  std::unique_lock<std::mutex> lk(s->mu);
+  while (!s->stop) {
+    const int64_t now = mono_us();
+    const bool due = s->open.size() && now - s->open.opened_us >= s->interval_us;
+    if (due) close_open(s);
+    if (s->closed.empty()) {
+      const int64_t wait = s->open.size() ? s->open.opened_us + s->interval_us - now : s->interval_us;
+      s->cv.wait_for(lk, std::chrono::microseconds(wait > 0 ? wait : 1));
+      continue;
+    }
+    lk.unlock();
+    {
+      std::lock_guard<std::mutex> lf(s->flush_mu);
+      (void)flush_closed(s, false, SIZE_MAX, nullptr);  // errors land in me_service_last_error
+    }
+    lk.lock();
+    if (s->failed) break;
   }
-  if (out_results || out_seq) {
-    if (n > results_cap) return s->fail(ME_E_INVALID, "results_cap smaller than the slice");
-    if (out_results) memcpy(out_results, res.data(), n * sizeof(me_order_result));
-    if (out_seq) memcpy(out_seq, s->seq.data(), n * sizeof(uint64_t));
-  }
-  s->seq.clear();
-  s->px.clear();
-  s->qty.clear();
-  s->sid.clear();
-  s->kind.clear();
-  s->meta.clear();
+}
+
+extern "C" int me_service_start(me_service* s, uint32_t interval_us, uint32_t slice_orders) {
+  if (!s || !s->eng) return ME_E_STATE;
+  std::lock_guard<std::mutex> lk(s->mu);
+  if (s->flusher.joinable()) return s->fail(ME_E_STATE, "flusher already running");
+  me_config c{};
+  me_get_config(s->eng, &c);
+  s->slice_max = slice_orders && slice_orders < c.max_batch ? slice_orders : c.max_batch;
+  s->interval_us = interval_us ? interval_us : 1000;
+  s->stop = false;
+  s->flusher = std::thread(flusher_main, s);
   return ME_OK;
+}
+
+extern "C" int me_service_stop(me_service* s) {
+  if (!s) return ME_E_INVALID;
+  {
+    std::lock_guard<std::mutex> lk(s->mu);
+    s->stop = true;
+    s->cv.notify_all();
+  }
+  if (s->flusher.joinable()) s->flusher.join();
+  return ME_OK;
+}
+
+extern "C" void me_service_destroy(me_service* s) {
+  if (!s) return;
+  me_service_stop(s);
+  close_db(s);
+  delete s;
 }
 
 extern "C" int me_service_book(me_service* s, const char* symbol, me_level* bids, me_level* asks, size_t depth,
                                size_t* n_bids, size_t* n_asks) {
   if (n_bids) *n_bids = 0;
   if (n_asks) *n_asks = 0;
-  auto it = s->sym.find(symbol ? symbol : "");
-  if (it == s->sym.end()) return ME_OK;  // unknown symbol: empty book (the reference's stub is always empty)
+  uint32_t sid = 0;
+  {
+    std::lock_guard<std::mutex> lk(s->mu);
+    auto it = s->sym.find(symbol ? symbol : "");
+    if (it == s->sym.end()) return ME_OK;  // unknown symbol: empty book (the reference's stub is always empty)
+    sid = it->second;
+  }
   if (!s->eng) return s->fail(ME_E_STATE, "no engine");
-  return me_book_snapshot(s->eng, it->second, bids, asks, depth, n_bids, n_asks);
+  std::lock_guard<std::mutex> le(s->eng_mu);
+  const int rc = me_book_snapshot(s->eng, sid, bids, asks, depth, n_bids, n_asks);
+  if (rc != ME_OK) {
+    char e[512];
+    me_last_error(s->eng, e, sizeof e);
+    return s->fail(rc, std::string("engine: ") + e);
+  }
+  return ME_OK;
 }
 
 extern "C" int me_service_market_data(me_service* s, const char* symbol, me_market_data* out) {
   memset(out, 0, sizeof(*out));
   out->scale = 4;
-  auto it = s->sym.find(symbol ? symbol : "");
-  if (it == s->sym.end()) return ME_OK;
-  if (!s->eng) return s->fail(ME_E_STATE, "no engine");
   me_level b{}, a{};
   size_t nb = 0, na = 0;
-  const int rc = me_book_snapshot(s->eng, it->second, &b, &a, 1, &nb, &na);
+  const int rc = me_service_book(s, symbol, &b, &a, 1, &nb, &na);
   if (rc != ME_OK) return rc;
   auto sat = [](int64_t v) { return (int32_t)(v > INT32_MAX ? INT32_MAX : v); };
   if (nb) {
@@ -568,6 +884,7 @@ extern "C" int me_service_market_data(me_service* s, const char* symbol, me_mark
 }
 
 extern "C" int me_service_last_error(const me_service* s, char* buf, size_t cap) {
+  std::lock_guard<std::mutex> lk(s->err_mu);
   if (buf && cap) put(buf, cap, s->err);
   return (int)s->err.size();
 }

@@ -27,6 +27,14 @@ def _check(lib, handle, rc: int) -> None:
         raise EngineError(rc, buf.value.decode(errors="replace"))
 
 
+def _view(addr, n: int, dtype) -> np.ndarray:
+    """numpy view of n records at a C address (no copy)."""
+    if not n:
+        return np.zeros(0, dtype=dtype)
+    buf = (C.c_char * (n * dtype.itemsize)).from_address(addr)
+    return np.frombuffer(buf, dtype=dtype, count=n)
+
+
 def normalize_to_q4(price: int, scale: int) -> int:
     """include/domain/price.hpp:15-29 through the product library; raises like the reference."""
     lib = _abi.load()
@@ -111,6 +119,8 @@ class Engine:
         symbol_ids=None,
         batches_per_launch: int = 0,
         far_levels: int = 0,
+        host_slots: int = 0,
+        host_tape_cap: int = 0,
     ):
         self.lib = _abi.load()
         self.num_symbols = int(num_symbols)
@@ -130,6 +140,8 @@ class Engine:
             None if self._ids is None else self._ids.ctypes.data_as(C.POINTER(C.c_uint32)),
             batches_per_launch,
             far_levels,
+            host_slots,
+            host_tape_cap,
         )
         self.max_batch = int(max_batch)
         h = self.lib.me_create(C.byref(cfg))
@@ -174,6 +186,40 @@ class Engine:
         )
         _check(self.lib, self.h, rc)
         return res, (fills[: nf.value].copy() if want_fills else nf.value)
+
+    # -- pipelined host batches (me_submit_host / me_collect)
+    def submit_host(self, b: Batch) -> int:
+        """Enqueue a host batch (staged into the next pinned slot unless it already lives there, see
+        host_inputs); returns its ticket at once."""
+        t = C.c_uint64(0)
+        soa = b.soa()
+        _check(self.lib, self.h, self.lib.me_submit_host(self.h, C.byref(soa), len(b), C.byref(t)))
+        return t.value
+
+    def collect(self, ticket: int, copy: bool = True):
+        """(results[n], fills[k]) of a ticket. copy=False returns views of the slot's pinned memory,
+        valid until the slot is reused (ticket + host_slots)."""
+        fp, rp = C.c_void_p(), C.c_void_p()
+        nf, nr = C.c_size_t(0), C.c_size_t(0)
+        _check(self.lib, self.h,
+               self.lib.me_collect(self.h, ticket, C.byref(fp), C.byref(nf), C.byref(rp), C.byref(nr)))
+        res = _view(rp.value, nr.value, RESULT_DTYPE)
+        fills = _view(fp.value, nf.value, FILL_DTYPE)
+        return (res.copy(), fills.copy()) if copy else (res, fills)
+
+    def host_inputs(self, n: int) -> Batch:
+        """Writable numpy views of the pinned arrays the next submit_host takes for an n-record batch
+        (fill them in place, then submit_host the returned Batch: no staging copy)."""
+        w = _abi.MeOrderSoaW()
+        _check(self.lib, self.h, self.lib.me_host_inputs(self.h, n, C.byref(w)))
+        arrs = [_view(getattr(w, f), n, np.dtype(t)) for f, t in
+                (("seq", "<u8"), ("price_q4", "<i8"), ("qty", "<i4"), ("symbol", "<u4"), ("kind", "u1"))]
+        return Batch(*arrs)
+
+    def config(self) -> dict:
+        cfg = MeConfig()
+        _check(self.lib, self.h, self.lib.me_get_config(self.h, C.byref(cfg)))
+        return {f: getattr(cfg, f) for f, _ in MeConfig._fields_ if f not in ("base_price", "symbol_ids")}
 
     def upload(self, b: Batch) -> DeviceBatch:
         return DeviceBatch(self, b)

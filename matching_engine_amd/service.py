@@ -35,6 +35,21 @@ class MatchingEngineService:
             self.lib.me_service_destroy(self.h)
             self.h = None
 
+    def start(self, interval_us: int = 1000, slice_orders: int = 0):
+        """Background flusher: slices close at slice_orders records or interval_us age and are matched
+        and persisted without a caller (errors: last_error())."""
+        rc = self.lib.me_service_start(self.h, interval_us, slice_orders)
+        if rc != 0:
+            raise ServiceError(f"start failed ({rc}): {self.last_error()}")
+
+    def stop(self):
+        self.lib.me_service_stop(self.h)
+
+    @property
+    def unpersisted(self) -> int:
+        """Matched records whose SQLite transaction has not committed yet."""
+        return int(self.lib.me_service_unpersisted(self.h))
+
     def __del__(self):
         try:
             self.close()
@@ -86,8 +101,14 @@ class MatchingEngineService:
     def next_oid(self) -> int:
         return int(self.lib.me_service_next_oid(self.h))
 
-    def flush(self):
-        """Match + persist the open time slice -> (seq[n], results[n], fills[k])."""
+    def flush(self, outputs: bool = True):
+        """Match + persist every slice submitted so far -> (seq[n], results[n], fills[k]) of the records
+        this call matched (outputs=False: nothing copied out, returns None)."""
+        if not outputs:
+            rc = self.lib.me_service_flush(self.h, None, 0, None, None, None, 0, None)
+            if rc != 0:
+                raise ServiceError(f"flush failed ({rc}): {self.last_error()}")
+            return None
         n = self.pending
         res = np.zeros(max(n, 1), dtype=RESULT_DTYPE)
         seq = np.zeros(max(n, 1), dtype=np.uint64)

@@ -62,15 +62,20 @@ def main():
         if k == 1:
             b.symbol[::997] = S + 5
         lb, pos = plan.split(b)[rank]
-        r, f = submit(lb)
+        if gath is not None:  # device-resident batch, the engine's outputs staged device to device
+            db = book.upload(lb)
+            book.submit_device(db)
+        else:
+            r, f = submit(lb)
         if engine_kind in ("gather", "gpu_gather"):
             import torch
 
             from matching_engine_amd.gather import gather_batch
 
             post = torch.from_numpy(pos.astype(np.int64))
-            if gath is not None:  # device staging of the engine's own outputs
+            if gath is not None:
                 tape, res = gath.gather(len(lb), post, len(b))
+                db.free()
             else:
                 tape, res = gather_batch(torch.from_numpy(f.view(np.uint8).copy()), len(f),
                                          torch.from_numpy(r.view(np.uint8).copy()), post, len(lb), len(b))

@@ -1,0 +1,127 @@
+"""The pipelined host-batch path (me_submit_host / me_collect, include/me_engine.h): host SoA batches
+staged in pinned slots, H2D on their own stream, matched in launch groups, results and tapes D2H'd
+behind the match — every batch's outputs bit-exact against the oracle, whatever the collect lag,
+including tapes longer than a slot (recovered from scratch at collect). Needs an MI355X."""
+import numpy as np
+import pytest
+
+from tests._parity import assert_books_equal, assert_fills_equal, assert_results_equal
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def me(built):
+    import matching_engine_amd
+
+    return matching_engine_amd
+
+
+@pytest.fixture(scope="module")
+def orc(built):
+    from oracle import oracle
+
+    return oracle
+
+
+def _stream(me, cfg, nbatches, **over):
+    sc = me.preset(cfg, **over)
+    st = me.Stream(sc)
+    return sc, st.base_prices(), [st.next(sc.batch) for _ in range(nbatches)]
+
+
+def _engine(me, sc, base, batches, **kw):
+    total = sum(len(b) for b in batches)
+    return me.Engine(sc.num_symbols, sc.levels, base, max_batch=max(len(b) for b in batches),
+                     max_resting=total + 1024, max_chunks=total + 2 * sc.num_symbols, seq_ring=1 << 22, **kw)
+
+
+def _pipelined(me, eng, batches, lag, zero_copy_every=0):
+    """Submit every batch through me_submit_host, collecting each `lag` submissions later (in order);
+    returns the outputs per batch. zero_copy_every = k: every k-th batch is written straight into the
+    pinned slot (me_host_inputs) instead of being staged by the engine."""
+    out, tickets = [None] * len(batches), []
+    for k, b in enumerate(batches):
+        if zero_copy_every and k % zero_copy_every == 0:
+            w = eng.host_inputs(len(b))
+            for f in ("seq", "price_q4", "qty", "symbol", "kind"):
+                getattr(w, f)[:] = getattr(b, f)
+            b = w
+        tickets.append((k, eng.submit_host(b)))
+        while len(tickets) > lag:
+            j, t = tickets.pop(0)
+            out[j] = eng.collect(t)
+    for j, t in tickets:
+        out[j] = eng.collect(t)
+    return out
+
+
+@pytest.mark.parametrize("levels,group,lag", [(128, 4, 1), (128, 4, 12), (128, 32, 96), (512, 1, 3)])
+def test_host_pipeline_every_batch(me, orc, levels, group, lag):
+    sc, base, batches = _stream(me, 2, 40, num_symbols=64, levels=levels, batch=2048)
+    ob = orc.OracleBook(sc.num_symbols)
+    with _engine(me, sc, base, batches, batches_per_launch=group) as eng:
+        assert eng.config()["host_slots"] == 3 * eng.config()["batches_per_launch"] + 1
+        outs = _pipelined(me, eng, batches, lag, zero_copy_every=3)
+        for k, b in enumerate(batches):
+            ro, fo = ob.submit(b)
+            assert_results_equal(outs[k][0], ro, f"L={levels} G={group} lag={lag} batch {k}")
+            assert_fills_equal(outs[k][1], fo, f"L={levels} G={group} lag={lag} batch {k}")
+        assert_books_equal(eng, ob, range(sc.num_symbols), "host pipeline")
+
+
+@pytest.mark.parametrize("levels", [128, 512])
+def test_host_tape_longer_than_slot(me, orc, levels):
+    """host_tape_cap = 64 fills: market sweeps outgrow the slot and the tail comes from scratch."""
+    sc, base, batches = _stream(me, 5, 12, num_symbols=16, levels=levels, batch=2048)
+    ob = orc.OracleBook(sc.num_symbols)
+    spilled = 0
+    with _engine(me, sc, base, batches, batches_per_launch=2, host_tape_cap=64) as eng:
+        for k, (r, f) in enumerate(_pipelined(me, eng, batches, lag=2)):
+            ro, fo = ob.submit(batches[k])
+            assert_results_equal(r, ro, f"spill L={levels} batch {k}")
+            assert_fills_equal(f, fo, f"spill L={levels} batch {k}")
+            spilled += len(fo) > 64
+        assert_books_equal(eng, ob, range(sc.num_symbols), "spill")
+    assert spilled >= 6
+
+
+def test_host_slot_reuse_needs_collect(me, orc):
+    sc, base, batches = _stream(me, 2, 6, num_symbols=32, batch=512)
+    ob = orc.OracleBook(sc.num_symbols)
+    with _engine(me, sc, base, batches, batches_per_launch=2, host_slots=3) as eng:
+        t = [eng.submit_host(b) for b in batches[:3]]
+        with pytest.raises(me.EngineError) as ei:
+            eng.submit_host(batches[3])
+        assert ei.value.code == me.ME_E_STATE and "collect ticket 0" in str(ei.value)
+        with pytest.raises(me.EngineError):
+            eng.host_inputs(len(batches[3]))
+        outs = [eng.collect(x) for x in t]
+        with pytest.raises(me.EngineError):  # collected once only
+            eng.collect(t[0])
+        outs += [eng.collect(eng.submit_host(b)) for b in batches[3:]]
+        for k, b in enumerate(batches):
+            ro, fo = ob.submit(b)
+            assert_results_equal(outs[k][0], ro, f"reuse batch {k}")
+            assert_fills_equal(outs[k][1], fo, f"reuse batch {k}")
+
+
+def test_host_and_device_batches_interleave(me, orc):
+    """Host and device batches share the launch groups and the books; the device-output fetches refuse
+    to read a host batch's outputs."""
+    sc, base, batches = _stream(me, 2, 8, num_symbols=64, batch=1024)
+    ob = orc.OracleBook(sc.num_symbols)
+    with _engine(me, sc, base, batches, batches_per_launch=4) as eng:
+        for k, b in enumerate(batches):
+            ro, fo = ob.submit(b)
+            if k % 2:
+                db = eng.upload(b)
+                eng.submit_device(db)
+                r, f = eng.fetch_outputs(len(b))
+                db.free()
+            else:
+                r, f = eng.collect(eng.submit_host(b))
+                with pytest.raises(me.EngineError, match="host batch"):
+                    eng.fetch_outputs(len(b))
+            assert_results_equal(r, ro, f"interleave batch {k}")
+            assert_fills_equal(f, fo, f"interleave batch {k}")

@@ -269,3 +269,267 @@ def test_cancels_and_order_update_stream(me, tmp_path):
     assert checked > 1000
     svc.close()
     eng.close()
+
+
+# ---------------------------------------------------------------- service hardening (round 2)
+def _limit_stream(rng, syms, mids, n, market_pct=0.2):
+    """(symbol, otype, side, q4 price, qty) requests; every one passes SubmitOrder's validation."""
+    out = []
+    for _ in range(n):
+        s = syms[int(rng.integers(len(syms)))]
+        otype = 1 if rng.random() < market_pct else 0
+        out.append((s, otype, int(rng.choice([1, 2])), 0 if otype else mids[s] + int(rng.integers(-20, 21)),
+                    int(rng.integers(1, 50))))
+    return out
+
+
+def _oracle_batch(me, reqs, oids, sid_of):
+    return me.Batch(oids, [r[3] for r in reqs], [r[4] for r in reqs], [sid_of[r[0]] for r in reqs],
+                    [me.kind(r[2], r[1]) for r in reqs])
+
+
+def test_cancel_requires_owner(me):
+    """CancelOrder only for the order's own client: another client's cancel is refused
+    in-band and consumes no OID."""
+    svc = me.MatchingEngineService(None, ["SYM"])
+    assert svc.submit_order("alice", "SYM", 0, 1, 100, 4, 5)["order_id"] == "OID-1"
+    r = svc.cancel_order("mallory", "SYM", "OID-1")
+    assert r == {"order_id": "", "success": False, "error_message": "order belongs to another client",
+                 "grpc_status": 0}
+    assert svc.next_oid == 2 and svc.pending == 1
+    assert svc.cancel_order("alice", "SYM", "OID-1")["success"]
+    # an order id nobody holds is queued (the engine answers REJECTED after the flush)
+    assert svc.cancel_order("mallory", "SYM", "OID-77")["success"]
+    assert svc.pending == 3
+
+
+def test_unknown_symbols_without_engine(me):
+    svc = me.MatchingEngineService(None, ["SYM"])
+    for s in ("NEW1", "NEW2", "SYM"):
+        assert svc.submit_order("C", s, 0, 1, 100, 4, 5)["success"]
+    assert svc.pending == 3
+
+
+@pytest.mark.gpu
+def test_unknown_symbols_interned_matched_and_persisted(me, tmp_path):
+    """A never-seen symbol takes the engine's next unused book (its window placed by its first orders)
+    and is matched and persisted exactly as the oracle says; past the engine's books SubmitOrder
+    answers RESOURCE_EXHAUSTED without an OID."""
+    from oracle.oracle import OracleBook
+
+    rng = np.random.default_rng(3)
+    syms = ["AAA", "BBB", "CCC", "DDD"]
+    mids = {s: 2_000_000 + 50_000 * i for i, s in enumerate(syms)}
+    db = str(tmp_path / "intern.sqlite")
+    with me.Engine(4, 128, [0, 0, 0, 0], max_batch=4096, max_resting=1 << 14) as eng:
+        svc = me.MatchingEngineService(eng, ["AAA"], db_path=db)
+        reqs = _limit_stream(rng, syms, mids, 3000)
+        oids = []
+        for r in reqs:
+            resp = svc.submit_order("C", r[0], r[1], r[2], r[3], 4, r[4])
+            assert resp["success"], resp
+            oids.append(int(resp["order_id"][4:]))
+        seq, res, fills = svc.flush()
+        sid_of = {"AAA": 0}
+        for r in reqs:
+            sid_of.setdefault(r[0], len(sid_of))
+        ob = OracleBook(4)
+        ro, fo = ob.submit(_oracle_batch(me, reqs, oids, sid_of))
+        assert_results_equal(res, ro, "interned symbols")
+        assert_fills_equal(fills, fo, "interned symbols")
+        con = sqlite3.connect(db)
+        for s in syms:
+            n = con.execute("SELECT COUNT(*) FROM orders WHERE symbol=?", (s,)).fetchone()[0]
+            assert n == sum(1 for r in reqs if r[0] == s)
+        b0, a0 = svc.get_order_book("DDD", 3)
+        ob0, oa0 = ob.snapshot(sid_of["DDD"], 3)
+        assert np.array_equal(b0, ob0) and np.array_equal(a0, oa0)
+        nxt = svc.next_oid
+        r = svc.submit_order("C", "EEE", 0, 1, 100, 4, 1)
+        assert r == {"order_id": "", "success": False, "error_message": "symbol capacity exhausted",
+                     "grpc_status": 8}
+        assert svc.next_oid == nxt
+        svc.close()
+
+
+@pytest.mark.gpu
+def test_slices_beyond_max_batch_split(me, tmp_path):
+    """More pending orders than the engine's max_batch: the slice closes at max_batch and the flush
+    matches every closed slice in order (the service no longer wedges)."""
+    from oracle.oracle import OracleBook
+
+    rng = np.random.default_rng(5)
+    syms = [f"S{i}" for i in range(8)]
+    mids = {s: 1_000_000 + 1000 * i for i, s in enumerate(syms)}
+    with me.Engine(8, 128, [mids[s] - 64 for s in syms], max_batch=1000, max_resting=1 << 14) as eng:
+        svc = me.MatchingEngineService(eng, syms, db_path=str(tmp_path / "split.sqlite"))
+        reqs = _limit_stream(rng, syms, mids, 3500)
+        oids = [int(svc.submit_order("C", r[0], r[1], r[2], r[3], 4, r[4])["order_id"][4:]) for r in reqs]
+        assert svc.pending == 3500
+        seq, res, fills = svc.flush()
+        assert svc.pending == 0 and len(seq) == 3500
+        ro, fo = OracleBook(8).submit(_oracle_batch(me, reqs, oids, {s: i for i, s in enumerate(syms)}))
+        assert_results_equal(res, ro, "split slices")
+        assert_fills_equal(fills, fo, "split slices")
+        svc.close()
+
+
+@pytest.mark.gpu
+def test_db_failure_keeps_matched_slice_and_retries(me, tmp_path):
+    """a failed transaction (another connection holds the write lock past the 5 s busy
+    timeout) neither loses nor re-matches the slice: the next flush commits it exactly once."""
+    from oracle.oracle import OracleBook
+
+    rng = np.random.default_rng(9)
+    syms = ["X", "Y"]
+    mids = {"X": 1_000_000, "Y": 1_500_000}
+    db = str(tmp_path / "busy.sqlite")
+    with me.Engine(2, 128, [mids[s] - 64 for s in syms], max_batch=4096, max_resting=1 << 14) as eng:
+        svc = me.MatchingEngineService(eng, syms, db_path=db)
+        ob = OracleBook(2)
+        sid = {"X": 0, "Y": 1}
+        total_fills = 0
+        reqs = _limit_stream(rng, syms, mids, 800)
+        oids = [int(svc.submit_order("C", *r[:4], 4, r[4])["order_id"][4:]) for r in reqs]
+        svc.flush()
+        total_fills += len(ob.submit(_oracle_batch(me, reqs, oids, sid))[1])
+        # slice 2 while the DB is locked
+        locker = sqlite3.connect(db, timeout=0.1)
+        locker.execute("BEGIN EXCLUSIVE")
+        reqs2 = _limit_stream(rng, syms, mids, 700)
+        oids2 = [int(svc.submit_order("C", *r[:4], 4, r[4])["order_id"][4:]) for r in reqs2]
+        with pytest.raises(me.ServiceError, match="persistence deferred"):
+            svc.flush()
+        assert svc.pending == 0 and svc.unpersisted == 700
+        ro2, fo2 = ob.submit(_oracle_batch(me, reqs2, oids2, sid))
+        total_fills += len(fo2)
+        # the engine holds slice 2 (matched once); the book equals the oracle's
+        for s in syms:
+            gb, ga = svc.get_order_book(s, 5)
+            eb, ea = ob.snapshot(sid[s], 5)
+            assert np.array_equal(gb, eb) and np.array_equal(ga, ea)
+        locker.rollback()
+        locker.close()
+        # slice 3 flushes after the kept slice 2 commits
+        reqs3 = _limit_stream(rng, syms, mids, 300)
+        oids3 = [int(svc.submit_order("C", *r[:4], 4, r[4])["order_id"][4:]) for r in reqs3]
+        seq, res, fills = svc.flush()
+        ro3, fo3 = ob.submit(_oracle_batch(me, reqs3, oids3, sid))
+        total_fills += len(fo3)
+        assert_results_equal(res, ro3, "after retry")
+        assert_fills_equal(fills, fo3, "after retry")
+        assert svc.unpersisted == 0
+        con = sqlite3.connect(db)
+        assert con.execute("SELECT COUNT(*) FROM orders").fetchone()[0] == 1800
+        assert con.execute("SELECT COUNT(*) FROM fills").fetchone()[0] == 2 * total_fills
+        for s in syms:  # resting rows carry the oracle's live remainders
+            for e in ob.dump(sid[s])[:30]:
+                rem = con.execute("SELECT remaining_quantity FROM orders WHERE order_id=?",
+                                  (f"OID-{int(e['seq'])}",)).fetchone()[0]
+                assert rem == int(e["qty"])
+        svc.close()
+
+
+@pytest.mark.gpu
+def test_submit_never_waits_for_a_flush(me, tmp_path):
+    """SubmitOrder is never blocked by a flush. One thread flushes a 60k-order slice
+    (GPU match + a 60k-row SQLite transaction) while this thread keeps submitting; a second thread
+    reads books and market data throughout (engine calls are serialized by the service)."""
+    import threading
+    import time
+
+    from oracle.oracle import OracleBook
+
+    rng = np.random.default_rng(21)
+    syms = [f"T{i}" for i in range(64)]
+    mids = {s: 3_000_000 + 500 * i for i, s in enumerate(syms)}
+    db = str(tmp_path / "concurrent.sqlite")
+    with me.Engine(64, 128, [mids[s] - 64 for s in syms], max_batch=65536, max_resting=1 << 18) as eng:
+        svc = me.MatchingEngineService(eng, syms, db_path=db)
+        reqs = _limit_stream(rng, syms, mids, 60000)
+        oids = [int(svc.submit_order("C", *r[:4], 4, r[4])["order_id"][4:]) for r in reqs]
+        done = threading.Event()
+        span = {}
+
+        def flusher():
+            span["t0"] = time.perf_counter()
+            svc.flush(outputs=False)
+            span["t1"] = time.perf_counter()
+            done.set()
+
+        def reader():
+            while not done.is_set():
+                svc.get_order_book(syms[int(rng.integers(64))], 5)
+                svc.market_data(syms[0])
+
+        tf, tr = threading.Thread(target=flusher), threading.Thread(target=reader)
+        tf.start()
+        tr.start()
+        lat, during = [], 0
+        reqs2 = _limit_stream(np.random.default_rng(22), syms, mids, 20000)
+        oids2 = []
+        for r in reqs2:
+            a = time.perf_counter()
+            oids2.append(int(svc.submit_order("C", *r[:4], 4, r[4])["order_id"][4:]))
+            lat.append(time.perf_counter() - a)
+            during += not done.is_set()
+        tf.join()
+        tr.join()
+        flush_s = span["t1"] - span["t0"]
+        assert during > 1000, "the flush finished before the concurrent submits started"
+        assert max(lat) < 0.05 and max(lat) < flush_s / 4, (max(lat), flush_s)
+        seq, res, fills = svc.flush()
+        ob = OracleBook(64)
+        sid = {s: i for i, s in enumerate(syms)}
+        ob.submit(_oracle_batch(me, reqs, oids, sid))
+        ro, fo = ob.submit(_oracle_batch(me, reqs2, oids2, sid))
+        assert_results_equal(res, ro, "after concurrent flush")
+        assert_fills_equal(fills, fo, "after concurrent flush")
+        con = sqlite3.connect(db)
+        assert con.execute("SELECT COUNT(*) FROM orders").fetchone()[0] == 80000
+        svc.close()
+
+
+@pytest.mark.gpu
+def test_background_flusher_time_and_size_trigger(me, tmp_path):
+    """me_service_start: slices close at 500 records or 2 ms and are matched and persisted with no
+    caller; the DB ends up exactly as the oracle's final state says."""
+    import time
+
+    from oracle.oracle import OracleBook
+
+    rng = np.random.default_rng(33)
+    syms = [f"B{i}" for i in range(16)]
+    mids = {s: 4_000_000 + 700 * i for i, s in enumerate(syms)}
+    db = str(tmp_path / "bg.sqlite")
+    with me.Engine(16, 128, [mids[s] - 64 for s in syms], max_batch=2048, max_resting=1 << 16) as eng:
+        svc = me.MatchingEngineService(eng, syms, db_path=db)
+        svc.start(interval_us=2000, slice_orders=500)
+        reqs = _limit_stream(rng, syms, mids, 6000)
+        oids = []
+        for k, r in enumerate(reqs):
+            oids.append(int(svc.submit_order("C", *r[:4], 4, r[4])["order_id"][4:]))
+            if k % 1000 == 999:
+                time.sleep(0.01)  # idle gaps: the time trigger closes partial slices
+        t0 = time.time()
+        while svc.pending and time.time() - t0 < 30:
+            time.sleep(0.005)
+        assert svc.pending == 0, svc.last_error()
+        svc.stop()
+        assert svc.last_error() == ""
+        ob = OracleBook(16)
+        ro, fo = ob.submit(_oracle_batch(me, reqs, oids, {s: i for i, s in enumerate(syms)}))
+        con = sqlite3.connect(db)
+        assert con.execute("SELECT COUNT(*) FROM orders").fetchone()[0] == 6000
+        assert con.execute("SELECT COUNT(*) FROM fills").fetchone()[0] == 2 * len(fo)
+        rows = {o: (st, rem) for o, st, rem in
+                con.execute("SELECT order_id, status, remaining_quantity FROM orders").fetchall()}
+        for k in range(6000):  # a taker that filled completely stays FILLED
+            if ro[k]["status"] == me.ST_FILLED:
+                assert rows[f"OID-{oids[k]}"] == (me.ST_FILLED, 0)
+        for s in range(16):  # every resting order's row carries its live remainder
+            for e in ob.dump(s):
+                assert rows[f"OID-{int(e['seq'])}"][1] == int(e["qty"])
+        ev = svc.order_updates()
+        assert sum(e["fill_quantity"] for e in ev) == 2 * int(fo["qty"].sum())
+        svc.close()
