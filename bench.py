@@ -9,9 +9,11 @@ hash-sharded by symbol (splitmix64(symbol) % N) with no cross-GPU matching: weak
 One step = one batch through the whole device pipeline (bucket by symbol -> match -> tape
 compaction; L > 128: sort -> match -> compaction) with the batch already resident in HBM. W warmup
 steps, then K timed steps bracketed by barrier + device sync; the max over ranks is the job time.
---workload c3|c4|c5 runs the other BASELINE configs as secondary lines (same JSON shape).
+--workload c1|c3|c4|c5 runs the other BASELINE configs as secondary lines (same JSON shape); c1 adds
+c1_paths: the reference's per-order SubmitOrder + SQLite path, the build's SubmitOrder -> slice ->
+GPU -> batched-ingest path and the CPU oracle, on the C1 1M-order stream.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c3|c4|c5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c1|c2|c3|c4|c5]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N   (one rank per GPU)
 """
 from __future__ import annotations
@@ -37,6 +39,10 @@ BYTES_PER_FILL = 48    # 32 B tape record + 16 B maker-slot RMW
 # Per-workload shape. Weak scaling: symbols and batch grow with N, except config 4
 # whose 100k Zipf symbols are global (symbol 0 alone draws ~13 % of the stream at every N).
 WORKLOADS = {
+    "c1": dict(preset=1, symbols_per_gpu=1, batch_per_gpu=62500,
+               text="BASELINE configs[0]: one symbol 'SYM', 80% LIMIT +-32 ticks / 20% MARKET, qty U[1,100], "
+                    "62,500-order batches (the C1 1M-order stream); with the reference-path, service-path and "
+                    "oracle timings of SURVEY.md \u00a78(d) C1 in c1_paths"),
     "c2": dict(preset=2, symbols_per_gpu=1024, batch_per_gpu=65536,
                text="BASELINE configs[1]: 1,024 symbols/GPU x uniform stream, 65,536-order batches/GPU, "
                     "80% LIMIT +-32 ticks / 20% MARKET, qty U[1,100]"),
@@ -247,6 +253,124 @@ def cpu_baseline(args):
     return out
 
 
+def c1_requests(n: int):
+    """The C1 request stream: me_gen config 1 on 'SYM' as raw OrderRequests — 1% of the
+    LIMITs re-expressed at scale 2 or 8 to exercise normalisation — and the Q4 records they normalise
+    to (seq = the OID each gets on a fresh DB)."""
+    sc = me.preset(1, batch=n)
+    st = me.Stream(sc)
+    base = st.base_prices()
+    b = st.next(n)
+    otype = ((b.kind >> 2) & 1).astype(np.int32)
+    side = (b.kind & 3).astype(np.int32)
+    rng = np.random.default_rng(1)
+    price, scale = b.price_q4.copy(), np.full(n, 4, dtype=np.int32)
+    sel, half = rng.random(n) < 0.01, rng.random(n) < 0.5
+    s2, s8 = sel & half & (otype == 0), sel & ~half & (otype == 0)
+    price[s2], scale[s2] = b.price_q4[s2] // 100, 2
+    price[s8], scale[s8] = b.price_q4[s8] * 10000, 8
+    price[otype == 1] = 0
+    q4 = price.copy()
+    q4[s2] = price[s2] * 100
+    q4[s8] = price[s8] // 10000
+    rec = me.Batch(np.arange(1, n + 1, dtype=np.uint64), q4, b.qty, np.zeros(n, dtype=np.uint32), b.kind)
+    return otype, side, price, scale, b.qty.astype(np.int32), rec, base
+
+
+def c1_paths(args):
+    """C1's three CPU-side timings (rank 0, N = 1): the reference's per-order SubmitOrder with one SQLite
+    transaction per order on one core (oracle/ref_submit.cpp, a bounded sample), the build's SubmitOrder
+    -> time slices -> GPU match -> one transaction per slice (me_service with its background flusher),
+    and the CPU oracle matcher alone on the same records."""
+    import ctypes as C
+    import sqlite3
+    import tempfile
+
+    from matching_engine_amd._abi import MeOrderRequest, MeOrderResponse
+    from oracle.oracle import OracleBook, ref_submit_run
+
+    n = 1_000_000
+    otype, side, price, scale, qty, rec, base = c1_requests(n)
+    tmp = tempfile.mkdtemp(prefix="me_c1_")
+    devnull = os.open(os.devnull, os.O_WRONLY)
+    out = {}
+    # (a) the reference path: calibrate on 5,000 orders, then ~cpu_seconds of it on a fresh DB
+    t = time.perf_counter()
+    ref_submit_run(os.path.join(tmp, "cal.db"), "C1", "SYM", otype[:5000], side[:5000], price[:5000],
+                   scale[:5000], qty[:5000], devnull)
+    k = int(min(n, max(5000, 5000 / (time.perf_counter() - t) * args.cpu_seconds)))
+    t = time.perf_counter()
+    rows, _ = ref_submit_run(os.path.join(tmp, "ref.db"), "C1", "SYM", otype[:k], side[:k], price[:k], scale[:k],
+                             qty[:k], devnull)
+    dt = time.perf_counter() - t
+    out["reference_submitorder"] = {
+        "value": k / dt, "unit": "orders/s", "cores": 1, "kind": "reference", "orders": k, "rows": int(rows),
+        "what": "SubmitOrder as the reference runs it per order (matching_engine_service.cpp:41-121 + "
+                "storage.cpp:78-123: logs to /dev/null with its std::endl flushes, OID, normalize_to_q4, one "
+                "SQLite transaction + fresh prepared INSERT per order, WAL / synchronous=NORMAL); no matching"}
+    # (b) the build: SubmitOrder -> 1 ms / 65,536-order slices -> GPU match -> one transaction per slice
+    reqs = (MeOrderRequest * n)()
+    a = np.frombuffer(reqs, dtype=np.dtype([("client", "<u8"), ("symbol", "<u8"), ("otype", "<i4"),
+                                            ("side", "<i4"), ("price", "<i8"), ("scale", "<i4"), ("qty", "<i4")]))
+    cs, ss = C.create_string_buffer(b"C1"), C.create_string_buffer(b"SYM")
+    a["client"], a["symbol"] = C.addressof(cs), C.addressof(ss)
+    a["otype"], a["side"], a["price"], a["scale"], a["qty"] = otype, side, price, scale, qty
+    resps = (MeOrderResponse * n)()
+    lib = me.load()
+    eng = me.Engine(1, 128, base, max_batch=65536, max_resting=n + 1024, seq_ring=1 << 22)
+    svc = me.MatchingEngineService(eng, ["SYM"], db_path=os.path.join(tmp, "build.db"))
+    svc.start(interval_us=1000, slice_orders=65536)
+    t = time.perf_counter()
+    step = 65536
+    for i in range(0, n, step):
+        lib.me_service_submit_orders(
+            svc.h, C.cast(C.addressof(reqs) + i * C.sizeof(MeOrderRequest), C.POINTER(MeOrderRequest)),
+            min(step, n - i), C.cast(C.addressof(resps) + i * C.sizeof(MeOrderResponse), C.POINTER(MeOrderResponse)))
+    t_sub = time.perf_counter() - t
+    while svc.pending or svc.unpersisted:
+        time.sleep(0.0005)
+    dt = time.perf_counter() - t
+    svc.stop()
+    err = svc.last_error()
+    con = sqlite3.connect(os.path.join(tmp, "build.db"))
+    nrows = con.execute("SELECT COUNT(*) FROM orders").fetchone()[0]
+    nfills = con.execute("SELECT COUNT(*) FROM fills").fetchone()[0]
+    con.close()
+    svc.close()
+    eng.close()
+    # (c) the oracle matcher alone, one core
+    ob = OracleBook(1)
+    t = time.perf_counter()
+    _, fo = ob.submit(rec)
+    dto = time.perf_counter() - t
+    ob.close()
+    out["build_submitorder_batched"] = {
+        "value": n / dt, "unit": "orders/s", "orders": n, "rows": int(nrows), "fill_rows": int(nfills),
+        "submit_only_orders_per_s": n / t_sub, "error": err,
+        "fills_match_oracle": int(nfills) == 2 * len(fo),
+        "what": "me_service_submit_order per request (one thread) -> time slices (1 ms / 65,536 orders, "
+                "background flusher) -> me_submit_host / me_collect on the GPU -> one SQLite transaction per "
+                "slice (orders rows with their matched status, fills rows, maker updates); clock stops when "
+                "every order is matched and committed"}
+    out["oracle_matcher"] = {"value": n / dto, "unit": "orders/s", "cores": 1, "kind": "port", "orders": n,
+                             "fills": len(fo), "what": "oracle/oracle_book.cpp alone (no SubmitOrder, no SQLite)"}
+    os.close(devnull)
+    return out
+
+
+def host_info():
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "cpu_model": model,
+            "cpus_allowed": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None}
+
+
 def main():
     args = parse()
     world, rank, local = dist_setup(args)
@@ -339,6 +463,7 @@ def main():
     if e2e_batches:
         eng.sync()
         slots = eng.config()["host_slots"]
+        eng.host_reserve()  # pinned slots are allocated on first use: a server does it at start-up
         t2 = time.perf_counter()
         n2, f2, pend = 0, 0, []
         for b in e2e_batches:
@@ -354,6 +479,7 @@ def main():
 
     if rank == 0:
         cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args)
+        c1 = c1_paths(args) if (args.workload == "c1" and world == 1 and not args.no_cpu_baseline) else None
         line = {
             "metric": "orders matched/sec (whole node); fills bit-exact vs CPU oracle",
             "value": orders_all / job_time,
@@ -393,6 +519,8 @@ def main():
                 "algorithmic_bytes_per_launch": bytes_per_launch,
             },
             "cpu_baseline": cpu,
+            "host": host_info(),
+            "c1_paths": c1,
         }
         print(json.dumps(line), flush=True)
     for db in dbs:

@@ -193,6 +193,9 @@ typedef struct me_order_soa_w {
   uint8_t* kind;
 } me_order_soa_w;
 int me_host_inputs(me_engine* e, size_t n, me_order_soa_w* out);
+/* Allocate the first nslots host slots now (0 = all of them) instead of on first use — a server's
+ * start-up, so no pinned allocation lands in the request path. */
+int me_host_reserve(me_engine* e, uint32_t nslots);
 /* The engine's configuration as created, defaults resolved (base_price / symbol_ids NULL). */
 int me_get_config(const me_engine* e, me_config* out);
 
@@ -226,9 +229,21 @@ int me_memcpy_h2d(me_engine* e, void* dst, const void* src, size_t bytes);
 /* Use an external hipStream_t (e.g. torch's current stream); NULL restores the engine's own. */
 int me_set_stream(me_engine* e, void* hip_stream);
 
-/* GetOrderBook: top `depth` levels per side, best first. */
+/* GetOrderBook: top `depth` levels per side, best first (one device snapshot launch). */
 int me_book_snapshot(me_engine* e, uint32_t symbol, me_level* bids, me_level* asks, size_t depth,
                      size_t* n_bids, size_t* n_asks);
+/* GetOrderBook in the reference's shape (OrderBookResponse = repeated Order, proto:16-23,57-60), from
+ * ONE device snapshot launch (k_book_snapshot, one workgroup per side): every resting order of the
+ * top `depth` levels of each side, best level first and FIFO order within a level, plus the levels'
+ * aggregates (bid_levels / ask_levels hold `depth` entries). Any output may be NULL; the counts are
+ * exact even when a cap is short (entries past it are not written). */
+int me_book_orders(me_engine* e, uint32_t symbol, uint32_t depth, me_book_entry* bids, size_t bids_cap,
+                   size_t* n_bids, me_book_entry* asks, size_t asks_cap, size_t* n_asks, me_level* bid_levels,
+                   me_level* ask_levels, size_t* n_bid_levels, size_t* n_ask_levels);
+/* The top `depth` levels per side of EVERY symbol of the shard in one launch — the periodic book
+ * snapshot a multi-GPU deployment gathers to its persistence root: levels[(s * 2 + side) * depth + k]
+ * (side 0 bids, 1 asks; best first), counts[s * 2 + side] = levels written. */
+int me_book_levels_all(me_engine* e, uint32_t depth, me_level* levels, uint32_t* counts);
 /* Full resting state of one symbol (side, price, FIFO). *n receives the count even when cap is short. */
 int me_book_dump(me_engine* e, uint32_t symbol, me_book_entry* out, size_t cap, size_t* n);
 /* Resting orders over all symbols (device counter). */

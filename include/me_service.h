@@ -70,6 +70,10 @@ void me_service_destroy(me_service* s);
 /* Always returns 0 (the RPC itself succeeded or failed in-band, like the reference). */
 int me_service_submit_order(me_service* s, const me_order_request* req, me_order_response* resp);
 
+/* n SubmitOrder calls in order (what a server's handler threads do one request at a time), for
+ * drivers and benchmarks holding many requests at once; resps[i] answers reqs[i]. */
+int me_service_submit_orders(me_service* s, const me_order_request* reqs, size_t n, me_order_response* resps);
+
 /* Orders waiting in the open time slice. */
 size_t me_service_pending(const me_service* s);
 /* Next OID number the service will allocate. */
@@ -94,9 +98,28 @@ size_t me_service_unpersisted(const me_service* s);
 int me_service_start(me_service* s, uint32_t interval_us, uint32_t slice_orders);
 int me_service_stop(me_service* s);
 
-/* GetOrderBook for a symbol string (top depth levels per side). */
+/* Level view of GetOrderBook for a symbol string (top depth levels per side, aggregates). */
 int me_service_book(me_service* s, const char* symbol, me_level* bids, me_level* asks, size_t depth,
                     size_t* n_bids, size_t* n_asks);
+
+/* Order (proto/matching_engine.proto:16-23): one resting order of an OrderBookResponse. */
+typedef struct me_book_order {
+  char order_id[32];  /* "OID-<n>" */
+  char client_id[64]; /* the submitting client ("" for orders that did not come through this service) */
+  int64_t price;      /* Q4 */
+  int32_t scale;      /* 4 */
+  int32_t quantity;   /* the resting (unfilled) quantity */
+  int32_t side;       /* ME_SIDE_BUY / ME_SIDE_SELL */
+  int32_t pad;
+} me_book_order;
+
+/* GetOrderBook (matching_engine_service.cpp:123-129) in the reference's shape: OrderBookResponse
+ * {repeated Order bids; repeated Order asks} (proto:57-60), bids best price first, asks best price
+ * first, FIFO (time) order within a price; from one device snapshot launch (me_book_orders). depth:
+ * price levels per side (0: the whole book, as OrderBookRequest carries no depth). Counts are exact
+ * even when a cap is short; unknown symbol: empty. */
+int me_service_order_book(me_service* s, const char* symbol, uint32_t depth, me_book_order* bids, size_t bids_cap,
+                          size_t* n_bids, me_book_order* asks, size_t asks_cap, size_t* n_asks);
 
 /* CancelOrder request (build extension, mirrors OrderRequest's conventions). */
 typedef struct me_cancel_request {

@@ -121,6 +121,7 @@ PROTOTYPES = {
     "me_collect": (C.c_int, [_P, C.c_uint64, C.POINTER(_P), C.POINTER(_SZ), C.POINTER(_P), C.POINTER(_SZ)]),
     "me_host_inputs": (C.c_int, [_P, _SZ, C.POINTER(MeOrderSoaW)]),
     "me_get_config": (C.c_int, [_P, C.POINTER(MeConfig)]),
+    "me_host_reserve": (C.c_int, [_P, C.c_uint32]),
     "me_submit_batch_device": (C.c_int, [_P, C.POINTER(MeOrderSoa), _SZ]),
     "me_sync": (C.c_int, [_P]),
     "me_fetch_outputs": (C.c_int, [_P, _P, _SZ, C.POINTER(_SZ), _P, _SZ]),
@@ -134,6 +135,9 @@ PROTOTYPES = {
     "me_set_stream": (C.c_int, [_P, _P]),
     "me_book_snapshot": (C.c_int, [_P, C.c_uint32, _P, _P, _SZ, C.POINTER(_SZ), C.POINTER(_SZ)]),
     "me_book_dump": (C.c_int, [_P, C.c_uint32, _P, _SZ, C.POINTER(_SZ)]),
+    "me_book_orders": (C.c_int, [_P, C.c_uint32, C.c_uint32, _P, _SZ, C.POINTER(_SZ), _P, _SZ, C.POINTER(_SZ),
+                                 _P, _P, C.POINTER(_SZ), C.POINTER(_SZ)]),
+    "me_book_levels_all": (C.c_int, [_P, C.c_uint32, _P, _P]),
     "me_resting_count": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
     "me_timing_enable": (C.c_int, [_P, C.c_int]),
     "me_timing_read": (
@@ -244,7 +248,23 @@ class MeMarketData(C.Structure):
         ("pad", C.c_int32),
     ]
 
+class MeBookOrder(C.Structure):
+    _fields_ = [
+        ("order_id", C.c_char * 32),
+        ("client_id", C.c_char * 64),
+        ("price", C.c_int64),
+        ("scale", C.c_int32),
+        ("quantity", C.c_int32),
+        ("side", C.c_int32),
+        ("pad", C.c_int32),
+    ]
+
+
+assert C.sizeof(MeBookOrder) == 120, "me_book_order layout"
+
 PROTOTYPES.update({
+    "me_service_order_book": (C.c_int, [_P, C.c_char_p, C.c_uint32, C.POINTER(MeBookOrder), _SZ, C.POINTER(_SZ),
+                                        C.POINTER(MeBookOrder), _SZ, C.POINTER(_SZ)]),
     "me_service_cancel_order": (C.c_int, [_P, C.POINTER(MeCancelRequest), C.POINTER(MeOrderResponse)]),
     "me_service_market_data": (C.c_int, [_P, C.c_char_p, C.POINTER(MeMarketData)]),
     "me_service_updates": (C.c_int, [_P, C.c_char_p, C.POINTER(MeOrderUpdate), _SZ, C.POINTER(_SZ)]),
@@ -257,6 +277,7 @@ PROTOTYPES.update({
     "me_service_book": (C.c_int, [_P, C.c_char_p, _P, _P, _SZ, C.POINTER(_SZ), C.POINTER(_SZ)]),
     "me_service_last_error": (C.c_int, [_P, C.c_char_p, _SZ]),
     "me_service_unpersisted": (_SZ, [_P]),
+    "me_service_submit_orders": (C.c_int, [_P, C.POINTER(MeOrderRequest), _SZ, C.POINTER(MeOrderResponse)]),
     "me_service_start": (C.c_int, [_P, C.c_uint32, C.c_uint32]),
     "me_service_stop": (C.c_int, [_P]),
 })

@@ -37,6 +37,7 @@ hipError_t launch_tape(hipStream_t st, const BatchDev& bt, me_fill* tape, unsign
 hipError_t launch_tape_spill(hipStream_t st, const me_order_result* res, const uint32_t* fstart, uint32_t n,
                              const me_fill* scratch, unsigned long long cap, me_fill* spill);
 hipError_t launch_init_levels(hipStream_t st, Level* levels, size_t count);
+hipError_t launch_book_snapshot(hipStream_t st, const BookDev& bk, const SnapReq& rq);
 hipError_t launch_init_chunks(hipStream_t st, Chunk* chunks, size_t count);
 }  // namespace me
 
@@ -156,6 +157,15 @@ struct me_engine {
   me_fill* d_spill = nullptr;
   size_t spill_cap = 0;
   bool last_host = false;  // the most recent batch was a host batch (the device-output fetches refuse)
+  struct SnapBufs {  // device buffers of the book snapshot kernel, grown on demand
+    uint32_t* sym = nullptr;
+    me_level* lv = nullptr;
+    uint32_t* nlv = nullptr;
+    me_book_entry* ord = nullptr;
+    unsigned long long* nord = nullptr;
+    uint32_t* err = nullptr;
+    size_t sym_cap = 0, lv_cap = 0, n_cap = 0, ord_cap = 0, nord_cap = 0, err_cap = 0;
+  } snap;
   uint32_t last_n = 0;
   uint32_t sq_idx = 0;  // seq-ring state the next k_seq_sweep reads (it writes the other one)
   struct LastGroup {    // the launch group holding the most recent batch: where its outputs live
@@ -232,6 +242,11 @@ static void free_all(me_engine* e) {
   }
   e->hs.clear();
   if (e->d_spill) (void)hipFree(e->d_spill);
+  {
+    void* sp[] = {e->snap.sym, e->snap.lv, e->snap.nlv, e->snap.ord, e->snap.nord, e->snap.err};
+    for (void* p : sp)
+      if (p) (void)hipFree(p);
+  }
   if (e->ev_tape) (void)hipEventDestroy(e->ev_tape);
   if (e->s_h2d) (void)hipStreamDestroy(e->s_h2d);
   if (e->s_d2h) (void)hipStreamDestroy(e->s_d2h);
@@ -973,6 +988,17 @@ extern "C" int me_host_inputs(me_engine* e, size_t n, me_order_soa_w* out) {
   return ME_OK;
 }
 
+extern "C" int me_host_reserve(me_engine* e, uint32_t nslots) {
+  if (!e) return ME_E_INVALID;
+  HIP_TRY(hipSetDevice(e->dev), "hipSetDevice");
+  const size_t k = nslots ? std::min<size_t>(nslots, e->hs.size()) : e->hs.size();
+  for (size_t i = 0; i < k; ++i) {
+    int rc = slot_alloc(e, e->hs[i]);
+    if (rc) return rc;
+  }
+  return ME_OK;
+}
+
 extern "C" int me_submit_host(me_engine* e, const me_order_soa* b, size_t n, uint64_t* ticket) {
   if (!e) return ME_E_INVALID;
   if (e->failed) return ME_E_STATE;
@@ -1185,93 +1211,116 @@ extern "C" int me_set_stream(me_engine* e, void* s) {
   return ME_OK;
 }
 
-// ---- book inspection (GetOrderBook / test dumps): host walk of device state ----------------
-namespace {
-struct HostLevelView {
-  std::vector<Level> levels;
-  SymState st;
-  std::vector<FarLevel> far[2];  // as stored: best last
-};
-// One price level in priority order (best first) of one side: window levels, then far levels.
-struct SideLevel {
-  int64_t price;
-  Level lv;
-};
-}  // namespace
+// ---- book inspection (GetOrderBook / test dumps): device snapshot kernel (me_snapshot.hip) ------
+// Run k_book_snapshot over syms[0..nsym) (host array), depth levels per side, orders into regions of
+// ocap per (symbol, side) (0: levels only). Results stay in e->snap.
+static int run_snapshot(me_engine* e, const uint32_t* syms, uint32_t nsym, uint32_t depth, uint64_t ocap) {
+  auto& sb = e->snap;
+  auto grow = [&](void** p, size_t& cap, size_t need, size_t elem) -> int {
+    if (need <= cap) return ME_OK;
+    if (*p) HIP_TRY(hipFree(*p), "hipFree");
+    *p = nullptr;
+    cap = 0;
+    HIP_TRY(hipMalloc(p, std::max<size_t>(need, 1) * elem), "hipMalloc snapshot");
+    cap = need;
+    return ME_OK;
+  };
+  int rc;
+  if ((rc = grow((void**)&sb.sym, sb.sym_cap, nsym, 4)) || (rc = grow((void**)&sb.nlv, sb.n_cap, 2ull * nsym, 4)) ||
+      (rc = grow((void**)&sb.nord, sb.nord_cap, 2ull * nsym, 8)) ||
+      (rc = grow((void**)&sb.lv, sb.lv_cap, 2ull * nsym * depth, sizeof(me_level))) ||
+      (rc = grow((void**)&sb.ord, sb.ord_cap, 2ull * nsym * ocap, sizeof(me_book_entry))) ||
+      (rc = grow((void**)&sb.err, sb.err_cap, 1, 4)))
+    return rc;
+  HIP_TRY(hipMemcpyAsync(sb.sym, syms, nsym * 4ull, hipMemcpyHostToDevice, e->stream), "H2D snapshot symbols");
+  HIP_TRY(hipMemsetAsync(sb.err, 0, 4, e->stream), "hipMemset");
+  SnapReq rq{};
+  rq.sym = sb.sym;
+  rq.nsym = nsym;
+  rq.depth = depth;
+  rq.lv = sb.lv;
+  rq.nlv = sb.nlv;
+  rq.ord = ocap ? sb.ord : nullptr;
+  rq.ocap = ocap;
+  rq.nord = sb.nord;
+  rq.err = sb.err;
+  hipError_t he = launch_book_snapshot(e->stream, e->bk, rq);
+  if (he != hipSuccess) return e->hip_fail(he, "snapshot launch");
+  uint32_t bad = 0;
+  HIP_TRY(hipMemcpyAsync(&bad, sb.err, 4, hipMemcpyDeviceToHost, e->stream), "D2H snapshot error");
+  HIP_TRY(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
+  if (bad) return e->fail(ME_E_STATE, "corrupt FIFO chain");
+  return ME_OK;
+}
 
-static int load_symbol(me_engine* e, uint32_t s, HostLevelView& v) {
-  const size_t L = e->bk.L;
-  v.levels.resize(L);
-  HIP_TRY(hipMemcpy(v.levels.data(), e->bk.levels + (size_t)s * L, L * sizeof(Level), hipMemcpyDeviceToHost),
-          "D2H levels");
-  HIP_TRY(hipMemcpy(&v.st, e->bk.sym + s, sizeof(SymState), hipMemcpyDeviceToHost), "D2H symbol");
-  for (uint32_t k = 0; k < 2; ++k) {
-    const uint32_t n = std::min(v.st.nfar[k], e->bk.fcap);
-    v.far[k].resize(n);
-    if (n)
-      HIP_TRY(hipMemcpy(v.far[k].data(), far_of(e->bk, s, k), n * sizeof(FarLevel), hipMemcpyDeviceToHost),
-              "D2H far levels");
+extern "C" int me_book_orders(me_engine* e, uint32_t symbol, uint32_t depth, me_book_entry* bids, size_t bids_cap,
+                              size_t* n_bids, me_book_entry* asks, size_t asks_cap, size_t* n_asks,
+                              me_level* bid_levels, me_level* ask_levels, size_t* n_bid_levels,
+                              size_t* n_ask_levels) {
+  if (!e) return ME_E_INVALID;
+  if (symbol >= e->bk.S) return e->fail(ME_E_INVALID, "symbol out of range");
+  int rc = me_sync(e);
+  if (rc) return rc;
+  const bool want_orders = bids || asks || n_bids || n_asks;
+  uint64_t ocap = 0;
+  if (want_orders) {  // the symbol's resting count bounds either side's orders
+    SymState ss;
+    HIP_TRY(hipMemcpy(&ss, e->bk.sym + symbol, sizeof ss, hipMemcpyDeviceToHost), "D2H symbol");
+    ocap = std::max<uint64_t>(ss.resting, 1);
+  }
+  if (!depth) {
+    if (n_bids) *n_bids = 0;
+    if (n_asks) *n_asks = 0;
+    if (n_bid_levels) *n_bid_levels = 0;
+    if (n_ask_levels) *n_ask_levels = 0;
+    return ME_OK;
+  }
+  if ((rc = run_snapshot(e, &symbol, 1, depth, ocap))) return rc;
+  auto& sb = e->snap;
+  uint32_t nl[2];
+  unsigned long long no[2];
+  HIP_TRY(hipMemcpy(nl, sb.nlv, sizeof nl, hipMemcpyDeviceToHost), "D2H snapshot counts");
+  HIP_TRY(hipMemcpy(no, sb.nord, sizeof no, hipMemcpyDeviceToHost), "D2H snapshot counts");
+  me_level* lo[2] = {bid_levels, ask_levels};
+  size_t* nlo[2] = {n_bid_levels, n_ask_levels};
+  me_book_entry* oo[2] = {bids, asks};
+  const size_t ocaps[2] = {bids_cap, asks_cap};
+  size_t* noo[2] = {n_bids, n_asks};
+  for (int k = 0; k < 2; ++k) {
+    if (nlo[k]) *nlo[k] = nl[k];
+    if (lo[k] && nl[k])
+      HIP_TRY(hipMemcpy(lo[k], sb.lv + (size_t)k * depth, nl[k] * sizeof(me_level), hipMemcpyDeviceToHost),
+              "D2H snapshot levels");
+    if (noo[k]) *noo[k] = (size_t)no[k];
+    const size_t m = std::min<size_t>({(size_t)no[k], ocaps[k], (size_t)ocap});
+    if (oo[k] && m)
+      HIP_TRY(hipMemcpy(oo[k], sb.ord + (size_t)k * ocap, m * sizeof(me_book_entry), hipMemcpyDeviceToHost),
+              "D2H snapshot orders");
   }
   return ME_OK;
 }
 
-// Bids (side 0) or asks (side 1) of a symbol, best first.
-static std::vector<SideLevel> side_levels(const me_engine* e, const HostLevelView& v, int side) {
-  std::vector<SideLevel> out;
-  const int L = (int)e->bk.L;
-  if (side == 0) {
-    for (int l = std::min(v.st.best_bid, L - 1); l >= 0; --l)
-      if (v.levels[l].total > 0) out.push_back({v.st.base + l, v.levels[l]});
-  } else {
-    for (int l = std::max(v.st.best_ask, 0); l < L; ++l)
-      if (v.levels[l].total > 0) out.push_back({v.st.base + l, v.levels[l]});
-  }
-  for (size_t i = v.far[side].size(); i-- > 0;) {
-    const FarLevel& f = v.far[side][i];
-    out.push_back({f.price, Level{f.total, f.head, f.tail}});
-  }
-  return out;
-}
-
-// Live (seq, qty) of a level FIFO in priority order.
-static int walk_fifo(me_engine* e, const Level& lv, std::vector<std::pair<uint64_t, int32_t>>& out) {
-  out.clear();
-  uint32_t ch = lv.head;
-  uint64_t guard = 0;
-  while (ch != NIL) {
-    if (ch >= e->bk.nchunks || ++guard > e->bk.nchunks) return e->fail(ME_E_STATE, "corrupt FIFO chain");
-    Chunk c;
-    HIP_TRY(hipMemcpy(&c, e->bk.chunks + ch, sizeof(c), hipMemcpyDeviceToHost), "D2H chunk");
-    for (uint32_t k = 0; k < (uint32_t)ME_C; ++k)  // a slot is live iff qty > 0; slot order = time order
-      if (c.qty[k] > 0) out.emplace_back(c.seq[k], c.qty[k]);
-    if (ch == lv.tail) break;
-    ch = c.hdr.next;
-  }
+extern "C" int me_book_levels_all(me_engine* e, uint32_t depth, me_level* levels, uint32_t* counts) {
+  if (!e) return ME_E_INVALID;
+  int rc = me_sync(e);
+  if (rc) return rc;
+  if (!depth) return ME_OK;
+  std::vector<uint32_t> syms(e->bk.S);
+  for (uint32_t k = 0; k < e->bk.S; ++k) syms[k] = k;
+  if ((rc = run_snapshot(e, syms.data(), e->bk.S, depth, 0))) return rc;
+  auto& sb = e->snap;
+  if (counts) HIP_TRY(hipMemcpy(counts, sb.nlv, 2ull * e->bk.S * 4, hipMemcpyDeviceToHost), "D2H snapshot counts");
+  if (levels)
+    HIP_TRY(hipMemcpy(levels, sb.lv, 2ull * e->bk.S * depth * sizeof(me_level), hipMemcpyDeviceToHost),
+            "D2H snapshot levels");
   return ME_OK;
 }
 
 extern "C" int me_book_snapshot(me_engine* e, uint32_t symbol, me_level* bids, me_level* asks, size_t depth,
                                 size_t* n_bids, size_t* n_asks) {
   if (!e) return ME_E_INVALID;
-  if (symbol >= e->bk.S) return e->fail(ME_E_INVALID, "symbol out of range");
-  int rc = me_sync(e);
-  if (rc) return rc;
-  HostLevelView v;
-  if ((rc = load_symbol(e, symbol, v))) return rc;
-  std::vector<std::pair<uint64_t, int32_t>> fifo;
-  for (int side = 0; side < 2; ++side) {
-    me_level* out = side ? asks : bids;
-    size_t k = 0;
-    for (const SideLevel& sl : side_levels(e, v, side)) {
-      if (k >= depth) break;
-      if ((rc = walk_fifo(e, sl.lv, fifo))) return rc;
-      if (out) out[k] = me_level{sl.price, sl.lv.total, (uint32_t)fifo.size(), 0};
-      ++k;
-    }
-    if (side == 0 && n_bids) *n_bids = k;
-    if (side == 1 && n_asks) *n_asks = k;
-  }
-  return ME_OK;
+  const uint32_t d = (uint32_t)std::min<size_t>(depth, 0xFFFFFFFFu);
+  return me_book_orders(e, symbol, d, nullptr, 0, nullptr, nullptr, 0, nullptr, bids, asks, n_bids, n_asks);
 }
 
 extern "C" int me_book_dump(me_engine* e, uint32_t symbol, me_book_entry* out, size_t cap, size_t* n) {
@@ -1279,27 +1328,21 @@ extern "C" int me_book_dump(me_engine* e, uint32_t symbol, me_book_entry* out, s
   if (symbol >= e->bk.S) return e->fail(ME_E_INVALID, "symbol out of range");
   int rc = me_sync(e);
   if (rc) return rc;
-  HostLevelView v;
-  if ((rc = load_symbol(e, symbol, v))) return rc;
-  std::vector<std::pair<uint64_t, int32_t>> fifo;
-  size_t k = 0;
-  for (int side = 0; side < 2; ++side) {
-    for (const SideLevel& sl : side_levels(e, v, side)) {
-      if ((rc = walk_fifo(e, sl.lv, fifo))) return rc;
-      for (auto& pr : fifo) {
-        if (out && k < cap) {
-          me_book_entry be{};
-          be.seq = pr.first;
-          be.price_q4 = sl.price;
-          be.qty = pr.second;
-          be.side = side ? ME_SIDE_SELL : ME_SIDE_BUY;
-          out[k] = be;
-        }
-        ++k;
-      }
-    }
+  SymState ss;
+  HIP_TRY(hipMemcpy(&ss, e->bk.sym + symbol, sizeof ss, hipMemcpyDeviceToHost), "D2H symbol");
+  // every level of both sides (the whole window plus the far arrays), bids then asks
+  std::vector<me_book_entry> side[2];
+  side[0].resize(ss.resting + 1);
+  side[1].resize(ss.resting + 1);
+  size_t nb = 0, na = 0;
+  rc = me_book_orders(e, symbol, e->bk.L + e->bk.fcap, side[0].data(), side[0].size(), &nb, side[1].data(),
+                      side[1].size(), &na, nullptr, nullptr, nullptr, nullptr);
+  if (rc) return rc;
+  if (out) {
+    memcpy(out, side[0].data(), std::min(nb, cap) * sizeof(me_book_entry));
+    if (cap > nb) memcpy(out + nb, side[1].data(), std::min(na, cap - nb) * sizeof(me_book_entry));
   }
-  if (n) *n = k;
+  if (n) *n = nb + na;
   return ME_OK;
 }
 

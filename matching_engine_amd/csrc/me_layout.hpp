@@ -265,6 +265,19 @@ struct AuxDev {
   AuxTape t[ME_GMAX];
 };
 
+// A book snapshot request (me_snapshot.hip k_book_snapshot): one workgroup per (symbol, side).
+struct SnapReq {
+  const uint32_t* sym;       // [nsym] symbols
+  uint32_t nsym;
+  uint32_t depth;            // levels per side at most
+  me_level* lv;              // [nsym][2][depth] level aggregates, best first
+  uint32_t* nlv;             // [nsym][2] levels written
+  me_book_entry* ord;        // [nsym][2][ocap] orders in priority order (nullptr: levels only)
+  unsigned long long ocap;   // orders per (symbol, side) region
+  unsigned long long* nord;  // [nsym][2] orders on those levels (exact, even past ocap)
+  uint32_t* err;             // set on a corrupt chain
+};
+
 constexpr int BK_CAP = 128;          // records per bucket (two 64-record blocks)
 constexpr int BK_KIND_SHIFT = 28;    // BkRec::ok: kind bits above the batch index
 constexpr uint32_t BK_IDX_MASK = (1u << BK_KIND_SHIFT) - 1u;

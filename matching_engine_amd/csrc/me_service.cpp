@@ -25,6 +25,7 @@
 #include <dlfcn.h>
 #include <string.h>
 
+#include <algorithm>
 #include <chrono>
 #include <condition_variable>
 #include <deque>
@@ -383,6 +384,12 @@ extern "C" int me_service_submit_order(me_service* s, const me_order_request* r,
   }
   append(s, id, q4, r->quantity, sid, ME_KIND(r->side, limit ? ME_TYPE_LIMIT : ME_TYPE_MARKET, ME_OP_NEW),
          Pending{std::move(client), sym, r->side, false, 0});
+  return 0;
+}
+
+extern "C" int me_service_submit_orders(me_service* s, const me_order_request* reqs, size_t n,
+                                        me_order_response* resps) {
+  for (size_t i = 0; i < n; ++i) me_service_submit_order(s, reqs + i, resps + i);
   return 0;
 }
 
@@ -859,6 +866,60 @@ extern "C" int me_service_book(me_service* s, const char* symbol, me_level* bids
     me_last_error(s->eng, e, sizeof e);
     return s->fail(rc, std::string("engine: ") + e);
   }
+  return ME_OK;
+}
+
+extern "C" int me_service_order_book(me_service* s, const char* symbol, uint32_t depth, me_book_order* bids,
+                                     size_t bids_cap, size_t* n_bids, me_book_order* asks, size_t asks_cap,
+                                     size_t* n_asks) {
+  if (n_bids) *n_bids = 0;
+  if (n_asks) *n_asks = 0;
+  uint32_t sid = 0;
+  {
+    std::lock_guard<std::mutex> lk(s->mu);
+    auto it = s->sym.find(symbol ? symbol : "");
+    if (it == s->sym.end()) return ME_OK;
+    sid = it->second;
+  }
+  if (!s->eng) return s->fail(ME_E_STATE, "no engine");
+  std::vector<me_book_entry> side[2];
+  size_t n[2] = {0, 0};
+  {
+    std::lock_guard<std::mutex> le(s->eng_mu);
+    me_config c{};
+    me_get_config(s->eng, &c);
+    const uint32_t d = depth ? depth : c.levels + c.far_levels;
+    side[0].resize(std::max<size_t>(bids_cap, 1));
+    side[1].resize(std::max<size_t>(asks_cap, 1));
+    const int rc = me_book_orders(s->eng, sid, d, bids ? side[0].data() : nullptr, bids ? side[0].size() : 0, &n[0],
+                                  asks ? side[1].data() : nullptr, asks ? side[1].size() : 0, &n[1], nullptr, nullptr,
+                                  nullptr, nullptr);
+    if (rc != ME_OK) {
+      char e[512];
+      me_last_error(s->eng, e, sizeof e);
+      return s->fail(rc, std::string("engine: ") + e);
+    }
+  }
+  me_book_order* out[2] = {bids, asks};
+  const size_t caps[2] = {bids_cap, asks_cap};
+  std::lock_guard<std::mutex> lv(s->live_mu);
+  for (int k = 0; k < 2; ++k) {
+    if (!out[k]) continue;
+    for (size_t i = 0; i < n[k] && i < caps[k]; ++i) {
+      const me_book_entry& e = side[k][i];
+      me_book_order& o = out[k][i];
+      memset(&o, 0, sizeof o);
+      put(o.order_id, sizeof o.order_id, "OID-" + std::to_string(e.seq));
+      auto it = s->live.find(e.seq);
+      if (it != s->live.end()) put(o.client_id, sizeof o.client_id, it->second.client);
+      o.price = e.price_q4;
+      o.scale = 4;
+      o.quantity = e.qty;
+      o.side = e.side;
+    }
+  }
+  if (n_bids) *n_bids = n[0];
+  if (n_asks) *n_asks = n[1];
   return ME_OK;
 }
 

@@ -216,6 +216,10 @@ class Engine:
                 (("seq", "<u8"), ("price_q4", "<i8"), ("qty", "<i4"), ("symbol", "<u4"), ("kind", "u1"))]
         return Batch(*arrs)
 
+    def host_reserve(self, nslots: int = 0):
+        """Allocate host slots now (0 = all) rather than on first use."""
+        _check(self.lib, self.h, self.lib.me_host_reserve(self.h, nslots))
+
     def config(self) -> dict:
         cfg = MeConfig()
         _check(self.lib, self.h, self.lib.me_get_config(self.h, C.byref(cfg)))
@@ -272,6 +276,27 @@ class Engine:
         rc = self.lib.me_book_snapshot(self.h, symbol, ptr(bids), ptr(asks), depth, C.byref(nb), C.byref(na))
         _check(self.lib, self.h, rc)
         return bids[: nb.value], asks[: na.value]
+
+    def book_orders(self, symbol: int, depth: int):
+        """GetOrderBook per order from one device snapshot launch: (bids, asks) BOOK_ENTRY_DTYPE in
+        priority order over the top `depth` levels per side, and (bid_levels, ask_levels)."""
+        nb, na, nlb, nla = C.c_size_t(0), C.c_size_t(0), C.c_size_t(0), C.c_size_t(0)
+        lb = np.zeros(max(depth, 1), dtype=LEVEL_DTYPE)
+        la = np.zeros(max(depth, 1), dtype=LEVEL_DTYPE)
+        _check(self.lib, self.h, self.lib.me_book_orders(self.h, symbol, depth, None, 0, C.byref(nb), None, 0,
+                                                         C.byref(na), ptr(lb), ptr(la), C.byref(nlb), C.byref(nla)))
+        bids = np.zeros(nb.value, dtype=BOOK_ENTRY_DTYPE)
+        asks = np.zeros(na.value, dtype=BOOK_ENTRY_DTYPE)
+        _check(self.lib, self.h, self.lib.me_book_orders(self.h, symbol, depth, ptr(bids), len(bids), C.byref(nb),
+                                                         ptr(asks), len(asks), C.byref(na), None, None, None, None))
+        return bids, asks, lb[: nlb.value], la[: nla.value]
+
+    def levels_all(self, depth: int):
+        """Top `depth` levels per side of every symbol (one launch): (levels[S, 2, depth], counts[S, 2])."""
+        lv = np.zeros(self.num_symbols * 2 * depth, dtype=LEVEL_DTYPE)
+        cnt = np.zeros(self.num_symbols * 2, dtype=np.uint32)
+        _check(self.lib, self.h, self.lib.me_book_levels_all(self.h, depth, ptr(lv), ptr(cnt)))
+        return lv.reshape(self.num_symbols, 2, depth), cnt.reshape(self.num_symbols, 2)
 
     def dump(self, symbol: int) -> np.ndarray:
         n = C.c_size_t(0)

@@ -7,8 +7,8 @@ import ctypes as C
 import numpy as np
 
 from . import _abi
-from ._abi import (FILL_DTYPE, LEVEL_DTYPE, RESULT_DTYPE, MeCancelRequest, MeOrderRequest, MeOrderResponse,
-                   MeMarketData, MeOrderUpdate, ptr)
+from ._abi import (FILL_DTYPE, LEVEL_DTYPE, RESULT_DTYPE, MeBookOrder, MeCancelRequest, MeOrderRequest,
+                   MeOrderResponse, MeMarketData, MeOrderUpdate, ptr)
 
 
 class ServiceError(RuntimeError):
@@ -140,3 +140,23 @@ class MatchingEngineService:
         if rc != 0:
             raise ServiceError(self.last_error())
         return bids[: nb.value], asks[: na.value]
+
+    def order_book(self, symbol, depth=0):
+        """GetOrderBook in the reference's shape (OrderBookResponse: repeated Order bids / asks, proto
+        :16-23,57-60): lists of {order_id, client_id, price, scale, quantity, side} dicts, best price
+        first, time order within a price; depth = price levels per side (0: the whole book)."""
+        nb, na = C.c_size_t(0), C.c_size_t(0)
+        rc = self.lib.me_service_order_book(self.h, symbol.encode(), depth, None, 0, C.byref(nb), None, 0, C.byref(na))
+        if rc != 0:
+            raise ServiceError(self.last_error())
+        bids, asks = (MeBookOrder * max(nb.value, 1))(), (MeBookOrder * max(na.value, 1))()
+        rc = self.lib.me_service_order_book(self.h, symbol.encode(), depth, bids, nb.value, C.byref(nb), asks,
+                                            na.value, C.byref(na))
+        if rc != 0:
+            raise ServiceError(self.last_error())
+
+        def conv(arr, n):
+            return [{"order_id": o.order_id.decode(), "client_id": o.client_id.decode(), "price": o.price,
+                     "scale": o.scale, "quantity": o.quantity, "side": o.side} for o in arr[:n]]
+
+        return conv(bids, nb.value), conv(asks, na.value)

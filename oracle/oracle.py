@@ -51,6 +51,8 @@ def load():
                                            C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int64),
                                            C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int64),
                                            C.POINTER(C.c_int32)]
+        lib.ref_submit_run.restype = C.c_longlong
+        lib.ref_submit_run.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, SZ, P, P, P, P, P, C.c_int, P]
         _lib = lib
     return _lib
 
@@ -156,3 +158,17 @@ def ref_normalize_many(pairs):
         else:
             res.append(int(parts[2]))
     return res
+
+
+def ref_submit_run(db_path, client_id, symbol, order_type, side, price, scale, quantity, log_fd):
+    """The reference's per-order SubmitOrder + insert_new_order path (oracle/ref_submit.cpp), one SQLite
+    transaction per order, logs to log_fd. Returns (rows written, ok[n])."""
+    n = len(order_type)
+    arrs = [np.ascontiguousarray(a, dtype=t) for a, t in
+            ((order_type, np.int32), (side, np.int32), (price, np.int64), (scale, np.int32), (quantity, np.int32))]
+    ok = np.zeros(n, dtype=np.uint8)
+    rows = load().ref_submit_run(db_path.encode(), client_id.encode(), symbol.encode(), n,
+                                 *[a.ctypes.data for a in arrs], log_fd, ok.ctypes.data)
+    if rows < 0:
+        raise RuntimeError("ref_submit_run: SQLite unavailable")
+    return rows, ok

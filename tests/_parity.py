@@ -81,3 +81,16 @@ def load_fixture(cid):
     meta = dict(num_symbols=int(z["num_symbols"][0]), levels=int(z["levels"][0]), base=z["base"],
                 book_counts=z["book_counts"])
     return meta, batches, res, fills, book
+
+
+def side_levels(dump, side, depth):
+    """Oracle resting orders of one side (dump order: priority) restricted to its first `depth`
+    distinct prices."""
+    d = dump[dump["side"] == side]
+    prices = []
+    keep = np.zeros(len(d), dtype=bool)
+    for i, p in enumerate(d["price_q4"]):
+        if not prices or prices[-1] != p:
+            prices.append(p)
+        keep[i] = len(prices) <= depth
+    return d[keep]

@@ -5,7 +5,7 @@ import numpy as np
 import pytest
 
 from tests._parity import (assert_books_equal, assert_fills_equal, assert_results_equal, load_fixture,
-                           run_both)
+                           run_both, side_levels)
 
 pytestmark = pytest.mark.gpu
 
@@ -531,3 +531,50 @@ def test_partial_groups_between_fetches(me, orc):
                 db.free()
         assert_books_equal(eng, ob, range(0, sc.num_symbols, 3), "partial groups")
         assert eng.resting_count() == ob.resting()
+
+
+# ---------------------------------------------------------------- device book snapshots
+@pytest.mark.parametrize("levels", [128, 1024])
+def test_book_orders_snapshot_kernel(me, orc, levels):
+    """GetOrderBook per order (one k_book_snapshot launch): the top-N levels' resting orders in
+    priority order and the level aggregates equal the oracle's, window and far levels alike; the
+    all-symbol level snapshot equals the per-symbol one."""
+    sc = me.preset(2, num_symbols=48, levels=levels, batch=4096, drift_step=3, drift_every=40, far_pct=3)
+    st = me.Stream(sc)
+    base = st.base_prices()
+    batches = [st.next(sc.batch) for _ in range(6)]
+    ob = orc.OracleBook(sc.num_symbols)
+    total = sum(len(b) for b in batches)
+    with engine_for(me, sc.num_symbols, sc.levels, base, sc.batch, total + 1024, max_chunks=total + 256) as eng:
+        run_both(eng, ob, batches, ctx="snapshot")
+        lv_all, cnt_all = eng.levels_all(7)
+        for s in range(sc.num_symbols):
+            dump = ob.dump(s)
+            for depth in (1, 7, 100000):
+                bids, asks, lb, la = eng.book_orders(s, depth)
+                eb = side_levels(dump, me.SIDE_BUY, depth)
+                ea = side_levels(dump, me.SIDE_SELL, depth)
+                assert np.array_equal(bids, eb), f"symbol {s} depth {depth}: bids"
+                assert np.array_equal(asks, ea), f"symbol {s} depth {depth}: asks"
+                sb, sa = ob.snapshot(s, depth)
+                assert np.array_equal(lb, sb) and np.array_equal(la, sa), f"symbol {s} depth {depth}: levels"
+                if depth == 7:
+                    assert np.array_equal(lv_all[s, 0, : cnt_all[s, 0]], sb)
+                    assert np.array_equal(lv_all[s, 1, : cnt_all[s, 1]], sa)
+
+
+def test_book_orders_ten_thousand_levels_one_launch(me, orc):
+    """A 10,000-level-per-side book (config 4's seeded shape, L = 32,768) snapshots per order in one
+    launch and equals the oracle."""
+    sc = me.preset(4, num_symbols=8, batch=65536)
+    st = me.Stream(sc)
+    base = st.base_prices()
+    seeds = st.seed_books(range(2), 10_000)
+    ob = orc.OracleBook(sc.num_symbols)
+    with engine_for(me, sc.num_symbols, sc.levels, base, 65536, len(seeds) + 1024, max_chunks=len(seeds) + 64) as eng:
+        run_both(eng, ob, [seeds.take(slice(0, 20000)), seeds.take(slice(20000, None))], check_books=False)
+        bids, asks, lb, la = eng.book_orders(0, 10_000)
+        dump = ob.dump(0)
+        assert len(lb) == 10_000 and len(la) == 10_000
+        assert np.array_equal(bids, dump[dump["side"] == me.SIDE_BUY])
+        assert np.array_equal(asks, dump[dump["side"] == me.SIDE_SELL])

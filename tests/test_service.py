@@ -8,7 +8,7 @@ import sqlite3
 import numpy as np
 import pytest
 
-from tests._parity import assert_fills_equal, assert_results_equal
+from tests._parity import assert_fills_equal, assert_results_equal, side_levels
 
 GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
@@ -156,6 +156,14 @@ def test_submitorder_stream_matches_oracle_and_db(me, tmp_path):
     bids, asks = svc.get_order_book("S3", 5)
     obids, oasks = ob.snapshot(3, 5)
     assert np.array_equal(bids, obids) and np.array_equal(asks, oasks)
+    # GetOrderBook in the reference's shape: repeated Order {order_id, client_id, price, scale, quantity, side}
+    for s in ("S3", "S9"):
+        gb, ga = svc.order_book(s)
+        d = ob.dump(syms.index(s))
+        exp = [{"order_id": f"OID-{int(e['seq'])}", "client_id": "C", "price": int(e["price_q4"]), "scale": 4,
+                "quantity": int(e["qty"]), "side": int(e["side"])} for e in d]
+        assert gb + ga == exp
+    assert svc.order_book("NOPE") == ([], [])
     # StreamMarketData's MarketDataUpdate: the top level of each side
     for s in syms[:4]:
         md = svc.market_data(s)
@@ -205,6 +213,7 @@ def test_cancels_and_order_update_stream(me, tmp_path):
     svc = me.MatchingEngineService(eng, syms, db_path=db)
     ob = OracleBook(len(syms))
     accepted = []  # (oid, symbol) of LIMIT orders
+    owner = {}
     events = []
     for slice_no in range(4):
         seqs, px, qty, sid, kinds = [], [], [], [], []
@@ -214,7 +223,7 @@ def test_cancels_and_order_update_stream(me, tmp_path):
                 oid, s = accepted[int(rng.integers(len(accepted)))]
                 if rng.random() < 0.1:
                     s = syms[(syms.index(s) + 1) % len(syms)]  # wrong symbol -> REJECTED
-                r = svc.cancel_order(f"C{oid % 3}", s, f"OID-{oid}")
+                r = svc.cancel_order(owner[oid], s, f"OID-{oid}")
                 assert r["success"] and r["order_id"] == f"OID-{oid}"
                 seqs.append(svc.next_oid - 1)
                 px.append(oid)
@@ -229,6 +238,7 @@ def test_cancels_and_order_update_stream(me, tmp_path):
             qn = int(rng.integers(1, 60))
             r = svc.submit_order(f"C{svc.next_oid % 3}", s, otype, side, 0 if otype else q4, 4, qn)
             oid = int(r["order_id"][4:])
+            owner[oid] = f"C{oid % 3}"
             if otype == 0:
                 accepted.append((oid, s))
             seqs.append(oid)
@@ -267,6 +277,13 @@ def test_cancels_and_order_update_stream(me, tmp_path):
         if e["status"] == 3:
             assert row[0] == 3
     assert checked > 1000
+    for s in syms[:3]:  # the per-order book carries every resting order's own client id
+        gb, ga = svc.order_book(s, depth=4)
+        for o in gb + ga:
+            assert o["client_id"] == owner[int(o["order_id"][4:])]
+        d = ob.dump(syms.index(s))
+        assert [o["order_id"] for o in gb] == [f"OID-{int(e['seq'])}" for e in
+                                               side_levels(d, me.SIDE_BUY, 4)]
     svc.close()
     eng.close()
 
