@@ -7,7 +7,11 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <mutex>
+#include <thread>
+#include <memory>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -51,6 +55,85 @@ struct TimedLaunch {
   hipEvent_t m0, m1;  // start / end of one match-kernel launch (recorded by the launch itself)
   uint64_t orders;
   uint64_t idx;       // batches matched (since timing was enabled) before this launch
+};
+
+// A few host threads for the staging copy of large host batches (me_submit_host): one memcpy into
+// pinned memory runs at ~10 GB/s, which alone would cap the host path near 400M orders/s (25 B each).
+class CopyPool {
+ public:
+  struct Piece {
+    void* dst;
+    const void* src;
+    size_t bytes;
+  };
+  explicit CopyPool(int n) {
+    for (int i = 0; i < n; ++i) th_.emplace_back([this] { worker(); });
+  }
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  // Copies every piece (the caller works too); no worker touches them after it returns.
+  void run(const std::vector<Piece>& p) {
+    std::unique_lock<std::mutex> lk(mu_);
+    jobs_ = p.data();
+    njobs_ = p.size();
+    next_.store(0);
+    done_ = 0;
+    ++gen_;
+    cv_.notify_all();
+    lk.unlock();
+    work(jobs_, njobs_);
+    lk.lock();
+    done_cv_.wait(lk, [&] { return done_ == njobs_ && active_ == 0; });
+    jobs_ = nullptr;
+    njobs_ = 0;
+  }
+
+ private:
+  void work(const Piece* jobs, size_t nj) {
+    size_t mine = 0;
+    for (;;) {
+      const size_t i = next_.fetch_add(1);
+      if (i >= nj) break;
+      memcpy(jobs[i].dst, jobs[i].src, jobs[i].bytes);
+      ++mine;
+    }
+    std::lock_guard<std::mutex> lk(mu_);
+    done_ += mine;
+    if (done_ == njobs_) done_cv_.notify_all();
+  }
+  void worker() {
+    std::unique_lock<std::mutex> lk(mu_);
+    uint64_t seen = 0;
+    for (;;) {
+      cv_.wait(lk, [&] { return stop_ || (gen_ != seen && jobs_); });
+      if (stop_) return;
+      seen = gen_;
+      const Piece* jobs = jobs_;
+      const size_t nj = njobs_;
+      ++active_;
+      lk.unlock();
+      work(jobs, nj);
+      lk.lock();
+      --active_;
+      done_cv_.notify_all();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  const Piece* jobs_ = nullptr;
+  size_t njobs_ = 0;
+  std::atomic<size_t> next_{0};
+  size_t done_ = 0;
+  int active_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
 };
 
 // Output block of a host slot (same layout in HBM and in pinned memory): SlotMeta, the tape (cap
@@ -157,6 +240,7 @@ struct me_engine {
   me_fill* d_spill = nullptr;
   size_t spill_cap = 0;
   bool last_host = false;  // the most recent batch was a host batch (the device-output fetches refuse)
+  std::unique_ptr<CopyPool> copy_pool;  // started on the first large host batch
   struct SnapBufs {  // device buffers of the book snapshot kernel, grown on demand
     uint32_t* sym = nullptr;
     me_level* lv = nullptr;
@@ -1018,11 +1102,18 @@ extern "C" int me_submit_host(me_engine* e, const me_order_soa* b, size_t n, uin
   slot_soa(h.h_in, n, seq, px, qty, sym, kind);
   if (b->seq != seq || b->price_q4 != px || b->qty != qty || b->symbol != sym || b->kind != kind) {
     HIP_TRY(hipEventSynchronize(h.ev_in), "hipEventSynchronize");
-    memcpy(seq, b->seq, 8 * n);
-    memcpy(px, b->price_q4, 8 * n);
-    memcpy(qty, b->qty, 4 * n);
-    memcpy(sym, b->symbol, 4 * n);
-    memcpy(kind, b->kind, n);
+    const CopyPool::Piece cols[5] = {{seq, b->seq, 8 * n}, {px, b->price_q4, 8 * n}, {qty, b->qty, 4 * n},
+                                     {sym, b->symbol, 4 * n}, {kind, b->kind, n}};
+    if (n < 16384) {
+      for (const auto& c : cols) memcpy(c.dst, c.src, c.bytes);
+    } else {  // 64-KB pieces over the copy threads
+      if (!e->copy_pool) e->copy_pool.reset(new CopyPool(4));
+      std::vector<CopyPool::Piece> pieces;
+      for (const auto& c : cols)
+        for (size_t o = 0; o < c.bytes; o += 65536)
+          pieces.push_back({(char*)c.dst + o, (const char*)c.src + o, std::min<size_t>(65536, c.bytes - o)});
+      e->copy_pool->run(pieces);
+    }
   }
   // one H2D of the packed batch on the H2D stream; the engine stream waits for it before the launch
   // that buckets (or sorts) the batch

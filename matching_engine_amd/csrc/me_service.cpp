@@ -158,6 +158,7 @@ struct Live {
 };
 
 constexpr size_t kMaxQueuedUpdates = size_t(1) << 24;  // oldest events are dropped beyond this
+constexpr int kRows = 64;  // rows per multi-row INSERT (11 * 64 parameters < SQLite's 999 floor)
 
 }  // namespace
 
@@ -196,6 +197,8 @@ struct me_service {
   sqlite3_stmt* st_upd = nullptr;
   sqlite3_stmt* st_fill = nullptr;
   sqlite3_stmt* st_maker = nullptr;
+  sqlite3_stmt* st_ins_k = nullptr;   // kRows-row INSERT INTO orders
+  sqlite3_stmt* st_fill_k = nullptr;  // kRows-row INSERT INTO fills
   bool failed = false;  // the engine lost a slice it had accepted: nothing more can be matched
   // --- err_mu
   mutable std::mutex err_mu;
@@ -210,9 +213,9 @@ struct me_service {
 };
 
 static void close_db(me_service* s) {
-  for (sqlite3_stmt* st : {s->st_ins, s->st_upd, s->st_fill, s->st_maker})
+  for (sqlite3_stmt* st : {s->st_ins, s->st_upd, s->st_fill, s->st_maker, s->st_ins_k, s->st_fill_k})
     if (st) g_sql.finalize(st);
-  s->st_ins = s->st_upd = s->st_fill = s->st_maker = nullptr;
+  s->st_ins = s->st_upd = s->st_fill = s->st_maker = s->st_ins_k = s->st_fill_k = nullptr;
   if (s->db) g_sql.close(s->db);
   s->db = nullptr;
 }
@@ -258,10 +261,23 @@ static bool open_db(me_service* s, const char* path, std::string& err) {
   const char* maker =
       "UPDATE orders SET remaining_quantity=remaining_quantity-?, status=CASE WHEN remaining_quantity-?=0 "
       "THEN 2 ELSE 1 END, updated_ts=? WHERE order_id=?";
+  // multi-row forms: one statement step per kRows rows
+  auto rows = [](const char* head, const char* tuple) {
+    std::string q(head);
+    for (int r = 0; r < kRows; ++r) q += (r ? "," : "") + std::string(tuple);
+    return q;
+  };
+  const std::string ins_k = rows("INSERT INTO orders(order_id, client_id, symbol, side, order_type, price, quantity, "
+                                 "status, remaining_quantity, created_ts, updated_ts) VALUES ",
+                                 "(?,?,?,?,?,?,?,?,?,?,?)");
+  const std::string fill_k =
+      rows("INSERT INTO fills(order_id, symbol, fill_price, fill_quantity, event_ts) VALUES ", "(?,?,?,?,?)");
   return chk(g_sql.prepare_v2(s->db, ins, -1, &s->st_ins, nullptr), "prepare insert") &&
          chk(g_sql.prepare_v2(s->db, upd, -1, &s->st_upd, nullptr), "prepare update") &&
          chk(g_sql.prepare_v2(s->db, fill, -1, &s->st_fill, nullptr), "prepare fill") &&
-         chk(g_sql.prepare_v2(s->db, maker, -1, &s->st_maker, nullptr), "prepare maker");
+         chk(g_sql.prepare_v2(s->db, maker, -1, &s->st_maker, nullptr), "prepare maker") &&
+         chk(g_sql.prepare_v2(s->db, ins_k.c_str(), -1, &s->st_ins_k, nullptr), "prepare insert rows") &&
+         chk(g_sql.prepare_v2(s->db, fill_k.c_str(), -1, &s->st_fill_k, nullptr), "prepare fill rows");
 }
 
 extern "C" me_service* me_service_create(me_engine* engine, const char* const* symbols, uint32_t num_symbols,
@@ -274,6 +290,7 @@ extern "C" me_service* me_service_create(me_engine* engine, const char* const* s
       s->sym_cap = c.num_symbols;
       s->slice_max = c.max_batch;
     }
+    me_host_reserve(engine, 1);  // the flusher reuses one warm pinned slot
   }
   for (uint32_t i = 0; i < num_symbols; ++i) {
     s->names.emplace_back(symbols[i]);
@@ -557,74 +574,152 @@ extern "C" int me_service_updates(me_service* s, const char* client_id, me_order
   return ME_OK;
 }
 
-// One transaction for one matched slice (flush_mu held).
+// One transaction for one matched slice (flush_mu held). The rows end exactly as the reference's
+// per-order statements would leave them — insert_new_order's row (storage.cpp:102-112, incl.
+// order_type=1, storage.cpp:106), then update_order_status-style changes (storage.cpp:160-181) as
+// later fills and cancels hit the order — but the slice's own orders are brought to their final
+// state in memory first, so each is ONE multi-row INSERT entry and only orders of earlier slices
+// take UPDATEs. Orders rows go in before fills rows (the fills' foreign key), fills rows in tape
+// order (taker's row, then maker's), through the corrected add_fill statement (5 columns, 5
+// placeholders; the reference's has 6, storage.cpp:190).
 static bool persist(me_service* s, const Slice& sl, const me_order_result* res, const me_fill* tape, int64_t ts,
                     std::string& err) {
   if (!s->db) return true;
+  const size_t n = sl.size();
+  // ---- final state of this slice's rows; changes to earlier slices' rows
+  std::vector<int32_t> fst(n), frem(n);
+  std::unordered_map<uint64_t, long long> ext_fill;       // earlier order -> quantity filled now
+  std::vector<std::pair<uint64_t, int32_t>> ext_cancel;   // earlier order -> quantity the cancel removed
+  auto find = [&](uint64_t q) -> long {  // row of order q in this slice (seqs ascend), or -1
+    auto it = std::lower_bound(sl.seq.begin(), sl.seq.end(), q);
+    if (it == sl.seq.end() || *it != q) return -1;
+    const long j = (long)(it - sl.seq.begin());
+    return sl.meta[j].cancel ? -1 : j;
+  };
+  size_t nfill = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const Pending& m = sl.meta[i];
+    if (m.cancel) {
+      if (res[i].status != ME_ST_CANCELED) continue;
+      const long j = find(m.target);
+      if (j >= 0) {
+        fst[j] = ME_ST_CANCELED;
+        frem[j] = res[i].remaining_qty;
+      } else {
+        ext_cancel.emplace_back(m.target, res[i].remaining_qty);
+      }
+      continue;
+    }
+    fst[i] = res[i].status;
+    frem[i] = res[i].remaining_qty;  // unfilled qty (0 once FILLED)
+    for (uint32_t f = 0; f < res[i].fill_count; ++f) {
+      const me_fill& fl = tape[res[i].tape_offset + f];
+      const long j = find(fl.maker_seq);
+      if (j >= 0) {
+        frem[j] -= fl.qty;
+        fst[j] = frem[j] == 0 ? ME_ST_FILLED : ME_ST_PARTIALLY_FILLED;
+      } else {
+        ext_fill[fl.maker_seq] += fl.qty;
+      }
+    }
+    nfill += res[i].fill_count;
+  }
+  std::vector<std::string> oid(n);
+  for (size_t i = 0; i < n; ++i)
+    if (!sl.meta[i].cancel) oid[i] = "OID-" + std::to_string(sl.seq[i]);
   bool ok = true;
   auto step = [&](sqlite3_stmt* st, const char* what) {
     const int rc = g_sql.step(st);
     g_sql.reset(st);
     if (!sql_ok(rc)) {
       err = s->sql_err(what);
-      return false;
+      ok = false;
     }
-    return true;
+    return ok;
   };
   if (!sql_ok(g_sql.exec(s->db, "BEGIN", nullptr, nullptr, nullptr))) {
     err = s->sql_err("begin");
     return false;
   }
-  for (size_t i = 0; i < sl.size() && ok; ++i) {
-    const Pending& m = sl.meta[i];
-    if (m.cancel) {  // no row of its own: the target's row becomes CANCELED
-      if (res[i].status == ME_ST_CANCELED) {
-        const std::string toid = "OID-" + std::to_string(m.target);
-        sqlite3_stmt* up = s->st_upd;
-        g_sql.bind_int64(up, 1, ME_ST_CANCELED);
-        g_sql.bind_int64(up, 2, res[i].remaining_qty);  // the quantity the cancel removed
-        g_sql.bind_int64(up, 3, ts);
-        g_sql.bind_text(up, 4, toid.c_str(), -1, SQLITE_TRANSIENT);
-        ok = step(up, "cancel order");
-      }
-      continue;
+  // ---- orders rows, kRows per statement
+  {
+    std::vector<size_t> rows;
+    rows.reserve(n);
+    for (size_t i = 0; i < n; ++i)
+      if (!sl.meta[i].cancel) rows.push_back(i);
+    auto bind_row = [&](sqlite3_stmt* st, int b, size_t i) {
+      const Pending& m = sl.meta[i];
+      g_sql.bind_text(st, b + 1, oid[i].c_str(), -1, nullptr);
+      g_sql.bind_text(st, b + 2, m.client.c_str(), -1, nullptr);
+      g_sql.bind_text(st, b + 3, m.symbol.c_str(), -1, nullptr);
+      g_sql.bind_int64(st, b + 4, m.side);
+      g_sql.bind_int64(st, b + 5, 1);  // order_type: the reference binds the constant 1 (storage.cpp:106)
+      g_sql.bind_int64(st, b + 6, sl.px[i]);
+      g_sql.bind_int64(st, b + 7, sl.qty[i]);
+      g_sql.bind_int64(st, b + 8, fst[i]);
+      g_sql.bind_int64(st, b + 9, frem[i]);
+      g_sql.bind_int64(st, b + 10, ts);
+      g_sql.bind_int64(st, b + 11, ts);
+    };
+    size_t k = 0;
+    for (; ok && k + kRows <= rows.size(); k += kRows) {
+      for (int r = 0; r < kRows; ++r) bind_row(s->st_ins_k, 11 * r, rows[k + r]);
+      step(s->st_ins_k, "insert orders");
     }
-    // insert_new_order's row (storage.cpp:102-112) with the matched outcome in the same INSERT:
-    // status and remaining_quantity are what an insert (NEW, quantity) followed by
-    // update_order_status (storage.cpp:160-181) would leave
-    const std::string oid = "OID-" + std::to_string(sl.seq[i]);
-    sqlite3_stmt* st = s->st_ins;
-    g_sql.bind_text(st, 1, oid.c_str(), -1, SQLITE_TRANSIENT);
-    g_sql.bind_text(st, 2, m.client.c_str(), -1, SQLITE_TRANSIENT);
-    g_sql.bind_text(st, 3, m.symbol.c_str(), -1, SQLITE_TRANSIENT);
-    g_sql.bind_int64(st, 4, m.side);
-    g_sql.bind_int64(st, 5, 1);  // order_type: the reference binds the constant 1 (storage.cpp:106)
-    g_sql.bind_int64(st, 6, sl.px[i]);
-    g_sql.bind_int64(st, 7, sl.qty[i]);
-    g_sql.bind_int64(st, 8, res[i].status);
-    g_sql.bind_int64(st, 9, res[i].remaining_qty);  // unfilled qty (0 once FILLED)
-    g_sql.bind_int64(st, 10, ts);
-    g_sql.bind_int64(st, 11, ts);
-    ok = step(st, "insert order");
-    // makers hit by this taker (earlier rows, possibly in this same transaction)
-    for (uint32_t f = 0; ok && f < res[i].fill_count; ++f) {
-      const me_fill& fl = tape[res[i].tape_offset + f];
-      const std::string moid = "OID-" + std::to_string(fl.maker_seq);
-      sqlite3_stmt* mk = s->st_maker;
-      g_sql.bind_int64(mk, 1, fl.qty);
-      g_sql.bind_int64(mk, 2, fl.qty);
-      g_sql.bind_int64(mk, 3, ts);
-      g_sql.bind_text(mk, 4, moid.c_str(), -1, SQLITE_TRANSIENT);
-      ok = step(mk, "update maker");
-      for (int side = 0; ok && side < 2; ++side) {  // one FillRow per order of the trade
-        sqlite3_stmt* fs = s->st_fill;
-        g_sql.bind_text(fs, 1, side ? moid.c_str() : oid.c_str(), -1, SQLITE_TRANSIENT);
-        g_sql.bind_text(fs, 2, m.symbol.c_str(), -1, SQLITE_TRANSIENT);
-        g_sql.bind_int64(fs, 3, fl.price_q4);
-        g_sql.bind_int64(fs, 4, fl.qty);
-        g_sql.bind_int64(fs, 5, ts);
-        ok = step(fs, "insert fill");
+    for (; ok && k < rows.size(); ++k) {
+      bind_row(s->st_ins, 0, rows[k]);
+      step(s->st_ins, "insert order");
+    }
+  }
+  // ---- earlier slices' rows: fills first (an order is filled before it can be canceled), then cancels
+  for (auto it = ext_fill.begin(); ok && it != ext_fill.end(); ++it) {
+    const std::string moid = "OID-" + std::to_string(it->first);
+    g_sql.bind_int64(s->st_maker, 1, it->second);
+    g_sql.bind_int64(s->st_maker, 2, it->second);
+    g_sql.bind_int64(s->st_maker, 3, ts);
+    g_sql.bind_text(s->st_maker, 4, moid.c_str(), -1, SQLITE_TRANSIENT);
+    step(s->st_maker, "update maker");
+  }
+  for (size_t k = 0; ok && k < ext_cancel.size(); ++k) {
+    const std::string toid = "OID-" + std::to_string(ext_cancel[k].first);
+    g_sql.bind_int64(s->st_upd, 1, ME_ST_CANCELED);
+    g_sql.bind_int64(s->st_upd, 2, ext_cancel[k].second);  // the quantity the cancel removed
+    g_sql.bind_int64(s->st_upd, 3, ts);
+    g_sql.bind_text(s->st_upd, 4, toid.c_str(), -1, SQLITE_TRANSIENT);
+    step(s->st_upd, "cancel order");
+  }
+  // ---- fills rows: one FillRow per order of each trade, kRows per statement
+  if (ok && nfill) {
+    std::vector<std::string> moid(nfill);
+    std::vector<std::pair<size_t, size_t>> fr;  // (taker row, fill index in the slice's fills)
+    fr.reserve(nfill);
+    size_t q = 0;
+    for (size_t i = 0; i < n; ++i) {
+      if (sl.meta[i].cancel) continue;
+      for (uint32_t f = 0; f < res[i].fill_count; ++f, ++q) {
+        moid[q] = "OID-" + std::to_string(tape[res[i].tape_offset + f].maker_seq);
+        fr.emplace_back(i, res[i].tape_offset + f);
       }
+    }
+    auto bind_fill = [&](sqlite3_stmt* st, int b, size_t r) {  // row r: fill r / 2, taker (even) or maker
+      const size_t i = fr[r / 2].first;
+      const me_fill& fl = tape[fr[r / 2].second];
+      const char* who = (r & 1) ? moid[r / 2].c_str() : oid[i].c_str();
+      g_sql.bind_text(st, b + 1, who, -1, nullptr);
+      g_sql.bind_text(st, b + 2, sl.meta[i].symbol.c_str(), -1, nullptr);
+      g_sql.bind_int64(st, b + 3, fl.price_q4);
+      g_sql.bind_int64(st, b + 4, fl.qty);
+      g_sql.bind_int64(st, b + 5, ts);
+    };
+    const size_t nrows = 2 * nfill;
+    size_t r = 0;
+    for (; ok && r + kRows <= nrows; r += kRows) {
+      for (int k = 0; k < kRows; ++k) bind_fill(s->st_fill_k, 5 * k, r + k);
+      step(s->st_fill_k, "insert fills");
+    }
+    for (; ok && r < nrows; ++r) {
+      bind_fill(s->st_fill, 0, r);
+      step(s->st_fill, "insert fill");
     }
   }
   if (!ok) {
