@@ -149,8 +149,10 @@ static_assert(sizeof(SlotMeta) == 16, "SlotMeta");
 struct HostSlot {
   char* h_in = nullptr;   // pinned staging: the batch packed as seq[n] px[n] qty[n] sym[n] kind[n]
   char* d_in = nullptr;   // its HBM copy
-  char* h_out = nullptr;  // pinned outputs (SlotMeta | tape | results)
-  char* d_out = nullptr;  // HBM outputs the tape job writes
+  char* h_out = nullptr;  // pinned outputs (SlotMeta | tape | results): the tape job writes the meta and
+                          // the tape straight into it over PCIe; the results arrive by DMA
+  char* h_out_dev = nullptr;  // h_out as the device addresses it
+  char* d_out = nullptr;  // HBM: the results the tape job finalises (DMA source, spill input)
   hipEvent_t ev_in = nullptr;    // H2D done (H2D stream)
   hipEvent_t ev_done = nullptr;  // outputs in pinned memory (D2H stream)
   uint64_t ticket = 0;
@@ -694,14 +696,15 @@ static void slot_soa(char* p, uint64_t n, uint64_t*& seq, int64_t*& px, int32_t*
   sym = (uint32_t*)(p + 20 * n);
   kind = (uint8_t*)(p + 24 * n);
 }
-// Where the tape job of a host batch writes (the slot's HBM output block).
+// Where the tape job of a host batch writes: meta and tape into the slot's pinned block (device
+// view), the finalised results into HBM.
 static void slot_outputs(me_engine* e, HostSlot& h, me_fill*& tape, unsigned long long*& count,
                          me_order_result*& res, uint32_t*& err) {
-  SlotMeta* m = (SlotMeta*)h.d_out;
+  SlotMeta* m = (SlotMeta*)h.h_out_dev;
   count = &m->count;
   err = &m->err;
-  tape = (me_fill*)(h.d_out + sizeof(SlotMeta));
-  res = (me_order_result*)(h.d_out + slot_res_off(e));
+  tape = (me_fill*)(h.h_out_dev + sizeof(SlotMeta));
+  res = (me_order_result*)h.d_out;
 }
 static int slot_alloc(me_engine* e, HostSlot& h) {
   if (h.h_in) return ME_OK;
@@ -709,26 +712,21 @@ static int slot_alloc(me_engine* e, HostSlot& h) {
   HIP_TRY(hipHostMalloc((void**)&h.h_in, in, hipHostMallocDefault), "hipHostMalloc slot inputs");
   HIP_TRY(hipHostMalloc((void**)&h.h_out, out, hipHostMallocDefault), "hipHostMalloc slot outputs");
   HIP_TRY(hipMalloc((void**)&h.d_in, in), "hipMalloc slot inputs");
-  HIP_TRY(hipMalloc((void**)&h.d_out, out), "hipMalloc slot outputs");
+  HIP_TRY(hipMalloc((void**)&h.d_out, (size_t)e->cfg.max_batch * sizeof(me_order_result)), "hipMalloc slot results");
+  HIP_TRY(hipHostGetDevicePointer((void**)&h.h_out_dev, h.h_out, 0), "hipHostGetDevicePointer");
   HIP_TRY(hipEventCreateWithFlags(&h.ev_in, hipEventDisableTiming), "hipEventCreate");
   HIP_TRY(hipEventCreateWithFlags(&h.ev_done, hipEventDisableTiming), "hipEventCreate");
   return ME_OK;
 }
-// After the launch that wrote the tapes of host slots[0..ns): the D2H stream waits for it and copies
-// each slot's meta + tape head + results into pinned memory. Nothing later on the engine stream
-// writes those HBM blocks before the slot is collected and reused.
+// After the launch whose tape jobs finished host slots[0..ns) (their meta and tapes are in pinned
+// memory once it completes): the D2H stream waits for it and copies each slot's results into pinned
+// memory. Nothing later on the engine stream writes those blocks before the slot is collected.
 static int enqueue_host_d2h(me_engine* e, const int* slots, int ns) {
   HIP_TRY(hipEventRecord(e->ev_tape, e->stream), "hipEventRecord");
   HIP_TRY(hipStreamWaitEvent(e->s_d2h, e->ev_tape, 0), "hipStreamWaitEvent");
   for (int k = 0; k < ns; ++k) {
     HostSlot& h = e->hs[slots[k]];
-    // the tape head copied with the results: room for 1.5 fills per record (the rest, when there is
-    // more, is read at me_collect)
-    const uint64_t head = std::min<uint64_t>(e->hcap, (uint64_t)h.n + h.n / 2 + 1024);
-    HIP_TRY(hipMemcpyAsync(h.h_out, h.d_out, sizeof(SlotMeta) + head * sizeof(me_fill), hipMemcpyDeviceToHost,
-                           e->s_d2h),
-            "D2H slot tape");
-    HIP_TRY(hipMemcpyAsync(h.h_out + slot_res_off(e), h.d_out + slot_res_off(e), (size_t)h.n * sizeof(me_order_result),
+    HIP_TRY(hipMemcpyAsync(h.h_out + slot_res_off(e), h.d_out, (size_t)h.n * sizeof(me_order_result),
                            hipMemcpyDeviceToHost, e->s_d2h),
             "D2H slot results");
     HIP_TRY(hipEventRecord(h.ev_done, e->s_d2h), "hipEventRecord");
@@ -1159,37 +1157,30 @@ extern "C" int me_collect(me_engine* e, uint64_t ticket, const me_fill** fills, 
   }
   const uint64_t cnt = m->count;
   me_fill* tape = (me_fill*)(h.h_out + sizeof(SlotMeta));
-  const uint64_t head = std::min<uint64_t>(e->hcap, (uint64_t)h.n + h.n / 2 + 1024);
-  if (cnt > head) {  // the rest of the slot's tape, and past its cap the spill from scratch
-    const uint64_t in_slot = std::min<uint64_t>(cnt, e->hcap);
-    HIP_TRY(hipMemcpy(tape + head, h.d_out + sizeof(SlotMeta) + head * sizeof(me_fill),
-                      (in_slot - head) * sizeof(me_fill), hipMemcpyDeviceToHost),
-            "D2H slot tape tail");
-    if (cnt > e->hcap) {
-      if (e->oset_gen[h.oset] != h.oset_gen) {  // this batch's output is lost; the books are intact (not sticky)
-        e->err = "host batch tape (" + std::to_string(cnt) + " fills) outgrew host_tape_cap and its scratch was "
-                 "reused before me_collect: raise host_tape_cap or collect within 3 launch groups";
-        return ME_E_CAPACITY;
-      }
-      const size_t extra = (size_t)(cnt - e->hcap);
-      if (extra > e->spill_cap) {
-        if (e->d_spill) HIP_TRY(hipFree(e->d_spill), "hipFree");
-        e->d_spill = nullptr;
-        e->spill_cap = 0;
-        HIP_TRY(hipMalloc((void**)&e->d_spill, extra * sizeof(me_fill)), "hipMalloc spill");
-        e->spill_cap = extra;
-      }
-      const auto& o = e->os[h.oset];
-      const me_order_result* dres = (const me_order_result*)(h.d_out + slot_res_off(e));
-      hipError_t he = launch_tape_spill(e->stream, dres, o.fstart, h.n, o.scratch, e->hcap, e->d_spill);
-      if (he != hipSuccess) return e->hip_fail(he, "spill launch");
-      HIP_TRY(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
-      h.big.resize(cnt);
-      memcpy(h.big.data(), tape, e->hcap * sizeof(me_fill));
-      HIP_TRY(hipMemcpy(h.big.data() + e->hcap, e->d_spill, extra * sizeof(me_fill), hipMemcpyDeviceToHost),
-              "D2H spill");
-      tape = h.big.data();
+  if (cnt > e->hcap) {  // past the slot: the spill from scratch
+    if (e->oset_gen[h.oset] != h.oset_gen) {  // this batch's output is lost; the books are intact (not sticky)
+      e->err = "host batch tape (" + std::to_string(cnt) + " fills) outgrew host_tape_cap and its scratch was "
+               "reused before me_collect: raise host_tape_cap or collect within 3 launch groups";
+      return ME_E_CAPACITY;
     }
+    const size_t extra = (size_t)(cnt - e->hcap);
+    if (extra > e->spill_cap) {
+      if (e->d_spill) HIP_TRY(hipFree(e->d_spill), "hipFree");
+      e->d_spill = nullptr;
+      e->spill_cap = 0;
+      HIP_TRY(hipMalloc((void**)&e->d_spill, extra * sizeof(me_fill)), "hipMalloc spill");
+      e->spill_cap = extra;
+    }
+    const auto& o = e->os[h.oset];
+    hipError_t he = launch_tape_spill(e->stream, (const me_order_result*)h.d_out, o.fstart, h.n, o.scratch, e->hcap,
+                                      e->d_spill);
+    if (he != hipSuccess) return e->hip_fail(he, "spill launch");
+    HIP_TRY(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
+    h.big.resize(cnt);
+    memcpy(h.big.data(), tape, e->hcap * sizeof(me_fill));
+    HIP_TRY(hipMemcpy(h.big.data() + e->hcap, e->d_spill, extra * sizeof(me_fill), hipMemcpyDeviceToHost),
+            "D2H spill");
+    tape = h.big.data();
   }
   if (fills) *fills = tape;
   if (n_fills) *n_fills = (size_t)cnt;

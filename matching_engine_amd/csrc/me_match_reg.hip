@@ -1013,14 +1013,25 @@ __device__ __forceinline__ void aux_tape_tile(const ColdArgs& G, uint32_t jb, ui
     if (lane == 0) atomicOr(ldsg(G.bk.err), ERR_SCRATCH_OOM);
     return;
   }
-  // each lane copies the fills of its own records (scratch runs are contiguous per record)
-  uint32_t o2 = (uint32_t)(incl - loc);
+  // The tile's fills are one contiguous tape run [base, base + total): lane i copies fill f0 + i, found
+  // by a binary search over the lanes' exclusive offsets (one record per lane), so every store
+  // instruction writes 64 consecutive 32-B records — whole lines in HBM, full-size PCIe writes when
+  // the tape is a host slot's pinned buffer.
+  static_assert(TILE_TAPE == 64, "one record per lane");
+  {
+    const uint32_t ex = (uint32_t)(incl - loc);
+    for (uint32_t f0 = 0; f0 < total; f0 += 64) {
+      const uint32_t f = f0 + (uint32_t)lane;
+      int lo = 0;  // last lane whose exclusive offset is <= f: the record that owns fill f
 #pragma unroll
-  for (int k = 0; k < TILE_TAPE / 64; ++k) {
-    if (c[k])
-      for (uint32_t q = 0; q < c[k]; ++q)
-        if (base + o2 + q < cap) tape[base + o2 + q] = scratch[src[k] + q];
-    o2 += c[k];
+      for (int step = 32; step >= 1; step >>= 1) {
+        const uint32_t e = (uint32_t)__shfl((int)ex, min(lo + step, 63), 64);
+        if (lo + step < 64 && e <= f) lo += step;
+      }
+      const uint32_t s0 = (uint32_t)__shfl((int)src[0], lo, 64);
+      const uint32_t e0 = (uint32_t)__shfl((int)ex, lo, 64);
+      if (f < total && base + f < cap) tape[base + f] = scratch[s0 + (f - e0)];
+    }
   }
   if (t == ntiles - 1 && lane == 0) {
     *ldsg(J.tape_count) = base + total;
