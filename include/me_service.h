@@ -67,6 +67,28 @@ me_service* me_service_create(me_engine* engine, const char* const* symbols, uin
                               const char* db_path);
 void me_service_destroy(me_service* s);
 
+/* A sharded deployment's matcher (matching_engine_amd/cluster.py): symbols live on
+ * several engines (one per GPU, splitmix64(symbol) % G); the service on the persistence root hands
+ * it each slice and gets back the merged outputs, exactly what one engine holding every symbol
+ * would produce (me_collect's shapes: tape ordered by taker seq, results in slice order). */
+typedef struct me_matcher {
+  void* ctx;
+  uint32_t num_symbols;  /* symbol ids it takes (the service interns up to this many) */
+  uint32_t max_batch;    /* largest slice */
+  uint64_t max_resting;  /* resting orders it holds at most (me_fill_bound's bound: max_resting + 2n) */
+  /* Match one slice; outputs valid until the next call. Nonzero: the slice is lost (service fails). */
+  int (*match)(void* ctx, const me_order_soa* slice, size_t n, const me_fill** fills, size_t* n_fills,
+               const me_order_result** results);
+  /* me_book_orders' contract for one symbol (depth 0: the whole book). */
+  int (*book)(void* ctx, uint32_t symbol, uint32_t depth, me_book_entry* bids, size_t bids_cap, size_t* n_bids,
+              me_book_entry* asks, size_t asks_cap, size_t* n_asks, me_level* bid_levels, me_level* ask_levels,
+              size_t* n_bid_levels, size_t* n_ask_levels);
+} me_matcher;
+
+/* The service over a matcher instead of an engine (same contract otherwise). NULL on a bad matcher. */
+me_service* me_service_create_matcher(const me_matcher* m, const char* const* symbols, uint32_t num_symbols,
+                                      const char* db_path);
+
 /* Always returns 0 (the RPC itself succeeded or failed in-band, like the reference). */
 int me_service_submit_order(me_service* s, const me_order_request* req, me_order_response* resp);
 

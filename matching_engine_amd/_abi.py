@@ -262,7 +262,26 @@ class MeBookOrder(C.Structure):
 
 assert C.sizeof(MeBookOrder) == 120, "me_book_order layout"
 
+MATCH_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(MeOrderSoa), C.c_size_t, C.POINTER(C.c_void_p),
+                       C.POINTER(C.c_size_t), C.POINTER(C.c_void_p))
+BOOK_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t),
+                      C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t), C.c_void_p, C.c_void_p, C.POINTER(C.c_size_t),
+                      C.POINTER(C.c_size_t))
+
+
+class MeMatcher(C.Structure):
+    _fields_ = [
+        ("ctx", C.c_void_p),
+        ("num_symbols", C.c_uint32),
+        ("max_batch", C.c_uint32),
+        ("max_resting", C.c_uint64),
+        ("match", MATCH_FN),
+        ("book", BOOK_FN),
+    ]
+
+
 PROTOTYPES.update({
+    "me_service_create_matcher": (_P, [C.POINTER(MeMatcher), C.POINTER(C.c_char_p), C.c_uint32, C.c_char_p]),
     "me_service_order_book": (C.c_int, [_P, C.c_char_p, C.c_uint32, C.POINTER(MeBookOrder), _SZ, C.POINTER(_SZ),
                                         C.POINTER(MeBookOrder), _SZ, C.POINTER(_SZ)]),
     "me_service_cancel_order": (C.c_int, [_P, C.POINTER(MeCancelRequest), C.POINTER(MeOrderResponse)]),

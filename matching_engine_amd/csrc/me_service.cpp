@@ -164,6 +164,7 @@ constexpr int kRows = 64;  // rows per multi-row INSERT (11 * 64 parameters < SQ
 
 struct me_service {
   me_engine* eng = nullptr;
+  me_matcher m{};           // the matcher when the service fronts shards it does not own (m.match set)
   uint32_t sym_cap = UINT32_MAX;  // symbols the engine holds (local ids 0 .. sym_cap-1)
   size_t slice_max = 0;           // records per slice (the engine's max_batch)
   // --- mu
@@ -280,8 +281,8 @@ static bool open_db(me_service* s, const char* path, std::string& err) {
          chk(g_sql.prepare_v2(s->db, fill_k.c_str(), -1, &s->st_fill_k, nullptr), "prepare fill rows");
 }
 
-extern "C" me_service* me_service_create(me_engine* engine, const char* const* symbols, uint32_t num_symbols,
-                                         const char* db_path) {
+static me_service* create(me_engine* engine, const me_matcher* m, const char* const* symbols, uint32_t num_symbols,
+                          const char* db_path) {
   me_service* s = new me_service();
   s->eng = engine;
   if (engine) {
@@ -291,6 +292,10 @@ extern "C" me_service* me_service_create(me_engine* engine, const char* const* s
       s->slice_max = c.max_batch;
     }
     me_host_reserve(engine, 1);  // the flusher reuses one warm pinned slot
+  } else if (m) {
+    s->m = *m;
+    s->sym_cap = m->num_symbols;
+    s->slice_max = m->max_batch;
   }
   for (uint32_t i = 0; i < num_symbols; ++i) {
     s->names.emplace_back(symbols[i]);
@@ -304,6 +309,57 @@ extern "C" me_service* me_service_create(me_engine* engine, const char* const* s
     s->fail(ME_E_SQLITE, "me_service_create: " + err);
   }
   return s;
+}
+
+extern "C" me_service* me_service_create(me_engine* engine, const char* const* symbols, uint32_t num_symbols,
+                                         const char* db_path) {
+  return create(engine, nullptr, symbols, num_symbols, db_path);
+}
+
+extern "C" me_service* me_service_create_matcher(const me_matcher* m, const char* const* symbols,
+                                                 uint32_t num_symbols, const char* db_path) {
+  if (!m || !m->match || !m->book || !m->max_batch) return nullptr;
+  return create(nullptr, m, symbols, num_symbols, db_path);
+}
+
+// The backend behind the service: its own engine, or the matcher of a sharded deployment.
+static bool has_backend(const me_service* s) { return s->eng || s->m.match; }
+
+static std::string backend_err(me_service* s) {
+  if (!s->eng) return "matcher failed";
+  char e[512];
+  me_last_error(s->eng, e, sizeof e);
+  return e;
+}
+
+// Match one slice (eng_mu held). accepted = the backend took it (a failure after that loses it).
+static int backend_match(me_service* s, const me_order_soa& b, size_t n, const me_fill** tape, size_t* nf,
+                         const me_order_result** res, bool& accepted) {
+  if (s->eng) {
+    uint64_t t = 0;
+    accepted = false;
+    int rc = me_submit_host(s->eng, &b, n, &t);
+    if (rc != ME_OK) return rc;
+    accepted = true;
+    size_t nr = 0;
+    return me_collect(s->eng, t, tape, nf, res, &nr);
+  }
+  accepted = true;
+  return s->m.match(s->m.ctx, &b, n, tape, nf, res);
+}
+
+static int backend_book(me_service* s, uint32_t sid, uint32_t depth, me_book_entry* bids, size_t bids_cap,
+                        size_t* n_bids, me_book_entry* asks, size_t asks_cap, size_t* n_asks, me_level* bl,
+                        me_level* al, size_t* nbl, size_t* nal) {
+  if (s->eng) {
+    if (!depth) {  // the whole book: every window level plus the far arrays
+      me_config c{};
+      me_get_config(s->eng, &c);
+      depth = c.levels + c.far_levels;
+    }
+    return me_book_orders(s->eng, sid, depth, bids, bids_cap, n_bids, asks, asks_cap, n_asks, bl, al, nbl, nal);
+  }
+  return s->m.book(s->m.ctx, sid, depth, bids, bids_cap, n_bids, asks, asks_cap, n_asks, bl, al, nbl, nal);
 }
 
 static void put(char* dst, size_t cap, const std::string& v) {
@@ -767,26 +823,23 @@ static int process(me_service* s, Slice&& sl, FlushOut* out) {
   {
     std::lock_guard<std::mutex> le(s->eng_mu);
     me_order_soa b{sl.seq.data(), sl.px.data(), sl.qty.data(), sl.sid.data(), sl.kind.data()};
-    uint64_t t = 0;
-    int rc = me_submit_host(s->eng, &b, n, &t);
-    if (rc != ME_OK) {  // not accepted: the slice goes back to the head of the queue
-      char e[512];
-      me_last_error(s->eng, e, sizeof e);
+    bool accepted = false;
+    const int rc = backend_match(s, b, n, &tape, &nf, &res, accepted);
+    nr = n;
+    if (rc != ME_OK && !accepted) {  // not accepted: the slice goes back to the head of the queue
+      const std::string e = backend_err(s);
       std::lock_guard<std::mutex> lk(s->mu);
       s->closed_records += n;
       s->closed.push_front(std::move(sl));
-      return s->fail(rc, std::string("engine: ") + e);
+      return s->fail(rc, "engine: " + e);
     }
-    rc = me_collect(s->eng, t, &tape, &nf, &res, &nr);
     if (rc != ME_OK) {  // accepted and lost: the books may hold the slice, the service cannot go on
-      char e[512];
-      me_last_error(s->eng, e, sizeof e);
       s->failed = true;
-      return s->fail(rc, std::string("engine lost an accepted slice: ") + e);
+      return s->fail(rc, "engine lost an accepted slice: " + backend_err(s));
     }
   }
-  // the slot's pinned outputs stay valid until the next me_submit_host, which only a later
-  // process() (this thread, flush_mu) can issue
+  // the outputs stay valid until the next match, which only a later process() (this thread,
+  // flush_mu) can issue
   int rc = ME_OK;
   std::string err;
   const int64_t ts = now_ms();
@@ -833,7 +886,7 @@ static int process(me_service* s, Slice&& sl, FlushOut* out) {
 // slices are taken (those present when the caller checked its output capacity).
 static int flush_closed(me_service* s, bool take_open, size_t limit, FlushOut* out) {
   if (s->failed) return s->fail(ME_E_STATE, "service failed: the engine lost an accepted slice");
-  if (!s->eng) {
+  if (!has_backend(s)) {
     std::lock_guard<std::mutex> lk(s->mu);
     if (s->open.size() || !s->closed.empty())
       return s->fail(ME_E_STATE, "me_service_flush: no engine (HIP device required)");
@@ -879,7 +932,8 @@ extern "C" int me_service_flush(me_service* s, me_fill* out_fills, size_t fills_
   // the caller's buffers are checked before anything is matched
   if ((out_results || out_seq) && total > results_cap)
     return s->fail(ME_E_INVALID, "results_cap smaller than the pending records");
-  if (out_fills && s->eng && fills_cap < me_fill_bound(s->eng, total))
+  const uint64_t bound = s->eng ? me_fill_bound(s->eng, total) : s->m.max_resting + 2 * (uint64_t)total;
+  if (out_fills && has_backend(s) && fills_cap < bound)
     return s->fail(ME_E_INVALID, "fills_cap smaller than me_fill_bound(pending records)");
   FlushOut out{out_fills, fills_cap, 0, out_results, out_seq, 0};
   const int rc = flush_closed(s, true, nslices, &out);
@@ -912,12 +966,16 @@ static void flusher_main(me_service* s) {
 }
 
 extern "C" int me_service_start(me_service* s, uint32_t interval_us, uint32_t slice_orders) {
-  if (!s || !s->eng) return ME_E_STATE;
+  if (!s || !has_backend(s)) return ME_E_STATE;
   std::lock_guard<std::mutex> lk(s->mu);
   if (s->flusher.joinable()) return s->fail(ME_E_STATE, "flusher already running");
-  me_config c{};
-  me_get_config(s->eng, &c);
-  s->slice_max = slice_orders && slice_orders < c.max_batch ? slice_orders : c.max_batch;
+  uint32_t mb = s->m.max_batch;
+  if (s->eng) {
+    me_config c{};
+    me_get_config(s->eng, &c);
+    mb = c.max_batch;
+  }
+  s->slice_max = slice_orders && slice_orders < mb ? slice_orders : mb;
   s->interval_us = interval_us ? interval_us : 1000;
   s->stop = false;
   s->flusher = std::thread(flusher_main, s);
@@ -953,14 +1011,11 @@ extern "C" int me_service_book(me_service* s, const char* symbol, me_level* bids
     if (it == s->sym.end()) return ME_OK;  // unknown symbol: empty book (the reference's stub is always empty)
     sid = it->second;
   }
-  if (!s->eng) return s->fail(ME_E_STATE, "no engine");
+  if (!has_backend(s)) return s->fail(ME_E_STATE, "no engine");
   std::lock_guard<std::mutex> le(s->eng_mu);
-  const int rc = me_book_snapshot(s->eng, sid, bids, asks, depth, n_bids, n_asks);
-  if (rc != ME_OK) {
-    char e[512];
-    me_last_error(s->eng, e, sizeof e);
-    return s->fail(rc, std::string("engine: ") + e);
-  }
+  const int rc = backend_book(s, sid, (uint32_t)std::min<size_t>(depth, 0xFFFFFFFFu), nullptr, 0, nullptr, nullptr,
+                              0, nullptr, bids, asks, n_bids, n_asks);
+  if (rc != ME_OK) return s->fail(rc, "engine: " + backend_err(s));
   return ME_OK;
 }
 
@@ -976,24 +1031,17 @@ extern "C" int me_service_order_book(me_service* s, const char* symbol, uint32_t
     if (it == s->sym.end()) return ME_OK;
     sid = it->second;
   }
-  if (!s->eng) return s->fail(ME_E_STATE, "no engine");
+  if (!has_backend(s)) return s->fail(ME_E_STATE, "no engine");
   std::vector<me_book_entry> side[2];
   size_t n[2] = {0, 0};
   {
     std::lock_guard<std::mutex> le(s->eng_mu);
-    me_config c{};
-    me_get_config(s->eng, &c);
-    const uint32_t d = depth ? depth : c.levels + c.far_levels;
     side[0].resize(std::max<size_t>(bids_cap, 1));
     side[1].resize(std::max<size_t>(asks_cap, 1));
-    const int rc = me_book_orders(s->eng, sid, d, bids ? side[0].data() : nullptr, bids ? side[0].size() : 0, &n[0],
-                                  asks ? side[1].data() : nullptr, asks ? side[1].size() : 0, &n[1], nullptr, nullptr,
-                                  nullptr, nullptr);
-    if (rc != ME_OK) {
-      char e[512];
-      me_last_error(s->eng, e, sizeof e);
-      return s->fail(rc, std::string("engine: ") + e);
-    }
+    const int rc = backend_book(s, sid, depth, bids ? side[0].data() : nullptr, bids ? side[0].size() : 0, &n[0],
+                                asks ? side[1].data() : nullptr, asks ? side[1].size() : 0, &n[1], nullptr, nullptr,
+                                nullptr, nullptr);
+    if (rc != ME_OK) return s->fail(rc, "engine: " + backend_err(s));
   }
   me_book_order* out[2] = {bids, asks};
   const size_t caps[2] = {bids_cap, asks_cap};

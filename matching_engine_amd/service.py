@@ -18,14 +18,24 @@ class ServiceError(RuntimeError):
 class MatchingEngineService:
     """SubmitOrder / GetOrderBook over one engine shard; SQLite persistence when db_path is given."""
 
-    def __init__(self, engine, symbols, db_path=None):
+    def __init__(self, engine, symbols, db_path=None, matcher=None):
+        """engine: the Engine the slices match on; or matcher: a cluster.ShardedMatcher (rank 0 of a
+        sharded deployment, me_service_create_matcher)."""
         self.lib = _abi.load()
         self.engine = engine
+        self.matcher = matcher
         self.symbols = list(symbols)
-        arr = (C.c_char_p * len(self.symbols))(*[s.encode() for s in self.symbols])
+        arr = (C.c_char_p * max(len(self.symbols), 1))(*[s.encode() for s in self.symbols])
         self._arr = arr
-        self.h = self.lib.me_service_create(engine.h if engine is not None else None, arr, len(self.symbols),
-                                            db_path.encode() if db_path else None)
+        if matcher is not None:
+            self._cm = matcher.c_matcher()
+            self.h = self.lib.me_service_create_matcher(C.byref(self._cm), arr, len(self.symbols),
+                                                        db_path.encode() if db_path else None)
+            if not self.h:
+                raise ServiceError("me_service_create_matcher refused the matcher")
+        else:
+            self.h = self.lib.me_service_create(engine.h if engine is not None else None, arr, len(self.symbols),
+                                                db_path.encode() if db_path else None)
         err = self.last_error()
         if db_path and err:
             raise ServiceError(err)
@@ -112,7 +122,10 @@ class MatchingEngineService:
         n = self.pending
         res = np.zeros(max(n, 1), dtype=RESULT_DTYPE)
         seq = np.zeros(max(n, 1), dtype=np.uint64)
-        cap = (self.engine.fill_bound(n) if self.engine is not None else 0) + 1
+        if self.engine is not None:
+            cap = self.engine.fill_bound(n) + 1
+        else:
+            cap = (self.matcher.max_resting + 2 * n + 1) if self.matcher is not None else 1
         fills = np.zeros(cap, dtype=FILL_DTYPE)
         nf, nr = C.c_size_t(0), C.c_size_t(0)
         rc = self.lib.me_service_flush(self.h, ptr(fills), cap, C.byref(nf), ptr(res), ptr(seq), len(res),

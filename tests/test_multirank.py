@@ -20,15 +20,16 @@ def _free_port():
     return p
 
 
-def _run(kind, world, tmp_path):
+def _run(kind, world, tmp_path, script="multirank_worker.py"):
     out = str(tmp_path / f"mr_{kind}.json")
     port = _free_port()
     procs = []
+    args = [kind, str(tmp_path), out] if script == "cluster_worker.py" else [kind, out]
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         # child processes (never exec over a GPU-initialised interpreter)
-        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "multirank_worker.py"), kind, out],
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, script)] + args,
                                       env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
     logs = []
     for p in procs:
@@ -69,3 +70,18 @@ def test_two_rank_tape_gather_gpu_engines(built, tmp_path):
     assert r["ok"], r["msg"]
     assert r["fills"] > 0
 
+
+def test_two_rank_sharded_service_db_equals_single_engine(built, tmp_path):
+    """SubmitOrder on rank 0 over two shards (cluster.ShardedMatcher, gloo): every
+    slice's merged tape/results, the SQLite rows, the per-order books, market data and the gathered
+    level snapshot equal a single book holding every symbol."""
+    r = _run("oracle", 2, tmp_path, script="cluster_worker.py")
+    assert r["ok"], r["msg"]
+    assert r["orders"] > 5000 and r["fill_rows"] > 1000
+
+
+@pytest.mark.gpu
+def test_two_rank_sharded_service_gpu_engines(built, tmp_path):
+    r = _run("gpu", 2, tmp_path, script="cluster_worker.py")
+    assert r["ok"], r["msg"]
+    assert r["orders"] > 5000 and r["fill_rows"] > 1000
