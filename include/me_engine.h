@@ -242,7 +242,7 @@ int me_book_orders(me_engine* e, uint32_t symbol, uint32_t depth, me_book_entry*
                    me_level* ask_levels, size_t* n_bid_levels, size_t* n_ask_levels);
 /* The top `depth` levels per side of EVERY symbol of the shard in one launch — the periodic book
  * snapshot a multi-GPU deployment gathers to its persistence root: levels[(s * 2 + side) * depth + k]
- * (side 0 bids, 1 asks; best first), counts[s * 2 + side] = levels written. */
+ * (side 0 bids, 1 asks; best first; zeros past the side's levels), counts[s * 2 + side] = levels written. */
 int me_book_levels_all(me_engine* e, uint32_t depth, me_level* levels, uint32_t* counts);
 /* Full resting state of one symbol (side, price, FIFO). *n receives the count even when cap is short. */
 int me_book_dump(me_engine* e, uint32_t symbol, me_book_entry* out, size_t cap, size_t* n);

@@ -1391,10 +1391,15 @@ extern "C" int me_book_levels_all(me_engine* e, uint32_t depth, me_level* levels
   for (uint32_t k = 0; k < e->bk.S; ++k) syms[k] = k;
   if ((rc = run_snapshot(e, syms.data(), e->bk.S, depth, 0))) return rc;
   auto& sb = e->snap;
-  if (counts) HIP_TRY(hipMemcpy(counts, sb.nlv, 2ull * e->bk.S * 4, hipMemcpyDeviceToHost), "D2H snapshot counts");
-  if (levels)
+  std::vector<uint32_t> cnt(2ull * e->bk.S);
+  HIP_TRY(hipMemcpy(cnt.data(), sb.nlv, cnt.size() * 4, hipMemcpyDeviceToHost), "D2H snapshot counts");
+  if (counts) memcpy(counts, cnt.data(), cnt.size() * 4);
+  if (levels) {
     HIP_TRY(hipMemcpy(levels, sb.lv, 2ull * e->bk.S * depth * sizeof(me_level), hipMemcpyDeviceToHost),
             "D2H snapshot levels");
+    for (size_t r = 0; r < cnt.size(); ++r)  // rows end in zeros past their levels
+      memset(levels + r * depth + cnt[r], 0, (depth - cnt[r]) * sizeof(me_level));
+  }
   return ME_OK;
 }
 
