@@ -89,7 +89,7 @@ def parse():
                     help="N>1: batches run after the timed loop with the RCCL tape/result gather to rank 0 "
                          "(reported beside value, never in it)")
     ap.add_argument("--traffic-from", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
-                    help="JSON {bytes_per_launch: ...} from tools/pmc_traffic.py for roofline.traffic")
+                    help="JSON {bytes_per_order: ...} from tools/gpu_pmc_traffic.sh for roofline.traffic (c2)")
     args = ap.parse_args()
     w = WORKLOADS[args.workload]
     if args.symbols_per_gpu is None:
@@ -424,9 +424,14 @@ def main():
     bytes_per_order = (BYTES_PER_ORDER * orders_local + BYTES_PER_FILL * tm["fills"]) / max(orders_local, 1)
     bytes_per_launch = bytes_per_order * tm["orders"] / timed
     achieved = bytes_per_launch / avg_match_s / 1e9
-    traffic = None
-    if args.traffic_from and os.path.exists(args.traffic_from):
-        traffic = json.load(open(args.traffic_from)).get("bytes_per_launch")
+    # roofline.traffic: PMC bytes per order of a steady full-group launch (tools/gpu_pmc_traffic.sh ->
+    # profiles/pmc_traffic.json, same workload) scaled to the orders of THIS run's timed launches, so
+    # it and algorithmic_bytes_per_launch describe the same launch shape
+    traffic = traffic_per_order = None
+    if args.traffic_from and os.path.exists(args.traffic_from) and args.workload == "c2":
+        traffic_per_order = json.load(open(args.traffic_from)).get("bytes_per_order")
+        if traffic_per_order:
+            traffic = traffic_per_order * tm["orders"] / timed
 
     # N > 1: the persistence path — every batch's tape and results gathered to rank 0 over RCCL
     # (matching_engine_amd/gather.py), timed separately; informational, never part of value
@@ -515,8 +520,10 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": "k_match",
+                "kernel": "k_match_reg" if sc.levels <= 128 else "k_match",
                 "algorithmic_bytes_per_launch": bytes_per_launch,
+                "algorithmic_bytes_per_order": bytes_per_order,
+                "traffic_bytes_per_order": traffic_per_order,
             },
             "cpu_baseline": cpu,
             "host": host_info(),

@@ -16,15 +16,30 @@ import sys
 
 
 def per_dispatch(d, counter, kernel):
+    """Counter per launch of `kernel`, in dispatch order. A continuation launch (the register kernel's
+    `<true>` instance, which follows its common launch on the same stream) is added to the launch
+    it continues: together they are one launch group's matching."""
     vals = []
     for f in glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True):
+        acc = {}
         for r in csv.DictReader(open(f)):
             name = r.get("Kernel_Name") or r.get("Kernel-Name") or ""
             cn = r.get("Counter_Name") or r.get("Counter-Name") or ""
             if kernel in name and cn == counter:
-                did = int(r.get("Dispatch_Id") or r.get("Dispatch-Id") or len(vals))
-                vals.append((did, float(r.get("Counter_Value") or r.get("Counter-Value"))))
-    return [v for _, v in sorted(vals)]
+                did = int(r.get("Dispatch_Id") or r.get("Dispatch-Id") or len(acc))
+                cont = "<true>" in name
+                v = float(r.get("Counter_Value") or r.get("Counter-Value"))
+                k = acc.setdefault(did, [cont, 0.0])
+                k[1] += v
+        merged = []
+        for did in sorted(acc):
+            cont, v = acc[did]
+            if cont and merged:
+                merged[-1] += v
+            elif not cont:
+                merged.append(v)
+        vals += merged
+    return vals
 
 
 def main():
@@ -33,6 +48,11 @@ def main():
     if "--kernel" in a:
         i = a.index("--kernel")
         kernel = a[i + 1]
+        del a[i:i + 2]
+    orders = None
+    if "--orders-per-launch" in a:
+        i = a.index("--orders-per-launch")
+        orders = int(a[i + 1])
         del a[i:i + 2]
     fdir, wdir = a[0], a[1]
     f = per_dispatch(fdir, "FETCH_SIZE", kernel)
@@ -58,6 +78,10 @@ def main():
         "bytes_per_launch_all_avg": (2.0 * fetch_kb + write_kb) * 1024.0,
         "bytes_per_dispatch": [round(x) for x in per],
         "correction": "FETCH_SIZE x2 (gfx950 half-count of wide reads), WRITE_SIZE x1, KB->B x1024",
+        "fetch_bytes_median": sorted(2.0 * x * 1024.0 for x in f)[len(f) // 2],
+        "write_bytes_median": sorted(x * 1024.0 for x in w)[len(w) // 2],
+        "orders_per_launch": orders,
+        "bytes_per_order": med / orders if orders else None,
     }
     print(json.dumps(out, indent=1))
     return 0
