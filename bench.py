@@ -407,6 +407,7 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     tm = eng.timing_read()
+    handoffs = eng.stats()["handoffs"]
     orders_local = sum(db.n for db in dbs[args.warmup:])
     import torch.distributed as tdist
 
@@ -506,6 +507,7 @@ def main():
                 "parallelism": f"symbol-hash shards x{world} (no cross-GPU matching)",
             },
             "fills_per_order": fills_all / max(orders_all, 1),
+            "handoffs_rank0": handoffs,
             "kernel_match_ms_avg": tm["match_ms"] / timed,
             "kernel_match_launches_timed": tm["launches"],
             "batches_per_launch": args.batches_per_launch or (32 if sc.levels <= 128 else 1),

@@ -259,6 +259,10 @@ int me_timing_enable(me_engine* e, int period);
 int me_timing_read(me_engine* e, double* match_ms, double* pipeline_ms, uint64_t* launches,
                    uint64_t* fills, uint64_t* orders);
 
+/* Event counters since me_create: handoffs = symbols the register-window kernel handed to its
+ * continuation launch (a far price level, a re-centre, a cancel of a far or very old order). */
+int me_stats_read(me_engine* e, uint64_t* handoffs);
+
 /* Last error text of e (or of the last failed me_create when e == NULL). */
 int me_last_error(const me_engine* e, char* buf, size_t cap);
 

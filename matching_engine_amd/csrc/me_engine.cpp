@@ -297,7 +297,8 @@ static void free_all(me_engine* e) {
   void* ptrs[] = {e->bk.levels,   e->bk.occ,      e->bk.sym,      e->bk.chunks,     e->bk.tend,
                   e->bk.loc,      e->bk.chunk_top, e->bk.err,       (void*)e->bk.gsym,
                   e->d_tape,      e->d_tape_count, e->d_fills_acc, e->bk.dbg,      e->bk.fcache,
-                  e->bk.far,      e->bk.old,       e->bk.sq,       e->bk.hcount,     e->bk.hand};
+                  e->bk.far,      e->bk.old,       e->bk.sq,       e->bk.hcount,     e->bk.hand,
+                  e->bk.stats};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   {
@@ -500,6 +501,7 @@ extern "C" me_engine* me_create(const me_config* cfg) {
   ALLOC(bk.sq, 2);
   ALLOC(bk.hcount, 1);
   ALLOC(bk.hand, S);
+  ALLOC(bk.stats, ME_STATS);
   ALLOC(bk.chunk_top, 1);
   ALLOC(bk.err, 1);
   uint32_t* gsym = nullptr;
@@ -574,6 +576,7 @@ extern "C" me_engine* me_create(const me_config* cfg) {
             hipMemsetAsync(bk.loc, 0xFF, ring * sizeof(uint32_t), st) == hipSuccess &&
             hipMemsetAsync(bk.old, 0, oldn * sizeof(OldEnt), st) == hipSuccess &&
             hipMemsetAsync(bk.hcount, 0, 4, st) == hipSuccess &&
+            hipMemsetAsync(bk.stats, 0, ME_STATS * 8, st) == hipSuccess &&
             hipMemcpyAsync(bk.sq, sq0, sizeof sq0, hipMemcpyHostToDevice, st) == hipSuccess &&
             hipMemsetAsync(bk.fcache, 0xFF, S * 64 * sizeof(uint32_t), st) == hipSuccess &&
             hipMemsetAsync(bk.chunk_top, 0, 4, st) == hipSuccess && hipMemsetAsync(bk.err, 0, 4, st) == hipSuccess &&
@@ -1491,6 +1494,16 @@ extern "C" int me_timing_read(me_engine* e, double* match_ms, double* pipeline_m
   HIP_TRY(hipMemcpy(&f, e->d_fills_acc, 8, hipMemcpyDeviceToHost), "read fill counter");
   if (orders) *orders = o;
   if (fills) *fills = f;
+  return ME_OK;
+}
+
+extern "C" int me_stats_read(me_engine* e, uint64_t* handoffs) {
+  if (!e) return ME_E_INVALID;
+  int rc = me_sync(e);
+  if (rc) return rc;
+  unsigned long long v[ME_STATS];
+  HIP_TRY(hipMemcpy(v, e->bk.stats, sizeof v, hipMemcpyDeviceToHost), "D2H stats");
+  if (handoffs) *handoffs = v[ST_HANDOFFS];
   return ME_OK;
 }
 

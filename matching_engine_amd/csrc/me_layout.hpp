@@ -141,6 +141,9 @@ struct Handoff {
   uint32_t pad[2];
 };
 
+// Event counters kept on the device (BookDev::stats, me_stats_read).
+enum : uint32_t { ST_HANDOFFS = 0, ME_STATS = 8 };
+
 struct BookDev {
   Level* levels;
   unsigned long long* occ;
@@ -158,6 +161,7 @@ struct BookDev {
   SeqState* sq;           // [2]
   uint32_t* hcount;       // hand-offs of the current match launch (zeroed by k_seq_sweep)
   Handoff* hand;          // [S]
+  unsigned long long* stats;  // [ME_STATS] event counters (me_stats_read)
   unsigned long long ring_mask;
   unsigned long long old_mask;
   uint32_t fcap;

@@ -1086,8 +1086,9 @@ __device__ __forceinline__ uint32_t make_cw(long long opx, uint32_t kd, long lon
                 : inw    ? (int)off
                 : buy    ? (above ? (int)L - 1 : -1)
                          : (above ? (int)L : 0);
-  const bool far = market || (buy ? above : (!inw && !above));
-  const bool out = !market && !inw;
+  // a CANCEL's price field is its target seq: none of the window / far tests apply to it
+  const bool far = !cancel && (market || (buy ? above : (!inw && !above)));
+  const bool out = !market && !cancel && !inw;
   const bool hand = out || (market && ((far_nz >> (buy ? 1 : 0)) & 1u));
   return (uint32_t)(lim + 1) | (buy ? CW_BUY : 0u) | (market ? CW_MKT : 0u) | (cancel ? CW_CXL : 0u) |
          (far ? CW_FAR : 0u) | (out ? CW_OUT : 0u) | (hand ? CW_HAND : 0u);
@@ -1109,6 +1110,7 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
   if constexpr (kSlow) {  // nothing handed off (the usual case): leave before the argument copy
     nhand = min(*(volatile uint32_t*)bk.hcount, bk.S);
     if (blockIdx.x * REG_WAVES >= nhand) return;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && bk.stats) atomicAdd(bk.stats + ST_HANDOFFS, (unsigned long long)nhand);
   }
   {
     for (uint32_t i = threadIdx.x; i < sizeof(ColdArgs) / 8; i += 128 * REG_WAVES)
@@ -1585,8 +1587,8 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
 
 // One launch: the match job of bt[0, ng) (ng == 0: none) on S / REG_WAVES workgroups (S + 1 for the
 // sort path's bad-symbol bin) and the side jobs of ax on the first dispatch round's extra waves; then,
-// when it matched anything, the continuation launch over the symbols it handed off (64 workgroups,
-// which leave at once when there are none). ev0 / ev1 bracket both.
+// when it matched anything, the continuation launch over the symbols it handed off (one wave per
+// symbol, like the common launch; workgroups with nothing to do leave at once). ev0 / ev1 bracket both.
 hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* bt, uint32_t ng, const AuxDev& ax,
                             hipEvent_t ev0, hipEvent_t ev1) {
   if (bk.L > (uint32_t)RL || bk.L < 64u || !bk.fcache || !bk.gsym || !bk.hand || !bk.hcount)
@@ -1612,8 +1614,8 @@ hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* b
   hipExtLaunchKernelGGL(k_match_reg<false>, dim3(grid), dim3(128 * REG_WAVES), 0, st, ev0, ng ? nullptr : ev1, 0, A);
   if (ng) {
     A.ax = AuxDev{};
-    hipExtLaunchKernelGGL(k_match_reg<true>, dim3(min(64u, match_wgs)), dim3(128 * REG_WAVES), 0, st, nullptr, ev1, 0,
-                          A);
+    // one wave per possible hand-off: workgroups past the hand-off count leave before the argument copy
+    hipExtLaunchKernelGGL(k_match_reg<true>, dim3(match_wgs), dim3(128 * REG_WAVES), 0, st, nullptr, ev1, 0, A);
   }
   return hipGetLastError();
 }

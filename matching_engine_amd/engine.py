@@ -310,6 +310,12 @@ class Engine:
         _check(self.lib, self.h, self.lib.me_resting_count(self.h, C.byref(v)))
         return v.value
 
+    def stats(self) -> dict:
+        """Device event counters since creation (me_stats_read)."""
+        h = C.c_uint64(0)
+        _check(self.lib, self.h, self.lib.me_stats_read(self.h, C.byref(h)))
+        return {"handoffs": h.value}
+
     # -- timing
     def timing_enable(self, period: int = 1):
         """HIP events on every `period`-th match launch (True = every launch, 0/False = off)."""

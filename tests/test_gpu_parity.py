@@ -578,3 +578,22 @@ def test_book_orders_ten_thousand_levels_one_launch(me, orc):
         assert len(lb) == 10_000 and len(la) == 10_000
         assert np.array_equal(bids, dump[dump["side"] == me.SIDE_BUY])
         assert np.array_equal(asks, dump[dump["side"] == me.SIDE_SELL])
+
+
+def test_handoffs_only_for_far_events(me, orc):
+    """The register-window kernel hands a symbol to its continuation launch only for a far price level
+    (or a re-centre / an old order): a cancel-heavy stream whose prices stay in the window never hands
+    off (cancel records carry a seq, not a price), a stream with far LIMITs does."""
+    for cfg, over, expect_far in ((5, dict(num_symbols=256, batch=16384), False),
+                                  (2, dict(num_symbols=64, batch=4096, far_pct=2), True)):
+        sc = me.preset(cfg, **over)
+        st = me.Stream(sc)
+        base = st.base_prices()
+        batches = [st.next(sc.batch) for _ in range(6)]
+        total = sum(len(b) for b in batches)
+        ob = orc.OracleBook(sc.num_symbols)
+        with engine_for(me, sc.num_symbols, sc.levels, base, sc.batch, total + 1024,
+                        max_chunks=total + 2 * sc.num_symbols) as eng:
+            run_both(eng, ob, batches, ctx=f"handoffs c{cfg}")
+            h = eng.stats()["handoffs"]
+        assert (h > 0) == expect_far, (cfg, h)
