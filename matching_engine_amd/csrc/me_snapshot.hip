@@ -9,7 +9,7 @@
 // block-wide compaction of the window's totals, every thread then walks ONE level's chunk chain to
 // count its live slots, a block scan turns the counts into output offsets, and a second walk writes
 // the orders. Chains are short (a chunk holds 16 slots), so a pass costs a few chunk-load latencies
-// however deep the book is: a 10,000-level side is three passes of one launch.
+// however deep the book is: a 10,000-level side is five passes of one launch.
 //
 // Bytes per resting order: one 256-B chunk read per 16 orders (twice: count + write) + 24 B out;
 // per level 16 B (window) or 32 B (far) read + 24 B out. HBM-bound in principle, latency-bound in
