@@ -96,12 +96,15 @@ int me_service_submit_order(me_service* s, const me_order_request* req, me_order
  * drivers and benchmarks holding many requests at once; resps[i] answers reqs[i]. */
 int me_service_submit_orders(me_service* s, const me_order_request* reqs, size_t n, me_order_response* resps);
 
-/* Orders waiting in the open time slice. */
+/* Submitted orders not matched yet (the open slice, closed slices, the slice being matched). */
 size_t me_service_pending(const me_service* s);
 /* Next OID number the service will allocate. */
 uint64_t me_service_next_oid(const me_service* s);
 
-/* Match and persist every slice submitted before the call, oldest first. Any output may be NULL;
+/* Match and persist every slice submitted before the call, oldest first (matching runs on the calling
+ * thread, ahead of the service's persister thread by at most 4 slices, so the engine overlaps
+ * SQLite); returns once every matched slice's OrderUpdates are out and its transaction committed.
+ * Any output may be NULL;
  * the outputs cover the records this call matched, in submission order (tape offsets into the
  * concatenated tape): *n_results records, out_seq[i] their numeric OIDs. The capacities are checked
  * before anything is matched (results_cap >= me_service_pending, fills_cap >= me_fill_bound of it),
@@ -112,11 +115,14 @@ uint64_t me_service_next_oid(const me_service* s);
  * (me_service_unpersisted counts the records waiting). */
 int me_service_flush(me_service* s, me_fill* out_fills, size_t fills_cap, size_t* n_fills,
                      me_order_result* out_results, uint64_t* out_seq, size_t results_cap, size_t* n_results);
-/* Matched records whose SQLite transaction has not committed yet. */
+/* Matched records whose SQLite transaction has not committed yet (queued for the persister, or kept
+ * after a failed transaction). me_service_pending + me_service_unpersisted is 0 exactly when every
+ * submitted order is matched and committed. */
 size_t me_service_unpersisted(const me_service* s);
 /* Background flusher (one thread): a slice closes at slice_orders records (0 or more than the
  * engine's max_batch: max_batch) or once it is interval_us old (0: 1000), and is flushed at once.
- * Errors go to me_service_last_error. me_service_stop joins it. */
+ * Errors go to me_service_last_error. me_service_stop joins it and waits for the persister to
+ * finish what it matched. */
 int me_service_start(me_service* s, uint32_t interval_us, uint32_t slice_orders);
 int me_service_stop(me_service* s);
 

@@ -12,10 +12,15 @@
 // update_order_status-style updates for makers and cancel targets, and fills rows through the
 // corrected add_fill statement (5 columns, 5 placeholders; the reference's has 6, storage.cpp:190).
 //
+// Two stages run concurrently: the flushing thread matches slice k+1 while the persister thread
+// (which alone owns the DB) emits slice k's OrderUpdates and commits its transaction, so the engine
+// (or the sharded matcher's gather) overlaps SQLite instead of waiting for it.
+//
 // Locks (always taken in this order, never the other way round):
-//   flush_mu  one flusher at a time: slices are matched and persisted in stream order; owns the DB
+//   flush_mu  one flusher at a time: slices are matched in stream order
 //   eng_mu    every engine call (the engine is single-threaded): flush matching, book reads
 //   mu        the open slice, the closed-slice queue, the symbol table, the OID counter
+//   pq_mu     the matched-slice queue between the two stages
 //   live_mu   resting orders' owners and remainders (cancel ownership, OrderUpdate bookkeeping)
 //   upd_mu    the OrderUpdate queue
 //   err_mu    the last error text
@@ -141,8 +146,9 @@ struct Slice {
   size_t size() const { return seq.size(); }
 };
 
-// A matched slice whose transaction failed: kept, in order, until a later flush commits it.
-struct Unpersisted {
+// A matched slice on its way to the DB (outputs copied out of the engine's buffers). One whose
+// transaction failed stays at the head of the queue, in order, until a later flush commits it.
+struct Matched {
   Slice sl;
   std::vector<me_order_result> res;
   std::vector<me_fill> tape;
@@ -159,6 +165,7 @@ struct Live {
 
 constexpr size_t kMaxQueuedUpdates = size_t(1) << 24;  // oldest events are dropped beyond this
 constexpr int kRows = 64;  // rows per multi-row INSERT (11 * 64 parameters < SQLite's 999 floor)
+constexpr size_t kMaxMatchedAhead = 4;  // matched slices the flusher may run ahead of the persister
 
 }  // namespace
 
@@ -175,10 +182,19 @@ struct me_service {
   Slice open;
   std::deque<Slice> closed;
   size_t closed_records = 0;
-  // --- flush_mu (persistence + retry queue)
+  size_t inflight_records = 0;  // taken off `closed`, not yet in pq (being matched)
+  // --- flush_mu
   std::mutex flush_mu;
-  std::deque<Unpersisted> unpersisted;
-  size_t unpersisted_records = 0;  // read without flush_mu through an atomic-free snapshot under mu
+  // --- pq_mu: matched slices, oldest first, until committed (the persister thread owns the DB)
+  std::mutex pq_mu;
+  std::condition_variable pq_cv;
+  std::deque<Matched> pq;
+  size_t pq_emitted = 0;    // slices at the head of pq whose OrderUpdates are out
+  size_t pq_records = 0;
+  bool pq_stalled = false;  // the head's transaction failed: retried when the next flush starts
+  bool pq_stop = false;
+  std::string pq_err;
+  std::thread persister;
   // --- eng_mu
   std::mutex eng_mu;
   // --- live_mu / upd_mu
@@ -192,7 +208,7 @@ struct me_service {
   std::condition_variable cv;  // with mu
   bool stop = false;
   int64_t interval_us = 0;
-  // --- persistence (under flush_mu)
+  // --- persistence (the persister thread; create/destroy otherwise)
   sqlite3* db = nullptr;
   sqlite3_stmt* st_ins = nullptr;
   sqlite3_stmt* st_upd = nullptr;
@@ -220,6 +236,8 @@ static void close_db(me_service* s) {
   if (s->db) g_sql.close(s->db);
   s->db = nullptr;
 }
+
+static void persister_main(me_service* s);
 
 static bool sql_ok(int rc) { return rc == SQLITE_OK || rc == SQLITE_DONE || rc == SQLITE_ROW; }
 
@@ -308,6 +326,7 @@ static me_service* create(me_engine* engine, const me_matcher* m, const char* co
     close_db(s);
     s->fail(ME_E_SQLITE, "me_service_create: " + err);
   }
+  s->persister = std::thread(persister_main, s);
   return s;
 }
 
@@ -517,7 +536,7 @@ extern "C" int me_service_cancel_order(me_service* s, const me_cancel_request* r
 extern "C" size_t me_service_pending(const me_service* s) {
   me_service* m = const_cast<me_service*>(s);
   std::lock_guard<std::mutex> lk(m->mu);
-  return m->open.size() + m->closed_records;
+  return m->open.size() + m->closed_records + m->inflight_records;
 }
 
 extern "C" uint64_t me_service_next_oid(const me_service* s) {
@@ -528,8 +547,8 @@ extern "C" uint64_t me_service_next_oid(const me_service* s) {
 
 extern "C" size_t me_service_unpersisted(const me_service* s) {
   me_service* m = const_cast<me_service*>(s);
-  std::lock_guard<std::mutex> lk(m->mu);
-  return m->unpersisted_records;
+  std::lock_guard<std::mutex> lk(m->pq_mu);
+  return m->pq_records;
 }
 
 static void push_update(me_service* s, uint64_t oid, const std::string& client, const std::string& symbol,
@@ -630,7 +649,7 @@ extern "C" int me_service_updates(me_service* s, const char* client_id, me_order
   return ME_OK;
 }
 
-// One transaction for one matched slice (flush_mu held). The rows end exactly as the reference's
+// One transaction for one matched slice (the persister thread). The rows end exactly as the reference's
 // per-order statements would leave them — insert_new_order's row (storage.cpp:102-112, incl.
 // order_type=1, storage.cpp:106), then update_order_status-style changes (storage.cpp:160-181) as
 // later fills and cancels hit the order — but the slice's own orders are brought to their final
@@ -790,18 +809,43 @@ static bool persist(me_service* s, const Slice& sl, const me_order_result* res, 
   return true;
 }
 
-// Commit the queued unpersisted slices, oldest first (flush_mu held). False when one still fails.
-static bool persist_backlog(me_service* s, std::string& err) {
-  while (!s->unpersisted.empty()) {
-    Unpersisted& u = s->unpersisted.front();
-    if (!persist(s, u.sl, u.res.data(), u.tape.data(), u.ts, err)) return false;
-    {
-      std::lock_guard<std::mutex> lk(s->mu);
-      s->unpersisted_records -= u.sl.size();
+// The persister: emits each matched slice's OrderUpdates, then commits its transaction, oldest
+// first. A failed transaction stalls the queue (later slices still get their updates) until the
+// next flush clears pq_stalled; on stop it drains what it can and exits.
+static void persister_main(me_service* s) {
+  std::unique_lock<std::mutex> lk(s->pq_mu);
+  for (;;) {
+    s->pq_cv.wait(lk, [&] {
+      return s->pq_stop || s->pq_emitted < s->pq.size() || (!s->pq_stalled && !s->pq.empty());
+    });
+    if (s->pq_emitted < s->pq.size()) {
+      const Matched* m = &s->pq[s->pq_emitted];  // deque elements stay put under push_back
+      lk.unlock();
+      emit_updates(s, m->sl, m->res.data(), m->tape.data());
+      lk.lock();
+      ++s->pq_emitted;
+      s->pq_cv.notify_all();
+      continue;
     }
-    s->unpersisted.pop_front();
+    if (!s->pq_stalled && !s->pq.empty()) {
+      const Matched* m = &s->pq.front();
+      lk.unlock();
+      std::string err;
+      const bool ok = persist(s, m->sl, m->res.data(), m->tape.data(), m->ts, err);
+      lk.lock();
+      if (ok) {
+        s->pq_records -= m->sl.size();
+        s->pq.pop_front();
+        --s->pq_emitted;
+      } else {
+        s->pq_stalled = true;
+        s->pq_err = err;
+      }
+      s->pq_cv.notify_all();
+      continue;
+    }
+    if (s->pq_stop) break;
   }
-  return true;
 }
 
 // Where a flush's caller wants the matched outputs (any pointer may be NULL).
@@ -814,86 +858,84 @@ struct FlushOut {
   size_t nr = 0;
 };
 
-// Match + persist one closed slice (flush_mu held, the slice already taken off the queue).
+// Match one closed slice and hand it to the persister (flush_mu held; the slice already taken off
+// the queue and counted in inflight_records).
 static int process(me_service* s, Slice&& sl, FlushOut* out) {
   const size_t n = sl.size();
-  const me_fill* tape = nullptr;
-  const me_order_result* res = nullptr;
-  size_t nf = 0, nr = 0;
+  {  // bounded run-ahead: at most kMaxMatchedAhead slices wait for the DB (unless it is stalled)
+    std::unique_lock<std::mutex> lq(s->pq_mu);
+    s->pq_cv.wait(lq, [&] { return s->pq_stalled || s->pq.size() < kMaxMatchedAhead; });
+  }
+  Matched mt;
   {
     std::lock_guard<std::mutex> le(s->eng_mu);
     me_order_soa b{sl.seq.data(), sl.px.data(), sl.qty.data(), sl.sid.data(), sl.kind.data()};
+    const me_fill* tape = nullptr;
+    const me_order_result* res = nullptr;
+    size_t nf = 0;
     bool accepted = false;
     const int rc = backend_match(s, b, n, &tape, &nf, &res, accepted);
-    nr = n;
     if (rc != ME_OK && !accepted) {  // not accepted: the slice goes back to the head of the queue
       const std::string e = backend_err(s);
       std::lock_guard<std::mutex> lk(s->mu);
+      s->inflight_records -= n;
       s->closed_records += n;
       s->closed.push_front(std::move(sl));
       return s->fail(rc, "engine: " + e);
     }
     if (rc != ME_OK) {  // accepted and lost: the books may hold the slice, the service cannot go on
       s->failed = true;
+      std::lock_guard<std::mutex> lk(s->mu);
+      s->inflight_records -= n;
       return s->fail(rc, "engine lost an accepted slice: " + backend_err(s));
     }
+    // the engine's output views stay valid until its next call: copy them out under eng_mu
+    mt.res.assign(res, res + n);
+    mt.tape.assign(tape, tape + nf);
   }
-  // the outputs stay valid until the next match, which only a later process() (this thread,
-  // flush_mu) can issue
-  int rc = ME_OK;
-  std::string err;
-  const int64_t ts = now_ms();
-  if (!persist_backlog(s, err) || !persist(s, sl, res, tape, ts, err)) {
-    Unpersisted u{std::move(sl), std::vector<me_order_result>(res, res + nr), std::vector<me_fill>(tape, tape + nf),
-                  ts};
-    {
-      std::lock_guard<std::mutex> lk(s->mu);
-      s->unpersisted_records += u.sl.size();
-    }
-    s->unpersisted.push_back(std::move(u));
-    rc = s->fail(ME_E_SQLITE, "persistence deferred (" + err + "); the slice is matched and kept for the next flush");
-    const Unpersisted& k = s->unpersisted.back();
-    emit_updates(s, k.sl, k.res.data(), k.tape.data());
-    if (out) {
-      if (out->fills) memcpy(out->fills + out->nf, k.tape.data(), nf * sizeof(me_fill));
-      if (out->res)
-        for (size_t i = 0; i < nr; ++i) {
-          out->res[out->nr + i] = k.res[i];
-          out->res[out->nr + i].tape_offset += (uint32_t)out->nf;
-        }
-      if (out->seq) memcpy(out->seq + out->nr, k.sl.seq.data(), nr * sizeof(uint64_t));
-      out->nf += nf;
-      out->nr += nr;
-    }
-    return rc;
-  }
-  emit_updates(s, sl, res, tape);
+  mt.ts = now_ms();
+  const size_t nf = mt.tape.size();
   if (out) {
-    if (out->fills) memcpy(out->fills + out->nf, tape, nf * sizeof(me_fill));
+    if (out->fills) memcpy(out->fills + out->nf, mt.tape.data(), nf * sizeof(me_fill));
     if (out->res)
-      for (size_t i = 0; i < nr; ++i) {
-        out->res[out->nr + i] = res[i];
+      for (size_t i = 0; i < n; ++i) {
+        out->res[out->nr + i] = mt.res[i];
         out->res[out->nr + i].tape_offset += (uint32_t)out->nf;
       }
-    if (out->seq) memcpy(out->seq + out->nr, sl.seq.data(), nr * sizeof(uint64_t));
+    if (out->seq) memcpy(out->seq + out->nr, sl.seq.data(), n * sizeof(uint64_t));
     out->nf += nf;
-    out->nr += nr;
+    out->nr += n;
   }
-  return rc;
+  mt.sl = std::move(sl);
+  {
+    std::lock_guard<std::mutex> lq(s->pq_mu);
+    s->pq.push_back(std::move(mt));
+    s->pq_records += n;
+    s->pq_cv.notify_all();
+  }
+  std::lock_guard<std::mutex> lk(s->mu);  // after the push: pending + unpersisted never dips to 0 early
+  s->inflight_records -= n;
+  return ME_OK;
 }
 
 // Flush the closed slices (and the open one when take_open), oldest first. `limit` bounds how many
-// slices are taken (those present when the caller checked its output capacity).
-static int flush_closed(me_service* s, bool take_open, size_t limit, FlushOut* out) {
+// slices are taken (those present when the caller checked its output capacity). With `wait`, returns
+// once the persister has emitted every matched slice and committed them (or stalled on a failed
+// transaction: ME_E_SQLITE, the slices kept in order for the next flush).
+static int flush_closed(me_service* s, bool take_open, size_t limit, FlushOut* out, bool wait) {
   if (s->failed) return s->fail(ME_E_STATE, "service failed: the engine lost an accepted slice");
   if (!has_backend(s)) {
     std::lock_guard<std::mutex> lk(s->mu);
     if (s->open.size() || !s->closed.empty())
       return s->fail(ME_E_STATE, "me_service_flush: no engine (HIP device required)");
   }
-  int rc = ME_OK;
-  std::string err;
-  if (!persist_backlog(s, err)) rc = s->fail(ME_E_SQLITE, "persistence deferred (" + err + ")");
+  {  // every flush retries the kept slices first
+    std::lock_guard<std::mutex> lq(s->pq_mu);
+    if (s->pq_stalled) {
+      s->pq_stalled = false;
+      s->pq_cv.notify_all();
+    }
+  }
   if (take_open) {
     std::lock_guard<std::mutex> lk(s->mu);
     close_open(s);
@@ -906,15 +948,18 @@ static int flush_closed(me_service* s, bool take_open, size_t limit, FlushOut* o
       sl = std::move(s->closed.front());
       s->closed.pop_front();
       s->closed_records -= sl.size();
+      s->inflight_records += sl.size();
     }
     const int r = process(s, std::move(sl), out);
-    if (r == ME_E_SQLITE) {
-      rc = r;  // matched and kept: later slices still match (and queue behind it for the DB)
-      continue;
-    }
     if (r != ME_OK) return r;
   }
-  return rc;
+  if (!wait) return ME_OK;
+  std::unique_lock<std::mutex> lq(s->pq_mu);
+  s->pq_cv.wait(lq, [&] { return s->pq_emitted == s->pq.size() && (s->pq.empty() || s->pq_stalled); });
+  if (s->pq_stalled)
+    return s->fail(ME_E_SQLITE, "persistence deferred (" + s->pq_err +
+                                    "); the matched slices are kept and retried at the next flush");
+  return ME_OK;
 }
 
 extern "C" int me_service_flush(me_service* s, me_fill* out_fills, size_t fills_cap, size_t* n_fills,
@@ -926,7 +971,7 @@ extern "C" int me_service_flush(me_service* s, me_fill* out_fills, size_t fills_
   size_t total = 0, nslices = 0;
   {
     std::lock_guard<std::mutex> lk(s->mu);
-    total = s->open.size() + s->closed_records;
+    total = s->open.size() + s->closed_records;  // inflight is 0 here (flush_mu held)
     nslices = s->closed.size() + (s->open.size() ? 1 : 0);
   }
   // the caller's buffers are checked before anything is matched
@@ -936,7 +981,7 @@ extern "C" int me_service_flush(me_service* s, me_fill* out_fills, size_t fills_
   if (out_fills && has_backend(s) && fills_cap < bound)
     return s->fail(ME_E_INVALID, "fills_cap smaller than me_fill_bound(pending records)");
   FlushOut out{out_fills, fills_cap, 0, out_results, out_seq, 0};
-  const int rc = flush_closed(s, true, nslices, &out);
+  const int rc = flush_closed(s, true, nslices, &out, true);
   if (n_fills) *n_fills = out.nf;
   if (n_results) *n_results = out.nr;
   return rc;
@@ -958,7 +1003,7 @@ static void flusher_main(me_service* s) {
     lk.unlock();
     {
       std::lock_guard<std::mutex> lf(s->flush_mu);
-      (void)flush_closed(s, false, SIZE_MAX, nullptr);  // errors land in me_service_last_error
+      (void)flush_closed(s, false, SIZE_MAX, nullptr, false);  // errors land in me_service_last_error
     }
     lk.lock();
     if (s->failed) break;
@@ -990,12 +1035,22 @@ extern "C" int me_service_stop(me_service* s) {
     s->cv.notify_all();
   }
   if (s->flusher.joinable()) s->flusher.join();
+  // what the flusher matched is out (updates emitted, committed or stalled) when stop returns
+  std::unique_lock<std::mutex> lq(s->pq_mu);
+  s->pq_cv.wait(lq, [&] { return s->pq_emitted == s->pq.size() && (s->pq.empty() || s->pq_stalled); });
   return ME_OK;
 }
 
 extern "C" void me_service_destroy(me_service* s) {
   if (!s) return;
   me_service_stop(s);
+  {  // the persister commits what it can (a stalled head is given one more try), then exits
+    std::lock_guard<std::mutex> lq(s->pq_mu);
+    s->pq_stalled = false;
+    s->pq_stop = true;
+    s->pq_cv.notify_all();
+  }
+  if (s->persister.joinable()) s->persister.join();
   close_db(s);
   delete s;
 }
