@@ -408,6 +408,7 @@ def main():
     elapsed = t1 - t0
     tm = eng.timing_read()
     handoffs = eng.stats()["handoffs"]
+    adm = eng.admission()  # after the timed region: exact counts taken by submits (0 = never drained)
     orders_local = sum(db.n for db in dbs[args.warmup:])
     import torch.distributed as tdist
 
@@ -441,26 +442,34 @@ def main():
         from matching_engine_amd.gather import EngineGather
 
         dev = torch.device("cuda", local)
-        gat = EngineGather(eng, dev, max(len(b) for b in gather_batches))
+        ts = torch.cuda.Stream(device=dev)
+        eng.set_stream(ts.cuda_stream)  # the gather of batch k overlaps the match of batch k + 1
+        gat = EngineGather(eng, dev, max(len(b) for b in gather_batches), stream=ts)
         gdbs = [eng.upload(b) for b in gather_batches]
         gpos = [torch.from_numpy(p.astype(np.int64)).to(dev) for p in gather_pos]
         barrier_sync(world, local)
         tg0 = time.perf_counter()
         gfills = 0
-        for db, p in zip(gdbs, gpos):
-            eng.submit_device(db)
-            tape, _ = gat.gather(db.n, p, sc.batch)
+        eng.submit_device(gdbs[0])
+        for k, (db, p) in enumerate(zip(gdbs, gpos)):
+            nf = gat.stage(db.n)
+            if k + 1 < len(gdbs):
+                eng.submit_device(gdbs[k + 1])
+            tape, _ = gat.collect(nf, db.n, p, sc.batch)
             if tape is not None:
                 gfills += len(tape)
+        eng.sync()
         barrier_sync(world, local)
         tg = allreduce(time.perf_counter() - tg0, world, MAX, local)
+        eng.set_stream(None)
         for db in gdbs:
             db.free()
         rccl = {"backend": tdist.get_backend(), "steps": len(gather_batches), "ms_per_step": tg / len(gather_batches) * 1e3,
                 "orders_per_s_incl_gather": sc.batch * len(gather_batches) / tg,
                 "tape_bytes_per_step_to_root": 32.0 * gfills / len(gather_batches),
                 "what": "submit + device tape/result copy + RCCL all_gather(sizes) + gather(tape, results) to "
-                        "rank 0 + stable merge by taker seq on rank 0's GPU + D2H of the merged tape"}
+                        "rank 0 + stable merge by taker seq on rank 0's GPU + D2H of the merged tape; batch "
+                        "k's gather overlaps batch k+1's match (EngineGather.stage / collect)"}
 
     # PCIe-inclusive host path (me_submit_host / me_collect: staging copy into a pinned slot, H2D on
     # its own stream, the grouped pipeline, D2H of results + tape into pinned memory), informational.
@@ -508,6 +517,8 @@ def main():
             },
             "fills_per_order": fills_all / max(orders_all, 1),
             "handoffs_rank0": handoffs,
+            "admission_rank0": {"exact_counts": adm["exact_counts"], "resting": adm["resting"],
+                                "max_resting": eng.config()["max_resting"]},
             "kernel_match_ms_avg": tm["match_ms"] / timed,
             "kernel_match_launches_timed": tm["launches"],
             "batches_per_launch": args.batches_per_launch or (32 if sc.levels <= 128 else 1),

@@ -71,7 +71,8 @@ enum {
   ME_OK = 0,
   ME_E_INVALID = -1,   /* bad argument / config */
   ME_E_HIP = -2,       /* HIP runtime failure (no device, launch failure, ...) */
-  ME_E_CAPACITY = -3,  /* a fixed-capacity pool (chunks, locator, scratch, tape) overflowed */
+  ME_E_CAPACITY = -3,  /* a batch refused by admission control (max_resting; not sticky), or a
+                          fixed-capacity pool (chunks, far levels, ...) overflowed inside a batch (sticky) */
   ME_E_STATE = -4,     /* engine in a failed state (a previous capacity/HIP error) */
   ME_E_SQLITE = -5     /* persistence failure */
 };
@@ -92,7 +93,12 @@ typedef struct me_config {
                                   Prices are not limited to it: levels outside live in far arrays and the
                                   window re-centres as the market moves */
   uint32_t max_batch;          /* largest n accepted by me_submit_batch* */
-  uint64_t max_resting;        /* resting orders the scratch/tape bound is sized for */
+  uint64_t max_resting;        /* resting orders the scratch/tape bound is sized for. Admission control:
+                                  a batch is accepted only while (resting orders) + (LIMIT records
+                                  accepted and not yet matched) + (its LIMIT records; every record of
+                                  a device batch) <= max_resting, else me_submit_* return
+                                  ME_E_CAPACITY for that batch, NOT sticky: nothing of it was enqueued
+                                  and the engine stays usable (me_admission_read) */
   uint64_t max_chunks;         /* FIFO chunk pool (ME_CHUNK_SLOTS slots each); 0 = max_resting + 2*S */
   uint64_t seq_ring;           /* seq-ring entries for cancels (power of two, 0 = 2^28). Any u64 seq is
                                   accepted; one launch group (batches_per_launch batches) must span fewer
@@ -262,6 +268,12 @@ int me_timing_read(me_engine* e, double* match_ms, double* pipeline_ms, uint64_t
 /* Event counters since me_create: handoffs = symbols the register-window kernel handed to its
  * continuation launch (a far price level, a re-centre, a cancel of a far or very old order). */
 int me_stats_read(me_engine* e, uint64_t* handoffs);
+
+/* Admission control state (any pointer may be NULL): resting = resting orders of every symbol after
+ * all enqueued work (waits for it); bound = the host's current upper bound (resting orders once every
+ * accepted record is matched); exact_counts = times a submit had to take an exact count (flush + sync)
+ * because the published count was too stale or too close to max_resting. */
+int me_admission_read(me_engine* e, uint64_t* resting, uint64_t* bound, uint64_t* exact_counts);
 
 /* Last error text of e (or of the last failed me_create when e == NULL). */
 int me_last_error(const me_engine* e, char* buf, size_t cap);

@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <mutex>
 #include <thread>
@@ -30,7 +31,7 @@ hipError_t launch_sort_pass(hipStream_t st, const uint32_t* keys_in, const uint3
                             uint32_t zero_words, unsigned long long* scratch_top, uint32_t* bin_start,
                             const uint64_t* seq, uint32_t* err);
 hipError_t launch_seq_sweep(hipStream_t st, const BookDev& bk, const uint64_t* const* seq, const uint32_t* n,
-                            uint32_t ng, uint32_t in_idx, uint32_t grid);
+                            uint32_t ng, uint32_t in_idx, uint32_t grid, uint32_t launch);
 hipError_t launch_match(hipStream_t st, const BookDev& bk, const BatchDev& bt, hipEvent_t ev0, hipEvent_t ev1);
 hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* bt, uint32_t ng, const AuxDev& ax, hipEvent_t ev0,
                             hipEvent_t ev1);
@@ -214,6 +215,7 @@ struct me_engine {
     uint32_t n = 0;
     int oset = 0, bset = 0;
     int slot = -1;  // host slot (me_submit_host), -1: a device batch
+    uint32_t nadm = 0;  // records admission control counted for it
   };
   struct Group {
     Pend b[ME_GMAX];
@@ -262,6 +264,19 @@ struct me_engine {
   } lastg;
   bool failed = false;
   std::string err;
+  // admission control (me_config.max_resting): a batch is accepted only while the resting orders
+  // the device can hold after it stay within max_resting, so the scratch / tape / old-order bounds
+  // sized from it can never overflow. Bound = resting orders known after k match launches + every
+  // record accepted since (each rests at most once). k_seq_sweep publishes {k, resting} into pinned
+  // memory ahead of every match launch; a synchronous exact count replaces it when it is too stale.
+  static constexpr uint32_t ADM_RING = 256;
+  unsigned long long* pub_host = nullptr;  // hipHostMalloc'd, device-mapped (bk.pub)
+  uint32_t launch_no = 0;                  // match launches enqueued
+  uint64_t adm_total = 0;                  // records accepted
+  uint64_t adm_matched = 0;                // records of the batches those launches matched
+  uint64_t adm_at[ADM_RING] = {};          // adm_matched after launch k (k % ADM_RING)
+  uint64_t ovr_resting = 0, ovr_adm = 0;   // the last exact count and the records accepted then
+  uint64_t adm_syncs = 0;                  // exact counts taken (diagnostic)
   // timing
   int timing = 0;           // 0: off; k >= 1: time every k-th match launch
   uint64_t nlaunch = 0;     // match launches since timing was enabled
@@ -334,6 +349,7 @@ static void free_all(me_engine* e) {
     for (void* p : sp)
       if (p) (void)hipFree(p);
   }
+  if (e->pub_host) (void)hipHostFree(e->pub_host);
   if (e->ev_tape) (void)hipEventDestroy(e->ev_tape);
   if (e->s_h2d) (void)hipStreamDestroy(e->s_h2d);
   if (e->s_d2h) (void)hipStreamDestroy(e->s_d2h);
@@ -502,6 +518,10 @@ extern "C" me_engine* me_create(const me_config* cfg) {
   ALLOC(bk.hcount, 1);
   ALLOC(bk.hand, S);
   ALLOC(bk.stats, ME_STATS);
+  if ((he = hipHostMalloc((void**)&e->pub_host, sizeof(unsigned long long), hipHostMallocDefault)) != hipSuccess ||
+      (he = hipHostGetDevicePointer((void**)&bk.pub, e->pub_host, 0)) != hipSuccess)
+    return bail(std::string("me_create: pinned admission word: ") + hipGetErrorString(he));
+  *e->pub_host = 0ull;  // {0 launches, 0 resting}
   ALLOC(bk.chunk_top, 1);
   ALLOC(bk.err, 1);
   uint32_t* gsym = nullptr;
@@ -677,7 +697,7 @@ static int seq_sweep(me_engine* e, const me_engine::Group& g) {
   }
   // a small grid: the launch is on the stream before every match launch and usually decides "no
   // sweep" (a 1,024-workgroup grid cost ~0.7 us per batch at config 2); a due sweep loops over the pool
-  hipError_t he = launch_seq_sweep(e->stream, e->bk, seq, n, g.n, e->sq_idx, 64);
+  hipError_t he = launch_seq_sweep(e->stream, e->bk, seq, n, g.n, e->sq_idx, 64, e->launch_no);
   if (he != hipSuccess) return e->hip_fail(he, "seq sweep launch");
   e->sq_idx ^= 1u;
   e->bk.sq_idx = e->sq_idx;
@@ -747,8 +767,10 @@ static int pipe_launch(me_engine* e, const me_engine::Group* nb) {
   const auto& gm = e->g_match;
   const auto& gt = e->g_tape;
   uint32_t orders = 0;
+  uint64_t admitted = 0;
   for (uint32_t g = 0; g < gm.n; ++g) {
     const auto& pm = gm.b[g];
+    admitted += pm.nadm;
     bt[g] = batch_dev(e, pm.seq, pm.px, pm.qty, pm.sym, pm.kind, pm.n, pm.oset);
     const auto& b = e->bu[pm.bset];
     bt[g].bcnt = b.cnt;
@@ -812,6 +834,10 @@ static int pipe_launch(me_engine* e, const me_engine::Group* nb) {
   hipError_t he = launch_match_reg(e->stream, e->bk, bt, gm.n, ax, tl.m0, tl.m1);
   if (he != hipSuccess) return e->hip_fail(he, "pipelined match launch");
   if (timed) e->timed.push_back(tl);
+  if (gm.n) {
+    e->adm_matched += admitted;
+    e->adm_at[++e->launch_no % me_engine::ADM_RING] = e->adm_matched;
+  }
   if (host_tapes) {
     int slots[ME_GMAX], ns = 0;
     for (uint32_t j = 0; j < gt.n; ++j)
@@ -845,7 +871,7 @@ static int flush_pipeline(me_engine* e) {
 
 // Enqueue a device-resident batch.
 static int enqueue_batch(me_engine* e, const uint64_t* seq, const int64_t* px, const int32_t* qty,
-                         const uint32_t* sym, const uint8_t* kind, uint32_t n, int slot = -1) {
+                         const uint32_t* sym, const uint8_t* kind, uint32_t n, uint32_t nadm, int slot = -1) {
   e->last_host = slot >= 0;
   if (e->bucketed) {
     auto& gf = e->g_fill;
@@ -861,6 +887,7 @@ static int enqueue_batch(me_engine* e, const uint64_t* seq, const int64_t* px, c
     nb.oset = (int)((e->ngroup % 3) * e->group + pos);
     nb.bset = (int)((e->ngroup % 2) * e->group + pos);
     nb.slot = slot;
+    nb.nadm = nadm;
     const uint64_t gen = ++e->oset_gen[nb.oset];
     if (slot >= 0) {
       e->hs[slot].oset = nb.oset;
@@ -922,6 +949,8 @@ static int enqueue_batch(me_engine* e, const uint64_t* seq, const int64_t* px, c
   const uint64_t gen = ++e->oset_gen[oset];
   hipError_t he = launch_match(st, e->bk, bt, tl.m0, tl.m1);
   if (he != hipSuccess) return e->hip_fail(he, "match launch");
+  e->adm_matched += nadm;
+  e->adm_at[++e->launch_no % me_engine::ADM_RING] = e->adm_matched;
   if (slot >= 0) {
     HostSlot& h = e->hs[slot];
     h.oset = oset;
@@ -976,6 +1005,78 @@ static int check_err_word(me_engine* e) {
   return check_err_bits(e, w);
 }
 
+// Upper bound on the resting orders once every accepted record has been matched.
+static uint64_t admission_bound(const me_engine* e) {
+  uint64_t b = e->ovr_resting + (e->adm_total - e->ovr_adm);
+  const unsigned long long v = __atomic_load_n(e->pub_host, __ATOMIC_ACQUIRE);
+  const uint32_t k = (uint32_t)(v >> 32);
+  const uint64_t r = v & 0xFFFFFFFFull;
+  if (r != 0xFFFFFFFFull && e->launch_no - k < me_engine::ADM_RING)
+    b = std::min<uint64_t>(b, r + (e->adm_total - e->adm_at[k % me_engine::ADM_RING]));
+  return b;
+}
+
+// Admission of an n-record batch (me_config.max_resting). Usually one pinned read. When the bound is
+// too high the caller waits while two or more match launches are still ahead of the published count
+// (the device stays busy meanwhile), then takes an exact count (flush + sync). A batch that still
+// does not fit is refused with ME_E_CAPACITY before anything of it is enqueued: the books are
+// untouched and the engine stays usable (the error is not sticky).
+static int admit(me_engine* e, uint64_t n) {  // n: records of the batch that may rest
+  const uint64_t cap = e->cfg.max_resting;
+  if (admission_bound(e) + n > cap) {
+    for (;;) {
+      const unsigned long long v = __atomic_load_n(e->pub_host, __ATOMIC_ACQUIRE);
+      if (admission_bound(e) + n <= cap) break;
+      if (e->launch_no - (uint32_t)(v >> 32) < 2u || hipStreamQuery(e->stream) != hipErrorNotReady) {
+        // exact count of what the launches so far matched; batches still waiting for their match
+        // launch stay in the bound, so a group being filled is not cut short unless it must be
+        auto exact = [&]() -> int {
+          HIP_TRY(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
+          int rc2 = check_err_word(e);
+          if (rc2) return rc2;
+          uint64_t r = 0;
+          HIP_TRY(hipMemcpy(&r, e->bk.stats + ST_RESTING, 8, hipMemcpyDeviceToHost), "D2H resting count");
+          e->ovr_resting = r;
+          e->ovr_adm = e->adm_matched;
+          e->adm_syncs++;
+          return ME_OK;
+        };
+        int rc = exact();
+        if (rc) return rc;
+        if (admission_bound(e) + n <= cap) break;
+        rc = flush_pipeline(e);  // the pending batches matched too
+        if (rc) return rc;
+        rc = exact();
+        if (rc) return rc;
+        const uint64_t r = e->ovr_resting;
+        if (r + n > cap) {
+          e->err = "batch refused: " + std::to_string(r) + " resting orders + " + std::to_string(n) +
+                   " records could exceed max_resting (" + std::to_string(cap) + "); the books are unchanged";
+          return ME_E_CAPACITY;
+        }
+        break;
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+  }
+  e->adm_total += n;
+  return ME_OK;
+}
+
+extern "C" int me_admission_read(me_engine* e, uint64_t* resting, uint64_t* bound, uint64_t* exact_counts) {
+  if (!e) return ME_E_INVALID;
+  HIP_TRY(hipSetDevice(e->dev), "hipSetDevice");
+  if (resting) {
+    uint64_t r = 0;
+    HIP_TRY(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
+    HIP_TRY(hipMemcpy(&r, e->bk.stats + ST_RESTING, 8, hipMemcpyDeviceToHost), "D2H resting count");
+    *resting = r;
+  }
+  if (bound) *bound = admission_bound(e);
+  if (exact_counts) *exact_counts = e->adm_syncs;
+  return ME_OK;
+}
+
 extern "C" int me_submit_batch_device(me_engine* e, const me_order_soa* b, size_t n) {
   if (!e) return ME_E_INVALID;
   if (e->failed) return ME_E_STATE;
@@ -986,7 +1087,9 @@ extern "C" int me_submit_batch_device(me_engine* e, const me_order_soa* b, size_
   }
   if (n > e->cfg.max_batch) return e->fail(ME_E_INVALID, "batch larger than max_batch");
   HIP_TRY(hipSetDevice(e->dev), "hipSetDevice");
-  return enqueue_batch(e, b->seq, b->price_q4, b->qty, b->symbol, b->kind, (uint32_t)n);
+  const int rc = admit(e, n);  // the kinds are on the device: every record counts as a LIMIT
+  if (rc) return rc;
+  return enqueue_batch(e, b->seq, b->price_q4, b->qty, b->symbol, b->kind, (uint32_t)n, (uint32_t)n);
 }
 
 extern "C" int me_sync(me_engine* e) {
@@ -1093,7 +1196,11 @@ extern "C" int me_submit_host(me_engine* e, const me_order_soa* b, size_t n, uin
   const int slot = e->free_slots.back();
   HostSlot& h = e->hs[slot];
   HIP_TRY(hipSetDevice(e->dev), "hipSetDevice");
-  int rc = slot_alloc(e, h);
+  uint64_t n_rest = 0;  // only LIMIT records can rest (the kinds are on the host here)
+  for (size_t i = 0; i < n; ++i) n_rest += (b->kind[i] & 0x0Cu) == 0u;
+  int rc = admit(e, n_rest);
+  if (rc) return rc;
+  rc = slot_alloc(e, h);
   if (rc) return rc;
   uint64_t* seq;
   int64_t* px;
@@ -1128,7 +1235,7 @@ extern "C" int me_submit_host(me_engine* e, const me_order_soa* b, size_t n, uin
   slot_soa(h.d_in, n, seq, px, qty, sym, kind);
   e->free_slots.pop_back();
   e->by_ticket[h.ticket] = slot;
-  rc = enqueue_batch(e, seq, px, qty, sym, kind, (uint32_t)n, slot);
+  rc = enqueue_batch(e, seq, px, qty, sym, kind, (uint32_t)n, (uint32_t)n_rest, slot);
   if (rc) return rc;
   if (ticket) *ticket = e->next_ticket;
   e->next_ticket++;

@@ -317,6 +317,7 @@ struct WaveCtx {
   uint32_t nfar0, nfar1;     // far-level counts (me_far.hpp)
   unsigned long long horizon;  // seq-ring horizon of this launch
   uint32_t epoch;            // old-order table epoch of this launch
+  uint32_t resting0;         // the symbol's resting orders when the wave started
 #ifdef ME_STAMPS
   unsigned long long st[PH_N];
   unsigned long long st_t;
@@ -1130,6 +1131,7 @@ __device__ __forceinline__ bool wave_begin(WaveCtx& c, const BookDev& bk, const 
   prefetch_free_next(c);
   c.bump_cur = c.bump_end = 0;
   c.resting_delta = (int)rl32(st.resting, 0);  // becomes the new resting count
+  c.resting0 = rl32(st.resting, 0);
   c.scratch = bt.scratch;
   // scratch run of this wave: fills <= resting makers + 2 * records
   const unsigned long long need = (unsigned long long)rl32(st.resting, 0) + 2ull * (hi - lo);
@@ -1157,6 +1159,8 @@ __device__ __forceinline__ void wave_end(WaveCtx& c) {
     o.nfar[1] = c.nfar1;
     for (int k = 0; k < 5; ++k) o.pad[k] = 0;
     c.bk.sym[c.s] = o;
+    const long long d = (long long)(uint32_t)c.resting_delta - (long long)c.resting0;
+    if (d) atomicAdd(c.bk.stats + ST_RESTING, (unsigned long long)d);
   }
 #ifdef ME_STAMPS
   STAMP_ADD(c, PH_EPILOGUE);
@@ -1240,6 +1244,7 @@ struct SeqGroup {
   uint32_t n[ME_GMAX];
   uint32_t ng;
   uint32_t in;  // state index read; the kernel writes state[in ^ 1]
+  uint32_t launch;  // match launches enqueued before this group's (all finished when this runs)
 };
 
 __global__ __launch_bounds__(256) void k_seq_sweep(BookDev bk, SeqGroup sg) {
@@ -1263,6 +1268,10 @@ __global__ __launch_bounds__(256) void k_seq_sweep(BookDev bk, SeqGroup sg) {
     o.pad[0] = o.pad[1] = o.pad[2] = 0;
     bk.sq[sg.in ^ 1u] = o;
     *bk.hcount = 0;  // the match launch after this one hands symbols off from 0
+    if (bk.pub) {  // resting orders after sg.launch match launches, for the host's admission bound
+      const unsigned long long r = bk.stats[ST_RESTING];
+      *bk.pub = ((unsigned long long)sg.launch << 32) | (r < 0xFFFFFFFFull ? r : 0xFFFFFFFFull);
+    }
   }
   if (!need) return;
   const uint32_t top = min(*bk.chunk_top, bk.nchunks);
@@ -1430,7 +1439,7 @@ hipError_t launch_match(hipStream_t st, const BookDev& bk, const BatchDev& bt, h
 // The seq-ring horizon check (and, when due, the old-order table rebuild) ahead of a match launch
 // over batches seq[0..ng) (n[g] > 0 each). Reads state in_idx, writes state in_idx ^ 1.
 hipError_t launch_seq_sweep(hipStream_t st, const BookDev& bk, const uint64_t* const* seq, const uint32_t* n,
-                            uint32_t ng, uint32_t in_idx, uint32_t grid) {
+                            uint32_t ng, uint32_t in_idx, uint32_t grid, uint32_t launch) {
   if (ng == 0 || ng > (uint32_t)ME_GMAX) return hipErrorInvalidValue;
   SeqGroup sg{};
   for (uint32_t g = 0; g < ng; ++g) {
@@ -1440,6 +1449,7 @@ hipError_t launch_seq_sweep(hipStream_t st, const BookDev& bk, const uint64_t* c
   }
   sg.ng = ng;
   sg.in = in_idx;
+  sg.launch = launch;
   hipLaunchKernelGGL(k_seq_sweep, dim3(grid ? grid : 1), dim3(256), 0, st, bk, sg);
   return hipGetLastError();
 }

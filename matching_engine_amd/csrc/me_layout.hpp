@@ -142,7 +142,9 @@ struct Handoff {
 };
 
 // Event counters kept on the device (BookDev::stats, me_stats_read).
-enum : uint32_t { ST_HANDOFFS = 0, ME_STATS = 8 };
+// ST_RESTING: resting orders of every symbol (each wave adds its symbol's change when it writes the
+// symbol state back); k_seq_sweep publishes it to the host for admission control (me_engine.cpp).
+enum : uint32_t { ST_HANDOFFS = 0, ST_RESTING = 1, ME_STATS = 8 };
 
 struct BookDev {
   Level* levels;
@@ -162,6 +164,7 @@ struct BookDev {
   uint32_t* hcount;       // hand-offs of the current match launch (zeroed by k_seq_sweep)
   Handoff* hand;          // [S]
   unsigned long long* stats;  // [ME_STATS] event counters (me_stats_read)
+  unsigned long long* pub;    // host-mapped {launches << 32 | resting} (k_seq_sweep), or null
   unsigned long long ring_mask;
   unsigned long long old_mask;
   uint32_t fcap;

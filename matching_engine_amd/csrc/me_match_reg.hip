@@ -57,7 +57,7 @@ struct RegLds {
   uint32_t cnext[RL];  // chunks[head].hdr.next of the cached head (kept in step with HBM)
   uint32_t free_head;  // overflow free list in HBM (hdr.next links), NIL if empty
   uint32_t bump_cur, bump_end;  // chunk ids reserved from the global bump allocator
-  uint32_t pad;
+  uint32_t resting0;  // the symbol's resting orders when the wave started (ST_RESTING delta)
   uint32_t scan_cur, scan_cnt, scan_pos;  // rescan of an overfull bucket: next batch index, list fill, list read
   uint32_t mode;  // record source: 0 bucket, 1 rescan, 2 sort path (perm run [run_lo, run_lo + run_n))
   uint32_t g_cur, g_next;  // batch of the group being matched (its outputs: G.bt[g_cur]), the next one
@@ -1232,6 +1232,7 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
     const SeqState sqs = bk.sq[bk.sq_idx];
     if (lane == 0) {
       c.M->free_head = st.free_head;
+      c.M->resting0 = st.resting;
       c.M->bump_cur = 0;
       c.M->bump_end = 0;
       c.M->nfar[0] = st.nfar[0];
@@ -1573,6 +1574,8 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
     so.nfar[1] = nf1;
     for (int k = 0; k < 5; ++k) so.pad[k] = 0;
     ldsg(G.bk.sym)[s] = so;
+    const long long d = (long long)(uint32_t)c.resting - (long long)c.M->resting0;
+    if (d) atomicAdd(ldsg(G.bk.stats) + ST_RESTING, (unsigned long long)d);
   }
 #ifdef ME_STAMPS
   __builtin_amdgcn_s_waitcnt(0);

@@ -316,6 +316,13 @@ class Engine:
         _check(self.lib, self.h, self.lib.me_stats_read(self.h, C.byref(h)))
         return {"handoffs": h.value}
 
+    def admission(self) -> dict:
+        """Admission control (me_admission_read): device resting count after all enqueued work, the
+        host's current bound, and how many submits had to take an exact count."""
+        r, b, x = C.c_uint64(0), C.c_uint64(0), C.c_uint64(0)
+        _check(self.lib, self.h, self.lib.me_admission_read(self.h, C.byref(r), C.byref(b), C.byref(x)))
+        return {"resting": r.value, "bound": b.value, "exact_counts": x.value}
+
     # -- timing
     def timing_enable(self, period: int = 1):
         """HIP events on every `period`-th match launch (True = every launch, 0/False = off)."""

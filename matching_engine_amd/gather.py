@@ -95,21 +95,56 @@ def gather_batch(tape, n_fills: int, results, positions, n_local: int, n_global:
 
 class EngineGather:
     """RCCL gather of one engine's batch outputs: device staging buffers sized for the engine, the
-    engine's tape / results copied into them device-to-device, then gather_batch."""
+    engine's tape / results copied into them device-to-device, then gather_batch.
 
-    def __init__(self, engine, device, max_batch: int, dst: int = 0, group=None):
+    With `stream` (a torch stream the engine runs on: engine.set_stream(stream.cuda_stream)) the
+    gather of batch k overlaps the match of batch k+1:
+
+        engine.submit_device(b[0])
+        for k: nf = g.stage(n[k]); engine.submit_device(b[k + 1]); out = g.collect(nf, n[k], ...)
+
+    stage() waits for batch k only and queues the staging copies on the engine stream; torch's
+    current stream (where the collectives are ordered) waits for those copies through an event, not
+    for the match launched after them. Without `stream`, stage() synchronises the engine."""
+
+    def __init__(self, engine, device, max_batch: int, dst: int = 0, group=None, stream=None):
         import torch
 
         self.engine = engine
         self.dst = dst
         self.group = group
+        self.stream = stream
         self.cap = engine.fill_bound(max_batch)
         self.tape = torch.empty(self.cap * FILL_BYTES, dtype=torch.uint8, device=device)
         self.res = torch.empty(max(max_batch, 1) * RESULT_BYTES, dtype=torch.uint8, device=device)
 
-    def gather(self, n_local: int, positions, n_global: int):
-        """After a batch of n_local records: -> (global tape, global results) on dst."""
+    def stage(self, n_local: int) -> int:
+        """The most recent batch's tape and results into the staging buffers; returns its fills."""
+        import torch
+
         nf = self.engine.copy_tape_device(self.tape.data_ptr(), self.cap)
         self.engine.copy_results_device(self.res.data_ptr(), n_local)
-        self.engine.sync()  # the copies ran on the engine stream; the collectives run on torch's
-        return gather_batch(self.tape, nf, self.res, positions, n_local, n_global, self.dst, self.group)
+        if self.stream is not None:
+            torch.cuda.current_stream(self.tape.device).wait_stream(self.stream)
+        else:
+            self.engine.sync()
+        return nf
+
+    def collect(self, nf: int, n_local: int, positions, n_global: int):
+        """The staged batch of every rank -> (global tape, global results) on dst. Returns after the
+        staging buffers were read, so the next stage() may overwrite them."""
+        import torch
+
+        out = gather_batch(self.tape, nf, self.res, positions, n_local, n_global, self.dst, self.group)
+        # the payload copies out of the staging buffers were queued on torch's current stream (and
+        # return at once off the root): the engine's next staging copies wait for them
+        cur = torch.cuda.current_stream(self.tape.device)
+        if self.stream is not None:
+            self.stream.wait_stream(cur)
+        else:
+            cur.synchronize()
+        return out
+
+    def gather(self, n_local: int, positions, n_global: int):
+        """After a batch of n_local records: -> (global tape, global results) on dst."""
+        return self.collect(self.stage(n_local), n_local, positions, n_global)

@@ -65,6 +65,8 @@ def run_both(eng, orc, batches, check_books=True, book_symbols=None, ctx=""):
         syms = range(eng.num_symbols) if book_symbols is None else book_symbols
         assert_books_equal(eng, orc, syms, ctx)
         assert eng.resting_count() == orc.resting(), f"{ctx}: resting count"
+        if hasattr(eng, "admission"):  # the device-wide counter admission control reads
+            assert eng.admission()["resting"] == orc.resting(), f"{ctx}: ST_RESTING counter"
     return total
 
 

@@ -49,22 +49,33 @@ def main():
 
             from matching_engine_amd.gather import EngineGather
 
-            gath = EngineGather(book, torch.device("cuda", 0), sc.batch)
+            ts = torch.cuda.Stream(device=torch.device("cuda", 0))
+            book.set_stream(ts.cuda_stream)  # the gather of batch k overlaps the match of k + 1
+            gath = EngineGather(book, torch.device("cuda", 0), sc.batch, stream=ts)
     else:
         book = OracleBook(len(ids), symbol_ids=ids)
         submit = book.submit
     ref = OracleBook(S) if rank == 0 else None
     ok, fills_total = True, 0
     msg = ""
+    batches = []
     for k in range(nb):
         b = st.next(sc.batch)
         # a few out-of-range symbol ids too: rejected as BAD_SYMBOL on shard 0
         if k == 1:
             b.symbol[::997] = S + 5
-        lb, pos = plan.split(b)[rank]
-        if gath is not None:  # device-resident batch, the engine's outputs staged device to device
-            db = book.upload(lb)
-            book.submit_device(db)
+        batches.append(b)
+    splits = [plan.split(b)[rank] for b in batches]
+    dbs = [book.upload(lb) for lb, _ in splits] if gath is not None else None
+    if gath is not None:  # device-resident batches, the engine's outputs staged device to device
+        book.submit_device(dbs[0])
+    for k in range(nb):
+        b = batches[k]
+        lb, pos = splits[k]
+        if gath is not None:
+            nf = gath.stage(len(lb))
+            if k + 1 < nb:
+                book.submit_device(dbs[k + 1])  # matches while batch k is gathered
         else:
             r, f = submit(lb)
         if engine_kind in ("gather", "gpu_gather"):
@@ -74,8 +85,7 @@ def main():
 
             post = torch.from_numpy(pos.astype(np.int64))
             if gath is not None:
-                tape, res = gath.gather(len(lb), post, len(b))
-                db.free()
+                tape, res = gath.collect(nf, len(lb), post, len(b))
             else:
                 tape, res = gather_batch(torch.from_numpy(f.view(np.uint8).copy()), len(f),
                                          torch.from_numpy(r.view(np.uint8).copy()), post, len(lb), len(b))
@@ -94,6 +104,11 @@ def main():
             if ok and not (same_t and same_r):  # keep going: every rank must reach every collective
                 ok = False
                 msg = f"batch {k}: tape equal {same_t}, results equal {same_r}"
+    if dbs is not None:
+        book.sync()
+        book.set_stream(None)
+        for db in dbs:
+            db.free()
     if rank == 0:
         json.dump({"ok": ok, "msg": msg, "fills": fills_total, "world": world}, open(out_path, "w"))
     dist.barrier()

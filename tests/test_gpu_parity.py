@@ -363,9 +363,11 @@ def test_cancelled_chunks_are_unlinked(me, orc):
 
 
 def test_capacity_exhaustion_is_loud(me):
+    """Pools sized below what a batch needs (within max_resting, so admission lets it in) fail the
+    engine loudly and stickily; tests/test_admission.py covers the refusals that are not sticky."""
     B, L = me.SIDE_BUY, me.TYPE_LIMIT
     rows = [(0, B, L, 0, 1000 + (k % 64), 1) for k in range(200)]  # 64 levels -> needs >= 64 chunks
-    with engine_for(me, 1, 128, [1000], 256, 16, max_chunks=8) as eng:
+    with engine_for(me, 1, 128, [1000], 256, 256, max_chunks=8) as eng:
         with pytest.raises(me.EngineError, match="chunk pool"):
             eng.submit_batch(_rows(me, rows))
         with pytest.raises(me.EngineError):
@@ -427,7 +429,9 @@ def test_every_batch_of_full_groups(me, orc, group):
     st = me.Stream(sc)
     base = st.base_prices()
     ob = orc.OracleBook(sc.num_symbols)
-    with engine_for(me, sc.num_symbols, sc.levels, base, sc.batch, 1 << 21, seq_ring=1 << 26,
+    # admission control counts every record of a device batch as a possible rest: size max_resting
+    # for both groups in flight so no submit has to cut a group short
+    with engine_for(me, sc.num_symbols, sc.levels, base, sc.batch, (2 * group + 2) * sc.batch, seq_ring=1 << 26,
                     batches_per_launch=group) as eng:
         for gi in range(2):
             batches = [st.next(sc.batch) for _ in range(group)]
@@ -489,7 +493,8 @@ def test_back_to_back_device_batches(me, orc, group, stream):
         for k, b in enumerate(batches):
             b.symbol[k * 97 % len(b)::4099] = sc.num_symbols + 3  # unknown symbols
     ob = orc.OracleBook(sc.num_symbols)
-    with engine_for(me, sc.num_symbols, sc.levels, base, sc.batch, 1 << 20, batches_per_launch=group) as eng:
+    with engine_for(me, sc.num_symbols, sc.levels, base, sc.batch, (len(batches) + 1) * sc.batch,
+                    batches_per_launch=group) as eng:
         dbs = [eng.upload(b) for b in batches]
         eng.timing_enable(True)
         for db in dbs:
