@@ -12,6 +12,8 @@ env: RANK, WORLD_SIZE, MASTER_ADDR, MASTER_PORT; argv: ENGINE(oracle|gpu|gather|
   gpu_gather: HIP engine shards, outputs staged device-to-device (EngineGather) and gathered with
               gather_batch (gloo stages the device tensors through the host; one GPU cannot host
               two RCCL ranks)
+  rccl_gather: gpu_gather over the nccl (RCCL) backend with device tensors — world size 1 on the
+              one-GPU box: the RCCL all_gather / gather calls and the overlapped staging run for real
 """
 import json
 import os
@@ -32,7 +34,14 @@ def main():
     from oracle.oracle import OracleBook
 
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if engine_kind == "rccl_gather":
+        import torch
+
+        torch.cuda.set_device(0)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", 0))
+        engine_kind = "gpu_gather"
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     S, nb = 300, 5
     sc = me.preset(5, num_symbols=S, batch=6000)
     st = me.Stream(sc)
@@ -84,6 +93,8 @@ def main():
             from matching_engine_amd.gather import gather_batch
 
             post = torch.from_numpy(pos.astype(np.int64))
+            if dist.get_backend() == "nccl":
+                post = post.to("cuda:0")
             if gath is not None:
                 tape, res = gath.collect(nf, len(lb), post, len(b))
             else:

@@ -71,6 +71,16 @@ def test_two_rank_tape_gather_gpu_engines(built, tmp_path):
     assert r["fills"] > 0
 
 
+@pytest.mark.gpu
+def test_rccl_gather_single_rank(built, tmp_path):
+    """The gather over the nccl backend (RCCL) with device tensors, world size 1 (the box has one
+    GPU): all_gather of sizes, gather of tapes and results, the overlapped staging on the engine's
+    stream — the code path an 8-GPU node runs, minus the xGMI hops."""
+    r = _run("rccl_gather", 1, tmp_path)
+    assert r["ok"], r["msg"]
+    assert r["fills"] > 0
+
+
 def test_two_rank_sharded_service_db_equals_single_engine(built, tmp_path):
     """SubmitOrder on rank 0 over two shards (cluster.ShardedMatcher, gloo): every
     slice's merged tape/results, the SQLite rows, the per-order books, market data and the gathered
