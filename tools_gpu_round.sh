@@ -20,8 +20,7 @@ tail -1 $O/smoke.log
 B="python3 $R/bench.py --steps 320 --warmup 32 --no-cpu-baseline --no-e2e"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d $O/prof_kt -o kt -- $B > $O/prof_kt.log 2>&1 || { echo PROF_FAIL; tail -20 $O/prof_kt.log; exit 1; }
 python3 $R/tools/trace_gaps.py $O/prof_kt > $O/trace_gaps.txt && cat $O/trace_gaps.txt
-timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_match --output-format csv -d $O/fetch -o pmc -- $B > $O/fetch.log 2>&1 || { echo PMC_FAIL fetch; tail -5 $O/fetch.log; exit 1; }
-timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_match --output-format csv -d $O/write -o pmc -- $B > $O/write.log 2>&1 || { echo PMC_FAIL write; tail -5 $O/write.log; exit 1; }
-python3 $R/tools/pmc_traffic.py $O/fetch $O/write > $O/traffic.json && cat $O/traffic.json
+bash $R/tools/gpu_pmc_traffic.sh $TAG/traffic || { echo PMC_FAIL; exit 1; }
+cp $O/traffic/traffic.json $O/traffic.json
 timeout -k 10 600 python bench.py --traffic-from $O/traffic.json > $O/bench.json 2> $O/bench.err || { echo BENCH_FAIL; tail -20 $O/bench.err; exit 1; }
 cat $O/bench.json
