@@ -78,7 +78,7 @@ def parse():
                     help="threads of the sharded CPU baseline (the GPU box's CPU share is 16); 1 = scalar only")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
-    ap.add_argument("--e2e-steps", type=int, default=192,
+    ap.add_argument("--e2e-steps", type=int, default=384,
                     help="batches through the pipelined host path (me_submit_host/me_collect) after the timed loop")
     ap.add_argument("--timing-every", type=int, default=4,
                     help="HIP events on every k-th match launch of the timed loop (each timed launch costs "

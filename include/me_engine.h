@@ -110,7 +110,7 @@ typedef struct me_config {
   uint32_t far_levels;         /* capacity per symbol and side of the far arrays (price levels outside the
                                   window), 0 = 1024 */
   uint32_t host_slots;         /* pinned slots of the host-batch pipeline (me_submit_host), 0 = enough to keep
-                                  three launch groups in flight (3 * batches_per_launch + 1); allocated on use */
+                                  four launch groups in flight (4 * batches_per_launch + 1); allocated on use */
   uint64_t host_tape_cap;      /* fills a slot holds (0 = 2 * max_batch + 4096). A longer tape is recovered at
                                   me_collect while its batch's scratch is intact (collected before 3 further
                                   launch groups were submitted), else that collect fails with ME_E_CAPACITY */
@@ -180,7 +180,8 @@ uint64_t me_fill_bound(const me_engine* e, size_t n);
  * me_submit_host stages the batch in the next of the engine's pinned slots (skipped when the batch
  * already lives there, see me_host_inputs), copies it to HBM on the engine's H2D stream and enqueues
  * it behind everything submitted before; it returns at once with a ticket (0, 1, 2, ...). The H2D of
- * batch k+1, the match of batch k and the D2H of batch k-1 (results + tape, on a D2H stream) overlap.
+ * batch k+1, the match of batch k and the PCIe writes of batch k-1's results and tape (by the tape
+ * job, straight into the slot's pinned block) overlap.
  * me_collect waits for the ticket's batch (launching a partial group first when it is still waiting
  * for one) and points into the slot's pinned outputs: valid until the slot is reused by ticket +
  * host_slots. A slot is reused only after its ticket was collected (else ME_E_STATE). Not

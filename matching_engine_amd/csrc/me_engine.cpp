@@ -137,8 +137,8 @@ class CopyPool {
   bool stop_ = false;
 };
 
-// Output block of a host slot (same layout in HBM and in pinned memory): SlotMeta, the tape (cap
-// records), the results (max_batch records).
+// Output block of a host slot in pinned memory: SlotMeta, the results (max_batch records), the tape
+// (cap records, 64-B aligned). The tape job writes all of it straight over PCIe (device-mapped).
 struct SlotMeta {
   unsigned long long count;  // the batch's tape length (may exceed the slot's cap)
   uint32_t err;              // the device error word when the tape job finished
@@ -153,9 +153,8 @@ struct HostSlot {
   char* h_out = nullptr;  // pinned outputs (SlotMeta | tape | results): the tape job writes the meta and
                           // the tape straight into it over PCIe; the results arrive by DMA
   char* h_out_dev = nullptr;  // h_out as the device addresses it
-  char* d_out = nullptr;  // HBM: the results the tape job finalises (DMA source, spill input)
   hipEvent_t ev_in = nullptr;    // H2D done (H2D stream)
-  hipEvent_t ev_done = nullptr;  // outputs in pinned memory (D2H stream)
+  hipEvent_t ev_done = nullptr;  // outputs in pinned memory (recorded after the launch with the tape job)
   uint64_t ticket = 0;
   uint32_t n = 0;
   int state = 0;  // 0 free (collected), 1 enqueued, 2 outputs copy enqueued
@@ -238,8 +237,7 @@ struct me_engine {
   std::unordered_map<uint64_t, int> by_ticket;  // uncollected tickets -> slot
   uint64_t hcap = 0;         // tape records per slot
   uint64_t next_ticket = 0;
-  hipStream_t s_h2d = nullptr, s_d2h = nullptr;
-  hipEvent_t ev_tape = nullptr;  // a launch that compacted host tapes finished (the D2H stream waits on it)
+  hipStream_t s_h2d = nullptr;
   std::vector<uint64_t> oset_gen;  // batches assigned to each output set so far
   me_fill* d_spill = nullptr;
   size_t spill_cap = 0;
@@ -338,7 +336,6 @@ static void free_all(me_engine* e) {
     if (h.h_in) (void)hipHostFree(h.h_in);
     if (h.h_out) (void)hipHostFree(h.h_out);
     if (h.d_in) (void)hipFree(h.d_in);
-    if (h.d_out) (void)hipFree(h.d_out);
     if (h.ev_in) (void)hipEventDestroy(h.ev_in);
     if (h.ev_done) (void)hipEventDestroy(h.ev_done);
   }
@@ -350,9 +347,7 @@ static void free_all(me_engine* e) {
       if (p) (void)hipFree(p);
   }
   if (e->pub_host) (void)hipHostFree(e->pub_host);
-  if (e->ev_tape) (void)hipEventDestroy(e->ev_tape);
   if (e->s_h2d) (void)hipStreamDestroy(e->s_h2d);
-  if (e->s_d2h) (void)hipStreamDestroy(e->s_d2h);
   for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
   e->ev_pool.clear();
   e->timed.clear();
@@ -608,16 +603,16 @@ extern "C" me_engine* me_create(const me_config* cfg) {
   if (!ok) return bail(std::string("me_create: book init failed: ") + hipGetErrorString(hipGetLastError()));
   // host-batch pipeline: slots are allocated on first use
   {
-    uint64_t H = cfg->host_slots ? cfg->host_slots : 3ull * e->group + 1;
+    // 4G + 1: a synchronous-lag caller keeps submitting the group after next while the launch that
+    // finishes an old group's tapes runs (3G + 1 serialised them: 372M vs 455M orders/s at G = 32)
+    uint64_t H = cfg->host_slots ? cfg->host_slots : 4ull * e->group + 1;
     if (H > 4096) return bail("me_create: host_slots exceeds 4096");
     e->hs.resize(H);
     for (uint64_t k = H; k-- > 0;) e->free_slots.push_back((int)k);
     e->hcap = cfg->host_tape_cap ? cfg->host_tape_cap : 2 * n + 4096;
     e->oset_gen.assign(e->nsets, 0);
-    if ((he = hipStreamCreateWithFlags(&e->s_h2d, hipStreamNonBlocking)) != hipSuccess ||
-        (he = hipStreamCreateWithFlags(&e->s_d2h, hipStreamNonBlocking)) != hipSuccess ||
-        (he = hipEventCreateWithFlags(&e->ev_tape, hipEventDisableTiming)) != hipSuccess)
-      return bail(std::string("me_create: host pipeline streams: ") + hipGetErrorString(he));
+    if ((he = hipStreamCreateWithFlags(&e->s_h2d, hipStreamNonBlocking)) != hipSuccess)
+      return bail(std::string("me_create: host pipeline stream: ") + hipGetErrorString(he));
   }
   // the configuration as resolved (me_get_config)
   e->cfg.max_chunks = nchunks;
@@ -636,7 +631,6 @@ extern "C" void me_destroy(me_engine* e) {
   (void)hipSetDevice(e->dev);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   if (e->s_h2d) (void)hipStreamSynchronize(e->s_h2d);
-  if (e->s_d2h) (void)hipStreamSynchronize(e->s_d2h);
   free_all(e);
   delete e;
 }
@@ -706,10 +700,11 @@ static int seq_sweep(me_engine* e, const me_engine::Group& g) {
 
 // ---- host slots ---------------------------------------------------------------------------
 static size_t slot_in_bytes(uint64_t n) { return (size_t)n * (8 + 8 + 4 + 4 + 1); }
-static size_t slot_res_off(const me_engine* e) { return sizeof(SlotMeta) + (size_t)e->hcap * sizeof(me_fill); }
-static size_t slot_out_bytes(const me_engine* e) {
-  return slot_res_off(e) + (size_t)e->cfg.max_batch * sizeof(me_order_result);
+static size_t slot_res_off(const me_engine*) { return sizeof(SlotMeta); }
+static size_t slot_tape_off(const me_engine* e) {
+  return (sizeof(SlotMeta) + (size_t)e->cfg.max_batch * sizeof(me_order_result) + 63) & ~(size_t)63;
 }
+static size_t slot_out_bytes(const me_engine* e) { return slot_tape_off(e) + (size_t)e->hcap * sizeof(me_fill); }
 // The packed SoA of an n-record batch at base p.
 static void slot_soa(char* p, uint64_t n, uint64_t*& seq, int64_t*& px, int32_t*& qty, uint32_t*& sym,
                      uint8_t*& kind) {
@@ -723,11 +718,11 @@ static void slot_soa(char* p, uint64_t n, uint64_t*& seq, int64_t*& px, int32_t*
 // view), the finalised results into HBM.
 static void slot_outputs(me_engine* e, HostSlot& h, me_fill*& tape, unsigned long long*& count,
                          me_order_result*& res, uint32_t*& err) {
-  SlotMeta* m = (SlotMeta*)h.h_out_dev;
+  SlotMeta* m = (SlotMeta*)h.h_out_dev;  // the slot's pinned block as the device addresses it
   count = &m->count;
   err = &m->err;
-  tape = (me_fill*)(h.h_out_dev + sizeof(SlotMeta));
-  res = (me_order_result*)h.d_out;
+  tape = (me_fill*)(h.h_out_dev + slot_tape_off(e));
+  res = (me_order_result*)(h.h_out_dev + slot_res_off(e));
 }
 static int slot_alloc(me_engine* e, HostSlot& h) {
   if (h.h_in) return ME_OK;
@@ -735,7 +730,6 @@ static int slot_alloc(me_engine* e, HostSlot& h) {
   HIP_TRY(hipHostMalloc((void**)&h.h_in, in, hipHostMallocDefault), "hipHostMalloc slot inputs");
   HIP_TRY(hipHostMalloc((void**)&h.h_out, out, hipHostMallocDefault), "hipHostMalloc slot outputs");
   HIP_TRY(hipMalloc((void**)&h.d_in, in), "hipMalloc slot inputs");
-  HIP_TRY(hipMalloc((void**)&h.d_out, (size_t)e->cfg.max_batch * sizeof(me_order_result)), "hipMalloc slot results");
   HIP_TRY(hipHostGetDevicePointer((void**)&h.h_out_dev, h.h_out, 0), "hipHostGetDevicePointer");
   HIP_TRY(hipEventCreateWithFlags(&h.ev_in, hipEventDisableTiming), "hipEventCreate");
   HIP_TRY(hipEventCreateWithFlags(&h.ev_done, hipEventDisableTiming), "hipEventCreate");
@@ -745,14 +739,14 @@ static int slot_alloc(me_engine* e, HostSlot& h) {
 // memory once it completes): the D2H stream waits for it and copies each slot's results into pinned
 // memory. Nothing later on the engine stream writes those blocks before the slot is collected.
 static int enqueue_host_d2h(me_engine* e, const int* slots, int ns) {
-  HIP_TRY(hipEventRecord(e->ev_tape, e->stream), "hipEventRecord");
-  HIP_TRY(hipStreamWaitEvent(e->s_d2h, e->ev_tape, 0), "hipStreamWaitEvent");
+  // The tape job wrote each slot's count, error word, results and tape straight into its pinned
+  // block (device-mapped): the launch's completion is the slots' completion. Measured against the
+  // alternatives (tools/e2e_probe.py, config 2, G = 32, 129-193 slots): an HBM block moved by one
+  // hipMemcpyAsync per slot (the runtime runs device-to-pinned copies as blit kernels, ~30 us of
+  // host time per call) or by one copy kernel per launch gave the same 470-500M orders/s.
   for (int k = 0; k < ns; ++k) {
     HostSlot& h = e->hs[slots[k]];
-    HIP_TRY(hipMemcpyAsync(h.h_out + slot_res_off(e), h.d_out, (size_t)h.n * sizeof(me_order_result),
-                           hipMemcpyDeviceToHost, e->s_d2h),
-            "D2H slot results");
-    HIP_TRY(hipEventRecord(h.ev_done, e->s_d2h), "hipEventRecord");
+    HIP_TRY(hipEventRecord(h.ev_done, e->stream), "hipEventRecord");
     h.state = 2;
   }
   return ME_OK;
@@ -1005,6 +999,20 @@ static int check_err_word(me_engine* e) {
   return check_err_bits(e, w);
 }
 
+// Records of kind LIMIT-new (neither the MARKET nor the CANCEL bit), eight kind bytes per step.
+static uint64_t count_limits(const uint8_t* kind, size_t n) {
+  uint64_t other = 0;
+  size_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t w;
+    memcpy(&w, kind + i, 8);
+    const uint64_t x = (w >> 2) & 0x0303030303030303ull;  // the MARKET and CANCEL bits of each byte
+    other += (uint64_t)__builtin_popcountll((x | (x >> 1)) & 0x0101010101010101ull);
+  }
+  for (; i < n; ++i) other += (kind[i] & 0x0Cu) != 0u;
+  return (uint64_t)n - other;
+}
+
 // Upper bound on the resting orders once every accepted record has been matched.
 static uint64_t admission_bound(const me_engine* e) {
   uint64_t b = e->ovr_resting + (e->adm_total - e->ovr_adm);
@@ -1196,8 +1204,7 @@ extern "C" int me_submit_host(me_engine* e, const me_order_soa* b, size_t n, uin
   const int slot = e->free_slots.back();
   HostSlot& h = e->hs[slot];
   HIP_TRY(hipSetDevice(e->dev), "hipSetDevice");
-  uint64_t n_rest = 0;  // only LIMIT records can rest (the kinds are on the host here)
-  for (size_t i = 0; i < n; ++i) n_rest += (b->kind[i] & 0x0Cu) == 0u;
+  const uint64_t n_rest = count_limits(b->kind, n);  // only LIMIT records can rest (kinds are on the host)
   int rc = admit(e, n_rest);
   if (rc) return rc;
   rc = slot_alloc(e, h);
@@ -1215,7 +1222,11 @@ extern "C" int me_submit_host(me_engine* e, const me_order_soa* b, size_t n, uin
     if (n < 16384) {
       for (const auto& c : cols) memcpy(c.dst, c.src, c.bytes);
     } else {  // 64-KB pieces over the copy threads
-      if (!e->copy_pool) e->copy_pool.reset(new CopyPool(4));
+      if (!e->copy_pool) {
+        const char* v = getenv("ME_COPY_THREADS");
+        const int nt = v ? std::max(1, std::min(32, atoi(v))) : 4;
+        e->copy_pool.reset(new CopyPool(nt));
+      }
       std::vector<CopyPool::Piece> pieces;
       for (const auto& c : cols)
         for (size_t o = 0; o < c.bytes; o += 65536)
@@ -1266,7 +1277,7 @@ extern "C" int me_collect(me_engine* e, uint64_t ticket, const me_fill** fills, 
     if (rc) return rc;
   }
   const uint64_t cnt = m->count;
-  me_fill* tape = (me_fill*)(h.h_out + sizeof(SlotMeta));
+  me_fill* tape = (me_fill*)(h.h_out + slot_tape_off(e));
   if (cnt > e->hcap) {  // past the slot: the spill from scratch
     if (e->oset_gen[h.oset] != h.oset_gen) {  // this batch's output is lost; the books are intact (not sticky)
       e->err = "host batch tape (" + std::to_string(cnt) + " fills) outgrew host_tape_cap and its scratch was "
@@ -1282,7 +1293,8 @@ extern "C" int me_collect(me_engine* e, uint64_t ticket, const me_fill** fills, 
       e->spill_cap = extra;
     }
     const auto& o = e->os[h.oset];
-    hipError_t he = launch_tape_spill(e->stream, (const me_order_result*)h.d_out, o.fstart, h.n, o.scratch, e->hcap,
+    hipError_t he = launch_tape_spill(e->stream, (const me_order_result*)(h.h_out_dev + slot_res_off(e)), o.fstart,
+                                      h.n, o.scratch, e->hcap,
                                       e->d_spill);
     if (he != hipSuccess) return e->hip_fail(he, "spill launch");
     HIP_TRY(hipStreamSynchronize(e->stream), "hipStreamSynchronize");

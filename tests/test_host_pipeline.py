@@ -56,12 +56,12 @@ def _pipelined(me, eng, batches, lag, zero_copy_every=0):
     return out
 
 
-@pytest.mark.parametrize("levels,group,lag", [(128, 4, 1), (128, 4, 12), (128, 32, 96), (512, 1, 3)])
+@pytest.mark.parametrize("levels,group,lag", [(128, 4, 1), (128, 4, 12), (128, 32, 96), (128, 8, 32), (512, 1, 3)])
 def test_host_pipeline_every_batch(me, orc, levels, group, lag):
     sc, base, batches = _stream(me, 2, 40, num_symbols=64, levels=levels, batch=2048)
     ob = orc.OracleBook(sc.num_symbols)
     with _engine(me, sc, base, batches, batches_per_launch=group) as eng:
-        assert eng.config()["host_slots"] == 3 * eng.config()["batches_per_launch"] + 1
+        assert eng.config()["host_slots"] == 4 * eng.config()["batches_per_launch"] + 1
         outs = _pipelined(me, eng, batches, lag, zero_copy_every=3)
         for k, b in enumerate(batches):
             ro, fo = ob.submit(b)
@@ -84,6 +84,42 @@ def test_host_tape_longer_than_slot(me, orc, levels):
             spilled += len(fo) > 64
         assert_books_equal(eng, ob, range(sc.num_symbols), "spill")
     assert spilled >= 6
+
+
+def test_host_tape_longer_than_batch(me, orc):
+    """Sweeping MARKETs give batches with more fills than records: the slot's DMA carries the first
+    n fills, me_collect copies the rest from the slot's HBM block (below host_tape_cap, no spill)."""
+    sc, base, _ = _stream(me, 2, 0, num_symbols=16, batch=1024)
+    rng = np.random.default_rng(4)
+    batches, seq = [], 1
+    for k in range(12):
+        if k % 2 == 0:  # 1,024 one-lot LIMITs on both sides, 1..40 ticks from the mid
+            n = 1024
+            side = rng.integers(1, 3, n)
+            off = rng.integers(1, 41, n)
+            sym = rng.integers(0, 16, n)
+            px = base[sym] + 64 + np.where(side == 1, -off, off)
+            kind = [me.kind(int(s)) for s in side]
+            qty = np.ones(n, np.int32)
+        else:  # 48 MARKETs of 40 lots: ~2,000 fills from 48 records
+            n = 48
+            side = rng.integers(1, 3, n)
+            sym = rng.integers(0, 16, n)
+            px = np.zeros(n, np.int64)
+            kind = [me.kind(int(s), me.TYPE_MARKET) for s in side]
+            qty = np.full(n, 40, np.int32)
+        batches.append(me.Batch(np.arange(seq, seq + n, dtype=np.uint64), px, qty, sym, kind))
+        seq += n
+    ob = orc.OracleBook(sc.num_symbols)
+    longer = 0
+    with _engine(me, sc, base, batches, batches_per_launch=4) as eng:
+        for k, (r, f) in enumerate(_pipelined(me, eng, batches, lag=3)):
+            ro, fo = ob.submit(batches[k])
+            assert_results_equal(r, ro, f"long tape batch {k}")
+            assert_fills_equal(f, fo, f"long tape batch {k}")
+            longer += len(fo) > len(batches[k])
+        assert_books_equal(eng, ob, range(sc.num_symbols), "long tape")
+    assert longer >= 3
 
 
 def test_host_slot_reuse_needs_collect(me, orc):
