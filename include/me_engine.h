@@ -275,6 +275,10 @@ int me_stats_read(me_engine* e, uint64_t* handoffs);
  * accepted record is matched); exact_counts = times a submit had to take an exact count (flush + sync)
  * because the published count was too stale or too close to max_resting. */
 int me_admission_read(me_engine* e, uint64_t* resting, uint64_t* bound, uint64_t* exact_counts);
+/* Would a batch with n_rest LIMIT records be admitted now? (*ok = 1/0; nothing is enqueued.) A submit
+ * from the same thread right after a 1 is admitted. Shards that must accept a slice all-or-none
+ * (cluster.ShardedMatcher) ask every engine first. */
+int me_admission_check(me_engine* e, uint64_t n_rest, int* ok);
 
 /* Last error text of e (or of the last failed me_create when e == NULL). */
 int me_last_error(const me_engine* e, char* buf, size_t cap);

@@ -76,7 +76,9 @@ typedef struct me_matcher {
   uint32_t num_symbols;  /* symbol ids it takes (the service interns up to this many) */
   uint32_t max_batch;    /* largest slice */
   uint64_t max_resting;  /* resting orders it holds at most (me_fill_bound's bound: max_resting + 2n) */
-  /* Match one slice; outputs valid until the next call. Nonzero: the slice is lost (service fails). */
+  /* Match one slice; outputs valid until the next call. ME_E_CAPACITY: refused, nothing of it was
+   * applied (admission control; the slice stays queued). Any other nonzero: the slice is lost (the
+   * service fails). */
   int (*match)(void* ctx, const me_order_soa* slice, size_t n, const me_fill** fills, size_t* n_fills,
                const me_order_result** results);
   /* me_book_orders' contract for one symbol (depth 0: the whole book). */

@@ -35,6 +35,10 @@ CMD_MATCH, CMD_BOOK, CMD_SNAPSHOT, CMD_STOP = 1, 2, 3, 4
 _REC = 8 + 8 + 4 + 4 + 1  # packed slice record: seq, price_q4, qty, symbol, kind
 
 
+class SliceRefused(RuntimeError):
+    """A shard's admission control refused its part of a slice; no shard applied anything."""
+
+
 class ShardedMatcher:
     """The matcher of a sharded deployment (one instance per rank).
 
@@ -107,6 +111,13 @@ class ShardedMatcher:
             o += n * w
         b = Batch(*cols)
         lb, pos = self.plan.split(b)[self.rank]
+        # all-or-none: every shard's admission control must take its part before any shard applies
+        # its part (a refused slice stays queued in the service, no book changed)
+        ok = torch.tensor([1 if (not len(lb) or not hasattr(self.book, "admits") or self.book.admits(lb)) else 0],
+                          dtype=torch.int64, device=self.dev)
+        self.dist.all_reduce(ok, op=self.dist.ReduceOp.MIN, group=self.group)
+        if int(ok.item()) == 0:
+            return None
         if len(lb):
             r, f = self.book.submit_batch(lb)
         else:
@@ -144,9 +155,13 @@ class ShardedMatcher:
 
     # ---------------------------------------------------------------- rank 0 API
     def match(self, batch: Batch):
-        """One slice through every shard -> (results, tape) merged on rank 0."""
+        """One slice through every shard -> (results, tape) merged on rank 0. Raises SliceRefused
+        when a shard's admission control refused its part: then no shard applied anything."""
         self._bcast_header(CMD_MATCH, len(batch))
-        tape, res = self._match(batch, len(batch))
+        got = self._match(batch, len(batch))
+        if got is None:
+            raise SliceRefused("a shard's max_resting refused the slice; no book changed")
+        tape, res = got
         return res, tape
 
     def book_orders(self, symbol: int, depth: int):
@@ -180,6 +195,8 @@ class ShardedMatcher:
                 nf[0] = len(tape)
                 results[0] = res.ctypes.data
                 return 0
+            except SliceRefused:  # nothing applied: the service keeps the slice queued
+                return _abi.ME_E_CAPACITY
             except Exception:  # a lost slice: the service fails loudly
                 return _abi.ME_E_STATE
 

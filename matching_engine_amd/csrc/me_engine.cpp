@@ -1029,7 +1029,7 @@ static uint64_t admission_bound(const me_engine* e) {
 // (the device stays busy meanwhile), then takes an exact count (flush + sync). A batch that still
 // does not fit is refused with ME_E_CAPACITY before anything of it is enqueued: the books are
 // untouched and the engine stays usable (the error is not sticky).
-static int admit(me_engine* e, uint64_t n) {  // n: records of the batch that may rest
+static int admit(me_engine* e, uint64_t n, bool commit = true) {  // n: records of the batch that may rest
   const uint64_t cap = e->cfg.max_resting;
   if (admission_bound(e) + n > cap) {
     for (;;) {
@@ -1067,7 +1067,19 @@ static int admit(me_engine* e, uint64_t n) {  // n: records of the batch that ma
       std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
   }
-  e->adm_total += n;
+  if (commit) e->adm_total += n;
+  return ME_OK;
+}
+
+extern "C" int me_admission_check(me_engine* e, uint64_t n_rest, int* ok) {
+  if (!e || !ok) return ME_E_INVALID;
+  *ok = 0;
+  if (e->failed) return ME_E_STATE;
+  HIP_TRY(hipSetDevice(e->dev), "hipSetDevice");
+  const int rc = admit(e, n_rest, false);
+  if (rc == ME_E_CAPACITY) return ME_OK;  // would be refused: *ok stays 0
+  if (rc) return rc;
+  *ok = 1;
   return ME_OK;
 }
 

@@ -363,8 +363,9 @@ static int backend_match(me_service* s, const me_order_soa& b, size_t n, const m
     size_t nr = 0;
     return me_collect(s->eng, t, tape, nf, res, &nr);
   }
-  accepted = true;
-  return s->m.match(s->m.ctx, &b, n, tape, nf, res);
+  const int rc = s->m.match(s->m.ctx, &b, n, tape, nf, res);
+  accepted = rc != ME_E_CAPACITY;  // the matcher's refusal: nothing of the slice was applied
+  return rc;
 }
 
 static int backend_book(me_service* s, uint32_t sid, uint32_t depth, me_book_entry* bids, size_t bids_cap,
@@ -876,7 +877,7 @@ static int process(me_service* s, Slice&& sl, FlushOut* out) {
     bool accepted = false;
     const int rc = backend_match(s, b, n, &tape, &nf, &res, accepted);
     if (rc != ME_OK && !accepted) {  // not accepted: the slice goes back to the head of the queue
-      const std::string e = backend_err(s);
+      const std::string e = s->eng ? backend_err(s) : "the matcher refused the slice (a shard's max_resting); no book changed";
       std::lock_guard<std::mutex> lk(s->mu);
       s->inflight_records -= n;
       s->closed_records += n;

@@ -316,6 +316,13 @@ class Engine:
         _check(self.lib, self.h, self.lib.me_stats_read(self.h, C.byref(h)))
         return {"handoffs": h.value}
 
+    def admits(self, b: Batch) -> bool:
+        """Would submit_batch(b) be admitted now (me_admission_check)? Nothing is enqueued."""
+        n_rest = int(np.count_nonzero((b.kind & 0x0C) == 0))
+        ok = C.c_int(0)
+        _check(self.lib, self.h, self.lib.me_admission_check(self.h, n_rest, C.byref(ok)))
+        return bool(ok.value)
+
     def admission(self) -> dict:
         """Admission control (me_admission_read): device resting count after all enqueued work, the
         host's current bound, and how many submits had to take an exact count."""

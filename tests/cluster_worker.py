@@ -6,9 +6,12 @@ runs the same request stream through a second service whose matcher spans rank 0
 holding every symbol) and compares the two SQLite databases row by row, the per-order books
 (GetOrderBook) and the gathered level snapshot.
 
-env: RANK, WORLD_SIZE, MASTER_ADDR, MASTER_PORT; argv: BOOK(oracle|gpu) TMPDIR OUT_JSON
+env: RANK, WORLD_SIZE, MASTER_ADDR, MASTER_PORT; argv: BOOK(oracle|gpu|oracle_refuse) TMPDIR OUT_JSON
   oracle: every shard book is the CPU oracle (the host protocol under gloo, CPU tensors)
   gpu:    every shard book is the HIP engine on cuda:0 (ranks share the box's one GPU; gloo)
+  oracle_refuse: oracle shards, and the last rank's admission control refuses its part of the
+          second slice once: no shard may apply anything of it, the service keeps it queued, the
+          next flush matches it (all-or-none admission, cluster.ShardedMatcher._match)
 """
 import json
 import os
@@ -24,11 +27,16 @@ sys.path.insert(0, ROOT)
 class OracleShard:
     """The oracle with the Engine methods the matcher uses (test infrastructure)."""
 
-    def __init__(self, ids):
+    def __init__(self, ids, refuse_calls=()):
         from oracle.oracle import OracleBook
 
         self.ids = np.asarray(ids, dtype=np.uint32)
         self.ob = OracleBook(max(len(ids), 1), symbol_ids=self.ids if len(ids) else None)
+        self.refuse_calls, self.calls = set(refuse_calls), 0
+
+    def admits(self, b):
+        self.calls += 1
+        return self.calls not in self.refuse_calls
 
     def submit_batch(self, b):
         return self.ob.submit(b)
@@ -78,13 +86,17 @@ def main():
     mids = {s: 1_000_000 + 1000 * i for i, s in enumerate(syms)}
     base = np.array([mids[s] - 64 for s in syms], dtype=np.int64)
 
-    def shard(ids):
-        return OracleShard(ids) if kind == "oracle" else None
+    refuse = kind == "oracle_refuse"
+
+    def shard(ids, last=False):
+        if kind in ("oracle", "oracle_refuse"):
+            return OracleShard(ids, refuse_calls=(2,) if (refuse and last) else ())
+        return None
 
     from matching_engine_amd.sharding import ShardPlan
 
     plan = ShardPlan(S, world)
-    m = ShardedMatcher(S, L, base, MB, MR, shard_book=shard(plan.members[rank]), device=0)
+    m = ShardedMatcher(S, L, base, MB, MR, shard_book=shard(plan.members[rank], last=rank == world - 1), device=0)
     if rank != 0:
         m.serve()
         dist.barrier()
@@ -98,6 +110,9 @@ def main():
     owner = {}
     live = []
     outs = [[], []]
+    refused = 0
+    msg = ""
+    ok = True
     for slice_no in range(5):
         for _ in range(1500):
             if live and rng.random() < 0.15:
@@ -119,9 +134,15 @@ def main():
             if otype == 0:
                 live.append(oid)
         for k, v in enumerate(svcs):
-            outs[k].append(v.flush())
-    msg = ""
-    ok = True
+            try:
+                outs[k].append(v.flush())
+            except me.ServiceError as e:
+                if not (refuse and k == 0 and refused == 0):
+                    raise
+                refused += 1  # the sharded service: nothing matched, the slice is still pending
+                if v.pending == 0 or "refused" not in str(e):
+                    ok, msg = False, f"refused flush: pending {v.pending}, error {e}"
+                outs[k].append(v.flush())
     for k in range(5):
         for a, b, what in zip(outs[0][k], outs[1][k], ("seq", "results", "tape")):
             if len(a) != len(b) or not np.array_equal(a, b):
@@ -143,7 +164,10 @@ def main():
         v.close()
     m.stop()
     dist.barrier()
-    json.dump({"ok": ok, "msg": msg, "orders": nrows, "fill_rows": nfills, "world": world}, open(out_path, "w"))
+    if refuse and refused != 1:
+        ok, msg = False, f"expected one refused flush, saw {refused}"
+    json.dump({"ok": ok, "msg": msg, "orders": nrows, "fill_rows": nfills, "world": world, "refused": refused},
+              open(out_path, "w"))
     dist.destroy_process_group()
 
 

@@ -130,3 +130,23 @@ def test_host_runs_ahead_without_exact_counts(me):
     for db in dbs:
         db.free()
     eng.close()
+
+
+def test_admission_check_enqueues_nothing(me):
+    """me_admission_check (Engine.admits): the all-or-none question a sharded matcher asks every shard
+    before any applies its part — true / false as submit would decide, with nothing enqueued."""
+    rng = np.random.default_rng(9)
+    seqs = Seqs()
+    eng = _engine(me, 3000)
+    a = _passive(me, seqs, 2000, rng)
+    assert eng.admits(a)
+    eng.submit_batch(a)
+    big = _passive(me, seqs, 1500, rng)
+    assert not eng.admits(big)
+    small = _passive(me, seqs, 1000, rng)
+    assert eng.admits(small)
+    assert eng.admission()["resting"] == 2000  # the checks enqueued nothing
+    assert eng.admits(_market(me, seqs, 1500, rng))  # MARKETs never rest
+    eng.submit_batch(small)
+    assert eng.admission()["resting"] == 3000
+    eng.close()

@@ -90,6 +90,15 @@ def test_two_rank_sharded_service_db_equals_single_engine(built, tmp_path):
     assert r["orders"] > 5000 and r["fill_rows"] > 1000
 
 
+def test_sharded_slice_refused_all_or_none(built, tmp_path):
+    """One shard's admission control refuses its part of a slice: no shard applies anything, the
+    service keeps the slice queued (ME_E_CAPACITY from the matcher), the next flush matches it once —
+    the DB, outputs and books still equal the single book's."""
+    r = _run("oracle_refuse", 2, tmp_path, script="cluster_worker.py")
+    assert r["ok"], r["msg"]
+    assert r["refused"] == 1
+
+
 @pytest.mark.gpu
 def test_two_rank_sharded_service_gpu_engines(built, tmp_path):
     r = _run("gpu", 2, tmp_path, script="cluster_worker.py")
