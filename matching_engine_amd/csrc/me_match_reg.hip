@@ -1186,9 +1186,12 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
   const uint32_t fst = bk.fcache[(size_t)sl * FSTK + lane];
   const uint32_t gsv = bk.gsym[sl];
   if (bucketed) {
-    // a count above the bucket keeps its bit in the rescan mask (rare; at most ME_GMAX lanes)
+    // the symbol's records over every batch of the group: lanes 0 .. ng-1 (up to ME_GMAX = 64) hold
+    // the per-batch counts. (An 8-lane sum here once dropped batches 8+ of a group: a continuation
+    // whose hand-off came in batch 8 or later saw 0 records and left them unmatched —
+    // test_long_drift_soak.)
     long long t = (long long)nsv;
-    for (int d = 1; d < 8; d <<= 1) t += __shfl_xor(t, d, 64);
+    for (int d = 1; d < 64; d <<= 1) t += __shfl_xor(t, d, 64);
     ns = (uint32_t)rli64(t, 0);
   }
   if (ns == 0u) {

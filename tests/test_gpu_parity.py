@@ -181,6 +181,66 @@ def test_drifting_stream_device_groups_every_batch(me, orc, group):
         assert eng.resting_count() == ob.resting()
 
 
+@pytest.mark.parametrize("group", [32, 64])
+def test_symbol_first_seen_late_in_a_group(me, orc, group):
+    """A symbol with no records in the first batches of a launch group and records later (a sparse
+    symbol): every batch of the group against the oracle. (The per-symbol record count of a group
+    once summed only batches 0-7.)"""
+    sc = me.preset(2, num_symbols=64, batch=4096)
+    st = me.Stream(sc)
+    base = st.base_prices()
+    batches = [st.next(sc.batch) for _ in range(group)]
+    for k, b in enumerate(batches):
+        late = (b.symbol % 8) == 3  # symbols 3, 11, ... only from batch 12 (and 40) on
+        if k < 12 or (group > 32 and 20 <= k < 40):
+            b.symbol[late] = (b.symbol[late] + 1) % sc.num_symbols
+    ob = orc.OracleBook(sc.num_symbols)
+    with engine_for(me, sc.num_symbols, sc.levels, base, sc.batch, (group + 2) * sc.batch,
+                    batches_per_launch=group) as eng:
+        dbs = [eng.upload(b) for b in batches]
+        for db in dbs:
+            eng.submit_device(db)
+        eng.sync()
+        assert eng.last_group_size() == group
+        for k, b in enumerate(batches):
+            r, f = eng.fetch_group_outputs(k, len(b))
+            ro, fo = ob.submit(b)
+            assert_results_equal(r, ro, f"late symbols G={group} batch {k}")
+            assert_fills_equal(f, fo, f"late symbols G={group} batch {k}")
+        assert_books_equal(eng, ob, range(sc.num_symbols), "late symbols")
+        for db in dbs:
+            db.free()
+
+
+def test_long_drift_soak(me, orc):
+    """A long session: 1,200 batches in which every symbol's mid trends ~60 windows (stale orders are
+    left behind as far levels, 1 % of LIMITs far away, 10 % cancels, sweeping MARKETs), device
+    batches 32 per launch. Every 100th batch and the final books against the oracle; no error, no
+    window / seq reject, the far arrays never overflow at the default far_levels."""
+    sc, base, batches = _drift_stream(me, 128, 256, 8192, 1200, drift_every=5)
+    ob = orc.OracleBook(sc.num_symbols)
+    with engine_for(me, sc.num_symbols, sc.levels, base, sc.batch, 1 << 22, batches_per_launch=32) as eng:
+        for g0 in range(0, len(batches), 100):
+            grp = batches[g0:g0 + 100]
+            dbs = [eng.upload(b) for b in grp]
+            for db in dbs:
+                eng.submit_device(db)
+            r, f = eng.fetch_outputs(len(grp[-1]))
+            for b in grp[:-1]:
+                ob.submit(b)
+            ro, fo = ob.submit(grp[-1])
+            assert_results_equal(r, ro, f"soak batch {g0 + len(grp) - 1}")
+            assert_fills_equal(f, fo, f"soak batch {g0 + len(grp) - 1}")
+            no_window_rejects(r)
+            for db in dbs:
+                db.free()
+        assert_books_equal(eng, ob, range(sc.num_symbols), "soak")
+        assert eng.resting_count() == ob.resting() == eng.admission()["resting"]
+    last = batches[-1]
+    lim = ((last.kind >> 2) & 3) == 0
+    assert np.median(np.abs(last.price_q4[lim] - base[last.symbol[lim]])) > 40 * sc.levels
+
+
 @pytest.mark.parametrize("levels", [1024, 4096])
 def test_drifting_mids_deep_windows(me, orc, levels):
     """The same unbounded semantics on the deep-window kernel (LDS window at 1,024 levels, HBM window
