@@ -122,6 +122,25 @@ def test_host_tape_longer_than_batch(me, orc):
     assert longer >= 3
 
 
+def test_host_pipeline_drifting_handoffs(me, orc):
+    """Host batches on a drifting far-price stream (hand-offs to the continuation launch, window
+    re-centring, far levels, cancels, OIDs above 2^33) at G = 32 with a 40-batch collect lag: every
+    batch's outputs from its pinned slot against the oracle."""
+    sc = me.preset(5, num_symbols=256, levels=128, batch=4096, cancel_pct=10, market_pct=15, market_qty_mult=3,
+                   drift_step=1, drift_every=3, far_pct=1, seq_start=(1 << 33) + 5)
+    st = me.Stream(sc)
+    base = st.base_prices()
+    batches = [st.next(sc.batch) for _ in range(96)]
+    ob = orc.OracleBook(sc.num_symbols)
+    with _engine(me, sc, base, batches, batches_per_launch=32) as eng:
+        for k, (r, f) in enumerate(_pipelined(me, eng, batches, lag=40)):
+            ro, fo = ob.submit(batches[k])
+            assert_results_equal(r, ro, f"drift host batch {k}")
+            assert_fills_equal(f, fo, f"drift host batch {k}")
+        assert_books_equal(eng, ob, range(sc.num_symbols), "drift host")
+        assert eng.stats()["handoffs"] > 0
+
+
 def test_host_slot_reuse_needs_collect(me, orc):
     sc, base, batches = _stream(me, 2, 6, num_symbols=32, batch=512)
     ob = orc.OracleBook(sc.num_symbols)
