@@ -527,7 +527,9 @@ __device__ __forceinline__ uint32_t reg_cancel(RegCtx& c, unsigned long long tgt
       const uint32_t own = rl32(owner, 0);
       const long long prc = rli64(price, 0);
       const long long lv64 = prc - rli64(c.base, 0);
-      const bool inw = own == c.s && (unsigned long long)lv64 < (unsigned long long)RL;
+      // in the window: [0, L) — not [0, RL): at L = 64 the second ladder row is no level (a far order
+      // 64..127 levels above base was once cancelled as a window order, corrupting the book)
+      const bool inw = own == c.s && (unsigned long long)lv64 < (unsigned long long)ldsu(c.G->bk.L);
       const int lvl = inw ? (int)lv64 : 0;
       const uint32_t hv = c.hd.get(lvl);
       const bool in_cache = inw && hv == ch;  // ch is the cached head: the on-chip copy is authoritative
