@@ -388,7 +388,7 @@ def main():
     n_seed = sum(len(b) for b in seeds)
     eng = me.Engine(len(ids), sc.levels, base,
                     max_batch=max(len(b) for b in batches + gather_batches + e2e_batches + seeds) + 1,
-                    max_resting=total_local // 3 + n_seed + 65536, seq_ring=args.seq_ring,
+                    max_resting=max(total_local // 3, sum(len(b) for b in batches)) + n_seed + 65536, seq_ring=args.seq_ring,
                     device=local, symbol_ids=ids, batches_per_launch=args.batches_per_launch)
     for b in seeds:
         eng.submit_batch(b, want_fills=False)

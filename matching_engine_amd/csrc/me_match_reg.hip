@@ -919,7 +919,8 @@ __device__ __forceinline__ void reject_bad_run(const ColdArgs& G, uint32_t lo, u
 // them little; what it saves is two launches per batch.
 
 // Bucket job: records [r0, r1) of bucket job j, one returning atomic per record on its bin's counter.
-__device__ __forceinline__ void aux_bucket(const ColdArgs& G, uint32_t j, uint32_t r0, uint32_t r1) {
+template <class GA>
+__device__ __forceinline__ void aux_bucket(const GA& G, uint32_t j, uint32_t r0, uint32_t r1) {
   const int lane = lane_id();
   const AuxBucket& J = G.ax.b[j];
   const gptr<const uint32_t> sym = ldsg(J.sym);
@@ -961,7 +962,8 @@ __device__ __forceinline__ void aux_bucket(const ColdArgs& G, uint32_t j, uint32
 
 // Tape job j, one TILE_TAPE-record tile per wave: tape offsets of its records and the copy of their
 // fills from scratch into the batch's tape (ordered by taker seq).
-__device__ __forceinline__ void aux_tape_tile(const ColdArgs& G, uint32_t jb, uint32_t t, uint32_t ntiles,
+template <class GA>
+__device__ __forceinline__ void aux_tape_tile(const GA& G, uint32_t jb, uint32_t t, uint32_t ntiles,
                                               uint32_t tn) {
   const int lane = lane_id();
   const AuxTape& J = G.ax.t[jb];
@@ -1043,7 +1045,6 @@ __device__ __forceinline__ void aux_tape_tile(const ColdArgs& G, uint32_t jb, ui
 }
 
 // Side-job wave a of A: its share of every bucket / clear job of group J and every tape job of J-2.
-// Side-job wave a of A: its share of every bucket / clear job of group J and every tape job of J-2.
 __device__ __forceinline__ void aux_jobs(const ColdArgs& G, uint32_t a, uint32_t A) {
   const int lane = lane_id();
   const uint32_t nb = ldsu(G.ax.nb);
@@ -1063,6 +1064,154 @@ __device__ __forceinline__ void aux_jobs(const ColdArgs& G, uint32_t a, uint32_t
     const uint32_t tn = ldsu(G.ax.t[j].tn);
     const uint32_t ntiles = (tn + TILE_TAPE - 1) / TILE_TAPE;
     for (uint32_t t = a; t < ntiles; t += A) aux_tape_tile(G, j, t, ntiles, tn);
+  }
+}
+
+// ---- launches with no match job: the side jobs alone ------------------------------------------
+// The pipeline's first launch of a run (bucket only) and its last (tape only) have no matching waves to
+// hide behind: in k_match_reg they ran on its 4 side waves per CU (one 145-KB workgroup per CU), 74 and
+// 87 us for a 20-batch group at config 2. k_side carries only the side jobs' arguments in LDS.
+//  * bucket: one workgroup per SB_REC records of a batch counts its records per symbol in LDS, then
+//    reserves each symbol's run with ONE returning global atomic (device-scope atomics execute at the
+//    memory side, one request each: one per record capped the fill launch at ~20 G records/s), then
+//    writes the records at run + rank. A bucket's order is free (the match wave sorts by batch index).
+//    Needs (S + 1) counters in LDS; above SB_SMAX symbols the waves bucket 64-record blocks with one
+//    atomic per record as the pipelined launch does.
+//  * tape: tiles dealt round-robin to the tape waves over a list flattened across the group's batches.
+struct SideArgs {
+  struct {
+    uint32_t* err;
+  } bk;
+  AuxDev ax;
+};
+constexpr int SIDE_THREADS = 512;
+constexpr int SIDE_WAVES = SIDE_THREADS / 64;
+constexpr uint32_t SB_REC = 4096;                  // records per bucket workgroup
+constexpr uint32_t SB_PER = SB_REC / SIDE_THREADS;  // records per thread
+constexpr uint32_t SB_SMAX = 16383;                // symbols bucketed through an LDS histogram (64 KB)
+
+// Units [off, off + cnt) of a list flattened over batches, dealt round-robin to waves: wave a's first.
+__device__ __forceinline__ uint32_t flat_first(uint32_t off, uint32_t a, uint32_t A) {
+  return off + (a + A - off % A) % A;
+}
+
+// Bucket records [r0, r1) of bucket job j with a workgroup histogram (cnt: S + 1 LDS counters).
+__device__ __forceinline__ void side_bucket_wg(const SideArgs& G, uint32_t j, uint32_t r0, uint32_t r1, uint32_t* cnt) {
+  const uint32_t tid = threadIdx.x;
+  const AuxBucket& J = G.ax.b[j];
+  const uint32_t S = ldsu(G.ax.S);
+  const gptr<const uint32_t> sym = ldsg(J.sym);
+  const gptr<const uint64_t> seq = ldsg(J.seq);
+  const gptr<const int64_t> px = ldsg(J.px);
+  const gptr<const int32_t> qty = ldsg(J.qty);
+  const gptr<const uint8_t> kind = ldsg(J.kind);
+  const gptr<uint32_t> bcnt = ldsg(J.bcnt);
+  const gptr<BkRec> brec = ldsg(J.b_rec);
+  const gptr<me_order_result> bres = ldsg(J.bres);
+  for (uint32_t b = tid; b <= S; b += SIDE_THREADS) cnt[b] = 0u;
+  {  // the tile sums of this record range, and the batch's scratch top, start at zero
+    const gptr<uint32_t> z = ldsg(J.zero_tile_sum);
+    const uint32_t t1 = min((r1 + TILE_TAPE - 1) / TILE_TAPE, ldsu(J.zero_tiles));
+    for (uint32_t t = r0 / TILE_TAPE + tid; t < t1; t += SIDE_THREADS) z[t] = 0u;
+    if (r0 == 0 && tid == 0) *ldsg(J.zero_top) = 0ull;
+  }
+  __syncthreads();
+  uint32_t bin[SB_PER], rank[SB_PER];
+  uint64_t sq[SB_PER];
+  int64_t p[SB_PER];
+  int32_t q[SB_PER];
+  uint32_t k8[SB_PER];
+  bool order_ok = true;
+#pragma unroll
+  for (uint32_t k = 0; k < SB_PER; ++k) {
+    const uint32_t i = r0 + k * SIDE_THREADS + tid;
+    bin[k] = S;
+    if (i < r1) {
+      bin[k] = min(sym[i], S);
+      sq[k] = seq[i];
+      p[k] = px[i];
+      q[k] = qty[i];
+      k8[k] = kind[i];
+      // API precondition (the seq ring relies on it): seqs strictly ascending through the batch
+      if (i > 0) order_ok &= sq[k] > seq[i - 1];
+    }
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < SB_PER; ++k) {
+    const uint32_t i = r0 + k * SIDE_THREADS + tid;
+    if (i < r1 && bin[k] == S) reject_bad_at(bres, i);  // unknown symbol: rejected here, never bucketed
+    if (bin[k] < S) rank[k] = atomicAdd(&cnt[bin[k]], 1u);
+  }
+  if (__ballot(!order_ok) && lane_id() == 0) atomicOr(ldsg(G.bk.err), ERR_SEQ_ORDER);
+  __syncthreads();
+  for (uint32_t b = tid; b < S; b += SIDE_THREADS) {
+    const uint32_t c = cnt[b];
+    if (c) cnt[b] = atomicAdd(&bcnt[(size_t)b * BK_CNT_STRIDE], c);
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t k = 0; k < SB_PER; ++k) {
+    if (bin[k] >= S) continue;
+    const uint32_t r = cnt[bin[k]] + rank[k];
+    if (r < (uint32_t)BK_CAP) {
+      const uint32_t i = r0 + k * SIDE_THREADS + tid;
+      const size_t d = (size_t)bin[k] * BK_CAP + r;
+      brec[d].seq = sq[k];
+      brec[d].px = p[k];
+      brec[d].qty = q[k];
+      brec[d].ok = i | ((k8[k] & 15u) << BK_KIND_SHIFT);
+    }
+  }
+}
+
+// Grid: [0, nbu) bucket workgroups (histogram path; 0 on the per-record path), then tape workgroups.
+__global__ __launch_bounds__(SIDE_THREADS) void k_side(SideArgs args, uint32_t nbu) {
+  __shared__ SideArgs G;
+  extern __shared__ uint32_t side_cnt[];
+  static_assert(sizeof(SideArgs) % 8 == 0, "SideArgs copy");
+  for (uint32_t i = threadIdx.x; i < sizeof(SideArgs) / 8; i += SIDE_THREADS)
+    reinterpret_cast<unsigned long long*>(&G)[i] = reinterpret_cast<const unsigned long long*>(&args)[i];
+  __syncthreads();
+  const int lane = lane_id();
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t nb = ldsu(G.ax.nb);
+  if (blockIdx.x < nbu) {  // histogram bucket unit: batch j, records [u * SB_REC, ...)
+    uint32_t off = 0;
+    for (uint32_t j = 0; j < nb; ++j) {
+      const uint32_t n = ldsu(G.ax.b[j].n), nu = (n + SB_REC - 1) / SB_REC;
+      if (blockIdx.x < off + nu) {
+        const uint32_t r0 = (blockIdx.x - off) * SB_REC;
+        side_bucket_wg(G, j, r0, min(n, r0 + SB_REC), side_cnt);
+        return;
+      }
+      off += nu;
+    }
+    return;
+  }
+  const uint32_t A = (gridDim.x - nbu) * SIDE_WAVES, a = (blockIdx.x - nbu) * SIDE_WAVES + wv;
+  uint32_t off = 0;
+  if (nbu == 0) {  // per-record bucket path (too many symbols for the LDS histogram)
+    for (uint32_t j = 0; j < nb; ++j) {
+      const AuxBucket& J = G.ax.b[j];
+      const uint32_t zt = ldsu(J.zero_tiles);
+      const gptr<uint32_t> z = ldsg(J.zero_tile_sum);
+      for (uint32_t i = a * 64u + (uint32_t)lane; i < zt; i += A * 64u) z[i] = 0u;
+      if (a == 0 && lane == 0) *ldsg(J.zero_top) = 0ull;
+      const uint32_t n = ldsu(J.n), nblk = (n + 63u) / 64u;
+      for (uint32_t u = flat_first(off, a, A); u < off + nblk; u += A) {
+        const uint32_t r0 = (u - off) * 64u;
+        aux_bucket(G, j, r0, min(n, r0 + 64u));
+      }
+      off += nblk;
+    }
+  }
+  const uint32_t nt = ldsu(G.ax.nt);
+  off = 0;
+  for (uint32_t j = 0; j < nt; ++j) {
+    const uint32_t tn = ldsu(G.ax.t[j].tn);
+    const uint32_t ntiles = (tn + TILE_TAPE - 1) / TILE_TAPE;
+    for (uint32_t u = flat_first(off, a, A); u < off + ntiles; u += A) aux_tape_tile(G, j, u - off, ntiles, tn);
+    off += ntiles;
   }
 }
 
@@ -1617,6 +1766,22 @@ hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* b
   uint32_t nbr = 0, ntr = 0;
   for (uint32_t j = 0; j < ax.nb; ++j) nbr += ax.b[j].n;
   for (uint32_t j = 0; j < ax.nt; ++j) ntr += ax.t[j].tn;
+  if (!ng) {  // side jobs only (the pipeline's fill and drain): k_side, all waves on them
+    SideArgs SA{};
+    SA.bk.err = bk.err;
+    SA.ax = ax;
+    const bool hist = ax.S <= SB_SMAX;
+    uint32_t nbu = 0;
+    if (hist)
+      for (uint32_t j = 0; j < ax.nb; ++j) nbu += (ax.b[j].n + SB_REC - 1) / SB_REC;
+    // the waves after the bucket workgroups: tape tiles (and per-record bucket blocks without hist)
+    const uint32_t units = max(hist ? 0u : (nbr + 63u) / 64u, (ntr + TILE_TAPE - 1) / TILE_TAPE);
+    const uint32_t twg = min((units + SIDE_WAVES - 1) / SIDE_WAVES, max(ax.nwg, 1u) * 2u);
+    const uint32_t sgrid = max(nbu + twg, 1u);
+    const size_t lds = hist ? (size_t)(ax.S + 1) * sizeof(uint32_t) : 0;
+    hipExtLaunchKernelGGL(k_side, dim3(sgrid), dim3(SIDE_THREADS), lds, st, ev0, ev1, 0, SA, nbu);
+    return hipGetLastError();
+  }
   const uint32_t aux_wgs = min((max(nbr, ntr) + 256u * REG_WAVES - 1) / (256u * REG_WAVES), max(ax.nwg, 1u));
   const uint32_t grid = max(max(match_wgs, aux_wgs), 1u);
   hipExtLaunchKernelGGL(k_match_reg<false>, dim3(grid), dim3(128 * REG_WAVES), 0, st, ev0, ng ? nullptr : ev1, 0, A);
