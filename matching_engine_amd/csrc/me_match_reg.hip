@@ -1776,7 +1776,7 @@ hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* b
       for (uint32_t j = 0; j < ax.nb; ++j) nbu += (ax.b[j].n + SB_REC - 1) / SB_REC;
     // the waves after the bucket workgroups: tape tiles (and per-record bucket blocks without hist)
     const uint32_t units = max(hist ? 0u : (nbr + 63u) / 64u, (ntr + TILE_TAPE - 1) / TILE_TAPE);
-    const uint32_t twg = min((units + SIDE_WAVES - 1) / SIDE_WAVES, max(ax.nwg, 1u) * 2u);
+    const uint32_t twg = min((units + SIDE_WAVES - 1) / SIDE_WAVES, max(ax.nwg, 1u) * 4u);
     const uint32_t sgrid = max(nbu + twg, 1u);
     const size_t lds = hist ? (size_t)(ax.S + 1) * sizeof(uint32_t) : 0;
     hipExtLaunchKernelGGL(k_side, dim3(sgrid), dim3(SIDE_THREADS), lds, st, ev0, ev1, 0, SA, nbu);
