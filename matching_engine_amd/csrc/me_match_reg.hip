@@ -1084,9 +1084,15 @@ struct SideArgs {
   } bk;
   AuxDev ax;
 };
-constexpr int SIDE_THREADS = 512;
+#ifndef ME_SIDE_THREADS
+#define ME_SIDE_THREADS 512
+#endif
+#ifndef ME_SB_REC
+#define ME_SB_REC 4096
+#endif
+constexpr int SIDE_THREADS = ME_SIDE_THREADS;
 constexpr int SIDE_WAVES = SIDE_THREADS / 64;
-constexpr uint32_t SB_REC = 4096;                  // records per bucket workgroup
+constexpr uint32_t SB_REC = ME_SB_REC;             // records per bucket workgroup
 constexpr uint32_t SB_PER = SB_REC / SIDE_THREADS;  // records per thread
 constexpr uint32_t SB_SMAX = 16383;                // symbols bucketed through an LDS histogram (64 KB)
 
