@@ -540,6 +540,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "host": host_info(),
+            "build": me._abi.load().me_build_info().decode(),  # source digest of the library that ran
             "c1_paths": c1,
         }
         print(json.dumps(line), flush=True)

@@ -83,6 +83,11 @@ enum {
  * 3 for overflow_error("underflow"). */
 int me_normalize_to_q4(int64_t price, int32_t scale, int64_t* out);
 
+/* Build record (no reference counterpart): "src=<16 hex> arch=gfx950", the first 16 hex digits of
+ * the sha256 of the product sources and headers the library was compiled from (Makefile
+ * DIGEST_SRCS order, restated by tools/src_digest.py). */
+const char* me_build_info(void);
+
 /* ---- the batched matching engine (one shard = one GPU) ------------------------------- */
 typedef struct me_engine me_engine;
 

@@ -113,6 +113,7 @@ _P = C.c_void_p
 _SZ = C.c_size_t
 PROTOTYPES = {
     "me_normalize_to_q4": (C.c_int, [C.c_int64, C.c_int32, C.POINTER(C.c_int64)]),
+    "me_build_info": (C.c_char_p, []),
     "me_create": (_P, [C.POINTER(MeConfig)]),
     "me_destroy": (None, [_P]),
     "me_submit_batch": (C.c_int, [_P, C.POINTER(MeOrderSoa), _SZ, _P, _SZ, C.POINTER(_SZ), _P]),

@@ -55,3 +55,17 @@ def test_invalid_config_rejected(built):
 
     with pytest.raises(me.EngineError, match="invalid config"):
         me.Engine(4, 100, [1000] * 4, 1024, 1024, 1 << 20)  # levels not a power of two
+
+
+def test_library_was_built_from_these_sources(built):
+    """The loaded libme_engine.so carries the digest of the sources it was compiled from: equal to
+    the working tree's, so the library a run loads (here, or shipped to the GPU box) is this tree."""
+    import sys
+
+    from matching_engine_amd import _abi
+
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from src_digest import digest
+
+    info = _abi.load().me_build_info().decode()
+    assert info == f"src={digest()} arch=gfx950", info
