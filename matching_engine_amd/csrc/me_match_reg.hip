@@ -1182,11 +1182,15 @@ __global__ __launch_bounds__(SIDE_THREADS) void k_side(SideArgs args, uint32_t n
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t nb = ldsu(G.ax.nb);
   if (blockIdx.x < nbu) {  // histogram bucket unit: batch j, records [u * SB_REC, ...)
+    // Blocks b and b + 8 share an XCD (round-robin placement; speed only): every unit of batch j runs
+    // on blocks b = j (mod 8), so the runs its workgroups write side by side into one bucket array
+    // meet in one L2 and leave it as whole lines, not as partial lines from several XCDs.
+    const uint32_t x = blockIdx.x % 8u, k = blockIdx.x / 8u;
     uint32_t off = 0;
-    for (uint32_t j = 0; j < nb; ++j) {
+    for (uint32_t j = x; j < nb; j += 8) {
       const uint32_t n = ldsu(G.ax.b[j].n), nu = (n + SB_REC - 1) / SB_REC;
-      if (blockIdx.x < off + nu) {
-        const uint32_t r0 = (blockIdx.x - off) * SB_REC;
+      if (k < off + nu) {
+        const uint32_t r0 = (k - off) * SB_REC;
         side_bucket_wg(G, j, r0, min(n, r0 + SB_REC), side_cnt);
         return;
       }
@@ -1778,8 +1782,11 @@ hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* b
     SA.ax = ax;
     const bool hist = ax.S <= SB_SMAX;
     uint32_t nbu = 0;
-    if (hist)
-      for (uint32_t j = 0; j < ax.nb; ++j) nbu += (ax.b[j].n + SB_REC - 1) / SB_REC;
+    if (hist) {  // 8 x the most units any XCD's batches have (batch j on blocks = j mod 8)
+      uint32_t per[8] = {};
+      for (uint32_t j = 0; j < ax.nb; ++j) per[j % 8] += (ax.b[j].n + SB_REC - 1) / SB_REC;
+      for (uint32_t x = 0; x < 8; ++x) nbu = max(nbu, 8u * per[x]);
+    }
     // the waves after the bucket workgroups: tape tiles (and per-record bucket blocks without hist)
     const uint32_t units = max(hist ? 0u : (nbr + 63u) / 64u, (ntr + TILE_TAPE - 1) / TILE_TAPE);
     const uint32_t twg = min((units + SIDE_WAVES - 1) / SIDE_WAVES, max(ax.nwg, 1u) * 4u);
