@@ -1044,19 +1044,27 @@ __device__ __forceinline__ void aux_tape_tile(const GA& G, uint32_t jb, uint32_t
   }
 }
 
-// Side-job wave a of A: its share of every bucket / clear job of group J and every tape job of J-2.
-__device__ __forceinline__ void aux_jobs(const ColdArgs& G, uint32_t a, uint32_t A) {
+// Side-job wave k of side workgroup b (of nwg): its share of every bucket / clear job of group J and
+// every tape job of J-2. A batch's bucket job runs on the side waves of the
+// workgroups b = j (mod 8) only — one XCD under round-robin placement (speed only): every bucket of the
+// batch is then written from one L2, whole lines instead of partial lines from eight XCDs.
+__device__ __forceinline__ void aux_jobs(const ColdArgs& G, uint32_t b, uint32_t k, uint32_t nwg) {
   const int lane = lane_id();
+  const uint32_t a = b * REG_WAVES + k, A = nwg * REG_WAVES;
   const uint32_t nb = ldsu(G.ax.nb);
+  const bool xg = nwg >= 8u;
+  const uint32_t x = b % 8u, ax_ = (b / 8u) * REG_WAVES + k, Ax = ((nwg - x + 7u) / 8u) * REG_WAVES;
   for (uint32_t j = 0; j < nb; ++j) {
     const AuxBucket& J = G.ax.b[j];
     const uint32_t zt = ldsu(J.zero_tiles);
     const gptr<uint32_t> z = ldsg(J.zero_tile_sum);
     for (uint32_t i = a * 64u + (uint32_t)lane; i < zt; i += A * 64u) z[i] = 0u;
     if (a == 0 && lane == 0) *ldsg(J.zero_top) = 0ull;
+    if (xg && j % 8u != x) continue;
+    const uint32_t wa = xg ? ax_ : a, WA = xg ? Ax : A;
     const uint32_t n = ldsu(J.n);
-    const uint32_t per = (((n + A - 1u) / A) + 63u) & ~63u;
-    const uint32_t r0 = min(n, a * per);
+    const uint32_t per = (((n + WA - 1u) / WA) + 63u) & ~63u;
+    const uint32_t r0 = min(n, wa * per);
     aux_bucket(G, j, r0, min(n, r0 + per));
   }
   const uint32_t nt = ldsu(G.ax.nt);
@@ -1284,7 +1292,7 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (wv >= (uint32_t)REG_WAVES) {  // side-job wave (only in the workgroups of the first dispatch round)
     const uint32_t k = wv - REG_WAVES, nwg = max(min(args.ax.nwg, gridDim.x), 1u);
-    if (!kSlow && blockIdx.x < nwg) aux_jobs(G, blockIdx.x * REG_WAVES + k, nwg * REG_WAVES);
+    if (!kSlow && blockIdx.x < nwg) aux_jobs(G, blockIdx.x, k, nwg);
     return;
   }
 #ifndef ME_NO_SETPRIO
