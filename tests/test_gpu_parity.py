@@ -388,8 +388,9 @@ def test_edge_bucket_boundaries(me, orc):
 
 
 def test_edge_symbol_count_sort_plans(me, orc):
-    """1-pass sort up to 2047 symbols, 2-pass from 2048: exercise both sides of the switch."""
-    for S in (1, 2, 2047, 2048, 70_000):
+    """1-pass sort up to 2047 symbols, 2-pass from 2048: exercise both sides of the switch; and the
+    fill launch's bucket job (k_side) on both sides of its LDS-histogram limit (16,383 symbols)."""
+    for S in (1, 2, 2047, 2048, 16_383, 16_384, 70_000):
         sc = me.preset(2, num_symbols=S, batch=20000)
         st = me.Stream(sc)
         base = st.base_prices()
