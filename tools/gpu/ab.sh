@@ -1,6 +1,6 @@
 #!/bin/bash
 # Same-box A/B of library variants: the default bench (no CPU baseline) per library, R rounds
-# interleaved.   usage: tools_gpu_ab.sh TAG ROUNDS lib1.so [lib2.so ...]
+# interleaved.   usage: tools/gpu/ab.sh TAG ROUNDS lib1.so [lib2.so ...]
 set -o pipefail
 TAG=$1; RN=$2; shift; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}

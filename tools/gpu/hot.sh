@@ -1,6 +1,6 @@
 #!/bin/bash
 # Deep-window hot-symbol path: GPU parity tests, then the config-4 bench line with and without the
-# k_match_hot hand-off (ME_HOT_MIN=0). usage: tools_gpu_hot.sh TAG [tests-filter]
+# k_match_hot hand-off (ME_HOT_MIN=0). usage: tools/gpu/hot.sh TAG [tests-filter]
 set -o pipefail
 TAG=${1:-hot}
 R=${GRAFT_REPO_ROOT:-$(pwd)}

@@ -1,6 +1,6 @@
 #!/bin/bash
 # config-4 A/B of the deep-window hand-off: old path (ME_HOT_MIN=0), hot kernel with / without
-# its head-chunk cache. usage: tools_gpu_hotab.sh TAG
+# its head-chunk cache. usage: tools/gpu/hotab.sh TAG
 set -o pipefail
 TAG=${1:-hotab}
 R=${GRAFT_REPO_ROOT:-$(pwd)}

@@ -1,6 +1,6 @@
 #!/bin/bash
 # SQ instruction-mix counters of k_match for several library variants (ME_ENGINE_LIB).
-# usage: tools_gpu_pmc_cmp.sh TAG lib1.so [lib2.so ...]
+# usage: tools/gpu/pmc_cmp.sh TAG lib1.so [lib2.so ...]
 set -o pipefail
 TAG=$1; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}

@@ -1,5 +1,5 @@
 #!/bin/bash
-# SQ counters of k_match_hot on config 4 (the busy symbols only). usage: tools_gpu_pmc_hot.sh TAG
+# SQ counters of k_match_hot on config 4 (the busy symbols only). usage: tools/gpu/pmc_hot.sh TAG
 set -o pipefail
 TAG=${1:-pmchot}
 R=${GRAFT_REPO_ROOT:-$(pwd)}

@@ -1,6 +1,6 @@
 #!/bin/bash
 # k_match PMC counter sets (one rocprofv3 pass per set) for one library variant.
-# usage: tools_gpu_pmc_sets.sh TAG LIB "CNT1 CNT2 ..." ["..."]
+# usage: tools/gpu/pmc_sets.sh TAG LIB "CNT1 CNT2 ..." ["..."]
 set -o pipefail
 TAG=$1; LIB=$2; shift; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Quick GPU iteration: parity tests, a short bench (no CPU baseline), phase stamps of config 2.
-# usage: tools_gpu_quick.sh TAG [notests]
+# usage: tools/gpu/quick.sh TAG [notests]
 set -o pipefail
 TAG=${1:-quick}
 R=${GRAFT_REPO_ROOT:-$(pwd)}

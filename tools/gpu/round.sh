@@ -2,7 +2,7 @@
 # One GPU session for the record: gpu tests, smoke, rocprofv3 kernel-trace stats of a short bench,
 # the HBM-traffic PMC passes (FETCH_SIZE / WRITE_SIZE, one counter per pass) on k_match, and the
 # default bench line carrying that traffic. Every GPU step has its own time limit; the first
-# failure ends the session.   usage: tools_gpu_round.sh TAG [skip-tests]
+# failure ends the session.   usage: tools/gpu/round.sh TAG [skip-tests]
 set -o pipefail
 TAG=${1:-run}
 R=${GRAFT_REPO_ROOT:-$(pwd)}

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Kernel timeline of a short bench run (rocprofv3 kernel trace) -> per-kernel averages and gaps.
-# usage: tools_gpu_trace.sh TAG [extra bench args]
+# usage: tools/gpu/trace.sh TAG [extra bench args]
 set -o pipefail
 TAG=${1:-trace}
 shift
