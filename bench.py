@@ -85,9 +85,11 @@ def parse():
                          "the stream a few us; 1 = every launch, 0 = off)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (RCCL, one rank per GPU: the real run); gloo only to rehearse N>1 on one GPU")
-    ap.add_argument("--gather-steps", type=int, default=10,
-                    help="N>1: batches run after the timed loop with the RCCL tape/result gather to rank 0 "
-                         "(reported beside value, never in it)")
+    ap.add_argument("--cluster-steps", type=int, default=None,
+                    help="global slices run after the timed loop through the C++ sharded deployment "
+                         "(include/me_cluster.h: split on rank 0, RCCL scatter, match, RCCL gather of tapes and "
+                         "results, merge by taker seq); reported beside value, never in it. Default: 16 at N > 1, "
+                         "0 at N = 1")
     ap.add_argument("--traffic-from", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="JSON {bytes_per_order: ...} from tools/gpu_pmc_traffic.sh for roofline.traffic (c2)")
     args = ap.parse_args()
@@ -146,9 +148,10 @@ def allreduce(v, world, op, local):
     return float(t.item())
 
 
-def build_rank_batches(args, world, rank, nbatches):
+def build_rank_batches(args, world, rank, nbatches, n_whole=0):
     """Global stream, hash-sharded; this rank's batches with local symbol ids (and, per batch, the
-    positions of its records in the global batch)."""
+    positions of its records in the global batch); then n_whole more global batches left whole (the
+    cluster leg's slices)."""
     w = WORKLOADS[args.workload]
     S = global_symbols(args, world)
     sc = me.preset(w["preset"], num_symbols=S, batch=args.batch_per_gpu * world)
@@ -172,7 +175,8 @@ def build_rank_batches(args, world, rank, nbatches):
         lb.symbol = np.ascontiguousarray(local[lb.symbol], dtype=np.uint32)
         out.append(lb)
         pos.append(sel)
-    return sc, base[ids], ids, out, pos, sc.batch * nbatches, seeds
+    whole = [st.next(sc.batch) for _ in range(n_whole)]
+    return sc, base, ids, out, pos, sc.batch * nbatches, seeds, whole
 
 
 def cpu_baseline(args):
@@ -371,23 +375,64 @@ def host_info():
             "cpus_allowed": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None}
 
 
+def cluster_leg(args, world, rank, local, sc, base, slices):
+    """N > 1: the sharded deployment as a server runs it — rank 0 submits each global slice to
+    me_cluster (split by symbol owner, parts scattered over RCCL, matched on every GPU, tapes and results
+    gathered back over RCCL and merged by taker seq), two slices in flight; the other ranks serve. Its
+    own engines (fresh books), informational: orders/s through the whole round trip, never `value`."""
+    from matching_engine_amd.cluster import Cluster
+
+    import torch.distributed as tdist
+
+    transport = "rccl" if (world == 1 or tdist.get_backend() == "nccl") else "tcp"
+    port = int(os.environ.get("MASTER_PORT", "29500")) + 11
+    cl = Cluster(rank, world, len(base), sc.batch, transport=transport, port=port, device=local, levels=sc.levels,
+                 base_prices=base, max_resting=sc.batch * (len(slices) + 1), timeout_ms=120000,
+                 seq_ring=args.seq_ring, batches_per_launch=2)
+    out = None
+    if rank == 0:
+        t0 = time.perf_counter()
+        pend, fills, n = [], 0, 0
+        for b in slices:
+            pend.append((cl.submit(b), len(b)))
+            n += len(b)
+            if len(pend) == 2:
+                t, k = pend.pop(0)
+                fills += len(cl.collect(t, k)[1])
+        for t, k in pend:
+            fills += len(cl.collect(t, k)[1])
+        dt = time.perf_counter() - t0
+        st = cl.stats()
+        cl.stop()
+        out = {"transport": transport, "slices": len(slices), "orders": n, "fills": fills,
+               "orders_per_s": n / dt, "ms_per_slice": dt / len(slices) * 1e3, "bytes_rank0": st["bytes"],
+               "what": "me_cluster_submit / me_cluster_collect (C++, include/me_cluster.h), two slices in flight: "
+                       "split on rank 0, grouped ncclSend/ncclRecv of the parts, admission vote (MIN "
+                       "all-reduce), match on every GPU, gather of tape lengths, grouped send of tapes + results "
+                       "to rank 0, k-way merge by taker seq on rank 0's host"}
+    else:
+        cl.serve()
+    cl.close()
+    return out
+
+
 def main():
     args = parse()
     world, rank, local = dist_setup(args)
     import torch
 
     nb = args.warmup + args.steps
-    n_gather = args.gather_steps if world > 1 else 0
+    n_cluster = args.cluster_steps if args.cluster_steps is not None else (16 if world > 1 else 0)
     n_e2e = 0 if args.no_e2e else args.e2e_steps
-    sc, base, ids, batches, positions, global_orders, seeds = build_rank_batches(args, world, rank,
-                                                                                 nb + n_gather + n_e2e)
-    gather_batches, gather_pos = batches[nb:nb + n_gather], positions[nb:nb + n_gather]
-    e2e_batches = batches[nb + n_gather:]
+    sc, gbase, ids, batches, positions, global_orders, seeds, whole = build_rank_batches(
+        args, world, rank, nb + n_e2e, n_cluster)
+    base = gbase[ids]
+    e2e_batches = batches[nb:]
     batches = batches[:nb]
-    total_local = sum(len(b) for b in batches + gather_batches + e2e_batches)
+    total_local = sum(len(b) for b in batches + e2e_batches)
     n_seed = sum(len(b) for b in seeds)
     eng = me.Engine(len(ids), sc.levels, base,
-                    max_batch=max(len(b) for b in batches + gather_batches + e2e_batches + seeds) + 1,
+                    max_batch=max(len(b) for b in batches + e2e_batches + seeds) + 1,
                     max_resting=max(total_local // 3, sum(len(b) for b in batches)) + n_seed + 65536, seq_ring=args.seq_ring,
                     device=local, symbol_ids=ids, batches_per_launch=args.batches_per_launch)
     for b in seeds:
@@ -426,50 +471,18 @@ def main():
     bytes_per_order = (BYTES_PER_ORDER * orders_local + BYTES_PER_FILL * tm["fills"]) / max(orders_local, 1)
     bytes_per_launch = bytes_per_order * tm["orders"] / timed
     achieved = bytes_per_launch / avg_match_s / 1e9
-    # roofline.traffic: PMC bytes per order of a steady full-group launch (tools/gpu_pmc_traffic.sh ->
-    # profiles/pmc_traffic.json, same workload) scaled to the orders of THIS run's timed launches, so
-    # it and algorithmic_bytes_per_launch describe the same launch shape
-    traffic = traffic_per_order = None
-    if args.traffic_from and os.path.exists(args.traffic_from) and args.workload == "c2":
-        traffic_per_order = json.load(open(args.traffic_from)).get("bytes_per_order")
+    # roofline.traffic: PMC bytes per order of a steady launch of the same workload (rocprofv3 FETCH_SIZE /
+    # WRITE_SIZE passes, tools/gpu_pmc_traffic.sh -> profiles/pmc_traffic[_cN].json) scaled to the orders of
+    # THIS run's timed launches, so it and algorithmic_bytes_per_launch describe the same launch shape
+    traffic = traffic_per_order = traffic_src = None
+    tfile = args.traffic_from
+    if args.workload != "c2":
+        tfile = os.path.join(ROOT, "profiles", f"pmc_traffic_{args.workload}.json")
+    if tfile and os.path.exists(tfile):
+        traffic_per_order = json.load(open(tfile)).get("bytes_per_order")
+        traffic_src = os.path.relpath(tfile, ROOT)
         if traffic_per_order:
             traffic = traffic_per_order * tm["orders"] / timed
-
-    # N > 1: the persistence path — every batch's tape and results gathered to rank 0 over RCCL
-    # (matching_engine_amd/gather.py), timed separately; informational, never part of value
-    rccl = None
-    if gather_batches:
-        from matching_engine_amd.gather import EngineGather
-
-        dev = torch.device("cuda", local)
-        ts = torch.cuda.Stream(device=dev)
-        eng.set_stream(ts.cuda_stream)  # the gather of batch k overlaps the match of batch k + 1
-        gat = EngineGather(eng, dev, max(len(b) for b in gather_batches), stream=ts)
-        gdbs = [eng.upload(b) for b in gather_batches]
-        gpos = [torch.from_numpy(p.astype(np.int64)).to(dev) for p in gather_pos]
-        barrier_sync(world, local)
-        tg0 = time.perf_counter()
-        gfills = 0
-        eng.submit_device(gdbs[0])
-        for k, (db, p) in enumerate(zip(gdbs, gpos)):
-            nf = gat.stage(db.n)
-            if k + 1 < len(gdbs):
-                eng.submit_device(gdbs[k + 1])
-            tape, _ = gat.collect(nf, db.n, p, sc.batch)
-            if tape is not None:
-                gfills += len(tape)
-        eng.sync()
-        barrier_sync(world, local)
-        tg = allreduce(time.perf_counter() - tg0, world, MAX, local)
-        eng.set_stream(None)
-        for db in gdbs:
-            db.free()
-        rccl = {"backend": tdist.get_backend(), "steps": len(gather_batches), "ms_per_step": tg / len(gather_batches) * 1e3,
-                "orders_per_s_incl_gather": sc.batch * len(gather_batches) / tg,
-                "tape_bytes_per_step_to_root": 32.0 * gfills / len(gather_batches),
-                "what": "submit + device tape/result copy + RCCL all_gather(sizes) + gather(tape, results) to "
-                        "rank 0 + stable merge by taker seq on rank 0's GPU + D2H of the merged tape; batch "
-                        "k's gather overlaps batch k+1's match (EngineGather.stage / collect)"}
 
     # PCIe-inclusive host path (me_submit_host / me_collect: staging copy into a pinned slot, H2D on
     # its own stream, the grouped pipeline, D2H of results + tape into pinned memory), informational.
@@ -491,7 +504,12 @@ def main():
             _, f = eng.collect(t, copy=False)
             f2 += len(f)
         e2e = n2 / (time.perf_counter() - t2)
+    max_resting = eng.config()["max_resting"]
+    for db in dbs:
+        db.free()
+    eng.close()
 
+    line = None
     if rank == 0:
         cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(args)
         c1 = c1_paths(args) if (args.workload == "c1" and world == 1 and not args.no_cpu_baseline) else None
@@ -518,14 +536,15 @@ def main():
             "fills_per_order": fills_all / max(orders_all, 1),
             "handoffs_rank0": handoffs,
             "admission_rank0": {"exact_counts": adm["exact_counts"], "resting": adm["resting"],
-                                "max_resting": eng.config()["max_resting"]},
+                                "max_resting": max_resting},
             "kernel_match_ms_avg": tm["match_ms"] / timed,
             "kernel_match_launches_timed": tm["launches"],
             "batches_per_launch": args.batches_per_launch or (32 if sc.levels <= 128 else 1),
-            "device_ms_per_step": tm["pipeline_ms"],
+            # start-to-start device time per batch between the first and last timed launches (needs two)
+            "device_ms_per_step": tm["pipeline_ms"] if tm["launches"] >= 2 else None,
             "host_enqueue_ms_per_step_rank0": t_enq / args.steps * 1e3,
             "e2e_host_path_orders_per_s_rank0": e2e,
-            "rccl_tape_gather": rccl,
+            "cluster": None,
             "roofline": {
                 "bound": "hbm",
                 "achieved": achieved,
@@ -537,16 +556,36 @@ def main():
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "algorithmic_bytes_per_order": bytes_per_order,
                 "traffic_bytes_per_order": traffic_per_order,
+                "traffic_source": traffic_src,
             },
             "cpu_baseline": cpu,
             "host": host_info(),
             "build": me._abi.load().me_build_info().decode(),  # source digest of the library that ran
             "c1_paths": c1,
         }
+    if n_cluster:
+        # the sharded deployment after the timed loop; a watchdog keeps a stuck collective from eating
+        # the run: past the limit, rank 0 prints the line without the leg and every rank exits
+        import threading
+
+        def expire():
+            if rank == 0:
+                line["cluster"] = {"error": "cluster leg timed out (180 s)"}
+                print(json.dumps(line), flush=True)
+            os._exit(0)
+
+        wd = threading.Timer(180.0, expire)
+        wd.daemon = True
+        wd.start()
+        try:
+            got = cluster_leg(args, world, rank, local, sc, gbase, whole)
+        except Exception as ex:  # reported, never fatal to the measured line
+            got = {"error": f"{type(ex).__name__}: {ex}"}
+        wd.cancel()
+        if rank == 0:
+            line["cluster"] = got
+    if rank == 0:
         print(json.dumps(line), flush=True)
-    for db in dbs:
-        db.free()
-    eng.close()
     if world > 1:
         tdist.destroy_process_group()
 

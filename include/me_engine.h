@@ -57,7 +57,9 @@ enum {
   ME_RJ_OUT_OF_WINDOW = 3, /* retired: every int64 price is accepted (never produced) */
   ME_RJ_BAD_SYMBOL = 4,    /* symbol id >= num_symbols */
   ME_RJ_UNKNOWN_ORDER = 5, /* CANCEL target is not a live resting order of this symbol */
-  ME_RJ_BAD_SEQ = 6        /* seq == 0 (no OID is 0: the counter starts at 1, storage.cpp:254-267) */
+  ME_RJ_BAD_SEQ = 6,       /* seq == 0 (no OID is 0: the counter starts at 1, storage.cpp:254-267) */
+  ME_RJ_CAPACITY = 7       /* service only: a LIMIT the shard could not admit while its books hold
+                              max_resting orders (me_service.h; never produced by the engine) */
 };
 
 /* kind byte of a batch record: bits 0-1 side, bit 2 type (1 = MARKET), bit 3 op (1 = CANCEL). */
@@ -121,8 +123,10 @@ typedef struct me_config {
                                   launch groups were submitted), else that collect fails with ME_E_CAPACITY */
 } me_config;
 
-/* One batch in structure-of-arrays form. Seqs (= numeric OIDs) strictly ascend across the whole
- * stream of an engine (checked on the device: a violation fails the batch with ME_E_INVALID). */
+/* One batch in structure-of-arrays form. Seqs (= numeric OIDs) ascend across the whole stream of an
+ * engine: a NEW record's seq is above every earlier record's, a CANCEL record's is at least the
+ * previous record's (a cancel never rests, so it may repeat the last OID instead of taking one).
+ * Checked on the device: a violation fails the batch with ME_E_INVALID. */
 typedef struct me_order_soa {
   const uint64_t* seq;      /* numeric OID of the record */
   const int64_t* price_q4;  /* NEW: normalized Q4 price (ignored for MARKET); CANCEL: target seq */
@@ -216,6 +220,11 @@ int me_get_config(const me_engine* e, me_config* out);
  * Outputs stay on the device until me_fetch_outputs (me_fetch_outputs / me_fetch_group_outputs /
  * me_copy_*_device read the most recent batch and fail with ME_E_INVALID when it was a host batch). */
 int me_submit_batch_device(me_engine* e, const me_order_soa* dev_batch, size_t n);
+/* The same with the batch's LIMIT-record count known to the caller (me_submit_batch_device counts
+ * every record of a device batch as one that may rest): admission control takes n_limits, which must
+ * be at least the batch's NEW records of type LIMIT (fewer can overflow the scratch bound: a loud,
+ * sticky ME_E_CAPACITY). The cluster's shards use it (the root counted them while splitting). */
+int me_submit_device_limits(me_engine* e, const me_order_soa* dev_batch, size_t n, uint64_t n_limits);
 /* Wait for all enqueued work; returns ME_E_CAPACITY if a pool overflowed in any batch. */
 int me_sync(me_engine* e);
 /* Copy the last batch's tape/results to host memory (synchronous). */

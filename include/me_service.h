@@ -11,8 +11,9 @@
  *                             normalisation throws), normalize_to_q4 (:89-97), side CHECK -> "DB insert
  *                             failed" with order_id set (:107-111). The order joins the open time slice.
  *                             Any non-empty symbol is accepted (:66-71): a new one takes the engine's
- *                             next unused book; only when all of them are taken is it refused
- *                             (grpc_status 8 RESOURCE_EXHAUSTED, "symbol capacity exhausted", no OID).
+ *                             next unused book, or an idle symbol's book once all are taken (below);
+ *                             only when every book holds orders is it refused (grpc_status 8
+ *                             RESOURCE_EXHAUSTED, "symbol capacity exhausted", no OID).
  *   me_service_flush          the time-slice batcher: matches every slice submitted so far on the engine
  *                             (me_submit_host / me_collect) and ingests each in ONE SQLite transaction
  *                             (orders rows as insert_new_order writes them carrying the matched status
@@ -27,6 +28,21 @@
  *   me_service_market_data    StreamMarketData's MarketDataUpdate (proto:60-67) from the GPU book.
  *   me_service_updates        StreamOrderUpdates (proto/matching_engine.proto:34,71-91): drains the
  *                             OrderUpdate events the flushes produced, optionally for one client_id.
+ *
+ * Restart: the reference resumes only its OID counter from the DB (matching_engine_service.cpp:18-22,
+ * storage.cpp:254-267). me_service_create does that and also rebuilds the books: every order the DB
+ * shows resting (status NEW / PARTIALLY_FILLED, remaining_quantity > 0) is replayed into the backend
+ * in OID order with its remainder, before the first SubmitOrder is matched, so it keeps its price-time
+ * priority, can trade and can be cancelled.
+ *
+ * Symbols: any non-empty symbol is accepted (:66-71). The backend holds a fixed number of books; when
+ * every book is taken, a new symbol takes over a book with no resting order and no record on its way
+ * (the old symbol's book is reclaimed). Only when every book is in use is the order refused
+ * (RESOURCE_EXHAUSTED, no OID).
+ *
+ * Capacity: a slice the backend refuses (its books near max_resting) is split and matched in parts;
+ * a single LIMIT that still does not fit is answered in-band with an OrderUpdate REJECTED (reason
+ * ME_RJ_CAPACITY) instead of stalling every later slice behind it.
  */
 #ifndef ME_SERVICE_H
 #define ME_SERVICE_H
@@ -85,6 +101,12 @@ typedef struct me_matcher {
   int (*book)(void* ctx, uint32_t symbol, uint32_t depth, me_book_entry* bids, size_t bids_cap, size_t* n_bids,
               me_book_entry* asks, size_t asks_cap, size_t* n_asks, me_level* bid_levels, me_level* ask_levels,
               size_t* n_bid_levels, size_t* n_ask_levels);
+  /* Optional, both or neither: match split in two, so the service keeps two slices in flight (slice k+1
+   * is submitted before slice k is collected). submit applies the slice and returns a ticket
+   * (ME_E_CAPACITY: refused, nothing applied); collect returns that ticket's outputs (valid until the
+   * next collect). Tickets are collected in submission order, at most two outstanding. */
+  int (*submit)(void* ctx, const me_order_soa* slice, size_t n, uint64_t* ticket);
+  int (*collect)(void* ctx, uint64_t ticket, const me_fill** fills, size_t* n_fills, const me_order_result** results);
 } me_matcher;
 
 /* The service over a matcher instead of an engine (same contract otherwise). NULL on a bad matcher. */
@@ -128,7 +150,8 @@ size_t me_service_unpersisted(const me_service* s);
 int me_service_start(me_service* s, uint32_t interval_us, uint32_t slice_orders);
 int me_service_stop(me_service* s);
 
-/* Level view of GetOrderBook for a symbol string (top depth levels per side, aggregates). */
+/* Level view of GetOrderBook for a symbol string (top depth levels per side, aggregates; depth 0:
+ * no levels). */
 int me_service_book(me_service* s, const char* symbol, me_level* bids, me_level* asks, size_t depth,
                     size_t* n_bids, size_t* n_asks);
 
@@ -160,8 +183,9 @@ typedef struct me_cancel_request {
 
 /* Validation (first failing check wins, in-band like SubmitOrder :66-83): "symbol is required",
  * "order_id is invalid" (not "OID-<n>", n >= 1), "order belongs to another client" (the target is a
- * resting or pending order of a different client_id). An accepted cancel consumes the next OID number as
- * its stream position (like any request reaching :85) and answers success=1 with order_id = the
+ * resting or pending order of a different client_id). An accepted cancel consumes NO OID: its stream
+ * position is the last OID allocated (a cancel record may repeat the previous seq, me_engine.h), so
+ * accepted orders keep the reference's gap-free OID sequence. It answers success=1 with order_id = the
  * TARGET's id; whether it removed anything arrives as an OrderUpdate after the flush (CANCELED with
  * the removed quantity, or REJECTED when the target was not resting on that symbol). */
 int me_service_cancel_order(me_service* s, const me_cancel_request* req, me_order_response* resp);
@@ -184,6 +208,12 @@ typedef struct me_order_update {
 /* Drain up to cap queued updates (client_id NULL or "": every client; else only that client's,
  * leaving the others queued). *n = updates written; returns ME_OK. */
 int me_service_updates(me_service* s, const char* client_id, me_order_update* out, size_t cap, size_t* n);
+/* Events dropped because the queue held 2^24 undrained updates (the oldest go first; each drop also
+ * sets me_service_last_error). */
+uint64_t me_service_updates_dropped(const me_service* s);
+/* Books handed from an idle symbol to a new one since create, and resting orders replayed into the
+ * books from the DB at create (restart recovery). */
+int me_service_stats(const me_service* s, uint64_t* reclaimed_books, uint64_t* recovered_orders);
 
 /* MarketDataUpdate (proto:60-67) for StreamMarketData, from the GPU book: best bid / ask (Q4,
  * scale 4) and the total quantity resting there (saturated to int32). The reference's

@@ -19,7 +19,7 @@ SIDE_UNSPECIFIED, SIDE_BUY, SIDE_SELL = 0, 1, 2
 TYPE_LIMIT, TYPE_MARKET = 0, 1
 OP_NEW, OP_CANCEL = 0, 1
 ST_NEW, ST_PARTIALLY_FILLED, ST_FILLED, ST_CANCELED, ST_REJECTED = 0, 1, 2, 3, 4
-RJ_NONE, RJ_BAD_QTY, RJ_BAD_SIDE, RJ_OUT_OF_WINDOW, RJ_BAD_SYMBOL, RJ_UNKNOWN_ORDER, RJ_BAD_SEQ = range(7)
+RJ_NONE, RJ_BAD_QTY, RJ_BAD_SIDE, RJ_OUT_OF_WINDOW, RJ_BAD_SYMBOL, RJ_UNKNOWN_ORDER, RJ_BAD_SEQ, RJ_CAPACITY = range(8)
 ME_OK, ME_E_INVALID, ME_E_HIP, ME_E_CAPACITY, ME_E_STATE, ME_E_SQLITE = 0, -1, -2, -3, -4, -5
 CHUNK_SLOTS = 16
 
@@ -124,6 +124,7 @@ PROTOTYPES = {
     "me_get_config": (C.c_int, [_P, C.POINTER(MeConfig)]),
     "me_host_reserve": (C.c_int, [_P, C.c_uint32]),
     "me_submit_batch_device": (C.c_int, [_P, C.POINTER(MeOrderSoa), _SZ]),
+    "me_submit_device_limits": (C.c_int, [_P, C.POINTER(MeOrderSoa), _SZ, C.c_uint64]),
     "me_sync": (C.c_int, [_P]),
     "me_fetch_outputs": (C.c_int, [_P, _P, _SZ, C.POINTER(_SZ), _P, _SZ]),
     "me_last_group_size": (C.c_uint32, [_P]),
@@ -271,6 +272,9 @@ MATCH_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(MeOrderSoa), C.c_size_t, C
 BOOK_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t),
                       C.c_void_p, C.c_size_t, C.POINTER(C.c_size_t), C.c_void_p, C.c_void_p, C.POINTER(C.c_size_t),
                       C.POINTER(C.c_size_t))
+SUBMIT_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(MeOrderSoa), C.c_size_t, C.POINTER(C.c_uint64))
+COLLECT_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_uint64, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t),
+                         C.POINTER(C.c_void_p))
 
 
 class MeMatcher(C.Structure):
@@ -281,6 +285,41 @@ class MeMatcher(C.Structure):
         ("max_resting", C.c_uint64),
         ("match", MATCH_FN),
         ("book", BOOK_FN),
+        ("submit", SUBMIT_FN),
+        ("collect", COLLECT_FN),
+    ]
+
+
+# ---- include/me_cluster.h ---------------------------------------------------------------------
+TRANSPORT_RCCL, TRANSPORT_TCP = 0, 1
+
+
+class MeClusterConfig(C.Structure):
+    _fields_ = [
+        ("rank", C.c_uint32),
+        ("world", C.c_uint32),
+        ("num_symbols", C.c_uint32),
+        ("max_batch", C.c_uint32),
+        ("transport", C.c_int32),
+        ("device", C.c_int32),
+        ("addr", C.c_char_p),
+        ("port", C.c_uint32),
+        ("timeout_ms", C.c_uint32),
+    ]
+
+
+ADMIT_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_uint64, C.POINTER(C.c_int))
+LEVELS_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p)
+
+
+class MeShardOps(C.Structure):
+    _fields_ = [
+        ("ctx", C.c_void_p),
+        ("max_resting", C.c_uint64),
+        ("admit", ADMIT_FN),
+        ("match", MATCH_FN),
+        ("book", BOOK_FN),
+        ("levels_all", LEVELS_FN),
     ]
 
 
@@ -303,4 +342,20 @@ PROTOTYPES.update({
     "me_service_submit_orders": (C.c_int, [_P, C.POINTER(MeOrderRequest), _SZ, C.POINTER(MeOrderResponse)]),
     "me_service_start": (C.c_int, [_P, C.c_uint32, C.c_uint32]),
     "me_service_stop": (C.c_int, [_P]),
+    "me_service_updates_dropped": (C.c_uint64, [_P]),
+    "me_service_stats": (C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "me_cluster_shard_symbols": (_SZ, [C.c_uint32, C.c_uint32, C.c_uint32, _P, _SZ]),
+    "me_cluster_create": (_P, [C.POINTER(MeClusterConfig), C.POINTER(MeConfig), C.POINTER(MeShardOps)]),
+    "me_cluster_stop": (C.c_int, [_P]),
+    "me_cluster_destroy": (None, [_P]),
+    "me_cluster_serve": (C.c_int, [_P]),
+    "me_cluster_submit": (C.c_int, [_P, C.POINTER(MeOrderSoa), _SZ, C.POINTER(C.c_uint64)]),
+    "me_cluster_collect": (C.c_int, [_P, C.c_uint64, C.POINTER(_P), C.POINTER(_SZ), C.POINTER(_P)]),
+    "me_cluster_match": (C.c_int, [_P, C.POINTER(MeOrderSoa), _SZ, C.POINTER(_P), C.POINTER(_SZ), C.POINTER(_P)]),
+    "me_cluster_book": (C.c_int, [_P, C.c_uint32, C.c_uint32, _P, _SZ, C.POINTER(_SZ), _P, _SZ, C.POINTER(_SZ),
+                                  _P, _P, C.POINTER(_SZ), C.POINTER(_SZ)]),
+    "me_cluster_snapshot": (C.c_int, [_P, C.c_uint32, _P, _P]),
+    "me_cluster_matcher": (C.c_int, [_P, C.POINTER(MeMatcher)]),
+    "me_cluster_stats": (C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "me_cluster_last_error": (C.c_int, [_P, C.c_char_p, _SZ]),
 })

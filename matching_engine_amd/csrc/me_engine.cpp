@@ -29,9 +29,9 @@ hipError_t launch_sort_pass(hipStream_t st, const uint32_t* keys_in, const uint3
                             uint32_t clamp_key, int shift, int dbits, uint32_t* hist, uint32_t* tot,
                             uint32_t* keys_out, uint32_t* idx_out, uint32_t* zero_buf,
                             uint32_t zero_words, unsigned long long* scratch_top, uint32_t* bin_start,
-                            const uint64_t* seq, uint32_t* err);
-hipError_t launch_seq_sweep(hipStream_t st, const BookDev& bk, const uint64_t* const* seq, const uint32_t* n,
-                            uint32_t ng, uint32_t in_idx, uint32_t grid, uint32_t launch);
+                            const uint64_t* seq, const uint8_t* kind, uint32_t* err);
+hipError_t launch_seq_sweep(hipStream_t st, const BookDev& bk, const uint64_t* const* seq, const uint8_t* const* kind,
+                            const uint32_t* n, uint32_t ng, uint32_t in_idx, uint32_t grid, uint32_t launch);
 hipError_t launch_match(hipStream_t st, const BookDev& bk, const BatchDev& bt, hipEvent_t ev0, hipEvent_t ev1);
 hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* bt, uint32_t ng, const AuxDev& ax, hipEvent_t ev0,
                             hipEvent_t ev1);
@@ -684,14 +684,16 @@ static BatchDev batch_dev(me_engine* e, const uint64_t* seq, const int64_t* px, 
 // index the match launches read.
 static int seq_sweep(me_engine* e, const me_engine::Group& g) {
   const uint64_t* seq[ME_GMAX];
+  const uint8_t* kind[ME_GMAX];
   uint32_t n[ME_GMAX];
   for (uint32_t k = 0; k < g.n; ++k) {
     seq[k] = g.b[k].seq;
+    kind[k] = g.b[k].kind;
     n[k] = g.b[k].n;
   }
   // a small grid: the launch is on the stream before every match launch and usually decides "no
   // sweep" (a 1,024-workgroup grid cost ~0.7 us per batch at config 2); a due sweep loops over the pool
-  hipError_t he = launch_seq_sweep(e->stream, e->bk, seq, n, g.n, e->sq_idx, 64, e->launch_no);
+  hipError_t he = launch_seq_sweep(e->stream, e->bk, seq, kind, n, g.n, e->sq_idx, 64, e->launch_no);
   if (he != hipSuccess) return e->hip_fail(he, "seq sweep launch");
   e->sq_idx ^= 1u;
   e->bk.sq_idx = e->sq_idx;
@@ -921,6 +923,7 @@ static int enqueue_batch(me_engine* e, const uint64_t* seq, const int64_t* px, c
     me_engine::Group g1;
     g1.n = 1;
     g1.b[0].seq = seq;
+    g1.b[0].kind = kind;
     g1.b[0].n = n;
     int rc2 = seq_sweep(e, g1);
     if (rc2) return rc2;
@@ -929,7 +932,7 @@ static int enqueue_batch(me_engine* e, const uint64_t* seq, const int64_t* px, c
     hipError_t he = launch_sort_pass(st, kin, iin, n, S, shift, e->dbits[p], sl.hist,
                                      sl.tot + ((size_t)p << MAX_DIGIT_BITS), sl.keys[p], sl.idx[p],
                                      p == 0 ? o.tile_sum : nullptr, p == 0 ? ntiles_tape : 0, o.top,
-                                     p == e->passes - 1 ? run_table : nullptr, p == 0 ? seq : nullptr, e->bk.err);
+                                     p == e->passes - 1 ? run_table : nullptr, p == 0 ? seq : nullptr, kind, e->bk.err);
     if (he != hipSuccess) return e->hip_fail(he, "grouping sort launch");
     kin = sl.keys[p];
     iin = sl.idx[p];
@@ -982,7 +985,7 @@ static int check_err_bits(me_engine* e, uint32_t w) {
     if (w & ERR_INCONSISTENT) m += " book inconsistency;";
     if (w & ERR_FAR_OOM) m += " far-level array full (raise far_levels);";
     if (w & ERR_OLD_OOM) m += " old-order table full (raise max_resting);";
-    if (w & ERR_SEQ_ORDER) m += " seqs not strictly ascending (API precondition);";
+    if (w & ERR_SEQ_ORDER) m += " seqs not ascending (API precondition: a NEW record's seq above every earlier seq, a CANCEL's at least the previous one);";
     if (w & ERR_SEQ_SPAN) m += " one launch group spans the whole seq ring (raise seq_ring);";
     const int code = (w & (ERR_SEQ_ORDER | ERR_SEQ_SPAN)) && !(w & ~(ERR_SEQ_ORDER | ERR_SEQ_SPAN)) ? ME_E_INVALID
                                                                                                     : ME_E_CAPACITY;
@@ -1098,6 +1101,10 @@ extern "C" int me_admission_read(me_engine* e, uint64_t* resting, uint64_t* boun
 }
 
 extern "C" int me_submit_batch_device(me_engine* e, const me_order_soa* b, size_t n) {
+  return me_submit_device_limits(e, b, n, n);  // the kinds are on the device: every record counts as a LIMIT
+}
+
+extern "C" int me_submit_device_limits(me_engine* e, const me_order_soa* b, size_t n, uint64_t n_limits) {
   if (!e) return ME_E_INVALID;
   if (e->failed) return ME_E_STATE;
   if (!b || !b->seq || !b->price_q4 || !b->qty || !b->symbol || !b->kind) return e->fail(ME_E_INVALID, "null batch");
@@ -1107,9 +1114,10 @@ extern "C" int me_submit_batch_device(me_engine* e, const me_order_soa* b, size_
   }
   if (n > e->cfg.max_batch) return e->fail(ME_E_INVALID, "batch larger than max_batch");
   HIP_TRY(hipSetDevice(e->dev), "hipSetDevice");
-  const int rc = admit(e, n);  // the kinds are on the device: every record counts as a LIMIT
+  const uint64_t nl = std::min<uint64_t>(n_limits, n);
+  const int rc = admit(e, nl);
   if (rc) return rc;
-  return enqueue_batch(e, b->seq, b->price_q4, b->qty, b->symbol, b->kind, (uint32_t)n, (uint32_t)n);
+  return enqueue_batch(e, b->seq, b->price_q4, b->qty, b->symbol, b->kind, (uint32_t)n, (uint32_t)nl);
 }
 
 extern "C" int me_sync(me_engine* e) {

@@ -45,11 +45,12 @@ __device__ __forceinline__ uint32_t sort_digit(uint32_t k, const SortPass& p) {
 }
 
 // Per-tile histograms, tile-major [tile][bin].
-// The first pass also checks the API precondition the seq ring relies on (seqs strictly ascending).
+// The first pass also checks the API precondition the seq ring relies on (seqs ascending, seq_follows).
 __global__ __launch_bounds__(256) void k_sort_hist(const uint32_t* __restrict__ keys_in, uint32_t n, SortPass p,
                                                    uint32_t* __restrict__ hist, uint32_t* zero_buf,
                                                    uint32_t zero_words, unsigned long long* scratch_top,
-                                                   const uint64_t* __restrict__ seq, uint32_t* err) {
+                                                   const uint64_t* __restrict__ seq,
+                                                   const uint8_t* __restrict__ kind, uint32_t* err) {
   __shared__ uint32_t h[1u << MAX_DIGIT_BITS];
   for (uint32_t b = threadIdx.x; b < p.nbins; b += blockDim.x) h[b] = 0;
   __syncthreads();
@@ -58,7 +59,7 @@ __global__ __launch_bounds__(256) void k_sort_hist(const uint32_t* __restrict__ 
   bool order_ok = true;
   for (uint32_t i = t0 + threadIdx.x; i < t1; i += blockDim.x) {
     atomicAdd(&h[sort_digit(keys_in[i], p)], 1u);
-    if (seq && i > 0) order_ok &= seq[i] > seq[i - 1];
+    if (seq && i > 0) order_ok &= seq_follows(seq[i - 1], seq[i], kind[i]);
   }
   if (!order_ok) atomicOr(err, ERR_SEQ_ORDER);
   __syncthreads();
@@ -1241,6 +1242,7 @@ __global__ __launch_bounds__(256) void k_match(BookDev bk, BatchDev bt) {
 // workgroup makes the same decision from state[in] and the group's first / last seqs.
 struct SeqGroup {
   const uint64_t* seq[ME_GMAX];
+  const uint8_t* kind[ME_GMAX];  // the first record's kind: a cancel may repeat the previous seq
   uint32_t n[ME_GMAX];
   uint32_t ng;
   uint32_t in;  // state index read; the kernel writes state[in ^ 1]
@@ -1255,8 +1257,9 @@ __global__ __launch_bounds__(256) void k_seq_sweep(BookDev bk, SeqGroup sg) {
   const bool need = gmax - st.horizon >= R;
   const uint32_t epoch = need ? st.epoch + 1u : st.epoch;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    bool order_ok = st.last == 0ull || gmin > st.last;
-    for (uint32_t g = 0; g + 1 < sg.ng; ++g) order_ok &= sg.seq[g][sg.n[g] - 1] < sg.seq[g + 1][0];
+    bool order_ok = st.last == 0ull || seq_follows(st.last, gmin, sg.kind[0][0]);
+    for (uint32_t g = 0; g + 1 < sg.ng; ++g)
+      order_ok &= seq_follows(sg.seq[g][sg.n[g] - 1], sg.seq[g + 1][0], sg.kind[g + 1][0]);
     uint32_t bits = 0;
     if (!order_ok) bits |= ERR_SEQ_ORDER;
     if (gmax - gmin >= R) bits |= ERR_SEQ_SPAN;
@@ -1402,7 +1405,7 @@ hipError_t launch_sort_pass(hipStream_t st, const uint32_t* keys_in, const uint3
                             uint32_t clamp_key, int shift, int dbits, uint32_t* hist, uint32_t* tot,
                             uint32_t* keys_out, uint32_t* idx_out, uint32_t* zero_buf,
                             uint32_t zero_words, unsigned long long* scratch_top, uint32_t* bin_start,
-                            const uint64_t* seq, uint32_t* err) {
+                            const uint64_t* seq, const uint8_t* kind, uint32_t* err) {
   SortPass p;
   p.shift = (uint32_t)shift;
   p.mask = (1u << dbits) - 1u;
@@ -1411,7 +1414,7 @@ hipError_t launch_sort_pass(hipStream_t st, const uint32_t* keys_in, const uint3
   p.ntiles = (n + p.tile - 1) / p.tile;
   p.clamp = clamp_key;
   hipLaunchKernelGGL(k_sort_hist, dim3(p.ntiles), dim3(256), 0, st, keys_in, n, p, hist, zero_buf, zero_words,
-                     scratch_top, seq, err);
+                     scratch_top, seq, kind, err);
   hipLaunchKernelGGL(k_sort_colscan, dim3((p.nbins + 63) / 64), dim3(64), 0, st, hist, tot, p.nbins, p.ntiles);
   hipLaunchKernelGGL(k_sort_scatter, dim3(p.ntiles), dim3(256), 0, st, keys_in, idx_in, n, p, (uint32_t)dbits, hist,
                      tot, keys_out, idx_out, bin_start);
@@ -1438,13 +1441,14 @@ hipError_t launch_match(hipStream_t st, const BookDev& bk, const BatchDev& bt, h
 
 // The seq-ring horizon check (and, when due, the old-order table rebuild) ahead of a match launch
 // over batches seq[0..ng) (n[g] > 0 each). Reads state in_idx, writes state in_idx ^ 1.
-hipError_t launch_seq_sweep(hipStream_t st, const BookDev& bk, const uint64_t* const* seq, const uint32_t* n,
-                            uint32_t ng, uint32_t in_idx, uint32_t grid, uint32_t launch) {
+hipError_t launch_seq_sweep(hipStream_t st, const BookDev& bk, const uint64_t* const* seq, const uint8_t* const* kind,
+                            const uint32_t* n, uint32_t ng, uint32_t in_idx, uint32_t grid, uint32_t launch) {
   if (ng == 0 || ng > (uint32_t)ME_GMAX) return hipErrorInvalidValue;
   SeqGroup sg{};
   for (uint32_t g = 0; g < ng; ++g) {
     if (!n[g]) return hipErrorInvalidValue;
     sg.seq[g] = seq[g];
+    sg.kind[g] = kind[g];
     sg.n[g] = n[g];
   }
   sg.ng = ng;

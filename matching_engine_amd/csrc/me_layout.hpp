@@ -49,9 +49,16 @@ enum : uint32_t {
   ERR_INCONSISTENT = 4u,
   ERR_FAR_OOM = 8u,      // a symbol's far-level array is full (me_config.far_levels)
   ERR_OLD_OOM = 16u,     // the old-order table overflowed (sized from max_resting)
-  ERR_SEQ_ORDER = 32u,   // seqs not strictly ascending across the stream (API precondition)
+  ERR_SEQ_ORDER = 32u,   // seqs not ascending across the stream (API precondition, seq_follows)
   ERR_SEQ_SPAN = 64u,    // one launch group spans >= the seq ring (raise me_config.seq_ring)
 };
+
+// API precondition the seq ring relies on: seqs ascend through an engine's stream. A CANCEL record
+// (it never rests, so no ring entry is keyed by its seq) may repeat the previous record's seq: the
+// service gives a cancel the last allocated OID as its stream position instead of consuming one.
+__host__ __device__ __forceinline__ bool seq_follows(unsigned long long prev, unsigned long long cur, uint32_t kind) {
+  return cur > prev || (cur == prev && ((kind >> 3) & 1u) != 0u);
+}
 
 struct alignas(16) Level {
   long long total;   // live quantity on the level (0 <=> empty, head == tail == NIL)

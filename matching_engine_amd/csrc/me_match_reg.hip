@@ -936,8 +936,9 @@ __device__ __forceinline__ void aux_bucket(const GA& G, uint32_t j, uint32_t r0,
   for (uint32_t i0 = r0; i0 < r1; i0 += 64) {
     const uint32_t i = i0 + (uint32_t)lane;
     if (i < r1) {
-      // API precondition (the seq ring relies on it): seqs strictly ascending through the batch
-      if (i > 0) order_ok &= seq[i] > seq[i - 1];
+      const uint32_t k = kind[i];
+      // API precondition (the seq ring relies on it): seqs ascending through the batch (seq_follows)
+      if (i > 0) order_ok &= seq_follows(seq[i - 1], seq[i], k);
       const uint32_t b = min(sym[i], S);
       if (b == S) {  // unknown symbol: rejected here, never bucketed (the batch's result set is free)
         reject_bad_at(bres, i);
@@ -946,7 +947,6 @@ __device__ __forceinline__ void aux_bucket(const GA& G, uint32_t j, uint32_t r0,
       const uint64_t sq = seq[i];  // the payload loads are in flight while the atomic returns
       const int64_t p = px[i];
       const int32_t q = qty[i];
-      const uint32_t k = kind[i];
       const uint32_t r = atomicAdd(&bcnt[(size_t)b * BK_CNT_STRIDE], 1u);
       if (r < (uint32_t)BK_CAP) {
         const size_t d = (size_t)b * BK_CAP + r;
@@ -1146,8 +1146,8 @@ __device__ __forceinline__ void side_bucket_wg(const SideArgs& G, uint32_t j, ui
       p[k] = px[i];
       q[k] = qty[i];
       k8[k] = kind[i];
-      // API precondition (the seq ring relies on it): seqs strictly ascending through the batch
-      if (i > 0) order_ok &= sq[k] > seq[i - 1];
+      // API precondition (the seq ring relies on it): seqs ascending through the batch (seq_follows)
+      if (i > 0) order_ok &= seq_follows(seq[i - 1], sq[k], k8[k]);
     }
   }
 #pragma unroll

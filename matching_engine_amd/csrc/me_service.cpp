@@ -23,7 +23,12 @@
 //   pq_mu     the matched-slice queue between the two stages
 //   live_mu   resting orders' owners and remainders (cancel ownership, OrderUpdate bookkeeping)
 //   upd_mu    the OrderUpdate queue
+//   ref_mu    per-book reference counts (which books an idle symbol may hand over)
 //   err_mu    the last error text
+//
+// The flusher keeps two slices in flight: slice k+1 is submitted to the backend (me_submit_host, or
+// the matcher's submit) before slice k is collected, so the backend's work on k+1 overlaps the
+// collect of k and its hand-off to the persister.
 //
 // SQLite is loaded at run time (dlopen libsqlite3.so.0) so the library has no build-time
 // dependency on a sqlite3 header.
@@ -65,6 +70,7 @@ struct Sql {
   int (*reset)(sqlite3_stmt*) = nullptr;
   int (*finalize)(sqlite3_stmt*) = nullptr;
   long long (*column_int64)(sqlite3_stmt*, int) = nullptr;
+  const unsigned char* (*column_text)(sqlite3_stmt*, int) = nullptr;
   const char* (*errmsg)(sqlite3*) = nullptr;
   int (*busy_timeout)(sqlite3*, int) = nullptr;
 
@@ -92,6 +98,7 @@ struct Sql {
     SYM(reset, "sqlite3_reset");
     SYM(finalize, "sqlite3_finalize");
     SYM(column_int64, "sqlite3_column_int64");
+    SYM(column_text, "sqlite3_column_text");
     SYM(errmsg, "sqlite3_errmsg");
     SYM(busy_timeout, "sqlite3_busy_timeout");
 #undef SYM
@@ -134,6 +141,10 @@ struct Pending {
   uint64_t target;
 };
 
+// The symbol id of a cancel whose symbol holds no book: out of the backend's range, so the record is
+// rejected (BAD_SYMBOL -> an OrderUpdate REJECTED) without taking a book for it.
+constexpr uint32_t kNoBook = 0xFFFFFFFFu;
+
 // One time slice: the SoA handed to the engine + the host-only fields persistence needs.
 struct Slice {
   std::vector<uint64_t> seq;
@@ -143,7 +154,25 @@ struct Slice {
   std::vector<uint8_t> kind;
   std::vector<Pending> meta;
   int64_t opened_us = 0;
+  bool recovery = false;  // resting orders replayed from the DB at create: their rows already exist
   size_t size() const { return seq.size(); }
+  // The first k records become their own slice; this one keeps the rest.
+  Slice take_prefix(size_t k) {
+    Slice p;
+    p.opened_us = opened_us;
+    p.recovery = recovery;
+    auto cut = [k](auto& src, auto& dst) {
+      dst.assign(std::make_move_iterator(src.begin()), std::make_move_iterator(src.begin() + k));
+      src.erase(src.begin(), src.begin() + k);
+    };
+    cut(seq, p.seq);
+    cut(px, p.px);
+    cut(qty, p.qty);
+    cut(sid, p.sid);
+    cut(kind, p.kind);
+    cut(meta, p.meta);
+    return p;
+  }
 };
 
 // A matched slice on its way to the DB (outputs copied out of the engine's buffers). One whose
@@ -161,6 +190,7 @@ struct Live {
   std::string client;
   std::string symbol;
   int32_t remaining;
+  uint32_t sid;  // its book (reference-counted: a book with live orders is never handed over)
 };
 
 constexpr size_t kMaxQueuedUpdates = size_t(1) << 24;  // oldest events are dropped beyond this
@@ -203,6 +233,13 @@ struct me_service {
   std::mutex upd_mu;
   std::deque<me_order_update> updates;
   uint64_t updates_dropped = 0;
+  // --- ref_mu: per book, live-table entries of its symbol + its records not yet emitted. A book at 0
+  // holds no resting order and has nothing on its way: a new symbol may take it over.
+  std::mutex ref_mu;
+  std::vector<int64_t> sref;
+  std::vector<uint32_t> idle;  // books whose count reached 0 (checked again when taken)
+  uint64_t reclaimed = 0;
+  uint64_t recovered = 0;
   // --- background flusher
   std::thread flusher;
   std::condition_variable cv;  // with mu
@@ -238,6 +275,7 @@ static void close_db(me_service* s) {
 }
 
 static void persister_main(me_service* s);
+static bool has_backend(const me_service* s);
 
 static bool sql_ok(int rc) { return rc == SQLITE_OK || rc == SQLITE_DONE || rc == SQLITE_ROW; }
 
@@ -299,6 +337,113 @@ static bool open_db(me_service* s, const char* path, std::string& err) {
          chk(g_sql.prepare_v2(s->db, fill_k.c_str(), -1, &s->st_fill_k, nullptr), "prepare fill rows");
 }
 
+// ---- per-book reference counts ----------------------------------------------------------------
+static void ref_add(me_service* s, uint32_t sid, int64_t d) {
+  if (sid == kNoBook || d == 0) return;
+  std::lock_guard<std::mutex> lr(s->ref_mu);
+  if (sid >= s->sref.size()) return;
+  int64_t& r = s->sref[sid];
+  r += d;
+  if (r == 0) s->idle.push_back(sid);
+}
+
+// Symbol string -> local book id (mu held). The reference accepts any non-empty symbol
+// (matching_engine_service.cpp:66-71) and keeps it forever; the backend holds sym_cap books. A new
+// symbol takes the next unused book, else a book whose symbol has no live order and no record on its
+// way (its count is 0 under ref_mu, and only this thread, holding mu, could raise it): the old symbol's
+// book is empty, so handing it over changes no order's outcome; the window re-centres on the new
+// symbol's first rest. False only when every book is in use.
+static bool intern(me_service* s, const std::string& symbol, uint32_t& sid) {
+  auto it = s->sym.find(symbol);
+  if (it != s->sym.end()) {
+    sid = it->second;
+    return true;
+  }
+  std::lock_guard<std::mutex> lr(s->ref_mu);
+  if (s->names.size() < s->sym_cap) {
+    sid = (uint32_t)s->names.size();
+    s->names.push_back(symbol);
+    s->sym.emplace(symbol, sid);
+    s->sref.push_back(0);
+    return true;
+  }
+  while (!s->idle.empty()) {
+    const uint32_t c = s->idle.back();
+    s->idle.pop_back();
+    if (c >= s->sref.size() || s->sref[c] != 0) continue;  // busy again since it went idle
+    s->sym.erase(s->names[c]);
+    s->names[c] = symbol;
+    s->sym.emplace(symbol, c);
+    s->reclaimed++;
+    sid = c;
+    return true;
+  }
+  return false;
+}
+
+static int flush_closed(me_service* s, bool take_open, size_t limit, struct FlushOut* out, bool wait);
+
+// Restart recovery: the orders the DB shows resting (status NEW / PARTIALLY_FILLED, remaining > 0) as
+// LIMIT records in OID order, with their remainders — replayed into the backend before any new
+// order, so each keeps its place in its level's FIFO. Chunks of at most slice_max records spanning
+// fewer than 2^20 OIDs (one launch group must span fewer seqs than the engine's seq ring).
+static bool load_resting(me_service* s, std::string& err) {
+  sqlite3_stmt* q = nullptr;
+  if (!sql_ok(g_sql.prepare_v2(s->db,
+                               "SELECT order_id, client_id, symbol, side, price, remaining_quantity FROM orders "
+                               "WHERE status IN (0, 1) AND remaining_quantity > 0 AND order_id LIKE 'OID-%' "
+                               "ORDER BY CAST(SUBSTR(order_id, 5) AS INTEGER)",
+                               -1, &q, nullptr))) {
+    err = s->sql_err("prepare recovery");
+    return false;
+  }
+  const size_t cap = s->slice_max ? s->slice_max : 65536;
+  bool ok = true;
+  std::lock_guard<std::mutex> lk(s->mu);
+  Slice cur;
+  cur.recovery = true;
+  auto close_chunk = [&] {
+    if (!cur.size()) return;
+    s->closed_records += cur.size();
+    s->closed.push_back(std::move(cur));
+    cur = Slice{};
+    cur.recovery = true;
+  };
+  for (int rc; (rc = g_sql.step(q)) == SQLITE_ROW;) {
+    const char* oid_s = (const char*)g_sql.column_text(q, 0);
+    const char* cl = (const char*)g_sql.column_text(q, 1);
+    const char* sy = (const char*)g_sql.column_text(q, 2);
+    const uint64_t oid = oid_s ? strtoull(oid_s + 4, nullptr, 10) : 0;
+    const int32_t side = (int32_t)g_sql.column_int64(q, 3);
+    const int64_t px = g_sql.column_int64(q, 4);
+    const long long rem = g_sql.column_int64(q, 5);
+    if (!oid || (side != ME_SIDE_BUY && side != ME_SIDE_SELL) || rem <= 0 || rem > INT32_MAX) continue;
+    const std::string symbol = sy ? sy : "";
+    uint32_t sid = 0;
+    if (!intern(s, symbol, sid)) {
+      err = "restart recovery: the DB holds resting orders on more symbols than the backend has books";
+      ok = false;
+      break;
+    }
+    if (cur.size() >= cap || (cur.size() && oid - cur.seq.front() >= (1ull << 20))) close_chunk();
+    cur.seq.push_back(oid);
+    cur.px.push_back(px);
+    cur.qty.push_back((int32_t)rem);
+    cur.sid.push_back(sid);
+    cur.kind.push_back(ME_KIND(side, ME_TYPE_LIMIT, ME_OP_NEW));
+    cur.meta.push_back(Pending{cl ? cl : "", symbol, side, false, 0});
+    {
+      std::lock_guard<std::mutex> lv(s->live_mu);
+      s->live[oid] = Live{cl ? cl : "", symbol, (int32_t)rem, sid};
+    }
+    ref_add(s, sid, 1);
+    s->recovered++;
+  }
+  g_sql.finalize(q);
+  close_chunk();
+  return ok;
+}
+
 static me_service* create(me_engine* engine, const me_matcher* m, const char* const* symbols, uint32_t num_symbols,
                           const char* db_path) {
   me_service* s = new me_service();
@@ -309,7 +454,7 @@ static me_service* create(me_engine* engine, const me_matcher* m, const char* co
       s->sym_cap = c.num_symbols;
       s->slice_max = c.max_batch;
     }
-    me_host_reserve(engine, 1);  // the flusher reuses one warm pinned slot
+    me_host_reserve(engine, 2);  // the flusher keeps two slices in flight in two warm pinned slots
   } else if (m) {
     s->m = *m;
     s->sym_cap = m->num_symbols;
@@ -318,7 +463,9 @@ static me_service* create(me_engine* engine, const me_matcher* m, const char* co
   for (uint32_t i = 0; i < num_symbols; ++i) {
     s->names.emplace_back(symbols[i]);
     s->sym.emplace(s->names.back(), i);
+    s->sref.push_back(0);
   }
+  for (uint32_t i = num_symbols; i-- > 0;) s->idle.push_back(i);  // nothing rests on them yet
   if (s->names.size() > s->sym_cap) s->fail(ME_E_INVALID, "me_service_create: more symbols than the engine holds");
   std::string err;
   if (db_path && !open_db(s, db_path, err)) {
@@ -327,6 +474,24 @@ static me_service* create(me_engine* engine, const me_matcher* m, const char* co
     s->fail(ME_E_SQLITE, "me_service_create: " + err);
   }
   s->persister = std::thread(persister_main, s);
+  if (s->db && has_backend(s)) {  // rebuild the books from the DB before the first SubmitOrder
+    if (!load_resting(s, err)) {
+      s->failed = true;
+      s->fail(ME_E_CAPACITY, "me_service_create: " + err);
+    } else {
+      std::lock_guard<std::mutex> lf(s->flush_mu);
+      const int rc = flush_closed(s, false, SIZE_MAX, nullptr, true);
+      if (rc != ME_OK) {
+        s->failed = true;
+        std::string e;
+        {
+          std::lock_guard<std::mutex> le(s->err_mu);
+          e = s->err;
+        }
+        s->fail(rc, "me_service_create: restart recovery failed: " + e);
+      }
+    }
+  }
   return s;
 }
 
@@ -351,21 +516,62 @@ static std::string backend_err(me_service* s) {
   return e;
 }
 
-// Match one slice (eng_mu held). accepted = the backend took it (a failure after that loses it).
-static int backend_match(me_service* s, const me_order_soa& b, size_t n, const me_fill** tape, size_t* nf,
-                         const me_order_result** res, bool& accepted) {
+// A slice handed to the backend and not collected yet.
+struct Inflight {
+  Slice sl;
+  uint64_t ticket = 0;
+  bool done = false;  // outputs already here (a matcher without submit / collect matches at once)
+  std::vector<me_order_result> res;
+  std::vector<me_fill> tape;
+};
+
+// Backends that take a slice now and hand its outputs back later: the engine (host slots and
+// tickets) and matchers with submit / collect. The flusher keeps two slices in flight with them.
+static bool backend_async(const me_service* s) { return s->eng || (s->m.submit && s->m.collect); }
+
+// Hand one slice to the backend (eng_mu held). accepted = the backend took it (a later failure loses
+// it); ME_E_CAPACITY with accepted false: refused, nothing of it was applied.
+static int backend_submit(me_service* s, Inflight& f, bool& accepted) {
+  Slice& sl = f.sl;
+  const size_t n = sl.size();
+  me_order_soa b{sl.seq.data(), sl.px.data(), sl.qty.data(), sl.sid.data(), sl.kind.data()};
+  accepted = false;
   if (s->eng) {
-    uint64_t t = 0;
-    accepted = false;
-    int rc = me_submit_host(s->eng, &b, n, &t);
-    if (rc != ME_OK) return rc;
-    accepted = true;
-    size_t nr = 0;
-    return me_collect(s->eng, t, tape, nf, res, &nr);
+    const int rc = me_submit_host(s->eng, &b, n, &f.ticket);
+    accepted = rc == ME_OK;
+    return rc;
   }
-  const int rc = s->m.match(s->m.ctx, &b, n, tape, nf, res);
-  accepted = rc != ME_E_CAPACITY;  // the matcher's refusal: nothing of the slice was applied
-  return rc;
+  if (s->m.submit && s->m.collect) {
+    const int rc = s->m.submit(s->m.ctx, &b, n, &f.ticket);
+    accepted = rc != ME_E_CAPACITY;
+    return rc;
+  }
+  const me_fill* tape = nullptr;
+  const me_order_result* res = nullptr;
+  size_t nf = 0;
+  const int rc = s->m.match(s->m.ctx, &b, n, &tape, &nf, &res);
+  accepted = rc != ME_E_CAPACITY;
+  if (rc != ME_OK) return rc;
+  // the matcher's output views stay valid until its next call: copy them out under eng_mu
+  f.res.assign(res, res + n);
+  f.tape.assign(tape, tape + nf);
+  f.done = true;
+  return ME_OK;
+}
+
+// The outputs of an accepted slice (eng_mu held), copied out of the backend's buffers.
+static int backend_collect(me_service* s, Inflight& f) {
+  if (f.done) return ME_OK;
+  const me_fill* tape = nullptr;
+  const me_order_result* res = nullptr;
+  size_t nf = 0, nr = 0;
+  const int rc = s->eng ? me_collect(s->eng, f.ticket, &tape, &nf, &res, &nr)
+                        : s->m.collect(s->m.ctx, f.ticket, &tape, &nf, &res);
+  if (rc != ME_OK) return rc;
+  f.res.assign(res, res + f.sl.size());
+  f.tape.assign(tape, tape + nf);
+  f.done = true;
+  return ME_OK;
 }
 
 static int backend_book(me_service* s, uint32_t sid, uint32_t depth, me_book_entry* bids, size_t bids_cap,
@@ -408,22 +614,6 @@ static void append(me_service* s, uint64_t seq, int64_t px, int32_t qty, uint32_
   o.kind.push_back(kind);
   o.meta.push_back(std::move(m));
   if (s->slice_max && o.size() >= s->slice_max) close_open(s);
-}
-
-// Symbol string -> local id, interning a new one while the engine has room (mu held). The reference
-// accepts any non-empty symbol (matching_engine_service.cpp:66-71): a new symbol's book is the
-// engine's next unused local book, its window placed by its first orders.
-static bool intern(me_service* s, const std::string& symbol, uint32_t& sid) {
-  auto it = s->sym.find(symbol);
-  if (it != s->sym.end()) {
-    sid = it->second;
-    return true;
-  }
-  if (s->names.size() >= s->sym_cap) return false;
-  sid = (uint32_t)s->names.size();
-  s->names.push_back(symbol);
-  s->sym.emplace(symbol, sid);
-  return true;
 }
 
 extern "C" int me_service_submit_order(me_service* s, const me_order_request* r, me_order_response* resp) {
@@ -473,8 +663,9 @@ extern "C" int me_service_submit_order(me_service* s, const me_order_request* r,
   const bool limit = r->order_type == ME_TYPE_LIMIT;
   if (limit) {  // its owner, for CancelOrder and the OrderUpdate stream
     std::lock_guard<std::mutex> lv(s->live_mu);
-    s->live[id] = Live{client, sym, r->quantity};
+    s->live[id] = Live{client, sym, r->quantity, sid};
   }
+  ref_add(s, sid, 1);  // a LIMIT's live entry, or a MARKET record on its way
   append(s, id, q4, r->quantity, sid, ME_KIND(r->side, limit ? ME_TYPE_LIMIT : ME_TYPE_MARKET, ME_OP_NEW),
          Pending{std::move(client), sym, r->side, false, 0});
   return 0;
@@ -520,15 +711,16 @@ extern "C" int me_service_cancel_order(me_service* s, const me_cancel_request* r
       return 0;
     }
   }
-  uint32_t sid = 0;
-  if (!intern(s, sym, sid)) {
-    resp->grpc_status = 8;
-    put(resp->error_message, sizeof resp->error_message, "symbol capacity exhausted");
-    return 0;
-  }
-  const uint64_t id = s->next_id++;  // the cancel's stream position (batch order == seq order)
+  // A symbol with no book has no resting order: the record goes out with an id the backend rejects
+  // (BAD_SYMBOL -> OrderUpdate REJECTED) and takes no book.
+  auto it = s->sym.find(sym);
+  const uint32_t sid = it != s->sym.end() ? it->second : kNoBook;
+  // Stream position: the last OID allocated, consuming none (a cancel record may repeat the previous
+  // record's seq, me_engine.h), so accepted orders keep the reference's gap-free OIDs (:29-32, :85).
+  const uint64_t id = s->next_id - 1;
   put(resp->order_id, sizeof resp->order_id, "OID-" + std::to_string(target));
   resp->success = 1;
+  ref_add(s, sid, 1);
   append(s, id, (int64_t)target, 0, sid, ME_KIND(ME_SIDE_BUY, ME_TYPE_LIMIT, ME_OP_CANCEL),
          Pending{client, sym, 0, true, target});
   return 0;
@@ -564,9 +756,10 @@ static void push_update(me_service* s, uint64_t oid, const std::string& client, 
   u.fill_price = price;
   u.fill_quantity = fq;
   u.remaining_quantity = remaining;
-  if (s->updates.size() >= kMaxQueuedUpdates) {
+  if (s->updates.size() >= kMaxQueuedUpdates) {  // nobody drains the stream: drop the oldest, loudly
     s->updates.pop_front();
-    s->updates_dropped++;
+    if (s->updates_dropped++ == 0)
+      s->fail(ME_OK, "OrderUpdate queue full (2^24 undrained events): dropping the oldest; drain with me_service_updates");
   }
   s->updates.push_back(u);
 }
@@ -574,11 +767,19 @@ static void push_update(me_service* s, uint64_t oid, const std::string& client, 
 // OrderUpdate events of one matched slice (order documented in me_service.h), and the live-order
 // table they are computed from. Locks are taken per block of records so SubmitOrder / CancelOrder
 // (which touch the live table) never wait for a whole slice.
+// Book reference counts move here too: every record's own count is released once its events are
+// out, and a live entry's when it stops resting (filled, cancelled, or never rested).
+// A recovery slice (orders replayed from the DB at create) emits only what is new: fills and
+// outcomes other than "still resting" (its NEW events went out in the earlier run).
 static void emit_updates(me_service* s, const Slice& sl, const me_order_result* res, const me_fill* tape) {
   constexpr size_t kBlock = 512;
   for (size_t i0 = 0; i0 < sl.size(); i0 += kBlock) {
     std::lock_guard<std::mutex> lv(s->live_mu);
     std::lock_guard<std::mutex> lu(s->upd_mu);
+    auto live_erase = [&](std::unordered_map<uint64_t, Live>::iterator it) {
+      ref_add(s, it->second.sid, -1);
+      s->live.erase(it);
+    };
     for (size_t i = i0; i < sl.size() && i < i0 + kBlock; ++i) {
       const Pending& m = sl.meta[i];
       const me_order_result& r = res[i];
@@ -586,11 +787,12 @@ static void emit_updates(me_service* s, const Slice& sl, const me_order_result* 
         auto it = s->live.find(m.target);
         if (r.status == ME_ST_CANCELED && it != s->live.end()) {
           push_update(s, m.target, it->second.client, it->second.symbol, ME_ST_CANCELED, 0, 0, r.remaining_qty);
-          s->live.erase(it);
+          live_erase(it);
         } else {
           push_update(s, m.target, m.client, m.symbol, r.status == ME_ST_CANCELED ? ME_ST_CANCELED : ME_ST_REJECTED,
                       0, 0, r.remaining_qty);
         }
+        ref_add(s, sl.sid[i], -1);  // the cancel record itself
         continue;
       }
       const uint64_t oid = sl.seq[i];
@@ -603,22 +805,32 @@ static void emit_updates(me_service* s, const Slice& sl, const me_order_result* 
           mk.remaining -= fl.qty;
           push_update(s, fl.maker_seq, mk.client, mk.symbol,
                       mk.remaining > 0 ? ME_ST_PARTIALLY_FILLED : ME_ST_FILLED, fl.price_q4, fl.qty, mk.remaining);
-          if (mk.remaining <= 0) s->live.erase(it);
+          if (mk.remaining <= 0) live_erase(it);
         }
         rem -= fl.qty;
         push_update(s, oid, m.client, m.symbol, rem > 0 ? ME_ST_PARTIALLY_FILLED : ME_ST_FILLED, fl.price_q4,
                     fl.qty, rem);
       }
       const bool market = ((sl.kind[i] >> 2) & 1u) != 0;
-      if (r.status == ME_ST_REJECTED || r.status == ME_ST_CANCELED || (r.fill_count == 0 && r.status == ME_ST_NEW))
+      if (r.status == ME_ST_REJECTED || r.status == ME_ST_CANCELED ||
+          (r.fill_count == 0 && r.status == ME_ST_NEW && !sl.recovery))
         push_update(s, oid, m.client, m.symbol, r.status, 0, 0, r.remaining_qty);
-      if (market) continue;
+      if (market) {
+        ref_add(s, sl.sid[i], -1);  // the MARKET record (it never rests)
+        continue;
+      }
+      // a LIMIT's count is its live entry, created at submit: it stays while the order rests
       if (r.remaining_qty > 0 && (r.status == ME_ST_NEW || r.status == ME_ST_PARTIALLY_FILLED)) {
         auto it = s->live.find(oid);
-        if (it != s->live.end()) it->second.remaining = r.remaining_qty;
-        else s->live[oid] = Live{m.client, m.symbol, r.remaining_qty};
+        if (it != s->live.end()) {
+          it->second.remaining = r.remaining_qty;
+        } else {
+          s->live[oid] = Live{m.client, m.symbol, r.remaining_qty, sl.sid[i]};
+          ref_add(s, sl.sid[i], 1);
+        }
       } else {
-        s->live.erase(oid);
+        auto it = s->live.find(oid);
+        if (it != s->live.end()) live_erase(it);
       }
     }
   }
@@ -662,6 +874,11 @@ static bool persist(me_service* s, const Slice& sl, const me_order_result* res, 
                     std::string& err) {
   if (!s->db) return true;
   const size_t n = sl.size();
+  if (sl.recovery) {  // replayed resting orders: their rows exist; a consistent DB produces no change
+    bool change = false;
+    for (size_t i = 0; i < n && !change; ++i) change = res[i].fill_count || res[i].status != ME_ST_NEW;
+    if (!change) return true;
+  }
   // ---- final state of this slice's rows; changes to earlier slices' rows
   std::vector<int32_t> fst(n), frem(n);
   std::unordered_map<uint64_t, long long> ext_fill;       // earlier order -> quantity filled now
@@ -717,8 +934,17 @@ static bool persist(me_service* s, const Slice& sl, const me_order_result* res, 
     err = s->sql_err("begin");
     return false;
   }
-  // ---- orders rows, kRows per statement
-  {
+  // ---- orders rows, kRows per statement (a recovery slice's rows exist: they take UPDATEs)
+  if (sl.recovery) {
+    for (size_t i = 0; ok && i < n; ++i) {
+      if (fst[i] == ME_ST_NEW && frem[i] == sl.qty[i]) continue;
+      g_sql.bind_int64(s->st_upd, 1, fst[i]);
+      g_sql.bind_int64(s->st_upd, 2, frem[i]);
+      g_sql.bind_int64(s->st_upd, 3, ts);
+      g_sql.bind_text(s->st_upd, 4, oid[i].c_str(), -1, SQLITE_TRANSIENT);
+      step(s->st_upd, "update recovered order");
+    }
+  } else {
     std::vector<size_t> rows;
     rows.reserve(n);
     for (size_t i = 0; i < n; ++i)
@@ -849,65 +1075,44 @@ static void persister_main(me_service* s) {
   }
 }
 
-// Where a flush's caller wants the matched outputs (any pointer may be NULL).
+// Where a flush's caller wants the matched outputs (any pointer may be NULL). The capacities are
+// checked against the pending records before anything is matched; a slice whose outputs still would
+// not fit (a matcher exceeding its own fill bound) is not copied: `short_buf`, ME_E_INVALID at the end.
 struct FlushOut {
   me_fill* fills = nullptr;
   size_t fills_cap = 0;
   size_t nf = 0;
   me_order_result* res = nullptr;
   uint64_t* seq = nullptr;
+  size_t res_cap = 0;
   size_t nr = 0;
+  bool short_buf = false;
 };
 
-// Match one closed slice and hand it to the persister (flush_mu held; the slice already taken off
-// the queue and counted in inflight_records).
-static int process(me_service* s, Slice&& sl, FlushOut* out) {
-  const size_t n = sl.size();
-  {  // bounded run-ahead: at most kMaxMatchedAhead slices wait for the DB (unless it is stalled)
-    std::unique_lock<std::mutex> lq(s->pq_mu);
-    s->pq_cv.wait(lq, [&] { return s->pq_stalled || s->pq.size() < kMaxMatchedAhead; });
+// A matched slice: its outputs to the caller, the slice to the persister (stream order).
+static void deliver(me_service* s, Slice&& sl, std::vector<me_order_result>&& res, std::vector<me_fill>&& tape,
+                    FlushOut* out) {
+  const size_t n = sl.size(), nf = tape.size();
+  if (out && !out->short_buf) {
+    if ((out->fills && out->nf + nf > out->fills_cap) || ((out->res || out->seq) && out->nr + n > out->res_cap)) {
+      out->short_buf = true;
+    } else {
+      if (out->fills) memcpy(out->fills + out->nf, tape.data(), nf * sizeof(me_fill));
+      if (out->res)
+        for (size_t i = 0; i < n; ++i) {
+          out->res[out->nr + i] = res[i];
+          out->res[out->nr + i].tape_offset += (uint32_t)out->nf;
+        }
+      if (out->seq) memcpy(out->seq + out->nr, sl.seq.data(), n * sizeof(uint64_t));
+      out->nf += nf;
+      out->nr += n;
+    }
   }
   Matched mt;
-  {
-    std::lock_guard<std::mutex> le(s->eng_mu);
-    me_order_soa b{sl.seq.data(), sl.px.data(), sl.qty.data(), sl.sid.data(), sl.kind.data()};
-    const me_fill* tape = nullptr;
-    const me_order_result* res = nullptr;
-    size_t nf = 0;
-    bool accepted = false;
-    const int rc = backend_match(s, b, n, &tape, &nf, &res, accepted);
-    if (rc != ME_OK && !accepted) {  // not accepted: the slice goes back to the head of the queue
-      const std::string e = s->eng ? backend_err(s) : "the matcher refused the slice (a shard's max_resting); no book changed";
-      std::lock_guard<std::mutex> lk(s->mu);
-      s->inflight_records -= n;
-      s->closed_records += n;
-      s->closed.push_front(std::move(sl));
-      return s->fail(rc, "engine: " + e);
-    }
-    if (rc != ME_OK) {  // accepted and lost: the books may hold the slice, the service cannot go on
-      s->failed = true;
-      std::lock_guard<std::mutex> lk(s->mu);
-      s->inflight_records -= n;
-      return s->fail(rc, "engine lost an accepted slice: " + backend_err(s));
-    }
-    // the engine's output views stay valid until its next call: copy them out under eng_mu
-    mt.res.assign(res, res + n);
-    mt.tape.assign(tape, tape + nf);
-  }
   mt.ts = now_ms();
-  const size_t nf = mt.tape.size();
-  if (out) {
-    if (out->fills) memcpy(out->fills + out->nf, mt.tape.data(), nf * sizeof(me_fill));
-    if (out->res)
-      for (size_t i = 0; i < n; ++i) {
-        out->res[out->nr + i] = mt.res[i];
-        out->res[out->nr + i].tape_offset += (uint32_t)out->nf;
-      }
-    if (out->seq) memcpy(out->seq + out->nr, sl.seq.data(), n * sizeof(uint64_t));
-    out->nf += nf;
-    out->nr += n;
-  }
   mt.sl = std::move(sl);
+  mt.res = std::move(res);
+  mt.tape = std::move(tape);
   {
     std::lock_guard<std::mutex> lq(s->pq_mu);
     s->pq.push_back(std::move(mt));
@@ -916,14 +1121,52 @@ static int process(me_service* s, Slice&& sl, FlushOut* out) {
   }
   std::lock_guard<std::mutex> lk(s->mu);  // after the push: pending + unpersisted never dips to 0 early
   s->inflight_records -= n;
+}
+
+// The backend refused a slice (its books near max_resting; nothing of it applied). Rather than
+// retrying the same slice forever — nothing could free capacity, since every later record (cancels
+// included) is queued behind it — it is split and its halves go back to the head of the queue; a
+// single LIMIT that still does not fit is answered in-band (REJECTED, ME_RJ_CAPACITY). `taken` counts
+// the records of this flush's budget handed out so far.
+static int on_refused(me_service* s, Slice&& sl, FlushOut* out, size_t& taken) {
+  const size_t n = sl.size();
+  if (sl.recovery) {  // the DB's resting orders do not fit the books: nothing sensible to do
+    s->failed = true;
+    {
+      std::lock_guard<std::mutex> lk(s->mu);
+      s->inflight_records -= n;
+    }
+    return s->fail(ME_E_CAPACITY, "the backend's max_resting is below the resting orders the DB holds: " +
+                                      backend_err(s));
+  }
+  if (n == 1 && (sl.kind[0] & 0x0Cu) == 0u) {  // one LIMIT and no room to rest it
+    me_order_result r{};
+    r.remaining_qty = sl.qty[0];
+    r.status = ME_ST_REJECTED;
+    r.reason = ME_RJ_CAPACITY;
+    deliver(s, std::move(sl), std::vector<me_order_result>{r}, std::vector<me_fill>{}, out);
+    return ME_OK;
+  }
+  std::lock_guard<std::mutex> lk(s->mu);
+  s->inflight_records -= n;
+  s->closed_records += n;
+  taken -= n;
+  if (n == 1) {  // a record that cannot rest, refused by a matcher: kept queued for the next flush
+    s->closed.push_front(std::move(sl));
+    return s->fail(ME_E_CAPACITY, "the matcher refused a record that cannot rest; it stays queued");
+  }
+  Slice head = sl.take_prefix(n / 2);
+  s->closed.push_front(std::move(sl));
+  s->closed.push_front(std::move(head));
   return ME_OK;
 }
 
-// Flush the closed slices (and the open one when take_open), oldest first. `limit` bounds how many
-// slices are taken (those present when the caller checked its output capacity). With `wait`, returns
-// once the persister has emitted every matched slice and committed them (or stalled on a failed
-// transaction: ME_E_SQLITE, the slices kept in order for the next flush).
-static int flush_closed(me_service* s, bool take_open, size_t limit, FlushOut* out, bool wait) {
+// Flush the closed slices (and the open one when take_open), oldest first, two in flight: slice k+1 is
+// submitted before slice k is collected. `rec_limit` bounds the records taken (those present when the
+// caller checked its output capacity). With `wait`, returns once the persister has emitted every
+// matched slice and committed them (or stalled on a failed transaction: ME_E_SQLITE, the slices kept
+// in order for the next flush).
+static int flush_closed(me_service* s, bool take_open, size_t rec_limit, FlushOut* out, bool wait) {
   if (s->failed) return s->fail(ME_E_STATE, "service failed: the engine lost an accepted slice");
   if (!has_backend(s)) {
     std::lock_guard<std::mutex> lk(s->mu);
@@ -941,19 +1184,70 @@ static int flush_closed(me_service* s, bool take_open, size_t limit, FlushOut* o
     std::lock_guard<std::mutex> lk(s->mu);
     close_open(s);
   }
-  for (size_t k = 0; k < limit; ++k) {
-    Slice sl;
+  std::deque<Inflight> fl;  // submitted, not collected (at most two)
+  auto lost = [&](int r, const std::string& what) {
+    s->failed = true;
+    size_t n = 0;
+    for (auto& f : fl) n += f.sl.size();
+    std::lock_guard<std::mutex> lk(s->mu);
+    s->inflight_records -= n;
+    return s->fail(r, what + backend_err(s));
+  };
+  auto finish_oldest = [&]() -> int {
+    int r;
+    {
+      std::lock_guard<std::mutex> le(s->eng_mu);
+      r = backend_collect(s, fl.front());
+    }
+    if (r != ME_OK) return lost(r, "engine lost an accepted slice: ");
+    Inflight& f = fl.front();
+    deliver(s, std::move(f.sl), std::move(f.res), std::move(f.tape), out);
+    fl.pop_front();
+    return ME_OK;
+  };
+  size_t taken = 0;
+  while (taken < rec_limit) {
+    Inflight f;
     {
       std::lock_guard<std::mutex> lk(s->mu);
       if (s->closed.empty()) break;
-      sl = std::move(s->closed.front());
+      f.sl = std::move(s->closed.front());
       s->closed.pop_front();
-      s->closed_records -= sl.size();
-      s->inflight_records += sl.size();
+      s->closed_records -= f.sl.size();
+      s->inflight_records += f.sl.size();
     }
-    const int r = process(s, std::move(sl), out);
+    taken += f.sl.size();
+    {  // bounded run-ahead: at most kMaxMatchedAhead slices wait for the DB (unless it is stalled)
+      std::unique_lock<std::mutex> lq(s->pq_mu);
+      s->pq_cv.wait(lq, [&] { return s->pq_stalled || s->pq.size() < kMaxMatchedAhead; });
+    }
+    bool accepted = false;
+    int r;
+    {
+      std::lock_guard<std::mutex> le(s->eng_mu);
+      r = backend_submit(s, f, accepted);
+    }
+    if (r != ME_OK && !accepted) {  // refused: the slices before it go first, then it is split
+      while (!fl.empty())
+        if ((r = finish_oldest()) != ME_OK) return r;
+      if ((r = on_refused(s, std::move(f.sl), out, taken)) != ME_OK) return r;
+      continue;
+    }
+    if (r != ME_OK) {  // accepted and lost: the books may hold the slice, the service cannot go on
+      fl.push_back(std::move(f));
+      return lost(r, "engine lost an accepted slice: ");
+    }
+    fl.push_back(std::move(f));
+    if (fl.size() > 1 || !backend_async(s))
+      if ((r = finish_oldest()) != ME_OK) return r;
+  }
+  while (!fl.empty()) {
+    const int r = finish_oldest();
     if (r != ME_OK) return r;
   }
+  if (out && out->short_buf)
+    return s->fail(ME_E_INVALID, "output buffers too small for the matched slices (they were matched and persisted; "
+                                 "outputs truncated to the slices that fit)");
   if (!wait) return ME_OK;
   std::unique_lock<std::mutex> lq(s->pq_mu);
   s->pq_cv.wait(lq, [&] { return s->pq_emitted == s->pq.size() && (s->pq.empty() || s->pq_stalled); });
@@ -969,11 +1263,10 @@ extern "C" int me_service_flush(me_service* s, me_fill* out_fills, size_t fills_
   if (n_fills) *n_fills = 0;
   if (n_results) *n_results = 0;
   std::lock_guard<std::mutex> lf(s->flush_mu);
-  size_t total = 0, nslices = 0;
+  size_t total = 0;
   {
     std::lock_guard<std::mutex> lk(s->mu);
     total = s->open.size() + s->closed_records;  // inflight is 0 here (flush_mu held)
-    nslices = s->closed.size() + (s->open.size() ? 1 : 0);
   }
   // the caller's buffers are checked before anything is matched
   if ((out_results || out_seq) && total > results_cap)
@@ -981,8 +1274,13 @@ extern "C" int me_service_flush(me_service* s, me_fill* out_fills, size_t fills_
   const uint64_t bound = s->eng ? me_fill_bound(s->eng, total) : s->m.max_resting + 2 * (uint64_t)total;
   if (out_fills && has_backend(s) && fills_cap < bound)
     return s->fail(ME_E_INVALID, "fills_cap smaller than me_fill_bound(pending records)");
-  FlushOut out{out_fills, fills_cap, 0, out_results, out_seq, 0};
-  const int rc = flush_closed(s, true, nslices, &out, true);
+  FlushOut out;
+  out.fills = out_fills;
+  out.fills_cap = fills_cap;
+  out.res = out_results;
+  out.seq = out_seq;
+  out.res_cap = results_cap;
+  const int rc = flush_closed(s, true, total, &out, true);
   if (n_fills) *n_fills = out.nf;
   if (n_results) *n_results = out.nr;
   return rc;
@@ -992,22 +1290,33 @@ extern "C" int me_service_flush(me_service* s, me_fill* out_fills, size_t fills_
 // it at the slice size) and flushes the closed ones.
 static void flusher_main(me_service* s) {
   std::unique_lock<std::mutex> lk(s->mu);
+  // after a failed flush (e.g. a matcher kept refusing a record): retry after 1 ms, doubling to 100 ms
+  int64_t backoff_us = 0, retry_at = 0;
   while (!s->stop) {
     const int64_t now = mono_us();
     const bool due = s->open.size() && now - s->open.opened_us >= s->interval_us;
     if (due) close_open(s);
-    if (s->closed.empty()) {
-      const int64_t wait = s->open.size() ? s->open.opened_us + s->interval_us - now : s->interval_us;
+    const bool blocked = backoff_us && now < retry_at;
+    if (s->closed.empty() || blocked) {
+      int64_t wait = s->open.size() ? s->open.opened_us + s->interval_us - now : s->interval_us;
+      if (blocked) wait = std::min(wait, retry_at - now);
       s->cv.wait_for(lk, std::chrono::microseconds(wait > 0 ? wait : 1));
       continue;
     }
     lk.unlock();
+    int rc;
     {
       std::lock_guard<std::mutex> lf(s->flush_mu);
-      (void)flush_closed(s, false, SIZE_MAX, nullptr, false);  // errors land in me_service_last_error
+      rc = flush_closed(s, false, SIZE_MAX, nullptr, false);  // errors land in me_service_last_error
     }
     lk.lock();
     if (s->failed) break;
+    if (rc == ME_OK) {
+      backoff_us = 0;
+    } else {
+      backoff_us = std::min<int64_t>(std::max<int64_t>(2 * backoff_us, 1000), 100000);
+      retry_at = mono_us() + backoff_us;
+    }
   }
 }
 
@@ -1060,6 +1369,7 @@ extern "C" int me_service_book(me_service* s, const char* symbol, me_level* bids
                                size_t* n_bids, size_t* n_asks) {
   if (n_bids) *n_bids = 0;
   if (n_asks) *n_asks = 0;
+  if (depth == 0) return ME_OK;  // no levels asked for (the backend would read 0 as "the whole book")
   uint32_t sid = 0;
   {
     std::lock_guard<std::mutex> lk(s->mu);
@@ -1140,6 +1450,24 @@ extern "C" int me_service_market_data(me_service* s, const char* symbol, me_mark
     out->best_ask = a.price_q4;
     out->ask_size = sat(a.total_qty);
   }
+  return ME_OK;
+}
+
+extern "C" uint64_t me_service_updates_dropped(const me_service* s) {
+  me_service* m = const_cast<me_service*>(s);
+  std::lock_guard<std::mutex> lk(m->upd_mu);
+  return m->updates_dropped;
+}
+
+extern "C" int me_service_stats(const me_service* s, uint64_t* reclaimed_books, uint64_t* recovered_orders) {
+  if (!s) return ME_E_INVALID;
+  me_service* m = const_cast<me_service*>(s);
+  std::lock_guard<std::mutex> lk(m->mu);
+  {
+    std::lock_guard<std::mutex> lr(m->ref_mu);
+    if (reclaimed_books) *reclaimed_books = m->reclaimed;
+  }
+  if (recovered_orders) *recovered_orders = m->recovered;
   return ME_OK;
 }
 

@@ -19,8 +19,9 @@ class MatchingEngineService:
     """SubmitOrder / GetOrderBook over one engine shard; SQLite persistence when db_path is given."""
 
     def __init__(self, engine, symbols, db_path=None, matcher=None):
-        """engine: the Engine the slices match on; or matcher: a cluster.ShardedMatcher (rank 0 of a
-        sharded deployment, me_service_create_matcher)."""
+        """engine: the Engine the slices match on; or matcher: an object with c_matcher() -> MeMatcher —
+        a cluster.Cluster (rank 0 of a sharded deployment, me_cluster_matcher) or a Python book behind
+        cluster.python_matcher (tests) — for me_service_create_matcher."""
         self.lib = _abi.load()
         self.engine = engine
         self.matcher = matcher
@@ -125,7 +126,7 @@ class MatchingEngineService:
         if self.engine is not None:
             cap = self.engine.fill_bound(n) + 1
         else:
-            cap = (self.matcher.max_resting + 2 * n + 1) if self.matcher is not None else 1
+            cap = (self._cm.max_resting + 2 * n + 1) if self.matcher is not None else 1
         fills = np.zeros(cap, dtype=FILL_DTYPE)
         nf, nr = C.c_size_t(0), C.c_size_t(0)
         rc = self.lib.me_service_flush(self.h, ptr(fills), cap, C.byref(nf), ptr(res), ptr(seq), len(res),
@@ -133,6 +134,16 @@ class MatchingEngineService:
         if rc != 0:
             raise ServiceError(f"flush failed ({rc}): {self.last_error()}")
         return seq[: nr.value].copy(), res[: nr.value].copy(), fills[: nf.value].copy()
+
+    @property
+    def updates_dropped(self) -> int:
+        return int(self.lib.me_service_updates_dropped(self.h))
+
+    def stats(self) -> dict:
+        """Books handed over from idle symbols, resting orders replayed from the DB at create."""
+        a, b = C.c_uint64(0), C.c_uint64(0)
+        self.lib.me_service_stats(self.h, C.byref(a), C.byref(b))
+        return {"reclaimed_books": a.value, "recovered_orders": b.value}
 
     def market_data(self, symbol) -> dict:
         """MarketDataUpdate (proto:60-67) from the GPU book; a missing side has has_* False and 0s."""

@@ -1,12 +1,10 @@
-"""Multi-GPU host logic: symbols are hash-sharded across GPUs with no cross-GPU matching
-(SURVEY.md §8(e)). A global batch is split into per-shard batches (local symbol ids, global seq
-kept); per-shard tapes and results merge back into exactly the single-engine output because
-every taker's fills live on one shard and the tape order is (taker seq, fill#)."""
+"""The symbol-hash partition as the bench's CPU baseline uses it: a global batch split
+into per-shard batches (local symbol ids, global seq kept). The deployment's split, scatter, gather
+and merge are C++ (csrc/me_cluster.cpp, include/me_cluster.h)."""
 from __future__ import annotations
 
 import numpy as np
 
-from ._abi import FILL_DTYPE, RESULT_DTYPE
 from .engine import Batch, shard_table
 
 
@@ -35,25 +33,3 @@ class ShardPlan:
             out.append((lb, pos))
         return out
 
-
-def merge_tapes(tapes) -> np.ndarray:
-    """Per-shard tapes (each ordered by taker seq) -> the global tape, stable by taker seq."""
-    tapes = [t for t in tapes if len(t)]
-    if not tapes:
-        return np.zeros(0, dtype=FILL_DTYPE)
-    allf = np.concatenate(tapes)
-    order = np.argsort(allf["taker_seq"], kind="stable")
-    return allf[order]
-
-
-def merge_results(n: int, parts) -> np.ndarray:
-    """parts: (results of a shard, positions in the global batch) -> global results, with
-    tape_offset recomputed against the merged tape."""
-    res = np.zeros(n, dtype=RESULT_DTYPE)
-    for r, pos in parts:
-        res[pos] = r
-    off = np.zeros(n, dtype=np.uint64)
-    if n:
-        off[1:] = np.cumsum(res["fill_count"].astype(np.uint64))[:-1]
-    res["tape_offset"] = off.astype(np.uint32)
-    return res

@@ -1,17 +1,19 @@
-"""One rank of the sharded-service check (launched by tests/test_multirank.py).
+"""One rank of the sharded-deployment checks (launched by tests/test_multirank.py), through the C++
+cluster (include/me_cluster.h, csrc/me_cluster.cpp) — no torch.distributed anywhere.
 
-Rank 0 hosts a MatchingEngineService over a cluster.ShardedMatcher (the shards: this rank's and
-the other ranks' books, symbols splitmix64-hashed); the other ranks serve its commands. Rank 0 also
-runs the same request stream through a second service whose matcher spans rank 0 alone (one book
-holding every symbol) and compares the two SQLite databases row by row, the per-order books
-(GetOrderBook) and the gathered level snapshot.
+Rank 0 drives the cluster: (1) direct slices through me_cluster_submit / collect (two in flight) against
+ONE oracle book over the whole stream, out-of-range symbol ids included; (2) a SubmitOrder service over
+me_cluster_matcher next to a service over a single oracle book fed the same requests: every flush's
+outputs, all SQLite rows, the per-order books, market data and the gathered level snapshot must be
+equal. The other ranks sit in me_cluster_serve.
 
-env: RANK, WORLD_SIZE, MASTER_ADDR, MASTER_PORT; argv: BOOK(oracle|gpu|oracle_refuse) TMPDIR OUT_JSON
-  oracle: every shard book is the CPU oracle (the host protocol under gloo, CPU tensors)
-  gpu:    every shard book is the HIP engine on cuda:0 (ranks share the box's one GPU; gloo)
-  oracle_refuse: oracle shards, and the last rank's admission control refuses its part of the
-          second slice once: no shard may apply anything of it, the service keeps it queued, the
-          next flush matches it (all-or-none admission, cluster.ShardedMatcher._match)
+env: RANK, WORLD_SIZE, MASTER_ADDR, MASTER_PORT; argv: KIND TMPDIR OUT_JSON
+  oracle:        oracle shards (me_shard_ops over the CPU oracle), TCP transport
+  oracle_refuse: oracle shards; the last rank's admission refuses its 2nd part once: nothing of that slice
+                 may apply anywhere, the service splits it and matches the halves
+  gpu:           HIP engine shards on cuda:0 (ranks share the box's one GPU), TCP transport
+  rccl:          HIP engine shard over RCCL (world size 1 on a one-GPU box: every RCCL call of the protocol,
+                 the self send / recv included)
 """
 import json
 import os
@@ -25,25 +27,29 @@ sys.path.insert(0, ROOT)
 
 
 class OracleShard:
-    """The oracle with the Engine methods the matcher uses (test infrastructure)."""
+    """The oracle behind me_shard_ops (test infrastructure)."""
 
     def __init__(self, ids, refuse_calls=()):
         from oracle.oracle import OracleBook
 
         self.ids = np.asarray(ids, dtype=np.uint32)
         self.ob = OracleBook(max(len(ids), 1), symbol_ids=self.ids if len(ids) else None)
-        self.refuse_calls, self.calls = set(refuse_calls), 0
+        self.refuse_calls, self.calls, self.refused = set(refuse_calls), 0, 0
 
-    def admits(self, b):
+    def admit(self, n_rest):
         self.calls += 1
-        return self.calls not in self.refuse_calls
+        if self.calls in self.refuse_calls:
+            self.refused += 1
+            return False
+        return True
 
-    def submit_batch(self, b):
+    def match(self, b):
         return self.ob.submit(b)
 
     def book_orders(self, s, depth):
         from tests._parity import side_levels
 
+        depth = depth or (1 << 20)  # 0: the whole book
         d = self.ob.dump(s)
         lb, la = self.ob.snapshot(s, depth)
         return side_levels(d, 1, depth), side_levels(d, 2, depth), lb, la
@@ -51,15 +57,34 @@ class OracleShard:
     def levels_all(self, depth):
         from matching_engine_amd import LEVEL_DTYPE
 
-        n = len(self.ids)
+        n = max(len(self.ids), 1)
         lv = np.zeros((n, 2, depth), dtype=LEVEL_DTYPE)
         cnt = np.zeros((n, 2), dtype=np.uint32)
-        for s in range(n):
+        for s in range(len(self.ids)):
             b, a = self.ob.snapshot(s, depth)
             lv[s, 0, : len(b)] = b
             lv[s, 1, : len(a)] = a
             cnt[s] = (len(b), len(a))
         return lv, cnt
+
+
+class SingleBook:
+    """One oracle book holding every symbol, as a me_matcher (cluster.python_matcher)."""
+
+    def __init__(self, S, max_batch, max_resting):
+        self.shard = OracleShard(np.arange(S, dtype=np.uint32))
+        self.num_symbols, self.max_batch, self.max_resting = S, max_batch, max_resting
+
+    def match(self, b):
+        return self.shard.match(b)
+
+    def book_orders(self, s, depth):
+        return self.shard.book_orders(s, depth)
+
+    def c_matcher(self):
+        from matching_engine_amd.cluster import python_matcher
+
+        return python_matcher(self)
 
 
 def rows(db):
@@ -71,57 +96,96 @@ def rows(db):
     return o, f
 
 
+def direct_batch(st, sc, S, k):
+    """Direct slices use the upper half of the symbol ids (the service below uses the lower half, so
+    its orders never meet these books' resting orders, which have no DB rows)."""
+    b = st.next(sc.batch)
+    b.symbol = (S // 2 + b.symbol % (S // 2)).astype(np.uint32)
+    if k == 1:
+        b.symbol[::997] = S + 5  # unknown ids: BAD_SYMBOL, like one engine
+    return b
+
+
+def direct_slices(me, cl, S, world):
+    """Slices straight through me_cluster_submit / collect, two in flight, against one oracle book."""
+    from oracle.oracle import OracleBook
+
+    sc = me.preset(5, num_symbols=S, batch=3000)
+    st = me.Stream(sc)
+    ref = OracleBook(S)
+    batches = [direct_batch(st, sc, S, k) for k in range(6)]
+    fills = 0
+    pend = []
+    for k, b in enumerate(batches):
+        pend.append((cl.submit(b), b))
+        if len(pend) == 2 or k == len(batches) - 1:
+            while pend:
+                t, bb = pend.pop(0)
+                res, tape = cl.collect(t, len(bb))
+                ro, fo = ref.submit(bb)
+                fills += len(fo)
+                if not (len(tape) == len(fo) and np.array_equal(tape, fo)):
+                    return False, f"direct slice {k}: tape differs ({len(tape)} vs {len(fo)})", fills
+                for x in ("filled_qty", "remaining_qty", "fill_count", "tape_offset", "status", "reason"):
+                    if not np.array_equal(res[x], ro[x]):
+                        return False, f"direct slice {k}: results.{x} differs", fills
+    return True, "", fills
+
+
 def main():
     kind, tmp, out_path = sys.argv[1], sys.argv[2], sys.argv[3]
-    import torch.distributed as dist
-
     import matching_engine_amd as me
-    from matching_engine_amd.cluster import ShardedMatcher
+    from matching_engine_amd.cluster import Cluster, ShardOps, shard_symbols
 
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    solo = dist.new_group([0])  # rank 0 alone: the single-engine run
+    port = int(os.environ["MASTER_PORT"])
     S, L, MB, MR = 40, 128, 4096, 1 << 16
     syms = [f"S{i:02d}" for i in range(S)]
     mids = {s: 1_000_000 + 1000 * i for i, s in enumerate(syms)}
     base = np.array([mids[s] - 64 for s in syms], dtype=np.int64)
-
     refuse = kind == "oracle_refuse"
-
-    def shard(ids, last=False):
-        if kind in ("oracle", "oracle_refuse"):
-            return OracleShard(ids, refuse_calls=(2,) if (refuse and last) else ())
-        return None
-
-    from matching_engine_amd.sharding import ShardPlan
-
-    plan = ShardPlan(S, world)
-    m = ShardedMatcher(S, L, base, MB, MR, shard_book=shard(plan.members[rank], last=rank == world - 1), device=0)
+    gpu = kind in ("gpu", "rccl")
+    ops = None
+    if not gpu:
+        shard = OracleShard(shard_symbols(S, world, rank), refuse_calls=(2,) if (refuse and rank == world - 1) else ())
+        ops = ShardOps(shard, MR)
+    cl = Cluster(rank, world, S, MB, transport="rccl" if kind == "rccl" else "tcp", port=port, device=0, levels=L,
+                 base_prices=base, max_resting=MR, shard_ops=ops, timeout_ms=120000)
     if rank != 0:
-        m.serve()
-        dist.barrier()
-        dist.destroy_process_group()
+        cl.serve()
+        res = {"refused": shard.refused if ops is not None else 0, "stats": cl.stats()}
+        json.dump(res, open(out_path + f".r{rank}", "w"))
+        cl.close()
         return
-    m1 = ShardedMatcher(S, L, base, MB, MR, shard_book=shard(np.arange(S, dtype=np.uint32)), device=0, group=solo)
+    ok, msg, direct_fills = (True, "", 0) if refuse else direct_slices(me, cl, S, world)
+    # fresh books for the service comparison: a second cluster would need a second port; instead the
+    # single-book side replays the direct slices first, so both sides start from the same books
+    single = SingleBook(S, MB, world * MR)
+    if not refuse:
+        sc = me.preset(5, num_symbols=S, batch=3000)
+        st = me.Stream(sc)
+        for k in range(6):
+            single.match(direct_batch(st, sc, S, k))
+    first_oid = 6 * 3000 + 1 if not refuse else 1
     dbs = [os.path.join(tmp, "sharded.sqlite"), os.path.join(tmp, "single.sqlite")]
-    svcs = [me.MatchingEngineService(None, syms[:5], db_path=dbs[0], matcher=m),
-            me.MatchingEngineService(None, syms[:5], db_path=dbs[1], matcher=m1)]
+    svcs = [me.MatchingEngineService(None, syms[:5], db_path=dbs[0], matcher=cl),
+            me.MatchingEngineService(None, syms[:5], db_path=dbs[1], matcher=single)]
     rng = np.random.default_rng(17)
-    owner = {}
-    live = []
+    owner, live = {}, []
     outs = [[], []]
-    refused = 0
-    msg = ""
-    ok = True
+    # the services start at OID 1 while the books already hold the direct slices' seqs (up to 18,000):
+    # burn OIDs below first_oid with requests the service rejects after allocating an OID (side 0)
+    for _ in range(first_oid - 1):
+        for v in svcs:
+            v.submit_order("C", "S00", 0, 0, 100, 4, 1)
     for slice_no in range(5):
         for _ in range(1500):
             if live and rng.random() < 0.15:
                 oid = live[int(rng.integers(len(live)))]
-                s = owner[oid][1]
                 for v in svcs:
-                    v.cancel_order(owner[oid][0], s, f"OID-{oid}")
+                    v.cancel_order(owner[oid][0], owner[oid][1], f"OID-{oid}")
                 continue
-            s = syms[int(rng.integers(S))]
+            s = syms[int(rng.integers(S // 2))]
             otype = 1 if rng.random() < 0.2 else 0
             side = int(rng.choice([1, 2]))
             px = mids[s] + int(rng.integers(-40, 41)) + (int(rng.integers(-900, 900)) if rng.random() < 0.02 else 0)
@@ -134,41 +198,53 @@ def main():
             if otype == 0:
                 live.append(oid)
         for k, v in enumerate(svcs):
-            try:
-                outs[k].append(v.flush())
-            except me.ServiceError as e:
-                if not (refuse and k == 0 and refused == 0):
-                    raise
-                refused += 1  # the sharded service: nothing matched, the slice is still pending
-                if v.pending == 0 or "refused" not in str(e):
-                    ok, msg = False, f"refused flush: pending {v.pending}, error {e}"
-                outs[k].append(v.flush())
+            outs[k].append(v.flush())
     for k in range(5):
         for a, b, what in zip(outs[0][k], outs[1][k], ("seq", "results", "tape")):
-            if len(a) != len(b) or not np.array_equal(a, b):
-                ok, msg = False, f"slice {k}: {what} differs"
+            if ok and (len(a) != len(b) or not np.array_equal(a, b)):
+                ok, msg = False, f"service slice {k}: {what} differs"
     ra, rb = rows(dbs[0]), rows(dbs[1])
-    if ra != rb:
+    if ok and ra != rb:
         ok, msg = False, f"DB rows differ: orders {len(ra[0])} vs {len(rb[0])}, fills {len(ra[1])} vs {len(rb[1])}"
     for s in syms[::7]:
-        if svcs[0].order_book(s) != svcs[1].order_book(s):
+        if ok and svcs[0].order_book(s) != svcs[1].order_book(s):
             ok, msg = False, f"order book of {s} differs"
-        if svcs[0].market_data(s) != svcs[1].market_data(s):
+        if ok and svcs[0].market_data(s) != svcs[1].market_data(s):
             ok, msg = False, f"market data of {s} differs"
-    lv, cnt = m.snapshot(5)
-    lv1, cnt1 = m1.snapshot(5)
-    if not (np.array_equal(cnt, cnt1) and np.array_equal(lv, lv1)):
+        if ok and [x.tolist() for x in svcs[0].get_order_book(s, 5)] != [x.tolist() for x in svcs[1].get_order_book(s, 5)]:
+            ok, msg = False, f"level view of {s} differs"
+    lv, cnt = cl.snapshot(5)
+    lv1 = np.zeros_like(lv)
+    cnt1 = np.zeros_like(cnt)
+    for s in range(S):
+        b, a = single.shard.ob.snapshot(s, 5)
+        lv1[s, 0, : len(b)] = b
+        lv1[s, 1, : len(a)] = a
+        cnt1[s] = (len(b), len(a))
+    if ok and not (np.array_equal(cnt, cnt1) and np.array_equal(lv, lv1)):
         ok, msg = False, "level snapshots differ"
     nrows, nfills = len(ra[0]), len(ra[1])
+    errs = [v.last_error() for v in svcs]
     for v in svcs:
         v.close()
-    m.stop()
-    dist.barrier()
-    if refuse and refused != 1:
-        ok, msg = False, f"expected one refused flush, saw {refused}"
-    json.dump({"ok": ok, "msg": msg, "orders": nrows, "fill_rows": nfills, "world": world, "refused": refused},
+    st0 = cl.stats()
+    cl.stop()
+    cl.close()
+    refused = 0
+    if refuse:
+        import time
+
+        path = out_path + f".r{world - 1}"
+        for _ in range(200):
+            if os.path.exists(path):
+                break
+            time.sleep(0.05)
+        refused = json.load(open(path))["refused"] if world > 1 else shard.refused
+        if refused != 1:
+            ok, msg = False, f"expected one refusal, saw {refused}"
+    json.dump({"ok": ok, "msg": msg, "orders": nrows, "fill_rows": nfills, "world": world, "refused": refused,
+               "direct_fills": direct_fills, "errors": errs, "slices": st0["slices"], "bytes": st0["bytes"]},
               open(out_path, "w"))
-    dist.destroy_process_group()
 
 
 if __name__ == "__main__":

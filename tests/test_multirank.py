@@ -1,6 +1,8 @@
-"""World-size-2 sharding tests: split by symbol hash, per-shard books, gather (gloo), merge by
-taker seq == one book over the whole stream. The CPU test exercises the host logic with the
-oracle as the per-shard book; the GPU test runs the HIP engine in every rank."""
+"""The sharded deployment through the C++ cluster (include/me_cluster.h): ranks as processes, symbols
+hash-partitioned, the protocol over TCP (CPU tests: oracle shards behind me_shard_ops) or RCCL (the GPU
+box: world size 1, since one GPU cannot host two RCCL ranks). Every check compares against ONE book
+holding every symbol: direct slices two in flight, then a SubmitOrder service over me_cluster_matcher
+against a service over a single book — outputs, SQLite rows, books, market data, level snapshot."""
 import json
 import os
 import socket
@@ -20,87 +22,62 @@ def _free_port():
     return p
 
 
-def _run(kind, world, tmp_path, script="multirank_worker.py"):
-    out = str(tmp_path / f"mr_{kind}.json")
+def _run(kind, world, tmp_path, timeout=240):
+    out = str(tmp_path / f"cl_{kind}_{world}.json")
     port = _free_port()
     procs = []
-    args = [kind, str(tmp_path), out] if script == "cluster_worker.py" else [kind, out]
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         # child processes (never exec over a GPU-initialised interpreter)
-        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, script)] + args,
-                                      env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "cluster_worker.py"), kind, str(tmp_path),
+                                       out], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
     logs = []
     for p in procs:
         try:
-            o, _ = p.communicate(timeout=240)
+            o, _ = p.communicate(timeout=timeout)
         except subprocess.TimeoutExpired:
             p.kill()
             o, _ = p.communicate()
-        logs.append(o.decode(errors="replace")[-2000:])
+        logs.append(o.decode(errors="replace")[-3000:])
     assert all(p.returncode == 0 for p in procs), "\n".join(logs)
     return json.load(open(out))
 
 
-def test_two_rank_sharding_gloo_cpu(built, tmp_path):
-    r = _run("oracle", 2, tmp_path)
+@pytest.mark.parametrize("world", [2, 3])
+def test_cluster_tcp_oracle_shards(built, tmp_path, world):
+    """the C++ cluster over a CPU transport (TCP star), oracle shards: direct slices
+    and the sharded service's DB equal one book's."""
+    r = _run("oracle", world, tmp_path)
     assert r["ok"], r["msg"]
-    assert r["fills"] > 0
+    assert r["orders"] > 5000 and r["fill_rows"] > 1000 and r["direct_fills"] > 0
+    assert r["errors"] == ["", ""], r["errors"]
+    assert r["slices"] >= 6 + 5
 
 
-@pytest.mark.gpu
-def test_two_rank_sharding_gpu_engines(built, tmp_path):
-    r = _run("gpu", 2, tmp_path)
-    assert r["ok"], r["msg"]
-    assert r["fills"] > 0
-
-
-def test_two_rank_tape_gather_gloo_cpu(built, tmp_path):
-    """matching_engine_amd.gather.gather_batch (the RCCL tape/result gather) over gloo: per-shard
-    tapes/results gathered to rank 0 equal one oracle book over the whole stream."""
-    r = _run("gather", 2, tmp_path)
-    assert r["ok"], r["msg"]
-    assert r["fills"] > 0
-
-
-@pytest.mark.gpu
-def test_two_rank_tape_gather_gpu_engines(built, tmp_path):
-    r = _run("gpu_gather", 2, tmp_path)
-    assert r["ok"], r["msg"]
-    assert r["fills"] > 0
-
-
-@pytest.mark.gpu
-def test_rccl_gather_single_rank(built, tmp_path):
-    """The gather over the nccl backend (RCCL) with device tensors, world size 1 (the box has one
-    GPU): all_gather of sizes, gather of tapes and results, the overlapped staging on the engine's
-    stream — the code path an 8-GPU node runs, minus the xGMI hops."""
-    r = _run("rccl_gather", 1, tmp_path)
-    assert r["ok"], r["msg"]
-    assert r["fills"] > 0
-
-
-def test_two_rank_sharded_service_db_equals_single_engine(built, tmp_path):
-    """SubmitOrder on rank 0 over two shards (cluster.ShardedMatcher, gloo): every
-    slice's merged tape/results, the SQLite rows, the per-order books, market data and the gathered
-    level snapshot equal a single book holding every symbol."""
-    r = _run("oracle", 2, tmp_path, script="cluster_worker.py")
-    assert r["ok"], r["msg"]
-    assert r["orders"] > 5000 and r["fill_rows"] > 1000
-
-
-def test_sharded_slice_refused_all_or_none(built, tmp_path):
-    """One shard's admission control refuses its part of a slice: no shard applies anything, the
-    service keeps the slice queued (ME_E_CAPACITY from the matcher), the next flush matches it once —
-    the DB, outputs and books still equal the single book's."""
-    r = _run("oracle_refuse", 2, tmp_path, script="cluster_worker.py")
+def test_cluster_refused_slice_is_split_all_or_none(built, tmp_path):
+    """One shard's admission control refuses its part of a slice once: no shard applies anything of it
+    (all-or-none vote), the service splits the slice and matches the halves — the DB, outputs and books
+    still equal the single book's, and the flush reports no error."""
+    r = _run("oracle_refuse", 2, tmp_path)
     assert r["ok"], r["msg"]
     assert r["refused"] == 1
+    assert r["errors"] == ["", ""], r["errors"]
 
 
 @pytest.mark.gpu
-def test_two_rank_sharded_service_gpu_engines(built, tmp_path):
-    r = _run("gpu", 2, tmp_path, script="cluster_worker.py")
+def test_cluster_tcp_gpu_engines(built, tmp_path):
+    """Two ranks, each with its own HIP engine on the box's GPU, protocol over TCP."""
+    r = _run("gpu", 2, tmp_path)
     assert r["ok"], r["msg"]
     assert r["orders"] > 5000 and r["fill_rows"] > 1000
+
+
+@pytest.mark.gpu
+def test_cluster_rccl_single_rank(built, tmp_path):
+    """The RCCL transport with an engine shard, world size 1: ncclCommInitRank over the TCP bootstrap,
+    broadcast / all-reduce / all-gather, and the grouped send / recv of parts, tapes and results (rank 0
+    sends to itself) — every RCCL call an 8-GPU node makes, minus the xGMI hops."""
+    r = _run("rccl", 1, tmp_path)
+    assert r["ok"], r["msg"]
+    assert r["orders"] > 5000 and r["fill_rows"] > 1000 and r["bytes"] > 0

@@ -181,8 +181,9 @@ def test_submitorder_stream_matches_oracle_and_db(me, tmp_path):
 
 
 def test_cancel_request_validation(me):
-    """CancelOrder (build extension): in-band rejects in SubmitOrder's style, no OID consumed on a
-    reject; an accepted cancel answers with the target's id and takes the next stream position."""
+    """CancelOrder (build extension): in-band rejects in SubmitOrder's style; an accepted cancel answers
+    with the target's id and consumes NO OID (its stream position repeats the last OID allocated), so
+    accepted orders keep the reference's gap-free OID sequence."""
     svc = me.MatchingEngineService(None, ["SYM"])
     assert svc.cancel_order("C", "", "OID-1")["error_message"] == "symbol is required"
     for bad in ("OID-", "OID-0", "OID-x1", "X-3", "OID-3a", ""):
@@ -192,7 +193,10 @@ def test_cancel_request_validation(me):
     assert svc.submit_order("C", "SYM", 0, 1, 100, 4, 5)["order_id"] == "OID-1"
     r = svc.cancel_order("C", "SYM", "OID-1")
     assert r == {"order_id": "OID-1", "success": True, "error_message": "", "grpc_status": 0}
-    assert svc.next_oid == 3 and svc.pending == 2
+    assert svc.next_oid == 2 and svc.pending == 2
+    assert svc.submit_order("C", "SYM", 0, 1, 100, 4, 5)["order_id"] == "OID-2"  # no gap
+    assert svc.cancel_order("C", "NOSUCH", "OID-2")["success"]  # an unknown symbol takes no book
+    assert svc.next_oid == 3 and svc.pending == 4
     assert svc.order_updates() == []  # nothing matched yet
 
 

@@ -39,9 +39,9 @@ class OracleMatcher:
         return side_levels(d, 1, depth), side_levels(d, 2, depth), lb, la
 
     def c_matcher(self):
-        from matching_engine_amd.cluster import ShardedMatcher
+        from matching_engine_amd.cluster import python_matcher
 
-        return ShardedMatcher.c_matcher(self)
+        return python_matcher(self)
 
 
 def _stream(rng, syms, mids, n):
