@@ -418,6 +418,11 @@ def cluster_leg(args, world, rank, local, sc, base, slices):
 
 def main():
     args = parse()
+    # the contract is ONE JSON line on stdout: whatever the runtimes print there (RCCL's version banner
+    # at its first communicator, library notices) goes to stderr, the line to the saved stdout
+    sys.stdout.flush()
+    json_out = os.dup(1)
+    os.dup2(2, 1)
     world, rank, local = dist_setup(args)
     import torch
 
@@ -571,7 +576,7 @@ def main():
         def expire():
             if rank == 0:
                 line["cluster"] = {"error": "cluster leg timed out (180 s)"}
-                print(json.dumps(line), flush=True)
+                os.write(json_out, (json.dumps(line) + "\n").encode())
             os._exit(0)
 
         wd = threading.Timer(180.0, expire)
@@ -585,7 +590,7 @@ def main():
         if rank == 0:
             line["cluster"] = got
     if rank == 0:
-        print(json.dumps(line), flush=True)
+        os.write(json_out, (json.dumps(line) + "\n").encode())
     if world > 1:
         tdist.destroy_process_group()
 

@@ -309,16 +309,16 @@ struct Rccl {
 Rccl g_rccl;
 std::mutex g_rccl_mu;
 
+// RCCL for the bulk payloads (device buffers over xGMI); the small host values (commands, votes, sizes)
+// go over the TCP star the bootstrap opened — a host word needs no H2D / collective / D2H round trip.
 class RcclTransport : public Transport {
  public:
   ncclComm_t comm = nullptr;
   hipStream_t st = nullptr;
-  int64_t* d_small = nullptr;  // small-value staging (kSmall words)
-  static constexpr size_t kSmall = 4096;
+  TcpTransport ctl;            // the control plane
   ~RcclTransport() override {
     if (st) (void)hipStreamSynchronize(st);
     if (comm) g_rccl.CommDestroy(comm);
-    if (d_small) (void)hipFree(d_small);
     if (st) (void)hipStreamDestroy(st);
   }
   bool device() const override { return true; }
@@ -334,33 +334,13 @@ class RcclTransport : public Transport {
     const hipError_t e = hipStreamSynchronize(st);
     return e == hipSuccess || hfail(e, "hipStreamSynchronize");
   }
-  bool small(int64_t* v, size_t n, int op, int64_t* all = nullptr) {  // op 0 bcast, 1 min, 2 sum, 3 gather
-    if (n * (op == 3 ? world + 1 : 1) > kSmall) {
-      err = "rccl transport: small collective too large";
-      return false;
-    }
-    hipError_t e = hipMemcpyAsync(d_small, v, 8 * n, hipMemcpyHostToDevice, st);
-    if (e != hipSuccess) return hfail(e, "H2D");
-    ncclResult_t r;
-    if (op == 0)
-      r = g_rccl.Broadcast(d_small, d_small, n, ncclInt64, 0, comm, st);
-    else if (op == 3)
-      r = g_rccl.AllGather(d_small, d_small + n, n, ncclInt64, comm, st);
-    else
-      r = g_rccl.AllReduce(d_small, d_small, n, ncclInt64, op == 1 ? ncclMin : ncclSum, comm, st);
-    if (r != ncclSuccess) return nfail(r, "collective");
-    e = op == 3 ? (rank == 0 ? hipMemcpyAsync(all, d_small + n, 8 * n * world, hipMemcpyDeviceToHost, st) : hipSuccess)
-                : hipMemcpyAsync(v, d_small, 8 * n, hipMemcpyDeviceToHost, st);
-    if (e != hipSuccess) return hfail(e, "D2H");
-    moved += 8 * n;
-    return sync();
+  bool ctl_ok(bool ok) {
+    if (!ok) err = ctl.error();
+    return ok;
   }
-  bool bcast(int64_t* v, size_t n) override { return small(v, n, 0); }
-  bool allreduce(int64_t* v, size_t n, bool min) override { return small(v, n, min ? 1 : 2); }
-  bool gather(const int64_t* mine, size_t n, int64_t* all) override {
-    std::vector<int64_t> tmp(mine, mine + n);
-    return small(tmp.data(), n, 3, all);
-  }
+  bool bcast(int64_t* v, size_t n) override { return ctl_ok(ctl.bcast(v, n)); }
+  bool allreduce(int64_t* v, size_t n, bool min) override { return ctl_ok(ctl.allreduce(v, n, min)); }
+  bool gather(const int64_t* mine, size_t n, int64_t* all) override { return ctl_ok(ctl.gather(mine, n, all)); }
   bool scatterv(const char* send, const std::vector<size_t>& bytes, char* recv) override {
     ncclResult_t r = g_rccl.GroupStart();
     if (r != ncclSuccess) return nfail(r, "group start");
@@ -421,11 +401,12 @@ class RcclTransport : public Transport {
     }
     hipError_t he = hipSetDevice(c.device);
     if (he != hipSuccess) return (e = std::string("hipSetDevice: ") + hipGetErrorString(he)), false;
-    if ((he = hipStreamCreateWithFlags(&st, hipStreamNonBlocking)) != hipSuccess ||
-        (he = hipMalloc((void**)&d_small, 8 * kSmall)) != hipSuccess)
+    if ((he = hipStreamCreateWithFlags(&st, hipStreamNonBlocking)) != hipSuccess)
       return (e = std::string("rccl transport: ") + hipGetErrorString(he)), false;
-    std::vector<int> fds;
+    std::vector<int>& fds = ctl.fds;
     if (!star_connect(c, fds, e)) return false;
+    ctl.rank = c.rank;
+    ctl.world = c.world;
     ncclUniqueId id;
     memset(&id, 0, sizeof id);
     bool ok = true;
@@ -440,8 +421,6 @@ class RcclTransport : public Transport {
       ok = recv_all(fds[0], &id, sizeof id);
       if (!ok) e = "bootstrap: no unique id from rank 0";
     }
-    for (int fd : fds)
-      if (fd >= 0) ::close(fd);
     if (!ok) return false;
     const ncclResult_t r = g_rccl.CommInitRank(&comm, (int)c.world, id, (int)c.rank);
     if (r != ncclSuccess) {
