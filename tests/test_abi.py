@@ -1,5 +1,5 @@
-"""The C-ABI library loads and exports exactly what include/me_engine.h declares; without a GPU
-the engine refuses to start (no CPU fallback). Runs on CPU."""
+"""The C-ABI library loads and exports exactly what include/*.h declare; without a GPU the engine
+refuses to start (no CPU fallback). Runs on CPU."""
 import ctypes as C
 import os
 import re
@@ -14,8 +14,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def declared_functions():
     src = open(os.path.join(ROOT, "include", "me_engine.h")).read()
     src += open(os.path.join(ROOT, "include", "me_service.h")).read()
+    src += open(os.path.join(ROOT, "include", "me_cluster.h")).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(me_[a-z0-9_]+)\s*\(", src)) - {"me_engine", "me_gen", "me_service"})
+    return sorted(set(re.findall(r"\b(me_[a-z0-9_]+)\s*\(", src)) - {"me_engine", "me_gen", "me_service", "me_cluster"})
 
 
 def test_header_declares_the_boundary():
