@@ -490,6 +490,12 @@ extern "C" me_engine* me_create(const me_config* cfg) {
   const uint64_t ring = cfg->seq_ring ? cfg->seq_ring : (1ull << 28);
   bk.ring_mask = ring - 1;
   bk.fcap = cfg->far_levels ? cfg->far_levels : 1024u;
+  // deep windows in HBM (L > LDS_MAX_LEVELS): a symbol with at least hot_min records in a batch runs
+  // the write-through top-of-book path (k_match_hot); ME_HOT_MIN overrides (0 = off)
+  {
+    const char* v = getenv("ME_HOT_MIN");
+    bk.hot_min = L > LDS_MAX_LEVELS ? (v ? (uint32_t)atoi(v) : 512u) : 0u;
+  }
   // old-order table: live orders <= resting, at load <= 1/2
   uint64_t oldn = 1024;
   while (oldn < 2 * (cfg->max_resting + 64)) oldn <<= 1;

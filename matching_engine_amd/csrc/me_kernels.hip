@@ -200,6 +200,7 @@ __global__ __launch_bounds__(256) void k_sort_scatter(const uint32_t* __restrict
 // levels stay on chip. The HBM copy is stale while an entry is dirty; write-back on eviction, on free
 // (freed chunks must hold qty 0 in HBM), before a re-centre and at kernel end.
 constexpr int CK_MEM = 64;  // entries (direct-mapped by level)
+constexpr uint32_t HOT_MAX_WORDS = 1024;  // k_match_hot keeps occupancy in LDS: windows up to 65,536 levels
 struct alignas(16) CacheEntry {
   uint32_t cid;    // cached chunk id, NIL = empty
   uint32_t dirty;  // slots differ from HBM
@@ -1024,10 +1025,90 @@ __host__ __device__ constexpr size_t lds_wave_bytes(uint32_t L) {
 // Window placement of a k_match instantiation.
 enum LadderKind { LAD_HBM = 0, LAD_LDS = 1 };
 
+// One record's outcome (ok = false: a pool is exhausted, the batch fails with the sticky error word).
+struct RecOut {
+  int filled, remaining;
+  uint32_t nfill;
+  uint32_t st;  // status | reason << 8
+  unsigned long long fstart;
+  bool ok;
+};
+__device__ __forceinline__ RecOut rec_out(int filled, int remaining, uint32_t nfill, uint8_t status, uint8_t reason,
+                                          unsigned long long fstart) {
+  RecOut o;
+  o.filled = filled;
+  o.remaining = remaining;
+  o.nfill = nfill;
+  o.st = (uint32_t)status | ((uint32_t)reason << 8);
+  o.fstart = fstart;
+  o.ok = true;
+  return o;
+}
+
+// One record in the generic way (deep windows): reject reasons, sweep, far levels, rest or cancel.
+__device__ __forceinline__ RecOut generic_record(WaveCtx& c, unsigned long long seq, long long px, int q,
+                                                 uint32_t kind) {
+  const uint32_t Lw = c.bk.L;
+  const uint32_t side = kind & 3u;
+  const bool market = (kind >> 2) & 1u;
+  const bool cancel = (kind >> 3) & 1u;
+  const unsigned long long fstart = c.wptr;
+  if (cancel) {
+    const int got = cancel_order(c, (unsigned long long)px);
+    STAMP_ADD(c, PH_CANCEL);
+    return got > 0 ? rec_out(0, got, 0, ME_ST_CANCELED, ME_RJ_NONE, fstart)
+                   : rec_out(0, 0, 0, ME_ST_REJECTED, ME_RJ_UNKNOWN_ORDER, fstart);
+  }
+  if (q <= 0) return rec_out(0, 0, 0, ME_ST_REJECTED, ME_RJ_BAD_QTY, fstart);
+  if (side != ME_SIDE_BUY && side != ME_SIDE_SELL) return rec_out(0, q, 0, ME_ST_REJECTED, ME_RJ_BAD_SIDE, fstart);
+  // no OID is 0 (the counter starts at 1, storage.cpp:254-267)
+  if (seq == 0ull) return rec_out(0, q, 0, ME_ST_REJECTED, ME_RJ_BAD_SEQ, fstart);
+  const bool buy = side == ME_SIDE_BUY;
+  const unsigned long long off = (unsigned long long)px - (unsigned long long)c.base;
+  const bool inw = off < (unsigned long long)Lw;
+  const bool above = !inw && px > c.base;
+  // last window level the taker may trade at (-1 / L: none) and whether it reaches past the window
+  const int lim = market ? (buy ? (int)Lw - 1 : 0)
+                : inw    ? (int)off
+                : buy    ? (above ? (int)Lw - 1 : -1)
+                         : (above ? (int)Lw : 0);
+  const bool far = market || (buy ? above : (!inw && !above));
+  long long got = sweep(c, buy ? 1 : -1, lim, (long long)q, seq);
+  if (got < q && far && c.fcount(buy ? 1u : 0u) != 0u)
+    got += far_take(c, buy, market, px, (uint32_t)(q - got), seq);
+  STAMP_ADD(c, PH_SWEEP);
+  const uint32_t nfill = (uint32_t)(c.wptr - fstart);
+  const int filled = (int)got;
+  const int rem = q - filled;
+  uint8_t stt;
+  if (market) {
+    stt = rem == 0 ? ME_ST_FILLED : ME_ST_CANCELED;
+  } else {
+    const bool failed = rem > 0 && !(inw ? rest_order(c, (int)off, seq, rem, buy)
+                                         : far_or_window_rest(c, px, seq, rem, buy));
+    STAMP_ADD(c, PH_REST);
+    if (failed) {
+      RecOut o = rec_out(0, 0, 0, 0, 0, fstart);
+      o.ok = false;
+      return o;
+    }
+    stt = rem == 0 ? ME_ST_FILLED : (filled > 0 ? ME_ST_PARTIALLY_FILLED : ME_ST_NEW);
+  }
+  return rec_out(filled, rem, nfill, stt, ME_RJ_NONE, fstart);
+}
+
+__device__ __forceinline__ void put_rec(ResultLanes& r, uint32_t k, const RecOut& o) {
+  const bool me_ = (uint32_t)lane_id() == k;
+  r.filled = me_ ? o.filled : r.filled;
+  r.remaining = me_ ? o.remaining : r.remaining;
+  r.nfill = me_ ? o.nfill : r.nfill;
+  r.fstart = me_ ? (uint32_t)o.fstart : r.fstart;
+  r.st = me_ ? o.st : r.st;
+}
+
 // The per-record loop of one symbol.
 __device__ __forceinline__ void match_records(WaveCtx& c, const BatchDev& bt, uint32_t lo, uint32_t hi) {
   const int lane = lane_id();
-  const uint32_t Lw = c.bk.L;
   bool ok = true;
   for (uint32_t blk = lo; blk < hi && ok; blk += 64) {
     const uint32_t j = blk + (uint32_t)lane;
@@ -1044,67 +1125,13 @@ __device__ __forceinline__ void match_records(WaveCtx& c, const BatchDev& bt, ui
     STAMP_ADD(c, PH_FETCH);
     uint32_t k = 0;
     for (; k < cnt; ++k) {
-      const unsigned long long seq = rl64(oseq, (int)k);
-      const long long px = rli64(opx, (int)k);
-      const int q = rli32(oq, (int)k);
-      const uint32_t kind = rl32(ok_, (int)k);
       c.recs_left = hi - (blk + k);
-      const uint32_t side = kind & 3u;
-      const bool market = (kind >> 2) & 1u;
-      const bool cancel = (kind >> 3) & 1u;
-      const unsigned long long fstart = c.wptr;
-      if (cancel) {
-        const int got = cancel_order(c, (unsigned long long)px);
-        STAMP_ADD(c, PH_CANCEL);
-        if (got > 0)
-          put_result(R, k, 0, got, 0, ME_ST_CANCELED, ME_RJ_NONE, fstart);
-        else
-          put_result(R, k, 0, 0, 0, ME_ST_REJECTED, ME_RJ_UNKNOWN_ORDER, fstart);
-        continue;
+      const RecOut o = generic_record(c, rl64(oseq, (int)k), rli64(opx, (int)k), rli32(oq, (int)k), rl32(ok_, (int)k));
+      if (!o.ok) {
+        ok = false;  // a pool is exhausted: the batch fails (sticky error word)
+        break;
       }
-      if (q <= 0) {
-        put_result(R, k, 0, 0, 0, ME_ST_REJECTED, ME_RJ_BAD_QTY, fstart);
-        continue;
-      }
-      if (side != ME_SIDE_BUY && side != ME_SIDE_SELL) {
-        put_result(R, k, 0, q, 0, ME_ST_REJECTED, ME_RJ_BAD_SIDE, fstart);
-        continue;
-      }
-      if (seq == 0ull) {  // no OID is 0 (the counter starts at 1, storage.cpp:254-267)
-        put_result(R, k, 0, q, 0, ME_ST_REJECTED, ME_RJ_BAD_SEQ, fstart);
-        continue;
-      }
-      const bool buy = side == ME_SIDE_BUY;
-      const unsigned long long off = (unsigned long long)px - (unsigned long long)c.base;
-      const bool inw = off < (unsigned long long)Lw;
-      const bool above = !inw && px > c.base;
-      // last window level the taker may trade at (-1 / L: none) and whether it reaches past the window
-      const int lim = market ? (buy ? (int)Lw - 1 : 0)
-                    : inw    ? (int)off
-                    : buy    ? (above ? (int)Lw - 1 : -1)
-                             : (above ? (int)Lw : 0);
-      const bool far = market || (buy ? above : (!inw && !above));
-      long long got = sweep(c, buy ? 1 : -1, lim, (long long)q, seq);
-      if (got < q && far && c.fcount(buy ? 1u : 0u) != 0u)
-        got += far_take(c, buy, market, px, (uint32_t)(q - got), seq);
-      STAMP_ADD(c, PH_SWEEP);
-      const uint32_t nfill = (uint32_t)(c.wptr - fstart);
-      const int filled = (int)got;
-      const int rem = q - filled;
-      uint8_t stt;
-      if (market) {
-        stt = rem == 0 ? ME_ST_FILLED : ME_ST_CANCELED;
-      } else {
-        const bool failed = rem > 0 && !(inw ? rest_order(c, (int)off, seq, rem, buy)
-                                             : far_or_window_rest(c, px, seq, rem, buy));
-        STAMP_ADD(c, PH_REST);
-        if (failed) {
-          ok = false;  // a pool is exhausted: the batch fails (sticky error word)
-          break;
-        }
-        stt = rem == 0 ? ME_ST_FILLED : (filled > 0 ? ME_ST_PARTIALLY_FILLED : ME_ST_NEW);
-      }
-      put_result(R, k, filled, rem, nfill, stt, ME_RJ_NONE, fstart);
+      put_rec(R, k, o);
     }
     store_results(bt, R, v && (uint32_t)lane < k, oi);
     STAMP_ADD(c, PH_RESULT);
@@ -1186,6 +1213,20 @@ __global__ __launch_bounds__(256) void k_match(BookDev bk, BatchDev bt) {
     reject_bad_symbols(bt, lo, hi);
     return;
   }
+  if (kLad == LAD_HBM && bk.hot_min && hi - lo >= bk.hot_min && bk.L <= HOT_MAX_WORDS * 64u) {
+    // a hot symbol: k_match_hot takes it (launched right after this kernel)
+    uint32_t idx = 0;
+    if (lane == 0) idx = atomicAdd(bk.hcount, 1u);
+    idx = rl32(idx, 0);
+    if (lane == 0) {
+      Handoff ho{};
+      ho.s = s;
+      ho.pos = lo;
+      ho.nsg = hi;
+      bk.hand[idx] = ho;
+    }
+    return;
+  }
   const uint32_t L = bk.L;
   Level* g_lv = bk.levels + (size_t)s * L;
   unsigned long long* g_occ = bk.occ + (size_t)s * bk.Lwords;
@@ -1232,6 +1273,960 @@ __global__ __launch_bounds__(256) void k_match(BookDev bk, BatchDev bt) {
   wave_end(c);
 }
 
+// ---- hot symbols of deep windows (k_match_hot) ------------------------------------------------
+// A Zipf-hot symbol (config 4: one symbol draws ~14 % of the stream) is a serial chain on one wave,
+// so its record loop sets the launch length. k_match's loop pays HBM round trips inside that chain —
+// window and chunk loads per sweep, level reads per rest — and gfx9's single in-order vmcnt makes each
+// of those loads also wait for every store the chain issued before it (measured: 2.25 us per record,
+// half of it waiting). This path moves every load to the boundary of a 64-record block:
+//
+//   * top-of-book lists: per side the next HT occupied levels from the best, entry i in lane i (level,
+//     total, head / tail chunk, tail fill, the head's next, its LDS row) with each head chunk's 16
+//     slots in an LDS row — rebuilt in vector form (occupancy scan in LDS, one round trip for the
+//     levels, one for their head chunks) when a side runs low; takers walk them as k_match_reg walks
+//     its ladder; a level emptied at the front leaves by a one-lane rotation, a new level inside the
+//     list's span enters at its sorted position by a one-lane shift (DPP wave_rol / wave_shr), so the
+//     list always is the exact prefix of the side's occupied levels;
+//   * deep rests: every record's own level (total, head, tail, tail fill) is loaded in vector form at
+//     the block start and kept current: an update of an unlisted level, and a level leaving a list
+//     (popped or truncated), is broadcast to the lanes of that level;
+//   * the occupancy bitmap lives in LDS (windows up to HOT_MAX_WORDS * 64 levels);
+//   * free chunks in a VGPR stack.
+// Every change is written through to HBM at once (fire-and-forget global stores: nothing in the chain
+// waits for them), so the HBM book is always current: a record the lists do not cover — a cancel, a
+// price outside the window, a taker while far levels exist — runs through generic_record after one full
+// wait, and the lists and lane states are rebuilt behind it. Same semantics and HBM layout as k_match.
+// The chain's state stays in registers (HotState): the generic code's WaveCtx lives in scratch memory
+// and is touched only at those sync points.
+constexpr int HT = 64;                  // list entries per side (one per lane)
+constexpr uint32_t HOT_STACK_LOW = 16;  // top the free-chunk stack up at a block start below this ...
+constexpr uint32_t HOT_STACK_FILL = 32; // ... to this
+
+struct HotLds {
+  int cq[2][HT][ME_C];                 // head chunk of the list entry owning row (side, row): slot quantities ...
+  unsigned long long cs[2][HT][ME_C];  // ... and seqs (side 0 bids, 1 asks)
+  unsigned long long occ[HOT_MAX_WORDS];
+};
+
+struct HSide {  // a top-of-book list: entry i in lane i, levels best first
+  int lvl;
+  long long tot;
+  uint32_t hd, tl, te, hn;
+  uint32_t row;  // the entry's LDS row; lanes >= n hold the free rows (the rows are a permutation)
+  int n;         // wave-uniform
+  bool more;     // wave-uniform: occupied levels of this side may lie beyond the last entry
+};
+
+// One-lane moves of a list (gfx9 DPP wavefront shifts): entries leave at the front, enter anywhere.
+__device__ __forceinline__ uint32_t lanes_down(uint32_t v) {  // lane i <- lane i + 1, lane 63 <- lane 0
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x134, 0xf, 0xf, false);  // wave_rol:1
+}
+__device__ __forceinline__ uint32_t lanes_up(uint32_t v) {  // lane i <- lane i - 1
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);  // wave_shr:1
+}
+__device__ __forceinline__ long long lanes_down64(long long v) {
+  return (long long)(((unsigned long long)lanes_down((uint32_t)((unsigned long long)v >> 32)) << 32) |
+                     lanes_down((uint32_t)v));
+}
+__device__ __forceinline__ long long lanes_up64(long long v) {
+  return (long long)(((unsigned long long)lanes_up((uint32_t)((unsigned long long)v >> 32)) << 32) |
+                     lanes_up((uint32_t)v));
+}
+
+struct HotState {
+  gptr<Chunk> chunks;  // the HBM book (global address space: global_* instructions, never flat_*)
+  gptr<uint32_t> loc;
+  gptr<me_fill> scratch;
+  gptr<Level> lv;
+  gptr<unsigned long long> occ;
+  gptr<uint8_t> tend;
+  gptr<uint32_t> err;
+  unsigned long long rmask;
+  uint32_t nchunks, L, W;
+  uint32_t gs;
+  long long base;
+  int bb, ba;  // best bid / ask, exact (-1 / L: the side is empty)
+  unsigned long long wptr;
+  int resting;
+  uint32_t free_head;  // HBM free list (hot frees only push onto it: a store) ...
+  uint32_t free_next;  // ... and free_head's next (the generic pop reads it instead of loading it)
+  uint32_t nfar0, nfar1;
+  uint32_t fstk, nfs;  // VGPR free-chunk stack: lane i holds entry i, entries [0, nfs)
+  HotLds* H;
+  HSide S0, S1;        // bids, asks
+  // per-record lane state of the current block (lane k = record k): the window level it rests at
+  // (-1: none) and that level's total / head / tail / tail fill, loaded at the block start, kept current
+  int rlvl;
+  long long rtot;
+  uint32_t rhd, rtl, rte;
+#ifdef ME_STAMPS
+  unsigned long long ev[8];   // event counts (stamps build): see HEV_*
+  unsigned long long cyc[8];  // cycles of the hot helpers' parts: see HC_*
+  unsigned long long ct;
+#endif
+};
+#ifdef ME_STAMPS
+enum { HEV_TAKE_REBUILD, HEV_ADVANCE, HEV_TRUNC_ENTRIES, HEV_GAP, HEV_NEWBEST, HEV_APPEND, HEV_DEEP, HEV_POP };
+enum { HC_CHUNK, HC_POP, HC_PARTIAL, HC_APPEND, HC_INSERT, HC_DEEP, HC_RESTHEAD, HC_TAKEHEAD };
+#define HEV(h, e) ((h).ev[e] += 1)
+#define HC_MARK(h) ((h).ct = stamp_now())
+#define HC_ADD(h, i)                          \
+  do {                                        \
+    const unsigned long long n_ = stamp_now(); \
+    (h).cyc[i] += n_ - (h).ct;                \
+    (h).ct = n_;                              \
+  } while (0)
+#else
+#define HEV(h, e) ((void)0)
+#define HC_MARK(h) ((void)0)
+#define HC_ADD(h, i) ((void)0)
+#endif
+
+// The generic code's view (sync points only): hot fields in, run, hot fields out.
+__device__ __forceinline__ void hot_to_wave(const HotState& h, WaveCtx& c) {
+  c.base = h.base;
+  c.bb = h.bb;
+  c.ba = h.ba;
+  c.wptr = h.wptr;
+  c.resting_delta = h.resting;
+  c.free_head = h.free_head;
+  c.free_next = h.free_next;
+  c.nfar0 = h.nfar0;
+  c.nfar1 = h.nfar1;
+}
+__device__ __forceinline__ void wave_to_hot(const WaveCtx& c, HotState& h) {
+  h.base = c.base;
+  h.bb = c.bb;
+  h.ba = c.ba;
+  h.wptr = c.wptr;
+  h.resting = c.resting_delta;
+  h.free_head = c.free_head;
+  h.free_next = rl32(c.free_next, 0);
+  h.nfar0 = c.nfar0;
+  h.nfar1 = c.nfar1;
+}
+
+
+// ---- occupancy (LDS copy, written through to HBM one word at a time)
+__device__ __forceinline__ void hot_occ_load(HotState& h) {
+  for (uint32_t i = (uint32_t)lane_id(); i < h.W; i += 64) h.H->occ[i] = h.occ[i];
+  wave_mem_order();
+}
+__device__ __forceinline__ void hot_occ_set(HotState& h, int lvl, bool on) {
+  const uint32_t w = (uint32_t)lvl >> 6;
+  const unsigned long long bit = 1ull << (lvl & 63);
+  if (lane_id() == 0) {
+    const unsigned long long o = h.H->occ[w];
+    const unsigned long long v = on ? (o | bit) : (o & ~bit);
+    h.H->occ[w] = v;
+    h.occ[w] = v;
+  }
+}
+
+// The r-th (0-based) set bit of w (w has more than r set bits).
+__device__ __forceinline__ uint32_t nth_set(unsigned long long w, uint32_t r) {
+  uint32_t pos = 0;
+#pragma unroll
+  for (uint32_t hsz = 32; hsz >= 1; hsz >>= 1) {
+    const uint32_t c = (uint32_t)__popcll(w & ((1ull << hsz) - 1ull));
+    const bool up = r >= c;
+    r = up ? r - c : r;
+    w = up ? (w >> hsz) : w;
+    pos += up ? hsz : 0u;
+  }
+  return pos;
+}
+
+// Lanes 0..n-1 <- the first (up to) HT occupied levels from `start` going up (K = 1, asks) or down
+// (K = 0, bids), from the LDS occupancy copy. *more: the list filled before the window side ended.
+template <int K>
+__device__ __forceinline__ int hot_scan(const HotState& h, int start, int& out_lvl, bool& more) {
+  const int lane = lane_id();
+  const int W = (int)h.W;
+  out_lvl = -1;
+  more = false;
+  if (start < 0 || start >= (int)h.L) return 0;
+  int found = 0;
+  const int w0 = start >> 6;
+  for (int base = 0;; base += 64) {
+    const int wi = K ? w0 + base + lane : w0 - base - lane;
+    const bool in = wi >= 0 && wi < W;
+    unsigned long long w = in ? h.H->occ[wi] : 0ull;
+    if (wi == w0)  // the start word: only levels at / beyond start
+      w &= K ? (~0ull << (start & 63)) : (~0ull >> (63 - (start & 63)));
+    if (!K) w = __builtin_bitreverse64(w);  // descending: bit 0 = the word's highest level
+    const uint32_t cnt = (uint32_t)__popcll(w);
+    const long long inc = wave_incl_scan((long long)cnt);
+    const uint32_t ex = (uint32_t)(inc - cnt);
+    const uint32_t tot = (uint32_t)rli64(inc, 63);
+    const int i = lane - found;  // output lane i takes bit (i - ex_j) of the lane j holding it
+    int lo = 0;
+#pragma unroll
+    for (int st = 32; st >= 1; st >>= 1) {
+      const uint32_t e = (uint32_t)__shfl((int)ex, min(lo + st, 63), 64);
+      if (lo + st < 64 && (int)e <= i) lo += st;
+    }
+    const unsigned long long wj = (unsigned long long)__shfl((long long)w, lo, 64);
+    const uint32_t r = (uint32_t)(i - __shfl((int)ex, lo, 64));
+    const uint32_t b = nth_set(wj, r);
+    const int wdx = K ? w0 + base + lo : w0 - base - lo;
+    if (i >= 0 && (uint32_t)i < tot) out_lvl = wdx * 64 + (K ? (int)b : 63 - (int)b);
+    found = min(found + (int)tot, HT);
+    const bool end = K ? (w0 + base + 64 >= W) : (w0 - base - 64 < 0);
+    if (found >= HT) {
+      more = true;  // conservative: a later rebuild finds out
+      return HT;
+    }
+    if (end) return found;
+  }
+}
+
+// Rebuild list K from its best level: occupancy scan (LDS), the levels (one round trip) and their head
+// chunks (one round trip) into lanes / LDS slots. The caller has waited for every store.
+template <int K>
+__device__ __forceinline__ void hot_rebuild(HotState& h, HSide& S) {
+  const int lane = lane_id();
+  const int L = (int)h.L;
+  int start = K ? h.ba : h.bb;  // the best (or a bound no level of either side lies between)
+  if (K ? start < 0 : start >= L) start = K ? 0 : L - 1;
+  int lvl;
+  bool more;
+  const int n = hot_scan<K>(h, start, lvl, more);
+  const bool v = lane < n;
+  const int li = v ? lvl : 0;
+  Level x{0, NIL, NIL};
+  uint32_t te = 0;
+  if (v) {
+    x = h.lv[li];
+    te = h.tend[li];
+  }
+  const bool hv = v && x.head < h.nchunks;
+  const gptr<Chunk> ch = h.chunks + (hv ? x.head : 0u);
+  // the head chunk's 16 quantities and seqs: 12 x 16-B loads per lane, all in flight, then into LDS
+  typedef int v4i __attribute__((ext_vector_type(4)));
+  const gptr<const v4i> src = reinterpret_cast<gptr<const v4i>>(ch->qty);  // qty[16] then seq[16]
+  const v4i a0 = src[0], a1 = src[1], a2 = src[2], a3 = src[3], b0 = src[4], b1 = src[5], b2 = src[6],
+            b3 = src[7], b4 = src[8], b5 = src[9], b6 = src[10], b7 = src[11];
+  const uint32_t hn = ch->hdr.next;
+  v4i* dq = reinterpret_cast<v4i*>(h.H->cq[K][lane]);
+  v4i* ds = reinterpret_cast<v4i*>(h.H->cs[K][lane]);
+  dq[0] = a0;
+  dq[1] = a1;
+  dq[2] = a2;
+  dq[3] = a3;
+  ds[0] = b0;
+  ds[1] = b1;
+  ds[2] = b2;
+  ds[3] = b3;
+  ds[4] = b4;
+  ds[5] = b5;
+  ds[6] = b6;
+  ds[7] = b7;
+  S.lvl = v ? lvl : -1;
+  S.tot = v ? x.total : 0;
+  S.hd = v ? x.head : NIL;
+  S.tl = v ? x.tail : NIL;
+  S.te = te;
+  S.hn = hv ? hn : NIL;
+  S.row = (uint32_t)lane;
+  S.n = n;
+  S.more = more;
+  const int b = n ? rli32(lvl, 0) : (K ? L : -1);  // exact best
+  if (K)
+    h.ba = b;
+  else
+    h.bb = b;
+}
+
+// The block's per-record level states, loaded in vector form (lanes with rlvl >= 0).
+__device__ __forceinline__ void hot_prefetch(HotState& h) {
+  const bool v = h.rlvl >= 0;
+  const int li = v ? h.rlvl : 0;
+  Level x{0, NIL, NIL};
+  uint32_t te = 0;
+  if (v) {
+    x = h.lv[li];
+    te = h.tend[li];
+  }
+  h.rtot = x.total;
+  h.rhd = x.head;
+  h.rtl = x.tail;
+  h.rte = te;
+}
+
+__device__ __forceinline__ void hot_drain() {
+  __builtin_amdgcn_s_waitcnt(0);
+  wave_mem_order();
+}
+
+// ---- chunks: VGPR stack
+__device__ __forceinline__ void hot_free(HotState& h, uint32_t ch) {
+  if (ME_LIKELY(h.nfs < (uint32_t)HT)) {
+    h.fstk = lane_id() == (int)h.nfs ? ch : h.fstk;
+    h.nfs += 1;
+  } else {  // onto the symbol's HBM free list: a store (as free_chunk)
+    if (lane_id() == 0) h.chunks[ch].hdr.next = h.free_head;
+    h.free_next = h.free_head;
+    h.free_head = ch;
+  }
+}
+
+// Record the level's header and tail fill in HBM.
+__device__ __forceinline__ void hot_level_store(HotState& h, int lvl, long long tot, uint32_t hd, uint32_t tl,
+                                                uint32_t te) {
+  if (lane_id() == 0) {
+    Level o;
+    o.total = tot;
+    o.head = tot ? hd : NIL;
+    o.tail = tot ? tl : NIL;
+    h.lv[lvl] = o;
+    h.tend[lvl] = (uint8_t)te;
+  }
+}
+
+// New chunk ch holding one order (seq, q) at level lvl, behind tail `prev` (NIL: the level's only chunk).
+__device__ __forceinline__ void hot_new_chunk(HotState& h, uint32_t ch, uint32_t prev, int lvl,
+                                              unsigned long long seq, int q) {
+  if (lane_id() == 0) {
+    ChunkHdr hh;
+    hh.next = NIL;
+    hh.prev = prev;
+    hh.price = h.base + lvl;
+    h.chunks[ch].hdr = hh;
+    h.chunks[ch].qty[0] = q;
+    h.chunks[ch].seq[0] = seq;
+    if (prev != NIL) h.chunks[prev].hdr.next = ch;
+    h.loc[seq & h.rmask] = ch * ME_C;
+  }
+}
+
+// Record lanes of level lvl take its state (a level that leaves a list, or a deep level just changed).
+__device__ __forceinline__ void hot_broadcast(HotState& h, int lvl, long long tot, uint32_t hd, uint32_t tl,
+                                             uint32_t te) {
+  const bool m = h.rlvl == lvl;
+  h.rtot = m ? tot : h.rtot;
+  h.rhd = m ? hd : h.rhd;
+  h.rtl = m ? tl : h.rtl;
+  h.rte = m ? te : h.rte;
+}
+// The last entry of a full list leaves it (a level entering the list takes its place and row).
+__device__ __forceinline__ void hot_drop_last(HotState& h, HSide& S) {
+  HEV(h, HEV_TRUNC_ENTRIES);
+  const int j = S.n - 1;
+  hot_broadcast(h, rli32(S.lvl, j), rli64(S.tot, j), rl32(S.hd, j), rl32(S.tl, j), rl32(S.te, j));
+  S.n -= 1;
+  S.more = true;
+}
+
+// Take up to rem from list K's front levels while they cross lim (K = 1: asks for a BUY).
+template <int K>
+__device__ __forceinline__ void hot_take(HotState& h, HSide& S, int lim, uint32_t& rem, unsigned long long taker) {
+  const int lane = lane_id();
+  const bool act = lane < ME_C;
+  const int sl = lane & (ME_C - 1);
+  HC_MARK(h);
+  while (rem) {
+    if (!S.n) return;  // the side is empty (a list runs dry only with it)
+    const int lvl = rli32(S.lvl, 0);
+    if (K ? lvl > lim : lvl < lim) return;
+    uint32_t hd = rl32(S.hd, 0);
+    const uint32_t tl = rl32(S.tl, 0);
+    const uint32_t r = rl32(S.row, 0);
+    long long tot = rli64(S.tot, 0);
+    const long long price = h.base + lvl;
+    uint32_t taken = 0;
+    HC_ADD(h, HC_TAKEHEAD);
+    if (ME_UNLIKELY(hd >= h.nchunks)) {  // a corrupt list entry: never index with it
+      if (lane == 0) atomicOr(h.err, ERR_INCONSISTENT);
+      rem = 0;
+      return;
+    }
+    for (;;) {  // the level's chunks, head first
+      const int q_ = h.H->cq[K][r][sl];
+      const unsigned long long mseq = vreg64(h.H->cs[K][r][sl]);
+      const uint32_t uq = act ? (uint32_t)q_ : 0u;
+      const uint32_t inc = scan16_sat(uq);
+      const uint32_t ex = inc - uq;
+      uint32_t fq = rem > ex ? rem - ex : 0u;
+      fq = fq < uq ? fq : uq;
+      const bool fe = fq != 0u;
+      const unsigned long long fm = __ballot(fe);
+      if (fe) {
+        me_fill F;
+        F.taker_seq = taker;
+        F.maker_seq = mseq;
+        F.price_q4 = price;
+        F.qty = (int)fq;
+        F.symbol = h.gs;
+        h.scratch[h.wptr + (unsigned long long)__builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u)] = F;
+        h.H->cq[K][r][sl] = (int)(uq - fq);
+        h.chunks[hd].qty[sl] = (int)(uq - fq);
+      }
+      h.wptr += (unsigned long long)__popcll(fm);
+      h.resting -= __popcll(__ballot(fq == uq) & fm);
+      const uint32_t live = rl32(inc, 15);
+      const uint32_t t = rem < live ? rem : live;
+      rem -= t;
+      taken += t;
+      if (__ballot(uq > fq) & 0xFFFFull) break;  // live slots remain: the taker is done
+      // the chunk is exhausted (its HBM slots read 0 already): free it, go on down the FIFO
+      hot_free(h, hd);
+      if (hd == tl) break;
+      const uint32_t nx = rl32(S.hn, 0);
+      if (ME_UNLIKELY(nx >= h.nchunks)) {  // a corrupt FIFO: stop the taker, report it
+        if (lane == 0) atomicOr(h.err, ERR_INCONSISTENT);
+        rem = 0;
+        return;
+      }
+      // the next chunk of a multi-chunk level: the one load of a walk (the chain's own stores to it
+      // land first)
+      HEV(h, HEV_ADVANCE);
+      hot_drain();
+      const int nq = h.chunks[nx].qty[sl];
+      const unsigned long long ns = h.chunks[nx].seq[sl];
+      const uint32_t nn = h.chunks[nx].hdr.next;
+      __builtin_amdgcn_s_waitcnt(0);
+      if (act) {
+        h.H->cq[K][r][sl] = nq;
+        h.H->cs[K][r][sl] = ns;
+      }
+      if (lane == 0) h.chunks[nx].hdr.prev = NIL;
+      hd = nx;
+      S.hd = lane == 0 ? nx : S.hd;
+      S.hn = lane == 0 ? rl32(nn, 0) : S.hn;
+      if (!rem) break;
+    }
+    tot -= taken;
+    HC_ADD(h, HC_CHUNK);
+    if (tot == 0) {  // the level emptied: pop it (record lanes of it learn: a later rest may find it deep)
+      HEV(h, HEV_POP);
+      hot_level_store(h, lvl, 0, NIL, NIL, 0);
+      hot_occ_set(h, lvl, false);
+      hot_broadcast(h, lvl, 0, NIL, NIL, 0);
+      // every entry one lane down; the front's row goes to lane 63 (free)
+      S.lvl = (int)lanes_down((uint32_t)S.lvl);
+      S.tot = lanes_down64(S.tot);
+      S.hd = lanes_down(S.hd);
+      S.tl = lanes_down(S.tl);
+      S.te = lanes_down(S.te);
+      S.hn = lanes_down(S.hn);
+      S.row = lanes_down(S.row);
+      S.n -= 1;
+      if (!S.n && S.more) {
+        // the list ran dry with levels beyond it: rebuild it now, so that an empty list always means
+        // an empty side and the best levels stay exact (a scan from a mere bound would run into the
+        // other side's levels: the occupancy bitmap holds both)
+        if (K)
+          h.ba = lvl + 1;
+        else
+          h.bb = lvl - 1;
+        HEV(h, HEV_TAKE_REBUILD);
+        hot_drain();
+        hot_rebuild<K>(h, S);
+        __builtin_amdgcn_s_waitcnt(0);
+        continue;
+      }
+      const int nb = S.n ? rli32(S.lvl, 0) : (K ? (int)h.L : -1);
+      if (K)
+        h.ba = nb;
+      else
+        h.bb = nb;
+      HC_ADD(h, HC_POP);
+      continue;
+    }
+    S.tot = lane == 0 ? tot : S.tot;
+    hot_level_store(h, lvl, tot, hd, tl, rl32(S.te, 0));
+    HC_ADD(h, HC_PARTIAL);
+    return;
+  }
+}
+
+// Rest (seq, q) at window level lvl on side K (0 bids, 1 asks); record lane kr holds the level's state.
+// False: the chunk stack ran dry (nothing changed).
+template <int K>
+__device__ __forceinline__ bool hot_rest(HotState& h, HSide& S, int lvl, unsigned long long seq, int q, int kr) {
+  const int lane = lane_id();
+  HC_MARK(h);
+  const bool ent = lane < S.n;
+  const int p = __popcll(__ballot(ent && (K ? S.lvl < lvl : S.lvl > lvl)));  // entries better than lvl
+  HC_ADD(h, HC_RESTHEAD);
+  if (p < S.n && rli32(S.lvl, p) == lvl) {  // a listed level: append
+    HEV(h, HEV_APPEND);
+    const int j = p;
+    const uint32_t te = rl32(S.te, j), tl = rl32(S.tl, j), hd = rl32(S.hd, j);
+    const long long tot = rli64(S.tot, j) + q;
+    uint32_t ntl = tl, nte = te + 1;
+    if (ME_UNLIKELY(tl >= h.nchunks)) {
+      if (lane == 0) atomicOr(h.err, ERR_INCONSISTENT);
+      return true;
+    }
+    if (te < (uint32_t)ME_C) {
+      if (tl == hd) {
+        const uint32_t r = rl32(S.row, j);
+        if (lane == 0) {
+          h.H->cq[K][r][te] = q;
+          h.H->cs[K][r][te] = seq;
+        }
+      }
+      if (lane == 0) {
+        h.chunks[tl].qty[te] = q;
+        h.chunks[tl].seq[te] = seq;
+        h.loc[seq & h.rmask] = tl * ME_C + te;
+      }
+    } else {
+      if (ME_UNLIKELY(!h.nfs)) return false;
+      h.nfs -= 1;
+      const uint32_t ch = rl32(h.fstk, (int)h.nfs);
+      hot_new_chunk(h, ch, tl, lvl, seq, q);
+      if (tl == hd) S.hn = lane == j ? ch : S.hn;
+      ntl = ch;
+      nte = 1;
+    }
+    hot_level_store(h, lvl, tot, hd, ntl, nte);
+    S.tot = lane == j ? tot : S.tot;
+    S.tl = lane == j ? ntl : S.tl;
+    S.te = lane == j ? nte : S.te;
+    h.resting += 1;
+    HC_ADD(h, HC_APPEND);
+    return true;
+  }
+  if (p < S.n || (!S.more && p < HT)) {
+    // an empty level inside the list's span (or past its end when nothing lies beyond): it enters
+    // at position p, the entries behind it move one lane up (a full list drops its last entry)
+    if (p == 0)
+      HEV(h, HEV_NEWBEST);
+    else
+      HEV(h, HEV_GAP);
+    if (ME_UNLIKELY(!h.nfs)) return false;  // the block start keeps the stack topped up
+    if (S.n == HT) hot_drop_last(h, S);
+    h.nfs -= 1;
+    const uint32_t ch = rl32(h.fstk, (int)h.nfs);
+    hot_new_chunk(h, ch, NIL, lvl, seq, q);
+    hot_level_store(h, lvl, q, ch, ch, 1);
+    hot_occ_set(h, lvl, true);
+    const uint32_t r = rl32(S.row, HT - 1);  // a free row (S.n < HT)
+    const bool up = lane > p, at = lane == p;
+    const int ulvl = (int)lanes_up((uint32_t)S.lvl);
+    const long long utot = lanes_up64(S.tot);
+    const uint32_t uhd = lanes_up(S.hd), utl = lanes_up(S.tl), ute = lanes_up(S.te), uhn = lanes_up(S.hn),
+                   urow = lanes_up(S.row);
+    S.lvl = up ? ulvl : (at ? lvl : S.lvl);
+    S.tot = up ? utot : (at ? (long long)q : S.tot);
+    S.hd = up ? uhd : (at ? ch : S.hd);
+    S.tl = up ? utl : (at ? ch : S.tl);
+    S.te = up ? ute : (at ? 1u : S.te);
+    S.hn = up ? uhn : (at ? NIL : S.hn);
+    S.row = up ? urow : (at ? r : S.row);
+    if (lane < ME_C) {
+      h.H->cq[K][r][lane] = lane == 0 ? q : 0;
+      h.H->cs[K][r][lane] = lane == 0 ? seq : 0ull;
+    }
+    S.n += 1;
+    if (p == 0) {
+      if (K)
+        h.ba = lvl;
+      else
+        h.bb = lvl;
+    }
+    hot_broadcast(h, lvl, q, ch, ch, 1);
+    h.resting += 1;
+    HC_ADD(h, HC_INSERT);
+    return true;
+  }
+  // deep (beyond the list's last entry, with unlisted levels there): the record lane's level state
+  HEV(h, HEV_DEEP);
+  const long long tot0 = rli64(h.rtot, kr);
+  const uint32_t hd0 = rl32(h.rhd, kr), tl0 = rl32(h.rtl, kr), te0 = rl32(h.rte, kr);
+  const long long tot = tot0 + q;
+  uint32_t hd = hd0, tl = tl0, te = te0 + 1;
+  if (ME_UNLIKELY(tot0 != 0 && tl0 >= h.nchunks)) {
+    if (lane == 0) atomicOr(h.err, ERR_INCONSISTENT);
+    return true;
+  }
+  if (tot0 == 0 || te0 >= (uint32_t)ME_C) {
+    if (ME_UNLIKELY(!h.nfs)) return false;
+    h.nfs -= 1;
+    const uint32_t ch = rl32(h.fstk, (int)h.nfs);
+    hot_new_chunk(h, ch, tot0 ? tl0 : NIL, lvl, seq, q);
+    if (!tot0) {
+      hd = ch;
+      hot_occ_set(h, lvl, true);
+    }
+    tl = ch;
+    te = 1;
+  } else if (lane == 0) {
+    h.chunks[tl0].qty[te0] = q;
+    h.chunks[tl0].seq[te0] = seq;
+    h.loc[seq & h.rmask] = tl0 * ME_C + te0;
+  }
+  hot_level_store(h, lvl, tot, hd, tl, te);
+  hot_broadcast(h, lvl, tot, hd, tl, te);
+  h.resting += 1;
+  HC_ADD(h, HC_DEEP);
+  return true;
+}
+
+// The generic code out of line: the hot loop's registers do not pay for it (its WaveCtx lives in
+// scratch memory anyway, since the generic helpers take its address).
+__device__ __noinline__ RecOut hot_generic_record(WaveCtx* c, unsigned long long seq, long long px, int q,
+                                                  uint32_t kind) {
+  return generic_record(*c, seq, px, q, kind);
+}
+__device__ __noinline__ uint32_t hot_alloc_slow(WaveCtx* c) { return alloc_chunk(*c); }
+__device__ __noinline__ void hot_free_slow(WaveCtx* c, uint32_t ch) { free_chunk(*c, ch); }
+
+// The generic path for record k (or the stack top-up) at a sync point: every store landed, the
+// WaveCtx takes the hot state, the generic code runs, the hot state and both lists come back.
+__device__ __forceinline__ void hot_sync_in(HotState& h, WaveCtx& c) {
+  hot_drain();
+  hot_to_wave(h, c);  // the best levels are exact (an empty list means an empty side)
+}
+__device__ __forceinline__ void hot_sync_out(HotState& h, const WaveCtx& c) {
+  wave_to_hot(c, h);
+  hot_drain();
+  hot_occ_load(h);
+  hot_rebuild<0>(h, h.S0);
+  hot_rebuild<1>(h, h.S1);
+}
+__device__ __forceinline__ void hot_topup(HotState& h, WaveCtx& c) {
+  hot_sync_in(h, c);
+  while (h.nfs < HOT_STACK_FILL) {
+    const uint32_t ch = hot_alloc_slow(&c);
+    if (ch == NIL) break;
+    h.fstk = lane_id() == (int)h.nfs ? ch : h.fstk;
+    h.nfs += 1;
+  }
+  wave_to_hot(c, h);
+}
+
+#ifdef ME_HOT_CHECK
+// Diagnostic build only (make hotcheck): after every record, the lists, record-lane states and LDS
+// copies against the HBM book; the first mismatch is printed and stops the wave (ERR_INCONSISTENT).
+template <int K>
+__device__ bool hot_check_side(HotState& h, const HSide& S, unsigned long long seq, int what) {
+  const int lane = lane_id();
+  const bool ent = lane < S.n;
+  bool bad = false;
+  int code = 0;
+  long long a0 = 0, a1 = 0;
+  if (ent) {
+    const int l = S.lvl;
+    if (l < 0 || l >= (int)h.L) {
+      bad = true, code = 1, a0 = l;
+    } else {
+      const Level x = h.lv[l];
+      const uint32_t te = h.tend[l];
+      const bool occ = (h.occ[l >> 6] >> (l & 63)) & 1ull;
+      const bool locc = (h.H->occ[l >> 6] >> (l & 63)) & 1ull;
+      if (x.total != S.tot || x.total <= 0) bad = true, code = 2, a0 = x.total, a1 = S.tot;
+      else if (x.head != S.hd) bad = true, code = 3, a0 = x.head, a1 = S.hd;
+      else if (x.tail != S.tl) bad = true, code = 4, a0 = x.tail, a1 = S.tl;
+      else if (te != S.te) bad = true, code = 5, a0 = te, a1 = S.te;
+      else if (!occ || !locc) bad = true, code = 6, a0 = occ, a1 = locc;
+      else if (S.hd >= h.nchunks || S.tl >= h.nchunks) bad = true, code = 7, a0 = S.hd, a1 = S.tl;
+      else {
+        const Chunk& C = h.chunks[S.hd];
+        if (C.hdr.next != (S.hd == S.tl ? NIL : S.hn)) bad = true, code = 8, a0 = C.hdr.next, a1 = S.hn;
+        else if (C.hdr.price != h.base + l) bad = true, code = 9, a0 = C.hdr.price, a1 = h.base + l;
+        else {
+          for (int j = 0; j < ME_C; ++j) {
+            if (C.qty[j] != h.H->cq[K][S.row][j]) {
+              bad = true, code = 10, a0 = C.qty[j], a1 = h.H->cq[K][S.row][j];
+              break;
+            }
+            if (C.qty[j] > 0 && C.seq[j] != h.H->cs[K][S.row][j]) {
+              bad = true, code = 11, a0 = (long long)C.seq[j], a1 = (long long)h.H->cs[K][S.row][j];
+              break;
+            }
+          }
+        }
+      }
+    }
+  }
+  // the entries are the first n occupied levels from the best, in order
+  int sl;
+  bool more;
+  const int best = K ? h.ba : h.bb;
+  const int n2 = hot_scan<K>(h, K ? (best < 0 ? 0 : best) : (best >= (int)h.L ? (int)h.L - 1 : best), sl, more);
+  if (!bad && S.n > n2) bad = true, code = 12, a0 = S.n, a1 = n2;
+  if (!bad && S.n && rli32(S.lvl, 0) != best) bad = true, code = 13, a0 = rli32(S.lvl, 0), a1 = best;
+  if (!bad && !S.n && best != (K ? (int)h.L : -1)) bad = true, code = 16, a0 = best;
+  {  // the rows are a permutation of 0..63
+    unsigned long long seen = 0;
+    for (int i = 0; i < HT; ++i) seen |= 1ull << (rl32(S.row, i) & 63u);
+    if (!bad && (seen != ~0ull || S.row >= (uint32_t)HT)) bad = true, code = 17, a0 = (long long)seen, a1 = S.row;
+  }
+  if (!bad && !S.n && !S.more && n2) {
+    const int f0 = rli32(sl, 0);
+    bad = true, code = 14, a0 = f0, a1 = h.lv[f0].total;
+  }
+  {
+    if (!bad && lane < S.n && S.lvl != sl) bad = true, code = 15, a0 = S.lvl, a1 = sl;
+  }
+  const unsigned long long bm = __ballot(bad);
+  if (!bm) return true;
+  const int j = __builtin_ctzll(bm);
+  if (lane == j)
+    printf("HOTCHECK s=%u side=%d what=%d seq=%llu lane=%d code=%d a0=%lld a1=%lld n=%d row=%u more=%d lvl=%d best=%d\n", h.gs, K,
+           what, seq, lane, code, a0, a1, S.n, S.row, (int)S.more, S.lvl, best);
+  return false;
+}
+__device__ bool hot_check_lists(HotState& h, unsigned long long seq, int what);
+__device__ bool hot_check(HotState& h, unsigned long long seq, int what, uint32_t kd = 0, int lm = 0, int q = 0,
+                          int rem = 0) {
+  hot_drain();
+  if (!hot_check_lists(h, seq, what)) {
+    if (lane_id() == 0)
+      printf("HOTCHECK after record s=%u seq=%llu kind=%u lm=%d q=%d rem=%d bb=%d ba=%d n0=%d n1=%d\n", h.gs, seq, kd, lm, q,
+             rem, h.bb, h.ba, h.S0.n, h.S1.n);
+    return false;
+  }
+  return true;
+}
+__device__ bool hot_check_lists(HotState& h, unsigned long long seq, int what) {
+  if (!hot_check_side<0>(h, h.S0, seq, what) || !hot_check_side<1>(h, h.S1, seq, what)) return false;
+  const int lane = lane_id();
+  bool bad = false;
+  for (uint32_t i = (uint32_t)lane; i < h.W; i += 64)
+    if (h.occ[i] != h.H->occ[i]) bad = true;
+  if (__ballot(bad)) {
+    if (lane == 0) printf("HOTCHECK occ copy differs what=%d seq=%llu\n", what, seq);
+    return false;
+  }
+  // record lanes of unlisted levels hold their HBM state
+  const int l = h.rlvl;
+  bool listed = false;
+  for (int i = 0; i < h.S0.n; ++i) listed |= rli32(h.S0.lvl, i) == l;
+  for (int i = 0; i < h.S1.n; ++i) listed |= rli32(h.S1.lvl, i) == l;
+  if (l >= 0 && !listed) {
+    const Level x = h.lv[l];
+    const uint32_t te = h.tend[l];
+    if (x.total != h.rtot || (x.total && (x.head != h.rhd || x.tail != h.rtl || te != h.rte))) bad = true;
+  }
+  const unsigned long long bm = __ballot(bad);
+  if (bm) {
+    if (lane == __builtin_ctzll(bm))
+      printf("HOTCHECK record lane %d lvl=%d what=%d seq=%llu rtot=%lld tot=%lld\n", lane, l, what, seq, h.rtot,
+             h.lv[l].total);
+    return false;
+  }
+  if (h.nfs > (uint32_t)HT || (lane < (int)h.nfs && h.fstk >= h.nchunks)) {
+    if (lane == 0) printf("HOTCHECK stack what=%d\n", what);
+    return false;
+  }
+  return true;
+}
+#define HOT_CHECK(what, seq_, ...)                                     \
+  if (!hot_check(h, (seq_), (what), ##__VA_ARGS__)) {                  \
+    if (lane == 0) atomicOr(h.err, ERR_INCONSISTENT);                  \
+    ok = false;                                                        \
+    break;                                                             \
+  }
+#else
+#define HOT_CHECK(what, seq_, ...)
+#endif
+
+// Diagnostic stamps of the hot loop (-DME_STAMPS): cycles in registers, into the WaveCtx at the end
+// (fetch: block starts; sweep: takes; rest: rests; cancel: generic records; result: results).
+#ifdef ME_STAMPS
+#define HS_DECL unsigned long long hs_[PH_N] = {}, hst_ = stamp_now()
+#define HS(ph)                          \
+  do {                                  \
+    const unsigned long long n_ = stamp_now(); \
+    hs_[ph] += n_ - hst_;               \
+    hst_ = n_;                          \
+  } while (0)
+#define HS_COUNT(ct) (hs_[ct] += 1)
+#define HS_FLUSH(c)                                    \
+  for (int p_ = 0; p_ < PH_N; ++p_) (c).st[p_] += hs_[p_]; \
+  for (int e_ = 0; e_ < 4; ++e_) (c).st[PH_SW_WINDOW + e_] += h.cyc[e_]; \
+  for (int e_ = 0; e_ < 4; ++e_) (c).st[WK_GET + e_] += h.cyc[4 + e_]
+#else
+#define HS_DECL
+#define HS(ph) ((void)0)
+#define HS_COUNT(ct) ((void)0)
+#define HS_FLUSH(c) ((void)0)
+#endif
+
+// Records [lo, hi) of the hot symbol in seq order, blocks of 64.
+__device__ __forceinline__ void match_records_hot(HotState& h, WaveCtx& c, const BatchDev& bt, uint32_t lo,
+                                                  uint32_t hi) {
+  const int lane = lane_id();
+  HS_DECL;
+#ifdef ME_STAMPS
+  for (int e_ = 0; e_ < 8; ++e_) h.ev[e_] = h.cyc[e_] = 0;
+#endif
+  const uint32_t Lw = h.L;
+  h.nfs = 0;
+  h.fstk = NIL;
+  h.rlvl = -1;
+  hot_occ_load(h);
+  hot_rebuild<0>(h, h.S0);
+  hot_rebuild<1>(h, h.S1);
+  bool ok = true;
+  for (uint32_t blk = lo; blk < hi && ok; blk += 64) {
+    c.recs_left = hi - blk;
+    HS(PH_RESULT);
+    if (h.nfs < HOT_STACK_LOW) {
+      hot_topup(h, c);
+      HS_COUNT(CT_WALK);
+    }
+    const uint32_t j = blk + (uint32_t)lane;
+    const bool v = j < hi;
+    const uint32_t oi = v ? bt.perm[j] : 0u;
+    const unsigned long long oseq = v ? bt.seq[oi] : 0ull;
+    const long long opx = v ? bt.px[oi] : 0ll;
+    const int oq = v ? bt.qty[oi] : 0;
+    const uint32_t okd = v ? (uint32_t)bt.kind[oi] : 0u;
+    const uint32_t cnt = min(64u, hi - blk);
+    const uint32_t side = okd & 3u;
+    const bool market = (okd >> 2) & 1u, cancel = (okd >> 3) & 1u;
+    const bool good = v && !cancel && oq > 0 && (side == ME_SIDE_BUY || side == ME_SIDE_SELL) && oseq != 0ull;
+    // which records the lists take (vector form; again after a generic record moved the window):
+    // cancels, LIMITs outside the window and takers while the side they cross has far levels are generic
+    unsigned long long slowm, fastm;
+    auto classify = [&]() {
+      const unsigned long long off = (unsigned long long)opx - (unsigned long long)h.base;
+      const bool inw = off < (unsigned long long)Lw;
+      const bool farx = (side == ME_SIDE_BUY ? h.nfar1 : h.nfar0) != 0u;
+      const bool fast = good && (market || inw) && !farx;
+      h.rlvl = fast && !market ? (int)off : -1;
+      fastm = __ballot(fast);
+      slowm = __ballot(v && !fast);
+    };
+    classify();
+    if (h.S0.n < HT / 2 && h.S0.more) {
+      hot_drain();
+      hot_rebuild<0>(h, h.S0);
+      HS_COUNT(CT_MISS);
+    }
+    if (h.S1.n < HT / 2 && h.S1.more) {
+      hot_drain();
+      hot_rebuild<1>(h, h.S1);
+      HS_COUNT(CT_MISS);
+    }
+    hot_prefetch(h);
+    __builtin_amdgcn_s_waitcnt(0);
+    HOT_CHECK(0, 0ull);
+    HS(PH_FETCH);
+    ResultLanes R;
+    R.filled = R.remaining = 0;
+    R.nfill = R.fstart = R.st = 0;
+    uint32_t k = 0;
+    for (; k < cnt; ++k) {
+      const unsigned long long seq = rl64(oseq, (int)k);
+      const int q = rli32(oq, (int)k);
+      const uint32_t kd = rl32(okd, (int)k);
+      if (ME_UNLIKELY(!((fastm >> k) & 1ull))) {  // generic (or a reject) at a sync point
+        HS_COUNT(CT_EVICT);
+        c.recs_left = hi - (blk + k);
+        hot_sync_in(h, c);
+        const RecOut o = hot_generic_record(&c, seq, rli64(opx, (int)k), q, kd);
+        if (!o.ok) {
+          ok = false;
+          break;
+        }
+        put_rec(R, k, o);
+        hot_sync_out(h, c);
+        classify();
+        fastm &= ~((2ull << k) - 1ull);
+        hot_prefetch(h);
+        __builtin_amdgcn_s_waitcnt(0);
+        HOT_CHECK(2, seq);
+        HS(PH_CANCEL);
+        continue;
+      }
+      const bool buy = (kd & 3u) == ME_SIDE_BUY;
+      const bool mkt = (kd >> 2) & 1u;
+      const int lm = mkt ? (buy ? (int)Lw - 1 : 0) : rli32(h.rlvl, (int)k);
+      const unsigned long long fstart = h.wptr;
+      uint32_t rem = (uint32_t)q;
+      HS_COUNT(CT_FAST);
+      if (buy)
+        hot_take<1>(h, h.S1, lm, rem, seq);
+      else
+        hot_take<0>(h, h.S0, lm, rem, seq);
+      HS(PH_SWEEP);
+      const int filled = q - (int)rem;
+      const uint32_t nfill = (uint32_t)(h.wptr - fstart);
+      uint8_t stt;
+      if (mkt) {
+        stt = rem == 0 ? ME_ST_FILLED : ME_ST_CANCELED;
+      } else {
+        if (rem) {
+          const bool rested = buy ? hot_rest<0>(h, h.S0, lm, seq, (int)rem, (int)k)
+                                  : hot_rest<1>(h, h.S1, lm, seq, (int)rem, (int)k);
+          if (ME_UNLIKELY(!rested)) {  // the stack ran dry: top it up and rest again
+            hot_topup(h, c);
+            hot_sync_out(h, c);
+            hot_prefetch(h);
+            __builtin_amdgcn_s_waitcnt(0);
+            const bool again = buy ? hot_rest<0>(h, h.S0, lm, seq, (int)rem, (int)k)
+                                   : hot_rest<1>(h, h.S1, lm, seq, (int)rem, (int)k);
+            if (!again) {  // the chunk pool is exhausted (sticky error word from alloc_chunk)
+              ok = false;
+              break;
+            }
+          }
+        }
+        stt = rem == 0 ? ME_ST_FILLED : (filled > 0 ? ME_ST_PARTIALLY_FILLED : ME_ST_NEW);
+      }
+      HS(PH_REST);
+      put_result(R, k, filled, (int)rem, nfill, stt, ME_RJ_NONE, fstart);
+      HOT_CHECK(1, seq, kd, lm, q, (int)rem);
+    }
+    store_results(bt, R, v && (uint32_t)lane < k, oi);
+  }
+  HS(PH_RESULT);
+  HS_FLUSH(c);
+  // the generic state for wave_end: exact best levels, the stack's chunks back onto the free list
+  hot_sync_in(h, c);
+  while (h.nfs) {
+    h.nfs -= 1;
+    hot_free_slow(&c, rl32(h.fstk, (int)h.nfs));
+  }
+  while (c.bump_cur < c.bump_end) hot_free_slow(&c, c.bump_cur++);
+}
+
+// One wave per hot symbol of the launch (k_match handed them over: bk.hand[i] = {s, pos = lo, nsg = hi}).
+__global__ __launch_bounds__(64) void k_match_hot(BookDev bk, BatchDev bt) {
+  __shared__ HotLds H;
+  const uint32_t nh = min(*(volatile uint32_t*)bk.hcount, bk.S);
+  for (uint32_t i = blockIdx.x; i < nh; i += gridDim.x) {
+    const Handoff ho = bk.hand[i];
+    const uint32_t s = rl32(ho.s, 0), lo = rl32(ho.pos, 0), hi = rl32(ho.nsg, 0);
+    WaveCtx c;
+#ifdef ME_STAMPS
+    for (int p = 0; p < PH_N; ++p) c.st[p] = 0;
+    STAMP_MARK(c);
+#endif
+    c.lad.L = bk.L;
+    c.lad.Lwords = bk.Lwords;
+    c.lad.lv = bk.levels + (size_t)s * bk.L;
+    c.lad.occ = bk.occ + (size_t)s * bk.Lwords;
+    c.lad.tend = bk.tend + (size_t)s * bk.L;
+    c.cache = nullptr;
+    c.cmask = 0;
+    if (!wave_begin(c, bk, bt, s, lo, hi)) return;
+    HotState h;
+    h.chunks = (gptr<Chunk>)vptr(bk.chunks);
+    h.loc = (gptr<uint32_t>)vptr(bk.loc);
+    h.scratch = (gptr<me_fill>)vptr(bt.scratch);
+    h.lv = (gptr<Level>)vptr(c.lad.lv);
+    h.occ = (gptr<unsigned long long>)vptr(c.lad.occ);
+    h.tend = (gptr<uint8_t>)vptr(c.lad.tend);
+    h.err = (gptr<uint32_t>)vptr(bk.err);
+    h.rmask = bk.ring_mask;
+    h.nchunks = bk.nchunks;
+    h.L = bk.L;
+    h.W = bk.Lwords;
+    h.gs = c.gs;
+    h.H = &H;
+    wave_to_hot(c, h);
+    match_records_hot(h, c, bt, lo, hi);
+    wave_end(c);
+  }
+}
 // ---- seq ring horizon ---------------------------------------------------------
 // Runs before every match launch. The ring holds loc[seq & (R - 1)]; a rest of seq y overwrites the
 // entry of y - R. Every live order at or above the horizon has its entry, every older live order is
@@ -1433,8 +2428,11 @@ hipError_t launch_match(hipStream_t st, const BookDev& bk, const BatchDev& bt, h
     return launch_match_reg(st, bk, &bt, 1u, AuxDev{}, ev0, ev1);
   } else if (bk.L <= LDS_MAX_LEVELS) {
     hipExtLaunchKernelGGL(k_match<LAD_LDS>, grid, block, 4 * lds_wave_bytes(bk.L), st, ev0, ev1, 0, bk, bt);
-  } else {
+  } else if (!bk.hot_min) {
     hipExtLaunchKernelGGL(k_match<LAD_HBM>, grid, block, 0, st, ev0, ev1, 0, bk, bt);
+  } else {  // hot symbols go on to k_match_hot (a few one-wave workgroups; hcount zeroed by k_seq_sweep)
+    hipExtLaunchKernelGGL(k_match<LAD_HBM>, grid, block, 0, st, ev0, nullptr, 0, bk, bt);
+    hipExtLaunchKernelGGL(k_match_hot, dim3(64), dim3(64), 0, st, nullptr, ev1, 0, bk, bt);
   }
   return hipGetLastError();
 }

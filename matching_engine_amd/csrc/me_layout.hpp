@@ -180,6 +180,8 @@ struct BookDev {
   uint32_t S;
   uint32_t L;
   uint32_t Lwords;
+  uint32_t hot_min;       // deep windows: a symbol with at least this many records in a batch is matched
+                          // by k_match_hot (me_kernels.hip) instead of k_match; 0 = never
 };
 
 // Far array of (symbol s, side k): k = 0 bids below the window, 1 asks above it.

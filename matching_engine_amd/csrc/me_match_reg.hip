@@ -40,9 +40,6 @@
 namespace me {
 
 constexpr int RL = 128;  // levels covered by this kernel
-// Block placement: rare paths out of line, so the common path runs without taken branches.
-#define ME_LIKELY(x) __builtin_expect(!!(x), 1)
-#define ME_UNLIKELY(x) __builtin_expect(!!(x), 0)
 constexpr int FSTK = 64; // free chunk ids a wave keeps in its VGPR stack (= fcache row length)
 // Head-row flag: set unless cache entry l holds level l's head chunk (chunk ids stay below 2^31;
 // NIL, an empty level, reads as not cached).
@@ -175,22 +172,6 @@ __device__ __forceinline__ void ldsw(uint32_t& f, uint32_t v) {
   if (lane_id() == 0) __hip_atomic_store(&f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// Keep a wave-uniform value in VGPRs: the empty asm makes it opaque (hence "divergent") to the
-// compiler, so it never takes an SGPR. For pointers and constants that only feed vector memory
-// operations and vector arithmetic.
-__device__ __forceinline__ uint32_t vreg(uint32_t x) {
-  asm volatile("" : "+v"(x));
-  return x;
-}
-__device__ __forceinline__ unsigned long long vreg64(unsigned long long x) {
-  uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
-  asm volatile("" : "+v"(lo), "+v"(hi));
-  return ((unsigned long long)hi << 32) | lo;
-}
-template <class T>
-__device__ __forceinline__ gptr<T> vptr(T* p) {
-  return (gptr<T>)vreg64((unsigned long long)p);
-}
 
 struct RegCtx {
   gptr<Chunk> chunks;    // VGPR

@@ -71,6 +71,28 @@ template <class T>
 using gptr = T*;
 #endif
 
+// Block placement: rare paths out of line, so the common path runs without taken branches.
+#define ME_LIKELY(x) __builtin_expect(!!(x), 1)
+#define ME_UNLIKELY(x) __builtin_expect(!!(x), 0)
+
+// Keep a wave-uniform value in VGPRs: the empty asm makes it opaque (hence "divergent") to the
+// compiler, so it never takes an SGPR. For pointers and constants that only feed vector memory
+// operations and vector arithmetic.
+__device__ __forceinline__ uint32_t vreg(uint32_t x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+__device__ __forceinline__ unsigned long long vreg64(unsigned long long x) {
+  uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  asm volatile("" : "+v"(lo), "+v"(hi));
+  return ((unsigned long long)hi << 32) | lo;
+}
+
+template <class T>
+__device__ __forceinline__ gptr<T> vptr(T* p) {
+  return (gptr<T>)vreg64((unsigned long long)p);
+}
+
 // Orders the wave's own global stores before its later loads of the same lines (another lane
 // may read what this lane wrote). Same-CU ordering: no cache maintenance, a compiler barrier.
 __device__ __forceinline__ void wave_mem_order() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup"); }

@@ -1,0 +1,133 @@
+"""k_match_hot — the write-through top-of-book path for hot symbols of deep windows (L > 1,024,
+me_kernels.hip) — against the CPU oracle, bit-exact per batch. ME_HOT_MIN (read at me_create) sets the
+records per batch that make a symbol hot; 1 sends every symbol through it, so the generic fallbacks
+(cancels, prices outside the window, far levels, re-centring) run inside the hot path too."""
+import os
+
+import numpy as np
+import pytest
+
+from tests._parity import assert_books_equal, assert_fills_equal, assert_results_equal
+
+
+def run_both(eng, ob, batches, ctx=""):
+    """run_both of tests/_parity.py, naming the batch an engine error came from."""
+    total = 0
+    for k, b in enumerate(batches):
+        try:
+            rg, fg = eng.submit_batch(b)
+        except Exception as ex:
+            raise AssertionError(f"{ctx}: batch {k}: {ex}") from ex
+        ro, fo = ob.submit(b)
+        assert_results_equal(rg, ro, f"{ctx} batch {k}")
+        assert_fills_equal(fg, fo, f"{ctx} batch {k}")
+        total += len(fo)
+    assert_books_equal(eng, ob, range(eng.num_symbols), ctx)
+    assert eng.resting_count() == ob.resting(), f"{ctx}: resting count"
+    return total
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def me(built):
+    import matching_engine_amd
+
+    return matching_engine_amd
+
+
+@pytest.fixture(scope="module")
+def orc(built):
+    from oracle import oracle
+
+    return oracle
+
+
+def _engine(me, hot_min, *a, **kw):
+    old = os.environ.get("ME_HOT_MIN")
+    os.environ["ME_HOT_MIN"] = str(hot_min)
+    try:
+        kw.setdefault("seq_ring", 1 << 22)
+        return me.Engine(*a, **kw)
+    finally:
+        if old is None:
+            del os.environ["ME_HOT_MIN"]
+        else:
+            os.environ["ME_HOT_MIN"] = old
+
+
+def _drift(me, levels, num_symbols, batch, nbatches, **over):
+    kw = dict(num_symbols=num_symbols, levels=levels, batch=batch, cancel_pct=10, market_pct=15, market_qty_mult=3,
+              drift_step=1, drift_every=4, far_pct=1, seq_start=(1 << 33) + 99)
+    kw.update(over)
+    sc = me.preset(5, **kw)
+    st = me.Stream(sc)
+    return sc, st.base_prices(), [st.next(batch) for _ in range(nbatches)]
+
+
+@pytest.mark.parametrize("hot_min", [1, 64])
+def test_hot_drift_far_cancels(me, orc, hot_min):
+    """Mids drifting past the 2,048-level windows, 1 % far LIMITs, 10 % cancels, sweeping MARKETs:
+    every generic fallback inside the hot path (cancel, out-of-window rest with re-centring, takers while
+    far levels exist), list rebuilds and deep rests."""
+    sc, base, batches = _drift(me, 2048, 6, 6144, 60)
+    ob = orc.OracleBook(sc.num_symbols)
+    total = sum(len(b) for b in batches)
+    with _engine(me, hot_min, sc.num_symbols, sc.levels, base, max_batch=sc.batch, max_resting=total + 64,
+                 max_chunks=total + 64) as eng:
+        nf = run_both(eng, ob, batches, ctx=f"hot drift min={hot_min}")
+    assert nf > 0
+
+
+def test_hot_sweeps_drain_lists(me, orc):
+    """MARKETs of up to 40 x 100 qty against thin levels: a sweep consumes more than the 64 listed
+    levels and the list is rebuilt mid-sweep; no cancels, no far prices."""
+    sc, base, batches = _drift(me, 4096, 3, 4096, 40, cancel_pct=0, far_pct=0, market_qty_mult=40,
+                               market_pct=10, drift_every=0, drift_step=0)
+    ob = orc.OracleBook(sc.num_symbols)
+    total = sum(len(b) for b in batches)
+    with _engine(me, 1, sc.num_symbols, sc.levels, base, max_batch=sc.batch, max_resting=total + 64,
+                 max_chunks=total + 64) as eng:
+        nf = run_both(eng, ob, batches, ctx="hot sweeps")
+    assert nf > 0
+
+
+def test_hot_multichunk_levels(me, orc):
+    """A 4-tick spread on a 2,048-level window: levels hold dozens of orders (chunk chains), walks cross
+    chunk boundaries (the one load of a walk) and appends open new tail chunks."""
+    sc, base, batches = _drift(me, 2048, 2, 4096, 30, cancel_pct=5, far_pct=0, spread_ticks=4, drift_every=0,
+                               drift_step=0, market_qty_mult=2)
+    ob = orc.OracleBook(sc.num_symbols)
+    total = sum(len(b) for b in batches)
+    with _engine(me, 1, sc.num_symbols, sc.levels, base, max_batch=sc.batch, max_resting=total + 64,
+                 max_chunks=total + 64) as eng:
+        nf = run_both(eng, ob, batches, ctx="hot multichunk")
+    assert nf > 0
+
+
+def test_hot_equals_generic_config4(me, orc):
+    """Config 4's shape (Zipf symbols, L = 32,768, books seeded to 3,000 levels per side): the hot path
+    (default threshold) and the generic kernel alone (ME_HOT_MIN=0) give identical outputs, both equal
+    to the oracle."""
+    sc = me.preset(4, num_symbols=300, batch=32768)
+    st = me.Stream(sc)
+    base = st.base_prices()
+    seeds = st.seed_books(range(8), 3000)
+    batches = [seeds.take(slice(i, i + 32768)) for i in range(0, len(seeds), 32768)]
+    batches += [st.next(sc.batch) for _ in range(4)]
+    total = sum(len(b) for b in batches)
+    outs = []
+    for hot_min in (512, 0):
+        ob = orc.OracleBook(sc.num_symbols)
+        with _engine(me, hot_min, sc.num_symbols, sc.levels, base, max_batch=32768, max_resting=total + 1024,
+                     max_chunks=total + 1024) as eng:
+            got = []
+            for b in batches:
+                got.append(eng.submit_batch(b))
+            for b, (r, f) in zip(batches, got):
+                ro, fo = ob.submit(b)
+                assert np.array_equal(f, fo) and all(np.array_equal(r[x], ro[x]) for x in
+                                                     ("filled_qty", "remaining_qty", "fill_count", "status"))
+            outs.append([eng.dump(s) for s in range(0, 300, 7)])
+    for a, b in zip(*outs):
+        assert np.array_equal(a, b)
