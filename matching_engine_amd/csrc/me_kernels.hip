@@ -1308,13 +1308,14 @@ struct HotLds {
   unsigned long long occ[HOT_MAX_WORDS];
 };
 
-struct HSide {  // a top-of-book list: entry i in lane i, levels best first
-  int lvl;
+struct HSide {  // a top-of-book list of side k: entry i in lane i, best first
+  int m;          // the entry's level in side coordinates (asks: the level; bids: L - 1 - level): smaller is better
   long long tot;
   uint32_t hd, tl, te, hn;
-  uint32_t row;  // the entry's LDS row; lanes >= n hold the free rows (the rows are a permutation)
-  int n;         // wave-uniform
-  bool more;     // wave-uniform: occupied levels of this side may lie beyond the last entry
+  uint32_t row;   // the entry's LDS row; lanes >= n hold the free rows (the rows are a permutation)
+  int n;          // wave-uniform
+  int more;       // wave-uniform: occupied levels of this side may lie beyond the last entry
+  int k;          // wave-uniform: the side (0 bids, 1 asks)
 };
 
 // One-lane moves of a list (gfx9 DPP wavefront shifts): entries leave at the front, enter anywhere.
@@ -1345,7 +1346,6 @@ struct HotState {
   uint32_t nchunks, L, W;
   uint32_t gs;
   long long base;
-  int bb, ba;  // best bid / ask, exact (-1 / L: the side is empty)
   unsigned long long wptr;
   int resting;
   uint32_t free_head;  // HBM free list (hot frees only push onto it: a store) ...
@@ -1353,7 +1353,9 @@ struct HotState {
   uint32_t nfar0, nfar1;
   uint32_t fstk, nfs;  // VGPR free-chunk stack: lane i holds entry i, entries [0, nfs)
   HotLds* H;
-  HSide S0, S1;        // bids, asks
+  // the two lists: A holds the side the current record takes from, B the side it rests on (swapped
+  // when a record of the other side comes: one instance of the record code serves both sides)
+  HSide A, B;
   // per-record lane state of the current block (lane k = record k): the window level it rests at
   // (-1: none) and that level's total / head / tail / tail fill, loaded at the block start, kept current
   int rlvl;
@@ -1382,11 +1384,55 @@ enum { HC_CHUNK, HC_POP, HC_PARTIAL, HC_APPEND, HC_INSERT, HC_DEEP, HC_RESTHEAD,
 #define HC_ADD(h, i) ((void)0)
 #endif
 
-// The generic code's view (sync points only): hot fields in, run, hot fields out.
+// Diagnostic ablation builds only (-DHOT_ABL=bits, never the product): drop classes of HBM stores to
+// measure what they cost the chain (results are then wrong).
+#ifndef HOT_ABL
+#define HOT_ABL 0
+#endif
+#define ABL(b) ((HOT_ABL & (b)) != 0)
+#ifdef HOT_MARKS  // asm listing landmarks (make asm HOT_MARKS=1): no instructions
+#define HMARK(s) asm volatile(";@@ " s)
+#else
+#define HMARK(s) ((void)0)
+#endif
+
+// Side coordinates <-> window levels (the same map both ways).
+__device__ __forceinline__ int side_lvl(const HotState& h, int k, int m) { return k ? m : (int)h.L - 1 - m; }
+
+// Field by field (a struct copy would drag padding through scratch memory); the wave-uniform fields
+// are pinned to SGPRs.
+template <class T>
+__device__ __forceinline__ void fswap(T& a, T& b) {
+  const T t = a;
+  a = b;
+  b = t;
+}
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ void hswap(HSide& a, HSide& b) {
+  fswap(a.m, b.m);
+  fswap(a.tot, b.tot);
+  fswap(a.hd, b.hd);
+  fswap(a.tl, b.tl);
+  fswap(a.te, b.te);
+  fswap(a.hn, b.hn);
+  fswap(a.row, b.row);
+  const int an = a.n, am = a.more, ak = a.k;
+  a.n = uni(b.n);
+  a.more = uni(b.more);
+  a.k = uni(b.k);
+  b.n = uni(an);
+  b.more = uni(am);
+  b.k = uni(ak);
+}
+
+// The generic code's view (sync points only): hot fields in, run, hot fields out. The best levels come
+// from the list fronts (a list is empty only with its side).
 __device__ __forceinline__ void hot_to_wave(const HotState& h, WaveCtx& c) {
+  const int L = (int)h.L;
+  const int a0 = h.A.n ? rli32(h.A.m, 0) : L, b0 = h.B.n ? rli32(h.B.m, 0) : L;
+  c.ba = h.A.k ? a0 : b0;
+  c.bb = L - 1 - (h.A.k ? b0 : a0);
   c.base = h.base;
-  c.bb = h.bb;
-  c.ba = h.ba;
   c.wptr = h.wptr;
   c.resting_delta = h.resting;
   c.free_head = h.free_head;
@@ -1394,18 +1440,17 @@ __device__ __forceinline__ void hot_to_wave(const HotState& h, WaveCtx& c) {
   c.nfar0 = h.nfar0;
   c.nfar1 = h.nfar1;
 }
+// (The WaveCtx lives in scratch memory: whatever comes back from it is pinned to SGPRs, or the
+// compiler would treat it — and every branch on it — as divergent.)
 __device__ __forceinline__ void wave_to_hot(const WaveCtx& c, HotState& h) {
-  h.base = c.base;
-  h.bb = c.bb;
-  h.ba = c.ba;
-  h.wptr = c.wptr;
-  h.resting = c.resting_delta;
-  h.free_head = c.free_head;
+  h.base = rli64(c.base, 0);
+  h.wptr = rl64(c.wptr, 0);
+  h.resting = rli32(c.resting_delta, 0);
+  h.free_head = rl32(c.free_head, 0);
   h.free_next = rl32(c.free_next, 0);
-  h.nfar0 = c.nfar0;
-  h.nfar1 = c.nfar1;
+  h.nfar0 = rl32(c.nfar0, 0);
+  h.nfar1 = rl32(c.nfar1, 0);
 }
-
 
 // ---- occupancy (LDS copy, written through to HBM one word at a time)
 __device__ __forceinline__ void hot_occ_load(HotState& h) {
@@ -1419,7 +1464,7 @@ __device__ __forceinline__ void hot_occ_set(HotState& h, int lvl, bool on) {
     const unsigned long long o = h.H->occ[w];
     const unsigned long long v = on ? (o | bit) : (o & ~bit);
     h.H->occ[w] = v;
-    h.occ[w] = v;
+    if (!ABL(8)) h.occ[w] = v;
   }
 }
 
@@ -1437,8 +1482,8 @@ __device__ __forceinline__ uint32_t nth_set(unsigned long long w, uint32_t r) {
   return pos;
 }
 
-// Lanes 0..n-1 <- the first (up to) HT occupied levels from `start` going up (K = 1, asks) or down
-// (K = 0, bids), from the LDS occupancy copy. *more: the list filled before the window side ended.
+// Lanes 0..n-1 <- the first (up to) HT occupied levels from window level `start` going up (K = 1) or
+// down (K = 0), from the LDS occupancy copy. *more: the list filled before the window ended.
 template <int K>
 __device__ __forceinline__ int hot_scan(const HotState& h, int start, int& out_lvl, bool& more) {
   const int lane = lane_id();
@@ -1481,17 +1526,20 @@ __device__ __forceinline__ int hot_scan(const HotState& h, int start, int& out_l
   }
 }
 
-// Rebuild list K from its best level: occupancy scan (LDS), the levels (one round trip) and their head
-// chunks (one round trip) into lanes / LDS slots. The caller has waited for every store.
-template <int K>
-__device__ __forceinline__ void hot_rebuild(HotState& h, HSide& S) {
+// Rebuild list S from side coordinate start_m (the best, or a bound no level of either side lies
+// inside): occupancy scan (LDS), the levels (one round trip) and their head chunks (one round trip)
+// into lanes / LDS rows. The caller has waited for every store.
+__device__ __forceinline__ void hot_rebuild(HotState& h, HSide& S, int start_m) {
   const int lane = lane_id();
   const int L = (int)h.L;
-  int start = K ? h.ba : h.bb;  // the best (or a bound no level of either side lies between)
-  if (K ? start < 0 : start >= L) start = K ? 0 : L - 1;
-  int lvl;
-  bool more;
-  const int n = hot_scan<K>(h, start, lvl, more);
+  int lvl = -1, n = 0;
+  bool more = false;
+  if (start_m < L) {
+    if (S.k)
+      n = hot_scan<1>(h, start_m < 0 ? 0 : start_m, lvl, more);
+    else
+      n = hot_scan<0>(h, L - 1 - (start_m < 0 ? 0 : start_m), lvl, more);
+  }
   const bool v = lane < n;
   const int li = v ? lvl : 0;
   Level x{0, NIL, NIL};
@@ -1508,8 +1556,8 @@ __device__ __forceinline__ void hot_rebuild(HotState& h, HSide& S) {
   const v4i a0 = src[0], a1 = src[1], a2 = src[2], a3 = src[3], b0 = src[4], b1 = src[5], b2 = src[6],
             b3 = src[7], b4 = src[8], b5 = src[9], b6 = src[10], b7 = src[11];
   const uint32_t hn = ch->hdr.next;
-  v4i* dq = reinterpret_cast<v4i*>(h.H->cq[K][lane]);
-  v4i* ds = reinterpret_cast<v4i*>(h.H->cs[K][lane]);
+  v4i* dq = reinterpret_cast<v4i*>(h.H->cq[S.k][lane]);
+  v4i* ds = reinterpret_cast<v4i*>(h.H->cs[S.k][lane]);
   dq[0] = a0;
   dq[1] = a1;
   dq[2] = a2;
@@ -1522,7 +1570,7 @@ __device__ __forceinline__ void hot_rebuild(HotState& h, HSide& S) {
   ds[5] = b5;
   ds[6] = b6;
   ds[7] = b7;
-  S.lvl = v ? lvl : -1;
+  S.m = v ? side_lvl(h, S.k, lvl) : L;
   S.tot = v ? x.total : 0;
   S.hd = v ? x.head : NIL;
   S.tl = v ? x.tail : NIL;
@@ -1531,11 +1579,6 @@ __device__ __forceinline__ void hot_rebuild(HotState& h, HSide& S) {
   S.row = (uint32_t)lane;
   S.n = n;
   S.more = more;
-  const int b = n ? rli32(lvl, 0) : (K ? L : -1);  // exact best
-  if (K)
-    h.ba = b;
-  else
-    h.bb = b;
 }
 
 // The block's per-record level states, loaded in vector form (lanes with rlvl >= 0).
@@ -1574,7 +1617,7 @@ __device__ __forceinline__ void hot_free(HotState& h, uint32_t ch) {
 // Record the level's header and tail fill in HBM.
 __device__ __forceinline__ void hot_level_store(HotState& h, int lvl, long long tot, uint32_t hd, uint32_t tl,
                                                 uint32_t te) {
-  if (lane_id() == 0) {
+  if (lane_id() == 0 && !ABL(4)) {
     Level o;
     o.total = tot;
     o.head = tot ? hd : NIL;
@@ -1587,7 +1630,7 @@ __device__ __forceinline__ void hot_level_store(HotState& h, int lvl, long long 
 // New chunk ch holding one order (seq, q) at level lvl, behind tail `prev` (NIL: the level's only chunk).
 __device__ __forceinline__ void hot_new_chunk(HotState& h, uint32_t ch, uint32_t prev, int lvl,
                                               unsigned long long seq, int q) {
-  if (lane_id() == 0) {
+  if (lane_id() == 0 && !ABL(16)) {
     ChunkHdr hh;
     hh.next = NIL;
     hh.prev = prev;
@@ -1609,31 +1652,53 @@ __device__ __forceinline__ void hot_broadcast(HotState& h, int lvl, long long to
   h.rtl = m ? tl : h.rtl;
   h.rte = m ? te : h.rte;
 }
+
 // The last entry of a full list leaves it (a level entering the list takes its place and row).
 __device__ __forceinline__ void hot_drop_last(HotState& h, HSide& S) {
   HEV(h, HEV_TRUNC_ENTRIES);
   const int j = S.n - 1;
-  hot_broadcast(h, rli32(S.lvl, j), rli64(S.tot, j), rl32(S.hd, j), rl32(S.tl, j), rl32(S.te, j));
+  hot_broadcast(h, side_lvl(h, S.k, rli32(S.m, j)), rli64(S.tot, j), rl32(S.hd, j), rl32(S.tl, j), rl32(S.te, j));
   S.n -= 1;
   S.more = true;
 }
 
-// Take up to rem from list K's front levels while they cross lim (K = 1: asks for a BUY).
-template <int K>
-__device__ __forceinline__ void hot_take(HotState& h, HSide& S, int lim, uint32_t& rem, unsigned long long taker) {
+__device__ __noinline__ uint32_t hot_alloc_slow(WaveCtx* c);
+
+// A free chunk: the VGPR stack, else (rare) the symbol's free list or the bump allocator through the
+// generic allocator, after one full wait (its free-list loads must see this wave's stores). NIL: the
+// chunk pool is exhausted (sticky error word).
+__device__ __forceinline__ uint32_t hot_alloc(HotState& h, WaveCtx& c) {
+  if (ME_LIKELY(h.nfs)) {
+    h.nfs -= 1;
+    return rl32(h.fstk, (int)h.nfs);
+  }
+  hot_drain();
+  hot_to_wave(h, c);
+  const uint32_t ch = (uint32_t)uni((int)hot_alloc_slow(&c));
+  wave_to_hot(c, h);
+  return ch;
+}
+
+// Take up to rem from list O's front levels while they cross lim (side coordinates of O).
+__device__ __forceinline__ void hot_take(HotState& h, HSide& O, int lim, uint32_t& rem, unsigned long long taker) {
   const int lane = lane_id();
   const bool act = lane < ME_C;
   const int sl = lane & (ME_C - 1);
   HC_MARK(h);
+  HMARK("take-entry");
   while (rem) {
-    if (!S.n) return;  // the side is empty (a list runs dry only with it)
-    const int lvl = rli32(S.lvl, 0);
-    if (K ? lvl > lim : lvl < lim) return;
-    uint32_t hd = rl32(S.hd, 0);
-    const uint32_t tl = rl32(S.tl, 0);
-    const uint32_t r = rl32(S.row, 0);
-    long long tot = rli64(S.tot, 0);
+    HMARK("take-level");
+    if (!O.n) return;  // the side is empty (a list runs dry only with it)
+    const int m0 = rli32(O.m, 0);
+    if (m0 > lim) return;
+    const int lvl = side_lvl(h, O.k, m0);
+    uint32_t hd = rl32(O.hd, 0);
+    const uint32_t tl = rl32(O.tl, 0);
+    const uint32_t r = rl32(O.row, 0);
+    long long tot = rli64(O.tot, 0);
     const long long price = h.base + lvl;
+    int* rq = h.H->cq[O.k][r];
+    unsigned long long* rs = h.H->cs[O.k][r];
     uint32_t taken = 0;
     HC_ADD(h, HC_TAKEHEAD);
     if (ME_UNLIKELY(hd >= h.nchunks)) {  // a corrupt list entry: never index with it
@@ -1642,8 +1707,9 @@ __device__ __forceinline__ void hot_take(HotState& h, HSide& S, int lim, uint32_
       return;
     }
     for (;;) {  // the level's chunks, head first
-      const int q_ = h.H->cq[K][r][sl];
-      const unsigned long long mseq = vreg64(h.H->cs[K][r][sl]);
+      HMARK("take-chunk");
+      const int q_ = rq[sl];
+      const unsigned long long mseq = vreg64(rs[sl]);
       const uint32_t uq = act ? (uint32_t)q_ : 0u;
       const uint32_t inc = scan16_sat(uq);
       const uint32_t ex = inc - uq;
@@ -1658,9 +1724,9 @@ __device__ __forceinline__ void hot_take(HotState& h, HSide& S, int lim, uint32_
         F.price_q4 = price;
         F.qty = (int)fq;
         F.symbol = h.gs;
-        h.scratch[h.wptr + (unsigned long long)__builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u)] = F;
-        h.H->cq[K][r][sl] = (int)(uq - fq);
-        h.chunks[hd].qty[sl] = (int)(uq - fq);
+        if (!ABL(1)) h.scratch[h.wptr + (unsigned long long)__builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u)] = F;
+        rq[sl] = (int)(uq - fq);
+        if (!ABL(2)) h.chunks[hd].qty[sl] = (int)(uq - fq);
       }
       h.wptr += (unsigned long long)__popcll(fm);
       h.resting -= __popcll(__ballot(fq == uq) & fm);
@@ -1668,11 +1734,12 @@ __device__ __forceinline__ void hot_take(HotState& h, HSide& S, int lim, uint32_
       const uint32_t t = rem < live ? rem : live;
       rem -= t;
       taken += t;
+      HMARK("take-chunk-done");
       if (__ballot(uq > fq) & 0xFFFFull) break;  // live slots remain: the taker is done
       // the chunk is exhausted (its HBM slots read 0 already): free it, go on down the FIFO
       hot_free(h, hd);
       if (hd == tl) break;
-      const uint32_t nx = rl32(S.hn, 0);
+      const uint32_t nx = rl32(O.hn, 0);
       if (ME_UNLIKELY(nx >= h.nchunks)) {  // a corrupt FIFO: stop the taker, report it
         if (lane == 0) atomicOr(h.err, ERR_INCONSISTENT);
         rem = 0;
@@ -1687,74 +1754,69 @@ __device__ __forceinline__ void hot_take(HotState& h, HSide& S, int lim, uint32_
       const uint32_t nn = h.chunks[nx].hdr.next;
       __builtin_amdgcn_s_waitcnt(0);
       if (act) {
-        h.H->cq[K][r][sl] = nq;
-        h.H->cs[K][r][sl] = ns;
+        rq[sl] = nq;
+        rs[sl] = ns;
       }
       if (lane == 0) h.chunks[nx].hdr.prev = NIL;
       hd = nx;
-      S.hd = lane == 0 ? nx : S.hd;
-      S.hn = lane == 0 ? rl32(nn, 0) : S.hn;
+      O.hd = lane == 0 ? nx : O.hd;
+      O.hn = lane == 0 ? rl32(nn, 0) : O.hn;
       if (!rem) break;
     }
     tot -= taken;
     HC_ADD(h, HC_CHUNK);
     if (tot == 0) {  // the level emptied: pop it (record lanes of it learn: a later rest may find it deep)
+      HMARK("take-pop");
       HEV(h, HEV_POP);
       hot_level_store(h, lvl, 0, NIL, NIL, 0);
       hot_occ_set(h, lvl, false);
       hot_broadcast(h, lvl, 0, NIL, NIL, 0);
       // every entry one lane down; the front's row goes to lane 63 (free)
-      S.lvl = (int)lanes_down((uint32_t)S.lvl);
-      S.tot = lanes_down64(S.tot);
-      S.hd = lanes_down(S.hd);
-      S.tl = lanes_down(S.tl);
-      S.te = lanes_down(S.te);
-      S.hn = lanes_down(S.hn);
-      S.row = lanes_down(S.row);
-      S.n -= 1;
-      if (!S.n && S.more) {
+      O.m = (int)lanes_down((uint32_t)O.m);
+      O.tot = lanes_down64(O.tot);
+      O.hd = lanes_down(O.hd);
+      O.tl = lanes_down(O.tl);
+      O.te = lanes_down(O.te);
+      O.hn = lanes_down(O.hn);
+      O.row = lanes_down(O.row);
+      O.n -= 1;
+      if (!O.n && O.more) {
         // the list ran dry with levels beyond it: rebuild it now, so that an empty list always means
-        // an empty side and the best levels stay exact (a scan from a mere bound would run into the
-        // other side's levels: the occupancy bitmap holds both)
-        if (K)
-          h.ba = lvl + 1;
-        else
-          h.bb = lvl - 1;
+        // an empty side (a scan from a mere bound could run into the other side's levels later: the
+        // occupancy bitmap holds both)
         HEV(h, HEV_TAKE_REBUILD);
         hot_drain();
-        hot_rebuild<K>(h, S);
+        hot_rebuild(h, O, m0 + 1);
         __builtin_amdgcn_s_waitcnt(0);
-        continue;
       }
-      const int nb = S.n ? rli32(S.lvl, 0) : (K ? (int)h.L : -1);
-      if (K)
-        h.ba = nb;
-      else
-        h.bb = nb;
       HC_ADD(h, HC_POP);
+      HMARK("take-pop-done");
       continue;
     }
-    S.tot = lane == 0 ? tot : S.tot;
-    hot_level_store(h, lvl, tot, hd, tl, rl32(S.te, 0));
+    HMARK("take-partial");
+    O.tot = lane == 0 ? tot : O.tot;
+    hot_level_store(h, lvl, tot, hd, tl, rl32(O.te, 0));
     HC_ADD(h, HC_PARTIAL);
     return;
   }
 }
 
-// Rest (seq, q) at window level lvl on side K (0 bids, 1 asks); record lane kr holds the level's state.
-// False: the chunk stack ran dry (nothing changed).
-template <int K>
-__device__ __forceinline__ bool hot_rest(HotState& h, HSide& S, int lvl, unsigned long long seq, int q, int kr) {
+// Rest (seq, q) on list M at side coordinate mm (window level lvl); record lane kr holds the level's
+// state. False: the chunk pool is exhausted.
+__device__ __forceinline__ bool hot_rest(HotState& h, WaveCtx& c, HSide& M, int mm, int lvl, unsigned long long seq,
+                                         int q, int kr) {
   const int lane = lane_id();
   HC_MARK(h);
-  const bool ent = lane < S.n;
-  const int p = __popcll(__ballot(ent && (K ? S.lvl < lvl : S.lvl > lvl)));  // entries better than lvl
+  HMARK("rest-entry");
+  const bool ent = lane < M.n;
+  const int p = __popcll(__ballot(ent && M.m < mm));  // entries better than the level
   HC_ADD(h, HC_RESTHEAD);
-  if (p < S.n && rli32(S.lvl, p) == lvl) {  // a listed level: append
+  if (p < M.n && rli32(M.m, p) == mm) {  // a listed level: append
+    HMARK("rest-append");
     HEV(h, HEV_APPEND);
     const int j = p;
-    const uint32_t te = rl32(S.te, j), tl = rl32(S.tl, j), hd = rl32(S.hd, j);
-    const long long tot = rli64(S.tot, j) + q;
+    const uint32_t te = rl32(M.te, j), tl = rl32(M.tl, j), hd = rl32(M.hd, j);
+    const long long tot = rli64(M.tot, j) + q;
     uint32_t ntl = tl, nte = te + 1;
     if (ME_UNLIKELY(tl >= h.nchunks)) {
       if (lane == 0) atomicOr(h.err, ERR_INCONSISTENT);
@@ -1762,10 +1824,10 @@ __device__ __forceinline__ bool hot_rest(HotState& h, HSide& S, int lvl, unsigne
     }
     if (te < (uint32_t)ME_C) {
       if (tl == hd) {
-        const uint32_t r = rl32(S.row, j);
+        const uint32_t r = rl32(M.row, j);
         if (lane == 0) {
-          h.H->cq[K][r][te] = q;
-          h.H->cs[K][r][te] = seq;
+          h.H->cq[M.k][r][te] = q;
+          h.H->cs[M.k][r][te] = seq;
         }
       }
       if (lane == 0) {
@@ -1774,66 +1836,60 @@ __device__ __forceinline__ bool hot_rest(HotState& h, HSide& S, int lvl, unsigne
         h.loc[seq & h.rmask] = tl * ME_C + te;
       }
     } else {
-      if (ME_UNLIKELY(!h.nfs)) return false;
-      h.nfs -= 1;
-      const uint32_t ch = rl32(h.fstk, (int)h.nfs);
+      const uint32_t ch = hot_alloc(h, c);
+      if (ME_UNLIKELY(ch == NIL)) return false;
       hot_new_chunk(h, ch, tl, lvl, seq, q);
-      if (tl == hd) S.hn = lane == j ? ch : S.hn;
+      if (tl == hd) M.hn = lane == j ? ch : M.hn;
       ntl = ch;
       nte = 1;
     }
     hot_level_store(h, lvl, tot, hd, ntl, nte);
-    S.tot = lane == j ? tot : S.tot;
-    S.tl = lane == j ? ntl : S.tl;
-    S.te = lane == j ? nte : S.te;
+    M.tot = lane == j ? tot : M.tot;
+    M.tl = lane == j ? ntl : M.tl;
+    M.te = lane == j ? nte : M.te;
     h.resting += 1;
     HC_ADD(h, HC_APPEND);
     return true;
   }
-  if (p < S.n || (!S.more && p < HT)) {
+  if (p < M.n || (!M.more && p < HT)) {
     // an empty level inside the list's span (or past its end when nothing lies beyond): it enters
     // at position p, the entries behind it move one lane up (a full list drops its last entry)
+    HMARK("rest-insert");
     if (p == 0)
       HEV(h, HEV_NEWBEST);
     else
       HEV(h, HEV_GAP);
-    if (ME_UNLIKELY(!h.nfs)) return false;  // the block start keeps the stack topped up
-    if (S.n == HT) hot_drop_last(h, S);
-    h.nfs -= 1;
-    const uint32_t ch = rl32(h.fstk, (int)h.nfs);
+    const uint32_t ch = hot_alloc(h, c);
+    if (ME_UNLIKELY(ch == NIL)) return false;
+    if (M.n == HT) hot_drop_last(h, M);
     hot_new_chunk(h, ch, NIL, lvl, seq, q);
     hot_level_store(h, lvl, q, ch, ch, 1);
     hot_occ_set(h, lvl, true);
-    const uint32_t r = rl32(S.row, HT - 1);  // a free row (S.n < HT)
+    const uint32_t r = rl32(M.row, HT - 1);  // a free row (M.n < HT)
     const bool up = lane > p, at = lane == p;
-    const int ulvl = (int)lanes_up((uint32_t)S.lvl);
-    const long long utot = lanes_up64(S.tot);
-    const uint32_t uhd = lanes_up(S.hd), utl = lanes_up(S.tl), ute = lanes_up(S.te), uhn = lanes_up(S.hn),
-                   urow = lanes_up(S.row);
-    S.lvl = up ? ulvl : (at ? lvl : S.lvl);
-    S.tot = up ? utot : (at ? (long long)q : S.tot);
-    S.hd = up ? uhd : (at ? ch : S.hd);
-    S.tl = up ? utl : (at ? ch : S.tl);
-    S.te = up ? ute : (at ? 1u : S.te);
-    S.hn = up ? uhn : (at ? NIL : S.hn);
-    S.row = up ? urow : (at ? r : S.row);
+    const int um = (int)lanes_up((uint32_t)M.m);
+    const long long utot = lanes_up64(M.tot);
+    const uint32_t uhd = lanes_up(M.hd), utl = lanes_up(M.tl), ute = lanes_up(M.te), uhn = lanes_up(M.hn),
+                   urow = lanes_up(M.row);
+    M.m = up ? um : (at ? mm : M.m);
+    M.tot = up ? utot : (at ? (long long)q : M.tot);
+    M.hd = up ? uhd : (at ? ch : M.hd);
+    M.tl = up ? utl : (at ? ch : M.tl);
+    M.te = up ? ute : (at ? 1u : M.te);
+    M.hn = up ? uhn : (at ? NIL : M.hn);
+    M.row = up ? urow : (at ? r : M.row);
     if (lane < ME_C) {
-      h.H->cq[K][r][lane] = lane == 0 ? q : 0;
-      h.H->cs[K][r][lane] = lane == 0 ? seq : 0ull;
+      h.H->cq[M.k][r][lane] = lane == 0 ? q : 0;
+      h.H->cs[M.k][r][lane] = lane == 0 ? seq : 0ull;
     }
-    S.n += 1;
-    if (p == 0) {
-      if (K)
-        h.ba = lvl;
-      else
-        h.bb = lvl;
-    }
+    M.n += 1;
     hot_broadcast(h, lvl, q, ch, ch, 1);
     h.resting += 1;
     HC_ADD(h, HC_INSERT);
     return true;
   }
   // deep (beyond the list's last entry, with unlisted levels there): the record lane's level state
+  HMARK("rest-deep");
   HEV(h, HEV_DEEP);
   const long long tot0 = rli64(h.rtot, kr);
   const uint32_t hd0 = rl32(h.rhd, kr), tl0 = rl32(h.rtl, kr), te0 = rl32(h.rte, kr);
@@ -1844,9 +1900,8 @@ __device__ __forceinline__ bool hot_rest(HotState& h, HSide& S, int lvl, unsigne
     return true;
   }
   if (tot0 == 0 || te0 >= (uint32_t)ME_C) {
-    if (ME_UNLIKELY(!h.nfs)) return false;
-    h.nfs -= 1;
-    const uint32_t ch = rl32(h.fstk, (int)h.nfs);
+    const uint32_t ch = hot_alloc(h, c);
+    if (ME_UNLIKELY(ch == NIL)) return false;
     hot_new_chunk(h, ch, tot0 ? tl0 : NIL, lvl, seq, q);
     if (!tot0) {
       hd = ch;
@@ -1879,19 +1934,21 @@ __device__ __noinline__ void hot_free_slow(WaveCtx* c, uint32_t ch) { free_chunk
 // WaveCtx takes the hot state, the generic code runs, the hot state and both lists come back.
 __device__ __forceinline__ void hot_sync_in(HotState& h, WaveCtx& c) {
   hot_drain();
-  hot_to_wave(h, c);  // the best levels are exact (an empty list means an empty side)
+  hot_to_wave(h, c);
 }
 __device__ __forceinline__ void hot_sync_out(HotState& h, const WaveCtx& c) {
   wave_to_hot(c, h);
   hot_drain();
   hot_occ_load(h);
-  hot_rebuild<0>(h, h.S0);
-  hot_rebuild<1>(h, h.S1);
+  const int L = (int)h.L;
+  const int ba = rli32(c.ba, 0), bb = rli32(c.bb, 0);
+  hot_rebuild(h, h.A, h.A.k ? ba : L - 1 - bb);
+  hot_rebuild(h, h.B, h.B.k ? ba : L - 1 - bb);
 }
 __device__ __forceinline__ void hot_topup(HotState& h, WaveCtx& c) {
   hot_sync_in(h, c);
   while (h.nfs < HOT_STACK_FILL) {
-    const uint32_t ch = hot_alloc_slow(&c);
+    const uint32_t ch = (uint32_t)uni((int)hot_alloc_slow(&c));
     if (ch == NIL) break;
     h.fstk = lane_id() == (int)h.nfs ? ch : h.fstk;
     h.nfs += 1;
@@ -1902,16 +1959,17 @@ __device__ __forceinline__ void hot_topup(HotState& h, WaveCtx& c) {
 #ifdef ME_HOT_CHECK
 // Diagnostic build only (make hotcheck): after every record, the lists, record-lane states and LDS
 // copies against the HBM book; the first mismatch is printed and stops the wave (ERR_INCONSISTENT).
-template <int K>
-__device__ bool hot_check_side(HotState& h, const HSide& S, unsigned long long seq, int what) {
+// other_best: the other side's best window level (-1 / L: none); no level lies between the two.
+__device__ bool hot_check_side(HotState& h, const HSide& S, int other_best, unsigned long long seq, int what) {
   const int lane = lane_id();
+  const int L = (int)h.L;
   const bool ent = lane < S.n;
   bool bad = false;
   int code = 0;
   long long a0 = 0, a1 = 0;
+  const int l = side_lvl(h, S.k, S.m);
   if (ent) {
-    const int l = S.lvl;
-    if (l < 0 || l >= (int)h.L) {
+    if (l < 0 || l >= L) {
       bad = true, code = 1, a0 = l;
     } else {
       const Level x = h.lv[l];
@@ -1930,12 +1988,12 @@ __device__ bool hot_check_side(HotState& h, const HSide& S, unsigned long long s
         else if (C.hdr.price != h.base + l) bad = true, code = 9, a0 = C.hdr.price, a1 = h.base + l;
         else {
           for (int j = 0; j < ME_C; ++j) {
-            if (C.qty[j] != h.H->cq[K][S.row][j]) {
-              bad = true, code = 10, a0 = C.qty[j], a1 = h.H->cq[K][S.row][j];
+            if (C.qty[j] != h.H->cq[S.k][S.row][j]) {
+              bad = true, code = 10, a0 = C.qty[j], a1 = h.H->cq[S.k][S.row][j];
               break;
             }
-            if (C.qty[j] > 0 && C.seq[j] != h.H->cs[K][S.row][j]) {
-              bad = true, code = 11, a0 = (long long)C.seq[j], a1 = (long long)h.H->cs[K][S.row][j];
+            if (C.qty[j] > 0 && C.seq[j] != h.H->cs[S.k][S.row][j]) {
+              bad = true, code = 11, a0 = (long long)C.seq[j], a1 = (long long)h.H->cs[S.k][S.row][j];
               break;
             }
           }
@@ -1943,48 +2001,35 @@ __device__ bool hot_check_side(HotState& h, const HSide& S, unsigned long long s
       }
     }
   }
-  // the entries are the first n occupied levels from the best, in order
+  // the entries are the first n occupied levels beyond the other side's best, in order
   int sl;
   bool more;
-  const int best = K ? h.ba : h.bb;
-  const int n2 = hot_scan<K>(h, K ? (best < 0 ? 0 : best) : (best >= (int)h.L ? (int)h.L - 1 : best), sl, more);
+  const int n2 = S.k ? hot_scan<1>(h, other_best + 1, sl, more) : hot_scan<0>(h, other_best - 1, sl, more);
   if (!bad && S.n > n2) bad = true, code = 12, a0 = S.n, a1 = n2;
-  if (!bad && S.n && rli32(S.lvl, 0) != best) bad = true, code = 13, a0 = rli32(S.lvl, 0), a1 = best;
-  if (!bad && !S.n && best != (K ? (int)h.L : -1)) bad = true, code = 16, a0 = best;
+  if (!bad && !S.n && n2) bad = true, code = 14, a0 = rli32(sl, 0), a1 = n2;
+  if (!bad && lane < S.n && l != sl) bad = true, code = 15, a0 = l, a1 = sl;
   {  // the rows are a permutation of 0..63
     unsigned long long seen = 0;
     for (int i = 0; i < HT; ++i) seen |= 1ull << (rl32(S.row, i) & 63u);
     if (!bad && (seen != ~0ull || S.row >= (uint32_t)HT)) bad = true, code = 17, a0 = (long long)seen, a1 = S.row;
   }
-  if (!bad && !S.n && !S.more && n2) {
-    const int f0 = rli32(sl, 0);
-    bad = true, code = 14, a0 = f0, a1 = h.lv[f0].total;
-  }
-  {
-    if (!bad && lane < S.n && S.lvl != sl) bad = true, code = 15, a0 = S.lvl, a1 = sl;
-  }
   const unsigned long long bm = __ballot(bad);
   if (!bm) return true;
   const int j = __builtin_ctzll(bm);
   if (lane == j)
-    printf("HOTCHECK s=%u side=%d what=%d seq=%llu lane=%d code=%d a0=%lld a1=%lld n=%d row=%u more=%d lvl=%d best=%d\n", h.gs, K,
-           what, seq, lane, code, a0, a1, S.n, S.row, (int)S.more, S.lvl, best);
+    printf("HOTCHECK s=%u side=%d what=%d seq=%llu lane=%d code=%d a0=%lld a1=%lld n=%d row=%u more=%d lvl=%d other=%d\n",
+           h.gs, S.k, what, seq, lane, code, a0, a1, S.n, S.row, (int)S.more, l, other_best);
   return false;
 }
-__device__ bool hot_check_lists(HotState& h, unsigned long long seq, int what);
-__device__ bool hot_check(HotState& h, unsigned long long seq, int what, uint32_t kd = 0, int lm = 0, int q = 0,
-                          int rem = 0) {
-  hot_drain();
-  if (!hot_check_lists(h, seq, what)) {
-    if (lane_id() == 0)
-      printf("HOTCHECK after record s=%u seq=%llu kind=%u lm=%d q=%d rem=%d bb=%d ba=%d n0=%d n1=%d\n", h.gs, seq, kd, lm, q,
-             rem, h.bb, h.ba, h.S0.n, h.S1.n);
+__device__ bool hot_check_lists(HotState& h, unsigned long long seq, int what) {
+  const int L = (int)h.L;
+  const int fa = h.A.n ? side_lvl(h, h.A.k, rli32(h.A.m, 0)) : (h.A.k ? L : -1);
+  const int fb = h.B.n ? side_lvl(h, h.B.k, rli32(h.B.m, 0)) : (h.B.k ? L : -1);
+  if (h.A.k == h.B.k) {
+    if (lane_id() == 0) printf("HOTCHECK both lists hold side %d\n", h.A.k);
     return false;
   }
-  return true;
-}
-__device__ bool hot_check_lists(HotState& h, unsigned long long seq, int what) {
-  if (!hot_check_side<0>(h, h.S0, seq, what) || !hot_check_side<1>(h, h.S1, seq, what)) return false;
+  if (!hot_check_side(h, h.A, fb, seq, what) || !hot_check_side(h, h.B, fa, seq, what)) return false;
   const int lane = lane_id();
   bool bad = false;
   for (uint32_t i = (uint32_t)lane; i < h.W; i += 64)
@@ -1996,8 +2041,8 @@ __device__ bool hot_check_lists(HotState& h, unsigned long long seq, int what) {
   // record lanes of unlisted levels hold their HBM state
   const int l = h.rlvl;
   bool listed = false;
-  for (int i = 0; i < h.S0.n; ++i) listed |= rli32(h.S0.lvl, i) == l;
-  for (int i = 0; i < h.S1.n; ++i) listed |= rli32(h.S1.lvl, i) == l;
+  for (int i = 0; i < h.A.n; ++i) listed |= side_lvl(h, h.A.k, rli32(h.A.m, i)) == l;
+  for (int i = 0; i < h.B.n; ++i) listed |= side_lvl(h, h.B.k, rli32(h.B.m, i)) == l;
   if (l >= 0 && !listed) {
     const Level x = h.lv[l];
     const uint32_t te = h.tend[l];
@@ -2012,6 +2057,17 @@ __device__ bool hot_check_lists(HotState& h, unsigned long long seq, int what) {
   }
   if (h.nfs > (uint32_t)HT || (lane < (int)h.nfs && h.fstk >= h.nchunks)) {
     if (lane == 0) printf("HOTCHECK stack what=%d\n", what);
+    return false;
+  }
+  return true;
+}
+__device__ bool hot_check(HotState& h, unsigned long long seq, int what, uint32_t kd = 0, int lm = 0, int q = 0,
+                          int rem = 0) {
+  hot_drain();
+  if (!hot_check_lists(h, seq, what)) {
+    if (lane_id() == 0)
+      printf("HOTCHECK after record s=%u seq=%llu kind=%u lm=%d q=%d rem=%d nA=%d nB=%d kA=%d\n", h.gs, seq, kd, lm, q,
+             rem, h.A.n, h.B.n, h.A.k);
     return false;
   }
   return true;
@@ -2056,13 +2112,15 @@ __device__ __forceinline__ void match_records_hot(HotState& h, WaveCtx& c, const
 #ifdef ME_STAMPS
   for (int e_ = 0; e_ < 8; ++e_) h.ev[e_] = h.cyc[e_] = 0;
 #endif
-  const uint32_t Lw = h.L;
+  const int L = (int)h.L;
   h.nfs = 0;
   h.fstk = NIL;
   h.rlvl = -1;
+  h.A.k = 1;  // asks
+  h.B.k = 0;  // bids
   hot_occ_load(h);
-  hot_rebuild<0>(h, h.S0);
-  hot_rebuild<1>(h, h.S1);
+  hot_rebuild(h, h.A, rli32(c.ba, 0));
+  hot_rebuild(h, h.B, L - 1 - rli32(c.bb, 0));
   bool ok = true;
   for (uint32_t blk = lo; blk < hi && ok; blk += 64) {
     c.recs_left = hi - blk;
@@ -2084,25 +2142,24 @@ __device__ __forceinline__ void match_records_hot(HotState& h, WaveCtx& c, const
     const bool good = v && !cancel && oq > 0 && (side == ME_SIDE_BUY || side == ME_SIDE_SELL) && oseq != 0ull;
     // which records the lists take (vector form; again after a generic record moved the window):
     // cancels, LIMITs outside the window and takers while the side they cross has far levels are generic
-    unsigned long long slowm, fastm;
+    unsigned long long fastm;
     auto classify = [&]() {
       const unsigned long long off = (unsigned long long)opx - (unsigned long long)h.base;
-      const bool inw = off < (unsigned long long)Lw;
+      const bool inw = off < (unsigned long long)L;
       const bool farx = (side == ME_SIDE_BUY ? h.nfar1 : h.nfar0) != 0u;
       const bool fast = good && (market || inw) && !farx;
       h.rlvl = fast && !market ? (int)off : -1;
       fastm = __ballot(fast);
-      slowm = __ballot(v && !fast);
     };
     classify();
-    if (h.S0.n < HT / 2 && h.S0.more) {
+    if (h.A.n < HT / 2 && h.A.more) {
       hot_drain();
-      hot_rebuild<0>(h, h.S0);
+      hot_rebuild(h, h.A, rli32(h.A.m, 0));
       HS_COUNT(CT_MISS);
     }
-    if (h.S1.n < HT / 2 && h.S1.more) {
+    if (h.B.n < HT / 2 && h.B.more) {
       hot_drain();
-      hot_rebuild<1>(h, h.S1);
+      hot_rebuild(h, h.B, rli32(h.B.m, 0));
       HS_COUNT(CT_MISS);
     }
     hot_prefetch(h);
@@ -2114,15 +2171,17 @@ __device__ __forceinline__ void match_records_hot(HotState& h, WaveCtx& c, const
     R.nfill = R.fstart = R.st = 0;
     uint32_t k = 0;
     for (; k < cnt; ++k) {
+      HMARK("record-start");
       const unsigned long long seq = rl64(oseq, (int)k);
       const int q = rli32(oq, (int)k);
       const uint32_t kd = rl32(okd, (int)k);
       if (ME_UNLIKELY(!((fastm >> k) & 1ull))) {  // generic (or a reject) at a sync point
+        HMARK("record-generic");
         HS_COUNT(CT_EVICT);
         c.recs_left = hi - (blk + k);
         hot_sync_in(h, c);
         const RecOut o = hot_generic_record(&c, seq, rli64(opx, (int)k), q, kd);
-        if (!o.ok) {
+        if (!uni(o.ok)) {
           ok = false;
           break;
         }
@@ -2136,16 +2195,15 @@ __device__ __forceinline__ void match_records_hot(HotState& h, WaveCtx& c, const
         HS(PH_CANCEL);
         continue;
       }
+      HMARK("record-fast");
       const bool buy = (kd & 3u) == ME_SIDE_BUY;
       const bool mkt = (kd >> 2) & 1u;
-      const int lm = mkt ? (buy ? (int)Lw - 1 : 0) : rli32(h.rlvl, (int)k);
+      const int lm = mkt ? 0 : rli32(h.rlvl, (int)k);  // the LIMIT's window level
+      if (h.A.k != (buy ? 1 : 0)) hswap(h.A, h.B);   // A: the side this record takes from
       const unsigned long long fstart = h.wptr;
       uint32_t rem = (uint32_t)q;
       HS_COUNT(CT_FAST);
-      if (buy)
-        hot_take<1>(h, h.S1, lm, rem, seq);
-      else
-        hot_take<0>(h, h.S0, lm, rem, seq);
+      hot_take(h, h.A, mkt ? L - 1 : (buy ? lm : L - 1 - lm), rem, seq);
       HS(PH_SWEEP);
       const int filled = q - (int)rem;
       const uint32_t nfill = (uint32_t)(h.wptr - fstart);
@@ -2153,25 +2211,14 @@ __device__ __forceinline__ void match_records_hot(HotState& h, WaveCtx& c, const
       if (mkt) {
         stt = rem == 0 ? ME_ST_FILLED : ME_ST_CANCELED;
       } else {
-        if (rem) {
-          const bool rested = buy ? hot_rest<0>(h, h.S0, lm, seq, (int)rem, (int)k)
-                                  : hot_rest<1>(h, h.S1, lm, seq, (int)rem, (int)k);
-          if (ME_UNLIKELY(!rested)) {  // the stack ran dry: top it up and rest again
-            hot_topup(h, c);
-            hot_sync_out(h, c);
-            hot_prefetch(h);
-            __builtin_amdgcn_s_waitcnt(0);
-            const bool again = buy ? hot_rest<0>(h, h.S0, lm, seq, (int)rem, (int)k)
-                                   : hot_rest<1>(h, h.S1, lm, seq, (int)rem, (int)k);
-            if (!again) {  // the chunk pool is exhausted (sticky error word from alloc_chunk)
-              ok = false;
-              break;
-            }
-          }
+        if (rem && ME_UNLIKELY(!hot_rest(h, c, h.B, buy ? L - 1 - lm : lm, lm, seq, (int)rem, (int)k))) {
+          ok = false;  // the chunk pool is exhausted (sticky error word from alloc_chunk)
+          break;
         }
         stt = rem == 0 ? ME_ST_FILLED : (filled > 0 ? ME_ST_PARTIALLY_FILLED : ME_ST_NEW);
       }
       HS(PH_REST);
+      HMARK("record-result");
       put_result(R, k, filled, (int)rem, nfill, stt, ME_RJ_NONE, fstart);
       HOT_CHECK(1, seq, kd, lm, q, (int)rem);
     }
@@ -2220,7 +2267,7 @@ __global__ __launch_bounds__(64) void k_match_hot(BookDev bk, BatchDev bt) {
     h.nchunks = bk.nchunks;
     h.L = bk.L;
     h.W = bk.Lwords;
-    h.gs = c.gs;
+    h.gs = rl32(c.gs, 0);
     h.H = &H;
     wave_to_hot(c, h);
     match_records_hot(h, c, bt, lo, hi);
