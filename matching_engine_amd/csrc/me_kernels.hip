@@ -1308,26 +1308,21 @@ struct HotLds {
   unsigned long long occ[HOT_MAX_WORDS];
 };
 
-struct HSide {  // a top-of-book list of side k: entry i in lane i, best first
+struct HSide {  // a top-of-book list of side k, best first: a ring over the lanes, entry i in lane (f + i) & 63
   int m;          // the entry's level in side coordinates (asks: the level; bids: L - 1 - level): smaller is better
   long long tot;
   uint32_t hd, tl, te, hn;
-  uint32_t row;   // the entry's LDS row; lanes >= n hold the free rows (the rows are a permutation)
-  int n;          // wave-uniform
+  uint32_t row;   // the entry's LDS row; lanes past the entries hold the free rows (the rows are a permutation)
+  int f, n;       // wave-uniform: the front lane, the entries
   int more;       // wave-uniform: occupied levels of this side may lie beyond the last entry
   int k;          // wave-uniform: the side (0 bids, 1 asks)
 };
+__device__ __forceinline__ int hlane(const HSide& S, int i) { return (S.f + i) & (HT - 1); }
 
-// One-lane moves of a list (gfx9 DPP wavefront shifts): entries leave at the front, enter anywhere.
-__device__ __forceinline__ uint32_t lanes_down(uint32_t v) {  // lane i <- lane i + 1, lane 63 <- lane 0
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x134, 0xf, 0xf, false);  // wave_rol:1
-}
-__device__ __forceinline__ uint32_t lanes_up(uint32_t v) {  // lane i <- lane i - 1
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xf, 0xf, false);  // wave_shr:1
-}
-__device__ __forceinline__ long long lanes_down64(long long v) {
-  return (long long)(((unsigned long long)lanes_down((uint32_t)((unsigned long long)v >> 32)) << 32) |
-                     lanes_down((uint32_t)v));
+// A one-lane rotation of a ring (gfx9 DPP wavefront rotate): lane i <- lane i - 1, lane 0 <- lane 63.
+// An entry enters mid-list by the rotation of the entries behind it.
+__device__ __forceinline__ uint32_t lanes_up(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x13C, 0xf, 0xf, false);  // wave_ror:1
 }
 __device__ __forceinline__ long long lanes_up64(long long v) {
   return (long long)(((unsigned long long)lanes_up((uint32_t)((unsigned long long)v >> 32)) << 32) |
@@ -1353,9 +1348,7 @@ struct HotState {
   uint32_t nfar0, nfar1;
   uint32_t fstk, nfs;  // VGPR free-chunk stack: lane i holds entry i, entries [0, nfs)
   HotLds* H;
-  // the two lists: A holds the side the current record takes from, B the side it rests on (swapped
-  // when a record of the other side comes: one instance of the record code serves both sides)
-  HSide A, B;
+  HSide A, B;  // the asks (k = 1) and the bids (k = 0)
   // per-record lane state of the current block (lane k = record k): the window level it rests at
   // (-1: none) and that level's total / head / tail / tail fill, loaded at the block start, kept current
   int rlvl;
@@ -1399,37 +1392,15 @@ enum { HC_CHUNK, HC_POP, HC_PARTIAL, HC_APPEND, HC_INSERT, HC_DEEP, HC_RESTHEAD,
 // Side coordinates <-> window levels (the same map both ways).
 __device__ __forceinline__ int side_lvl(const HotState& h, int k, int m) { return k ? m : (int)h.L - 1 - m; }
 
-// Field by field (a struct copy would drag padding through scratch memory); the wave-uniform fields
-// are pinned to SGPRs.
-template <class T>
-__device__ __forceinline__ void fswap(T& a, T& b) {
-  const T t = a;
-  a = b;
-  b = t;
-}
+// Pins a wave-uniform value to an SGPR (values that come back from memory or calls are otherwise
+// treated as divergent, and so is every branch on them).
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
-__device__ __forceinline__ void hswap(HSide& a, HSide& b) {
-  fswap(a.m, b.m);
-  fswap(a.tot, b.tot);
-  fswap(a.hd, b.hd);
-  fswap(a.tl, b.tl);
-  fswap(a.te, b.te);
-  fswap(a.hn, b.hn);
-  fswap(a.row, b.row);
-  const int an = a.n, am = a.more, ak = a.k;
-  a.n = uni(b.n);
-  a.more = uni(b.more);
-  a.k = uni(b.k);
-  b.n = uni(an);
-  b.more = uni(am);
-  b.k = uni(ak);
-}
 
 // The generic code's view (sync points only): hot fields in, run, hot fields out. The best levels come
 // from the list fronts (a list is empty only with its side).
 __device__ __forceinline__ void hot_to_wave(const HotState& h, WaveCtx& c) {
   const int L = (int)h.L;
-  const int a0 = h.A.n ? rli32(h.A.m, 0) : L, b0 = h.B.n ? rli32(h.B.m, 0) : L;
+  const int a0 = h.A.n ? rli32(h.A.m, h.A.f) : L, b0 = h.B.n ? rli32(h.B.m, h.B.f) : L;
   c.ba = h.A.k ? a0 : b0;
   c.bb = L - 1 - (h.A.k ? b0 : a0);
   c.base = h.base;
@@ -1577,6 +1548,7 @@ __device__ __forceinline__ void hot_rebuild(HotState& h, HSide& S, int start_m) 
   S.te = te;
   S.hn = hv ? hn : NIL;
   S.row = (uint32_t)lane;
+  S.f = 0;
   S.n = n;
   S.more = more;
 }
@@ -1656,7 +1628,7 @@ __device__ __forceinline__ void hot_broadcast(HotState& h, int lvl, long long to
 // The last entry of a full list leaves it (a level entering the list takes its place and row).
 __device__ __forceinline__ void hot_drop_last(HotState& h, HSide& S) {
   HEV(h, HEV_TRUNC_ENTRIES);
-  const int j = S.n - 1;
+  const int j = hlane(S, S.n - 1);
   hot_broadcast(h, side_lvl(h, S.k, rli32(S.m, j)), rli64(S.tot, j), rl32(S.hd, j), rl32(S.tl, j), rl32(S.te, j));
   S.n -= 1;
   S.more = true;
@@ -1679,108 +1651,79 @@ __device__ __forceinline__ uint32_t hot_alloc(HotState& h, WaveCtx& c) {
   return ch;
 }
 
-// Take up to rem from list O's front levels while they cross lim (side coordinates of O).
+// Take up to rem from list O (side K) front levels while they cross lim (side coordinates). One pass
+// per chunk of the front level: a partial take ends the taker, an exhausted chunk frees it and then
+// pops the level (its last chunk) or moves the level's head to the next chunk (a load, rare).
+template <int K>
 __device__ __forceinline__ void hot_take(HotState& h, HSide& O, int lim, uint32_t& rem, unsigned long long taker) {
   const int lane = lane_id();
   const bool act = lane < ME_C;
   const int sl = lane & (ME_C - 1);
   HC_MARK(h);
   HMARK("take-entry");
-  while (rem) {
+  while (rem && O.n) {
     HMARK("take-level");
-    if (!O.n) return;  // the side is empty (a list runs dry only with it)
-    const int m0 = rli32(O.m, 0);
-    if (m0 > lim) return;
-    const int lvl = side_lvl(h, O.k, m0);
-    uint32_t hd = rl32(O.hd, 0);
-    const uint32_t tl = rl32(O.tl, 0);
-    const uint32_t r = rl32(O.row, 0);
-    long long tot = rli64(O.tot, 0);
-    const long long price = h.base + lvl;
-    int* rq = h.H->cq[O.k][r];
-    unsigned long long* rs = h.H->cs[O.k][r];
-    uint32_t taken = 0;
-    HC_ADD(h, HC_TAKEHEAD);
+    const int f = O.f;
+    const int m0 = rli32(O.m, f);
+    if (m0 > lim) break;
+    const int lvl = side_lvl(h, K, m0);
+    const uint32_t hd = rl32(O.hd, f), tl = rl32(O.tl, f), r = rl32(O.row, f);
+    const long long tot = rli64(O.tot, f);
     if (ME_UNLIKELY(hd >= h.nchunks)) {  // a corrupt list entry: never index with it
       if (lane == 0) atomicOr(h.err, ERR_INCONSISTENT);
       rem = 0;
-      return;
+      break;
     }
-    for (;;) {  // the level's chunks, head first
-      HMARK("take-chunk");
-      const int q_ = rq[sl];
-      const unsigned long long mseq = vreg64(rs[sl]);
-      const uint32_t uq = act ? (uint32_t)q_ : 0u;
-      const uint32_t inc = scan16_sat(uq);
-      const uint32_t ex = inc - uq;
-      uint32_t fq = rem > ex ? rem - ex : 0u;
-      fq = fq < uq ? fq : uq;
-      const bool fe = fq != 0u;
-      const unsigned long long fm = __ballot(fe);
-      if (fe) {
-        me_fill F;
-        F.taker_seq = taker;
-        F.maker_seq = mseq;
-        F.price_q4 = price;
-        F.qty = (int)fq;
-        F.symbol = h.gs;
-        if (!ABL(1)) h.scratch[h.wptr + (unsigned long long)__builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u)] = F;
-        rq[sl] = (int)(uq - fq);
-        if (!ABL(2)) h.chunks[hd].qty[sl] = (int)(uq - fq);
-      }
-      h.wptr += (unsigned long long)__popcll(fm);
-      h.resting -= __popcll(__ballot(fq == uq) & fm);
-      const uint32_t live = rl32(inc, 15);
-      const uint32_t t = rem < live ? rem : live;
-      rem -= t;
-      taken += t;
-      HMARK("take-chunk-done");
-      if (__ballot(uq > fq) & 0xFFFFull) break;  // live slots remain: the taker is done
-      // the chunk is exhausted (its HBM slots read 0 already): free it, go on down the FIFO
-      hot_free(h, hd);
-      if (hd == tl) break;
-      const uint32_t nx = rl32(O.hn, 0);
-      if (ME_UNLIKELY(nx >= h.nchunks)) {  // a corrupt FIFO: stop the taker, report it
-        if (lane == 0) atomicOr(h.err, ERR_INCONSISTENT);
-        rem = 0;
-        return;
-      }
-      // the next chunk of a multi-chunk level: the one load of a walk (the chain's own stores to it
-      // land first)
-      HEV(h, HEV_ADVANCE);
-      hot_drain();
-      const int nq = h.chunks[nx].qty[sl];
-      const unsigned long long ns = h.chunks[nx].seq[sl];
-      const uint32_t nn = h.chunks[nx].hdr.next;
-      __builtin_amdgcn_s_waitcnt(0);
-      if (act) {
-        rq[sl] = nq;
-        rs[sl] = ns;
-      }
-      if (lane == 0) h.chunks[nx].hdr.prev = NIL;
-      hd = nx;
-      O.hd = lane == 0 ? nx : O.hd;
-      O.hn = lane == 0 ? rl32(nn, 0) : O.hn;
-      if (!rem) break;
+    int* rq = h.H->cq[K][r];
+    unsigned long long* rs = h.H->cs[K][r];
+    HC_ADD(h, HC_TAKEHEAD);
+    HMARK("take-chunk");
+    const int q_ = rq[sl];
+    const unsigned long long mseq = vreg64(rs[sl]);
+    const uint32_t uq = act ? (uint32_t)q_ : 0u;
+    const uint32_t inc = scan16_sat(uq);
+    const uint32_t ex = inc - uq;
+    uint32_t fq = rem > ex ? rem - ex : 0u;
+    fq = fq < uq ? fq : uq;
+    const bool fe = fq != 0u;
+    const unsigned long long fm = __ballot(fe);
+    if (fe) {
+      me_fill F;
+      F.taker_seq = taker;
+      F.maker_seq = mseq;
+      F.price_q4 = h.base + lvl;
+      F.qty = (int)fq;
+      F.symbol = h.gs;
+      if (!ABL(1)) h.scratch[h.wptr + (unsigned long long)__builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u)] = F;
+      rq[sl] = (int)(uq - fq);
+      if (!ABL(2)) h.chunks[hd].qty[sl] = (int)(uq - fq);
     }
-    tot -= taken;
+    h.wptr += (unsigned long long)__popcll(fm);
+    h.resting -= __popcll(__ballot(fq == uq) & fm);
+    const uint32_t live = rl32(inc, 15);
+    const uint32_t t = rem < live ? rem : live;
+    rem -= t;
+    const long long ntot = tot - t;
     HC_ADD(h, HC_CHUNK);
-    if (tot == 0) {  // the level emptied: pop it (record lanes of it learn: a later rest may find it deep)
+    HMARK("take-chunk-done");
+    if (__ballot(uq > fq) & 0xFFFFull) {  // live slots remain: the taker is done, the level stays
+      HMARK("take-partial");
+      O.tot = lane == f ? ntot : O.tot;
+      hot_level_store(h, lvl, ntot, hd, tl, rl32(O.te, f));
+      HC_ADD(h, HC_PARTIAL);
+      break;
+    }
+    // the chunk is exhausted (its HBM slots read 0 already)
+    hot_free(h, hd);
+    if (ntot == 0) {  // the level emptied: pop it (record lanes of it learn: a later rest may find it deep)
       HMARK("take-pop");
       HEV(h, HEV_POP);
       hot_level_store(h, lvl, 0, NIL, NIL, 0);
       hot_occ_set(h, lvl, false);
       hot_broadcast(h, lvl, 0, NIL, NIL, 0);
-      // every entry one lane down; the front's row goes to lane 63 (free)
-      O.m = (int)lanes_down((uint32_t)O.m);
-      O.tot = lanes_down64(O.tot);
-      O.hd = lanes_down(O.hd);
-      O.tl = lanes_down(O.tl);
-      O.te = lanes_down(O.te);
-      O.hn = lanes_down(O.hn);
-      O.row = lanes_down(O.row);
+      O.f = (f + 1) & (HT - 1);  // the front lane and its row join the free ones
       O.n -= 1;
-      if (!O.n && O.more) {
+      if (ME_UNLIKELY(!O.n && O.more)) {
         // the list ran dry with levels beyond it: rebuild it now, so that an empty list always means
         // an empty side (a scan from a mere bound could run into the other side's levels later: the
         // occupancy bitmap holds both)
@@ -1793,28 +1736,51 @@ __device__ __forceinline__ void hot_take(HotState& h, HSide& O, int lim, uint32_
       HMARK("take-pop-done");
       continue;
     }
-    HMARK("take-partial");
-    O.tot = lane == 0 ? tot : O.tot;
-    hot_level_store(h, lvl, tot, hd, tl, rl32(O.te, 0));
-    HC_ADD(h, HC_PARTIAL);
-    return;
+    // a multi-chunk level: its head moves to the next chunk (the one load of a walk; the chain's own
+    // stores to it land first); the next pass takes from it
+    const uint32_t nx = rl32(O.hn, f);
+    if (ME_UNLIKELY(hd == tl || nx >= h.nchunks)) {  // a corrupt FIFO: stop the taker, report it
+      if (lane == 0) atomicOr(h.err, ERR_INCONSISTENT);
+      rem = 0;
+      break;
+    }
+    HEV(h, HEV_ADVANCE);
+    hot_drain();
+    const int nq = h.chunks[nx].qty[sl];
+    const unsigned long long ns = h.chunks[nx].seq[sl];
+    const uint32_t nn = h.chunks[nx].hdr.next;
+    __builtin_amdgcn_s_waitcnt(0);
+    if (act) {
+      rq[sl] = nq;
+      rs[sl] = ns;
+    }
+    if (lane == 0) h.chunks[nx].hdr.prev = NIL;
+    O.hd = lane == f ? nx : O.hd;
+    O.hn = lane == f ? rl32(nn, 0) : O.hn;
+    O.tot = lane == f ? ntot : O.tot;
+    if (!rem) {
+      hot_level_store(h, lvl, ntot, nx, tl, rl32(O.te, f));
+      break;
+    }
   }
 }
 
-// Rest (seq, q) on list M at side coordinate mm (window level lvl); record lane kr holds the level's
-// state. False: the chunk pool is exhausted.
+// Rest (seq, q) on list M (side K) at side coordinate mm (window level lvl); record lane kr holds the
+// level's state. False: the chunk pool is exhausted.
+template <int K>
 __device__ __forceinline__ bool hot_rest(HotState& h, WaveCtx& c, HSide& M, int mm, int lvl, unsigned long long seq,
                                          int q, int kr) {
   const int lane = lane_id();
   HC_MARK(h);
   HMARK("rest-entry");
-  const bool ent = lane < M.n;
+  const int rel = (lane - M.f) & (HT - 1);
+  const bool ent = rel < M.n;
   const int p = __popcll(__ballot(ent && M.m < mm));  // entries better than the level
   HC_ADD(h, HC_RESTHEAD);
-  if (p < M.n && rli32(M.m, p) == mm) {  // a listed level: append
+  if (p < M.n && rli32(M.m, hlane(M, p)) == mm) {  // a listed level: append
     HMARK("rest-append");
     HEV(h, HEV_APPEND);
-    const int j = p;
+    const int j = hlane(M, p);
     const uint32_t te = rl32(M.te, j), tl = rl32(M.tl, j), hd = rl32(M.hd, j);
     const long long tot = rli64(M.tot, j) + q;
     uint32_t ntl = tl, nte = te + 1;
@@ -1826,8 +1792,8 @@ __device__ __forceinline__ bool hot_rest(HotState& h, WaveCtx& c, HSide& M, int 
       if (tl == hd) {
         const uint32_t r = rl32(M.row, j);
         if (lane == 0) {
-          h.H->cq[M.k][r][te] = q;
-          h.H->cs[M.k][r][te] = seq;
+          h.H->cq[K][r][te] = q;
+          h.H->cs[K][r][te] = seq;
         }
       }
       if (lane == 0) {
@@ -1865,22 +1831,40 @@ __device__ __forceinline__ bool hot_rest(HotState& h, WaveCtx& c, HSide& M, int 
     hot_new_chunk(h, ch, NIL, lvl, seq, q);
     hot_level_store(h, lvl, q, ch, ch, 1);
     hot_occ_set(h, lvl, true);
-    const uint32_t r = rl32(M.row, HT - 1);  // a free row (M.n < HT)
-    const bool up = lane > p, at = lane == p;
-    const int um = (int)lanes_up((uint32_t)M.m);
-    const long long utot = lanes_up64(M.tot);
-    const uint32_t uhd = lanes_up(M.hd), utl = lanes_up(M.tl), ute = lanes_up(M.te), uhn = lanes_up(M.hn),
-                   urow = lanes_up(M.row);
-    M.m = up ? um : (at ? mm : M.m);
-    M.tot = up ? utot : (at ? (long long)q : M.tot);
-    M.hd = up ? uhd : (at ? ch : M.hd);
-    M.tl = up ? utl : (at ? ch : M.tl);
-    M.te = up ? ute : (at ? 1u : M.te);
-    M.hn = up ? uhn : (at ? NIL : M.hn);
-    M.row = up ? urow : (at ? r : M.row);
+    int j;
+    uint32_t r;
+    if (p == 0) {  // a new best: the front moves one lane back, onto a free lane and its row
+      M.f = (M.f - 1) & (HT - 1);
+      j = M.f;
+      r = rl32(M.row, j);
+    } else {  // entries p.. move one lane up (the ring rotates under them); the new one takes the
+              // row of the first free lane
+      j = hlane(M, p);
+      r = rl32(M.row, hlane(M, M.n));
+      const bool up = rel > p && rel <= M.n;
+      const int um = (int)lanes_up((uint32_t)M.m);
+      const long long utot = lanes_up64(M.tot);
+      const uint32_t uhd = lanes_up(M.hd), utl = lanes_up(M.tl), ute = lanes_up(M.te), uhn = lanes_up(M.hn),
+                     urow = lanes_up(M.row);
+      M.m = up ? um : M.m;
+      M.tot = up ? utot : M.tot;
+      M.hd = up ? uhd : M.hd;
+      M.tl = up ? utl : M.tl;
+      M.te = up ? ute : M.te;
+      M.hn = up ? uhn : M.hn;
+      M.row = up ? urow : M.row;
+    }
+    const bool at = lane == j;
+    M.m = at ? mm : M.m;
+    M.tot = at ? (long long)q : M.tot;
+    M.hd = at ? ch : M.hd;
+    M.tl = at ? ch : M.tl;
+    M.te = at ? 1u : M.te;
+    M.hn = at ? NIL : M.hn;
+    M.row = at ? r : M.row;
     if (lane < ME_C) {
-      h.H->cq[M.k][r][lane] = lane == 0 ? q : 0;
-      h.H->cs[M.k][r][lane] = lane == 0 ? seq : 0ull;
+      h.H->cq[K][r][lane] = lane == 0 ? q : 0;
+      h.H->cs[K][r][lane] = lane == 0 ? seq : 0ull;
     }
     M.n += 1;
     hot_broadcast(h, lvl, q, ch, ch, 1);
@@ -1963,7 +1947,8 @@ __device__ __forceinline__ void hot_topup(HotState& h, WaveCtx& c) {
 __device__ bool hot_check_side(HotState& h, const HSide& S, int other_best, unsigned long long seq, int what) {
   const int lane = lane_id();
   const int L = (int)h.L;
-  const bool ent = lane < S.n;
+  const int rel = (lane - S.f) & (HT - 1);
+  const bool ent = rel < S.n;
   bool bad = false;
   int code = 0;
   long long a0 = 0, a1 = 0;
@@ -2007,7 +1992,10 @@ __device__ bool hot_check_side(HotState& h, const HSide& S, int other_best, unsi
   const int n2 = S.k ? hot_scan<1>(h, other_best + 1, sl, more) : hot_scan<0>(h, other_best - 1, sl, more);
   if (!bad && S.n > n2) bad = true, code = 12, a0 = S.n, a1 = n2;
   if (!bad && !S.n && n2) bad = true, code = 14, a0 = rli32(sl, 0), a1 = n2;
-  if (!bad && lane < S.n && l != sl) bad = true, code = 15, a0 = l, a1 = sl;
+  {
+    const int mine = __shfl(l, hlane(S, lane), 64);  // entry `lane` of the list
+    if (!bad && lane < S.n && mine != sl) bad = true, code = 15, a0 = mine, a1 = sl;
+  }
   {  // the rows are a permutation of 0..63
     unsigned long long seen = 0;
     for (int i = 0; i < HT; ++i) seen |= 1ull << (rl32(S.row, i) & 63u);
@@ -2023,8 +2011,8 @@ __device__ bool hot_check_side(HotState& h, const HSide& S, int other_best, unsi
 }
 __device__ bool hot_check_lists(HotState& h, unsigned long long seq, int what) {
   const int L = (int)h.L;
-  const int fa = h.A.n ? side_lvl(h, h.A.k, rli32(h.A.m, 0)) : (h.A.k ? L : -1);
-  const int fb = h.B.n ? side_lvl(h, h.B.k, rli32(h.B.m, 0)) : (h.B.k ? L : -1);
+  const int fa = h.A.n ? side_lvl(h, h.A.k, rli32(h.A.m, h.A.f)) : (h.A.k ? L : -1);
+  const int fb = h.B.n ? side_lvl(h, h.B.k, rli32(h.B.m, h.B.f)) : (h.B.k ? L : -1);
   if (h.A.k == h.B.k) {
     if (lane_id() == 0) printf("HOTCHECK both lists hold side %d\n", h.A.k);
     return false;
@@ -2041,8 +2029,8 @@ __device__ bool hot_check_lists(HotState& h, unsigned long long seq, int what) {
   // record lanes of unlisted levels hold their HBM state
   const int l = h.rlvl;
   bool listed = false;
-  for (int i = 0; i < h.A.n; ++i) listed |= side_lvl(h, h.A.k, rli32(h.A.m, i)) == l;
-  for (int i = 0; i < h.B.n; ++i) listed |= side_lvl(h, h.B.k, rli32(h.B.m, i)) == l;
+  for (int i = 0; i < h.A.n; ++i) listed |= side_lvl(h, h.A.k, rli32(h.A.m, hlane(h.A, i))) == l;
+  for (int i = 0; i < h.B.n; ++i) listed |= side_lvl(h, h.B.k, rli32(h.B.m, hlane(h.B, i))) == l;
   if (l >= 0 && !listed) {
     const Level x = h.lv[l];
     const uint32_t te = h.tend[l];
@@ -2154,12 +2142,12 @@ __device__ __forceinline__ void match_records_hot(HotState& h, WaveCtx& c, const
     classify();
     if (h.A.n < HT / 2 && h.A.more) {
       hot_drain();
-      hot_rebuild(h, h.A, rli32(h.A.m, 0));
+      hot_rebuild(h, h.A, rli32(h.A.m, h.A.f));
       HS_COUNT(CT_MISS);
     }
     if (h.B.n < HT / 2 && h.B.more) {
       hot_drain();
-      hot_rebuild(h, h.B, rli32(h.B.m, 0));
+      hot_rebuild(h, h.B, rli32(h.B.m, h.B.f));
       HS_COUNT(CT_MISS);
     }
     hot_prefetch(h);
@@ -2199,24 +2187,32 @@ __device__ __forceinline__ void match_records_hot(HotState& h, WaveCtx& c, const
       const bool buy = (kd & 3u) == ME_SIDE_BUY;
       const bool mkt = (kd >> 2) & 1u;
       const int lm = mkt ? 0 : rli32(h.rlvl, (int)k);  // the LIMIT's window level
-      if (h.A.k != (buy ? 1 : 0)) hswap(h.A, h.B);   // A: the side this record takes from
       const unsigned long long fstart = h.wptr;
       uint32_t rem = (uint32_t)q;
       HS_COUNT(CT_FAST);
-      hot_take(h, h.A, mkt ? L - 1 : (buy ? lm : L - 1 - lm), rem, seq);
-      HS(PH_SWEEP);
+      // A holds the asks, B the bids: a BUY takes from A and rests on B, a SELL the other way round
+      // (one instance of the code per side: no list state moves between registers)
+      bool rested = true;
+      if (buy) {
+        hot_take<1>(h, h.A, mkt ? L - 1 : lm, rem, seq);
+        HS(PH_SWEEP);
+        if (!mkt && rem) rested = hot_rest<0>(h, c, h.B, L - 1 - lm, lm, seq, (int)rem, (int)k);
+      } else {
+        hot_take<0>(h, h.B, mkt ? L - 1 : L - 1 - lm, rem, seq);
+        HS(PH_SWEEP);
+        if (!mkt && rem) rested = hot_rest<1>(h, c, h.A, lm, lm, seq, (int)rem, (int)k);
+      }
+      if (ME_UNLIKELY(!rested)) {
+        ok = false;  // the chunk pool is exhausted (sticky error word from alloc_chunk)
+        break;
+      }
       const int filled = q - (int)rem;
       const uint32_t nfill = (uint32_t)(h.wptr - fstart);
       uint8_t stt;
-      if (mkt) {
+      if (mkt)
         stt = rem == 0 ? ME_ST_FILLED : ME_ST_CANCELED;
-      } else {
-        if (rem && ME_UNLIKELY(!hot_rest(h, c, h.B, buy ? L - 1 - lm : lm, lm, seq, (int)rem, (int)k))) {
-          ok = false;  // the chunk pool is exhausted (sticky error word from alloc_chunk)
-          break;
-        }
+      else
         stt = rem == 0 ? ME_ST_FILLED : (filled > 0 ? ME_ST_PARTIALLY_FILLED : ME_ST_NEW);
-      }
       HS(PH_REST);
       HMARK("record-result");
       put_result(R, k, filled, (int)rem, nfill, stt, ME_RJ_NONE, fstart);

@@ -12,6 +12,7 @@ run() { timeout -s KILL 300 rocprofv3 --pmc $2 --kernel-include-regex k_match_ho
 run sq1 "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM" &&
 run sq2 "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH SQ_WAVES SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR SQ_WAIT_INST_LDS" || exit 1
 run ic "SQ_IFETCH SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE" || echo "icache pass failed"
+python3 tools/pmc_last.py $O 3 34500; exit 0
 python3 - <<PY
 import csv,glob,collections
 acc=collections.defaultdict(list)
