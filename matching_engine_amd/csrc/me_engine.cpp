@@ -32,7 +32,8 @@ hipError_t launch_sort_pass(hipStream_t st, const uint32_t* keys_in, const uint3
                             const uint64_t* seq, const uint8_t* kind, uint32_t* err);
 hipError_t launch_seq_sweep(hipStream_t st, const BookDev& bk, const uint64_t* const* seq, const uint8_t* const* kind,
                             const uint32_t* n, uint32_t ng, uint32_t in_idx, uint32_t grid, uint32_t launch);
-hipError_t launch_match(hipStream_t st, const BookDev& bk, const BatchDev& bt, hipEvent_t ev0, hipEvent_t ev1);
+hipError_t launch_match(hipStream_t st, const BookDev& bk, const BatchDev& bt, hipEvent_t ev0, hipEvent_t ev1,
+                        const HotLaunch& hot);
 hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* bt, uint32_t ng, const AuxDev& ax, hipEvent_t ev0,
                             hipEvent_t ev1);
 uint32_t sort_tile(uint32_t n);
@@ -169,6 +170,7 @@ struct me_engine {
   int dev = 0;
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
+  HotLaunch hot;  // deep windows with hot symbols: k_match_hot's stream and fork / join events
   BookDev bk{};
   std::vector<int64_t> base_host;
   // grouping sort plan
@@ -351,6 +353,9 @@ static void free_all(me_engine* e) {
   for (auto ev : e->ev_pool) (void)hipEventDestroy(ev);
   e->ev_pool.clear();
   e->timed.clear();
+  if (e->hot.fork) (void)hipEventDestroy(e->hot.fork);
+  if (e->hot.join) (void)hipEventDestroy(e->hot.join);
+  if (e->hot.st) (void)hipStreamDestroy(e->hot.st);
   if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
 }
 
@@ -495,6 +500,12 @@ extern "C" me_engine* me_create(const me_config* cfg) {
   {
     const char* v = getenv("ME_HOT_MIN");
     bk.hot_min = L > LDS_MAX_LEVELS ? (v ? (uint32_t)atoi(v) : 512u) : 0u;
+    if (bk.hot_min) {
+      if ((he = hipStreamCreateWithFlags(&e->hot.st, hipStreamNonBlocking)) != hipSuccess ||
+          (he = hipEventCreateWithFlags(&e->hot.fork, hipEventDisableTiming)) != hipSuccess ||
+          (he = hipEventCreateWithFlags(&e->hot.join, hipEventDisableTiming)) != hipSuccess)
+        return bail(std::string("hot stream: ") + hipGetErrorString(he));
+    }
   }
   // old-order table: live orders <= resting, at load <= 1/2
   uint64_t oldn = 1024;
@@ -950,7 +961,7 @@ static int enqueue_batch(me_engine* e, const uint64_t* seq, const int64_t* px, c
   bt.bin_start = run_table;  // bins are symbols: the run table
   // timing: the launch itself records start/end (hipExtLaunchKernelGGL), no marker packets
   const uint64_t gen = ++e->oset_gen[oset];
-  hipError_t he = launch_match(st, e->bk, bt, tl.m0, tl.m1);
+  hipError_t he = launch_match(st, e->bk, bt, tl.m0, tl.m1, e->hot);
   if (he != hipSuccess) return e->hip_fail(he, "match launch");
   e->adm_matched += nadm;
   e->adm_at[++e->launch_no % me_engine::ADM_RING] = e->adm_matched;

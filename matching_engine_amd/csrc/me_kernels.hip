@@ -1213,20 +1213,7 @@ __global__ __launch_bounds__(256) void k_match(BookDev bk, BatchDev bt) {
     reject_bad_symbols(bt, lo, hi);
     return;
   }
-  if (kLad == LAD_HBM && bk.hot_min && hi - lo >= bk.hot_min && bk.L <= HOT_MAX_WORDS * 64u) {
-    // a hot symbol: k_match_hot takes it (launched right after this kernel)
-    uint32_t idx = 0;
-    if (lane == 0) idx = atomicAdd(bk.hcount, 1u);
-    idx = rl32(idx, 0);
-    if (lane == 0) {
-      Handoff ho{};
-      ho.s = s;
-      ho.pos = lo;
-      ho.nsg = hi;
-      bk.hand[idx] = ho;
-    }
-    return;
-  }
+  if (kLad == LAD_HBM && bk.hot_min && hi - lo >= bk.hot_min) return;  // k_match_hot's (k_hot_pick)
   const uint32_t L = bk.L;
   Level* g_lv = bk.levels + (size_t)s * L;
   unsigned long long* g_occ = bk.occ + (size_t)s * bk.Lwords;
@@ -1428,14 +1415,19 @@ __device__ __forceinline__ void hot_occ_load(HotState& h) {
   for (uint32_t i = (uint32_t)lane_id(); i < h.W; i += 64) h.H->occ[i] = h.occ[i];
   wave_mem_order();
 }
+// Non-returning atomics on both copies: nothing in the chain waits for them (a read-modify-write
+// would wait for the LDS read).
 __device__ __forceinline__ void hot_occ_set(HotState& h, int lvl, bool on) {
   const uint32_t w = (uint32_t)lvl >> 6;
   const unsigned long long bit = 1ull << (lvl & 63);
   if (lane_id() == 0) {
-    const unsigned long long o = h.H->occ[w];
-    const unsigned long long v = on ? (o | bit) : (o & ~bit);
-    h.H->occ[w] = v;
-    if (!ABL(8)) h.occ[w] = v;
+    if (on) {
+      __atomic_fetch_or(&h.H->occ[w], bit, __ATOMIC_RELAXED);
+      if (!ABL(8)) __atomic_fetch_or(&h.occ[w], bit, __ATOMIC_RELAXED);
+    } else {
+      __atomic_fetch_and(&h.H->occ[w], ~bit, __ATOMIC_RELAXED);
+      if (!ABL(8)) __atomic_fetch_and(&h.occ[w], ~bit, __ATOMIC_RELAXED);
+    }
   }
 }
 
@@ -2231,7 +2223,46 @@ __device__ __forceinline__ void match_records_hot(HotState& h, WaveCtx& c, const
   while (c.bump_cur < c.bump_end) hot_free_slow(&c, c.bump_cur++);
 }
 
-// One wave per hot symbol of the launch (k_match handed them over: bk.hand[i] = {s, pos = lo, nsg = hi}).
+// The hot symbols of a launch (at least hot_min records in the batch) into bk.hand[] = {s, pos = lo,
+// nsg = hi}: one thread per symbol over the run table. k_match skips them; k_match_hot, on a second
+// stream, runs them concurrently.
+// Without a run table (a multi-pass sort), one thread per grouped position: a run start whose run
+// reaches hot_min records finds the run's end by a binary search.
+__global__ __launch_bounds__(256) void k_hot_pick(BookDev bk, BatchDev bt) {
+  const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+  uint32_t s, lo, hi;
+  if (bt.bin_start) {
+    s = t;
+    if (s >= bk.S) return;
+    lo = bt.bin_start[s];
+    hi = bt.bin_start[s + 1];
+  } else {
+    const uint32_t n = bt.n;
+    if (t >= n) return;
+    s = bt.skeys[t];
+    if (s >= bk.S || (t > 0 && bt.skeys[t - 1] == s)) return;  // not a run start (or the reject bin)
+    if (t + bk.hot_min > n || bt.skeys[t + bk.hot_min - 1] != s) return;  // too short to be hot
+    uint32_t a = t + bk.hot_min, b = n;  // the run ends in [a - 1, b): first position with a larger key
+    while (a < b) {
+      const uint32_t m = (a + b) / 2;
+      if (bt.skeys[m] == s)
+        a = m + 1;
+      else
+        b = m;
+    }
+    lo = t;
+    hi = a;
+  }
+  if (hi - lo < bk.hot_min) return;
+  const uint32_t idx = atomicAdd(bk.hcount, 1u);
+  Handoff ho{};
+  ho.s = s;
+  ho.pos = lo;
+  ho.nsg = hi;
+  bk.hand[idx] = ho;
+}
+
+// One wave per hot symbol of the launch (k_hot_pick listed them: bk.hand[i] = {s, pos = lo, nsg = hi}).
 __global__ __launch_bounds__(64) void k_match_hot(BookDev bk, BatchDev bt) {
   __shared__ HotLds H;
   const uint32_t nh = min(*(volatile uint32_t*)bk.hcount, bk.S);
@@ -2459,23 +2490,55 @@ hipError_t launch_sort_pass(hipStream_t st, const uint32_t* keys_in, const uint3
   return hipGetLastError();
 }
 
+namespace rc64 {
 hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* bt, uint32_t ng, const AuxDev& ax,
                             hipEvent_t ev0, hipEvent_t ev1);
+}
+namespace rc128 {
+hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* bt, uint32_t ng, const AuxDev& ax,
+                            hipEvent_t ev0, hipEvent_t ev1);
+}
+// The register-ladder launch (me_match_reg.hip, two builds): one head-cache entry per level while one
+// workgroup per CU covers the symbols (rc128), 64 shared entries and two workgroups per CU beyond
+// that (rc64). ax.nwg is the CU count (0: assume 256).
+hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* bt, uint32_t ng, const AuxDev& ax,
+                            hipEvent_t ev0, hipEvent_t ev1) {
+  constexpr uint32_t kWaves = 4;  // matching waves per workgroup (me_match_reg.hip REG_WAVES)
+  const uint32_t waves = ng && bt[0].bcnt ? bk.S : bk.S + 1;
+  const uint32_t wgs = (waves + kWaves - 1) / kWaves;
+  const uint32_t ncu = ax.nwg ? ax.nwg : 256u;
+  return wgs > ncu ? rc64::launch_match_reg(st, bk, bt, ng, ax, ev0, ev1)
+                   : rc128::launch_match_reg(st, bk, bt, ng, ax, ev0, ev1);
+}
 
 // ev0 / ev1 (optional, timing): the launch records the kernel's own start and end
 // (hipExtLaunchKernelGGL), so timing adds no marker packet — and no gap — to the stream.
-hipError_t launch_match(hipStream_t st, const BookDev& bk, const BatchDev& bt, hipEvent_t ev0, hipEvent_t ev1) {
+// hot (deep windows with bk.hot_min): the stream and fork / join events k_match_hot runs with, beside
+// k_match (same symbols never meet: k_match skips what k_hot_pick listed).
+hipError_t launch_match(hipStream_t st, const BookDev& bk, const BatchDev& bt, hipEvent_t ev0, hipEvent_t ev1,
+                        const HotLaunch& hot) {
   const uint32_t waves = bk.S + 1;
   const dim3 grid((waves + 3) / 4), block(256);
   if (bk.L <= 128) {
     return launch_match_reg(st, bk, &bt, 1u, AuxDev{}, ev0, ev1);
   } else if (bk.L <= LDS_MAX_LEVELS) {
     hipExtLaunchKernelGGL(k_match<LAD_LDS>, grid, block, 4 * lds_wave_bytes(bk.L), st, ev0, ev1, 0, bk, bt);
-  } else if (!bk.hot_min) {
-    hipExtLaunchKernelGGL(k_match<LAD_HBM>, grid, block, 0, st, ev0, ev1, 0, bk, bt);
-  } else {  // hot symbols go on to k_match_hot (a few one-wave workgroups; hcount zeroed by k_seq_sweep)
-    hipExtLaunchKernelGGL(k_match<LAD_HBM>, grid, block, 0, st, ev0, nullptr, 0, bk, bt);
-    hipExtLaunchKernelGGL(k_match_hot, dim3(64), dim3(64), 0, st, nullptr, ev1, 0, bk, bt);
+  } else if (!bk.hot_min || !hot.st || bk.L > HOT_MAX_WORDS * 64u) {
+    BookDev b2 = bk;
+    b2.hot_min = 0;
+    hipExtLaunchKernelGGL(k_match<LAD_HBM>, grid, block, 0, st, ev0, ev1, 0, b2, bt);
+  } else {
+    // hcount was zeroed by k_seq_sweep; the pick starts the timed span, the join ends it
+    const uint32_t pick = bt.bin_start ? bk.S : bt.n;
+    hipExtLaunchKernelGGL(k_hot_pick, dim3((pick + 255) / 256), dim3(256), 0, st, ev0, nullptr, 0, bk, bt);
+    hipError_t e;
+    if ((e = hipEventRecord(hot.fork, st)) != hipSuccess || (e = hipStreamWaitEvent(hot.st, hot.fork, 0)) != hipSuccess)
+      return e;
+    hipLaunchKernelGGL(k_match_hot, dim3(64), dim3(64), 0, hot.st, bk, bt);
+    if ((e = hipEventRecord(hot.join, hot.st)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_match<LAD_HBM>, grid, block, 0, st, bk, bt);
+    if ((e = hipStreamWaitEvent(st, hot.join, 0)) != hipSuccess) return e;
+    if (ev1 && (e = hipEventRecord(ev1, st)) != hipSuccess) return e;
   }
   return hipGetLastError();
 }

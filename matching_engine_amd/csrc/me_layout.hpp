@@ -148,6 +148,13 @@ struct Handoff {
   uint32_t pad[2];
 };
 
+// Host side of a deep-window launch with hot symbols: k_match_hot runs on `st`, forked from and joined
+// back into the engine stream by two events (me_kernels.hip launch_match).
+struct HotLaunch {
+  hipStream_t st = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+
 // Event counters kept on the device (BookDev::stats, me_stats_read).
 // ST_RESTING: resting orders of every symbol (each wave adds its symbol's change when it writes the
 // symbol state back); k_seq_sweep publishes it to the host for admission control (me_engine.cpp).
@@ -231,7 +238,8 @@ struct BatchDev {
 // order, so a launch costs the heaviest symbol's share of the whole group rather than the sum of
 // each batch's heaviest share.
 #ifndef ME_GROUP_MAX
-#define ME_GROUP_MAX 64
+#define ME_GROUP_MAX 32  // (the launch arguments k_match_reg copies to LDS grow with it: 32 leaves room
+                         // for two workgroups per CU)
 #endif
 constexpr int ME_GMAX = ME_GROUP_MAX;
 constexpr uint32_t ME_DEFAULT_GROUP = 32;

@@ -37,21 +37,46 @@
 #include "me_layout.hpp"
 #include "me_wave.hpp"
 
+// Compiled twice (Makefile): rc128 (a head-chunk cache entry per level, one workgroup per CU) and
+// rc64 (64 shared entries, half the LDS: two workgroups per CU). launch_match_reg (me_kernels.hip)
+// takes rc128 while the grid fits the chip — every symbol's chain has a SIMD to itself, no entry is
+// ever evicted — and rc64 beyond it, where two matching waves per SIMD hide each other's latency
+// (same-box A/B, DESIGN.md §4: config 2 1,056 vs 888M, config 3 777 vs 1,231M orders/s).
+#ifndef ME_REG_VARIANT
+#define ME_REG_VARIANT rc64
+#endif
 namespace me {
+namespace ME_REG_VARIANT {
 
 constexpr int RL = 128;  // levels covered by this kernel
+#ifndef ME_REG_CACHE
+#define ME_REG_CACHE 64
+#endif
+// Head-chunk cache entries per wave: level l uses entry l & (RC - 1). At 64, levels l and l + 64 share
+// an entry (the one cached is written back when the other comes in), which halves the wave's LDS so
+// that two matching workgroups fit a CU (two matching waves per SIMD) at grids beyond one per CU.
+constexpr int RC = ME_REG_CACHE;
+static_assert(RC == 64 || RC == 128, "head cache: 64 or 128 entries");
+// Rescan window (records of a batch scanned per pass for a bucket that overflowed): 64 * RSU.
+#ifndef ME_RESCAN_UNITS
+#define ME_RESCAN_UNITS 12
+#endif
+constexpr int RSU = ME_RESCAN_UNITS;
+constexpr uint32_t RSW = 64u * RSU;
+__device__ __forceinline__ int ce(int lvl) { return lvl & (RC - 1); }
 constexpr int FSTK = 64; // free chunk ids a wave keeps in its VGPR stack (= fcache row length)
 // Head-row flag: set unless cache entry l holds level l's head chunk (chunk ids stay below 2^31;
 // NIL, an empty level, reads as not cached).
 constexpr uint32_t HC = 0x80000000u;
 
-// One wave's LDS: the head-chunk cache (entry l = head chunk of level l) and the level totals.
+// One wave's LDS: the head-chunk cache (entry ce(l) = head chunk of level l when l is cached) and the
+// level totals.
 struct RegLds {
-  int cq[RL][ME_C];
-  unsigned long long cs[RL][ME_C];
+  int cq[RC][ME_C];
+  unsigned long long cs[RC][ME_C];
   long long tot[RL];
   long long tdummy[64];  // tot_add: the slots of lanes 1..63
-  uint32_t cnext[RL];  // chunks[head].hdr.next of the cached head (kept in step with HBM)
+  uint32_t cnext[RC];  // chunks[head].hdr.next of the cached head (kept in step with HBM)
   uint32_t free_head;  // overflow free list in HBM (hdr.next links), NIL if empty
   uint32_t bump_cur, bump_end;  // chunk ids reserved from the global bump allocator
   uint32_t resting0;  // the symbol's resting orders when the wave started (ST_RESTING delta)
@@ -72,7 +97,7 @@ struct RegLds {
       int qty[BK_CAP];
       uint32_t ok[BK_CAP];
     } b;
-    uint32_t lst[1024];  // rescan: batch indices of the symbol's records in one 1024-record window
+    uint32_t lst[RSW];  // rescan: batch indices of the symbol's records in one RSW-record window
   } in;
 };
 #ifndef ME_REG_WAVES
@@ -292,6 +317,24 @@ __device__ __forceinline__ uint32_t RegCtx::falloc() { return reg_alloc(*this); 
 __device__ __forceinline__ void RegCtx::ffree(uint32_t ch) { reg_free(*this, ch); }
 
 // ---- head-chunk cache ------------------------------------------------------------------------
+// Level lvl's head is about to enter entry ce(lvl): if the level sharing the entry holds it, that
+// level's head goes back to HBM and becomes uncached (its head row gets HC again).
+__device__ __forceinline__ void reg_evict_partner(RegCtx& c, int lvl) {
+  if constexpr (RC < RL) {
+    const int p = lvl ^ RC;
+    const uint32_t hv = c.hd.get(p);
+    if (ME_UNLIKELY((hv & HC) == 0u)) {
+      const int lane = lane_id();
+      const int e = ce(lvl);
+      if (lane < ME_C) {
+        c.chunks[hv].qty[lane] = c.M->cq[e][lane];
+        c.chunks[hv].seq[lane] = c.M->cs[e][lane];
+      }
+      c.hd.put(p, hv | HC);
+    }
+  }
+}
+
 // Miss: copy chunk ch (the head of level lvl) into cache entry lvl. The only global load of a walk;
 // its registers die at the LDS writes, so no wait on it leaks into the hit path.
 __device__ __forceinline__ bool reg_fill_entry(RegCtx& c, int lvl, uint32_t ch) {
@@ -308,10 +351,10 @@ __device__ __forceinline__ bool reg_fill_entry(RegCtx& c, int lvl, uint32_t ch) 
   // LDS writes below would make the compiler wait for it (and all later stores) in the hit path.
   __builtin_amdgcn_s_waitcnt(VMCNT0);
   if (lane < ME_C) {
-    c.M->cq[lvl][sl] = qv;
-    c.M->cs[lvl][sl] = sv;
+    c.M->cq[ce(lvl)][sl] = qv;
+    c.M->cs[ce(lvl)][sl] = sv;
   }
-  if (lane == 0) c.M->cnext[lvl] = nx;
+  if (lane == 0) c.M->cnext[ce(lvl)] = nx;
   return true;
 }
 
@@ -325,10 +368,10 @@ __device__ __forceinline__ bool reg_take_chunk(RegCtx& c, int lvl, uint32_t& rem
   const bool act = lane < ME_C;
   const int sl = lane & (ME_C - 1);
   COUNT(c, CT_WALK);
-  const int q_ = c.M->cq[lvl][sl];
+  const int q_ = c.M->cq[ce(lvl)][sl];
   // read with the quantities (one LDS round trip); the opaque use keeps it from sinking into the
   // fill branch, where it would be a second round trip
-  const unsigned long long mseq = vreg64(c.M->cs[lvl][sl]);
+  const unsigned long long mseq = vreg64(c.M->cs[ce(lvl)][sl]);
   const uint32_t uq = act ? (uint32_t)q_ : 0u;
   const uint32_t inc = scan16_sat(uq);
   const uint32_t ex = inc - uq;
@@ -345,7 +388,7 @@ __device__ __forceinline__ bool reg_take_chunk(RegCtx& c, int lvl, uint32_t& rem
     F.symbol = c.gs;
     // fills only ever come from lanes 0..15: mbcnt_lo alone ranks them
     c.scratch[c.wptr + (uint32_t)__builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u)] = F;
-    c.M->cq[lvl][sl] = (int)(uq - f);
+    c.M->cq[ce(lvl)][sl] = (int)(uq - f);
   }
   c.wptr += (uint32_t)__popcll(fm);
   c.resting -= __popcll(__ballot(f == uq) & fm);  // makers filled completely leave the book
@@ -365,6 +408,7 @@ __device__ __forceinline__ bool reg_walk(RegCtx& c, int lvl, uint32_t& rem, unsi
   uint32_t ch = hv & ~HC;  // an occupied level: a real chunk id
   if (ME_UNLIKELY(hv & HC)) {
     COUNT(c, CT_MISS);
+    reg_evict_partner(c, lvl);
     if (!reg_fill_entry(c, lvl, ch)) return false;
     c.hd.put(lvl, ch);  // now cached
   }
@@ -377,7 +421,7 @@ __device__ __forceinline__ bool reg_walk(RegCtx& c, int lvl, uint32_t& rem, unsi
   const uint32_t tail = c.tl.get(lvl);
   bool cached = false;  // whether the level's new head ends up in the cache
   for (;;) {
-    const uint32_t nx = rl32(c.M->cnext[lvl], 0);
+    const uint32_t nx = rl32(c.M->cnext[ce(lvl)], 0);
     if (lane < ME_C) c.chunks[ch].qty[lane] = 0;  // a freed chunk must read all-zero in HBM
     reg_free(c, ch);
     if (ch == tail) {
@@ -422,18 +466,19 @@ __device__ __forceinline__ bool reg_rest_new_chunk(RegCtx& c, int lvl, unsigned 
     c.loc[seq & c.rmask] = ch * ME_C;
   }
   if (tl == NIL) {  // empty level: the new chunk is its head, installed in the cache
+    reg_evict_partner(c, lvl);
     c.hd.put(lvl, ch);  // cached
-    if (lane < ME_C) c.M->cq[lvl][lane] = lane == 0 ? (int)qty : 0;
+    if (lane < ME_C) c.M->cq[ce(lvl)][lane] = lane == 0 ? (int)qty : 0;
     if (lane == 0) {
-      c.M->cs[lvl][0] = seq;
-      c.M->cnext[lvl] = NIL;
+      c.M->cs[ce(lvl)][0] = seq;
+      c.M->cnext[ce(lvl)] = NIL;
     }
     c.occ.set(lvl);
   } else {
     const bool tl_cached = c.hd.get(lvl) == tl;  // the tail is the cached head
     if (lane == 0) {
       if (tl < c.nchunks) c.chunks[tl].hdr.next = ch;
-      if (tl_cached) c.M->cnext[lvl] = ch;
+      if (tl_cached) c.M->cnext[ce(lvl)] = ch;
       c.chunks[ch].qty[0] = (int)qty;
       c.chunks[ch].seq[0] = seq;
     }
@@ -456,8 +501,8 @@ __device__ __forceinline__ bool reg_rest(RegCtx& c, int lvl, unsigned long long 
     if (lane == 0) {
       // no branch on in_cache: the HBM slot is written either way (a cached tail is written back
       // from LDS at the end anyway) and the LDS copy goes to the entry or to a dummy slot
-      int* lq = in_cache ? &c.M->cq[lvl][te] : &c.M->dq;
-      unsigned long long* ls = in_cache ? &c.M->cs[lvl][te] : &c.M->dsq;
+      int* lq = in_cache ? &c.M->cq[ce(lvl)][te] : &c.M->dq;
+      unsigned long long* ls = in_cache ? &c.M->cs[ce(lvl)][te] : &c.M->dsq;
       *lq = (int)qty;
       *ls = seq;
       c.chunks[tl].qty[te] = (int)qty;
@@ -515,9 +560,9 @@ __device__ __forceinline__ uint32_t reg_cancel(RegCtx& c, unsigned long long tgt
       const uint32_t hv = c.hd.get(lvl);
       const bool in_cache = inw && hv == ch;  // ch is the cached head: the on-chip copy is authoritative
       if (in_cache) {
-        const int qc = c.M->cq[lvl][lane & (ME_C - 1)];
+        const int qc = c.M->cq[ce(lvl)][lane & (ME_C - 1)];
         qv = act ? qc : 0;
-        sq = rl64(c.M->cs[lvl][slot], 0);
+        sq = rl64(c.M->cs[ce(lvl)][slot], 0);
       }
       if (own == c.s && sq == tgt) {  // the order's slot: live or dead, it never moves
         const int q = rli32(qv, (int)slot);
@@ -534,7 +579,7 @@ __device__ __forceinline__ uint32_t reg_cancel(RegCtx& c, unsigned long long tgt
         const uint32_t live_after = (uint32_t)__popcll(__ballot(qv > 0)) - 1u;
         if (lane == 0) {
           if (in_cache)
-            c.M->cq[lvl][slot] = 0;
+            c.M->cq[ce(lvl)][slot] = 0;
           else
             c.chunks[ch].qty[slot] = 0;
         }
@@ -562,13 +607,13 @@ __device__ __forceinline__ uint32_t reg_cancel(RegCtx& c, unsigned long long tgt
             c.te.put(lvl, ME_C);  // a non-tail chunk is always full
             if (lane == 0) {
               c.chunks[prv].hdr.next = NIL;
-              if (mirror) c.M->cnext[lvl] = NIL;
+              if (mirror) c.M->cnext[ce(lvl)] = NIL;
             }
           } else {
             if (lane == 0) {
               c.chunks[prv].hdr.next = nxt;
               c.chunks[nxt].hdr.prev = prv;
-              if (mirror) c.M->cnext[lvl] = nxt;
+              if (mirror) c.M->cnext[ce(lvl)] = nxt;
             }
           }
           reg_free(c, ch);
@@ -646,7 +691,7 @@ __device__ __forceinline__ void reg_recentre(RegCtx& c, long long target) {
       const int jj = __builtin_ctzll(cm);
       cm &= cm - 1ull;
       const uint32_t cid = rl32(row ? c.hd.r1 : c.hd.r0, jj);
-      const int e = row * 64 + jj;
+      const int e = ce(row * 64 + jj);
       if (lane < ME_C) {
         c.chunks[cid].qty[lane] = c.M->cq[e][lane];
         c.chunks[cid].seq[lane] = c.M->cs[e][lane];
@@ -830,7 +875,7 @@ __device__ __forceinline__ void sort128(uint32_t& a, uint32_t& b) {
   b = bitonic_merge<64>(hi, true);
 }
 
-// Rescan of an overfull bucket: the next 1024-record window of the batch that holds records of
+// Rescan of an overfull bucket: the next RSW-record window of the batch that holds records of
 // bin s, as a list of batch indices in LDS (batch order). Returns false when the batch is done.
 __device__ __forceinline__ bool rescan_window(RegLds* M, const ColdArgs& G, uint32_t g, uint32_t s) {
   const int lane = lane_id();
@@ -838,19 +883,19 @@ __device__ __forceinline__ bool rescan_window(RegLds* M, const ColdArgs& G, uint
   const gptr<const uint32_t> sym = ldsg(G.bt[g].sym);
   uint32_t cur = ldsu(M->scan_cur);
   while (cur < n) {
-    uint32_t sy[16];
+    uint32_t sy[RSU];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) sy[u] = sym[min(cur + 64u * u + (uint32_t)lane, n - 1u)];
+    for (int u = 0; u < RSU; ++u) sy[u] = sym[min(cur + 64u * u + (uint32_t)lane, n - 1u)];
     uint32_t cnt = 0;
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
+    for (int u = 0; u < RSU; ++u) {
       const uint32_t idx = cur + 64u * u + (uint32_t)lane;
       const bool m = idx < n && min(sy[u], S) == s;
       const unsigned long long bm = __ballot(m);
       if (m) M->in.lst[cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u))] = idx;
       cnt += (uint32_t)__popcll(bm);
     }
-    cur += 1024u;
+    cur += RSW;
     if (cnt) {
       ldsw(M->scan_cur, cur);
       ldsw(M->scan_cnt, cnt);
@@ -1425,7 +1470,7 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
       if (lane == 0) ldsg(B.bcnt)[(size_t)s * BK_CNT_STRIDE] = 0u;  // ready for a later group's bucket job
       // ---- batch order. A bucket (<= BK_CAP records, arbitrary order) is staged in LDS and its keys
       // (batch index << 7 | bucket slot) sorted across the wave; an overfull bucket is replaced by a
-      // rescan of the batch (1024-record windows, batch order by construction).
+      // rescan of the batch (RSW-record windows, batch order by construction).
       mode = nsg <= (uint32_t)BK_CAP ? 0u : 1u;
       if (mode == 0u) {
         c.M->in.b.seq[lane] = bq0;
@@ -1686,7 +1731,7 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
       const int jj = __builtin_ctzll(d);
       d &= d - 1ull;
       const uint32_t cid = rl32(row ? c.hd.r1 : c.hd.r0, jj);
-      const int e = row * 64 + jj;
+      const int e = ce(row * 64 + jj);
       if (lane < ME_C) {
         c.chunks[cid].qty[lane] = c.M->cq[e][lane];
         c.chunks[cid].seq[lane] = c.M->cs[e][lane];
@@ -1795,4 +1840,5 @@ hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* b
   return hipGetLastError();
 }
 
+}  // namespace ME_REG_VARIANT
 }  // namespace me

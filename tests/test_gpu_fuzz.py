@@ -24,7 +24,7 @@ def _case(me, seed):
     levels = int(rng.choice([64, 128, 128, 256, 1024, 4096]))
     S = int(rng.choice([1, 3, 17, 64, 300]))
     batch = int(rng.choice([64, 500, 2048, 6000]))
-    group = int(rng.choice([1, 2, 7, 32, 64]))
+    group = int(rng.choice([1, 2, 7, 16, 32]))
     nb = int(rng.integers(6, 40))
     cancel = int(rng.choice([0, 10, 40]))
     market = int(rng.choice([5, 20]))
