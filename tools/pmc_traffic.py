@@ -15,10 +15,13 @@ import os
 import sys
 
 
-def per_dispatch(d, counter, kernel):
+def per_dispatch(d, counter, kernel, merge_next=None):
     """Counter per launch of `kernel`, in dispatch order. A continuation launch (the register kernel's
     `<true>` instance, which follows its common launch on the same stream) is added to the launch
-    it continues: together they are one launch group's matching."""
+    it continues: together they are one launch group's matching. Dispatches matching `merge_next`
+    (k_match_hot: launched, on its own stream, just before the k_match of the same batch) are added
+    to the next launch."""
+    import re
     vals = []
     for f in glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True):
         acc = {}
@@ -29,15 +32,19 @@ def per_dispatch(d, counter, kernel):
                 did = int(r.get("Dispatch_Id") or r.get("Dispatch-Id") or len(acc))
                 cont = "<true>" in name
                 v = float(r.get("Counter_Value") or r.get("Counter-Value"))
-                k = acc.setdefault(did, [cont, 0.0])
+                k = acc.setdefault(did, [cont, 0.0, name])
                 k[1] += v
         merged = []
+        carry = 0.0
         for did in sorted(acc):
-            cont, v = acc[did]
-            if cont and merged:
+            cont, v, name = acc[did]
+            if merge_next and re.search(merge_next, name):
+                carry += v
+            elif cont and merged:
                 merged[-1] += v
             elif not cont:
-                merged.append(v)
+                merged.append(v + carry)
+                carry = 0.0
         vals += merged
     return vals
 
@@ -54,9 +61,14 @@ def main():
         i = a.index("--orders-per-launch")
         orders = int(a[i + 1])
         del a[i:i + 2]
+    merge_next = None
+    if "--merge-next" in a:
+        i = a.index("--merge-next")
+        merge_next = a[i + 1]
+        del a[i:i + 2]
     fdir, wdir = a[0], a[1]
-    f = per_dispatch(fdir, "FETCH_SIZE", kernel)
-    w = per_dispatch(wdir, "WRITE_SIZE", kernel)
+    f = per_dispatch(fdir, "FETCH_SIZE", kernel, merge_next)
+    w = per_dispatch(wdir, "WRITE_SIZE", kernel, merge_next)
     if not f or not w:
         print(json.dumps({"error": "no samples", "fetch": len(f), "write": len(w)}))
         return 1
