@@ -61,6 +61,11 @@ def main():
         i = a.index("--orders-per-launch")
         orders = int(a[i + 1])
         del a[i:i + 2]
+    last = None
+    if "--last" in a:  # only the last N launches (the steady steps after warmup / seeding)
+        i = a.index("--last")
+        last = int(a[i + 1])
+        del a[i:i + 2]
     merge_next = None
     if "--merge-next" in a:
         i = a.index("--merge-next")
@@ -69,6 +74,8 @@ def main():
     fdir, wdir = a[0], a[1]
     f = per_dispatch(fdir, "FETCH_SIZE", kernel, merge_next)
     w = per_dispatch(wdir, "WRITE_SIZE", kernel, merge_next)
+    if last:
+        f, w = f[-last:], w[-last:]
     if not f or not w:
         print(json.dumps({"error": "no samples", "fetch": len(f), "write": len(w)}))
         return 1
