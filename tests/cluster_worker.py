@@ -154,7 +154,10 @@ def main():
     if rank != 0:
         cl.serve()
         res = {"refused": shard.refused if ops is not None else 0, "stats": cl.stats()}
-        json.dump(res, open(out_path + f".r{rank}", "w"))
+        tmp = out_path + f".r{rank}.tmp"
+        with open(tmp, "w") as f:
+            json.dump(res, f)
+        os.replace(tmp, out_path + f".r{rank}")  # rank 0 polls for the file: it appears complete
         cl.close()
         return
     ok, msg, direct_fills = (True, "", 0) if refuse else direct_slices(me, cl, S, world)
@@ -235,11 +238,15 @@ def main():
         import time
 
         path = out_path + f".r{world - 1}"
-        for _ in range(200):
+        for _ in range(400):
             if os.path.exists(path):
                 break
             time.sleep(0.05)
-        refused = json.load(open(path))["refused"] if world > 1 else shard.refused
+        if world > 1:
+            with open(path) as f:
+                refused = json.load(f)["refused"]
+        else:
+            refused = shard.refused
         if refused != 1:
             ok, msg = False, f"expected one refusal, saw {refused}"
     json.dump({"ok": ok, "msg": msg, "orders": nrows, "fill_rows": nfills, "world": world, "refused": refused,
