@@ -527,8 +527,8 @@ extern "C" me_engine* me_create(const me_config* cfg) {
   ALLOC(bk.far, S * 2 * (uint64_t)bk.fcap);
   ALLOC(bk.old, oldn);
   ALLOC(bk.sq, 2);
-  ALLOC(bk.hcount, 1);
-  ALLOC(bk.hand, S);
+  ALLOC(bk.hcount, 2);  // [0] hand-offs of a launch, [1] k_match_hot's continuations
+  ALLOC(bk.hand, 2 * S);  // continuations from S on
   ALLOC(bk.stats, ME_STATS);
   if ((he = hipHostMalloc((void**)&e->pub_host, sizeof(unsigned long long), hipHostMallocDefault)) != hipSuccess ||
       (he = hipHostGetDevicePointer((void**)&bk.pub, e->pub_host, 0)) != hipSuccess)
@@ -607,7 +607,7 @@ extern "C" me_engine* me_create(const me_config* cfg) {
             launch_init_chunks(st, bk.chunks, nchunks) == hipSuccess &&
             hipMemsetAsync(bk.loc, 0xFF, ring * sizeof(uint32_t), st) == hipSuccess &&
             hipMemsetAsync(bk.old, 0, oldn * sizeof(OldEnt), st) == hipSuccess &&
-            hipMemsetAsync(bk.hcount, 0, 4, st) == hipSuccess &&
+            hipMemsetAsync(bk.hcount, 0, 8, st) == hipSuccess &&
             hipMemsetAsync(bk.stats, 0, ME_STATS * 8, st) == hipSuccess &&
             hipMemcpyAsync(bk.sq, sq0, sizeof sq0, hipMemcpyHostToDevice, st) == hipSuccess &&
             hipMemsetAsync(bk.fcache, 0xFF, S * 64 * sizeof(uint32_t), st) == hipSuccess &&

@@ -1140,8 +1140,10 @@ __device__ __forceinline__ void match_records(WaveCtx& c, const BatchDev& bt, ui
   while (c.bump_cur < c.bump_end) free_chunk(c, c.bump_cur++);
 }
 
+// cont_w != ~0: a continuation (k_match_hot_cont) that writes its fills from cont_w on, inside the
+// scratch run the symbol's first wave reserved for all its records of the batch.
 __device__ __forceinline__ bool wave_begin(WaveCtx& c, const BookDev& bk, const BatchDev& bt, uint32_t s, uint32_t lo,
-                                           uint32_t hi) {
+                                           uint32_t hi, unsigned long long cont_w = ~0ull) {
   const int lane = lane_id();
   c.bk = bk;
   c.s = s;
@@ -1161,6 +1163,10 @@ __device__ __forceinline__ bool wave_begin(WaveCtx& c, const BookDev& bk, const 
   c.resting_delta = (int)rl32(st.resting, 0);  // becomes the new resting count
   c.resting0 = rl32(st.resting, 0);
   c.scratch = bt.scratch;
+  if (cont_w != ~0ull) {
+    c.wptr = cont_w;
+    return true;
+  }
   // scratch run of this wave: fills <= resting makers + 2 * records
   const unsigned long long need = (unsigned long long)rl32(st.resting, 0) + 2ull * (hi - lo);
   unsigned long long w0 = 0;
@@ -1280,9 +1286,10 @@ __global__ __launch_bounds__(256) void k_match(BookDev bk, BatchDev bt) {
 //   * the occupancy bitmap lives in LDS (windows up to HOT_MAX_WORDS * 64 levels);
 //   * free chunks in a VGPR stack.
 // Every change is written through to HBM at once (fire-and-forget global stores: nothing in the chain
-// waits for them), so the HBM book is always current: a record the lists do not cover — a cancel, a
-// price outside the window, a taker while far levels exist — runs through generic_record after one full
-// wait, and the lists and lane states are rebuilt behind it. Same semantics and HBM layout as k_match.
+// waits for them), so the HBM book is always current: at the first record the lists do not cover — a
+// cancel, a price outside the window, a taker while far levels exist — the wave hands the symbol's
+// remaining records to k_match_hot_cont (the generic record loop) and ends. Same semantics and HBM
+// layout as k_match.
 // The chain's state stays in registers (HotState): the generic code's WaveCtx lives in scratch memory
 // and is touched only at those sync points.
 constexpr int HT = 64;                  // list entries per side (one per lane)
@@ -1897,29 +1904,16 @@ __device__ __forceinline__ bool hot_rest(HotState& h, WaveCtx& c, HSide& M, int 
   return true;
 }
 
-// The generic code out of line: the hot loop's registers do not pay for it (its WaveCtx lives in
+// The generic allocator out of line: the hot loop's registers do not pay for it (its WaveCtx lives in
 // scratch memory anyway, since the generic helpers take its address).
-__device__ __noinline__ RecOut hot_generic_record(WaveCtx* c, unsigned long long seq, long long px, int q,
-                                                  uint32_t kind) {
-  return generic_record(*c, seq, px, q, kind);
-}
 __device__ __noinline__ uint32_t hot_alloc_slow(WaveCtx* c) { return alloc_chunk(*c); }
 __device__ __noinline__ void hot_free_slow(WaveCtx* c, uint32_t ch) { free_chunk(*c, ch); }
 
-// The generic path for record k (or the stack top-up) at a sync point: every store landed, the
-// WaveCtx takes the hot state, the generic code runs, the hot state and both lists come back.
+// The stack top-up (and the end of the wave) at a sync point: every store landed, the WaveCtx takes
+// the hot state.
 __device__ __forceinline__ void hot_sync_in(HotState& h, WaveCtx& c) {
   hot_drain();
   hot_to_wave(h, c);
-}
-__device__ __forceinline__ void hot_sync_out(HotState& h, const WaveCtx& c) {
-  wave_to_hot(c, h);
-  hot_drain();
-  hot_occ_load(h);
-  const int L = (int)h.L;
-  const int ba = rli32(c.ba, 0), bb = rli32(c.bb, 0);
-  hot_rebuild(h, h.A, h.A.k ? ba : L - 1 - bb);
-  hot_rebuild(h, h.B, h.B.k ? ba : L - 1 - bb);
 }
 __device__ __forceinline__ void hot_topup(HotState& h, WaveCtx& c) {
   hot_sync_in(h, c);
@@ -2101,8 +2095,8 @@ __device__ __forceinline__ void match_records_hot(HotState& h, WaveCtx& c, const
   hot_occ_load(h);
   hot_rebuild(h, h.A, rli32(c.ba, 0));
   hot_rebuild(h, h.B, L - 1 - rli32(c.bb, 0));
-  bool ok = true;
-  for (uint32_t blk = lo; blk < hi && ok; blk += 64) {
+  bool ok = true, handed = false;
+  for (uint32_t blk = lo; blk < hi && ok && !handed; blk += 64) {
     c.recs_left = hi - blk;
     HS(PH_RESULT);
     if (h.nfs < HOT_STACK_LOW) {
@@ -2155,25 +2149,24 @@ __device__ __forceinline__ void match_records_hot(HotState& h, WaveCtx& c, const
       const unsigned long long seq = rl64(oseq, (int)k);
       const int q = rli32(oq, (int)k);
       const uint32_t kd = rl32(okd, (int)k);
-      if (ME_UNLIKELY(!((fastm >> k) & 1ull))) {  // generic (or a reject) at a sync point
+      if (ME_UNLIKELY(!((fastm >> k) & 1ull))) {
+        // a record the lists do not cover (a cancel, a price outside the window, a taker while far
+        // levels exist, a reject): the symbol's records from here on go to k_match_hot_cont, the
+        // generic record loop, behind this wave (no generic code on the hot loop's paths)
         HMARK("record-generic");
         HS_COUNT(CT_EVICT);
-        c.recs_left = hi - (blk + k);
-        hot_sync_in(h, c);
-        const RecOut o = hot_generic_record(&c, seq, rli64(opx, (int)k), q, kd);
-        if (!uni(o.ok)) {
-          ok = false;
-          break;
+        if (lane == 0) {
+          const uint32_t idx = atomicAdd(c.bk.hcount + 1, 1u);
+          Handoff ho{};
+          ho.s = c.s;
+          ho.pos = blk + k;
+          ho.nsg = hi;
+          ho.wptr = (uint32_t)h.wptr;
+          ho.wend = (uint32_t)(h.wptr >> 32);
+          c.bk.hand[c.bk.S + idx] = ho;
         }
-        put_rec(R, k, o);
-        hot_sync_out(h, c);
-        classify();
-        fastm &= ~((2ull << k) - 1ull);
-        hot_prefetch(h);
-        __builtin_amdgcn_s_waitcnt(0);
-        HOT_CHECK(2, seq);
-        HS(PH_CANCEL);
-        continue;
+        handed = true;
+        break;
       }
       HMARK("record-fast");
       const bool buy = (kd & 3u) == ME_SIDE_BUY;
@@ -2301,6 +2294,32 @@ __global__ __launch_bounds__(64) void k_match_hot(BookDev bk, BatchDev bt) {
     wave_end(c);
   }
 }
+// The rest of a hot symbol's records after the first one k_match_hot does not cover: the generic
+// record loop (k_match's), on the same stream right after k_match_hot; hand-off i is bk.hand[S + i].
+__global__ __launch_bounds__(64) void k_match_hot_cont(BookDev bk, BatchDev bt) {
+  const uint32_t nh = min(*(volatile uint32_t*)(bk.hcount + 1), bk.S);
+  for (uint32_t i = blockIdx.x; i < nh; i += gridDim.x) {
+    const Handoff ho = bk.hand[bk.S + i];
+    const uint32_t s = rl32(ho.s, 0), pos = rl32(ho.pos, 0), hi = rl32(ho.nsg, 0);
+    const unsigned long long w = ((unsigned long long)rl32(ho.wend, 0) << 32) | rl32(ho.wptr, 0);
+    WaveCtx c;
+#ifdef ME_STAMPS
+    for (int p = 0; p < PH_N; ++p) c.st[p] = 0;
+    STAMP_MARK(c);
+#endif
+    c.lad.L = bk.L;
+    c.lad.Lwords = bk.Lwords;
+    c.lad.lv = bk.levels + (size_t)s * bk.L;
+    c.lad.occ = bk.occ + (size_t)s * bk.Lwords;
+    c.lad.tend = bk.tend + (size_t)s * bk.L;
+    c.cache = nullptr;
+    c.cmask = 0;
+    if (!wave_begin(c, bk, bt, s, pos, hi, w)) return;
+    match_records(c, bt, pos, hi);
+    wave_end(c);
+  }
+}
+
 // ---- seq ring horizon ---------------------------------------------------------
 // Runs before every match launch. The ring holds loc[seq & (R - 1)]; a rest of seq y overwrites the
 // entry of y - R. Every live order at or above the horizon has its entry, every older live order is
@@ -2339,7 +2358,8 @@ __global__ __launch_bounds__(256) void k_seq_sweep(BookDev bk, SeqGroup sg) {
     o.epoch = epoch;
     o.pad[0] = o.pad[1] = o.pad[2] = 0;
     bk.sq[sg.in ^ 1u] = o;
-    *bk.hcount = 0;  // the match launch after this one hands symbols off from 0
+    bk.hcount[0] = 0;  // the match launch after this one hands symbols off from 0 ...
+    bk.hcount[1] = 0;  // ... and continues them (k_match_hot_cont) from 0
     if (bk.pub) {  // resting orders after sg.launch match launches, for the host's admission bound
       const unsigned long long r = bk.stats[ST_RESTING];
       *bk.pub = ((unsigned long long)sg.launch << 32) | (r < 0xFFFFFFFFull ? r : 0xFFFFFFFFull);
@@ -2535,6 +2555,7 @@ hipError_t launch_match(hipStream_t st, const BookDev& bk, const BatchDev& bt, h
     if ((e = hipEventRecord(hot.fork, st)) != hipSuccess || (e = hipStreamWaitEvent(hot.st, hot.fork, 0)) != hipSuccess)
       return e;
     hipLaunchKernelGGL(k_match_hot, dim3(64), dim3(64), 0, hot.st, bk, bt);
+    hipLaunchKernelGGL(k_match_hot_cont, dim3(64), dim3(64), 0, hot.st, bk, bt);
     if ((e = hipEventRecord(hot.join, hot.st)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_match<LAD_HBM>, grid, block, 0, st, bk, bt);
     if ((e = hipStreamWaitEvent(st, hot.join, 0)) != hipSuccess) return e;
