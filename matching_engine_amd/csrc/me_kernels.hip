@@ -1499,17 +1499,13 @@ __device__ __forceinline__ int hot_scan(const HotState& h, int start, int& out_l
 // Rebuild list S from side coordinate start_m (the best, or a bound no level of either side lies
 // inside): occupancy scan (LDS), the levels (one round trip) and their head chunks (one round trip)
 // into lanes / LDS rows. The caller has waited for every store.
+template <int K>
 __device__ __forceinline__ void hot_rebuild(HotState& h, HSide& S, int start_m) {
   const int lane = lane_id();
   const int L = (int)h.L;
   int lvl = -1, n = 0;
   bool more = false;
-  if (start_m < L) {
-    if (S.k)
-      n = hot_scan<1>(h, start_m < 0 ? 0 : start_m, lvl, more);
-    else
-      n = hot_scan<0>(h, L - 1 - (start_m < 0 ? 0 : start_m), lvl, more);
-  }
+  if (start_m < L) n = hot_scan<K>(h, K ? (start_m < 0 ? 0 : start_m) : L - 1 - (start_m < 0 ? 0 : start_m), lvl, more);
   const bool v = lane < n;
   const int li = v ? lvl : 0;
   Level x{0, NIL, NIL};
@@ -1526,8 +1522,8 @@ __device__ __forceinline__ void hot_rebuild(HotState& h, HSide& S, int start_m) 
   const v4i a0 = src[0], a1 = src[1], a2 = src[2], a3 = src[3], b0 = src[4], b1 = src[5], b2 = src[6],
             b3 = src[7], b4 = src[8], b5 = src[9], b6 = src[10], b7 = src[11];
   const uint32_t hn = ch->hdr.next;
-  v4i* dq = reinterpret_cast<v4i*>(h.H->cq[S.k][lane]);
-  v4i* ds = reinterpret_cast<v4i*>(h.H->cs[S.k][lane]);
+  v4i* dq = reinterpret_cast<v4i*>(h.H->cq[K][lane]);
+  v4i* ds = reinterpret_cast<v4i*>(h.H->cs[K][lane]);
   dq[0] = a0;
   dq[1] = a1;
   dq[2] = a2;
@@ -1540,7 +1536,7 @@ __device__ __forceinline__ void hot_rebuild(HotState& h, HSide& S, int start_m) 
   ds[5] = b5;
   ds[6] = b6;
   ds[7] = b7;
-  S.m = v ? side_lvl(h, S.k, lvl) : L;
+  S.m = v ? side_lvl(h, K, lvl) : L;
   S.tot = v ? x.total : 0;
   S.hd = v ? x.head : NIL;
   S.tl = v ? x.tail : NIL;
@@ -1728,7 +1724,7 @@ __device__ __forceinline__ void hot_take(HotState& h, HSide& O, int lim, uint32_
         // occupancy bitmap holds both)
         HEV(h, HEV_TAKE_REBUILD);
         hot_drain();
-        hot_rebuild(h, O, m0 + 1);
+        hot_rebuild<K>(h, O, m0 + 1);
         __builtin_amdgcn_s_waitcnt(0);
       }
       HC_ADD(h, HC_POP);
@@ -2093,8 +2089,8 @@ __device__ __forceinline__ void match_records_hot(HotState& h, WaveCtx& c, const
   h.A.k = 1;  // asks
   h.B.k = 0;  // bids
   hot_occ_load(h);
-  hot_rebuild(h, h.A, rli32(c.ba, 0));
-  hot_rebuild(h, h.B, L - 1 - rli32(c.bb, 0));
+  hot_rebuild<1>(h, h.A, rli32(c.ba, 0));
+  hot_rebuild<0>(h, h.B, L - 1 - rli32(c.bb, 0));
   bool ok = true, handed = false;
   for (uint32_t blk = lo; blk < hi && ok && !handed; blk += 64) {
     c.recs_left = hi - blk;
@@ -2128,12 +2124,12 @@ __device__ __forceinline__ void match_records_hot(HotState& h, WaveCtx& c, const
     classify();
     if (h.A.n < HT / 2 && h.A.more) {
       hot_drain();
-      hot_rebuild(h, h.A, rli32(h.A.m, h.A.f));
+      hot_rebuild<1>(h, h.A, rli32(h.A.m, h.A.f));
       HS_COUNT(CT_MISS);
     }
     if (h.B.n < HT / 2 && h.B.more) {
       hot_drain();
-      hot_rebuild(h, h.B, rli32(h.B.m, h.B.f));
+      hot_rebuild<0>(h, h.B, rli32(h.B.m, h.B.f));
       HS_COUNT(CT_MISS);
     }
     hot_prefetch(h);
