@@ -14,6 +14,6 @@ else
   git -C $R archive $REV matching_engine_amd/csrc include | tar -x -C $S --strip-components=0
   mv $S/matching_engine_amd/csrc/* $S/csrc/; cp $S/include/* $S/include/ 2>/dev/null || true
 fi
-make -s -C $R/matching_engine_amd CSRC=$S/csrc OBJDIR=$B/obj_$NAME OUT=$B/var/libme_$NAME.so ${REGFLAGS+REGFLAGS="$REGFLAGS"} \
+make -s -C $R/matching_engine_amd CSRC=$S/csrc OBJDIR=$B/obj_$NAME OUT=$B/var/libme_$NAME.so ${REGFLAGS+REGFLAGS="$REGFLAGS"} ${KERNFLAGS+KERNFLAGS="$KERNFLAGS"} \
   CXXFLAGS="-O3 -std=c++17 -fPIC -Wall -Wno-unused-function -I$S/include -I$S/csrc $*" -j8 >/dev/null
 echo built $B/var/libme_$NAME.so
