@@ -39,7 +39,10 @@ BYTES_PER_FILL = 48    # 32 B tape record + 16 B maker-slot RMW
 # Per-workload shape. Weak scaling: symbols and batch grow with N, except config 4
 # whose 100k Zipf symbols are global (symbol 0 alone draws ~13 % of the stream at every N).
 WORKLOADS = {
-    "c1": dict(preset=1, symbols_per_gpu=1, batch_per_gpu=62500,
+    # c1: one book carries every record, so the engine runs it as a hot symbol of a 256-level window
+    # (the sort path, the aggregate hot-symbol kernels of me_agg.hip) instead of the 128-level register
+    # kernel, whose one wave per symbol is a serial chain of ~0.8 us per record
+    "c1": dict(preset=1, symbols_per_gpu=1, batch_per_gpu=62500, levels=256,
                text="BASELINE configs[0]: one symbol 'SYM', 80% LIMIT +-32 ticks / 20% MARKET, qty U[1,100], "
                     "62,500-order batches (the C1 1M-order stream); with the reference-path, service-path and "
                     "oracle timings of SURVEY.md \u00a78(d) C1 in c1_paths"),
@@ -101,6 +104,11 @@ def parse():
     return args
 
 
+def _wl_levels(w):
+    """The workload's window override (c1), else the preset's."""
+    return {"levels": w["levels"]} if "levels" in w else {}
+
+
 def global_symbols(args, world):
     w = WORKLOADS[args.workload]
     return w["symbols"] if "symbols" in w else args.symbols_per_gpu * world
@@ -154,7 +162,7 @@ def build_rank_batches(args, world, rank, nbatches, n_whole=0):
     cluster leg's slices)."""
     w = WORKLOADS[args.workload]
     S = global_symbols(args, world)
-    sc = me.preset(w["preset"], num_symbols=S, batch=args.batch_per_gpu * world)
+    sc = me.preset(w["preset"], num_symbols=S, batch=args.batch_per_gpu * world, **_wl_levels(w))
     st = me.Stream(sc)
     base = st.base_prices()
     shard, local, members = me.shard_table(S, world)
@@ -191,7 +199,7 @@ def cpu_baseline(args):
 
     w = WORKLOADS[args.workload]
     S = global_symbols(args, 1)
-    sc = me.preset(w["preset"], num_symbols=S, batch=args.batch_per_gpu)
+    sc = me.preset(w["preset"], num_symbols=S, batch=args.batch_per_gpu, **_wl_levels(w))
 
     def seeded_stream():
         st = me.Stream(sc)

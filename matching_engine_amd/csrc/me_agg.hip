@@ -1,0 +1,1108 @@
+// me_agg.hip — hot symbols of deep windows in aggregate form (DESIGN.md §4 "k_agg").
+//
+// A hot symbol (config 4's Zipf head, config 1's single book) is one serial chain of records, so
+// whatever one record costs on its wave sets the launch length. Price-time priority splits that cost
+// in two parts of very different shape:
+//
+//   * WHICH levels a taker takes from, how much from the last one, and where a remainder rests
+//     depend only on the level TOTALS — a serial chain, but a short one: k_agg_walk runs it on one
+//     wave per hot symbol with the top of each side as a 64-lane list of (level, total), no chunk,
+//     no FIFO, no fill in the chain. Each record appends "take q from level l" / "rest q at level l"
+//     events to a log.
+//   * WHICH makers a take consumed is FIFO bookkeeping inside one level: in the level's maker
+//     space (the initial FIFO's live orders, then this batch's rests in record order, each an
+//     interval of its quantity) the takes of the batch cover [0, C) in order, so the fills are the
+//     overlaps of two interval partitions — independent across levels, resolved for all levels at
+//     once after the walk (k_agg_levels, k_agg_place), and written where the tape job expects them.
+//
+// Kernels (the engine's hot stream, after k_hot_pick, beside k_match on the main stream):
+//   k_agg_walk    one wave per hot symbol: the level-total chain, the event log, the records' status
+//   k_agg_group   one workgroup per hot symbol: a stable counting sort of its log by level -> segments
+//   k_agg_levels  one wave per (symbol, level) segment: quantity taken, initial-FIFO walk, consumed
+//                 makers, emptied chunks (zeroed), each take's first maker and fill count
+//   k_agg_alloc   one wave per hot symbol: chunks for the surviving rests — the symbol's own emptied
+//                 chunks first, then its free list, then the bump allocator; the surplus freed
+//   k_agg_place   one wave per segment: surviving rests into the level's tail / new chunks, seq ring
+//   k_agg_fin     one workgroup per hot symbol: fill offsets (scan over the log), record results,
+//                 symbol state, the continuation's scratch position
+//   k_agg_emit    one thread per take event: its fills into the scratch run, in tape order
+// A record the walk does not cover (a cancel, a LIMIT outside the window, a MARKET while far levels
+// exist on the side it crosses) hands the symbol's remaining records to k_match_hot_cont, the generic
+// record loop, exactly as k_match_hot does; the HBM book is complete before it runs.
+// Same semantics and HBM layout as k_match (me_kernels.hip); parity: tests/test_hot_path.py.
+#include "me_wave.hpp"
+
+namespace me {
+namespace {
+
+constexpr uint32_t AGG_WORDS = AGG_MAX_L / 64;
+
+__device__ __forceinline__ int auni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint32_t auniu(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+
+__device__ __forceinline__ void a_set_err(const BookDev& bk, uint32_t bits) {
+  if (lane_id() == 0) atomicOr(bk.err, bits);
+}
+
+// lane i <- lane i - 1 (gfx9 DPP wave_ror:1): an entry enters mid-list by rotating the ones behind it
+__device__ __forceinline__ uint32_t a_up(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x13C, 0xf, 0xf, false);
+}
+__device__ __forceinline__ long long a_up64(long long v) {
+  return (long long)(((unsigned long long)a_up((uint32_t)((unsigned long long)v >> 32)) << 32) |
+                     a_up((uint32_t)v));
+}
+// lane `l` of `old` <- the uniform value v (one compare, shared by the fields written for the same
+// lane, and a select per 32 bits; gfx9's v_writelane cannot take both operands from SGPRs)
+__device__ __forceinline__ uint32_t a_wlu(uint32_t old, uint32_t v, int l) { return lane_id() == l ? v : old; }
+__device__ __forceinline__ int a_wl(int old, int v, int l) { return (int)a_wlu((uint32_t)old, (uint32_t)v, l); }
+__device__ __forceinline__ long long a_wl64(long long old, long long v, int l) {
+  const uint32_t lo = a_wlu((uint32_t)old, (uint32_t)v, l);
+  const uint32_t hi = a_wlu((uint32_t)((unsigned long long)old >> 32), (uint32_t)((unsigned long long)v >> 32), l);
+  return (long long)(((unsigned long long)hi << 32) | lo);
+}
+__device__ __forceinline__ void a_drain() {
+  __builtin_amdgcn_s_waitcnt(0);
+  wave_mem_order();
+}
+
+// ------------------------------------------------------------------ the level-total walk
+// Top of one side, best first: a ring over the lanes, entry i in lane (f + i) & 63. Side coordinates:
+// asks m = level, bids m = L - 1 - level, so "better" is "smaller" on both sides. The list is always
+// the exact prefix of the side's occupied window levels (an empty list = an empty side); `more`: there
+// may be occupied levels beyond the last entry.
+struct AList {
+  int m;          // lane: side coordinate of the entry
+  long long tot;  // lane: its live quantity (authoritative while listed; HBM's copy is stale)
+  int f, n, more; // wave-uniform
+};
+
+struct AWalk {
+  gptr<Level> lv;
+  gptr<unsigned long long> occ;
+  gptr<AggEv> ev;
+  unsigned long long* locc;  // LDS copy of the occupancy bitmap (both sides)
+  uint32_t evp;              // next log index
+  int L, W;
+};
+
+__device__ __forceinline__ int a_side_lvl(int L, int k, int m) { return k ? m : L - 1 - m; }
+
+__device__ __forceinline__ void a_emit(AWalk& w, int lvl, uint32_t jt, int q) {
+  if (lane_id() == 0) {
+    AggEv e;
+    e.lvl = (uint32_t)lvl;
+    e.j = jt;
+    e.qty = q;
+    e.pad = 0;
+    w.ev[w.evp] = e;
+  }
+  w.evp += 1;
+}
+
+// Occupancy: non-returning atomics on the LDS copy and on HBM (nothing in the chain waits for them).
+__device__ __forceinline__ void a_occ(AWalk& w, int lvl, bool on) {
+  const uint32_t wi = (uint32_t)lvl >> 6;
+  const unsigned long long bit = 1ull << (lvl & 63);
+  if (lane_id() == 0) {
+    if (on) {
+      __atomic_fetch_or(&w.locc[wi], bit, __ATOMIC_RELAXED);
+      __atomic_fetch_or(&w.occ[wi], bit, __ATOMIC_RELAXED);
+    } else {
+      __atomic_fetch_and(&w.locc[wi], ~bit, __ATOMIC_RELAXED);
+      __atomic_fetch_and(&w.occ[wi], ~bit, __ATOMIC_RELAXED);
+    }
+  }
+}
+
+// The r-th (0-based) set bit of w (w has more than r set bits).
+__device__ __forceinline__ uint32_t a_nth_set(unsigned long long w, uint32_t r) {
+  uint32_t pos = 0;
+#pragma unroll
+  for (uint32_t hsz = 32; hsz >= 1; hsz >>= 1) {
+    const uint32_t c = (uint32_t)__popcll(w & ((1ull << hsz) - 1ull));
+    const bool up = r >= c;
+    r = up ? r - c : r;
+    w = up ? (w >> hsz) : w;
+    pos += up ? hsz : 0u;
+  }
+  return pos;
+}
+
+// Lanes 0..n-1 <- the first (up to) 64 occupied levels from window level `start` going up (K = 1) or
+// down (K = 0), from the LDS occupancy copy; *more: the list filled before the window ended.
+template <int K>
+__device__ int a_scan(const AWalk& w, int start, int& out_lvl, int& more) {
+  const int lane = lane_id();
+  out_lvl = -1;
+  more = 0;
+  if (start < 0 || start >= w.L) return 0;
+  int found = 0;
+  const int w0 = start >> 6;
+  for (int b = 0;; b += 64) {
+    const int wi = K ? w0 + b + lane : w0 - b - lane;
+    const bool in = wi >= 0 && wi < w.W;
+    unsigned long long x = in ? w.locc[wi] : 0ull;
+    if (wi == w0) x &= K ? (~0ull << (start & 63)) : (~0ull >> (63 - (start & 63)));
+    if (!K) x = __builtin_bitreverse64(x);  // descending: bit 0 = the word's highest level
+    const uint32_t c = (uint32_t)__popcll(x);
+    const long long inc = wave_incl_scan((long long)c);
+    const uint32_t ex = (uint32_t)(inc - c);
+    const uint32_t tot = (uint32_t)rli64(inc, 63);
+    const int i = lane - found;  // output lane i takes bit (i - ex_j) of the lane j holding it
+    int lo = 0;
+#pragma unroll
+    for (int st = 32; st >= 1; st >>= 1) {
+      const uint32_t e = (uint32_t)__shfl((int)ex, min(lo + st, 63), 64);
+      if (lo + st < 64 && (int)e <= i) lo += st;
+    }
+    const unsigned long long wj = (unsigned long long)__shfl((long long)x, lo, 64);
+    const uint32_t r = (uint32_t)(i - __shfl((int)ex, lo, 64));
+    const uint32_t bpos = a_nth_set(wj, r);
+    const int wdx = K ? w0 + b + lo : w0 - b - lo;
+    if (i >= 0 && (uint32_t)i < tot) out_lvl = wdx * 64 + (K ? (int)bpos : 63 - (int)bpos);
+    found = min(found + (int)tot, 64);
+    const bool end = K ? (w0 + b + 64 >= w.W) : (w0 - b - 64 < 0);
+    if (found >= 64) {
+      more = 1;  // conservative: a later rebuild finds out
+      return 64;
+    }
+    if (end) return found;
+  }
+}
+
+// Rebuild list S from side coordinate start_m (the best, or a bound no level of either side lies
+// inside): occupancy scan in LDS, the totals in one round trip. The caller has flushed the list's own
+// totals and waited for every store.
+template <int K>
+__device__ __forceinline__ void a_rebuild(AWalk& w, AList& S, int start_m) {
+  const int lane = lane_id();
+  int lvl = -1, more = 0, n = 0;
+  if (start_m < w.L) {
+    const int sm = start_m < 0 ? 0 : start_m;
+    n = a_scan<K>(w, K ? sm : w.L - 1 - sm, lvl, more);
+  }
+  const bool v = lane < n;
+  long long t = 0;
+  if (v) t = w.lv[lvl].total;
+  S.m = v ? a_side_lvl(w.L, K, lvl) : w.L;
+  S.tot = t;
+  S.f = 0;
+  S.n = auni(n);
+  S.more = auni(more);
+}
+
+// The listed totals back to HBM (before a rebuild re-reads them, and at the end).
+__device__ __forceinline__ void a_flush(AWalk& w, const AList& S, int K) {
+  const int rel = (lane_id() - S.f) & 63;
+  if (rel < S.n) w.lv[a_side_lvl(w.L, K, S.m)].total = S.tot;
+}
+
+// Take up to rem from list O (side K) while its front crosses lim (side coordinates): one event per
+// level taken from; a level taken whole leaves the list (the front moves) and the book.
+template <int K>
+__device__ __forceinline__ void a_take(AWalk& w, AList& O, int lim, uint32_t& rem, uint32_t jt) {
+  const int lane = lane_id();
+  while (rem && O.n) {
+    const int f = O.f;
+    const int m0 = rli32(O.m, f);
+    if (m0 > lim) break;
+    const long long tot = rli64(O.tot, f);
+    const int lvl = a_side_lvl(w.L, K, m0);
+    if ((long long)rem < tot) {
+      O.tot = a_wl64(O.tot, tot - (long long)rem, f);
+      a_emit(w, lvl, jt, (int)rem);
+      rem = 0;
+      break;
+    }
+    a_emit(w, lvl, jt, (int)tot);
+    rem -= (uint32_t)tot;
+    if (lane == 0) w.lv[lvl].total = 0;
+    a_occ(w, lvl, false);
+    O.f = (f + 1) & 63;
+    O.n -= 1;
+    if (ME_UNLIKELY(!O.n && O.more)) {
+      // ran dry with levels beyond it: rebuild now, so that an empty list always means an empty side
+      a_drain();
+      a_rebuild<K>(w, O, m0 + 1);
+    }
+  }
+}
+
+// Rest q at side coordinate mm (window level lvl) on list M (side K).
+template <int K>
+__device__ __forceinline__ void a_rest(AWalk& w, AList& M, int mm, int lvl, int q, uint32_t jt) {
+  const int lane = lane_id();
+  const int rel = (lane - M.f) & 63;
+  const bool ent = rel < M.n;
+  const int p = __popcll(__ballot(ent && M.m < mm));  // entries better than the level
+  if (p < M.n) {
+    const int j = (M.f + p) & 63;
+    if (rli32(M.m, j) == mm) {  // a listed level: its total grows
+      M.tot = a_wl64(M.tot, rli64(M.tot, j) + q, j);
+      a_emit(w, lvl, jt, q);
+      return;
+    }
+  }
+  if (p < M.n || (!M.more && p < 64)) {
+    // an empty level inside the list's span (or past its end when nothing lies beyond): it enters at
+    // position p; the entries behind it move one lane up (a full list drops its last entry)
+    if (M.n == 64) {
+      const int jl = (M.f + 63) & 63;
+      if (lane == jl) w.lv[a_side_lvl(w.L, K, M.m)].total = M.tot;
+      __builtin_amdgcn_s_waitcnt(0);  // a later rest there is an atomic behind this store
+      M.n = 63;
+      M.more = 1;
+    }
+    int j;
+    if (p == 0) {  // a new best: the front moves one lane back
+      M.f = (M.f - 1) & 63;
+      j = M.f;
+    } else {
+      j = (M.f + p) & 63;
+      const bool up = rel > p && rel <= M.n;
+      const int um = (int)a_up((uint32_t)M.m);
+      const long long ut = a_up64(M.tot);
+      M.m = up ? um : M.m;
+      M.tot = up ? ut : M.tot;
+    }
+    M.m = a_wl(M.m, mm, j);
+    M.tot = a_wl64(M.tot, (long long)q, j);
+    M.n += 1;
+    a_occ(w, lvl, true);
+  } else {
+    // deep (beyond the list's last entry): the HBM total grows by a non-returning atomic
+    if (lane == 0) __atomic_fetch_add(&w.lv[lvl].total, (long long)q, __ATOMIC_RELAXED);
+    a_occ(w, lvl, true);
+    M.more = 1;
+  }
+  a_emit(w, lvl, jt, q);
+}
+
+__device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const AggDev& ag, uint32_t i, uint32_t s,
+                                uint32_t lo, uint32_t hi, unsigned long long* locc) {
+  const int lane = lane_id();
+  const int L = (int)bk.L;
+  const SymState st = bk.sym[s];
+  const long long base = rli64(st.base, 0);
+  const int bb0 = rli32(st.best_bid, 0), ba0 = rli32(st.best_ask, 0);
+  const uint32_t resting = rl32(st.resting, 0), free_head = rl32(st.free_head, 0);
+  const uint32_t nfar0 = rl32(st.nfar[0], 0), nfar1 = rl32(st.nfar[1], 0);
+  const uint32_t cnt = hi - lo;
+  gptr<AggSlot> slot = (gptr<AggSlot>)(ag.slot + i);
+  // scratch run of the symbol: fills <= resting makers + 2 * records (k_match's bound)
+  const unsigned long long need = (unsigned long long)resting + 2ull * cnt;
+  unsigned long long w0 = 0;
+  if (lane == 0) w0 = atomicAdd(bt.scratch_top, need);
+  w0 = rl64(w0, 0);
+  // the log: events <= rests + takes; a take ends its taker or empties a level, and the levels that
+  // can empty are the ones occupied at the start (<= min(L, resting)) or created by rests
+  const uint32_t evneed = 3u * cnt + min((uint32_t)L, resting) + 64u;
+  uint32_t eb = 0;
+  if (lane == 0) eb = atomicAdd(&ag.ctr[AC_EV], evneed);
+  eb = rl32(eb, 0);
+  const bool sok = w0 + need <= bt.scratch_cap;
+  const bool eok = (unsigned long long)eb + evneed <= ag.ev_cap;
+  if (lane == 0) {
+    AggSlot o{};
+    o.s = s;
+    o.lo = lo;
+    o.hi = hi;
+    o.pos = sok ? lo : hi;
+    o.wbase = w0;
+    o.base = base;
+    o.ev_base = eb;
+    o.free_head = free_head;
+    o.resting0 = resting;
+    o.bb = bb0;
+    o.ba = ba0;
+    o.active = 0;
+    o.hidx = NIL;
+    o.gs = bk.gsym ? bk.gsym[s] : s;
+    *slot = o;
+  }
+  if (!sok) {
+    a_set_err(bk, ERR_SCRATCH_OOM);
+    return;
+  }
+  if (!eok) {  // no room in the log: every record of the symbol goes to the generic loop
+    if (lane == 0) {
+      const uint32_t idx = atomicAdd(bk.hcount + 1, 1u);
+      Handoff ho{};
+      ho.s = s;
+      ho.pos = lo;
+      ho.nsg = hi;
+      ho.wptr = (uint32_t)w0;
+      ho.wend = (uint32_t)(w0 >> 32);
+      bk.hand[bk.S + idx] = ho;
+    }
+    return;
+  }
+  AWalk w;
+  w.lv = (gptr<Level>)vptr(bk.levels + (size_t)s * bk.L);
+  w.occ = (gptr<unsigned long long>)vptr(bk.occ + (size_t)s * bk.Lwords);
+  w.ev = (gptr<AggEv>)vptr(ag.ev);
+  w.locc = locc;
+  w.evp = eb;
+  w.L = L;
+  w.W = (int)bk.Lwords;
+  for (int k = lane; k < w.W; k += 64) locc[k] = w.occ[k];
+  wave_mem_order();
+  AList A, B;  // asks (side 1), bids (side 0)
+  a_rebuild<1>(w, A, ba0);
+  a_rebuild<0>(w, B, L - 1 - bb0);
+  uint32_t pos = hi;
+  bool stop = false;
+  for (uint32_t blk = lo; blk < hi && !stop; blk += 64) {
+    const uint32_t j = blk + (uint32_t)lane;
+    const bool v = j < hi;
+    const uint32_t oi = v ? bt.perm[j] : 0u;
+    const unsigned long long oseq = v ? bt.seq[oi] : 0ull;
+    const long long opx = v ? bt.px[oi] : 0ll;
+    const int oq = v ? bt.qty[oi] : 0;
+    const uint32_t okd = v ? (uint32_t)bt.kind[oi] : 0u;
+    const uint32_t cntb = min(64u, hi - blk);
+    const uint32_t side = okd & 3u;
+    const bool market = (okd >> 2) & 1u, cancel = (okd >> 3) & 1u;
+    // k_match's reject reasons, in its order (cancels are the generic loop's)
+    const uint32_t rj = oq <= 0                                          ? (uint32_t)ME_RJ_BAD_QTY
+                        : (side != ME_SIDE_BUY && side != ME_SIDE_SELL) ? (uint32_t)ME_RJ_BAD_SIDE
+                        : oseq == 0ull                                   ? (uint32_t)ME_RJ_BAD_SEQ
+                                                                         : 0u;
+    const unsigned long long off = (unsigned long long)opx - (unsigned long long)base;
+    const bool inw = off < (unsigned long long)L;
+    const bool farx = (side == ME_SIDE_BUY ? nfar1 : nfar0) != 0u;  // far levels on the side a MARKET crosses
+    const bool fast = v && !cancel && (rj != 0u || (market ? !farx : inw));
+    const int olm = (int)off;
+    const unsigned long long fastm = __ballot(fast);
+    if (A.n < 32 && A.more) {
+      a_flush(w, A, 1);
+      a_drain();
+      a_rebuild<1>(w, A, rli32(A.m, A.f));
+    }
+    if (B.n < 32 && B.more) {
+      a_flush(w, B, 0);
+      a_drain();
+      a_rebuild<0>(w, B, rli32(B.m, B.f));
+    }
+    int rf = 0, rr = 0;
+    uint32_t rs = 0, rlo = 0, rn = 0;
+    uint32_t k = 0;
+    for (; k < cntb; ++k) {
+      if (ME_UNLIKELY(!((fastm >> k) & 1ull))) {
+        pos = blk + k;  // the generic loop takes over from here (k_match_hot_cont)
+        stop = true;
+        break;
+      }
+      const uint32_t jt = blk + k;
+      const int q = rli32(oq, (int)k);
+      const uint32_t rjk = rl32(rj, (int)k);
+      if (ME_UNLIKELY(rjk != 0u)) {
+        rf = a_wl(rf, 0, (int)k);
+        rr = a_wl(rr, rjk == ME_RJ_BAD_QTY ? 0 : q, (int)k);
+        rs = a_wlu(rs, (uint32_t)ME_ST_REJECTED | (rjk << 8), (int)k);
+        rlo = a_wlu(rlo, w.evp, (int)k);
+        rn = a_wlu(rn, 0u, (int)k);
+        continue;
+      }
+      const uint32_t kd = rl32(okd, (int)k);
+      const bool buy = (kd & 3u) == ME_SIDE_BUY;
+      const bool mkt = (kd >> 2) & 1u;
+      const int lm = rli32(olm, (int)k);
+      const uint32_t ev_lo = w.evp;
+      uint32_t rem = (uint32_t)q;
+      uint32_t nte;
+      if (buy) {
+        a_take<1>(w, A, mkt ? L - 1 : lm, rem, jt | AGG_TAKE);
+        nte = w.evp - ev_lo;
+        if (!mkt && rem) a_rest<0>(w, B, L - 1 - lm, lm, (int)rem, jt);
+      } else {
+        a_take<0>(w, B, mkt ? L - 1 : L - 1 - lm, rem, jt | AGG_TAKE);
+        nte = w.evp - ev_lo;
+        if (!mkt && rem) a_rest<1>(w, A, lm, lm, (int)rem, jt);
+      }
+      const int filled = q - (int)rem;
+      uint32_t stt;
+      if (mkt)
+        stt = rem == 0 ? ME_ST_FILLED : ME_ST_CANCELED;
+      else
+        stt = rem == 0 ? ME_ST_FILLED : (filled > 0 ? ME_ST_PARTIALLY_FILLED : ME_ST_NEW);
+      rf = a_wl(rf, filled, (int)k);
+      rr = a_wl(rr, (int)rem, (int)k);
+      rs = a_wlu(rs, stt, (int)k);
+      rlo = a_wlu(rlo, ev_lo, (int)k);
+      rn = a_wlu(rn, nte, (int)k);
+    }
+    if (v && (uint32_t)lane < k) {
+      AggRec r;
+      r.filled = rf;
+      r.rem = rr;
+      r.st = rs;
+      r.ev_lo = rlo;
+      r.ev_n = rn;
+      r.pad = 0;
+      ag.rec[j] = r;
+    }
+  }
+  a_flush(w, A, 1);
+  a_flush(w, B, 0);
+  const int ba = A.n ? rli32(A.m, A.f) : L;
+  const int bb = B.n ? L - 1 - rli32(B.m, B.f) : -1;
+  if (lane == 0) {
+    slot->pos = pos;
+    slot->ev_cnt = w.evp - eb;
+    slot->bb = bb;
+    slot->ba = ba;
+    slot->active = 1;
+    if (pos < hi) {
+      const uint32_t idx = atomicAdd(bk.hcount + 1, 1u);
+      Handoff ho{};
+      ho.s = s;
+      ho.pos = pos;
+      ho.nsg = hi;
+      ho.wptr = (uint32_t)w0;  // k_agg_fin moves it past the fills of [lo, pos)
+      ho.wend = (uint32_t)(w0 >> 32);
+      bk.hand[bk.S + idx] = ho;
+      slot->hidx = idx;
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) void k_agg_walk(BookDev bk, BatchDev bt, AggDev ag) {
+  __shared__ unsigned long long locc[AGG_WORDS];
+  const uint32_t nh = min(*(volatile uint32_t*)bk.hcount, bk.S);
+  for (uint32_t i = blockIdx.x; i < nh; i += gridDim.x) {
+    const Handoff ho = bk.hand[i];
+    agg_walk_symbol(bk, bt, ag, i, auniu(ho.s), auniu(ho.pos), auniu(ho.nsg), locc);
+  }
+}
+
+// ------------------------------------------------------------------ grouping the log by level
+// One 1024-thread workgroup per hot symbol: level histogram in LDS, segments (one per level with
+// events, in level order), then a stable scatter of the log indices (one wave, 64 events per step,
+// ranks by ballot multisplit over the level bits).
+__global__ __launch_bounds__(1024) void k_agg_group(BookDev bk, AggDev ag) {
+  extern __shared__ uint32_t cnt_l[];  // [L]
+  __shared__ uint32_t wsum[16], wnz[16], sbase;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint32_t L = bk.L;
+  const uint32_t per = (L + 1023) / 1024;
+  uint32_t nbits = 0;
+  while ((1u << nbits) < L) ++nbits;
+  const uint32_t nh = min(*(volatile uint32_t*)bk.hcount, bk.S);
+  for (uint32_t i = blockIdx.x; i < nh; i += gridDim.x) {
+    const AggSlot& sl = ag.slot[i];
+    if (!sl.active) continue;  // uniform over the workgroup
+    const uint32_t eb = sl.ev_base, n = sl.ev_cnt;
+    for (uint32_t b = tid; b < L; b += 1024) cnt_l[b] = 0;
+    __syncthreads();
+    for (uint32_t e = tid; e < n; e += 1024) atomicAdd(&cnt_l[ag.ev[eb + e].lvl], 1u);
+    __syncthreads();
+    const uint32_t b0 = tid * per;
+    uint32_t lsum = 0, lnz = 0;
+    for (uint32_t k = 0; k < per; ++k)
+      if (b0 + k < L) {
+        const uint32_t c = cnt_l[b0 + k];
+        lsum += c;
+        lnz += c != 0u;
+      }
+    uint32_t xs = lsum, xn = lnz;  // wave inclusive scans
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t ts = __shfl_up(xs, d, 64), tn = __shfl_up(xn, d, 64);
+      if (lane >= d) {
+        xs += ts;
+        xn += tn;
+      }
+    }
+    if (lane == 63) {
+      wsum[wv] = xs;
+      wnz[wv] = xn;
+    }
+    __syncthreads();
+    uint32_t ps = 0, pn = 0, tn_all = 0;
+    for (int k = 0; k < 16; ++k) {
+      if (k < wv) {
+        ps += wsum[k];
+        pn += wnz[k];
+      }
+      tn_all += wnz[k];
+    }
+    if (tid == 0) {
+      const uint32_t sb = atomicAdd(&ag.ctr[AC_SEG], tn_all);
+      sbase = sb;
+      ag.slot[i].seg_base = sb;
+      ag.slot[i].nseg = tn_all;
+    }
+    __syncthreads();
+    uint32_t run = ps + xs - lsum, sid = pn + xn - lnz;
+    for (uint32_t k = 0; k < per; ++k)
+      if (b0 + k < L) {
+        const uint32_t c = cnt_l[b0 + k];
+        if (c) {
+          AggSeg g;
+          g.slot = i;
+          g.lvl = b0 + k;
+          g.start = eb + run;
+          g.cnt = c;
+          ag.seg[sbase + sid] = g;
+          ++sid;
+        }
+        cnt_l[b0 + k] = run;
+        run += c;
+      }
+    __syncthreads();
+    if (wv == 0) {
+      for (uint32_t c0 = 0; c0 < n; c0 += 64) {
+        const uint32_t e = c0 + (uint32_t)lane;
+        const bool v = e < n;
+        const uint32_t key = v ? ag.ev[eb + e].lvl : 0u;
+        unsigned long long peers = __ballot(v);
+        for (uint32_t bit = 0; bit < nbits; ++bit) {
+          const unsigned long long bb = __ballot((key >> bit) & 1u);
+          peers &= ((key >> bit) & 1u) ? bb : ~bb;
+        }
+        const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
+        const uint32_t cp = (uint32_t)__popcll(peers);
+        const uint32_t start = cnt_l[key];
+        if (v) ag.evs[eb + start + rank] = eb + e;
+        __builtin_amdgcn_wave_barrier();
+        if (v && rank == 0) cnt_l[key] = start + cp;
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------ per-level FIFO resolution
+__device__ __forceinline__ unsigned long long a_seq_of(const BatchDev& bt, uint32_t j) { return bt.seq[bt.perm[j]]; }
+
+// First index in mk[b, b + n) whose end is > x (strict = false: >= x).
+__device__ __forceinline__ uint32_t a_search(const AggMk* mk, uint32_t b, uint32_t n, unsigned long long x, bool strict) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    const unsigned long long e = mk[b + mid].end;
+    if (strict ? e <= x : e < x)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
+// One wave per segment (symbol, level): the quantity C the batch took from the level; the initial
+// FIFO walked until C is covered (count pass, then a write pass: consumed makers into mk, emptied
+// chunks zeroed into fr, the chunk C ends in updated); the rests C reaches; each take's first maker
+// and fill count; what the surviving rests need.
+__global__ __launch_bounds__(256) void k_agg_levels(BookDev bk, BatchDev bt, AggDev ag) {
+  const int lane = lane_id();
+  const bool act = lane < ME_C;
+  const uint32_t gw = blockIdx.x * 4u + (threadIdx.x >> 6), nw = gridDim.x * 4u;
+  const uint32_t nseg = min(*(volatile uint32_t*)&ag.ctr[AC_SEG], ag.ev_cap);
+  for (uint32_t si = gw; si < nseg; si += nw) {
+    const AggSeg sg = ag.seg[si];
+    const uint32_t slot_i = auniu(sg.slot), lvl = auniu(sg.lvl), start = auniu(sg.start), cnt = auniu(sg.cnt);
+    AggSlot* sl = ag.slot + slot_i;
+    const uint32_t s = auniu(sl->s);
+    const size_t li = (size_t)s * bk.L + lvl;
+    const uint32_t head0 = auniu(bk.levels[li].head);
+    // 1. takes: C and each take's interval start
+    unsigned long long C = 0;
+    uint32_t nrest = 0;
+    for (uint32_t b = 0; b < cnt; b += 64) {
+      const bool v = b + (uint32_t)lane < cnt;
+      const uint32_t e = v ? ag.evs[start + b + lane] : 0u;
+      AggEv E{};
+      if (v) E = ag.ev[e];
+      const bool tk = v && (E.j & AGG_TAKE) != 0u;
+      const bool rs = v && !tk;
+      const long long tq = tk ? (long long)E.qty : 0ll;
+      const long long inc = wave_incl_scan(tq);
+      if (tk) ag.eva[e] = C + (unsigned long long)(inc - tq);
+      if (rs) ag.evn[e] = 0u;
+      C += (unsigned long long)rli64(inc, 63);
+      nrest += (uint32_t)__popcll(__ballot(rs));
+    }
+    // 2. count pass over the initial FIFO
+    unsigned long long W = 0;
+    uint32_t nmk = 0, nfreed = 0, nfull = 0, newhead = NIL, ch = head0;
+    bool exhausted = false;
+    for (;;) {
+      if (ch == NIL) {
+        exhausted = true;
+        break;
+      }
+      if (W >= C) {
+        newhead = ch;
+        break;
+      }
+      if (ch >= bk.nchunks) {
+        a_set_err(bk, ERR_INCONSISTENT);
+        exhausted = true;
+        break;
+      }
+      const int q = act ? bk.chunks[ch].qty[lane] : 0;
+      const uint32_t nx = auniu(bk.chunks[ch].hdr.next);
+      const long long inc = wave_incl_scan((long long)q);
+      const unsigned long long ex = (unsigned long long)(inc - q);
+      const unsigned long long live = (unsigned long long)rli64(inc, 63);
+      nmk += (uint32_t)__popcll(__ballot(q > 0 && W + ex < C));
+      nfull += (uint32_t)__popcll(__ballot(q > 0 && W + (unsigned long long)inc <= C));
+      if (W + live <= C) {
+        ++nfreed;
+        W += live;
+        ch = nx;
+        continue;
+      }
+      newhead = ch;  // C ends inside this chunk
+      break;
+    }
+    const unsigned long long T0 = exhausted ? W : ~0ull;
+    const unsigned long long Cr = exhausted && C > W ? C - W : 0ull;  // taken from this batch's rests
+    // rests C reaches (makers too) and rests that survive
+    uint32_t nrc = 0, ks = 0;
+    {
+      unsigned long long RR = 0;
+      for (uint32_t b = 0; b < cnt; b += 64) {
+        const bool v = b + (uint32_t)lane < cnt;
+        const uint32_t e = v ? ag.evs[start + b + lane] : 0u;
+        AggEv E{};
+        if (v) E = ag.ev[e];
+        const bool rs = v && (E.j & AGG_TAKE) == 0u;
+        const long long rq = rs ? (long long)E.qty : 0ll;
+        const long long inc = wave_incl_scan(rq);
+        const unsigned long long st0 = RR + (unsigned long long)(inc - rq), en = RR + (unsigned long long)inc;
+        nrc += (uint32_t)__popcll(__ballot(rs && st0 < Cr));
+        ks += (uint32_t)__popcll(__ballot(rs && en > Cr));
+        RR += (unsigned long long)rli64(inc, 63);
+      }
+    }
+    const uint32_t te0 = newhead != NIL ? auniu((uint32_t)bk.tend[li]) : 0u;  // the tail survives iff newhead does
+    const uint32_t tailfree = newhead != NIL ? (uint32_t)ME_C - te0 : 0u;
+    const uint32_t need = ks > tailfree ? (ks - tailfree + ME_C - 1) / ME_C : 0u;
+    const uint32_t own = min(need, nfreed), deficit = need - own;
+    const uint32_t nmkt = nmk + nrc;
+    uint32_t mk_base = 0, fr_base = 0, d_off = 0;
+    if (lane == 0) {
+      mk_base = atomicAdd(&ag.ctr[AC_MK], nmkt);
+      fr_base = atomicAdd(&ag.ctr[AC_FR], nfreed);
+      if (deficit) d_off = atomicAdd(&sl->deficit, deficit);
+      const int dr = (int)ks - (int)nfull;
+      if (dr) atomicAdd(&sl->dresting, dr);
+    }
+    mk_base = rl32(mk_base, 0);
+    fr_base = rl32(fr_base, 0);
+    d_off = rl32(d_off, 0);
+    if (mk_base + nmkt > ag.mk_cap || fr_base + nfreed > ag.fr_cap) {
+      a_set_err(bk, ERR_SCRATCH_OOM);  // sized so this cannot happen; leaves the level alone
+      for (uint32_t b = lane; b < cnt; b += 64) ag.evn[ag.evs[start + b]] = 0u;
+      if (lane == 0) {
+        AggSegS o{};
+        o.T0 = ~0ull;
+        o.newhead = head0;
+        ag.segs[si] = o;
+      }
+      continue;
+    }
+    // 3. write pass over the initial FIFO
+    {
+      unsigned long long Wv = 0;
+      uint32_t mi = 0, fi = 0;
+      ch = head0;
+      while (Wv < C && ch < bk.nchunks) {
+        const int q = act ? bk.chunks[ch].qty[lane] : 0;
+        const unsigned long long sq = act ? bk.chunks[ch].seq[lane] : 0ull;
+        const uint32_t nx = auniu(bk.chunks[ch].hdr.next);
+        const long long inc = wave_incl_scan((long long)q);
+        const unsigned long long ex = (unsigned long long)(inc - q), en = Wv + (unsigned long long)inc;
+        const unsigned long long live = (unsigned long long)rli64(inc, 63);
+        const bool cons = q > 0 && Wv + ex < C;
+        const unsigned long long cm = __ballot(cons);
+        if (cons) {
+          AggMk m;
+          m.seq = sq;
+          m.end = en;
+          ag.mk[mk_base + mi + (uint32_t)__popcll(cm & lanemask_lt())] = m;
+        }
+        mi += (uint32_t)__popcll(cm);
+        if (Wv + live <= C) {  // emptied: zero it (free chunks hold qty 0) and list it
+          if (act) bk.chunks[ch].qty[lane] = 0;
+          if (lane == 0) ag.fr[fr_base + fi] = ch;
+          ++fi;
+          Wv += live;
+          ch = nx;
+          continue;
+        }
+        if (cons) bk.chunks[ch].qty[lane] = en <= C ? 0 : (int)(en - C);
+        break;
+      }
+      // makers from this batch's rests
+      if (Cr) {
+        unsigned long long RR = 0;
+        for (uint32_t b = 0; b < cnt; b += 64) {
+          const bool v = b + (uint32_t)lane < cnt;
+          const uint32_t e = v ? ag.evs[start + b + lane] : 0u;
+          AggEv E{};
+          if (v) E = ag.ev[e];
+          const bool rs = v && (E.j & AGG_TAKE) == 0u;
+          const long long rq = rs ? (long long)E.qty : 0ll;
+          const long long inc = wave_incl_scan(rq);
+          const unsigned long long st0 = RR + (unsigned long long)(inc - rq), en = RR + (unsigned long long)inc;
+          const bool cons = rs && st0 < Cr;
+          const unsigned long long cm = __ballot(cons);
+          if (cons) {
+            AggMk m;
+            m.seq = a_seq_of(bt, E.j);
+            m.end = T0 + en;
+            ag.mk[mk_base + mi + (uint32_t)__popcll(cm & lanemask_lt())] = m;
+          }
+          mi += (uint32_t)__popcll(cm);
+          RR += (unsigned long long)rli64(inc, 63);
+        }
+      }
+    }
+    a_drain();
+    // 4. each take: its first maker and its fill count (makers overlapping its interval)
+    for (uint32_t b = 0; b < cnt; b += 64) {
+      const bool v = b + (uint32_t)lane < cnt;
+      const uint32_t e = v ? ag.evs[start + b + lane] : 0u;
+      AggEv E{};
+      if (v) E = ag.ev[e];
+      const bool tk = v && (E.j & AGG_TAKE) != 0u;
+      if (tk) {
+        const unsigned long long a = ag.eva[e], z = a + (unsigned long long)E.qty;
+        const uint32_t first = a_search(ag.mk, mk_base, nmkt, a, true);
+        const uint32_t last = a_search(ag.mk, mk_base, nmkt, z, false);
+        ag.evf[e] = mk_base + first;
+        ag.evn[e] = last - first + 1u;
+      }
+    }
+    if (lane == 0) {
+      AggSegS o;
+      o.C = C;
+      o.T0 = T0;
+      o.newhead = newhead;
+      o.mk_base = mk_base;
+      o.nmk = nmkt;
+      o.fr_base = fr_base;
+      o.nfreed = nfreed;
+      o.need = need;
+      o.d_off = d_off;
+      o.ks = ks;
+      ag.segs[si] = o;
+    }
+    (void)nrest;
+  }
+}
+
+// One wave per hot symbol: the chunks the surviving rests need beyond their levels' own emptied ones
+// (the slot's deficit) come from other levels' surpluses, then the symbol's free list, then the bump
+// allocator; surpluses left over join the free list. fr[alloc_base + t], t < deficit: the allocation;
+// fr[alloc_base + deficit + u], u < surplus: the surpluses gathered.
+__global__ __launch_bounds__(64) void k_agg_alloc(BookDev bk, AggDev ag) {
+  const int lane = lane_id();
+  const uint32_t nh = min(*(volatile uint32_t*)bk.hcount, bk.S);
+  for (uint32_t i = blockIdx.x; i < nh; i += gridDim.x) {
+    AggSlot* sl = ag.slot + i;
+    if (!auniu(sl->active)) continue;
+    const uint32_t s = auniu(sl->s), sb = auniu(sl->seg_base), ns = auniu(sl->nseg);
+    const uint32_t D = auniu(sl->deficit);
+    uint32_t fh = auniu(sl->free_head);
+    uint32_t Stot = 0;
+    for (uint32_t b = 0; b < ns; b += 64) {
+      uint32_t sp = 0;
+      if (b + lane < ns) {
+        const AggSegS& g = ag.segs[sb + b + lane];
+        sp = g.nfreed - min(g.need, g.nfreed);
+      }
+      Stot += (uint32_t)rli64(wave_incl_scan((long long)sp), 63);
+    }
+    if (!D && !Stot) continue;
+    uint32_t ab = 0;
+    if (lane == 0) ab = atomicAdd(&ag.ctr[AC_FR], D + Stot);
+    ab = rl32(ab, 0);
+    if ((unsigned long long)ab + D + Stot > ag.fr_cap) {
+      a_set_err(bk, ERR_SCRATCH_OOM);
+      continue;
+    }
+    // gather the surpluses (level order) into fr[ab + D, ab + D + Stot)
+    uint32_t run = 0;
+    for (uint32_t b = 0; b < ns; b += 64) {
+      uint32_t sp = 0, src = 0;
+      if (b + lane < ns) {
+        const AggSegS& g = ag.segs[sb + b + lane];
+        const uint32_t own = min(g.need, g.nfreed);
+        sp = g.nfreed - own;
+        src = g.fr_base + own;
+      }
+      const long long inc = wave_incl_scan((long long)sp);
+      const uint32_t ex = run + (uint32_t)(inc - sp);
+      for (uint32_t k = 0; k < sp; ++k) ag.fr[ab + D + ex + k] = ag.fr[src + k];
+      run += (uint32_t)rli64(inc, 63);
+    }
+    a_drain();
+    const uint32_t k1 = min(D, Stot);
+    for (uint32_t t = lane; t < k1; t += 64) ag.fr[ab + t] = ag.fr[ab + D + t];
+    if (D > k1) {  // the book grows: the free list, then fresh chunks
+      uint32_t t = k1;
+      if (lane == 0) {
+        while (t < D && fh != NIL && fh < bk.nchunks) {
+          ag.fr[ab + t] = fh;
+          fh = bk.chunks[fh].hdr.next;
+          ++t;
+        }
+      }
+      t = rl32(t, 0);
+      fh = rl32(fh, 0);
+      if (t < D) {
+        const uint32_t left = D - t;
+        uint32_t got = 0;
+        if (lane == 0) got = atomicAdd(bk.chunk_top, left);
+        got = rl32(got, 0);
+        if ((unsigned long long)got + left > bk.nchunks) {
+          a_set_err(bk, ERR_CHUNK_OOM);
+          for (uint32_t u = lane; u < left; u += 64) ag.fr[ab + t + u] = 0u;  // never indexed past the pool
+        } else {
+          for (uint32_t u = lane; u < left; u += 64) {
+            ag.fr[ab + t + u] = got + u;
+            bk.chunks[got + u].owner = s;  // fresh chunks belong to this symbol for good
+          }
+        }
+      }
+    } else if (Stot > D) {  // surpluses left over: linked in front of the free list
+      for (uint32_t u = D + lane; u < Stot; u += 64) {
+        const uint32_t c = ag.fr[ab + D + u];
+        bk.chunks[c].hdr.next = u + 1 < Stot ? ag.fr[ab + D + u + 1] : fh;
+      }
+      fh = auniu(ag.fr[ab + D + D]);
+    }
+    if (lane == 0) {
+      sl->alloc_base = ab;
+      sl->free_head = fh;
+    }
+  }
+}
+
+// One wave per segment: the surviving rests into the level's tail chunk and new chunks (in order),
+// the new chunks' headers and links, the seq ring, the level's head / tail / tail fill.
+__global__ __launch_bounds__(256) void k_agg_place(BookDev bk, BatchDev bt, AggDev ag) {
+  const int lane = lane_id();
+  const uint32_t gw = blockIdx.x * 4u + (threadIdx.x >> 6), nw = gridDim.x * 4u;
+  const uint32_t nseg = min(*(volatile uint32_t*)&ag.ctr[AC_SEG], ag.ev_cap);
+  for (uint32_t si = gw; si < nseg; si += nw) {
+    const AggSeg sg = ag.seg[si];
+    const uint32_t slot_i = auniu(sg.slot), lvl = auniu(sg.lvl), start = auniu(sg.start), cnt = auniu(sg.cnt);
+    const AggSlot* sl = ag.slot + slot_i;
+    const uint32_t s = auniu(sl->s), alloc_base = auniu(sl->alloc_base);
+    const long long base = (long long)rl64((unsigned long long)sl->base, 0);
+    const AggSegS g = ag.segs[si];
+    const unsigned long long C = rl64(g.C, 0), T0 = rl64(g.T0, 0);
+    const uint32_t newhead = auniu(g.newhead), need = auniu(g.need), ks = auniu(g.ks);
+    const uint32_t nfreed = auniu(g.nfreed), fr_base = auniu(g.fr_base), d_off = auniu(g.d_off);
+    const uint32_t own = min(need, nfreed);
+    const size_t li = (size_t)s * bk.L + lvl;
+    const uint32_t head0 = auniu(bk.levels[li].head), tail0 = auniu(bk.levels[li].tail);
+    const uint32_t te0 = newhead != NIL ? auniu((uint32_t)bk.tend[li]) : 0u;
+    const uint32_t tailfree = newhead != NIL ? (uint32_t)ME_C - te0 : 0u;
+    auto newchunk = [&](uint32_t c) -> uint32_t {
+      return c < own ? ag.fr[fr_base + c] : ag.fr[alloc_base + d_off + (c - own)];
+    };
+    const bool exhausted = T0 != ~0ull;
+    const unsigned long long Cr = exhausted && C > T0 ? C - T0 : 0ull;
+    if (ks) {
+      unsigned long long RR = 0;
+      uint32_t g0 = 0;
+      for (uint32_t b = 0; b < cnt; b += 64) {
+        const bool v = b + (uint32_t)lane < cnt;
+        const uint32_t e = v ? ag.evs[start + b + lane] : 0u;
+        AggEv E{};
+        if (v) E = ag.ev[e];
+        const bool rs = v && (E.j & AGG_TAKE) == 0u;
+        const long long rq = rs ? (long long)E.qty : 0ll;
+        const long long inc = wave_incl_scan(rq);
+        const unsigned long long st0 = RR + (unsigned long long)(inc - rq), en = RR + (unsigned long long)inc;
+        const bool surv = rs && en > Cr;
+        const unsigned long long sm = __ballot(surv);
+        if (surv) {
+          const uint32_t gi = g0 + (uint32_t)__popcll(sm & lanemask_lt());
+          uint32_t chk, slt;
+          if (gi < tailfree) {
+            chk = tail0;
+            slt = te0 + gi;
+          } else {
+            const uint32_t gg = gi - tailfree;
+            chk = newchunk(gg / ME_C);
+            slt = gg % ME_C;
+          }
+          const unsigned long long sq = a_seq_of(bt, E.j);
+          const int left = (int)(en - (st0 > Cr ? st0 : Cr));
+          if (chk < bk.nchunks) {
+            bk.chunks[chk].qty[slt] = left;
+            bk.chunks[chk].seq[slt] = sq;
+            bk.loc[sq & bk.ring_mask] = chk * ME_C + slt;
+          }
+        }
+        g0 += (uint32_t)__popcll(sm);
+        RR += (unsigned long long)rli64(inc, 63);
+      }
+    }
+    for (uint32_t c = lane; c < need; c += 64) {
+      const uint32_t chk = newchunk(c);
+      if (chk >= bk.nchunks) continue;
+      ChunkHdr h;
+      h.next = c + 1 < need ? newchunk(c + 1) : NIL;
+      h.prev = c ? newchunk(c - 1) : (newhead != NIL ? tail0 : NIL);
+      h.price = base + (long long)lvl;
+      bk.chunks[chk].hdr = h;
+    }
+    const uint32_t first_new = need ? auniu(newchunk(0)) : NIL;
+    const uint32_t last_new = need ? auniu(newchunk(need - 1)) : NIL;
+    if (lane == 0) {
+      if (newhead != NIL && need && tail0 < bk.nchunks) bk.chunks[tail0].hdr.next = first_new;
+      if (newhead != NIL && newhead != head0 && newhead < bk.nchunks) bk.chunks[newhead].hdr.prev = NIL;
+      const uint32_t hd = newhead != NIL ? newhead : first_new;
+      const uint32_t tl = need ? last_new : (newhead != NIL ? tail0 : NIL);
+      const uint32_t te = need ? ((ks - tailfree - 1u) % ME_C) + 1u : (newhead != NIL ? te0 + ks : 0u);
+      bk.levels[li].head = hd;
+      bk.levels[li].tail = tl;
+      bk.tend[li] = (uint8_t)te;
+    }
+  }
+}
+
+// One workgroup per hot symbol: the fill offsets (exclusive scan of the events' fill counts in log
+// order = tape order), the records' results, the symbol's state, the continuation's scratch position.
+__global__ __launch_bounds__(1024) void k_agg_fin(BookDev bk, BatchDev bt, AggDev ag) {
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t carry_s;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint32_t nh = min(*(volatile uint32_t*)bk.hcount, bk.S);
+  constexpr uint32_t PER = 8;
+  for (uint32_t i = blockIdx.x; i < nh; i += gridDim.x) {
+    const AggSlot sl = ag.slot[i];
+    if (!sl.active) continue;
+    const uint32_t eb = sl.ev_base, n = sl.ev_cnt;
+    uint32_t carry = 0;
+    for (uint32_t t0 = 0; t0 < n; t0 += 1024 * PER) {
+      const uint32_t b = t0 + (uint32_t)tid * PER;
+      uint32_t v[PER], loc = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < PER; ++k) {
+        v[k] = b + k < n ? ag.evn[eb + b + k] : 0u;
+        loc += v[k];
+      }
+      uint32_t x = loc;
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t t = __shfl_up(x, d, 64);
+        if (lane >= d) x += t;
+      }
+      if (lane == 63) wsum[wv] = x;
+      __syncthreads();
+      uint32_t pre = 0, tot = 0;
+      for (int k = 0; k < 16; ++k) {
+        if (k < wv) pre += wsum[k];
+        tot += wsum[k];
+      }
+      uint32_t r = carry + pre + x - loc;
+#pragma unroll
+      for (uint32_t k = 0; k < PER; ++k)
+        if (b + k < n) {
+          ag.evx[eb + b + k] = r;
+          r += v[k];
+        }
+      carry += tot;
+      __syncthreads();
+    }
+    if (tid == 0) carry_s = carry;
+    __syncthreads();
+    const uint32_t ftot = carry_s;
+    __threadfence_block();
+    for (uint32_t j = sl.lo + (uint32_t)tid; j < sl.pos; j += 1024) {
+      const AggRec rc = ag.rec[j];
+      uint32_t nfill = 0, fo = 0;
+      if (rc.ev_n) {
+        const uint32_t la = rc.ev_lo + rc.ev_n - 1u;
+        fo = ag.evx[rc.ev_lo];
+        nfill = ag.evx[la] + ag.evn[la] - fo;
+      }
+      const uint32_t oi = bt.perm[j];
+      me_order_result o;
+      o.filled_qty = rc.filled;
+      o.remaining_qty = rc.rem;
+      o.fill_count = nfill;
+      o.tape_offset = 0;
+      o.status = (uint8_t)(rc.st & 0xFF);
+      o.reason = (uint8_t)(rc.st >> 8);
+      o.pad[0] = o.pad[1] = 0;
+      bt.res[oi] = o;
+      bt.fstart[oi] = (uint32_t)(sl.wbase + fo);
+      if (nfill) atomicAdd(&bt.tile_sum[oi / TILE_TAPE], nfill);
+    }
+    if (tid == 0) {
+      SymState o = bk.sym[sl.s];
+      o.best_bid = sl.bb;
+      o.best_ask = sl.ba;
+      o.free_head = ag.slot[i].free_head;
+      const int dr = ag.slot[i].dresting;
+      o.resting = (uint32_t)((int)sl.resting0 + dr);
+      bk.sym[sl.s] = o;
+      if (dr) atomicAdd(bk.stats + ST_RESTING, (unsigned long long)(long long)dr);
+      if (sl.hidx != NIL) {
+        const unsigned long long wp = sl.wbase + ftot;
+        bk.hand[bk.S + sl.hidx].wptr = (uint32_t)wp;
+        bk.hand[bk.S + sl.hidx].wend = (uint32_t)(wp >> 32);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// One thread per take event: its fills (the makers overlapping its interval) into the scratch run at
+// the record's tape position.
+__global__ __launch_bounds__(1024) void k_agg_emit(BookDev bk, BatchDev bt, AggDev ag) {
+  const uint32_t nh = min(*(volatile uint32_t*)bk.hcount, bk.S);
+  for (uint32_t i = blockIdx.x; i < nh; i += gridDim.x) {
+    const AggSlot sl = ag.slot[i];
+    if (!sl.active) continue;
+    const uint32_t eb = sl.ev_base, n = sl.ev_cnt;
+    for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) {
+      const uint32_t e = eb + t;
+      const AggEv E = ag.ev[e];
+      if (!(E.j & AGG_TAKE)) continue;
+      const uint32_t nf = ag.evn[e];
+      if (!nf) continue;
+      const uint32_t first = ag.evf[e];
+      const unsigned long long a = ag.eva[e], z = a + (unsigned long long)E.qty;
+      const unsigned long long p = sl.wbase + ag.evx[e];
+      me_fill f;
+      f.taker_seq = a_seq_of(bt, E.j & ~AGG_TAKE);
+      f.price_q4 = sl.base + (long long)E.lvl;
+      f.symbol = sl.gs;
+      unsigned long long lo = a;
+      for (uint32_t k = 0; k < nf; ++k) {
+        const AggMk m = ag.mk[first + k];
+        const unsigned long long hi = m.end < z ? m.end : z;
+        f.maker_seq = m.seq;
+        f.qty = (int)(hi - lo);
+        bt.scratch[p + k] = f;
+        lo = hi;
+      }
+    }
+  }
+}
+
+}  // namespace
+
+hipError_t launch_agg(hipStream_t hs, const BookDev& bk, const BatchDev& bt, const AggDev& ag) {
+  hipLaunchKernelGGL(k_agg_walk, dim3(64), dim3(64), 0, hs, bk, bt, ag);
+  hipLaunchKernelGGL(k_agg_group, dim3(64), dim3(1024), (size_t)bk.L * 4u, hs, bk, ag);
+  hipLaunchKernelGGL(k_agg_levels, dim3(1024), dim3(256), 0, hs, bk, bt, ag);
+  hipLaunchKernelGGL(k_agg_alloc, dim3(64), dim3(64), 0, hs, bk, ag);
+  hipLaunchKernelGGL(k_agg_place, dim3(1024), dim3(256), 0, hs, bk, bt, ag);
+  hipLaunchKernelGGL(k_agg_fin, dim3(64), dim3(1024), 0, hs, bk, bt, ag);
+  hipLaunchKernelGGL(k_agg_emit, dim3(64), dim3(1024), 0, hs, bk, bt, ag);
+  return hipGetLastError();
+}
+
+}  // namespace me

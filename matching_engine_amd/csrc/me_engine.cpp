@@ -332,6 +332,12 @@ static void free_all(me_engine* e) {
         if (p) (void)hipFree(p);
     }
   }
+  {
+    const AggDev& a = e->hot.ag;
+    void* ap[] = {a.slot, a.ev, a.evs, a.eva, a.evf, a.evn, a.evx, a.seg, a.segs, a.mk, a.fr, a.rec, a.ctr};
+    for (void* p : ap)
+      if (p) (void)hipFree(p);
+  }
   for (void* p : e->user_allocs) (void)hipFree(p);
   e->user_allocs.clear();
   for (auto& h : e->hs) {
@@ -495,11 +501,14 @@ extern "C" me_engine* me_create(const me_config* cfg) {
   const uint64_t ring = cfg->seq_ring ? cfg->seq_ring : (1ull << 28);
   bk.ring_mask = ring - 1;
   bk.fcap = cfg->far_levels ? cfg->far_levels : 1024u;
-  // deep windows in HBM (L > LDS_MAX_LEVELS): a symbol with at least hot_min records in a batch runs
-  // the write-through top-of-book path (k_match_hot); ME_HOT_MIN overrides (0 = off)
+  // deep windows (L > 128, the sort path): a symbol with at least hot_min records in a batch runs the
+  // aggregate path (me_agg.hip, L <= AGG_MAX_L) — or, with ME_HOT_AGG=0, the write-through top-of-book
+  // path k_match_hot (HBM ladders, L > LDS_MAX_LEVELS); ME_HOT_MIN overrides the threshold (0 = off)
   {
     const char* v = getenv("ME_HOT_MIN");
-    bk.hot_min = L > LDS_MAX_LEVELS ? (v ? (uint32_t)atoi(v) : 512u) : 0u;
+    const char* va = getenv("ME_HOT_AGG");
+    e->hot.agg = L > 128 && L <= AGG_MAX_L && !(va && atoi(va) == 0);
+    bk.hot_min = (e->hot.agg || L > LDS_MAX_LEVELS) ? (v ? (uint32_t)atoi(v) : 512u) : 0u;
     if (bk.hot_min) {
       if ((he = hipStreamCreateWithFlags(&e->hot.st, hipStreamNonBlocking)) != hipSuccess ||
           (he = hipEventCreateWithFlags(&e->hot.fork, hipEventDisableTiming)) != hipSuccess ||
@@ -530,6 +539,35 @@ extern "C" me_engine* me_create(const me_config* cfg) {
   ALLOC(bk.hcount, 2);  // [0] hand-offs of a launch, [1] k_match_hot's continuations
   ALLOC(bk.hand, 2 * S);  // continuations from S on
   ALLOC(bk.stats, ME_STATS);
+  if (bk.hot_min && e->hot.agg) {
+    // the aggregate path's pools (me_agg.hip): the log holds every hot symbol's events (<= 3 records +
+    // its occupied levels each; a symbol that finds no room goes to the generic loop), consumed makers
+    // <= fills <= max_resting + 2n, chunk ids <= 2 x consumed makers + rests
+    AggDev& a = e->hot.ag;
+    const uint64_t evc = 3 * n + 16 * (L + 64) + 4096;
+    const uint64_t mkc = cfg->max_resting + 2 * n + 64;
+    const uint64_t frc = 2 * mkc + n + 64;
+    if (evc >= 0x7FFFFFFFull || frc >= 0xFFFFFFFFull) return bail("me_create: aggregate-path pools exceed 32-bit ids");
+    a.ev_cap = (uint32_t)evc;
+    a.mk_cap = (uint32_t)mkc;
+    a.fr_cap = (uint32_t)frc;
+    ALLOC(a.slot, S);
+    ALLOC(a.ev, evc);
+    ALLOC(a.evs, evc);
+    ALLOC(a.eva, evc);
+    ALLOC(a.evf, evc);
+    ALLOC(a.evn, evc);
+    ALLOC(a.evx, evc);
+    ALLOC(a.seg, evc);
+    ALLOC(a.segs, evc);
+    ALLOC(a.mk, mkc);
+    ALLOC(a.fr, frc);
+    ALLOC(a.rec, n);
+    ALLOC(a.ctr, AC_N);
+    if ((he = hipMemset(a.ctr, 0, AC_N * sizeof(uint32_t))) != hipSuccess)
+      return bail(std::string("hipMemset agg ctr: ") + hipGetErrorString(he));
+    bk.agg_ctr = a.ctr;
+  }
   if ((he = hipHostMalloc((void**)&e->pub_host, sizeof(unsigned long long), hipHostMallocDefault)) != hipSuccess ||
       (he = hipHostGetDevicePointer((void**)&bk.pub, e->pub_host, 0)) != hipSuccess)
     return bail(std::string("me_create: pinned admission word: ") + hipGetErrorString(he));

@@ -1219,7 +1219,7 @@ __global__ __launch_bounds__(256) void k_match(BookDev bk, BatchDev bt) {
     reject_bad_symbols(bt, lo, hi);
     return;
   }
-  if (kLad == LAD_HBM && bk.hot_min && hi - lo >= bk.hot_min) return;  // k_match_hot's (k_hot_pick)
+  if (bk.hot_min && hi - lo >= bk.hot_min) return;  // k_match_hot's / the aggregate path's (k_hot_pick)
   const uint32_t L = bk.L;
   Level* g_lv = bk.levels + (size_t)s * L;
   unsigned long long* g_occ = bk.occ + (size_t)s * bk.Lwords;
@@ -2356,6 +2356,8 @@ __global__ __launch_bounds__(256) void k_seq_sweep(BookDev bk, SeqGroup sg) {
     bk.sq[sg.in ^ 1u] = o;
     bk.hcount[0] = 0;  // the match launch after this one hands symbols off from 0 ...
     bk.hcount[1] = 0;  // ... and continues them (k_match_hot_cont) from 0
+    if (bk.agg_ctr)
+      for (uint32_t k = 0; k < AC_N; ++k) bk.agg_ctr[k] = 0;  // the aggregate path's pools (me_agg.hip)
     if (bk.pub) {  // resting orders after sg.launch match launches, for the host's admission bound
       const unsigned long long r = bk.stats[ST_RESTING];
       *bk.pub = ((unsigned long long)sg.launch << 32) | (r < 0xFFFFFFFFull ? r : 0xFFFFFFFFull);
@@ -2531,32 +2533,46 @@ hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* b
 // (hipExtLaunchKernelGGL), so timing adds no marker packet — and no gap — to the stream.
 // hot (deep windows with bk.hot_min): the stream and fork / join events k_match_hot runs with, beside
 // k_match (same symbols never meet: k_match skips what k_hot_pick listed).
+hipError_t launch_agg(hipStream_t hs, const BookDev& bk, const BatchDev& bt, const AggDev& ag);  // me_agg.hip
+
 hipError_t launch_match(hipStream_t st, const BookDev& bk, const BatchDev& bt, hipEvent_t ev0, hipEvent_t ev1,
                         const HotLaunch& hot) {
   const uint32_t waves = bk.S + 1;
   const dim3 grid((waves + 3) / 4), block(256);
-  if (bk.L <= 128) {
-    return launch_match_reg(st, bk, &bt, 1u, AuxDev{}, ev0, ev1);
-  } else if (bk.L <= LDS_MAX_LEVELS) {
-    hipExtLaunchKernelGGL(k_match<LAD_LDS>, grid, block, 4 * lds_wave_bytes(bk.L), st, ev0, ev1, 0, bk, bt);
-  } else if (!bk.hot_min || !hot.st || bk.L > HOT_MAX_WORDS * 64u) {
+  if (bk.L <= 128) return launch_match_reg(st, bk, &bt, 1u, AuxDev{}, ev0, ev1);
+  const bool lds = bk.L <= LDS_MAX_LEVELS;
+  // hot symbols: the aggregate path (windows up to AGG_MAX_L) or k_match_hot (HBM ladders up to
+  // HOT_MAX_WORDS * 64 levels), on the hot stream beside k_match
+  const bool hot_on = bk.hot_min && hot.st &&
+                      (hot.agg ? bk.L <= AGG_MAX_L : (!lds && bk.L <= HOT_MAX_WORDS * 64u));
+  if (!hot_on) {
     BookDev b2 = bk;
     b2.hot_min = 0;
-    hipExtLaunchKernelGGL(k_match<LAD_HBM>, grid, block, 0, st, ev0, ev1, 0, b2, bt);
-  } else {
-    // hcount was zeroed by k_seq_sweep; the pick starts the timed span, the join ends it
-    const uint32_t pick = bt.bin_start ? bk.S : bt.n;
-    hipExtLaunchKernelGGL(k_hot_pick, dim3((pick + 255) / 256), dim3(256), 0, st, ev0, nullptr, 0, bk, bt);
-    hipError_t e;
-    if ((e = hipEventRecord(hot.fork, st)) != hipSuccess || (e = hipStreamWaitEvent(hot.st, hot.fork, 0)) != hipSuccess)
-      return e;
-    hipLaunchKernelGGL(k_match_hot, dim3(64), dim3(64), 0, hot.st, bk, bt);
-    hipLaunchKernelGGL(k_match_hot_cont, dim3(64), dim3(64), 0, hot.st, bk, bt);
-    if ((e = hipEventRecord(hot.join, hot.st)) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_match<LAD_HBM>, grid, block, 0, st, bk, bt);
-    if ((e = hipStreamWaitEvent(st, hot.join, 0)) != hipSuccess) return e;
-    if (ev1 && (e = hipEventRecord(ev1, st)) != hipSuccess) return e;
+    if (lds)
+      hipExtLaunchKernelGGL(k_match<LAD_LDS>, grid, block, 4 * lds_wave_bytes(bk.L), st, ev0, ev1, 0, b2, bt);
+    else
+      hipExtLaunchKernelGGL(k_match<LAD_HBM>, grid, block, 0, st, ev0, ev1, 0, b2, bt);
+    return hipGetLastError();
   }
+  // hcount was zeroed by k_seq_sweep; the pick starts the timed span, the join ends it
+  const uint32_t pick = bt.bin_start ? bk.S : bt.n;
+  hipExtLaunchKernelGGL(k_hot_pick, dim3((pick + 255) / 256), dim3(256), 0, st, ev0, nullptr, 0, bk, bt);
+  hipError_t e;
+  if ((e = hipEventRecord(hot.fork, st)) != hipSuccess || (e = hipStreamWaitEvent(hot.st, hot.fork, 0)) != hipSuccess)
+    return e;
+  if (hot.agg) {
+    if ((e = launch_agg(hot.st, bk, bt, hot.ag)) != hipSuccess) return e;
+  } else {
+    hipLaunchKernelGGL(k_match_hot, dim3(64), dim3(64), 0, hot.st, bk, bt);
+  }
+  hipLaunchKernelGGL(k_match_hot_cont, dim3(64), dim3(64), 0, hot.st, bk, bt);
+  if ((e = hipEventRecord(hot.join, hot.st)) != hipSuccess) return e;
+  if (lds)
+    hipLaunchKernelGGL(k_match<LAD_LDS>, grid, block, 4 * lds_wave_bytes(bk.L), st, bk, bt);
+  else
+    hipLaunchKernelGGL(k_match<LAD_HBM>, grid, block, 0, st, bk, bt);
+  if ((e = hipStreamWaitEvent(st, hot.join, 0)) != hipSuccess) return e;
+  if (ev1 && (e = hipEventRecord(ev1, st)) != hipSuccess) return e;
   return hipGetLastError();
 }
 

@@ -148,11 +148,76 @@ struct Handoff {
   uint32_t pad[2];
 };
 
-// Host side of a deep-window launch with hot symbols: k_match_hot runs on `st`, forked from and joined
-// back into the engine stream by two events (me_kernels.hip launch_match).
+// ---- hot symbols in aggregate form (me_agg.hip) ------------------------------------
+// A hot symbol's records are matched against LEVEL TOTALS only (one serial wave: which levels a taker
+// empties, how much it takes from the last, where a remainder rests), logged as events; the FIFO
+// detail — which makers each take consumed — is resolved afterwards for all levels in parallel.
+struct AggEv {       // one event of the log, in record order
+  uint32_t lvl;      // window level
+  uint32_t j;        // grouped position of the record | AGG_TAKE for a take
+  int32_t qty;       // quantity taken from / rested on the level
+  uint32_t pad;
+};
+constexpr uint32_t AGG_TAKE = 1u << 31;
+constexpr uint32_t AGG_MAX_L = 32768;  // windows up to this depth (level histogram in LDS)
+struct AggRec {      // a record the walk handled (indexed by grouped position)
+  int32_t filled, rem;
+  uint32_t st;       // status | reason << 8
+  uint32_t ev_lo;    // its first take event (log index) ...
+  uint32_t ev_n;     // ... and its take events
+  uint32_t pad;
+};
+struct AggSeg {      // the events of one (slot, level), in log order: evs[start, start + cnt)
+  uint32_t slot, lvl, start, cnt;
+};
+struct AggSegS {     // what the first per-level pass found (k_agg_levels), for the second (k_agg_place)
+  unsigned long long C;   // quantity taken from the level by the batch
+  unsigned long long T0;  // live quantity of the initial FIFO if the takes exhausted it, else ~0
+  uint32_t newhead;       // first surviving chunk of the initial FIFO (NIL: none)
+  uint32_t mk_base, nmk;  // consumed makers in AggDev::mk
+  uint32_t fr_base, nfreed;  // initial chunks the takes emptied, in AggDev::fr
+  uint32_t need;          // chunks the surviving rests need beyond the tail's free slots
+  uint32_t d_off;         // this level's share of the slot's deficit (need beyond its own freed chunks)
+  uint32_t ks;            // surviving rests
+};
+struct AggMk {       // a consumed maker: seq and the end of its interval in the level's maker space
+  unsigned long long seq, end;
+};
+struct AggSlot {     // one hot symbol of the launch (index = k_hot_pick's hand-off index)
+  uint32_t s, lo, hi, pos;   // symbol, grouped records [lo, hi), first record left to k_match_hot_cont
+  unsigned long long wbase;  // scratch run
+  long long base;
+  uint32_t ev_base, ev_cnt, seg_base, nseg;
+  uint32_t deficit, alloc_base, free_head, resting0;
+  int32_t dresting;
+  int32_t bb, ba;
+  uint32_t active, hidx, gs, pad[2];
+};
+enum : uint32_t { AC_EV = 0, AC_SEG = 1, AC_MK = 2, AC_FR = 3, AC_N = 8 };
+struct AggDev {
+  AggSlot* slot;               // [S]
+  AggEv* ev;                   // [ev_cap] event log (per-slot regions)
+  uint32_t* evs;               // [ev_cap] log indices grouped by level (stable)
+  unsigned long long* eva;     // [ev_cap] take: start of its interval in the level's maker space
+  uint32_t* evf;               // [ev_cap] take: its first maker (AggDev::mk index)
+  uint32_t* evn;               // [ev_cap] fills of the event (0 for rests)
+  uint32_t* evx;               // [ev_cap] exclusive scan of evn over the slot's log
+  AggSeg* seg;                 // [ev_cap]
+  AggSegS* segs;               // [ev_cap]
+  AggMk* mk;                   // [mk_cap]
+  uint32_t* fr;                // [fr_cap] chunk ids: freed by levels, surpluses, allocations
+  AggRec* rec;                 // [max_batch]
+  uint32_t* ctr;               // [AC_N] pool tops (zeroed by k_seq_sweep)
+  uint32_t ev_cap, mk_cap, fr_cap, pad;
+};
+
+// Host side of a deep-window launch with hot symbols: k_match_hot (or the aggregate path) runs on `st`,
+// forked from and joined back into the engine stream by two events (me_kernels.hip launch_match).
 struct HotLaunch {
   hipStream_t st = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
+  bool agg = false;  // the aggregate path (me_agg.hip) instead of k_match_hot
+  AggDev ag{};
 };
 
 // Event counters kept on the device (BookDev::stats, me_stats_read).
@@ -188,7 +253,9 @@ struct BookDev {
   uint32_t L;
   uint32_t Lwords;
   uint32_t hot_min;       // deep windows: a symbol with at least this many records in a batch is matched
-                          // by k_match_hot (me_kernels.hip) instead of k_match; 0 = never
+                          // by k_match_hot (me_kernels.hip) or the aggregate path (me_agg.hip) instead
+                          // of k_match; 0 = never
+  uint32_t* agg_ctr;      // AggDev::ctr (zeroed by k_seq_sweep with hcount), or null
 };
 
 // Far array of (symbol s, side k): k = 0 bids below the window, 1 asks above it.

@@ -1,7 +1,9 @@
-"""k_match_hot — the write-through top-of-book path for hot symbols of deep windows (L > 1,024,
-me_kernels.hip) — against the CPU oracle, bit-exact per batch. ME_HOT_MIN (read at me_create) sets the
-records per batch that make a symbol hot; 1 sends every symbol through it, so the generic fallbacks
-(cancels, prices outside the window, far levels, re-centring) run inside the hot path too."""
+"""The hot-symbol paths of deep windows against the CPU oracle, bit-exact per batch: the aggregate path
+(me_agg.hip: a level-total walk per hot symbol, FIFO resolution per level in parallel; the default for
+128 < L <= 32,768) and k_match_hot (the write-through top-of-book path, me_kernels.hip; ME_HOT_AGG=0).
+ME_HOT_MIN (read at me_create) sets the records per batch that make a symbol hot; 1 sends every symbol
+through the hot path, so the generic fallbacks (cancels, prices outside the window, far levels,
+re-centring: k_match_hot_cont) run behind it too."""
 import os
 
 import numpy as np
@@ -43,17 +45,19 @@ def orc(built):
     return oracle
 
 
-def _engine(me, hot_min, *a, **kw):
-    old = os.environ.get("ME_HOT_MIN")
-    os.environ["ME_HOT_MIN"] = str(hot_min)
+def _engine(me, hot_min, *a, agg=1, **kw):
+    env = {"ME_HOT_MIN": str(hot_min), "ME_HOT_AGG": str(agg)}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         kw.setdefault("seq_ring", 1 << 22)
         return me.Engine(*a, **kw)
     finally:
-        if old is None:
-            del os.environ["ME_HOT_MIN"]
-        else:
-            os.environ["ME_HOT_MIN"] = old
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
 
 
 def _drift(me, levels, num_symbols, batch, nbatches, **over):
@@ -65,47 +69,51 @@ def _drift(me, levels, num_symbols, batch, nbatches, **over):
     return sc, st.base_prices(), [st.next(batch) for _ in range(nbatches)]
 
 
+@pytest.mark.parametrize("agg", [1, 0])
 @pytest.mark.parametrize("hot_min", [1, 64])
-def test_hot_drift_far_cancels(me, orc, hot_min):
+def test_hot_drift_far_cancels(me, orc, hot_min, agg):
     """Mids drifting past the 2,048-level windows, 1 % far LIMITs, 10 % cancels, sweeping MARKETs:
     every generic fallback inside the hot path (cancel, out-of-window rest with re-centring, takers while
     far levels exist), list rebuilds and deep rests."""
     sc, base, batches = _drift(me, 2048, 6, 6144, 60)
     ob = orc.OracleBook(sc.num_symbols)
     total = sum(len(b) for b in batches)
-    with _engine(me, hot_min, sc.num_symbols, sc.levels, base, max_batch=sc.batch, max_resting=total + 64,
-                 max_chunks=total + 64) as eng:
-        nf = run_both(eng, ob, batches, ctx=f"hot drift min={hot_min}")
+    with _engine(me, hot_min, sc.num_symbols, sc.levels, base, agg=agg, max_batch=sc.batch,
+                 max_resting=total + 64, max_chunks=total + 64) as eng:
+        nf = run_both(eng, ob, batches, ctx=f"hot drift min={hot_min} agg={agg}")
     assert nf > 0
 
 
-def test_hot_sweeps_drain_lists(me, orc):
+@pytest.mark.parametrize("agg", [1, 0])
+def test_hot_sweeps_drain_lists(me, orc, agg):
     """MARKETs of up to 40 x 100 qty against thin levels: a sweep consumes more than the 64 listed
     levels and the list is rebuilt mid-sweep; no cancels, no far prices."""
     sc, base, batches = _drift(me, 4096, 3, 4096, 40, cancel_pct=0, far_pct=0, market_qty_mult=40,
                                market_pct=10, drift_every=0, drift_step=0)
     ob = orc.OracleBook(sc.num_symbols)
     total = sum(len(b) for b in batches)
-    with _engine(me, 1, sc.num_symbols, sc.levels, base, max_batch=sc.batch, max_resting=total + 64,
+    with _engine(me, 1, sc.num_symbols, sc.levels, base, agg=agg, max_batch=sc.batch, max_resting=total + 64,
                  max_chunks=total + 64) as eng:
-        nf = run_both(eng, ob, batches, ctx="hot sweeps")
+        nf = run_both(eng, ob, batches, ctx=f"hot sweeps agg={agg}")
     assert nf > 0
 
 
-def test_hot_multichunk_levels(me, orc):
+@pytest.mark.parametrize("agg", [1, 0])
+def test_hot_multichunk_levels(me, orc, agg):
     """A 4-tick spread on a 2,048-level window: levels hold dozens of orders (chunk chains), walks cross
     chunk boundaries (the one load of a walk) and appends open new tail chunks."""
     sc, base, batches = _drift(me, 2048, 2, 4096, 30, cancel_pct=5, far_pct=0, spread_ticks=4, drift_every=0,
                                drift_step=0, market_qty_mult=2)
     ob = orc.OracleBook(sc.num_symbols)
     total = sum(len(b) for b in batches)
-    with _engine(me, 1, sc.num_symbols, sc.levels, base, max_batch=sc.batch, max_resting=total + 64,
+    with _engine(me, 1, sc.num_symbols, sc.levels, base, agg=agg, max_batch=sc.batch, max_resting=total + 64,
                  max_chunks=total + 64) as eng:
-        nf = run_both(eng, ob, batches, ctx="hot multichunk")
+        nf = run_both(eng, ob, batches, ctx=f"hot multichunk agg={agg}")
     assert nf > 0
 
 
-def test_hot_equals_generic_config4(me, orc):
+@pytest.mark.parametrize("agg", [1, 0])
+def test_hot_equals_generic_config4(me, orc, agg):
     """Config 4's shape (Zipf symbols, L = 32,768, books seeded to 3,000 levels per side): the hot path
     (default threshold) and the generic kernel alone (ME_HOT_MIN=0) give identical outputs, both equal
     to the oracle."""
@@ -119,8 +127,8 @@ def test_hot_equals_generic_config4(me, orc):
     outs = []
     for hot_min in (512, 0):
         ob = orc.OracleBook(sc.num_symbols)
-        with _engine(me, hot_min, sc.num_symbols, sc.levels, base, max_batch=32768, max_resting=total + 1024,
-                     max_chunks=total + 1024) as eng:
+        with _engine(me, hot_min, sc.num_symbols, sc.levels, base, agg=agg, max_batch=32768,
+                     max_resting=total + 1024, max_chunks=total + 1024) as eng:
             got = []
             for b in batches:
                 got.append(eng.submit_batch(b))
@@ -131,3 +139,35 @@ def test_hot_equals_generic_config4(me, orc):
             outs.append([eng.dump(s) for s in range(0, 300, 7)])
     for a, b in zip(*outs):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("levels", [256, 2048])
+def test_agg_single_symbol_config1(me, orc, levels):
+    """Config 1's shape (one symbol, 80 % LIMIT +-32 ticks, 20 % MARKET): every record of every batch on
+    the aggregate path (no hand-off), deep multi-chunk levels, the walk's list inserts and pops; L = 256
+    runs k_match's LDS-ladder build beside it, 2,048 the HBM build."""
+    sc = me.preset(1, levels=levels, batch=16384)
+    st = me.Stream(sc)
+    base = st.base_prices()
+    batches = [st.next(sc.batch) for _ in range(12)]
+    ob = orc.OracleBook(sc.num_symbols)
+    total = sum(len(b) for b in batches)
+    with _engine(me, 512, sc.num_symbols, sc.levels, base, max_batch=sc.batch, max_resting=total + 64,
+                 max_chunks=total + 64) as eng:
+        nf = run_both(eng, ob, batches, ctx=f"agg c1 L={levels}")
+    assert nf > 0
+
+
+@pytest.mark.parametrize("spread", [2, 40, 700])
+def test_agg_many_symbols_no_handoff(me, orc, spread):
+    """Every symbol hot (ME_HOT_MIN=1) on a 1,024-level window, no cancels, no far prices: the aggregate
+    path alone, with tight spreads (long FIFOs, sweeps through many makers per level) and wide ones
+    (deep rests beyond the 64-entry lists, list rebuilds)."""
+    sc, base, batches = _drift(me, 1024, 40, 8192, 25, cancel_pct=0, far_pct=0, spread_ticks=spread,
+                               drift_every=0, drift_step=0, market_qty_mult=4, market_pct=20)
+    ob = orc.OracleBook(sc.num_symbols)
+    total = sum(len(b) for b in batches)
+    with _engine(me, 1, sc.num_symbols, sc.levels, base, max_batch=sc.batch, max_resting=total + 64,
+                 max_chunks=total + 64) as eng:
+        nf = run_both(eng, ob, batches, ctx=f"agg many spread={spread}")
+    assert nf > 0
