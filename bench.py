@@ -71,6 +71,9 @@ def parse():
                     help="c2 (default) = BASELINE configs[1], the metric's workload; c3/c4/c5 = the other "
                          "BASELINE configs as secondary lines (DESIGN.md §7)")
     ap.add_argument("--symbols-per-gpu", type=int, default=None)
+    ap.add_argument("--levels", type=int, default=None,
+                    help="window L override (experiments: L > 128 runs the sort path; with ME_HOT_MIN=1 every "
+                         "symbol takes the aggregate hot-symbol path)")
     ap.add_argument("--batch-per-gpu", type=int, default=None)
     ap.add_argument("--seq-ring", type=int, default=1 << 28,
                     help="me_config.seq_ring (seq-ring entries for cancels; 2^28 is the engine default)")
@@ -101,6 +104,8 @@ def parse():
         args.symbols_per_gpu = w.get("symbols_per_gpu", 0)
     if args.batch_per_gpu is None:
         args.batch_per_gpu = w["batch_per_gpu"]
+    if args.levels is not None:
+        w["levels"] = args.levels
     return args
 
 

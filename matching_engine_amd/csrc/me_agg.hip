@@ -43,6 +43,10 @@ __device__ __forceinline__ uint32_t auniu(uint32_t v) { return (uint32_t)__built
 __device__ __forceinline__ void a_set_err(const BookDev& bk, uint32_t bits) {
   if (lane_id() == 0) atomicOr(bk.err, bits);
 }
+// Slots of the launch: every symbol (grouped launches) or k_hot_pick's hot symbols.
+__device__ __forceinline__ uint32_t a_nslots(const BookDev& bk, const AggDev& ag) {
+  return ag.nslots ? ag.nslots : min(*(volatile uint32_t*)bk.hcount, bk.S);
+}
 
 // lane i <- lane i - 1 (gfx9 DPP wave_ror:1): an entry enters mid-list by rotating the ones behind it
 __device__ __forceinline__ uint32_t a_up(uint32_t v) {
@@ -82,22 +86,34 @@ struct AWalk {
   gptr<unsigned long long> occ;
   gptr<AggEv> ev;
   unsigned long long* locc;  // LDS copy of the occupancy bitmap (both sides)
-  uint32_t evp;              // next log index
+  uint32_t evp;              // next log index (the slot's log starts 64-aligned)
   int L, W;
+  // the log's current 64-event block, event i in lane i: stored by the whole wave when it fills (one
+  // coalesced 1-KB store instead of a lane-0 store per event)
+  uint32_t q_lvl, q_j;
+  int q_q;
 };
 
 __device__ __forceinline__ int a_side_lvl(int L, int k, int m) { return k ? m : L - 1 - m; }
 
-__device__ __forceinline__ void a_emit(AWalk& w, int lvl, uint32_t jt, int q) {
-  if (lane_id() == 0) {
+// Lanes [0, n) of the staged block to log indices [base, base + n).
+__device__ __forceinline__ void a_evstore(AWalk& w, uint32_t base, uint32_t n) {
+  if ((uint32_t)lane_id() < n) {
     AggEv e;
-    e.lvl = (uint32_t)lvl;
-    e.j = jt;
-    e.qty = q;
+    e.lvl = w.q_lvl;
+    e.j = w.q_j;
+    e.qty = w.q_q;
     e.pad = 0;
-    w.ev[w.evp] = e;
+    w.ev[base + (uint32_t)lane_id()] = e;
   }
+}
+__device__ __forceinline__ void a_emit(AWalk& w, int lvl, uint32_t jt, int q) {
+  const bool me = lane_id() == (int)(w.evp & 63u);
+  w.q_lvl = me ? (uint32_t)lvl : w.q_lvl;
+  w.q_j = me ? jt : w.q_j;
+  w.q_q = me ? q : w.q_q;
   w.evp += 1;
+  if (ME_UNLIKELY((w.evp & 63u) == 0u)) a_evstore(w, w.evp - 64u, 64u);
 }
 
 // Occupancy: non-returning atomics on the LDS copy and on HBM (nothing in the chain waits for them).
@@ -279,6 +295,124 @@ __device__ __forceinline__ void a_rest(AWalk& w, AList& M, int mm, int lvl, int 
   a_emit(w, lvl, jt, q);
 }
 
+// Results of one block's records, lane k = record k.
+struct ARes {
+  int rf, rr;
+  uint32_t rs;   // status | reason << 8
+  uint32_t rlo;  // first take event (log index)
+  uint32_t rn;   // take events
+};
+
+// Reject reason (k_match's, in its order; cancels are the generic loop's) and whether the walk covers
+// the record: not a cancel, and a LIMIT inside the window or a MARKET while the side it crosses has no
+// far levels.
+__device__ __forceinline__ bool a_classify(bool v, unsigned long long oseq, long long opx, int oq, uint32_t okd,
+                                           long long base, int L, uint32_t nfar0, uint32_t nfar1, uint32_t& rj,
+                                           int& olm) {
+  const uint32_t side = okd & 3u;
+  const bool market = (okd >> 2) & 1u, cancel = (okd >> 3) & 1u;
+  rj = oq <= 0                                          ? (uint32_t)ME_RJ_BAD_QTY
+       : (side != ME_SIDE_BUY && side != ME_SIDE_SELL) ? (uint32_t)ME_RJ_BAD_SIDE
+       : oseq == 0ull                                   ? (uint32_t)ME_RJ_BAD_SEQ
+                                                        : 0u;
+  const unsigned long long off = (unsigned long long)opx - (unsigned long long)base;
+  const bool inw = off < (unsigned long long)L;
+  const bool farx = (side == ME_SIDE_BUY ? nfar1 : nfar0) != 0u;
+  olm = (int)off;
+  return v && !cancel && (rj != 0u || (market ? !farx : inw));
+}
+
+// A list running low with levels beyond it is rebuilt at a block start (its totals flushed first).
+__device__ __forceinline__ void a_refill(AWalk& w, AList& A, AList& B) {
+  if (A.n < 32 && A.more) {
+    a_flush(w, A, 1);
+    a_drain();
+    a_rebuild<1>(w, A, rli32(A.m, A.f));
+  }
+  if (B.n < 32 && B.more) {
+    a_flush(w, B, 0);
+    a_drain();
+    a_rebuild<0>(w, B, rli32(B.m, B.f));
+  }
+}
+
+// The serial chain over records [0, cnt) of a block in vector form (lane k = record k: quantity, kind,
+// window level, reject reason, log id). Returns the records it matched: fewer than cnt when record k is
+// one the walk does not cover (fastm bit clear).
+__device__ __forceinline__ uint32_t a_block(AWalk& w, AList& A, AList& B, int oq, uint32_t okd, int olm, uint32_t rj,
+                                            uint32_t ojt, unsigned long long fastm, uint32_t cnt, ARes& R) {
+  const int L = w.L;
+  R.rf = R.rr = 0;
+  R.rs = R.rlo = R.rn = 0u;
+  uint32_t k = 0;
+  for (; k < cnt; ++k) {
+    if (ME_UNLIKELY(!((fastm >> k) & 1ull))) break;
+    const uint32_t jt = rl32(ojt, (int)k);
+    const int q = rli32(oq, (int)k);
+    const uint32_t rjk = rl32(rj, (int)k);
+    if (ME_UNLIKELY(rjk != 0u)) {
+      R.rf = a_wl(R.rf, 0, (int)k);
+      R.rr = a_wl(R.rr, rjk == ME_RJ_BAD_QTY ? 0 : q, (int)k);
+      R.rs = a_wlu(R.rs, (uint32_t)ME_ST_REJECTED | (rjk << 8), (int)k);
+      R.rlo = a_wlu(R.rlo, w.evp, (int)k);
+      R.rn = a_wlu(R.rn, 0u, (int)k);
+      continue;
+    }
+    const uint32_t kd = rl32(okd, (int)k);
+    const bool buy = (kd & 3u) == ME_SIDE_BUY;
+    const bool mkt = (kd >> 2) & 1u;
+    const int lm = rli32(olm, (int)k);
+    const uint32_t ev_lo = w.evp;
+    uint32_t rem = (uint32_t)q;
+    uint32_t nte;
+    if (buy) {
+      a_take<1>(w, A, mkt ? L - 1 : lm, rem, jt | AGG_TAKE);
+      nte = w.evp - ev_lo;
+      if (!mkt && rem) a_rest<0>(w, B, L - 1 - lm, lm, (int)rem, jt);
+    } else {
+      a_take<0>(w, B, mkt ? L - 1 : L - 1 - lm, rem, jt | AGG_TAKE);
+      nte = w.evp - ev_lo;
+      if (!mkt && rem) a_rest<1>(w, A, lm, lm, (int)rem, jt);
+    }
+    const int filled = q - (int)rem;
+    uint32_t stt;
+    if (mkt)
+      stt = rem == 0 ? ME_ST_FILLED : ME_ST_CANCELED;
+    else
+      stt = rem == 0 ? ME_ST_FILLED : (filled > 0 ? ME_ST_PARTIALLY_FILLED : ME_ST_NEW);
+    R.rf = a_wl(R.rf, filled, (int)k);
+    R.rr = a_wl(R.rr, (int)rem, (int)k);
+    R.rs = a_wlu(R.rs, stt, (int)k);
+    R.rlo = a_wlu(R.rlo, ev_lo, (int)k);
+    R.rn = a_wlu(R.rn, nte, (int)k);
+  }
+  return k;
+}
+
+__device__ __forceinline__ void a_walk_init(AWalk& w, const BookDev& bk, const AggDev& ag, uint32_t s, uint32_t eb,
+                                            unsigned long long* locc) {
+  w.lv = (gptr<Level>)vptr(bk.levels + (size_t)s * bk.L);
+  w.occ = (gptr<unsigned long long>)vptr(bk.occ + (size_t)s * bk.Lwords);
+  w.ev = (gptr<AggEv>)vptr(ag.ev);
+  w.locc = locc;
+  w.evp = eb;
+  w.q_lvl = w.q_j = 0u;
+  w.q_q = 0;
+  w.L = (int)bk.L;
+  w.W = (int)bk.Lwords;
+  for (int k = lane_id(); k < w.W; k += 64) locc[k] = w.occ[k];
+  wave_mem_order();
+}
+
+// The walk's end: the staged log tail and the listed totals to HBM; the best levels.
+__device__ __forceinline__ void a_walk_end(AWalk& w, AList& A, AList& B, int& bb, int& ba) {
+  if (w.evp & 63u) a_evstore(w, w.evp & ~63u, w.evp & 63u);
+  a_flush(w, A, 1);
+  a_flush(w, B, 0);
+  ba = A.n ? rli32(A.m, A.f) : w.L;
+  bb = B.n ? w.L - 1 - rli32(B.m, B.f) : -1;
+}
+
 __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const AggDev& ag, uint32_t i, uint32_t s,
                                 uint32_t lo, uint32_t hi, unsigned long long* locc) {
   const int lane = lane_id();
@@ -299,8 +433,8 @@ __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const Agg
   // can empty are the ones occupied at the start (<= min(L, resting)) or created by rests
   const uint32_t evneed = 3u * cnt + min((uint32_t)L, resting) + 64u;
   uint32_t eb = 0;
-  if (lane == 0) eb = atomicAdd(&ag.ctr[AC_EV], evneed);
-  eb = rl32(eb, 0);
+  if (lane == 0) eb = atomicAdd(&ag.ctr[AC_EV], evneed + 64u);
+  eb = (rl32(eb, 0) + 63u) & ~63u;  // 64-aligned: the staged blocks are whole lines of the log
   const bool sok = w0 + need <= bt.scratch_cap;
   const bool eok = (unsigned long long)eb + evneed <= ag.ev_cap;
   if (lane == 0) {
@@ -339,21 +473,12 @@ __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const Agg
     return;
   }
   AWalk w;
-  w.lv = (gptr<Level>)vptr(bk.levels + (size_t)s * bk.L);
-  w.occ = (gptr<unsigned long long>)vptr(bk.occ + (size_t)s * bk.Lwords);
-  w.ev = (gptr<AggEv>)vptr(ag.ev);
-  w.locc = locc;
-  w.evp = eb;
-  w.L = L;
-  w.W = (int)bk.Lwords;
-  for (int k = lane; k < w.W; k += 64) locc[k] = w.occ[k];
-  wave_mem_order();
+  a_walk_init(w, bk, ag, s, eb, locc);
   AList A, B;  // asks (side 1), bids (side 0)
   a_rebuild<1>(w, A, ba0);
   a_rebuild<0>(w, B, L - 1 - bb0);
   uint32_t pos = hi;
-  bool stop = false;
-  for (uint32_t blk = lo; blk < hi && !stop; blk += 64) {
+  for (uint32_t blk = lo; blk < hi; blk += 64) {
     const uint32_t j = blk + (uint32_t)lane;
     const bool v = j < hi;
     const uint32_t oi = v ? bt.perm[j] : 0u;
@@ -362,92 +487,29 @@ __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const Agg
     const int oq = v ? bt.qty[oi] : 0;
     const uint32_t okd = v ? (uint32_t)bt.kind[oi] : 0u;
     const uint32_t cntb = min(64u, hi - blk);
-    const uint32_t side = okd & 3u;
-    const bool market = (okd >> 2) & 1u, cancel = (okd >> 3) & 1u;
-    // k_match's reject reasons, in its order (cancels are the generic loop's)
-    const uint32_t rj = oq <= 0                                          ? (uint32_t)ME_RJ_BAD_QTY
-                        : (side != ME_SIDE_BUY && side != ME_SIDE_SELL) ? (uint32_t)ME_RJ_BAD_SIDE
-                        : oseq == 0ull                                   ? (uint32_t)ME_RJ_BAD_SEQ
-                                                                         : 0u;
-    const unsigned long long off = (unsigned long long)opx - (unsigned long long)base;
-    const bool inw = off < (unsigned long long)L;
-    const bool farx = (side == ME_SIDE_BUY ? nfar1 : nfar0) != 0u;  // far levels on the side a MARKET crosses
-    const bool fast = v && !cancel && (rj != 0u || (market ? !farx : inw));
-    const int olm = (int)off;
-    const unsigned long long fastm = __ballot(fast);
-    if (A.n < 32 && A.more) {
-      a_flush(w, A, 1);
-      a_drain();
-      a_rebuild<1>(w, A, rli32(A.m, A.f));
-    }
-    if (B.n < 32 && B.more) {
-      a_flush(w, B, 0);
-      a_drain();
-      a_rebuild<0>(w, B, rli32(B.m, B.f));
-    }
-    int rf = 0, rr = 0;
-    uint32_t rs = 0, rlo = 0, rn = 0;
-    uint32_t k = 0;
-    for (; k < cntb; ++k) {
-      if (ME_UNLIKELY(!((fastm >> k) & 1ull))) {
-        pos = blk + k;  // the generic loop takes over from here (k_match_hot_cont)
-        stop = true;
-        break;
-      }
-      const uint32_t jt = blk + k;
-      const int q = rli32(oq, (int)k);
-      const uint32_t rjk = rl32(rj, (int)k);
-      if (ME_UNLIKELY(rjk != 0u)) {
-        rf = a_wl(rf, 0, (int)k);
-        rr = a_wl(rr, rjk == ME_RJ_BAD_QTY ? 0 : q, (int)k);
-        rs = a_wlu(rs, (uint32_t)ME_ST_REJECTED | (rjk << 8), (int)k);
-        rlo = a_wlu(rlo, w.evp, (int)k);
-        rn = a_wlu(rn, 0u, (int)k);
-        continue;
-      }
-      const uint32_t kd = rl32(okd, (int)k);
-      const bool buy = (kd & 3u) == ME_SIDE_BUY;
-      const bool mkt = (kd >> 2) & 1u;
-      const int lm = rli32(olm, (int)k);
-      const uint32_t ev_lo = w.evp;
-      uint32_t rem = (uint32_t)q;
-      uint32_t nte;
-      if (buy) {
-        a_take<1>(w, A, mkt ? L - 1 : lm, rem, jt | AGG_TAKE);
-        nte = w.evp - ev_lo;
-        if (!mkt && rem) a_rest<0>(w, B, L - 1 - lm, lm, (int)rem, jt);
-      } else {
-        a_take<0>(w, B, mkt ? L - 1 : L - 1 - lm, rem, jt | AGG_TAKE);
-        nte = w.evp - ev_lo;
-        if (!mkt && rem) a_rest<1>(w, A, lm, lm, (int)rem, jt);
-      }
-      const int filled = q - (int)rem;
-      uint32_t stt;
-      if (mkt)
-        stt = rem == 0 ? ME_ST_FILLED : ME_ST_CANCELED;
-      else
-        stt = rem == 0 ? ME_ST_FILLED : (filled > 0 ? ME_ST_PARTIALLY_FILLED : ME_ST_NEW);
-      rf = a_wl(rf, filled, (int)k);
-      rr = a_wl(rr, (int)rem, (int)k);
-      rs = a_wlu(rs, stt, (int)k);
-      rlo = a_wlu(rlo, ev_lo, (int)k);
-      rn = a_wlu(rn, nte, (int)k);
-    }
+    uint32_t rj;
+    int olm;
+    const unsigned long long fastm = __ballot(a_classify(v, oseq, opx, oq, okd, base, L, nfar0, nfar1, rj, olm));
+    a_refill(w, A, B);
+    ARes R;
+    const uint32_t k = a_block(w, A, B, oq, okd, olm, rj, j, fastm, cntb, R);
     if (v && (uint32_t)lane < k) {
       AggRec r;
-      r.filled = rf;
-      r.rem = rr;
-      r.st = rs;
-      r.ev_lo = rlo;
-      r.ev_n = rn;
+      r.filled = R.rf;
+      r.rem = R.rr;
+      r.st = R.rs;
+      r.ev_lo = R.rlo;
+      r.ev_n = R.rn;
       r.pad = 0;
       ag.rec[j] = r;
     }
+    if (k < cntb) {
+      pos = blk + k;  // the generic loop takes over from here (k_match_hot_cont)
+      break;
+    }
   }
-  a_flush(w, A, 1);
-  a_flush(w, B, 0);
-  const int ba = A.n ? rli32(A.m, A.f) : L;
-  const int bb = B.n ? L - 1 - rli32(B.m, B.f) : -1;
+  int bb, ba;
+  a_walk_end(w, A, B, bb, ba);
   if (lane == 0) {
     slot->pos = pos;
     slot->ev_cnt = w.evp - eb;
@@ -489,7 +551,7 @@ __global__ __launch_bounds__(1024) void k_agg_group(BookDev bk, AggDev ag) {
   const uint32_t per = (L + 1023) / 1024;
   uint32_t nbits = 0;
   while ((1u << nbits) < L) ++nbits;
-  const uint32_t nh = min(*(volatile uint32_t*)bk.hcount, bk.S);
+  const uint32_t nh = a_nslots(bk, ag);
   for (uint32_t i = blockIdx.x; i < nh; i += gridDim.x) {
     const AggSlot& sl = ag.slot[i];
     if (!sl.active) continue;  // uniform over the workgroup
@@ -576,6 +638,9 @@ __global__ __launch_bounds__(1024) void k_agg_group(BookDev bk, AggDev ag) {
 
 // ------------------------------------------------------------------ per-level FIFO resolution
 __device__ __forceinline__ unsigned long long a_seq_of(const BatchDev& bt, uint32_t j) { return bt.seq[bt.perm[j]]; }
+__device__ __forceinline__ unsigned long long a_seq_of(const AggSrc& src, uint32_t j) {
+  return src.perm ? src.seq[0][src.perm[j]] : src.seq[j >> AGG_GSHIFT][j & AGG_IMASK];
+}
 
 // First index in mk[b, b + n) whose end is > x (strict = false: >= x).
 __device__ __forceinline__ uint32_t a_search(const AggMk* mk, uint32_t b, uint32_t n, unsigned long long x, bool strict) {
@@ -595,7 +660,7 @@ __device__ __forceinline__ uint32_t a_search(const AggMk* mk, uint32_t b, uint32
 // FIFO walked until C is covered (count pass, then a write pass: consumed makers into mk, emptied
 // chunks zeroed into fr, the chunk C ends in updated); the rests C reaches; each take's first maker
 // and fill count; what the surviving rests need.
-__global__ __launch_bounds__(256) void k_agg_levels(BookDev bk, BatchDev bt, AggDev ag) {
+__global__ __launch_bounds__(256) void k_agg_levels(BookDev bk, AggSrc src, AggDev ag) {
   const int lane = lane_id();
   const bool act = lane < ME_C;
   const uint32_t gw = blockIdx.x * 4u + (threadIdx.x >> 6), nw = gridDim.x * 4u;
@@ -753,7 +818,7 @@ __global__ __launch_bounds__(256) void k_agg_levels(BookDev bk, BatchDev bt, Agg
           const unsigned long long cm = __ballot(cons);
           if (cons) {
             AggMk m;
-            m.seq = a_seq_of(bt, E.j);
+            m.seq = a_seq_of(src, E.j);
             m.end = T0 + en;
             ag.mk[mk_base + mi + (uint32_t)__popcll(cm & lanemask_lt())] = m;
           }
@@ -802,7 +867,7 @@ __global__ __launch_bounds__(256) void k_agg_levels(BookDev bk, BatchDev bt, Agg
 // fr[alloc_base + deficit + u], u < surplus: the surpluses gathered.
 __global__ __launch_bounds__(64) void k_agg_alloc(BookDev bk, AggDev ag) {
   const int lane = lane_id();
-  const uint32_t nh = min(*(volatile uint32_t*)bk.hcount, bk.S);
+  const uint32_t nh = a_nslots(bk, ag);
   for (uint32_t i = blockIdx.x; i < nh; i += gridDim.x) {
     AggSlot* sl = ag.slot + i;
     if (!auniu(sl->active)) continue;
@@ -886,7 +951,7 @@ __global__ __launch_bounds__(64) void k_agg_alloc(BookDev bk, AggDev ag) {
 
 // One wave per segment: the surviving rests into the level's tail chunk and new chunks (in order),
 // the new chunks' headers and links, the seq ring, the level's head / tail / tail fill.
-__global__ __launch_bounds__(256) void k_agg_place(BookDev bk, BatchDev bt, AggDev ag) {
+__global__ __launch_bounds__(256) void k_agg_place(BookDev bk, AggSrc src, AggDev ag) {
   const int lane = lane_id();
   const uint32_t gw = blockIdx.x * 4u + (threadIdx.x >> 6), nw = gridDim.x * 4u;
   const uint32_t nseg = min(*(volatile uint32_t*)&ag.ctr[AC_SEG], ag.ev_cap);
@@ -935,7 +1000,7 @@ __global__ __launch_bounds__(256) void k_agg_place(BookDev bk, BatchDev bt, AggD
             chk = newchunk(gg / ME_C);
             slt = gg % ME_C;
           }
-          const unsigned long long sq = a_seq_of(bt, E.j);
+          const unsigned long long sq = a_seq_of(src, E.j);
           const int left = (int)(en - (st0 > Cr ? st0 : Cr));
           if (chk < bk.nchunks) {
             bk.chunks[chk].qty[slt] = left;
@@ -1092,17 +1157,394 @@ __global__ __launch_bounds__(1024) void k_agg_emit(BookDev bk, BatchDev bt, AggD
   }
 }
 
+// ------------------------------------------------------------------ grouped launches (L <= 128)
+// The register-window path's groups of up to ME_GMAX bucketed batches, every symbol through the
+// aggregate path: k_agg_gwalk (one wave per symbol over its records of every batch of the group, from
+// the batches' buckets, in batch order) replaces k_match_reg's serial loop; the per-level kernels are
+// the hot path's; k_agg_gfin / k_agg_gemit place each batch's fills in its own scratch (the symbol's
+// slab, or the overflow region) and fill in the results the pipeline's tape job reads. A record the walk
+// does not cover (a cancel, a price outside the window, a bucket past BK_CAP records) hands the symbol's
+// rest of the group to k_match_reg's continuation launch (me_match_reg.hip, kSlow).
+struct AggGArgs {
+  uint32_t* bcnt[ME_GMAX];
+  const BkRec* b_rec[ME_GMAX];
+  me_order_result* res[ME_GMAX];
+  uint32_t* tile_sum[ME_GMAX];
+  me_fill* scratch[ME_GMAX];
+  unsigned long long* scratch_top[ME_GMAX];
+  unsigned long long ovf_base, scratch_cap;
+  uint32_t slab, ng;
+};
+
+// Ascending bitonic sort of 64 (one register) / 128 (two) distinct keys across the wave.
+__device__ __forceinline__ uint32_t a_bstep(uint32_t v, int J, bool asc) {
+  const uint32_t p = (uint32_t)__shfl_xor((int)v, J, 64);
+  const bool lower = (lane_id() & J) == 0;
+  return (lower == asc) ? min(v, p) : max(v, p);
+}
+__device__ __forceinline__ uint32_t a_bmerge(uint32_t v, int K, bool asc) {
+  for (int J = K / 2; J >= 1; J >>= 1) v = a_bstep(v, J, asc);
+  return v;
+}
+__device__ __forceinline__ uint32_t a_sort64(uint32_t v, bool desc) {
+  const int lane = lane_id();
+  for (int K = 2; K < 64; K <<= 1) v = a_bmerge(v, K, (lane & K) == 0);
+  return a_bmerge(v, 64, !desc);
+}
+__device__ __forceinline__ void a_sort128(uint32_t& a, uint32_t& b) {
+  a = a_sort64(a, false);
+  b = a_sort64(b, true);
+  const uint32_t lo = min(a, b), hi = max(a, b);
+  a = a_bmerge(lo, 64, true);
+  b = a_bmerge(hi, 64, true);
+}
+
+struct AStage {  // a symbol's bucket of one batch, staged for the batch-order gather
+  unsigned long long seq[BK_CAP];
+  long long px[BK_CAP];
+  int qty[BK_CAP];
+  uint32_t ok[BK_CAP];
+};
+
+__device__ __forceinline__ uint32_t* a_gtab(uint32_t* t, uint32_t s, uint32_t g) { return t + (size_t)s * (ME_GMAX + 1) + g; }
+
+// The register-window continuation takes the symbol from record `pos` (in its batch order) of batch g.
+__device__ __forceinline__ uint32_t a_ghand(const BookDev& bk, uint32_t s, uint32_t g, uint32_t pos, uint32_t nsg,
+                                            uint32_t wptr, uint32_t wend) {
+  uint32_t idx = 0;
+  if (lane_id() == 0) {
+    idx = atomicAdd(bk.hcount, 1u);
+    Handoff h{};
+    h.s = s;
+    h.g = g;
+    h.pos = pos;
+    h.nsg = nsg;
+    h.wptr = wptr;
+    h.wend = wend;
+    bk.hand[idx] = h;
+  }
+  return rl32(idx, 0);
+}
+
+__global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDev ag) {
+  __shared__ unsigned long long locc[2];
+  __shared__ AStage stg;
+  const int lane = lane_id();
+  const int L = (int)bk.L;  // <= 128
+  const uint32_t ng = ga.ng;
+  for (uint32_t s = blockIdx.x; s < bk.S; s += gridDim.x) {
+    // lane g < ng: the symbol's records in batch g
+    const uint32_t gl = min((uint32_t)lane, ng - 1u);
+    const uint32_t nsv = (uint32_t)lane < ng ? ga.bcnt[gl][(size_t)s * BK_CNT_STRIDE] : 0u;
+    long long t = (long long)nsv;
+    for (int d = 1; d < 64; d <<= 1) t += __shfl_xor(t, d, 64);
+    const uint32_t total = (uint32_t)rli64(t, 0);
+    const SymState st = bk.sym[s];
+    const long long base = rli64(st.base, 0);
+    const int bb0 = rli32(st.best_bid, 0), ba0 = rli32(st.best_ask, 0);
+    const uint32_t resting = rl32(st.resting, 0);
+    const uint32_t nfar0 = rl32(st.nfar[0], 0), nfar1 = rl32(st.nfar[1], 0);
+    gptr<AggSlot> slot = (gptr<AggSlot>)(ag.slot + s);
+    const uint32_t evneed = 3u * total + min((uint32_t)L, resting) + 64u;
+    uint32_t eb = 0;
+    if (total && lane == 0) eb = atomicAdd(&ag.ctr[AC_EV], evneed + 64u);
+    eb = (rl32(eb, 0) + 63u) & ~63u;
+    const bool eok = (unsigned long long)eb + evneed <= ag.ev_cap;
+    if (lane == 0) {
+      AggSlot o{};
+      o.s = s;
+      o.base = base;
+      o.ev_base = eb;
+      o.free_head = st.free_head;
+      o.resting0 = resting;
+      o.bb = bb0;
+      o.ba = ba0;
+      o.active = 0;
+      o.hidx = NIL;
+      o.gs = bk.gsym ? bk.gsym[s] : s;
+      *slot = o;
+    }
+    if (!total) continue;
+    if (!eok) {  // no room in the log: the whole group of the symbol goes to the continuation
+      const uint32_t g0 = (uint32_t)__builtin_ctzll(__ballot(nsv != 0u));
+      a_ghand(bk, s, g0, 0u, rl32(nsv, (int)g0), s * ga.slab, s * ga.slab + ga.slab);
+      continue;
+    }
+    AWalk w;
+    a_walk_init(w, bk, ag, s, eb, locc);
+    AList A, B;
+    a_rebuild<1>(w, A, ba0);
+    a_rebuild<0>(w, B, L - 1 - bb0);
+    uint32_t hidx = NIL, gstop = ng;
+    for (uint32_t g = 0; g < ng; ++g) {
+      if (lane == 0) *a_gtab(ag.gev, s, g) = w.evp;
+      const uint32_t cnt = rl32(nsv, (int)g);
+      if (!cnt) continue;
+      if (cnt > (uint32_t)BK_CAP) {  // an overfull bucket: the continuation rescans the batch
+        hidx = a_ghand(bk, s, g, 0u, cnt, 0u, 0u);
+        gstop = g;
+        break;
+      }
+      const size_t bb = (size_t)s * BK_CAP;
+      const BkRec r0 = ga.b_rec[g][bb + lane], r1 = ga.b_rec[g][bb + 64 + lane];
+      if (lane == 0) ga.bcnt[g][(size_t)s * BK_CNT_STRIDE] = 0u;  // ready for a later group's bucket job
+      stg.seq[lane] = r0.seq;
+      stg.seq[64 + lane] = r1.seq;
+      stg.px[lane] = r0.px;
+      stg.px[64 + lane] = r1.px;
+      stg.qty[lane] = r0.qty;
+      stg.qty[64 + lane] = r1.qty;
+      stg.ok[lane] = r0.ok;
+      stg.ok[64 + lane] = r1.ok;
+      uint32_t k0 = (uint32_t)lane < cnt ? ((r0.ok & BK_IDX_MASK) << 7) | (uint32_t)lane : ~0u;
+      uint32_t k1 = 64u + (uint32_t)lane < cnt ? ((r1.ok & BK_IDX_MASK) << 7) | (64u + (uint32_t)lane) : ~0u;
+      if (cnt > 64u)
+        a_sort128(k0, k1);
+      else
+        k0 = a_sort64(k0, false);
+      wave_mem_order();
+      me_order_result* res = ga.res[g];
+      bool stop = false;
+      for (uint32_t blk = 0; blk < cnt; blk += 64) {
+        const uint32_t key = blk ? k1 : k0;
+        const bool v = blk + (uint32_t)lane < cnt;
+        const uint32_t sl = key & (BK_CAP - 1), oi = v ? key >> 7 : 0u;
+        const unsigned long long oseq = stg.seq[sl];
+        const long long opx = stg.px[sl];
+        const int oq = v ? stg.qty[sl] : 0;
+        const uint32_t okd = v ? stg.ok[sl] >> BK_KIND_SHIFT : 0u;
+        const uint32_t cntb = min(64u, cnt - blk);
+        uint32_t rj;
+        int olm;
+        const unsigned long long fastm = __ballot(a_classify(v, oseq, opx, oq, okd, base, L, nfar0, nfar1, rj, olm));
+        a_refill(w, A, B);
+        ARes R;
+        const uint32_t k = a_block(w, A, B, oq, okd, olm, rj, (g << AGG_GSHIFT) | oi, fastm, cntb, R);
+        if (v && (uint32_t)lane < k) {
+          // fill_count = the record's take events and tape_offset = its first one, until k_agg_gfin
+          me_order_result o;
+          o.filled_qty = R.rf;
+          o.remaining_qty = R.rr;
+          o.fill_count = R.rn;
+          o.tape_offset = R.rlo;
+          o.status = (uint8_t)(R.rs & 0xFF);
+          o.reason = (uint8_t)(R.rs >> 8);
+          o.pad[0] = o.pad[1] = 0;
+          res[oi] = o;
+        }
+        if (k < cntb) {
+          hidx = a_ghand(bk, s, g, blk + k, cnt, 0u, 0u);  // scratch position: k_agg_gfin
+          stop = true;
+          break;
+        }
+      }
+      if (stop) {
+        gstop = g;
+        break;
+      }
+    }
+    // the log's end for every batch from the stop on
+    for (uint32_t g = (gstop < ng ? gstop + 1u : ng) + (uint32_t)lane; g <= ng; g += 64)
+      *a_gtab(ag.gev, s, g) = w.evp;
+    if (gstop < ng && lane == 0) *a_gtab(ag.gev, s, gstop + 1u) = w.evp;
+    int bb, ba;
+    a_walk_end(w, A, B, bb, ba);
+    if (lane == 0) {
+      slot->ev_cnt = w.evp - eb;
+      slot->bb = bb;
+      slot->ba = ba;
+      slot->active = 1;
+      slot->hidx = hidx;
+      slot->pos = gstop;  // the batch the continuation starts in (ng: none)
+    }
+  }
+}
+
+// One workgroup per symbol: the fill offsets (scan of the events' fill counts in log order), each
+// batch's share placed in the symbol's slab of that batch (or the overflow region), the results' fill
+// counts and scratch starts, the symbol's state, the continuation's scratch position.
+__global__ __launch_bounds__(1024) void k_agg_gfin(BookDev bk, AggGArgs ga, AggDev ag) {
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t carry_s;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  constexpr uint32_t PER = 8;
+  for (uint32_t s = blockIdx.x; s < bk.S; s += gridDim.x) {
+    const AggSlot sl = ag.slot[s];
+    if (!sl.active) continue;
+    const uint32_t eb = sl.ev_base, n = sl.ev_cnt;
+    uint32_t carry = 0;
+    for (uint32_t t0 = 0; t0 < n; t0 += 1024 * PER) {
+      const uint32_t b = t0 + (uint32_t)tid * PER;
+      uint32_t v[PER], loc = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < PER; ++k) {
+        v[k] = b + k < n ? ag.evn[eb + b + k] : 0u;
+        loc += v[k];
+      }
+      uint32_t x = loc;
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t t = __shfl_up(x, d, 64);
+        if (lane >= d) x += t;
+      }
+      if (lane == 63) wsum[wv] = x;
+      __syncthreads();
+      uint32_t pre = 0, tot = 0;
+      for (int k = 0; k < 16; ++k) {
+        if (k < wv) pre += wsum[k];
+        tot += wsum[k];
+      }
+      uint32_t r = carry + pre + x - loc;
+#pragma unroll
+      for (uint32_t k = 0; k < PER; ++k)
+        if (b + k < n) {
+          ag.evx[eb + b + k] = r;
+          r += v[k];
+        }
+      carry += tot;
+      __syncthreads();
+    }
+    if (tid == 0) carry_s = carry;
+    __syncthreads();
+    const uint32_t ftot = carry_s;
+    auto EX = [&](uint32_t e) -> uint32_t { return e < eb + n ? ag.evx[e] : ftot; };
+    // each batch's fills: the symbol's slab of that batch if they fit, else the overflow region
+    if ((uint32_t)tid < ga.ng) {
+      const uint32_t g = (uint32_t)tid;
+      const uint32_t x0 = EX(*a_gtab(ag.gev, s, g)), x1 = EX(*a_gtab(ag.gev, s, g + 1));
+      const uint32_t f = x1 - x0;
+      unsigned long long b0 = (unsigned long long)s * ga.slab;
+      if (f > ga.slab) {
+        b0 = ga.ovf_base + atomicAdd(ga.scratch_top[g], (unsigned long long)f);
+        if (b0 + f > ga.scratch_cap) {
+          atomicOr(bk.err, ERR_SCRATCH_OOM);
+          b0 = 0;
+        }
+      }
+      *a_gtab(ag.gex, s, g) = x0;
+      *a_gtab(ag.gbase, s, g) = (uint32_t)b0;
+    }
+    __syncthreads();
+    // the first take of each record: its fill count and scratch start
+    for (uint32_t t = (uint32_t)tid; t < n; t += 1024) {
+      const uint32_t e = eb + t;
+      const uint32_t j = ag.ev[e].j;
+      if (!(j & AGG_TAKE) || (t > 0 && ag.ev[e - 1].j == j)) continue;
+      const uint32_t g = (j & ~AGG_TAKE) >> AGG_GSHIFT, oi = j & AGG_IMASK;
+      me_order_result* res = ga.res[g];
+      const uint32_t nte = res[oi].fill_count;
+      const uint32_t x0 = EX(e), nfill = EX(e + nte) - x0;
+      res[oi].fill_count = nfill;
+      res[oi].tape_offset = *a_gtab(ag.gbase, s, g) + (x0 - *a_gtab(ag.gex, s, g));
+      if (nfill) atomicAdd(&ga.tile_sum[g][oi / TILE_TAPE], nfill);
+    }
+    if (tid == 0) {
+      SymState o = bk.sym[s];
+      o.best_bid = sl.bb;
+      o.best_ask = sl.ba;
+      o.free_head = ag.slot[s].free_head;
+      const int dr = ag.slot[s].dresting;
+      o.resting = (uint32_t)((int)sl.resting0 + dr);
+      bk.sym[s] = o;
+      if (dr) atomicAdd(bk.stats + ST_RESTING, (unsigned long long)(long long)dr);
+      if (sl.hidx != NIL) {  // the continuation goes on behind the walk's fills of its batch
+        const uint32_t g = sl.pos;
+        const uint32_t x0 = *a_gtab(ag.gex, s, g);
+        const uint32_t f = EX(*a_gtab(ag.gev, s, g + 1)) - x0;
+        const uint32_t b0 = *a_gtab(ag.gbase, s, g);
+        const bool in_slab = f <= ga.slab;
+        bk.hand[sl.hidx].wptr = b0 + f;
+        bk.hand[sl.hidx].wend = in_slab ? s * ga.slab + ga.slab : b0 + f;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// One thread per take event: its fills into its batch's scratch.
+__global__ __launch_bounds__(1024) void k_agg_gemit(BookDev bk, AggGArgs ga, AggSrc src, AggDev ag) {
+  for (uint32_t s = blockIdx.x; s < bk.S; s += gridDim.x) {
+    const AggSlot sl = ag.slot[s];
+    if (!sl.active) continue;
+    const uint32_t eb = sl.ev_base, n = sl.ev_cnt;
+    for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) {
+      const uint32_t e = eb + t;
+      const AggEv E = ag.ev[e];
+      if (!(E.j & AGG_TAKE)) continue;
+      const uint32_t nf = ag.evn[e];
+      if (!nf) continue;
+      const uint32_t j = E.j & ~AGG_TAKE, g = j >> AGG_GSHIFT;
+      const uint32_t first = ag.evf[e];
+      const unsigned long long a = ag.eva[e], z = a + (unsigned long long)E.qty;
+      const uint32_t p = *a_gtab(ag.gbase, s, g) + (ag.evx[e] - *a_gtab(ag.gex, s, g));
+      me_fill f;
+      f.taker_seq = a_seq_of(src, j);
+      f.price_q4 = sl.base + (long long)E.lvl;
+      f.symbol = sl.gs;
+      me_fill* sc = ga.scratch[g];
+      unsigned long long lo = a;
+      for (uint32_t k = 0; k < nf; ++k) {
+        const AggMk m = ag.mk[first + k];
+        const unsigned long long hi = m.end < z ? m.end : z;
+        f.maker_seq = m.seq;
+        f.qty = (int)(hi - lo);
+        sc[p + k] = f;
+        lo = hi;
+      }
+    }
+  }
+}
+
 }  // namespace
 
-hipError_t launch_agg(hipStream_t hs, const BookDev& bk, const BatchDev& bt, const AggDev& ag) {
+hipError_t launch_agg(hipStream_t hs, const BookDev& bk, const BatchDev& bt, const AggDev& ag0) {
+  AggDev ag = ag0;
+  ag.nslots = 0;  // k_hot_pick's hot symbols
+  AggSrc src{};
+  src.perm = bt.perm;
+  src.seq[0] = bt.seq;
   hipLaunchKernelGGL(k_agg_walk, dim3(64), dim3(64), 0, hs, bk, bt, ag);
   hipLaunchKernelGGL(k_agg_group, dim3(64), dim3(1024), (size_t)bk.L * 4u, hs, bk, ag);
-  hipLaunchKernelGGL(k_agg_levels, dim3(1024), dim3(256), 0, hs, bk, bt, ag);
+  hipLaunchKernelGGL(k_agg_levels, dim3(1024), dim3(256), 0, hs, bk, src, ag);
   hipLaunchKernelGGL(k_agg_alloc, dim3(64), dim3(64), 0, hs, bk, ag);
-  hipLaunchKernelGGL(k_agg_place, dim3(1024), dim3(256), 0, hs, bk, bt, ag);
+  hipLaunchKernelGGL(k_agg_place, dim3(1024), dim3(256), 0, hs, bk, src, ag);
   hipLaunchKernelGGL(k_agg_fin, dim3(64), dim3(1024), 0, hs, bk, bt, ag);
   hipLaunchKernelGGL(k_agg_emit, dim3(64), dim3(1024), 0, hs, bk, bt, ag);
   return hipGetLastError();
 }
 
+}  // namespace me
+
+namespace me {
+// A grouped register-window launch through the aggregate path (batches bt[0, ng), all bucketed): the
+// walk, the per-level kernels, the fills; the continuation launch follows (me_kernels.hip).
+hipError_t launch_agg_group(hipStream_t st, const BookDev& bk, const BatchDev* bt, uint32_t ng, const AggDev& ag0) {
+  if (!ng || ng > (uint32_t)ME_GMAX || bk.L > 128u) return hipErrorInvalidValue;
+  AggDev ag = ag0;
+  ag.nslots = bk.S;
+  AggGArgs ga{};
+  AggSrc src{};
+  for (uint32_t g = 0; g < ng; ++g) {
+    if (!bt[g].bcnt) return hipErrorInvalidValue;
+    ga.bcnt[g] = bt[g].bcnt;
+    ga.b_rec[g] = bt[g].b_rec;
+    ga.res[g] = bt[g].res;
+    ga.tile_sum[g] = bt[g].tile_sum;
+    ga.scratch[g] = bt[g].scratch;
+    ga.scratch_top[g] = bt[g].scratch_top;
+    src.seq[g] = bt[g].seq;
+  }
+  ga.ovf_base = bt[0].ovf_base;
+  ga.scratch_cap = bt[0].scratch_cap;
+  ga.slab = bt[0].slab;
+  ga.ng = ng;
+  const uint32_t grid = bk.S < 2048u ? bk.S : 2048u;
+  hipLaunchKernelGGL(k_agg_gwalk, dim3(grid), dim3(64), 0, st, bk, ga, ag);
+  hipLaunchKernelGGL(k_agg_group, dim3(grid), dim3(1024), (size_t)bk.L * 4u, st, bk, ag);
+  hipLaunchKernelGGL(k_agg_levels, dim3(2048), dim3(256), 0, st, bk, src, ag);
+  hipLaunchKernelGGL(k_agg_alloc, dim3(grid), dim3(64), 0, st, bk, ag);
+  hipLaunchKernelGGL(k_agg_place, dim3(2048), dim3(256), 0, st, bk, src, ag);
+  hipLaunchKernelGGL(k_agg_gfin, dim3(grid), dim3(1024), 0, st, bk, ga, ag);
+  hipLaunchKernelGGL(k_agg_gemit, dim3(grid), dim3(1024), 0, st, bk, ga, src, ag);
+  return hipGetLastError();
+}
 }  // namespace me

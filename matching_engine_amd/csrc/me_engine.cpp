@@ -35,7 +35,7 @@ hipError_t launch_seq_sweep(hipStream_t st, const BookDev& bk, const uint64_t* c
 hipError_t launch_match(hipStream_t st, const BookDev& bk, const BatchDev& bt, hipEvent_t ev0, hipEvent_t ev1,
                         const HotLaunch& hot);
 hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* bt, uint32_t ng, const AuxDev& ax, hipEvent_t ev0,
-                            hipEvent_t ev1);
+                            hipEvent_t ev1, const HotLaunch* hot);
 uint32_t sort_tile(uint32_t n);
 hipError_t launch_tape(hipStream_t st, const BatchDev& bt, me_fill* tape, unsigned long long tape_cap,
                        unsigned long long* tape_count, unsigned long long* fills_acc, uint32_t* err,
@@ -334,7 +334,8 @@ static void free_all(me_engine* e) {
   }
   {
     const AggDev& a = e->hot.ag;
-    void* ap[] = {a.slot, a.ev, a.evs, a.eva, a.evf, a.evn, a.evx, a.seg, a.segs, a.mk, a.fr, a.rec, a.ctr};
+    void* ap[] = {a.slot, a.ev, a.evs, a.eva, a.evf, a.evn, a.evx, a.seg, a.segs, a.mk, a.fr, a.rec, a.ctr,
+                  a.gev, a.gex, a.gbase};
     for (void* p : ap)
       if (p) (void)hipFree(p);
   }
@@ -508,6 +509,10 @@ extern "C" me_engine* me_create(const me_config* cfg) {
     const char* v = getenv("ME_HOT_MIN");
     const char* va = getenv("ME_HOT_AGG");
     e->hot.agg = L > 128 && L <= AGG_MAX_L && !(va && atoi(va) == 0);
+    // L <= 128: every symbol of a launch group through the aggregate path (k_agg_gwalk) instead of
+    // k_match_reg's serial loop — ME_REG_AGG=1 (measured per workload)
+    const char* vr = getenv("ME_REG_AGG");
+    e->hot.agg_reg = L <= 128 && vr && atoi(vr) != 0;
     bk.hot_min = (e->hot.agg || L > LDS_MAX_LEVELS) ? (v ? (uint32_t)atoi(v) : 512u) : 0u;
     if (bk.hot_min) {
       if ((he = hipStreamCreateWithFlags(&e->hot.st, hipStreamNonBlocking)) != hipSuccess ||
@@ -539,14 +544,17 @@ extern "C" me_engine* me_create(const me_config* cfg) {
   ALLOC(bk.hcount, 2);  // [0] hand-offs of a launch, [1] k_match_hot's continuations
   ALLOC(bk.hand, 2 * S);  // continuations from S on
   ALLOC(bk.stats, ME_STATS);
-  if (bk.hot_min && e->hot.agg) {
+  if ((bk.hot_min && e->hot.agg) || e->hot.agg_reg) {
     // the aggregate path's pools (me_agg.hip): the log holds every hot symbol's events (<= 3 records +
     // its occupied levels each; a symbol that finds no room goes to the generic loop), consumed makers
-    // <= fills <= max_resting + 2n, chunk ids <= 2 x consumed makers + rests
+    // <= fills <= max_resting + 2n, chunk ids <= 2 x consumed makers + rests. Grouped launches (L <= 128):
+    // every symbol, the records of a whole group.
     AggDev& a = e->hot.ag;
-    const uint64_t evc = 3 * n + 16 * (L + 64) + 4096;
-    const uint64_t mkc = cfg->max_resting + 2 * n + 64;
-    const uint64_t frc = 2 * mkc + n + 64;
+    const uint64_t gmax = e->hot.agg_reg ? (cfg->batches_per_launch ? cfg->batches_per_launch : ME_DEFAULT_GROUP) : 1;
+    const uint64_t nrec = n * gmax;
+    const uint64_t evc = e->hot.agg_reg ? 3 * nrec + S * (L + 128) + 4096 : 3 * n + 16 * (L + 64) + 4096;
+    const uint64_t mkc = cfg->max_resting + 2 * nrec + 64;
+    const uint64_t frc = 2 * mkc + nrec + 64;
     if (evc >= 0x7FFFFFFFull || frc >= 0xFFFFFFFFull) return bail("me_create: aggregate-path pools exceed 32-bit ids");
     a.ev_cap = (uint32_t)evc;
     a.mk_cap = (uint32_t)mkc;
@@ -564,6 +572,11 @@ extern "C" me_engine* me_create(const me_config* cfg) {
     ALLOC(a.fr, frc);
     ALLOC(a.rec, n);
     ALLOC(a.ctr, AC_N);
+    if (e->hot.agg_reg) {
+      ALLOC(a.gev, S * (ME_GMAX + 1));
+      ALLOC(a.gex, S * (ME_GMAX + 1));
+      ALLOC(a.gbase, S * (ME_GMAX + 1));
+    }
     if ((he = hipMemset(a.ctr, 0, AC_N * sizeof(uint32_t))) != hipSuccess)
       return bail(std::string("hipMemset agg ctr: ") + hipGetErrorString(he));
     bk.agg_ctr = a.ctr;
@@ -882,7 +895,7 @@ static int pipe_launch(me_engine* e, const me_engine::Group* nb) {
     rc = timing_slot(e, orders, gm.n, tl, timed);
     if (rc) return rc;
   }
-  hipError_t he = launch_match_reg(e->stream, e->bk, bt, gm.n, ax, tl.m0, tl.m1);
+  hipError_t he = launch_match_reg(e->stream, e->bk, bt, gm.n, ax, tl.m0, tl.m1, &e->hot);
   if (he != hipSuccess) return e->hip_fail(he, "pipelined match launch");
   if (timed) e->timed.push_back(tl);
   if (gm.n) {

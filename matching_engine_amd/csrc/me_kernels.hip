@@ -2511,22 +2511,39 @@ hipError_t launch_sort_pass(hipStream_t st, const uint32_t* keys_in, const uint3
 namespace rc64 {
 hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* bt, uint32_t ng, const AuxDev& ax,
                             hipEvent_t ev0, hipEvent_t ev1);
+hipError_t launch_match_reg_cont(hipStream_t st, const BookDev& bk, const BatchDev* bt, uint32_t ng, hipEvent_t ev1);
 }
 namespace rc128 {
 hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* bt, uint32_t ng, const AuxDev& ax,
                             hipEvent_t ev0, hipEvent_t ev1);
+hipError_t launch_match_reg_cont(hipStream_t st, const BookDev& bk, const BatchDev* bt, uint32_t ng, hipEvent_t ev1);
 }
+hipError_t launch_agg_group(hipStream_t st, const BookDev& bk, const BatchDev* bt, uint32_t ng, const AggDev& ag);  // me_agg.hip
 // The register-ladder launch (me_match_reg.hip, two builds): one head-cache entry per level while one
 // workgroup per CU covers the symbols (rc128), 64 shared entries and two workgroups per CU beyond
 // that (rc64). ax.nwg is the CU count (0: assume 256).
 hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* bt, uint32_t ng, const AuxDev& ax,
-                            hipEvent_t ev0, hipEvent_t ev1) {
+                            hipEvent_t ev0, hipEvent_t ev1, const HotLaunch* hot) {
   constexpr uint32_t kWaves = 4;  // matching waves per workgroup (me_match_reg.hip REG_WAVES)
   const uint32_t waves = ng && bt[0].bcnt ? bk.S : bk.S + 1;
   const uint32_t wgs = (waves + kWaves - 1) / kWaves;
   const uint32_t ncu = ax.nwg ? ax.nwg : 256u;
-  return wgs > ncu ? rc64::launch_match_reg(st, bk, bt, ng, ax, ev0, ev1)
-                   : rc128::launch_match_reg(st, bk, bt, ng, ax, ev0, ev1);
+  const bool big = wgs > ncu;
+  if (hot && hot->agg_reg && ng && bt[0].bcnt) {
+    // the group through the aggregate path: side jobs (k_side), walk + per-level kernels, continuation
+    hipError_t e;
+    if (ax.nb || ax.nt) {
+      e = big ? rc64::launch_match_reg(st, bk, bt, 0, ax, ev0, nullptr)
+              : rc128::launch_match_reg(st, bk, bt, 0, ax, ev0, nullptr);
+    } else {
+      e = ev0 ? hipEventRecord(ev0, st) : hipSuccess;
+    }
+    if (e != hipSuccess) return e;
+    if ((e = launch_agg_group(st, bk, bt, ng, hot->ag)) != hipSuccess) return e;
+    return big ? rc64::launch_match_reg_cont(st, bk, bt, ng, ev1) : rc128::launch_match_reg_cont(st, bk, bt, ng, ev1);
+  }
+  return big ? rc64::launch_match_reg(st, bk, bt, ng, ax, ev0, ev1)
+             : rc128::launch_match_reg(st, bk, bt, ng, ax, ev0, ev1);
 }
 
 // ev0 / ev1 (optional, timing): the launch records the kernel's own start and end
@@ -2539,7 +2556,7 @@ hipError_t launch_match(hipStream_t st, const BookDev& bk, const BatchDev& bt, h
                         const HotLaunch& hot) {
   const uint32_t waves = bk.S + 1;
   const dim3 grid((waves + 3) / 4), block(256);
-  if (bk.L <= 128) return launch_match_reg(st, bk, &bt, 1u, AuxDev{}, ev0, ev1);
+  if (bk.L <= 128) return launch_match_reg(st, bk, &bt, 1u, AuxDev{}, ev0, ev1, nullptr);
   const bool lds = bk.L <= LDS_MAX_LEVELS;
   // hot symbols: the aggregate path (windows up to AGG_MAX_L) or k_match_hot (HBM ladders up to
   // HOT_MAX_WORDS * 64 levels), on the hot stream beside k_match

@@ -42,6 +42,17 @@ constexpr int TILE_TAPE = 64;            // records per tape tile (one side-job 
 constexpr int MAX_DIGIT_BITS = 11;       // radix digit width (LDS histogram of 2048 bins)
 constexpr uint32_t LDS_MAX_LEVELS = 1024; // ladders up to this depth are staged in LDS (17.5 KB/wave)
 
+// Batches per register-ladder launch at most (me_config.batches_per_launch). One launch matches a
+// group of up to ME_GMAX batches: every symbol's wave runs through its records of all of them in
+// order, so a launch costs the heaviest symbol's share of the whole group rather than the sum of
+// each batch's heaviest share (DESIGN.md §4).
+#ifndef ME_GROUP_MAX
+#define ME_GROUP_MAX 32  // (the launch arguments k_match_reg copies to LDS grow with it: 32 leaves room
+                         // for two workgroups per CU)
+#endif
+constexpr int ME_GMAX = ME_GROUP_MAX;
+constexpr uint32_t ME_DEFAULT_GROUP = 32;
+
 // Sticky error bits (BookDev::err).
 enum : uint32_t {
   ERR_CHUNK_OOM = 1u,
@@ -208,8 +219,20 @@ struct AggDev {
   uint32_t* fr;                // [fr_cap] chunk ids: freed by levels, surpluses, allocations
   AggRec* rec;                 // [max_batch]
   uint32_t* ctr;               // [AC_N] pool tops (zeroed by k_seq_sweep)
-  uint32_t ev_cap, mk_cap, fr_cap, pad;
+  uint32_t ev_cap, mk_cap, fr_cap;
+  uint32_t nslots;             // grouped launches: slot = symbol, nslots = S (0: k_hot_pick's hcount)
+  // grouped launches (register-window path, k_agg_gwalk): per symbol and batch of the group, [S][ME_GMAX + 1]
+  uint32_t* gev;               // the symbol's first log index of batch g (g = ng: the log's end)
+  uint32_t* gex;               // the fill offset (k_agg_fin's scan) at gev
+  uint32_t* gbase;             // scratch position of the symbol's first fill of batch g
 };
+// Where the record of a log entry lives (k_agg_levels / k_agg_place read the seq of a rest there).
+struct AggSrc {
+  const uint32_t* perm;          // sort path: j = grouped position, its batch index perm[j] in seq[0]
+  const uint64_t* seq[ME_GMAX];  // grouped launches (perm null): j = g << AGG_GSHIFT | batch index
+};
+constexpr uint32_t AGG_GSHIFT = 25;  // batch index bits of a grouped log entry (BK_MAX_BATCH)
+constexpr uint32_t AGG_IMASK = (1u << AGG_GSHIFT) - 1u;
 
 // Host side of a deep-window launch with hot symbols: k_match_hot (or the aggregate path) runs on `st`,
 // forked from and joined back into the engine stream by two events (me_kernels.hip launch_match).
@@ -217,6 +240,7 @@ struct HotLaunch {
   hipStream_t st = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
   bool agg = false;  // the aggregate path (me_agg.hip) instead of k_match_hot
+  bool agg_reg = false;  // L <= 128: grouped launches through the aggregate path (me_agg.hip k_agg_gwalk)
   AggDev ag{};
 };
 
@@ -300,16 +324,6 @@ struct BatchDev {
   const struct BkRec* b_rec;  // [(S + 1) * bcap] bucketed records
   uint32_t bcap;
 };
-// Batches per register-ladder launch at most (me_config.batches_per_launch). One launch matches a
-// group of up to ME_GMAX batches: every symbol's wave runs through its records of all of them in
-// order, so a launch costs the heaviest symbol's share of the whole group rather than the sum of
-// each batch's heaviest share (DESIGN.md §4).
-#ifndef ME_GROUP_MAX
-#define ME_GROUP_MAX 32  // (the launch arguments k_match_reg copies to LDS grow with it: 32 leaves room
-                         // for two workgroups per CU)
-#endif
-constexpr int ME_GMAX = ME_GROUP_MAX;
-constexpr uint32_t ME_DEFAULT_GROUP = 32;
 
 // Side jobs of one pipelined register-ladder launch (me_match_reg.hip), run by each workgroup's
 // extra waves while its matching waves work on group J-1: group the batches of group J into their

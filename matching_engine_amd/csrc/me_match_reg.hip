@@ -1840,5 +1840,18 @@ hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* b
   return hipGetLastError();
 }
 
+// The continuation launch alone (grouped launches through the aggregate path, me_agg.hip: the walk
+// handed its symbols off into bk.hand / hcount[0] exactly as the common launch does).
+hipError_t launch_match_reg_cont(hipStream_t st, const BookDev& bk, const BatchDev* bt, uint32_t ng, hipEvent_t ev1) {
+  if (!ng || ng > (uint32_t)ME_GMAX || bk.L > (uint32_t)RL) return hipErrorInvalidValue;
+  ColdArgs A{};
+  A.bk = bk;
+  A.ng = ng;
+  for (uint32_t g = 0; g < ng; ++g) A.bt[g] = bt[g];
+  const uint32_t match_wgs = (bk.S + REG_WAVES - 1) / REG_WAVES;
+  hipExtLaunchKernelGGL(k_match_reg<true>, dim3(match_wgs), dim3(128 * REG_WAVES), 0, st, nullptr, ev1, 0, A);
+  return hipGetLastError();
+}
+
 }  // namespace ME_REG_VARIANT
 }  // namespace me

@@ -1,0 +1,148 @@
+"""Grouped launches through the aggregate path (ME_REG_AGG=1, windows of at most 128 levels): every
+symbol of a launch group walked on level totals by k_agg_gwalk (me_agg.hip), FIFOs resolved per level,
+each batch's fills placed in its own scratch — every batch's outputs bit-exact against the oracle, through
+the pipelined host path (per-batch results and tapes) and back-to-back device batches. Cancels, prices
+outside the window and overfull buckets hand a symbol's rest of the group to k_match_reg's continuation
+launch. Needs an MI355X."""
+import os
+
+import numpy as np
+import pytest
+
+from tests._parity import assert_books_equal, assert_fills_equal, assert_results_equal
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def me(built):
+    import matching_engine_amd
+
+    return matching_engine_amd
+
+
+@pytest.fixture(scope="module")
+def orc(built):
+    from oracle import oracle
+
+    return oracle
+
+
+def _engine(me, sc, base, batches, **kw):
+    total = sum(len(b) for b in batches)
+    old = os.environ.get("ME_REG_AGG")
+    os.environ["ME_REG_AGG"] = "1"
+    try:
+        return me.Engine(sc.num_symbols, sc.levels, base, max_batch=max(len(b) for b in batches),
+                         max_resting=total + 1024, max_chunks=total + 2 * sc.num_symbols, seq_ring=1 << 22, **kw)
+    finally:
+        if old is None:
+            del os.environ["ME_REG_AGG"]
+        else:
+            os.environ["ME_REG_AGG"] = old
+
+
+def _pipelined(eng, batches, lag):
+    out, tickets = [None] * len(batches), []
+    for k, b in enumerate(batches):
+        tickets.append((k, eng.submit_host(b)))
+        while len(tickets) > lag:
+            j, t = tickets.pop(0)
+            out[j] = eng.collect(t)
+    for j, t in tickets:
+        out[j] = eng.collect(t)
+    return out
+
+
+def _check(eng, ob, batches, outs, ctx):
+    nf = 0
+    for k, b in enumerate(batches):
+        ro, fo = ob.submit(b)
+        assert_results_equal(outs[k][0], ro, f"{ctx} batch {k}")
+        assert_fills_equal(outs[k][1], fo, f"{ctx} batch {k}")
+        nf += len(fo)
+    assert_books_equal(eng, ob, range(eng.num_symbols), ctx)
+    assert eng.resting_count() == ob.resting(), f"{ctx}: resting count"
+    return nf
+
+
+@pytest.mark.parametrize("group,lag", [(1, 2), (4, 9), (32, 70)])
+def test_agg_groups_config2_every_batch(me, orc, group, lag):
+    """Config 2's stream (80 % LIMIT +-32 ticks, 20 % MARKET) on 96 symbols: no record leaves the
+    aggregate path; every batch of full and partial groups against the oracle."""
+    sc = me.preset(2, num_symbols=96, batch=4096)
+    st = me.Stream(sc)
+    base = st.base_prices()
+    batches = [st.next(sc.batch) for _ in range(72)]
+    ob = orc.OracleBook(sc.num_symbols)
+    with _engine(me, sc, base, batches, batches_per_launch=group) as eng:
+        nf = _check(eng, ob, batches, _pipelined(eng, batches, lag), f"agg G={group}")
+        assert eng.stats()["handoffs"] == 0
+    assert nf > 0
+
+
+@pytest.mark.parametrize("spread", [2, 60])
+def test_agg_groups_long_fifos_and_sweeps(me, orc, spread):
+    """Tight spreads (a few levels with long chunk chains) and wide ones (rests beyond the 64-entry
+    lists), sweeping MARKETs of up to 6 x 100 lots, G = 16."""
+    sc = me.preset(2, num_symbols=48, batch=4096, spread_ticks=spread, market_qty_mult=6, market_pct=25)
+    st = me.Stream(sc)
+    base = st.base_prices()
+    batches = [st.next(sc.batch) for _ in range(48)]
+    ob = orc.OracleBook(sc.num_symbols)
+    with _engine(me, sc, base, batches, batches_per_launch=16) as eng:
+        assert _check(eng, ob, batches, _pipelined(eng, batches, 20), f"agg spread={spread}") > 0
+
+
+def test_agg_groups_handoffs(me, orc):
+    """Cancels, a drifting mid with far LIMITs (re-centring) and OIDs above 2^33 at G = 32: symbols are
+    handed to the register kernel's continuation mid-group; every batch against the oracle."""
+    sc = me.preset(5, num_symbols=128, levels=128, batch=4096, cancel_pct=10, market_pct=15, market_qty_mult=3,
+                   drift_step=1, drift_every=3, far_pct=1, seq_start=(1 << 33) + 5)
+    st = me.Stream(sc)
+    base = st.base_prices()
+    batches = [st.next(sc.batch) for _ in range(80)]
+    ob = orc.OracleBook(sc.num_symbols)
+    with _engine(me, sc, base, batches, batches_per_launch=32) as eng:
+        _check(eng, ob, batches, _pipelined(eng, batches, 40), "agg handoffs")
+        assert eng.stats()["handoffs"] > 0
+
+
+def test_agg_groups_overfull_buckets(me, orc):
+    """A Zipf-skewed stream: the head symbols' buckets overflow BK_CAP records, so the walk hands them to
+    the continuation (which rescans the batch); every batch against the oracle."""
+    sc = me.preset(2, num_symbols=64, batch=8192, zipf_s=1.3)
+    st = me.Stream(sc)
+    base = st.base_prices()
+    batches = [st.next(sc.batch) for _ in range(24)]
+    ob = orc.OracleBook(sc.num_symbols)
+    with _engine(me, sc, base, batches, batches_per_launch=8) as eng:
+        _check(eng, ob, batches, _pipelined(eng, batches, 10), "agg overfull")
+        assert eng.stats()["handoffs"] > 0
+
+
+def test_agg_groups_device_back_to_back(me, orc):
+    """The bench's pattern at config 2's shape (1,024 symbols, 65,536-record batches, G = 32), device
+    batches back to back: books, resting count, fill total and the last batch against the oracle."""
+    sc = me.preset(2)
+    st = me.Stream(sc)
+    base = st.base_prices()
+    batches = [st.next(sc.batch) for _ in range(40)]
+    ob = orc.OracleBook(sc.num_symbols)
+    with _engine(me, sc, base, batches) as eng:
+        dbs = [eng.upload(b) for b in batches]
+        eng.timing_enable(True)
+        for db in dbs:
+            eng.submit_device(db)
+        r, f = eng.fetch_outputs(len(batches[-1]))
+        nfo = 0
+        for b in batches:
+            ro, fo = ob.submit(b)
+            nfo += len(fo)
+        assert_results_equal(r, ro, "agg back-to-back last batch")
+        assert_fills_equal(f, fo, "agg back-to-back last batch")
+        assert eng.timing_read()["fills"] == nfo
+        assert_books_equal(eng, ob, range(0, sc.num_symbols, 3), "agg back-to-back")
+        assert eng.resting_count() == ob.resting()
+        for db in dbs:
+            db.free()

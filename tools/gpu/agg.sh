@@ -4,7 +4,7 @@
 set -o pipefail
 TAG=${1:-agg}
 O=gpurun_out/$TAG; mkdir -p $O; export TMPDIR=/tmp
-timeout -k 10 700 python -u -m pytest tests/test_hot_path.py -m gpu -v -p no:cacheprovider --timeout 240 --timeout-method thread > $O/pytest_hot.log 2>&1
+timeout -k 10 700 python -u -m pytest tests/test_hot_path.py tests/test_agg_groups.py -m gpu -v -p no:cacheprovider --timeout 240 --timeout-method thread > $O/pytest_hot.log 2>&1
 rc=$?; grep -E "PASSED|FAILED|ERROR|passed|failed" $O/pytest_hot.log | tail -30
 if [ $rc -ne 0 ]; then grep -E "^E " $O/pytest_hot.log | head -40; exit 1; fi
 [ "$2" = "bench" ] || exit 0
