@@ -36,6 +36,7 @@ namespace me {
 namespace {
 
 constexpr uint32_t AGG_WORDS = AGG_MAX_L / 64;
+constexpr uint32_t AGG_GCHUNK = 8192;  // log keys k_agg_group stages in LDS per scatter chunk (16 KB)
 
 __device__ __forceinline__ int auni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ uint32_t auniu(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
@@ -478,14 +479,30 @@ __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const Agg
   a_rebuild<1>(w, A, ba0);
   a_rebuild<0>(w, B, L - 1 - bb0);
   uint32_t pos = hi;
+  // the blocks' records are gathered ahead of the chain: block b's fields were issued while block b - 1
+  // ran, its permutation entries while block b - 2 ran (no HBM round trip between blocks)
+  const gptr<const uint32_t> perm = (gptr<const uint32_t>)vptr(bt.perm);
+  auto perm_at = [&](uint32_t b) -> uint32_t { return perm[min(b + (uint32_t)lane, hi - 1u)]; };
+  uint32_t n_oi = perm_at(lo);
+  unsigned long long n_seq = bt.seq[n_oi];
+  long long n_px = bt.px[n_oi];
+  int n_q = bt.qty[n_oi];
+  uint32_t n_kd = bt.kind[n_oi];
+  uint32_t nn_oi = perm_at(lo + 64u);
   for (uint32_t blk = lo; blk < hi; blk += 64) {
     const uint32_t j = blk + (uint32_t)lane;
     const bool v = j < hi;
-    const uint32_t oi = v ? bt.perm[j] : 0u;
-    const unsigned long long oseq = v ? bt.seq[oi] : 0ull;
-    const long long opx = v ? bt.px[oi] : 0ll;
-    const int oq = v ? bt.qty[oi] : 0;
-    const uint32_t okd = v ? (uint32_t)bt.kind[oi] : 0u;
+    const unsigned long long oseq = v ? n_seq : 0ull;
+    const long long opx = v ? n_px : 0ll;
+    const int oq = v ? n_q : 0;
+    const uint32_t okd = v ? n_kd : 0u;
+    if (blk + 64u < hi) {  // the next block's fields and the one after's permutation, in flight
+      n_seq = bt.seq[nn_oi];
+      n_px = bt.px[nn_oi];
+      n_q = bt.qty[nn_oi];
+      n_kd = bt.kind[nn_oi];
+      nn_oi = perm_at(blk + 128u);
+    }
     const uint32_t cntb = min(64u, hi - blk);
     uint32_t rj;
     int olm;
@@ -544,7 +561,8 @@ __global__ __launch_bounds__(64) void k_agg_walk(BookDev bk, BatchDev bt, AggDev
 // events, in level order), then a stable scatter of the log indices (one wave, 64 events per step,
 // ranks by ballot multisplit over the level bits).
 __global__ __launch_bounds__(1024) void k_agg_group(BookDev bk, AggDev ag) {
-  extern __shared__ uint32_t cnt_l[];  // [L]
+  extern __shared__ uint32_t cnt_l[];  // [L], then AGG_GCHUNK 16-bit keys
+  uint16_t* keys = reinterpret_cast<uint16_t*>(cnt_l + bk.L);
   __shared__ uint32_t wsum[16], wnz[16], sbase;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint32_t L = bk.L;
@@ -613,24 +631,32 @@ __global__ __launch_bounds__(1024) void k_agg_group(BookDev bk, AggDev ag) {
         run += c;
       }
     __syncthreads();
-    if (wv == 0) {
-      for (uint32_t c0 = 0; c0 < n; c0 += 64) {
-        const uint32_t e = c0 + (uint32_t)lane;
-        const bool v = e < n;
-        const uint32_t key = v ? ag.ev[eb + e].lvl : 0u;
-        unsigned long long peers = __ballot(v);
-        for (uint32_t bit = 0; bit < nbits; ++bit) {
-          const unsigned long long bb = __ballot((key >> bit) & 1u);
-          peers &= ((key >> bit) & 1u) ? bb : ~bb;
+    // the scatter: chunks of AGG_GCHUNK keys staged in LDS by the whole workgroup (coalesced), then
+    // ranked and placed by one wave (its steps read LDS only: no HBM round trip per 64 events)
+    for (uint32_t c1 = 0; c1 < n; c1 += AGG_GCHUNK) {
+      const uint32_t m = min(AGG_GCHUNK, n - c1);
+      for (uint32_t e = tid; e < m; e += 1024) keys[e] = (uint16_t)ag.ev[eb + c1 + e].lvl;
+      __syncthreads();
+      if (wv == 0) {
+        for (uint32_t c0 = 0; c0 < m; c0 += 64) {
+          const uint32_t e = c0 + (uint32_t)lane;
+          const bool v = e < m;
+          const uint32_t key = v ? (uint32_t)keys[e] : 0u;
+          unsigned long long peers = __ballot(v);
+          for (uint32_t bit = 0; bit < nbits; ++bit) {
+            const unsigned long long bb = __ballot((key >> bit) & 1u);
+            peers &= ((key >> bit) & 1u) ? bb : ~bb;
+          }
+          const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
+          const uint32_t cp = (uint32_t)__popcll(peers);
+          const uint32_t start = cnt_l[key];
+          if (v) ag.evs[eb + start + rank] = eb + c1 + e;
+          __builtin_amdgcn_wave_barrier();
+          if (v && rank == 0) cnt_l[key] = start + cp;
+          __builtin_amdgcn_wave_barrier();
         }
-        const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
-        const uint32_t cp = (uint32_t)__popcll(peers);
-        const uint32_t start = cnt_l[key];
-        if (v) ag.evs[eb + start + rank] = eb + e;
-        __builtin_amdgcn_wave_barrier();
-        if (v && rank == 0) cnt_l[key] = start + cp;
-        __builtin_amdgcn_wave_barrier();
       }
+      __syncthreads();
     }
     __syncthreads();
   }
@@ -1276,17 +1302,23 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
     a_rebuild<1>(w, A, ba0);
     a_rebuild<0>(w, B, L - 1 - bb0);
     uint32_t hidx = NIL, gstop = ng;
+    // a batch's bucket is loaded while the batch before it runs (no HBM round trip between batches)
+    const size_t bko = (size_t)s * BK_CAP;
+    BkRec n0 = ga.b_rec[0][bko + lane], n1 = ga.b_rec[0][bko + 64 + lane];
     for (uint32_t g = 0; g < ng; ++g) {
       if (lane == 0) *a_gtab(ag.gev, s, g) = w.evp;
       const uint32_t cnt = rl32(nsv, (int)g);
+      const BkRec r0 = n0, r1 = n1;
+      if (g + 1u < ng) {
+        n0 = ga.b_rec[g + 1][bko + lane];
+        n1 = ga.b_rec[g + 1][bko + 64 + lane];
+      }
       if (!cnt) continue;
       if (cnt > (uint32_t)BK_CAP) {  // an overfull bucket: the continuation rescans the batch
         hidx = a_ghand(bk, s, g, 0u, cnt, 0u, 0u);
         gstop = g;
         break;
       }
-      const size_t bb = (size_t)s * BK_CAP;
-      const BkRec r0 = ga.b_rec[g][bb + lane], r1 = ga.b_rec[g][bb + 64 + lane];
       if (lane == 0) ga.bcnt[g][(size_t)s * BK_CNT_STRIDE] = 0u;  // ready for a later group's bucket job
       stg.seq[lane] = r0.seq;
       stg.seq[64 + lane] = r1.seq;
@@ -1503,7 +1535,7 @@ hipError_t launch_agg(hipStream_t hs, const BookDev& bk, const BatchDev& bt, con
   src.perm = bt.perm;
   src.seq[0] = bt.seq;
   hipLaunchKernelGGL(k_agg_walk, dim3(64), dim3(64), 0, hs, bk, bt, ag);
-  hipLaunchKernelGGL(k_agg_group, dim3(64), dim3(1024), (size_t)bk.L * 4u, hs, bk, ag);
+  hipLaunchKernelGGL(k_agg_group, dim3(64), dim3(1024), (size_t)bk.L * 4u + AGG_GCHUNK * 2u, hs, bk, ag);
   hipLaunchKernelGGL(k_agg_levels, dim3(1024), dim3(256), 0, hs, bk, src, ag);
   hipLaunchKernelGGL(k_agg_alloc, dim3(64), dim3(64), 0, hs, bk, ag);
   hipLaunchKernelGGL(k_agg_place, dim3(1024), dim3(256), 0, hs, bk, src, ag);
@@ -1539,7 +1571,7 @@ hipError_t launch_agg_group(hipStream_t st, const BookDev& bk, const BatchDev* b
   ga.ng = ng;
   const uint32_t grid = bk.S < 2048u ? bk.S : 2048u;
   hipLaunchKernelGGL(k_agg_gwalk, dim3(grid), dim3(64), 0, st, bk, ga, ag);
-  hipLaunchKernelGGL(k_agg_group, dim3(grid), dim3(1024), (size_t)bk.L * 4u, st, bk, ag);
+  hipLaunchKernelGGL(k_agg_group, dim3(grid), dim3(1024), (size_t)bk.L * 4u + AGG_GCHUNK * 2u, st, bk, ag);
   hipLaunchKernelGGL(k_agg_levels, dim3(2048), dim3(256), 0, st, bk, src, ag);
   hipLaunchKernelGGL(k_agg_alloc, dim3(grid), dim3(64), 0, st, bk, ag);
   hipLaunchKernelGGL(k_agg_place, dim3(2048), dim3(256), 0, st, bk, src, ag);
