@@ -37,6 +37,7 @@ namespace {
 
 constexpr uint32_t AGG_WORDS = AGG_MAX_L / 64;
 constexpr uint32_t AGG_GCHUNK = 8192;  // log keys k_agg_group stages in LDS per scatter chunk (16 KB)
+constexpr int AGG_VMCNT0 = 0x0F70;     // s_waitcnt immediate: vmcnt(0) only (gfx9 encoding)
 
 __device__ __forceinline__ int auni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ uint32_t auniu(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
@@ -202,6 +203,10 @@ __device__ __forceinline__ void a_rebuild(AWalk& w, AList& S, int start_m) {
   const bool v = lane < n;
   long long t = 0;
   if (v) t = w.lv[lvl].total;
+  // wait here, on the rare path: otherwise the list registers carry a possibly pending load into the
+  // record loop, and every read of them there waits vmcnt(0) — which, gfx9 counting loads and stores in
+  // one in-order counter, also waits for every store the chain has issued (~1 us per record measured)
+  __builtin_amdgcn_s_waitcnt(AGG_VMCNT0);
   S.m = v ? a_side_lvl(w.L, K, lvl) : w.L;
   S.tot = t;
   S.f = 0;
@@ -294,6 +299,26 @@ __device__ __forceinline__ void a_rest(AWalk& w, AList& M, int mm, int lvl, int 
     M.more = 1;
   }
   a_emit(w, lvl, jt, q);
+}
+
+// The slot's regions of the consumed-maker list and of the chunk-id pool, sized by the slot's fill bound
+// (consumed makers <= fills <= resting makers + 2 * records): the per-level kernels then reserve from
+// the slot's own cursors (no pool-wide atomic per level). False: the pools are full.
+__device__ __forceinline__ bool a_reserve(const AggDev& ag, gptr<AggSlot> slot, uint32_t resting, uint32_t cnt) {
+  const unsigned long long mkb = (unsigned long long)resting + 2ull * cnt + 64ull;
+  const unsigned long long frb = 2ull * mkb + cnt + 64ull;
+  uint32_t mb = 0, fb = 0;
+  if (lane_id() == 0) {
+    mb = atomicAdd(&ag.ctr[AC_MK], (uint32_t)mkb);
+    fb = atomicAdd(&ag.ctr[AC_FR], (uint32_t)frb);
+    slot->mk_base = mb;
+    slot->mk_cur = 0u;
+    slot->fr_base = fb;
+    slot->fr_cur = 0u;
+  }
+  mb = rl32(mb, 0);
+  fb = rl32(fb, 0);
+  return mb + mkb <= (unsigned long long)ag.mk_cap && fb + frb <= (unsigned long long)ag.fr_cap;
 }
 
 // Results of one block's records, lane k = record k.
@@ -460,7 +485,8 @@ __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const Agg
     a_set_err(bk, ERR_SCRATCH_OOM);
     return;
   }
-  if (!eok) {  // no room in the log: every record of the symbol goes to the generic loop
+  if (!eok || !a_reserve(ag, slot, resting, cnt)) {  // no room in the pools: every record of the symbol
+                                                     // goes to the generic loop
     if (lane == 0) {
       const uint32_t idx = atomicAdd(bk.hcount + 1, 1u);
       Handoff ho{};
@@ -776,8 +802,8 @@ __global__ __launch_bounds__(256) void k_agg_levels(BookDev bk, AggSrc src, AggD
     const uint32_t nmkt = nmk + nrc;
     uint32_t mk_base = 0, fr_base = 0, d_off = 0;
     if (lane == 0) {
-      mk_base = atomicAdd(&ag.ctr[AC_MK], nmkt);
-      fr_base = atomicAdd(&ag.ctr[AC_FR], nfreed);
+      mk_base = sl->mk_base + atomicAdd(&sl->mk_cur, nmkt);
+      fr_base = sl->fr_base + atomicAdd(&sl->fr_cur, nfreed);
       if (deficit) d_off = atomicAdd(&sl->deficit, deficit);
       const int dr = (int)ks - (int)nfull;
       if (dr) atomicAdd(&sl->dresting, dr);
@@ -911,7 +937,7 @@ __global__ __launch_bounds__(64) void k_agg_alloc(BookDev bk, AggDev ag) {
     }
     if (!D && !Stot) continue;
     uint32_t ab = 0;
-    if (lane == 0) ab = atomicAdd(&ag.ctr[AC_FR], D + Stot);
+    if (lane == 0) ab = sl->fr_base + atomicAdd(&sl->fr_cur, D + Stot);
     ab = rl32(ab, 0);
     if ((unsigned long long)ab + D + Stot > ag.fr_cap) {
       a_set_err(bk, ERR_SCRATCH_OOM);
@@ -1291,7 +1317,8 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
       *slot = o;
     }
     if (!total) continue;
-    if (!eok) {  // no room in the log: the whole group of the symbol goes to the continuation
+    if (!eok || !a_reserve(ag, slot, resting, total)) {  // no room in the pools: the whole group of the
+                                                          // symbol goes to the continuation
       const uint32_t g0 = (uint32_t)__builtin_ctzll(__ballot(nsv != 0u));
       a_ghand(bk, s, g0, 0u, rl32(nsv, (int)g0), s * ga.slab, s * ga.slab + ga.slab);
       continue;

@@ -553,8 +553,10 @@ extern "C" me_engine* me_create(const me_config* cfg) {
     const uint64_t gmax = e->hot.agg_reg ? (cfg->batches_per_launch ? cfg->batches_per_launch : ME_DEFAULT_GROUP) : 1;
     const uint64_t nrec = n * gmax;
     const uint64_t evc = e->hot.agg_reg ? 3 * nrec + S * (L + 128) + 4096 : 3 * n + 16 * (L + 64) + 4096;
-    const uint64_t mkc = cfg->max_resting + 2 * nrec + 64;
-    const uint64_t frc = 2 * mkc + nrec + 64;
+    // (per slot: resting + 2 records + 64 makers, twice that + records + 64 chunk ids; the slots of a
+    // launch are at most S)
+    const uint64_t mkc = cfg->max_resting + 2 * nrec + 64 * (S + 1);
+    const uint64_t frc = 2 * mkc + nrec + 64 * (S + 1);
     if (evc >= 0x7FFFFFFFull || frc >= 0xFFFFFFFFull) return bail("me_create: aggregate-path pools exceed 32-bit ids");
     a.ev_cap = (uint32_t)evc;
     a.mk_cap = (uint32_t)mkc;

@@ -202,7 +202,10 @@ struct AggSlot {     // one hot symbol of the launch (index = k_hot_pick's hand-
   uint32_t deficit, alloc_base, free_head, resting0;
   int32_t dresting;
   int32_t bb, ba;
-  uint32_t active, hidx, gs, pad[2];
+  uint32_t active, hidx, gs;
+  uint32_t mk_base, mk_cur;  // the slot's region of AggDev::mk (reserved by the walk) and its cursor
+  uint32_t fr_base, fr_cur;  // the same for AggDev::fr
+  uint32_t pad;
 };
 enum : uint32_t { AC_EV = 0, AC_SEG = 1, AC_MK = 2, AC_FR = 3, AC_N = 8 };
 struct AggDev {

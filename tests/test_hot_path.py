@@ -158,7 +158,7 @@ def test_agg_single_symbol_config1(me, orc, levels):
     assert nf > 0
 
 
-@pytest.mark.parametrize("spread", [2, 40, 700])
+@pytest.mark.parametrize("spread", [2, 40, 400])
 def test_agg_many_symbols_no_handoff(me, orc, spread):
     """Every symbol hot (ME_HOT_MIN=1) on a 1,024-level window, no cancels, no far prices: the aggregate
     path alone, with tight spreads (long FIFOs, sweeps through many makers per level) and wide ones
