@@ -439,8 +439,239 @@ __device__ __forceinline__ void a_walk_end(AWalk& w, AList& A, AList& B, int& bb
   bb = B.n ? w.L - 1 - rli32(B.m, B.f) : -1;
 }
 
+// ------------------------------------------------------------------ the ladder walk (L <= 256)
+// Windows of at most 256 levels need no lists: the level totals live in LDS indexed by level, the
+// occupancy in up to four SGPR words, and the totals of the two best levels in SGPRs (their LDS copies
+// are stale while cached). A rest is an LDS add and a bit set (plus a swap of the cached best when it
+// becomes the best); a take compares with an SGPR and only when it empties a level finds the next bit
+// and reads one LDS total. No global memory operation on the chain but the log's 1-KB block stores.
+constexpr uint32_t LW_BUY = 1u << 9, LW_MKT = 1u << 10, LW_RJ_SHIFT = 11;
+
+template <int NW>
+struct LWalk {
+  long long* tot;    // LDS [L]
+  long long* dummy;  // LDS [64]: the other lanes' targets of a one-lane LDS operation
+  unsigned long long o[NW];
+  int bb, ba;        // best bid (-1: none), best ask (L: none)
+  long long tbb, tba;
+  int L;
+};
+
+template <int NW>
+__device__ __forceinline__ void lw_set(LWalk<NW>& w, int l) {
+  const int wi = l >> 6;
+  const unsigned long long b = 1ull << (l & 63);
+#pragma unroll
+  for (int i = 0; i < NW; ++i) w.o[i] |= i == wi ? b : 0ull;
+}
+template <int NW>
+__device__ __forceinline__ void lw_clr(LWalk<NW>& w, int l) {
+  const int wi = l >> 6;
+  const unsigned long long b = 1ull << (l & 63);
+#pragma unroll
+  for (int i = 0; i < NW; ++i) w.o[i] &= i == wi ? ~b : ~0ull;
+}
+// smallest occupied level >= x, or L
+template <int NW>
+__device__ __forceinline__ int lw_next(const LWalk<NW>& w, int x) {
+  int r = w.L;
+#pragma unroll
+  for (int i = NW - 1; i >= 0; --i) {
+    const int b0 = i * 64;
+    unsigned long long m = w.o[i];
+    m = x <= b0 ? m : (x >= b0 + 64 ? 0ull : m & (~0ull << (x - b0)));
+    r = m ? b0 + __builtin_ctzll(m) : r;
+  }
+  return r;
+}
+// largest occupied level <= x, or -1
+template <int NW>
+__device__ __forceinline__ int lw_prev(const LWalk<NW>& w, int x) {
+  int r = -1;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    const int b0 = i * 64;
+    unsigned long long m = w.o[i];
+    m = x >= b0 + 63 ? m : (x < b0 ? 0ull : m & (~0ull >> (63 - (x - b0))));
+    r = m ? b0 + 63 - __builtin_clzll(m) : r;
+  }
+  return r;
+}
+// one-lane LDS writes: lane 0 on the level, every other lane on its own dummy slot (no exec change)
+template <int NW>
+__device__ __forceinline__ void lw_add(LWalk<NW>& w, int l, long long d) {
+  const int lane = lane_id();
+  long long* p = lane == 0 ? &w.tot[l] : &w.dummy[lane];
+  __hip_atomic_fetch_add(p, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+template <int NW>
+__device__ __forceinline__ void lw_put(LWalk<NW>& w, int l, long long v) {
+  const int lane = lane_id();
+  long long* p = lane == 0 ? &w.tot[l] : &w.dummy[lane];
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+template <int NW>
+__device__ __forceinline__ long long lw_get(const LWalk<NW>& w, int l) {
+  return (long long)rl64((unsigned long long)__hip_atomic_load(&w.tot[l], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP), 0);
+}
+
+template <int NW>
+__device__ __forceinline__ void lw_take_buy(AWalk& e, LWalk<NW>& w, int lim, uint32_t& rem, uint32_t jt) {
+  while (rem && w.ba <= lim) {
+    if ((long long)rem < w.tba) {
+      w.tba -= (long long)rem;
+      a_emit(e, w.ba, jt, (int)rem);
+      rem = 0;
+      return;
+    }
+    a_emit(e, w.ba, jt, (int)w.tba);
+    rem -= (uint32_t)w.tba;
+    lw_put(w, w.ba, 0ll);  // empty levels hold 0 (a rest there adds)
+    lw_clr(w, w.ba);
+    w.ba = lw_next(w, w.ba + 1);
+    w.tba = w.ba < w.L ? lw_get(w, w.ba) : 0ll;
+  }
+}
+template <int NW>
+__device__ __forceinline__ void lw_take_sell(AWalk& e, LWalk<NW>& w, int lim, uint32_t& rem, uint32_t jt) {
+  while (rem && w.bb >= lim) {
+    if ((long long)rem < w.tbb) {
+      w.tbb -= (long long)rem;
+      a_emit(e, w.bb, jt, (int)rem);
+      rem = 0;
+      return;
+    }
+    a_emit(e, w.bb, jt, (int)w.tbb);
+    rem -= (uint32_t)w.tbb;
+    lw_put(w, w.bb, 0ll);
+    lw_clr(w, w.bb);
+    w.bb = lw_prev(w, w.bb - 1);
+    w.tbb = w.bb >= 0 ? lw_get(w, w.bb) : 0ll;
+  }
+}
+// a bid rests at l (< ba: every ask up to the limit was taken)
+template <int NW>
+__device__ __forceinline__ void lw_rest_buy(AWalk& e, LWalk<NW>& w, int l, int q, uint32_t jt) {
+  if (l == w.bb) {
+    w.tbb += q;
+  } else if (l > w.bb) {  // a new best bid (an empty level)
+    if (w.bb >= 0) lw_put(w, w.bb, w.tbb);
+    lw_set(w, l);
+    w.bb = l;
+    w.tbb = q;
+  } else {
+    lw_add(w, l, q);
+    lw_set(w, l);
+  }
+  a_emit(e, l, jt, q);
+}
+template <int NW>
+__device__ __forceinline__ void lw_rest_sell(AWalk& e, LWalk<NW>& w, int l, int q, uint32_t jt) {
+  if (l == w.ba) {
+    w.tba += q;
+  } else if (l < w.ba) {
+    if (w.ba < w.L) lw_put(w, w.ba, w.tba);
+    lw_set(w, l);
+    w.ba = l;
+    w.tba = q;
+  } else {
+    lw_add(w, l, q);
+    lw_set(w, l);
+  }
+  a_emit(e, l, jt, q);
+}
+
+// The ladder from HBM: LDS totals, occupancy from them, the cached best totals.
+template <int NW>
+__device__ __forceinline__ void lw_init(LWalk<NW>& w, const BookDev& bk, uint32_t s, long long* lds, int bb, int ba) {
+  const int lane = lane_id();
+  w.L = (int)bk.L;
+  w.tot = lds;
+  w.dummy = lds + 256;
+  const Level* lv = bk.levels + (size_t)s * bk.L;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    const int l = i * 64 + lane;
+    const long long t = l < w.L ? lv[l].total : 0ll;
+    w.tot[l] = t;
+    w.o[i] = __ballot(t > 0);
+  }
+  wave_mem_order();
+  w.bb = bb;
+  w.ba = ba;
+  w.tbb = bb >= 0 ? lw_get(w, bb) : 0ll;
+  w.tba = ba < w.L ? lw_get(w, ba) : 0ll;
+}
+// The ladder back to HBM (totals, occupancy); the cached totals first.
+template <int NW>
+__device__ __forceinline__ void lw_end(LWalk<NW>& w, const BookDev& bk, uint32_t s) {
+  const int lane = lane_id();
+  if (w.bb >= 0) lw_put(w, w.bb, w.tbb);
+  if (w.ba < w.L) lw_put(w, w.ba, w.tba);
+  wave_mem_order();
+  Level* lv = bk.levels + (size_t)s * bk.L;
+  unsigned long long* oc = bk.occ + (size_t)s * bk.Lwords;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    const int l = i * 64 + lane;
+    if (l < w.L) lv[l].total = w.tot[l];
+    if (lane == 0 && i < (int)bk.Lwords) oc[i] = w.o[i];
+  }
+}
+
+// Control word of a record in vector form: the level a LIMIT rests at / the last level a taker may
+// trade at (MARKET: the far end of the window), side, type, reject reason.
+__device__ __forceinline__ uint32_t lw_cw(uint32_t okd, int olm, uint32_t rj, int L) {
+  const bool buy = (okd & 3u) == ME_SIDE_BUY, mkt = (okd >> 2) & 1u;
+  const int lim = mkt ? (buy ? L - 1 : 0) : (olm & 0x1FF);
+  return (uint32_t)lim | (buy ? LW_BUY : 0u) | (mkt ? LW_MKT : 0u) | (rj << LW_RJ_SHIFT);
+}
+
+template <int NW>
+__device__ __forceinline__ uint32_t lw_block(AWalk& e, LWalk<NW>& w, int oq, uint32_t ocw, uint32_t ojt,
+                                             unsigned long long fastm, uint32_t cnt, int& rr) {
+  uint32_t k = 0;
+  for (; k < cnt; ++k) {
+    if (ME_UNLIKELY(!((fastm >> k) & 1ull))) break;
+    const uint32_t cw = rl32(ocw, (int)k);
+    if (ME_UNLIKELY(cw >> LW_RJ_SHIFT)) continue;  // rejected: its result comes from the reason
+    const uint32_t jt = rl32(ojt, (int)k);
+    const int lim = (int)(cw & 0x1FFu);
+    uint32_t rem = (uint32_t)rli32(oq, (int)k);
+    if (cw & LW_BUY) {
+      lw_take_buy(e, w, lim, rem, jt | AGG_TAKE);
+      if (!(cw & LW_MKT) && rem) lw_rest_buy(e, w, lim, (int)rem, jt);
+    } else {
+      lw_take_sell(e, w, lim, rem, jt | AGG_TAKE);
+      if (!(cw & LW_MKT) && rem) lw_rest_sell(e, w, lim, (int)rem, jt);
+    }
+    rr = lane_id() == (int)k ? (int)rem : rr;
+  }
+  return k;
+}
+
+// A record's result from its fields and the remainder the chain left (vector form); fill count and
+// scratch start come later (k_agg_fin / k_agg_gfin, from the log).
+__device__ __forceinline__ me_order_result a_result(int oq, uint32_t okd, uint32_t rj, int rem) {
+  const bool mkt = (okd >> 2) & 1u;
+  const int filled = rj ? 0 : oq - rem;
+  me_order_result o;
+  o.filled_qty = filled;
+  o.remaining_qty = rj ? (rj == ME_RJ_BAD_QTY ? 0 : oq) : rem;
+  o.fill_count = 0;
+  o.tape_offset = 0;
+  o.status = (uint8_t)(rj ? ME_ST_REJECTED
+                          : rem == 0 ? ME_ST_FILLED
+                          : mkt      ? ME_ST_CANCELED
+                          : filled   ? ME_ST_PARTIALLY_FILLED
+                                     : ME_ST_NEW);
+  o.reason = (uint8_t)rj;
+  o.pad[0] = o.pad[1] = 0;
+  return o;
+}
+
 __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const AggDev& ag, uint32_t i, uint32_t s,
-                                uint32_t lo, uint32_t hi, unsigned long long* locc) {
+                                uint32_t lo, uint32_t hi, unsigned long long* locc, long long* ltot) {
   const int lane = lane_id();
   const int L = (int)bk.L;
   const SymState st = bk.sym[s];
@@ -501,9 +732,16 @@ __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const Agg
   }
   AWalk w;
   a_walk_init(w, bk, ag, s, eb, locc);
+  // windows of at most 256 levels: the ladder walk; deeper ones: the top-of-book lists
+  const bool ladder = L <= 4 * 64;
   AList A, B;  // asks (side 1), bids (side 0)
-  a_rebuild<1>(w, A, ba0);
-  a_rebuild<0>(w, B, L - 1 - bb0);
+  LWalk<4> lw;
+  if (ladder) {
+    lw_init(lw, bk, s, ltot, bb0, ba0);
+  } else {
+    a_rebuild<1>(w, A, ba0);
+    a_rebuild<0>(w, B, L - 1 - bb0);
+  }
   uint32_t pos = hi;
   // the blocks' records are gathered ahead of the chain: block b's fields were issued while block b - 1
   // ran, its permutation entries while block b - 2 ran (no HBM round trip between blocks)
@@ -518,11 +756,13 @@ __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const Agg
   for (uint32_t blk = lo; blk < hi; blk += 64) {
     const uint32_t j = blk + (uint32_t)lane;
     const bool v = j < hi;
+    const uint32_t oi = n_oi;
     const unsigned long long oseq = v ? n_seq : 0ull;
     const long long opx = v ? n_px : 0ll;
     const int oq = v ? n_q : 0;
     const uint32_t okd = v ? n_kd : 0u;
     if (blk + 64u < hi) {  // the next block's fields and the one after's permutation, in flight
+      n_oi = nn_oi;
       n_seq = bt.seq[nn_oi];
       n_px = bt.px[nn_oi];
       n_q = bt.qty[nn_oi];
@@ -533,18 +773,19 @@ __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const Agg
     uint32_t rj;
     int olm;
     const unsigned long long fastm = __ballot(a_classify(v, oseq, opx, oq, okd, base, L, nfar0, nfar1, rj, olm));
-    a_refill(w, A, B);
-    ARes R;
-    const uint32_t k = a_block(w, A, B, oq, okd, olm, rj, j, fastm, cntb, R);
-    if (v && (uint32_t)lane < k) {
-      AggRec r;
-      r.filled = R.rf;
-      r.rem = R.rr;
-      r.st = R.rs;
-      r.ev_lo = R.rlo;
-      r.ev_n = R.rn;
-      r.pad = 0;
-      ag.rec[j] = r;
+    int rr = 0;
+    uint32_t k;
+    if (ladder) {
+      k = lw_block(w, lw, oq, lw_cw(okd, olm, rj, L), j, fastm, cntb, rr);
+    } else {
+      a_refill(w, A, B);
+      ARes R;
+      k = a_block(w, A, B, oq, okd, olm, rj, j, fastm, cntb, R);
+      rr = R.rr;
+    }
+    if (v && (uint32_t)lane < k) {  // fill count and scratch start: k_agg_fin
+      bt.res[oi] = a_result(oq, okd, rj, rr);
+      bt.fstart[oi] = 0u;
     }
     if (k < cntb) {
       pos = blk + k;  // the generic loop takes over from here (k_match_hot_cont)
@@ -552,7 +793,14 @@ __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const Agg
     }
   }
   int bb, ba;
-  a_walk_end(w, A, B, bb, ba);
+  if (ladder) {
+    if (w.evp & 63u) a_evstore(w, w.evp & ~63u, w.evp & 63u);
+    lw_end(lw, bk, s);
+    bb = lw.bb;
+    ba = lw.ba;
+  } else {
+    a_walk_end(w, A, B, bb, ba);
+  }
   if (lane == 0) {
     slot->pos = pos;
     slot->ev_cnt = w.evp - eb;
@@ -575,10 +823,11 @@ __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const Agg
 
 __global__ __launch_bounds__(64) void k_agg_walk(BookDev bk, BatchDev bt, AggDev ag) {
   __shared__ unsigned long long locc[AGG_WORDS];
+  __shared__ long long ltot[256 + 64];  // the ladder walk's totals and dummy slots
   const uint32_t nh = min(*(volatile uint32_t*)bk.hcount, bk.S);
   for (uint32_t i = blockIdx.x; i < nh; i += gridDim.x) {
     const Handoff ho = bk.hand[i];
-    agg_walk_symbol(bk, bt, ag, i, auniu(ho.s), auniu(ho.pos), auniu(ho.nsg), locc);
+    agg_walk_symbol(bk, bt, ag, i, auniu(ho.s), auniu(ho.pos), auniu(ho.nsg), locc, ltot);
   }
 }
 
@@ -684,6 +933,13 @@ __global__ __launch_bounds__(1024) void k_agg_group(BookDev bk, AggDev ag) {
       }
       __syncthreads();
     }
+    // the sorted copies the per-level kernels read (one hop instead of index -> entry)
+    for (uint32_t p = tid; p < n; p += 1024) {
+      const uint32_t e = ag.evs[eb + p];
+      AggEv E = ag.ev[e];
+      E.pad = e;
+      ag.evq[eb + p] = E;
+    }
     __syncthreads();
   }
 }
@@ -708,14 +964,37 @@ __device__ __forceinline__ uint32_t a_search(const AggMk* mk, uint32_t b, uint32
   return lo;
 }
 
-// One wave per segment (symbol, level): the quantity C the batch took from the level; the initial
-// FIFO walked until C is covered (count pass, then a write pass: consumed makers into mk, emptied
-// chunks zeroed into fr, the chunk C ends in updated); the rests C reaches; each take's first maker
-// and fill count; what the surviving rests need.
+// First index in the LDS maker list m[0, n) whose end is > x (strict = false: >= x).
+__device__ __forceinline__ uint32_t a_search_lds(const AggMk* m, uint32_t n, unsigned long long x, bool strict) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    const unsigned long long e = m[mid].end;
+    if (strict ? e <= x : e < x)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
+constexpr uint32_t LV_STAGE = 64;  // consumed makers / emptied chunks a level keeps in LDS (else: HBM)
+
+// One wave per segment (symbol, level): the quantity C the batch took from the level; the initial FIFO
+// read once until C is covered — consumed makers (seq, interval end) and emptied chunks staged in LDS —
+// and the rests C reaches; then the makers and emptied chunks to HBM, the emptied chunks zeroed, the
+// chunk C ends in updated; each take's first maker and fill count (binary search in the staged list);
+// what the surviving rests need. A level whose takes consume more than LV_STAGE makers (or empty more
+// chunks) reads its FIFO a second time, writing straight into HBM.
 __global__ __launch_bounds__(256) void k_agg_levels(BookDev bk, AggSrc src, AggDev ag) {
+  __shared__ AggMk smk[4][LV_STAGE];
+  __shared__ uint32_t sfr[4][LV_STAGE];
   const int lane = lane_id();
   const bool act = lane < ME_C;
-  const uint32_t gw = blockIdx.x * 4u + (threadIdx.x >> 6), nw = gridDim.x * 4u;
+  const uint32_t wv = threadIdx.x >> 6;
+  AggMk* mkl = smk[wv];
+  uint32_t* frl = sfr[wv];
+  const uint32_t gw = blockIdx.x * 4u + wv, nw = gridDim.x * 4u;
   const uint32_t nseg = min(*(volatile uint32_t*)&ag.ctr[AC_SEG], ag.ev_cap);
   for (uint32_t si = gw; si < nseg; si += nw) {
     const AggSeg sg = ag.seg[si];
@@ -724,26 +1003,31 @@ __global__ __launch_bounds__(256) void k_agg_levels(BookDev bk, AggSrc src, AggD
     const uint32_t s = auniu(sl->s);
     const size_t li = (size_t)s * bk.L + lvl;
     const uint32_t head0 = auniu(bk.levels[li].head);
-    // 1. takes: C and each take's interval start
-    unsigned long long C = 0;
-    uint32_t nrest = 0;
-    for (uint32_t b = 0; b < cnt; b += 64) {
-      const bool v = b + (uint32_t)lane < cnt;
-      const uint32_t e = v ? ag.evs[start + b + lane] : 0u;
+    const uint32_t te_raw = (uint32_t)bk.tend[li];
+    // the first 64 entries stay in registers (most levels have no more)
+    AggEv E0{};
+    if ((uint32_t)lane < cnt) E0 = ag.evq[start + lane];
+    auto entry = [&](uint32_t b) -> AggEv {
+      if (b == 0) return E0;
       AggEv E{};
-      if (v) E = ag.ev[e];
+      if (b + (uint32_t)lane < cnt) E = ag.evq[start + b + lane];
+      return E;
+    };
+    // 1. C: the takes' total
+    unsigned long long C = 0;
+    for (uint32_t b = 0; b < cnt; b += 64) {
+      const AggEv E = entry(b);
+      const bool v = b + (uint32_t)lane < cnt;
       const bool tk = v && (E.j & AGG_TAKE) != 0u;
-      const bool rs = v && !tk;
-      const long long tq = tk ? (long long)E.qty : 0ll;
-      const long long inc = wave_incl_scan(tq);
-      if (tk) ag.eva[e] = C + (unsigned long long)(inc - tq);
-      if (rs) ag.evn[e] = 0u;
-      C += (unsigned long long)rli64(inc, 63);
-      nrest += (uint32_t)__popcll(__ballot(rs));
+      if (v && !tk) ag.evn[E.pad] = 0u;
+      C += (unsigned long long)rli64(wave_incl_scan(tk ? (long long)E.qty : 0ll), 63);
     }
-    // 2. count pass over the initial FIFO
+    // 2. the initial FIFO, read once: consumed makers and emptied chunks staged in LDS; the chunk C ends
+    //    in keeps its quantities and interval ends in registers (pq, pen)
     unsigned long long W = 0;
-    uint32_t nmk = 0, nfreed = 0, nfull = 0, newhead = NIL, ch = head0;
+    uint32_t nmk = 0, nfreed = 0, nfull = 0, newhead = NIL, ch = head0, pch = NIL;
+    int pq = 0;
+    unsigned long long pen = 0;
     bool exhausted = false;
     for (;;) {
       if (ch == NIL) {
@@ -760,42 +1044,59 @@ __global__ __launch_bounds__(256) void k_agg_levels(BookDev bk, AggSrc src, AggD
         break;
       }
       const int q = act ? bk.chunks[ch].qty[lane] : 0;
+      const unsigned long long sq = act ? bk.chunks[ch].seq[lane] : 0ull;
       const uint32_t nx = auniu(bk.chunks[ch].hdr.next);
       const long long inc = wave_incl_scan((long long)q);
-      const unsigned long long ex = (unsigned long long)(inc - q);
+      const unsigned long long ex = (unsigned long long)(inc - q), en = W + (unsigned long long)inc;
       const unsigned long long live = (unsigned long long)rli64(inc, 63);
-      nmk += (uint32_t)__popcll(__ballot(q > 0 && W + ex < C));
-      nfull += (uint32_t)__popcll(__ballot(q > 0 && W + (unsigned long long)inc <= C));
-      if (W + live <= C) {
+      const bool cons = q > 0 && W + ex < C;
+      const unsigned long long cm = __ballot(cons);
+      const uint32_t r = nmk + (uint32_t)__popcll(cm & lanemask_lt());
+      if (cons && r < LV_STAGE) {
+        mkl[r].seq = sq;
+        mkl[r].end = en;
+      }
+      nmk += (uint32_t)__popcll(cm);
+      nfull += (uint32_t)__popcll(__ballot(q > 0 && en <= C));
+      if (W + live <= C) {  // emptied
+        if (lane == 0 && nfreed < LV_STAGE) frl[nfreed] = ch;
         ++nfreed;
         W += live;
         ch = nx;
         continue;
       }
-      newhead = ch;  // C ends inside this chunk
+      pch = ch;  // C ends inside this chunk
+      pq = q;
+      pen = en;
+      newhead = ch;
       break;
     }
     const unsigned long long T0 = exhausted ? W : ~0ull;
     const unsigned long long Cr = exhausted && C > W ? C - W : 0ull;  // taken from this batch's rests
-    // rests C reaches (makers too) and rests that survive
+    // 3. the rests: those C reaches are makers too (staged after the FIFO's), the others survive
     uint32_t nrc = 0, ks = 0;
     {
       unsigned long long RR = 0;
       for (uint32_t b = 0; b < cnt; b += 64) {
+        const AggEv E = entry(b);
         const bool v = b + (uint32_t)lane < cnt;
-        const uint32_t e = v ? ag.evs[start + b + lane] : 0u;
-        AggEv E{};
-        if (v) E = ag.ev[e];
         const bool rs = v && (E.j & AGG_TAKE) == 0u;
         const long long rq = rs ? (long long)E.qty : 0ll;
         const long long inc = wave_incl_scan(rq);
         const unsigned long long st0 = RR + (unsigned long long)(inc - rq), en = RR + (unsigned long long)inc;
-        nrc += (uint32_t)__popcll(__ballot(rs && st0 < Cr));
+        const bool cons = rs && st0 < Cr;
+        const unsigned long long cm = __ballot(cons);
+        const uint32_t r = nmk + nrc + (uint32_t)__popcll(cm & lanemask_lt());
+        if (cons && r < LV_STAGE) {
+          mkl[r].seq = a_seq_of(src, E.j);
+          mkl[r].end = T0 + en;
+        }
+        nrc += (uint32_t)__popcll(cm);
         ks += (uint32_t)__popcll(__ballot(rs && en > Cr));
         RR += (unsigned long long)rli64(inc, 63);
       }
     }
-    const uint32_t te0 = newhead != NIL ? auniu((uint32_t)bk.tend[li]) : 0u;  // the tail survives iff newhead does
+    const uint32_t te0 = newhead != NIL ? auniu(te_raw) : 0u;  // the tail survives iff newhead does
     const uint32_t tailfree = newhead != NIL ? (uint32_t)ME_C - te0 : 0u;
     const uint32_t need = ks > tailfree ? (ks - tailfree + ME_C - 1) / ME_C : 0u;
     const uint32_t own = min(need, nfreed), deficit = need - own;
@@ -813,7 +1114,7 @@ __global__ __launch_bounds__(256) void k_agg_levels(BookDev bk, AggSrc src, AggD
     d_off = rl32(d_off, 0);
     if (mk_base + nmkt > ag.mk_cap || fr_base + nfreed > ag.fr_cap) {
       a_set_err(bk, ERR_SCRATCH_OOM);  // sized so this cannot happen; leaves the level alone
-      for (uint32_t b = lane; b < cnt; b += 64) ag.evn[ag.evs[start + b]] = 0u;
+      for (uint32_t b = lane; b < cnt; b += 64) ag.evn[ag.evq[start + b].pad] = 0u;
       if (lane == 0) {
         AggSegS o{};
         o.T0 = ~0ull;
@@ -822,8 +1123,13 @@ __global__ __launch_bounds__(256) void k_agg_levels(BookDev bk, AggSrc src, AggD
       }
       continue;
     }
-    // 3. write pass over the initial FIFO
-    {
+    const bool staged = nmkt <= LV_STAGE && nfreed <= LV_STAGE;
+    // 4. makers and emptied chunks to HBM: from LDS, or past LV_STAGE by a second read of the FIFO
+    wave_mem_order();
+    if (staged) {
+      if ((uint32_t)lane < nmkt) ag.mk[mk_base + lane] = mkl[lane];
+      if ((uint32_t)lane < nfreed) ag.fr[fr_base + lane] = frl[lane];
+    } else {
       unsigned long long Wv = 0;
       uint32_t mi = 0, fi = 0;
       ch = head0;
@@ -843,25 +1149,17 @@ __global__ __launch_bounds__(256) void k_agg_levels(BookDev bk, AggSrc src, AggD
           ag.mk[mk_base + mi + (uint32_t)__popcll(cm & lanemask_lt())] = m;
         }
         mi += (uint32_t)__popcll(cm);
-        if (Wv + live <= C) {  // emptied: zero it (free chunks hold qty 0) and list it
-          if (act) bk.chunks[ch].qty[lane] = 0;
-          if (lane == 0) ag.fr[fr_base + fi] = ch;
-          ++fi;
-          Wv += live;
-          ch = nx;
-          continue;
-        }
-        if (cons) bk.chunks[ch].qty[lane] = en <= C ? 0 : (int)(en - C);
-        break;
+        if (Wv + live > C) break;
+        if (lane == 0) ag.fr[fr_base + fi] = ch;
+        ++fi;
+        Wv += live;
+        ch = nx;
       }
-      // makers from this batch's rests
       if (Cr) {
         unsigned long long RR = 0;
         for (uint32_t b = 0; b < cnt; b += 64) {
+          const AggEv E = entry(b);
           const bool v = b + (uint32_t)lane < cnt;
-          const uint32_t e = v ? ag.evs[start + b + lane] : 0u;
-          AggEv E{};
-          if (v) E = ag.ev[e];
           const bool rs = v && (E.j & AGG_TAKE) == 0u;
           const long long rq = rs ? (long long)E.qty : 0ll;
           const long long inc = wave_incl_scan(rq);
@@ -879,20 +1177,37 @@ __global__ __launch_bounds__(256) void k_agg_levels(BookDev bk, AggSrc src, AggD
         }
       }
     }
-    a_drain();
-    // 4. each take: its first maker and its fill count (makers overlapping its interval)
-    for (uint32_t b = 0; b < cnt; b += 64) {
-      const bool v = b + (uint32_t)lane < cnt;
-      const uint32_t e = v ? ag.evs[start + b + lane] : 0u;
-      AggEv E{};
-      if (v) E = ag.ev[e];
-      const bool tk = v && (E.j & AGG_TAKE) != 0u;
-      if (tk) {
-        const unsigned long long a = ag.eva[e], z = a + (unsigned long long)E.qty;
-        const uint32_t first = a_search(ag.mk, mk_base, nmkt, a, true);
-        const uint32_t last = a_search(ag.mk, mk_base, nmkt, z, false);
-        ag.evf[e] = mk_base + first;
-        ag.evn[e] = last - first + 1u;
+    // 5. the FIFO's new state: emptied chunks hold qty 0 (free chunks do), the chunk C ends in keeps
+    //    what is left of its makers
+    wave_mem_order();
+    for (uint32_t f0 = 0; f0 < nfreed; f0 += 4) {
+      const uint32_t f = f0 + (uint32_t)lane / ME_C;
+      if (f < nfreed) {
+        const uint32_t c = staged ? frl[f] : ag.fr[fr_base + f];
+        if (c < bk.nchunks) bk.chunks[c].qty[lane % ME_C] = 0;
+      }
+    }
+    if (pch != NIL && act && pq > 0 && pen - (unsigned long long)pq < C)
+      bk.chunks[pch].qty[lane] = pen <= C ? 0 : (int)(pen - C);
+    // 6. each take: its first maker and its fill count (makers overlapping its interval)
+    wave_mem_order();
+    {
+      unsigned long long A0 = 0;
+      for (uint32_t b = 0; b < cnt; b += 64) {
+        const AggEv E = entry(b);
+        const bool v = b + (uint32_t)lane < cnt;
+        const bool tk = v && (E.j & AGG_TAKE) != 0u;
+        const long long tq = tk ? (long long)E.qty : 0ll;
+        const long long inc = wave_incl_scan(tq);
+        if (tk) {
+          const unsigned long long a = A0 + (unsigned long long)(inc - tq), z = a + (unsigned long long)E.qty;
+          const uint32_t first = staged ? a_search_lds(mkl, nmkt, a, true) : a_search(ag.mk, mk_base, nmkt, a, true);
+          const uint32_t last = staged ? a_search_lds(mkl, nmkt, z, false) : a_search(ag.mk, mk_base, nmkt, z, false);
+          ag.eva[E.pad] = a;
+          ag.evf[E.pad] = mk_base + first;
+          ag.evn[E.pad] = last - first + 1u;
+        }
+        A0 += (unsigned long long)rli64(inc, 63);
       }
     }
     if (lane == 0) {
@@ -909,7 +1224,7 @@ __global__ __launch_bounds__(256) void k_agg_levels(BookDev bk, AggSrc src, AggD
       o.ks = ks;
       ag.segs[si] = o;
     }
-    (void)nrest;
+    wave_mem_order();  // the next segment reuses the staging
   }
 }
 
@@ -1032,9 +1347,8 @@ __global__ __launch_bounds__(256) void k_agg_place(BookDev bk, AggSrc src, AggDe
       uint32_t g0 = 0;
       for (uint32_t b = 0; b < cnt; b += 64) {
         const bool v = b + (uint32_t)lane < cnt;
-        const uint32_t e = v ? ag.evs[start + b + lane] : 0u;
         AggEv E{};
-        if (v) E = ag.ev[e];
+        if (v) E = ag.evq[start + b + lane];
         const bool rs = v && (E.j & AGG_TAKE) == 0u;
         const long long rq = rs ? (long long)E.qty : 0ll;
         const long long inc = wave_incl_scan(rq);
@@ -1135,25 +1449,18 @@ __global__ __launch_bounds__(1024) void k_agg_fin(BookDev bk, BatchDev bt, AggDe
     __syncthreads();
     const uint32_t ftot = carry_s;
     __threadfence_block();
-    for (uint32_t j = sl.lo + (uint32_t)tid; j < sl.pos; j += 1024) {
-      const AggRec rc = ag.rec[j];
-      uint32_t nfill = 0, fo = 0;
-      if (rc.ev_n) {
-        const uint32_t la = rc.ev_lo + rc.ev_n - 1u;
-        fo = ag.evx[rc.ev_lo];
-        nfill = ag.evx[la] + ag.evn[la] - fo;
-      }
-      const uint32_t oi = bt.perm[j];
-      me_order_result o;
-      o.filled_qty = rc.filled;
-      o.remaining_qty = rc.rem;
-      o.fill_count = nfill;
-      o.tape_offset = 0;
-      o.status = (uint8_t)(rc.st & 0xFF);
-      o.reason = (uint8_t)(rc.st >> 8);
-      o.pad[0] = o.pad[1] = 0;
-      bt.res[oi] = o;
-      bt.fstart[oi] = (uint32_t)(sl.wbase + fo);
+    auto EX = [&](uint32_t e) -> uint32_t { return e < eb + n ? ag.evx[e] : ftot; };
+    // the first take of each record (the walk wrote its result with no fills): fill count, scratch start
+    for (uint32_t t = (uint32_t)tid; t < n; t += 1024) {
+      const uint32_t e = eb + t;
+      const uint32_t j = ag.ev[e].j;
+      if (!(j & AGG_TAKE) || (t > 0 && ag.ev[e - 1].j == j)) continue;
+      uint32_t nte = 1;  // the record's take events follow each other in the log
+      while (t + nte < n && ag.ev[e + nte].j == j) ++nte;
+      const uint32_t x0 = EX(e), nfill = EX(e + nte) - x0;
+      const uint32_t oi = bt.perm[j & ~AGG_TAKE];
+      bt.res[oi].fill_count = nfill;
+      bt.fstart[oi] = (uint32_t)(sl.wbase + x0);
       if (nfill) atomicAdd(&bt.tile_sum[oi / TILE_TAPE], nfill);
     }
     if (tid == 0) {
@@ -1281,6 +1588,7 @@ __device__ __forceinline__ uint32_t a_ghand(const BookDev& bk, uint32_t s, uint3
 __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDev ag) {
   __shared__ unsigned long long locc[2];
   __shared__ AStage stg;
+  __shared__ long long ltot[256 + 64];
   const int lane = lane_id();
   const int L = (int)bk.L;  // <= 128
   const uint32_t ng = ga.ng;
@@ -1325,9 +1633,8 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
     }
     AWalk w;
     a_walk_init(w, bk, ag, s, eb, locc);
-    AList A, B;
-    a_rebuild<1>(w, A, ba0);
-    a_rebuild<0>(w, B, L - 1 - bb0);
+    LWalk<2> lw;
+    lw_init(lw, bk, s, ltot, bb0, ba0);
     uint32_t hidx = NIL, gstop = ng;
     // a batch's bucket is loaded while the batch before it runs (no HBM round trip between batches)
     const size_t bko = (size_t)s * BK_CAP;
@@ -1376,21 +1683,9 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
         uint32_t rj;
         int olm;
         const unsigned long long fastm = __ballot(a_classify(v, oseq, opx, oq, okd, base, L, nfar0, nfar1, rj, olm));
-        a_refill(w, A, B);
-        ARes R;
-        const uint32_t k = a_block(w, A, B, oq, okd, olm, rj, (g << AGG_GSHIFT) | oi, fastm, cntb, R);
-        if (v && (uint32_t)lane < k) {
-          // fill_count = the record's take events and tape_offset = its first one, until k_agg_gfin
-          me_order_result o;
-          o.filled_qty = R.rf;
-          o.remaining_qty = R.rr;
-          o.fill_count = R.rn;
-          o.tape_offset = R.rlo;
-          o.status = (uint8_t)(R.rs & 0xFF);
-          o.reason = (uint8_t)(R.rs >> 8);
-          o.pad[0] = o.pad[1] = 0;
-          res[oi] = o;
-        }
+        int rr = 0;
+        const uint32_t k = lw_block(w, lw, oq, lw_cw(okd, olm, rj, L), (g << AGG_GSHIFT) | oi, fastm, cntb, rr);
+        if (v && (uint32_t)lane < k) res[oi] = a_result(oq, okd, rj, rr);  // fills: k_agg_gfin
         if (k < cntb) {
           hidx = a_ghand(bk, s, g, blk + k, cnt, 0u, 0u);  // scratch position: k_agg_gfin
           stop = true;
@@ -1406,8 +1701,9 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
     for (uint32_t g = (gstop < ng ? gstop + 1u : ng) + (uint32_t)lane; g <= ng; g += 64)
       *a_gtab(ag.gev, s, g) = w.evp;
     if (gstop < ng && lane == 0) *a_gtab(ag.gev, s, gstop + 1u) = w.evp;
-    int bb, ba;
-    a_walk_end(w, A, B, bb, ba);
+    if (w.evp & 63u) a_evstore(w, w.evp & ~63u, w.evp & 63u);
+    lw_end(lw, bk, s);
+    const int bb = lw.bb, ba = lw.ba;
     if (lane == 0) {
       slot->ev_cnt = w.evp - eb;
       slot->bb = bb;
@@ -1490,7 +1786,8 @@ __global__ __launch_bounds__(1024) void k_agg_gfin(BookDev bk, AggGArgs ga, AggD
       if (!(j & AGG_TAKE) || (t > 0 && ag.ev[e - 1].j == j)) continue;
       const uint32_t g = (j & ~AGG_TAKE) >> AGG_GSHIFT, oi = j & AGG_IMASK;
       me_order_result* res = ga.res[g];
-      const uint32_t nte = res[oi].fill_count;
+      uint32_t nte = 1;  // the record's take events follow each other in the log
+      while (t + nte < n && ag.ev[e + nte].j == j) ++nte;
       const uint32_t x0 = EX(e), nfill = EX(e + nte) - x0;
       res[oi].fill_count = nfill;
       res[oi].tape_offset = *a_gtab(ag.gbase, s, g) + (x0 - *a_gtab(ag.gex, s, g));

@@ -334,7 +334,7 @@ static void free_all(me_engine* e) {
   }
   {
     const AggDev& a = e->hot.ag;
-    void* ap[] = {a.slot, a.ev, a.evs, a.eva, a.evf, a.evn, a.evx, a.seg, a.segs, a.mk, a.fr, a.rec, a.ctr,
+    void* ap[] = {a.slot, a.ev, a.evs, a.evq, a.eva, a.evf, a.evn, a.evx, a.seg, a.segs, a.mk, a.fr, a.rec, a.ctr,
                   a.gev, a.gex, a.gbase};
     for (void* p : ap)
       if (p) (void)hipFree(p);
@@ -564,6 +564,7 @@ extern "C" me_engine* me_create(const me_config* cfg) {
     ALLOC(a.slot, S);
     ALLOC(a.ev, evc);
     ALLOC(a.evs, evc);
+    ALLOC(a.evq, evc);
     ALLOC(a.eva, evc);
     ALLOC(a.evf, evc);
     ALLOC(a.evn, evc);

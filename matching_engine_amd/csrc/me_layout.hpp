@@ -212,6 +212,7 @@ struct AggDev {
   AggSlot* slot;               // [S]
   AggEv* ev;                   // [ev_cap] event log (per-slot regions)
   uint32_t* evs;               // [ev_cap] log indices grouped by level (stable)
+  AggEv* evq;                  // [ev_cap] the entries in that order (pad: the log index)
   unsigned long long* eva;     // [ev_cap] take: start of its interval in the level's maker space
   uint32_t* evf;               // [ev_cap] take: its first maker (AggDev::mk index)
   uint32_t* evn;               // [ev_cap] fills of the event (0 for rests)
