@@ -449,53 +449,37 @@ constexpr uint32_t LW_BUY = 1u << 9, LW_MKT = 1u << 10, LW_RJ_SHIFT = 11;
 
 template <int NW>
 struct LWalk {
-  long long* tot;    // LDS [L]
+  long long* tot;    // LDS [L] (empty levels hold 0)
   long long* dummy;  // LDS [64]: the other lanes' targets of a one-lane LDS operation
-  unsigned long long o[NW];
   int bb, ba;        // best bid (-1: none), best ask (L: none)
   long long tbb, tba;
   int L;
 };
 
-template <int NW>
-__device__ __forceinline__ void lw_set(LWalk<NW>& w, int l) {
-  const int wi = l >> 6;
-  const unsigned long long b = 1ull << (l & 63);
-#pragma unroll
-  for (int i = 0; i < NW; ++i) w.o[i] |= i == wi ? b : 0ull;
-}
-template <int NW>
-__device__ __forceinline__ void lw_clr(LWalk<NW>& w, int l) {
-  const int wi = l >> 6;
-  const unsigned long long b = 1ull << (l & 63);
-#pragma unroll
-  for (int i = 0; i < NW; ++i) w.o[i] &= i == wi ? ~b : ~0ull;
-}
-// smallest occupied level >= x, or L
+// smallest occupied level >= x, or L: a scan of the LDS totals. Only levels on the side being searched
+// lie there (the other side's cached best, whose LDS copy is stale, is on the other side of x).
 template <int NW>
 __device__ __forceinline__ int lw_next(const LWalk<NW>& w, int x) {
-  int r = w.L;
-#pragma unroll
-  for (int i = NW - 1; i >= 0; --i) {
-    const int b0 = i * 64;
-    unsigned long long m = w.o[i];
-    m = x <= b0 ? m : (x >= b0 + 64 ? 0ull : m & (~0ull << (x - b0)));
-    r = m ? b0 + __builtin_ctzll(m) : r;
+  const int lane = lane_id();
+  for (int b = x & ~63; b < w.L; b += 64) {
+    const int l = b + lane;
+    const long long t = l < w.L ? w.tot[l] : 0ll;
+    const unsigned long long m = __ballot(l >= x && t > 0);
+    if (m) return b + __builtin_ctzll(m);
   }
-  return r;
+  return w.L;
 }
 // largest occupied level <= x, or -1
 template <int NW>
 __device__ __forceinline__ int lw_prev(const LWalk<NW>& w, int x) {
-  int r = -1;
-#pragma unroll
-  for (int i = 0; i < NW; ++i) {
-    const int b0 = i * 64;
-    unsigned long long m = w.o[i];
-    m = x >= b0 + 63 ? m : (x < b0 ? 0ull : m & (~0ull >> (63 - (x - b0))));
-    r = m ? b0 + 63 - __builtin_clzll(m) : r;
+  const int lane = lane_id();
+  for (int b = x & ~63; b >= 0; b -= 64) {
+    const int l = b + lane;
+    const long long t = w.tot[l];
+    const unsigned long long m = __ballot(l <= x && t > 0);
+    if (m) return b + 63 - __builtin_clzll(m);
   }
-  return r;
+  return -1;
 }
 // one-lane LDS writes: lane 0 on the level, every other lane on its own dummy slot (no exec change)
 template <int NW>
@@ -527,7 +511,6 @@ __device__ __forceinline__ void lw_take_buy(AWalk& e, LWalk<NW>& w, int lim, uin
     a_emit(e, w.ba, jt, (int)w.tba);
     rem -= (uint32_t)w.tba;
     lw_put(w, w.ba, 0ll);  // empty levels hold 0 (a rest there adds)
-    lw_clr(w, w.ba);
     w.ba = lw_next(w, w.ba + 1);
     w.tba = w.ba < w.L ? lw_get(w, w.ba) : 0ll;
   }
@@ -544,7 +527,6 @@ __device__ __forceinline__ void lw_take_sell(AWalk& e, LWalk<NW>& w, int lim, ui
     a_emit(e, w.bb, jt, (int)w.tbb);
     rem -= (uint32_t)w.tbb;
     lw_put(w, w.bb, 0ll);
-    lw_clr(w, w.bb);
     w.bb = lw_prev(w, w.bb - 1);
     w.tbb = w.bb >= 0 ? lw_get(w, w.bb) : 0ll;
   }
@@ -556,12 +538,10 @@ __device__ __forceinline__ void lw_rest_buy(AWalk& e, LWalk<NW>& w, int l, int q
     w.tbb += q;
   } else if (l > w.bb) {  // a new best bid (an empty level)
     if (w.bb >= 0) lw_put(w, w.bb, w.tbb);
-    lw_set(w, l);
     w.bb = l;
     w.tbb = q;
   } else {
     lw_add(w, l, q);
-    lw_set(w, l);
   }
   a_emit(e, l, jt, q);
 }
@@ -571,12 +551,10 @@ __device__ __forceinline__ void lw_rest_sell(AWalk& e, LWalk<NW>& w, int l, int 
     w.tba += q;
   } else if (l < w.ba) {
     if (w.ba < w.L) lw_put(w, w.ba, w.tba);
-    lw_set(w, l);
     w.ba = l;
     w.tba = q;
   } else {
     lw_add(w, l, q);
-    lw_set(w, l);
   }
   a_emit(e, l, jt, q);
 }
@@ -592,9 +570,7 @@ __device__ __forceinline__ void lw_init(LWalk<NW>& w, const BookDev& bk, uint32_
 #pragma unroll
   for (int i = 0; i < NW; ++i) {
     const int l = i * 64 + lane;
-    const long long t = l < w.L ? lv[l].total : 0ll;
-    w.tot[l] = t;
-    w.o[i] = __ballot(t > 0);
+    w.tot[l] = l < w.L ? lv[l].total : 0ll;
   }
   wave_mem_order();
   w.bb = bb;
@@ -614,8 +590,10 @@ __device__ __forceinline__ void lw_end(LWalk<NW>& w, const BookDev& bk, uint32_t
 #pragma unroll
   for (int i = 0; i < NW; ++i) {
     const int l = i * 64 + lane;
-    if (l < w.L) lv[l].total = w.tot[l];
-    if (lane == 0 && i < (int)bk.Lwords) oc[i] = w.o[i];
+    const long long t = l < w.L ? w.tot[l] : 0ll;
+    if (l < w.L) lv[l].total = t;
+    const unsigned long long m = __ballot(t > 0);
+    if (lane == 0 && i < (int)bk.Lwords) oc[i] = m;
   }
 }
 
