@@ -608,14 +608,19 @@ __device__ __forceinline__ uint32_t lw_cw(uint32_t okd, int olm, uint32_t rj, in
 template <int NW>
 __device__ __forceinline__ uint32_t lw_block(AWalk& e, LWalk<NW>& w, int oq, uint32_t ocw, uint32_t ojt,
                                              unsigned long long fastm, uint32_t cnt, int& rr) {
-  uint32_t k = 0;
-  for (; k < cnt; ++k) {
-    if (ME_UNLIKELY(!((fastm >> k) & 1ull))) break;
-    const uint32_t cw = rl32(ocw, (int)k);
-    if (ME_UNLIKELY(cw >> LW_RJ_SHIFT)) continue;  // rejected: its result comes from the reason
-    const uint32_t jt = rl32(ojt, (int)k);
+  // the records the walk covers run up to the first it does not (k); rejected ones need no chain work:
+  // the loop visits the set bits of `work` (a scalar bit scan, no per-record tests)
+  const unsigned long long upto = (cnt >= 64u ? ~0ull : ((1ull << cnt) - 1ull)) & ~fastm;
+  const uint32_t k = upto ? (uint32_t)__builtin_ctzll(upto) : cnt;
+  const unsigned long long rjm = __ballot((ocw >> LW_RJ_SHIFT) != 0u);
+  unsigned long long work = (k >= 64u ? ~0ull : ((1ull << k) - 1ull)) & ~rjm;
+  while (work) {
+    const int r = __builtin_ctzll(work);
+    work &= work - 1ull;
+    const uint32_t cw = rl32(ocw, r);
+    const uint32_t jt = rl32(ojt, r);
     const int lim = (int)(cw & 0x1FFu);
-    uint32_t rem = (uint32_t)rli32(oq, (int)k);
+    uint32_t rem = (uint32_t)rli32(oq, r);
     if (cw & LW_BUY) {
       lw_take_buy(e, w, lim, rem, jt | AGG_TAKE);
       if (!(cw & LW_MKT) && rem) lw_rest_buy(e, w, lim, (int)rem, jt);
@@ -623,7 +628,7 @@ __device__ __forceinline__ uint32_t lw_block(AWalk& e, LWalk<NW>& w, int oq, uin
       lw_take_sell(e, w, lim, rem, jt | AGG_TAKE);
       if (!(cw & LW_MKT) && rem) lw_rest_sell(e, w, lim, (int)rem, jt);
     }
-    rr = lane_id() == (int)k ? (int)rem : rr;
+    rr = lane_id() == r ? (int)rem : rr;
   }
   return k;
 }
