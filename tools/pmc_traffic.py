@@ -28,7 +28,7 @@ def per_dispatch(d, counter, kernel, merge_next=None):
         for r in csv.DictReader(open(f)):
             name = r.get("Kernel_Name") or r.get("Kernel-Name") or ""
             cn = r.get("Counter_Name") or r.get("Counter-Name") or ""
-            if kernel in name and cn == counter:
+            if re.search(kernel, name) and cn == counter:
                 did = int(r.get("Dispatch_Id") or r.get("Dispatch-Id") or len(acc))
                 cont = "<true>" in name
                 v = float(r.get("Counter_Value") or r.get("Counter-Value"))
