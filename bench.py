@@ -523,6 +523,7 @@ def main():
             f2 += len(f)
         e2e = n2 / (time.perf_counter() - t2)
     max_resting = eng.config()["max_resting"]
+    paths = eng.paths()
     for db in dbs:
         db.free()
     eng.close()
@@ -570,7 +571,10 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": "k_match_reg" if sc.levels <= 128 else "k_match",
+                # the timed launch: k_match_reg, or with grouped_agg the group's aggregate-path kernels
+                # (k_side, k_agg_gwalk ... k_agg_gemit, the continuation) between the same two events
+                "kernel": ("k_agg group" if paths["grouped_agg"] else "k_match_reg") if sc.levels <= 128 else "k_match",
+                "paths": paths,
                 "algorithmic_bytes_per_launch": bytes_per_launch,
                 "algorithmic_bytes_per_order": bytes_per_order,
                 "traffic_bytes_per_order": traffic_per_order,

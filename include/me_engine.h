@@ -284,6 +284,13 @@ int me_timing_read(me_engine* e, double* match_ms, double* pipeline_ms, uint64_t
  * continuation launch (a far price level, a re-centre, a cancel of a far or very old order). */
 int me_stats_read(me_engine* e, uint64_t* handoffs);
 
+/* The matching paths the engine runs now (no reference counterpart: the reference has one CPU path).
+ * *flags bit 0 (ME_PATH_GROUPED_AGG): launch groups of windows <= 128 levels go through the aggregate
+ * path (k_agg_gwalk); bit 1 (ME_PATH_HOT_AGG): hot symbols of deeper windows do. */
+#define ME_PATH_GROUPED_AGG 1u
+#define ME_PATH_HOT_AGG 2u
+int me_paths_read(const me_engine* e, uint32_t* flags);
+
 /* Admission control state (any pointer may be NULL): resting = resting orders of every symbol after
  * all enqueued work (waits for it); bound = the host's current upper bound (resting orders once every
  * accepted record is matched); exact_counts = times a submit had to take an exact count (flush + sync)

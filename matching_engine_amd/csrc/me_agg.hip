@@ -36,6 +36,9 @@ namespace me {
 namespace {
 
 constexpr uint32_t AGG_WORDS = AGG_MAX_L / 64;
+// M0 is set only by this file's v_writelane sequences (no LDS-direct, GWS or interpolation use here)
+#pragma clang diagnostic ignored "-Winline-asm"
+
 constexpr uint32_t AGG_GCHUNK = 8192;  // log keys k_agg_group stages in LDS per scatter chunk (16 KB)
 constexpr int AGG_VMCNT0 = 0x0F70;     // s_waitcnt immediate: vmcnt(0) only (gfx9 encoding)
 
@@ -92,28 +95,30 @@ struct AWalk {
   int L, W;
   // the log's current 64-event block, event i in lane i: stored by the whole wave when it fills (one
   // coalesced 1-KB store instead of a lane-0 store per event)
-  uint32_t q_lvl, q_j;
-  int q_q;
+  AggEv* stg;  // LDS [128]: the block's events by log index mod 64, then the other lanes' dummy slots
 };
 
 __device__ __forceinline__ int a_side_lvl(int L, int k, int m) { return k ? m : L - 1 - m; }
 
 // Lanes [0, n) of the staged block to log indices [base, base + n).
 __device__ __forceinline__ void a_evstore(AWalk& w, uint32_t base, uint32_t n) {
-  if ((uint32_t)lane_id() < n) {
-    AggEv e;
-    e.lvl = w.q_lvl;
-    e.j = w.q_j;
-    e.qty = w.q_q;
-    e.pad = 0;
-    w.ev[base + (uint32_t)lane_id()] = e;
-  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (a wave's LDS operations complete in order)
+  const AggEv e = w.stg[lane_id()];
+  if ((uint32_t)lane_id() < n) w.ev[base + (uint32_t)lane_id()] = e;
 }
+// The event into the LDS block (one 16-B write by lane 0; the other lanes write their dummy slots, so no
+// exec change), one coalesced 1-KB store per 64 events. Nothing loop-carried in VGPRs: staging in
+// registers (a select or v_writelane per field) made the compiler copy the staging registers at every
+// join of the record loop.
 __device__ __forceinline__ void a_emit(AWalk& w, int lvl, uint32_t jt, int q) {
-  const bool me = lane_id() == (int)(w.evp & 63u);
-  w.q_lvl = me ? (uint32_t)lvl : w.q_lvl;
-  w.q_j = me ? jt : w.q_j;
-  w.q_q = me ? q : w.q_q;
+  const int lane = lane_id();
+  AggEv e;
+  e.lvl = (uint32_t)lvl;
+  e.j = jt;
+  e.qty = q;
+  e.pad = 0;
+  AggEv* p = lane == 0 ? &w.stg[w.evp & 63u] : &w.stg[64 + lane];
+  *p = e;
   w.evp += 1;
   if (ME_UNLIKELY((w.evp & 63u) == 0u)) a_evstore(w, w.evp - 64u, 64u);
 }
@@ -416,14 +421,13 @@ __device__ __forceinline__ uint32_t a_block(AWalk& w, AList& A, AList& B, int oq
 }
 
 __device__ __forceinline__ void a_walk_init(AWalk& w, const BookDev& bk, const AggDev& ag, uint32_t s, uint32_t eb,
-                                            unsigned long long* locc) {
+                                            unsigned long long* locc, AggEv* stg) {
   w.lv = (gptr<Level>)vptr(bk.levels + (size_t)s * bk.L);
   w.occ = (gptr<unsigned long long>)vptr(bk.occ + (size_t)s * bk.Lwords);
   w.ev = (gptr<AggEv>)vptr(ag.ev);
   w.locc = locc;
   w.evp = eb;
-  w.q_lvl = w.q_j = 0u;
-  w.q_q = 0;
+  w.stg = stg;
   w.L = (int)bk.L;
   w.W = (int)bk.Lwords;
   for (int k = lane_id(); k < w.W; k += 64) locc[k] = w.occ[k];
@@ -439,174 +443,206 @@ __device__ __forceinline__ void a_walk_end(AWalk& w, AList& A, AList& B, int& bb
   bb = B.n ? w.L - 1 - rli32(B.m, B.f) : -1;
 }
 
-// ------------------------------------------------------------------ the ladder walk (L <= 256)
-// Windows of at most 256 levels need no lists: the level totals live in LDS indexed by level, the
-// occupancy in up to four SGPR words, and the totals of the two best levels in SGPRs (their LDS copies
-// are stale while cached). A rest is an LDS add and a bit set (plus a swap of the cached best when it
-// becomes the best); a take compares with an SGPR and only when it empties a level finds the next bit
-// and reads one LDS total. No global memory operation on the chain but the log's 1-KB block stores.
-constexpr uint32_t LW_BUY = 1u << 9, LW_MKT = 1u << 10, LW_RJ_SHIFT = 11;
+// ------------------------------------------------------------------ the ladder walk
+// The level totals live in LDS as 32-bit words indexed by level (128 KB at L = 32,768) and the two best
+// levels' totals are cached in SGPRs (their LDS copies are stale while cached). A rest is an LDS add
+// (plus a swap of the cached best when it becomes the best); a take compares with an SGPR and only when
+// it empties a level scans the LDS totals for the next one. No global memory operation on the chain but
+// the log's 1-KB block stores.
+//
+// 32 bits: SALU has no ordered 64-bit compare (a 64-bit total is compared, and then kept, in VGPRs, with
+// copies at every join of the record loop). Exact while the symbol's whole book stays below 2^31: the
+// walk starts only if the book's sum is, and adds every block's quantities to that bound before the
+// block runs (a block that could cross it goes to the generic loop, from its first record on).
+constexpr uint32_t LW_BUY = 1u << 15, LW_MKT = 1u << 16, LW_RJ_SHIFT = 17, LW_LIM = 0x7FFFu;
+constexpr unsigned long long LW_CAP = 1ull << 31;
 
-template <int NW>
 struct LWalk {
-  long long* tot;    // LDS [L] (empty levels hold 0)
-  long long* dummy;  // LDS [64]: the other lanes' targets of a one-lane LDS operation
+  uint32_t* tot;     // LDS [L] (empty levels hold 0)
+  uint32_t* dummy;   // LDS [64]: the other lanes' targets of a one-lane LDS operation
   int bb, ba;        // best bid (-1: none), best ask (L: none)
-  long long tbb, tba;
+  uint32_t cbb, cba; // cached totals of the best levels
   int L;
+  unsigned long long ub;  // the book's sum plus the quantities of the blocks walked (< LW_CAP)
 };
 
 // smallest occupied level >= x, or L: a scan of the LDS totals. Only levels on the side being searched
 // lie there (the other side's cached best, whose LDS copy is stale, is on the other side of x).
-template <int NW>
-__device__ __forceinline__ int lw_next(const LWalk<NW>& w, int x) {
+__device__ __forceinline__ int lw_next(const LWalk& w, int x) {
   const int lane = lane_id();
   for (int b = x & ~63; b < w.L; b += 64) {
     const int l = b + lane;
-    const long long t = l < w.L ? w.tot[l] : 0ll;
-    const unsigned long long m = __ballot(l >= x && t > 0);
+    const uint32_t t = w.tot[l];  // (l < L + 64: beyond L, the dummy slots)
+    const unsigned long long m = __ballot(l >= x && l < w.L && t != 0u);
     if (m) return b + __builtin_ctzll(m);
   }
   return w.L;
 }
 // largest occupied level <= x, or -1
-template <int NW>
-__device__ __forceinline__ int lw_prev(const LWalk<NW>& w, int x) {
+__device__ __forceinline__ int lw_prev(const LWalk& w, int x) {
   const int lane = lane_id();
   for (int b = x & ~63; b >= 0; b -= 64) {
     const int l = b + lane;
-    const long long t = w.tot[l];
-    const unsigned long long m = __ballot(l <= x && t > 0);
+    const uint32_t t = w.tot[l];
+    const unsigned long long m = __ballot(l <= x && t != 0u);  // (x < L)
     if (m) return b + 63 - __builtin_clzll(m);
   }
   return -1;
 }
 // one-lane LDS writes: lane 0 on the level, every other lane on its own dummy slot (no exec change)
-template <int NW>
-__device__ __forceinline__ void lw_add(LWalk<NW>& w, int l, long long d) {
+__device__ __forceinline__ void lw_add(LWalk& w, int l, uint32_t d) {
   const int lane = lane_id();
-  long long* p = lane == 0 ? &w.tot[l] : &w.dummy[lane];
+  uint32_t* p = lane == 0 ? &w.tot[l] : &w.dummy[lane];
   __hip_atomic_fetch_add(p, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-template <int NW>
-__device__ __forceinline__ void lw_put(LWalk<NW>& w, int l, long long v) {
+__device__ __forceinline__ void lw_put(LWalk& w, int l, uint32_t v) {
   const int lane = lane_id();
-  long long* p = lane == 0 ? &w.tot[l] : &w.dummy[lane];
+  uint32_t* p = lane == 0 ? &w.tot[l] : &w.dummy[lane];
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-template <int NW>
-__device__ __forceinline__ long long lw_get(const LWalk<NW>& w, int l) {
-  return (long long)rl64((unsigned long long)__hip_atomic_load(&w.tot[l], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP), 0);
+__device__ __forceinline__ uint32_t lw_get(const LWalk& w, int l) {
+  return rl32(__hip_atomic_load(&w.tot[l], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP), 0);
 }
 
-template <int NW>
-__device__ __forceinline__ void lw_take_buy(AWalk& e, LWalk<NW>& w, int lim, uint32_t& rem, uint32_t jt) {
-  while (rem && w.ba <= lim) {
-    if ((long long)rem < w.tba) {
-      w.tba -= (long long)rem;
+// A taker's partial take from the best level is the common case and stays out of the loop (no loop
+// entry, so none of the loop's register copies); the loop runs only when the best level empties.
+__device__ __forceinline__ void lw_take_buy(AWalk& e, LWalk& w, int lim, uint32_t& rem, uint32_t jt) {
+  if (w.ba > lim) return;  // (rem > 0: rejected records never reach the chain)
+  if (ME_LIKELY(w.cba > rem)) {
+    w.cba -= rem;
+    a_emit(e, w.ba, jt, (int)rem);
+    rem = 0;
+    return;
+  }
+  while (true) {  // the best level empties
+    a_emit(e, w.ba, jt, (int)w.cba);
+    rem -= w.cba;
+    lw_put(w, w.ba, 0u);  // empty levels hold 0 (a rest there adds)
+    w.ba = lw_next(w, w.ba + 1);
+    w.cba = w.ba < w.L ? lw_get(w, w.ba) : 0u;
+    if (!rem || w.ba > lim) return;
+    if (w.cba > rem) {
+      w.cba -= rem;
       a_emit(e, w.ba, jt, (int)rem);
       rem = 0;
       return;
     }
-    a_emit(e, w.ba, jt, (int)w.tba);
-    rem -= (uint32_t)w.tba;
-    lw_put(w, w.ba, 0ll);  // empty levels hold 0 (a rest there adds)
-    w.ba = lw_next(w, w.ba + 1);
-    w.tba = w.ba < w.L ? lw_get(w, w.ba) : 0ll;
   }
 }
-template <int NW>
-__device__ __forceinline__ void lw_take_sell(AWalk& e, LWalk<NW>& w, int lim, uint32_t& rem, uint32_t jt) {
-  while (rem && w.bb >= lim) {
-    if ((long long)rem < w.tbb) {
-      w.tbb -= (long long)rem;
+__device__ __forceinline__ void lw_take_sell(AWalk& e, LWalk& w, int lim, uint32_t& rem, uint32_t jt) {
+  if (w.bb < lim) return;
+  if (ME_LIKELY(w.cbb > rem)) {
+    w.cbb -= rem;
+    a_emit(e, w.bb, jt, (int)rem);
+    rem = 0;
+    return;
+  }
+  while (true) {
+    a_emit(e, w.bb, jt, (int)w.cbb);
+    rem -= w.cbb;
+    lw_put(w, w.bb, 0u);
+    w.bb = lw_prev(w, w.bb - 1);
+    w.cbb = w.bb >= 0 ? lw_get(w, w.bb) : 0u;
+    if (!rem || w.bb < lim) return;
+    if (w.cbb > rem) {
+      w.cbb -= rem;
       a_emit(e, w.bb, jt, (int)rem);
       rem = 0;
       return;
     }
-    a_emit(e, w.bb, jt, (int)w.tbb);
-    rem -= (uint32_t)w.tbb;
-    lw_put(w, w.bb, 0ll);
-    w.bb = lw_prev(w, w.bb - 1);
-    w.tbb = w.bb >= 0 ? lw_get(w, w.bb) : 0ll;
   }
 }
 // a bid rests at l (< ba: every ask up to the limit was taken)
-template <int NW>
-__device__ __forceinline__ void lw_rest_buy(AWalk& e, LWalk<NW>& w, int l, int q, uint32_t jt) {
+__device__ __forceinline__ void lw_rest_buy(AWalk& e, LWalk& w, int l, uint32_t q, uint32_t jt) {
   if (l == w.bb) {
-    w.tbb += q;
+    w.cbb += q;
   } else if (l > w.bb) {  // a new best bid (an empty level)
-    if (w.bb >= 0) lw_put(w, w.bb, w.tbb);
+    if (w.bb >= 0) lw_put(w, w.bb, w.cbb);
     w.bb = l;
-    w.tbb = q;
+    w.cbb = q;
   } else {
     lw_add(w, l, q);
   }
-  a_emit(e, l, jt, q);
+  a_emit(e, l, jt, (int)q);
 }
-template <int NW>
-__device__ __forceinline__ void lw_rest_sell(AWalk& e, LWalk<NW>& w, int l, int q, uint32_t jt) {
+__device__ __forceinline__ void lw_rest_sell(AWalk& e, LWalk& w, int l, uint32_t q, uint32_t jt) {
   if (l == w.ba) {
-    w.tba += q;
+    w.cba += q;
   } else if (l < w.ba) {
-    if (w.ba < w.L) lw_put(w, w.ba, w.tba);
+    if (w.ba < w.L) lw_put(w, w.ba, w.cba);
     w.ba = l;
-    w.tba = q;
+    w.cba = q;
   } else {
     lw_add(w, l, q);
   }
-  a_emit(e, l, jt, q);
+  a_emit(e, l, jt, (int)q);
 }
 
-// The ladder from HBM: LDS totals, occupancy from them, the cached best totals.
-template <int NW>
-__device__ __forceinline__ void lw_init(LWalk<NW>& w, const BookDev& bk, uint32_t s, long long* lds, int bb, int ba) {
+// The ladder from HBM: 32-bit LDS totals, the cached best totals, the book's sum (false: LW_CAP or more,
+// the ladder cannot hold the book)
+__device__ __forceinline__ bool lw_init(LWalk& w, const BookDev& bk, uint32_t s, uint32_t* lds, int bb, int ba) {
   const int lane = lane_id();
   w.L = (int)bk.L;
   w.tot = lds;
-  w.dummy = lds + 256;
+  w.dummy = lds + w.L;
   const Level* lv = bk.levels + (size_t)s * bk.L;
+  unsigned long long sum = 0;
+  for (int b = 0; b < w.L; b += 16 * 64) {  // sixteen loads in flight per lane
+    long long t[16];
 #pragma unroll
-  for (int i = 0; i < NW; ++i) {
-    const int l = i * 64 + lane;
-    w.tot[l] = l < w.L ? lv[l].total : 0ll;
+    for (int u = 0; u < 16; ++u) {
+      const int l = b + u * 64 + lane;
+      t[u] = l < w.L ? lv[l].total : 0ll;
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int l = b + u * 64 + lane;
+      if (l < w.L) w.tot[l] = (uint32_t)t[u];
+      sum += (unsigned long long)t[u];
+    }
   }
+  for (int d = 1; d < 64; d <<= 1) sum += __shfl_xor(sum, d, 64);
+  w.ub = rl64(sum, 0);
   wave_mem_order();
   w.bb = bb;
   w.ba = ba;
-  w.tbb = bb >= 0 ? lw_get(w, bb) : 0ll;
-  w.tba = ba < w.L ? lw_get(w, ba) : 0ll;
+  w.cbb = bb >= 0 ? lw_get(w, bb) : 0u;
+  w.cba = ba < w.L ? lw_get(w, ba) : 0u;
+  return w.ub < LW_CAP;
 }
 // The ladder back to HBM (totals, occupancy); the cached totals first.
-template <int NW>
-__device__ __forceinline__ void lw_end(LWalk<NW>& w, const BookDev& bk, uint32_t s) {
+__device__ __forceinline__ void lw_end(LWalk& w, const BookDev& bk, uint32_t s) {
   const int lane = lane_id();
-  if (w.bb >= 0) lw_put(w, w.bb, w.tbb);
-  if (w.ba < w.L) lw_put(w, w.ba, w.tba);
+  if (w.bb >= 0) lw_put(w, w.bb, w.cbb);
+  if (w.ba < w.L) lw_put(w, w.ba, w.cba);
   wave_mem_order();
   Level* lv = bk.levels + (size_t)s * bk.L;
   unsigned long long* oc = bk.occ + (size_t)s * bk.Lwords;
-#pragma unroll
-  for (int i = 0; i < NW; ++i) {
-    const int l = i * 64 + lane;
-    const long long t = l < w.L ? w.tot[l] : 0ll;
-    if (l < w.L) lv[l].total = t;
-    const unsigned long long m = __ballot(t > 0);
-    if (lane == 0 && i < (int)bk.Lwords) oc[i] = m;
+  for (int b = 0; b < w.L; b += 64) {
+    const int l = b + lane;
+    const uint32_t t = l < w.L ? w.tot[l] : 0u;
+    if (l < w.L) lv[l].total = (long long)t;
+    const unsigned long long m = __ballot(t != 0u);
+    if (lane == 0 && (b >> 6) < (int)bk.Lwords) oc[b >> 6] = m;
   }
+}
+// The block's quantities onto the bound; false: the block could take the book to LW_CAP
+__device__ __forceinline__ bool lw_admit(LWalk& w, int oq) {
+  unsigned long long q = (unsigned long long)(uint32_t)max(oq, 0);
+  for (int d = 1; d < 64; d <<= 1) q += __shfl_xor(q, d, 64);
+  w.ub += rl64(q, 0);
+  return w.ub < LW_CAP;
 }
 
 // Control word of a record in vector form: the level a LIMIT rests at / the last level a taker may
 // trade at (MARKET: the far end of the window), side, type, reject reason.
 __device__ __forceinline__ uint32_t lw_cw(uint32_t okd, int olm, uint32_t rj, int L) {
   const bool buy = (okd & 3u) == ME_SIDE_BUY, mkt = (okd >> 2) & 1u;
-  const int lim = mkt ? (buy ? L - 1 : 0) : (olm & 0x1FF);
+  const int lim = mkt ? (buy ? L - 1 : 0) : (olm & (int)LW_LIM);
   return (uint32_t)lim | (buy ? LW_BUY : 0u) | (mkt ? LW_MKT : 0u) | (rj << LW_RJ_SHIFT);
 }
 
-template <int NW>
-__device__ __forceinline__ uint32_t lw_block(AWalk& e, LWalk<NW>& w, int oq, uint32_t ocw, uint32_t ojt,
+__device__ __forceinline__ uint32_t lw_block(AWalk& e, LWalk& w, int oq, uint32_t ocw, uint32_t ojt,
                                              unsigned long long fastm, uint32_t cnt, int& rr) {
   // the records the walk covers run up to the first it does not (k); rejected ones need no chain work:
   // the loop visits the set bits of `work` (a scalar bit scan, no per-record tests)
@@ -619,16 +655,16 @@ __device__ __forceinline__ uint32_t lw_block(AWalk& e, LWalk<NW>& w, int oq, uin
     work &= work - 1ull;
     const uint32_t cw = rl32(ocw, r);
     const uint32_t jt = rl32(ojt, r);
-    const int lim = (int)(cw & 0x1FFu);
+    const int lim = (int)(cw & LW_LIM);
     uint32_t rem = (uint32_t)rli32(oq, r);
     if (cw & LW_BUY) {
       lw_take_buy(e, w, lim, rem, jt | AGG_TAKE);
-      if (!(cw & LW_MKT) && rem) lw_rest_buy(e, w, lim, (int)rem, jt);
+      if (!(cw & LW_MKT) && rem) lw_rest_buy(e, w, lim, rem, jt);
     } else {
       lw_take_sell(e, w, lim, rem, jt | AGG_TAKE);
-      if (!(cw & LW_MKT) && rem) lw_rest_sell(e, w, lim, (int)rem, jt);
+      if (!(cw & LW_MKT) && rem) lw_rest_sell(e, w, lim, rem, jt);
     }
-    rr = lane_id() == r ? (int)rem : rr;
+    asm volatile("s_mov_b32 m0, %1\n\tv_writelane_b32 %0, %2, m0" : "+v"(rr) : "s"(r), "s"(auniu(rem)) : "m0");
   }
   return k;
 }
@@ -654,7 +690,7 @@ __device__ __forceinline__ me_order_result a_result(int oq, uint32_t okd, uint32
 }
 
 __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const AggDev& ag, uint32_t i, uint32_t s,
-                                uint32_t lo, uint32_t hi, unsigned long long* locc, long long* ltot) {
+                                uint32_t lo, uint32_t hi, unsigned long long* locc, uint32_t* ltot, AggEv* stg) {
   const int lane = lane_id();
   const int L = (int)bk.L;
   const SymState st = bk.sym[s];
@@ -714,14 +750,13 @@ __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const Agg
     return;
   }
   AWalk w;
-  a_walk_init(w, bk, ag, s, eb, locc);
-  // windows of at most 256 levels: the ladder walk; deeper ones: the top-of-book lists
-  const bool ladder = L <= 4 * 64;
+  a_walk_init(w, bk, ag, s, eb, locc, stg);
+  // the ladder walk; the top-of-book lists (64-bit totals) for a book the ladder cannot hold, or beyond
+  // ag.ladder_max levels
   AList A, B;  // asks (side 1), bids (side 0)
-  LWalk<4> lw;
-  if (ladder) {
-    lw_init(lw, bk, s, ltot, bb0, ba0);
-  } else {
+  LWalk lw;
+  const bool ladder = L <= (int)ag.ladder_max && lw_init(lw, bk, s, ltot, bb0, ba0);
+  if (!ladder) {
     a_rebuild<1>(w, A, ba0);
     a_rebuild<0>(w, B, L - 1 - bb0);
   }
@@ -759,7 +794,8 @@ __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const Agg
     int rr = 0;
     uint32_t k;
     if (ladder) {
-      k = lw_block(w, lw, oq, lw_cw(okd, olm, rj, L), j, fastm, cntb, rr);
+      const bool adm = lw_admit(lw, v ? oq : 0);  // else: the generic loop from this block on
+      k = lw_block(w, lw, oq, lw_cw(okd, olm, rj, L), j, adm ? fastm : 0ull, cntb, rr);
     } else {
       a_refill(w, A, B);
       ARes R;
@@ -806,11 +842,12 @@ __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const Agg
 
 __global__ __launch_bounds__(64) void k_agg_walk(BookDev bk, BatchDev bt, AggDev ag) {
   __shared__ unsigned long long locc[AGG_WORDS];
-  __shared__ long long ltot[256 + 64];  // the ladder walk's totals and dummy slots
+  __shared__ AggEv stg[128];
+  extern __shared__ uint32_t ltot[];  // the ladder walk's totals [L] and dummy slots [64]
   const uint32_t nh = min(*(volatile uint32_t*)bk.hcount, bk.S);
   for (uint32_t i = blockIdx.x; i < nh; i += gridDim.x) {
     const Handoff ho = bk.hand[i];
-    agg_walk_symbol(bk, bt, ag, i, auniu(ho.s), auniu(ho.pos), auniu(ho.nsg), locc, ltot);
+    agg_walk_symbol(bk, bt, ag, i, auniu(ho.s), auniu(ho.pos), auniu(ho.nsg), locc, ltot, stg);
   }
 }
 
@@ -1571,7 +1608,8 @@ __device__ __forceinline__ uint32_t a_ghand(const BookDev& bk, uint32_t s, uint3
 __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDev ag) {
   __shared__ unsigned long long locc[2];
   __shared__ AStage stg;
-  __shared__ long long ltot[256 + 64];
+  __shared__ uint32_t ltot[128 + 64];
+  __shared__ AggEv evstg[128];
   const int lane = lane_id();
   const int L = (int)bk.L;  // <= 128
   const uint32_t ng = ga.ng;
@@ -1615,9 +1653,9 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
       continue;
     }
     AWalk w;
-    a_walk_init(w, bk, ag, s, eb, locc);
-    LWalk<2> lw;
-    lw_init(lw, bk, s, ltot, bb0, ba0);
+    a_walk_init(w, bk, ag, s, eb, locc, evstg);
+    LWalk lw;
+    const bool lok = lw_init(lw, bk, s, ltot, bb0, ba0);  // else: the continuation from the first record
     uint32_t hidx = NIL, gstop = ng;
     // a batch's bucket is loaded while the batch before it runs (no HBM round trip between batches)
     const size_t bko = (size_t)s * BK_CAP;
@@ -1667,7 +1705,8 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
         int olm;
         const unsigned long long fastm = __ballot(a_classify(v, oseq, opx, oq, okd, base, L, nfar0, nfar1, rj, olm));
         int rr = 0;
-        const uint32_t k = lw_block(w, lw, oq, lw_cw(okd, olm, rj, L), (g << AGG_GSHIFT) | oi, fastm, cntb, rr);
+        const bool adm = lok && lw_admit(lw, v ? oq : 0);
+        const uint32_t k = lw_block(w, lw, oq, lw_cw(okd, olm, rj, L), (g << AGG_GSHIFT) | oi, adm ? fastm : 0ull, cntb, rr);
         if (v && (uint32_t)lane < k) res[oi] = a_result(oq, okd, rj, rr);  // fills: k_agg_gfin
         if (k < cntb) {
           hidx = a_ghand(bk, s, g, blk + k, cnt, 0u, 0u);  // scratch position: k_agg_gfin
@@ -1685,7 +1724,7 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
       *a_gtab(ag.gev, s, g) = w.evp;
     if (gstop < ng && lane == 0) *a_gtab(ag.gev, s, gstop + 1u) = w.evp;
     if (w.evp & 63u) a_evstore(w, w.evp & ~63u, w.evp & 63u);
-    lw_end(lw, bk, s);
+    if (lok) lw_end(lw, bk, s);  // (else the LDS copy is truncated and nothing was walked)
     const int bb = lw.bb, ba = lw.ba;
     if (lane == 0) {
       slot->ev_cnt = w.evp - eb;
@@ -1841,7 +1880,8 @@ hipError_t launch_agg(hipStream_t hs, const BookDev& bk, const BatchDev& bt, con
   AggSrc src{};
   src.perm = bt.perm;
   src.seq[0] = bt.seq;
-  hipLaunchKernelGGL(k_agg_walk, dim3(64), dim3(64), 0, hs, bk, bt, ag);
+  const size_t lwb = bk.L <= ag.ladder_max ? ((size_t)bk.L + 64u) * 4u : 0u;
+  hipLaunchKernelGGL(k_agg_walk, dim3(64), dim3(64), lwb, hs, bk, bt, ag);
   hipLaunchKernelGGL(k_agg_group, dim3(64), dim3(1024), (size_t)bk.L * 4u + AGG_GCHUNK * 2u, hs, bk, ag);
   hipLaunchKernelGGL(k_agg_levels, dim3(1024), dim3(256), 0, hs, bk, src, ag);
   hipLaunchKernelGGL(k_agg_alloc, dim3(64), dim3(64), 0, hs, bk, ag);

@@ -270,7 +270,13 @@ struct me_engine {
   // record accepted since (each rests at most once). k_seq_sweep publishes {k, resting} into pinned
   // memory ahead of every match launch; a synchronous exact count replaces it when it is too stale.
   static constexpr uint32_t ADM_RING = 256;
-  unsigned long long* pub_host = nullptr;  // hipHostMalloc'd, device-mapped (bk.pub)
+  unsigned long long* pub_host = nullptr;  // hipHostMalloc'd, device-mapped (bk.pub): [0] {launch, resting},
+                                           // [1] {launch, hand-offs}
+  // grouped launches through the aggregate path (hot.agg_reg) chosen by shape, not by ME_REG_AGG: turned
+  // off for good when symbols hand off to the continuation in more than 1/16 of their launches (cancels,
+  // far prices — config 5's stream), which then pays both paths
+  bool reg_agg_auto = false;
+  uint64_t ho_k = 0, ho_h = 0;  // the last {launch, hand-offs} sample
   uint32_t launch_no = 0;                  // match launches enqueued
   uint64_t adm_total = 0;                  // records accepted
   uint64_t adm_matched = 0;                // records of the batches those launches matched
@@ -511,8 +517,15 @@ extern "C" me_engine* me_create(const me_config* cfg) {
     e->hot.agg = L > 128 && L <= AGG_MAX_L && !(va && atoi(va) == 0);
     // L <= 128: every symbol of a launch group through the aggregate path (k_agg_gwalk) instead of
     // k_match_reg's serial loop — ME_REG_AGG=1 (measured per workload)
+    // (unset: on when a batch holds >= 32 records per symbol — config 2's shape, 64; config 3 has ~10 and
+    // runs faster on k_match_reg — and off for good once hand-offs show up, see reg_agg_auto)
     const char* vr = getenv("ME_REG_AGG");
-    e->hot.agg_reg = L <= 128 && vr && atoi(vr) != 0;
+    const uint64_t grp = cfg->batches_per_launch ? cfg->batches_per_launch : ME_DEFAULT_GROUP;
+    e->hot.agg_reg = L <= 128 && (vr ? atoi(vr) != 0
+                                     : (uint64_t)cfg->max_batch >= 32ull * S &&
+                                           (uint64_t)cfg->max_batch * grp <= (4ull << 20));  // (pools of a
+                                                                                             // group's records)
+    e->reg_agg_auto = e->hot.agg_reg && !vr;
     bk.hot_min = (e->hot.agg || L > LDS_MAX_LEVELS) ? (v ? (uint32_t)atoi(v) : 512u) : 0u;
     if (bk.hot_min) {
       if ((he = hipStreamCreateWithFlags(&e->hot.st, hipStreamNonBlocking)) != hipSuccess ||
@@ -559,6 +572,12 @@ extern "C" me_engine* me_create(const me_config* cfg) {
     const uint64_t frc = 2 * mkc + nrec + 64 * (S + 1);
     if (evc >= 0x7FFFFFFFull || frc >= 0xFFFFFFFFull) return bail("me_create: aggregate-path pools exceed 32-bit ids");
     a.ev_cap = (uint32_t)evc;
+    // k_agg_walk's two forms: the ladder walk (32-bit LDS totals indexed by level) up to ladder_max
+    // levels, the top-of-book lists beyond — config 4's 32,768-level books, whose takes empty a level
+    // every record or so, run faster on the lists (their next level is in a register, the ladder's is
+    // an LDS scan away). ME_AGG_LADDER overrides (up to AGG_MAX_L; 0: lists only).
+    const char* vl = getenv("ME_AGG_LADDER");
+    a.ladder_max = vl ? (uint32_t)atoi(vl) : 256u;
     a.mk_cap = (uint32_t)mkc;
     a.fr_cap = (uint32_t)frc;
     ALLOC(a.slot, S);
@@ -584,10 +603,10 @@ extern "C" me_engine* me_create(const me_config* cfg) {
       return bail(std::string("hipMemset agg ctr: ") + hipGetErrorString(he));
     bk.agg_ctr = a.ctr;
   }
-  if ((he = hipHostMalloc((void**)&e->pub_host, sizeof(unsigned long long), hipHostMallocDefault)) != hipSuccess ||
+  if ((he = hipHostMalloc((void**)&e->pub_host, 2 * sizeof(unsigned long long), hipHostMallocDefault)) != hipSuccess ||
       (he = hipHostGetDevicePointer((void**)&bk.pub, e->pub_host, 0)) != hipSuccess)
     return bail(std::string("me_create: pinned admission word: ") + hipGetErrorString(he));
-  *e->pub_host = 0ull;  // {0 launches, 0 resting}
+  e->pub_host[0] = e->pub_host[1] = 0ull;  // {0 launches, 0 resting / hand-offs}
   ALLOC(bk.chunk_top, 1);
   ALLOC(bk.err, 1);
   uint32_t* gsym = nullptr;
@@ -897,6 +916,15 @@ static int pipe_launch(me_engine* e, const me_engine::Group* nb) {
     if (rc) return rc;
     rc = timing_slot(e, orders, gm.n, tl, timed);
     if (rc) return rc;
+  }
+  if (e->reg_agg_auto && e->hot.agg_reg) {  // the hand-off rate since the last sample k_seq_sweep published
+    const unsigned long long p = *(volatile unsigned long long*)(e->pub_host + 1);
+    const uint64_t k = p >> 32, h = p & 0xFFFFFFFFull;
+    if (k > e->ho_k) {
+      if ((h - e->ho_h) * 16 > (k - e->ho_k) * (uint64_t)e->bk.S) e->hot.agg_reg = false;
+      e->ho_k = k;
+      e->ho_h = h;
+    }
   }
   hipError_t he = launch_match_reg(e->stream, e->bk, bt, gm.n, ax, tl.m0, tl.m1, &e->hot);
   if (he != hipSuccess) return e->hip_fail(he, "pipelined match launch");
@@ -1714,6 +1742,12 @@ extern "C" int me_stats_read(me_engine* e, uint64_t* handoffs) {
   unsigned long long v[ME_STATS];
   HIP_TRY(hipMemcpy(v, e->bk.stats, sizeof v, hipMemcpyDeviceToHost), "D2H stats");
   if (handoffs) *handoffs = v[ST_HANDOFFS];
+  return ME_OK;
+}
+
+extern "C" int me_paths_read(const me_engine* e, uint32_t* flags) {
+  if (!e || !flags) return ME_E_INVALID;
+  *flags = (e->hot.agg_reg ? ME_PATH_GROUPED_AGG : 0u) | (e->bk.hot_min && e->hot.agg ? ME_PATH_HOT_AGG : 0u);
   return ME_OK;
 }
 

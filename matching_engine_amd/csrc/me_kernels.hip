@@ -2361,6 +2361,9 @@ __global__ __launch_bounds__(256) void k_seq_sweep(BookDev bk, SeqGroup sg) {
     if (bk.pub) {  // resting orders after sg.launch match launches, for the host's admission bound
       const unsigned long long r = bk.stats[ST_RESTING];
       *bk.pub = ((unsigned long long)sg.launch << 32) | (r < 0xFFFFFFFFull ? r : 0xFFFFFFFFull);
+      // and the hand-offs so far (the engine's grouped-aggregate policy, me_engine.cpp)
+      const unsigned long long h = bk.stats[ST_HANDOFFS];
+      bk.pub[1] = ((unsigned long long)sg.launch << 32) | (h < 0xFFFFFFFFull ? h : 0xFFFFFFFFull);
     }
   }
   if (!need) return;

@@ -225,6 +225,7 @@ struct AggDev {
   uint32_t* ctr;               // [AC_N] pool tops (zeroed by k_seq_sweep)
   uint32_t ev_cap, mk_cap, fr_cap;
   uint32_t nslots;             // grouped launches: slot = symbol, nslots = S (0: k_hot_pick's hcount)
+  uint32_t ladder_max;         // k_agg_walk: windows up to this many levels take the ladder walk
   // grouped launches (register-window path, k_agg_gwalk): per symbol and batch of the group, [S][ME_GMAX + 1]
   uint32_t* gev;               // the symbol's first log index of batch g (g = ng: the log's end)
   uint32_t* gex;               // the fill offset (k_agg_fin's scan) at gev
@@ -271,7 +272,8 @@ struct BookDev {
   uint32_t* hcount;       // hand-offs of the current match launch (zeroed by k_seq_sweep)
   Handoff* hand;          // [S]
   unsigned long long* stats;  // [ME_STATS] event counters (me_stats_read)
-  unsigned long long* pub;    // host-mapped {launches << 32 | resting} (k_seq_sweep), or null
+  unsigned long long* pub;    // host-mapped [0] {launches << 32 | resting}, [1] {launches << 32 |
+                              // hand-offs} (k_seq_sweep), or null
   unsigned long long ring_mask;
   unsigned long long old_mask;
   uint32_t fcap;

@@ -316,6 +316,13 @@ class Engine:
         _check(self.lib, self.h, self.lib.me_stats_read(self.h, C.byref(h)))
         return {"handoffs": h.value}
 
+    def paths(self) -> dict:
+        """The matching paths running now (me_paths_read): grouped launches / hot symbols through the
+        aggregate path (me_agg.hip)."""
+        f = C.c_uint32(0)
+        _check(self.lib, self.h, self.lib.me_paths_read(self.h, C.byref(f)))
+        return {"grouped_agg": bool(f.value & 1), "hot_agg": bool(f.value & 2)}
+
     def admits(self, b: Batch) -> bool:
         """Would submit_batch(b) be admitted now (me_admission_check)? Nothing is enqueued."""
         n_rest = int(np.count_nonzero((b.kind & 0x0C) == 0))

@@ -108,6 +108,19 @@ def test_agg_groups_handoffs(me, orc):
         assert eng.stats()["handoffs"] > 0
 
 
+def test_agg_groups_large_quantities(me, orc):
+    """Quantities up to 2^25 at G = 8: books whose sum reaches 2^31 (the ladder's 32-bit limit) hand the
+    symbol's rest of the group to the continuation; every batch against the oracle."""
+    sc = me.preset(2, num_symbols=32, batch=4096, max_qty=1 << 25)
+    st = me.Stream(sc)
+    base = st.base_prices()
+    batches = [st.next(sc.batch) for _ in range(24)]
+    ob = orc.OracleBook(sc.num_symbols)
+    with _engine(me, sc, base, batches, batches_per_launch=8) as eng:
+        _check(eng, ob, batches, _pipelined(eng, batches, 10), "agg large qty")
+        assert eng.stats()["handoffs"] > 0
+
+
 def test_agg_groups_overfull_buckets(me, orc):
     """A Zipf-skewed stream: the head symbols' buckets overflow BK_CAP records, so the walk hands them to
     the continuation (which rescans the batch); every batch against the oracle."""

@@ -45,8 +45,10 @@ def orc(built):
     return oracle
 
 
-def _engine(me, hot_min, *a, agg=1, **kw):
+def _engine(me, hot_min, *a, agg=1, ladder=None, **kw):
     env = {"ME_HOT_MIN": str(hot_min), "ME_HOT_AGG": str(agg)}
+    if ladder is not None:  # ME_AGG_LADDER: the largest window k_agg_walk's ladder walk takes (0: lists)
+        env["ME_AGG_LADDER"] = str(ladder)
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
@@ -156,6 +158,39 @@ def test_agg_single_symbol_config1(me, orc, levels):
                  max_chunks=total + 64) as eng:
         nf = run_both(eng, ob, batches, ctx=f"agg c1 L={levels}")
     assert nf > 0
+
+
+@pytest.mark.parametrize("levels,ladder", [(256, 0), (2048, 32768)])
+def test_agg_config1_walk_forms(me, orc, levels, ladder):
+    """Config 1's shape on the walk form the default does not pick at that window (ME_AGG_LADDER): the
+    top-of-book lists at L = 256 (they also take any book the 32-bit ladder cannot hold), the ladder at
+    L = 2,048."""
+    sc = me.preset(1, levels=levels, batch=16384)
+    st = me.Stream(sc)
+    base = st.base_prices()
+    batches = [st.next(sc.batch) for _ in range(8)]
+    ob = orc.OracleBook(sc.num_symbols)
+    total = sum(len(b) for b in batches)
+    with _engine(me, 512, sc.num_symbols, sc.levels, base, ladder=ladder, max_batch=sc.batch,
+                 max_resting=total + 64, max_chunks=total + 64) as eng:
+        assert run_both(eng, ob, batches, ctx=f"agg c1 L={levels} ladder<={ladder}") > 0
+
+
+@pytest.mark.parametrize("levels", [256, 2048])
+@pytest.mark.parametrize("max_qty", [1 << 20, 1 << 26])
+def test_agg_large_quantities(me, orc, levels, max_qty):
+    """Quantities up to 2^20 / 2^26: the ladder's 32-bit totals are exact only while the book's sum stays
+    below 2^31, so blocks that could cross it go to the generic loop and books beyond it take the list
+    walk (64-bit totals) — level totals past 2^32 included; every batch against the oracle."""
+    sc = me.preset(1, levels=levels, batch=8192, max_qty=max_qty)
+    st = me.Stream(sc)
+    base = st.base_prices()
+    batches = [st.next(sc.batch) for _ in range(10)]
+    ob = orc.OracleBook(sc.num_symbols)
+    total = sum(len(b) for b in batches)
+    with _engine(me, 512, sc.num_symbols, sc.levels, base, max_batch=sc.batch, max_resting=total + 64,
+                 max_chunks=total + 64) as eng:
+        assert run_both(eng, ob, batches, ctx=f"agg qty<={max_qty} L={levels}") > 0
 
 
 @pytest.mark.parametrize("spread", [2, 40, 400])
