@@ -518,11 +518,12 @@ extern "C" me_engine* me_create(const me_config* cfg) {
     // L <= 128: every symbol of a launch group through the aggregate path (k_agg_gwalk) instead of
     // k_match_reg's serial loop — ME_REG_AGG=1 (measured per workload)
     // (unset: on when a batch holds >= 32 records per symbol — config 2's shape, 64; config 3 has ~10 and
-    // runs faster on k_match_reg — and off for good once hand-offs show up, see reg_agg_auto)
+    // runs faster on k_match_reg — in batches of >= 8,192 records, and off for good once hand-offs show
+    // up, see reg_agg_auto)
     const char* vr = getenv("ME_REG_AGG");
     const uint64_t grp = cfg->batches_per_launch ? cfg->batches_per_launch : ME_DEFAULT_GROUP;
     e->hot.agg_reg = L <= 128 && (vr ? atoi(vr) != 0
-                                     : (uint64_t)cfg->max_batch >= 32ull * S &&
+                                     : (uint64_t)cfg->max_batch >= 32ull * S && cfg->max_batch >= 8192u &&
                                            (uint64_t)cfg->max_batch * grp <= (4ull << 20));  // (pools of a
                                                                                              // group's records)
     e->reg_agg_auto = e->hot.agg_reg && !vr;

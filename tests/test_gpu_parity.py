@@ -1,6 +1,8 @@
 """GPU parity: the HIP engine (through the C-ABI) against the CPU oracle — an unbounded price-time
 book — and the committed golden fixtures: bit-exact per-record results, trade tapes and resting
 books. Needs an MI355X."""
+import os
+
 import numpy as np
 import pytest
 
@@ -661,8 +663,17 @@ def test_handoffs_only_for_far_events(me, orc):
         batches = [st.next(sc.batch) for _ in range(6)]
         total = sum(len(b) for b in batches)
         ob = orc.OracleBook(sc.num_symbols)
-        with engine_for(me, sc.num_symbols, sc.levels, base, sc.batch, total + 1024,
-                        max_chunks=total + 2 * sc.num_symbols) as eng:
+        old = os.environ.get("ME_REG_AGG")
+        os.environ["ME_REG_AGG"] = "0"  # k_match_reg's hand-offs (the grouped aggregate path hands cancels off)
+        try:
+            eng = engine_for(me, sc.num_symbols, sc.levels, base, sc.batch, total + 1024,
+                             max_chunks=total + 2 * sc.num_symbols)
+        finally:
+            if old is None:
+                del os.environ["ME_REG_AGG"]
+            else:
+                os.environ["ME_REG_AGG"] = old
+        with eng:
             run_both(eng, ob, batches, ctx=f"handoffs c{cfg}")
             h = eng.stats()["handoffs"]
         assert (h > 0) == expect_far, (cfg, h)

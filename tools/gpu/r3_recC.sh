@@ -17,3 +17,4 @@ for w in c3 c5; do
 done
 timeout -k 10 300 python bench.py --workload c1 > $O/workload_c1.json 2> $O/workload_c1.err && line $O/workload_c1.json c1 || { echo BENCH_FAIL c1; exit 1; }
 timeout -k 10 300 python bench.py --workload c4 > $O/workload_c4.json 2> $O/workload_c4.err && line $O/workload_c4.json c4 || { echo BENCH_FAIL c4; exit 1; }
+ME_REG_AGG=1 timeout -k 10 120 python -u -m pytest tests/test_gpu_parity.py -k "cancelled_chunks or capacity_exhaustion" -m gpu -q -p no:cacheprovider --timeout 100 --timeout-method thread > $O/diag_agg_tiny_pool.log 2>&1; tail -3 $O/diag_agg_tiny_pool.log
