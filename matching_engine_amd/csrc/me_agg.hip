@@ -468,25 +468,36 @@ struct LWalk {
 
 // smallest occupied level >= x, or L: a scan of the LDS totals. Only levels on the side being searched
 // lie there (the other side's cached best, whose LDS copy is stale, is on the other side of x).
-__device__ __forceinline__ int lw_next(const LWalk& w, int x) {
+// (*tot: its total, read by the scan itself — no second LDS round trip on the chain)
+__device__ __forceinline__ int lw_next(const LWalk& w, int x, uint32_t& tot) {
   const int lane = lane_id();
   for (int b = x & ~63; b < w.L; b += 64) {
     const int l = b + lane;
     const uint32_t t = w.tot[l];  // (l < L + 64: beyond L, the dummy slots)
     const unsigned long long m = __ballot(l >= x && l < w.L && t != 0u);
-    if (m) return b + __builtin_ctzll(m);
+    if (m) {
+      const int i = __builtin_ctzll(m);
+      tot = rl32(t, i);
+      return b + i;
+    }
   }
+  tot = 0u;
   return w.L;
 }
 // largest occupied level <= x, or -1
-__device__ __forceinline__ int lw_prev(const LWalk& w, int x) {
+__device__ __forceinline__ int lw_prev(const LWalk& w, int x, uint32_t& tot) {
   const int lane = lane_id();
   for (int b = x & ~63; b >= 0; b -= 64) {
     const int l = b + lane;
     const uint32_t t = w.tot[l];
     const unsigned long long m = __ballot(l <= x && t != 0u);  // (x < L)
-    if (m) return b + 63 - __builtin_clzll(m);
+    if (m) {
+      const int i = 63 - __builtin_clzll(m);
+      tot = rl32(t, i);
+      return b + i;
+    }
   }
+  tot = 0u;
   return -1;
 }
 // one-lane LDS writes: lane 0 on the level, every other lane on its own dummy slot (no exec change)
@@ -518,8 +529,7 @@ __device__ __forceinline__ void lw_take_buy(AWalk& e, LWalk& w, int lim, uint32_
     a_emit(e, w.ba, jt, (int)w.cba);
     rem -= w.cba;
     lw_put(w, w.ba, 0u);  // empty levels hold 0 (a rest there adds)
-    w.ba = lw_next(w, w.ba + 1);
-    w.cba = w.ba < w.L ? lw_get(w, w.ba) : 0u;
+    w.ba = lw_next(w, w.ba + 1, w.cba);
     if (!rem || w.ba > lim) return;
     if (w.cba > rem) {
       w.cba -= rem;
@@ -541,8 +551,7 @@ __device__ __forceinline__ void lw_take_sell(AWalk& e, LWalk& w, int lim, uint32
     a_emit(e, w.bb, jt, (int)w.cbb);
     rem -= w.cbb;
     lw_put(w, w.bb, 0u);
-    w.bb = lw_prev(w, w.bb - 1);
-    w.cbb = w.bb >= 0 ? lw_get(w, w.bb) : 0u;
+    w.bb = lw_prev(w, w.bb - 1, w.cbb);
     if (!rem || w.bb < lim) return;
     if (w.cbb > rem) {
       w.cbb -= rem;
