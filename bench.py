@@ -97,7 +97,8 @@ def parse():
                          "results, merge by taker seq); reported beside value, never in it. Default: 16 at N > 1, "
                          "0 at N = 1")
     ap.add_argument("--traffic-from", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
-                    help="JSON {bytes_per_order: ...} from tools/gpu_pmc_traffic.sh for roofline.traffic (c2)")
+                    help="JSON {bytes_per_order: ...} from tools/gpu/pmc_traffic_wl.sh for roofline.traffic (c2; the "
+                         "k_match_reg measurement when the engine runs c2 without grouped aggregate launches)")
     args = ap.parse_args()
     w = WORKLOADS[args.workload]
     if args.symbols_per_gpu is None:
@@ -493,7 +494,10 @@ def main():
     # WRITE_SIZE passes, tools/gpu_pmc_traffic.sh -> profiles/pmc_traffic[_cN].json) scaled to the orders of
     # THIS run's timed launches, so it and algorithmic_bytes_per_launch describe the same launch shape
     traffic = traffic_per_order = traffic_src = None
+    paths = eng.paths()
     tfile = args.traffic_from
+    if args.workload == "c2" and not paths["grouped_agg"] and tfile == os.path.join(ROOT, "profiles", "pmc_traffic.json"):
+        tfile = os.path.join(ROOT, "profiles", "pmc_traffic_k_match_reg.json")  # (ME_REG_AGG=0)
     if args.workload != "c2":
         tfile = os.path.join(ROOT, "profiles", f"pmc_traffic_{args.workload}.json")
     if tfile and os.path.exists(tfile):
@@ -523,7 +527,6 @@ def main():
             f2 += len(f)
         e2e = n2 / (time.perf_counter() - t2)
     max_resting = eng.config()["max_resting"]
-    paths = eng.paths()
     for db in dbs:
         db.free()
     eng.close()
