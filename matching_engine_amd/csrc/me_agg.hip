@@ -1661,6 +1661,17 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
       a_ghand(bk, s, g0, 0u, rl32(nsv, (int)g0), s * ga.slab, s * ga.slab + ga.slab);
       continue;
     }
+    // free chunks k_match_reg parked in fcache[s][0, nfree) join the front of the free list (one header
+    // store per lane), so k_agg_alloc reuses them before it takes fresh chunks; k_agg_gfin writes nfree = 0
+    {
+      const uint32_t nfc = min(rl32(st.nfree, 0), 64u);
+      if (nfc) {
+        const uint32_t fc = bk.fcache[(size_t)s * 64u + lane];
+        const uint32_t nx = (uint32_t)__shfl((int)fc, min(lane + 1, 63), 64);
+        if ((uint32_t)lane < nfc) bk.chunks[fc].hdr.next = (uint32_t)lane + 1u < nfc ? nx : st.free_head;
+        if (lane == 0) slot->free_head = fc;
+      }
+    }
     AWalk w;
     a_walk_init(w, bk, ag, s, eb, locc, evstg);
     LWalk lw;
@@ -1829,6 +1840,7 @@ __global__ __launch_bounds__(1024) void k_agg_gfin(BookDev bk, AggGArgs ga, AggD
       o.best_bid = sl.bb;
       o.best_ask = sl.ba;
       o.free_head = ag.slot[s].free_head;
+      o.nfree = 0;  // the walk linked the parked chunks into the free list
       const int dr = ag.slot[s].dresting;
       o.resting = (uint32_t)((int)sl.resting0 + dr);
       bk.sym[s] = o;

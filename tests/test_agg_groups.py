@@ -159,3 +159,69 @@ def test_agg_groups_device_back_to_back(me, orc):
         assert eng.resting_count() == ob.resting()
         for db in dbs:
             db.free()
+
+
+def _peak_resting(orc, sc, batches):
+    """The most orders resting at any record of the stream (the oracle fed one record at a time)."""
+    ob = orc.OracleBook(sc.num_symbols)
+    peak = 0
+    for b in batches:
+        for i in range(len(b)):
+            ob.submit(b.take(slice(i, i + 1)))
+            peak = max(peak, ob.resting())
+    return peak
+
+
+@pytest.mark.parametrize("group", [1, 8])
+def test_agg_groups_cancels_tight_chunk_pool(me, orc, group):
+    """One symbol, 40 % cancels and sweeping MARKETs, ME_REG_AGG=1: adds go through the walk, cancels
+    hand the symbol to k_match_reg's continuation, which parks freed chunks in fcache. The pool holds
+    only the stream's peak resting orders (+ the 2S slack and a few): every parked chunk must be reused
+    by the walk (k_agg_gwalk links them into the free list), or the pool runs dry."""
+    sc = me.preset(5, num_symbols=1, levels=128, batch=512, cancel_pct=40, market_pct=15, market_qty_mult=3,
+                   spread_ticks=8)
+    st = me.Stream(sc)
+    base = st.base_prices()
+    batches = [st.next(sc.batch) for _ in range(40)]
+    peak = _peak_resting(orc, sc, batches)
+    ob = orc.OracleBook(sc.num_symbols)
+    old = os.environ.get("ME_REG_AGG")
+    os.environ["ME_REG_AGG"] = "1"
+    try:
+        eng = me.Engine(1, sc.levels, base, max_batch=sc.batch, max_resting=sum(len(b) for b in batches),
+                        max_chunks=peak + 2 + 8, seq_ring=1 << 22, batches_per_launch=group)
+    finally:
+        if old is None:
+            del os.environ["ME_REG_AGG"]
+        else:
+            os.environ["ME_REG_AGG"] = old
+    with eng:
+        _check(eng, ob, batches, _pipelined(eng, batches, 2 * group + 1), f"agg tight pool G={group}")
+        assert eng.stats()["handoffs"] > 0
+        assert eng.paths()["grouped_agg"]
+
+
+def test_agg_auto_mode_turns_off_under_cancels(me, orc):
+    """Automatic path choice (ME_REG_AGG unset) at a shape that picks the grouped aggregate path (8,192-
+    record batches, 128 records per symbol): a cancel-free first phase runs on it; a second phase with
+    30 % cancels hands symbols off until the engine turns it off for good. max_chunks = max_resting + 2S,
+    every batch of both phases against the oracle."""
+    sc = me.preset(5, num_symbols=64, levels=128, batch=8192, cancel_pct=30, market_pct=15, market_qty_mult=3)
+    st = me.Stream(sc)
+    base = st.base_prices()
+    raw = [st.next(sc.batch) for _ in range(40)]
+    # phase 1: the first 16 batches with their cancel records dropped (the generator's later cancels
+    # never target an order it already cancelled, and the oracle rejects unknown targets anyway)
+    batches = [b.take((b.kind & 8) == 0) if k < 16 else b for k, b in enumerate(raw)]
+    total = sum(len(b) for b in batches)
+    max_resting = total + 1024
+    assert os.environ.get("ME_REG_AGG") is None
+    ob = orc.OracleBook(sc.num_symbols)
+    with me.Engine(sc.num_symbols, sc.levels, base, max_batch=sc.batch, max_resting=max_resting,
+                   max_chunks=max_resting + 2 * sc.num_symbols, seq_ring=1 << 22, batches_per_launch=8) as eng:
+        outs = _pipelined(eng, batches[:16], 9)
+        assert eng.paths()["grouped_agg"], "phase 1 should run on the grouped aggregate path"
+        assert eng.stats()["handoffs"] == 0
+        outs += _pipelined(eng, batches[16:], 9)
+        assert not eng.paths()["grouped_agg"], "hand-offs should have turned the aggregate path off"
+        _check(eng, ob, batches, outs, "agg auto flip")

@@ -19,13 +19,20 @@ def me(built):
     return matching_engine_amd
 
 
-def _case(me, seed):
-    rng = np.random.default_rng(1000 + seed)
-    levels = int(rng.choice([64, 128, 128, 256, 1024, 4096]))
-    S = int(rng.choice([1, 3, 17, 64, 300]))
-    batch = int(rng.choice([64, 500, 2048, 6000]))
-    group = int(rng.choice([1, 2, 7, 16, 32]))
-    nb = int(rng.integers(6, 40))
+def _case(me, seed, agg=False):
+    rng = np.random.default_rng((5000 if agg else 1000) + seed)
+    if agg:  # the grouped aggregate path's shapes: register windows, batches of >= 8,192 records
+        levels = int(rng.choice([64, 128]))
+        S = int(rng.choice([1, 17, 64, 256]))
+        batch = int(rng.choice([8192, 16384]))
+        group = int(rng.choice([1, 4, 16, 32]))
+        nb = int(rng.integers(4, 24))
+    else:
+        levels = int(rng.choice([64, 128, 128, 256, 1024, 4096]))
+        S = int(rng.choice([1, 3, 17, 64, 300]))
+        batch = int(rng.choice([64, 500, 2048, 6000]))
+        group = int(rng.choice([1, 2, 7, 16, 32]))
+        nb = int(rng.integers(6, 40))
     cancel = int(rng.choice([0, 10, 40]))
     market = int(rng.choice([5, 20]))
     over = dict(num_symbols=S, levels=levels, batch=batch, cancel_pct=cancel, market_pct=market,
@@ -49,15 +56,29 @@ def _case(me, seed):
 
 @pytest.mark.parametrize("seed", range(24))
 def test_fuzz_case(me, seed):
+    _run_case(me, seed, False)
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_fuzz_agg_case(me, seed, monkeypatch):
+    """ME_REG_AGG=1: every launch group through k_agg_gwalk (cancels, far prices and overfull buckets hand
+    symbols to k_match_reg's continuation mid-group), chunk pool max_resting + 2S."""
+    monkeypatch.setenv("ME_REG_AGG", "1")
+    _run_case(me, seed, True)
+
+
+def _run_case(me, seed, agg):
     from oracle.oracle import OracleBook
 
-    sc, base, batches, group, path, lag = _case(me, seed)
+    sc, base, batches, group, path, lag = _case(me, seed, agg)
     total = sum(len(b) for b in batches)
-    ctx = (f"seed {seed}: L={sc.levels} S={sc.num_symbols} batch={sc.batch} G={group} path={path} "
+    ctx = (f"{'agg ' if agg else ''}seed {seed}: L={sc.levels} S={sc.num_symbols} batch={sc.batch} G={group} path={path} "
            f"lag={lag} cancel={sc.cancel_pct} far={sc.far_pct} drift={sc.drift_step}/{sc.drift_every}")
     ob = OracleBook(sc.num_symbols)
     with me.Engine(sc.num_symbols, sc.levels, base, max_batch=sc.batch, max_resting=total + 1024,
-                   max_chunks=total + 2 * sc.num_symbols + 64, seq_ring=1 << 20, batches_per_launch=group) as eng:
+                   max_chunks=total + 1024 + 2 * sc.num_symbols, seq_ring=1 << 20, batches_per_launch=group) as eng:
+        if agg:
+            assert eng.paths()["grouped_agg"], ctx
         outs = [None] * len(batches)
         if path == "device":
             group = eng.config()["batches_per_launch"]  # deep windows: one batch per launch

@@ -402,9 +402,13 @@ def test_edge_symbol_count_sort_plans(me, orc):
             run_both(eng, ob, batches, book_symbols=range(0, S, max(1, S // 50)), ctx=f"S={S}")
 
 
-def test_cancelled_chunks_are_unlinked(me, orc):
+@pytest.mark.parametrize("reg_agg", ["0", "1"])
+def test_cancelled_chunks_are_unlinked(me, orc, monkeypatch, reg_agg):
     """A level that never empties, with chunk after chunk filled and then cancelled: dead chunks
-    (head, middle, tail) must be unlinked and reused, so a 4-chunk pool suffices for 30 rounds."""
+    (head, middle, tail) must be unlinked and reused, so a 4-chunk pool suffices for 30 rounds.
+    ME_REG_AGG=1: the adds go through the grouped aggregate path and the cancels through k_match_reg's
+    continuation, which parks freed chunks in fcache — the walk must reuse them (k_agg_gwalk)."""
+    monkeypatch.setenv("ME_REG_AGG", reg_agg)
     B, S, L, M = me.SIDE_BUY, me.SIDE_SELL, me.TYPE_LIMIT, me.TYPE_MARKET
     C = me._abi.CHUNK_SLOTS
     ob = orc.OracleBook(1)
@@ -426,6 +430,7 @@ def test_cancelled_chunks_are_unlinked(me, orc):
             run_both(eng, ob, [b, cancels], ctx=f"round {rnd}")
         sweep = _rows(me, [(0, S, M, 0, 0, 5)], start_seq=seq)
         run_both(eng, ob, [sweep], ctx="final sweep")
+        assert eng.paths()["grouped_agg"] == (reg_agg == "1")
 
 
 def test_capacity_exhaustion_is_loud(me):

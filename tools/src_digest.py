@@ -10,6 +10,7 @@ CSRC = os.path.join(ROOT, "matching_engine_amd", "csrc")
 FILES = [os.path.join(CSRC, f) for f in ("me_kernels.hip", "me_match_reg.hip", "me_snapshot.hip", "me_agg.hip", "me_engine.cpp",
                                          "me_gen.cpp", "me_service.cpp", "me_cluster.cpp", "me_far.hpp", "me_layout.hpp", "me_wave.hpp")]
 FILES += [os.path.join(ROOT, "include", f) for f in ("me_engine.h", "me_service.h", "me_cluster.h")]
+FILES += [os.path.join(ROOT, "matching_engine_amd", "Makefile")]  # the compiler flags shape the kernels
 
 
 def digest() -> str:
