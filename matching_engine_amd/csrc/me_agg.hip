@@ -1893,6 +1893,668 @@ __global__ __launch_bounds__(1024) void k_agg_gemit(BookDev bk, AggGArgs ga, Agg
   }
 }
 
+// ------------------------------------------------------------------ grouped launches: one workgroup per symbol
+// k_agg_gres does the work of k_agg_group ... k_agg_gemit for a grouped launch in ONE launch, one 512-thread
+// workgroup per symbol (the walk's workgroup of the same symbol ran on the same XCD, blockIdx = symbol):
+//   A  the symbol's log sorted by level in LDS (per-wave histograms of contiguous log ranges, a stable
+//      ballot-multisplit scatter of 16-bit log indices) — no sorted copies, segment tables or per-event
+//      arrays in HBM;
+//   B  its levels resolved by the waves (a level per wave, taken from an LDS counter): the initial FIFO
+//      walked until the batch's takes are covered, consumed makers, emptied chunks, each take's fill count
+//      into an LDS array indexed by log position; the slot's cursors are LDS atomics, not pool-wide ones;
+//   C  the fill offsets (exclusive scan of the fill counts in log order = tape order, in place in LDS), each
+//      batch's scratch base, the records' fill counts and scratch starts;
+//   D  the chunk allocation (wave 0) beside the fills of every take (the other waves), then the surviving
+//      rests placed into the levels' tails and new chunks.
+// The per-event LDS arrays hold `ne` events (the launch sizes them from the group's mean records per
+// symbol); a symbol with a longer log keeps them in the log's own HBM regions (AggDev::evn / evs) instead.
+constexpr int GR_WAVES = 8;
+constexpr uint32_t GR_THREADS = GR_WAVES * 64;
+
+struct GrLevel {  // what phase B found for one level
+  unsigned long long C, T0;
+  uint32_t newhead, mk_base, nmk, fr_base, nfreed, need, d_off, ks;
+};
+struct GrStage {  // a wave's maker / emptied-chunk staging (phases B and D)
+  AggMk mk[LV_STAGE];
+  uint32_t fr[LV_STAGE];
+};
+struct GrShared {
+  union {
+    uint32_t wh[GR_WAVES][128];  // phase A: per-wave level histograms, then scatter cursors
+    GrStage st[GR_WAVES];
+  } u;
+  GrLevel lv[128];
+  uint32_t lstart[129];
+  uint32_t lhead[128], ltail[128];
+  uint32_t lvlist[128];
+  uint32_t gev[ME_GMAX + 1], gex[ME_GMAX + 1], gbase[ME_GMAX + 1];
+  uint32_t wsum[GR_WAVES];
+  uint32_t nlv, next, next2, cur_mk, cur_fr, deficit, alloc_base, free_head;
+  int dresting;
+  uint8_t ltend[128];
+};
+
+// Level work items of phases B and D: lane 0 takes the next from an LDS counter.
+__device__ __forceinline__ uint32_t gr_take(uint32_t* ctr) {
+  uint32_t i = 0;
+  if (lane_id() == 0) i = atomicAdd(ctr, 1u);
+  return rl32(i, 0);
+}
+
+template <bool kLds>
+__device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& ga, const AggSrc& src, const AggDev& ag,
+                                            uint32_t s, const AggSlot& sl, GrShared& sh, uint32_t* nf, uint16_t* idx) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint32_t L = bk.L;  // <= 128
+  const uint32_t eb = sl.ev_base, n = sl.ev_cnt, ng = ga.ng;
+  const AggEv* ev = ag.ev + eb;
+  const size_t lo_l = (size_t)s * L;
+  // ---- A: level heads (one coalesced load), the batches' log boundaries, the scalars
+  if ((uint32_t)tid < L) {
+    const Level v = bk.levels[lo_l + tid];
+    sh.lhead[tid] = v.head;
+    sh.ltail[tid] = v.tail;
+    sh.ltend[tid] = bk.tend[lo_l + tid];
+  }
+  if ((uint32_t)tid <= ng) sh.gev[tid] = *a_gtab(ag.gev, s, (uint32_t)tid) - eb;
+  if (tid == 0) {
+    sh.next = sh.next2 = 0u;
+    sh.cur_mk = sh.cur_fr = sh.deficit = 0u;
+    sh.dresting = 0;
+  }
+  sh.u.wh[wv][lane] = 0u;
+  sh.u.wh[wv][64 + lane] = 0u;
+  wave_mem_order();
+  // per-wave histograms of contiguous log ranges (64-aligned), then a stable scatter with the same ranges
+  const uint32_t per = ((n + GR_WAVES - 1u) / GR_WAVES + 63u) & ~63u;
+  const uint32_t r0 = min(n, (uint32_t)wv * per), r1 = min(n, r0 + per);
+  for (uint32_t b = r0; b < r1; b += 64) {
+    const uint32_t e = b + (uint32_t)lane;
+    if (e < r1) atomicAdd(&sh.u.wh[wv][ev[e].lvl & 127u], 1u);
+  }
+  __syncthreads();
+  if (wv == 0) {
+    uint32_t c0 = 0, c1 = 0;
+    for (int w = 0; w < GR_WAVES; ++w) {
+      c0 += sh.u.wh[w][lane];
+      c1 += sh.u.wh[w][64 + lane];
+    }
+    const uint32_t i0 = (uint32_t)wave_incl_scan((long long)c0), t0 = rl32(i0, 63);
+    const uint32_t i1 = (uint32_t)wave_incl_scan((long long)c1);
+    uint32_t a0 = i0 - c0, a1 = t0 + i1 - c1;
+    sh.lstart[lane] = a0;
+    sh.lstart[64 + lane] = a1;
+    if (lane == 0) sh.lstart[128] = n;
+    const unsigned long long m0 = __ballot(c0 != 0u), m1 = __ballot(c1 != 0u);
+    if (c0) sh.lvlist[__popcll(m0 & lanemask_lt())] = (uint32_t)lane;
+    if (c1) sh.lvlist[__popcll(m0) + __popcll(m1 & lanemask_lt())] = 64u + (uint32_t)lane;
+    if (lane == 0) sh.nlv = (uint32_t)(__popcll(m0) + __popcll(m1));
+    for (int w = 0; w < GR_WAVES; ++w) {  // wave w's events of level l start at its running base
+      const uint32_t x0 = sh.u.wh[w][lane], x1 = sh.u.wh[w][64 + lane];
+      sh.u.wh[w][lane] = a0;
+      sh.u.wh[w][64 + lane] = a1;
+      a0 += x0;
+      a1 += x1;
+    }
+  }
+  __syncthreads();
+  for (uint32_t b = r0; b < r1; b += 64) {
+    const uint32_t e = b + (uint32_t)lane;
+    const bool v = e < r1;
+    const uint32_t key = v ? (ev[e].lvl & 127u) : 0u;
+    unsigned long long peers = __ballot(v);
+#pragma unroll
+    for (uint32_t bit = 0; bit < 7; ++bit) {
+      const unsigned long long bb = __ballot((key >> bit) & 1u);
+      peers &= ((key >> bit) & 1u) ? bb : ~bb;
+    }
+    const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
+    const uint32_t start = sh.u.wh[wv][key];
+    if (v) idx[start + rank] = (uint16_t)e;
+    wave_mem_order();
+    if (v && rank == 0) sh.u.wh[wv][key] = start + (uint32_t)__popcll(peers);
+    wave_mem_order();
+  }
+  __syncthreads();
+  // ---- B: the levels
+  const uint32_t nlv = sh.nlv;
+  const bool act = lane < ME_C;
+  AggMk* mkl = sh.u.st[wv].mk;
+  uint32_t* frl = sh.u.st[wv].fr;
+  auto entry = [&](uint32_t start, uint32_t cnt, uint32_t b, uint32_t& er) -> AggEv {
+    AggEv E{};
+    er = 0;
+    if (b + (uint32_t)lane < cnt) {
+      er = idx[start + b + lane];
+      E = ev[er];
+    }
+    return E;
+  };
+  for (uint32_t it = gr_take(&sh.next); it < nlv; it = gr_take(&sh.next)) {
+    const uint32_t lvl = __builtin_amdgcn_readfirstlane(sh.lvlist[it]);
+    const uint32_t start = __builtin_amdgcn_readfirstlane(sh.lstart[lvl]);
+    const uint32_t cnt = __builtin_amdgcn_readfirstlane(sh.lstart[lvl + 1]) - start;
+    const uint32_t head0 = __builtin_amdgcn_readfirstlane(sh.lhead[lvl]);
+    const uint32_t te_raw = sh.ltend[lvl];
+    uint32_t er0;
+    const AggEv E0 = entry(start, cnt, 0, er0);  // the first 64 entries stay in registers
+    auto ent = [&](uint32_t b, uint32_t& er) -> AggEv {
+      if (b == 0) {
+        er = er0;
+        return E0;
+      }
+      return entry(start, cnt, b, er);
+    };
+    // 1. C: the takes' total
+    unsigned long long C = 0;
+    for (uint32_t b = 0; b < cnt; b += 64) {
+      uint32_t er;
+      const AggEv E = ent(b, er);
+      const bool v = b + (uint32_t)lane < cnt;
+      const bool tk = v && (E.j & AGG_TAKE) != 0u;
+      if (v && !tk) nf[er] = 0u;
+      C += (unsigned long long)rli64(wave_incl_scan(tk ? (long long)E.qty : 0ll), 63);
+    }
+    // 2. the initial FIFO, read once
+    unsigned long long W = 0;
+    uint32_t nmk = 0, nfreed = 0, nfull = 0, newhead = NIL, ch = head0, pch = NIL;
+    int pq = 0;
+    unsigned long long pen = 0;
+    bool exhausted = false;
+    for (;;) {
+      if (ch == NIL) {
+        exhausted = true;
+        break;
+      }
+      if (W >= C) {
+        newhead = ch;
+        break;
+      }
+      if (ch >= bk.nchunks) {
+        a_set_err(bk, ERR_INCONSISTENT);
+        exhausted = true;
+        break;
+      }
+      const int q = act ? bk.chunks[ch].qty[lane] : 0;
+      const unsigned long long sq = act ? bk.chunks[ch].seq[lane] : 0ull;
+      const uint32_t nx = auniu(bk.chunks[ch].hdr.next);
+      const long long inc = wave_incl_scan((long long)q);
+      const unsigned long long ex = (unsigned long long)(inc - q), en = W + (unsigned long long)inc;
+      const unsigned long long live = (unsigned long long)rli64(inc, 63);
+      const bool cons = q > 0 && W + ex < C;
+      const unsigned long long cm = __ballot(cons);
+      const uint32_t r = nmk + (uint32_t)__popcll(cm & lanemask_lt());
+      if (cons && r < LV_STAGE) {
+        mkl[r].seq = sq;
+        mkl[r].end = en;
+      }
+      nmk += (uint32_t)__popcll(cm);
+      nfull += (uint32_t)__popcll(__ballot(q > 0 && en <= C));
+      if (W + live <= C) {  // emptied
+        if (lane == 0 && nfreed < LV_STAGE) frl[nfreed] = ch;
+        ++nfreed;
+        W += live;
+        ch = nx;
+        continue;
+      }
+      pch = ch;  // C ends inside this chunk
+      pq = q;
+      pen = en;
+      newhead = ch;
+      break;
+    }
+    const unsigned long long T0 = exhausted ? W : ~0ull;
+    const unsigned long long Cr = exhausted && C > W ? C - W : 0ull;  // taken from this group's rests
+    // 3. the rests: those C reaches are makers too (after the FIFO's), the others survive
+    uint32_t nrc = 0, ks = 0;
+    {
+      unsigned long long RR = 0;
+      for (uint32_t b = 0; b < cnt; b += 64) {
+        uint32_t er;
+        const AggEv E = ent(b, er);
+        const bool v = b + (uint32_t)lane < cnt;
+        const bool rs = v && (E.j & AGG_TAKE) == 0u;
+        const long long rq = rs ? (long long)E.qty : 0ll;
+        const long long inc = wave_incl_scan(rq);
+        const unsigned long long st0 = RR + (unsigned long long)(inc - rq), en = RR + (unsigned long long)inc;
+        const bool cons = rs && st0 < Cr;
+        const unsigned long long cm = __ballot(cons);
+        const uint32_t r = nmk + nrc + (uint32_t)__popcll(cm & lanemask_lt());
+        if (cons && r < LV_STAGE) {
+          mkl[r].seq = a_seq_of(src, E.j);
+          mkl[r].end = T0 + en;
+        }
+        nrc += (uint32_t)__popcll(cm);
+        ks += (uint32_t)__popcll(__ballot(rs && en > Cr));
+        RR += (unsigned long long)rli64(inc, 63);
+      }
+    }
+    const uint32_t te0 = newhead != NIL ? auniu(te_raw) : 0u;  // the tail survives iff newhead does
+    const uint32_t tailfree = newhead != NIL ? (uint32_t)ME_C - te0 : 0u;
+    const uint32_t need = ks > tailfree ? (ks - tailfree + ME_C - 1) / ME_C : 0u;
+    const uint32_t own = min(need, nfreed), deficit = need - own;
+    const uint32_t nmkt = nmk + nrc;
+    uint32_t mk_base = 0, fr_base = 0, d_off = 0;
+    if (lane == 0) {
+      mk_base = sl.mk_base + atomicAdd(&sh.cur_mk, nmkt);
+      fr_base = sl.fr_base + atomicAdd(&sh.cur_fr, nfreed);
+      if (deficit) d_off = atomicAdd(&sh.deficit, deficit);
+      const int dr = (int)ks - (int)nfull;
+      if (dr) atomicAdd(&sh.dresting, dr);
+    }
+    mk_base = rl32(mk_base, 0);
+    fr_base = rl32(fr_base, 0);
+    d_off = rl32(d_off, 0);
+    if (mk_base + nmkt > ag.mk_cap || fr_base + nfreed > ag.fr_cap) {
+      a_set_err(bk, ERR_SCRATCH_OOM);  // sized so this cannot happen; leaves the level alone
+      for (uint32_t b = 0; b < cnt; b += 64) {
+        uint32_t er;
+        (void)ent(b, er);
+        if (b + (uint32_t)lane < cnt) nf[er] = 0u;
+      }
+      if (lane == 0) {
+        GrLevel o{};
+        o.T0 = ~0ull;
+        o.newhead = head0;
+        sh.lv[lvl] = o;
+      }
+      wave_mem_order();
+      continue;
+    }
+    const bool staged = nmkt <= LV_STAGE && nfreed <= LV_STAGE;
+    // 4. makers and emptied chunks to HBM: from LDS, or past LV_STAGE by a second read of the FIFO
+    wave_mem_order();
+    if (staged) {
+      if ((uint32_t)lane < nmkt) ag.mk[mk_base + lane] = mkl[lane];
+      if ((uint32_t)lane < nfreed) ag.fr[fr_base + lane] = frl[lane];
+    } else {
+      unsigned long long Wv = 0;
+      uint32_t mi = 0, fi = 0;
+      ch = head0;
+      while (Wv < C && ch < bk.nchunks) {
+        const int q = act ? bk.chunks[ch].qty[lane] : 0;
+        const unsigned long long sq = act ? bk.chunks[ch].seq[lane] : 0ull;
+        const uint32_t nx = auniu(bk.chunks[ch].hdr.next);
+        const long long inc = wave_incl_scan((long long)q);
+        const unsigned long long ex = (unsigned long long)(inc - q), en = Wv + (unsigned long long)inc;
+        const unsigned long long live = (unsigned long long)rli64(inc, 63);
+        const bool cons = q > 0 && Wv + ex < C;
+        const unsigned long long cm = __ballot(cons);
+        if (cons) {
+          AggMk m;
+          m.seq = sq;
+          m.end = en;
+          ag.mk[mk_base + mi + (uint32_t)__popcll(cm & lanemask_lt())] = m;
+        }
+        mi += (uint32_t)__popcll(cm);
+        if (Wv + live > C) break;
+        if (lane == 0) ag.fr[fr_base + fi] = ch;
+        ++fi;
+        Wv += live;
+        ch = nx;
+      }
+      if (Cr) {
+        unsigned long long RR = 0;
+        for (uint32_t b = 0; b < cnt; b += 64) {
+          uint32_t er;
+          const AggEv E = ent(b, er);
+          const bool v = b + (uint32_t)lane < cnt;
+          const bool rs = v && (E.j & AGG_TAKE) == 0u;
+          const long long rq = rs ? (long long)E.qty : 0ll;
+          const long long inc = wave_incl_scan(rq);
+          const unsigned long long st0 = RR + (unsigned long long)(inc - rq), en = RR + (unsigned long long)inc;
+          const bool cons = rs && st0 < Cr;
+          const unsigned long long cm = __ballot(cons);
+          if (cons) {
+            AggMk m;
+            m.seq = a_seq_of(src, E.j);
+            m.end = T0 + en;
+            ag.mk[mk_base + mi + (uint32_t)__popcll(cm & lanemask_lt())] = m;
+          }
+          mi += (uint32_t)__popcll(cm);
+          RR += (unsigned long long)rli64(inc, 63);
+        }
+      }
+    }
+    // 5. the FIFO's new state: emptied chunks hold qty 0, the chunk C ends in keeps what is left
+    wave_mem_order();
+    for (uint32_t f0 = 0; f0 < nfreed; f0 += 4) {
+      const uint32_t f = f0 + (uint32_t)lane / ME_C;
+      if (f < nfreed) {
+        const uint32_t c = staged ? frl[f] : ag.fr[fr_base + f];
+        if (c < bk.nchunks) bk.chunks[c].qty[lane % ME_C] = 0;
+      }
+    }
+    if (pch != NIL && act && pq > 0 && pen - (unsigned long long)pq < C)
+      bk.chunks[pch].qty[lane] = pen <= C ? 0 : (int)(pen - C);
+    // 6. each take's fill count: the makers overlapping its interval of the level's maker space
+    wave_mem_order();
+    {
+      unsigned long long A0 = 0;
+      for (uint32_t b = 0; b < cnt; b += 64) {
+        uint32_t er;
+        const AggEv E = ent(b, er);
+        const bool v = b + (uint32_t)lane < cnt;
+        const bool tk = v && (E.j & AGG_TAKE) != 0u;
+        const long long tq = tk ? (long long)E.qty : 0ll;
+        const long long inc = wave_incl_scan(tq);
+        if (tk) {
+          const unsigned long long a = A0 + (unsigned long long)(inc - tq), z = a + (unsigned long long)E.qty;
+          const uint32_t first = staged ? a_search_lds(mkl, nmkt, a, true) : a_search(ag.mk, mk_base, nmkt, a, true);
+          const uint32_t last = staged ? a_search_lds(mkl, nmkt, z, false) : a_search(ag.mk, mk_base, nmkt, z, false);
+          nf[er] = last - first + 1u;
+        }
+        A0 += (unsigned long long)rli64(inc, 63);
+      }
+    }
+    if (lane == 0) {
+      GrLevel o;
+      o.C = C;
+      o.T0 = T0;
+      o.newhead = newhead;
+      o.mk_base = mk_base;
+      o.nmk = nmkt;
+      o.fr_base = fr_base;
+      o.nfreed = nfreed;
+      o.need = need;
+      o.d_off = d_off;
+      o.ks = ks;
+      sh.lv[lvl] = o;
+    }
+    wave_mem_order();  // the next level reuses the staging
+  }
+  __syncthreads();
+  // ---- C: fill offsets in log order (exclusive scan of nf in place), each batch's scratch base
+  uint32_t carry = 0;
+  for (uint32_t t0 = 0; t0 < n; t0 += GR_THREADS) {
+    const uint32_t e = t0 + (uint32_t)tid;
+    const uint32_t c = e < n ? nf[e] : 0u;
+    const uint32_t x = (uint32_t)wave_incl_scan((long long)c);
+    if (lane == 63) sh.wsum[wv] = x;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < GR_WAVES; ++k) {
+      const uint32_t w = sh.wsum[k];
+      pre += k < wv ? w : 0u;
+      tot += w;
+    }
+    if (e < n) nf[e] = carry + pre + x - c;
+    carry += tot;
+    __syncthreads();
+  }
+  const uint32_t ftot = carry;
+  auto EX = [&](uint32_t e) -> uint32_t { return e < n ? nf[e] : ftot; };
+  if ((uint32_t)tid < ng) {  // each batch's fills: the symbol's slab of that batch if they fit, else overflow
+    const uint32_t g = (uint32_t)tid;
+    const uint32_t x0 = EX(sh.gev[g]), x1 = EX(sh.gev[g + 1]);
+    const uint32_t f = x1 - x0;
+    unsigned long long b0 = (unsigned long long)s * ga.slab;
+    if (f > ga.slab) {
+      b0 = ga.ovf_base + atomicAdd(ga.scratch_top[g], (unsigned long long)f);
+      if (b0 + f > ga.scratch_cap) {
+        atomicOr(bk.err, ERR_SCRATCH_OOM);
+        b0 = 0;
+      }
+    }
+    sh.gex[g] = x0;
+    sh.gbase[g] = (uint32_t)b0;
+  }
+  __syncthreads();
+  // the first take of each record: its fill count and scratch start
+  for (uint32_t t = (uint32_t)tid; t < n; t += GR_THREADS) {
+    const uint32_t j = ev[t].j;
+    if (!(j & AGG_TAKE) || (t > 0 && ev[t - 1].j == j)) continue;
+    const uint32_t g = (j & ~AGG_TAKE) >> AGG_GSHIFT, oi = j & AGG_IMASK;
+    uint32_t nte = 1;  // the record's take events follow each other in the log
+    while (t + nte < n && ev[t + nte].j == j) ++nte;
+    const uint32_t x0 = EX(t), nfill = EX(t + nte) - x0;
+    me_order_result* res = ga.res[g];
+    res[oi].fill_count = nfill;
+    res[oi].tape_offset = sh.gbase[g] + (x0 - sh.gex[g]);
+    if (nfill) atomicAdd(&ga.tile_sum[g][oi / TILE_TAPE], nfill);
+  }
+  if (tid == 0 && sl.hidx != NIL) {  // the continuation goes on behind the walk's fills of its batch
+    const uint32_t g = sl.pos;
+    const uint32_t f = EX(sh.gev[g + 1]) - sh.gex[g];
+    const uint32_t b0 = sh.gbase[g];
+    bk.hand[sl.hidx].wptr = b0 + f;
+    bk.hand[sl.hidx].wend = f <= ga.slab ? s * ga.slab + ga.slab : b0 + f;
+  }
+  // ---- D1: chunk allocation (wave 0) beside the fills (the other waves)
+  if (wv == 0) {
+    uint32_t D = sh.deficit, fh = sl.free_head;
+    uint32_t Stot = 0;
+    for (uint32_t b = 0; b < nlv; b += 64) {
+      uint32_t sp = 0;
+      if (b + lane < nlv) {
+        const GrLevel& g = sh.lv[sh.lvlist[b + lane]];
+        sp = g.nfreed - min(g.need, g.nfreed);
+      }
+      Stot += (uint32_t)rli64(wave_incl_scan((long long)sp), 63);
+    }
+    uint32_t ab = 0;
+    bool ok = true;
+    if (D || Stot) {
+      ab = sl.fr_base + sh.cur_fr;  // (no other wave reserves any more)
+      if ((unsigned long long)ab + D + Stot > ag.fr_cap) {
+        a_set_err(bk, ERR_SCRATCH_OOM);
+        ok = false;
+      }
+    }
+    if ((D || Stot) && ok) {
+      uint32_t run = 0;  // the surpluses (level order) into fr[ab + D, ab + D + Stot)
+      for (uint32_t b = 0; b < nlv; b += 64) {
+        uint32_t sp = 0, srcf = 0;
+        if (b + lane < nlv) {
+          const GrLevel& g = sh.lv[sh.lvlist[b + lane]];
+          const uint32_t own = min(g.need, g.nfreed);
+          sp = g.nfreed - own;
+          srcf = g.fr_base + own;
+        }
+        const long long inc = wave_incl_scan((long long)sp);
+        const uint32_t ex = run + (uint32_t)(inc - sp);
+        for (uint32_t k = 0; k < sp; ++k) ag.fr[ab + D + ex + k] = ag.fr[srcf + k];
+        run += (uint32_t)rli64(inc, 63);
+      }
+      a_drain();
+      const uint32_t k1 = min(D, Stot);
+      for (uint32_t t = lane; t < k1; t += 64) ag.fr[ab + t] = ag.fr[ab + D + t];
+      if (D > k1) {  // the book grows: the free list, then fresh chunks
+        uint32_t t = k1;
+        if (lane == 0) {
+          while (t < D && fh != NIL && fh < bk.nchunks) {
+            ag.fr[ab + t] = fh;
+            fh = bk.chunks[fh].hdr.next;
+            ++t;
+          }
+        }
+        t = rl32(t, 0);
+        fh = rl32(fh, 0);
+        if (t < D) {
+          const uint32_t left = D - t;
+          uint32_t got = 0;
+          if (lane == 0) got = atomicAdd(bk.chunk_top, left);
+          got = rl32(got, 0);
+          if ((unsigned long long)got + left > bk.nchunks) {
+            a_set_err(bk, ERR_CHUNK_OOM);
+            for (uint32_t u = lane; u < left; u += 64) ag.fr[ab + t + u] = 0u;  // never indexed past the pool
+          } else {
+            for (uint32_t u = lane; u < left; u += 64) {
+              ag.fr[ab + t + u] = got + u;
+              bk.chunks[got + u].owner = s;  // fresh chunks belong to this symbol for good
+            }
+          }
+        }
+      } else if (Stot > D) {  // surpluses left over: linked in front of the free list
+        for (uint32_t u = D + lane; u < Stot; u += 64) {
+          const uint32_t c = ag.fr[ab + D + u];
+          bk.chunks[c].hdr.next = u + 1 < Stot ? ag.fr[ab + D + u + 1] : fh;
+        }
+        fh = auniu(ag.fr[ab + D + D]);
+      }
+    }
+    if (lane == 0) {
+      sh.alloc_base = ab;
+      SymState o = bk.sym[s];
+      o.best_bid = sl.bb;
+      o.best_ask = sl.ba;
+      o.free_head = fh;
+      o.nfree = 0;  // the walk linked the parked chunks into the free list
+      const int dr = sh.dresting;
+      o.resting = (uint32_t)((int)sl.resting0 + dr);
+      bk.sym[s] = o;
+      if (dr) atomicAdd(bk.stats + ST_RESTING, (unsigned long long)(long long)dr);
+    }
+  } else {
+    // the fills of every take: makers of its level overlapping its interval, at the record's scratch position
+    for (uint32_t it = gr_take(&sh.next2); it < nlv; it = gr_take(&sh.next2)) {
+      const uint32_t lvl = __builtin_amdgcn_readfirstlane(sh.lvlist[it]);
+      const uint32_t nmk = __builtin_amdgcn_readfirstlane(sh.lv[lvl].nmk);
+      if (!nmk) continue;
+      const uint32_t start = __builtin_amdgcn_readfirstlane(sh.lstart[lvl]);
+      const uint32_t cnt = __builtin_amdgcn_readfirstlane(sh.lstart[lvl + 1]) - start;
+      const uint32_t mk_base = __builtin_amdgcn_readfirstlane(sh.lv[lvl].mk_base);
+      const bool staged = nmk <= LV_STAGE;
+      if (staged && (uint32_t)lane < nmk) mkl[lane] = ag.mk[mk_base + lane];
+      wave_mem_order();
+      const long long price = sl.base + (long long)lvl;
+      unsigned long long A0 = 0;
+      for (uint32_t b = 0; b < cnt; b += 64) {
+        uint32_t er;
+        const AggEv E = entry(start, cnt, b, er);
+        const bool v = b + (uint32_t)lane < cnt;
+        const bool tk = v && (E.j & AGG_TAKE) != 0u;
+        const long long tq = tk ? (long long)E.qty : 0ll;
+        const long long inc = wave_incl_scan(tq);
+        if (tk) {
+          const uint32_t x0 = nf[er], nfl = EX(er + 1) - x0;
+          if (nfl) {
+            const unsigned long long a = A0 + (unsigned long long)(inc - tq), z = a + (unsigned long long)E.qty;
+            const uint32_t first = staged ? a_search_lds(mkl, nmk, a, true) : a_search(ag.mk, mk_base, nmk, a, true);
+            const uint32_t j = E.j & ~AGG_TAKE, g = j >> AGG_GSHIFT;
+            const uint32_t p = sh.gbase[g] + (x0 - sh.gex[g]);
+            me_fill f;
+            f.taker_seq = a_seq_of(src, j);
+            f.price_q4 = price;
+            f.symbol = sl.gs;
+            me_fill* sc = ga.scratch[g];
+            unsigned long long lo = a;
+            for (uint32_t k = 0; k < nfl; ++k) {
+              const AggMk m = staged ? mkl[first + k] : ag.mk[mk_base + first + k];
+              const unsigned long long hi = m.end < z ? m.end : z;
+              f.maker_seq = m.seq;
+              f.qty = (int)(hi - lo);
+              sc[p + k] = f;
+              lo = hi;
+            }
+          }
+        }
+        A0 += (unsigned long long)rli64(inc, 63);
+      }
+      wave_mem_order();  // the next level reuses the staging
+    }
+  }
+  __syncthreads();
+  // ---- D2: the surviving rests into the levels' tail chunks and new chunks; heads, tails, tail fills
+  const uint32_t alloc_base = sh.alloc_base;
+  for (uint32_t it = (uint32_t)wv; it < nlv; it += GR_WAVES) {
+    const uint32_t lvl = __builtin_amdgcn_readfirstlane(sh.lvlist[it]);
+    const uint32_t start = __builtin_amdgcn_readfirstlane(sh.lstart[lvl]);
+    const uint32_t cnt = __builtin_amdgcn_readfirstlane(sh.lstart[lvl + 1]) - start;
+    const GrLevel& gl = sh.lv[lvl];
+    const unsigned long long C = rl64(gl.C, 0), T0 = rl64(gl.T0, 0);
+    const uint32_t newhead = auniu(gl.newhead), need = auniu(gl.need), ks = auniu(gl.ks);
+    const uint32_t nfreed = auniu(gl.nfreed), fr_base = auniu(gl.fr_base), d_off = auniu(gl.d_off);
+    const uint32_t own = min(need, nfreed);
+    const size_t li = lo_l + lvl;
+    const uint32_t head0 = auniu(sh.lhead[lvl]), tail0 = auniu(sh.ltail[lvl]);
+    const uint32_t te0 = newhead != NIL ? auniu((uint32_t)sh.ltend[lvl]) : 0u;
+    const uint32_t tailfree = newhead != NIL ? (uint32_t)ME_C - te0 : 0u;
+    auto newchunk = [&](uint32_t c) -> uint32_t {
+      return c < own ? ag.fr[fr_base + c] : ag.fr[alloc_base + d_off + (c - own)];
+    };
+    const bool exhausted = T0 != ~0ull;
+    const unsigned long long Cr = exhausted && C > T0 ? C - T0 : 0ull;
+    if (ks) {
+      unsigned long long RR = 0;
+      uint32_t g0 = 0;
+      for (uint32_t b = 0; b < cnt; b += 64) {
+        uint32_t er;
+        const AggEv E = entry(start, cnt, b, er);
+        const bool v = b + (uint32_t)lane < cnt;
+        const bool rs = v && (E.j & AGG_TAKE) == 0u;
+        const long long rq = rs ? (long long)E.qty : 0ll;
+        const long long inc = wave_incl_scan(rq);
+        const unsigned long long st0 = RR + (unsigned long long)(inc - rq), en = RR + (unsigned long long)inc;
+        const bool surv = rs && en > Cr;
+        const unsigned long long sm = __ballot(surv);
+        if (surv) {
+          const uint32_t gi = g0 + (uint32_t)__popcll(sm & lanemask_lt());
+          uint32_t chk, slt;
+          if (gi < tailfree) {
+            chk = tail0;
+            slt = te0 + gi;
+          } else {
+            const uint32_t gg = gi - tailfree;
+            chk = newchunk(gg / ME_C);
+            slt = gg % ME_C;
+          }
+          const unsigned long long sq = a_seq_of(src, E.j);
+          const int left = (int)(en - (st0 > Cr ? st0 : Cr));
+          if (chk < bk.nchunks) {
+            bk.chunks[chk].qty[slt] = left;
+            bk.chunks[chk].seq[slt] = sq;
+            bk.loc[sq & bk.ring_mask] = chk * ME_C + slt;
+          }
+        }
+        g0 += (uint32_t)__popcll(sm);
+        RR += (unsigned long long)rli64(inc, 63);
+      }
+    }
+    for (uint32_t c = lane; c < need; c += 64) {
+      const uint32_t chk = newchunk(c);
+      if (chk >= bk.nchunks) continue;
+      ChunkHdr h;
+      h.next = c + 1 < need ? newchunk(c + 1) : NIL;
+      h.prev = c ? newchunk(c - 1) : (newhead != NIL ? tail0 : NIL);
+      h.price = sl.base + (long long)lvl;
+      bk.chunks[chk].hdr = h;
+    }
+    const uint32_t first_new = need ? auniu(newchunk(0)) : NIL;
+    const uint32_t last_new = need ? auniu(newchunk(need - 1)) : NIL;
+    if (lane == 0) {
+      if (newhead != NIL && need && tail0 < bk.nchunks) bk.chunks[tail0].hdr.next = first_new;
+      if (newhead != NIL && newhead != head0 && newhead < bk.nchunks) bk.chunks[newhead].hdr.prev = NIL;
+      const uint32_t hd = newhead != NIL ? newhead : first_new;
+      const uint32_t tl = need ? last_new : (newhead != NIL ? tail0 : NIL);
+      const uint32_t te = need ? ((ks - tailfree - 1u) % ME_C) + 1u : (newhead != NIL ? te0 + ks : 0u);
+      bk.levels[li].head = hd;
+      bk.levels[li].tail = tl;
+      bk.tend[li] = (uint8_t)te;
+    }
+  }
+}
+
+__global__ __launch_bounds__(GR_THREADS) void k_agg_gres(BookDev bk, AggGArgs ga, AggSrc src, AggDev ag, uint32_t ne) {
+  __shared__ GrShared sh;
+  extern __shared__ uint32_t gr_dyn[];  // [ne] fill counts / offsets, then [ne] 16-bit sorted log indices
+  for (uint32_t s = blockIdx.x; s < bk.S; s += gridDim.x) {
+    const AggSlot sl = ag.slot[s];
+    if (!sl.active) continue;  // (uniform over the workgroup)
+    if (sl.ev_cnt >= 65536u) {  // 16-bit log indices: a grouped log is at most 3 x 32 x BK_CAP + L + 64 long
+      if (threadIdx.x == 0) atomicOr(bk.err, ERR_INCONSISTENT);
+      continue;
+    }
+    if (sl.ev_cnt <= ne)
+      gres_symbol<true>(bk, ga, src, ag, s, sl, sh, gr_dyn, reinterpret_cast<uint16_t*>(gr_dyn + ne));
+    else
+      gres_symbol<false>(bk, ga, src, ag, s, sl, sh, ag.evn + sl.ev_base, reinterpret_cast<uint16_t*>(ag.evs + sl.ev_base));
+    __syncthreads();
+  }
+}
+
 }  // namespace
 
 hipError_t launch_agg(hipStream_t hs, const BookDev& bk, const BatchDev& bt, const AggDev& ag0) {
@@ -1939,12 +2601,28 @@ hipError_t launch_agg_group(hipStream_t st, const BookDev& bk, const BatchDev* b
   ga.ng = ng;
   const uint32_t grid = bk.S < 2048u ? bk.S : 2048u;
   hipLaunchKernelGGL(k_agg_gwalk, dim3(grid), dim3(64), 0, st, bk, ga, ag);
-  hipLaunchKernelGGL(k_agg_group, dim3(grid), dim3(1024), (size_t)bk.L * 4u + AGG_GCHUNK * 2u, st, bk, ag);
-  hipLaunchKernelGGL(k_agg_levels, dim3(2048), dim3(256), 0, st, bk, src, ag);
-  hipLaunchKernelGGL(k_agg_alloc, dim3(grid), dim3(64), 0, st, bk, ag);
-  hipLaunchKernelGGL(k_agg_place, dim3(2048), dim3(256), 0, st, bk, src, ag);
-  hipLaunchKernelGGL(k_agg_gfin, dim3(grid), dim3(1024), 0, st, bk, ga, ag);
-  hipLaunchKernelGGL(k_agg_gemit, dim3(grid), dim3(1024), 0, st, bk, ga, src, ag);
+  static const bool multi = [] {  // ME_AGG_GRES=0: the six per-phase kernels (same-box A/B only)
+    const char* v = getenv("ME_AGG_GRES");
+    return v && atoi(v) == 0;
+  }();
+  if (multi) {
+    hipLaunchKernelGGL(k_agg_group, dim3(grid), dim3(1024), (size_t)bk.L * 4u + AGG_GCHUNK * 2u, st, bk, ag);
+    hipLaunchKernelGGL(k_agg_levels, dim3(2048), dim3(256), 0, st, bk, src, ag);
+    hipLaunchKernelGGL(k_agg_alloc, dim3(grid), dim3(64), 0, st, bk, ag);
+    hipLaunchKernelGGL(k_agg_place, dim3(2048), dim3(256), 0, st, bk, src, ag);
+    hipLaunchKernelGGL(k_agg_gfin, dim3(grid), dim3(1024), 0, st, bk, ga, ag);
+    hipLaunchKernelGGL(k_agg_gemit, dim3(grid), dim3(1024), 0, st, bk, ga, src, ag);
+    return hipGetLastError();
+  }
+  // per-event LDS arrays (6 B per event) sized for ~2.75 events per record of the group's mean symbol plus
+  // slack; a longer log keeps them in HBM. Capped so the workgroup's LDS stays within 64 KB.
+  uint64_t recs = 0;
+  for (uint32_t g = 0; g < ng; ++g) recs += bt[g].n;
+  uint64_t ne = (recs * 11u / 4u) / (bk.S ? bk.S : 1u) + 320u;
+  ne = (ne + 63u) & ~63ull;
+  const uint64_t ne_cap = ((64u << 10) - sizeof(GrShared)) / 6u & ~63ull;
+  if (ne > ne_cap) ne = ne_cap;
+  hipLaunchKernelGGL(k_agg_gres, dim3(grid), dim3(GR_THREADS), (size_t)ne * 6u, st, bk, ga, src, ag, (uint32_t)ne);
   return hipGetLastError();
 }
 }  // namespace me
