@@ -80,8 +80,11 @@ def parse():
     ap.add_argument("--batches-per-launch", type=int, default=0,
                     help="batches matched per kernel launch (me_config.batches_per_launch; 0 = engine default 32)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample")
-    ap.add_argument("--cpu-threads", type=int, default=min(16, os.cpu_count() or 1),
-                    help="threads of the sharded CPU baseline (the GPU box's CPU share is 16); 1 = scalar only")
+    ap.add_argument("--cpu-threads", type=int, default=len(os.sched_getaffinity(0)),
+                    help="threads of the sharded CPU baseline (default: every core this process may run on, "
+                         "SURVEY.md §8(d)); 1 = scalar only")
+    ap.add_argument("--cpu-threads-alt", type=int, default=16,
+                    help="a second sharded CPU run at this many threads, reported beside the first (0 = none)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--e2e-steps", type=int, default=384,
@@ -94,8 +97,9 @@ def parse():
     ap.add_argument("--cluster-steps", type=int, default=None,
                     help="global slices run after the timed loop through the C++ sharded deployment "
                          "(include/me_cluster.h: split on rank 0, RCCL scatter, match, RCCL gather of tapes and "
-                         "results, merge by taker seq); reported beside value, never in it. Default: 16 at N > 1, "
-                         "0 at N = 1")
+                         "results, merge by taker seq); reported beside value, never in it. Default: 16 at N > 1 "
+                         "or with --workload c3, else 0. c3's slices have config 3's global shape (1,048,576 "
+                         "orders over 100,000 symbols) at every N")
     ap.add_argument("--traffic-from", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="JSON {bytes_per_order: ...} from tools/gpu/pmc_traffic_wl.sh for roofline.traffic (c2; the "
                          "k_match_reg measurement when the engine runs c2 without grouped aggregate launches)")
@@ -233,41 +237,49 @@ def cpu_baseline(args):
     out = {"value": one, "unit": "orders/s", "cores": 1, "kind": "port",
            "sample": f"first {k} batches ({done} orders) of the {args.workload} stream, oracle/oracle_book.cpp "
                      f"scalar price-time book, {t_cpu:.1f}s{seeded}"}
-    T = args.cpu_threads
+
+    def sharded(T):
+        """The same k batches on T threads, symbols hash-sharded (one book per thread): orders/s of the wall."""
+        st, seeds = seeded_stream()
+        from matching_engine_amd.sharding import ShardPlan
+
+        plan = ShardPlan(S, T)
+        books = [OracleBook(len(plan.members[r])) for r in range(T)]
+        if seeds is not None:
+            for i in range(0, len(seeds), 1 << 20):
+                for r, (lb, _) in enumerate(plan.split(seeds.take(slice(i, i + (1 << 20))))):
+                    books[r].submit(lb)
+        parts = [[] for _ in range(T)]
+        for _ in range(k):
+            for r, (lb, _) in enumerate(plan.split(st.next(sc.batch))):
+                parts[r].append(lb)
+
+        def run(r):
+            for lb in parts[r]:
+                books[r].submit(lb)
+
+        th = [threading.Thread(target=run, args=(r,)) for r in range(T)]
+        t0 = time.perf_counter()
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        tw = time.perf_counter() - t0
+        for bk in books:
+            bk.close()
+        return done / tw, tw
+
+    T = min(args.cpu_threads, S)  # (a thread without a symbol would idle)
     if T <= 1:
         return out
-    # ---- T threads, symbols hash-sharded (the same prefix length as the 1-thread sample)
-    st, seeds = seeded_stream()
-    from matching_engine_amd.sharding import ShardPlan
-
-    plan = ShardPlan(S, T)
-    base = st.base_prices()
-    books = [OracleBook(len(plan.members[r])) for r in range(T)]
-    if seeds is not None:
-        for i in range(0, len(seeds), 1 << 20):
-            for r, (lb, _) in enumerate(plan.split(seeds.take(slice(i, i + (1 << 20))))):
-                books[r].submit(lb)
-    parts = [[] for _ in range(T)]
-    for _ in range(k):
-        for r, (lb, _) in enumerate(plan.split(st.next(sc.batch))):
-            parts[r].append(lb)
-
-    def run(r):
-        for lb in parts[r]:
-            books[r].submit(lb)
-
-    th = [threading.Thread(target=run, args=(r,)) for r in range(T)]
-    t0 = time.perf_counter()
-    for t in th:
-        t.start()
-    for t in th:
-        t.join()
-    tw = time.perf_counter() - t0
-    for bk in books:
-        bk.close()
-    out.update({"value": done / tw, "cores": T, "single_core_value": one,
-                "sample": out["sample"] + f"; then the same {k} batches on {T} threads, symbols hash-sharded "
-                          f"(one book per thread), {tw:.1f}s wall"})
+    v, tw = sharded(T)
+    out.update({"value": v, "cores": T, "single_core_value": one,
+                "sample": out["sample"] + f"; then the same {k} batches on {T} threads (every core of the process's "
+                          f"affinity mask), symbols hash-sharded (one book per thread), {tw:.2f}s wall"})
+    Ta = min(args.cpu_threads_alt, S)
+    if Ta > 1 and Ta != T:
+        va, _ = sharded(Ta)
+        out["alt"] = {"value": va, "cores": Ta}
     return out
 
 
@@ -389,7 +401,7 @@ def host_info():
             "cpus_allowed": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None}
 
 
-def cluster_leg(args, world, rank, local, sc, base, slices):
+def cluster_leg(args, world, rank, local, sc, base, slices, n_slices):
     """N > 1: the sharded deployment as a server runs it — rank 0 submits each global slice to
     me_cluster (split by symbol owner, parts scattered over RCCL, matched on every GPU, tapes and results
     gathered back over RCCL and merged by taker seq), two slices in flight; the other ranks serve. Its
@@ -401,7 +413,7 @@ def cluster_leg(args, world, rank, local, sc, base, slices):
     transport = "rccl" if (world == 1 or tdist.get_backend() == "nccl") else "tcp"
     port = int(os.environ.get("MASTER_PORT", "29500")) + 11
     cl = Cluster(rank, world, len(base), sc.batch, transport=transport, port=port, device=local, levels=sc.levels,
-                 base_prices=base, max_resting=sc.batch * (len(slices) + 1), timeout_ms=120000,
+                 base_prices=base, max_resting=sc.batch * (n_slices + 1), timeout_ms=120000,
                  seq_ring=args.seq_ring, batches_per_launch=2)
     out = None
     if rank == 0:
@@ -417,13 +429,18 @@ def cluster_leg(args, world, rank, local, sc, base, slices):
             fills += len(cl.collect(t, k)[1])
         dt = time.perf_counter() - t0
         st = cl.stats()
+        ph = cl.phases()
         cl.stop()
-        out = {"transport": transport, "slices": len(slices), "orders": n, "fills": fills,
-               "orders_per_s": n / dt, "ms_per_slice": dt / len(slices) * 1e3, "bytes_rank0": st["bytes"],
-               "what": "me_cluster_submit / me_cluster_collect (C++, include/me_cluster.h), two slices in flight: "
-                       "split on rank 0, grouped ncclSend/ncclRecv of the parts, admission vote (MIN "
-                       "all-reduce), match on every GPU, gather of tape lengths, grouped send of tapes + results "
-                       "to rank 0, k-way merge by taker seq on rank 0's host"}
+        out = {"transport": transport, "slices": len(slices), "slice_orders": sc.batch, "symbols": len(base),
+               "orders": n, "fills": fills, "orders_per_s": n / dt, "ms_per_slice": dt / len(slices) * 1e3,
+               "bytes_rank0": st["bytes"],
+               "phase_ms_per_slice_rank0": {k: round(v / len(slices) * 1e3, 4) for k, v in ph.items()},
+               "what": "me_cluster_submit / me_cluster_collect (C++, include/me_cluster.h), two slices in flight, "
+                       "host slices in and merged host outputs out (the persistence root's view): split on rank 0 "
+                       "(its own part packed straight into its engine's pinned slot inputs), grouped "
+                       "ncclSend/ncclRecv of the other parts, admission vote (MIN all-reduce), match on every GPU, "
+                       "gather of tape lengths, grouped send of tapes + results to rank 0, results back to slice "
+                       "order and tapes by taker on rank 0's host (world 1: the slot's outputs in place)"}
     else:
         cl.serve()
     cl.close()
@@ -441,10 +458,17 @@ def main():
     import torch
 
     nb = args.warmup + args.steps
-    n_cluster = args.cluster_steps if args.cluster_steps is not None else (16 if world > 1 else 0)
+    n_cluster = args.cluster_steps if args.cluster_steps is not None else (
+        16 if world > 1 or args.workload == "c3" else 0)
     n_e2e = 0 if args.no_e2e else args.e2e_steps
     sc, gbase, ids, batches, positions, global_orders, seeds, whole = build_rank_batches(
-        args, world, rank, nb + n_e2e, n_cluster)
+        args, world, rank, nb + n_e2e, 0 if args.workload == "c3" else n_cluster)
+    csc, cbase = sc, gbase
+    if n_cluster and args.workload == "c3":  # config 3's global slice shape, the same at every N
+        csc = me.preset(3, num_symbols=100_000, batch=1 << 20)
+        cst = me.Stream(csc)
+        cbase = cst.base_prices()
+        whole = [cst.next(csc.batch) for _ in range(n_cluster)] if rank == 0 else []
     base = gbase[ids]
     e2e_batches = batches[nb:]
     batches = batches[:nb]
@@ -603,7 +627,7 @@ def main():
         wd.daemon = True
         wd.start()
         try:
-            got = cluster_leg(args, world, rank, local, sc, gbase, whole)
+            got = cluster_leg(args, world, rank, local, csc, cbase, whole, n_cluster)
         except Exception as ex:  # reported, never fatal to the measured line
             got = {"error": f"{type(ex).__name__}: {ex}"}
         wd.cancel()

@@ -97,7 +97,7 @@ int me_cluster_serve(me_cluster* c);
  * shard's admission control refused its part (nothing of it was applied anywhere). At most two
  * tickets outstanding. collect: the merged outputs of the oldest ticket, exactly what one engine
  * holding every symbol returns (tape ordered by taker seq, results in slice order); valid until the
- * next collect. match = submit + collect. */
+ * next collect (at world 1 they are rank 0's engine slot outputs, in place). match = submit + collect. */
 int me_cluster_submit(me_cluster* c, const me_order_soa* slice, size_t n, uint64_t* ticket);
 int me_cluster_collect(me_cluster* c, uint64_t ticket, const me_fill** fills, size_t* n_fills,
                        const me_order_result** results);
@@ -117,6 +117,12 @@ int me_cluster_matcher(me_cluster* c, me_matcher* out);
 
 /* Counters: slices matched, bytes moved by the transport (this rank, both directions). */
 int me_cluster_stats(const me_cluster* c, uint64_t* slices, uint64_t* bytes);
+/* Rank 0's wall time per protocol phase since create, in seconds: [0] split (owner counts, stable pack:
+ * rank 0's part straight into its engine's pinned slot inputs), [1] control (command broadcast), [2]
+ * scatter (H2D + parts over the transport), [3] admission vote, [4] match (enqueue on every shard), [5]
+ * collect (rank 0's own outputs: waits for its engine), [6] gather (sizes, tapes and results to rank 0,
+ * D2H), [7] merge (results to slice order, tapes by taker). Writes min(n, 8) values, returns 8. */
+int me_cluster_phases(const me_cluster* c, double* seconds, size_t n);
 int me_cluster_last_error(const me_cluster* c, char* buf, size_t cap);
 
 #ifdef __cplusplus

@@ -358,5 +358,6 @@ PROTOTYPES.update({
     "me_cluster_snapshot": (C.c_int, [_P, C.c_uint32, _P, _P]),
     "me_cluster_matcher": (C.c_int, [_P, C.POINTER(MeMatcher)]),
     "me_cluster_stats": (C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "me_cluster_phases": (C.c_int, [_P, C.POINTER(C.c_double), _SZ]),
     "me_cluster_last_error": (C.c_int, [_P, C.c_char_p, _SZ]),
 })

@@ -254,3 +254,11 @@ class Cluster:
         s, b = C.c_uint64(0), C.c_uint64(0)
         self.lib.me_cluster_stats(self.h, C.byref(s), C.byref(b))
         return {"slices": s.value, "bytes": b.value}
+
+    PHASES = ("split", "control", "scatter", "vote", "match", "collect", "gather", "merge")
+
+    def phases(self) -> dict:
+        """Rank 0's seconds per protocol phase since create (me_cluster_phases)."""
+        v = (C.c_double * len(self.PHASES))()
+        self.lib.me_cluster_phases(self.h, v, len(self.PHASES))
+        return dict(zip(self.PHASES, list(v)))

@@ -75,6 +75,16 @@ __device__ __forceinline__ void a_drain() {
   wave_mem_order();
 }
 
+// Diagnostic build (-DME_STAMPS): absolute s_memtime stamps per symbol into bk.dbg[s * 24 + 16 + k]
+// (16 walk start, 17 walk end, 18 k_agg_gres start, 19..23 its phases A, B, C, D1, D2 done), read by
+// tools/gres_probe.py. The product build compiles them away.
+#ifdef ME_STAMPS
+#define GR_STAMP(bk, s, k) \
+  do { if (threadIdx.x == 0) (bk).dbg[(size_t)(s) * 24u + 16u + (k)] = stamp_now(); } while (0)
+#else
+#define GR_STAMP(bk, s, k) ((void)0)
+#endif
+
 // ------------------------------------------------------------------ the level-total walk
 // Top of one side, best first: a ring over the lanes, entry i in lane (f + i) & 63. Side coordinates:
 // asks m = level, bids m = L - 1 - level, so "better" is "smaller" on both sides. The list is always
@@ -1561,6 +1571,7 @@ struct AggGArgs {
   me_fill* scratch[ME_GMAX];
   unsigned long long* scratch_top[ME_GMAX];
   unsigned long long ovf_base, scratch_cap;
+  const uint64_t* seq0;  // the group's first record's seq (k_agg_gres: events carry their seq's offset from it)
   uint32_t slab, ng;
 };
 
@@ -1655,6 +1666,7 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
       *slot = o;
     }
     if (!total) continue;
+    GR_STAMP(bk, s, 0);
     if (!eok || !a_reserve(ag, slot, resting, total)) {  // no room in the pools: the whole group of the
                                                           // symbol goes to the continuation
       const uint32_t g0 = (uint32_t)__builtin_ctzll(__ballot(nsv != 0u));
@@ -1754,6 +1766,7 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
       slot->hidx = hidx;
       slot->pos = gstop;  // the batch the continuation starts in (ng: none)
     }
+    GR_STAMP(bk, s, 1);
   }
 }
 
@@ -1897,27 +1910,33 @@ __global__ __launch_bounds__(1024) void k_agg_gemit(BookDev bk, AggGArgs ga, Agg
 // k_agg_gres does the work of k_agg_group ... k_agg_gemit for a grouped launch in ONE launch, one 512-thread
 // workgroup per symbol (the walk's workgroup of the same symbol ran on the same XCD, blockIdx = symbol):
 //   A  the symbol's log sorted by level in LDS (per-wave histograms of contiguous log ranges, a stable
-//      ballot-multisplit scatter of 16-bit log indices) — no sorted copies, segment tables or per-event
-//      arrays in HBM;
+//      ballot-multisplit scatter of 16-bit log indices); each event's seq gathered once, in parallel, into
+//      the event itself (its offset from the group's first seq) — no sorted copies, segment tables or
+//      per-event arrays in HBM;
 //   B  its levels resolved by the waves (a level per wave, taken from an LDS counter): the initial FIFO
-//      walked until the batch's takes are covered, consumed makers, emptied chunks, each take's fill count
+//      walked until the group's takes are covered, consumed makers, emptied chunks, each take's fill count
 //      into an LDS array indexed by log position; the slot's cursors are LDS atomics, not pool-wide ones;
-//   C  the fill offsets (exclusive scan of the fill counts in log order = tape order, in place in LDS), each
-//      batch's scratch base, the records' fill counts and scratch starts;
-//   D  the chunk allocation (wave 0) beside the fills of every take (the other waves), then the surviving
-//      rests placed into the levels' tails and new chunks.
+//   C  the fill offsets (exclusive scan of the fill counts in log order = tape order, in place, each wave
+//      over its log range), each batch's scratch base, the records' fill counts and scratch starts;
+//   D  the chunk allocation (wave 0), then per level in one pass over its events: the fills of its takes and
+//      the surviving rests placed into the level's tail and new chunks.
 // The per-event LDS arrays hold `ne` events (the launch sizes them from the group's mean records per
 // symbol); a symbol with a longer log keeps them in the log's own HBM regions (AggDev::evn / evs) instead.
+// ~16 KB of static LDS and a register budget of GR_WPE waves per SIMD.
 constexpr int GR_WAVES = 8;
 constexpr uint32_t GR_THREADS = GR_WAVES * 64;
+#ifndef GR_WPE
+#define GR_WPE 6  // waves per SIMD the register budget is cut for (same-box A/B: 5 / 6 / 8)
+#endif
+constexpr uint32_t GR_STAGE = 48;  // consumed makers / emptied chunks a level stages in LDS (else: HBM)
 
 struct GrLevel {  // what phase B found for one level
   unsigned long long C, T0;
   uint32_t newhead, mk_base, nmk, fr_base, nfreed, need, d_off, ks;
 };
 struct GrStage {  // a wave's maker / emptied-chunk staging (phases B and D)
-  AggMk mk[LV_STAGE];
-  uint32_t fr[LV_STAGE];
+  AggMk mk[GR_STAGE];
+  uint32_t fr[GR_STAGE];
 };
 struct GrShared {
   union {
@@ -1930,7 +1949,7 @@ struct GrShared {
   uint32_t lvlist[128];
   uint32_t gev[ME_GMAX + 1], gex[ME_GMAX + 1], gbase[ME_GMAX + 1];
   uint32_t wsum[GR_WAVES];
-  uint32_t nlv, next, next2, cur_mk, cur_fr, deficit, alloc_base, free_head;
+  uint32_t nlv, next, next2, cur_mk, cur_fr, deficit, alloc_base;
   int dresting;
   uint8_t ltend[128];
 };
@@ -1948,8 +1967,11 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint32_t L = bk.L;  // <= 128
   const uint32_t eb = sl.ev_base, n = sl.ev_cnt, ng = ga.ng;
-  const AggEv* ev = ag.ev + eb;
+  AggEv* ev = ag.ev + eb;
   const size_t lo_l = (size_t)s * L;
+  // every seq of the group lies in [gmin, gmin + seq_ring) (k_seq_sweep's check; seq_ring <= 2^32 here)
+  const unsigned long long gmin = *ga.seq0;
+  GR_STAMP(bk, s, 2);
   // ---- A: level heads (one coalesced load), the batches' log boundaries, the scalars
   if ((uint32_t)tid < L) {
     const Level v = bk.levels[lo_l + tid];
@@ -1966,12 +1988,19 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
   sh.u.wh[wv][lane] = 0u;
   sh.u.wh[wv][64 + lane] = 0u;
   wave_mem_order();
-  // per-wave histograms of contiguous log ranges (64-aligned), then a stable scatter with the same ranges
+  // each wave owns a contiguous 64-aligned log range: its level histogram, the events' seqs (into the
+  // events' pad: offset from gmin), then a stable scatter of the same range
   const uint32_t per = ((n + GR_WAVES - 1u) / GR_WAVES + 63u) & ~63u;
   const uint32_t r0 = min(n, (uint32_t)wv * per), r1 = min(n, r0 + per);
+#pragma unroll 4
   for (uint32_t b = r0; b < r1; b += 64) {
     const uint32_t e = b + (uint32_t)lane;
-    if (e < r1) atomicAdd(&sh.u.wh[wv][ev[e].lvl & 127u], 1u);
+    if (e < r1) {
+      const AggEv E = ev[e];
+      atomicAdd(&sh.u.wh[wv][E.lvl & 127u], 1u);
+      const uint32_t j = E.j & ~AGG_TAKE;
+      ev[e].pad = (uint32_t)(src.seq[j >> AGG_GSHIFT][j & AGG_IMASK] - gmin);
+    }
   }
   __syncthreads();
   if (wv == 0) {
@@ -2017,6 +2046,7 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
     wave_mem_order();
   }
   __syncthreads();
+  GR_STAMP(bk, s, 3);
   // ---- B: the levels
   const uint32_t nlv = sh.nlv;
   const bool act = lane < ME_C;
@@ -2085,14 +2115,14 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
       const bool cons = q > 0 && W + ex < C;
       const unsigned long long cm = __ballot(cons);
       const uint32_t r = nmk + (uint32_t)__popcll(cm & lanemask_lt());
-      if (cons && r < LV_STAGE) {
+      if (cons && r < GR_STAGE) {
         mkl[r].seq = sq;
         mkl[r].end = en;
       }
       nmk += (uint32_t)__popcll(cm);
       nfull += (uint32_t)__popcll(__ballot(q > 0 && en <= C));
       if (W + live <= C) {  // emptied
-        if (lane == 0 && nfreed < LV_STAGE) frl[nfreed] = ch;
+        if (lane == 0 && nfreed < GR_STAGE) frl[nfreed] = ch;
         ++nfreed;
         W += live;
         ch = nx;
@@ -2121,8 +2151,8 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
         const bool cons = rs && st0 < Cr;
         const unsigned long long cm = __ballot(cons);
         const uint32_t r = nmk + nrc + (uint32_t)__popcll(cm & lanemask_lt());
-        if (cons && r < LV_STAGE) {
-          mkl[r].seq = a_seq_of(src, E.j);
+        if (cons && r < GR_STAGE) {
+          mkl[r].seq = gmin + E.pad;
           mkl[r].end = T0 + en;
         }
         nrc += (uint32_t)__popcll(cm);
@@ -2162,8 +2192,8 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
       wave_mem_order();
       continue;
     }
-    const bool staged = nmkt <= LV_STAGE && nfreed <= LV_STAGE;
-    // 4. makers and emptied chunks to HBM: from LDS, or past LV_STAGE by a second read of the FIFO
+    const bool staged = nmkt <= GR_STAGE && nfreed <= GR_STAGE;
+    // 4. makers and emptied chunks to HBM: from LDS, or past GR_STAGE by a second read of the FIFO
     wave_mem_order();
     if (staged) {
       if ((uint32_t)lane < nmkt) ag.mk[mk_base + lane] = mkl[lane];
@@ -2208,7 +2238,7 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
           const unsigned long long cm = __ballot(cons);
           if (cons) {
             AggMk m;
-            m.seq = a_seq_of(src, E.j);
+            m.seq = gmin + E.pad;
             m.end = T0 + en;
             ag.mk[mk_base + mi + (uint32_t)__popcll(cm & lanemask_lt())] = m;
           }
@@ -2265,26 +2295,33 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
     wave_mem_order();  // the next level reuses the staging
   }
   __syncthreads();
-  // ---- C: fill offsets in log order (exclusive scan of nf in place), each batch's scratch base
-  uint32_t carry = 0;
-  for (uint32_t t0 = 0; t0 < n; t0 += GR_THREADS) {
-    const uint32_t e = t0 + (uint32_t)tid;
-    const uint32_t c = e < n ? nf[e] : 0u;
-    const uint32_t x = (uint32_t)wave_incl_scan((long long)c);
-    if (lane == 63) sh.wsum[wv] = x;
-    __syncthreads();
-    uint32_t pre = 0, tot = 0;
-#pragma unroll
-    for (int k = 0; k < GR_WAVES; ++k) {
-      const uint32_t w = sh.wsum[k];
-      pre += k < wv ? w : 0u;
-      tot += w;
+  GR_STAMP(bk, s, 4);
+  // ---- C: fill offsets in log order (exclusive scan of nf in place, each wave over its log range)
+  {
+    uint32_t sum = 0;
+    for (uint32_t b = r0; b < r1; b += 64) {
+      const uint32_t e = b + (uint32_t)lane;
+      sum += e < r1 ? nf[e] : 0u;
     }
-    if (e < n) nf[e] = carry + pre + x - c;
-    carry += tot;
-    __syncthreads();
+    sum = (uint32_t)rli64(wave_incl_scan((long long)sum), 63);
+    if (lane == 0) sh.wsum[wv] = sum;
   }
-  const uint32_t ftot = carry;
+  __syncthreads();
+  uint32_t ftot = 0, base = 0;
+#pragma unroll
+  for (int k = 0; k < GR_WAVES; ++k) {
+    const uint32_t w = sh.wsum[k];
+    base += k < wv ? w : 0u;
+    ftot += w;
+  }
+  for (uint32_t b = r0; b < r1; b += 64) {
+    const uint32_t e = b + (uint32_t)lane;
+    const uint32_t c = e < r1 ? nf[e] : 0u;
+    const uint32_t inc = (uint32_t)wave_incl_scan((long long)c);
+    if (e < r1) nf[e] = base + inc - c;
+    base += rl32(inc, 63);
+  }
+  __syncthreads();
   auto EX = [&](uint32_t e) -> uint32_t { return e < n ? nf[e] : ftot; };
   if ((uint32_t)tid < ng) {  // each batch's fills: the symbol's slab of that batch if they fit, else overflow
     const uint32_t g = (uint32_t)tid;
@@ -2302,18 +2339,33 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
     sh.gbase[g] = (uint32_t)b0;
   }
   __syncthreads();
-  // the first take of each record: its fill count and scratch start
-  for (uint32_t t = (uint32_t)tid; t < n; t += GR_THREADS) {
-    const uint32_t j = ev[t].j;
-    if (!(j & AGG_TAKE) || (t > 0 && ev[t - 1].j == j)) continue;
-    const uint32_t g = (j & ~AGG_TAKE) >> AGG_GSHIFT, oi = j & AGG_IMASK;
-    uint32_t nte = 1;  // the record's take events follow each other in the log
-    while (t + nte < n && ev[t + nte].j == j) ++nte;
-    const uint32_t x0 = EX(t), nfill = EX(t + nte) - x0;
-    me_order_result* res = ga.res[g];
-    res[oi].fill_count = nfill;
-    res[oi].tape_offset = sh.gbase[g] + (x0 - sh.gex[g]);
-    if (nfill) atomicAdd(&ga.tile_sum[g][oi / TILE_TAPE], nfill);
+  // the first take event of each record (the records' events are consecutive in the log): its fill count
+  // and scratch start; each wave over its log range, 64 events at a time
+  {
+    uint32_t prevj = r0 > 0 && r0 < r1 ? auniu(ev[r0 - 1].j) : NIL;
+    for (uint32_t b = r0; b < r1; b += 64) {
+      const uint32_t e = b + (uint32_t)lane;
+      const bool v = e < r1;
+      const uint32_t j = v ? ev[e].j : NIL;
+      uint32_t pj = (uint32_t)__shfl_up((int)j, 1, 64);
+      pj = lane == 0 ? prevj : pj;
+      uint32_t nj = (uint32_t)__shfl_down((int)j, 1, 64);
+      nj = lane == 63 ? NIL : nj;
+      const unsigned long long same = __ballot(v && nj == j);  // bit k: event k + 1 continues k's run
+      prevj = rl32(j, 63);
+      if (v && (j & AGG_TAKE) && pj != j) {
+        // the record's take events: the run of j from here (lane 63's bit is clear)
+        uint32_t nte = (uint32_t)__builtin_ctzll(~(same >> lane)) + 1u;
+        if (lane + (int)nte == 64)
+          while (e + nte < n && ev[e + nte].j == j) ++nte;  // the run goes past this block
+        const uint32_t g = (j & ~AGG_TAKE) >> AGG_GSHIFT, oi = j & AGG_IMASK;
+        const uint32_t x0 = EX(e), nfill = EX(e + nte) - x0;
+        me_order_result* res = ga.res[g];
+        res[oi].fill_count = nfill;
+        res[oi].tape_offset = sh.gbase[g] + (x0 - sh.gex[g]);
+        if (nfill) atomicAdd(&ga.tile_sum[g][oi / TILE_TAPE], nfill);
+      }
+    }
   }
   if (tid == 0 && sl.hidx != NIL) {  // the continuation goes on behind the walk's fills of its batch
     const uint32_t g = sl.pos;
@@ -2322,7 +2374,8 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
     bk.hand[sl.hidx].wptr = b0 + f;
     bk.hand[sl.hidx].wend = f <= ga.slab ? s * ga.slab + ga.slab : b0 + f;
   }
-  // ---- D1: chunk allocation (wave 0) beside the fills (the other waves)
+  GR_STAMP(bk, s, 5);
+  // ---- D: chunk allocation (wave 0); the symbol's state
   if (wv == 0) {
     uint32_t D = sh.deficit, fh = sl.free_head;
     uint32_t Stot = 0;
@@ -2407,59 +2460,14 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
       bk.sym[s] = o;
       if (dr) atomicAdd(bk.stats + ST_RESTING, (unsigned long long)(long long)dr);
     }
-  } else {
-    // the fills of every take: makers of its level overlapping its interval, at the record's scratch position
-    for (uint32_t it = gr_take(&sh.next2); it < nlv; it = gr_take(&sh.next2)) {
-      const uint32_t lvl = __builtin_amdgcn_readfirstlane(sh.lvlist[it]);
-      const uint32_t nmk = __builtin_amdgcn_readfirstlane(sh.lv[lvl].nmk);
-      if (!nmk) continue;
-      const uint32_t start = __builtin_amdgcn_readfirstlane(sh.lstart[lvl]);
-      const uint32_t cnt = __builtin_amdgcn_readfirstlane(sh.lstart[lvl + 1]) - start;
-      const uint32_t mk_base = __builtin_amdgcn_readfirstlane(sh.lv[lvl].mk_base);
-      const bool staged = nmk <= LV_STAGE;
-      if (staged && (uint32_t)lane < nmk) mkl[lane] = ag.mk[mk_base + lane];
-      wave_mem_order();
-      const long long price = sl.base + (long long)lvl;
-      unsigned long long A0 = 0;
-      for (uint32_t b = 0; b < cnt; b += 64) {
-        uint32_t er;
-        const AggEv E = entry(start, cnt, b, er);
-        const bool v = b + (uint32_t)lane < cnt;
-        const bool tk = v && (E.j & AGG_TAKE) != 0u;
-        const long long tq = tk ? (long long)E.qty : 0ll;
-        const long long inc = wave_incl_scan(tq);
-        if (tk) {
-          const uint32_t x0 = nf[er], nfl = EX(er + 1) - x0;
-          if (nfl) {
-            const unsigned long long a = A0 + (unsigned long long)(inc - tq), z = a + (unsigned long long)E.qty;
-            const uint32_t first = staged ? a_search_lds(mkl, nmk, a, true) : a_search(ag.mk, mk_base, nmk, a, true);
-            const uint32_t j = E.j & ~AGG_TAKE, g = j >> AGG_GSHIFT;
-            const uint32_t p = sh.gbase[g] + (x0 - sh.gex[g]);
-            me_fill f;
-            f.taker_seq = a_seq_of(src, j);
-            f.price_q4 = price;
-            f.symbol = sl.gs;
-            me_fill* sc = ga.scratch[g];
-            unsigned long long lo = a;
-            for (uint32_t k = 0; k < nfl; ++k) {
-              const AggMk m = staged ? mkl[first + k] : ag.mk[mk_base + first + k];
-              const unsigned long long hi = m.end < z ? m.end : z;
-              f.maker_seq = m.seq;
-              f.qty = (int)(hi - lo);
-              sc[p + k] = f;
-              lo = hi;
-            }
-          }
-        }
-        A0 += (unsigned long long)rli64(inc, 63);
-      }
-      wave_mem_order();  // the next level reuses the staging
-    }
   }
   __syncthreads();
-  // ---- D2: the surviving rests into the levels' tail chunks and new chunks; heads, tails, tail fills
+  GR_STAMP(bk, s, 6);
+  // ---- D: per level, one pass over its events: the fills of its takes (makers overlapping each take's
+  //      interval, at the record's scratch position) and its surviving rests into the tail chunk and new
+  //      chunks; the new chunks' headers, the level's head / tail / tail fill
   const uint32_t alloc_base = sh.alloc_base;
-  for (uint32_t it = (uint32_t)wv; it < nlv; it += GR_WAVES) {
+  for (uint32_t it = gr_take(&sh.next2); it < nlv; it = gr_take(&sh.next2)) {
     const uint32_t lvl = __builtin_amdgcn_readfirstlane(sh.lvlist[it]);
     const uint32_t start = __builtin_amdgcn_readfirstlane(sh.lstart[lvl]);
     const uint32_t cnt = __builtin_amdgcn_readfirstlane(sh.lstart[lvl + 1]) - start;
@@ -2467,6 +2475,7 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
     const unsigned long long C = rl64(gl.C, 0), T0 = rl64(gl.T0, 0);
     const uint32_t newhead = auniu(gl.newhead), need = auniu(gl.need), ks = auniu(gl.ks);
     const uint32_t nfreed = auniu(gl.nfreed), fr_base = auniu(gl.fr_base), d_off = auniu(gl.d_off);
+    const uint32_t nmk = auniu(gl.nmk), mk_base = auniu(gl.mk_base);
     const uint32_t own = min(need, nfreed);
     const size_t li = lo_l + lvl;
     const uint32_t head0 = auniu(sh.lhead[lvl]), tail0 = auniu(sh.ltail[lvl]);
@@ -2477,41 +2486,68 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
     };
     const bool exhausted = T0 != ~0ull;
     const unsigned long long Cr = exhausted && C > T0 ? C - T0 : 0ull;
-    if (ks) {
-      unsigned long long RR = 0;
-      uint32_t g0 = 0;
-      for (uint32_t b = 0; b < cnt; b += 64) {
-        uint32_t er;
-        const AggEv E = entry(start, cnt, b, er);
-        const bool v = b + (uint32_t)lane < cnt;
-        const bool rs = v && (E.j & AGG_TAKE) == 0u;
-        const long long rq = rs ? (long long)E.qty : 0ll;
-        const long long inc = wave_incl_scan(rq);
-        const unsigned long long st0 = RR + (unsigned long long)(inc - rq), en = RR + (unsigned long long)inc;
-        const bool surv = rs && en > Cr;
-        const unsigned long long sm = __ballot(surv);
-        if (surv) {
-          const uint32_t gi = g0 + (uint32_t)__popcll(sm & lanemask_lt());
-          uint32_t chk, slt;
-          if (gi < tailfree) {
-            chk = tail0;
-            slt = te0 + gi;
-          } else {
-            const uint32_t gg = gi - tailfree;
-            chk = newchunk(gg / ME_C);
-            slt = gg % ME_C;
-          }
-          const unsigned long long sq = a_seq_of(src, E.j);
-          const int left = (int)(en - (st0 > Cr ? st0 : Cr));
-          if (chk < bk.nchunks) {
-            bk.chunks[chk].qty[slt] = left;
-            bk.chunks[chk].seq[slt] = sq;
-            bk.loc[sq & bk.ring_mask] = chk * ME_C + slt;
+    const bool staged = nmk <= GR_STAGE;
+    if (nmk && staged && (uint32_t)lane < nmk) mkl[lane] = ag.mk[mk_base + lane];
+    wave_mem_order();
+    const long long price = sl.base + (long long)lvl;
+    unsigned long long A0 = 0, RR = 0;
+    uint32_t g0 = 0;
+    for (uint32_t b = 0; b < cnt; b += 64) {
+      uint32_t er;
+      const AggEv E = entry(start, cnt, b, er);
+      const bool v = b + (uint32_t)lane < cnt;
+      const bool tk = v && (E.j & AGG_TAKE) != 0u, rs = v && !tk;
+      const long long tq = tk ? (long long)E.qty : 0ll, rq = rs ? (long long)E.qty : 0ll;
+      const long long tinc = wave_incl_scan(tq), rinc = wave_incl_scan(rq);
+      const unsigned long long sq = gmin + E.pad;
+      if (tk && nmk) {  // fills
+        const uint32_t x0 = nf[er], nfl = EX(er + 1) - x0;
+        if (nfl) {
+          const unsigned long long a = A0 + (unsigned long long)(tinc - tq), z = a + (unsigned long long)E.qty;
+          const uint32_t first = staged ? a_search_lds(mkl, nmk, a, true) : a_search(ag.mk, mk_base, nmk, a, true);
+          const uint32_t g = (E.j & ~AGG_TAKE) >> AGG_GSHIFT;
+          const uint32_t p = sh.gbase[g] + (x0 - sh.gex[g]);
+          me_fill f;
+          f.taker_seq = sq;
+          f.price_q4 = price;
+          f.symbol = sl.gs;
+          me_fill* sc = ga.scratch[g];
+          unsigned long long lo = a;
+          for (uint32_t k = 0; k < nfl; ++k) {
+            const AggMk m = staged ? mkl[first + k] : ag.mk[mk_base + first + k];
+            const unsigned long long hi = m.end < z ? m.end : z;
+            f.maker_seq = m.seq;
+            f.qty = (int)(hi - lo);
+            sc[p + k] = f;
+            lo = hi;
           }
         }
-        g0 += (uint32_t)__popcll(sm);
-        RR += (unsigned long long)rli64(inc, 63);
       }
+      // surviving rests
+      const unsigned long long st0 = RR + (unsigned long long)(rinc - rq), en = RR + (unsigned long long)rinc;
+      const bool surv = rs && en > Cr;
+      const unsigned long long sm = __ballot(surv);
+      if (surv) {
+        const uint32_t gi = g0 + (uint32_t)__popcll(sm & lanemask_lt());
+        uint32_t chk, slt;
+        if (gi < tailfree) {
+          chk = tail0;
+          slt = te0 + gi;
+        } else {
+          const uint32_t gg = gi - tailfree;
+          chk = newchunk(gg / ME_C);
+          slt = gg % ME_C;
+        }
+        const int left = (int)(en - (st0 > Cr ? st0 : Cr));
+        if (chk < bk.nchunks) {
+          bk.chunks[chk].qty[slt] = left;
+          bk.chunks[chk].seq[slt] = sq;
+          bk.loc[sq & bk.ring_mask] = chk * ME_C + slt;
+        }
+      }
+      g0 += (uint32_t)__popcll(sm);
+      A0 += (unsigned long long)rli64(tinc, 63);
+      RR += (unsigned long long)rli64(rinc, 63);
     }
     for (uint32_t c = lane; c < need; c += 64) {
       const uint32_t chk = newchunk(c);
@@ -2519,7 +2555,7 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
       ChunkHdr h;
       h.next = c + 1 < need ? newchunk(c + 1) : NIL;
       h.prev = c ? newchunk(c - 1) : (newhead != NIL ? tail0 : NIL);
-      h.price = sl.base + (long long)lvl;
+      h.price = price;
       bk.chunks[chk].hdr = h;
     }
     const uint32_t first_new = need ? auniu(newchunk(0)) : NIL;
@@ -2534,10 +2570,14 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
       bk.levels[li].tail = tl;
       bk.tend[li] = (uint8_t)te;
     }
+    wave_mem_order();  // the next level reuses the staging
   }
+  __syncthreads();
+  GR_STAMP(bk, s, 7);
 }
 
-__global__ __launch_bounds__(GR_THREADS) void k_agg_gres(BookDev bk, AggGArgs ga, AggSrc src, AggDev ag, uint32_t ne) {
+__global__ __launch_bounds__(GR_THREADS, GR_WPE) void k_agg_gres(BookDev bk, AggGArgs ga, AggSrc src, AggDev ag,
+                                                          uint32_t ne) {
   __shared__ GrShared sh;
   extern __shared__ uint32_t gr_dyn[];  // [ne] fill counts / offsets, then [ne] 16-bit sorted log indices
   for (uint32_t s = blockIdx.x; s < bk.S; s += gridDim.x) {
@@ -2597,6 +2637,7 @@ hipError_t launch_agg_group(hipStream_t st, const BookDev& bk, const BatchDev* b
   }
   ga.ovf_base = bt[0].ovf_base;
   ga.scratch_cap = bt[0].scratch_cap;
+  ga.seq0 = bt[0].seq;
   ga.slab = bt[0].slab;
   ga.ng = ng;
   const uint32_t grid = bk.S < 2048u ? bk.S : 2048u;
@@ -2614,11 +2655,11 @@ hipError_t launch_agg_group(hipStream_t st, const BookDev& bk, const BatchDev* b
     hipLaunchKernelGGL(k_agg_gemit, dim3(grid), dim3(1024), 0, st, bk, ga, src, ag);
     return hipGetLastError();
   }
-  // per-event LDS arrays (6 B per event) sized for ~2.75 events per record of the group's mean symbol plus
+  // per-event LDS arrays (6 B per event) sized for 1.75 events per record of the group's mean symbol plus
   // slack; a longer log keeps them in HBM. Capped so the workgroup's LDS stays within 64 KB.
   uint64_t recs = 0;
   for (uint32_t g = 0; g < ng; ++g) recs += bt[g].n;
-  uint64_t ne = (recs * 11u / 4u) / (bk.S ? bk.S : 1u) + 320u;
+  uint64_t ne = (recs * 7u / 4u) / (bk.S ? bk.S : 1u) + 256u;  // (config 2: 1.4 events per record)
   ne = (ne + 63u) & ~63ull;
   const uint64_t ne_cap = ((64u << 10) - sizeof(GrShared)) / 6u & ~63ull;
   if (ne > ne_cap) ne = ne_cap;

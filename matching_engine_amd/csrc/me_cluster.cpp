@@ -43,8 +43,36 @@ std::string g_create_err;
 constexpr size_t kRec = 8 + 8 + 4 + 4 + 1;  // packed slice record: seq, price_q4, qty, symbol, kind
 enum : int64_t { CMD_SUBMIT = 1, CMD_COLLECT = 2, CMD_BOOK = 3, CMD_SNAPSHOT = 4, CMD_STOP = 5 };
 constexpr int kMaxInflight = 2;
+// rank 0's time per protocol phase (me_cluster_phases)
+enum { PH_SPLIT, PH_CTRL, PH_SCATTER, PH_VOTE, PH_MATCH, PH_COLLECT, PH_GATHER, PH_MERGE, PH_N };
 
 inline size_t round8(size_t x) { return (x + 7) & ~(size_t)7; }
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// f(t, lo, hi) over [0, n) in T contiguous chunks on T threads (the caller runs chunk 0); one thread below
+// `grain` records per chunk. The host halves of a large slice (split, pack, merge) are memory-bound loops.
+template <class F>
+void par_chunks(size_t n, size_t grain, F f) {
+  const size_t hw = std::max<unsigned>(1u, std::thread::hardware_concurrency());
+  const size_t T = std::max<size_t>(1, std::min<size_t>({hw, (size_t)16, n / std::max<size_t>(grain, 1)}));
+  if (T <= 1) {
+    f(0, 0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  th.reserve(T - 1);
+  for (size_t t = 1; t < T; ++t) th.emplace_back(f, t, n * t / T, n * (t + 1) / T);
+  f(0, 0, n / T);
+  for (auto& x : th) x.join();
+}
+size_t par_threads(size_t n, size_t grain) {
+  const size_t hw = std::max<unsigned>(1u, std::thread::hardware_concurrency());
+  return std::max<size_t>(1, std::min<size_t>({hw, (size_t)16, n / std::max<size_t>(grain, 1)}));
+}
+constexpr size_t kGrain = 65536;  // records per host thread at least
 
 // ---- sockets ----------------------------------------------------------------------------------
 bool send_all(int fd, const void* p, size_t n) {
@@ -449,7 +477,8 @@ struct Part {
 struct Ticket {
   uint64_t t = 0;
   size_t n = 0;
-  std::vector<std::vector<uint32_t>> pos;  // per rank: positions of its records in the slice
+  std::vector<uint32_t> pos;      // positions of each rank's records in the slice, rank after rank ...
+  std::vector<size_t> pos_off;    // ... rank r's at [pos_off[r], pos_off[r + 1])
 };
 
 // The packed part of n records at p: seq[n] px[n] qty[n] sym[n] kind[n].
@@ -486,6 +515,15 @@ struct me_cluster {
   std::vector<char> h_gather;
   std::vector<me_fill> tape;
   std::vector<me_order_result> res;
+  // rank 0 with an engine: its own part goes straight into the engine's pinned host slots (me_host_inputs,
+  // me_submit_host, me_collect) — no pack copy, scatter or gather for it; at world 1 collect hands out the
+  // slot's outputs as they are (one shard: its tape and results are the slice's)
+  bool direct0 = false;
+  me_order_soa w0{};  // the slot inputs rank 0's part was packed into (SUBMIT in flight)
+  const me_fill* out_tape = nullptr;
+  size_t out_nf = 0;
+  const me_order_result* out_res = nullptr;
+  double ph[PH_N] = {};
   uint64_t max_resting_total = 0;
   bool failed = false;
   bool stopped = false;
@@ -634,6 +672,10 @@ extern "C" me_cluster* me_cluster_create(const me_cluster_config* cfg, const me_
       return nullptr;
     }
   }
+  {  // ME_CLUSTER_DIRECT=0: rank 0's part through the transport like the others' (tests of the RCCL calls)
+    const char* v = getenv("ME_CLUSTER_DIRECT");
+    c->direct0 = cfg->rank == 0 && !c->use_ops && c->eng && !(v && atoi(v) == 0);
+  }
   if (cfg->rank == 0) {
     c->t_send = c->tp->alloc(kRec * cfg->max_batch);
     if (!c->t_send) {
@@ -664,6 +706,7 @@ static int run_submit(me_cluster* c, const int64_t* hdr) {
   const uint32_t W = c->cfg.world, me = c->cfg.rank;
   const uint64_t ticket = (uint64_t)hdr[1];
   Part& p = c->part[ticket & 1];
+  const bool direct = me == 0 && c->direct0;  // rank 0's part is already in its engine's slot inputs
   p.used = false;
   p.ticket = ticket;
   p.n = (size_t)hdr[6 + me];
@@ -672,12 +715,16 @@ static int run_submit(me_cluster* c, const int64_t* hdr) {
   p.eng_ticket = 0;
   std::vector<size_t> bytes(W);
   for (uint32_t r = 0; r < W; ++r) bytes[r] = kRec * (size_t)hdr[6 + r];
-  if (me == 0) {
-    size_t tot = 0;
-    for (size_t b : bytes) tot += b;
-    if (!c->tp->put(c->t_send, c->h_send.data(), tot)) return c->tfail("scatter");
+  if (direct) bytes[0] = 0;
+  double t = now_s();
+  size_t tot = 0;
+  for (size_t b : bytes) tot += b;
+  // a rank with nothing to send or receive stays out of the scatter (sends and receives pair up per rank)
+  if (me == 0 ? tot > 0 : bytes[me] > 0) {
+    if (me == 0 && !c->tp->put(c->t_send, c->h_send.data(), tot)) return c->tfail("scatter");
+    if (!c->tp->scatterv(c->t_send, bytes, p.in)) return c->tfail("scatter");
   }
-  if (!c->tp->scatterv(c->t_send, bytes, p.in)) return c->tfail("scatter");
+  if (me == 0) c->ph[PH_SCATTER] += now_s() - t;
   // all-or-none: every shard's admission control first
   int rc = ME_OK, ok = 1;
   if (p.n && !c->failed) {
@@ -687,11 +734,14 @@ static int run_submit(me_cluster* c, const int64_t* hdr) {
       rc = me_admission_check(c->eng, p.nl, &ok);
     }
   }
+  t = now_s();
   int64_t vote[2] = {rc != ME_OK || c->failed ? 0 : ok, c->failed ? ME_E_STATE : rc};
   if (!c->tp->allreduce(vote, 2, true)) return c->tfail("admission vote");
+  if (me == 0) c->ph[PH_VOTE] += now_s() - t;
   if (vote[1] != ME_OK) return c->fail((int)vote[1], "a shard failed its admission check");
   if (vote[0] == 0) return c->fail(ME_E_CAPACITY, "a shard's max_resting refused its part; no book changed");
   // match this rank's part
+  t = now_s();
   rc = ME_OK;
   if (p.n) {
     if (c->use_ops) {
@@ -707,6 +757,8 @@ static int run_submit(me_cluster* c, const int64_t* hdr) {
         if (nf) memcpy(p.h_out.data(), f, nf * sizeof(me_fill));
         memcpy(p.h_out.data() + nf * sizeof(me_fill), r, p.n * sizeof(me_order_result));
       }
+    } else if (direct) {  // the pipelined host path: collected at COLLECT, outputs in pinned memory
+      rc = me_submit_host(c->eng, &c->w0, p.n, &p.eng_ticket);
     } else if (c->tp->device()) {  // device batch; outputs into the staging buffer, HBM to HBM
       PackView v(p.in, p.n);
       me_order_soa b{v.seq, v.px, v.qty, v.sym, v.kind};
@@ -721,6 +773,7 @@ static int run_submit(me_cluster* c, const int64_t* hdr) {
       rc = me_submit_host(c->eng, &b, p.n, &p.eng_ticket);
     }
   }
+  if (me == 0) c->ph[PH_MATCH] += now_s() - t;
   if (!agree(c, rc)) return c->tfail("status");
   if (rc != ME_OK) {
     c->failed = true;  // some shard may have applied its part: the slice is lost
@@ -731,33 +784,46 @@ static int run_submit(me_cluster* c, const int64_t* hdr) {
 }
 
 static int run_collect(me_cluster* c, const int64_t* hdr) {
-  const uint32_t W = c->cfg.world;
+  const uint32_t W = c->cfg.world, me = c->cfg.rank;
   const uint64_t ticket = (uint64_t)hdr[1];
   Part& p = c->part[ticket & 1];
+  const bool direct = me == 0 && c->direct0;
   int rc = (p.used && p.ticket == ticket) ? ME_OK : ME_E_STATE;
   const char* send = nullptr;
-  if (rc == ME_OK && !c->use_ops && !c->tp->device() && p.n) {  // engine over TCP: collect now
+  const me_fill* f0 = nullptr;  // rank 0's own outputs (direct: the engine slot's pinned memory)
+  const me_order_result* r0 = nullptr;
+  double t = now_s();
+  if (rc == ME_OK && !c->use_ops && (direct || !c->tp->device()) && p.n) {  // host-slot batches: collect now
     const me_fill* f = nullptr;
     const me_order_result* r = nullptr;
     size_t nf = 0, nr = 0;
     rc = me_collect(c->eng, p.eng_ticket, &f, &nf, &r, &nr);
     if (rc == ME_OK) {
       p.nf = nf;
-      p.h_out.resize(round8(nf * sizeof(me_fill) + p.n * sizeof(me_order_result)));
-      if (nf) memcpy(p.h_out.data(), f, nf * sizeof(me_fill));
-      memcpy(p.h_out.data() + nf * sizeof(me_fill), r, p.n * sizeof(me_order_result));
+      if (direct) {
+        f0 = f;
+        r0 = r;
+      } else {
+        p.h_out.resize(round8(nf * sizeof(me_fill) + p.n * sizeof(me_order_result)));
+        if (nf) memcpy(p.h_out.data(), f, nf * sizeof(me_fill));
+        memcpy(p.h_out.data() + nf * sizeof(me_fill), r, p.n * sizeof(me_order_result));
+      }
     }
   }
+  if (me == 0) c->ph[PH_COLLECT] += now_s() - t;
   if (!agree(c, rc)) return c->tfail("status");
   p.used = false;
   if (rc != ME_OK) {
     c->failed = true;
     return c->fail(ME_E_STATE, "a shard lost its part of the slice");
   }
-  // payloads padded to 8 B, so every rank's tape starts aligned in rank 0's gather buffer
-  const size_t mine = round8(p.nf * sizeof(me_fill) + p.n * sizeof(me_order_result));
+  t = now_s();
+  // payloads padded to 8 B, so every rank's tape starts aligned in rank 0's gather buffer (rank 0's own
+  // outputs, direct, stay where the engine put them)
+  const size_t mine = direct ? 0 : round8(p.nf * sizeof(me_fill) + p.n * sizeof(me_order_result));
   char* staged = nullptr;  // a host payload (shard ops) on a device transport
-  if (c->tp->device() && !c->use_ops) {
+  if (!mine) {
+  } else if (c->tp->device() && !c->use_ops) {
     send = p.out;  // HBM to HBM: the engine's tape and results never left the device
   } else if (c->tp->device()) {
     staged = c->tp->alloc(mine);
@@ -776,11 +842,11 @@ static int run_collect(me_cluster* c, const int64_t* hdr) {
     c->tp->release(staged);
     return c->tfail("size gather");
   }
-  if (c->cfg.rank != 0) szs[2 * c->cfg.rank + 1] = (int64_t)mine;
+  if (me != 0) szs[2 * me + 1] = (int64_t)mine;
   std::vector<size_t> bytes(W);
   size_t tot = 0;
   for (uint32_t r = 0; r < W; ++r) tot += (bytes[r] = (size_t)szs[2 * r + 1]);
-  if (c->cfg.rank == 0 && tot > c->t_gather_cap) {
+  if (me == 0 && tot > c->t_gather_cap) {
     c->tp->release(c->t_gather);
     c->t_gather = c->tp->alloc(tot);
     c->t_gather_cap = c->t_gather ? tot : 0;
@@ -789,49 +855,81 @@ static int run_collect(me_cluster* c, const int64_t* hdr) {
       return c->tfail("gather buffer");
     }
   }
-  const bool gok = c->tp->gatherv(send, bytes, c->t_gather);
+  const bool gok = (me == 0 ? tot == 0 : mine == 0) || c->tp->gatherv(send, bytes, c->t_gather);
   c->tp->release(staged);
   if (!gok) return c->tfail("gather");
-  if (c->cfg.rank != 0) return ME_OK;
+  if (me != 0) return ME_OK;
   c->h_gather.resize(tot);
-  if (!c->tp->get(c->h_gather.data(), c->t_gather, tot)) return c->tfail("gather D2H");
-  // merge: results back to slice order, tapes by taker seq (u64 keys; each shard's tape is already
-  // in taker order and a taker's fills are all on its shard)
+  if (tot && !c->tp->get(c->h_gather.data(), c->t_gather, tot)) return c->tfail("gather D2H");
+  c->ph[PH_GATHER] += now_s() - t;
+  t = now_s();
   const Ticket& tk = c->tickets.front();
-  c->res.assign(tk.n, me_order_result{});
-  std::vector<const me_fill*> tp_(W);
-  std::vector<size_t> nf(W), at(W, 0);
-  size_t off = 0, ftot = 0;
-  for (uint32_t r = 0; r < W; ++r) {
-    nf[r] = (size_t)szs[2 * r];
-    tp_[r] = (const me_fill*)(c->h_gather.data() + off);
-    const char* rr = c->h_gather.data() + off + nf[r] * sizeof(me_fill);
-    const auto& pos = tk.pos[r];
-    for (size_t i = 0; i < pos.size(); ++i) memcpy(&c->res[pos[i]], rr + i * sizeof(me_order_result), sizeof(me_order_result));
-    off += bytes[r];
-    ftot += nf[r];
-  }
-  c->tape.resize(ftot);
-  for (size_t k = 0; k < ftot; ++k) {
-    uint32_t best = W;
-    uint64_t bq = 0;
-    for (uint32_t r = 0; r < W; ++r)
-      if (at[r] < nf[r] && (best == W || tp_[r][at[r]].taker_seq < bq)) {
-        best = r;
-        bq = tp_[r][at[r]].taker_seq;
+  if (W == 1 && direct) {  // one shard: its tape and results are the slice's, in place
+    c->out_tape = f0;
+    c->out_nf = p.nf;
+    c->out_res = r0;
+  } else {
+    // merge: results back to slice order; the merged tape in slice order (= taker seq order: every taker's
+    // fills are consecutive on its one shard, at its result's tape offset there)
+    std::vector<const me_fill*> tf(W);
+    std::vector<const me_order_result*> tr(W);
+    size_t off = 0;
+    for (uint32_t r = 0; r < W; ++r) {
+      const size_t nfr = (size_t)szs[2 * r];
+      if (r == 0 && direct) {
+        tf[0] = f0;
+        tr[0] = r0;
+      } else {
+        tf[r] = (const me_fill*)(c->h_gather.data() + off);
+        tr[r] = (const me_order_result*)(c->h_gather.data() + off + nfr * sizeof(me_fill));
+        off += bytes[r];
       }
-    const me_fill* src = &tp_[best][at[best]];
-    size_t run = 1;  // the rest of this taker's fills come from the same shard
-    while (at[best] + run < nf[best] && src[run].taker_seq == bq) ++run;
-    memcpy(&c->tape[k], src, run * sizeof(me_fill));
-    at[best] += run;
-    k += run - 1;
+    }
+    c->res.resize(tk.n);
+    me_order_result* res = c->res.data();
+    for (uint32_t r = 0; r < W; ++r) {
+      const size_t lo = tk.pos_off[r], np = tk.pos_off[r + 1] - lo;
+      const uint32_t* pos = tk.pos.data() + lo;
+      const me_order_result* rr = tr[r];
+      par_chunks(np, kGrain, [&](size_t, size_t a, size_t b) {
+        for (size_t k = a; k < b; ++k) res[pos[k]] = rr[k];
+      });
+    }
+    // merged tape offsets: exclusive scan of the fill counts in slice order (chunk sums, then chunk scans)
+    const size_t T = par_threads(tk.n, kGrain);
+    std::vector<uint64_t> csum(T + 1, 0);
+    par_chunks(tk.n, kGrain, [&](size_t i, size_t a, size_t b) {
+      uint64_t x = 0;
+      for (size_t k = a; k < b; ++k) x += res[k].fill_count;
+      csum[i + 1] = x;
+    });
+    for (size_t i = 0; i < T; ++i) csum[i + 1] += csum[i];
+    c->tape.resize(csum[T]);
+    me_fill* tape = c->tape.data();
+    par_chunks(tk.n, kGrain, [&](size_t i, size_t a, size_t b) {
+      uint64_t o = csum[i];
+      for (size_t k = a; k < b; ++k) {
+        const uint32_t fc = res[k].fill_count;
+        res[k].tape_offset = (uint32_t)o;
+        o += fc;
+      }
+    });
+    for (uint32_t r = 0; r < W; ++r) {  // each taker's fills from its shard's tape
+      const size_t lo = tk.pos_off[r], np = tk.pos_off[r + 1] - lo;
+      const uint32_t* pos = tk.pos.data() + lo;
+      const me_order_result* rr = tr[r];
+      const me_fill* fr = tf[r];
+      par_chunks(np, kGrain, [&](size_t, size_t a, size_t b) {
+        for (size_t k = a; k < b; ++k)
+          if (rr[k].fill_count)
+            memcpy(tape + res[pos[k]].tape_offset, fr + rr[k].tape_offset, rr[k].fill_count * sizeof(me_fill));
+      });
+    }
+    c->out_tape = tape;
+    c->out_nf = c->tape.size();
+    c->out_res = res;
   }
-  uint64_t o = 0;
-  for (auto& r : c->res) {
-    r.tape_offset = (uint32_t)o;
-    o += r.fill_count;
-  }
+  c->ph[PH_MERGE] += now_s() - t;
   c->tickets.pop_front();
   c->slices++;
   return ME_OK;
@@ -1039,7 +1137,9 @@ static int issue(me_cluster* c, std::vector<int64_t>& hdr, const BookReq* q = nu
                  uint32_t* counts = nullptr) {
   if (c->cfg.rank != 0) return c->fail(ME_E_INVALID, "only rank 0 issues commands");
   if (c->stopped) return c->fail(ME_E_STATE, "cluster stopped");
+  const double t = now_s();
   if (!c->tp->bcast(hdr.data(), hdr.size())) return c->tfail("command channel");
+  c->ph[PH_CTRL] += now_s() - t;
   BookReq none{};
   return dispatch(c, hdr.data(), q ? q : &none, levels, counts);
 }
@@ -1050,38 +1150,95 @@ extern "C" int me_cluster_submit(me_cluster* c, const me_order_soa* b, size_t n,
   if (n == 0 || n > c->cfg.max_batch) return c->fail(ME_E_INVALID, "slice size must be in [1, max_batch]");
   if (c->tickets.size() >= (size_t)kMaxInflight) return c->fail(ME_E_STATE, "two slices in flight: collect first");
   const uint32_t W = c->cfg.world, S = c->cfg.num_symbols;
+  double t = now_s();
   Ticket tk;
   tk.t = c->next_ticket;
   tk.n = n;
-  tk.pos.assign(W, {});
   std::vector<int64_t> hdr(c->hdr_words(), 0);
   hdr[0] = CMD_SUBMIT;
   hdr[1] = (int64_t)tk.t;
   hdr[2] = (int64_t)n;
-  // split by owner: local symbol ids (an unknown global id stays out of range: BAD_SYMBOL on rank 0)
-  for (size_t i = 0; i < n; ++i) {
-    const uint32_t s = b->symbol[i];
-    const uint32_t r = s < S ? c->owner[s] : 0;
-    tk.pos[r].push_back((uint32_t)i);
-    hdr[6 + r]++;
-    if ((b->kind[i] & 0x0Cu) == 0u) hdr[6 + W + r]++;  // NEW LIMIT: may rest
-  }
-  c->h_send.resize(kRec * n);
-  size_t off = 0;
-  for (uint32_t r = 0; r < W; ++r) {
-    const auto& pos = tk.pos[r];
-    PackView v(c->h_send.data() + off, pos.size());
-    for (size_t k = 0; k < pos.size(); ++k) {
-      const size_t i = pos[k];
-      const uint32_t s = b->symbol[i];
-      v.seq[k] = b->seq[i];
-      v.px[k] = b->price_q4[i];
-      v.qty[k] = b->qty[i];
-      v.sym[k] = s < S ? c->local[s] : 0xFFFFFFFFu;
-      v.kind[k] = b->kind[i];
+  // split by owner, stable (each part keeps slice order = seq order): per-chunk counts of records and of
+  // NEW LIMITs per rank, their prefix, then every chunk packs its records at its offsets. An unknown global
+  // id goes to rank 0 out of range (BAD_SYMBOL there).
+  const size_t T = par_threads(n, kGrain);
+  std::vector<uint64_t> cnt(T * W, 0), lim(T * W, 0);
+  const uint32_t* owner = c->owner.data();
+  par_chunks(n, kGrain, [&](size_t i, size_t lo, size_t hi) {
+    uint64_t* ci = cnt.data() + i * W;
+    uint64_t* li = lim.data() + i * W;
+    for (size_t k = lo; k < hi; ++k) {
+      const uint32_t s = b->symbol[k];
+      const uint32_t r = s < S ? owner[s] : 0;
+      ci[r]++;
+      li[r] += (b->kind[k] & 0x0Cu) == 0u;  // NEW LIMIT: may rest
     }
-    off += kRec * pos.size();
+  });
+  for (uint32_t r = 0; r < W; ++r)
+    for (size_t i = 0; i < T; ++i) {
+      hdr[6 + r] += (int64_t)cnt[i * W + r];
+      hdr[6 + W + r] += (int64_t)lim[i * W + r];
+    }
+  tk.pos_off.assign(W + 1, 0);
+  for (uint32_t r = 0; r < W; ++r) tk.pos_off[r + 1] = tk.pos_off[r] + (size_t)hdr[6 + r];
+  tk.pos.resize(n);
+  // where each rank's part goes: rank 0's into its engine's slot inputs (direct), the others' packed into
+  // h_send in rank order
+  const size_t n0 = (size_t)hdr[6];
+  std::vector<PackView> dst;
+  dst.reserve(W);
+  c->h_send.resize(kRec * n);
+  {
+    size_t off = 0;
+    for (uint32_t r = 0; r < W; ++r) {
+      const size_t nr = (size_t)hdr[6 + r];
+      if (r == 0 && c->direct0 && n0) {
+        me_order_soa_w w{};
+        if (me_host_inputs(c->eng, n0, &w) != ME_OK) return c->fail(ME_E_STATE, "rank 0 slot inputs: " + eng_err(c->eng));
+        PackView v(c->h_send.data(), 0);
+        v.seq = w.seq;
+        v.px = w.price_q4;
+        v.qty = w.qty;
+        v.sym = w.symbol;
+        v.kind = w.kind;
+        dst.push_back(v);
+        c->w0 = me_order_soa{w.seq, w.price_q4, w.qty, w.symbol, w.kind};
+        continue;
+      }
+      if (r == 0 && c->direct0) {
+        dst.push_back(PackView(c->h_send.data(), 0));
+        continue;
+      }
+      dst.push_back(PackView(c->h_send.data() + off, nr));
+      off += kRec * nr;
+    }
   }
+  // chunk i's first record of rank r lands at base[i][r] within the part
+  std::vector<uint64_t> base(T * W, 0);
+  for (uint32_t r = 0; r < W; ++r) {
+    uint64_t x = 0;
+    for (size_t i = 0; i < T; ++i) {
+      base[i * W + r] = x;
+      x += cnt[i * W + r];
+    }
+  }
+  const uint32_t* local = c->local.data();
+  par_chunks(n, kGrain, [&](size_t i, size_t lo, size_t hi) {
+    std::vector<uint64_t> at(base.begin() + i * W, base.begin() + (i + 1) * W);
+    for (size_t k = lo; k < hi; ++k) {
+      const uint32_t s = b->symbol[k];
+      const uint32_t r = s < S ? owner[s] : 0;
+      const uint64_t j = at[r]++;
+      PackView& v = dst[r];
+      v.seq[j] = b->seq[k];
+      v.px[j] = b->price_q4[k];
+      v.qty[j] = b->qty[k];
+      v.sym[j] = s < S ? local[s] : 0xFFFFFFFFu;
+      v.kind[j] = b->kind[k];
+      tk.pos[tk.pos_off[r] + j] = (uint32_t)k;
+    }
+  });
+  c->ph[PH_SPLIT] += now_s() - t;
   const int rc = issue(c, hdr);
   if (rc != ME_OK) return rc;
   c->tickets.push_back(std::move(tk));
@@ -1099,9 +1256,9 @@ extern "C" int me_cluster_collect(me_cluster* c, uint64_t ticket, const me_fill*
   hdr[1] = (int64_t)ticket;
   const int rc = issue(c, hdr);
   if (rc != ME_OK) return rc;
-  if (fills) *fills = c->tape.data();
-  if (n_fills) *n_fills = c->tape.size();
-  if (results) *results = c->res.data();
+  if (fills) *fills = c->out_tape;
+  if (n_fills) *n_fills = c->out_nf;
+  if (results) *results = c->out_res;
   return ME_OK;
 }
 
@@ -1177,6 +1334,12 @@ extern "C" int me_cluster_stats(const me_cluster* c, uint64_t* slices, uint64_t*
   if (slices) *slices = c->slices;
   if (bytes) *bytes = c->tp ? c->tp->moved : 0;
   return ME_OK;
+}
+
+extern "C" int me_cluster_phases(const me_cluster* c, double* seconds, size_t n) {
+  if (!c) return ME_E_INVALID;
+  for (size_t k = 0; k < n && k < (size_t)PH_N; ++k) seconds[k] = c->ph[k];
+  return PH_N;
 }
 
 extern "C" int me_cluster_last_error(const me_cluster* c, char* buf, size_t cap) {

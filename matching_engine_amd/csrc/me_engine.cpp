@@ -522,7 +522,8 @@ extern "C" me_engine* me_create(const me_config* cfg) {
     // up, see reg_agg_auto)
     const char* vr = getenv("ME_REG_AGG");
     const uint64_t grp = cfg->batches_per_launch ? cfg->batches_per_launch : ME_DEFAULT_GROUP;
-    e->hot.agg_reg = L <= 128 && (vr ? atoi(vr) != 0
+    // (k_agg_gres keeps each event's seq as a 32-bit offset from the group's first seq: seq_ring <= 2^32)
+    e->hot.agg_reg = L <= 128 && ring <= (1ull << 32) && (vr ? atoi(vr) != 0
                                      : (uint64_t)cfg->max_batch >= 32ull * S && cfg->max_batch >= 8192u &&
                                            (uint64_t)cfg->max_batch * grp <= (4ull << 20));  // (pools of a
                                                                                              // group's records)

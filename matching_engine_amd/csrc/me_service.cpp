@@ -237,7 +237,8 @@ struct me_service {
   // holds no resting order and has nothing on its way: a new symbol may take it over.
   std::mutex ref_mu;
   std::vector<int64_t> sref;
-  std::vector<uint32_t> idle;  // books whose count reached 0 (checked again when taken)
+  std::vector<uint32_t> idle;     // books whose count reached 0 (checked again when taken) ...
+  std::vector<uint8_t> in_idle;   // ... each at most once: a book's count returns to 0 again and again
   uint64_t reclaimed = 0;
   uint64_t recovered = 0;
   // --- background flusher
@@ -344,7 +345,10 @@ static void ref_add(me_service* s, uint32_t sid, int64_t d) {
   if (sid >= s->sref.size()) return;
   int64_t& r = s->sref[sid];
   r += d;
-  if (r == 0) s->idle.push_back(sid);
+  if (r == 0 && !s->in_idle[sid]) {
+    s->in_idle[sid] = 1;
+    s->idle.push_back(sid);
+  }
 }
 
 // Symbol string -> local book id (mu held). The reference accepts any non-empty symbol
@@ -365,11 +369,13 @@ static bool intern(me_service* s, const std::string& symbol, uint32_t& sid) {
     s->names.push_back(symbol);
     s->sym.emplace(symbol, sid);
     s->sref.push_back(0);
+    s->in_idle.push_back(0);
     return true;
   }
   while (!s->idle.empty()) {
     const uint32_t c = s->idle.back();
     s->idle.pop_back();
+    if (c < s->in_idle.size()) s->in_idle[c] = 0;
     if (c >= s->sref.size() || s->sref[c] != 0) continue;  // busy again since it went idle
     s->sym.erase(s->names[c]);
     s->names[c] = symbol;
@@ -386,7 +392,8 @@ static int flush_closed(me_service* s, bool take_open, size_t limit, struct Flus
 // Restart recovery: the orders the DB shows resting (status NEW / PARTIALLY_FILLED, remaining > 0) as
 // LIMIT records in OID order, with their remainders — replayed into the backend before any new
 // order, so each keeps its place in its level's FIFO. Chunks of at most slice_max records spanning
-// fewer than 2^20 OIDs (one launch group must span fewer seqs than the engine's seq ring).
+// fewer than half the engine's seq ring, each matched alone (one launch group must span fewer seqs than
+// the seq ring, and old resting orders can be sparse).
 static bool load_resting(me_service* s, std::string& err) {
   sqlite3_stmt* q = nullptr;
   if (!sql_ok(g_sql.prepare_v2(s->db,
@@ -398,6 +405,13 @@ static bool load_resting(me_service* s, std::string& err) {
     return false;
   }
   const size_t cap = s->slice_max ? s->slice_max : 65536;
+  // a recovery chunk is matched alone (flush_closed collects it before the next submit), so one launch
+  // group spans only its own OIDs: below half the engine's seq ring (a matcher: 2^20)
+  uint64_t span = 1ull << 20;
+  if (s->eng) {
+    me_config c{};
+    if (me_get_config(s->eng, &c) == ME_OK && c.seq_ring) span = std::max<uint64_t>(c.seq_ring / 2, 1);
+  }
   bool ok = true;
   std::lock_guard<std::mutex> lk(s->mu);
   Slice cur;
@@ -425,7 +439,7 @@ static bool load_resting(me_service* s, std::string& err) {
       ok = false;
       break;
     }
-    if (cur.size() >= cap || (cur.size() && oid - cur.seq.front() >= (1ull << 20))) close_chunk();
+    if (cur.size() >= cap || (cur.size() && oid - cur.seq.front() >= span)) close_chunk();
     cur.seq.push_back(oid);
     cur.px.push_back(px);
     cur.qty.push_back((int32_t)rem);
@@ -464,6 +478,7 @@ static me_service* create(me_engine* engine, const me_matcher* m, const char* co
     s->names.emplace_back(symbols[i]);
     s->sym.emplace(s->names.back(), i);
     s->sref.push_back(0);
+    s->in_idle.push_back(1);
   }
   for (uint32_t i = num_symbols; i-- > 0;) s->idle.push_back(i);  // nothing rests on them yet
   if (s->names.size() > s->sym_cap) s->fail(ME_E_INVALID, "me_service_create: more symbols than the engine holds");
@@ -1240,6 +1255,9 @@ static int flush_closed(me_service* s, bool take_open, size_t rec_limit, FlushOu
     fl.push_back(std::move(f));
     if (fl.size() > 1 || !backend_async(s))
       if ((r = finish_oldest()) != ME_OK) return r;
+    if (!fl.empty() && fl.back().sl.recovery)  // a recovery chunk is matched alone (load_resting)
+      while (!fl.empty())
+        if ((r = finish_oldest()) != ME_OK) return r;
   }
   while (!fl.empty()) {
     const int r = finish_oldest();
@@ -1264,9 +1282,11 @@ extern "C" int me_service_flush(me_service* s, me_fill* out_fills, size_t fills_
   if (n_results) *n_results = 0;
   std::lock_guard<std::mutex> lf(s->flush_mu);
   size_t total = 0;
-  {
+  {  // the open slice closes in the same critical section that counts it: SubmitOrders after this point go
+     // into a new open slice (the next flush's), so `total` is exactly what this flush matches
     std::lock_guard<std::mutex> lk(s->mu);
-    total = s->open.size() + s->closed_records;  // inflight is 0 here (flush_mu held)
+    close_open(s);
+    total = s->closed_records;  // inflight is 0 here (flush_mu held)
   }
   // the caller's buffers are checked before anything is matched
   if ((out_results || out_seq) && total > results_cap)
@@ -1280,7 +1300,7 @@ extern "C" int me_service_flush(me_service* s, me_fill* out_fills, size_t fills_
   out.res = out_results;
   out.seq = out_seq;
   out.res_cap = results_cap;
-  const int rc = flush_closed(s, true, total, &out, true);
+  const int rc = flush_closed(s, false, total, &out, true);
   if (n_fills) *n_fills = out.nf;
   if (n_results) *n_results = out.nr;
   return rc;

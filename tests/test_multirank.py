@@ -22,13 +22,13 @@ def _free_port():
     return p
 
 
-def _run(kind, world, tmp_path, timeout=240):
+def _run(kind, world, tmp_path, timeout=240, env_extra=None):
     out = str(tmp_path / f"cl_{kind}_{world}.json")
     port = _free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), **(env_extra or {}))
         # child processes (never exec over a GPU-initialised interpreter)
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "cluster_worker.py"), kind, str(tmp_path),
                                        out], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT))
@@ -75,9 +75,18 @@ def test_cluster_tcp_gpu_engines(built, tmp_path):
 
 @pytest.mark.gpu
 def test_cluster_rccl_single_rank(built, tmp_path):
-    """The RCCL transport with an engine shard, world size 1: ncclCommInitRank over the TCP bootstrap,
-    broadcast / all-reduce / all-gather, and the grouped send / recv of parts, tapes and results (rank 0
-    sends to itself) — every RCCL call an 8-GPU node makes, minus the xGMI hops."""
-    r = _run("rccl", 1, tmp_path)
+    """The RCCL transport with an engine shard, world size 1, rank 0's part forced through the transport
+    (ME_CLUSTER_DIRECT=0): ncclCommInitRank over the TCP bootstrap, and the grouped send / recv of parts,
+    tapes and results (rank 0 sends to itself) — every RCCL call an 8-GPU node makes, minus the xGMI hops."""
+    r = _run("rccl", 1, tmp_path, env_extra={"ME_CLUSTER_DIRECT": "0"})
     assert r["ok"], r["msg"]
     assert r["orders"] > 5000 and r["fill_rows"] > 1000 and r["bytes"] > 0
+
+
+@pytest.mark.gpu
+def test_cluster_rccl_single_rank_direct(built, tmp_path):
+    """World size 1 as deployed: rank 0's part goes straight into its engine's pinned slots (no pack copy,
+    scatter or gather) and collect hands out the slot's outputs in place; the same checks against one book."""
+    r = _run("rccl", 1, tmp_path)
+    assert r["ok"], r["msg"]
+    assert r["orders"] > 5000 and r["fill_rows"] > 1000
