@@ -81,8 +81,17 @@ __device__ __forceinline__ void a_drain() {
 #ifdef ME_STAMPS
 #define GR_STAMP(bk, s, k) \
   do { if (threadIdx.x == 0) (bk).dbg[(size_t)(s) * 24u + 16u + (k)] = stamp_now(); } while (0)
+// The grouped walk's cycles per symbol by part, accumulated (dbg[s * 24 + 0..3]: batch set-up — bucket
+// loads, staging, sort —, block set-up and results, the record loop, records walked)
+#define GW_T(k)                                  \
+  do {                                           \
+    const unsigned long long _n = stamp_now();   \
+    gw_t[k] += _n - gw_m;                        \
+    gw_m = _n;                                   \
+  } while (0)
 #else
 #define GR_STAMP(bk, s, k) ((void)0)
+#define GW_T(k) ((void)0)
 #endif
 
 // ------------------------------------------------------------------ the level-total walk
@@ -620,8 +629,7 @@ __device__ __forceinline__ bool lw_init(LWalk& w, const BookDev& bk, uint32_t s,
       sum += (unsigned long long)t[u];
     }
   }
-  for (int d = 1; d < 64; d <<= 1) sum += __shfl_xor(sum, d, 64);
-  w.ub = rl64(sum, 0);
+  w.ub = (unsigned long long)rli64(wave_incl_scan((long long)sum), 63);  // (DPP: no LDS round trips)
   wave_mem_order();
   w.bb = bb;
   w.ba = ba;
@@ -648,8 +656,7 @@ __device__ __forceinline__ void lw_end(LWalk& w, const BookDev& bk, uint32_t s) 
 // The block's quantities onto the bound; false: the block could take the book to LW_CAP
 __device__ __forceinline__ bool lw_admit(LWalk& w, int oq) {
   unsigned long long q = (unsigned long long)(uint32_t)max(oq, 0);
-  for (int d = 1; d < 64; d <<= 1) q += __shfl_xor(q, d, 64);
-  w.ub += rl64(q, 0);
+  w.ub += (unsigned long long)rli64(wave_incl_scan((long long)q), 63);
   return w.ub < LW_CAP;
 }
 
@@ -1575,27 +1582,38 @@ struct AggGArgs {
   uint32_t slab, ng;
 };
 
-// Ascending bitonic sort of 64 (one register) / 128 (two) distinct keys across the wave.
-__device__ __forceinline__ uint32_t a_bstep(uint32_t v, int J, bool asc) {
-  const uint32_t p = (uint32_t)__shfl_xor((int)v, J, 64);
+// Ascending bitonic sort of 64 (one register) / 128 (two) distinct keys across the wave; partners over
+// DPP / permlane swaps (xor_lane, me_wave.hpp), no LDS round trip per step.
+template <int J>
+__device__ __forceinline__ uint32_t a_bstep(uint32_t v, bool asc) {
+  const uint32_t p = xor_lane<J>(v);
   const bool lower = (lane_id() & J) == 0;
   return (lower == asc) ? min(v, p) : max(v, p);
 }
-__device__ __forceinline__ uint32_t a_bmerge(uint32_t v, int K, bool asc) {
-  for (int J = K / 2; J >= 1; J >>= 1) v = a_bstep(v, J, asc);
-  return v;
+template <int K>
+__device__ __forceinline__ uint32_t a_bmerge(uint32_t v, bool asc) {
+  if constexpr (K >= 64) v = a_bstep<32>(v, asc);
+  if constexpr (K >= 32) v = a_bstep<16>(v, asc);
+  if constexpr (K >= 16) v = a_bstep<8>(v, asc);
+  if constexpr (K >= 8) v = a_bstep<4>(v, asc);
+  if constexpr (K >= 4) v = a_bstep<2>(v, asc);
+  return a_bstep<1>(v, asc);
 }
 __device__ __forceinline__ uint32_t a_sort64(uint32_t v, bool desc) {
   const int lane = lane_id();
-  for (int K = 2; K < 64; K <<= 1) v = a_bmerge(v, K, (lane & K) == 0);
-  return a_bmerge(v, 64, !desc);
+  v = a_bmerge<2>(v, (lane & 2) == 0);
+  v = a_bmerge<4>(v, (lane & 4) == 0);
+  v = a_bmerge<8>(v, (lane & 8) == 0);
+  v = a_bmerge<16>(v, (lane & 16) == 0);
+  v = a_bmerge<32>(v, (lane & 32) == 0);
+  return a_bmerge<64>(v, !desc);
 }
 __device__ __forceinline__ void a_sort128(uint32_t& a, uint32_t& b) {
   a = a_sort64(a, false);
   b = a_sort64(b, true);
   const uint32_t lo = min(a, b), hi = max(a, b);
-  a = a_bmerge(lo, 64, true);
-  b = a_bmerge(hi, 64, true);
+  a = a_bmerge<64>(lo, true);
+  b = a_bmerge<64>(hi, true);
 }
 
 struct AStage {  // a symbol's bucket of one batch, staged for the batch-order gather
@@ -1638,8 +1656,7 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
     const uint32_t gl = min((uint32_t)lane, ng - 1u);
     const uint32_t nsv = (uint32_t)lane < ng ? ga.bcnt[gl][(size_t)s * BK_CNT_STRIDE] : 0u;
     long long t = (long long)nsv;
-    for (int d = 1; d < 64; d <<= 1) t += __shfl_xor(t, d, 64);
-    const uint32_t total = (uint32_t)rli64(t, 0);
+    const uint32_t total = (uint32_t)rli64(wave_incl_scan(t), 63);
     const SymState st = bk.sym[s];
     const long long base = rli64(st.base, 0);
     const int bb0 = rli32(st.best_bid, 0), ba0 = rli32(st.best_ask, 0);
@@ -1667,6 +1684,9 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
     }
     if (!total) continue;
     GR_STAMP(bk, s, 0);
+#ifdef ME_STAMPS
+    unsigned long long gw_t[4] = {0ull, 0ull, 0ull, 0ull}, gw_m = stamp_now();
+#endif
     if (!eok || !a_reserve(ag, slot, resting, total)) {  // no room in the pools: the whole group of the
                                                           // symbol goes to the continuation
       const uint32_t g0 = (uint32_t)__builtin_ctzll(__ballot(nsv != 0u));
@@ -1724,6 +1744,7 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
       wave_mem_order();
       me_order_result* res = ga.res[g];
       bool stop = false;
+      GW_T(0);
       for (uint32_t blk = 0; blk < cnt; blk += 64) {
         const uint32_t key = blk ? k1 : k0;
         const bool v = blk + (uint32_t)lane < cnt;
@@ -1738,7 +1759,12 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
         const unsigned long long fastm = __ballot(a_classify(v, oseq, opx, oq, okd, base, L, nfar0, nfar1, rj, olm));
         int rr = 0;
         const bool adm = lok && lw_admit(lw, v ? oq : 0);
+        GW_T(1);
         const uint32_t k = lw_block(w, lw, oq, lw_cw(okd, olm, rj, L), (g << AGG_GSHIFT) | oi, adm ? fastm : 0ull, cntb, rr);
+        GW_T(2);
+#ifdef ME_STAMPS
+        gw_t[3] += k;
+#endif
         if (v && (uint32_t)lane < k) res[oi] = a_result(oq, okd, rj, rr);  // fills: k_agg_gfin
         if (k < cntb) {
           hidx = a_ghand(bk, s, g, blk + k, cnt, 0u, 0u);  // scratch position: k_agg_gfin
@@ -1767,6 +1793,10 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
       slot->pos = gstop;  // the batch the continuation starts in (ng: none)
     }
     GR_STAMP(bk, s, 1);
+#ifdef ME_STAMPS
+    if (lane == 0)
+      for (int q = 0; q < 4; ++q) bk.dbg[(size_t)s * 24u + q] = gw_t[q];
+#endif
   }
 }
 

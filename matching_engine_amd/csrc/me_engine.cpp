@@ -369,6 +369,9 @@ static void free_all(me_engine* e) {
   if (e->hot.fork) (void)hipEventDestroy(e->hot.fork);
   if (e->hot.join) (void)hipEventDestroy(e->hot.join);
   if (e->hot.st) (void)hipStreamDestroy(e->hot.st);
+  if (e->hot.sfork) (void)hipEventDestroy(e->hot.sfork);
+  if (e->hot.sjoin) (void)hipEventDestroy(e->hot.sjoin);
+  if (e->hot.sst) (void)hipStreamDestroy(e->hot.sst);
   if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
 }
 
@@ -528,6 +531,14 @@ extern "C" me_engine* me_create(const me_config* cfg) {
                                            (uint64_t)cfg->max_batch * grp <= (4ull << 20));  // (pools of a
                                                                                              // group's records)
     e->reg_agg_auto = e->hot.agg_reg && !vr;
+    // the grouped aggregate path's side jobs on a stream of their own (ME_SIDE_STREAM=0: in line)
+    const char* vs = getenv("ME_SIDE_STREAM");
+    if (e->hot.agg_reg && !(vs && atoi(vs) == 0)) {
+      if ((he = hipStreamCreateWithFlags(&e->hot.sst, hipStreamNonBlocking)) != hipSuccess ||
+          (he = hipEventCreateWithFlags(&e->hot.sfork, hipEventDisableTiming)) != hipSuccess ||
+          (he = hipEventCreateWithFlags(&e->hot.sjoin, hipEventDisableTiming)) != hipSuccess)
+        return bail(std::string("side stream: ") + hipGetErrorString(he));
+    }
     bk.hot_min = (e->hot.agg || L > LDS_MAX_LEVELS) ? (v ? (uint32_t)atoi(v) : 512u) : 0u;
     if (bk.hot_min) {
       if ((he = hipStreamCreateWithFlags(&e->hot.st, hipStreamNonBlocking)) != hipSuccess ||

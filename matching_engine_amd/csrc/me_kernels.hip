@@ -2535,7 +2535,18 @@ hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* b
   if (hot && hot->agg_reg && ng && bt[0].bcnt) {
     // the group through the aggregate path: side jobs (k_side), walk + per-level kernels, continuation
     hipError_t e;
-    if (ax.nb || ax.nt) {
+    const bool side = ax.nb || ax.nt, fork = side && hot->sst;
+    if (fork) {
+      // the side jobs beside the group: the next group's buckets and the tapes of the group before touch
+      // nothing this group's walk, per-level launch or continuation reads or writes (other bucket and
+      // output sets), and everything they read was final when the fork was recorded
+      if ((e = hipEventRecord(hot->sfork, st)) != hipSuccess || (e = hipStreamWaitEvent(hot->sst, hot->sfork, 0)) != hipSuccess)
+        return e;
+      e = big ? rc64::launch_match_reg(hot->sst, bk, bt, 0, ax, nullptr, nullptr)
+              : rc128::launch_match_reg(hot->sst, bk, bt, 0, ax, nullptr, nullptr);
+      if (e != hipSuccess || (e = hipEventRecord(hot->sjoin, hot->sst)) != hipSuccess) return e;
+      e = ev0 ? hipEventRecord(ev0, st) : hipSuccess;
+    } else if (side) {
       e = big ? rc64::launch_match_reg(st, bk, bt, 0, ax, ev0, nullptr)
               : rc128::launch_match_reg(st, bk, bt, 0, ax, ev0, nullptr);
     } else {
@@ -2543,7 +2554,11 @@ hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* b
     }
     if (e != hipSuccess) return e;
     if ((e = launch_agg_group(st, bk, bt, ng, hot->ag)) != hipSuccess) return e;
-    return big ? rc64::launch_match_reg_cont(st, bk, bt, ng, ev1) : rc128::launch_match_reg_cont(st, bk, bt, ng, ev1);
+    e = big ? rc64::launch_match_reg_cont(st, bk, bt, ng, ev1) : rc128::launch_match_reg_cont(st, bk, bt, ng, ev1);
+    if (e != hipSuccess) return e;
+    // the next launch (its walk reads the buckets made here) and every completion event recorded on st
+    // after this (host batches' tapes) wait for the side jobs
+    return fork ? hipStreamWaitEvent(st, hot->sjoin, 0) : hipSuccess;
   }
   return big ? rc64::launch_match_reg(st, bk, bt, ng, ax, ev0, ev1)
              : rc128::launch_match_reg(st, bk, bt, ng, ax, ev0, ev1);

@@ -247,6 +247,10 @@ struct HotLaunch {
   bool agg = false;  // the aggregate path (me_agg.hip) instead of k_match_hot
   bool agg_reg = false;  // L <= 128: grouped launches through the aggregate path (me_agg.hip k_agg_gwalk)
   AggDev ag{};
+  // grouped aggregate launches: the side jobs (bucketing of the next group, tapes of the one before) on
+  // their own stream, forked before and joined after the group's walk / per-level launch / continuation
+  hipStream_t sst = nullptr;
+  hipEvent_t sfork = nullptr, sjoin = nullptr;
 };
 
 // Event counters kept on the device (BookDev::stats, me_stats_read).

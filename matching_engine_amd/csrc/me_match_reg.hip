@@ -827,17 +827,7 @@ __device__ __forceinline__ bool reg_reserve_overflow(RegCtx& c) {
 
 // ---- batch order of a bucket -----------------------------------------------------------------
 // Bitonic sort of 64 (one register) or 128 (two registers: element 64 + lane in b) distinct 32-bit
-// keys across the wave, ascending. Partners at lane distance 1 and 2 come over DPP, the rest
-// through ds_bpermute.
-template <int J>
-__device__ __forceinline__ uint32_t xor_lane(uint32_t v) {
-  if constexpr (J == 1)
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-  else if constexpr (J == 2)
-    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
-  else
-    return (uint32_t)__builtin_amdgcn_ds_bpermute((lane_id() ^ J) << 2, (int)v);
-}
+// keys across the wave, ascending; partners come over DPP / permlane swaps (xor_lane, me_wave.hpp).
 template <int J>
 __device__ __forceinline__ uint32_t bitonic_step(uint32_t v, bool asc) {
   const uint32_t p = xor_lane<J>(v);

@@ -60,6 +60,32 @@ __device__ __forceinline__ uint32_t scan16_sat(uint32_t x) {
   return x;
 }
 
+// v of lane (lane ^ J), with no LDS round trip (a ds_bpermute is a ~50-cycle dependent LDS access):
+// DPP inside a 16-lane row — quad_perm for 1 and 2, row_ror:8 for 8, two row rotations and a select for
+// 4 — and gfx950's permlane swaps across rows for 16 and 32 (the swap of a register with itself hands
+// each half the other's values in one of its two results).
+template <int J>
+__device__ __forceinline__ uint32_t xor_lane(uint32_t v) {
+  if constexpr (J == 1) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+  } else if constexpr (J == 2) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+  } else if constexpr (J == 4) {
+    const uint32_t up = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x12C, 0xF, 0xF, false);  // row_ror:12 (i + 4)
+    const uint32_t dn = (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xF, 0xF, false);  // row_ror:4 (i - 4)
+    return (lane_id() & 4) ? dn : up;
+  } else if constexpr (J == 8) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
+  } else if constexpr (J == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);  // rows {1,3} <-> rows {0,2}
+    return (lane_id() & 16) ? (uint32_t)r[0] : (uint32_t)r[1];
+  } else {
+    static_assert(J == 32, "xor_lane: J in {1, 2, 4, 8, 16, 32}");
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);  // lanes 32-63 <-> lanes 0-31
+    return (lane_id() & 32) ? (uint32_t)r[0] : (uint32_t)r[1];
+  }
+}
+
 // Global-address-space (1) pointers: an opaque round trip (vreg64, ldsu) would otherwise leave a
 // generic pointer, and vector memory ops on it would be flat_* (counted in both vmcnt and lgkmcnt)
 // instead of global_*.

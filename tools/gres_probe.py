@@ -41,6 +41,7 @@ def main():
     eng.sync()
     buf = np.zeros(sc.num_symbols * 24, dtype=np.uint64)
     lib.me_debug_stamps(eng.h, buf.ctypes.data, buf.size)
+    gw = buf.reshape(-1, 24)[:, 0:4].astype(np.float64)  # the walk's parts (cycles) and records, per symbol
     m = buf.reshape(-1, 24)[:, 16:24].astype(np.float64)
     t0 = m[:, 0].min()
     m -= t0
@@ -48,6 +49,10 @@ def main():
     print("walk start      ", pct(m[:, 0]))
     print("walk duration   ", pct(m[:, 1] - m[:, 0]))
     print("walk end        ", pct(m[:, 1]))
+    rec = np.maximum(gw[:, 3], 1)
+    for i, n in enumerate(["batch set-up", "block set-up", "record loop"]):
+        print(f"walk {n:13s}   ", pct(gw[:, i]), f"  per record (median) {np.median(gw[:, i] / rec):7.1f}")
+    print("walk records    ", pct(gw[:, 3]))
     print("gres start      ", pct(m[:, 2]))
     names = ["A sort", "B levels", "C scan+results", "D1 alloc+fills", "D2 place"]
     for i, n in enumerate(names):
