@@ -534,54 +534,89 @@ __device__ __forceinline__ uint32_t lw_get(const LWalk& w, int l) {
   return rl32(__hip_atomic_load(&w.tot[l], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP), 0);
 }
 
+// The ladder walk's log staging: event i of the current 64-event block is lane i of three VGPRs, written
+// by v_writelane (one instruction per field: no LDS access, no address arithmetic, no lane select), and
+// the block leaves as one 16-byte store per lane when it fills.
+struct LEv {
+  gptr<AggEv> ev;
+  uint32_t vl, vj, vq;  // lane i: event i of the block (level, record | AGG_TAKE, quantity)
+  uint32_t evp;         // next log index (the slot's log starts 64-aligned)
+};
+__device__ __forceinline__ void le_store(const LEv& e, uint32_t base, uint32_t n) {
+  AggEv x;
+  x.lvl = e.vl;
+  x.j = e.vj;
+  x.qty = (int)e.vq;
+  x.pad = 0u;
+  if ((uint32_t)lane_id() < n) e.ev[base + (uint32_t)lane_id()] = x;
+}
+__device__ __forceinline__ void le_emit(LEv& e, uint32_t lvl, uint32_t j, uint32_t q) {
+  const uint32_t slot = e.evp & 63u;
+  asm volatile(
+      "s_mov_b32 m0, %3\n\tv_writelane_b32 %0, %4, m0\n\tv_writelane_b32 %1, %5, m0\n\tv_writelane_b32 %2, %6, m0"
+      : "+v"(e.vl), "+v"(e.vj), "+v"(e.vq)
+      : "s"(slot), "s"(lvl), "s"(j), "s"(q)
+      : "m0");
+  e.evp += 1u;
+  if (ME_UNLIKELY(slot == 63u)) le_store(e, e.evp - 64u, 64u);
+}
+__device__ __forceinline__ void le_init(LEv& e, const AggDev& ag, uint32_t eb) {
+  e.ev = (gptr<AggEv>)vptr(ag.ev);
+  e.vl = e.vj = e.vq = 0u;
+  e.evp = eb;
+}
+__device__ __forceinline__ void le_end(LEv& e) {
+  if (e.evp & 63u) le_store(e, e.evp & ~63u, e.evp & 63u);
+}
+
 // A taker's partial take from the best level is the common case and stays out of the loop (no loop
 // entry, so none of the loop's register copies); the loop runs only when the best level empties.
-__device__ __forceinline__ void lw_take_buy(AWalk& e, LWalk& w, int lim, uint32_t& rem, uint32_t jt) {
+__device__ __forceinline__ void lw_take_buy(LEv& e, LWalk& w, int lim, uint32_t& rem, uint32_t jt) {
   if (w.ba > lim) return;  // (rem > 0: rejected records never reach the chain)
   if (ME_LIKELY(w.cba > rem)) {
     w.cba -= rem;
-    a_emit(e, w.ba, jt, (int)rem);
+    le_emit(e, (uint32_t)w.ba, jt, rem);
     rem = 0;
     return;
   }
   while (true) {  // the best level empties
-    a_emit(e, w.ba, jt, (int)w.cba);
+    le_emit(e, (uint32_t)w.ba, jt, w.cba);
     rem -= w.cba;
     lw_put(w, w.ba, 0u);  // empty levels hold 0 (a rest there adds)
     w.ba = lw_next(w, w.ba + 1, w.cba);
     if (!rem || w.ba > lim) return;
     if (w.cba > rem) {
       w.cba -= rem;
-      a_emit(e, w.ba, jt, (int)rem);
+      le_emit(e, (uint32_t)w.ba, jt, rem);
       rem = 0;
       return;
     }
   }
 }
-__device__ __forceinline__ void lw_take_sell(AWalk& e, LWalk& w, int lim, uint32_t& rem, uint32_t jt) {
+__device__ __forceinline__ void lw_take_sell(LEv& e, LWalk& w, int lim, uint32_t& rem, uint32_t jt) {
   if (w.bb < lim) return;
   if (ME_LIKELY(w.cbb > rem)) {
     w.cbb -= rem;
-    a_emit(e, w.bb, jt, (int)rem);
+    le_emit(e, (uint32_t)w.bb, jt, rem);
     rem = 0;
     return;
   }
   while (true) {
-    a_emit(e, w.bb, jt, (int)w.cbb);
+    le_emit(e, (uint32_t)w.bb, jt, w.cbb);
     rem -= w.cbb;
     lw_put(w, w.bb, 0u);
     w.bb = lw_prev(w, w.bb - 1, w.cbb);
     if (!rem || w.bb < lim) return;
     if (w.cbb > rem) {
       w.cbb -= rem;
-      a_emit(e, w.bb, jt, (int)rem);
+      le_emit(e, (uint32_t)w.bb, jt, rem);
       rem = 0;
       return;
     }
   }
 }
 // a bid rests at l (< ba: every ask up to the limit was taken)
-__device__ __forceinline__ void lw_rest_buy(AWalk& e, LWalk& w, int l, uint32_t q, uint32_t jt) {
+__device__ __forceinline__ void lw_rest_buy(LEv& e, LWalk& w, int l, uint32_t q, uint32_t jt) {
   if (l == w.bb) {
     w.cbb += q;
   } else if (l > w.bb) {  // a new best bid (an empty level)
@@ -591,9 +626,9 @@ __device__ __forceinline__ void lw_rest_buy(AWalk& e, LWalk& w, int l, uint32_t 
   } else {
     lw_add(w, l, q);
   }
-  a_emit(e, l, jt, (int)q);
+  le_emit(e, (uint32_t)l, jt, q);
 }
-__device__ __forceinline__ void lw_rest_sell(AWalk& e, LWalk& w, int l, uint32_t q, uint32_t jt) {
+__device__ __forceinline__ void lw_rest_sell(LEv& e, LWalk& w, int l, uint32_t q, uint32_t jt) {
   if (l == w.ba) {
     w.cba += q;
   } else if (l < w.ba) {
@@ -603,7 +638,7 @@ __device__ __forceinline__ void lw_rest_sell(AWalk& e, LWalk& w, int l, uint32_t
   } else {
     lw_add(w, l, q);
   }
-  a_emit(e, l, jt, (int)q);
+  le_emit(e, (uint32_t)l, jt, q);
 }
 
 // The ladder from HBM: 32-bit LDS totals, the cached best totals, the book's sum (false: LW_CAP or more,
@@ -668,7 +703,7 @@ __device__ __forceinline__ uint32_t lw_cw(uint32_t okd, int olm, uint32_t rj, in
   return (uint32_t)lim | (buy ? LW_BUY : 0u) | (mkt ? LW_MKT : 0u) | (rj << LW_RJ_SHIFT);
 }
 
-__device__ __forceinline__ uint32_t lw_block(AWalk& e, LWalk& w, int oq, uint32_t ocw, uint32_t ojt,
+__device__ __forceinline__ uint32_t lw_block(LEv& e, LWalk& w, int oq, uint32_t ocw, uint32_t ojt,
                                              unsigned long long fastm, uint32_t cnt, int& rr) {
   // the records the walk covers run up to the first it does not (k); rejected ones need no chain work:
   // the loop visits the set bits of `work` (a scalar bit scan, no per-record tests)
@@ -678,17 +713,23 @@ __device__ __forceinline__ uint32_t lw_block(AWalk& e, LWalk& w, int oq, uint32_
   unsigned long long work = (k >= 64u ? ~0ull : ((1ull << k) - 1ull)) & ~rjm;
   while (work) {
     const int r = __builtin_ctzll(work);
-    work &= work - 1ull;
+    asm volatile("s_bitset0_b64 %0, %1" : "+s"(work) : "s"(r));  // (one SALU op; work & (work - 1) is three)
     const uint32_t cw = rl32(ocw, r);
     const uint32_t jt = rl32(ojt, r);
     const int lim = (int)(cw & LW_LIM);
     uint32_t rem = (uint32_t)rli32(oq, r);
+    // (a MARKET's remainder is dropped: the rest is decided by one integer test — the opaque copy keeps
+    // the compiler from re-deriving `!market && rem` as 64-bit boolean masks)
     if (cw & LW_BUY) {
       lw_take_buy(e, w, lim, rem, jt | AGG_TAKE);
-      if (!(cw & LW_MKT) && rem) lw_rest_buy(e, w, lim, rem, jt);
+      uint32_t rq = (cw & LW_MKT) ? 0u : rem;
+      asm volatile("" : "+s"(rq));
+      if (rq) lw_rest_buy(e, w, lim, rq, jt);
     } else {
       lw_take_sell(e, w, lim, rem, jt | AGG_TAKE);
-      if (!(cw & LW_MKT) && rem) lw_rest_sell(e, w, lim, rem, jt);
+      uint32_t rq = (cw & LW_MKT) ? 0u : rem;
+      asm volatile("" : "+s"(rq));
+      if (rq) lw_rest_sell(e, w, lim, rq, jt);
     }
     asm volatile("s_mov_b32 m0, %1\n\tv_writelane_b32 %0, %2, m0" : "+v"(rr) : "s"(r), "s"(auniu(rem)) : "m0");
   }
@@ -781,6 +822,8 @@ __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const Agg
   // ag.ladder_max levels
   AList A, B;  // asks (side 1), bids (side 0)
   LWalk lw;
+  LEv le;
+  le_init(le, ag, eb);
   const bool ladder = L <= (int)ag.ladder_max && lw_init(lw, bk, s, ltot, bb0, ba0);
   if (!ladder) {
     a_rebuild<1>(w, A, ba0);
@@ -821,7 +864,7 @@ __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const Agg
     uint32_t k;
     if (ladder) {
       const bool adm = lw_admit(lw, v ? oq : 0);  // else: the generic loop from this block on
-      k = lw_block(w, lw, oq, lw_cw(okd, olm, rj, L), j, adm ? fastm : 0ull, cntb, rr);
+      k = lw_block(le, lw, oq, lw_cw(okd, olm, rj, L), j, adm ? fastm : 0ull, cntb, rr);
     } else {
       a_refill(w, A, B);
       ARes R;
@@ -839,7 +882,8 @@ __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const Agg
   }
   int bb, ba;
   if (ladder) {
-    if (w.evp & 63u) a_evstore(w, w.evp & ~63u, w.evp & 63u);
+    le_end(le);
+    w.evp = le.evp;
     lw_end(lw, bk, s);
     bb = lw.bb;
     ba = lw.ba;
@@ -1644,10 +1688,8 @@ __device__ __forceinline__ uint32_t a_ghand(const BookDev& bk, uint32_t s, uint3
 }
 
 __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDev ag) {
-  __shared__ unsigned long long locc[2];
   __shared__ AStage stg;
   __shared__ uint32_t ltot[128 + 64];
-  __shared__ AggEv evstg[128];
   const int lane = lane_id();
   const int L = (int)bk.L;  // <= 128
   const uint32_t ng = ga.ng;
@@ -1704,8 +1746,8 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
         if (lane == 0) slot->free_head = fc;
       }
     }
-    AWalk w;
-    a_walk_init(w, bk, ag, s, eb, locc, evstg);
+    LEv w;
+    le_init(w, ag, eb);
     LWalk lw;
     const bool lok = lw_init(lw, bk, s, ltot, bb0, ba0);  // else: the continuation from the first record
     uint32_t hidx = NIL, gstop = ng;
@@ -1781,7 +1823,7 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
     for (uint32_t g = (gstop < ng ? gstop + 1u : ng) + (uint32_t)lane; g <= ng; g += 64)
       *a_gtab(ag.gev, s, g) = w.evp;
     if (gstop < ng && lane == 0) *a_gtab(ag.gev, s, gstop + 1u) = w.evp;
-    if (w.evp & 63u) a_evstore(w, w.evp & ~63u, w.evp & 63u);
+    le_end(w);
     if (lok) lw_end(lw, bk, s);  // (else the LDS copy is truncated and nothing was walked)
     const int bb = lw.bb, ba = lw.ba;
     if (lane == 0) {
