@@ -271,7 +271,7 @@ struct me_engine {
   // memory ahead of every match launch; a synchronous exact count replaces it when it is too stale.
   static constexpr uint32_t ADM_RING = 256;
   unsigned long long* pub_host = nullptr;  // hipHostMalloc'd, device-mapped (bk.pub): [0] {launch, resting},
-                                           // [1] {launch, hand-offs}
+                                           // [1] {launch, hand-offs}, [2] me_sync's error-word copy
   // grouped launches through the aggregate path (hot.agg_reg) chosen by shape, not by ME_REG_AGG: turned
   // off for good when symbols hand off to the continuation in more than 1/16 of their launches (cancels,
   // far prices — config 5's stream), which then pays both paths
@@ -616,10 +616,11 @@ extern "C" me_engine* me_create(const me_config* cfg) {
       return bail(std::string("hipMemset agg ctr: ") + hipGetErrorString(he));
     bk.agg_ctr = a.ctr;
   }
-  if ((he = hipHostMalloc((void**)&e->pub_host, 2 * sizeof(unsigned long long), hipHostMallocDefault)) != hipSuccess ||
+  if ((he = hipHostMalloc((void**)&e->pub_host, 4 * sizeof(unsigned long long), hipHostMallocDefault)) != hipSuccess ||
       (he = hipHostGetDevicePointer((void**)&bk.pub, e->pub_host, 0)) != hipSuccess)
     return bail(std::string("me_create: pinned admission word: ") + hipGetErrorString(he));
   e->pub_host[0] = e->pub_host[1] = 0ull;  // {0 launches, 0 resting / hand-offs}
+  e->pub_host[2] = e->pub_host[3] = 0ull;  // [2]: me_sync's copy of the error word
   ALLOC(bk.chunk_top, 1);
   ALLOC(bk.err, 1);
   uint32_t* gsym = nullptr;
@@ -1239,9 +1240,13 @@ extern "C" int me_sync(me_engine* e) {
     int rc = flush_pipeline(e);
     if (rc) return rc;
   }
+  // the error word rides behind the last launch into pinned memory: one stream synchronisation, not a
+  // second synchronous round trip after it
+  uint32_t* w = reinterpret_cast<uint32_t*>(e->pub_host + 2);
+  HIP_TRY(hipMemcpyAsync(w, e->bk.err, 4, hipMemcpyDeviceToHost, e->stream), "D2H error word");
   HIP_TRY(hipStreamSynchronize(e->stream), "hipStreamSynchronize");
   if (e->failed) return ME_E_STATE;
-  return check_err_word(e);
+  return check_err_bits(e, *(volatile uint32_t*)w);
 }
 
 extern "C" int me_fetch_outputs(me_engine* e, me_fill* out_fills, size_t fills_cap, size_t* n_fills,
