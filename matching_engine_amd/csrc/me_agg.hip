@@ -1995,10 +1995,14 @@ __global__ __launch_bounds__(1024) void k_agg_gemit(BookDev bk, AggGArgs ga, Agg
 // The per-event LDS arrays hold `ne` events (the launch sizes them from the group's mean records per
 // symbol); a symbol with a longer log keeps them in the log's own HBM regions (AggDev::evn / evs) instead.
 // ~16 KB of static LDS and a register budget of GR_WPE waves per SIMD.
-constexpr int GR_WAVES = 8;
+#ifndef GR_WAVES
+#define GR_WAVES 8  // waves per workgroup (same-box A/B)
+#endif
 constexpr uint32_t GR_THREADS = GR_WAVES * 64;
 #ifndef GR_WPE
-#define GR_WPE 6  // waves per SIMD the register budget is cut for (same-box A/B: 5 / 6 / 8)
+#define GR_WPE 8  // waves per SIMD the register budget is cut for: 8 puts all four workgroups of a CU (1,024
+                  // symbols) in one round (same-box A/B, profiles/r4/g2: 640 steps 2,300 -> 2,515M, the group
+                  // launch 588 -> 560 us at the driver shape; 6 was the round-3 choice)
 #endif
 constexpr uint32_t GR_STAGE = 48;  // consumed makers / emptied chunks a level stages in LDS (else: HBM)
 
