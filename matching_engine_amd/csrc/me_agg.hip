@@ -568,10 +568,41 @@ __device__ __forceinline__ void le_init(LEv& e, const AggDev& ag, uint32_t eb) {
 __device__ __forceinline__ void le_end(LEv& e) {
   if (e.evp & 63u) le_store(e, e.evp & ~63u, e.evp & 63u);
 }
+// Grouped launches: 8-B events (AggGEv), two VGPRs — the level and the record number share one word
+// (jt already holds record << AGG_GREC_SHIFT | AGG_TAKE), so an event is one SALU or and two v_writelane.
+struct LEvG {
+  gptr<AggGEv> ev;
+  uint32_t vw, vq;
+  uint32_t evp;
+};
+__device__ __forceinline__ void le_store(const LEvG& e, uint32_t base, uint32_t n) {
+  AggGEv x;
+  x.w = e.vw;
+  x.qty = (int)e.vq;
+  if ((uint32_t)lane_id() < n) e.ev[base + (uint32_t)lane_id()] = x;
+}
+__device__ __forceinline__ void le_emit(LEvG& e, uint32_t lvl, uint32_t j, uint32_t q) {
+  const uint32_t slot = e.evp & 63u;
+  asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %3, m0\n\tv_writelane_b32 %1, %4, m0"
+               : "+v"(e.vw), "+v"(e.vq)
+               : "s"(slot), "s"(lvl | j), "s"(q)
+               : "m0");
+  e.evp += 1u;
+  if (ME_UNLIKELY(slot == 63u)) le_store(e, e.evp - 64u, 64u);
+}
+__device__ __forceinline__ void le_init(LEvG& e, AggGEv* ev, uint32_t eb) {
+  e.ev = (gptr<AggGEv>)vptr(ev);
+  e.vw = e.vq = 0u;
+  e.evp = eb;
+}
+__device__ __forceinline__ void le_end(LEvG& e) {
+  if (e.evp & 63u) le_store(e, e.evp & ~63u, e.evp & 63u);
+}
 
 // A taker's partial take from the best level is the common case and stays out of the loop (no loop
 // entry, so none of the loop's register copies); the loop runs only when the best level empties.
-__device__ __forceinline__ void lw_take_buy(LEv& e, LWalk& w, int lim, uint32_t& rem, uint32_t jt) {
+template <class LE>
+__device__ __forceinline__ void lw_take_buy(LE& e, LWalk& w, int lim, uint32_t& rem, uint32_t jt) {
   if (w.ba > lim) return;  // (rem > 0: rejected records never reach the chain)
   if (ME_LIKELY(w.cba > rem)) {
     w.cba -= rem;
@@ -593,7 +624,8 @@ __device__ __forceinline__ void lw_take_buy(LEv& e, LWalk& w, int lim, uint32_t&
     }
   }
 }
-__device__ __forceinline__ void lw_take_sell(LEv& e, LWalk& w, int lim, uint32_t& rem, uint32_t jt) {
+template <class LE>
+__device__ __forceinline__ void lw_take_sell(LE& e, LWalk& w, int lim, uint32_t& rem, uint32_t jt) {
   if (w.bb < lim) return;
   if (ME_LIKELY(w.cbb > rem)) {
     w.cbb -= rem;
@@ -616,7 +648,8 @@ __device__ __forceinline__ void lw_take_sell(LEv& e, LWalk& w, int lim, uint32_t
   }
 }
 // a bid rests at l (< ba: every ask up to the limit was taken)
-__device__ __forceinline__ void lw_rest_buy(LEv& e, LWalk& w, int l, uint32_t q, uint32_t jt) {
+template <class LE>
+__device__ __forceinline__ void lw_rest_buy(LE& e, LWalk& w, int l, uint32_t q, uint32_t jt) {
   if (l == w.bb) {
     w.cbb += q;
   } else if (l > w.bb) {  // a new best bid (an empty level)
@@ -628,7 +661,8 @@ __device__ __forceinline__ void lw_rest_buy(LEv& e, LWalk& w, int l, uint32_t q,
   }
   le_emit(e, (uint32_t)l, jt, q);
 }
-__device__ __forceinline__ void lw_rest_sell(LEv& e, LWalk& w, int l, uint32_t q, uint32_t jt) {
+template <class LE>
+__device__ __forceinline__ void lw_rest_sell(LE& e, LWalk& w, int l, uint32_t q, uint32_t jt) {
   if (l == w.ba) {
     w.cba += q;
   } else if (l < w.ba) {
@@ -703,7 +737,9 @@ __device__ __forceinline__ uint32_t lw_cw(uint32_t okd, int olm, uint32_t rj, in
   return (uint32_t)lim | (buy ? LW_BUY : 0u) | (mkt ? LW_MKT : 0u) | (rj << LW_RJ_SHIFT);
 }
 
-__device__ __forceinline__ uint32_t lw_block(LEv& e, LWalk& w, int oq, uint32_t ocw, uint32_t ojt,
+// (record r of the block logs its events with jt = (jb + r) << JS: scalar arithmetic, no v_readlane)
+template <int JS, class LE>
+__device__ __forceinline__ uint32_t lw_block(LE& e, LWalk& w, int oq, uint32_t ocw, uint32_t jb,
                                              unsigned long long fastm, uint32_t cnt, int& rr) {
   // the records the walk covers run up to the first it does not (k); rejected ones need no chain work:
   // the loop visits the set bits of `work` (a scalar bit scan, no per-record tests)
@@ -715,7 +751,7 @@ __device__ __forceinline__ uint32_t lw_block(LEv& e, LWalk& w, int oq, uint32_t 
     const int r = __builtin_ctzll(work);
     asm volatile("s_bitset0_b64 %0, %1" : "+s"(work) : "s"(r));  // (one SALU op; work & (work - 1) is three)
     const uint32_t cw = rl32(ocw, r);
-    const uint32_t jt = rl32(ojt, r);
+    const uint32_t jt = (jb + (uint32_t)r) << JS;
     const int lim = (int)(cw & LW_LIM);
     uint32_t rem = (uint32_t)rli32(oq, r);
     // (a MARKET's remainder is dropped: the rest is decided by one integer test — the opaque copy keeps
@@ -737,7 +773,7 @@ __device__ __forceinline__ uint32_t lw_block(LEv& e, LWalk& w, int oq, uint32_t 
 }
 
 // A record's result from its fields and the remainder the chain left (vector form); fill count and
-// scratch start come later (k_agg_fin / k_agg_gfin, from the log).
+// scratch start come later (k_agg_fin / k_agg_gres, from the log).
 __device__ __forceinline__ me_order_result a_result(int oq, uint32_t okd, uint32_t rj, int rem) {
   const bool mkt = (okd >> 2) & 1u;
   const int filled = rj ? 0 : oq - rem;
@@ -864,7 +900,7 @@ __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const Agg
     uint32_t k;
     if (ladder) {
       const bool adm = lw_admit(lw, v ? oq : 0);  // else: the generic loop from this block on
-      k = lw_block(le, lw, oq, lw_cw(okd, olm, rj, L), j, adm ? fastm : 0ull, cntb, rr);
+      k = lw_block<0>(le, lw, oq, lw_cw(okd, olm, rj, L), blk, adm ? fastm : 0ull, cntb, rr);
     } else {
       a_refill(w, A, B);
       ARes R;
@@ -1609,9 +1645,10 @@ __global__ __launch_bounds__(1024) void k_agg_emit(BookDev bk, BatchDev bt, AggD
 // ------------------------------------------------------------------ grouped launches (L <= 128)
 // The register-window path's groups of up to ME_GMAX bucketed batches, every symbol through the
 // aggregate path: k_agg_gwalk (one wave per symbol over its records of every batch of the group, from
-// the batches' buckets, in batch order) replaces k_match_reg's serial loop; the per-level kernels are
-// the hot path's; k_agg_gfin / k_agg_gemit place each batch's fills in its own scratch (the symbol's
-// slab, or the overflow region) and fill in the results the pipeline's tape job reads. A record the walk
+// the batches' buckets, in batch order) replaces k_match_reg's serial loop, logging 8-B events (AggGEv);
+// k_agg_gres (one workgroup per symbol) resolves every level's FIFO, places each batch's fills in its own
+// scratch (the symbol's slab, or the overflow region) and fills in the results the pipeline's tape job
+// reads. A record the walk
 // does not cover (a cancel, a price outside the window, a bucket past BK_CAP records) hands the symbol's
 // rest of the group to k_match_reg's continuation launch (me_match_reg.hip, kSlow).
 struct AggGArgs {
@@ -1715,6 +1752,8 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
       o.s = s;
       o.base = base;
       o.ev_base = eb;
+      o.lo = evneed;  // the region: evneed 8-B events, then the records' seqs and positions [total] each
+      o.hi = total;   // (8 evneed + 8 total <= 16 evneed bytes: the region reserved in 16-B units)
       o.free_head = st.free_head;
       o.resting0 = resting;
       o.bb = bb0;
@@ -1736,7 +1775,7 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
       continue;
     }
     // free chunks k_match_reg parked in fcache[s][0, nfree) join the front of the free list (one header
-    // store per lane), so k_agg_alloc reuses them before it takes fresh chunks; k_agg_gfin writes nfree = 0
+    // store per lane), so k_agg_gres reuses them before it takes fresh chunks, and writes nfree = 0
     {
       const uint32_t nfc = min(rl32(st.nfree, 0), 64u);
       if (nfc) {
@@ -1746,8 +1785,14 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
         if (lane == 0) slot->free_head = fc;
       }
     }
-    LEv w;
-    le_init(w, ag, eb);
+    LEvG w;
+    AggGEv* const log8 = reinterpret_cast<AggGEv*>(ag.ev + eb);
+    le_init(w, log8, 0u);  // (w.evp: relative to the region)
+    // the records' seqs (offset from the group's first) and grouped positions, in walk order
+    const gptr<uint32_t> rsq = vptr(reinterpret_cast<uint32_t*>(log8 + evneed));
+    const gptr<uint32_t> rjs = rsq + total;
+    const unsigned long long gmin = *ga.seq0;
+    uint32_t rbase = 0;
     LWalk lw;
     const bool lok = lw_init(lw, bk, s, ltot, bb0, ba0);  // else: the continuation from the first record
     uint32_t hidx = NIL, gstop = ng;
@@ -1755,7 +1800,7 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
     const size_t bko = (size_t)s * BK_CAP;
     BkRec n0 = ga.b_rec[0][bko + lane], n1 = ga.b_rec[0][bko + 64 + lane];
     for (uint32_t g = 0; g < ng; ++g) {
-      if (lane == 0) *a_gtab(ag.gev, s, g) = w.evp;
+      if (lane == 0) *a_gtab(ag.gev, s, g) = eb + w.evp;
       const uint32_t cnt = rl32(nsv, (int)g);
       const BkRec r0 = n0, r1 = n1;
       if (g + 1u < ng) {
@@ -1801,15 +1846,21 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
         const unsigned long long fastm = __ballot(a_classify(v, oseq, opx, oq, okd, base, L, nfar0, nfar1, rj, olm));
         int rr = 0;
         const bool adm = lok && lw_admit(lw, v ? oq : 0);
+        if (v) {
+          rsq[rbase + (uint32_t)lane] = (uint32_t)(oseq - gmin);
+          rjs[rbase + (uint32_t)lane] = (g << AGG_GSHIFT) | oi;
+        }
         GW_T(1);
-        const uint32_t k = lw_block(w, lw, oq, lw_cw(okd, olm, rj, L), (g << AGG_GSHIFT) | oi, adm ? fastm : 0ull, cntb, rr);
+        const uint32_t k = lw_block<AGG_GREC_SHIFT>(w, lw, oq, lw_cw(okd, olm, rj, L), rbase, adm ? fastm : 0ull,
+                                                     cntb, rr);
+        rbase += cntb;
         GW_T(2);
 #ifdef ME_STAMPS
         gw_t[3] += k;
 #endif
-        if (v && (uint32_t)lane < k) res[oi] = a_result(oq, okd, rj, rr);  // fills: k_agg_gfin
+        if (v && (uint32_t)lane < k) res[oi] = a_result(oq, okd, rj, rr);  // fills: k_agg_gres
         if (k < cntb) {
-          hidx = a_ghand(bk, s, g, blk + k, cnt, 0u, 0u);  // scratch position: k_agg_gfin
+          hidx = a_ghand(bk, s, g, blk + k, cnt, 0u, 0u);  // scratch position: k_agg_gres
           stop = true;
           break;
         }
@@ -1821,13 +1872,13 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
     }
     // the log's end for every batch from the stop on
     for (uint32_t g = (gstop < ng ? gstop + 1u : ng) + (uint32_t)lane; g <= ng; g += 64)
-      *a_gtab(ag.gev, s, g) = w.evp;
-    if (gstop < ng && lane == 0) *a_gtab(ag.gev, s, gstop + 1u) = w.evp;
+      *a_gtab(ag.gev, s, g) = eb + w.evp;
+    if (gstop < ng && lane == 0) *a_gtab(ag.gev, s, gstop + 1u) = eb + w.evp;
     le_end(w);
     if (lok) lw_end(lw, bk, s);  // (else the LDS copy is truncated and nothing was walked)
     const int bb = lw.bb, ba = lw.ba;
     if (lane == 0) {
-      slot->ev_cnt = w.evp - eb;
+      slot->ev_cnt = w.evp;
       slot->bb = bb;
       slot->ba = ba;
       slot->active = 1;
@@ -1842,149 +1893,13 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
   }
 }
 
-// One workgroup per symbol: the fill offsets (scan of the events' fill counts in log order), each
-// batch's share placed in the symbol's slab of that batch (or the overflow region), the results' fill
-// counts and scratch starts, the symbol's state, the continuation's scratch position.
-__global__ __launch_bounds__(1024) void k_agg_gfin(BookDev bk, AggGArgs ga, AggDev ag) {
-  __shared__ uint32_t wsum[16];
-  __shared__ uint32_t carry_s;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  constexpr uint32_t PER = 8;
-  for (uint32_t s = blockIdx.x; s < bk.S; s += gridDim.x) {
-    const AggSlot sl = ag.slot[s];
-    if (!sl.active) continue;
-    const uint32_t eb = sl.ev_base, n = sl.ev_cnt;
-    uint32_t carry = 0;
-    for (uint32_t t0 = 0; t0 < n; t0 += 1024 * PER) {
-      const uint32_t b = t0 + (uint32_t)tid * PER;
-      uint32_t v[PER], loc = 0;
-#pragma unroll
-      for (uint32_t k = 0; k < PER; ++k) {
-        v[k] = b + k < n ? ag.evn[eb + b + k] : 0u;
-        loc += v[k];
-      }
-      uint32_t x = loc;
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t t = __shfl_up(x, d, 64);
-        if (lane >= d) x += t;
-      }
-      if (lane == 63) wsum[wv] = x;
-      __syncthreads();
-      uint32_t pre = 0, tot = 0;
-      for (int k = 0; k < 16; ++k) {
-        if (k < wv) pre += wsum[k];
-        tot += wsum[k];
-      }
-      uint32_t r = carry + pre + x - loc;
-#pragma unroll
-      for (uint32_t k = 0; k < PER; ++k)
-        if (b + k < n) {
-          ag.evx[eb + b + k] = r;
-          r += v[k];
-        }
-      carry += tot;
-      __syncthreads();
-    }
-    if (tid == 0) carry_s = carry;
-    __syncthreads();
-    const uint32_t ftot = carry_s;
-    auto EX = [&](uint32_t e) -> uint32_t { return e < eb + n ? ag.evx[e] : ftot; };
-    // each batch's fills: the symbol's slab of that batch if they fit, else the overflow region
-    if ((uint32_t)tid < ga.ng) {
-      const uint32_t g = (uint32_t)tid;
-      const uint32_t x0 = EX(*a_gtab(ag.gev, s, g)), x1 = EX(*a_gtab(ag.gev, s, g + 1));
-      const uint32_t f = x1 - x0;
-      unsigned long long b0 = (unsigned long long)s * ga.slab;
-      if (f > ga.slab) {
-        b0 = ga.ovf_base + atomicAdd(ga.scratch_top[g], (unsigned long long)f);
-        if (b0 + f > ga.scratch_cap) {
-          atomicOr(bk.err, ERR_SCRATCH_OOM);
-          b0 = 0;
-        }
-      }
-      *a_gtab(ag.gex, s, g) = x0;
-      *a_gtab(ag.gbase, s, g) = (uint32_t)b0;
-    }
-    __syncthreads();
-    // the first take of each record: its fill count and scratch start
-    for (uint32_t t = (uint32_t)tid; t < n; t += 1024) {
-      const uint32_t e = eb + t;
-      const uint32_t j = ag.ev[e].j;
-      if (!(j & AGG_TAKE) || (t > 0 && ag.ev[e - 1].j == j)) continue;
-      const uint32_t g = (j & ~AGG_TAKE) >> AGG_GSHIFT, oi = j & AGG_IMASK;
-      me_order_result* res = ga.res[g];
-      uint32_t nte = 1;  // the record's take events follow each other in the log
-      while (t + nte < n && ag.ev[e + nte].j == j) ++nte;
-      const uint32_t x0 = EX(e), nfill = EX(e + nte) - x0;
-      res[oi].fill_count = nfill;
-      res[oi].tape_offset = *a_gtab(ag.gbase, s, g) + (x0 - *a_gtab(ag.gex, s, g));
-      if (nfill) atomicAdd(&ga.tile_sum[g][oi / TILE_TAPE], nfill);
-    }
-    if (tid == 0) {
-      SymState o = bk.sym[s];
-      o.best_bid = sl.bb;
-      o.best_ask = sl.ba;
-      o.free_head = ag.slot[s].free_head;
-      o.nfree = 0;  // the walk linked the parked chunks into the free list
-      const int dr = ag.slot[s].dresting;
-      o.resting = (uint32_t)((int)sl.resting0 + dr);
-      bk.sym[s] = o;
-      if (dr) atomicAdd(bk.stats + ST_RESTING, (unsigned long long)(long long)dr);
-      if (sl.hidx != NIL) {  // the continuation goes on behind the walk's fills of its batch
-        const uint32_t g = sl.pos;
-        const uint32_t x0 = *a_gtab(ag.gex, s, g);
-        const uint32_t f = EX(*a_gtab(ag.gev, s, g + 1)) - x0;
-        const uint32_t b0 = *a_gtab(ag.gbase, s, g);
-        const bool in_slab = f <= ga.slab;
-        bk.hand[sl.hidx].wptr = b0 + f;
-        bk.hand[sl.hidx].wend = in_slab ? s * ga.slab + ga.slab : b0 + f;
-      }
-    }
-    __syncthreads();
-  }
-}
-
-// One thread per take event: its fills into its batch's scratch.
-__global__ __launch_bounds__(1024) void k_agg_gemit(BookDev bk, AggGArgs ga, AggSrc src, AggDev ag) {
-  for (uint32_t s = blockIdx.x; s < bk.S; s += gridDim.x) {
-    const AggSlot sl = ag.slot[s];
-    if (!sl.active) continue;
-    const uint32_t eb = sl.ev_base, n = sl.ev_cnt;
-    for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) {
-      const uint32_t e = eb + t;
-      const AggEv E = ag.ev[e];
-      if (!(E.j & AGG_TAKE)) continue;
-      const uint32_t nf = ag.evn[e];
-      if (!nf) continue;
-      const uint32_t j = E.j & ~AGG_TAKE, g = j >> AGG_GSHIFT;
-      const uint32_t first = ag.evf[e];
-      const unsigned long long a = ag.eva[e], z = a + (unsigned long long)E.qty;
-      const uint32_t p = *a_gtab(ag.gbase, s, g) + (ag.evx[e] - *a_gtab(ag.gex, s, g));
-      me_fill f;
-      f.taker_seq = a_seq_of(src, j);
-      f.price_q4 = sl.base + (long long)E.lvl;
-      f.symbol = sl.gs;
-      me_fill* sc = ga.scratch[g];
-      unsigned long long lo = a;
-      for (uint32_t k = 0; k < nf; ++k) {
-        const AggMk m = ag.mk[first + k];
-        const unsigned long long hi = m.end < z ? m.end : z;
-        f.maker_seq = m.seq;
-        f.qty = (int)(hi - lo);
-        sc[p + k] = f;
-        lo = hi;
-      }
-    }
-  }
-}
-
 // ------------------------------------------------------------------ grouped launches: one workgroup per symbol
-// k_agg_gres does the work of k_agg_group ... k_agg_gemit for a grouped launch in ONE launch, one 512-thread
-// workgroup per symbol (the walk's workgroup of the same symbol ran on the same XCD, blockIdx = symbol):
+// k_agg_gres does the work of the hot path's k_agg_group ... k_agg_emit for a grouped launch in ONE launch,
+// one 512-thread workgroup per symbol (the walk's workgroup of the same symbol ran on the same XCD,
+// blockIdx = symbol):
 //   A  the symbol's log sorted by level in LDS (per-wave histograms of contiguous log ranges, a stable
-//      ballot-multisplit scatter of 16-bit log indices); each event's seq gathered once, in parallel, into
-//      the event itself (its offset from the group's first seq) — no sorted copies, segment tables or
-//      per-event arrays in HBM;
+//      ballot-multisplit scatter of 16-bit log indices) — no sorted copies, segment tables or per-event
+//      arrays in HBM; a seq is read from the symbol's own record array beside its log (the walk wrote it);
 //   B  its levels resolved by the waves (a level per wave, taken from an LDS counter): the initial FIFO
 //      walked until the group's takes are covered, consumed makers, emptied chunks, each take's fill count
 //      into an LDS array indexed by log position; the slot's cursors are LDS atomics, not pool-wide ones;
@@ -2043,7 +1958,10 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint32_t L = bk.L;  // <= 128
   const uint32_t eb = sl.ev_base, n = sl.ev_cnt, ng = ga.ng;
-  AggEv* ev = ag.ev + eb;
+  const AggGEv* ev = reinterpret_cast<const AggGEv*>(ag.ev + eb);
+  const uint32_t* rsq = reinterpret_cast<const uint32_t*>(ev + sl.lo);  // the records' seq offsets ...
+  const uint32_t* rjs = rsq + sl.hi;                                    // ... and grouped positions
+  auto erec = [](uint32_t w) -> uint32_t { return (w & ~AGG_TAKE) >> AGG_GREC_SHIFT; };
   const size_t lo_l = (size_t)s * L;
   // every seq of the group lies in [gmin, gmin + seq_ring) (k_seq_sweep's check; seq_ring <= 2^32 here)
   const unsigned long long gmin = *ga.seq0;
@@ -2064,19 +1982,14 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
   sh.u.wh[wv][lane] = 0u;
   sh.u.wh[wv][64 + lane] = 0u;
   wave_mem_order();
-  // each wave owns a contiguous 64-aligned log range: its level histogram, the events' seqs (into the
-  // events' pad: offset from gmin), then a stable scatter of the same range
+  // each wave owns a contiguous 64-aligned log range: its level histogram, then a stable scatter of the
+  // same range
   const uint32_t per = ((n + GR_WAVES - 1u) / GR_WAVES + 63u) & ~63u;
   const uint32_t r0 = min(n, (uint32_t)wv * per), r1 = min(n, r0 + per);
 #pragma unroll 4
   for (uint32_t b = r0; b < r1; b += 64) {
     const uint32_t e = b + (uint32_t)lane;
-    if (e < r1) {
-      const AggEv E = ev[e];
-      atomicAdd(&sh.u.wh[wv][E.lvl & 127u], 1u);
-      const uint32_t j = E.j & ~AGG_TAKE;
-      ev[e].pad = (uint32_t)(src.seq[j >> AGG_GSHIFT][j & AGG_IMASK] - gmin);
-    }
+    if (e < r1) atomicAdd(&sh.u.wh[wv][ev[e].w & AGG_GLVL_MASK], 1u);
   }
   __syncthreads();
   if (wv == 0) {
@@ -2107,7 +2020,7 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
   for (uint32_t b = r0; b < r1; b += 64) {
     const uint32_t e = b + (uint32_t)lane;
     const bool v = e < r1;
-    const uint32_t key = v ? (ev[e].lvl & 127u) : 0u;
+    const uint32_t key = v ? (ev[e].w & AGG_GLVL_MASK) : 0u;
     unsigned long long peers = __ballot(v);
 #pragma unroll
     for (uint32_t bit = 0; bit < 7; ++bit) {
@@ -2128,8 +2041,8 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
   const bool act = lane < ME_C;
   AggMk* mkl = sh.u.st[wv].mk;
   uint32_t* frl = sh.u.st[wv].fr;
-  auto entry = [&](uint32_t start, uint32_t cnt, uint32_t b, uint32_t& er) -> AggEv {
-    AggEv E{};
+  auto entry = [&](uint32_t start, uint32_t cnt, uint32_t b, uint32_t& er) -> AggGEv {
+    AggGEv E{};
     er = 0;
     if (b + (uint32_t)lane < cnt) {
       er = idx[start + b + lane];
@@ -2144,8 +2057,8 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
     const uint32_t head0 = __builtin_amdgcn_readfirstlane(sh.lhead[lvl]);
     const uint32_t te_raw = sh.ltend[lvl];
     uint32_t er0;
-    const AggEv E0 = entry(start, cnt, 0, er0);  // the first 64 entries stay in registers
-    auto ent = [&](uint32_t b, uint32_t& er) -> AggEv {
+    const AggGEv E0 = entry(start, cnt, 0, er0);  // the first 64 entries stay in registers
+    auto ent = [&](uint32_t b, uint32_t& er) -> AggGEv {
       if (b == 0) {
         er = er0;
         return E0;
@@ -2156,9 +2069,9 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
     unsigned long long C = 0;
     for (uint32_t b = 0; b < cnt; b += 64) {
       uint32_t er;
-      const AggEv E = ent(b, er);
+      const AggGEv E = ent(b, er);
       const bool v = b + (uint32_t)lane < cnt;
-      const bool tk = v && (E.j & AGG_TAKE) != 0u;
+      const bool tk = v && (E.w & AGG_TAKE) != 0u;
       if (v && !tk) nf[er] = 0u;
       C += (unsigned long long)rli64(wave_incl_scan(tk ? (long long)E.qty : 0ll), 63);
     }
@@ -2218,9 +2131,9 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
       unsigned long long RR = 0;
       for (uint32_t b = 0; b < cnt; b += 64) {
         uint32_t er;
-        const AggEv E = ent(b, er);
+        const AggGEv E = ent(b, er);
         const bool v = b + (uint32_t)lane < cnt;
-        const bool rs = v && (E.j & AGG_TAKE) == 0u;
+        const bool rs = v && (E.w & AGG_TAKE) == 0u;
         const long long rq = rs ? (long long)E.qty : 0ll;
         const long long inc = wave_incl_scan(rq);
         const unsigned long long st0 = RR + (unsigned long long)(inc - rq), en = RR + (unsigned long long)inc;
@@ -2228,7 +2141,7 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
         const unsigned long long cm = __ballot(cons);
         const uint32_t r = nmk + nrc + (uint32_t)__popcll(cm & lanemask_lt());
         if (cons && r < GR_STAGE) {
-          mkl[r].seq = gmin + E.pad;
+          mkl[r].seq = gmin + rsq[erec(E.w)];
           mkl[r].end = T0 + en;
         }
         nrc += (uint32_t)__popcll(cm);
@@ -2304,9 +2217,9 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
         unsigned long long RR = 0;
         for (uint32_t b = 0; b < cnt; b += 64) {
           uint32_t er;
-          const AggEv E = ent(b, er);
+          const AggGEv E = ent(b, er);
           const bool v = b + (uint32_t)lane < cnt;
-          const bool rs = v && (E.j & AGG_TAKE) == 0u;
+          const bool rs = v && (E.w & AGG_TAKE) == 0u;
           const long long rq = rs ? (long long)E.qty : 0ll;
           const long long inc = wave_incl_scan(rq);
           const unsigned long long st0 = RR + (unsigned long long)(inc - rq), en = RR + (unsigned long long)inc;
@@ -2314,7 +2227,7 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
           const unsigned long long cm = __ballot(cons);
           if (cons) {
             AggMk m;
-            m.seq = gmin + E.pad;
+            m.seq = gmin + rsq[erec(E.w)];
             m.end = T0 + en;
             ag.mk[mk_base + mi + (uint32_t)__popcll(cm & lanemask_lt())] = m;
           }
@@ -2340,9 +2253,9 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
       unsigned long long A0 = 0;
       for (uint32_t b = 0; b < cnt; b += 64) {
         uint32_t er;
-        const AggEv E = ent(b, er);
+        const AggGEv E = ent(b, er);
         const bool v = b + (uint32_t)lane < cnt;
-        const bool tk = v && (E.j & AGG_TAKE) != 0u;
+        const bool tk = v && (E.w & AGG_TAKE) != 0u;
         const long long tq = tk ? (long long)E.qty : 0ll;
         const long long inc = wave_incl_scan(tq);
         if (tk) {
@@ -2418,23 +2331,24 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
   // the first take event of each record (the records' events are consecutive in the log): its fill count
   // and scratch start; each wave over its log range, 64 events at a time
   {
-    uint32_t prevj = r0 > 0 && r0 < r1 ? auniu(ev[r0 - 1].j) : NIL;
+    uint32_t prevj = r0 > 0 && r0 < r1 ? auniu(ev[r0 - 1].w >> AGG_GREC_SHIFT) : NIL;
     for (uint32_t b = r0; b < r1; b += 64) {
       const uint32_t e = b + (uint32_t)lane;
       const bool v = e < r1;
-      const uint32_t j = v ? ev[e].j : NIL;
+      const uint32_t j = v ? ev[e].w >> AGG_GREC_SHIFT : NIL;  // record | take (the level shifted out)
       uint32_t pj = (uint32_t)__shfl_up((int)j, 1, 64);
       pj = lane == 0 ? prevj : pj;
       uint32_t nj = (uint32_t)__shfl_down((int)j, 1, 64);
       nj = lane == 63 ? NIL : nj;
       const unsigned long long same = __ballot(v && nj == j);  // bit k: event k + 1 continues k's run
       prevj = rl32(j, 63);
-      if (v && (j & AGG_TAKE) && pj != j) {
+      if (v && (j & (AGG_TAKE >> AGG_GREC_SHIFT)) && pj != j) {
         // the record's take events: the run of j from here (lane 63's bit is clear)
         uint32_t nte = (uint32_t)__builtin_ctzll(~(same >> lane)) + 1u;
         if (lane + (int)nte == 64)
-          while (e + nte < n && ev[e + nte].j == j) ++nte;  // the run goes past this block
-        const uint32_t g = (j & ~AGG_TAKE) >> AGG_GSHIFT, oi = j & AGG_IMASK;
+          while (e + nte < n && (ev[e + nte].w >> AGG_GREC_SHIFT) == j) ++nte;  // the run goes past this block
+        const uint32_t gp = rjs[j & ~(AGG_TAKE >> AGG_GREC_SHIFT)];
+        const uint32_t g = gp >> AGG_GSHIFT, oi = gp & AGG_IMASK;
         const uint32_t x0 = EX(e), nfill = EX(e + nte) - x0;
         me_order_result* res = ga.res[g];
         res[oi].fill_count = nfill;
@@ -2570,18 +2484,18 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
     uint32_t g0 = 0;
     for (uint32_t b = 0; b < cnt; b += 64) {
       uint32_t er;
-      const AggEv E = entry(start, cnt, b, er);
+      const AggGEv E = entry(start, cnt, b, er);
       const bool v = b + (uint32_t)lane < cnt;
-      const bool tk = v && (E.j & AGG_TAKE) != 0u, rs = v && !tk;
+      const bool tk = v && (E.w & AGG_TAKE) != 0u, rs = v && !tk;
       const long long tq = tk ? (long long)E.qty : 0ll, rq = rs ? (long long)E.qty : 0ll;
       const long long tinc = wave_incl_scan(tq), rinc = wave_incl_scan(rq);
-      const unsigned long long sq = gmin + E.pad;
+      const unsigned long long sq = gmin + rsq[erec(E.w)];
       if (tk && nmk) {  // fills
         const uint32_t x0 = nf[er], nfl = EX(er + 1) - x0;
         if (nfl) {
           const unsigned long long a = A0 + (unsigned long long)(tinc - tq), z = a + (unsigned long long)E.qty;
           const uint32_t first = staged ? a_search_lds(mkl, nmk, a, true) : a_search(ag.mk, mk_base, nmk, a, true);
-          const uint32_t g = (E.j & ~AGG_TAKE) >> AGG_GSHIFT;
+          const uint32_t g = rjs[erec(E.w)] >> AGG_GSHIFT;
           const uint32_t p = sh.gbase[g] + (x0 - sh.gex[g]);
           me_fill f;
           f.taker_seq = sq;
@@ -2718,19 +2632,6 @@ hipError_t launch_agg_group(hipStream_t st, const BookDev& bk, const BatchDev* b
   ga.ng = ng;
   const uint32_t grid = bk.S < 2048u ? bk.S : 2048u;
   hipLaunchKernelGGL(k_agg_gwalk, dim3(grid), dim3(64), 0, st, bk, ga, ag);
-  static const bool multi = [] {  // ME_AGG_GRES=0: the six per-phase kernels (same-box A/B only)
-    const char* v = getenv("ME_AGG_GRES");
-    return v && atoi(v) == 0;
-  }();
-  if (multi) {
-    hipLaunchKernelGGL(k_agg_group, dim3(grid), dim3(1024), (size_t)bk.L * 4u + AGG_GCHUNK * 2u, st, bk, ag);
-    hipLaunchKernelGGL(k_agg_levels, dim3(2048), dim3(256), 0, st, bk, src, ag);
-    hipLaunchKernelGGL(k_agg_alloc, dim3(grid), dim3(64), 0, st, bk, ag);
-    hipLaunchKernelGGL(k_agg_place, dim3(2048), dim3(256), 0, st, bk, src, ag);
-    hipLaunchKernelGGL(k_agg_gfin, dim3(grid), dim3(1024), 0, st, bk, ga, ag);
-    hipLaunchKernelGGL(k_agg_gemit, dim3(grid), dim3(1024), 0, st, bk, ga, src, ag);
-    return hipGetLastError();
-  }
   // per-event LDS arrays (6 B per event) sized for 1.75 events per record of the group's mean symbol plus
   // slack; a longer log keeps them in HBM. Capped so the workgroup's LDS stays within 64 KB.
   uint64_t recs = 0;

@@ -170,6 +170,16 @@ struct AggEv {       // one event of the log, in record order
   uint32_t pad;
 };
 constexpr uint32_t AGG_TAKE = 1u << 31;
+// Grouped launches (k_agg_gwalk -> k_agg_gres) log 8-B events: the level (L <= 128) and the record's
+// number in the symbol's walk order (< ME_GMAX x BK_CAP) in one word. The records' seqs (offsets from the
+// group's first seq) and grouped positions sit beside the log in two arrays the walk writes 64 at a time,
+// so the resolve reads a seq from the symbol's own small array instead of gathering it from the batches.
+struct AggGEv {
+  uint32_t w;        // level | record << AGG_GREC_SHIFT | AGG_TAKE for a take
+  int32_t qty;
+};
+constexpr uint32_t AGG_GREC_SHIFT = 7;
+constexpr uint32_t AGG_GLVL_MASK = (1u << AGG_GREC_SHIFT) - 1u;
 constexpr uint32_t AGG_MAX_L = 32768;  // windows up to this depth (level histogram in LDS)
 struct AggRec {      // a record the walk handled (indexed by grouped position)
   int32_t filled, rem;
@@ -196,6 +206,8 @@ struct AggMk {       // a consumed maker: seq and the end of its interval in the
 };
 struct AggSlot {     // one hot symbol of the launch (index = k_hot_pick's hand-off index)
   uint32_t s, lo, hi, pos;   // symbol, grouped records [lo, hi), first record left to k_match_hot_cont
+                             // (grouped launches: lo = the 8-B events the log region holds before the
+                             // records' seq array, hi = that array's length; pos = the hand-off batch)
   unsigned long long wbase;  // scratch run
   long long base;
   uint32_t ev_base, ev_cnt, seg_base, nseg;
