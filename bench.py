@@ -424,9 +424,9 @@ def cluster_leg(args, world, rank, local, sc, base, slices, n_slices):
             n += len(b)
             if len(pend) == 2:
                 t, k = pend.pop(0)
-                fills += len(cl.collect(t, k)[1])
+                fills += len(cl.collect(t, k, copy=False)[1])
         for t, k in pend:
-            fills += len(cl.collect(t, k)[1])
+            fills += len(cl.collect(t, k, copy=False)[1])
         dt = time.perf_counter() - t0
         st = cl.stats()
         ph = cl.phases()

@@ -121,7 +121,8 @@ int me_cluster_stats(const me_cluster* c, uint64_t* slices, uint64_t* bytes);
  * rank 0's part straight into its engine's pinned slot inputs), [1] control (command broadcast), [2]
  * scatter (H2D + parts over the transport), [3] admission vote, [4] match (enqueue on every shard), [5]
  * collect (rank 0's own outputs: waits for its engine), [6] gather (sizes, tapes and results to rank 0,
- * D2H), [7] merge (results to slice order, tapes by taker). Writes min(n, 8) values, returns 8. */
+ * D2H), [7] merge (results to slice order, tapes by taker); parts of [0]: [8] the owner-count pass, [9]
+ * waiting for rank 0's engine slot inputs. Writes min(n, 10) values, returns 10. */
 int me_cluster_phases(const me_cluster* c, double* seconds, size_t n);
 int me_cluster_last_error(const me_cluster* c, char* buf, size_t cap);
 

@@ -215,11 +215,12 @@ class Cluster:
         self._check(self.lib.me_cluster_submit(self.h, C.byref(soa), len(b), C.byref(t)))
         return t.value
 
-    def collect(self, ticket: int, n: int):
-        """(results[n], tape) of the oldest ticket (copies)."""
+    def collect(self, ticket: int, n: int, copy: bool = True):
+        """(results[n], tape) of the oldest ticket: copies, or (copy=False) views valid until the next call."""
         f, r, nf = C.c_void_p(), C.c_void_p(), C.c_size_t(0)
         self._check(self.lib.me_cluster_collect(self.h, ticket, C.byref(f), C.byref(nf), C.byref(r)))
-        return _view(r.value, n, RESULT_DTYPE).copy(), _view(f.value, nf.value, FILL_DTYPE).copy()
+        res, tape = _view(r.value, n, RESULT_DTYPE), _view(f.value, nf.value, FILL_DTYPE)
+        return (res.copy(), tape.copy()) if copy else (res, tape)
 
     def match(self, b: Batch):
         return self.collect(self.submit(b), len(b))
@@ -255,7 +256,7 @@ class Cluster:
         self.lib.me_cluster_stats(self.h, C.byref(s), C.byref(b))
         return {"slices": s.value, "bytes": b.value}
 
-    PHASES = ("split", "control", "scatter", "vote", "match", "collect", "gather", "merge")
+    PHASES = ("split", "control", "scatter", "vote", "match", "collect", "gather", "merge", "split_count", "split_slot")
 
     def phases(self) -> dict:
         """Rank 0's seconds per protocol phase since create (me_cluster_phases)."""

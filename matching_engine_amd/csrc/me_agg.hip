@@ -18,14 +18,16 @@
 // Kernels (the engine's hot stream, after k_hot_pick, beside k_match on the main stream):
 //   k_agg_walk    one wave per hot symbol: the level-total chain, the event log, the records' status
 //   k_agg_group   one workgroup per hot symbol: a stable counting sort of its log by level -> segments
+//   k_agg_sorted  the sorted log entries (every slot over the whole grid)
 //   k_agg_levels  one wave per (symbol, level) segment: quantity taken, initial-FIFO walk, consumed
 //                 makers, emptied chunks (zeroed), each take's first maker and fill count
 //   k_agg_alloc   one wave per hot symbol: chunks for the surviving rests — the symbol's own emptied
 //                 chunks first, then its free list, then the bump allocator; the surplus freed
 //   k_agg_place   one wave per segment: surviving rests into the level's tail / new chunks, seq ring
-//   k_agg_fin     one workgroup per hot symbol: fill offsets (scan over the log), record results,
-//                 symbol state, the continuation's scratch position
-//   k_agg_emit    one thread per take event: its fills into the scratch run, in tape order
+//   k_agg_fin     one workgroup per hot symbol: fill offsets (scan over the log), symbol state, the
+//                 continuation's scratch position
+//   k_agg_out     every take event over the whole grid: the records' fill counts and scratch starts,
+//                 the fills into the scratch run, in tape order
 // A record the walk does not cover (a cancel, a LIMIT outside the window, a MARKET while far levels
 // exist on the side it crosses) hands the symbol's remaining records to k_match_hot_cont, the generic
 // record loop, exactly as k_match_hot does; the HBM book is complete before it runs.
@@ -907,7 +909,7 @@ __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const Agg
       k = a_block(w, A, B, oq, okd, olm, rj, j, fastm, cntb, R);
       rr = R.rr;
     }
-    if (v && (uint32_t)lane < k) {  // fill count and scratch start: k_agg_fin
+    if (v && (uint32_t)lane < k) {  // fill count and scratch start: k_agg_out
       bt.res[oi] = a_result(oq, okd, rj, rr);
       bt.fstart[oi] = 0u;
     }
@@ -959,14 +961,21 @@ __global__ __launch_bounds__(64) void k_agg_walk(BookDev bk, BatchDev bt, AggDev
 
 // ------------------------------------------------------------------ grouping the log by level
 // One 1024-thread workgroup per hot symbol: level histogram in LDS, segments (one per level with
-// events, in level order), then a stable scatter of the log indices (one wave, 64 events per step,
-// ranks by ballot multisplit over the level bits).
+// events, in level order), then a stable scatter of the log indices (ranks by ballot multisplit over the
+// level bits). Windows up to AGG_GW_LMAX levels (config 1's 256): every wave histograms and scatters its
+// own contiguous log range (per-wave histograms [16][L] in LDS give each wave its cursors); deeper ones:
+// one wave scatters, from log keys staged in LDS chunk by chunk.
+constexpr uint32_t AGG_GW_LMAX = 512;
+__host__ __device__ constexpr size_t agg_group_lds(uint32_t L) {
+  return L <= AGG_GW_LMAX ? (size_t)16 * L * 4u : (size_t)L * 4u + AGG_GCHUNK * 2u;
+}
 __global__ __launch_bounds__(1024) void k_agg_group(BookDev bk, AggDev ag) {
-  extern __shared__ uint32_t cnt_l[];  // [L], then AGG_GCHUNK 16-bit keys
+  extern __shared__ uint32_t cnt_l[];  // [L], then AGG_GCHUNK 16-bit keys; per-wave: [16][L]
   uint16_t* keys = reinterpret_cast<uint16_t*>(cnt_l + bk.L);
   __shared__ uint32_t wsum[16], wnz[16], sbase;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint32_t L = bk.L;
+  const bool pw = L <= AGG_GW_LMAX;  // (uniform over the launch)
   const uint32_t per = (L + 1023) / 1024;
   uint32_t nbits = 0;
   while ((1u << nbits) < L) ++nbits;
@@ -975,15 +984,29 @@ __global__ __launch_bounds__(1024) void k_agg_group(BookDev bk, AggDev ag) {
     const AggSlot& sl = ag.slot[i];
     if (!sl.active) continue;  // uniform over the workgroup
     const uint32_t eb = sl.ev_base, n = sl.ev_cnt;
-    for (uint32_t b = tid; b < L; b += 1024) cnt_l[b] = 0;
-    __syncthreads();
-    for (uint32_t e = tid; e < n; e += 1024) atomicAdd(&cnt_l[ag.ev[eb + e].lvl], 1u);
+    // per-wave: wave wv's contiguous, 64-aligned log range
+    const uint32_t wper = ((n + 15u) / 16u + 63u) & ~63u;
+    const uint32_t r0 = min(n, (uint32_t)wv * wper), r1 = min(n, r0 + wper);
+    if (pw) {
+      for (uint32_t b = tid; b < 16u * L; b += 1024) cnt_l[b] = 0;
+      __syncthreads();
+      for (uint32_t e = r0 + (uint32_t)lane; e < r1; e += 64) atomicAdd(&cnt_l[(uint32_t)wv * L + ag.ev[eb + e].lvl], 1u);
+    } else {
+      for (uint32_t b = tid; b < L; b += 1024) cnt_l[b] = 0;
+      __syncthreads();
+      for (uint32_t e = tid; e < n; e += 1024) atomicAdd(&cnt_l[ag.ev[eb + e].lvl], 1u);
+    }
     __syncthreads();
     const uint32_t b0 = tid * per;
     uint32_t lsum = 0, lnz = 0;
     for (uint32_t k = 0; k < per; ++k)
       if (b0 + k < L) {
-        const uint32_t c = cnt_l[b0 + k];
+        uint32_t c = 0;
+        if (pw) {
+          for (uint32_t w = 0; w < 16; ++w) c += cnt_l[w * L + b0 + k];
+        } else {
+          c = cnt_l[b0 + k];
+        }
         lsum += c;
         lnz += c != 0u;
       }
@@ -1018,55 +1041,99 @@ __global__ __launch_bounds__(1024) void k_agg_group(BookDev bk, AggDev ag) {
     uint32_t run = ps + xs - lsum, sid = pn + xn - lnz;
     for (uint32_t k = 0; k < per; ++k)
       if (b0 + k < L) {
-        const uint32_t c = cnt_l[b0 + k];
+        const uint32_t l = b0 + k;
+        uint32_t c = 0;
+        if (pw) {  // each wave's cursor: the level's start plus the earlier waves' events there
+          uint32_t r = run;
+          for (uint32_t w = 0; w < 16; ++w) {
+            const uint32_t x = cnt_l[w * L + l];
+            cnt_l[w * L + l] = r;
+            r += x;
+          }
+          c = r - run;
+        } else {
+          c = cnt_l[l];
+          cnt_l[l] = run;
+        }
         if (c) {
           AggSeg g;
           g.slot = i;
-          g.lvl = b0 + k;
+          g.lvl = l;
           g.start = eb + run;
           g.cnt = c;
           ag.seg[sbase + sid] = g;
           ++sid;
         }
-        cnt_l[b0 + k] = run;
         run += c;
       }
     __syncthreads();
-    // the scatter: chunks of AGG_GCHUNK keys staged in LDS by the whole workgroup (coalesced), then
-    // ranked and placed by one wave (its steps read LDS only: no HBM round trip per 64 events)
-    for (uint32_t c1 = 0; c1 < n; c1 += AGG_GCHUNK) {
-      const uint32_t m = min(AGG_GCHUNK, n - c1);
-      for (uint32_t e = tid; e < m; e += 1024) keys[e] = (uint16_t)ag.ev[eb + c1 + e].lvl;
-      __syncthreads();
-      if (wv == 0) {
-        for (uint32_t c0 = 0; c0 < m; c0 += 64) {
-          const uint32_t e = c0 + (uint32_t)lane;
-          const bool v = e < m;
-          const uint32_t key = v ? (uint32_t)keys[e] : 0u;
-          unsigned long long peers = __ballot(v);
-          for (uint32_t bit = 0; bit < nbits; ++bit) {
-            const unsigned long long bb = __ballot((key >> bit) & 1u);
-            peers &= ((key >> bit) & 1u) ? bb : ~bb;
-          }
-          const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
-          const uint32_t cp = (uint32_t)__popcll(peers);
-          const uint32_t start = cnt_l[key];
-          if (v) ag.evs[eb + start + rank] = eb + c1 + e;
-          __builtin_amdgcn_wave_barrier();
-          if (v && rank == 0) cnt_l[key] = start + cp;
-          __builtin_amdgcn_wave_barrier();
+    if (pw) {  // every wave scatters its range (ranks by ballot multisplit, cursors in its own histogram)
+      uint32_t* cur = cnt_l + (uint32_t)wv * L;
+      for (uint32_t c0 = r0; c0 < r1; c0 += 64) {
+        const uint32_t e = c0 + (uint32_t)lane;
+        const bool v = e < r1;
+        const uint32_t key = v ? ag.ev[eb + e].lvl : 0u;
+        unsigned long long peers = __ballot(v);
+        for (uint32_t bit = 0; bit < nbits; ++bit) {
+          const unsigned long long bb = __ballot((key >> bit) & 1u);
+          peers &= ((key >> bit) & 1u) ? bb : ~bb;
         }
+        const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
+        const uint32_t cp = (uint32_t)__popcll(peers);
+        const uint32_t start = cur[key];
+        if (v) ag.evs[eb + start + rank] = eb + e;
+        __builtin_amdgcn_wave_barrier();
+        if (v && rank == 0) cur[key] = start + cp;
+        __builtin_amdgcn_wave_barrier();
       }
       __syncthreads();
+    } else {
+      // the scatter: chunks of AGG_GCHUNK keys staged in LDS by the whole workgroup (coalesced), then
+      // ranked and placed by one wave (its steps read LDS only: no HBM round trip per 64 events)
+      for (uint32_t c1 = 0; c1 < n; c1 += AGG_GCHUNK) {
+        const uint32_t m = min(AGG_GCHUNK, n - c1);
+        for (uint32_t e = tid; e < m; e += 1024) keys[e] = (uint16_t)ag.ev[eb + c1 + e].lvl;
+        __syncthreads();
+        if (wv == 0) {
+          for (uint32_t c0 = 0; c0 < m; c0 += 64) {
+            const uint32_t e = c0 + (uint32_t)lane;
+            const bool v = e < m;
+            const uint32_t key = v ? (uint32_t)keys[e] : 0u;
+            unsigned long long peers = __ballot(v);
+            for (uint32_t bit = 0; bit < nbits; ++bit) {
+              const unsigned long long bb = __ballot((key >> bit) & 1u);
+              peers &= ((key >> bit) & 1u) ? bb : ~bb;
+            }
+            const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
+            const uint32_t cp = (uint32_t)__popcll(peers);
+            const uint32_t start = cnt_l[key];
+            if (v) ag.evs[eb + start + rank] = eb + c1 + e;
+            __builtin_amdgcn_wave_barrier();
+            if (v && rank == 0) cnt_l[key] = start + cp;
+            __builtin_amdgcn_wave_barrier();
+          }
+        }
+        __syncthreads();
+      }
     }
-    // the sorted copies the per-level kernels read (one hop instead of index -> entry)
-    for (uint32_t p = tid; p < n; p += 1024) {
+  }
+}
+
+// The sorted copies the per-level kernels read (one hop instead of index -> entry), every slot's log over
+// the whole grid.
+__global__ __launch_bounds__(256) void k_agg_sorted(BookDev bk, AggDev ag) {
+  const uint32_t nh = a_nslots(bk, ag);
+  const uint32_t T = gridDim.x * blockDim.x;
+  for (uint32_t i = 0; i < nh; ++i) {
+    const AggSlot& sl = ag.slot[i];
+    if (!sl.active) continue;
+    const uint32_t eb = sl.ev_base, n = sl.ev_cnt;
+    for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p < n; p += T) {
       const uint32_t e = ag.evs[eb + p];
       AggEv E = ag.ev[e];
       E.pad = e;
       ag.evq[eb + p] = E;
     }
-    __syncthreads();
   }
 }
 
@@ -1574,22 +1641,9 @@ __global__ __launch_bounds__(1024) void k_agg_fin(BookDev bk, BatchDev bt, AggDe
     if (tid == 0) carry_s = carry;
     __syncthreads();
     const uint32_t ftot = carry_s;
-    __threadfence_block();
-    auto EX = [&](uint32_t e) -> uint32_t { return e < eb + n ? ag.evx[e] : ftot; };
-    // the first take of each record (the walk wrote its result with no fills): fill count, scratch start
-    for (uint32_t t = (uint32_t)tid; t < n; t += 1024) {
-      const uint32_t e = eb + t;
-      const uint32_t j = ag.ev[e].j;
-      if (!(j & AGG_TAKE) || (t > 0 && ag.ev[e - 1].j == j)) continue;
-      uint32_t nte = 1;  // the record's take events follow each other in the log
-      while (t + nte < n && ag.ev[e + nte].j == j) ++nte;
-      const uint32_t x0 = EX(e), nfill = EX(e + nte) - x0;
-      const uint32_t oi = bt.perm[j & ~AGG_TAKE];
-      bt.res[oi].fill_count = nfill;
-      bt.fstart[oi] = (uint32_t)(sl.wbase + x0);
-      if (nfill) atomicAdd(&bt.tile_sum[oi / TILE_TAPE], nfill);
-    }
     if (tid == 0) {
+      ag.evx[eb + n] = ftot;  // (the log's region has room: n < evneed) so evx[e + 1] - evx[e] is e's count
+
       SymState o = bk.sym[sl.s];
       o.best_bid = sl.bb;
       o.best_ask = sl.ba;
@@ -1608,35 +1662,69 @@ __global__ __launch_bounds__(1024) void k_agg_fin(BookDev bk, BatchDev bt, AggDe
   }
 }
 
-// One thread per take event: its fills (the makers overlapping its interval) into the scratch run at
-// the record's tape position.
-__global__ __launch_bounds__(1024) void k_agg_emit(BookDev bk, BatchDev bt, AggDev ag) {
+// Every take event of every slot over the whole grid (a single hot symbol — config 1 — fills the chip, not
+// one workgroup): a record's first take event writes its fill count and scratch start (the walk wrote the
+// rest of its result), every take event its fills (the makers overlapping its interval) into the scratch
+// run at its tape position. Tape-tile sums are added once per wave and tile.
+__global__ __launch_bounds__(256) void k_agg_out(BookDev bk, BatchDev bt, AggDev ag) {
   const uint32_t nh = min(*(volatile uint32_t*)bk.hcount, bk.S);
-  for (uint32_t i = blockIdx.x; i < nh; i += gridDim.x) {
-    const AggSlot sl = ag.slot[i];
-    if (!sl.active) continue;
-    const uint32_t eb = sl.ev_base, n = sl.ev_cnt;
-    for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) {
+  const uint32_t T = gridDim.x * blockDim.x;
+  const uint32_t gt = blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = lane_id();
+  for (uint32_t i = 0; i < nh; ++i) {
+    const AggSlot& slr = ag.slot[i];
+    if (!slr.active) continue;
+    const uint32_t eb = slr.ev_base, n = slr.ev_cnt;
+    const unsigned long long wbase = slr.wbase;
+    const long long base = slr.base;
+    const uint32_t gs = slr.gs;
+    for (uint32_t t0 = gt - (uint32_t)lane; t0 < n; t0 += T) {  // (whole waves: the tile sums below)
+      const uint32_t t = t0 + (uint32_t)lane;
       const uint32_t e = eb + t;
-      const AggEv E = ag.ev[e];
-      if (!(E.j & AGG_TAKE)) continue;
-      const uint32_t nf = ag.evn[e];
-      if (!nf) continue;
-      const uint32_t first = ag.evf[e];
-      const unsigned long long a = ag.eva[e], z = a + (unsigned long long)E.qty;
-      const unsigned long long p = sl.wbase + ag.evx[e];
-      me_fill f;
-      f.taker_seq = a_seq_of(bt, E.j & ~AGG_TAKE);
-      f.price_q4 = sl.base + (long long)E.lvl;
-      f.symbol = sl.gs;
-      unsigned long long lo = a;
-      for (uint32_t k = 0; k < nf; ++k) {
-        const AggMk m = ag.mk[first + k];
-        const unsigned long long hi = m.end < z ? m.end : z;
-        f.maker_seq = m.seq;
-        f.qty = (int)(hi - lo);
-        bt.scratch[p + k] = f;
-        lo = hi;
+      AggEv E{};
+      if (t < n) E = ag.ev[e];
+      const bool tk = t < n && (E.j & AGG_TAKE) != 0u;
+      uint32_t add = 0, tile = 0;
+      if (tk) {
+        const uint32_t x0 = ag.evx[e];
+        if (t == 0 || ag.ev[e - 1].j != E.j) {  // the record's first take event
+          uint32_t nte = 1;  // its take events follow each other in the log
+          while (t + nte < n && ag.ev[e + nte].j == E.j) ++nte;
+          const uint32_t nfill = ag.evx[e + nte] - x0;
+          const uint32_t oi = bt.perm[E.j & ~AGG_TAKE];
+          bt.res[oi].fill_count = nfill;
+          bt.fstart[oi] = (uint32_t)(wbase + x0);
+          add = nfill;
+          tile = oi / TILE_TAPE;
+        }
+        const uint32_t nf = ag.evx[e + 1] - x0;
+        if (nf) {
+          const uint32_t first = ag.evf[e];
+          const unsigned long long a = ag.eva[e], z = a + (unsigned long long)E.qty;
+          const unsigned long long p = wbase + x0;
+          me_fill f;
+          f.taker_seq = a_seq_of(bt, E.j & ~AGG_TAKE);
+          f.price_q4 = base + (long long)E.lvl;
+          f.symbol = gs;
+          unsigned long long lo = a;
+          for (uint32_t k = 0; k < nf; ++k) {
+            const AggMk m = ag.mk[first + k];
+            const unsigned long long hi = m.end < z ? m.end : z;
+            f.maker_seq = m.seq;
+            f.qty = (int)(hi - lo);
+            bt.scratch[p + k] = f;
+            lo = hi;
+          }
+        }
+      }
+      // the wave's tile sums: one atomic per distinct tile (a run of records shares one)
+      unsigned long long m = __ballot(add != 0u);
+      while (m) {
+        const uint32_t t1 = rl32(tile, __builtin_ctzll(m));
+        const unsigned long long mm = __ballot(add != 0u && tile == t1);
+        const uint32_t sum = (uint32_t)rli64(wave_incl_scan((mm >> lane) & 1ull ? (long long)add : 0ll), 63);
+        if (lane == __builtin_ctzll(m)) atomicAdd(&bt.tile_sum[t1], sum);
+        m &= ~mm;
       }
     }
   }
@@ -1797,16 +1885,20 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
     const bool lok = lw_init(lw, bk, s, ltot, bb0, ba0);  // else: the continuation from the first record
     uint32_t hidx = NIL, gstop = ng;
     // a batch's bucket is loaded while the batch before it runs (no HBM round trip between batches)
+    // (only the lanes of the bucket's records load: a 128-slot bucket holds ~64 at config 2)
     const size_t bko = (size_t)s * BK_CAP;
-    BkRec n0 = ga.b_rec[0][bko + lane], n1 = ga.b_rec[0][bko + 64 + lane];
+    BkRec n0{}, n1{};
+    auto bload = [&](uint32_t g) {
+      const uint32_t c = rl32(nsv, (int)g);
+      if ((uint32_t)lane < c) n0 = ga.b_rec[g][bko + lane];
+      if (64u + (uint32_t)lane < c) n1 = ga.b_rec[g][bko + 64 + lane];
+    };
+    bload(0);
     for (uint32_t g = 0; g < ng; ++g) {
       if (lane == 0) *a_gtab(ag.gev, s, g) = eb + w.evp;
       const uint32_t cnt = rl32(nsv, (int)g);
       const BkRec r0 = n0, r1 = n1;
-      if (g + 1u < ng) {
-        n0 = ga.b_rec[g + 1][bko + lane];
-        n1 = ga.b_rec[g + 1][bko + 64 + lane];
-      }
+      if (g + 1u < ng) bload(g + 1u);
       if (!cnt) continue;
       if (cnt > (uint32_t)BK_CAP) {  // an overfull bucket: the continuation rescans the batch
         hidx = a_ghand(bk, s, g, 0u, cnt, 0u, 0u);
@@ -1894,7 +1986,7 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
 }
 
 // ------------------------------------------------------------------ grouped launches: one workgroup per symbol
-// k_agg_gres does the work of the hot path's k_agg_group ... k_agg_emit for a grouped launch in ONE launch,
+// k_agg_gres does the work of the hot path's k_agg_group ... k_agg_out for a grouped launch in ONE launch,
 // one 512-thread workgroup per symbol (the walk's workgroup of the same symbol ran on the same XCD,
 // blockIdx = symbol):
 //   A  the symbol's log sorted by level in LDS (per-wave histograms of contiguous log ranges, a stable
@@ -2595,12 +2687,13 @@ hipError_t launch_agg(hipStream_t hs, const BookDev& bk, const BatchDev& bt, con
   src.seq[0] = bt.seq;
   const size_t lwb = bk.L <= ag.ladder_max ? ((size_t)bk.L + 64u) * 4u : 0u;
   hipLaunchKernelGGL(k_agg_walk, dim3(64), dim3(64), lwb, hs, bk, bt, ag);
-  hipLaunchKernelGGL(k_agg_group, dim3(64), dim3(1024), (size_t)bk.L * 4u + AGG_GCHUNK * 2u, hs, bk, ag);
+  hipLaunchKernelGGL(k_agg_group, dim3(64), dim3(1024), agg_group_lds(bk.L), hs, bk, ag);
+  hipLaunchKernelGGL(k_agg_sorted, dim3(1024), dim3(256), 0, hs, bk, ag);
   hipLaunchKernelGGL(k_agg_levels, dim3(1024), dim3(256), 0, hs, bk, src, ag);
   hipLaunchKernelGGL(k_agg_alloc, dim3(64), dim3(64), 0, hs, bk, ag);
   hipLaunchKernelGGL(k_agg_place, dim3(1024), dim3(256), 0, hs, bk, src, ag);
   hipLaunchKernelGGL(k_agg_fin, dim3(64), dim3(1024), 0, hs, bk, bt, ag);
-  hipLaunchKernelGGL(k_agg_emit, dim3(64), dim3(1024), 0, hs, bk, bt, ag);
+  hipLaunchKernelGGL(k_agg_out, dim3(1024), dim3(256), 0, hs, bk, bt, ag);
   return hipGetLastError();
 }
 

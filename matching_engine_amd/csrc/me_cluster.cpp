@@ -44,7 +44,7 @@ constexpr size_t kRec = 8 + 8 + 4 + 4 + 1;  // packed slice record: seq, price_q
 enum : int64_t { CMD_SUBMIT = 1, CMD_COLLECT = 2, CMD_BOOK = 3, CMD_SNAPSHOT = 4, CMD_STOP = 5 };
 constexpr int kMaxInflight = 2;
 // rank 0's time per protocol phase (me_cluster_phases)
-enum { PH_SPLIT, PH_CTRL, PH_SCATTER, PH_VOTE, PH_MATCH, PH_COLLECT, PH_GATHER, PH_MERGE, PH_N };
+enum { PH_SPLIT, PH_CTRL, PH_SCATTER, PH_VOTE, PH_MATCH, PH_COLLECT, PH_GATHER, PH_MERGE, PH_SPLIT_COUNT, PH_SPLIT_SLOT, PH_N };
 
 inline size_t round8(size_t x) { return (x + 7) & ~(size_t)7; }
 
@@ -676,6 +676,14 @@ extern "C" me_cluster* me_cluster_create(const me_cluster_config* cfg, const me_
     const char* v = getenv("ME_CLUSTER_DIRECT");
     c->direct0 = cfg->rank == 0 && !c->use_ops && c->eng && !(v && atoi(v) == 0);
   }
+  // ranks that match through the engine's pinned host slots (rank 0's direct part, every rank on a host
+  // transport) allocate them now: a slot's first use would otherwise pin ~100 MB inside a slice's split
+  // (config 3's 1M-record slices: 51 ms per slice over 16 slices, profiles/r4/r4c)
+  if (c->eng && (c->direct0 || !dev) && me_host_reserve(c->eng, 0) != ME_OK) {
+    set_create_err("me_cluster_create: host slots: " + eng_err(c->eng));
+    free_cluster(c.get());
+    return nullptr;
+  }
   if (cfg->rank == 0) {
     c->t_send = c->tp->alloc(kRec * cfg->max_batch);
     if (!c->t_send) {
@@ -1179,6 +1187,7 @@ extern "C" int me_cluster_submit(me_cluster* c, const me_order_soa* b, size_t n,
       hdr[6 + r] += (int64_t)cnt[i * W + r];
       hdr[6 + W + r] += (int64_t)lim[i * W + r];
     }
+  c->ph[PH_SPLIT_COUNT] += now_s() - t;
   tk.pos_off.assign(W + 1, 0);
   for (uint32_t r = 0; r < W; ++r) tk.pos_off[r + 1] = tk.pos_off[r] + (size_t)hdr[6 + r];
   tk.pos.resize(n);
@@ -1194,7 +1203,9 @@ extern "C" int me_cluster_submit(me_cluster* c, const me_order_soa* b, size_t n,
       const size_t nr = (size_t)hdr[6 + r];
       if (r == 0 && c->direct0 && n0) {
         me_order_soa_w w{};
+        const double ts = now_s();
         if (me_host_inputs(c->eng, n0, &w) != ME_OK) return c->fail(ME_E_STATE, "rank 0 slot inputs: " + eng_err(c->eng));
+        c->ph[PH_SPLIT_SLOT] += now_s() - ts;
         PackView v(c->h_send.data(), 0);
         v.seq = w.seq;
         v.px = w.price_q4;

@@ -9,6 +9,7 @@
 #          trace[:WL[:K[:W]]]    rocprofv3 --kernel-trace --stats of that bench; per-kernel summary
 #          traffic[:WL]          FETCH_SIZE and WRITE_SIZE passes (one counter each) over the match group's
 #                                kernels -> pmc_traffic_WL.json (bytes per order, gfx950 FETCH x2 correction)
+#          dram[:WL]             byte-exact EA traffic (32-B-unit read / write / atomic request counters, one pass)
 #          sq[:WL]               SQ counters (instructions, waits, LDS bank conflicts) of the agg kernels
 #          cpu[:WL]              bench.py with the CPU baseline at the host's cores (and 1 core)
 # env: BENCH_ARGS (extra bench.py args), ME_* engine switches pass through.
@@ -51,6 +52,10 @@ for step in "$@"; do
       timeout -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex "$KRE" --output-format csv -d $O/pmc_${wl}_$c -o pmc -- $(bench_cmd $wl 64 32) > $O/pmc_${wl}_$c.log 2>&1 || { echo "PMC_FAIL $wl $c"; tail -5 $O/pmc_${wl}_$c.log; exit 1; }
     done
     python3 $R/tools/prof_summary.py traffic $O/pmc_${wl}_FETCH_SIZE $O/pmc_${wl}_WRITE_SIZE --bench $O/pmc_${wl}_WRITE_SIZE.log > $O/pmc_traffic_$wl.json && cat $O/pmc_traffic_$wl.json
+    ;;
+  dram)
+    timeout -s KILL 300 rocprofv3 --pmc TCC_EA0_RDREQ_DRAM_32B TCC_EA0_WRREQ_WRITE_DRAM_32B TCC_EA0_WRREQ_WRITE_ATOMIC_32B TCC_EA0_RDREQ --kernel-include-regex "$KRE" --output-format csv -d $O/dram_$wl -o pmc -- $(bench_cmd $wl 64 32) > $O/dram_$wl.log 2>&1 || { echo "DRAM_FAIL $wl"; tail -5 $O/dram_$wl.log; exit 1; }
+    python3 $R/tools/prof_summary.py dram $O/dram_$wl --bench $O/dram_$wl.log > $O/dram_traffic_$wl.json && head -8 $O/dram_traffic_$wl.json
     ;;
   sq)
     KA='k_agg_|k_side|k_match_reg'

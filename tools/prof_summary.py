@@ -3,6 +3,7 @@
 
     prof_summary.py trace DIR [--steps K]        per-kernel count / avg / total (us) of a kernel trace, and
                                                  the timeline of the run's last launch group
+    prof_summary.py dram DIR --bench LOG       byte-exact EA traffic per order from the 32-B-unit counters
     prof_summary.py traffic FETCH_DIR WRITE_DIR --bench LOG
                                                  HBM bytes per order over every included dispatch of the run
                                                  (FETCH_SIZE x2, the gfx950 correction of MI355X_MICROARCH.md;
@@ -105,6 +106,42 @@ def traffic(fdir, wdir, log):
     print(json.dumps(out, indent=1))
 
 
+DRAM = ("TCC_EA0_RDREQ_DRAM_32B", "TCC_EA0_WRREQ_WRITE_DRAM_32B", "TCC_EA0_WRREQ_WRITE_ATOMIC_32B", "TCC_EA0_RDREQ")
+
+
+def dram(ddir, log):
+    """Byte-exact EA traffic: the gfx950 32-byte-unit request counters (a 64-B request counts 2, a 128-B one
+    4), so no request-size correction is needed — the cross-check of FETCH_SIZE x2 + WRITE_SIZE."""
+    d, orders = bench_orders(log)
+    c = counters(ddir)
+    per = {}
+    tot = defaultdict(float)
+    for n, cs in c.items():
+        v = {k: sum(cs.get(k, [])) for k in DRAM}
+        rd, wr, at = 32.0 * v[DRAM[0]], 32.0 * v[DRAM[1]], 32.0 * v[DRAM[2]]
+        for k, x in (("rd", rd), ("wr", wr), ("at", at), ("req", v[DRAM[3]])):
+            tot[k] += x
+        per[n] = {"dispatches": len(cs.get(DRAM[0], [])), "read_bytes_per_order": rd / orders,
+                  "write_bytes_per_order": wr / orders, "atomic_bytes_per_order": at / orders,
+                  "bytes_per_order": (rd + wr + at) / orders,
+                  "mean_read_request_bytes": rd / v[DRAM[3]] if v[DRAM[3]] else None}
+    out = {
+        "bytes_per_order": (tot["rd"] + tot["wr"] + tot["at"]) / orders,
+        "read_bytes_per_order": tot["rd"] / orders,
+        "write_bytes_per_order": tot["wr"] / orders,
+        "atomic_bytes_per_order": tot["at"] / orders,
+        "orders": orders,
+        "counters": "32 x (TCC_EA0_RDREQ_DRAM_32B + TCC_EA0_WRREQ_WRITE_DRAM_32B + TCC_EA0_WRREQ_WRITE_ATOMIC_32B), "
+                    "one pass; TCC_EA0_RDREQ for the mean read request size",
+        "statistic": "sum over every dispatch of the match pipeline's kernels in the run / the orders of those batches",
+        "per_kernel": dict(sorted(per.items(), key=lambda x: -x[1]["bytes_per_order"])),
+        "build": d.get("build"),
+        "workload": d["config"].get("workload"),
+        "steps": d["steps"], "warmup": d["warmup"],
+    }
+    print(json.dumps(out, indent=1))
+
+
 def sq(dirs):
     allc = defaultdict(dict)
     for d in dirs:
@@ -135,6 +172,8 @@ def main():
         trace(a[1], steps)
     elif a[0] == "traffic":
         traffic(a[1], a[2], a[a.index("--bench") + 1])
+    elif a[0] == "dram":
+        dram(a[1], a[a.index("--bench") + 1])
     elif a[0] == "sq":
         sq(a[1:])
     else:
