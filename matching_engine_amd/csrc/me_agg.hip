@@ -1989,9 +1989,10 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
 // k_agg_gres does the work of the hot path's k_agg_group ... k_agg_out for a grouped launch in ONE launch,
 // one 512-thread workgroup per symbol (the walk's workgroup of the same symbol ran on the same XCD,
 // blockIdx = symbol):
-//   A  the symbol's log sorted by level in LDS (per-wave histograms of contiguous log ranges, a stable
-//      ballot-multisplit scatter of 16-bit log indices) — no sorted copies, segment tables or per-event
-//      arrays in HBM; a seq is read from the symbol's own record array beside its log (the walk wrote it);
+//   A  the symbol's log sorted by level (per-wave histograms of contiguous log ranges in LDS, a stable
+//      ballot-multisplit scatter of 8-B entries {log index | record, qty} into the slot's region of
+//      AggDev::evq), so phases B and D read each level's events as one contiguous run instead of gathering
+//      them from the log line by line; a seq is read from the symbol's own record array beside its log;
 //   B  its levels resolved by the waves (a level per wave, taken from an LDS counter): the initial FIFO
 //      walked until the group's takes are covered, consumed makers, emptied chunks, each take's fill count
 //      into an LDS array indexed by log position; the slot's cursors are LDS atomics, not pool-wide ones;
@@ -1999,8 +2000,8 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
 //      over its log range), each batch's scratch base, the records' fill counts and scratch starts;
 //   D  the chunk allocation (wave 0), then per level in one pass over its events: the fills of its takes and
 //      the surviving rests placed into the level's tail and new chunks.
-// The per-event LDS arrays hold `ne` events (the launch sizes them from the group's mean records per
-// symbol); a symbol with a longer log keeps them in the log's own HBM regions (AggDev::evn / evs) instead.
+// The per-event LDS array (fill counts) holds `ne` events (the launch sizes it from the group's mean records
+// per symbol); a symbol with a longer log keeps it in the log's own HBM region (AggDev::evn) instead.
 // ~16 KB of static LDS and a register budget of GR_WPE waves per SIMD.
 #ifndef GR_WAVES
 #define GR_WAVES 8  // waves per workgroup (same-box A/B)
@@ -2046,14 +2047,17 @@ __device__ __forceinline__ uint32_t gr_take(uint32_t* ctr) {
 
 template <bool kLds>
 __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& ga, const AggSrc& src, const AggDev& ag,
-                                            uint32_t s, const AggSlot& sl, GrShared& sh, uint32_t* nf, uint16_t* idx) {
+                                            uint32_t s, const AggSlot& sl, GrShared& sh, uint32_t* nf) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint32_t L = bk.L;  // <= 128
   const uint32_t eb = sl.ev_base, n = sl.ev_cnt, ng = ga.ng;
   const AggGEv* ev = reinterpret_cast<const AggGEv*>(ag.ev + eb);
   const uint32_t* rsq = reinterpret_cast<const uint32_t*>(ev + sl.lo);  // the records' seq offsets ...
   const uint32_t* rjs = rsq + sl.hi;                                    // ... and grouped positions
-  auto erec = [](uint32_t w) -> uint32_t { return (w & ~AGG_TAKE) >> AGG_GREC_SHIFT; };
+  // the log sorted by level (phase A), read by phases B and D one level segment at a time (coalesced):
+  // entry w = log index | record << 16 | AGG_TAKE (the level is the segment's)
+  AggGEv* const srt = reinterpret_cast<AggGEv*>(ag.evq + eb);
+  auto srec = [](uint32_t w) -> uint32_t { return (w >> 16) & 0x7FFFu; };
   const size_t lo_l = (size_t)s * L;
   // every seq of the group lies in [gmin, gmin + seq_ring) (k_seq_sweep's check; seq_ring <= 2^32 here)
   const unsigned long long gmin = *ga.seq0;
@@ -2112,7 +2116,9 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
   for (uint32_t b = r0; b < r1; b += 64) {
     const uint32_t e = b + (uint32_t)lane;
     const bool v = e < r1;
-    const uint32_t key = v ? (ev[e].w & AGG_GLVL_MASK) : 0u;
+    AggGEv E{};
+    if (v) E = ev[e];
+    const uint32_t key = v ? (E.w & AGG_GLVL_MASK) : 0u;
     unsigned long long peers = __ballot(v);
 #pragma unroll
     for (uint32_t bit = 0; bit < 7; ++bit) {
@@ -2121,7 +2127,12 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
     }
     const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
     const uint32_t start = sh.u.wh[wv][key];
-    if (v) idx[start + rank] = (uint16_t)e;
+    if (v) {
+      AggGEv S;
+      S.w = e | (((E.w & ~AGG_TAKE) >> AGG_GREC_SHIFT) << 16) | (E.w & AGG_TAKE);
+      S.qty = E.qty;
+      srt[start + rank] = S;
+    }
     wave_mem_order();
     if (v && rank == 0) sh.u.wh[wv][key] = start + (uint32_t)__popcll(peers);
     wave_mem_order();
@@ -2137,8 +2148,8 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
     AggGEv E{};
     er = 0;
     if (b + (uint32_t)lane < cnt) {
-      er = idx[start + b + lane];
-      E = ev[er];
+      E = srt[start + b + lane];
+      er = E.w & 0xFFFFu;
     }
     return E;
   };
@@ -2233,7 +2244,7 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
         const unsigned long long cm = __ballot(cons);
         const uint32_t r = nmk + nrc + (uint32_t)__popcll(cm & lanemask_lt());
         if (cons && r < GR_STAGE) {
-          mkl[r].seq = gmin + rsq[erec(E.w)];
+          mkl[r].seq = gmin + rsq[srec(E.w)];
           mkl[r].end = T0 + en;
         }
         nrc += (uint32_t)__popcll(cm);
@@ -2319,7 +2330,7 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
           const unsigned long long cm = __ballot(cons);
           if (cons) {
             AggMk m;
-            m.seq = gmin + rsq[erec(E.w)];
+            m.seq = gmin + rsq[srec(E.w)];
             m.end = T0 + en;
             ag.mk[mk_base + mi + (uint32_t)__popcll(cm & lanemask_lt())] = m;
           }
@@ -2581,13 +2592,13 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
       const bool tk = v && (E.w & AGG_TAKE) != 0u, rs = v && !tk;
       const long long tq = tk ? (long long)E.qty : 0ll, rq = rs ? (long long)E.qty : 0ll;
       const long long tinc = wave_incl_scan(tq), rinc = wave_incl_scan(rq);
-      const unsigned long long sq = gmin + rsq[erec(E.w)];
+      const unsigned long long sq = gmin + rsq[srec(E.w)];
       if (tk && nmk) {  // fills
         const uint32_t x0 = nf[er], nfl = EX(er + 1) - x0;
         if (nfl) {
           const unsigned long long a = A0 + (unsigned long long)(tinc - tq), z = a + (unsigned long long)E.qty;
           const uint32_t first = staged ? a_search_lds(mkl, nmk, a, true) : a_search(ag.mk, mk_base, nmk, a, true);
-          const uint32_t g = rjs[erec(E.w)] >> AGG_GSHIFT;
+          const uint32_t g = rjs[srec(E.w)] >> AGG_GSHIFT;
           const uint32_t p = sh.gbase[g] + (x0 - sh.gex[g]);
           me_fill f;
           f.taker_seq = sq;
@@ -2661,18 +2672,18 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
 __global__ __launch_bounds__(GR_THREADS, GR_WPE) void k_agg_gres(BookDev bk, AggGArgs ga, AggSrc src, AggDev ag,
                                                           uint32_t ne) {
   __shared__ GrShared sh;
-  extern __shared__ uint32_t gr_dyn[];  // [ne] fill counts / offsets, then [ne] 16-bit sorted log indices
+  extern __shared__ uint32_t gr_dyn[];  // [ne] fill counts / offsets
   for (uint32_t s = blockIdx.x; s < bk.S; s += gridDim.x) {
     const AggSlot sl = ag.slot[s];
     if (!sl.active) continue;  // (uniform over the workgroup)
-    if (sl.ev_cnt >= 65536u) {  // 16-bit log indices: a grouped log is at most 3 x 32 x BK_CAP + L + 64 long
+    if (sl.ev_cnt >= 65536u) {  // 16-bit log indices in the sorted entries: a grouped log is at most 3 x 32 x BK_CAP + L + 64 long
       if (threadIdx.x == 0) atomicOr(bk.err, ERR_INCONSISTENT);
       continue;
     }
     if (sl.ev_cnt <= ne)
-      gres_symbol<true>(bk, ga, src, ag, s, sl, sh, gr_dyn, reinterpret_cast<uint16_t*>(gr_dyn + ne));
+      gres_symbol<true>(bk, ga, src, ag, s, sl, sh, gr_dyn);
     else
-      gres_symbol<false>(bk, ga, src, ag, s, sl, sh, ag.evn + sl.ev_base, reinterpret_cast<uint16_t*>(ag.evs + sl.ev_base));
+      gres_symbol<false>(bk, ga, src, ag, s, sl, sh, ag.evn + sl.ev_base);
     __syncthreads();
   }
 }
@@ -2725,15 +2736,15 @@ hipError_t launch_agg_group(hipStream_t st, const BookDev& bk, const BatchDev* b
   ga.ng = ng;
   const uint32_t grid = bk.S < 2048u ? bk.S : 2048u;
   hipLaunchKernelGGL(k_agg_gwalk, dim3(grid), dim3(64), 0, st, bk, ga, ag);
-  // per-event LDS arrays (6 B per event) sized for 1.75 events per record of the group's mean symbol plus
-  // slack; a longer log keeps them in HBM. Capped so the workgroup's LDS stays within 64 KB.
+  // the per-event LDS array (fill counts, 4 B per event) sized for 1.75 events per record of the group's
+  // mean symbol plus slack; a longer log keeps it in HBM. Capped so the workgroup's LDS stays within 64 KB.
   uint64_t recs = 0;
   for (uint32_t g = 0; g < ng; ++g) recs += bt[g].n;
   uint64_t ne = (recs * 7u / 4u) / (bk.S ? bk.S : 1u) + 256u;  // (config 2: 1.4 events per record)
   ne = (ne + 63u) & ~63ull;
-  const uint64_t ne_cap = ((64u << 10) - sizeof(GrShared)) / 6u & ~63ull;
+  const uint64_t ne_cap = ((64u << 10) - sizeof(GrShared)) / 4u & ~63ull;
   if (ne > ne_cap) ne = ne_cap;
-  hipLaunchKernelGGL(k_agg_gres, dim3(grid), dim3(GR_THREADS), (size_t)ne * 6u, st, bk, ga, src, ag, (uint32_t)ne);
+  hipLaunchKernelGGL(k_agg_gres, dim3(grid), dim3(GR_THREADS), (size_t)ne * 4u, st, bk, ga, src, ag, (uint32_t)ne);
   return hipGetLastError();
 }
 }  // namespace me
