@@ -520,15 +520,18 @@ extern "C" me_engine* me_create(const me_config* cfg) {
     e->hot.agg = L > 128 && L <= AGG_MAX_L && !(va && atoi(va) == 0);
     // L <= 128: every symbol of a launch group through the aggregate path (k_agg_gwalk) instead of
     // k_match_reg's serial loop — ME_REG_AGG=1 (measured per workload)
-    // (unset: on when a batch holds >= 32 records per symbol — config 2's shape, 64; config 3 has ~10 and
-    // runs faster on k_match_reg — in batches of >= 8,192 records, and off for good once hand-offs show
-    // up, see reg_agg_auto)
+    // (unset: on when a batch holds >= 8 records per symbol and a group >= 256 — config 2's shape, 64 and
+    // 2,048; config 3's ~10.5 and ~336 runs 1,296M vs 1,124M on k_match_reg at the driver's shape, 1,590M
+    // vs 1,209M over 64 batches, same box, profiles/r4/c3agg; a group's per-symbol set-up — the ladder
+    // load, the resolve's workgroup — needs the records to amortise it — in batches of >= 8,192 records,
+    // and off for good once hand-offs show up, see reg_agg_auto)
     const char* vr = getenv("ME_REG_AGG");
     const uint64_t grp = cfg->batches_per_launch ? cfg->batches_per_launch : ME_DEFAULT_GROUP;
     // (k_agg_gres keeps each event's seq as a 32-bit offset from the group's first seq: seq_ring <= 2^32)
     e->hot.agg_reg = L <= 128 && ring <= (1ull << 32) && (vr ? atoi(vr) != 0
-                                     : (uint64_t)cfg->max_batch >= 32ull * S && cfg->max_batch >= 8192u &&
-                                           (uint64_t)cfg->max_batch * grp <= (4ull << 20));  // (pools of a
+                                     : (uint64_t)cfg->max_batch >= 8ull * S && cfg->max_batch >= 8192u &&
+                                           (uint64_t)cfg->max_batch * grp >= 256ull * S &&
+                                           (uint64_t)cfg->max_batch * grp <= (8ull << 20));  // (pools of a
                                                                                              // group's records)
     e->reg_agg_auto = e->hot.agg_reg && !vr;
     // the grouped aggregate path's side jobs on a stream of their own (ME_SIDE_STREAM=0: in line)
