@@ -2354,6 +2354,7 @@ __global__ __launch_bounds__(256) void k_seq_sweep(BookDev bk, SeqGroup sg) {
     o.epoch = epoch;
     o.pad[0] = o.pad[1] = o.pad[2] = 0;
     bk.sq[sg.in ^ 1u] = o;
+    bk.stats[ST_LAUNCH] = sg.launch;
     bk.hcount[0] = 0;  // the match launch after this one hands symbols off from 0 ...
     bk.hcount[1] = 0;  // ... and continues them (k_match_hot_cont) from 0
     if (bk.agg_ctr)

@@ -268,7 +268,9 @@ struct HotLaunch {
 // Event counters kept on the device (BookDev::stats, me_stats_read).
 // ST_RESTING: resting orders of every symbol (each wave adds its symbol's change when it writes the
 // symbol state back); k_seq_sweep publishes it to the host for admission control (me_engine.cpp).
-enum : uint32_t { ST_HANDOFFS = 0, ST_RESTING = 1, ME_STATS = 8 };
+// ST_LAUNCH: the match launches enqueued before the current group (k_seq_sweep), for the continuation's
+// hand-off publication.
+enum : uint32_t { ST_HANDOFFS = 0, ST_RESTING = 1, ST_LAUNCH = 2, ME_STATS = 8 };
 
 struct BookDev {
   Level* levels;

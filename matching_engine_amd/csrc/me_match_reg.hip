@@ -1295,7 +1295,13 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
   if constexpr (kSlow) {  // nothing handed off (the usual case): leave before the argument copy
     nhand = min(*(volatile uint32_t*)bk.hcount, bk.S);
     if (blockIdx.x * REG_WAVES >= nhand) return;
-    if (blockIdx.x == 0 && threadIdx.x == 0 && bk.stats) atomicAdd(bk.stats + ST_HANDOFFS, (unsigned long long)nhand);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && bk.stats) {
+      const unsigned long long h = atomicAdd(bk.stats + ST_HANDOFFS, (unsigned long long)nhand) + nhand;
+      // published at once (k_seq_sweep would publish it only ahead of the launch after next): the
+      // engine's grouped-aggregate policy sees this group's hand-offs before it launches the next group
+      if (bk.pub)
+        bk.pub[1] = ((bk.stats[ST_LAUNCH] + 1ull) << 32) | (h < 0xFFFFFFFFull ? h : 0xFFFFFFFFull);
+    }
   }
   {
     for (uint32_t i = threadIdx.x; i < sizeof(ColdArgs) / 8; i += 128 * REG_WAVES)
