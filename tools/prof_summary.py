@@ -4,7 +4,7 @@
     prof_summary.py trace DIR [--steps K]        per-kernel count / avg / total (us) of a kernel trace, and
                                                  the timeline of the run's last launch group
     prof_summary.py dram DIR --bench LOG       byte-exact EA traffic per order from the 32-B-unit counters
-    prof_summary.py traffic FETCH_DIR WRITE_DIR --bench LOG
+    prof_summary.py traffic FETCH_DIR WRITE_DIR --bench LOG [--from-sweep K]
                                                  HBM bytes per order over every included dispatch of the run
                                                  (FETCH_SIZE x2, the gfx950 correction of MI355X_MICROARCH.md;
                                                  WRITE_SIZE x1; KB -> B), per kernel and in total, divided by
@@ -62,11 +62,19 @@ def bench_orders(log):
     raise SystemExit(f"no bench line in {log}")
 
 
-def counters(d, want=None):
-    """{kernel: {counter: [value per dispatch]}} (values summed over the dispatch's rows)."""
+def counters(d, want=None, from_sweep=0):
+    """{kernel: {counter: [value per dispatch]}} (values summed over the dispatch's rows); from_sweep = k:
+    only the dispatches from the k-th k_seq_sweep on (the batches before it — config 4's seeding — dropped)."""
     out = defaultdict(lambda: defaultdict(dict))
     for f in glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True):
-        for r in csv.DictReader(open(f)):
+        rows = list(csv.DictReader(open(f)))
+        first = 0
+        if from_sweep:
+            sw = sorted({int(r.get("Dispatch_Id") or 0) for r in rows if "k_seq_sweep" in (r.get("Kernel_Name") or "")})
+            first = sw[from_sweep] if from_sweep < len(sw) else 1 << 62
+        for r in rows:
+            if int(r.get("Dispatch_Id") or 0) < first:
+                continue
             cn = r.get("Counter_Name") or r.get("Counter-Name")
             if want and cn != want:
                 continue
@@ -77,10 +85,10 @@ def counters(d, want=None):
     return {n: {c: [v[k] for k in sorted(v)] for c, v in cs.items()} for n, cs in out.items()}
 
 
-def traffic(fdir, wdir, log):
+def traffic(fdir, wdir, log, from_sweep=0):
     d, orders = bench_orders(log)
-    f = counters(fdir, "FETCH_SIZE")
-    w = counters(wdir, "WRITE_SIZE")
+    f = counters(fdir, "FETCH_SIZE", from_sweep)
+    w = counters(wdir, "WRITE_SIZE", from_sweep)
     per = {}
     tot_f = tot_w = 0.0
     for n in sorted(set(f) | set(w)):
@@ -98,6 +106,7 @@ def traffic(fdir, wdir, log):
         "statistic": "sum over every dispatch of the match pipeline's kernels in the run (warmup + timed "
                      "batches, fill and drain launches included) / the orders of those batches",
         "correction": "FETCH_SIZE x2 (gfx950 half-count of wide reads, MI355X_MICROARCH.md), WRITE_SIZE x1, KB->B x1024",
+        "from_sweep": from_sweep,
         "per_kernel": dict(sorted(per.items(), key=lambda x: -x[1]["bytes_per_order"])),
         "build": d.get("build"),
         "workload": d["config"].get("workload"),
@@ -171,7 +180,7 @@ def main():
         steps = int(a[a.index("--steps") + 1]) if "--steps" in a else None
         trace(a[1], steps)
     elif a[0] == "traffic":
-        traffic(a[1], a[2], a[a.index("--bench") + 1])
+        traffic(a[1], a[2], a[a.index("--bench") + 1], int(a[a.index("--from-sweep") + 1]) if "--from-sweep" in a else 0)
     elif a[0] == "dram":
         dram(a[1], a[a.index("--bench") + 1])
     elif a[0] == "sq":
