@@ -42,7 +42,11 @@
  *
  * Capacity: a slice the backend refuses (its books near max_resting) is split and matched in parts;
  * a single LIMIT that still does not fit is answered in-band with an OrderUpdate REJECTED (reason
- * ME_RJ_CAPACITY) instead of stalling every later slice behind it.
+ * ME_RJ_CAPACITY) instead of stalling every later slice behind it. Deliberate deviation from the
+ * reference, which has no capacity: admission counts every LIMIT as one that may rest (whether it fills
+ * is only known once matched), so near max_resting a marketable LIMIT that would have filled completely is
+ * refused too. max_resting is a deployment parameter sized to HBM; a deployment sizes it
+ * above its resting high-water mark.
  */
 #ifndef ME_SERVICE_H
 #define ME_SERVICE_H
