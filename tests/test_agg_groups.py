@@ -225,3 +225,22 @@ def test_agg_auto_mode_turns_off_under_cancels(me, orc):
         outs += _pipelined(eng, batches[16:], 9)
         assert not eng.paths()["grouped_agg"], "hand-offs should have turned the aggregate path off"
         _check(eng, ob, batches, outs, "agg auto flip")
+
+
+@pytest.mark.parametrize("symbols,agg", [(768, True), (2048, False)])
+def test_agg_auto_choice_by_records_per_symbol(me, orc, symbols, agg):
+    """Automatic path choice (ME_REG_AGG unset) by shape: 8,192-record batches over 768 symbols (~10.7
+    records per symbol and batch, ~340 per 32-batch group: config 3's shape) take the grouped aggregate
+    path; over 2,048 symbols (4 per batch) they stay on k_match_reg. Every batch against the oracle."""
+    sc = me.preset(3, num_symbols=symbols, levels=128, batch=8192)
+    st = me.Stream(sc)
+    base = st.base_prices()
+    batches = [st.next(sc.batch) for _ in range(40)]
+    total = sum(len(b) for b in batches)
+    assert os.environ.get("ME_REG_AGG") is None
+    ob = orc.OracleBook(sc.num_symbols)
+    with me.Engine(sc.num_symbols, sc.levels, base, max_batch=sc.batch, max_resting=total + 1024,
+                   seq_ring=1 << 22) as eng:
+        outs = _pipelined(eng, batches, 70)
+        assert eng.paths()["grouped_agg"] == agg
+        _check(eng, ob, batches, outs, f"auto choice S={symbols}")
