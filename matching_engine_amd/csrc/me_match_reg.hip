@@ -1112,7 +1112,9 @@ struct SideArgs {
 #define ME_SIDE_THREADS 512
 #endif
 #ifndef ME_SB_REC
-#define ME_SB_REC 4096
+#define ME_SB_REC 2048  // records per bucket workgroup: same box, config 2's driver shape 1,818-1,836M at 4,096,
+                        // 1,911-1,918M at 2,048, 1,804-1,820M at 1,024; 640 steps 2,561 / 2,604 / 2,572M; config
+                        // 3 1,301 / 1,317M (profiles/r4/sb) — the group's walk + resolve 549 -> 514 us
 #endif
 constexpr int SIDE_THREADS = ME_SIDE_THREADS;
 constexpr int SIDE_WAVES = SIDE_THREADS / 64;
