@@ -2526,6 +2526,9 @@ hipError_t launch_agg_group(hipStream_t st, const BookDev& bk, const BatchDev* b
 // The register-ladder launch (me_match_reg.hip, two builds): one head-cache entry per level while one
 // workgroup per CU covers the symbols (rc128), 64 shared entries and two workgroups per CU beyond
 // that (rc64). ax.nwg is the CU count (0: assume 256).
+#ifndef ME_SIDE_XSEQ
+#define ME_SIDE_XSEQ 1
+#endif
 hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* bt, uint32_t ng, const AuxDev& ax,
                             hipEvent_t ev0, hipEvent_t ev1, const HotLaunch* hot) {
   constexpr uint32_t kWaves = 4;  // matching waves per workgroup (me_match_reg.hip REG_WAVES)
@@ -2543,8 +2546,10 @@ hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* b
       // output sets), and everything they read was final when the fork was recorded
       if ((e = hipEventRecord(hot->sfork, st)) != hipSuccess || (e = hipStreamWaitEvent(hot->sst, hot->sfork, 0)) != hipSuccess)
         return e;
-      e = big ? rc64::launch_match_reg(hot->sst, bk, bt, 0, ax, nullptr, nullptr)
-              : rc128::launch_match_reg(hot->sst, bk, bt, 0, ax, nullptr, nullptr);
+      AuxDev sx = ax;
+      sx.xseq = ME_SIDE_XSEQ;  // off the critical path: bucket the batches per XCD in turn (fewer partial lines)
+      e = big ? rc64::launch_match_reg(hot->sst, bk, bt, 0, sx, nullptr, nullptr)
+              : rc128::launch_match_reg(hot->sst, bk, bt, 0, sx, nullptr, nullptr);
       if (e != hipSuccess || (e = hipEventRecord(hot->sjoin, hot->sst)) != hipSuccess) return e;
       e = ev0 ? hipEventRecord(ev0, st) : hipSuccess;
     } else if (side) {

@@ -389,6 +389,8 @@ struct AuxDev {
   uint32_t nwg;  // workgroups that run side jobs (those of the first dispatch round)
   uint32_t nb;   // bucket jobs (batches of group J)
   uint32_t nt;   // tape jobs (batches of group J-2)
+  uint32_t xseq; // k_side beside a walk: each XCD buckets its batches one after another (me_match_reg.hip)
+  uint32_t rsv;
   unsigned long long* fills_acc;
   AuxBucket b[ME_GMAX];
   AuxTape t[ME_GMAX];

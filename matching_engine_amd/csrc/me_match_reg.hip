@@ -1212,6 +1212,18 @@ __global__ __launch_bounds__(SIDE_THREADS) void k_side(SideArgs args, uint32_t n
     // on blocks b = j (mod 8), so the runs its workgroups write side by side into one bucket array
     // meet in one L2 and leave it as whole lines, not as partial lines from several XCDs.
     const uint32_t x = blockIdx.x % 8u, k = blockIdx.x / 8u;
+    if (ldsu(G.ax.xseq)) {
+      // beside a walk (off the critical path): unit k of each of the XCD's batches in turn, so one
+      // batch's buckets (1.5 MB at config 2) are being filled per L2 at a time, not four batches' 6 MB
+      // whose partial lines the 4-MB L2 evicts before the later units complete them (profiles/r4/xs)
+      for (uint32_t j = x; j < nb; j += 8) {
+        const uint32_t n = ldsu(G.ax.b[j].n), r0 = k * SB_REC;
+        if (r0 >= n) continue;  // (uniform over the workgroup)
+        side_bucket_wg(G, j, r0, min(n, r0 + SB_REC), side_cnt);
+        __syncthreads();  // the LDS counters are zeroed again by the next batch
+      }
+      return;
+    }
     uint32_t off = 0;
     for (uint32_t j = x; j < nb; j += 8) {
       const uint32_t n = ldsu(G.ax.b[j].n), nu = (n + SB_REC - 1) / SB_REC;
@@ -1816,7 +1828,10 @@ hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* b
     uint32_t nbu = 0;
     if (hist) {  // 8 x the most units any XCD's batches have (batch j on blocks = j mod 8)
       uint32_t per[8] = {};
-      for (uint32_t j = 0; j < ax.nb; ++j) per[j % 8] += (ax.b[j].n + SB_REC - 1) / SB_REC;
+      for (uint32_t j = 0; j < ax.nb; ++j) {
+        const uint32_t nu = (ax.b[j].n + SB_REC - 1) / SB_REC;
+        per[j % 8] = ax.xseq ? max(per[j % 8], nu) : per[j % 8] + nu;  // xseq: the batches in turn
+      }
       for (uint32_t x = 0; x < 8; ++x) nbu = max(nbu, 8u * per[x]);
     }
     // the waves after the bucket workgroups: tape tiles (and per-record bucket blocks without hist)
