@@ -4,6 +4,8 @@ stream's mix (cancels, sweeping MARKETs, far LIMITs, drifting mids, Zipf symbols
 and the submission path (device groups, host pipeline with a collect lag, synchronous batches) are
 drawn per case from a seeded generator; every batch's results and tape and the final books must
 equal the oracle's. Cheap cases, many shapes: the kind of test that found the group-count bug."""
+import os
+
 import numpy as np
 import pytest
 
@@ -54,12 +56,16 @@ def _case(me, seed, agg=False):
     return sc, base, batches, group, path, lag
 
 
-@pytest.mark.parametrize("seed", range(24))
+# ME_FUZZ_SEEDS=N widens both draws to N seeds for soak runs (profiles/r4/soak); the suite's default stays cheap
+_SEEDS = int(os.environ.get("ME_FUZZ_SEEDS", "0"))
+
+
+@pytest.mark.parametrize("seed", range(_SEEDS or 24))
 def test_fuzz_case(me, seed):
     _run_case(me, seed, False)
 
 
-@pytest.mark.parametrize("seed", range(10))
+@pytest.mark.parametrize("seed", range(_SEEDS or 10))
 def test_fuzz_agg_case(me, seed, monkeypatch):
     """ME_REG_AGG=1: every launch group through k_agg_gwalk (cancels, far prices and overfull buckets hand
     symbols to k_match_reg's continuation mid-group), chunk pool max_resting + 2S."""
@@ -75,8 +81,19 @@ def _run_case(me, seed, agg):
     ctx = (f"{'agg ' if agg else ''}seed {seed}: L={sc.levels} S={sc.num_symbols} batch={sc.batch} G={group} path={path} "
            f"lag={lag} cancel={sc.cancel_pct} far={sc.far_pct} drift={sc.drift_step}/{sc.drift_every}")
     ob = OracleBook(sc.num_symbols)
+    # far-level capacity (me_config.far_levels, a documented per-symbol-and-side bound): the busiest
+    # symbol's records outside its initial window bound its far levels — a 180k-record single-symbol
+    # stream with 5 % far prices (up to 64 windows out) rests more distinct far levels than the default
+    # 1,024 and the engine rightly refuses it (agg seed 55 of a soak, profiles/r4/soak)
+    far = np.zeros(sc.num_symbols + 1, dtype=np.int64)
+    for b in batches:
+        sym = np.minimum(b.symbol, sc.num_symbols)
+        off = b.price_q4 - np.asarray(base, dtype=np.int64)[np.minimum(sym, sc.num_symbols - 1)]
+        np.add.at(far, sym, ((off < 0) | (off >= sc.levels)).astype(np.int64))  # outside the initial window
+    far_levels = max(1024, min(int(far[:-1].max()) + 64, (1 << 21) // sc.num_symbols))
     with me.Engine(sc.num_symbols, sc.levels, base, max_batch=sc.batch, max_resting=total + 1024,
-                   max_chunks=total + 1024 + 2 * sc.num_symbols, seq_ring=1 << 20, batches_per_launch=group) as eng:
+                   max_chunks=total + 1024 + 2 * sc.num_symbols, seq_ring=1 << 20, batches_per_launch=group,
+                   far_levels=far_levels) as eng:
         if agg:
             assert eng.paths()["grouped_agg"], ctx
         outs = [None] * len(batches)
