@@ -2340,10 +2340,17 @@ __global__ __launch_bounds__(256) void k_seq_sweep(BookDev bk, SeqGroup sg) {
   const unsigned long long R = bk.ring_mask + 1ull;
   const bool need = gmax - st.horizon >= R;
   const uint32_t epoch = need ? st.epoch + 1u : st.epoch;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    bool order_ok = st.last == 0ull || seq_follows(st.last, gmin, sg.kind[0][0]);
-    for (uint32_t g = 0; g + 1 < sg.ng; ++g)
+  bool order_ok = true;
+  if (blockIdx.x == 0 && threadIdx.x < 64) {
+    // the batch boundaries of the group, one lane each (one thread's loop waited ~0.4 us per batch:
+    // 11.9 -> 4.7 us for config 2's 20-batch group, profiles/r4/ev)
+    const uint32_t l = threadIdx.x;
+    if (l == 0) order_ok = st.last == 0ull || seq_follows(st.last, gmin, sg.kind[0][0]);
+    for (uint32_t g = l; g + 1 < sg.ng; g += 64)
       order_ok &= seq_follows(sg.seq[g][sg.n[g] - 1], sg.seq[g + 1][0], sg.kind[g + 1][0]);
+    order_ok = __ballot(!order_ok) == 0ull;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
     uint32_t bits = 0;
     if (!order_ok) bits |= ERR_SEQ_ORDER;
     if (gmax - gmin >= R) bits |= ERR_SEQ_SPAN;
