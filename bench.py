@@ -80,11 +80,10 @@ def parse():
     ap.add_argument("--batches-per-launch", type=int, default=0,
                     help="batches matched per kernel launch (me_config.batches_per_launch; 0 = engine default 32)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample")
-    ap.add_argument("--cpu-threads", type=int, default=len(os.sched_getaffinity(0)),
-                    help="threads of the sharded CPU baseline (default: every core this process may run on, "
-                         "SURVEY.md §8(d)); 1 = scalar only")
-    ap.add_argument("--cpu-threads-alt", type=int, default=16,
-                    help="a second sharded CPU run at this many threads, reported beside the first (0 = none)")
+    ap.add_argument("--cpu-threads-sweep", default="1,16,64,128,256",
+                    help="thread counts of the native CPU baseline (every core of the affinity mask is added, "
+                         "SURVEY.md §8(d)); value = the best")
+    ap.add_argument("--cpu-warmup", type=int, default=4, help="untimed stream batches before the CPU sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--e2e-steps", type=int, default=384,
@@ -104,6 +103,10 @@ def parse():
                     help="JSON {bytes_per_order: ...} from tools/gpu/pmc_traffic_wl.sh for roofline.traffic (c2; the "
                          "k_match_reg measurement when the engine runs c2 without grouped aggregate launches)")
     args = ap.parse_args()
+    args.cpu_threads_sweep = [int(t) for t in args.cpu_threads_sweep.split(",") if t]
+    # a shape override makes a c3 run an experiment: its cluster leg (config 3's fixed global slice shape)
+    # then runs only when asked for with --cluster-steps
+    args.shape_override = any(v is not None for v in (args.symbols_per_gpu, args.batch_per_gpu, args.levels))
     w = WORKLOADS[args.workload]
     if args.symbols_per_gpu is None:
         args.symbols_per_gpu = w.get("symbols_per_gpu", 0)
@@ -199,88 +202,65 @@ def build_rank_batches(args, world, rank, nbatches, n_whole=0):
 
 def cpu_baseline(args):
     """CPU oracle (oracle/, the scalar price-time book of the build-defined semantics; the reference
-    itself has no matcher) on a bounded prefix of the same N=1 stream: 1 thread, and `--cpu-threads`
-    threads with the symbols hash-sharded across them exactly as across GPUs (one book per thread,
-    no shared state; ctypes drops the GIL inside orc_submit). Batches are split per thread before
-    the clock starts, like the GPU's HBM-resident inputs."""
-    import threading
+    itself has no matcher) on a bounded prefix of the same N=1 stream, natively multi-threaded
+    (oracle_book.cpp orc_run_sharded: one std::thread and one book per shard, symbols hash-sharded
+    across threads exactly as across GPUs, batches split per thread before the clock starts like the
+    GPU's HBM-resident inputs, no Python in the timed loop). Swept over --cpu-threads-sweep thread
+    counts (plus every core of the affinity mask); `value` is the best, `sweep` lists them all.
+    Every leg first runs the stream's first --cpu-warmup batches (and config 4's seeded books) untimed."""
+    from oracle.oracle import OracleBook, run_sharded
 
-    from oracle.oracle import OracleBook
+    from matching_engine_amd.sharding import ShardPlan
 
     w = WORKLOADS[args.workload]
     S = global_symbols(args, 1)
     sc = me.preset(w["preset"], num_symbols=S, batch=args.batch_per_gpu, **_wl_levels(w))
-
-    def seeded_stream():
-        st = me.Stream(sc)
-        seeds = st.seed_books(range(w["seeded"]), w["per_side"]) if w.get("seeded") else None
-        return st, seeds
-
-    # ---- 1 thread
-    st, seeds = seeded_stream()
+    st = me.Stream(sc)
+    seeds = st.seed_books(range(w["seeded"]), w["per_side"]) if w.get("seeded") else None
+    warm = [st.next(sc.batch) for _ in range(args.cpu_warmup)]
+    pre = []  # untimed batches: the seeded books (config 4), then the warm-up batches
+    if seeds is not None:
+        pre += [seeds.take(np.arange(i, min(i + (1 << 20), len(seeds)))) for i in range(0, len(seeds), 1 << 20)]
+    pre += warm
+    # k = the batches one thread matches in about --cpu-seconds (the single-core sample, timed per batch)
     ob = OracleBook(S)
-    seeded = ""
-    if seeds is not None:  # config 4: the same pre-seeded deep books as the GPU run (untimed)
-        for i in range(0, len(seeds), 1 << 20):
-            ob.submit(seeds.take(slice(i, i + (1 << 20))))
-        seeded = f" after seeding {len(seeds)} resting orders (untimed)"
-    done, t_cpu, k = 0, 0.0, 0
+    for b in pre:
+        ob.submit(b)
+    timed, t_cpu = [], 0.0
     while t_cpu < args.cpu_seconds:
         b = st.next(sc.batch)
         t0 = time.perf_counter()
         ob.submit(b)
         t_cpu += time.perf_counter() - t0
-        done += len(b)
-        k += 1
+        timed.append(b)
     ob.close()
-    one = done / t_cpu
-    out = {"value": one, "unit": "orders/s", "cores": 1, "kind": "port",
-           "sample": f"first {k} batches ({done} orders) of the {args.workload} stream, oracle/oracle_book.cpp "
-                     f"scalar price-time book, {t_cpu:.1f}s{seeded}"}
+    k, done = len(timed), sum(len(b) for b in timed)
 
     def sharded(T):
-        """The same k batches on T threads, symbols hash-sharded (one book per thread): orders/s of the wall."""
-        st, seeds = seeded_stream()
-        from matching_engine_amd.sharding import ShardPlan
-
         plan = ShardPlan(S, T)
-        books = [OracleBook(len(plan.members[r])) for r in range(T)]
-        if seeds is not None:
-            for i in range(0, len(seeds), 1 << 20):
-                for r, (lb, _) in enumerate(plan.split(seeds.take(slice(i, i + (1 << 20))))):
-                    books[r].submit(lb)
         parts = [[] for _ in range(T)]
-        for _ in range(k):
-            for r, (lb, _) in enumerate(plan.split(st.next(sc.batch))):
+        for b in pre + timed:
+            for r, (lb, _) in enumerate(plan.split(b)):
                 parts[r].append(lb)
-
-        def run(r):
-            for lb in parts[r]:
-                books[r].submit(lb)
-
-        th = [threading.Thread(target=run, args=(r,)) for r in range(T)]
-        t0 = time.perf_counter()
-        for t in th:
-            t.start()
-        for t in th:
-            t.join()
-        tw = time.perf_counter() - t0
+        books = [OracleBook(len(plan.members[r])) for r in range(T)]
+        wall, _ = run_sharded(books, parts, nwarm=len(pre))
         for bk in books:
             bk.close()
-        return done / tw, tw
+        return done / wall, wall
 
-    T = min(args.cpu_threads, S)  # (a thread without a symbol would idle)
-    if T <= 1:
-        return out
-    v, tw = sharded(T)
-    out.update({"value": v, "cores": T, "single_core_value": one,
-                "sample": out["sample"] + f"; then the same {k} batches on {T} threads (every core of the process's "
-                          f"affinity mask), symbols hash-sharded (one book per thread), {tw:.2f}s wall"})
-    Ta = min(args.cpu_threads_alt, S)
-    if Ta > 1 and Ta != T:
-        va, _ = sharded(Ta)
-        out["alt"] = {"value": va, "cores": Ta}
-    return out
+    allowed = len(os.sched_getaffinity(0))
+    ts = sorted({t for t in args.cpu_threads_sweep + [allowed] if 1 <= t <= min(S, allowed)})
+    sweep = {}
+    for T in ts:
+        v, wall = sharded(T)
+        sweep[str(T)] = {"value": v, "wall_s": round(wall, 4)}
+    best = max(sweep, key=lambda t: sweep[t]["value"])
+    seeded = f", after seeding {len(seeds)} resting orders" if seeds is not None else ""
+    return {"value": sweep[best]["value"], "unit": "orders/s", "cores": int(best), "kind": "port",
+            "single_core_value": sweep["1"]["value"] if "1" in sweep else None, "sweep": sweep,
+            "sample": f"{k} batches ({done} orders) of the {args.workload} stream after {args.cpu_warmup} untimed "
+                      f"warm-up batches{seeded}; oracle/oracle_book.cpp scalar price-time book, one book and one "
+                      f"std::thread per shard (orc_run_sharded), symbols hash-sharded; best of threads {ts}"}
 
 
 def c1_requests(n: int):
@@ -397,8 +377,21 @@ def host_info():
                 break
     except OSError:
         pass
-    return {"nproc": os.cpu_count(), "cpu_model": model,
-            "cpus_allowed": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None}
+    quota = None
+    try:  # the cgroup's CPU quota ("max" = none) and the affinity mask the CPU baseline's threads run on
+        quota = open("/sys/fs/cgroup/cpu.max").read().strip()
+    except OSError:
+        pass
+    aff = sorted(os.sched_getaffinity(0))
+    ranges, i = [], 0
+    while i < len(aff):
+        j = i
+        while j + 1 < len(aff) and aff[j + 1] == aff[j] + 1:
+            j += 1
+        ranges.append(f"{aff[i]}-{aff[j]}" if j > i else str(aff[i]))
+        i = j + 1
+    return {"nproc": os.cpu_count(), "cpu_model": model, "cpus_allowed": len(aff), "affinity": ",".join(ranges),
+            "cgroup_cpu_max": quota, "loadavg": os.getloadavg()}
 
 
 def cluster_leg(args, world, rank, local, sc, base, slices, n_slices):
@@ -459,7 +452,7 @@ def main():
 
     nb = args.warmup + args.steps
     n_cluster = args.cluster_steps if args.cluster_steps is not None else (
-        16 if world > 1 or args.workload == "c3" else 0)
+        16 if world > 1 or (args.workload == "c3" and not args.shape_override) else 0)
     n_e2e = 0 if args.no_e2e else args.e2e_steps
     sc, gbase, ids, batches, positions, global_orders, seeds, whole = build_rank_batches(
         args, world, rank, nb + n_e2e, 0 if args.workload == "c3" else n_cluster)

@@ -114,8 +114,9 @@ typedef struct me_config {
   const uint32_t* symbol_ids;  /* optional [num_symbols] ids written to me_fill.symbol (NULL = local id) */
   uint32_t batches_per_launch; /* L <= 128: device batches matched per kernel launch, 1..64 (0 = 32). Back-to-back
                                   me_submit_batch_device calls fill a group; me_sync flushes a partial one */
-  uint32_t far_levels;         /* capacity per symbol and side of the far arrays (price levels outside the
-                                  window), 0 = 1024 */
+  uint32_t far_levels;         /* far levels (price levels outside the window) each symbol and side holds in
+                                  its inline region, 0 = 256. Not a limit: a side that outgrows it moves to
+                                  the far arena, sized from max_resting so it never runs out (me_far_stats) */
   uint32_t host_slots;         /* pinned slots of the host-batch pipeline (me_submit_host), 0 = enough to keep
                                   four launch groups in flight (4 * batches_per_launch + 1); allocated on use */
   uint64_t host_tape_cap;      /* fills a slot holds (0 = 2 * max_batch + 4096). A longer tape is recovered at
@@ -192,8 +193,9 @@ uint64_t me_fill_bound(const me_engine* e, size_t n);
  * batch k+1, the match of batch k and the PCIe writes of batch k-1's results and tape (by the tape
  * job, straight into the slot's pinned block) overlap.
  * me_collect waits for the ticket's batch (launching a partial group first when it is still waiting
- * for one) and points into the slot's pinned outputs: valid until the slot is reused by ticket +
- * host_slots. A slot is reused only after its ticket was collected (else ME_E_STATE). Not
+ * for one) and points into the slot's pinned outputs: valid until the next me_collect (the engine holds
+ * the last collected slot back; only a submit that finds every other slot busy takes it). A slot is
+ * reused only after its ticket was collected (else ME_E_STATE). Not
  * thread-safe, like every other entry point: serialize calls on one engine. */
 int me_submit_host(me_engine* e, const me_order_soa* batch, size_t n, uint64_t* ticket);
 int me_collect(me_engine* e, uint64_t ticket, const me_fill** fills, size_t* n_fills,
@@ -283,6 +285,12 @@ int me_timing_read(me_engine* e, double* match_ms, double* pipeline_ms, uint64_t
 /* Event counters since me_create: handoffs = symbols the register-window kernel handed to its
  * continuation launch (a far price level, a re-centre, a cancel of a far or very old order). */
 int me_stats_read(me_engine* e, uint64_t* handoffs);
+
+/* Far levels (price levels outside a symbol's window; unbounded since round 5): moves =
+ * sides that outgrew their region and moved to a larger one in the far arena, collections = the
+ * arena's copying collections (k_seq_sweep), arena_used = entries taken from the active half. Any
+ * pointer may be NULL. No reference counterpart (the reference keeps no book). */
+int me_far_stats(me_engine* e, uint64_t* moves, uint64_t* collections, uint64_t* arena_used);
 
 /* The matching paths the engine runs now (no reference counterpart: the reference has one CPU path).
  * *flags bit 0 (ME_PATH_GROUPED_AGG): launch groups of windows <= 128 levels go through the aggregate

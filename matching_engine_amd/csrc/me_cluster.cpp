@@ -24,6 +24,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <deque>
 #include <memory>
@@ -679,7 +680,9 @@ extern "C" me_cluster* me_cluster_create(const me_cluster_config* cfg, const me_
   // ranks that match through the engine's pinned host slots (rank 0's direct part, every rank on a host
   // transport) allocate them now: a slot's first use would otherwise pin ~100 MB inside a slice's split
   // (config 3's 1M-record slices: 51 ms per slice over 16 slices, profiles/r4/r4c)
-  if (c->eng && (c->direct0 || !dev) && me_host_reserve(c->eng, 0) != ME_OK) {
+  // (the protocol's slots only: kMaxInflight tickets, the slot the last collect holds, one spare — not the
+  // engine's 4G + 1, which at 1M-record slices would pin ~14 GB)
+  if (c->eng && (c->direct0 || !dev) && me_host_reserve(c->eng, kMaxInflight + 2) != ME_OK) {
     set_create_err("me_cluster_create: host slots: " + eng_err(c->eng));
     free_cluster(c.get());
     return nullptr;
@@ -893,6 +896,28 @@ static int run_collect(me_cluster* c, const int64_t* hdr) {
         off += bytes[r];
       }
     }
+    // every shard's results must account for its tape exactly (fill counts summing to its fills, each run
+    // inside the tape): the copy below trusts them
+    for (uint32_t r = 0; r < W; ++r) {
+      const size_t np = tk.pos_off[r + 1] - tk.pos_off[r], nfr = (size_t)szs[2 * r];
+      const me_order_result* rr = tr[r];
+      std::atomic<uint64_t> sum{0};
+      std::atomic<bool> bad{false};
+      par_chunks(np, kGrain, [&](size_t, size_t a, size_t b) {
+        uint64_t x = 0;
+        bool out = false;
+        for (size_t k = a; k < b; ++k) {
+          x += rr[k].fill_count;
+          out |= rr[k].fill_count && (uint64_t)rr[k].tape_offset + rr[k].fill_count > nfr;
+        }
+        sum += x;
+        if (out) bad = true;
+      });
+      if (bad || sum != nfr) {
+        c->failed = true;
+        return c->fail(ME_E_STATE, "shard " + std::to_string(r) + "'s results do not account for its tape");
+      }
+    }
     c->res.resize(tk.n);
     me_order_result* res = c->res.data();
     for (uint32_t r = 0; r < W; ++r) {
@@ -1002,11 +1027,7 @@ static int run_book(me_cluster* c, const int64_t* hdr, const BookReq* q) {
   if (known && own == c->cfg.rank && !c->failed) {
     const uint32_t ls = c->local[sym];
     uint32_t d = depth;
-    if (!d && !c->use_ops) {  // the whole book: every window level plus the far arrays
-      me_config ec{};
-      me_get_config(c->eng, &ec);
-      d = ec.levels + ec.far_levels;
-    }
+    if (!d && !c->use_ops) d = 0xFFFFFFFFu;  // the whole book: every window level plus the far levels
     auto call = [&](me_book_entry* b, size_t bc, size_t* nb, me_book_entry* a, size_t ac, size_t* na, me_level* bl,
                     me_level* al, size_t* nbl, size_t* nal) {
       return c->use_ops ? c->ops.book(c->ops.ctx, ls, d, b, bc, nb, a, ac, na, bl, al, nbl, nal)

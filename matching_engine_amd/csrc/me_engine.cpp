@@ -235,7 +235,9 @@ struct me_engine {
   uint32_t ntiles_sort = 0;            // sort tiles of a max_batch batch (histogram row stride)
   // host-batch pipeline
   std::vector<HostSlot> hs;
-  std::vector<int> free_slots;  // LIFO: a synchronous caller keeps reusing one warm slot
+  std::vector<int> free_slots;  // LIFO: a synchronous caller keeps reusing two warm slots
+  int held_slot = -1;           // the last collected slot: its outputs stay readable until the next
+                                // me_collect (or a submit that finds every other slot busy)
   std::unordered_map<uint64_t, int> by_ticket;  // uncollected tickets -> slot
   uint64_t hcap = 0;         // tape records per slot
   uint64_t next_ticket = 0;
@@ -319,7 +321,7 @@ static void free_all(me_engine* e) {
                   e->bk.loc,      e->bk.chunk_top, e->bk.err,       (void*)e->bk.gsym,
                   e->d_tape,      e->d_tape_count, e->d_fills_acc, e->bk.dbg,      e->bk.fcache,
                   e->bk.far,      e->bk.old,       e->bk.sq,       e->bk.hcount,     e->bk.hand,
-                  e->bk.stats};
+                  e->bk.stats,    e->bk.fdir,      e->bk.far_ctl};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   {
@@ -510,7 +512,13 @@ extern "C" me_engine* me_create(const me_config* cfg) {
   bk.nchunks = (uint32_t)nchunks;
   const uint64_t ring = cfg->seq_ring ? cfg->seq_ring : (1ull << 28);
   bk.ring_mask = ring - 1;
-  bk.fcap = cfg->far_levels ? cfg->far_levels : 1024u;
+  // far levels: an inline region of fcap entries per (symbol, side), and two halves of 6 x max_resting
+  // entries that sides outgrowing it move into, collected above 2 x max_resting (me_far.hpp's bound)
+  bk.fcap = cfg->far_levels ? cfg->far_levels : 256u;
+  bk.far_gc_at = 2 * (cfg->max_resting + 64);
+  bk.far_half = 6 * (cfg->max_resting + 64) + 4ull * bk.fcap;
+  if (const char* v = getenv("ME_FAR_GC_AT"))  // (tests: collect earlier — any lower trigger keeps the bound)
+    bk.far_gc_at = std::min<uint64_t>(bk.far_gc_at, strtoull(v, nullptr, 10));
   // deep windows (L > 128, the sort path): a symbol with at least hot_min records in a batch runs the
   // aggregate path (me_agg.hip, L <= AGG_MAX_L) — or, with ME_HOT_AGG=0, the write-through top-of-book
   // path k_match_hot (HBM ladders, L > LDS_MAX_LEVELS); ME_HOT_MIN overrides the threshold (0 = off)
@@ -567,7 +575,9 @@ extern "C" me_engine* me_create(const me_config* cfg) {
   ALLOC(bk.sym, S);
   ALLOC(bk.chunks, nchunks);
   ALLOC(bk.loc, ring);
-  ALLOC(bk.far, S * 2 * (uint64_t)bk.fcap);
+  ALLOC(bk.far, S * 2 * (uint64_t)bk.fcap + 2 * bk.far_half);
+  ALLOC(bk.fdir, S * 2);
+  ALLOC(bk.far_ctl, FC_N);
   ALLOC(bk.old, oldn);
   ALLOC(bk.sq, 2);
   ALLOC(bk.hcount, 2);  // [0] hand-offs of a launch, [1] k_match_hot's continuations
@@ -687,6 +697,12 @@ extern "C" me_engine* me_create(const me_config* cfg) {
     ss[i].free_head = NIL;
     gs[i] = cfg->symbol_ids ? cfg->symbol_ids[i] : (uint32_t)i;
   }
+  std::vector<FarDir> fd(2 * S);
+  for (uint64_t i = 0; i < 2 * S; ++i) {
+    fd[i].off = i * bk.fcap;
+    fd[i].cap = bk.fcap;
+    fd[i].pad = 0;
+  }
   SeqState sq0[2];
   memset(sq0, 0, sizeof sq0);
   sq0[0].epoch = sq0[1].epoch = 1;  // old-order entries of epoch 0 (the zeroed table) read as empty
@@ -699,6 +715,8 @@ extern "C" me_engine* me_create(const me_config* cfg) {
             hipMemsetAsync(bk.old, 0, oldn * sizeof(OldEnt), st) == hipSuccess &&
             hipMemsetAsync(bk.hcount, 0, 8, st) == hipSuccess &&
             hipMemsetAsync(bk.stats, 0, ME_STATS * 8, st) == hipSuccess &&
+            hipMemsetAsync(bk.far_ctl, 0, FC_N * 8, st) == hipSuccess &&
+            hipMemcpyAsync(bk.fdir, fd.data(), fd.size() * sizeof(FarDir), hipMemcpyHostToDevice, st) == hipSuccess &&
             hipMemcpyAsync(bk.sq, sq0, sizeof sq0, hipMemcpyHostToDevice, st) == hipSuccess &&
             hipMemsetAsync(bk.fcache, 0xFF, S * 64 * sizeof(uint32_t), st) == hipSuccess &&
             hipMemsetAsync(bk.chunk_top, 0, 4, st) == hipSuccess && hipMemsetAsync(bk.err, 0, 4, st) == hipSuccess &&
@@ -1099,7 +1117,7 @@ static int check_err_bits(me_engine* e, uint32_t w) {
     if (w & ERR_CHUNK_OOM) m += " chunk pool exhausted (raise max_chunks);";
     if (w & ERR_SCRATCH_OOM) m += " fill scratch/tape bound exceeded (raise max_resting);";
     if (w & ERR_INCONSISTENT) m += " book inconsistency;";
-    if (w & ERR_FAR_OOM) m += " far-level array full (raise far_levels);";
+    if (w & ERR_FAR_OOM) m += " far arena exhausted (internal bound broken);";
     if (w & ERR_OLD_OOM) m += " old-order table full (raise max_resting);";
     if (w & ERR_SEQ_ORDER) m += " seqs not ascending (API precondition: a NEW record's seq above every earlier seq, a CANCEL's at least the previous one);";
     if (w & ERR_SEQ_SPAN) m += " one launch group spans the whole seq ring (raise seq_ring);";
@@ -1303,6 +1321,15 @@ extern "C" int me_fetch_group_outputs(me_engine* e, uint32_t k, me_fill* out_fil
 }
 
 // ---- host-batch pipeline (include/me_engine.h) ----------------------------------------------
+// A free slot for the next submit; the held slot (last collected) goes back only when no other is free.
+static bool has_free_slot(me_engine* e) {
+  if (e->free_slots.empty() && e->held_slot >= 0) {
+    e->free_slots.push_back(e->held_slot);
+    e->held_slot = -1;
+  }
+  return !e->free_slots.empty();
+}
+
 static int slots_busy(me_engine* e) {
   uint64_t oldest = UINT64_MAX;
   for (auto& kv : e->by_ticket) oldest = std::min(oldest, kv.first);
@@ -1312,7 +1339,7 @@ static int slots_busy(me_engine* e) {
 extern "C" int me_host_inputs(me_engine* e, size_t n, me_order_soa_w* out) {
   if (!e || !out) return ME_E_INVALID;
   if (n == 0 || n > e->cfg.max_batch) return e->fail(ME_E_INVALID, "me_host_inputs: n must be in [1, max_batch]");
-  if (e->free_slots.empty()) return slots_busy(e);
+  if (!has_free_slot(e)) return slots_busy(e);
   HostSlot& h = e->hs[e->free_slots.back()];
   HIP_TRY(hipSetDevice(e->dev), "hipSetDevice");
   int rc = slot_alloc(e, h);
@@ -1340,7 +1367,7 @@ extern "C" int me_submit_host(me_engine* e, const me_order_soa* b, size_t n, uin
   if (e->failed) return ME_E_STATE;
   if (!b || !b->seq || !b->price_q4 || !b->qty || !b->symbol || !b->kind) return e->fail(ME_E_INVALID, "null batch");
   if (n == 0 || n > e->cfg.max_batch) return e->fail(ME_E_INVALID, "host batch size must be in [1, max_batch]");
-  if (e->free_slots.empty()) return slots_busy(e);
+  if (!has_free_slot(e)) return slots_busy(e);
   const int slot = e->free_slots.back();
   HostSlot& h = e->hs[slot];
   HIP_TRY(hipSetDevice(e->dev), "hipSetDevice");
@@ -1408,9 +1435,10 @@ extern "C" int me_collect(me_engine* e, uint64_t ticket, const me_fill** fills, 
   }
   if (h.state != 2) return e->fail(ME_E_STATE, "host batch outputs were never enqueued");
   HIP_TRY(hipEventSynchronize(h.ev_done), "hipEventSynchronize");
-  h.state = 0;  // collected: the outputs stay readable until the slot is reused
+  h.state = 0;  // collected: the outputs stay readable until the next collect releases the slot
   e->by_ticket.erase(it);
-  e->free_slots.push_back(slot);
+  if (e->held_slot >= 0) e->free_slots.push_back(e->held_slot);
+  e->held_slot = slot;
   const SlotMeta* m = (const SlotMeta*)h.h_out;
   {
     int rc = check_err_bits(e, m->err);
@@ -1607,11 +1635,12 @@ extern "C" int me_book_orders(me_engine* e, uint32_t symbol, uint32_t depth, me_
   if (rc) return rc;
   const bool want_orders = bids || asks || n_bids || n_asks;
   uint64_t ocap = 0;
-  if (want_orders) {  // the symbol's resting count bounds either side's orders
-    SymState ss;
-    HIP_TRY(hipMemcpy(&ss, e->bk.sym + symbol, sizeof ss, hipMemcpyDeviceToHost), "D2H symbol");
-    ocap = std::max<uint64_t>(ss.resting, 1);
-  }
+  SymState ss;
+  HIP_TRY(hipMemcpy(&ss, e->bk.sym + symbol, sizeof ss, hipMemcpyDeviceToHost), "D2H symbol");
+  if (want_orders) ocap = std::max<uint64_t>(ss.resting, 1);  // bounds either side's orders
+  // a side has at most L window levels and its far levels: any larger depth (0xFFFFFFFF: the whole book)
+  // is that
+  depth = (uint32_t)std::min<uint64_t>(depth, (uint64_t)e->bk.L + std::max(ss.nfar[0], ss.nfar[1]));
   if (!depth) {
     if (n_bids) *n_bids = 0;
     if (n_asks) *n_asks = 0;
@@ -1684,7 +1713,7 @@ extern "C" int me_book_dump(me_engine* e, uint32_t symbol, me_book_entry* out, s
   side[0].resize(ss.resting + 1);
   side[1].resize(ss.resting + 1);
   size_t nb = 0, na = 0;
-  rc = me_book_orders(e, symbol, e->bk.L + e->bk.fcap, side[0].data(), side[0].size(), &nb, side[1].data(),
+  rc = me_book_orders(e, symbol, 0xFFFFFFFFu, side[0].data(), side[0].size(), &nb, side[1].data(),
                       side[1].size(), &na, nullptr, nullptr, nullptr, nullptr);
   if (rc) return rc;
   if (out) {
@@ -1763,6 +1792,19 @@ extern "C" int me_stats_read(me_engine* e, uint64_t* handoffs) {
   unsigned long long v[ME_STATS];
   HIP_TRY(hipMemcpy(v, e->bk.stats, sizeof v, hipMemcpyDeviceToHost), "D2H stats");
   if (handoffs) *handoffs = v[ST_HANDOFFS];
+  return ME_OK;
+}
+
+extern "C" int me_far_stats(me_engine* e, uint64_t* moves, uint64_t* collections, uint64_t* arena_used) {
+  if (!e) return ME_E_INVALID;
+  int rc = me_sync(e);
+  if (rc) return rc;
+  unsigned long long v[ME_STATS], ctl[FC_N];
+  HIP_TRY(hipMemcpy(v, e->bk.stats, sizeof v, hipMemcpyDeviceToHost), "D2H stats");
+  HIP_TRY(hipMemcpy(ctl, e->bk.far_ctl, sizeof ctl, hipMemcpyDeviceToHost), "D2H far arena");
+  if (moves) *moves = v[ST_FAR_GROW];
+  if (collections) *collections = v[ST_FAR_GC];
+  if (arena_used) *arena_used = ctl[ctl[FC_HALF] & 1];
   return ME_OK;
 }
 

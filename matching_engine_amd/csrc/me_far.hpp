@@ -11,15 +11,80 @@
 // re-centres the window first (the kernels' recentre routines). Far levels are the rare path: no
 // caching, plain HBM round trips, wave-uniform control flow.
 //
+// The arrays are unbounded (round 5; before, `far_levels` per side was a hard cap whose overflow failed
+// the engine). Each (symbol, side) owns a region of the far arena named by fdir[s][k] = {off, cap}:
+// first its inline region of `far_levels` entries; a rest or re-centre that finds the region full moves
+// the side to a region twice as large taken from the active half of the arena (far_grow: one atomic
+// add on that half's top, a copy, the new fdir entry). Abandoned regions are reclaimed by a copying
+// collection in k_seq_sweep (me_kernels.hip) ahead of a launch group, when the active half's top has
+// passed far_gc_at: every moved side goes to a region of nextpow2(n) entries in the other half, or
+// back inline when it fits, and the halves swap. The sizes make overflow impossible under admission
+// control (me_config.max_resting, M): a far level holds >= 1 resting order, so the sides' peak counts
+// during one group sum to <= M and the regions one group allocates to <= 2 + 4 + ... <= 4 x peak,
+// i.e. <= 4M; a collection leaves <= 2M (nextpow2(n) < 2n); so a half of 6M entries, collected above
+// 2M, never runs out (ERR_FAR_OOM marks that bound broken, an internal error).
+//
 // A kernel context C provides: fchunks() / fnchunks(), fsym() / fgsym() (local symbol, id written
-// into fills), farr(k) / fcount(k) / fset_count(k, n) / fcap(), falloc() / ffree(ch) (its chunk
-// pool; a freed chunk reads all-zero quantities in HBM), femit(e, mask, fill) (scratch fills, lane
-// order), fresting(delta), ferr(bits), floc(seq, slot) (seq-ring write).
+// into fills), fcount(k) / fset_count(k, n), the arena: fdirp(k) (its fdir entry), farena(),
+// fctl() (BookDev::far_ctl), fstats(), fcap0() (inline entries), finline() (inline region end),
+// fhalf() (entries per half), falloc() / ffree(ch) (its chunk pool; a freed chunk reads all-zero
+// quantities in HBM), femit(e, mask, fill) (scratch fills, lane order), fresting(delta), ferr(bits),
+// floc(seq, slot) (seq-ring write).
 #pragma once
 #include "me_layout.hpp"
 #include "me_wave.hpp"
 
 namespace me {
+
+// The region of side k (wave-uniform). Read with vector loads: far_grow rewrites it during a launch.
+template <class C>
+__device__ __forceinline__ FarDir far_dir(const C& c, uint32_t k) {
+  FarDir* p = c.fdirp(k);
+  FarDir d;
+  d.off = rl64(__hip_atomic_load(&p->off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), 0);
+  d.cap = rl32(__hip_atomic_load(&p->cap, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), 0);
+  d.pad = 0;
+  return d;
+}
+template <class C>
+__device__ __forceinline__ gptr<FarLevel> far_arr(const C& c, uint32_t k) {
+  return (gptr<FarLevel>)(c.farena() + far_dir(c, k).off);
+}
+
+// Side k holds n levels and its region is full: move it to a region twice as large (at least twice the
+// inline size) in the active half. Returns false (ERR_FAR_OOM, sticky) only if the bound above broke.
+template <class C>
+__device__ bool far_grow(C& c, uint32_t k, uint32_t n) {
+  const int lane = lane_id();
+  const FarDir d = far_dir(c, k);
+  const unsigned long long c0 = c.fcap0();
+  unsigned long long ncap = 2ull * d.cap;
+  if (ncap < 2ull * c0) ncap = 2ull * c0;
+  unsigned long long* ctl = c.fctl();
+  unsigned long long o = ~0ull;
+  if (lane == 0 && ncap <= 0x80000000ull) {
+    const unsigned long long h = __hip_atomic_load(ctl + FC_HALF, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1ull;
+    const unsigned long long t = atomicAdd(ctl + h, ncap);
+    if (t + ncap <= c.fhalf()) o = c.finline() + h * c.fhalf() + t;
+  }
+  o = rl64(o, 0);
+  if (o == ~0ull) {
+    c.ferr(ERR_FAR_OOM);
+    return false;
+  }
+  const gptr<FarLevel> src = (gptr<FarLevel>)(c.farena() + d.off);
+  const gptr<FarLevel> dst = (gptr<FarLevel>)(c.farena() + o);
+  for (uint32_t i = (uint32_t)lane; i < n; i += 64) dst[i] = src[i];
+  wave_mem_order();
+  if (lane == 0) {
+    FarDir* p = c.fdirp(k);
+    __hip_atomic_store(&p->off, o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&p->cap, (uint32_t)ncap, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    atomicAdd(c.fstats() + ST_FAR_GROW, 1ull);
+  }
+  wave_mem_order();
+  return true;
+}
 
 // Wave-uniform read of entry i (every lane loads the same 32 B).
 __device__ __forceinline__ FarLevel far_get(gptr<FarLevel> a, uint32_t i) {
@@ -90,11 +155,8 @@ __device__ __forceinline__ void far_shift_down(gptr<FarLevel> a, uint32_t pos, u
 template <class C>
 __device__ __forceinline__ bool far_push(C& c, uint32_t k, const FarLevel& e) {
   const uint32_t n = c.fcount(k);
-  if (n >= c.fcap()) {
-    c.ferr(ERR_FAR_OOM);
-    return false;
-  }
-  far_put(c.farr(k), n, e);
+  if (n >= far_dir(c, k).cap && !far_grow(c, k, n)) return false;
+  far_put(far_arr(c, k), n, e);
   c.fset_count(k, n + 1);
   return true;
 }
@@ -108,7 +170,7 @@ __device__ uint32_t far_take(C& c, bool buy, bool market, long long limit, uint3
   const int lane = lane_id();
   const int sl = lane & (ME_C - 1);
   const uint32_t k = buy ? 1u : 0u;
-  const gptr<FarLevel> a = c.farr(k);
+  const gptr<FarLevel> a = far_arr(c, k);
   const gptr<Chunk> chunks = c.fchunks();
   const uint32_t NC = c.fnchunks();
   uint32_t n = c.fcount(k);
@@ -178,7 +240,8 @@ __device__ uint32_t far_take(C& c, bool buy, bool market, long long limit, uint3
 // Rest (seq, qty) at price p on far side k (0: a bid below the window, 1: an ask above it).
 template <class C>
 __device__ bool far_rest(C& c, uint32_t k, long long p, unsigned long long seq, uint32_t qty) {
-  const gptr<FarLevel> a = c.farr(k);
+  const FarDir d = far_dir(c, k);
+  gptr<FarLevel> a = (gptr<FarLevel>)(c.farena() + d.off);
   const gptr<Chunk> chunks = c.fchunks();
   uint32_t n = c.fcount(k);
   wave_mem_order();
@@ -190,9 +253,9 @@ __device__ bool far_rest(C& c, uint32_t k, long long p, unsigned long long seq, 
     exists = e.price == p;
   }
   if (!exists) {
-    if (n >= c.fcap()) {
-      c.ferr(ERR_FAR_OOM);
-      return false;
+    if (n >= d.cap) {  // the region is full: a larger one (same entries, so pos still holds)
+      if (!far_grow(c, k, n)) return false;
+      a = far_arr(c, k);
     }
     far_shift_up(a, pos, n);
     e.price = p;
@@ -246,7 +309,7 @@ template <class C>
 __device__ uint32_t far_cancel(C& c, uint32_t k, long long p, uint32_t ch, uint32_t slot, int q, int qv,
                                uint32_t nxt, uint32_t prv) {
   const int lane = lane_id();
-  const gptr<FarLevel> a = c.farr(k);
+  const gptr<FarLevel> a = far_arr(c, k);
   const gptr<Chunk> chunks = c.fchunks();
   const uint32_t n = c.fcount(k);
   wave_mem_order();

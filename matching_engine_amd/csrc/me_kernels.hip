@@ -329,8 +329,14 @@ struct WaveCtx {
   __device__ __forceinline__ uint32_t fnchunks() const { return bk.nchunks; }
   __device__ __forceinline__ uint32_t fsym() const { return s; }
   __device__ __forceinline__ uint32_t fgsym() const { return gs; }
-  __device__ __forceinline__ uint32_t fcap() const { return bk.fcap; }
-  __device__ __forceinline__ gptr<FarLevel> farr(uint32_t k) const { return (gptr<FarLevel>)far_of(bk, s, k); }
+  __device__ __forceinline__ FarDir* fdirp(uint32_t k) const { return bk.fdir + (size_t)s * 2u + k; }
+  __device__ __forceinline__ FarLevel* farena() const { return bk.far; }
+  __device__ __forceinline__ unsigned long long* fctl() const { return bk.far_ctl; }
+  __device__ __forceinline__ unsigned long long* fstats() const { return bk.stats; }
+  __device__ __forceinline__ uint32_t fcap0() const { return bk.fcap; }
+  __device__ __forceinline__ unsigned long long finline() const { return 2ull * bk.S * bk.fcap; }
+  __device__ __forceinline__ unsigned long long fhalf() const { return bk.far_half; }
+  __device__ __forceinline__ gptr<FarLevel> farr(uint32_t k) const { return far_arr(*this, k); }
   __device__ __forceinline__ uint32_t fcount(uint32_t k) const { return k ? nfar1 : nfar0; }
   __device__ __forceinline__ void fset_count(uint32_t k, uint32_t n) {
     if (k)
@@ -2333,6 +2339,62 @@ struct SeqGroup {
   uint32_t launch;  // match launches enqueued before this group's (all finished when this runs)
 };
 
+// The far arena's copying collection (me_far.hpp), by k_seq_sweep's workgroups when the active half's top
+// has passed far_gc_at: no launch allocates while this kernel runs, so every workgroup reads the same
+// {half, top} and takes the same decision. Each wave takes sides in turn; a side living in the active half
+// moves to the inline region when it fits, else to nextpow2(n) (>= 2 x inline) entries of the other half.
+// The last workgroup to finish (ticket) swaps the halves and empties the old one.
+__device__ void far_collect(const BookDev& bk) {
+  unsigned long long* ctl = bk.far_ctl;
+  const unsigned long long h = __hip_atomic_load(ctl + FC_HALF, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 1ull;
+  const unsigned long long top = __hip_atomic_load(ctl + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (top <= bk.far_gc_at) return;
+  const unsigned long long nh = h ^ 1ull;
+  const int lane = lane_id();
+  const uint32_t nwv = blockDim.x >> 6;
+  const uint32_t wid = blockIdx.x * nwv + (threadIdx.x >> 6), nw = gridDim.x * nwv;
+  const unsigned long long c0 = bk.fcap, inl = 2ull * bk.S * c0;
+  for (uint32_t i = wid; i < 2u * bk.S; i += nw) {
+    const unsigned long long off = rl64(__hip_atomic_load(&bk.fdir[i].off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), 0);
+    if (off < inl) continue;  // inline: nothing to move
+    const uint32_t n = rl32(bk.sym[i >> 1].nfar[i & 1u], 0);
+    unsigned long long o = i * c0, cap = c0;
+    if (n > c0) {
+      cap = 2ull * c0;
+      while (cap < n) cap <<= 1;
+      unsigned long long t = 0;
+      if (lane == 0) t = atomicAdd(ctl + nh, cap);
+      o = inl + nh * bk.far_half + rl64(t, 0);
+      if (rl64(t, 0) + cap > bk.far_half) {  // impossible by the bound (me_far.hpp)
+        if (lane == 0) atomicOr(bk.err, ERR_FAR_OOM);
+        continue;
+      }
+    }
+    const FarLevel* src = bk.far + off;
+    FarLevel* dst = bk.far + o;
+    for (uint32_t j = (uint32_t)lane; j < n; j += 64) dst[j] = src[j];
+    if (lane == 0) {
+      FarDir d;
+      d.off = o;
+      d.cap = (uint32_t)cap;
+      d.pad = 0;
+      bk.fdir[i] = d;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const uint32_t t = atomicAdd((uint32_t*)(ctl + FC_TICKET), 1u);
+    if (t == gridDim.x - 1u) {  // every workgroup has moved its sides
+      ctl[h] = 0;
+      ctl[FC_HALF] = nh;
+      ctl[FC_TICKET] = 0;
+      bk.stats[ST_FAR_GC] += 1ull;
+      __threadfence();
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void k_seq_sweep(BookDev bk, SeqGroup sg) {
   const SeqState st = bk.sq[sg.in];
   const unsigned long long gmin = sg.seq[0][0];
@@ -2374,6 +2436,7 @@ __global__ __launch_bounds__(256) void k_seq_sweep(BookDev bk, SeqGroup sg) {
       bk.pub[1] = ((unsigned long long)sg.launch << 32) | (h < 0xFFFFFFFFull ? h : 0xFFFFFFFFull);
     }
   }
+  far_collect(bk);
   if (!need) return;
   const uint32_t top = min(*bk.chunk_top, bk.nchunks);
   const size_t slots = (size_t)top * ME_C;

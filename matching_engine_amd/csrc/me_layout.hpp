@@ -7,10 +7,12 @@
 //   levels [S][L]   16 B {total, head chunk, tail chunk}: the fixed-depth WINDOW of price levels
 //                   [base, base + L). Bids and asks share it: after every order best_bid < best_ask,
 //                   so a level's side is implied by its position.
-//   far    [S][2][F] 32 B {price, total, head, tail, tend}: levels OUTSIDE the window. Side 0 holds
-//                   bids below the window (ascending price, best last), side 1 asks above it
-//                   (descending price, best last). Invariant: no bid rests above the window and no
-//                   ask below it; a rest that would break this re-centres the window first.
+//   far    arena    32 B {price, total, head, tail, tend}: levels OUTSIDE the window, one sorted array
+//                   per (symbol, side) located by fdir [S][2]. Side 0 holds bids below the window
+//                   (ascending price, best last), side 1 asks above it (descending price, best last).
+//                   Invariant: no bid rests above the window and no ask below it; a rest that would
+//                   break this re-centres the window first. Unbounded: a side outgrowing its region
+//                   moves to a larger one (me_far.hpp).
 //   occ    [S][L/64] occupancy bitmap of the window (bit set <=> total > 0).
 //   sym    [S]      64 B per-symbol scalars (window base, best bid/ask level, chunk free list,
 //                   far-level counts).
@@ -58,7 +60,7 @@ enum : uint32_t {
   ERR_CHUNK_OOM = 1u,
   ERR_SCRATCH_OOM = 2u,
   ERR_INCONSISTENT = 4u,
-  ERR_FAR_OOM = 8u,      // a symbol's far-level array is full (me_config.far_levels)
+  ERR_FAR_OOM = 8u,      // the far arena is exhausted (sized so admission control rules it out: internal)
   ERR_OLD_OOM = 16u,     // the old-order table overflowed (sized from max_resting)
   ERR_SEQ_ORDER = 32u,   // seqs not ascending across the stream (API precondition, seq_follows)
   ERR_SEQ_SPAN = 64u,    // one launch group spans >= the seq ring (raise me_config.seq_ring)
@@ -122,6 +124,19 @@ struct alignas(32) FarLevel {
   uint32_t pad;
 };
 static_assert(sizeof(FarLevel) == 32, "FarLevel is 32 B");
+
+// Where the far levels of one (symbol, side) live (BookDev::fdir, me_far.hpp): entries
+// [off, off + cap) of the far arena. Every side starts in its own inline region of `far_levels`
+// entries; a side that outgrows it moves into a region twice as large in the active half of the arena
+// (and again, doubling, as it grows), and k_seq_sweep's collection pass brings every moved side back to
+// a compact region of the other half — or to its inline region when it fits again.
+struct alignas(16) FarDir {
+  unsigned long long off;
+  uint32_t cap;
+  uint32_t pad;
+};
+// BookDev::far_ctl words: the allocation tops of the two halves, the active half, the collection's ticket
+enum : uint32_t { FC_TOP0 = 0, FC_TOP1 = 1, FC_HALF = 2, FC_TICKET = 3, FC_N = 4 };
 
 // Old-order table entry: the claim word {epoch, slot} is CAS'd by k_seq_sweep; an entry is empty
 // unless its epoch is the current one (no clearing pass).
@@ -270,7 +285,8 @@ struct HotLaunch {
 // symbol state back); k_seq_sweep publishes it to the host for admission control (me_engine.cpp).
 // ST_LAUNCH: the match launches enqueued before the current group (k_seq_sweep), for the continuation's
 // hand-off publication.
-enum : uint32_t { ST_HANDOFFS = 0, ST_RESTING = 1, ST_LAUNCH = 2, ME_STATS = 8 };
+// ST_FAR_GROW / ST_FAR_GC: far sides moved to a larger arena region / collection passes (me_far_stats).
+enum : uint32_t { ST_HANDOFFS = 0, ST_RESTING = 1, ST_LAUNCH = 2, ST_FAR_GROW = 3, ST_FAR_GC = 4, ME_STATS = 8 };
 
 struct BookDev {
   Level* levels;
@@ -284,7 +300,11 @@ struct BookDev {
   uint32_t* err;
   const uint32_t* gsym;  // [S] id written into me_fill.symbol
   unsigned long long* dbg;  // [S][8] phase cycles, diagnostic (-DME_STAMPS) builds only
-  FarLevel* far;          // [S][2][fcap]
+  FarLevel* far;          // far arena: [2S][fcap] inline regions, then two halves of far_half entries
+  FarDir* fdir;           // [S][2] each side's region of the arena (me_far.hpp)
+  unsigned long long* far_ctl;  // [FC_N] half tops, active half, collection ticket
+  unsigned long long far_half;  // entries per half (6 x max_resting + slack: the bound of me_far.hpp)
+  unsigned long long far_gc_at; // a half's top above this at k_seq_sweep: collect (2 x max_resting)
   OldEnt* old;            // [old_mask + 1]
   SeqState* sq;           // [2]
   uint32_t* hcount;       // hand-offs of the current match launch (zeroed by k_seq_sweep)
@@ -294,8 +314,8 @@ struct BookDev {
                               // hand-offs} (k_seq_sweep), or null
   unsigned long long ring_mask;
   unsigned long long old_mask;
-  uint32_t fcap;
-  uint32_t sq_idx;        // state the match launches read (k_seq_sweep wrote it)
+  uint32_t fcap;          // inline far levels per (symbol, side) (me_config.far_levels)
+  uint32_t sq_idx;       // state the match launches read (k_seq_sweep wrote it)
   uint32_t nchunks;
   uint32_t S;
   uint32_t L;
@@ -306,9 +326,10 @@ struct BookDev {
   uint32_t* agg_ctr;      // AggDev::ctr (zeroed by k_seq_sweep with hcount), or null
 };
 
-// Far array of (symbol s, side k): k = 0 bids below the window, 1 asks above it.
-__host__ __device__ __forceinline__ FarLevel* far_of(const BookDev& bk, uint32_t s, uint32_t k) {
-  return bk.far + ((size_t)s * 2u + k) * bk.fcap;
+// Far levels of (symbol s, side k) (k = 0 bids below the window, 1 asks above it): device code, read
+// between launches (the snapshot kernel); the matching kernels go through me_far.hpp's far_dir.
+__device__ __forceinline__ FarLevel* far_of(const BookDev& bk, uint32_t s, uint32_t k) {
+  return bk.far + bk.fdir[(size_t)s * 2u + k].off;
 }
 // Hash of a seq into the old-order table.
 __host__ __device__ __forceinline__ unsigned long long old_hash(unsigned long long q) {

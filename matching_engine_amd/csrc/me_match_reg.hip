@@ -226,10 +226,16 @@ struct RegCtx {
   __device__ __forceinline__ uint32_t fnchunks() const { return nchunks; }
   __device__ __forceinline__ uint32_t fsym() const { return s; }
   __device__ __forceinline__ uint32_t fgsym() const { return gs; }
-  __device__ __forceinline__ uint32_t fcap() const { return ldsu(G->bk.fcap); }
-  __device__ __forceinline__ gptr<FarLevel> farr(uint32_t k) const {
-    return ldsg(G->bk.far) + ((size_t)s * 2u + k) * (size_t)fcap();
+  __device__ __forceinline__ FarDir* fdirp(uint32_t k) const {
+    return (FarDir*)(ldsg(G->bk.fdir) + (size_t)s * 2u + k);
   }
+  __device__ __forceinline__ FarLevel* farena() const { return (FarLevel*)ldsg(G->bk.far); }
+  __device__ __forceinline__ unsigned long long* fctl() const { return (unsigned long long*)ldsg(G->bk.far_ctl); }
+  __device__ __forceinline__ unsigned long long* fstats() const { return (unsigned long long*)ldsg(G->bk.stats); }
+  __device__ __forceinline__ uint32_t fcap0() const { return ldsu(G->bk.fcap); }
+  __device__ __forceinline__ unsigned long long finline() const { return 2ull * ldsu(G->bk.S) * fcap0(); }
+  __device__ __forceinline__ unsigned long long fhalf() const { return ldsu(G->bk.far_half); }
+  __device__ __forceinline__ gptr<FarLevel> farr(uint32_t k) const { return far_arr(*this, k); }
   __device__ __forceinline__ uint32_t fcount(uint32_t k) const { return ldsu(M->nfar[k]); }
   __device__ __forceinline__ void fset_count(uint32_t k, uint32_t n) {
     if (lane_id() == 0) __hip_atomic_store(&M->nfar[k], n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);

@@ -593,11 +593,7 @@ static int backend_book(me_service* s, uint32_t sid, uint32_t depth, me_book_ent
                         size_t* n_bids, me_book_entry* asks, size_t asks_cap, size_t* n_asks, me_level* bl,
                         me_level* al, size_t* nbl, size_t* nal) {
   if (s->eng) {
-    if (!depth) {  // the whole book: every window level plus the far arrays
-      me_config c{};
-      me_get_config(s->eng, &c);
-      depth = c.levels + c.far_levels;
-    }
+    if (!depth) depth = 0xFFFFFFFFu;  // the whole book: every window level plus the far levels
     return me_book_orders(s->eng, sid, depth, bids, bids_cap, n_bids, asks, asks_cap, n_asks, bl, al, nbl, nal);
   }
   return s->m.book(s->m.ctx, sid, depth, bids, bids_cap, n_bids, asks, asks_cap, n_asks, bl, al, nbl, nal);

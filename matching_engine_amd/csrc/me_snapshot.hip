@@ -60,8 +60,9 @@ __global__ __launch_bounds__(SNAP_T) void k_book_snapshot(BookDev bk, SnapReq rq
   const int L = (int)bk.L;
   const SymState st = bk.sym[s];
   const Level* lv = bk.levels + (size_t)s * L;
-  const FarLevel* far = far_of(bk, s, side);
-  const uint32_t nfar = min(st.nfar[side], bk.fcap);
+  const FarDir fd = bk.fdir[(size_t)s * 2u + side];
+  const FarLevel* far = bk.far + fd.off;
+  const uint32_t nfar = min(st.nfar[side], fd.cap);
   const size_t reg = (size_t)q * 2 + side;
   me_level* lv_out = rq.lv + reg * rq.depth;
   me_book_entry* ord_out = rq.ord ? rq.ord + reg * rq.ocap : nullptr;

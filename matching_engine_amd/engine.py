@@ -198,7 +198,7 @@ class Engine:
 
     def collect(self, ticket: int, copy: bool = True):
         """(results[n], fills[k]) of a ticket. copy=False returns views of the slot's pinned memory,
-        valid until the slot is reused (ticket + host_slots)."""
+        valid until the next collect (me_collect's contract)."""
         fp, rp = C.c_void_p(), C.c_void_p()
         nf, nr = C.c_size_t(0), C.c_size_t(0)
         _check(self.lib, self.h,
@@ -315,6 +315,12 @@ class Engine:
         h = C.c_uint64(0)
         _check(self.lib, self.h, self.lib.me_stats_read(self.h, C.byref(h)))
         return {"handoffs": h.value}
+
+    def far_stats(self) -> dict:
+        """The far arena (me_far_stats): sides moved to a larger region, collections, entries in use."""
+        m, g, u = C.c_uint64(0), C.c_uint64(0), C.c_uint64(0)
+        _check(self.lib, self.h, self.lib.me_far_stats(self.h, C.byref(m), C.byref(g), C.byref(u)))
+        return {"moves": m.value, "collections": g.value, "arena_used": u.value}
 
     def paths(self) -> dict:
         """The matching paths running now (me_paths_read): grouped launches / hot symbols through the

@@ -18,12 +18,15 @@ class ShardPlan:
 
     def split(self, b: Batch):
         """-> list over shards of (batch with local ids, positions in the global batch)."""
-        out = []
         sym = b.symbol
         ok = sym < self.num_symbols
         owner = np.where(ok, self.shard[np.minimum(sym, self.num_symbols - 1)], 0)
+        # one stable sort by owner (batch order kept inside each shard), then a slice per shard
+        order = np.argsort(owner, kind="stable")
+        ends = np.cumsum(np.bincount(owner, minlength=self.shards))
+        out = []
         for r in range(self.shards):
-            pos = np.nonzero(owner == r)[0]
+            pos = order[(ends[r - 1] if r else 0):ends[r]]
             lb = b.take(pos)
             s = lb.symbol
             inr = s < self.num_symbols
@@ -32,4 +35,3 @@ class ShardPlan:
                                  np.uint32(0xFFFFFFFF)).astype(np.uint32)
             out.append((lb, pos))
         return out
-

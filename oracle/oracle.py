@@ -51,6 +51,8 @@ def load():
                                            C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int64),
                                            C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int64),
                                            C.POINTER(C.c_int32)]
+        lib.orc_run_sharded.restype = C.c_double
+        lib.orc_run_sharded.argtypes = [C.c_uint32, C.c_uint32, P, P, P, P, P, P, P, P, P]
         lib.ref_submit_run.restype = C.c_longlong
         lib.ref_submit_run.argtypes = [C.c_char_p, C.c_char_p, C.c_char_p, SZ, P, P, P, P, P, C.c_int, P]
         _lib = lib
@@ -110,6 +112,34 @@ class OracleBook:
         nb, na = C.c_size_t(0), C.c_size_t(0)
         self.lib.orc_snapshot(self.h, symbol, _p(bids), _p(asks), depth, C.byref(nb), C.byref(na))
         return bids[: nb.value], asks[: na.value]
+
+
+def run_sharded(books, parts, nwarm=0):
+    """The native CPU baseline (orc_run_sharded): books[r] (OracleBook) runs the batches parts[r] on its
+    own std::thread, no Python inside the timed region; each thread's first nwarm batches run untimed
+    before the clock starts. Returns (wall seconds of the rest, their fills)."""
+    T = len(books)
+    lib = load()
+    cols = {f: [] for f in ("seq", "price_q4", "qty", "symbol", "kind")}
+    nb = np.array([len(p) for p in parts], dtype=np.uint32)
+    offs = []
+    for p in parts:
+        assert p, "every thread needs its list of batches (empty batches allowed)"
+        o = np.zeros(len(p) + 1, dtype=np.uint64)
+        o[1:] = np.cumsum([len(b) for b in p])
+        offs.append(o)
+        for f in cols:  # (+ one pad element: an empty part still has a valid pointer)
+            a = np.concatenate([getattr(b, f) for b in p])
+            cols[f].append(np.ascontiguousarray(np.concatenate([a, a[:0].copy().resize(1) or np.zeros(1, a.dtype)])))
+
+    def ptrs(arrs):
+        return (C.c_void_p * T)(*[a.ctypes.data for a in arrs])
+
+    hb = (C.c_void_p * T)(*[b.h for b in books])
+    fills = np.zeros(T, dtype=np.uint64)
+    w = lib.orc_run_sharded(T, nwarm, hb, nb.ctypes.data, ptrs(offs), ptrs(cols["seq"]), ptrs(cols["price_q4"]),
+                            ptrs(cols["qty"]), ptrs(cols["symbol"]), ptrs(cols["kind"]), fills.ctypes.data)
+    return float(w), int(fills.sum())
 
 
 class OracleService:

@@ -21,10 +21,14 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <deque>
 #include <functional>
 #include <map>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -107,12 +111,10 @@ static int64_t match_side(orc* o, Map& side, uint32_t sym, bool market, int64_t 
   return want - rem;
 }
 
-// One batch in seq order. res_out[n]; fills appended in taker order.
-extern "C" int orc_submit(orc* o, size_t n, const uint64_t* seq, const int64_t* px, const int32_t* qty,
-                          const uint32_t* sym, const uint8_t* kind, const uint32_t* gsym_map, me_order_result* res_out,
-                          me_fill* fills_out, size_t fills_cap, size_t* nfills) {
-  std::vector<me_fill> tape;
-  tape.reserve(n * 2);
+// One batch in seq order into res_out[n]; its fills appended to `tape` in taker order.
+static void submit_core(orc* o, size_t n, const uint64_t* seq, const int64_t* px, const int32_t* qty,
+                        const uint32_t* sym, const uint8_t* kind, const uint32_t* gsym_map, me_order_result* res_out,
+                        std::vector<me_fill>& tape) {
   for (size_t i = 0; i < n; ++i) {
     me_order_result r{};
     r.tape_offset = (uint32_t)tape.size();
@@ -198,6 +200,15 @@ extern "C" int orc_submit(orc* o, size_t n, const uint64_t* seq, const int64_t* 
     }
     res_out[i] = r;
   }
+}
+
+// One batch in seq order. res_out[n]; fills appended in taker order.
+extern "C" int orc_submit(orc* o, size_t n, const uint64_t* seq, const int64_t* px, const int32_t* qty,
+                          const uint32_t* sym, const uint8_t* kind, const uint32_t* gsym_map, me_order_result* res_out,
+                          me_fill* fills_out, size_t fills_cap, size_t* nfills) {
+  std::vector<me_fill> tape;
+  tape.reserve(n * 2);
+  submit_core(o, n, seq, px, qty, sym, kind, gsym_map, res_out, tape);
   if (nfills) *nfills = tape.size();
   if (fills_out) {
     if (tape.size() > fills_cap) return -3;
@@ -346,4 +357,59 @@ extern "C" int orc_service_submit(orc_service* svc, const char* symbol, int32_t 
   *row_remaining = quantity;
   *row_side = side;
   return 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// The CPU baseline at the host's cores (bench.py cpu_baseline): T books, one per
+// std::thread, each over its own pre-split batches (symbols hash-sharded across threads as across GPUs:
+// independent books, no shared state), with no Python in the timed loop. Thread r runs book books[r]
+// through nb[r] batches: records [boff[r][j], boff[r][j + 1]) of its SoA arrays, results into a reused
+// buffer, fills into a reused tape (cleared per batch). Every thread allocates and touches its buffers
+// first; the clock starts when all are ready (a spin barrier) and stops when the last one finishes.
+// The first nwarm batches of every thread run before the barrier, untimed (the allocator's arenas warm up:
+// first-touch page faults of many threads serialise on the process's memory map). Returns the wall
+// seconds of the rest; fills_out (optional) receives each thread's fill count over the timed batches.
+extern "C" double orc_run_sharded(uint32_t T, uint32_t nwarm, orc* const* books, const uint32_t* nb,
+                                  const uint64_t* const* boff,
+                                  const uint64_t* const* seq, const int64_t* const* px, const int32_t* const* qty,
+                                  const uint32_t* const* sym, const uint8_t* const* kind, uint64_t* fills_out) {
+  std::atomic<uint32_t> ready{0};
+  std::atomic<bool> go{false};
+  std::vector<double> end(T, 0.0);
+  std::chrono::steady_clock::time_point t0;
+  std::vector<std::thread> th;
+  th.reserve(T);
+  for (uint32_t r = 0; r < T; ++r) {
+    th.emplace_back([&, r]() {
+      size_t mx = 0;
+      for (uint32_t j = 0; j < nb[r]; ++j) mx = std::max<size_t>(mx, boff[r][j + 1] - boff[r][j]);
+      std::vector<me_order_result> res(mx + 1);
+      std::vector<me_fill> tape;
+      tape.reserve(2 * mx + 16);
+      uint64_t nf = 0;
+      auto run = [&](uint32_t j) {
+        const uint64_t a = boff[r][j], n = boff[r][j + 1] - a;
+        tape.clear();
+        submit_core(books[r], n, seq[r] + a, px[r] + a, qty[r] + a, sym[r] + a, kind[r] + a, nullptr, res.data(),
+                    tape);
+      };
+      const uint32_t w0 = std::min(nwarm, nb[r]);
+      for (uint32_t j = 0; j < w0; ++j) run(j);
+      ready.fetch_add(1);
+      while (!go.load(std::memory_order_acquire)) std::this_thread::yield();
+      for (uint32_t j = w0; j < nb[r]; ++j) {
+        run(j);
+        nf += tape.size();
+      }
+      end[r] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      if (fills_out) fills_out[r] = nf;
+    });
+  }
+  while (ready.load() < T) std::this_thread::yield();
+  t0 = std::chrono::steady_clock::now();
+  go.store(true, std::memory_order_release);
+  for (auto& t : th) t.join();
+  double w = 0;
+  for (double x : end) w = std::max(w, x);
+  return w;
 }

@@ -73,6 +73,16 @@ def test_fuzz_agg_case(me, seed, monkeypatch):
     _run_case(me, seed, True)
 
 
+def test_fuzz_agg_seed55_default_far_levels(me, monkeypatch):
+    """The soak draw that once failed the engine (profiles/r4/soak/fuzz80.log: agg seed 55, one symbol,
+    180k records, 5 % far LIMITs up to 64 windows out): more distinct far levels per side than the inline
+    region holds. At the DEFAULT far_levels the sides move into the far arena and every batch, the
+    final book and the resting counts equal the oracle's (no sticky failure)."""
+    monkeypatch.setenv("ME_REG_AGG", "1")
+    st = _run_case(me, 55, True)
+    assert st["moves"] > 0, st
+
+
 def _run_case(me, seed, agg):
     from oracle.oracle import OracleBook
 
@@ -81,19 +91,8 @@ def _run_case(me, seed, agg):
     ctx = (f"{'agg ' if agg else ''}seed {seed}: L={sc.levels} S={sc.num_symbols} batch={sc.batch} G={group} path={path} "
            f"lag={lag} cancel={sc.cancel_pct} far={sc.far_pct} drift={sc.drift_step}/{sc.drift_every}")
     ob = OracleBook(sc.num_symbols)
-    # far-level capacity (me_config.far_levels, a documented per-symbol-and-side bound): the busiest
-    # symbol's records outside its initial window bound its far levels — a 180k-record single-symbol
-    # stream with 5 % far prices (up to 64 windows out) rests more distinct far levels than the default
-    # 1,024 and the engine rightly refuses it (agg seed 55 of a soak, profiles/r4/soak)
-    far = np.zeros(sc.num_symbols + 1, dtype=np.int64)
-    for b in batches:
-        sym = np.minimum(b.symbol, sc.num_symbols)
-        off = b.price_q4 - np.asarray(base, dtype=np.int64)[np.minimum(sym, sc.num_symbols - 1)]
-        np.add.at(far, sym, ((off < 0) | (off >= sc.levels)).astype(np.int64))  # outside the initial window
-    far_levels = max(1024, min(int(far[:-1].max()) + 64, (1 << 21) // sc.num_symbols))
     with me.Engine(sc.num_symbols, sc.levels, base, max_batch=sc.batch, max_resting=total + 1024,
-                   max_chunks=total + 1024 + 2 * sc.num_symbols, seq_ring=1 << 20, batches_per_launch=group,
-                   far_levels=far_levels) as eng:
+                   max_chunks=total + 1024 + 2 * sc.num_symbols, seq_ring=1 << 20, batches_per_launch=group) as eng:
         if agg:
             assert eng.paths()["grouped_agg"], ctx
         outs = [None] * len(batches)
@@ -127,3 +126,4 @@ def _run_case(me, seed, agg):
             assert_fills_equal(outs[k][1], fo, f"{ctx} batch {k}")
         assert_books_equal(eng, ob, range(sc.num_symbols), ctx)
         assert eng.resting_count() == ob.resting() == eng.admission()["resting"], ctx
+        return eng.far_stats()

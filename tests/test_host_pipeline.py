@@ -180,3 +180,28 @@ def test_host_and_device_batches_interleave(me, orc):
                     eng.fetch_outputs(len(b))
             assert_results_equal(r, ro, f"interleave batch {k}")
             assert_fills_equal(f, fo, f"interleave batch {k}")
+
+
+def test_collected_outputs_survive_the_next_submit(me, orc):
+    """me_collect's outputs (pinned views, copy=False) stay valid until the next me_collect: collect A,
+    submit and match C (the LIFO free list would hand C A's slot), then read A — still A's results and
+    tape. (the cluster's world-1 direct path hands exactly these views to its caller.)"""
+    sc, base, batches = _stream(me, 2, 6, num_symbols=64, batch=2048)
+    ob = orc.OracleBook(sc.num_symbols)
+    exp = [ob.submit(b) for b in batches]
+    with _engine(me, sc, base, batches, batches_per_launch=2) as eng:
+        t = [eng.submit_host(b) for b in batches[:2]]
+        views = eng.collect(t[0], copy=False)
+        t.append(eng.submit_host(batches[2]))
+        eng.sync()  # C matched and its outputs written
+        assert_results_equal(views[0], exp[0][0], "A after C's submit")
+        assert_fills_equal(views[1], exp[0][1], "A after C's submit")
+        for k in (1, 2):
+            r, f = eng.collect(t[k])
+            assert_results_equal(r, exp[k][0], f"batch {k}")
+            assert_fills_equal(f, exp[k][1], f"batch {k}")
+        # a synchronous caller alternates two warm slots; any lag keeps working
+        for k in range(3, 6):
+            r, f = eng.collect(eng.submit_host(batches[k]))
+            assert_results_equal(r, exp[k][0], f"batch {k}")
+            assert_fills_equal(f, exp[k][1], f"batch {k}")
