@@ -125,6 +125,12 @@ int me_cluster_stats(const me_cluster* c, uint64_t* slices, uint64_t* bytes);
  * waiting for rank 0's engine slot inputs. Writes min(n, 10) values, returns 10. */
 int me_cluster_phases(const me_cluster* c, double* seconds, size_t n);
 int me_cluster_last_error(const me_cluster* c, char* buf, size_t cap);
+/* Rank 0's host work per slice at `world` shards, without GPUs or a transport: the exact split and merge
+ * code of me_cluster_submit / me_cluster_collect over `slice` (global symbol ids < num_symbols), with
+ * synthetic shard outputs of fills_per_order fills per record on average, `iters` times. seconds[0] = the
+ * owner-count pass, [1] = the pack, [2] = the merge, per slice; [3] = the merged tape's fills. */
+int me_cluster_host_probe(uint32_t world, uint32_t num_symbols, const me_order_soa* slice, size_t n,
+                          double fills_per_order, uint32_t iters, double* seconds);
 
 #ifdef __cplusplus
 }

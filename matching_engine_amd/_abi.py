@@ -361,4 +361,5 @@ PROTOTYPES.update({
     "me_cluster_stats": (C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "me_cluster_phases": (C.c_int, [_P, C.POINTER(C.c_double), _SZ]),
     "me_cluster_last_error": (C.c_int, [_P, C.c_char_p, _SZ]),
+    "me_cluster_host_probe": (C.c_int, [C.c_uint32, C.c_uint32, _P, _SZ, C.c_double, C.c_uint32, _P]),
 })

@@ -25,6 +25,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cmath>
 #include <chrono>
 #include <deque>
 #include <memory>
@@ -494,6 +495,142 @@ struct PackView {
         kind((uint8_t*)(p + 24 * n)) {}
 };
 
+// Rank 0's split of a slice by owner, stable (each part keeps slice order = seq order), in two passes:
+// split_count — per-chunk counts of records and of NEW LIMITs per rank (counted in each thread's own
+// arrays, published once: the threads' rows share cache lines — at world 1 all sixteen in one line: 66 ms
+// per 1M-record slice of false sharing, profiles/r4/r4e); split_pack — every chunk packs its records at its
+// offsets into the parts' views and records where each came from. An unknown global id goes to rank 0 out
+// of range (BAD_SYMBOL there).
+struct SplitCounts {
+  size_t T = 0;
+  std::vector<uint64_t> cnt, lim;  // [T][W]
+  std::vector<uint64_t> per_rank, lim_rank;  // [W]
+};
+void split_count(const uint32_t* owner, uint32_t W, uint32_t S, const me_order_soa* b, size_t n, SplitCounts& sc) {
+  sc.T = par_threads(n, kGrain);
+  sc.cnt.assign(sc.T * W, 0);
+  sc.lim.assign(sc.T * W, 0);
+  par_chunks(n, kGrain, [&](size_t i, size_t lo, size_t hi) {
+    std::vector<uint64_t> ci(W, 0), li(W, 0);
+    for (size_t k = lo; k < hi; ++k) {
+      const uint32_t s = b->symbol[k];
+      const uint32_t r = s < S ? owner[s] : 0;
+      ci[r]++;
+      li[r] += (b->kind[k] & 0x0Cu) == 0u;  // NEW LIMIT: may rest
+    }
+    std::copy(ci.begin(), ci.end(), sc.cnt.begin() + i * W);
+    std::copy(li.begin(), li.end(), sc.lim.begin() + i * W);
+  });
+  sc.per_rank.assign(W, 0);
+  sc.lim_rank.assign(W, 0);
+  for (uint32_t r = 0; r < W; ++r)
+    for (size_t i = 0; i < sc.T; ++i) {
+      sc.per_rank[r] += sc.cnt[i * W + r];
+      sc.lim_rank[r] += sc.lim[i * W + r];
+    }
+}
+void split_pack(const uint32_t* owner, const uint32_t* local, uint32_t W, uint32_t S, const me_order_soa* b, size_t n,
+                const SplitCounts& sc, std::vector<PackView>& dst, Ticket& tk) {
+  tk.pos_off.assign(W + 1, 0);
+  for (uint32_t r = 0; r < W; ++r) tk.pos_off[r + 1] = tk.pos_off[r] + sc.per_rank[r];
+  tk.pos.resize(n);
+  // chunk i's first record of rank r lands at base[i][r] within the part
+  std::vector<uint64_t> base(sc.T * W, 0);
+  for (uint32_t r = 0; r < W; ++r) {
+    uint64_t x = 0;
+    for (size_t i = 0; i < sc.T; ++i) {
+      base[i * W + r] = x;
+      x += sc.cnt[i * W + r];
+    }
+  }
+  par_chunks(n, kGrain, [&](size_t i, size_t lo, size_t hi) {
+    std::vector<uint64_t> at(base.begin() + i * W, base.begin() + (i + 1) * W);
+    for (size_t k = lo; k < hi; ++k) {
+      const uint32_t s = b->symbol[k];
+      const uint32_t r = s < S ? owner[s] : 0;
+      const uint64_t j = at[r]++;
+      PackView& v = dst[r];
+      v.seq[j] = b->seq[k];
+      v.px[j] = b->price_q4[k];
+      v.qty[j] = b->qty[k];
+      v.sym[j] = s < S ? local[s] : 0xFFFFFFFFu;
+      v.kind[j] = b->kind[k];
+      tk.pos[tk.pos_off[r] + j] = (uint32_t)k;
+    }
+  });
+}
+
+// Rank 0's merge of the shards' outputs: results back to slice order, the merged tape in slice order (= taker
+// seq order: every taker's fills are consecutive on its one shard, at its result's tape offset there). tr[r] /
+// tf[r] / nf[r]: shard r's results (its part's order), tape and fill count. Every shard's results must account
+// for its tape exactly (fill counts summing to its fills, each run inside the tape) — the copy trusts them;
+// false (bad = the shard) otherwise.
+bool merge_parts(uint32_t W, const Ticket& tk, const std::vector<const me_order_result*>& tr,
+                 const std::vector<const me_fill*>& tf, const std::vector<size_t>& nf, std::vector<me_order_result>& res_v,
+                 std::vector<me_fill>& tape_v, uint32_t* bad) {
+  for (uint32_t r = 0; r < W; ++r) {
+    const size_t np = tk.pos_off[r + 1] - tk.pos_off[r], nfr = nf[r];
+    const me_order_result* rr = tr[r];
+    std::atomic<uint64_t> sum{0};
+    std::atomic<bool> out{false};
+    par_chunks(np, kGrain, [&](size_t, size_t a, size_t b) {
+      uint64_t x = 0;
+      bool o = false;
+      for (size_t k = a; k < b; ++k) {
+        x += rr[k].fill_count;
+        o |= rr[k].fill_count && (uint64_t)rr[k].tape_offset + rr[k].fill_count > nfr;
+      }
+      sum += x;
+      if (o) out = true;
+    });
+    if (out || sum != nfr) {
+      if (bad) *bad = r;
+      return false;
+    }
+  }
+  res_v.resize(tk.n);
+  me_order_result* res = res_v.data();
+  for (uint32_t r = 0; r < W; ++r) {
+    const size_t lo = tk.pos_off[r], np = tk.pos_off[r + 1] - lo;
+    const uint32_t* pos = tk.pos.data() + lo;
+    const me_order_result* rr = tr[r];
+    par_chunks(np, kGrain, [&](size_t, size_t a, size_t b) {
+      for (size_t k = a; k < b; ++k) res[pos[k]] = rr[k];
+    });
+  }
+  // merged tape offsets: exclusive scan of the fill counts in slice order (chunk sums, then chunk scans)
+  const size_t T = par_threads(tk.n, kGrain);
+  std::vector<uint64_t> csum(T + 1, 0);
+  par_chunks(tk.n, kGrain, [&](size_t i, size_t a, size_t b) {
+    uint64_t x = 0;
+    for (size_t k = a; k < b; ++k) x += res[k].fill_count;
+    csum[i + 1] = x;
+  });
+  for (size_t i = 0; i < T; ++i) csum[i + 1] += csum[i];
+  tape_v.resize(csum[T]);
+  me_fill* tape = tape_v.data();
+  par_chunks(tk.n, kGrain, [&](size_t i, size_t a, size_t b) {
+    uint64_t o = csum[i];
+    for (size_t k = a; k < b; ++k) {
+      const uint32_t fc = res[k].fill_count;
+      res[k].tape_offset = (uint32_t)o;
+      o += fc;
+    }
+  });
+  for (uint32_t r = 0; r < W; ++r) {  // each taker's fills from its shard's tape
+    const size_t lo = tk.pos_off[r], np = tk.pos_off[r + 1] - lo;
+    const uint32_t* pos = tk.pos.data() + lo;
+    const me_order_result* rr = tr[r];
+    const me_fill* fr = tf[r];
+    par_chunks(np, kGrain, [&](size_t, size_t a, size_t b) {
+      for (size_t k = a; k < b; ++k)
+        if (rr[k].fill_count)
+          memcpy(tape + res[pos[k]].tape_offset, fr + rr[k].tape_offset, rr[k].fill_count * sizeof(me_fill));
+    });
+  }
+  return true;
+}
+
 }  // namespace
 
 struct me_cluster {
@@ -880,84 +1017,28 @@ static int run_collect(me_cluster* c, const int64_t* hdr) {
     c->out_nf = p.nf;
     c->out_res = r0;
   } else {
-    // merge: results back to slice order; the merged tape in slice order (= taker seq order: every taker's
-    // fills are consecutive on its one shard, at its result's tape offset there)
     std::vector<const me_fill*> tf(W);
     std::vector<const me_order_result*> tr(W);
+    std::vector<size_t> nfs(W);
     size_t off = 0;
     for (uint32_t r = 0; r < W; ++r) {
-      const size_t nfr = (size_t)szs[2 * r];
+      nfs[r] = (size_t)szs[2 * r];
       if (r == 0 && direct) {
         tf[0] = f0;
         tr[0] = r0;
       } else {
         tf[r] = (const me_fill*)(c->h_gather.data() + off);
-        tr[r] = (const me_order_result*)(c->h_gather.data() + off + nfr * sizeof(me_fill));
+        tr[r] = (const me_order_result*)(c->h_gather.data() + off + nfs[r] * sizeof(me_fill));
         off += bytes[r];
       }
     }
-    // every shard's results must account for its tape exactly (fill counts summing to its fills, each run
-    // inside the tape): the copy below trusts them
-    for (uint32_t r = 0; r < W; ++r) {
-      const size_t np = tk.pos_off[r + 1] - tk.pos_off[r], nfr = (size_t)szs[2 * r];
-      const me_order_result* rr = tr[r];
-      std::atomic<uint64_t> sum{0};
-      std::atomic<bool> bad{false};
-      par_chunks(np, kGrain, [&](size_t, size_t a, size_t b) {
-        uint64_t x = 0;
-        bool out = false;
-        for (size_t k = a; k < b; ++k) {
-          x += rr[k].fill_count;
-          out |= rr[k].fill_count && (uint64_t)rr[k].tape_offset + rr[k].fill_count > nfr;
-        }
-        sum += x;
-        if (out) bad = true;
-      });
-      if (bad || sum != nfr) {
-        c->failed = true;
-        return c->fail(ME_E_STATE, "shard " + std::to_string(r) + "'s results do not account for its tape");
-      }
+    uint32_t bad = 0;
+    if (!merge_parts(W, tk, tr, tf, nfs, c->res, c->tape, &bad)) {
+      c->failed = true;
+      return c->fail(ME_E_STATE, "shard " + std::to_string(bad) + "'s results do not account for its tape");
     }
-    c->res.resize(tk.n);
-    me_order_result* res = c->res.data();
-    for (uint32_t r = 0; r < W; ++r) {
-      const size_t lo = tk.pos_off[r], np = tk.pos_off[r + 1] - lo;
-      const uint32_t* pos = tk.pos.data() + lo;
-      const me_order_result* rr = tr[r];
-      par_chunks(np, kGrain, [&](size_t, size_t a, size_t b) {
-        for (size_t k = a; k < b; ++k) res[pos[k]] = rr[k];
-      });
-    }
-    // merged tape offsets: exclusive scan of the fill counts in slice order (chunk sums, then chunk scans)
-    const size_t T = par_threads(tk.n, kGrain);
-    std::vector<uint64_t> csum(T + 1, 0);
-    par_chunks(tk.n, kGrain, [&](size_t i, size_t a, size_t b) {
-      uint64_t x = 0;
-      for (size_t k = a; k < b; ++k) x += res[k].fill_count;
-      csum[i + 1] = x;
-    });
-    for (size_t i = 0; i < T; ++i) csum[i + 1] += csum[i];
-    c->tape.resize(csum[T]);
-    me_fill* tape = c->tape.data();
-    par_chunks(tk.n, kGrain, [&](size_t i, size_t a, size_t b) {
-      uint64_t o = csum[i];
-      for (size_t k = a; k < b; ++k) {
-        const uint32_t fc = res[k].fill_count;
-        res[k].tape_offset = (uint32_t)o;
-        o += fc;
-      }
-    });
-    for (uint32_t r = 0; r < W; ++r) {  // each taker's fills from its shard's tape
-      const size_t lo = tk.pos_off[r], np = tk.pos_off[r + 1] - lo;
-      const uint32_t* pos = tk.pos.data() + lo;
-      const me_order_result* rr = tr[r];
-      const me_fill* fr = tf[r];
-      par_chunks(np, kGrain, [&](size_t, size_t a, size_t b) {
-        for (size_t k = a; k < b; ++k)
-          if (rr[k].fill_count)
-            memcpy(tape + res[pos[k]].tape_offset, fr + rr[k].tape_offset, rr[k].fill_count * sizeof(me_fill));
-      });
-    }
+    const me_fill* tape = c->tape.data();
+    const me_order_result* res = c->res.data();
     c->out_tape = tape;
     c->out_nf = c->tape.size();
     c->out_res = res;
@@ -1187,34 +1268,13 @@ extern "C" int me_cluster_submit(me_cluster* c, const me_order_soa* b, size_t n,
   hdr[0] = CMD_SUBMIT;
   hdr[1] = (int64_t)tk.t;
   hdr[2] = (int64_t)n;
-  // split by owner, stable (each part keeps slice order = seq order): per-chunk counts of records and of
-  // NEW LIMITs per rank, their prefix, then every chunk packs its records at its offsets. An unknown global
-  // id goes to rank 0 out of range (BAD_SYMBOL there).
-  const size_t T = par_threads(n, kGrain);
-  std::vector<uint64_t> cnt(T * W, 0), lim(T * W, 0);
-  const uint32_t* owner = c->owner.data();
-  par_chunks(n, kGrain, [&](size_t i, size_t lo, size_t hi) {
-    // counted in the thread's own arrays, published once: the threads' rows of cnt / lim share cache lines
-    // (at world 1 all sixteen in one line: 66 ms per 1M-record slice of false sharing, profiles/r4/r4e)
-    std::vector<uint64_t> ci(W, 0), li(W, 0);
-    for (size_t k = lo; k < hi; ++k) {
-      const uint32_t s = b->symbol[k];
-      const uint32_t r = s < S ? owner[s] : 0;
-      ci[r]++;
-      li[r] += (b->kind[k] & 0x0Cu) == 0u;  // NEW LIMIT: may rest
-    }
-    std::copy(ci.begin(), ci.end(), cnt.begin() + i * W);
-    std::copy(li.begin(), li.end(), lim.begin() + i * W);
-  });
-  for (uint32_t r = 0; r < W; ++r)
-    for (size_t i = 0; i < T; ++i) {
-      hdr[6 + r] += (int64_t)cnt[i * W + r];
-      hdr[6 + W + r] += (int64_t)lim[i * W + r];
-    }
+  SplitCounts sc;
+  split_count(c->owner.data(), W, S, b, n, sc);
+  for (uint32_t r = 0; r < W; ++r) {
+    hdr[6 + r] = (int64_t)sc.per_rank[r];
+    hdr[6 + W + r] = (int64_t)sc.lim_rank[r];
+  }
   c->ph[PH_SPLIT_COUNT] += now_s() - t;
-  tk.pos_off.assign(W + 1, 0);
-  for (uint32_t r = 0; r < W; ++r) tk.pos_off[r + 1] = tk.pos_off[r] + (size_t)hdr[6 + r];
-  tk.pos.resize(n);
   // where each rank's part goes: rank 0's into its engine's slot inputs (direct), the others' packed into
   // h_send in rank order
   const size_t n0 = (size_t)hdr[6];
@@ -1248,31 +1308,7 @@ extern "C" int me_cluster_submit(me_cluster* c, const me_order_soa* b, size_t n,
       off += kRec * nr;
     }
   }
-  // chunk i's first record of rank r lands at base[i][r] within the part
-  std::vector<uint64_t> base(T * W, 0);
-  for (uint32_t r = 0; r < W; ++r) {
-    uint64_t x = 0;
-    for (size_t i = 0; i < T; ++i) {
-      base[i * W + r] = x;
-      x += cnt[i * W + r];
-    }
-  }
-  const uint32_t* local = c->local.data();
-  par_chunks(n, kGrain, [&](size_t i, size_t lo, size_t hi) {
-    std::vector<uint64_t> at(base.begin() + i * W, base.begin() + (i + 1) * W);
-    for (size_t k = lo; k < hi; ++k) {
-      const uint32_t s = b->symbol[k];
-      const uint32_t r = s < S ? owner[s] : 0;
-      const uint64_t j = at[r]++;
-      PackView& v = dst[r];
-      v.seq[j] = b->seq[k];
-      v.px[j] = b->price_q4[k];
-      v.qty[j] = b->qty[k];
-      v.sym[j] = s < S ? local[s] : 0xFFFFFFFFu;
-      v.kind[j] = b->kind[k];
-      tk.pos[tk.pos_off[r] + j] = (uint32_t)k;
-    }
-  });
+  split_pack(c->owner.data(), c->local.data(), W, S, b, n, sc, dst, tk);
   c->ph[PH_SPLIT] += now_s() - t;
   const int rc = issue(c, hdr);
   if (rc != ME_OK) return rc;
@@ -1391,4 +1427,75 @@ extern "C" int me_cluster_last_error(const me_cluster* c, char* buf, size_t cap)
     buf[k] = 0;
   }
   return (int)s.size();
+}
+
+// Rank 0's host work per slice at `world` shards without any GPU or transport (does rank 0
+// keep up with 100M orders/s at W = 8?): the exact split (split_count + split_pack into packed parts, the
+// path of every rank but a direct rank 0) and merge (merge_parts) code of me_cluster_submit / collect, over
+// `slice` with synthetic shard outputs — each record of a part gets floor((k + 1) F) - floor(k F) fills
+// (mean F = fills_per_order), tapes laid out as a shard returns them. seconds[0..3] = per-slice mean of the
+// owner-count pass, the pack, the merge, and the merged tape's length (fills).
+extern "C" int me_cluster_host_probe(uint32_t world, uint32_t num_symbols, const me_order_soa* slice, size_t n,
+                                     double fills_per_order, uint32_t iters, double* seconds) {
+  if (!world || !num_symbols || !slice || !n || !iters || !seconds || fills_per_order < 0) return ME_E_INVALID;
+  const uint32_t W = world, S = num_symbols;
+  std::vector<uint32_t> owner(S), local(S), cntl(W, 0);
+  for (uint32_t s = 0; s < S; ++s) {
+    owner[s] = me_shard_of(s, W);
+    local[s] = cntl[owner[s]]++;
+  }
+  std::vector<char> h_send(kRec * n);
+  // synthetic shard outputs, sized from a first split
+  SplitCounts sc;
+  split_count(owner.data(), W, S, slice, n, sc);
+  std::vector<std::vector<me_order_result>> rres(W);
+  std::vector<std::vector<me_fill>> rtape(W);
+  std::vector<const me_order_result*> tr(W);
+  std::vector<const me_fill*> tf(W);
+  std::vector<size_t> nf(W);
+  for (uint32_t r = 0; r < W; ++r) {
+    const size_t np = sc.per_rank[r];
+    rres[r].assign(np, me_order_result{});
+    uint64_t o = 0;
+    for (size_t k = 0; k < np; ++k) {
+      const uint32_t fc = (uint32_t)(std::floor((k + 1) * fills_per_order) - std::floor(k * fills_per_order));
+      rres[r][k].fill_count = fc;
+      rres[r][k].tape_offset = (uint32_t)o;
+      rres[r][k].status = fc ? ME_ST_FILLED : ME_ST_NEW;
+      o += fc;
+    }
+    rtape[r].assign(o, me_fill{});
+    for (uint64_t f = 0; f < o; ++f) rtape[r][f].qty = 1;
+    tr[r] = rres[r].data();
+    tf[r] = rtape[r].data();
+    nf[r] = o;
+  }
+  std::vector<me_order_result> res;
+  std::vector<me_fill> tape;
+  double t_count = 0, t_pack = 0, t_merge = 0;
+  for (uint32_t it = 0; it < iters; ++it) {
+    Ticket tk;
+    tk.n = n;
+    double t = now_s();
+    SplitCounts c2;
+    split_count(owner.data(), W, S, slice, n, c2);
+    t_count += now_s() - t;
+    std::vector<PackView> dst;
+    size_t off = 0;
+    for (uint32_t r = 0; r < W; ++r) {
+      dst.push_back(PackView(h_send.data() + off, c2.per_rank[r]));
+      off += kRec * c2.per_rank[r];
+    }
+    split_pack(owner.data(), local.data(), W, S, slice, n, c2, dst, tk);
+    t_pack += now_s() - t;
+    t = now_s();
+    uint32_t bad = 0;
+    if (!merge_parts(W, tk, tr, tf, nf, res, tape, &bad)) return ME_E_STATE;
+    t_merge += now_s() - t;
+  }
+  seconds[0] = t_count / iters;
+  seconds[1] = (t_pack - t_count) / iters;
+  seconds[2] = t_merge / iters;
+  seconds[3] = (double)tape.size();
+  return ME_OK;
 }
