@@ -476,6 +476,10 @@ __device__ __forceinline__ void a_walk_end(AWalk& w, AList& A, AList& B, int& bb
 // walk starts only if the book's sum is, and adds every block's quantities to that bound before the
 // block runs (a block that could cross it goes to the generic loop, from its first record on).
 constexpr uint32_t LW_BUY = 1u << 15, LW_MKT = 1u << 16, LW_RJ_SHIFT = 17, LW_LIM = 0x7FFFu;
+#ifndef ME_LW_SEL
+#define ME_LW_SEL 2  // the select walk (1: lw_block_sel; 2: the grouped walk's in hand-scheduled SALU, lw_block_x)
+                     // instead of the side-specific one (0: lw_block)
+#endif
 constexpr unsigned long long LW_CAP = 1ull << 31;
 
 struct LWalk {
@@ -485,6 +489,11 @@ struct LWalk {
   uint32_t cbb, cba; // cached totals of the best levels
   int L;
   unsigned long long ub;  // the book's sum plus the quantities of the blocks walked (< LW_CAP)
+  // the select walk (lw_block_sel): the best levels in SIDE coordinates — u0 = -best bid (1: none), u1 = best
+  // ask (L: none), so "better" is "smaller" on both sides — and their cached totals (0: the level emptied and
+  // the next best is not looked up until a taker needs it); a cached level's LDS word holds 0
+  int u0, u1;
+  uint32_t c0, c1;
 };
 
 // smallest occupied level >= x, or L: a scan of the LDS totals. Only levels on the side being searched
@@ -599,6 +608,29 @@ __device__ __forceinline__ void le_init(LEvG& e, AggGEv* ev, uint32_t eb) {
 }
 __device__ __forceinline__ void le_end(LEvG& e) {
   if (e.evp & 63u) le_store(e, e.evp & ~63u, e.evp & 63u);
+}
+// Conditional events (the select walk): the lanes are written whatever q is, and the log advances only
+// when q != 0 — an empty event's lane is overwritten by the next one. No branch but the block store's.
+__device__ __forceinline__ void le_emit_c(LEv& e, uint32_t lvl, uint32_t j, uint32_t q) {
+  const uint32_t slot = e.evp & 63u;
+  asm volatile(
+      "s_mov_b32 m0, %3\n\tv_writelane_b32 %0, %4, m0\n\tv_writelane_b32 %1, %5, m0\n\tv_writelane_b32 %2, %6, m0"
+      : "+v"(e.vl), "+v"(e.vj), "+v"(e.vq)
+      : "s"(slot), "s"(lvl), "s"(j), "s"(q)
+      : "m0");
+  const uint32_t full = (q != 0u) & (slot == 63u);
+  e.evp += q != 0u;
+  if (ME_UNLIKELY(full)) le_store(e, e.evp - 64u, 64u);
+}
+__device__ __forceinline__ void le_emit_c(LEvG& e, uint32_t lvl, uint32_t j, uint32_t q) {
+  const uint32_t slot = e.evp & 63u;
+  asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %3, m0\n\tv_writelane_b32 %1, %4, m0"
+               : "+v"(e.vw), "+v"(e.vq)
+               : "s"(slot), "s"(lvl | j), "s"(q)
+               : "m0");
+  const uint32_t full = (q != 0u) & (slot == 63u);
+  e.evp += q != 0u;
+  if (ME_UNLIKELY(full)) le_store(e, e.evp - 64u, 64u);
 }
 
 // A taker's partial take from the best level is the common case and stays out of the loop (no loop
@@ -795,6 +827,269 @@ __device__ __forceinline__ uint32_t lw_block(LE& e, LWalk& w, int oq, uint32_t o
   return k;
 }
 
+// ---- the select walk: one record path for both sides, selects instead of branches
+// The side-specific walk above costs ~11 branches per record (side, take / partial / pop, rest same / better /
+// worse, event-block checks) on a chain with one wave per SIMD, where a taken branch is ~20 cycles of nothing
+// (DESIGN.md §4). Here a record loads the state of its OPPOSITE side (the one it takes from) and its OWN side
+// (the one it rests on) by s_cselect, in side coordinates where both sides compare the same way:
+//   take:  crosses while u_opp <= its limit; tk = min(rem, cached total) — a level it empties stays cached
+//          with total 0 and is popped (an LDS scan) only when a taker still has quantity for the side;
+//   rest:  same level as the own best: the cached total grows; better: the old best's total goes to LDS and
+//          the rest becomes the cached best; worse: an LDS add at its level — one LDS add always (lane 0 on
+//          the chosen word, the dummy when there is nothing to add);
+//   events: written to their lanes unconditionally, the log advancing by (q != 0).
+// The only branches on a record's path: the pop loop (a taker that empties the best and has more to take)
+// and the 64-event block stores.
+__device__ __forceinline__ void lw_sel_init(LWalk& w) {
+  // the cached levels' LDS words hold 0 from here on
+  w.u0 = -w.bb;
+  w.u1 = w.ba;
+  w.c0 = w.cbb;
+  w.c1 = w.cba;
+  if (w.bb >= 0) lw_put(w, w.bb, 0u);
+  if (w.ba < w.L) lw_put(w, w.ba, 0u);
+}
+// The cached totals back into LDS, the exact best levels (a lazily emptied best is popped now).
+__device__ __forceinline__ void lw_sel_end(LWalk& w) {
+  int bb = -w.u0, ba = w.u1;
+  if (bb >= 0 && w.c0) lw_put(w, bb, w.c0);
+  if (ba < w.L && w.c1) lw_put(w, ba, w.c1);
+  wave_mem_order();
+  uint32_t t;
+  if (bb >= 0 && !w.c0) bb = lw_prev(w, bb, t);
+  if (ba < w.L && !w.c1) ba = lw_next(w, ba, t);
+  // lw_end puts the cached totals of bb / ba again: they are in LDS already
+  w.bb = bb;
+  w.ba = ba;
+  w.cbb = bb >= 0 ? lw_get(w, bb) : 0u;
+  w.cba = ba < w.L ? lw_get(w, ba) : 0u;
+}
+// one-lane LDS add at level index a (a = L: lane 0's own dummy word — nothing to add)
+__device__ __forceinline__ void lw_add_at(LWalk& w, int a, uint32_t d) {
+  const int lane = lane_id();
+  uint32_t* p = lane == 0 ? &w.tot[a] : &w.dummy[lane];
+  __hip_atomic_fetch_add(p, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <int JS, class LE>
+__device__ __forceinline__ uint32_t lw_block_sel(LE& e, LWalk& w, int oq, uint32_t ocw, uint32_t jb,
+                                                 unsigned long long fastm, uint32_t cnt, int& rr) {
+  const unsigned long long upto = (cnt >= 64u ? ~0ull : ((1ull << cnt) - 1ull)) & ~fastm;
+  const uint32_t k = upto ? (uint32_t)__builtin_ctzll(upto) : cnt;
+  const unsigned long long rjm = __ballot((ocw >> LW_RJ_SHIFT) != 0u);
+  unsigned long long work = (k >= 64u ? ~0ull : ((1ull << k) - 1ull)) & ~rjm;
+  const int L = w.L;
+  int rn = 0;
+  uint32_t cwn = 0, oqn = 0;
+  if constexpr (JS == 0) {
+    rn = __builtin_ctzll(work | (1ull << 63));
+    asm volatile("v_readlane_b32 %0, %2, %4\n\tv_readlane_b32 %1, %3, %4" : "=s"(cwn), "=s"(oqn) : "v"(ocw), "v"(oq), "s"(rn));
+  }
+  while (work) {
+    int r;
+    uint32_t cw, rem;
+    if constexpr (JS == 0) {
+      r = rn;
+      asm volatile("s_bitset0_b64 %0, %1" : "+s"(work) : "s"(r));
+      cw = cwn;
+      rem = oqn;
+      rn = __builtin_ctzll(work | (1ull << 63));
+      asm volatile("v_readlane_b32 %0, %2, %4\n\tv_readlane_b32 %1, %3, %4" : "=s"(cwn), "=s"(oqn) : "v"(ocw), "v"(oq), "s"(rn));
+    } else {
+      r = __builtin_ctzll(work);
+      asm volatile("s_bitset0_b64 %0, %1" : "+s"(work) : "s"(r));
+      cw = rl32(ocw, r);
+      rem = (uint32_t)rli32(oq, r);
+    }
+    const uint32_t jt = (jb + (uint32_t)r) << JS;
+    const int lim = (int)(cw & LW_LIM);
+    const bool buy = (cw & LW_BUY) != 0u;
+    // the opposite side (taken from) and the own side (rested on), in side coordinates
+    int uo = buy ? w.u1 : w.u0;
+    uint32_t co = buy ? w.c1 : w.c0;
+    int un = buy ? w.u0 : w.u1;
+    uint32_t cn = buy ? w.c0 : w.c1;
+    const int ulo = buy ? lim : -lim;  // the limit in the opposite side's coordinates (MARKET: the far end)
+    // take from the cached best
+    bool cross = uo <= ulo;
+    uint32_t tk = cross ? min(rem, co) : 0u;
+    co -= tk;
+    rem -= tk;
+    le_emit_c(e, (uint32_t)(buy ? uo : -uo), jt | AGG_TAKE, tk);
+    if (ME_UNLIKELY(cross && rem != 0u)) {  // the best is empty (co == 0) and the taker has more: pop
+      do {
+        uint32_t t;
+        int lv = buy ? lw_next(w, uo + 1, t) : lw_prev(w, -uo - 1, t);
+        if (t) lw_put(w, lv, 0u);  // the new cached best
+        uo = buy ? lv : -lv;
+        co = t;
+        cross = uo <= ulo;
+        tk = cross ? min(rem, co) : 0u;
+        co -= tk;
+        rem -= tk;
+        le_emit_c(e, (uint32_t)lv, jt | AGG_TAKE, tk);
+      } while (cross && rem != 0u);
+    }
+    // rest the LIMIT's remainder (a MARKET's is dropped)
+    uint32_t rq = (cw & LW_MKT) ? 0u : rem;
+    asm volatile("" : "+s"(rq));
+    const int uln = -ulo;  // the limit in the own side's coordinates
+    const bool eq = uln == un, better = uln < un;
+    const int lvn = buy ? -un : un;  // the own best's level
+    // the one LDS add: nothing (rq == 0 or the same level), the evicted best's total, or the rest itself
+    const int a = rq == 0u || eq ? L : (better ? (cn ? lvn : L) : lim);
+    const uint32_t d = better ? cn : rq;
+    lw_add_at(w, a, d);
+    cn = rq == 0u ? cn : (eq ? cn + rq : (better ? rq : cn));
+    un = rq != 0u && better ? uln : un;
+    le_emit_c(e, (uint32_t)lim, jt, rq);
+    w.u1 = buy ? uo : un;
+    w.c1 = buy ? co : cn;
+    w.u0 = buy ? un : uo;
+    w.c0 = buy ? cn : co;
+    asm volatile("s_mov_b32 m0, %1\n\tv_writelane_b32 %0, %2, m0" : "+v"(rr) : "s"(r), "s"(auniu(rem)) : "m0");
+  }
+  return k;
+}
+
+// The grouped walk's record path of lw_block_sel in hand-scheduled SALU (the compiler keeps uniform booleans
+// as 64-bit lane masks and re-tests them against exec at every select — ~40 extra SALU per record): one SCC
+// test feeds each run of s_cselect, arithmetic that clobbers SCC goes first. Same semantics, same events.
+__device__ __forceinline__ uint32_t lw_block_x(LEvG& e, LWalk& w, int oq, uint32_t ocw, uint32_t jb,
+                                               unsigned long long fastm, uint32_t cnt, int& rr) {
+  const unsigned long long upto = (cnt >= 64u ? ~0ull : ((1ull << cnt) - 1ull)) & ~fastm;
+  const uint32_t k = upto ? (uint32_t)__builtin_ctzll(upto) : cnt;
+  const unsigned long long rjm = __ballot((ocw >> LW_RJ_SHIFT) != 0u);
+  unsigned long long work = (k >= 64u ? ~0ull : ((1ull << k) - 1ull)) & ~rjm;
+  const uint32_t L = (uint32_t)w.L;
+  uint32_t u0 = (uint32_t)w.u0, u1 = (uint32_t)w.u1, c0 = w.c0, c1 = w.c1, evp = e.evp;
+  while (work) {
+    const int r = __builtin_ctzll(work);
+    asm volatile("s_bitset0_b64 %0, %1" : "+s"(work) : "s"(r));
+    const uint32_t cw = rl32(ocw, r);
+    uint32_t rem = (uint32_t)rli32(oq, r);
+    const uint32_t jt = (jb + (uint32_t)r) << AGG_GREC_SHIFT;
+    const uint32_t jtt = jt | AGG_TAKE;
+    uint32_t uo, co, un, cn, ulo, lim, lvo, fl, pp, t0, t1;
+    // side select, the take from the cached best, the take's event (its lane written whatever tk is; the log
+    // advances by tk != 0)
+    asm volatile(
+        "s_and_b32 %[lim], %[cw], 0x7fff\n\t"
+        "s_sub_i32 %[t0], 0, %[lim]\n\t"
+        "s_sub_i32 %[t1], 0, %[u0]\n\t"
+        "s_bitcmp1_b32 %[cw], 15\n\t"  // SCC = BUY
+        "s_cselect_b32 %[uo], %[u1], %[u0]\n\t"
+        "s_cselect_b32 %[co], %[c1], %[c0]\n\t"
+        "s_cselect_b32 %[un], %[u0], %[u1]\n\t"
+        "s_cselect_b32 %[cn], %[c0], %[c1]\n\t"
+        "s_cselect_b32 %[ulo], %[lim], %[t0]\n\t"  // the limit in the opposite side's coordinates
+        "s_cselect_b32 %[lvo], %[u1], %[t1]\n\t"   // the opposite best's level
+        "s_or_b32 %[lvo], %[lvo], %[jtt]\n\t"      // its event word
+        "s_min_u32 %[t0], %[rem], %[co]\n\t"
+        "s_cmp_le_i32 %[uo], %[ulo]\n\t"  // SCC = crosses
+        "s_cselect_b32 %[t0], %[t0], 0\n\t"  // tk
+        "s_sub_u32 %[co], %[co], %[t0]\n\t"
+        "s_sub_u32 %[rem], %[rem], %[t0]\n\t"
+        "s_cmp_le_i32 %[uo], %[ulo]\n\t"
+        "s_cselect_b32 %[pp], %[rem], 0\n\t"  // != 0: crosses with more to take (the best is empty): pop
+        "s_and_b32 %[t1], %[evp], 63\n\t"
+        "s_mov_b32 m0, %[t1]\n\t"
+        "v_writelane_b32 %[vw], %[lvo], m0\n\t"
+        "v_writelane_b32 %[vq], %[t0], m0\n\t"
+        "s_cmp_eq_u32 %[t1], 63\n\t"
+        "s_cselect_b32 %[fl], %[t0], 0\n\t"  // != 0: this event fills the staged block
+        "s_cmp_lg_u32 %[t0], 0\n\t"
+        "s_addc_u32 %[evp], %[evp], 0"
+        : [uo] "=&s"(uo), [co] "=&s"(co), [un] "=&s"(un), [cn] "=&s"(cn), [ulo] "=&s"(ulo), [lim] "=&s"(lim),
+          [lvo] "=&s"(lvo), [fl] "=&s"(fl), [pp] "=&s"(pp), [t0] "=&s"(t0), [t1] "=&s"(t1), [rem] "+s"(rem),
+          [evp] "+s"(evp), [vw] "+v"(e.vw), [vq] "+v"(e.vq)
+        : [cw] "s"(cw), [u0] "s"(u0), [u1] "s"(u1), [c0] "s"(c0), [c1] "s"(c1), [jtt] "s"(jtt)
+        : "m0", "scc");
+    if (ME_UNLIKELY(fl != 0u)) le_store(e, evp - 64u, 64u);
+    if (ME_UNLIKELY(pp != 0u)) {  // the cached best is empty and the taker has more: pop
+      const bool buy = (cw & LW_BUY) != 0u;
+      bool cross;
+      e.evp = evp;
+      do {
+        uint32_t t;
+        const int lv = buy ? lw_next(w, (int)uo + 1, t) : lw_prev(w, -(int)uo - 1, t);
+        if (t) lw_put(w, lv, 0u);  // the new cached best: its LDS word holds 0
+        uo = buy ? (uint32_t)lv : (uint32_t)(-lv);
+        co = t;
+        cross = (int)uo <= (int)ulo;
+        const uint32_t tk = cross ? min(rem, co) : 0u;
+        co -= tk;
+        rem -= tk;
+        le_emit_c(e, (uint32_t)lv, jtt, tk);
+      } while (cross && rem != 0u);
+      evp = e.evp;
+    }
+    // the rest (a MARKET's remainder is dropped): at the own best (its cached total grows), better (the old
+    // best's total goes to its LDS word, the rest is the new cached best) or worse (an LDS add at its level);
+    // one LDS add always — a = L is the dummy word
+    uint32_t a, d, rq, tq, tw, tb;
+    asm volatile(
+        "s_sub_i32 %[tq], 0, %[ulo]\n\t"  // the limit in the own side's coordinates
+        "s_sub_i32 %[tw], 0, %[un]\n\t"
+        "s_bitcmp1_b32 %[cw], 15\n\t"
+        "s_cselect_b32 %[tw], %[tw], %[un]\n\t"  // the own best's level
+        "s_cmp_lg_u32 %[cn], 0\n\t"
+        "s_cselect_b32 %[a], %[tw], %[L]\n\t"  // where an evicted best's total goes
+        "s_bitcmp1_b32 %[cw], 16\n\t"  // SCC = MARKET
+        "s_cselect_b32 %[rq], 0, %[rem]\n\t"
+        "s_cmp_eq_u32 %[tq], %[un]\n\t"
+        "s_cselect_b32 %[tw], %[rq], 0\n\t"  // at the own best
+        "s_cmp_lt_i32 %[tq], %[un]\n\t"
+        "s_cselect_b32 %[tb], %[rq], 0\n\t"  // better than the own best
+        "s_add_u32 %[d], %[cn], %[tw]\n\t"
+        "s_sub_u32 %[tw], %[rq], %[tw]\n\t"
+        "s_sub_u32 %[tw], %[tw], %[tb]\n\t"  // worse: the rest's quantity
+        "s_cmp_lg_u32 %[tb], 0\n\t"  // SCC = a better rest
+        "s_cselect_b32 %[un], %[tq], %[un]\n\t"
+        "s_cselect_b32 %[tq], %[cn], %[tw]\n\t"  // the LDS add's value
+        "s_cselect_b32 %[cn], %[tb], %[d]\n\t"
+        "s_cselect_b32 %[d], %[a], %[L]\n\t"
+        "s_cmp_lg_u32 %[tw], 0\n\t"
+        "s_cselect_b32 %[a], %[lim], %[d]\n\t"  // the LDS add's level
+        "s_mov_b32 %[d], %[tq]"
+        : [a] "=&s"(a), [d] "=&s"(d), [rq] "=&s"(rq), [tq] "=&s"(tq), [tw] "=&s"(tw), [tb] "=&s"(tb), [un] "+s"(un),
+          [cn] "+s"(cn)
+        : [cw] "s"(cw), [rem] "s"(rem), [ulo] "s"(ulo), [lim] "s"(lim), [L] "s"(L)
+        : "scc");
+    lw_add_at(w, (int)a, d);
+    uint32_t fl2;
+    asm volatile(
+        "s_and_b32 %[t1], %[evp], 63\n\t"
+        "s_or_b32 %[t0], %[lim], %[jt]\n\t"
+        "s_mov_b32 m0, %[t1]\n\t"
+        "v_writelane_b32 %[vw], %[t0], m0\n\t"
+        "v_writelane_b32 %[vq], %[rq], m0\n\t"
+        "s_cmp_eq_u32 %[t1], 63\n\t"
+        "s_cselect_b32 %[fl], %[rq], 0\n\t"
+        "s_cmp_lg_u32 %[rq], 0\n\t"
+        "s_addc_u32 %[evp], %[evp], 0\n\t"
+        "s_bitcmp1_b32 %[cw], 15\n\t"  // the state back
+        "s_cselect_b32 %[u1], %[uo], %[un]\n\t"
+        "s_cselect_b32 %[c1], %[co], %[cn]\n\t"
+        "s_cselect_b32 %[u0], %[un], %[uo]\n\t"
+        "s_cselect_b32 %[c0], %[cn], %[co]\n\t"
+        "s_mov_b32 m0, %[r]\n\t"
+        "v_writelane_b32 %[rr], %[rem], m0"
+        : [fl] "=&s"(fl2), [t0] "=&s"(t0), [t1] "=&s"(t1), [evp] "+s"(evp), [u0] "+s"(u0), [u1] "+s"(u1),
+          [c0] "+s"(c0), [c1] "+s"(c1), [vw] "+v"(e.vw), [vq] "+v"(e.vq), [rr] "+v"(rr)
+        : [cw] "s"(cw), [lim] "s"(lim), [jt] "s"(jt), [rq] "s"(rq), [uo] "s"(uo), [co] "s"(co), [un] "s"(un),
+          [cn] "s"(cn), [rem] "s"(rem), [r] "s"(r)
+        : "m0", "scc");
+    if (ME_UNLIKELY(fl2 != 0u)) le_store(e, evp - 64u, 64u);
+  }
+  w.u0 = (int)u0;
+  w.u1 = (int)u1;
+  w.c0 = c0;
+  w.c1 = c1;
+  e.evp = evp;
+  return k;
+}
+
 // A record's result from its fields and the remainder the chain left (vector form); fill count and
 // scratch start come later (k_agg_fin / k_agg_gres, from the log).
 __device__ __forceinline__ me_order_result a_result(int oq, uint32_t okd, uint32_t rj, int rem) {
@@ -884,6 +1179,7 @@ __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const Agg
   LEv le;
   le_init(le, ag, eb);
   const bool ladder = L <= (int)ag.ladder_max && lw_init(lw, bk, s, ltot, bb0, ba0);
+  if (ME_LW_SEL && ladder) lw_sel_init(lw);
   if (!ladder) {
     a_rebuild<1>(w, A, ba0);
     a_rebuild<0>(w, B, L - 1 - bb0);
@@ -923,7 +1219,8 @@ __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const Agg
     uint32_t k;
     if (ladder) {
       const bool adm = lw_admit(lw, v ? oq : 0);  // else: the generic loop from this block on
-      k = lw_block<0>(le, lw, oq, lw_cw(okd, olm, rj, L), blk, adm ? fastm : 0ull, cntb, rr);
+      k = ME_LW_SEL ? lw_block_sel<0>(le, lw, oq, lw_cw(okd, olm, rj, L), blk, adm ? fastm : 0ull, cntb, rr)
+                    : lw_block<0>(le, lw, oq, lw_cw(okd, olm, rj, L), blk, adm ? fastm : 0ull, cntb, rr);
     } else {
       a_refill(w, A, B);
       ARes R;
@@ -943,6 +1240,7 @@ __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const Agg
   if (ladder) {
     le_end(le);
     w.evp = le.evp;
+    if (ME_LW_SEL) lw_sel_end(lw);
     lw_end(lw, bk, s);
     bb = lw.bb;
     ba = lw.ba;
@@ -1904,6 +2202,7 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
     uint32_t rbase = 0;
     LWalk lw;
     const bool lok = lw_init(lw, bk, s, ltot, bb0, ba0);  // else: the continuation from the first record
+    if (ME_LW_SEL && lok) lw_sel_init(lw);
     uint32_t hidx = NIL, gstop = ng;
     // a batch's bucket is loaded while the batch before it runs (no HBM round trip between batches)
     // (only the lanes of the bucket's records load: a 128-slot bucket holds ~64 at config 2)
@@ -1964,8 +2263,10 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
           rjs[rbase + (uint32_t)lane] = (g << AGG_GSHIFT) | oi;
         }
         GW_T(1);
-        const uint32_t k = lw_block<AGG_GREC_SHIFT>(w, lw, oq, lw_cw(okd, olm, rj, L), rbase, adm ? fastm : 0ull,
-                                                     cntb, rr);
+        const uint32_t k =
+            ME_LW_SEL == 2 ? lw_block_x(w, lw, oq, lw_cw(okd, olm, rj, L), rbase, adm ? fastm : 0ull, cntb, rr)
+            : ME_LW_SEL ? lw_block_sel<AGG_GREC_SHIFT>(w, lw, oq, lw_cw(okd, olm, rj, L), rbase, adm ? fastm : 0ull, cntb, rr)
+                      : lw_block<AGG_GREC_SHIFT>(w, lw, oq, lw_cw(okd, olm, rj, L), rbase, adm ? fastm : 0ull, cntb, rr);
         rbase += cntb;
         GW_T(2);
 #ifdef ME_STAMPS
@@ -1988,6 +2289,7 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
       *a_gtab(ag.gev, s, g) = eb + w.evp;
     if (gstop < ng && lane == 0) *a_gtab(ag.gev, s, gstop + 1u) = eb + w.evp;
     le_end(w);
+    if (ME_LW_SEL && lok) lw_sel_end(lw);
     if (lok) lw_end(lw, bk, s);  // (else the LDS copy is truncated and nothing was walked)
     const int bb = lw.bb, ba = lw.ba;
     if (lane == 0) {
