@@ -955,56 +955,89 @@ __device__ __forceinline__ uint32_t lw_block_sel(LE& e, LWalk& w, int oq, uint32
 // The grouped walk's record path of lw_block_sel in hand-scheduled SALU (the compiler keeps uniform booleans
 // as 64-bit lane masks and re-tests them against exec at every select — ~40 extra SALU per record): one SCC
 // test feeds each run of s_cselect, arithmetic that clobbers SCC goes first. Same semantics, same events.
-__device__ __forceinline__ uint32_t lw_block_x(LEvG& e, LWalk& w, int oq, uint32_t ocw, uint32_t jb,
+// event lanes of the select walk (m0 = the slot): grouped events {level | record, qty}, the hot path's
+// {level, record, qty}
+__device__ __forceinline__ void le_lanes(LEvG& e, uint32_t slot, uint32_t lvl, uint32_t j, uint32_t q) {
+  asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %3, m0\n\tv_writelane_b32 %1, %4, m0"
+               : "+v"(e.vw), "+v"(e.vq)
+               : "s"(slot), "s"(lvl | j), "s"(q)
+               : "m0");
+}
+__device__ __forceinline__ void le_lanes(LEv& e, uint32_t slot, uint32_t lvl, uint32_t j, uint32_t q) {
+  asm volatile(
+      "s_mov_b32 m0, %3\n\tv_writelane_b32 %0, %4, m0\n\tv_writelane_b32 %1, %5, m0\n\tv_writelane_b32 %2, %6, m0"
+      : "+v"(e.vl), "+v"(e.vj), "+v"(e.vq)
+      : "s"(slot), "s"(lvl), "s"(j), "s"(q)
+      : "m0");
+}
+
+template <int JS, class LE>
+__device__ __forceinline__ uint32_t lw_block_x(LE& e, LWalk& w, int oq, uint32_t ocw, uint32_t jb,
                                                unsigned long long fastm, uint32_t cnt, int& rr) {
   const unsigned long long upto = (cnt >= 64u ? ~0ull : ((1ull << cnt) - 1ull)) & ~fastm;
   const uint32_t k = upto ? (uint32_t)__builtin_ctzll(upto) : cnt;
   const unsigned long long rjm = __ballot((ocw >> LW_RJ_SHIFT) != 0u);
   unsigned long long work = (k >= 64u ? ~0ull : ((1ull << k) - 1ull)) & ~rjm;
-  const uint32_t L = (uint32_t)w.L;
-  uint32_t u0 = (uint32_t)w.u0, u1 = (uint32_t)w.u1, c0 = w.c0, c1 = w.c1, evp = e.evp;
+  const uint32_t L = auniu((uint32_t)w.L);
+  uint32_t u0 = auniu((uint32_t)w.u0), u1 = auniu((uint32_t)w.u1), c0 = auniu(w.c0), c1 = auniu(w.c1),
+           evp = auniu(e.evp);
+  // config 1's walk (JS = 0) reads the next record's control word and quantity one record ahead (lw_block)
+  int rn = 0;
+  uint32_t cwn = 0, oqn = 0;
+  if constexpr (JS == 0) {
+    rn = __builtin_ctzll(work | (1ull << 63));
+    asm volatile("v_readlane_b32 %0, %2, %4\n\tv_readlane_b32 %1, %3, %4" : "=s"(cwn), "=s"(oqn) : "v"(ocw), "v"(oq), "s"(rn));
+  }
   while (work) {
-    const int r = __builtin_ctzll(work);
-    asm volatile("s_bitset0_b64 %0, %1" : "+s"(work) : "s"(r));
-    const uint32_t cw = rl32(ocw, r);
-    uint32_t rem = (uint32_t)rli32(oq, r);
-    const uint32_t jt = (jb + (uint32_t)r) << AGG_GREC_SHIFT;
+    int r;
+    uint32_t cw, rem;
+    if constexpr (JS == 0) {
+      r = rn;
+      asm volatile("s_bitset0_b64 %0, %1" : "+s"(work) : "s"(r));
+      cw = cwn;
+      rem = oqn;
+      rn = __builtin_ctzll(work | (1ull << 63));
+      asm volatile("v_readlane_b32 %0, %2, %4\n\tv_readlane_b32 %1, %3, %4" : "=s"(cwn), "=s"(oqn) : "v"(ocw), "v"(oq), "s"(rn));
+    } else {
+      r = __builtin_ctzll(work);
+      asm volatile("s_bitset0_b64 %0, %1" : "+s"(work) : "s"(r));
+      cw = rl32(ocw, r);
+      rem = (uint32_t)rli32(oq, r);
+    }
+    const uint32_t jt = (jb + (uint32_t)r) << JS;
     const uint32_t jtt = jt | AGG_TAKE;
-    uint32_t uo, co, un, cn, ulo, lim, lvo, fl, pp, t0, t1;
-    // side select, the take from the cached best, the take's event (its lane written whatever tk is; the log
+    uint32_t uo, co, un, cn, ulo, lim, lvo, fl, pp, tk, slot;
+    // side select and the take from the cached best (its event's lanes written whatever tk is; the log
     // advances by tk != 0)
     asm volatile(
         "s_and_b32 %[lim], %[cw], 0x7fff\n\t"
-        "s_sub_i32 %[t0], 0, %[lim]\n\t"
-        "s_sub_i32 %[t1], 0, %[u0]\n\t"
+        "s_sub_i32 %[tk], 0, %[lim]\n\t"
+        "s_sub_i32 %[slot], 0, %[u0]\n\t"
         "s_bitcmp1_b32 %[cw], 15\n\t"  // SCC = BUY
         "s_cselect_b32 %[uo], %[u1], %[u0]\n\t"
         "s_cselect_b32 %[co], %[c1], %[c0]\n\t"
         "s_cselect_b32 %[un], %[u0], %[u1]\n\t"
         "s_cselect_b32 %[cn], %[c0], %[c1]\n\t"
-        "s_cselect_b32 %[ulo], %[lim], %[t0]\n\t"  // the limit in the opposite side's coordinates
-        "s_cselect_b32 %[lvo], %[u1], %[t1]\n\t"   // the opposite best's level
-        "s_or_b32 %[lvo], %[lvo], %[jtt]\n\t"      // its event word
-        "s_min_u32 %[t0], %[rem], %[co]\n\t"
+        "s_cselect_b32 %[ulo], %[lim], %[tk]\n\t"  // the limit in the opposite side's coordinates
+        "s_cselect_b32 %[lvo], %[u1], %[slot]\n\t" // the opposite best's level
+        "s_min_u32 %[tk], %[rem], %[co]\n\t"
         "s_cmp_le_i32 %[uo], %[ulo]\n\t"  // SCC = crosses
-        "s_cselect_b32 %[t0], %[t0], 0\n\t"  // tk
-        "s_sub_u32 %[co], %[co], %[t0]\n\t"
-        "s_sub_u32 %[rem], %[rem], %[t0]\n\t"
+        "s_cselect_b32 %[tk], %[tk], 0\n\t"
+        "s_sub_u32 %[co], %[co], %[tk]\n\t"
+        "s_sub_u32 %[rem], %[rem], %[tk]\n\t"
         "s_cmp_le_i32 %[uo], %[ulo]\n\t"
         "s_cselect_b32 %[pp], %[rem], 0\n\t"  // != 0: crosses with more to take (the best is empty): pop
-        "s_and_b32 %[t1], %[evp], 63\n\t"
-        "s_mov_b32 m0, %[t1]\n\t"
-        "v_writelane_b32 %[vw], %[lvo], m0\n\t"
-        "v_writelane_b32 %[vq], %[t0], m0\n\t"
-        "s_cmp_eq_u32 %[t1], 63\n\t"
-        "s_cselect_b32 %[fl], %[t0], 0\n\t"  // != 0: this event fills the staged block
-        "s_cmp_lg_u32 %[t0], 0\n\t"
+        "s_and_b32 %[slot], %[evp], 63\n\t"
+        "s_cmp_eq_u32 %[slot], 63\n\t"
+        "s_cselect_b32 %[fl], %[tk], 0\n\t"  // != 0: this event fills the staged block
+        "s_cmp_lg_u32 %[tk], 0\n\t"
         "s_addc_u32 %[evp], %[evp], 0"
         : [uo] "=&s"(uo), [co] "=&s"(co), [un] "=&s"(un), [cn] "=&s"(cn), [ulo] "=&s"(ulo), [lim] "=&s"(lim),
-          [lvo] "=&s"(lvo), [fl] "=&s"(fl), [pp] "=&s"(pp), [t0] "=&s"(t0), [t1] "=&s"(t1), [rem] "+s"(rem),
-          [evp] "+s"(evp), [vw] "+v"(e.vw), [vq] "+v"(e.vq)
-        : [cw] "s"(cw), [u0] "s"(u0), [u1] "s"(u1), [c0] "s"(c0), [c1] "s"(c1), [jtt] "s"(jtt)
-        : "m0", "scc");
+          [lvo] "=&s"(lvo), [fl] "=&s"(fl), [pp] "=&s"(pp), [tk] "=&s"(tk), [slot] "=&s"(slot), [rem] "+s"(rem),
+          [evp] "+s"(evp)
+        : [cw] "s"(cw), [u0] "s"(u0), [u1] "s"(u1), [c0] "s"(c0), [c1] "s"(c1)
+        : "scc");
+    le_lanes(e, slot, lvo, jtt, tk);
     if (ME_UNLIKELY(fl != 0u)) le_store(e, evp - 64u, 64u);
     if (ME_UNLIKELY(pp != 0u)) {  // the cached best is empty and the taker has more: pop
       const bool buy = (cw & LW_BUY) != 0u;
@@ -1017,10 +1050,10 @@ __device__ __forceinline__ uint32_t lw_block_x(LEvG& e, LWalk& w, int oq, uint32
         uo = buy ? (uint32_t)lv : (uint32_t)(-lv);
         co = t;
         cross = (int)uo <= (int)ulo;
-        const uint32_t tk = cross ? min(rem, co) : 0u;
-        co -= tk;
-        rem -= tk;
-        le_emit_c(e, (uint32_t)lv, jtt, tk);
+        const uint32_t tq = cross ? min(rem, co) : 0u;
+        co -= tq;
+        rem -= tq;
+        le_emit_c(e, (uint32_t)lv, jtt, tq);
       } while (cross && rem != 0u);
       evp = e.evp;
     }
@@ -1057,14 +1090,10 @@ __device__ __forceinline__ uint32_t lw_block_x(LEvG& e, LWalk& w, int oq, uint32
         : [cw] "s"(cw), [rem] "s"(rem), [ulo] "s"(ulo), [lim] "s"(lim), [L] "s"(L)
         : "scc");
     lw_add_at(w, (int)a, d);
-    uint32_t fl2;
+    uint32_t fl2, slot2;
     asm volatile(
-        "s_and_b32 %[t1], %[evp], 63\n\t"
-        "s_or_b32 %[t0], %[lim], %[jt]\n\t"
-        "s_mov_b32 m0, %[t1]\n\t"
-        "v_writelane_b32 %[vw], %[t0], m0\n\t"
-        "v_writelane_b32 %[vq], %[rq], m0\n\t"
-        "s_cmp_eq_u32 %[t1], 63\n\t"
+        "s_and_b32 %[slot], %[evp], 63\n\t"
+        "s_cmp_eq_u32 %[slot], 63\n\t"
         "s_cselect_b32 %[fl], %[rq], 0\n\t"
         "s_cmp_lg_u32 %[rq], 0\n\t"
         "s_addc_u32 %[evp], %[evp], 0\n\t"
@@ -1072,14 +1101,13 @@ __device__ __forceinline__ uint32_t lw_block_x(LEvG& e, LWalk& w, int oq, uint32
         "s_cselect_b32 %[u1], %[uo], %[un]\n\t"
         "s_cselect_b32 %[c1], %[co], %[cn]\n\t"
         "s_cselect_b32 %[u0], %[un], %[uo]\n\t"
-        "s_cselect_b32 %[c0], %[cn], %[co]\n\t"
-        "s_mov_b32 m0, %[r]\n\t"
-        "v_writelane_b32 %[rr], %[rem], m0"
-        : [fl] "=&s"(fl2), [t0] "=&s"(t0), [t1] "=&s"(t1), [evp] "+s"(evp), [u0] "+s"(u0), [u1] "+s"(u1),
-          [c0] "+s"(c0), [c1] "+s"(c1), [vw] "+v"(e.vw), [vq] "+v"(e.vq), [rr] "+v"(rr)
-        : [cw] "s"(cw), [lim] "s"(lim), [jt] "s"(jt), [rq] "s"(rq), [uo] "s"(uo), [co] "s"(co), [un] "s"(un),
-          [cn] "s"(cn), [rem] "s"(rem), [r] "s"(r)
-        : "m0", "scc");
+        "s_cselect_b32 %[c0], %[cn], %[co]"
+        : [fl] "=&s"(fl2), [slot] "=&s"(slot2), [evp] "+s"(evp), [u0] "+s"(u0), [u1] "+s"(u1), [c0] "+s"(c0),
+          [c1] "+s"(c1)
+        : [cw] "s"(cw), [rq] "s"(rq), [uo] "s"(uo), [co] "s"(co), [un] "s"(un), [cn] "s"(cn)
+        : "scc");
+    le_lanes(e, slot2, (uint32_t)lim, jt, rq);
+    asm volatile("s_mov_b32 m0, %1\n\tv_writelane_b32 %0, %2, m0" : "+v"(rr) : "s"(r), "s"(rem) : "m0");
     if (ME_UNLIKELY(fl2 != 0u)) le_store(e, evp - 64u, 64u);
   }
   w.u0 = (int)u0;
@@ -1219,7 +1247,8 @@ __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const Agg
     uint32_t k;
     if (ladder) {
       const bool adm = lw_admit(lw, v ? oq : 0);  // else: the generic loop from this block on
-      k = ME_LW_SEL ? lw_block_sel<0>(le, lw, oq, lw_cw(okd, olm, rj, L), blk, adm ? fastm : 0ull, cntb, rr)
+      k = ME_LW_SEL == 2 ? lw_block_x<0>(le, lw, oq, lw_cw(okd, olm, rj, L), blk, adm ? fastm : 0ull, cntb, rr)
+          : ME_LW_SEL    ? lw_block_sel<0>(le, lw, oq, lw_cw(okd, olm, rj, L), blk, adm ? fastm : 0ull, cntb, rr)
                     : lw_block<0>(le, lw, oq, lw_cw(okd, olm, rj, L), blk, adm ? fastm : 0ull, cntb, rr);
     } else {
       a_refill(w, A, B);
@@ -2264,7 +2293,7 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
         }
         GW_T(1);
         const uint32_t k =
-            ME_LW_SEL == 2 ? lw_block_x(w, lw, oq, lw_cw(okd, olm, rj, L), rbase, adm ? fastm : 0ull, cntb, rr)
+            ME_LW_SEL == 2 ? lw_block_x<AGG_GREC_SHIFT>(w, lw, oq, lw_cw(okd, olm, rj, L), rbase, adm ? fastm : 0ull, cntb, rr)
             : ME_LW_SEL ? lw_block_sel<AGG_GREC_SHIFT>(w, lw, oq, lw_cw(okd, olm, rj, L), rbase, adm ? fastm : 0ull, cntb, rr)
                       : lw_block<AGG_GREC_SHIFT>(w, lw, oq, lw_cw(okd, olm, rj, L), rbase, adm ? fastm : 0ull, cntb, rr);
         rbase += cntb;
