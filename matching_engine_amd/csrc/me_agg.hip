@@ -2088,6 +2088,7 @@ __global__ __launch_bounds__(256) void k_agg_out(BookDev bk, BatchDev bt, AggDev
 // does not cover (a cancel, a price outside the window, a bucket past BK_CAP records) hands the symbol's
 // rest of the group to k_match_reg's continuation launch (me_match_reg.hip, kSlow).
 struct AggGArgs {
+  uint32_t nrec[ME_GMAX], ntiles[ME_GMAX];  // records and tape tiles of batch g
   uint32_t* bcnt[ME_GMAX];
   const BkRec* b_rec[ME_GMAX];
   me_order_result* res[ME_GMAX];
@@ -2097,6 +2098,14 @@ struct AggGArgs {
   unsigned long long ovf_base, scratch_cap;
   const uint64_t* seq0;  // the group's first record's seq (k_agg_gres: events carry their seq's offset from it)
   uint32_t slab, ng;
+  // the direct tape (device batches before the group's first hand-off): k_agg_gres2 writes their fills at
+  // their tape positions, k_agg_tscan having turned the fill counts into tape offsets
+  me_fill* tape[ME_GMAX];
+  unsigned long long* tape_count[ME_GMAX];
+  uint32_t* done[ME_GMAX];        // the output set's "tape written" flag (the tape job skips the batch)
+  unsigned long long* fills_acc;
+  uint32_t* ticket;               // k_agg_gres1's last-workgroup counter (the tile scans)
+  uint32_t direct;                // bit g: batch g is a device batch (its tape may be written directly)
 };
 
 // Ascending bitonic sort of 64 (one register) / 128 (two) distinct keys across the wave; partners over
@@ -2208,6 +2217,7 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
                                                           // symbol goes to the continuation
       const uint32_t g0 = (uint32_t)__builtin_ctzll(__ballot(nsv != 0u));
       a_ghand(bk, s, g0, 0u, rl32(nsv, (int)g0), s * ga.slab, s * ga.slab + ga.slab);
+      if (lane == 0) atomicMax(&ag.ctr[AC_HB], ng - g0);  // (no direct tape from this batch on)
       continue;
     }
     // free chunks k_match_reg parked in fcache[s][0, nfree) join the front of the free list (one header
@@ -2251,6 +2261,7 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
       if (!cnt) continue;
       if (cnt > (uint32_t)BK_CAP) {  // an overfull bucket: the continuation rescans the batch
         hidx = a_ghand(bk, s, g, 0u, cnt, 0u, 0u);
+        if (lane == 0) atomicMax(&ag.ctr[AC_HB], ng - g);
         gstop = g;
         break;
       }
@@ -2304,6 +2315,7 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
         if (v && (uint32_t)lane < k) res[oi] = a_result(oq, okd, rj, rr);  // fills: k_agg_gres
         if (k < cntb) {
           hidx = a_ghand(bk, s, g, blk + k, cnt, 0u, 0u);  // scratch position: k_agg_gres
+          if (lane == 0) atomicMax(&ag.ctr[AC_HB], ng - g);
           stop = true;
           break;
         }
@@ -2366,10 +2378,6 @@ constexpr uint32_t GR_THREADS = GR_WAVES * 64;
 #endif
 constexpr uint32_t GR_STAGE = 48;  // consumed makers / emptied chunks a level stages in LDS (else: HBM)
 
-struct GrLevel {  // what phase B found for one level
-  unsigned long long C, T0;
-  uint32_t newhead, mk_base, nmk, fr_base, nfreed, need, d_off, ks;
-};
 struct GrStage {  // a wave's maker / emptied-chunk staging (phases B and D)
   AggMk mk[GR_STAGE];
   uint32_t fr[GR_STAGE];
@@ -2386,6 +2394,7 @@ struct GrShared {
   uint32_t gev[ME_GMAX + 1], gex[ME_GMAX + 1], gbase[ME_GMAX + 1];
   uint32_t wsum[GR_WAVES];
   uint32_t nlv, next, next2, cur_mk, cur_fr, deficit, alloc_base;
+  uint32_t dmask;  // bit g: batch g's fills go straight to its tape
   int dresting;
   uint8_t ltend[128];
 };
@@ -2398,8 +2407,8 @@ __device__ __forceinline__ uint32_t gr_take(uint32_t* ctr) {
 }
 
 template <bool kLds>
-__device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& ga, const AggSrc& src, const AggDev& ag,
-                                            uint32_t s, const AggSlot& sl, GrShared& sh, uint32_t* nf) {
+__device__ __forceinline__ void gres_symbol1(const BookDev& bk, const AggGArgs& ga, const AggSrc& src, const AggDev& ag,
+                                             uint32_t s, const AggSlot& sl, GrShared& sh, uint32_t* nf) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint32_t L = bk.L;  // <= 128
   const uint32_t eb = sl.ev_base, n = sl.ev_cnt, ng = ga.ng;
@@ -2426,6 +2435,10 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
     sh.next = sh.next2 = 0u;
     sh.cur_mk = sh.cur_fr = sh.deficit = 0u;
     sh.dresting = 0;
+    // the batches before the group's first hand-off (a continuation's fills go to scratch behind the walk's
+    // of their batch) whose tapes are the engine's: their fills go straight to the tape
+    const uint32_t hb = ng - min(ag.ctr[AC_HB], ng);
+    sh.dmask = ga.direct & (hb >= 32u ? ~0u : ((1u << hb) - 1u));
   }
   sh.u.wh[wv][lane] = 0u;
   sh.u.wh[wv][64 + lane] = 0u;
@@ -2767,12 +2780,13 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
   }
   __syncthreads();
   auto EX = [&](uint32_t e) -> uint32_t { return e < n ? nf[e] : ftot; };
+  const uint32_t dmask = sh.dmask;
   if ((uint32_t)tid < ng) {  // each batch's fills: the symbol's slab of that batch if they fit, else overflow
     const uint32_t g = (uint32_t)tid;
     const uint32_t x0 = EX(sh.gev[g]), x1 = EX(sh.gev[g + 1]);
     const uint32_t f = x1 - x0;
     unsigned long long b0 = (unsigned long long)s * ga.slab;
-    if (f > ga.slab) {
+    if (f > ga.slab && !((dmask >> g) & 1u)) {  // (a direct batch's fills need no scratch)
       b0 = ga.ovf_base + atomicAdd(ga.scratch_top[g], (unsigned long long)f);
       if (b0 + f > ga.scratch_cap) {
         atomicOr(bk.err, ERR_SCRATCH_OOM);
@@ -2807,7 +2821,7 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
         const uint32_t x0 = EX(e), nfill = EX(e + nte) - x0;
         me_order_result* res = ga.res[g];
         res[oi].fill_count = nfill;
-        res[oi].tape_offset = sh.gbase[g] + (x0 - sh.gex[g]);
+        if (!((dmask >> g) & 1u)) res[oi].tape_offset = sh.gbase[g] + (x0 - sh.gex[g]);  // (direct: k_agg_tscan)
         if (nfill) atomicAdd(&ga.tile_sum[g][oi / TILE_TAPE], nfill);
       }
     }
@@ -2908,10 +2922,116 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
   }
   __syncthreads();
   GR_STAMP(bk, s, 6);
+  // ---- hand-off to k_agg_gres2: the level state, the batches' fill bases, the fill offsets
+  GrSave* sv = ag.gsave + s;
+  const uint32_t nlv2 = sh.nlv;
+  for (uint32_t i = tid; i < 129u; i += GR_THREADS) sv->lstart[i] = sh.lstart[i];
+  for (uint32_t i = tid; i < L; i += GR_THREADS) {
+    sv->lhead[i] = sh.lhead[i];
+    sv->ltail[i] = sh.ltail[i];
+    sv->ltend[i] = sh.ltend[i];
+  }
+  for (uint32_t i = tid; i < nlv2; i += GR_THREADS) {
+    const uint32_t l = sh.lvlist[i];
+    sv->lvlist[i] = l;
+    sv->lv[l] = sh.lv[l];
+  }
+  for (uint32_t i = tid; i <= ng; i += GR_THREADS) {
+    sv->gex[i] = sh.gex[i];
+    sv->gbase[i] = sh.gbase[i];
+  }
+  if (tid == 0) {
+    sv->nlv = nlv2;
+    sv->alloc_base = sh.alloc_base;
+    sv->pad[0] = sh.dmask;
+    sv->pad[1] = ftot;
+  }
+  if constexpr (kLds) {  // the fill offsets (LDS) to the log's HBM array
+    uint32_t* hn = ag.evn + eb;
+    for (uint32_t i = tid; i < n; i += GR_THREADS) hn[i] = nf[i];
+  }
+}
+
+// Phase D of a symbol (k_agg_gres2), from k_agg_gres1's hand-off: the fills of each level's takes — a direct
+// batch's at its tape position (k_agg_tscan's record offset + the take's place among the record's fills), a
+// scratch batch's in its scratch run — and the surviving rests.
+template <bool kLds>
+__device__ __forceinline__ void gres_symbol2(const BookDev& bk, const AggGArgs& ga, const AggDev& ag, uint32_t s,
+                                             const AggSlot& sl, GrShared& sh, uint32_t* nf) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint32_t L = bk.L;
+  const uint32_t eb = sl.ev_base, n = sl.ev_cnt, ng = ga.ng;
+  const AggGEv* ev = reinterpret_cast<const AggGEv*>(ag.ev + eb);
+  const uint32_t* rsq = reinterpret_cast<const uint32_t*>(ev + sl.lo);
+  const uint32_t* rjs = rsq + sl.hi;
+  AggGEv* const srt = reinterpret_cast<AggGEv*>(ag.evq + eb);
+  auto srec = [](uint32_t w) -> uint32_t { return (w >> 16) & 0x7FFFu; };
+  const size_t lo_l = (size_t)s * L;
+  const unsigned long long gmin = *ga.seq0;
+  const GrSave* sv = ag.gsave + s;
+  for (uint32_t i = tid; i < 129u; i += GR_THREADS) sh.lstart[i] = sv->lstart[i];
+  for (uint32_t i = tid; i < L; i += GR_THREADS) {
+    sh.lhead[i] = sv->lhead[i];
+    sh.ltail[i] = sv->ltail[i];
+    sh.ltend[i] = sv->ltend[i];
+  }
+  const uint32_t nlv = sv->nlv;
+  for (uint32_t i = tid; i < nlv; i += GR_THREADS) {
+    const uint32_t l = sv->lvlist[i];
+    sh.lvlist[i] = l;
+    sh.lv[l] = sv->lv[l];
+  }
+  for (uint32_t i = tid; i <= ng; i += GR_THREADS) {
+    sh.gex[i] = sv->gex[i];
+    sh.gbase[i] = sv->gbase[i];
+  }
+  if constexpr (kLds) {
+    const uint32_t* hn = ag.evn + eb;
+    for (uint32_t i = tid; i < n; i += GR_THREADS) nf[i] = hn[i];
+  }
+  if (tid == 0) sh.next2 = 0u;
+  const uint32_t dmask = sv->pad[0];
+  const uint32_t ftot_n = n;  // (EX past the log's end: the symbol's fill total, nf's exclusive scan end)
+  __syncthreads();
+  const uint32_t ftot = sv->pad[1];
+  auto EX = [&](uint32_t e) -> uint32_t { return e < ftot_n ? nf[e] : ftot; };
+  // each direct record's fill base: its tape offset (k_agg_tscan) less its first take event's fill offset,
+  // so a take event's fills start at base + nf[event]; in the records' HBM array beside the log
+  uint32_t* rbase = ag.evx + eb;
+  if (dmask) {
+    const uint32_t per = ((n + GR_WAVES - 1u) / GR_WAVES + 63u) & ~63u;
+    const uint32_t r0 = min(n, (uint32_t)wv * per), r1 = min(n, r0 + per);
+    uint32_t prevj = r0 > 0 && r0 < r1 ? auniu(ev[r0 - 1].w >> AGG_GREC_SHIFT) : NIL;
+    for (uint32_t b = r0; b < r1; b += 64) {
+      const uint32_t e = b + (uint32_t)lane;
+      const bool v = e < r1;
+      const uint32_t j = v ? ev[e].w >> AGG_GREC_SHIFT : NIL;
+      uint32_t pj = (uint32_t)__shfl_up((int)j, 1, 64);
+      pj = lane == 0 ? prevj : pj;
+      prevj = rl32(j, 63);
+      if (v && (j & (AGG_TAKE >> AGG_GREC_SHIFT)) && pj != j) {
+        const uint32_t r = j & ~(AGG_TAKE >> AGG_GREC_SHIFT);
+        const uint32_t gp = rjs[r];
+        const uint32_t g = gp >> AGG_GSHIFT, oi = gp & AGG_IMASK;
+        if ((dmask >> g) & 1u) rbase[r] = ga.res[g][oi].tape_offset - EX(e);
+      }
+    }
+  }
+  __syncthreads();
+  AggMk* mkl = sh.u.st[wv].mk;
+  auto entry = [&](uint32_t start, uint32_t cnt, uint32_t b, uint32_t& er) -> AggGEv {
+    AggGEv E{};
+    er = 0;
+    if (b + (uint32_t)lane < cnt) {
+      E = srt[start + b + lane];
+      er = E.w & 0xFFFFu;
+    }
+    return E;
+  };
+  const uint32_t alloc_base = sv->alloc_base;
   // ---- D: per level, one pass over its events: the fills of its takes (makers overlapping each take's
   //      interval, at the record's scratch position) and its surviving rests into the tail chunk and new
   //      chunks; the new chunks' headers, the level's head / tail / tail fill
-  const uint32_t alloc_base = sh.alloc_base;
   for (uint32_t it = gr_take(&sh.next2); it < nlv; it = gr_take(&sh.next2)) {
     const uint32_t lvl = __builtin_amdgcn_readfirstlane(sh.lvlist[it]);
     const uint32_t start = __builtin_amdgcn_readfirstlane(sh.lstart[lvl]);
@@ -2951,12 +3071,13 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
           const unsigned long long a = A0 + (unsigned long long)(tinc - tq), z = a + (unsigned long long)E.qty;
           const uint32_t first = staged ? a_search_lds(mkl, nmk, a, true) : a_search(ag.mk, mk_base, nmk, a, true);
           const uint32_t g = rjs[srec(E.w)] >> AGG_GSHIFT;
-          const uint32_t p = sh.gbase[g] + (x0 - sh.gex[g]);
+          const bool dir = (dmask >> g) & 1u;
+          const uint32_t p = dir ? rbase[srec(E.w)] + x0 : sh.gbase[g] + (x0 - sh.gex[g]);
           me_fill f;
           f.taker_seq = sq;
           f.price_q4 = price;
           f.symbol = sl.gs;
-          me_fill* sc = ga.scratch[g];
+          me_fill* sc = dir ? ga.tape[g] : ga.scratch[g];
           unsigned long long lo = a;
           for (uint32_t k = 0; k < nfl; ++k) {
             const AggMk m = staged ? mkl[first + k] : ag.mk[mk_base + first + k];
@@ -3021,9 +3142,12 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
   GR_STAMP(bk, s, 7);
 }
 
-__global__ __launch_bounds__(GR_THREADS, GR_WPE) void k_agg_gres(BookDev bk, AggGArgs ga, AggSrc src, AggDev ag,
-                                                          uint32_t ne) {
+// k_agg_gres1: phases A-C and the chunk allocation per symbol; the last workgroup to finish turns each direct
+// batch's tile sums into exclusive tile bases (in place) for k_agg_tscan.
+__global__ __launch_bounds__(GR_THREADS, GR_WPE) void k_agg_gres1(BookDev bk, AggGArgs ga, AggSrc src, AggDev ag,
+                                                           uint32_t ne) {
   __shared__ GrShared sh;
+  __shared__ uint32_t last;
   extern __shared__ uint32_t gr_dyn[];  // [ne] fill counts / offsets
   for (uint32_t s = blockIdx.x; s < bk.S; s += gridDim.x) {
     const AggSlot sl = ag.slot[s];
@@ -3033,9 +3157,79 @@ __global__ __launch_bounds__(GR_THREADS, GR_WPE) void k_agg_gres(BookDev bk, Agg
       continue;
     }
     if (sl.ev_cnt <= ne)
-      gres_symbol<true>(bk, ga, src, ag, s, sl, sh, gr_dyn);
+      gres_symbol1<true>(bk, ga, src, ag, s, sl, sh, gr_dyn);
     else
-      gres_symbol<false>(bk, ga, src, ag, s, sl, sh, ag.evn + sl.ev_base);
+      gres_symbol1<false>(bk, ga, src, ag, s, sl, sh, ag.evn + sl.ev_base);
+    __syncthreads();
+  }
+  if (!ga.direct) return;  // (uniform: no device batch in the group)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    last = atomicAdd(ga.ticket, 1u) == gridDim.x - 1u;
+  }
+  __syncthreads();
+  if (!last) return;
+  // every workgroup's tile-sum atomics are done: the tile bases of the direct batches (one wave per batch)
+  const uint32_t hb = ga.ng - min(__hip_atomic_load(&ag.ctr[AC_HB], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), ga.ng);
+  const uint32_t dmask = ga.direct & (hb >= 32u ? ~0u : ((1u << hb) - 1u));
+  const int lane = lane_id(), wv = threadIdx.x >> 6;
+  for (uint32_t g = (uint32_t)wv; g < ga.ng; g += GR_WAVES) {
+    if (!((dmask >> g) & 1u)) continue;
+    uint32_t* ts = ga.tile_sum[g];
+    const uint32_t nt = ga.ntiles[g];
+    uint32_t run = 0;
+    for (uint32_t b = 0; b < nt; b += 64) {
+      const uint32_t t = b + (uint32_t)lane;
+      const uint32_t x = t < nt ? __hip_atomic_load(&ts[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+      const uint32_t inc = (uint32_t)wave_incl_scan((long long)x);
+      if (t < nt) ts[t] = run + inc - x;
+      run += rl32(inc, 63);
+    }
+    if (lane == 0) {
+      *ga.tape_count[g] = run;
+      atomicAdd(ga.fills_acc, (unsigned long long)run);
+    }
+  }
+  if (threadIdx.x == 0) *ga.ticket = 0u;  // ready for the next group
+}
+
+// k_agg_tscan: the direct batches' tape offsets, one wave per 64-record tile: the tile base (k_agg_gres1) plus
+// the exclusive scan of the tile's fill counts; the batch's "tape written" flag.
+__global__ __launch_bounds__(256) void k_agg_tscan(AggGArgs ga, AggDev ag) {
+  const uint32_t hb = ga.ng - min(ag.ctr[AC_HB], ga.ng);
+  const uint32_t dmask = ga.direct & (hb >= 32u ? ~0u : ((1u << hb) - 1u));
+  const int lane = lane_id();
+  const uint32_t w = blockIdx.x * 4u + (threadIdx.x >> 6), nw = gridDim.x * 4u;
+  uint32_t base = 0;  // the first tile of batch g in the flattened tile list
+  for (uint32_t g = 0; g < ga.ng; ++g) {
+    const uint32_t nt = ga.ntiles[g];
+    if ((dmask >> g) & 1u) {
+      me_order_result* res = ga.res[g];
+      const uint32_t n = ga.nrec[g];
+      for (uint32_t t = (w + nw - base % nw) % nw; t < nt; t += nw) {
+        const uint32_t i = t * TILE_TAPE + (uint32_t)lane;
+        const uint32_t c = i < n ? res[i].fill_count : 0u;
+        const uint32_t inc = (uint32_t)wave_incl_scan((long long)c);
+        if (i < n) res[i].tape_offset = ga.tile_sum[g][t] + inc - c;
+      }
+      if (w == 0 && lane == 0) *ga.done[g] = 1u;
+    }
+    base += nt;
+  }
+}
+
+// k_agg_gres2: phase D per symbol (the fills, the surviving rests).
+__global__ __launch_bounds__(GR_THREADS, GR_WPE) void k_agg_gres2(BookDev bk, AggGArgs ga, AggDev ag, uint32_t ne) {
+  __shared__ GrShared sh;
+  extern __shared__ uint32_t gr_dyn[];
+  for (uint32_t s = blockIdx.x; s < bk.S; s += gridDim.x) {
+    const AggSlot sl = ag.slot[s];
+    if (!sl.active || sl.ev_cnt >= 65536u) continue;
+    if (sl.ev_cnt <= ne)
+      gres_symbol2<true>(bk, ga, ag, s, sl, sh, gr_dyn);
+    else
+      gres_symbol2<false>(bk, ga, ag, s, sl, sh, ag.evn + sl.ev_base);
     __syncthreads();
   }
 }
@@ -3065,22 +3259,32 @@ hipError_t launch_agg(hipStream_t hs, const BookDev& bk, const BatchDev& bt, con
 namespace me {
 // A grouped register-window launch through the aggregate path (batches bt[0, ng), all bucketed): the
 // walk, the per-level kernels, the fills; the continuation launch follows (me_kernels.hip).
-hipError_t launch_agg_group(hipStream_t st, const BookDev& bk, const BatchDev* bt, uint32_t ng, const AggDev& ag0) {
+hipError_t launch_agg_group(hipStream_t st, const BookDev& bk, const BatchDev* bt, uint32_t ng, const HotLaunch& hot,
+                            hipEvent_t join) {
   if (!ng || ng > (uint32_t)ME_GMAX || bk.L > 128u) return hipErrorInvalidValue;
-  AggDev ag = ag0;
+  AggDev ag = hot.ag;
   ag.nslots = bk.S;
   AggGArgs ga{};
   AggSrc src{};
+  const DirectTape& dt = hot.dt;
   for (uint32_t g = 0; g < ng; ++g) {
     if (!bt[g].bcnt) return hipErrorInvalidValue;
+    ga.nrec[g] = bt[g].n;
+    ga.ntiles[g] = (bt[g].n + TILE_TAPE - 1) / TILE_TAPE;
     ga.bcnt[g] = bt[g].bcnt;
     ga.b_rec[g] = bt[g].b_rec;
     ga.res[g] = bt[g].res;
     ga.tile_sum[g] = bt[g].tile_sum;
     ga.scratch[g] = bt[g].scratch;
     ga.scratch_top[g] = bt[g].scratch_top;
+    ga.tape[g] = dt.tape[g];
+    ga.tape_count[g] = dt.count[g];
+    ga.done[g] = dt.done[g];
     src.seq[g] = bt[g].seq;
   }
+  ga.direct = dt.ticket ? dt.mask & (ng >= 32u ? ~0u : ((1u << ng) - 1u)) : 0u;
+  ga.fills_acc = dt.fills_acc;
+  ga.ticket = dt.ticket;
   ga.ovf_base = bt[0].ovf_base;
   ga.scratch_cap = bt[0].scratch_cap;
   ga.seq0 = bt[0].seq;
@@ -3096,7 +3300,20 @@ hipError_t launch_agg_group(hipStream_t st, const BookDev& bk, const BatchDev* b
   ne = (ne + 63u) & ~63ull;
   const uint64_t ne_cap = ((64u << 10) - sizeof(GrShared)) / 4u & ~63ull;
   if (ne > ne_cap) ne = ne_cap;
-  hipLaunchKernelGGL(k_agg_gres, dim3(grid), dim3(GR_THREADS), (size_t)ne * 4u, st, bk, ga, src, ag, (uint32_t)ne);
+  hipLaunchKernelGGL(k_agg_gres1, dim3(grid), dim3(GR_THREADS), (size_t)ne * 4u, st, bk, ga, src, ag, (uint32_t)ne);
+  if (ga.direct) {
+    uint32_t tiles = 0;
+    for (uint32_t g = 0; g < ng; ++g) tiles += ga.ntiles[g];
+    const uint32_t tg = (tiles + 3u) / 4u;
+    hipLaunchKernelGGL(k_agg_tscan, dim3(tg < 4096u ? tg : 4096u), dim3(256), 0, st, ga, ag);
+    // the tapes are the engine's per-position buffers: the tape jobs of the group before (on the side
+    // stream) must be done with them before this group's fills land there
+    if (join) {
+      hipError_t e = hipStreamWaitEvent(st, join, 0);
+      if (e != hipSuccess) return e;
+    }
+  }
+  hipLaunchKernelGGL(k_agg_gres2, dim3(grid), dim3(GR_THREADS), (size_t)ne * 4u, st, bk, ga, ag, (uint32_t)ne);
   return hipGetLastError();
 }
 }  // namespace me
