@@ -1118,7 +1118,8 @@ static int run_book(me_cluster* c, const int64_t* hdr, const BookReq* q) {
     rc = c->use_ops && !c->ops.book ? ME_E_INVALID : call(nullptr, 0, &nb, nullptr, 0, &na, nullptr, nullptr, &nbl, &nal);
     if (rc == ME_OK) {
       std::vector<me_book_entry> eb(std::max<size_t>(nb, 1)), ea(std::max<size_t>(na, 1));
-      std::vector<me_level> lb(std::max<size_t>(d, 1)), la(std::max<size_t>(d, 1));
+      // (level buffers as long as the first call's counts: d may be 0xFFFFFFFF, "the whole book")
+      std::vector<me_level> lb(std::max<size_t>(std::min<size_t>(nbl, d), 1)), la(std::max<size_t>(std::min<size_t>(nal, d), 1));
       rc = call(eb.data(), nb, &nb, ea.data(), na, &na, d ? lb.data() : nullptr, d ? la.data() : nullptr, &nbl, &nal);
       nbl = std::min<size_t>(nbl, d);
       nal = std::min<size_t>(nal, d);

@@ -10,7 +10,7 @@ export TMPDIR=/tmp
 cd $R
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo SMOKE_FAIL; tail -20 $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 240 --timeout-method thread > $O/pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 150 --timeout-method thread > $O/pytest_gpu.log 2>&1
 rc=$?; tail -2 $O/pytest_gpu.log
 if [ $rc -ne 0 ]; then
   grep -E "^E |FAILED|Error" $O/pytest_gpu.log | head -30
