@@ -476,10 +476,6 @@ __device__ __forceinline__ void a_walk_end(AWalk& w, AList& A, AList& B, int& bb
 // walk starts only if the book's sum is, and adds every block's quantities to that bound before the
 // block runs (a block that could cross it goes to the generic loop, from its first record on).
 constexpr uint32_t LW_BUY = 1u << 15, LW_MKT = 1u << 16, LW_RJ_SHIFT = 17, LW_LIM = 0x7FFFu;
-#ifndef ME_LW_SEL
-#define ME_LW_SEL 2  // the select walk (1: lw_block_sel; 2: the grouped walk's in hand-scheduled SALU, lw_block_x)
-                     // instead of the side-specific one (0: lw_block)
-#endif
 constexpr unsigned long long LW_CAP = 1ull << 31;
 
 struct LWalk {
@@ -489,11 +485,6 @@ struct LWalk {
   uint32_t cbb, cba; // cached totals of the best levels
   int L;
   unsigned long long ub;  // the book's sum plus the quantities of the blocks walked (< LW_CAP)
-  // the select walk (lw_block_sel): the best levels in SIDE coordinates — u0 = -best bid (1: none), u1 = best
-  // ask (L: none), so "better" is "smaller" on both sides — and their cached totals (0: the level emptied and
-  // the next best is not looked up until a taker needs it); a cached level's LDS word holds 0
-  int u0, u1;
-  uint32_t c0, c1;
 };
 
 // smallest occupied level >= x, or L: a scan of the LDS totals. Only levels on the side being searched
@@ -608,29 +599,6 @@ __device__ __forceinline__ void le_init(LEvG& e, AggGEv* ev, uint32_t eb) {
 }
 __device__ __forceinline__ void le_end(LEvG& e) {
   if (e.evp & 63u) le_store(e, e.evp & ~63u, e.evp & 63u);
-}
-// Conditional events (the select walk): the lanes are written whatever q is, and the log advances only
-// when q != 0 — an empty event's lane is overwritten by the next one. No branch but the block store's.
-__device__ __forceinline__ void le_emit_c(LEv& e, uint32_t lvl, uint32_t j, uint32_t q) {
-  const uint32_t slot = e.evp & 63u;
-  asm volatile(
-      "s_mov_b32 m0, %3\n\tv_writelane_b32 %0, %4, m0\n\tv_writelane_b32 %1, %5, m0\n\tv_writelane_b32 %2, %6, m0"
-      : "+v"(e.vl), "+v"(e.vj), "+v"(e.vq)
-      : "s"(slot), "s"(lvl), "s"(j), "s"(q)
-      : "m0");
-  const uint32_t full = (q != 0u) & (slot == 63u);
-  e.evp += q != 0u;
-  if (ME_UNLIKELY(full)) le_store(e, e.evp - 64u, 64u);
-}
-__device__ __forceinline__ void le_emit_c(LEvG& e, uint32_t lvl, uint32_t j, uint32_t q) {
-  const uint32_t slot = e.evp & 63u;
-  asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %3, m0\n\tv_writelane_b32 %1, %4, m0"
-               : "+v"(e.vw), "+v"(e.vq)
-               : "s"(slot), "s"(lvl | j), "s"(q)
-               : "m0");
-  const uint32_t full = (q != 0u) & (slot == 63u);
-  e.evp += q != 0u;
-  if (ME_UNLIKELY(full)) le_store(e, e.evp - 64u, 64u);
 }
 
 // A taker's partial take from the best level is the common case and stays out of the loop (no loop
@@ -827,297 +795,6 @@ __device__ __forceinline__ uint32_t lw_block(LE& e, LWalk& w, int oq, uint32_t o
   return k;
 }
 
-// ---- the select walk: one record path for both sides, selects instead of branches
-// The side-specific walk above costs ~11 branches per record (side, take / partial / pop, rest same / better /
-// worse, event-block checks) on a chain with one wave per SIMD, where a taken branch is ~20 cycles of nothing
-// (DESIGN.md §4). Here a record loads the state of its OPPOSITE side (the one it takes from) and its OWN side
-// (the one it rests on) by s_cselect, in side coordinates where both sides compare the same way:
-//   take:  crosses while u_opp <= its limit; tk = min(rem, cached total) — a level it empties stays cached
-//          with total 0 and is popped (an LDS scan) only when a taker still has quantity for the side;
-//   rest:  same level as the own best: the cached total grows; better: the old best's total goes to LDS and
-//          the rest becomes the cached best; worse: an LDS add at its level — one LDS add always (lane 0 on
-//          the chosen word, the dummy when there is nothing to add);
-//   events: written to their lanes unconditionally, the log advancing by (q != 0).
-// The only branches on a record's path: the pop loop (a taker that empties the best and has more to take)
-// and the 64-event block stores.
-__device__ __forceinline__ void lw_sel_init(LWalk& w) {
-  // the cached levels' LDS words hold 0 from here on
-  w.u0 = -w.bb;
-  w.u1 = w.ba;
-  w.c0 = w.cbb;
-  w.c1 = w.cba;
-  if (w.bb >= 0) lw_put(w, w.bb, 0u);
-  if (w.ba < w.L) lw_put(w, w.ba, 0u);
-}
-// The cached totals back into LDS, the exact best levels (a lazily emptied best is popped now).
-__device__ __forceinline__ void lw_sel_end(LWalk& w) {
-  int bb = -w.u0, ba = w.u1;
-  if (bb >= 0 && w.c0) lw_put(w, bb, w.c0);
-  if (ba < w.L && w.c1) lw_put(w, ba, w.c1);
-  wave_mem_order();
-  uint32_t t;
-  if (bb >= 0 && !w.c0) bb = lw_prev(w, bb, t);
-  if (ba < w.L && !w.c1) ba = lw_next(w, ba, t);
-  // lw_end puts the cached totals of bb / ba again: they are in LDS already
-  w.bb = bb;
-  w.ba = ba;
-  w.cbb = bb >= 0 ? lw_get(w, bb) : 0u;
-  w.cba = ba < w.L ? lw_get(w, ba) : 0u;
-}
-// one-lane LDS add at level index a (a = L: lane 0's own dummy word — nothing to add)
-__device__ __forceinline__ void lw_add_at(LWalk& w, int a, uint32_t d) {
-  const int lane = lane_id();
-  uint32_t* p = lane == 0 ? &w.tot[a] : &w.dummy[lane];
-  __hip_atomic_fetch_add(p, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-template <int JS, class LE>
-__device__ __forceinline__ uint32_t lw_block_sel(LE& e, LWalk& w, int oq, uint32_t ocw, uint32_t jb,
-                                                 unsigned long long fastm, uint32_t cnt, int& rr) {
-  const unsigned long long upto = (cnt >= 64u ? ~0ull : ((1ull << cnt) - 1ull)) & ~fastm;
-  const uint32_t k = upto ? (uint32_t)__builtin_ctzll(upto) : cnt;
-  const unsigned long long rjm = __ballot((ocw >> LW_RJ_SHIFT) != 0u);
-  unsigned long long work = (k >= 64u ? ~0ull : ((1ull << k) - 1ull)) & ~rjm;
-  const int L = w.L;
-  int rn = 0;
-  uint32_t cwn = 0, oqn = 0;
-  if constexpr (JS == 0) {
-    rn = __builtin_ctzll(work | (1ull << 63));
-    asm volatile("v_readlane_b32 %0, %2, %4\n\tv_readlane_b32 %1, %3, %4" : "=s"(cwn), "=s"(oqn) : "v"(ocw), "v"(oq), "s"(rn));
-  }
-  while (work) {
-    int r;
-    uint32_t cw, rem;
-    if constexpr (JS == 0) {
-      r = rn;
-      asm volatile("s_bitset0_b64 %0, %1" : "+s"(work) : "s"(r));
-      cw = cwn;
-      rem = oqn;
-      rn = __builtin_ctzll(work | (1ull << 63));
-      asm volatile("v_readlane_b32 %0, %2, %4\n\tv_readlane_b32 %1, %3, %4" : "=s"(cwn), "=s"(oqn) : "v"(ocw), "v"(oq), "s"(rn));
-    } else {
-      r = __builtin_ctzll(work);
-      asm volatile("s_bitset0_b64 %0, %1" : "+s"(work) : "s"(r));
-      cw = rl32(ocw, r);
-      rem = (uint32_t)rli32(oq, r);
-    }
-    const uint32_t jt = (jb + (uint32_t)r) << JS;
-    const int lim = (int)(cw & LW_LIM);
-    const bool buy = (cw & LW_BUY) != 0u;
-    // the opposite side (taken from) and the own side (rested on), in side coordinates
-    int uo = buy ? w.u1 : w.u0;
-    uint32_t co = buy ? w.c1 : w.c0;
-    int un = buy ? w.u0 : w.u1;
-    uint32_t cn = buy ? w.c0 : w.c1;
-    const int ulo = buy ? lim : -lim;  // the limit in the opposite side's coordinates (MARKET: the far end)
-    // take from the cached best
-    bool cross = uo <= ulo;
-    uint32_t tk = cross ? min(rem, co) : 0u;
-    co -= tk;
-    rem -= tk;
-    le_emit_c(e, (uint32_t)(buy ? uo : -uo), jt | AGG_TAKE, tk);
-    if (ME_UNLIKELY(cross && rem != 0u)) {  // the best is empty (co == 0) and the taker has more: pop
-      do {
-        uint32_t t;
-        int lv = buy ? lw_next(w, uo + 1, t) : lw_prev(w, -uo - 1, t);
-        if (t) lw_put(w, lv, 0u);  // the new cached best
-        uo = buy ? lv : -lv;
-        co = t;
-        cross = uo <= ulo;
-        tk = cross ? min(rem, co) : 0u;
-        co -= tk;
-        rem -= tk;
-        le_emit_c(e, (uint32_t)lv, jt | AGG_TAKE, tk);
-      } while (cross && rem != 0u);
-    }
-    // rest the LIMIT's remainder (a MARKET's is dropped)
-    uint32_t rq = (cw & LW_MKT) ? 0u : rem;
-    asm volatile("" : "+s"(rq));
-    const int uln = -ulo;  // the limit in the own side's coordinates
-    const bool eq = uln == un, better = uln < un;
-    const int lvn = buy ? -un : un;  // the own best's level
-    // the one LDS add: nothing (rq == 0 or the same level), the evicted best's total, or the rest itself
-    const int a = rq == 0u || eq ? L : (better ? (cn ? lvn : L) : lim);
-    const uint32_t d = better ? cn : rq;
-    lw_add_at(w, a, d);
-    cn = rq == 0u ? cn : (eq ? cn + rq : (better ? rq : cn));
-    un = rq != 0u && better ? uln : un;
-    le_emit_c(e, (uint32_t)lim, jt, rq);
-    w.u1 = buy ? uo : un;
-    w.c1 = buy ? co : cn;
-    w.u0 = buy ? un : uo;
-    w.c0 = buy ? cn : co;
-    asm volatile("s_mov_b32 m0, %1\n\tv_writelane_b32 %0, %2, m0" : "+v"(rr) : "s"(r), "s"(auniu(rem)) : "m0");
-  }
-  return k;
-}
-
-// The grouped walk's record path of lw_block_sel in hand-scheduled SALU (the compiler keeps uniform booleans
-// as 64-bit lane masks and re-tests them against exec at every select — ~40 extra SALU per record): one SCC
-// test feeds each run of s_cselect, arithmetic that clobbers SCC goes first. Same semantics, same events.
-// event lanes of the select walk (m0 = the slot): grouped events {level | record, qty}, the hot path's
-// {level, record, qty}
-__device__ __forceinline__ void le_lanes(LEvG& e, uint32_t slot, uint32_t lvl, uint32_t j, uint32_t q) {
-  asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %3, m0\n\tv_writelane_b32 %1, %4, m0"
-               : "+v"(e.vw), "+v"(e.vq)
-               : "s"(slot), "s"(lvl | j), "s"(q)
-               : "m0");
-}
-__device__ __forceinline__ void le_lanes(LEv& e, uint32_t slot, uint32_t lvl, uint32_t j, uint32_t q) {
-  asm volatile(
-      "s_mov_b32 m0, %3\n\tv_writelane_b32 %0, %4, m0\n\tv_writelane_b32 %1, %5, m0\n\tv_writelane_b32 %2, %6, m0"
-      : "+v"(e.vl), "+v"(e.vj), "+v"(e.vq)
-      : "s"(slot), "s"(lvl), "s"(j), "s"(q)
-      : "m0");
-}
-
-template <int JS, class LE>
-__device__ __forceinline__ uint32_t lw_block_x(LE& e, LWalk& w, int oq, uint32_t ocw, uint32_t jb,
-                                               unsigned long long fastm, uint32_t cnt, int& rr) {
-  const unsigned long long upto = (cnt >= 64u ? ~0ull : ((1ull << cnt) - 1ull)) & ~fastm;
-  const uint32_t k = upto ? (uint32_t)__builtin_ctzll(upto) : cnt;
-  const unsigned long long rjm = __ballot((ocw >> LW_RJ_SHIFT) != 0u);
-  unsigned long long work = (k >= 64u ? ~0ull : ((1ull << k) - 1ull)) & ~rjm;
-  const uint32_t L = auniu((uint32_t)w.L);
-  uint32_t u0 = auniu((uint32_t)w.u0), u1 = auniu((uint32_t)w.u1), c0 = auniu(w.c0), c1 = auniu(w.c1),
-           evp = auniu(e.evp);
-  // config 1's walk (JS = 0) reads the next record's control word and quantity one record ahead (lw_block)
-  int rn = 0;
-  uint32_t cwn = 0, oqn = 0;
-  if constexpr (JS == 0) {
-    rn = __builtin_ctzll(work | (1ull << 63));
-    asm volatile("v_readlane_b32 %0, %2, %4\n\tv_readlane_b32 %1, %3, %4" : "=s"(cwn), "=s"(oqn) : "v"(ocw), "v"(oq), "s"(rn));
-  }
-  while (work) {
-    int r;
-    uint32_t cw, rem;
-    if constexpr (JS == 0) {
-      r = rn;
-      asm volatile("s_bitset0_b64 %0, %1" : "+s"(work) : "s"(r));
-      cw = cwn;
-      rem = oqn;
-      rn = __builtin_ctzll(work | (1ull << 63));
-      asm volatile("v_readlane_b32 %0, %2, %4\n\tv_readlane_b32 %1, %3, %4" : "=s"(cwn), "=s"(oqn) : "v"(ocw), "v"(oq), "s"(rn));
-    } else {
-      r = __builtin_ctzll(work);
-      asm volatile("s_bitset0_b64 %0, %1" : "+s"(work) : "s"(r));
-      cw = rl32(ocw, r);
-      rem = (uint32_t)rli32(oq, r);
-    }
-    const uint32_t jt = (jb + (uint32_t)r) << JS;
-    const uint32_t jtt = jt | AGG_TAKE;
-    uint32_t uo, co, un, cn, ulo, lim, lvo, fl, pp, tk, slot;
-    // side select and the take from the cached best (its event's lanes written whatever tk is; the log
-    // advances by tk != 0)
-    asm volatile(
-        "s_and_b32 %[lim], %[cw], 0x7fff\n\t"
-        "s_sub_i32 %[tk], 0, %[lim]\n\t"
-        "s_sub_i32 %[slot], 0, %[u0]\n\t"
-        "s_bitcmp1_b32 %[cw], 15\n\t"  // SCC = BUY
-        "s_cselect_b32 %[uo], %[u1], %[u0]\n\t"
-        "s_cselect_b32 %[co], %[c1], %[c0]\n\t"
-        "s_cselect_b32 %[un], %[u0], %[u1]\n\t"
-        "s_cselect_b32 %[cn], %[c0], %[c1]\n\t"
-        "s_cselect_b32 %[ulo], %[lim], %[tk]\n\t"  // the limit in the opposite side's coordinates
-        "s_cselect_b32 %[lvo], %[u1], %[slot]\n\t" // the opposite best's level
-        "s_min_u32 %[tk], %[rem], %[co]\n\t"
-        "s_cmp_le_i32 %[uo], %[ulo]\n\t"  // SCC = crosses
-        "s_cselect_b32 %[tk], %[tk], 0\n\t"
-        "s_sub_u32 %[co], %[co], %[tk]\n\t"
-        "s_sub_u32 %[rem], %[rem], %[tk]\n\t"
-        "s_cmp_le_i32 %[uo], %[ulo]\n\t"
-        "s_cselect_b32 %[pp], %[rem], 0\n\t"  // != 0: crosses with more to take (the best is empty): pop
-        "s_and_b32 %[slot], %[evp], 63\n\t"
-        "s_cmp_eq_u32 %[slot], 63\n\t"
-        "s_cselect_b32 %[fl], %[tk], 0\n\t"  // != 0: this event fills the staged block
-        "s_cmp_lg_u32 %[tk], 0\n\t"
-        "s_addc_u32 %[evp], %[evp], 0"
-        : [uo] "=&s"(uo), [co] "=&s"(co), [un] "=&s"(un), [cn] "=&s"(cn), [ulo] "=&s"(ulo), [lim] "=&s"(lim),
-          [lvo] "=&s"(lvo), [fl] "=&s"(fl), [pp] "=&s"(pp), [tk] "=&s"(tk), [slot] "=&s"(slot), [rem] "+s"(rem),
-          [evp] "+s"(evp)
-        : [cw] "s"(cw), [u0] "s"(u0), [u1] "s"(u1), [c0] "s"(c0), [c1] "s"(c1)
-        : "scc");
-    le_lanes(e, slot, lvo, jtt, tk);
-    if (ME_UNLIKELY(fl != 0u)) le_store(e, evp - 64u, 64u);
-    if (ME_UNLIKELY(pp != 0u)) {  // the cached best is empty and the taker has more: pop
-      const bool buy = (cw & LW_BUY) != 0u;
-      bool cross;
-      e.evp = evp;
-      do {
-        uint32_t t;
-        const int lv = buy ? lw_next(w, (int)uo + 1, t) : lw_prev(w, -(int)uo - 1, t);
-        if (t) lw_put(w, lv, 0u);  // the new cached best: its LDS word holds 0
-        uo = buy ? (uint32_t)lv : (uint32_t)(-lv);
-        co = t;
-        cross = (int)uo <= (int)ulo;
-        const uint32_t tq = cross ? min(rem, co) : 0u;
-        co -= tq;
-        rem -= tq;
-        le_emit_c(e, (uint32_t)lv, jtt, tq);
-      } while (cross && rem != 0u);
-      evp = e.evp;
-    }
-    // the rest (a MARKET's remainder is dropped): at the own best (its cached total grows), better (the old
-    // best's total goes to its LDS word, the rest is the new cached best) or worse (an LDS add at its level);
-    // one LDS add always — a = L is the dummy word
-    uint32_t a, d, rq, tq, tw, tb;
-    asm volatile(
-        "s_sub_i32 %[tq], 0, %[ulo]\n\t"  // the limit in the own side's coordinates
-        "s_sub_i32 %[tw], 0, %[un]\n\t"
-        "s_bitcmp1_b32 %[cw], 15\n\t"
-        "s_cselect_b32 %[tw], %[tw], %[un]\n\t"  // the own best's level
-        "s_cmp_lg_u32 %[cn], 0\n\t"
-        "s_cselect_b32 %[a], %[tw], %[L]\n\t"  // where an evicted best's total goes
-        "s_bitcmp1_b32 %[cw], 16\n\t"  // SCC = MARKET
-        "s_cselect_b32 %[rq], 0, %[rem]\n\t"
-        "s_cmp_eq_u32 %[tq], %[un]\n\t"
-        "s_cselect_b32 %[tw], %[rq], 0\n\t"  // at the own best
-        "s_cmp_lt_i32 %[tq], %[un]\n\t"
-        "s_cselect_b32 %[tb], %[rq], 0\n\t"  // better than the own best
-        "s_add_u32 %[d], %[cn], %[tw]\n\t"
-        "s_sub_u32 %[tw], %[rq], %[tw]\n\t"
-        "s_sub_u32 %[tw], %[tw], %[tb]\n\t"  // worse: the rest's quantity
-        "s_cmp_lg_u32 %[tb], 0\n\t"  // SCC = a better rest
-        "s_cselect_b32 %[un], %[tq], %[un]\n\t"
-        "s_cselect_b32 %[tq], %[cn], %[tw]\n\t"  // the LDS add's value
-        "s_cselect_b32 %[cn], %[tb], %[d]\n\t"
-        "s_cselect_b32 %[d], %[a], %[L]\n\t"
-        "s_cmp_lg_u32 %[tw], 0\n\t"
-        "s_cselect_b32 %[a], %[lim], %[d]\n\t"  // the LDS add's level
-        "s_mov_b32 %[d], %[tq]"
-        : [a] "=&s"(a), [d] "=&s"(d), [rq] "=&s"(rq), [tq] "=&s"(tq), [tw] "=&s"(tw), [tb] "=&s"(tb), [un] "+s"(un),
-          [cn] "+s"(cn)
-        : [cw] "s"(cw), [rem] "s"(rem), [ulo] "s"(ulo), [lim] "s"(lim), [L] "s"(L)
-        : "scc");
-    lw_add_at(w, (int)a, d);
-    uint32_t fl2, slot2;
-    asm volatile(
-        "s_and_b32 %[slot], %[evp], 63\n\t"
-        "s_cmp_eq_u32 %[slot], 63\n\t"
-        "s_cselect_b32 %[fl], %[rq], 0\n\t"
-        "s_cmp_lg_u32 %[rq], 0\n\t"
-        "s_addc_u32 %[evp], %[evp], 0\n\t"
-        "s_bitcmp1_b32 %[cw], 15\n\t"  // the state back
-        "s_cselect_b32 %[u1], %[uo], %[un]\n\t"
-        "s_cselect_b32 %[c1], %[co], %[cn]\n\t"
-        "s_cselect_b32 %[u0], %[un], %[uo]\n\t"
-        "s_cselect_b32 %[c0], %[cn], %[co]"
-        : [fl] "=&s"(fl2), [slot] "=&s"(slot2), [evp] "+s"(evp), [u0] "+s"(u0), [u1] "+s"(u1), [c0] "+s"(c0),
-          [c1] "+s"(c1)
-        : [cw] "s"(cw), [rq] "s"(rq), [uo] "s"(uo), [co] "s"(co), [un] "s"(un), [cn] "s"(cn)
-        : "scc");
-    le_lanes(e, slot2, (uint32_t)lim, jt, rq);
-    asm volatile("s_mov_b32 m0, %1\n\tv_writelane_b32 %0, %2, m0" : "+v"(rr) : "s"(r), "s"(rem) : "m0");
-    if (ME_UNLIKELY(fl2 != 0u)) le_store(e, evp - 64u, 64u);
-  }
-  w.u0 = (int)u0;
-  w.u1 = (int)u1;
-  w.c0 = c0;
-  w.c1 = c1;
-  e.evp = evp;
-  return k;
-}
-
 // A record's result from its fields and the remainder the chain left (vector form); fill count and
 // scratch start come later (k_agg_fin / k_agg_gres, from the log).
 __device__ __forceinline__ me_order_result a_result(int oq, uint32_t okd, uint32_t rj, int rem) {
@@ -1207,7 +884,6 @@ __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const Agg
   LEv le;
   le_init(le, ag, eb);
   const bool ladder = L <= (int)ag.ladder_max && lw_init(lw, bk, s, ltot, bb0, ba0);
-  if (ME_LW_SEL && ladder) lw_sel_init(lw);
   if (!ladder) {
     a_rebuild<1>(w, A, ba0);
     a_rebuild<0>(w, B, L - 1 - bb0);
@@ -1247,9 +923,7 @@ __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const Agg
     uint32_t k;
     if (ladder) {
       const bool adm = lw_admit(lw, v ? oq : 0);  // else: the generic loop from this block on
-      k = ME_LW_SEL == 2 ? lw_block_x<0>(le, lw, oq, lw_cw(okd, olm, rj, L), blk, adm ? fastm : 0ull, cntb, rr)
-          : ME_LW_SEL    ? lw_block_sel<0>(le, lw, oq, lw_cw(okd, olm, rj, L), blk, adm ? fastm : 0ull, cntb, rr)
-                    : lw_block<0>(le, lw, oq, lw_cw(okd, olm, rj, L), blk, adm ? fastm : 0ull, cntb, rr);
+      k = lw_block<0>(le, lw, oq, lw_cw(okd, olm, rj, L), blk, adm ? fastm : 0ull, cntb, rr);
     } else {
       a_refill(w, A, B);
       ARes R;
@@ -1269,7 +943,6 @@ __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const Agg
   if (ladder) {
     le_end(le);
     w.evp = le.evp;
-    if (ME_LW_SEL) lw_sel_end(lw);
     lw_end(lw, bk, s);
     bb = lw.bb;
     ba = lw.ba;
@@ -2088,7 +1761,6 @@ __global__ __launch_bounds__(256) void k_agg_out(BookDev bk, BatchDev bt, AggDev
 // does not cover (a cancel, a price outside the window, a bucket past BK_CAP records) hands the symbol's
 // rest of the group to k_match_reg's continuation launch (me_match_reg.hip, kSlow).
 struct AggGArgs {
-  uint32_t nrec[ME_GMAX], ntiles[ME_GMAX];  // records and tape tiles of batch g
   uint32_t* bcnt[ME_GMAX];
   const BkRec* b_rec[ME_GMAX];
   me_order_result* res[ME_GMAX];
@@ -2098,14 +1770,6 @@ struct AggGArgs {
   unsigned long long ovf_base, scratch_cap;
   const uint64_t* seq0;  // the group's first record's seq (k_agg_gres: events carry their seq's offset from it)
   uint32_t slab, ng;
-  // the direct tape (device batches before the group's first hand-off): k_agg_gres2 writes their fills at
-  // their tape positions, k_agg_tscan having turned the fill counts into tape offsets
-  me_fill* tape[ME_GMAX];
-  unsigned long long* tape_count[ME_GMAX];
-  uint32_t* done[ME_GMAX];        // the output set's "tape written" flag (the tape job skips the batch)
-  unsigned long long* fills_acc;
-  uint32_t* ticket;               // k_agg_gres1's last-workgroup counter (the tile scans)
-  uint32_t direct;                // bit g: batch g is a device batch (its tape may be written directly)
 };
 
 // Ascending bitonic sort of 64 (one register) / 128 (two) distinct keys across the wave; partners over
@@ -2217,7 +1881,6 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
                                                           // symbol goes to the continuation
       const uint32_t g0 = (uint32_t)__builtin_ctzll(__ballot(nsv != 0u));
       a_ghand(bk, s, g0, 0u, rl32(nsv, (int)g0), s * ga.slab, s * ga.slab + ga.slab);
-      if (lane == 0) atomicMax(&ag.ctr[AC_HB], ng - g0);  // (no direct tape from this batch on)
       continue;
     }
     // free chunks k_match_reg parked in fcache[s][0, nfree) join the front of the free list (one header
@@ -2241,7 +1904,6 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
     uint32_t rbase = 0;
     LWalk lw;
     const bool lok = lw_init(lw, bk, s, ltot, bb0, ba0);  // else: the continuation from the first record
-    if (ME_LW_SEL && lok) lw_sel_init(lw);
     uint32_t hidx = NIL, gstop = ng;
     // a batch's bucket is loaded while the batch before it runs (no HBM round trip between batches)
     // (only the lanes of the bucket's records load: a 128-slot bucket holds ~64 at config 2)
@@ -2261,7 +1923,6 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
       if (!cnt) continue;
       if (cnt > (uint32_t)BK_CAP) {  // an overfull bucket: the continuation rescans the batch
         hidx = a_ghand(bk, s, g, 0u, cnt, 0u, 0u);
-        if (lane == 0) atomicMax(&ag.ctr[AC_HB], ng - g);
         gstop = g;
         break;
       }
@@ -2303,10 +1964,8 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
           rjs[rbase + (uint32_t)lane] = (g << AGG_GSHIFT) | oi;
         }
         GW_T(1);
-        const uint32_t k =
-            ME_LW_SEL == 2 ? lw_block_x<AGG_GREC_SHIFT>(w, lw, oq, lw_cw(okd, olm, rj, L), rbase, adm ? fastm : 0ull, cntb, rr)
-            : ME_LW_SEL ? lw_block_sel<AGG_GREC_SHIFT>(w, lw, oq, lw_cw(okd, olm, rj, L), rbase, adm ? fastm : 0ull, cntb, rr)
-                      : lw_block<AGG_GREC_SHIFT>(w, lw, oq, lw_cw(okd, olm, rj, L), rbase, adm ? fastm : 0ull, cntb, rr);
+        const uint32_t k = lw_block<AGG_GREC_SHIFT>(w, lw, oq, lw_cw(okd, olm, rj, L), rbase, adm ? fastm : 0ull,
+                                                     cntb, rr);
         rbase += cntb;
         GW_T(2);
 #ifdef ME_STAMPS
@@ -2315,7 +1974,6 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
         if (v && (uint32_t)lane < k) res[oi] = a_result(oq, okd, rj, rr);  // fills: k_agg_gres
         if (k < cntb) {
           hidx = a_ghand(bk, s, g, blk + k, cnt, 0u, 0u);  // scratch position: k_agg_gres
-          if (lane == 0) atomicMax(&ag.ctr[AC_HB], ng - g);
           stop = true;
           break;
         }
@@ -2330,7 +1988,6 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
       *a_gtab(ag.gev, s, g) = eb + w.evp;
     if (gstop < ng && lane == 0) *a_gtab(ag.gev, s, gstop + 1u) = eb + w.evp;
     le_end(w);
-    if (ME_LW_SEL && lok) lw_sel_end(lw);
     if (lok) lw_end(lw, bk, s);  // (else the LDS copy is truncated and nothing was walked)
     const int bb = lw.bb, ba = lw.ba;
     if (lane == 0) {
@@ -2378,6 +2035,10 @@ constexpr uint32_t GR_THREADS = GR_WAVES * 64;
 #endif
 constexpr uint32_t GR_STAGE = 48;  // consumed makers / emptied chunks a level stages in LDS (else: HBM)
 
+struct GrLevel {  // what phase B found for one level
+  unsigned long long C, T0;
+  uint32_t newhead, mk_base, nmk, fr_base, nfreed, need, d_off, ks;
+};
 struct GrStage {  // a wave's maker / emptied-chunk staging (phases B and D)
   AggMk mk[GR_STAGE];
   uint32_t fr[GR_STAGE];
@@ -2394,7 +2055,6 @@ struct GrShared {
   uint32_t gev[ME_GMAX + 1], gex[ME_GMAX + 1], gbase[ME_GMAX + 1];
   uint32_t wsum[GR_WAVES];
   uint32_t nlv, next, next2, cur_mk, cur_fr, deficit, alloc_base;
-  uint32_t dmask;  // bit g: batch g's fills go straight to its tape
   int dresting;
   uint8_t ltend[128];
 };
@@ -2407,8 +2067,8 @@ __device__ __forceinline__ uint32_t gr_take(uint32_t* ctr) {
 }
 
 template <bool kLds>
-__device__ __forceinline__ void gres_symbol1(const BookDev& bk, const AggGArgs& ga, const AggSrc& src, const AggDev& ag,
-                                             uint32_t s, const AggSlot& sl, GrShared& sh, uint32_t* nf) {
+__device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& ga, const AggSrc& src, const AggDev& ag,
+                                            uint32_t s, const AggSlot& sl, GrShared& sh, uint32_t* nf) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint32_t L = bk.L;  // <= 128
   const uint32_t eb = sl.ev_base, n = sl.ev_cnt, ng = ga.ng;
@@ -2435,10 +2095,6 @@ __device__ __forceinline__ void gres_symbol1(const BookDev& bk, const AggGArgs& 
     sh.next = sh.next2 = 0u;
     sh.cur_mk = sh.cur_fr = sh.deficit = 0u;
     sh.dresting = 0;
-    // the batches before the group's first hand-off (a continuation's fills go to scratch behind the walk's
-    // of their batch) whose tapes are the engine's: their fills go straight to the tape
-    const uint32_t hb = ng - min(ag.ctr[AC_HB], ng);
-    sh.dmask = ga.direct & (hb >= 32u ? ~0u : ((1u << hb) - 1u));
   }
   sh.u.wh[wv][lane] = 0u;
   sh.u.wh[wv][64 + lane] = 0u;
@@ -2780,13 +2436,12 @@ __device__ __forceinline__ void gres_symbol1(const BookDev& bk, const AggGArgs& 
   }
   __syncthreads();
   auto EX = [&](uint32_t e) -> uint32_t { return e < n ? nf[e] : ftot; };
-  const uint32_t dmask = sh.dmask;
   if ((uint32_t)tid < ng) {  // each batch's fills: the symbol's slab of that batch if they fit, else overflow
     const uint32_t g = (uint32_t)tid;
     const uint32_t x0 = EX(sh.gev[g]), x1 = EX(sh.gev[g + 1]);
     const uint32_t f = x1 - x0;
     unsigned long long b0 = (unsigned long long)s * ga.slab;
-    if (f > ga.slab && !((dmask >> g) & 1u)) {  // (a direct batch's fills need no scratch)
+    if (f > ga.slab) {
       b0 = ga.ovf_base + atomicAdd(ga.scratch_top[g], (unsigned long long)f);
       if (b0 + f > ga.scratch_cap) {
         atomicOr(bk.err, ERR_SCRATCH_OOM);
@@ -2821,7 +2476,7 @@ __device__ __forceinline__ void gres_symbol1(const BookDev& bk, const AggGArgs& 
         const uint32_t x0 = EX(e), nfill = EX(e + nte) - x0;
         me_order_result* res = ga.res[g];
         res[oi].fill_count = nfill;
-        if (!((dmask >> g) & 1u)) res[oi].tape_offset = sh.gbase[g] + (x0 - sh.gex[g]);  // (direct: k_agg_tscan)
+        res[oi].tape_offset = sh.gbase[g] + (x0 - sh.gex[g]);
         if (nfill) atomicAdd(&ga.tile_sum[g][oi / TILE_TAPE], nfill);
       }
     }
@@ -2922,116 +2577,10 @@ __device__ __forceinline__ void gres_symbol1(const BookDev& bk, const AggGArgs& 
   }
   __syncthreads();
   GR_STAMP(bk, s, 6);
-  // ---- hand-off to k_agg_gres2: the level state, the batches' fill bases, the fill offsets
-  GrSave* sv = ag.gsave + s;
-  const uint32_t nlv2 = sh.nlv;
-  for (uint32_t i = tid; i < 129u; i += GR_THREADS) sv->lstart[i] = sh.lstart[i];
-  for (uint32_t i = tid; i < L; i += GR_THREADS) {
-    sv->lhead[i] = sh.lhead[i];
-    sv->ltail[i] = sh.ltail[i];
-    sv->ltend[i] = sh.ltend[i];
-  }
-  for (uint32_t i = tid; i < nlv2; i += GR_THREADS) {
-    const uint32_t l = sh.lvlist[i];
-    sv->lvlist[i] = l;
-    sv->lv[l] = sh.lv[l];
-  }
-  for (uint32_t i = tid; i <= ng; i += GR_THREADS) {
-    sv->gex[i] = sh.gex[i];
-    sv->gbase[i] = sh.gbase[i];
-  }
-  if (tid == 0) {
-    sv->nlv = nlv2;
-    sv->alloc_base = sh.alloc_base;
-    sv->pad[0] = sh.dmask;
-    sv->pad[1] = ftot;
-  }
-  if constexpr (kLds) {  // the fill offsets (LDS) to the log's HBM array
-    uint32_t* hn = ag.evn + eb;
-    for (uint32_t i = tid; i < n; i += GR_THREADS) hn[i] = nf[i];
-  }
-}
-
-// Phase D of a symbol (k_agg_gres2), from k_agg_gres1's hand-off: the fills of each level's takes — a direct
-// batch's at its tape position (k_agg_tscan's record offset + the take's place among the record's fills), a
-// scratch batch's in its scratch run — and the surviving rests.
-template <bool kLds>
-__device__ __forceinline__ void gres_symbol2(const BookDev& bk, const AggGArgs& ga, const AggDev& ag, uint32_t s,
-                                             const AggSlot& sl, GrShared& sh, uint32_t* nf) {
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const uint32_t L = bk.L;
-  const uint32_t eb = sl.ev_base, n = sl.ev_cnt, ng = ga.ng;
-  const AggGEv* ev = reinterpret_cast<const AggGEv*>(ag.ev + eb);
-  const uint32_t* rsq = reinterpret_cast<const uint32_t*>(ev + sl.lo);
-  const uint32_t* rjs = rsq + sl.hi;
-  AggGEv* const srt = reinterpret_cast<AggGEv*>(ag.evq + eb);
-  auto srec = [](uint32_t w) -> uint32_t { return (w >> 16) & 0x7FFFu; };
-  const size_t lo_l = (size_t)s * L;
-  const unsigned long long gmin = *ga.seq0;
-  const GrSave* sv = ag.gsave + s;
-  for (uint32_t i = tid; i < 129u; i += GR_THREADS) sh.lstart[i] = sv->lstart[i];
-  for (uint32_t i = tid; i < L; i += GR_THREADS) {
-    sh.lhead[i] = sv->lhead[i];
-    sh.ltail[i] = sv->ltail[i];
-    sh.ltend[i] = sv->ltend[i];
-  }
-  const uint32_t nlv = sv->nlv;
-  for (uint32_t i = tid; i < nlv; i += GR_THREADS) {
-    const uint32_t l = sv->lvlist[i];
-    sh.lvlist[i] = l;
-    sh.lv[l] = sv->lv[l];
-  }
-  for (uint32_t i = tid; i <= ng; i += GR_THREADS) {
-    sh.gex[i] = sv->gex[i];
-    sh.gbase[i] = sv->gbase[i];
-  }
-  if constexpr (kLds) {
-    const uint32_t* hn = ag.evn + eb;
-    for (uint32_t i = tid; i < n; i += GR_THREADS) nf[i] = hn[i];
-  }
-  if (tid == 0) sh.next2 = 0u;
-  const uint32_t dmask = sv->pad[0];
-  const uint32_t ftot_n = n;  // (EX past the log's end: the symbol's fill total, nf's exclusive scan end)
-  __syncthreads();
-  const uint32_t ftot = sv->pad[1];
-  auto EX = [&](uint32_t e) -> uint32_t { return e < ftot_n ? nf[e] : ftot; };
-  // each direct record's fill base: its tape offset (k_agg_tscan) less its first take event's fill offset,
-  // so a take event's fills start at base + nf[event]; in the records' HBM array beside the log
-  uint32_t* rbase = ag.evx + eb;
-  if (dmask) {
-    const uint32_t per = ((n + GR_WAVES - 1u) / GR_WAVES + 63u) & ~63u;
-    const uint32_t r0 = min(n, (uint32_t)wv * per), r1 = min(n, r0 + per);
-    uint32_t prevj = r0 > 0 && r0 < r1 ? auniu(ev[r0 - 1].w >> AGG_GREC_SHIFT) : NIL;
-    for (uint32_t b = r0; b < r1; b += 64) {
-      const uint32_t e = b + (uint32_t)lane;
-      const bool v = e < r1;
-      const uint32_t j = v ? ev[e].w >> AGG_GREC_SHIFT : NIL;
-      uint32_t pj = (uint32_t)__shfl_up((int)j, 1, 64);
-      pj = lane == 0 ? prevj : pj;
-      prevj = rl32(j, 63);
-      if (v && (j & (AGG_TAKE >> AGG_GREC_SHIFT)) && pj != j) {
-        const uint32_t r = j & ~(AGG_TAKE >> AGG_GREC_SHIFT);
-        const uint32_t gp = rjs[r];
-        const uint32_t g = gp >> AGG_GSHIFT, oi = gp & AGG_IMASK;
-        if ((dmask >> g) & 1u) rbase[r] = ga.res[g][oi].tape_offset - EX(e);
-      }
-    }
-  }
-  __syncthreads();
-  AggMk* mkl = sh.u.st[wv].mk;
-  auto entry = [&](uint32_t start, uint32_t cnt, uint32_t b, uint32_t& er) -> AggGEv {
-    AggGEv E{};
-    er = 0;
-    if (b + (uint32_t)lane < cnt) {
-      E = srt[start + b + lane];
-      er = E.w & 0xFFFFu;
-    }
-    return E;
-  };
-  const uint32_t alloc_base = sv->alloc_base;
   // ---- D: per level, one pass over its events: the fills of its takes (makers overlapping each take's
   //      interval, at the record's scratch position) and its surviving rests into the tail chunk and new
   //      chunks; the new chunks' headers, the level's head / tail / tail fill
+  const uint32_t alloc_base = sh.alloc_base;
   for (uint32_t it = gr_take(&sh.next2); it < nlv; it = gr_take(&sh.next2)) {
     const uint32_t lvl = __builtin_amdgcn_readfirstlane(sh.lvlist[it]);
     const uint32_t start = __builtin_amdgcn_readfirstlane(sh.lstart[lvl]);
@@ -3071,13 +2620,12 @@ __device__ __forceinline__ void gres_symbol2(const BookDev& bk, const AggGArgs& 
           const unsigned long long a = A0 + (unsigned long long)(tinc - tq), z = a + (unsigned long long)E.qty;
           const uint32_t first = staged ? a_search_lds(mkl, nmk, a, true) : a_search(ag.mk, mk_base, nmk, a, true);
           const uint32_t g = rjs[srec(E.w)] >> AGG_GSHIFT;
-          const bool dir = (dmask >> g) & 1u;
-          const uint32_t p = dir ? rbase[srec(E.w)] + x0 : sh.gbase[g] + (x0 - sh.gex[g]);
+          const uint32_t p = sh.gbase[g] + (x0 - sh.gex[g]);
           me_fill f;
           f.taker_seq = sq;
           f.price_q4 = price;
           f.symbol = sl.gs;
-          me_fill* sc = dir ? ga.tape[g] : ga.scratch[g];
+          me_fill* sc = ga.scratch[g];
           unsigned long long lo = a;
           for (uint32_t k = 0; k < nfl; ++k) {
             const AggMk m = staged ? mkl[first + k] : ag.mk[mk_base + first + k];
@@ -3142,12 +2690,9 @@ __device__ __forceinline__ void gres_symbol2(const BookDev& bk, const AggGArgs& 
   GR_STAMP(bk, s, 7);
 }
 
-// k_agg_gres1: phases A-C and the chunk allocation per symbol; the last workgroup to finish turns each direct
-// batch's tile sums into exclusive tile bases (in place) for k_agg_tscan.
-__global__ __launch_bounds__(GR_THREADS, GR_WPE) void k_agg_gres1(BookDev bk, AggGArgs ga, AggSrc src, AggDev ag,
-                                                           uint32_t ne) {
+__global__ __launch_bounds__(GR_THREADS, GR_WPE) void k_agg_gres(BookDev bk, AggGArgs ga, AggSrc src, AggDev ag,
+                                                          uint32_t ne) {
   __shared__ GrShared sh;
-  __shared__ uint32_t last;
   extern __shared__ uint32_t gr_dyn[];  // [ne] fill counts / offsets
   for (uint32_t s = blockIdx.x; s < bk.S; s += gridDim.x) {
     const AggSlot sl = ag.slot[s];
@@ -3157,79 +2702,9 @@ __global__ __launch_bounds__(GR_THREADS, GR_WPE) void k_agg_gres1(BookDev bk, Ag
       continue;
     }
     if (sl.ev_cnt <= ne)
-      gres_symbol1<true>(bk, ga, src, ag, s, sl, sh, gr_dyn);
+      gres_symbol<true>(bk, ga, src, ag, s, sl, sh, gr_dyn);
     else
-      gres_symbol1<false>(bk, ga, src, ag, s, sl, sh, ag.evn + sl.ev_base);
-    __syncthreads();
-  }
-  if (!ga.direct) return;  // (uniform: no device batch in the group)
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    last = atomicAdd(ga.ticket, 1u) == gridDim.x - 1u;
-  }
-  __syncthreads();
-  if (!last) return;
-  // every workgroup's tile-sum atomics are done: the tile bases of the direct batches (one wave per batch)
-  const uint32_t hb = ga.ng - min(__hip_atomic_load(&ag.ctr[AC_HB], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), ga.ng);
-  const uint32_t dmask = ga.direct & (hb >= 32u ? ~0u : ((1u << hb) - 1u));
-  const int lane = lane_id(), wv = threadIdx.x >> 6;
-  for (uint32_t g = (uint32_t)wv; g < ga.ng; g += GR_WAVES) {
-    if (!((dmask >> g) & 1u)) continue;
-    uint32_t* ts = ga.tile_sum[g];
-    const uint32_t nt = ga.ntiles[g];
-    uint32_t run = 0;
-    for (uint32_t b = 0; b < nt; b += 64) {
-      const uint32_t t = b + (uint32_t)lane;
-      const uint32_t x = t < nt ? __hip_atomic_load(&ts[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-      const uint32_t inc = (uint32_t)wave_incl_scan((long long)x);
-      if (t < nt) ts[t] = run + inc - x;
-      run += rl32(inc, 63);
-    }
-    if (lane == 0) {
-      *ga.tape_count[g] = run;
-      atomicAdd(ga.fills_acc, (unsigned long long)run);
-    }
-  }
-  if (threadIdx.x == 0) *ga.ticket = 0u;  // ready for the next group
-}
-
-// k_agg_tscan: the direct batches' tape offsets, one wave per 64-record tile: the tile base (k_agg_gres1) plus
-// the exclusive scan of the tile's fill counts; the batch's "tape written" flag.
-__global__ __launch_bounds__(256) void k_agg_tscan(AggGArgs ga, AggDev ag) {
-  const uint32_t hb = ga.ng - min(ag.ctr[AC_HB], ga.ng);
-  const uint32_t dmask = ga.direct & (hb >= 32u ? ~0u : ((1u << hb) - 1u));
-  const int lane = lane_id();
-  const uint32_t w = blockIdx.x * 4u + (threadIdx.x >> 6), nw = gridDim.x * 4u;
-  uint32_t base = 0;  // the first tile of batch g in the flattened tile list
-  for (uint32_t g = 0; g < ga.ng; ++g) {
-    const uint32_t nt = ga.ntiles[g];
-    if ((dmask >> g) & 1u) {
-      me_order_result* res = ga.res[g];
-      const uint32_t n = ga.nrec[g];
-      for (uint32_t t = (w + nw - base % nw) % nw; t < nt; t += nw) {
-        const uint32_t i = t * TILE_TAPE + (uint32_t)lane;
-        const uint32_t c = i < n ? res[i].fill_count : 0u;
-        const uint32_t inc = (uint32_t)wave_incl_scan((long long)c);
-        if (i < n) res[i].tape_offset = ga.tile_sum[g][t] + inc - c;
-      }
-      if (w == 0 && lane == 0) *ga.done[g] = 1u;
-    }
-    base += nt;
-  }
-}
-
-// k_agg_gres2: phase D per symbol (the fills, the surviving rests).
-__global__ __launch_bounds__(GR_THREADS, GR_WPE) void k_agg_gres2(BookDev bk, AggGArgs ga, AggDev ag, uint32_t ne) {
-  __shared__ GrShared sh;
-  extern __shared__ uint32_t gr_dyn[];
-  for (uint32_t s = blockIdx.x; s < bk.S; s += gridDim.x) {
-    const AggSlot sl = ag.slot[s];
-    if (!sl.active || sl.ev_cnt >= 65536u) continue;
-    if (sl.ev_cnt <= ne)
-      gres_symbol2<true>(bk, ga, ag, s, sl, sh, gr_dyn);
-    else
-      gres_symbol2<false>(bk, ga, ag, s, sl, sh, ag.evn + sl.ev_base);
+      gres_symbol<false>(bk, ga, src, ag, s, sl, sh, ag.evn + sl.ev_base);
     __syncthreads();
   }
 }
@@ -3259,32 +2734,22 @@ hipError_t launch_agg(hipStream_t hs, const BookDev& bk, const BatchDev& bt, con
 namespace me {
 // A grouped register-window launch through the aggregate path (batches bt[0, ng), all bucketed): the
 // walk, the per-level kernels, the fills; the continuation launch follows (me_kernels.hip).
-hipError_t launch_agg_group(hipStream_t st, const BookDev& bk, const BatchDev* bt, uint32_t ng, const HotLaunch& hot,
-                            hipEvent_t join) {
+hipError_t launch_agg_group(hipStream_t st, const BookDev& bk, const BatchDev* bt, uint32_t ng, const AggDev& ag0) {
   if (!ng || ng > (uint32_t)ME_GMAX || bk.L > 128u) return hipErrorInvalidValue;
-  AggDev ag = hot.ag;
+  AggDev ag = ag0;
   ag.nslots = bk.S;
   AggGArgs ga{};
   AggSrc src{};
-  const DirectTape& dt = hot.dt;
   for (uint32_t g = 0; g < ng; ++g) {
     if (!bt[g].bcnt) return hipErrorInvalidValue;
-    ga.nrec[g] = bt[g].n;
-    ga.ntiles[g] = (bt[g].n + TILE_TAPE - 1) / TILE_TAPE;
     ga.bcnt[g] = bt[g].bcnt;
     ga.b_rec[g] = bt[g].b_rec;
     ga.res[g] = bt[g].res;
     ga.tile_sum[g] = bt[g].tile_sum;
     ga.scratch[g] = bt[g].scratch;
     ga.scratch_top[g] = bt[g].scratch_top;
-    ga.tape[g] = dt.tape[g];
-    ga.tape_count[g] = dt.count[g];
-    ga.done[g] = dt.done[g];
     src.seq[g] = bt[g].seq;
   }
-  ga.direct = dt.ticket ? dt.mask & (ng >= 32u ? ~0u : ((1u << ng) - 1u)) : 0u;
-  ga.fills_acc = dt.fills_acc;
-  ga.ticket = dt.ticket;
   ga.ovf_base = bt[0].ovf_base;
   ga.scratch_cap = bt[0].scratch_cap;
   ga.seq0 = bt[0].seq;
@@ -3300,20 +2765,7 @@ hipError_t launch_agg_group(hipStream_t st, const BookDev& bk, const BatchDev* b
   ne = (ne + 63u) & ~63ull;
   const uint64_t ne_cap = ((64u << 10) - sizeof(GrShared)) / 4u & ~63ull;
   if (ne > ne_cap) ne = ne_cap;
-  hipLaunchKernelGGL(k_agg_gres1, dim3(grid), dim3(GR_THREADS), (size_t)ne * 4u, st, bk, ga, src, ag, (uint32_t)ne);
-  if (ga.direct) {
-    uint32_t tiles = 0;
-    for (uint32_t g = 0; g < ng; ++g) tiles += ga.ntiles[g];
-    const uint32_t tg = (tiles + 3u) / 4u;
-    hipLaunchKernelGGL(k_agg_tscan, dim3(tg < 4096u ? tg : 4096u), dim3(256), 0, st, ga, ag);
-    // the tapes are the engine's per-position buffers: the tape jobs of the group before (on the side
-    // stream) must be done with them before this group's fills land there
-    if (join) {
-      hipError_t e = hipStreamWaitEvent(st, join, 0);
-      if (e != hipSuccess) return e;
-    }
-  }
-  hipLaunchKernelGGL(k_agg_gres2, dim3(grid), dim3(GR_THREADS), (size_t)ne * 4u, st, bk, ga, ag, (uint32_t)ne);
+  hipLaunchKernelGGL(k_agg_gres, dim3(grid), dim3(GR_THREADS), (size_t)ne * 4u, st, bk, ga, src, ag, (uint32_t)ne);
   return hipGetLastError();
 }
 }  // namespace me

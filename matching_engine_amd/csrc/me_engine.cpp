@@ -194,7 +194,6 @@ struct me_engine {
     uint32_t* tile_sum = nullptr;
     me_fill* scratch = nullptr;
     unsigned long long* top = nullptr;
-    uint32_t* done = nullptr;  // the grouped resolve wrote this set's batch tape itself (DirectTape)
   } os[3 * ME_GMAX];
   int nsets = 1;
   int last_set = 0;  // output set of the most recent batch
@@ -336,7 +335,7 @@ static void free_all(me_engine* e) {
         if (p) (void)hipFree(p);
     }
     for (auto& o : e->os) {
-      void* op[] = {o.res, o.fstart, o.tile_sum, o.scratch, o.top, o.done};
+      void* op[] = {o.res, o.fstart, o.tile_sum, o.scratch, o.top};
       for (void* p : op)
         if (p) (void)hipFree(p);
     }
@@ -344,7 +343,7 @@ static void free_all(me_engine* e) {
   {
     const AggDev& a = e->hot.ag;
     void* ap[] = {a.slot, a.ev, a.evs, a.evq, a.eva, a.evf, a.evn, a.evx, a.seg, a.segs, a.mk, a.fr, a.rec, a.ctr,
-                  a.gev, a.gex, a.gbase, (void*)a.gsave, e->hot.dt.ticket};
+                  a.gev, a.gex, a.gbase};
     for (void* p : ap)
       if (p) (void)hipFree(p);
   }
@@ -625,14 +624,6 @@ extern "C" me_engine* me_create(const me_config* cfg) {
       ALLOC(a.gev, S * (ME_GMAX + 1));
       ALLOC(a.gex, S * (ME_GMAX + 1));
       ALLOC(a.gbase, S * (ME_GMAX + 1));
-      ALLOC(a.gsave, S);
-      // the direct tape (me_agg.hip k_agg_gres2; ME_DIRECT_TAPE=0: every batch through scratch and the tape job)
-      const char* vd = getenv("ME_DIRECT_TAPE");
-      if (!(vd && atoi(vd) == 0)) {
-        ALLOC(e->hot.dt.ticket, 1);
-        if ((he = hipMemset(e->hot.dt.ticket, 0, 4)) != hipSuccess)
-          return bail(std::string("hipMemset ticket: ") + hipGetErrorString(he));
-      }
     }
     if ((he = hipMemset(a.ctr, 0, AC_N * sizeof(uint32_t))) != hipSuccess)
       return bail(std::string("hipMemset agg ctr: ") + hipGetErrorString(he));
@@ -679,10 +670,7 @@ extern "C" me_engine* me_create(const me_config* cfg) {
     ALLOC(o.tile_sum, ntiles_tape);
     ALLOC(o.scratch, ovf_base + scap);
     ALLOC(o.top, 1);
-    ALLOC(o.done, 1);
   }
-  for (int k = 0; k < e->nsets; ++k)
-    if ((he = hipMemset(e->os[k].done, 0, 4)) != hipSuccess) return bail(std::string("hipMemset done: ") + hipGetErrorString(he));
   ALLOC(bk.fcache, S * 64);
   ALLOC(e->d_tape, scap * e->group);
   ALLOC(e->d_tape_count, ME_GMAX);
@@ -901,18 +889,10 @@ static int pipe_launch(me_engine* e, const me_engine::Group* nb) {
   const auto& gt = e->g_tape;
   uint32_t orders = 0;
   uint64_t admitted = 0;
-  DirectTape& dt = e->hot.dt;
-  dt.mask = 0;
-  dt.fills_acc = e->d_fills_acc;
   for (uint32_t g = 0; g < gm.n; ++g) {
     const auto& pm = gm.b[g];
     admitted += pm.nadm;
     bt[g] = batch_dev(e, pm.seq, pm.px, pm.qty, pm.sym, pm.kind, pm.n, pm.oset);
-    // the grouped resolve may write a device batch's tape itself (its position's buffer, as the tape job would)
-    dt.tape[g] = e->d_tape + (size_t)g * e->tape_cap;
-    dt.count[g] = e->d_tape_count + g;
-    dt.done[g] = e->os[pm.oset].done;
-    if (pm.slot < 0) dt.mask |= 1u << g;
     const auto& b = e->bu[pm.bset];
     bt[g].bcnt = b.cnt;
     bt[g].b_rec = b.rec;
@@ -941,7 +921,6 @@ static int pipe_launch(me_engine* e, const me_engine::Group* nb) {
       J.zero_tile_sum = o.tile_sum;
       J.zero_tiles = (p.n + TILE_TAPE - 1) / TILE_TAPE;
       J.zero_top = o.top;
-      J.zero_done = o.done;
     }
   }
   ax.nt = gt.n;
@@ -955,7 +934,6 @@ static int pipe_launch(me_engine* e, const me_engine::Group* nb) {
     J.res = o.res;
     J.fstart = o.fstart;
     J.scratch = o.scratch;
-    J.done = o.done;
     if (gt.b[j].slot >= 0) {
       host_tapes = true;
       slot_outputs(e, e->hs[gt.b[j].slot], J.tape, J.tape_count, J.hres, J.err_out);

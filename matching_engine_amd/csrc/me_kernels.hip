@@ -2592,8 +2592,7 @@ hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* b
                             hipEvent_t ev0, hipEvent_t ev1);
 hipError_t launch_match_reg_cont(hipStream_t st, const BookDev& bk, const BatchDev* bt, uint32_t ng, hipEvent_t ev1);
 }
-hipError_t launch_agg_group(hipStream_t st, const BookDev& bk, const BatchDev* bt, uint32_t ng, const HotLaunch& hot,
-                            hipEvent_t join);  // me_agg.hip
+hipError_t launch_agg_group(hipStream_t st, const BookDev& bk, const BatchDev* bt, uint32_t ng, const AggDev& ag);  // me_agg.hip
 // The register-ladder launch (me_match_reg.hip, two builds): one head-cache entry per level while one
 // workgroup per CU covers the symbols (rc128), 64 shared entries and two workgroups per CU beyond
 // that (rc64). ax.nwg is the CU count (0: assume 256).
@@ -2630,7 +2629,7 @@ hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* b
       e = ev0 ? hipEventRecord(ev0, st) : hipSuccess;
     }
     if (e != hipSuccess) return e;
-    if ((e = launch_agg_group(st, bk, bt, ng, *hot, fork ? hot->sjoin : nullptr)) != hipSuccess) return e;
+    if ((e = launch_agg_group(st, bk, bt, ng, hot->ag)) != hipSuccess) return e;
     e = big ? rc64::launch_match_reg_cont(st, bk, bt, ng, ev1) : rc128::launch_match_reg_cont(st, bk, bt, ng, ev1);
     if (e != hipSuccess) return e;
     // the next launch (its walk reads the buckets made here) and every completion event recorded on st

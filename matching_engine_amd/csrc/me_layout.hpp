@@ -216,21 +216,6 @@ struct AggSegS {     // what the first per-level pass found (k_agg_levels), for 
   uint32_t d_off;         // this level's share of the slot's deficit (need beyond its own freed chunks)
   uint32_t ks;            // surviving rests
 };
-struct GrLevel {  // what the grouped resolve's phase B found for one level (me_agg.hip)
-  unsigned long long C, T0;
-  uint32_t newhead, mk_base, nmk, fr_base, nfreed, need, d_off, ks;
-};
-// A symbol's resolve state between k_agg_gres1 (phases A-C, the chunk allocation) and k_agg_gres2 (phase D):
-// the launch between them turns the fill counts into tape offsets (me_agg.hip)
-struct GrSave {
-  uint32_t nlv, alloc_base, pad[2];
-  uint32_t lvlist[128];
-  uint32_t lstart[132];  // [129] used
-  uint32_t lhead[128], ltail[128];
-  uint32_t gex[ME_GMAX + 1], gbase[ME_GMAX + 1];
-  uint8_t ltend[128];
-  GrLevel lv[128];
-};
 struct AggMk {       // a consumed maker: seq and the end of its interval in the level's maker space
   unsigned long long seq, end;
 };
@@ -249,9 +234,7 @@ struct AggSlot {     // one hot symbol of the launch (index = k_hot_pick's hand-
   uint32_t fr_base, fr_cur;  // the same for AggDev::fr
   uint32_t pad;
 };
-// AC_HB (grouped launches): max over symbols of (ng - g) for a hand-off in batch g (0: none) — the batches
-// before the first hand-off write their fills straight to the tape (k_agg_gres2)
-enum : uint32_t { AC_EV = 0, AC_SEG = 1, AC_MK = 2, AC_FR = 3, AC_HB = 4, AC_N = 8 };
+enum : uint32_t { AC_EV = 0, AC_SEG = 1, AC_MK = 2, AC_FR = 3, AC_N = 8 };
 struct AggDev {
   AggSlot* slot;               // [S]
   AggEv* ev;                   // [ev_cap] event log (per-slot regions)
@@ -274,7 +257,6 @@ struct AggDev {
   uint32_t* gev;               // the symbol's first log index of batch g (g = ng: the log's end)
   uint32_t* gex;               // the fill offset (k_agg_fin's scan) at gev
   uint32_t* gbase;             // scratch position of the symbol's first fill of batch g
-  struct GrSave* gsave;        // [S] what k_agg_gres1 hands to k_agg_gres2 (grouped launches)
 };
 // Where the record of a log entry lives (k_agg_levels / k_agg_place read the seq of a rest there).
 struct AggSrc {
@@ -283,18 +265,6 @@ struct AggSrc {
 };
 constexpr uint32_t AGG_GSHIFT = 25;  // batch index bits of a grouped log entry (BK_MAX_BATCH)
 constexpr uint32_t AGG_IMASK = (1u << AGG_GSHIFT) - 1u;
-
-// The grouped aggregate path's direct tape (me_agg.hip k_agg_gres2): where batch g of the launch group writes
-// its tape and count (the engine's per-position buffers) and its output set's "tape written" flag; bit g of
-// mask: a device batch (host batches keep the tape job, which writes their pinned slot).
-struct DirectTape {
-  me_fill* tape[ME_GMAX];
-  unsigned long long* count[ME_GMAX];
-  uint32_t* done[ME_GMAX];
-  uint32_t mask;
-  unsigned long long* fills_acc;
-  uint32_t* ticket;  // device word, 0 between launches (k_agg_gres1's last-workgroup count); null: no direct tape
-};
 
 // Host side of a deep-window launch with hot symbols: k_match_hot (or the aggregate path) runs on `st`,
 // forked from and joined back into the engine stream by two events (me_kernels.hip launch_match).
@@ -308,7 +278,6 @@ struct HotLaunch {
   // their own stream, forked before and joined after the group's walk / per-level launch / continuation
   hipStream_t sst = nullptr;
   hipEvent_t sfork = nullptr, sjoin = nullptr;
-  DirectTape dt{};  // set per launch by the engine (pipe_launch)
 };
 
 // Event counters kept on the device (BookDev::stats, me_stats_read).
@@ -418,7 +387,6 @@ struct AuxBucket {  // bucket + clear job of one batch
   uint32_t* bfstart;
   uint32_t* zero_tile_sum;
   unsigned long long* zero_top;
-  uint32_t* zero_done;    // the output set's "tape written by the resolve" flag (cleared here)
 };
 struct AuxTape {  // tape job of one batch
   const uint32_t* tile_sum;
@@ -436,7 +404,6 @@ struct AuxTape {  // tape job of one batch
   unsigned long long cap;
   uint32_t tn;
   uint32_t pad;
-  const uint32_t* done;   // set: the grouped resolve wrote this batch's tape itself (k_agg_gres2), nothing to do
 };
 struct AuxDev {
   uint32_t S;

@@ -989,10 +989,6 @@ __device__ __forceinline__ void aux_tape_tile(const GA& G, uint32_t jb, uint32_t
                                               uint32_t tn) {
   const int lane = lane_id();
   const AuxTape& J = G.ax.t[jb];
-  {  // the grouped resolve wrote this batch's tape, tape offsets and count itself (me_agg.hip k_agg_gres2)
-    const gptr<const uint32_t> dn = ldsg(J.done);
-    if (dn && __hip_atomic_load((const uint32_t*)dn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-  }
   const gptr<const uint32_t> tile_sum = ldsg(J.tile_sum);
   const gptr<me_order_result> res = ldsg(J.res);
   const gptr<const me_fill> scratch = ldsg(J.scratch);
@@ -1085,10 +1081,7 @@ __device__ __forceinline__ void aux_jobs(const ColdArgs& G, uint32_t b, uint32_t
     const uint32_t zt = ldsu(J.zero_tiles);
     const gptr<uint32_t> z = ldsg(J.zero_tile_sum);
     for (uint32_t i = a * 64u + (uint32_t)lane; i < zt; i += A * 64u) z[i] = 0u;
-    if (a == 0 && lane == 0) {
-      *ldsg(J.zero_top) = 0ull;
-      if (ldsg(J.zero_done)) *ldsg(J.zero_done) = 0u;
-    }
+    if (a == 0 && lane == 0) *ldsg(J.zero_top) = 0ull;
     if (xg && j % 8u != x) continue;
     const uint32_t wa = xg ? ax_ : a, WA = xg ? Ax : A;
     const uint32_t n = ldsu(J.n);
@@ -1158,10 +1151,7 @@ __device__ __forceinline__ void side_bucket_wg(const SideArgs& G, uint32_t j, ui
     const gptr<uint32_t> z = ldsg(J.zero_tile_sum);
     const uint32_t t1 = min((r1 + TILE_TAPE - 1) / TILE_TAPE, ldsu(J.zero_tiles));
     for (uint32_t t = r0 / TILE_TAPE + tid; t < t1; t += SIDE_THREADS) z[t] = 0u;
-    if (r0 == 0 && tid == 0) {
-      *ldsg(J.zero_top) = 0ull;
-      if (ldsg(J.zero_done)) *ldsg(J.zero_done) = 0u;
-    }
+    if (r0 == 0 && tid == 0) *ldsg(J.zero_top) = 0ull;
   }
   __syncthreads();
   uint32_t bin[SB_PER], rank[SB_PER];
@@ -1260,10 +1250,7 @@ __global__ __launch_bounds__(SIDE_THREADS) void k_side(SideArgs args, uint32_t n
       const uint32_t zt = ldsu(J.zero_tiles);
       const gptr<uint32_t> z = ldsg(J.zero_tile_sum);
       for (uint32_t i = a * 64u + (uint32_t)lane; i < zt; i += A * 64u) z[i] = 0u;
-      if (a == 0 && lane == 0) {
-        *ldsg(J.zero_top) = 0ull;
-        if (ldsg(J.zero_done)) *ldsg(J.zero_done) = 0u;
-      }
+      if (a == 0 && lane == 0) *ldsg(J.zero_top) = 0ull;
       const uint32_t n = ldsu(J.n), nblk = (n + 63u) / 64u;
       for (uint32_t u = flat_first(off, a, A); u < off + nblk; u += A) {
         const uint32_t r0 = (u - off) * 64u;

@@ -8,7 +8,7 @@ O=gpurun_out/$TAG; mkdir -p $O
 export TMPDIR=/tmp
 if [ "$TESTS" != none ]; then
   [ "$TESTS" = all ] && TESTS=tests
-  timeout -k 10 900 python -u -m pytest $TESTS -m gpu -x -q -p no:cacheprovider --timeout 240 --timeout-method thread > $O/pytest.log 2>&1
+  timeout -k 10 900 python -u -m pytest $TESTS -m gpu -x -q -p no:cacheprovider --timeout 150 --timeout-method thread > $O/pytest.log 2>&1
   rc=$?; tail -3 $O/pytest.log
   if [ $rc -ne 0 ]; then grep -E "^E |FAILED|Error" $O/pytest.log | head -30; exit 1; fi
 fi

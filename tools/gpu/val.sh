@@ -1,7 +1,5 @@
 #!/bin/bash
-# Validation of the current build: smoke, the -m gpu suite, and on a plain test failure (an assertion, not a
-# fault / abort / timeout: those end the call) the failing test file again with ME_DIRECT_TAPE=0 to tell the
-# direct tape from the rest; then bench lines.   tools/gpu/val.sh TAG [bench specs as record.sh: bench:WL:K:W ...]
+# Validation of the current build: smoke, the -m gpu suite, then bench lines (a failure of either ends the call).   tools/gpu/val.sh TAG [bench specs as record.sh: bench:WL:K:W ...]
 set -o pipefail
 TAG=$1; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -14,14 +12,6 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --t
 rc=$?; tail -2 $O/pytest_gpu.log
 if [ $rc -ne 0 ]; then
   grep -E "^E |FAILED|Error" $O/pytest_gpu.log | head -30
-  if [ $rc -eq 1 ]; then
-    f=$(grep -m1 -oE "^FAILED tests/[a-z_0-9]+\.py" $O/pytest_gpu.log | sed 's/FAILED //')
-    if [ -n "$f" ]; then
-      echo "--- $f with ME_DIRECT_TAPE=0"
-      ME_DIRECT_TAPE=0 timeout -k 10 400 python -u -m pytest $f -m gpu -x -q -p no:cacheprovider --timeout 240 --timeout-method thread > $O/pytest_nodirect.log 2>&1
-      tail -3 $O/pytest_nodirect.log
-    fi
-  fi
   exit 1
 fi
 exec_steps="$@"
