@@ -127,6 +127,11 @@ def global_symbols(args, world):
     return w["symbols"] if "symbols" in w else args.symbols_per_gpu * world
 
 
+def progress(msg):
+    """A progress line on stderr (long phases — config 4's seeding, the CPU sweep — print as they go)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def dist_setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -182,6 +187,7 @@ def build_rank_batches(args, world, rank, nbatches, n_whole=0):
     ids = members[rank]
     seeds = []
     if w.get("seeded"):  # config 4: deep pre-seeded books of the most popular symbols (not timed)
+        progress(f"generating the seeded books of {w['seeded']} symbols")
         sb = st.seed_books(range(w["seeded"]), w["per_side"])
         sel = np.nonzero(shard[sb.symbol] == rank)[0]
         sb = sb.take(sel)
@@ -223,6 +229,7 @@ def cpu_baseline(args):
         pre += [seeds.take(np.arange(i, min(i + (1 << 20), len(seeds)))) for i in range(0, len(seeds), 1 << 20)]
     pre += warm
     # k = the batches one thread matches in about --cpu-seconds (the single-core sample, timed per batch)
+    progress(f"cpu baseline: {sum(len(b) for b in pre)} untimed orders, then a ~{args.cpu_seconds} s sample on 1 core")
     ob = OracleBook(S)
     for b in pre:
         ob.submit(b)
@@ -252,6 +259,7 @@ def cpu_baseline(args):
     ts = sorted({t for t in args.cpu_threads_sweep + [allowed] if 1 <= t <= min(S, allowed)})
     sweep = {}
     for T in ts:
+        progress(f"cpu baseline: {T} threads")
         v, wall = sharded(T)
         sweep[str(T)] = {"value": v, "wall_s": round(wall, 4)}
     best = max(sweep, key=lambda t: sweep[t]["value"])
@@ -471,9 +479,12 @@ def main():
                     max_batch=max(len(b) for b in batches + e2e_batches + seeds) + 1,
                     max_resting=max(total_local // 3, sum(len(b) for b in batches)) + n_seed + 65536, seq_ring=args.seq_ring,
                     device=local, symbol_ids=ids, batches_per_launch=args.batches_per_launch)
+    if seeds:
+        progress(f"seeding {n_seed} resting orders (untimed)")
     for b in seeds:
         eng.submit_batch(b, want_fills=False)
     dbs = [eng.upload(b) for b in batches]
+    progress(f"{len(dbs)} batches resident; warmup {args.warmup}, timed {args.steps}")
     for db in dbs[: args.warmup]:
         eng.submit_device(db)
     eng.sync()
