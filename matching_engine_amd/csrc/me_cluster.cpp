@@ -479,8 +479,9 @@ struct Part {
 struct Ticket {
   uint64_t t = 0;
   size_t n = 0;
-  std::vector<uint32_t> pos;      // positions of each rank's records in the slice, rank after rank ...
-  std::vector<size_t> pos_off;    // ... rank r's at [pos_off[r], pos_off[r + 1])
+  std::vector<size_t> pos_off;    // rank r's records are [pos_off[r], pos_off[r + 1]) of the parts laid end to end
+  std::vector<uint16_t> srank;    // per slice record: its rank ...
+  std::vector<uint32_t> sidx;     // ... and its index in that rank's part (merge gathers in slice order)
 };
 
 // The packed part of n records at p: seq[n] px[n] qty[n] sym[n] kind[n].
@@ -533,7 +534,8 @@ void split_pack(const uint32_t* owner, const uint32_t* local, uint32_t W, uint32
                 const SplitCounts& sc, std::vector<PackView>& dst, Ticket& tk) {
   tk.pos_off.assign(W + 1, 0);
   for (uint32_t r = 0; r < W; ++r) tk.pos_off[r + 1] = tk.pos_off[r] + sc.per_rank[r];
-  tk.pos.resize(n);
+  tk.srank.resize(n);
+  tk.sidx.resize(n);
   // chunk i's first record of rank r lands at base[i][r] within the part
   std::vector<uint64_t> base(sc.T * W, 0);
   for (uint32_t r = 0; r < W; ++r) {
@@ -555,7 +557,8 @@ void split_pack(const uint32_t* owner, const uint32_t* local, uint32_t W, uint32
       v.qty[j] = b->qty[k];
       v.sym[j] = s < S ? local[s] : 0xFFFFFFFFu;
       v.kind[j] = b->kind[k];
-      tk.pos[tk.pos_off[r] + j] = (uint32_t)k;
+      tk.srank[k] = (uint16_t)r;
+      tk.sidx[k] = (uint32_t)j;
     }
   });
 }
@@ -565,9 +568,11 @@ void split_pack(const uint32_t* owner, const uint32_t* local, uint32_t W, uint32
 // tf[r] / nf[r]: shard r's results (its part's order), tape and fill count. Every shard's results must account
 // for its tape exactly (fill counts summing to its fills, each run inside the tape) — the copy trusts them;
 // false (bad = the shard) otherwise.
-// Every pass runs as one parallel region over the parts laid end to end ([0, n): rank r's records at
-// [pos_off[r], pos_off[r + 1])), so its thread count does not shrink as W grows (a region per part gave each
-// n / W records: 2 threads per part at W = 8, 24.7 ms per 1M-record slice, profiles/r5/rank0).
+// The check runs over the parts laid end to end, everything else in slice order — results gathered from the
+// parts (W sequential read streams, sequential writes), the tape copied taker by taker — and every pass is one
+// parallel region over the whole slice, so its threads do not shrink as W grows (a region per part, with the
+// results and fills scattered to their slice positions, took 24.7 ms per 1M-record slice at W = 8,
+// profiles/r5/rank0).
 template <class G>
 void part_runs(const Ticket& tk, size_t a, size_t b, G&& g) {  // g(r, first, last) in rank r's own indices
   uint32_t r = (uint32_t)(std::upper_bound(tk.pos_off.begin(), tk.pos_off.end(), a) - tk.pos_off.begin()) - 1u;
@@ -612,40 +617,30 @@ bool merge_parts(uint32_t W, const Ticket& tk, const std::vector<const me_order_
   }
   res_v.resize(n);
   me_order_result* res = res_v.data();
-  par_chunks(n, kGrain, [&](size_t, size_t a, size_t b) {
-    part_runs(tk, a, b, [&](uint32_t r, size_t ka, size_t kb) {
-      const uint32_t* pos = tk.pos.data() + tk.pos_off[r];
-      const me_order_result* rr = tr[r];
-      for (size_t k = ka; k < kb; ++k) res[pos[k]] = rr[k];
-    });
-  });
-  // merged tape offsets: exclusive scan of the fill counts in slice order (chunk sums, then chunk scans)
+  const uint16_t* srank = tk.srank.data();
+  const uint32_t* sidx = tk.sidx.data();
+  // results in slice order (tape_offset still the shard's) + each chunk's fill count
   std::vector<uint64_t> csum(T + 1, 0);
-  par_chunks(n, kGrain, [&](size_t i, size_t a, size_t b) {
+  par_chunks(n, kGrain, [&](size_t t, size_t a, size_t b) {
     uint64_t x = 0;
-    for (size_t k = a; k < b; ++k) x += res[k].fill_count;
-    csum[i + 1] = x;
+    for (size_t k = a; k < b; ++k) {
+      res[k] = tr[srank[k]][sidx[k]];
+      x += res[k].fill_count;
+    }
+    csum[t + 1] = x;
   });
-  for (size_t i = 0; i < T; ++i) csum[i + 1] += csum[i];
+  for (size_t t = 0; t < T; ++t) csum[t + 1] += csum[t];
   tape_v.resize(csum[T]);
   me_fill* tape = tape_v.data();
-  par_chunks(n, kGrain, [&](size_t i, size_t a, size_t b) {
-    uint64_t o = csum[i];
+  // merged tape offsets (exclusive scan in slice order = taker seq order) and each taker's fills from its shard
+  par_chunks(n, kGrain, [&](size_t t, size_t a, size_t b) {
+    uint64_t o = csum[t];
     for (size_t k = a; k < b; ++k) {
       const uint32_t fc = res[k].fill_count;
+      if (fc) memcpy(tape + o, tf[srank[k]] + res[k].tape_offset, fc * sizeof(me_fill));
       res[k].tape_offset = (uint32_t)o;
       o += fc;
     }
-  });
-  par_chunks(n, kGrain, [&](size_t, size_t a, size_t b) {  // each taker's fills from its shard's tape
-    part_runs(tk, a, b, [&](uint32_t r, size_t ka, size_t kb) {
-      const uint32_t* pos = tk.pos.data() + tk.pos_off[r];
-      const me_order_result* rr = tr[r];
-      const me_fill* fr = tf[r];
-      for (size_t k = ka; k < kb; ++k)
-        if (rr[k].fill_count)
-          memcpy(tape + res[pos[k]].tape_offset, fr + rr[k].tape_offset, rr[k].fill_count * sizeof(me_fill));
-    });
   });
   return true;
 }
