@@ -34,6 +34,8 @@
 // Same semantics and HBM layout as k_match (me_kernels.hip); parity: tests/test_hot_path.py.
 #include "me_wave.hpp"
 
+#include <cstdlib>
+
 namespace me {
 namespace {
 
@@ -2006,6 +2008,241 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
   }
 }
 
+// The same walk with its per-batch set-up on a second wave (ME_GW_HELPER, default on). The walker's batch
+// set-up — the bucket's load (and, gfx9's single in-order vmcnt, the wait for every store the last batch's
+// records issued), its LDS staging, the batch-order sort, the records' classification and control words,
+// the admission sums, the records' seq / position arrays — was ~110 of the ~615 cycles a record took on the
+// walker's chain (tools/gres_probe.py, profiles/r5/s2). Here wave 1 prepares batch g + 1 into one of two LDS
+// buffers while wave 0 walks batch g from the other; one workgroup barrier per batch hands them over. The
+// walker keeps what depends on the chain: the log bases, the bucket-count reset (only for batches it walks:
+// a hand-off's continuation still reads the later buckets), the walk, the results.
+struct GwBuf {
+  uint32_t cw[BK_CAP];  // record i of the batch in batch order: control word (lw_cw) ...
+  int oq[BK_CAP];       // ... quantity (0: none) ...
+  uint32_t oi[BK_CAP];  // ... and index in the batch (the result's position)
+  unsigned long long fastm[2];  // per 64-record block: the records the walk covers (a_classify)
+  long long qsum[2];            // per block: its quantities (the ladder's admission bound)
+};
+struct GwShared {
+  AStage stg;  // the helper's staging of the raw bucket
+  GwBuf buf[2];
+  uint32_t ltot[128 + 64];
+  uint32_t go, eb, stop[2];
+};
+
+__device__ __forceinline__ void gw_prepare(GwBuf& B, AStage& stg, const AggGArgs& ga, uint32_t g, uint32_t cnt,
+                                           size_t bko, long long base, int L, uint32_t nfar0, uint32_t nfar1,
+                                           gptr<uint32_t> rsq, gptr<uint32_t> rjs, unsigned long long gmin,
+                                           uint32_t& rbase) {
+  const int lane = lane_id();
+  BkRec r0{}, r1{};
+  if ((uint32_t)lane < cnt) r0 = ga.b_rec[g][bko + lane];
+  if (64u + (uint32_t)lane < cnt) r1 = ga.b_rec[g][bko + 64 + lane];
+  stg.seq[lane] = r0.seq;
+  stg.seq[64 + lane] = r1.seq;
+  stg.px[lane] = r0.px;
+  stg.px[64 + lane] = r1.px;
+  stg.qty[lane] = r0.qty;
+  stg.qty[64 + lane] = r1.qty;
+  stg.ok[lane] = r0.ok;
+  stg.ok[64 + lane] = r1.ok;
+  uint32_t k0 = (uint32_t)lane < cnt ? ((r0.ok & BK_IDX_MASK) << 7) | (uint32_t)lane : ~0u;
+  uint32_t k1 = 64u + (uint32_t)lane < cnt ? ((r1.ok & BK_IDX_MASK) << 7) | (64u + (uint32_t)lane) : ~0u;
+  if (cnt > 64u)
+    a_sort128(k0, k1);
+  else
+    k0 = a_sort64(k0, false);
+  wave_mem_order();
+  for (uint32_t blk = 0; blk < cnt; blk += 64) {
+    const uint32_t key = blk ? k1 : k0;
+    const bool v = blk + (uint32_t)lane < cnt;
+    const uint32_t sl = key & (BK_CAP - 1), oi = v ? key >> 7 : 0u;
+    const unsigned long long oseq = stg.seq[sl];
+    const long long opx = stg.px[sl];
+    const int oq = v ? stg.qty[sl] : 0;
+    const uint32_t okd = v ? stg.ok[sl] >> BK_KIND_SHIFT : 0u;
+    uint32_t rj;
+    int olm;
+    const unsigned long long fastm = __ballot(a_classify(v, oseq, opx, oq, okd, base, L, nfar0, nfar1, rj, olm));
+    const long long qs = rli64(wave_incl_scan((long long)(uint32_t)max(oq, 0)), 63);
+    B.cw[blk + lane] = lw_cw(okd, olm, rj, L);
+    B.oq[blk + lane] = oq;
+    B.oi[blk + lane] = oi;
+    if (lane == 0) {
+      B.fastm[blk >> 6] = fastm;
+      B.qsum[blk >> 6] = qs;
+    }
+    if (v) {
+      rsq[rbase + (uint32_t)lane] = (uint32_t)(oseq - gmin);
+      rjs[rbase + (uint32_t)lane] = (g << AGG_GSHIFT) | oi;
+    }
+    rbase += min(64u, cnt - blk);
+  }
+}
+
+__global__ __launch_bounds__(128) void k_agg_gwalk2(BookDev bk, AggGArgs ga, AggDev ag) {
+  __shared__ GwShared sh;
+  const int lane = lane_id();
+  const bool walker = auni((int)(threadIdx.x >> 6)) == 0;
+  const int L = (int)bk.L;  // <= 128
+  const uint32_t ng = ga.ng;
+  for (uint32_t s = blockIdx.x; s < bk.S; s += gridDim.x) {
+    const uint32_t gl = min((uint32_t)lane, ng - 1u);
+    const uint32_t nsv = (uint32_t)lane < ng ? ga.bcnt[gl][(size_t)s * BK_CNT_STRIDE] : 0u;
+    const uint32_t total = (uint32_t)rli64(wave_incl_scan((long long)nsv), 63);
+    const SymState st = bk.sym[s];
+    const long long base = rli64(st.base, 0);
+    const int bb0 = rli32(st.best_bid, 0), ba0 = rli32(st.best_ask, 0);
+    const uint32_t resting = rl32(st.resting, 0);
+    const uint32_t nfar0 = rl32(st.nfar[0], 0), nfar1 = rl32(st.nfar[1], 0);
+    gptr<AggSlot> slot = (gptr<AggSlot>)(ag.slot + s);
+    const uint32_t evneed = 3u * total + min((uint32_t)L, resting) + 64u;
+    if (walker) {
+      uint32_t eb = 0;
+      if (total && lane == 0) eb = atomicAdd(&ag.ctr[AC_EV], evneed + 64u);
+      eb = (rl32(eb, 0) + 63u) & ~63u;
+      const bool eok = (unsigned long long)eb + evneed <= ag.ev_cap;
+      if (lane == 0) {
+        AggSlot o{};
+        o.s = s;
+        o.base = base;
+        o.ev_base = eb;
+        o.lo = evneed;
+        o.hi = total;
+        o.free_head = st.free_head;
+        o.resting0 = resting;
+        o.bb = bb0;
+        o.ba = ba0;
+        o.active = 0;
+        o.hidx = NIL;
+        o.gs = bk.gsym ? bk.gsym[s] : s;
+        *slot = o;
+      }
+      bool go = total != 0u;
+      if (go && (!eok || !a_reserve(ag, slot, resting, total))) {  // no room: the whole group of the symbol
+        const uint32_t g0 = (uint32_t)__builtin_ctzll(__ballot(nsv != 0u));  // goes to the continuation
+        a_ghand(bk, s, g0, 0u, rl32(nsv, (int)g0), s * ga.slab, s * ga.slab + ga.slab);
+        go = false;
+      }
+      if (lane == 0) {
+        sh.go = go ? 1u : 0u;
+        sh.eb = eb;
+      }
+    }
+    __syncthreads();
+    const bool go = auniu(sh.go) != 0u;
+    const uint32_t eb = auniu(sh.eb);
+    __syncthreads();  // (the walker's next symbol overwrites go / eb)
+    if (!go) continue;
+    GR_STAMP(bk, s, 0);
+#ifdef ME_STAMPS
+    unsigned long long gw_t[4] = {0ull, 0ull, 0ull, 0ull}, gw_m = stamp_now();
+#endif
+    AggGEv* const log8 = reinterpret_cast<AggGEv*>(ag.ev + eb);
+    const gptr<uint32_t> rsq = vptr(reinterpret_cast<uint32_t*>(log8 + evneed));
+    const gptr<uint32_t> rjs = rsq + total;
+    const size_t bko = (size_t)s * BK_CAP;
+    if (walker) {
+      const uint32_t nfc = min(rl32(st.nfree, 0), 64u);
+      if (nfc) {  // k_match_reg's parked free chunks join the front of the free list (k_agg_gwalk)
+        const uint32_t fc = bk.fcache[(size_t)s * 64u + lane];
+        const uint32_t nx = (uint32_t)__shfl((int)fc, min(lane + 1, 63), 64);
+        if ((uint32_t)lane < nfc) bk.chunks[fc].hdr.next = (uint32_t)lane + 1u < nfc ? nx : st.free_head;
+        if (lane == 0) slot->free_head = fc;
+      }
+    } else {
+      uint32_t hrb = 0;
+      const unsigned long long gmin = *ga.seq0;
+      const uint32_t c0 = rl32(nsv, 0);
+      if (c0 && c0 <= (uint32_t)BK_CAP)
+        gw_prepare(sh.buf[0], sh.stg, ga, 0u, c0, bko, base, L, nfar0, nfar1, rsq, rjs, gmin, hrb);
+      __syncthreads();
+      for (uint32_t g = 0; g < ng; ++g) {
+        const uint32_t c = g + 1u < ng ? rl32(nsv, (int)(g + 1u)) : 0u;
+        if (c && c <= (uint32_t)BK_CAP)
+          gw_prepare(sh.buf[(g + 1u) & 1u], sh.stg, ga, g + 1u, c, bko, base, L, nfar0, nfar1, rsq, rjs, gmin, hrb);
+        __syncthreads();
+        if (auniu(sh.stop[g & 1u])) break;
+      }
+      continue;
+    }
+    LEvG w;
+    le_init(w, log8, 0u);
+    uint32_t rbase = 0;
+    LWalk lw;
+    const bool lok = lw_init(lw, bk, s, sh.ltot, bb0, ba0);
+    uint32_t hidx = NIL, gstop = ng;
+    __syncthreads();  // batch 0 prepared
+    for (uint32_t g = 0; g < ng; ++g) {
+      if (lane == 0) *a_gtab(ag.gev, s, g) = eb + w.evp;
+      const uint32_t cnt = rl32(nsv, (int)g);
+      bool stop = false;
+      if (cnt > (uint32_t)BK_CAP) {  // an overfull bucket: the continuation rescans the batch
+        hidx = a_ghand(bk, s, g, 0u, cnt, 0u, 0u);
+        stop = true;
+      } else if (cnt) {
+        if (lane == 0) ga.bcnt[g][(size_t)s * BK_CNT_STRIDE] = 0u;  // ready for a later group's bucket job
+        const GwBuf& B = sh.buf[g & 1u];
+        me_order_result* res = ga.res[g];
+        GW_T(0);
+        for (uint32_t blk = 0; blk < cnt; blk += 64) {
+          const bool v = blk + (uint32_t)lane < cnt;
+          const uint32_t ocw = B.cw[blk + lane];
+          const int oq = B.oq[blk + lane];
+          const uint32_t oi = B.oi[blk + lane];
+          const unsigned long long fastm = rl64(B.fastm[blk >> 6], 0);
+          const uint32_t cntb = min(64u, cnt - blk);
+          int rr = 0;
+          bool adm = false;
+          if (lok) {
+            lw.ub += (unsigned long long)rli64(B.qsum[blk >> 6], 0);
+            adm = lw.ub < LW_CAP;
+          }
+          GW_T(1);
+          const uint32_t k = lw_block<AGG_GREC_SHIFT>(w, lw, oq, ocw, rbase, adm ? fastm : 0ull, cntb, rr);
+          rbase += cntb;
+          GW_T(2);
+#ifdef ME_STAMPS
+          gw_t[3] += k;
+#endif
+          if (v && (uint32_t)lane < k)
+            res[oi] = a_result(oq, (ocw & LW_MKT) ? 4u : 0u, ocw >> LW_RJ_SHIFT, rr);  // fills: k_agg_gres
+          if (k < cntb) {
+            hidx = a_ghand(bk, s, g, blk + k, cnt, 0u, 0u);  // scratch position: k_agg_gres
+            stop = true;
+            break;
+          }
+        }
+      }
+      if (lane == 0) sh.stop[g & 1u] = stop ? 1u : 0u;
+      __syncthreads();  // batch g + 1 prepared; the helper sees the stop
+      if (stop) {
+        gstop = g;
+        break;
+      }
+    }
+    for (uint32_t g = (gstop < ng ? gstop + 1u : ng) + (uint32_t)lane; g <= ng; g += 64)
+      *a_gtab(ag.gev, s, g) = eb + w.evp;
+    if (gstop < ng && lane == 0) *a_gtab(ag.gev, s, gstop + 1u) = eb + w.evp;
+    le_end(w);
+    if (lok) lw_end(lw, bk, s);
+    const int bb = lw.bb, ba = lw.ba;
+    if (lane == 0) {
+      slot->ev_cnt = w.evp;
+      slot->bb = bb;
+      slot->ba = ba;
+      slot->active = 1;
+      slot->hidx = hidx;
+      slot->pos = gstop;
+    }
+    GR_STAMP(bk, s, 1);
+#ifdef ME_STAMPS
+    if (lane == 0)
+      for (int q = 0; q < 4; ++q) bk.dbg[(size_t)s * 24u + q] = gw_t[q];
+#endif
+  }
+}
+
 // ------------------------------------------------------------------ grouped launches: one workgroup per symbol
 // k_agg_gres does the work of the hot path's k_agg_group ... k_agg_out for a grouped launch in ONE launch,
 // one 512-thread workgroup per symbol (the walk's workgroup of the same symbol ran on the same XCD,
@@ -2756,7 +2993,14 @@ hipError_t launch_agg_group(hipStream_t st, const BookDev& bk, const BatchDev* b
   ga.slab = bt[0].slab;
   ga.ng = ng;
   const uint32_t grid = bk.S < 2048u ? bk.S : 2048u;
-  hipLaunchKernelGGL(k_agg_gwalk, dim3(grid), dim3(64), 0, st, bk, ga, ag);
+  static const bool helper = [] {
+    const char* e = getenv("ME_GW_HELPER");
+    return !e || atoi(e) != 0;
+  }();
+  if (helper)
+    hipLaunchKernelGGL(k_agg_gwalk2, dim3(grid), dim3(128), 0, st, bk, ga, ag);
+  else
+    hipLaunchKernelGGL(k_agg_gwalk, dim3(grid), dim3(64), 0, st, bk, ga, ag);
   // the per-event LDS array (fill counts, 4 B per event) sized for 1.75 events per record of the group's
   // mean symbol plus slack; a longer log keeps it in HBM. Capped so the workgroup's LDS stays within 64 KB.
   uint64_t recs = 0;
