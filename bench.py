@@ -86,6 +86,8 @@ def parse():
     ap.add_argument("--cpu-warmup", type=int, default=4, help="untimed stream batches before the CPU sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-fills-check", action="store_true", help="skip the post-run oracle check of the last group")
+    ap.add_argument("--fills-check-max", type=int, default=8_000_000, help="largest oracle replay (orders) to check")
     ap.add_argument("--e2e-steps", type=int, default=384,
                     help="batches through the pipelined host path (me_submit_host/me_collect) after the timed loop")
     ap.add_argument("--timing-every", type=int, default=4,
@@ -204,6 +206,39 @@ def build_rank_batches(args, world, rank, nbatches, n_whole=0):
         pos.append(sel)
     whole = [st.next(sc.batch) for _ in range(n_whole)]
     return sc, base, ids, out, pos, sc.batch * nbatches, seeds, whole
+
+
+def check_fills(eng, seeds, batches, ids, args):
+    """The last launch group's batches (results and tapes) against the oracle replaying the whole stream
+    (tests/_parity.py's fields; the oracle is the checker here, after the timed region). Skipped above
+    --fills-check-max orders of replay (config 4's 20M seeded orders, long runs)."""
+    n_replay = sum(len(b) for b in seeds) + sum(len(b) for b in batches)
+    if n_replay > args.fills_check_max:
+        return {"checked": False, "reason": f"replay of {n_replay} orders > --fills-check-max {args.fills_check_max}"}
+    from oracle.oracle import OracleBook
+
+    progress(f"fills check: oracle replay of {n_replay} orders")
+    g = eng.last_group_size()
+    first = len(batches) - g
+    fields = ("filled_qty", "remaining_qty", "fill_count", "tape_offset", "status", "reason")
+    ob = OracleBook(len(ids), symbol_ids=ids)  # (fills carry global symbol ids, as the engine's)
+    bad, orders, fills = 0, 0, 0
+    try:
+        for b in seeds:
+            ob.submit(b)
+        for i, b in enumerate(batches):
+            ro, fo = ob.submit(b)
+            if i < first:
+                continue
+            r, f = eng.fetch_group_outputs(i - first, len(b))
+            same = len(f) == len(fo) and bool(np.all(f == fo)) and all(bool(np.all(r[x] == ro[x])) for x in fields)
+            bad += 0 if same else 1
+            orders += len(b)
+            fills += len(f)
+    finally:
+        ob.close()
+    return {"checked": True, "batches": g, "orders": orders, "fills": fills, "mismatched_batches": bad,
+            "how": "the last launch group's results and tapes vs oracle/oracle_book.cpp replaying the stream"}
 
 
 def cpu_baseline(args):
@@ -534,6 +569,14 @@ def main():
         if traffic_per_order:
             traffic = traffic_per_order * tm["orders"] / timed
 
+    # fills check (after the timed region, before anything else runs on the engine): the oracle replays
+    # this rank's stream from the start (seeded books, warmup, timed batches) and every batch of the last
+    # timed launch group — its results and tape — must equal it bit for bit; the metric's "fills bit-exact"
+    # is this check plus the -m gpu parity suite
+    fills_check = check_fills(eng, seeds, batches, ids, args) if not args.no_fills_check else None
+    bad_all = allreduce(float(fills_check["mismatched_batches"] if fills_check and fills_check["checked"] else 0),
+                        world, SUM, local)
+
     # PCIe-inclusive host path (me_submit_host / me_collect: staging copy into a pinned slot, H2D on
     # its own stream, the grouped pipeline, D2H of results + tape into pinned memory), informational.
     # Each ticket is collected when its slot is needed again (host_slots submissions later).
@@ -594,6 +637,8 @@ def main():
             "device_ms_per_step": tm["pipeline_ms"] if tm["launches"] >= 2 else None,
             "host_enqueue_ms_per_step_rank0": t_enq / args.steps * 1e3,
             "e2e_host_path_orders_per_s_rank0": e2e,
+            "fills_check_rank0": fills_check,
+            "fills_check_mismatched_batches_all_ranks": int(bad_all),
             "cluster": None,
             "roofline": {
                 "bound": "hbm",
