@@ -139,7 +139,8 @@ def main():
 
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     port = int(os.environ["MASTER_PORT"])
-    S, L, MB, MR = 40, 128, 4096, 1 << 16
+    S, L, MR = 40, 128, 1 << 16
+    MB = int(os.environ.get("ME_TEST_MAX_BATCH", "4096"))  # (a large one: the cluster reserves few slots)
     syms = [f"S{i:02d}" for i in range(S)]
     mids = {s: 1_000_000 + 1000 * i for i, s in enumerate(syms)}
     base = np.array([mids[s] - 64 for s in syms], dtype=np.int64)

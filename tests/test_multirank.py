@@ -90,3 +90,14 @@ def test_cluster_rccl_single_rank_direct(built, tmp_path):
     r = _run("rccl", 1, tmp_path)
     assert r["ok"], r["msg"]
     assert r["orders"] > 5000 and r["fill_rows"] > 1000
+
+
+@pytest.mark.gpu
+def test_cluster_large_max_batch_reserves_protocol_slots(built, tmp_path):
+    """me_cluster_create reserves only the host slots its protocol can use (two slices in flight
+    plus the held one), not the engine's default 4 * 32 + 1. With a 4M-record max_batch each slot pins
+    ~0.45 GB, so the default-config cluster here (batches_per_launch 32) would pin ~57 GB up front; it
+    must come up and match the same direct slices and service traffic as the small one."""
+    r = _run("rccl", 1, tmp_path, env_extra={"ME_TEST_MAX_BATCH": str(1 << 22)})
+    assert r["ok"], r["msg"]
+    assert r["orders"] > 5000 and r["fill_rows"] > 1000
