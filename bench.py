@@ -87,7 +87,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-fills-check", action="store_true", help="skip the post-run oracle check of the last group")
-    ap.add_argument("--fills-check-max", type=int, default=8_000_000, help="largest oracle replay (orders) to check")
+    ap.add_argument("--fills-check-max", type=int, default=24_000_000,
+                    help="largest oracle replay (orders) to check (config 4's 20M seeded orders included)")
     ap.add_argument("--e2e-steps", type=int, default=384,
                     help="batches through the pipelined host path (me_submit_host/me_collect) after the timed loop")
     ap.add_argument("--timing-every", type=int, default=4,
@@ -211,7 +212,7 @@ def build_rank_batches(args, world, rank, nbatches, n_whole=0):
 def check_fills(eng, seeds, batches, ids, args):
     """The last launch group's batches (results and tapes) against the oracle replaying the whole stream
     (tests/_parity.py's fields; the oracle is the checker here, after the timed region). Skipped above
-    --fills-check-max orders of replay (config 4's 20M seeded orders, long runs)."""
+    --fills-check-max orders of replay (long runs)."""
     n_replay = sum(len(b) for b in seeds) + sum(len(b) for b in batches)
     if n_replay > args.fills_check_max:
         return {"checked": False, "reason": f"replay of {n_replay} orders > --fills-check-max {args.fills_check_max}"}
@@ -634,7 +635,11 @@ def main():
             "kernel_match_launches_timed": tm["launches"],
             "batches_per_launch": args.batches_per_launch or (32 if sc.levels <= 128 else 1),
             # start-to-start device time per batch between the first and last timed launches (needs two)
-            "device_ms_per_step": tm["pipeline_ms"] if tm["launches"] >= 2 else None,
+            # the match pipeline's device time per batch: the steady launch-to-launch time with two or more
+            # timed launches, else the one timed launch group's event-timed duration / the batches it matched
+            # (no fill or drain launch in either)
+            "device_ms_per_step": tm["pipeline_ms"] if tm["launches"] >= 2 else (
+                tm["match_ms"] / (tm["orders"] / (orders_local / args.steps)) if tm["orders"] and orders_local else None),
             "host_enqueue_ms_per_step_rank0": t_enq / args.steps * 1e3,
             "e2e_host_path_orders_per_s_rank0": e2e,
             "fills_check_rank0": fills_check,

@@ -877,6 +877,11 @@ __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const Agg
     }
     return;
   }
+#ifdef ME_STAMPS
+  // the hot walk's cycles by part, accumulated over launches (dbg[s * 24 + 0..4]: set-up, block set-up,
+  // record loop, records walked, end), read by tools/hot_probe.py
+  unsigned long long gw_t[5] = {0ull, 0ull, 0ull, 0ull, 0ull}, gw_m = stamp_now();
+#endif
   AWalk w;
   a_walk_init(w, bk, ag, s, eb, locc, stg);
   // the ladder walk; the top-of-book lists (64-bit totals) for a book the ladder cannot hold, or beyond
@@ -890,6 +895,7 @@ __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const Agg
     a_rebuild<1>(w, A, ba0);
     a_rebuild<0>(w, B, L - 1 - bb0);
   }
+  GW_T(0);
   uint32_t pos = hi;
   // the blocks' records are gathered ahead of the chain: block b's fields were issued while block b - 1
   // ran, its permutation entries while block b - 2 ran (no HBM round trip between blocks)
@@ -925,13 +931,19 @@ __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const Agg
     uint32_t k;
     if (ladder) {
       const bool adm = lw_admit(lw, v ? oq : 0);  // else: the generic loop from this block on
+      GW_T(1);
       k = lw_block<0>(le, lw, oq, lw_cw(okd, olm, rj, L), blk, adm ? fastm : 0ull, cntb, rr);
     } else {
       a_refill(w, A, B);
+      GW_T(1);
       ARes R;
       k = a_block(w, A, B, oq, okd, olm, rj, j, fastm, cntb, R);
       rr = R.rr;
     }
+    GW_T(2);
+#ifdef ME_STAMPS
+    gw_t[3] += k;
+#endif
     if (v && (uint32_t)lane < k) {  // fill count and scratch start: k_agg_out
       bt.res[oi] = a_result(oq, okd, rj, rr);
       bt.fstart[oi] = 0u;
@@ -951,6 +963,11 @@ __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const Agg
   } else {
     a_walk_end(w, A, B, bb, ba);
   }
+  GW_T(4);
+#ifdef ME_STAMPS
+  if (lane == 0)
+    for (int q = 0; q < 5; ++q) bk.dbg[(size_t)s * 24u + q] += gw_t[q];
+#endif
   if (lane == 0) {
     slot->pos = pos;
     slot->ev_cnt = w.evp - eb;

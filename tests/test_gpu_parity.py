@@ -112,6 +112,28 @@ def test_config4_bench_shape(me, orc):
     assert nf > 0
 
 
+def test_config4_full_bench_shape(me, orc):
+    """Config 4 exactly as the bench runs it on one GPU: 100,000 symbols, the 1,000 most
+    popular books seeded to 10,000 levels per side (20M resting orders, matched on both sides without
+    comparison), then two 65,536-order batches of the Zipf stream compared record for record and fill for
+    fill, and the hot symbols' books."""
+    sc = me.preset(4, batch=65536)
+    st = me.Stream(sc)
+    base = st.base_prices()
+    seeds = st.seed_books(range(1000), 10_000)
+    step = 1 << 20
+    ob = orc.OracleBook(sc.num_symbols)
+    total = len(seeds) + 2 * sc.batch
+    with engine_for(me, sc.num_symbols, sc.levels, base, step, total + 65536) as eng:
+        for i in range(0, len(seeds), step):
+            part = seeds.take(slice(i, i + step))
+            eng.submit_batch(part, want_fills=False)
+            ob.submit(part)
+        nf = run_both(eng, ob, [st.next(sc.batch) for _ in range(2)], book_symbols=[0, 1, 2, 3, 500, 999, 54321],
+                      ctx="c4 full shape")
+    assert nf > 0
+
+
 def test_deep_window_many_symbols(me, orc):
     """More symbols than one dispatch round of deep-window workgroups, busy and idle alike."""
     nf, total = _stream_run(me, orc, 2, 2, num_symbols=1100, levels=2048, batch=1100 * 80,
