@@ -40,6 +40,9 @@ namespace me {
 namespace {
 
 constexpr uint32_t AGG_WORDS = AGG_MAX_L / 64;
+#ifndef ME_LIST_EMIT
+#define ME_LIST_EMIT 0  // the list walk's event staging: 0 LDS (one 16-B lane-0 write per event), 1 VGPR lanes
+#endif
 // M0 is set only by this file's v_writelane sequences (no LDS-direct, GWS or interpolation use here)
 #pragma clang diagnostic ignored "-Winline-asm"
 
@@ -116,23 +119,51 @@ struct AWalk {
   unsigned long long* locc;  // LDS copy of the occupancy bitmap (both sides)
   uint32_t evp;              // next log index (the slot's log starts 64-aligned)
   int L, W;
+#if ME_LIST_EMIT
+  // the log's current 64-event block, event i in lane i of three VGPRs (v_writelane, as the ladder walk's
+  // LEv): one coalesced 1-KB store per 64 events
+  uint32_t vl, vj, vq;
+#else
   // the log's current 64-event block, event i in lane i: stored by the whole wave when it fills (one
   // coalesced 1-KB store instead of a lane-0 store per event)
   AggEv* stg;  // LDS [128]: the block's events by log index mod 64, then the other lanes' dummy slots
+#endif
 };
 
 __device__ __forceinline__ int a_side_lvl(int L, int k, int m) { return k ? m : L - 1 - m; }
 
+#if ME_LIST_EMIT
 // Lanes [0, n) of the staged block to log indices [base, base + n).
-__device__ __forceinline__ void a_evstore(AWalk& w, uint32_t base, uint32_t n) {
+__device__ __forceinline__ void a_evstore(const AWalk& w, uint32_t base, uint32_t n) {
+  AggEv e;
+  e.lvl = w.vl;
+  e.j = w.vj;
+  e.qty = (int)w.vq;
+  e.pad = 0u;
+  if ((uint32_t)lane_id() < n) w.ev[base + (uint32_t)lane_id()] = e;
+}
+// The event into lane evp & 63 of the staging VGPRs (three v_writelane, no LDS traffic; the block leaves
+// as one coalesced store when it fills). lvl, jt and q are wave-uniform.
+__device__ __forceinline__ void a_emit(AWalk& w, int lvl, uint32_t jt, int q) {
+  const uint32_t slot = w.evp & 63u;
+  asm volatile(
+      "s_mov_b32 m0, %3\n\tv_writelane_b32 %0, %4, m0\n\tv_writelane_b32 %1, %5, m0\n\tv_writelane_b32 %2, %6, m0"
+      : "+v"(w.vl), "+v"(w.vj), "+v"(w.vq)
+      : "s"(slot), "s"(auniu((uint32_t)lvl)), "s"(auniu(jt)), "s"(auniu((uint32_t)q))
+      : "m0");
+  w.evp += 1;
+  if (ME_UNLIKELY(slot == 63u)) a_evstore(w, w.evp - 64u, 64u);
+}
+
+#else
+// Lanes [0, n) of the staged block to log indices [base, base + n).
+__device__ __forceinline__ void a_evstore(const AWalk& w, uint32_t base, uint32_t n) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (a wave's LDS operations complete in order)
   const AggEv e = w.stg[lane_id()];
   if ((uint32_t)lane_id() < n) w.ev[base + (uint32_t)lane_id()] = e;
 }
 // The event into the LDS block (one 16-B write by lane 0; the other lanes write their dummy slots, so no
-// exec change), one coalesced 1-KB store per 64 events. Nothing loop-carried in VGPRs: staging in
-// registers (a select or v_writelane per field) made the compiler copy the staging registers at every
-// join of the record loop.
+// exec change), one coalesced 1-KB store per 64 events.
 __device__ __forceinline__ void a_emit(AWalk& w, int lvl, uint32_t jt, int q) {
   const int lane = lane_id();
   AggEv e;
@@ -146,6 +177,7 @@ __device__ __forceinline__ void a_emit(AWalk& w, int lvl, uint32_t jt, int q) {
   if (ME_UNLIKELY((w.evp & 63u) == 0u)) a_evstore(w, w.evp - 64u, 64u);
 }
 
+#endif
 // Occupancy: non-returning atomics on the LDS copy and on HBM (nothing in the chain waits for them).
 __device__ __forceinline__ void a_occ(AWalk& w, int lvl, bool on) {
   const uint32_t wi = (uint32_t)lvl >> 6;
@@ -349,13 +381,6 @@ __device__ __forceinline__ bool a_reserve(const AggDev& ag, gptr<AggSlot> slot, 
   return mb + mkb <= (unsigned long long)ag.mk_cap && fb + frb <= (unsigned long long)ag.fr_cap;
 }
 
-// Results of one block's records, lane k = record k.
-struct ARes {
-  int rf, rr;
-  uint32_t rs;   // status | reason << 8
-  uint32_t rlo;  // first take event (log index)
-  uint32_t rn;   // take events
-};
 
 // Reject reason (k_match's, in its order; cancels are the generic loop's) and whether the walk covers
 // the record: not a cancel, and a LIMIT inside the window or a MARKET while the side it crosses has no
@@ -390,55 +415,34 @@ __device__ __forceinline__ void a_refill(AWalk& w, AList& A, AList& B) {
   }
 }
 
-// The serial chain over records [0, cnt) of a block in vector form (lane k = record k: quantity, kind,
-// window level, reject reason, log id). Returns the records it matched: fewer than cnt when record k is
-// one the walk does not cover (fastm bit clear).
-__device__ __forceinline__ uint32_t a_block(AWalk& w, AList& A, AList& B, int oq, uint32_t okd, int olm, uint32_t rj,
-                                            uint32_t ojt, unsigned long long fastm, uint32_t cnt, ARes& R) {
+// A record's control word (lw_cw): its level (LIMIT) or last level a taker may trade at (MARKET: the window's
+// far end), side, type, reject reason.
+constexpr uint32_t LW_BUY = 1u << 15, LW_MKT = 1u << 16, LW_RJ_SHIFT = 17, LW_LIM = 0x7FFFu;
+
+// The serial chain over records [0, cnt) of a block in vector form (lane k = record k: quantity and the
+// control word of lw_cw — window level / a taker's last level, side, type, reject reason); record k's log
+// id is jb + k. Returns the records it walked (fewer than cnt when record k is one the walk does not cover:
+// fastm bit clear); rr lane k = record k's remainder.
+__device__ __forceinline__ uint32_t a_block(AWalk& w, AList& A, AList& B, int oq, uint32_t ocw, uint32_t jb,
+                                            unsigned long long fastm, uint32_t cnt, int& rr) {
   const int L = w.L;
-  R.rf = R.rr = 0;
-  R.rs = R.rlo = R.rn = 0u;
   uint32_t k = 0;
   for (; k < cnt; ++k) {
     if (ME_UNLIKELY(!((fastm >> k) & 1ull))) break;
-    const uint32_t jt = rl32(ojt, (int)k);
-    const int q = rli32(oq, (int)k);
-    const uint32_t rjk = rl32(rj, (int)k);
-    if (ME_UNLIKELY(rjk != 0u)) {
-      R.rf = a_wl(R.rf, 0, (int)k);
-      R.rr = a_wl(R.rr, rjk == ME_RJ_BAD_QTY ? 0 : q, (int)k);
-      R.rs = a_wlu(R.rs, (uint32_t)ME_ST_REJECTED | (rjk << 8), (int)k);
-      R.rlo = a_wlu(R.rlo, w.evp, (int)k);
-      R.rn = a_wlu(R.rn, 0u, (int)k);
-      continue;
-    }
-    const uint32_t kd = rl32(okd, (int)k);
-    const bool buy = (kd & 3u) == ME_SIDE_BUY;
-    const bool mkt = (kd >> 2) & 1u;
-    const int lm = rli32(olm, (int)k);
-    const uint32_t ev_lo = w.evp;
-    uint32_t rem = (uint32_t)q;
-    uint32_t nte;
-    if (buy) {
-      a_take<1>(w, A, mkt ? L - 1 : lm, rem, jt | AGG_TAKE);
-      nte = w.evp - ev_lo;
+    const uint32_t cw = rl32(ocw, (int)k);
+    if (ME_UNLIKELY((cw >> LW_RJ_SHIFT) != 0u)) continue;  // rejected: no chain work (a_result: from cw)
+    const uint32_t jt = jb + k;
+    uint32_t rem = (uint32_t)rli32(oq, (int)k);
+    const int lm = (int)(cw & LW_LIM);
+    const bool mkt = (cw & LW_MKT) != 0u;
+    if (cw & LW_BUY) {
+      a_take<1>(w, A, lm, rem, jt | AGG_TAKE);  // (a MARKET's lm is the window's far end)
       if (!mkt && rem) a_rest<0>(w, B, L - 1 - lm, lm, (int)rem, jt);
     } else {
-      a_take<0>(w, B, mkt ? L - 1 : L - 1 - lm, rem, jt | AGG_TAKE);
-      nte = w.evp - ev_lo;
+      a_take<0>(w, B, L - 1 - lm, rem, jt | AGG_TAKE);
       if (!mkt && rem) a_rest<1>(w, A, lm, lm, (int)rem, jt);
     }
-    const int filled = q - (int)rem;
-    uint32_t stt;
-    if (mkt)
-      stt = rem == 0 ? ME_ST_FILLED : ME_ST_CANCELED;
-    else
-      stt = rem == 0 ? ME_ST_FILLED : (filled > 0 ? ME_ST_PARTIALLY_FILLED : ME_ST_NEW);
-    R.rf = a_wl(R.rf, filled, (int)k);
-    R.rr = a_wl(R.rr, (int)rem, (int)k);
-    R.rs = a_wlu(R.rs, stt, (int)k);
-    R.rlo = a_wlu(R.rlo, ev_lo, (int)k);
-    R.rn = a_wlu(R.rn, nte, (int)k);
+    asm volatile("s_mov_b32 m0, %1\n\tv_writelane_b32 %0, %2, m0" : "+v"(rr) : "s"(k), "s"(auniu(rem)) : "m0");
   }
   return k;
 }
@@ -450,7 +454,11 @@ __device__ __forceinline__ void a_walk_init(AWalk& w, const BookDev& bk, const A
   w.ev = (gptr<AggEv>)vptr(ag.ev);
   w.locc = locc;
   w.evp = eb;
+#if ME_LIST_EMIT
+  w.vl = w.vj = w.vq = 0u;
+#else
   w.stg = stg;
+#endif
   w.L = (int)bk.L;
   w.W = (int)bk.Lwords;
   for (int k = lane_id(); k < w.W; k += 64) locc[k] = w.occ[k];
@@ -477,7 +485,6 @@ __device__ __forceinline__ void a_walk_end(AWalk& w, AList& A, AList& B, int& bb
 // copies at every join of the record loop). Exact while the symbol's whole book stays below 2^31: the
 // walk starts only if the book's sum is, and adds every block's quantities to that bound before the
 // block runs (a block that could cross it goes to the generic loop, from its first record on).
-constexpr uint32_t LW_BUY = 1u << 15, LW_MKT = 1u << 16, LW_RJ_SHIFT = 17, LW_LIM = 0x7FFFu;
 constexpr unsigned long long LW_CAP = 1ull << 31;
 
 struct LWalk {
@@ -936,9 +943,7 @@ __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const Agg
     } else {
       a_refill(w, A, B);
       GW_T(1);
-      ARes R;
-      k = a_block(w, A, B, oq, okd, olm, rj, j, fastm, cntb, R);
-      rr = R.rr;
+      k = a_block(w, A, B, oq, lw_cw(okd, olm, rj, L), blk, fastm, cntb, rr);
     }
     GW_T(2);
 #ifdef ME_STAMPS
@@ -990,7 +995,7 @@ __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const Agg
 
 __global__ __launch_bounds__(64) void k_agg_walk(BookDev bk, BatchDev bt, AggDev ag) {
   __shared__ unsigned long long locc[AGG_WORDS];
-  __shared__ AggEv stg[128];
+  __shared__ AggEv stg[128];  // (the list walk's LDS event staging, ME_LIST_EMIT=0)
   extern __shared__ uint32_t ltot[];  // the ladder walk's totals [L] and dummy slots [64]
   const uint32_t nh = min(*(volatile uint32_t*)bk.hcount, bk.S);
   for (uint32_t i = blockIdx.x; i < nh; i += gridDim.x) {
