@@ -2292,6 +2292,7 @@ constexpr uint32_t GR_THREADS = GR_WAVES * 64;
                   // symbols) in one round (same-box A/B, profiles/r4/g2: 640 steps 2,300 -> 2,515M, the group
                   // launch 588 -> 560 us at the driver shape; 6 was the round-3 choice)
 #endif
+constexpr uint64_t GR_FOUR_BELOW = 512;  // records per symbol per group below which the resolve runs 4 waves
 constexpr uint32_t GR_STAGE = 48;  // consumed makers / emptied chunks a level stages in LDS (else: HBM)
 
 struct GrLevel {  // what phase B found for one level
@@ -2302,17 +2303,18 @@ struct GrStage {  // a wave's maker / emptied-chunk staging (phases B and D)
   AggMk mk[GR_STAGE];
   uint32_t fr[GR_STAGE];
 };
+template <int NW>
 struct GrShared {
   union {
-    uint32_t wh[GR_WAVES][128];  // phase A: per-wave level histograms, then scatter cursors
-    GrStage st[GR_WAVES];
+    uint32_t wh[NW][128];  // phase A: per-wave level histograms, then scatter cursors
+    GrStage st[NW];
   } u;
   GrLevel lv[128];
   uint32_t lstart[129];
   uint32_t lhead[128], ltail[128];
   uint32_t lvlist[128];
   uint32_t gev[ME_GMAX + 1], gex[ME_GMAX + 1], gbase[ME_GMAX + 1];
-  uint32_t wsum[GR_WAVES];
+  uint32_t wsum[NW];
   uint32_t nlv, next, next2, cur_mk, cur_fr, deficit, alloc_base;
   int dresting;
   uint8_t ltend[128];
@@ -2325,9 +2327,9 @@ __device__ __forceinline__ uint32_t gr_take(uint32_t* ctr) {
   return rl32(i, 0);
 }
 
-template <bool kLds>
+template <int NW, bool kLds>
 __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& ga, const AggSrc& src, const AggDev& ag,
-                                            uint32_t s, const AggSlot& sl, GrShared& sh, uint32_t* nf) {
+                                            uint32_t s, const AggSlot& sl, GrShared<NW>& sh, uint32_t* nf) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint32_t L = bk.L;  // <= 128
   const uint32_t eb = sl.ev_base, n = sl.ev_cnt, ng = ga.ng;
@@ -2360,7 +2362,7 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
   wave_mem_order();
   // each wave owns a contiguous 64-aligned log range: its level histogram, then a stable scatter of the
   // same range
-  const uint32_t per = ((n + GR_WAVES - 1u) / GR_WAVES + 63u) & ~63u;
+  const uint32_t per = ((n + NW - 1u) / NW + 63u) & ~63u;
   const uint32_t r0 = min(n, (uint32_t)wv * per), r1 = min(n, r0 + per);
 #pragma unroll 4
   for (uint32_t b = r0; b < r1; b += 64) {
@@ -2370,7 +2372,7 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
   __syncthreads();
   if (wv == 0) {
     uint32_t c0 = 0, c1 = 0;
-    for (int w = 0; w < GR_WAVES; ++w) {
+    for (int w = 0; w < NW; ++w) {
       c0 += sh.u.wh[w][lane];
       c1 += sh.u.wh[w][64 + lane];
     }
@@ -2384,7 +2386,7 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
     if (c0) sh.lvlist[__popcll(m0 & lanemask_lt())] = (uint32_t)lane;
     if (c1) sh.lvlist[__popcll(m0) + __popcll(m1 & lanemask_lt())] = 64u + (uint32_t)lane;
     if (lane == 0) sh.nlv = (uint32_t)(__popcll(m0) + __popcll(m1));
-    for (int w = 0; w < GR_WAVES; ++w) {  // wave w's events of level l start at its running base
+    for (int w = 0; w < NW; ++w) {  // wave w's events of level l start at its running base
       const uint32_t x0 = sh.u.wh[w][lane], x1 = sh.u.wh[w][64 + lane];
       sh.u.wh[w][lane] = a0;
       sh.u.wh[w][64 + lane] = a1;
@@ -2681,7 +2683,7 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
   __syncthreads();
   uint32_t ftot = 0, base = 0;
 #pragma unroll
-  for (int k = 0; k < GR_WAVES; ++k) {
+  for (int k = 0; k < NW; ++k) {
     const uint32_t w = sh.wsum[k];
     base += k < wv ? w : 0u;
     ftot += w;
@@ -2949,9 +2951,10 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
   GR_STAMP(bk, s, 7);
 }
 
-__global__ __launch_bounds__(GR_THREADS, GR_WPE) void k_agg_gres(BookDev bk, AggGArgs ga, AggSrc src, AggDev ag,
-                                                          uint32_t ne) {
-  __shared__ GrShared sh;
+template <int NW>
+__global__ __launch_bounds__(NW * 64, GR_WPE) void k_agg_gres(BookDev bk, AggGArgs ga, AggSrc src, AggDev ag,
+                                                       uint32_t ne) {
+  __shared__ GrShared<NW> sh;
   extern __shared__ uint32_t gr_dyn[];  // [ne] fill counts / offsets
   for (uint32_t s = blockIdx.x; s < bk.S; s += gridDim.x) {
     const AggSlot sl = ag.slot[s];
@@ -2961,9 +2964,9 @@ __global__ __launch_bounds__(GR_THREADS, GR_WPE) void k_agg_gres(BookDev bk, Agg
       continue;
     }
     if (sl.ev_cnt <= ne)
-      gres_symbol<true>(bk, ga, src, ag, s, sl, sh, gr_dyn);
+      gres_symbol<NW, true>(bk, ga, src, ag, s, sl, sh, gr_dyn);
     else
-      gres_symbol<false>(bk, ga, src, ag, s, sl, sh, ag.evn + sl.ev_base);
+      gres_symbol<NW, false>(bk, ga, src, ag, s, sl, sh, ag.evn + sl.ev_base);
     __syncthreads();
   }
 }
@@ -3014,7 +3017,13 @@ hipError_t launch_agg_group(hipStream_t st, const BookDev& bk, const BatchDev* b
   ga.seq0 = bt[0].seq;
   ga.slab = bt[0].slab;
   ga.ng = ng;
-  const uint32_t grid = bk.S < 2048u ? bk.S : 2048u;
+  // one workgroup per symbol up to the grid cap, then symbols striding over the grid (blockIdx = symbol mod
+  // grid: a symbol's walk and resolve run on the same XCD either way)
+  static const uint32_t gcap = [] {
+    const char* e = getenv("ME_AGG_GRID");
+    return e && atoi(e) > 0 ? (uint32_t)atoi(e) : 65536u;
+  }();
+  const uint32_t grid = bk.S < gcap ? bk.S : gcap;
   static const bool helper = [] {
     const char* e = getenv("ME_GW_HELPER");
     return !e || atoi(e) != 0;
@@ -3029,9 +3038,20 @@ hipError_t launch_agg_group(hipStream_t st, const BookDev& bk, const BatchDev* b
   for (uint32_t g = 0; g < ng; ++g) recs += bt[g].n;
   uint64_t ne = (recs * 7u / 4u) / (bk.S ? bk.S : 1u) + 256u;  // (config 2: 1.4 events per record)
   ne = (ne + 63u) & ~63ull;
-  const uint64_t ne_cap = ((64u << 10) - sizeof(GrShared)) / 4u & ~63ull;
+  // resolve workgroups of 8 waves, or of 4 for groups with few records per symbol (config 3's ~210: twice
+  // the workgroups in flight); ME_GRES_WAVES=4/8 forces either
+  static const int gw_env = [] {
+    const char* e = getenv("ME_GRES_WAVES");
+    return e ? atoi(e) : 0;
+  }();
+  const bool four = gw_env ? gw_env == 4 : recs / (bk.S ? bk.S : 1u) < GR_FOUR_BELOW;
+  const uint64_t ne_cap = ((64u << 10) - (four ? sizeof(GrShared<4>) : sizeof(GrShared<GR_WAVES>))) / 4u & ~63ull;
   if (ne > ne_cap) ne = ne_cap;
-  hipLaunchKernelGGL(k_agg_gres, dim3(grid), dim3(GR_THREADS), (size_t)ne * 4u, st, bk, ga, src, ag, (uint32_t)ne);
+  if (four)
+    hipLaunchKernelGGL(k_agg_gres<4>, dim3(grid), dim3(256), (size_t)ne * 4u, st, bk, ga, src, ag, (uint32_t)ne);
+  else
+    hipLaunchKernelGGL(k_agg_gres<GR_WAVES>, dim3(grid), dim3(GR_THREADS), (size_t)ne * 4u, st, bk, ga, src, ag,
+                       (uint32_t)ne);
   return hipGetLastError();
 }
 }  // namespace me
