@@ -40,6 +40,9 @@ namespace me {
 namespace {
 
 constexpr uint32_t AGG_WORDS = AGG_MAX_L / 64;
+#ifndef ME_WALK_PRIO
+#define ME_WALK_PRIO 1  // s_setprio(3) on the walking waves (0: off; profiles/r5/prio)
+#endif
 #ifndef ME_LIST_EMIT
 #define ME_LIST_EMIT 0  // the list walk's event staging: 0 LDS (one 16-B lane-0 write per event), 1 VGPR lanes
 #endif
@@ -994,6 +997,9 @@ __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const Agg
 }
 
 __global__ __launch_bounds__(64) void k_agg_walk(BookDev bk, BatchDev bt, AggDev ag) {
+#if ME_WALK_PRIO
+  __builtin_amdgcn_s_setprio(3);  // the serial chain before the short chains of k_match sharing its SIMD
+#endif
   __shared__ unsigned long long locc[AGG_WORDS];
   __shared__ AggEv stg[128];  // (the list walk's LDS event staging, ME_LIST_EMIT=0)
   extern __shared__ uint32_t ltot[];  // the ladder walk's totals [L] and dummy slots [64]
@@ -2106,6 +2112,9 @@ __global__ __launch_bounds__(128) void k_agg_gwalk2(BookDev bk, AggGArgs ga, Agg
   __shared__ GwShared sh;
   const int lane = lane_id();
   const bool walker = auni((int)(threadIdx.x >> 6)) == 0;
+#if ME_WALK_PRIO
+  if (walker) __builtin_amdgcn_s_setprio(3);  // the chain before the helper waves sharing its SIMD
+#endif
   const int L = (int)bk.L;  // <= 128
   const uint32_t ng = ga.ng;
   for (uint32_t s = blockIdx.x; s < bk.S; s += gridDim.x) {
