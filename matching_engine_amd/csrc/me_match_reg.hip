@@ -1124,6 +1124,9 @@ struct SideArgs {
 #endif
 constexpr int SIDE_THREADS = ME_SIDE_THREADS;
 constexpr int SIDE_WAVES = SIDE_THREADS / 64;
+#ifndef ME_TAPE_XCD
+#define ME_TAPE_XCD 1  // tape tiles: each half of a batch's tape on one XCD (1) or dealt over all (0); profiles/r5/tx
+#endif
 constexpr uint32_t SB_REC = ME_SB_REC;             // records per bucket workgroup
 constexpr uint32_t SB_PER = SB_REC / SIDE_THREADS;  // records per thread
 constexpr uint32_t SB_SMAX = 16383;                // symbols bucketed through an LDS histogram (64 KB)
@@ -1260,6 +1263,24 @@ __global__ __launch_bounds__(SIDE_THREADS) void k_side(SideArgs args, uint32_t n
     }
   }
   const uint32_t nt = ldsu(G.ax.nt);
+#if ME_TAPE_XCD
+  // Each half of a batch's tape on one XCD (blocks b = x mod 8 under round-robin placement; speed only): a
+  // 128-B line of a symbol's scratch slab holds fills of takers ~16 tiles apart, so the tiles that read it
+  // meet in one L2 instead of fetching the line once per XCD. Halves, not batches, keep the XCDs balanced.
+  if (gridDim.x - nbu >= 8u) {
+    const uint32_t x = blockIdx.x % 8u;
+    const uint32_t b0 = nbu + (x + 8u - nbu % 8u) % 8u;  // the first tape block on XCD x
+    const uint32_t AX = ((gridDim.x - b0 + 7u) / 8u) * SIDE_WAVES, ax = ((blockIdx.x - b0) / 8u) * SIDE_WAVES + wv;
+    for (uint32_t v = x; v < 2u * nt; v += 8u) {
+      const uint32_t j = v >> 1, h = v & 1u;
+      const uint32_t tn = ldsu(G.ax.t[j].tn);
+      const uint32_t ntiles = (tn + TILE_TAPE - 1) / TILE_TAPE, half = (ntiles + 1u) / 2u;
+      const uint32_t t0 = h * half, t1 = min(ntiles, t0 + half);
+      for (uint32_t t = t0 + ax; t < t1; t += AX) aux_tape_tile(G, j, t, ntiles, tn);
+    }
+    return;
+  }
+#endif
   off = 0;
   for (uint32_t j = 0; j < nt; ++j) {
     const uint32_t tn = ldsu(G.ax.t[j].tn);
