@@ -18,6 +18,8 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "me_far.hpp"
 #include "me_layout.hpp"
 #include "me_wave.hpp"
@@ -2636,8 +2638,16 @@ hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* b
     // after this (host batches' tapes) wait for the side jobs
     return fork ? hipStreamWaitEvent(st, hot->sjoin, 0) : hipSuccess;
   }
-  return big ? rc64::launch_match_reg(st, bk, bt, ng, ax, ev0, ev1)
-             : rc128::launch_match_reg(st, bk, bt, ng, ax, ev0, ev1);
+  // a launch with no match job (the pipeline's fill and drain): its bucket units too per XCD in turn (one
+  // batch's buckets per L2 at a time; driver shape +1 %, profiles/r5/fx); ME_FILL_XSEQ=0: all at once
+  static const bool fill_xseq = [] {
+    const char* e = getenv("ME_FILL_XSEQ");
+    return !e || atoi(e) != 0;
+  }();
+  AuxDev axx = ax;
+  if (ng == 0 && fill_xseq) axx.xseq = 1u;
+  return big ? rc64::launch_match_reg(st, bk, bt, ng, axx, ev0, ev1)
+             : rc128::launch_match_reg(st, bk, bt, ng, axx, ev0, ev1);
 }
 
 // ev0 / ev1 (optional, timing): the launch records the kernel's own start and end
