@@ -25,7 +25,7 @@ cd $R
 KRE='k_agg|k_match_reg|k_side|k_seq_sweep|k_match|k_sort|k_tape|k_hot'
 
 bench_cmd() {  # WL K W
-  echo "python3 $R/bench.py --workload $1 --steps $2 --warmup $3 --no-cpu-baseline --no-e2e $BENCH_ARGS"
+  echo "python3 $R/bench.py --workload $1 --steps $2 --warmup $3 --no-cpu-baseline --no-e2e --no-fills-check $BENCH_ARGS"
 }
 
 for step in "$@"; do
