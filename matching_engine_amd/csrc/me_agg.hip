@@ -3053,10 +3053,14 @@ hipError_t launch_agg_group(hipStream_t st, const BookDev& bk, const BatchDev* b
     const char* e = getenv("ME_GRES_WAVES");
     return e ? atoi(e) : 0;
   }();
-  const bool four = gw_env ? gw_env == 4 : recs / (bk.S ? bk.S : 1u) < GR_FOUR_BELOW;
-  const uint64_t ne_cap = ((64u << 10) - (four ? sizeof(GrShared<4>) : sizeof(GrShared<GR_WAVES>))) / 4u & ~63ull;
+  const uint64_t per_sym = recs / (bk.S ? bk.S : 1u);
+  const int nw = gw_env == 2 || gw_env == 4 || gw_env == 8 ? gw_env : per_sym < GR_FOUR_BELOW ? 4 : 8;
+  const size_t shb = nw == 2 ? sizeof(GrShared<2>) : nw == 4 ? sizeof(GrShared<4>) : sizeof(GrShared<GR_WAVES>);
+  const uint64_t ne_cap = ((64u << 10) - shb) / 4u & ~63ull;
   if (ne > ne_cap) ne = ne_cap;
-  if (four)
+  if (nw == 2)
+    hipLaunchKernelGGL(k_agg_gres<2>, dim3(grid), dim3(128), (size_t)ne * 4u, st, bk, ga, src, ag, (uint32_t)ne);
+  else if (nw == 4)
     hipLaunchKernelGGL(k_agg_gres<4>, dim3(grid), dim3(256), (size_t)ne * 4u, st, bk, ga, src, ag, (uint32_t)ne);
   else
     hipLaunchKernelGGL(k_agg_gres<GR_WAVES>, dim3(grid), dim3(GR_THREADS), (size_t)ne * 4u, st, bk, ga, src, ag,
