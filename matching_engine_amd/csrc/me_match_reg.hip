@@ -537,14 +537,20 @@ __device__ __forceinline__ bool reg_rest(RegCtx& c, int lvl, unsigned long long 
 // other case (a far level, a stale ring entry of an order older than the horizon) returns HANDOFF
 // before anything changed, and the continuation launch (kSlow = true) does the whole cancel.
 constexpr uint32_t HANDOFF = 0xFFFFFFFFu;
+// gh: the ring entry read for the whole block at its start (NIL: none); a slot it names is verified like
+// any other, and one that does not hold tgt sends the cancel to the ring as if there were no hint.
 template <bool kSlow>
-__device__ __forceinline__ uint32_t reg_cancel(RegCtx& c, unsigned long long tgt) {
+__device__ __forceinline__ uint32_t reg_cancel(RegCtx& c, unsigned long long tgt, uint32_t gh) {
   const int lane = lane_id();
   const bool act = lane < ME_C;
   if (tgt == 0ull) return 0;
-  wave_mem_order();
-  uint32_t g = rl32(c.loc[tgt & c.rmask], 0);
-  __builtin_amdgcn_s_waitcnt(VMCNT0);
+  bool hinted = gh != NIL;
+  uint32_t g = gh;
+  if (!hinted) {
+    wave_mem_order();
+    g = rl32(c.loc[tgt & c.rmask], 0);
+    __builtin_amdgcn_s_waitcnt(VMCNT0);
+  }
   for (int pass = 0;; ++pass) {
     if (g != NIL && g / ME_C < c.nchunks) {
       const uint32_t ch = g / ME_C, slot = g % ME_C;
@@ -627,6 +633,14 @@ __device__ __forceinline__ uint32_t reg_cancel(RegCtx& c, unsigned long long tgt
         c.resting -= 1;
         return (uint32_t)q;
       }
+    }
+    if (hinted) {  // the block-start entry is stale: the ring now
+      hinted = false;
+      wave_mem_order();
+      g = rl32(c.loc[tgt & c.rmask], 0);
+      __builtin_amdgcn_s_waitcnt(VMCNT0);
+      --pass;
+      continue;
     }
     // the ring entry is someone else's: only an order older than the horizon can still be live
     if (pass != 0 || tgt >= ldsu(c.M->horizon)) return 0;
@@ -1609,6 +1623,13 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
         if (!v) rj = 0xFFu;  // lanes past the run (or before the continuation point): no record
       }
       unsigned long long work = __ballot(rj == ME_RJ_NONE);
+      // cancels: every target's ring entry in one gather at the block start, so that a cancel's chunk read
+      // is its only round trip on the chain (the ring load in reg_cancel was the other; reg_cancel verifies
+      // the slot a hint names). No wait here: a block-start vmcnt(0) also waits for the stores of the block
+      // before (measured slower: 1,003 -> 990M on config 5, profiles/r5/cx)
+      const unsigned long long cxm = __ballot(rj == ME_RJ_NONE && (cw & CW_CXL));
+      uint32_t gpre = NIL;
+      if (cxm && ((cxm >> lane) & 1ull)) gpre = c.loc[(unsigned long long)opx_ & c.rmask];
       uint32_t stop = cnt;  // records [0, stop) of the block get results
       bool handoff = false;
       if constexpr (!kSlow) {  // from the first record that needs a far level on: the continuation's
@@ -1635,7 +1656,10 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
         COUNT(c, CT_FAST);
         STAMP_ADD(c, PH_SWEEP);
         if (ME_UNLIKELY(ctl & CW_CXL)) {
-          outq = reg_cancel<kSlow>(c, (unsigned long long)rli64(opx_, k));
+          const unsigned long long tgt = (unsigned long long)rli64(opx_, k);
+          // (a target an earlier record of this block rested as: its block-start ring entry is stale)
+          const bool inblk = __ballot(lane < k && oseq_ == tgt) != 0ull;
+          outq = reg_cancel<kSlow>(c, tgt, inblk ? NIL : rl32(gpre, k));
           if (!kSlow && ME_UNLIKELY(outq == HANDOFF)) {
             stop = (uint32_t)k;
             handoff = true;
