@@ -493,6 +493,7 @@ constexpr unsigned long long LW_CAP = 1ull << 31;
 struct LWalk {
   uint32_t* tot;     // LDS [L] (empty levels hold 0)
   uint32_t* dummy;   // LDS [64]: the other lanes' targets of a one-lane LDS operation
+  uint32_t* occ;     // LDS [L / 32]: occupancy bitmap of the OCC form (bit l: level l's total is nonzero), or null
   int bb, ba;        // best bid (-1: none), best ask (L: none)
   uint32_t cbb, cba; // cached totals of the best levels
   int L;
@@ -502,8 +503,31 @@ struct LWalk {
 // smallest occupied level >= x, or L: a scan of the LDS totals. Only levels on the side being searched
 // lie there (the other side's cached best, whose LDS copy is stale, is on the other side of x).
 // (*tot: its total, read by the scan itself — no second LDS round trip on the chain)
+__device__ __forceinline__ uint32_t lw_get(const LWalk& w, int l);
+// The OCC form (deep ladders: config 4's hot symbols trade across gaps of hundreds of empty levels): the
+// lanes read 64 consecutive 64-bit occupancy words at once, so one LDS read crosses 4,096 levels, and a
+// second reads the found level's total.
+template <bool OCC = false>
 __device__ __forceinline__ int lw_next(const LWalk& w, int x, uint32_t& tot) {
   const int lane = lane_id();
+  if constexpr (OCC) {
+    const unsigned long long* oc = reinterpret_cast<const unsigned long long*>(w.occ);
+    const int nw = w.L >> 6, w0 = x >> 6;
+    for (int wb = w0; wb < nw; wb += 64) {
+      const int wi = wb + lane;
+      unsigned long long m = wi < nw ? oc[wi] : 0ull;
+      if (wi == w0) m &= ~0ull << (x & 63);
+      const unsigned long long nz = __ballot(m != 0ull);
+      if (nz) {
+        const int i = __builtin_ctzll(nz);
+        const int l = ((wb + i) << 6) + __builtin_ctzll(rl64(m, i));
+        tot = lw_get(w, l);
+        return l;
+      }
+    }
+    tot = 0u;
+    return w.L;
+  }
   for (int b = x & ~63; b < w.L; b += 64) {
     const int l = b + lane;
     const uint32_t t = w.tot[l];  // (l < L + 64: beyond L, the dummy slots)
@@ -518,8 +542,27 @@ __device__ __forceinline__ int lw_next(const LWalk& w, int x, uint32_t& tot) {
   return w.L;
 }
 // largest occupied level <= x, or -1
+template <bool OCC = false>
 __device__ __forceinline__ int lw_prev(const LWalk& w, int x, uint32_t& tot) {
   const int lane = lane_id();
+  if constexpr (OCC) {  // lane i reads word w0 - i: the lowest lane with a bit holds the highest level
+    const unsigned long long* oc = reinterpret_cast<const unsigned long long*>(w.occ);
+    const int w0 = x >> 6;  // (x = -1: -1, no word)
+    for (int wb = w0; wb >= 0; wb -= 64) {
+      const int wi = wb - lane;
+      unsigned long long m = wi >= 0 ? oc[wi] : 0ull;
+      if (wi == w0) m &= ~0ull >> (63 - (x & 63));
+      const unsigned long long nz = __ballot(m != 0ull);
+      if (nz) {
+        const int i = __builtin_ctzll(nz);
+        const int l = ((wb - i) << 6) + 63 - __builtin_clzll(rl64(m, i));
+        tot = lw_get(w, l);
+        return l;
+      }
+    }
+    tot = 0u;
+    return -1;
+  }
   for (int b = x & ~63; b >= 0; b -= 64) {
     const int l = b + lane;
     const uint32_t t = w.tot[l];
@@ -546,6 +589,24 @@ __device__ __forceinline__ void lw_put(LWalk& w, int l, uint32_t v) {
 }
 __device__ __forceinline__ uint32_t lw_get(const LWalk& w, int l) {
   return rl32(__hip_atomic_load(&w.tot[l], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP), 0);
+}
+// The OCC form's bitmap: a level's bit is set by every rest that reaches its LDS total or makes it the best,
+// and cleared when a take empties it (non-returning one-lane LDS operations, like lw_add)
+template <bool OCC>
+__device__ __forceinline__ void lw_occ_set(LWalk& w, int l) {
+  if constexpr (OCC) {
+    const int lane = lane_id();
+    uint32_t* p = lane == 0 ? &w.occ[l >> 5] : &w.dummy[lane];
+    __hip_atomic_fetch_or(p, 1u << (l & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+}
+template <bool OCC>
+__device__ __forceinline__ void lw_occ_clr(LWalk& w, int l) {
+  if constexpr (OCC) {
+    const int lane = lane_id();
+    uint32_t* p = lane == 0 ? &w.occ[l >> 5] : &w.dummy[lane];
+    __hip_atomic_fetch_and(p, ~(1u << (l & 31)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
 }
 
 // The ladder walk's log staging: event i of the current 64-event block is lane i of three VGPRs, written
@@ -615,7 +676,7 @@ __device__ __forceinline__ void le_end(LEvG& e) {
 
 // A taker's partial take from the best level is the common case and stays out of the loop (no loop
 // entry, so none of the loop's register copies); the loop runs only when the best level empties.
-template <class LE>
+template <class LE, bool OCC = false>
 __device__ __forceinline__ void lw_take_buy(LE& e, LWalk& w, int lim, uint32_t& rem, uint32_t jt) {
   if (w.ba > lim) return;  // (rem > 0: rejected records never reach the chain)
   if (ME_LIKELY(w.cba > rem)) {
@@ -628,7 +689,8 @@ __device__ __forceinline__ void lw_take_buy(LE& e, LWalk& w, int lim, uint32_t& 
     le_emit(e, (uint32_t)w.ba, jt, w.cba);
     rem -= w.cba;
     lw_put(w, w.ba, 0u);  // empty levels hold 0 (a rest there adds)
-    w.ba = lw_next(w, w.ba + 1, w.cba);
+    lw_occ_clr<OCC>(w, w.ba);
+    w.ba = lw_next<OCC>(w, w.ba + 1, w.cba);
     if (!rem || w.ba > lim) return;
     if (w.cba > rem) {
       w.cba -= rem;
@@ -638,7 +700,7 @@ __device__ __forceinline__ void lw_take_buy(LE& e, LWalk& w, int lim, uint32_t& 
     }
   }
 }
-template <class LE>
+template <class LE, bool OCC = false>
 __device__ __forceinline__ void lw_take_sell(LE& e, LWalk& w, int lim, uint32_t& rem, uint32_t jt) {
   if (w.bb < lim) return;
   if (ME_LIKELY(w.cbb > rem)) {
@@ -651,7 +713,8 @@ __device__ __forceinline__ void lw_take_sell(LE& e, LWalk& w, int lim, uint32_t&
     le_emit(e, (uint32_t)w.bb, jt, w.cbb);
     rem -= w.cbb;
     lw_put(w, w.bb, 0u);
-    w.bb = lw_prev(w, w.bb - 1, w.cbb);
+    lw_occ_clr<OCC>(w, w.bb);
+    w.bb = lw_prev<OCC>(w, w.bb - 1, w.cbb);
     if (!rem || w.bb < lim) return;
     if (w.cbb > rem) {
       w.cbb -= rem;
@@ -662,7 +725,7 @@ __device__ __forceinline__ void lw_take_sell(LE& e, LWalk& w, int lim, uint32_t&
   }
 }
 // a bid rests at l (< ba: every ask up to the limit was taken)
-template <class LE>
+template <class LE, bool OCC = false>
 __device__ __forceinline__ void lw_rest_buy(LE& e, LWalk& w, int l, uint32_t q, uint32_t jt) {
   if (l == w.bb) {
     w.cbb += q;
@@ -670,12 +733,14 @@ __device__ __forceinline__ void lw_rest_buy(LE& e, LWalk& w, int l, uint32_t q, 
     if (w.bb >= 0) lw_put(w, w.bb, w.cbb);
     w.bb = l;
     w.cbb = q;
+    lw_occ_set<OCC>(w, l);
   } else {
     lw_add(w, l, q);
+    lw_occ_set<OCC>(w, l);
   }
   le_emit(e, (uint32_t)l, jt, q);
 }
-template <class LE>
+template <class LE, bool OCC = false>
 __device__ __forceinline__ void lw_rest_sell(LE& e, LWalk& w, int l, uint32_t q, uint32_t jt) {
   if (l == w.ba) {
     w.cba += q;
@@ -683,19 +748,24 @@ __device__ __forceinline__ void lw_rest_sell(LE& e, LWalk& w, int l, uint32_t q,
     if (w.ba < w.L) lw_put(w, w.ba, w.cba);
     w.ba = l;
     w.cba = q;
+    lw_occ_set<OCC>(w, l);
   } else {
     lw_add(w, l, q);
+    lw_occ_set<OCC>(w, l);
   }
   le_emit(e, (uint32_t)l, jt, q);
 }
 
 // The ladder from HBM: 32-bit LDS totals, the cached best totals, the book's sum (false: LW_CAP or more,
 // the ladder cannot hold the book)
-__device__ __forceinline__ bool lw_init(LWalk& w, const BookDev& bk, uint32_t s, uint32_t* lds, int bb, int ba) {
+// (occ: the OCC form's bitmap in LDS, built here from the totals; L a multiple of 64)
+__device__ __forceinline__ bool lw_init(LWalk& w, const BookDev& bk, uint32_t s, uint32_t* lds, int bb, int ba,
+                                        uint32_t* occ = nullptr) {
   const int lane = lane_id();
   w.L = (int)bk.L;
   w.tot = lds;
   w.dummy = lds + w.L;
+  w.occ = occ;
   const Level* lv = bk.levels + (size_t)s * bk.L;
   unsigned long long sum = 0;
   for (int b = 0; b < w.L; b += 16 * 64) {  // sixteen loads in flight per lane
@@ -710,6 +780,10 @@ __device__ __forceinline__ bool lw_init(LWalk& w, const BookDev& bk, uint32_t s,
       const int l = b + u * 64 + lane;
       if (l < w.L) w.tot[l] = (uint32_t)t[u];
       sum += (unsigned long long)t[u];
+      if (occ) {
+        const unsigned long long m = __ballot(l < w.L && t[u] != 0ll);
+        if (lane == 0 && b + u * 64 < w.L) reinterpret_cast<unsigned long long*>(occ)[(b + u * 64) >> 6] = m;
+      }
     }
   }
   w.ub = (unsigned long long)rli64(wave_incl_scan((long long)sum), 63);  // (DPP: no LDS round trips)
@@ -752,7 +826,7 @@ __device__ __forceinline__ uint32_t lw_cw(uint32_t okd, int olm, uint32_t rj, in
 }
 
 // (record r of the block logs its events with jt = (jb + r) << JS: scalar arithmetic, no v_readlane)
-template <int JS, class LE>
+template <int JS, class LE, bool OCC = false>
 __device__ __forceinline__ uint32_t lw_block(LE& e, LWalk& w, int oq, uint32_t ocw, uint32_t jb,
                                              unsigned long long fastm, uint32_t cnt, int& rr) {
   // the records the walk covers run up to the first it does not (k); rejected ones need no chain work:
@@ -792,15 +866,15 @@ __device__ __forceinline__ uint32_t lw_block(LE& e, LWalk& w, int oq, uint32_t o
     // (a MARKET's remainder is dropped: the rest is decided by one integer test — the opaque copy keeps
     // the compiler from re-deriving `!market && rem` as 64-bit boolean masks)
     if (cw & LW_BUY) {
-      lw_take_buy(e, w, lim, rem, jt | AGG_TAKE);
+      lw_take_buy<LE, OCC>(e, w, lim, rem, jt | AGG_TAKE);
       uint32_t rq = (cw & LW_MKT) ? 0u : rem;
       asm volatile("" : "+s"(rq));
-      if (rq) lw_rest_buy(e, w, lim, rq, jt);
+      if (rq) lw_rest_buy<LE, OCC>(e, w, lim, rq, jt);
     } else {
-      lw_take_sell(e, w, lim, rem, jt | AGG_TAKE);
+      lw_take_sell<LE, OCC>(e, w, lim, rem, jt | AGG_TAKE);
       uint32_t rq = (cw & LW_MKT) ? 0u : rem;
       asm volatile("" : "+s"(rq));
-      if (rq) lw_rest_sell(e, w, lim, rq, jt);
+      if (rq) lw_rest_sell<LE, OCC>(e, w, lim, rq, jt);
     }
     asm volatile("s_mov_b32 m0, %1\n\tv_writelane_b32 %0, %2, m0" : "+v"(rr) : "s"(r), "s"(auniu(rem)) : "m0");
   }
@@ -900,7 +974,10 @@ __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const Agg
   LWalk lw;
   LEv le;
   le_init(le, ag, eb);
-  const bool ladder = L <= (int)ag.ladder_max && lw_init(lw, bk, s, ltot, bb0, ba0);
+  // the OCC form (next level through an occupancy bitmap in LDS, in locc) for ladders deeper than lw_occ
+  const bool occf = ag.lw_occ && L > (int)ag.lw_occ && (L & 63) == 0;
+  const bool ladder = L <= (int)ag.ladder_max &&
+                      lw_init(lw, bk, s, ltot, bb0, ba0, occf ? reinterpret_cast<uint32_t*>(locc) : nullptr);
   if (!ladder) {
     a_rebuild<1>(w, A, ba0);
     a_rebuild<0>(w, B, L - 1 - bb0);
@@ -942,7 +1019,8 @@ __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const Agg
     if (ladder) {
       const bool adm = lw_admit(lw, v ? oq : 0);  // else: the generic loop from this block on
       GW_T(1);
-      k = lw_block<0>(le, lw, oq, lw_cw(okd, olm, rj, L), blk, adm ? fastm : 0ull, cntb, rr);
+      k = occf ? lw_block<0, LEv, true>(le, lw, oq, lw_cw(okd, olm, rj, L), blk, adm ? fastm : 0ull, cntb, rr)
+               : lw_block<0>(le, lw, oq, lw_cw(okd, olm, rj, L), blk, adm ? fastm : 0ull, cntb, rr);
     } else {
       a_refill(w, A, B);
       GW_T(1);

@@ -599,11 +599,16 @@ extern "C" me_engine* me_create(const me_config* cfg) {
     if (evc >= 0x7FFFFFFFull || frc >= 0xFFFFFFFFull) return bail("me_create: aggregate-path pools exceed 32-bit ids");
     a.ev_cap = (uint32_t)evc;
     // k_agg_walk's two forms: the ladder walk (32-bit LDS totals indexed by level) up to ladder_max
-    // levels, the top-of-book lists beyond — config 4's 32,768-level books, whose takes empty a level
-    // every record or so, run faster on the lists (their next level is in a register, the ladder's is
-    // an LDS scan away). ME_AGG_LADDER overrides (up to AGG_MAX_L; 0: lists only).
+    // levels, the top-of-book lists beyond (and for any book whose sum the 32-bit ladder cannot hold).
+    // ME_AGG_LADDER overrides (up to AGG_MAX_L; 0: lists only). Ladders deeper than lw_occ find the next
+    // occupied level through an occupancy bitmap in LDS (one read covers 4,096 levels) instead of scanning
+    // the totals 64 levels at a time: config 4's 32,768-level books, whose takes empty a level about every
+    // record with gaps of hundreds of levels to the next, ran 11.0M orders/s on the lists, 8.6M on the
+    // scanning ladder and 15.6M on the bitmap ladder (same box, profiles/r5/occ). ME_LW_OCC overrides (0: off).
     const char* vl = getenv("ME_AGG_LADDER");
-    a.ladder_max = vl ? (uint32_t)atoi(vl) : 256u;
+    a.ladder_max = vl ? (uint32_t)atoi(vl) : AGG_MAX_L;
+    const char* vo = getenv("ME_LW_OCC");
+    a.lw_occ = vo ? (uint32_t)atoi(vo) : 256u;
     a.mk_cap = (uint32_t)mkc;
     a.fr_cap = (uint32_t)frc;
     ALLOC(a.slot, S);

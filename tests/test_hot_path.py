@@ -45,10 +45,12 @@ def orc(built):
     return oracle
 
 
-def _engine(me, hot_min, *a, agg=1, ladder=None, **kw):
+def _engine(me, hot_min, *a, agg=1, ladder=None, occ=None, **kw):
     env = {"ME_HOT_MIN": str(hot_min), "ME_HOT_AGG": str(agg)}
     if ladder is not None:  # ME_AGG_LADDER: the largest window k_agg_walk's ladder walk takes (0: lists)
         env["ME_AGG_LADDER"] = str(ladder)
+    if occ is not None:  # ME_LW_OCC: ladders deeper than this search through the LDS occupancy bitmap (0: off)
+        env["ME_LW_OCC"] = str(occ)
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
@@ -89,13 +91,13 @@ def test_hot_drift_far_cancels(me, orc, hot_min, agg):
 @pytest.mark.parametrize("agg", [1, 0])
 def test_hot_sweeps_drain_lists(me, orc, agg):
     """MARKETs of up to 40 x 100 qty against thin levels: a sweep consumes more than the 64 listed
-    levels and the list is rebuilt mid-sweep; no cancels, no far prices."""
+    levels and the list is rebuilt mid-sweep (the list walk, ME_AGG_LADDER=0); no cancels, no far prices."""
     sc, base, batches = _drift(me, 4096, 3, 4096, 40, cancel_pct=0, far_pct=0, market_qty_mult=40,
                                market_pct=10, drift_every=0, drift_step=0)
     ob = orc.OracleBook(sc.num_symbols)
     total = sum(len(b) for b in batches)
-    with _engine(me, 1, sc.num_symbols, sc.levels, base, agg=agg, max_batch=sc.batch, max_resting=total + 64,
-                 max_chunks=total + 64) as eng:
+    with _engine(me, 1, sc.num_symbols, sc.levels, base, agg=agg, ladder=0, max_batch=sc.batch,
+                 max_resting=total + 64, max_chunks=total + 64) as eng:
         nf = run_both(eng, ob, batches, ctx=f"hot sweeps agg={agg}")
     assert nf > 0
 
@@ -160,11 +162,10 @@ def test_agg_single_symbol_config1(me, orc, levels):
     assert nf > 0
 
 
-@pytest.mark.parametrize("levels,ladder", [(256, 0), (2048, 32768)])
+@pytest.mark.parametrize("levels,ladder", [(256, 0), (2048, 0)])
 def test_agg_config1_walk_forms(me, orc, levels, ladder):
-    """Config 1's shape on the walk form the default does not pick at that window (ME_AGG_LADDER): the
-    top-of-book lists at L = 256 (they also take any book the 32-bit ladder cannot hold), the ladder at
-    L = 2,048."""
+    """Config 1's shape on the walk form the default does not pick (ME_AGG_LADDER=0): the top-of-book
+    lists, which also take any book the 32-bit ladder cannot hold, at L = 256 and 2,048."""
     sc = me.preset(1, levels=levels, batch=16384)
     st = me.Stream(sc)
     base = st.base_prices()
@@ -193,16 +194,77 @@ def test_agg_large_quantities(me, orc, levels, max_qty):
         assert run_both(eng, ob, batches, ctx=f"agg qty<={max_qty} L={levels}") > 0
 
 
+@pytest.mark.parametrize("ladder", [None, 0])
 @pytest.mark.parametrize("spread", [2, 40, 400])
-def test_agg_many_symbols_no_handoff(me, orc, spread):
+def test_agg_many_symbols_no_handoff(me, orc, spread, ladder):
     """Every symbol hot (ME_HOT_MIN=1) on a 1,024-level window, no cancels, no far prices: the aggregate
     path alone, with tight spreads (long FIFOs, sweeps through many makers per level) and wide ones
-    (deep rests beyond the 64-entry lists, list rebuilds)."""
+    (deep rests beyond the 64-entry lists, list rebuilds), on the default walk (the bitmap ladder) and on
+    the list walk (ME_AGG_LADDER=0)."""
     sc, base, batches = _drift(me, 1024, 40, 8192, 25, cancel_pct=0, far_pct=0, spread_ticks=spread,
                                drift_every=0, drift_step=0, market_qty_mult=4, market_pct=20)
     ob = orc.OracleBook(sc.num_symbols)
     total = sum(len(b) for b in batches)
-    with _engine(me, 1, sc.num_symbols, sc.levels, base, max_batch=sc.batch, max_resting=total + 64,
-                 max_chunks=total + 64) as eng:
-        nf = run_both(eng, ob, batches, ctx=f"agg many spread={spread}")
+    with _engine(me, 1, sc.num_symbols, sc.levels, base, ladder=ladder, max_batch=sc.batch,
+                 max_resting=total + 64, max_chunks=total + 64) as eng:
+        nf = run_both(eng, ob, batches, ctx=f"agg many spread={spread} ladder={ladder}")
     assert nf > 0
+
+
+@pytest.mark.parametrize("occ", [256, 0])
+@pytest.mark.parametrize("levels", [2048, 32768])
+def test_agg_ladder_occ_config1(me, orc, levels, occ):
+    """The ladder walk on deep windows (ME_AGG_LADDER=32768) in both next-level forms: the occupancy
+    bitmap in LDS (ME_LW_OCC=256: bits set by rests, cleared by the takes that empty a level, one read per
+    4,096 levels) and the 64-level scan of the totals (0); config 1's shape, every batch against the
+    oracle."""
+    sc = me.preset(1, levels=levels, batch=16384)
+    st = me.Stream(sc)
+    base = st.base_prices()
+    batches = [st.next(sc.batch) for _ in range(8)]
+    ob = orc.OracleBook(sc.num_symbols)
+    total = sum(len(b) for b in batches)
+    with _engine(me, 512, sc.num_symbols, sc.levels, base, ladder=32768, occ=occ, max_batch=sc.batch,
+                 max_resting=total + 64, max_chunks=total + 64) as eng:
+        assert run_both(eng, ob, batches, ctx=f"agg c1 L={levels} occ={occ}") > 0
+
+
+@pytest.mark.parametrize("spread", [2, 400, 3000])
+def test_agg_ladder_occ_wide_spreads(me, orc, spread):
+    """The bitmap form where it matters: every symbol hot on an 8,192-level window with spreads up to 3,000
+    ticks (gaps of hundreds of empty levels between the bests, sweeps emptying level after level, rests at
+    the far ends of the window in words no other level shares), no cancels, no far prices."""
+    sc, base, batches = _drift(me, 8192, 24, 8192, 20, cancel_pct=0, far_pct=0, spread_ticks=spread,
+                               drift_every=0, drift_step=0, market_qty_mult=6, market_pct=20)
+    ob = orc.OracleBook(sc.num_symbols)
+    total = sum(len(b) for b in batches)
+    with _engine(me, 1, sc.num_symbols, sc.levels, base, ladder=32768, max_batch=sc.batch,
+                 max_resting=total + 64, max_chunks=total + 64) as eng:
+        assert run_both(eng, ob, batches, ctx=f"agg occ spread={spread}") > 0
+
+
+def test_agg_ladder_occ_drift_far_cancels(me, orc):
+    """The bitmap form behind the generic fallbacks: drifting mids, far LIMITs, cancels and re-centring
+    hand symbols to k_match_hot_cont, whose book the next batch's ladder (and bitmap) is rebuilt from."""
+    sc, base, batches = _drift(me, 2048, 6, 6144, 40)
+    ob = orc.OracleBook(sc.num_symbols)
+    total = sum(len(b) for b in batches)
+    with _engine(me, 64, sc.num_symbols, sc.levels, base, ladder=32768, max_batch=sc.batch,
+                 max_resting=total + 64, max_chunks=total + 64) as eng:
+        assert run_both(eng, ob, batches, ctx="agg occ drift") > 0
+
+
+def test_agg_ladder_occ_config4(me, orc):
+    """Config 4's shape (Zipf symbols, L = 32,768, books seeded to 3,000 levels per side) with the hot
+    symbols on the ladder's bitmap form: every batch, and the books, against the oracle."""
+    sc = me.preset(4, num_symbols=300, batch=32768)
+    st = me.Stream(sc)
+    base = st.base_prices()
+    seeds = st.seed_books(range(8), 3000)
+    batches = [seeds.take(slice(i, i + 32768)) for i in range(0, len(seeds), 32768)]
+    batches += [st.next(sc.batch) for _ in range(4)]
+    ob = orc.OracleBook(sc.num_symbols)
+    total = sum(len(b) for b in batches)
+    with _engine(me, 512, sc.num_symbols, sc.levels, base, ladder=32768, max_batch=32768,
+                 max_resting=total + 1024, max_chunks=total + 1024) as eng:
+        assert run_both(eng, ob, batches, ctx="agg occ c4") > 0
