@@ -1308,6 +1308,7 @@ constexpr uint32_t LV_STAGE = 64;  // consumed makers / emptied chunks a level k
 // chunk C ends in updated; each take's first maker and fill count (binary search in the staged list);
 // what the surviving rests need. A level whose takes consume more than LV_STAGE makers (or empty more
 // chunks) reads its FIFO a second time, writing straight into HBM.
+template <bool COUNT>
 __global__ __launch_bounds__(256) void k_agg_levels(BookDev bk, AggSrc src, AggDev ag) {
   __shared__ AggMk smk[4][LV_STAGE];
   __shared__ uint32_t sfr[4][LV_STAGE];
@@ -1341,7 +1342,7 @@ __global__ __launch_bounds__(256) void k_agg_levels(BookDev bk, AggSrc src, AggD
       const AggEv E = entry(b);
       const bool v = b + (uint32_t)lane < cnt;
       const bool tk = v && (E.j & AGG_TAKE) != 0u;
-      if (v && !tk) ag.evn[E.pad] = 0u;
+      if (!COUNT && v && !tk) ag.evn[E.pad] = 0u;
       C += (unsigned long long)rli64(wave_incl_scan(tk ? (long long)E.qty : 0ll), 63);
     }
     // 2. the initial FIFO, read once: consumed makers and emptied chunks staged in LDS; the chunk C ends
@@ -1374,14 +1375,14 @@ __global__ __launch_bounds__(256) void k_agg_levels(BookDev bk, AggSrc src, AggD
       const bool cons = q > 0 && W + ex < C;
       const unsigned long long cm = __ballot(cons);
       const uint32_t r = nmk + (uint32_t)__popcll(cm & lanemask_lt());
-      if (cons && r < LV_STAGE) {
+      if (!COUNT && cons && r < LV_STAGE) {
         mkl[r].seq = sq;
         mkl[r].end = en;
       }
       nmk += (uint32_t)__popcll(cm);
       nfull += (uint32_t)__popcll(__ballot(q > 0 && en <= C));
       if (W + live <= C) {  // emptied
-        if (lane == 0 && nfreed < LV_STAGE) frl[nfreed] = ch;
+        if (!COUNT && lane == 0 && nfreed < LV_STAGE) frl[nfreed] = ch;
         ++nfreed;
         W += live;
         ch = nx;
@@ -1409,7 +1410,7 @@ __global__ __launch_bounds__(256) void k_agg_levels(BookDev bk, AggSrc src, AggD
         const bool cons = rs && st0 < Cr;
         const unsigned long long cm = __ballot(cons);
         const uint32_t r = nmk + nrc + (uint32_t)__popcll(cm & lanemask_lt());
-        if (cons && r < LV_STAGE) {
+        if (!COUNT && cons && r < LV_STAGE) {
           mkl[r].seq = a_seq_of(src, E.j);
           mkl[r].end = T0 + en;
         }
@@ -1423,17 +1424,22 @@ __global__ __launch_bounds__(256) void k_agg_levels(BookDev bk, AggSrc src, AggD
     const uint32_t need = ks > tailfree ? (ks - tailfree + ME_C - 1) / ME_C : 0u;
     const uint32_t own = min(need, nfreed), deficit = need - own;
     const uint32_t nmkt = nmk + nrc;
-    uint32_t mk_base = 0, fr_base = 0, d_off = 0;
-    if (lane == 0) {
-      mk_base = sl->mk_base + atomicAdd(&sl->mk_cur, nmkt);
-      fr_base = sl->fr_base + atomicAdd(&sl->fr_cur, nfreed);
-      if (deficit) d_off = atomicAdd(&sl->deficit, deficit);
-      const int dr = (int)ks - (int)nfull;
-      if (dr) atomicAdd(&sl->dresting, dr);
+    if constexpr (COUNT) {  // the counts for k_agg_lvscan (nothing else is written by this pass)
+      if (lane == 0) {
+        AggSegS o{};
+        o.nmk = nmkt;
+        o.nfreed = nfreed;
+        o.d_off = deficit;
+        o.ks = (uint32_t)((int)ks - (int)nfull);
+        ag.segs[si] = o;
+      }
+      continue;
     }
-    mk_base = rl32(mk_base, 0);
-    fr_base = rl32(fr_base, 0);
-    d_off = rl32(d_off, 0);
+    // the level's regions of the slot's makers / freed chunks and its share of the deficit: k_agg_lvscan's
+    // exclusive scans of the counting pass, which ran this same code (a mismatch is an internal error)
+    const uint32_t mk_base = auniu(ag.segs[si].mk_base), fr_base = auniu(ag.segs[si].fr_base);
+    const uint32_t d_off = auniu(ag.segs[si].d_off);
+    if (auniu(ag.segs[si].nmk) != nmkt || auniu(ag.segs[si].nfreed) != nfreed) a_set_err(bk, ERR_INCONSISTENT);
     if (mk_base + nmkt > ag.mk_cap || fr_base + nfreed > ag.fr_cap) {
       a_set_err(bk, ERR_SCRATCH_OOM);  // sized so this cannot happen; leaves the level alone
       for (uint32_t b = lane; b < cnt; b += 64) ag.evn[ag.evq[start + b].pad] = 0u;
@@ -1547,6 +1553,72 @@ __global__ __launch_bounds__(256) void k_agg_levels(BookDev bk, AggSrc src, AggD
       ag.segs[si] = o;
     }
     wave_mem_order();  // the next segment reuses the staging
+  }
+}
+
+// The segments' allocations, by scan instead of returning atomics: one workgroup per hot symbol turns the
+// counting pass's per-level counts (makers consumed, chunks emptied, chunk deficit, resting change) into
+// each level's offsets in the slot's regions of AggDev::mk / ::fr and of its deficit, and sets the slot's
+// cursors and totals. (A returning atomic per segment on the slot's cursors serialised config 4's ~7,000
+// segments of the hot symbol on one L2 line: k_agg_levels 640-740 us per batch, profiles/r5/occ.)
+__global__ __launch_bounds__(1024) void k_agg_lvscan(BookDev bk, AggDev ag) {
+  __shared__ long long wsum[3][16];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint32_t nh = a_nslots(bk, ag);
+  for (uint32_t i = blockIdx.x; i < nh; i += gridDim.x) {
+    AggSlot* sl = ag.slot + i;
+    if (!auniu(sl->active)) continue;
+    const uint32_t sb = auniu(sl->seg_base), ns = auniu(sl->nseg);
+    const uint32_t mb = auniu(sl->mk_base), fb = auniu(sl->fr_base);
+    long long c0 = 0, c1 = 0, c2 = 0, cd = 0;  // running totals (every thread keeps them)
+    for (uint32_t b = 0; b < ns; b += 1024u) {
+      const uint32_t si = sb + b + (uint32_t)tid;
+      const bool v = b + (uint32_t)tid < ns;
+      long long x0 = 0, x1 = 0, x2 = 0, xd = 0;
+      if (v) {
+        const AggSegS g = ag.segs[si];
+        x0 = g.nmk;
+        x1 = g.nfreed;
+        x2 = g.d_off;
+        xd = (int)g.ks;
+      }
+      const long long i0 = wave_incl_scan(x0), i1 = wave_incl_scan(x1), i2 = wave_incl_scan(x2);
+      const long long id = wave_incl_scan(xd);
+      if (lane == 63) {
+        wsum[0][wv] = i0;
+        wsum[1][wv] = i1;
+        wsum[2][wv] = i2;
+      }
+      __syncthreads();
+      long long p0 = 0, p1 = 0, p2 = 0, t0 = 0, t1 = 0, t2 = 0;
+      for (int k = 0; k < 16; ++k) {
+        if (k < wv) {
+          p0 += wsum[0][k];
+          p1 += wsum[1][k];
+          p2 += wsum[2][k];
+        }
+        t0 += wsum[0][k];
+        t1 += wsum[1][k];
+        t2 += wsum[2][k];
+      }
+      __syncthreads();  // (wsum is rewritten by the next chunk)
+      if (v) {
+        ag.segs[si].mk_base = mb + (uint32_t)(c0 + p0 + i0 - x0);
+        ag.segs[si].fr_base = fb + (uint32_t)(c1 + p1 + i1 - x1);
+        ag.segs[si].d_off = (uint32_t)(c2 + p2 + i2 - x2);
+      }
+      c0 += t0;
+      c1 += t1;
+      c2 += t2;
+      if (lane == 63) cd += id;  // (per wave; summed below by atomics on the slot)
+    }
+    if (lane == 63 && cd) atomicAdd(&sl->dresting, (int)cd);
+    if (tid == 0) {
+      sl->mk_cur = (uint32_t)c0;
+      sl->fr_cur = (uint32_t)c1;
+      sl->deficit = (uint32_t)c2;
+    }
+    __syncthreads();
   }
 }
 
@@ -3070,7 +3142,9 @@ hipError_t launch_agg(hipStream_t hs, const BookDev& bk, const BatchDev& bt, con
   hipLaunchKernelGGL(k_agg_walk, dim3(64), dim3(64), lwb, hs, bk, bt, ag);
   hipLaunchKernelGGL(k_agg_group, dim3(64), dim3(1024), agg_group_lds(bk.L), hs, bk, ag);
   hipLaunchKernelGGL(k_agg_sorted, dim3(1024), dim3(256), 0, hs, bk, ag);
-  hipLaunchKernelGGL(k_agg_levels, dim3(1024), dim3(256), 0, hs, bk, src, ag);
+  hipLaunchKernelGGL(k_agg_levels<true>, dim3(1024), dim3(256), 0, hs, bk, src, ag);
+  hipLaunchKernelGGL(k_agg_lvscan, dim3(64), dim3(1024), 0, hs, bk, ag);
+  hipLaunchKernelGGL(k_agg_levels<false>, dim3(1024), dim3(256), 0, hs, bk, src, ag);
   hipLaunchKernelGGL(k_agg_alloc, dim3(64), dim3(64), 0, hs, bk, ag);
   hipLaunchKernelGGL(k_agg_place, dim3(1024), dim3(256), 0, hs, bk, src, ag);
   hipLaunchKernelGGL(k_agg_fin, dim3(64), dim3(1024), 0, hs, bk, bt, ag);
