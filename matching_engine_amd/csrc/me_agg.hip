@@ -1095,12 +1095,16 @@ __global__ __launch_bounds__(64) void k_agg_walk(BookDev bk, BatchDev bt, AggDev
 // own contiguous log range (per-wave histograms [16][L] in LDS give each wave its cursors); deeper ones:
 // one wave scatters, from log keys staged in LDS chunk by chunk.
 constexpr uint32_t AGG_GW_LMAX = 512;
+// Deep windows keep one histogram word per level with a pad word after every 32 (level l at l + l / 32): each
+// thread owns 32 consecutive levels in the prefix pass, and unpadded, a wave's 64 reads of step k all fell
+// in one bank (64-way conflicts, ~60 us of config 4's 188-us launch)
+__host__ __device__ constexpr uint32_t agg_gpad(uint32_t l) { return l + (l >> 5); }
 __host__ __device__ constexpr size_t agg_group_lds(uint32_t L) {
-  return L <= AGG_GW_LMAX ? (size_t)16 * L * 4u : (size_t)L * 4u + AGG_GCHUNK * 2u;
+  return L <= AGG_GW_LMAX ? (size_t)16 * L * 4u : (size_t)agg_gpad(L) * 4u + AGG_GCHUNK * 2u;
 }
 __global__ __launch_bounds__(1024) void k_agg_group(BookDev bk, AggDev ag) {
   extern __shared__ uint32_t cnt_l[];  // [L], then AGG_GCHUNK 16-bit keys; per-wave: [16][L]
-  uint16_t* keys = reinterpret_cast<uint16_t*>(cnt_l + bk.L);
+  uint16_t* keys = reinterpret_cast<uint16_t*>(cnt_l + agg_gpad(bk.L));
   __shared__ uint32_t wsum[16], wnz[16], sbase;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint32_t L = bk.L;
@@ -1121,9 +1125,9 @@ __global__ __launch_bounds__(1024) void k_agg_group(BookDev bk, AggDev ag) {
       __syncthreads();
       for (uint32_t e = r0 + (uint32_t)lane; e < r1; e += 64) atomicAdd(&cnt_l[(uint32_t)wv * L + ag.ev[eb + e].lvl], 1u);
     } else {
-      for (uint32_t b = tid; b < L; b += 1024) cnt_l[b] = 0;
+      for (uint32_t b = tid; b < agg_gpad(L); b += 1024) cnt_l[b] = 0;
       __syncthreads();
-      for (uint32_t e = tid; e < n; e += 1024) atomicAdd(&cnt_l[ag.ev[eb + e].lvl], 1u);
+      for (uint32_t e = tid; e < n; e += 1024) atomicAdd(&cnt_l[agg_gpad(ag.ev[eb + e].lvl)], 1u);
     }
     __syncthreads();
     const uint32_t b0 = tid * per;
@@ -1134,7 +1138,7 @@ __global__ __launch_bounds__(1024) void k_agg_group(BookDev bk, AggDev ag) {
         if (pw) {
           for (uint32_t w = 0; w < 16; ++w) c += cnt_l[w * L + b0 + k];
         } else {
-          c = cnt_l[b0 + k];
+          c = cnt_l[agg_gpad(b0 + k)];
         }
         lsum += c;
         lnz += c != 0u;
@@ -1181,8 +1185,8 @@ __global__ __launch_bounds__(1024) void k_agg_group(BookDev bk, AggDev ag) {
           }
           c = r - run;
         } else {
-          c = cnt_l[l];
-          cnt_l[l] = run;
+          c = cnt_l[agg_gpad(l)];
+          cnt_l[agg_gpad(l)] = run;
         }
         if (c) {
           AggSeg g;
@@ -1235,10 +1239,10 @@ __global__ __launch_bounds__(1024) void k_agg_group(BookDev bk, AggDev ag) {
             }
             const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
             const uint32_t cp = (uint32_t)__popcll(peers);
-            const uint32_t start = cnt_l[key];
+            const uint32_t start = cnt_l[agg_gpad(key)];
             if (v) ag.evs[eb + start + rank] = eb + c1 + e;
             __builtin_amdgcn_wave_barrier();
-            if (v && rank == 0) cnt_l[key] = start + cp;
+            if (v && rank == 0) cnt_l[agg_gpad(key)] = start + cp;
             __builtin_amdgcn_wave_barrier();
           }
         }
@@ -2897,7 +2901,9 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
         me_order_result* res = ga.res[g];
         res[oi].fill_count = nfill;
         res[oi].tape_offset = sh.gbase[g] + (x0 - sh.gex[g]);
+#ifndef ME_AB_NO_TILESUM  // (measurement-only switch: the tape's tile sums left out, tapes wrong)
         if (nfill) atomicAdd(&ga.tile_sum[g][oi / TILE_TAPE], nfill);
+#endif
       }
     }
   }
