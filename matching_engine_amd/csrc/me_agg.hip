@@ -1102,6 +1102,78 @@ __host__ __device__ constexpr uint32_t agg_gpad(uint32_t l) { return l + (l >> 5
 __host__ __device__ constexpr size_t agg_group_lds(uint32_t L) {
   return L <= AGG_GW_LMAX ? (size_t)16 * L * 4u : (size_t)agg_gpad(L) * 4u + AGG_GCHUNK * 2u;
 }
+// The deep path's scatter for logs of up to 16 x 64 x AGG_RX_R events: a stable LSD radix sort of the log by
+// level (8-bit digits, two passes), every wave over its own contiguous range held in registers as
+// (level << 17 | log index), per-wave digit cursors in LDS (cur [16][256]), the first pass's order through
+// the log's evx region (free until k_agg_fin) — instead of one wave ranking the whole log 64 events at a time.
+constexpr uint32_t AGG_RX_R = 32;
+__device__ __forceinline__ void agg_group_radix(const AggDev& ag, uint32_t eb, uint32_t n, uint32_t nbits,
+                                                uint32_t* cur, uint32_t* wtot) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  uint32_t* const tmp = ag.evx + eb;
+  const uint32_t per = ((n + 15u) / 16u + 63u) & ~63u;  // <= 64 * AGG_RX_R
+  const uint32_t r0 = min(n, (uint32_t)wv * per), r1 = min(n, r0 + per);
+  constexpr uint32_t NONE = 0xFFFFFFFFu;  // (no element: level < 2^15, index < 2^17 - 1)
+  uint32_t x[AGG_RX_R];
+  for (uint32_t pass = 0; pass < 2; ++pass) {
+    const uint32_t sh = 17u + (pass ? 8u : 0u), db = pass ? nbits - 8u : 8u;
+#pragma unroll
+    for (int k = 0; k < (int)AGG_RX_R; ++k) {
+      const uint32_t i = r0 + (uint32_t)k * 64u + (uint32_t)lane;
+      x[k] = NONE;
+      if (i < r1) x[k] = pass ? tmp[i] : ((ag.ev[eb + i].lvl << 17) | i);
+    }
+    for (uint32_t b = tid; b < 16u * 256u; b += 1024) cur[b] = 0u;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < (int)AGG_RX_R; ++k)
+      if (x[k] != NONE) atomicAdd(&cur[wv * 256 + ((x[k] >> sh) & 255u)], 1u);
+    __syncthreads();
+    // digit-major offsets: digit d of wave w after every smaller digit and after digit d of the earlier waves
+    uint32_t c = 0;
+    if (tid < 256)
+      for (int w = 0; w < 16; ++w) c += cur[w * 256 + tid];
+    const uint32_t inc = (uint32_t)wave_incl_scan((long long)c);
+    if (lane == 63 && wv < 4) wtot[wv] = inc;
+    __syncthreads();
+    if (tid < 256) {
+      uint32_t base = inc - c;
+      for (int w = 0; w < wv; ++w) base += wtot[w];
+      for (int w = 0; w < 16; ++w) {
+        const uint32_t y = cur[w * 256 + tid];
+        cur[w * 256 + tid] = base;
+        base += y;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < (int)AGG_RX_R; ++k) {
+      if (r0 + (uint32_t)k * 64u >= r1) break;  // (uniform over the wave)
+      const bool v = x[k] != NONE;
+      const uint32_t key = v ? (x[k] >> sh) & 255u : 0u;
+      unsigned long long peers = __ballot(v);
+      for (uint32_t bit = 0; bit < db; ++bit) {
+        const unsigned long long bb = __ballot((key >> bit) & 1u);
+        peers &= ((key >> bit) & 1u) ? bb : ~bb;
+      }
+      const uint32_t rank = (uint32_t)__popcll(peers & lanemask_lt());
+      const uint32_t cp = (uint32_t)__popcll(peers);
+      const uint32_t start = cur[wv * 256 + key];
+      if (v) {
+        if (pass)
+          ag.evs[eb + start + rank] = eb + (x[k] & 0x1FFFFu);
+        else
+          tmp[start + rank] = x[k];
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (v && rank == 0) cur[wv * 256 + key] = start + cp;
+      __builtin_amdgcn_wave_barrier();
+    }
+    __threadfence();  // the second pass reads the other waves' first-pass writes
+    __syncthreads();
+  }
+}
+
 __global__ __launch_bounds__(1024) void k_agg_group(BookDev bk, AggDev ag) {
   extern __shared__ uint32_t cnt_l[];  // [L], then AGG_GCHUNK 16-bit keys; per-wave: [16][L]
   uint16_t* keys = reinterpret_cast<uint16_t*>(cnt_l + agg_gpad(bk.L));
@@ -1220,6 +1292,8 @@ __global__ __launch_bounds__(1024) void k_agg_group(BookDev bk, AggDev ag) {
         __builtin_amdgcn_wave_barrier();
       }
       __syncthreads();
+    } else if (n <= 16u * 64u * AGG_RX_R && L <= 32768u) {
+      agg_group_radix(ag, eb, n, nbits, reinterpret_cast<uint32_t*>(keys), wsum);
     } else {
       // the scatter: chunks of AGG_GCHUNK keys staged in LDS by the whole workgroup (coalesced), then
       // ranked and placed by one wave (its steps read LDS only: no HBM round trip per 64 events)
