@@ -794,7 +794,10 @@ __device__ __forceinline__ bool lw_init(LWalk& w, const BookDev& bk, uint32_t s,
   w.cba = ba < w.L ? lw_get(w, ba) : 0u;
   return w.ub < LW_CAP;
 }
-// The ladder back to HBM (totals, occupancy); the cached totals first.
+// The ladder back to HBM (totals, occupancy); the cached totals first. The OCC form writes only the 64-level
+// blocks occupied at the start (the book's occupancy words, not yet overwritten) or at the end (its exact
+// bitmap): a block empty at both ends holds zeros in HBM already (config 4's seeded books leave ~40 % of a
+// 32,768-level window empty).
 __device__ __forceinline__ void lw_end(LWalk& w, const BookDev& bk, uint32_t s) {
   const int lane = lane_id();
   if (w.bb >= 0) lw_put(w, w.bb, w.cbb);
@@ -802,6 +805,31 @@ __device__ __forceinline__ void lw_end(LWalk& w, const BookDev& bk, uint32_t s) 
   wave_mem_order();
   Level* lv = bk.levels + (size_t)s * bk.L;
   unsigned long long* oc = bk.occ + (size_t)s * bk.Lwords;
+  if (w.occ && (w.L >> 6) <= 512 && (int)bk.Lwords == (w.L >> 6)) {
+    const int W = w.L >> 6;
+    const unsigned long long* eo = reinterpret_cast<const unsigned long long*>(w.occ);
+    unsigned long long so[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int b = r * 64 + lane;
+      so[r] = b < W ? oc[b] : 0ull;
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      if (r * 64 >= W) break;
+      const int b = r * 64 + lane;
+      const unsigned long long e = b < W ? eo[b] : 0ull;
+      unsigned long long need = __ballot(b < W && (so[r] | e) != 0ull);
+      if (b < W && so[r] != e) oc[b] = e;
+      while (need) {
+        const int bl = r * 64 + __builtin_ctzll(need);
+        need &= need - 1ull;
+        const int l = bl * 64 + lane;
+        lv[l].total = (long long)w.tot[l];
+      }
+    }
+    return;
+  }
   for (int b = 0; b < w.L; b += 64) {
     const int l = b + lane;
     const uint32_t t = l < w.L ? w.tot[l] : 0u;
