@@ -300,11 +300,29 @@ def cpu_baseline(args):
         sweep[str(T)] = {"value": v, "wall_s": round(wall, 4)}
     best = max(sweep, key=lambda t: sweep[t]["value"])
     seeded = f", after seeding {len(seeds)} resting orders" if seeds is not None else ""
-    return {"value": sweep[best]["value"], "unit": "orders/s", "cores": int(best), "kind": "port",
+    qcpu = cgroup_cpus()
+    # the CPUs the threads actually had: never more than the threads, the affinity mask or the job's quota
+    cores = min(int(best), allowed, qcpu if qcpu else allowed)
+    for t in sweep:
+        sweep[t]["cores"] = min(int(t), allowed, qcpu if qcpu else allowed)
+    quota = f"a cgroup CPU quota of {qcpu} CPUs" if qcpu else "no cgroup CPU quota"
+    return {"value": sweep[best]["value"], "unit": "orders/s", "cores": cores, "threads": int(best), "kind": "port",
             "single_core_value": sweep["1"]["value"] if "1" in sweep else None, "sweep": sweep,
             "sample": f"{k} batches ({done} orders) of the {args.workload} stream after {args.cpu_warmup} untimed "
                       f"warm-up batches{seeded}; oracle/oracle_book.cpp scalar price-time book, one book and one "
-                      f"std::thread per shard (orc_run_sharded), symbols hash-sharded; best of threads {ts}"}
+                      f"std::thread per shard (orc_run_sharded), symbols hash-sharded; best of threads {ts}, "
+                      f"run on {allowed} CPUs of the affinity mask under {quota} (cores = min(threads, quota, mask))"}
+
+
+def cgroup_cpus():
+    """CPUs the job's cgroup quota allows (cpu.max "quota period", rounded up), or None without a quota."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q == "max":
+            return None
+        return max(1, -(-int(q) // int(per)))
+    except (OSError, ValueError):
+        return None
 
 
 def c1_requests(n: int):
@@ -435,7 +453,7 @@ def host_info():
         ranges.append(f"{aff[i]}-{aff[j]}" if j > i else str(aff[i]))
         i = j + 1
     return {"nproc": os.cpu_count(), "cpu_model": model, "cpus_allowed": len(aff), "affinity": ",".join(ranges),
-            "cgroup_cpu_max": quota, "loadavg": os.getloadavg()}
+            "cgroup_cpu_max": quota, "cgroup_cpus": cgroup_cpus(), "loadavg": os.getloadavg()}
 
 
 def cluster_leg(args, world, rank, local, sc, base, slices, n_slices):

@@ -106,7 +106,9 @@ typedef struct me_config {
                                   a device batch) <= max_resting, else me_submit_* return
                                   ME_E_CAPACITY for that batch, NOT sticky: nothing of it was enqueued
                                   and the engine stays usable (me_admission_read) */
-  uint64_t max_chunks;         /* FIFO chunk pool (ME_CHUNK_SLOTS slots each); 0 = max_resting + 2*S */
+  uint64_t max_chunks;         /* FIFO chunk pool (ME_CHUNK_SLOTS slots each, 256 B); 0 = max_resting + 32*S + 64,
+                                  enough for any book shape and any movement of liquidity between symbols:
+                                  free chunks go back to a shared pool (me_chunk_stats) */
   uint64_t seq_ring;           /* seq-ring entries for cancels (power of two, 0 = 2^28). Any u64 seq is
                                   accepted; one launch group (batches_per_launch batches) must span fewer
                                   than seq_ring seqs */
@@ -291,6 +293,11 @@ int me_stats_read(me_engine* e, uint64_t* handoffs);
  * arena's copying collections (k_seq_sweep), arena_used = entries taken from the active half. Any
  * pointer may be NULL. No reference counterpart (the reference keeps no book). */
 int me_far_stats(me_engine* e, uint64_t* moves, uint64_t* collections, uint64_t* arena_used);
+
+/* The FIFO chunk pool: reclaims = reclamations so far (k_seq_sweep returned every symbol's free chunks
+ * to the shared pool ahead of a launch group that could otherwise have run out), high_water = chunk ids
+ * ever handed out, pool = max_chunks. Any pointer may be NULL. No reference counterpart. */
+int me_chunk_stats(me_engine* e, uint64_t* reclaims, uint64_t* high_water, uint64_t* pool);
 
 /* The matching paths the engine runs now (no reference counterpart: the reference has one CPU path).
  * *flags bit 0 (ME_PATH_GROUPED_AGG): launch groups of windows <= 128 levels go through the aggregate

@@ -150,6 +150,7 @@ PROTOTYPES = {
     "me_last_error": (C.c_int, [_P, C.c_char_p, _SZ]),
     "me_stats_read": (C.c_int, [_P, C.POINTER(C.c_uint64)]),
     "me_far_stats": (C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "me_chunk_stats": (C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "me_paths_read": (C.c_int, [_P, C.POINTER(C.c_uint32)]),
     "me_admission_read": (C.c_int, [_P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "me_admission_check": (C.c_int, [_P, C.c_uint64, C.POINTER(C.c_int)]),

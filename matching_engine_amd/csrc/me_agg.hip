@@ -1792,13 +1792,15 @@ __global__ __launch_bounds__(64) void k_agg_alloc(BookDev bk, AggDev ag) {
         uint32_t got = 0;
         if (lane == 0) got = atomicAdd(bk.chunk_top, left);
         got = rl32(got, 0);
-        if ((unsigned long long)got + left > bk.nchunks) {
+        const CPool cp = cp_read(bk.cpool);
+        if ((unsigned long long)got + left > cp_vcap(cp, bk.nchunks)) {
           a_set_err(bk, ERR_CHUNK_OOM);
           for (uint32_t u = lane; u < left; u += 64) ag.fr[ab + t + u] = 0u;  // never indexed past the pool
         } else {
           for (uint32_t u = lane; u < left; u += 64) {
-            ag.fr[ab + t + u] = got + u;
-            bk.chunks[got + u].owner = s;  // fresh chunks belong to this symbol for good
+            const uint32_t id = cp_id(bk.recl, cp, got + u);
+            ag.fr[ab + t + u] = id;
+            bk.chunks[id].owner = s;  // the symbol's until a reclamation finds the chunk free
           }
         }
       }
@@ -3107,13 +3109,15 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
           uint32_t got = 0;
           if (lane == 0) got = atomicAdd(bk.chunk_top, left);
           got = rl32(got, 0);
-          if ((unsigned long long)got + left > bk.nchunks) {
+          const CPool cp = cp_read(bk.cpool);
+          if ((unsigned long long)got + left > cp_vcap(cp, bk.nchunks)) {
             a_set_err(bk, ERR_CHUNK_OOM);
             for (uint32_t u = lane; u < left; u += 64) ag.fr[ab + t + u] = 0u;  // never indexed past the pool
           } else {
             for (uint32_t u = lane; u < left; u += 64) {
-              ag.fr[ab + t + u] = got + u;
-              bk.chunks[got + u].owner = s;  // fresh chunks belong to this symbol for good
+              const uint32_t id = cp_id(bk.recl, cp, got + u);
+              ag.fr[ab + t + u] = id;
+              bk.chunks[id].owner = s;  // the symbol's until a reclamation finds the chunk free
             }
           }
         }

@@ -235,7 +235,8 @@ struct me_engine {
   uint32_t ntiles_sort = 0;            // sort tiles of a max_batch batch (histogram row stride)
   // host-batch pipeline
   std::vector<HostSlot> hs;
-  std::vector<int> free_slots;  // LIFO: a synchronous caller keeps reusing two warm slots
+  std::vector<int> free_slots;  // LIFO: a synchronous caller keeps reusing the same few warm slots (two in
+                                // flight plus the one me_collect holds back)
   int held_slot = -1;           // the last collected slot: its outputs stay readable until the next
                                 // me_collect (or a submit that finds every other slot busy)
   std::unordered_map<uint64_t, int> by_ticket;  // uncollected tickets -> slot
@@ -321,7 +322,7 @@ static void free_all(me_engine* e) {
                   e->bk.loc,      e->bk.chunk_top, e->bk.err,       (void*)e->bk.gsym,
                   e->d_tape,      e->d_tape_count, e->d_fills_acc, e->bk.dbg,      e->bk.fcache,
                   e->bk.far,      e->bk.old,       e->bk.sq,       e->bk.hcount,     e->bk.hand,
-                  e->bk.stats,    e->bk.fdir,      e->bk.far_ctl};
+                  e->bk.stats,    e->bk.fdir,      e->bk.far_ctl,  e->bk.cpool,      e->bk.recl};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   {
@@ -471,8 +472,12 @@ extern "C" me_engine* me_create(const me_config* cfg) {
   e->dbits[1] = d1;
   const uint64_t L = cfg->levels;
   uint64_t nchunks = cfg->max_chunks;
-  // chunks in use <= resting orders (every linked chunk holds a live order), whatever the book shape
-  if (nchunks == 0) nchunks = cfg->max_resting + 2 * S;
+  // chunks in use <= resting orders (every linked chunk holds a live order), whatever the book shape and
+  // whichever symbols hold them: k_seq_sweep's reclamation returns every symbol's free chunks to the pool
+  // before a launch group that could otherwise run out (me_kernels.hip chunk_reclaim). On top of
+  // max_resting, one group draws for its LIMIT records (admission control) plus, per wave, the unused
+  // rest of one reservation block (< 16 chunks) — at most two waves per symbol and group.
+  if (nchunks == 0) nchunks = cfg->max_resting + 32 * S + 64;
   const uint64_t n = cfg->max_batch;
   const unsigned long long scap = cfg->max_resting + 2 * n;
   auto bail = [&](const std::string& m) -> me_engine* {
@@ -640,6 +645,8 @@ extern "C" me_engine* me_create(const me_config* cfg) {
   e->pub_host[0] = e->pub_host[1] = 0ull;  // {0 launches, 0 resting / hand-offs}
   e->pub_host[2] = e->pub_host[3] = 0ull;  // [2]: me_sync's copy of the error word
   ALLOC(bk.chunk_top, 1);
+  ALLOC(bk.cpool, CP_N);
+  ALLOC(bk.recl, nchunks);
   ALLOC(bk.err, 1);
   uint32_t* gsym = nullptr;
   ALLOC(gsym, S);
@@ -725,6 +732,7 @@ extern "C" me_engine* me_create(const me_config* cfg) {
             hipMemcpyAsync(bk.sq, sq0, sizeof sq0, hipMemcpyHostToDevice, st) == hipSuccess &&
             hipMemsetAsync(bk.fcache, 0xFF, S * 64 * sizeof(uint32_t), st) == hipSuccess &&
             hipMemsetAsync(bk.chunk_top, 0, 4, st) == hipSuccess && hipMemsetAsync(bk.err, 0, 4, st) == hipSuccess &&
+            hipMemsetAsync(bk.cpool, 0, CP_N * sizeof(uint32_t), st) == hipSuccess &&
             hipMemcpyAsync(bk.sym, ss.data(), S * sizeof(SymState), hipMemcpyHostToDevice, st) == hipSuccess &&
             hipMemcpyAsync(gsym, gs.data(), S * 4, hipMemcpyHostToDevice, st) == hipSuccess &&
             hipMemsetAsync(e->d_tape_count, 0, 8 * ME_GMAX, st) == hipSuccess &&
@@ -1810,6 +1818,22 @@ extern "C" int me_far_stats(me_engine* e, uint64_t* moves, uint64_t* collections
   if (moves) *moves = v[ST_FAR_GROW];
   if (collections) *collections = v[ST_FAR_GC];
   if (arena_used) *arena_used = ctl[ctl[FC_HALF] & 1];
+  return ME_OK;
+}
+
+extern "C" int me_chunk_stats(me_engine* e, uint64_t* reclaims, uint64_t* high_water, uint64_t* pool) {
+  if (!e) return ME_E_INVALID;
+  int rc = me_sync(e);
+  if (rc) return rc;
+  unsigned long long v[ME_STATS];
+  uint32_t cp[CP_N], top = 0;
+  HIP_TRY(hipMemcpy(v, e->bk.stats, sizeof v, hipMemcpyDeviceToHost), "D2H stats");
+  HIP_TRY(hipMemcpy(cp, e->bk.cpool, sizeof cp, hipMemcpyDeviceToHost), "D2H chunk pool");
+  HIP_TRY(hipMemcpy(&top, e->bk.chunk_top, 4, hipMemcpyDeviceToHost), "D2H chunk top");
+  const uint64_t hw = top > cp[CP_NRECL] ? (uint64_t)cp[CP_FRESH] + (top - cp[CP_NRECL]) : cp[CP_FRESH];
+  if (reclaims) *reclaims = v[ST_CHUNK_GC];
+  if (high_water) *high_water = std::min<uint64_t>(hw, e->bk.nchunks);
+  if (pool) *pool = e->bk.nchunks;
   return ME_OK;
 }
 

@@ -313,7 +313,8 @@ struct WaveCtx {
   int bb, ba;                // best bid / best ask level of the window
   uint32_t free_head;        // chunk free list of this symbol ...
   uint32_t free_next;        // ... and chdr[free_head].next, loaded ahead of the pop that needs it
-  uint32_t bump_cur, bump_end;  // chunk ids reserved from the global bump allocator
+  uint32_t bump_ids;         // VGPR: chunk ids reserved from the global pool (lane i: entry i) ...
+  uint32_t bump_cur, bump_end;  // ... entries [bump_cur, bump_end) are still unused
   uint32_t recs_left;        // records of this wave not processed yet (>= chunks it can still need)
   int resting_delta;
   unsigned long long wptr;   // next scratch slot of this wave
@@ -492,16 +493,21 @@ __device__ __forceinline__ uint32_t alloc_chunk(WaveCtx& c) {
     uint32_t got = 0;
     if (lane_id() == 0) got = atomicAdd(c.bk.chunk_top, BLK);
     got = rl32(got, 0);
-    if (got >= c.bk.nchunks) {
+    const CPool p = cp_read(c.bk.cpool);
+    const uint32_t vcap = cp_vcap(p, c.bk.nchunks);
+    if (got >= vcap) {
       set_err(c.bk, ERR_CHUNK_OOM);
       return NIL;
     }
-    c.bump_cur = got;
-    c.bump_end = min(got + BLK, c.bk.nchunks);
-    // fresh chunks belong to this symbol for good (unused ones join its free list)
-    if ((uint32_t)lane_id() < BLK && got + (uint32_t)lane_id() < c.bk.nchunks) c.bk.chunks[got + lane_id()].owner = c.s;
+    const uint32_t nb = min(BLK, vcap - got);
+    const uint32_t l = (uint32_t)lane_id();
+    c.bump_ids = l < nb ? cp_id(c.bk.recl, p, got + l) : NIL;
+    // the chunks belong to this symbol until a reclamation finds them free (unused ones join its free list)
+    if (l < nb) c.bk.chunks[c.bump_ids].owner = c.s;
+    c.bump_cur = 0;
+    c.bump_end = nb;
   }
-  return c.bump_cur++;
+  return rl32(c.bump_ids, (int)c.bump_cur++);
 }
 
 // Append one fill per lane where e holds, in lane order, to the wave's scratch run.
@@ -1145,7 +1151,7 @@ __device__ __forceinline__ void match_records(WaveCtx& c, const BatchDev& bt, ui
     STAMP_ADD(c, PH_RESULT);
   }
   // return unused bump-reserved chunks to this symbol's free list
-  while (c.bump_cur < c.bump_end) free_chunk(c, c.bump_cur++);
+  while (c.bump_cur < c.bump_end) free_chunk(c, rl32(c.bump_ids, (int)c.bump_cur++));
 }
 
 // cont_w != ~0: a continuation (k_match_hot_cont) that writes its fills from cont_w on, inside the
@@ -2217,7 +2223,7 @@ __device__ __forceinline__ void match_records_hot(HotState& h, WaveCtx& c, const
     h.nfs -= 1;
     hot_free_slow(&c, rl32(h.fstk, (int)h.nfs));
   }
-  while (c.bump_cur < c.bump_end) hot_free_slow(&c, c.bump_cur++);
+  while (c.bump_cur < c.bump_end) hot_free_slow(&c, rl32(c.bump_ids, (int)c.bump_cur++));
 }
 
 // The hot symbols of a launch (at least hot_min records in the batch) into bk.hand[] = {s, pos = lo,
@@ -2339,7 +2345,56 @@ struct SeqGroup {
   uint32_t ng;
   uint32_t in;  // state index read; the kernel writes state[in ^ 1]
   uint32_t launch;  // match launches enqueued before this group's (all finished when this runs)
+  uint32_t recs;    // records of the group (each draws at most one chunk from the pool)
 };
+
+// Chunk-pool reclamation (me_layout.hpp cp_id), by k_seq_sweep's workgroups ahead of a launch
+// group when the pool's high-water mark hw plus what the group can draw (<= one chunk per record and one
+// reservation block per wave that has none left) could pass the pool. Between launches a chunk is free iff
+// all its quantities are 0 (every linked chunk holds a live order; a freed chunk is zeroed in HBM before it
+// is listed anywhere), so one pass over [0, hw) finds every free chunk, wherever it is parked — symbols' free
+// lists, fcache rows, the last reclamation's unused tail. Every symbol's free list and fcache row are
+// dropped, the chunks found become the list allocation numbers map to first, and the last workgroup
+// (ticket) publishes it: {nrecl = found, fresh = hw}, allocation counter 0. Afterwards chunks held = chunks
+// in use <= resting orders, so max_resting + the group's reservation slack always suffices.
+__device__ void chunk_reclaim(const BookDev& bk, uint32_t hw) {
+  const int lane = lane_id();
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < bk.S; i += gridDim.x * blockDim.x) {
+    bk.sym[i].free_head = NIL;
+    bk.sym[i].nfree = 0;
+  }
+  const uint32_t nwv = blockDim.x >> 6;
+  const uint32_t wid = blockIdx.x * nwv + (threadIdx.x >> 6), nw = gridDim.x * nwv;
+  for (uint32_t c0 = wid * 64u; c0 < hw; c0 += nw * 64u) {
+    const uint32_t c = c0 + (uint32_t)lane;
+    bool fr = false;
+    if (c < hw) {
+      const int4* q = reinterpret_cast<const int4*>(bk.chunks[c].qty);
+      const int4 a = q[0], b = q[1], d = q[2], e = q[3];
+      fr = ((a.x | a.y | a.z | a.w) | (b.x | b.y | b.z | b.w) | (d.x | d.y | d.z | d.w) | (e.x | e.y | e.z | e.w)) == 0;
+    }
+    const unsigned long long m = __ballot(fr);
+    uint32_t off = 0;
+    if (lane == 0 && m) off = atomicAdd(bk.cpool + CP_FOUND, (uint32_t)__popcll(m));
+    off = rl32(off, 0);
+    if (fr) bk.recl[off + (uint32_t)__popcll(m & lanemask_lt())] = c;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const uint32_t t = atomicAdd(bk.cpool + CP_TICKET, 1u);
+    if (t == gridDim.x - 1u) {  // every workgroup has listed its chunks
+      const uint32_t found = __hip_atomic_load(bk.cpool + CP_FOUND, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      bk.cpool[CP_NRECL] = found;
+      bk.cpool[CP_FRESH] = hw;
+      bk.cpool[CP_FOUND] = 0;
+      bk.cpool[CP_TICKET] = 0;
+      *bk.chunk_top = 0;
+      bk.stats[ST_CHUNK_GC] += 1ull;
+      __threadfence();
+    }
+  }
+}
 
 // The far arena's copying collection (me_far.hpp), by k_seq_sweep's workgroups when the active half's top
 // has passed far_gc_at: no launch allocates while this kernel runs, so every workgroup reads the same
@@ -2399,6 +2454,10 @@ __device__ void far_collect(const BookDev& bk) {
 
 __global__ __launch_bounds__(256) void k_seq_sweep(BookDev bk, SeqGroup sg) {
   const SeqState st = bk.sq[sg.in];
+  // the pool's state as the previous launches left it (only the last workgroup of a reclamation changes it,
+  // after every workgroup has read it)
+  const CPool cp = cp_read(bk.cpool);
+  const uint32_t hw = cp_hw(cp, __builtin_amdgcn_readfirstlane(*bk.chunk_top), bk.nchunks);
   const unsigned long long gmin = sg.seq[0][0];
   const unsigned long long gmax = sg.seq[sg.ng - 1][sg.n[sg.ng - 1] - 1];
   const unsigned long long R = bk.ring_mask + 1ull;
@@ -2439,9 +2498,9 @@ __global__ __launch_bounds__(256) void k_seq_sweep(BookDev bk, SeqGroup sg) {
     }
   }
   far_collect(bk);
+  if ((unsigned long long)hw + sg.recs + 2ull * bk.S + 64ull > bk.nchunks) chunk_reclaim(bk, hw);
   if (!need) return;
-  const uint32_t top = min(*bk.chunk_top, bk.nchunks);
-  const size_t slots = (size_t)top * ME_C;
+  const size_t slots = (size_t)hw * ME_C;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < slots; i += (size_t)gridDim.x * blockDim.x) {
     if (cq_at(bk.chunks, i) <= 0) continue;
     const unsigned long long q = cs_at(bk.chunks, i);
@@ -2712,6 +2771,7 @@ hipError_t launch_seq_sweep(hipStream_t st, const BookDev& bk, const uint64_t* c
   sg.ng = ng;
   sg.in = in_idx;
   sg.launch = launch;
+  for (uint32_t g = 0; g < ng; ++g) sg.recs += n[g];
   hipLaunchKernelGGL(k_seq_sweep, dim3(grid ? grid : 1), dim3(256), 0, st, bk, sg);
   return hipGetLastError();
 }

@@ -92,8 +92,8 @@ struct alignas(16) ChunkHdr {
 // g = chunk * ME_C + slot.
 struct alignas(256) Chunk {
   ChunkHdr hdr;
-  uint32_t owner;  // symbol that took the chunk from the global pool (chunks never change symbol:
-                   // written once, when the bump allocator hands the chunk out)
+  uint32_t owner;  // symbol that took the chunk from the global pool (written whenever the pool hands
+                   // the chunk out: a reclaimed chunk may go to another symbol)
   uint32_t pad[11];
   int qty[ME_C];
   unsigned long long seq[ME_C];
@@ -288,7 +288,8 @@ struct HotLaunch {
 // ST_LAUNCH: the match launches enqueued before the current group (k_seq_sweep), for the continuation's
 // hand-off publication.
 // ST_FAR_GROW / ST_FAR_GC: far sides moved to a larger arena region / collection passes (me_far_stats).
-enum : uint32_t { ST_HANDOFFS = 0, ST_RESTING = 1, ST_LAUNCH = 2, ST_FAR_GROW = 3, ST_FAR_GC = 4, ME_STATS = 8 };
+// ST_CHUNK_GC: chunk-pool reclamations (k_seq_sweep, me_chunk_stats).
+enum : uint32_t { ST_HANDOFFS = 0, ST_RESTING = 1, ST_LAUNCH = 2, ST_FAR_GROW = 3, ST_FAR_GC = 4, ST_CHUNK_GC = 5, ME_STATS = 8 };
 
 struct BookDev {
   Level* levels;
@@ -326,7 +327,42 @@ struct BookDev {
                           // by k_match_hot (me_kernels.hip) or the aggregate path (me_agg.hip) instead
                           // of k_match; 0 = never
   uint32_t* agg_ctr;      // AggDev::ctr (zeroed by k_seq_sweep with hcount), or null
+  // Chunk pool (cp_id below): *chunk_top counts the allocations since the last reclamation; the v-th of
+  // them is recl[v] while v < nrecl (a chunk the reclamation found free), then fresh + (v - nrecl).
+  uint32_t* recl;         // [nchunks] free chunk ids found by the last reclamation (k_seq_sweep)
+  uint32_t* cpool;        // [CP_N] {nrecl, fresh, found counter, ticket}
 };
+
+// ---- chunk pool ------------------------------------------------------------------------------------
+// Chunks are drawn by one atomic add on *chunk_top (a block of consecutive allocation numbers); the
+// number maps to a chunk id through the reclamation's list, then past it to never-used ids from `fresh`
+// on. A symbol keeps the chunks its levels free (its free list, fcache row) until k_seq_sweep's
+// reclamation — due when the high-water mark plus the group's bound could pass the pool — returns every
+// free chunk of every symbol to the list: so chunks in use never exceed resting orders
+// and the pool needs max_resting + the launch group's reservation slack, whichever symbols the
+// liquidity moves between.
+enum : uint32_t { CP_NRECL = 0, CP_FRESH = 1, CP_FOUND = 2, CP_TICKET = 3, CP_N = 4 };
+struct CPool {
+  uint32_t nrecl, fresh;
+};
+#ifdef __HIPCC__
+__device__ __forceinline__ CPool cp_read(const uint32_t* cpool) {
+  CPool p;
+  p.nrecl = __builtin_amdgcn_readfirstlane(cpool[CP_NRECL]);
+  p.fresh = __builtin_amdgcn_readfirstlane(cpool[CP_FRESH]);
+  return p;
+}
+// allocation numbers [0, vcap) name distinct chunks (recl ids are < fresh, so nrecl <= fresh <= nchunks)
+__device__ __forceinline__ uint32_t cp_vcap(const CPool& p, uint32_t nchunks) { return p.nrecl + (nchunks - p.fresh); }
+__device__ __forceinline__ uint32_t cp_id(const uint32_t* recl, const CPool& p, uint32_t v) {
+  return v < p.nrecl ? recl[v] : p.fresh + (v - p.nrecl);
+}
+// chunk ids below this have been handed out at some point (the scans of k_seq_sweep stop here)
+__device__ __forceinline__ uint32_t cp_hw(const CPool& p, uint32_t top, uint32_t nchunks) {
+  const uint32_t h = top > p.nrecl ? p.fresh + (top - p.nrecl) : p.fresh;
+  return h < nchunks ? h : nchunks;
+}
+#endif
 
 // Far levels of (symbol s, side k) (k = 0 bids below the window, 1 asks above it): device code, read
 // between launches (the snapshot kernel); the matching kernels go through me_far.hpp's far_dir.

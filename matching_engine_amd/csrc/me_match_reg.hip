@@ -280,8 +280,8 @@ __device__ __forceinline__ void reg_free(RegCtx& c, uint32_t ch) {
   }
 }
 
-// Stack ran dry: pop the HBM overflow list (one dependent load) or take a reserved / freshly
-// reserved id of the global bump allocator. Cursors live in the wave's LDS (rare path).
+// Stack ran dry: pop the HBM overflow list (one dependent load) or reserve a block of the global
+// pool, which becomes the (empty) stack. Rare path.
 __device__ __forceinline__ uint32_t reg_alloc_slow(RegCtx& c) {
   const uint32_t fh = ldsu(c.M->free_head);
   if (fh != NIL) {
@@ -292,24 +292,25 @@ __device__ __forceinline__ uint32_t reg_alloc_slow(RegCtx& c) {
     ldsw(c.M->free_head, rl32(c.chunks[fh].hdr.next, 0));
     return fh;
   }
-  uint32_t cur = ldsu(c.M->bump_cur);
-  if (cur >= ldsu(c.M->bump_end)) {
-    // each record needs at most one new chunk: never reserve more than the records left
-    const uint32_t blk = min(16u, max(c.recs_left, 1u));
-    uint32_t got = 0;
-    if (lane_id() == 0) got = atomicAdd(ldsg(c.G->bk.chunk_top), blk);
-    got = rl32(got, 0);
-    if (got >= c.nchunks) {
-      reg_err(c, ERR_CHUNK_OOM);
-      return NIL;
-    }
-    cur = got;
-    ldsw(c.M->bump_end, min(got + blk, c.nchunks));
-    // fresh chunks belong to this symbol for good (unused ones join its free stack)
-    if ((uint32_t)lane_id() < blk && got + (uint32_t)lane_id() < c.nchunks) c.chunks[got + lane_id()].owner = c.s;
+  // each record needs at most one new chunk: never reserve more than the records left
+  const uint32_t blk = min(16u, max(c.recs_left, 1u));
+  uint32_t got = 0;
+  if (lane_id() == 0) got = atomicAdd(ldsg(c.G->bk.chunk_top), blk);
+  got = rl32(got, 0);
+  const CPool p = cp_read(ldsg(c.G->bk.cpool));
+  const uint32_t vcap = cp_vcap(p, c.nchunks);
+  if (got >= vcap) {
+    reg_err(c, ERR_CHUNK_OOM);
+    return NIL;
   }
-  ldsw(c.M->bump_cur, cur + 1);
-  return cur;
+  const uint32_t nb = min(blk, vcap - got);
+  const uint32_t l = (uint32_t)lane_id();
+  const uint32_t id = l < nb ? cp_id(ldsg(c.G->bk.recl), p, got + l) : NIL;
+  // the chunks belong to this symbol until a reclamation finds them free (unused ones stay on its stack)
+  if (l < nb) c.chunks[id].owner = c.s;
+  c.fstk = l < nb ? id : c.fstk;  // (reg_alloc pops the stack first: it is empty here)
+  c.nfs = nb - 1u;
+  return rl32(id, (int)(nb - 1u));
 }
 
 __device__ __forceinline__ uint32_t reg_alloc(RegCtx& c) {

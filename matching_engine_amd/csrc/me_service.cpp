@@ -468,7 +468,9 @@ static me_service* create(me_engine* engine, const me_matcher* m, const char* co
       s->sym_cap = c.num_symbols;
       s->slice_max = c.max_batch;
     }
-    me_host_reserve(engine, 2);  // the flusher keeps two slices in flight in two warm pinned slots
+    // the flusher keeps two slices in flight, and me_collect holds the last collected slot back: three
+    // warm pinned slots, so no slot is pinned inside the serving path
+    me_host_reserve(engine, 3);
   } else if (m) {
     s->m = *m;
     s->sym_cap = m->num_symbols;

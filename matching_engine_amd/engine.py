@@ -197,8 +197,9 @@ class Engine:
         return t.value
 
     def collect(self, ticket: int, copy: bool = True):
-        """(results[n], fills[k]) of a ticket. copy=False returns views of the slot's pinned memory,
-        valid until the next collect (me_collect's contract)."""
+        """(results[n], fills[k]) of a ticket. copy=False returns views of the slot's pinned memory, valid
+        until the next collect, or until a submit_host / host_inputs call that finds every other slot busy
+        and takes the held slot back (me_collect's contract, include/me_engine.h)."""
         fp, rp = C.c_void_p(), C.c_void_p()
         nf, nr = C.c_size_t(0), C.c_size_t(0)
         _check(self.lib, self.h,
@@ -321,6 +322,12 @@ class Engine:
         m, g, u = C.c_uint64(0), C.c_uint64(0), C.c_uint64(0)
         _check(self.lib, self.h, self.lib.me_far_stats(self.h, C.byref(m), C.byref(g), C.byref(u)))
         return {"moves": m.value, "collections": g.value, "arena_used": u.value}
+
+    def chunk_stats(self) -> dict:
+        """The FIFO chunk pool (me_chunk_stats): reclamations, chunk ids ever handed out, pool size."""
+        r, h, p = C.c_uint64(0), C.c_uint64(0), C.c_uint64(0)
+        _check(self.lib, self.h, self.lib.me_chunk_stats(self.h, C.byref(r), C.byref(h), C.byref(p)))
+        return {"reclaims": r.value, "high_water": h.value, "pool": p.value}
 
     def paths(self) -> dict:
         """The matching paths running now (me_paths_read): grouped launches / hot symbols through the

@@ -130,7 +130,7 @@ def run_sharded(books, parts, nwarm=0):
         offs.append(o)
         for f in cols:  # (+ one pad element: an empty part still has a valid pointer)
             a = np.concatenate([getattr(b, f) for b in p])
-            cols[f].append(np.ascontiguousarray(np.concatenate([a, a[:0].copy().resize(1) or np.zeros(1, a.dtype)])))
+            cols[f].append(np.ascontiguousarray(np.concatenate([a, np.zeros(1, a.dtype)])))
 
     def ptrs(arrs):
         return (C.c_void_p * T)(*[a.ctypes.data for a in arrs])
