@@ -304,6 +304,7 @@ int me_chunk_stats(me_engine* e, uint64_t* reclaims, uint64_t* high_water, uint6
  * path (k_agg_gwalk); bit 1 (ME_PATH_HOT_AGG): hot symbols of deeper windows do. */
 #define ME_PATH_GROUPED_AGG 1u
 #define ME_PATH_HOT_AGG 2u
+#define ME_PATH_GROUPED_CANCELS 4u /* the grouped walk covers cancels (k_agg_gwalk_cx) */
 int me_paths_read(const me_engine* e, uint32_t* flags);
 
 /* Admission control state (any pointer may be NULL): resting = resting orders of every symbol after

@@ -33,6 +33,7 @@
 // record loop, exactly as k_match_hot does; the HBM book is complete before it runs.
 // Same semantics and HBM layout as k_match (me_kernels.hip); parity: tests/test_hot_path.py.
 #include "me_wave.hpp"
+#include "me_far.hpp"  // old_lookup (k_agg_gwalk_cx)
 
 #include <cstdlib>
 
@@ -2567,6 +2568,554 @@ __global__ __launch_bounds__(128) void k_agg_gwalk2(BookDev bk, AggGArgs ga, Agg
   }
 }
 
+// ------------------------------------------------------------------ the grouped walk with cancels
+// k_agg_gwalk_cx: k_agg_gwalk2 for groups that carry cancels (config 5's 60 %), so a cancel no longer hands
+// its symbol to k_match_reg's continuation. A cancel of order X at level l removes X's remaining quantity at
+// that moment. In the level's maker space (the initial FIFO's live orders, then the group's rests, each an
+// interval of its quantity at its FIXED position U: the live quantity ahead of it at the group start, or the
+// level's initial total plus the group's earlier rests there) the takes consume from the front, and a cancel
+// shortens its maker to the part already consumed. With F_l = T0_l + R_l - X_l - tot_l the quantity the takes
+// consumed so far (T0: the initial total, R: the group's rests, X: the quantities the group's cancels removed,
+// tot: the live total) and C_X the quantities cancelled ahead of X (makers with U < U_X), X has consumed
+// clamp(F_l - (U_X - C_X), 0, q_X) and the cancel removes the rest. X's start U_X - C_X lies between
+// max(F at its rest, U_X - X_l) and U_X, so the bounds decide most cancels (untouched since it rested, or
+// consumed whole); the rest take the exact C_X from the level's list of the group's cancels {U, removed} in
+// LDS (its first GW_CXL; a level with more hands the symbol off when it needs the exact start). The walk logs
+// a cancel as two 8-B events {removed} {U}; the resolve shortens that maker to its consumed part, so its
+// interval overlaps stay exact (k_agg_gres).
+// Targets: the helper wave finds every cancel's target while preparing its batch — an order of this group
+// through a tagged seq-ring entry (it writes TAG | record for the group's LIMITs first; the record's seq
+// confirms it), an older one through the ring / old-order table and a walk of its level's initial FIFO (its
+// live quantity ahead). A rest's {U, qty | level, F} is kept in a 256-record LDS ring (the batch being walked
+// and the one before) and in the symbol's HBM region, from which the helper fetches it for older records.
+// Only a far level's order, one behind more than 64 chunks, a level past GW_CXN cancels in one group or past
+// GW_CXP older-order cancels hands the symbol to the continuation.
+constexpr uint32_t GW_CXL = 20;      // cancels a level lists per group (p99 11 on config 5's 20-batch groups)
+constexpr uint32_t GW_CXN = 64;      // cancels a level takes per group (k_agg_gres stages them in lanes)
+constexpr uint32_t GW_CXP = 64;      // cancels of orders from before the group per symbol and group
+constexpr uint32_t GW_RING = 256;    // records of the rest ring (two batches of BK_CAP)
+constexpr uint32_t CT_PRE = 1u << 31;  // target descriptor: an order from before the group (level, qty, U)
+constexpr uint32_t CT_RING = 1u << 30; // ... a record of the batch being walked or the one before: the ring
+constexpr uint32_t CX_TAG = 1u << 31;  // seq-ring entry of one of this group's LIMITs: TAG | its record number
+constexpr uint32_t LW_CX = 1u << 30;   // control word: a cancel (lw_cw's reject reason stays below it)
+constexpr uint32_t LW_RJ_MASK = 0x1FFFu;
+// record-field flags of the two events of a cancel (log word bits 7 + x; k_agg_gres's sorted entries bits 16 + x)
+constexpr uint32_t AGG_CXF = 1u << 14, AGG_CXU = 1u << 13, AGG_CXP = 1u << 12;
+constexpr uint32_t RI_BIG = 0xFFFFFFFFu;  // rest info of a rest too large to pack (>= 2^25): its cancel hands off
+
+struct GwCx {
+  uint32_t ct0[2][BK_CAP], ct1[2][BK_CAP], ct2[2][BK_CAP], ct3[2][BK_CAP];  // per batch buffer: each cancel's
+                                            // target {CT_PRE | level << 24 | qty, U, -, 0} or {record | CT_RING,
+                                            // -, -, -} or {record, U, qty << 7 | level, F at its rest}
+  uint32_t t0[128], rl[128], n[128], xl[128];  // per level: initial total, the group's rests, its cancels, the
+                                               // quantity they removed
+  uint32_t u[128 * GW_CXL], rm[128 * GW_CXL];  // per level: its first GW_CXL cancels {maker position, removed}
+  uint32_t ru[GW_RING], rlq[GW_RING], rf[GW_RING];  // rest ring: U, qty << 7 | level (0: no rest), F at the rest
+  uint32_t dbit[ME_GMAX * BK_CAP / 32];     // per record: its rest was cancelled
+  uint32_t npre, preu[GW_CXP], prel[GW_CXP];  // cancelled orders from before the group {position, level}
+};
+
+__device__ __forceinline__ uint32_t a_ldg(const uint32_t* p) {  // (past the L1: another wave's recent store)
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t a_wsum(uint32_t v) { return (uint32_t)rli64(wave_incl_scan((long long)v), 63); }
+
+// An order from before the group (uniform seq T < gmin): live at the group start in this symbol's window?
+// Ring entry, else the old-order table (seq below the horizon); then its live quantity ahead in its level's
+// FIFO. d0 / d1: the descriptor; returns 0 live, 1 unknown (not live), 2 hand off.
+__device__ __forceinline__ uint32_t gw_pre_target(const BookDev& bk, uint32_t s, unsigned long long T, long long base,
+                                                  uint32_t& d0, uint32_t& d1) {
+  const int lane = lane_id();
+  const SeqState sqs = bk.sq[bk.sq_idx];
+  auto live = [&](uint32_t g) -> bool {
+    if (g == NIL || g / ME_C >= bk.nchunks) return false;
+    const Chunk* c = bk.chunks + g / ME_C;
+    return auniu(c->owner) == s && (unsigned long long)rl64(c->seq[g % ME_C], 0) == T && (int)auniu((uint32_t)c->qty[g % ME_C]) > 0;
+  };
+  uint32_t g = auniu(a_ldg(bk.loc + (T & bk.ring_mask)));
+  if (!live(g)) {
+    if (T >= sqs.horizon) return 1u;
+    g = old_lookup((gptr<const OldEnt>)bk.old, bk.old_mask, sqs.epoch, T);
+    if (!live(g)) return 1u;
+  }
+  const uint32_t cx = g / ME_C, sx = g % ME_C;
+  const long long px = rli64(bk.chunks[cx].hdr.price, 0);
+  const unsigned long long off = (unsigned long long)px - (unsigned long long)base;
+  if (off >= (unsigned long long)bk.L) return 2u;  // a far level: the continuation
+  const uint32_t q = auniu((uint32_t)bk.chunks[cx].qty[sx]);
+  if (q >= (1u << 24)) return 2u;
+  unsigned long long U = 0;
+  uint32_t ch = auniu(bk.levels[(size_t)s * bk.L + off].head);
+  for (uint32_t steps = 0; ch != cx; ++steps) {
+    if (ch >= bk.nchunks || steps >= 64u) return 2u;
+    const int qv = lane < ME_C ? bk.chunks[ch].qty[lane] : 0;
+    U += a_wsum((uint32_t)max(qv, 0));
+    ch = auniu(bk.chunks[ch].hdr.next);
+  }
+  const int qv = lane < (int)sx ? bk.chunks[cx].qty[lane] : 0;
+  U += a_wsum((uint32_t)max(qv, 0));
+  if (U >= (1ull << 31)) return 2u;
+  d0 = CT_PRE | ((uint32_t)off << 24) | q;
+  d1 = (uint32_t)U;
+  return 0u;
+}
+
+// The symbol's per-record rest info in HBM (beside rsq / rjs in its log region): U, qty << 7 | level, F.
+struct GwRest {
+  gptr<uint32_t> u, lq, f;
+};
+
+// gw_prepare with cancels: the same batch set-up, the group's LIMITs tagged in the seq ring (and their rest
+// info cleared), then every cancel's target classified (cw: unknown -> ME_RJ_UNKNOWN_ORDER; fastm: hand-offs
+// cleared; the descriptor). cut: the first record of the batch the walker walks now (older ones: HBM).
+__device__ __forceinline__ void gw_prepare_cx(GwBuf& B, GwCx& X, uint32_t bsel, AStage& stg, const AggGArgs& ga,
+                                              const BookDev& bk, uint32_t s, uint32_t g, uint32_t cnt, size_t bko,
+                                              long long base, int L, uint32_t nfar0, uint32_t nfar1,
+                                              gptr<uint32_t> rsq, gptr<uint32_t> rjs, const GwRest& rr,
+                                              unsigned long long gmin, uint32_t& rbase, uint32_t cut) {
+  const int lane = lane_id();
+  BkRec r0{}, r1{};
+  if ((uint32_t)lane < cnt) r0 = ga.b_rec[g][bko + lane];
+  if (64u + (uint32_t)lane < cnt) r1 = ga.b_rec[g][bko + 64 + lane];
+  stg.seq[lane] = r0.seq;
+  stg.seq[64 + lane] = r1.seq;
+  stg.px[lane] = r0.px;
+  stg.px[64 + lane] = r1.px;
+  stg.qty[lane] = r0.qty;
+  stg.qty[64 + lane] = r1.qty;
+  stg.ok[lane] = r0.ok;
+  stg.ok[64 + lane] = r1.ok;
+  uint32_t k0 = (uint32_t)lane < cnt ? ((r0.ok & BK_IDX_MASK) << 7) | (uint32_t)lane : ~0u;
+  uint32_t k1 = 64u + (uint32_t)lane < cnt ? ((r1.ok & BK_IDX_MASK) << 7) | (64u + (uint32_t)lane) : ~0u;
+  if (cnt > 64u)
+    a_sort128(k0, k1);
+  else
+    k0 = a_sort64(k0, false);
+  wave_mem_order();
+  const uint32_t rb0 = rbase;
+  long long tgt[2] = {0ll, 0ll};
+  bool isc[2] = {false, false};
+  for (uint32_t blk = 0; blk < cnt; blk += 64) {
+    const uint32_t key = blk ? k1 : k0;
+    const bool v = blk + (uint32_t)lane < cnt;
+    const uint32_t sl = key & (BK_CAP - 1), oi = v ? key >> 7 : 0u;
+    const unsigned long long oseq = stg.seq[sl];
+    const long long opx = stg.px[sl];
+    const int oq = v ? stg.qty[sl] : 0;
+    const uint32_t okd = v ? stg.ok[sl] >> BK_KIND_SHIFT : 0u;
+    const bool cancel = v && ((okd >> 3) & 1u);
+    uint32_t rj;
+    int olm;
+    const bool cov = a_classify(v, oseq, opx, oq, okd, base, L, nfar0, nfar1, rj, olm);
+    const unsigned long long fastm = __ballot(cov || cancel);
+    const long long qs = rli64(wave_incl_scan(cancel ? 0ll : (long long)(uint32_t)max(oq, 0)), 63);
+    B.cw[blk + lane] = cancel ? LW_CX : lw_cw(okd, olm, rj, L);
+    B.oq[blk + lane] = cancel ? 0 : oq;
+    B.oi[blk + lane] = oi;
+    if (lane == 0) {
+      B.fastm[blk >> 6] = fastm;
+      B.qsum[blk >> 6] = qs;
+    }
+    const uint32_t j = rbase + (uint32_t)lane;
+    if (v) {
+      rsq[j] = (uint32_t)(oseq - gmin);
+      rjs[j] = (g << AGG_GSHIFT) | oi;
+      rr.lq[j] = 0u;  // (the walker writes a rest's)
+      // a LIMIT of this group the walk may rest: its ring entry names its record until k_agg_gres places it
+      if (!cancel && !((okd >> 2) & 1u) && cov && rj == 0u) bk.loc[oseq & bk.ring_mask] = CX_TAG | j;
+    }
+    tgt[blk >> 6] = opx;
+    isc[blk >> 6] = cancel;
+    rbase += min(64u, cnt - blk);
+  }
+  if (!__ballot(isc[0] || isc[1])) return;
+  a_drain();  // the tags and record seqs above, before the lookups below read them
+  for (uint32_t blk = 0; blk < cnt; blk += 64) {
+    const bool c = isc[blk >> 6];
+    const unsigned long long T = (unsigned long long)tgt[blk >> 6];
+    const uint32_t jself = rb0 + blk + (uint32_t)lane;
+    uint32_t d0 = 0, d1 = 0, d2 = 0, d3 = 0, cls = 1;  // 0 live, 1 unknown, 2 hand off
+    if (c && T >= gmin && T - gmin < (1ull << 32)) {  // this group's order: its tagged ring entry, confirmed by its seq
+      const uint32_t e = a_ldg(bk.loc + (T & bk.ring_mask));
+      const uint32_t jj = e & ~CX_TAG;
+      if ((e & CX_TAG) && jj < jself && a_ldg((const uint32_t*)&rsq[jj]) == (uint32_t)(T - gmin)) {
+        cls = 0u;
+        if (jj >= cut) {  // walked in this batch or the one before: the walker reads the ring
+          d0 = jj | CT_RING;
+        } else {  // walked before: its rest info from HBM now
+          d0 = jj;
+          d1 = a_ldg((const uint32_t*)&rr.u[jj]);
+          d2 = a_ldg((const uint32_t*)&rr.lq[jj]);
+          d3 = a_ldg((const uint32_t*)&rr.f[jj]);
+        }
+      }
+    }
+    unsigned long long pm = __ballot(c && T < gmin);
+    while (pm) {  // orders from before the group: one at a time (~0.6 per symbol and group at config 5)
+      const int i = __builtin_ctzll(pm);
+      pm &= pm - 1ull;
+      uint32_t e0 = 0, e1 = 0;
+      const uint32_t r = gw_pre_target(bk, s, rl64(T, i), base, e0, e1);
+      if (lane == i) {
+        cls = r;
+        d0 = e0;
+        d1 = e1;
+      }
+    }
+    if (c) {
+      X.ct0[bsel][blk + lane] = d0;
+      X.ct1[bsel][blk + lane] = d1;
+      X.ct2[bsel][blk + lane] = d2;
+      X.ct3[bsel][blk + lane] = d3;
+      if (cls == 1u) B.cw[blk + lane] = LW_CX | ((uint32_t)ME_RJ_UNKNOWN_ORDER << LW_RJ_SHIFT);
+    }
+    const unsigned long long ho = __ballot(c && cls == 2u);
+    if (ho && lane == 0) B.fastm[blk >> 6] &= ~ho;
+  }
+}
+
+// The chain of a block with cancels (lw_block's loop; rests also record their maker position, cancels as
+// above). Returns the records walked: fewer than cnt at the first one the walk does not cover.
+__device__ __forceinline__ uint32_t lw_block_cx(LEvG& e, LWalk& w, GwCx& X, const GwRest& ri, int oq, uint32_t ocw,
+                                                uint32_t c0v, uint32_t c1v, uint32_t c2v, uint32_t c3v, uint32_t jb,
+                                                unsigned long long fastm, uint32_t cnt, int& rr) {
+  const int lane = lane_id();
+  const unsigned long long upto = (cnt >= 64u ? ~0ull : ((1ull << cnt) - 1ull)) & ~fastm;
+  const uint32_t k = upto ? (uint32_t)__builtin_ctzll(upto) : cnt;
+  const unsigned long long rjm = __ballot(((ocw >> LW_RJ_SHIFT) & LW_RJ_MASK) != 0u);
+  unsigned long long work = (k >= 64u ? ~0ull : ((1ull << k) - 1ull)) & ~rjm;
+  while (work) {
+    const int r = __builtin_ctzll(work);
+    asm volatile("s_bitset0_b64 %0, %1" : "+s"(work) : "s"(r));
+    const uint32_t cw = rl32(ocw, r);
+    const uint32_t jr = jb + (uint32_t)r;
+    if (cw & LW_CX) {
+      const uint32_t d0 = rl32(c0v, r), d1 = rl32(c1v, r);
+      uint32_t l, U, q, Fr, flg, uev, jt = 0;
+      bool dup;
+      if (d0 & CT_PRE) {
+        l = (d0 >> 24) & 127u;
+        q = d0 & 0xFFFFFFu;
+        U = d1;
+        Fr = 0u;  // (nothing was consumed at the group start)
+        flg = AGG_CXF | AGG_CXP;
+        const uint32_t np = auniu(X.npre);  // an older order cancelled before in this group: same {U, level}
+        const bool vp = (uint32_t)lane < np;
+        dup = __ballot(vp && X.preu[vp ? lane : 0] == U && X.prel[vp ? lane : 0] == l) != 0ull;
+      } else {
+        jt = d0 & 0xFFFFu;
+        uint32_t lq;
+        if (d0 & CT_RING) {
+          const uint32_t x = jt & (GW_RING - 1u);
+          lq = auniu(X.rlq[x]);
+          U = auniu(X.ru[x]);
+          Fr = auniu(X.rf[x]);
+        } else {
+          lq = rl32(c2v, r);
+          U = d1;
+          Fr = rl32(c3v, r);
+        }
+        if (lq == RI_BIG) return (uint32_t)r;  // (before anything changed: the continuation from here)
+        l = lq & 127u;
+        q = lq >> 7;
+        flg = AGG_CXF;
+        dup = lq == 0u || ((auniu(X.dbit[jt >> 5]) >> (jt & 31u)) & 1u);  // never rested, or cancelled already
+      }
+      uint32_t rem = 0;
+      if (!dup) {
+        const uint32_t n = auniu(X.n[l]), xl = auniu(X.xl[l]);
+        const uint32_t tot = (int)l == w.bb ? w.cbb : (int)l == w.ba ? w.cba : lw_get(w, (int)l);
+        const uint32_t F = auniu(X.t0[l]) + auniu(X.rl[l]) - xl - tot;  // consumed by the group's takes
+        const uint32_t lo = max(Fr, U > xl ? U - xl : 0u);  // X's start is at least this, and at most U
+        uint32_t cons;
+        if (F <= lo) {
+          cons = 0u;
+        } else if (F >= U + q) {
+          cons = q;
+        } else {
+          if (n > GW_CXL) return (uint32_t)r;  // the list no longer holds every cancel: the continuation
+          const bool vl = (uint32_t)lane < n;
+          const uint32_t cu = vl ? X.u[l * GW_CXL + lane] : 0u, cr = vl ? X.rm[l * GW_CXL + lane] : 0u;
+          const uint32_t st = U - a_wsum(vl && cu < U ? cr : 0u);
+          cons = F > st ? min(F - st, q) : 0u;
+        }
+        rem = q - cons;
+        if (rem) {
+          if (n + 1u >= GW_CXN || ((d0 & CT_PRE) && auniu(X.npre) >= GW_CXP)) return (uint32_t)r;
+          if (lane == 0) {
+            if (n < GW_CXL) {
+              X.u[l * GW_CXL + n] = U;
+              X.rm[l * GW_CXL + n] = rem;
+            }
+            X.n[l] = n + 1u;
+            X.xl[l] = xl + rem;
+            if (d0 & CT_PRE) {
+              const uint32_t np = X.npre;
+              X.preu[np] = U;
+              X.prel[np] = l;
+              X.npre = np + 1u;
+            } else {
+              X.dbit[jt >> 5] |= 1u << (jt & 31u);
+            }
+          }
+          if ((int)l == w.bb) {
+            w.cbb -= rem;
+            if (!w.cbb) {
+              lw_put(w, w.bb, 0u);
+              w.bb = lw_prev(w, w.bb - 1, w.cbb);
+            }
+          } else if ((int)l == w.ba) {
+            w.cba -= rem;
+            if (!w.cba) {
+              lw_put(w, w.ba, 0u);
+              w.ba = lw_next(w, w.ba + 1, w.cba);
+            }
+          } else {
+            lw_add(w, (int)l, 0u - rem);
+          }
+          uev = (d0 & CT_PRE) ? U : U - auniu(X.t0[l]);  // in the resolve: the FIFO's or the rests' position
+          le_emit(e, auniu(l), auniu((jr | flg) << AGG_GREC_SHIFT), auniu(rem));
+          le_emit(e, auniu(l), auniu((jr | flg | AGG_CXU) << AGG_GREC_SHIFT), auniu(uev));
+        }
+      }
+      if (lane == 0) X.rlq[jr & (GW_RING - 1u)] = 0u;  // (a cancel never rests)
+      asm volatile("s_mov_b32 m0, %1\n\tv_writelane_b32 %0, %2, m0" : "+v"(rr) : "s"(r), "s"(auniu(rem)) : "m0");
+      continue;
+    }
+    uint32_t rem = (uint32_t)rli32(oq, r);
+    const uint32_t jt = jr << AGG_GREC_SHIFT;
+    const int lim = (int)(cw & LW_LIM);
+    uint32_t rq;
+    if (cw & LW_BUY) {
+      lw_take_buy<LEvG>(e, w, lim, rem, jt | AGG_TAKE);
+      rq = (cw & LW_MKT) ? 0u : rem;
+      asm volatile("" : "+s"(rq));
+      if (rq) lw_rest_buy<LEvG>(e, w, lim, rq, jt);
+    } else {
+      lw_take_sell<LEvG>(e, w, lim, rem, jt | AGG_TAKE);
+      rq = (cw & LW_MKT) ? 0u : rem;
+      asm volatile("" : "+s"(rq));
+      if (rq) lw_rest_sell<LEvG>(e, w, lim, rq, jt);
+    }
+    // the record's rest info (none: 0) in the ring and, for a rest, in HBM: its maker position, and what the
+    // level's takes had consumed when it rested (a lower bound on its start ever after)
+    uint32_t lq = 0, U = 0, Fr = 0;
+    if (rq) {
+      uint32_t R0 = 0;
+      if (lane == 0) R0 = __hip_atomic_fetch_add(&X.rl[lim], rq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      U = auniu(X.t0[lim]) + rl32(R0, 0);
+      const uint32_t tot = lim == w.bb ? w.cbb : lim == w.ba ? w.cba : lw_get(w, lim);
+      Fr = U + rq - auniu(X.xl[lim]) - tot;
+      lq = rq < (1u << 25) ? (rq << 7) | (uint32_t)lim : RI_BIG;
+    }
+    if (lane == 0) {
+      const uint32_t x = jr & (GW_RING - 1u);
+      X.rlq[x] = lq;
+      if (rq) {
+        X.ru[x] = U;
+        X.rf[x] = Fr;
+        ri.u[jr] = U;
+        ri.lq[jr] = lq;
+        ri.f[jr] = Fr;
+      }
+    }
+    asm volatile("s_mov_b32 m0, %1\n\tv_writelane_b32 %0, %2, m0" : "+v"(rr) : "s"(r), "s"(auniu(rem)) : "m0");
+  }
+  return k;
+}
+
+// A cancel's result: CANCELED with the quantity removed, or REJECTED / UNKNOWN_ORDER (the oracle's order of
+// checks: a cancel is never rejected for its quantity, side or seq).
+__device__ __forceinline__ me_order_result a_result_cx(uint32_t rj, int rem) {
+  me_order_result o;
+  const bool ok = rj == 0u && rem > 0;
+  o.filled_qty = 0;
+  o.remaining_qty = ok ? rem : 0;
+  o.fill_count = 0;
+  o.tape_offset = 0;
+  o.status = (uint8_t)(ok ? ME_ST_CANCELED : ME_ST_REJECTED);
+  o.reason = (uint8_t)(ok ? ME_RJ_NONE : ME_RJ_UNKNOWN_ORDER);
+  o.pad[0] = o.pad[1] = 0;
+  return o;
+}
+
+__global__ __launch_bounds__(128) void k_agg_gwalk_cx(BookDev bk, AggGArgs ga, AggDev ag) {
+  __shared__ GwShared sh;
+  __shared__ GwCx cx;
+  const int lane = lane_id();
+  const bool walker = auni((int)(threadIdx.x >> 6)) == 0;
+#if ME_WALK_PRIO
+  if (walker) __builtin_amdgcn_s_setprio(3);
+#endif
+  const int L = (int)bk.L;  // <= 128
+  const uint32_t ng = ga.ng;
+  for (uint32_t s = blockIdx.x; s < bk.S; s += gridDim.x) {
+    const uint32_t gl = min((uint32_t)lane, ng - 1u);
+    const uint32_t nsv = (uint32_t)lane < ng ? ga.bcnt[gl][(size_t)s * BK_CNT_STRIDE] : 0u;
+    const uint32_t total = (uint32_t)rli64(wave_incl_scan((long long)nsv), 63);
+    const SymState st = bk.sym[s];
+    const long long base = rli64(st.base, 0);
+    const int bb0 = rli32(st.best_bid, 0), ba0 = rli32(st.best_ask, 0);
+    const uint32_t resting = rl32(st.resting, 0);
+    const uint32_t nfar0 = rl32(st.nfar[0], 0), nfar1 = rl32(st.nfar[1], 0);
+    gptr<AggSlot> slot = (gptr<AggSlot>)(ag.slot + s);
+    const uint32_t evneed = 3u * total + min((uint32_t)L, resting) + 64u;
+    if (walker) {
+      uint32_t eb = 0;
+      if (total && lane == 0) eb = atomicAdd(&ag.ctr[AC_EV], evneed + 64u);
+      eb = (rl32(eb, 0) + 63u) & ~63u;
+      const bool eok = (unsigned long long)eb + evneed <= ag.ev_cap;
+      if (lane == 0) {
+        AggSlot o{};
+        o.s = s;
+        o.base = base;
+        o.ev_base = eb;
+        o.lo = evneed;
+        o.hi = total;
+        o.free_head = st.free_head;
+        o.resting0 = resting;
+        o.bb = bb0;
+        o.ba = ba0;
+        o.active = 0;
+        o.hidx = NIL;
+        o.gs = bk.gsym ? bk.gsym[s] : s;
+        *slot = o;
+      }
+      bool go = total != 0u;
+      if (go && (!eok || !a_reserve(ag, slot, resting, total))) {
+        const uint32_t g0 = (uint32_t)__builtin_ctzll(__ballot(nsv != 0u));
+        a_ghand(bk, s, g0, 0u, rl32(nsv, (int)g0), s * ga.slab, s * ga.slab + ga.slab);
+        go = false;
+      }
+      if (lane == 0) {
+        sh.go = go ? 1u : 0u;
+        sh.eb = eb;
+      }
+    }
+    __syncthreads();
+    const bool go = auniu(sh.go) != 0u;
+    const uint32_t eb = auniu(sh.eb);
+    __syncthreads();
+    if (!go) continue;
+    AggGEv* const log8 = reinterpret_cast<AggGEv*>(ag.ev + eb);
+    // the region: evneed 8-B events, then the records' seqs, positions and rest info [total] each
+    // (8 evneed + 20 total <= 16 evneed bytes: evneed >= 3 total)
+    const gptr<uint32_t> rsq = vptr(reinterpret_cast<uint32_t*>(log8 + evneed));
+    const gptr<uint32_t> rjs = rsq + total;
+    GwRest ri;
+    ri.u = rjs + total;
+    ri.lq = ri.u + total;
+    ri.f = ri.lq + total;
+    const size_t bko = (size_t)s * BK_CAP;
+    if (walker) {
+      const uint32_t nfc = min(rl32(st.nfree, 0), 64u);
+      if (nfc) {
+        const uint32_t fc = bk.fcache[(size_t)s * 64u + lane];
+        const uint32_t nx = (uint32_t)__shfl((int)fc, min(lane + 1, 63), 64);
+        if ((uint32_t)lane < nfc) bk.chunks[fc].hdr.next = (uint32_t)lane + 1u < nfc ? nx : st.free_head;
+        if (lane == 0) slot->free_head = fc;
+      }
+    } else {
+      uint32_t hrb = 0;
+      const unsigned long long gmin = *ga.seq0;
+      const uint32_t c0 = rl32(nsv, 0);
+      if (c0 && c0 <= (uint32_t)BK_CAP)
+        gw_prepare_cx(sh.buf[0], cx, 0u, sh.stg, ga, bk, s, 0u, c0, bko, base, L, nfar0, nfar1, rsq, rjs, ri, gmin,
+                      hrb, 0u);
+      __syncthreads();
+      for (uint32_t g = 0; g < ng; ++g) {
+        const uint32_t c = g + 1u < ng ? rl32(nsv, (int)(g + 1u)) : 0u;
+        // batch g's first record: when batch g + 1 is walked the ring holds batches g and g + 1
+        const uint32_t cg = rl32(nsv, (int)g);
+        const uint32_t cut = hrb - (cg <= (uint32_t)BK_CAP ? cg : 0u);
+        if (c && c <= (uint32_t)BK_CAP)
+          gw_prepare_cx(sh.buf[(g + 1u) & 1u], cx, (g + 1u) & 1u, sh.stg, ga, bk, s, g + 1u, c, bko, base, L, nfar0,
+                        nfar1, rsq, rjs, ri, gmin, hrb, cut);
+        __syncthreads();
+        if (auniu(sh.stop[g & 1u])) break;
+      }
+      continue;
+    }
+    LEvG w;
+    le_init(w, log8, 0u);
+    uint32_t rbase = 0;
+    LWalk lw;
+    const bool lok = lw_init(lw, bk, s, sh.ltot, bb0, ba0);
+    for (int l = lane; l < L; l += 64) {  // the levels' initial totals, no rests or cancels yet
+      cx.t0[l] = sh.ltot[l];
+      cx.rl[l] = 0u;
+      cx.n[l] = 0u;
+      cx.xl[l] = 0u;
+    }
+    for (uint32_t j = (uint32_t)lane; j < ME_GMAX * BK_CAP / 32; j += 64) cx.dbit[j] = 0u;
+    if (lane == 0) cx.npre = 0u;
+    wave_mem_order();
+    uint32_t hidx = NIL, gstop = ng;
+    __syncthreads();  // batch 0 prepared
+    for (uint32_t g = 0; g < ng; ++g) {
+      if (lane == 0) *a_gtab(ag.gev, s, g) = eb + w.evp;
+      const uint32_t cnt = rl32(nsv, (int)g);
+      bool stop = false;
+      if (cnt > (uint32_t)BK_CAP) {
+        hidx = a_ghand(bk, s, g, 0u, cnt, 0u, 0u);
+        stop = true;
+      } else if (cnt) {
+        if (lane == 0) ga.bcnt[g][(size_t)s * BK_CNT_STRIDE] = 0u;
+        const GwBuf& B = sh.buf[g & 1u];
+        me_order_result* res = ga.res[g];
+        for (uint32_t blk = 0; blk < cnt; blk += 64) {
+          const bool v = blk + (uint32_t)lane < cnt;
+          const uint32_t ocw = B.cw[blk + lane];
+          const int oq = B.oq[blk + lane];
+          const uint32_t oi = B.oi[blk + lane];
+          const uint32_t b2 = g & 1u;
+          const uint32_t c0v = cx.ct0[b2][blk + lane], c1v = cx.ct1[b2][blk + lane];
+          const uint32_t c2v = cx.ct2[b2][blk + lane], c3v = cx.ct3[b2][blk + lane];
+          const unsigned long long fastm = rl64(B.fastm[blk >> 6], 0);
+          const uint32_t cntb = min(64u, cnt - blk);
+          int rr = 0;
+          bool adm = false;
+          if (lok) {
+            lw.ub += (unsigned long long)rli64(B.qsum[blk >> 6], 0);
+            adm = lw.ub < LW_CAP;
+          }
+          const uint32_t k = lw_block_cx(w, lw, cx, ri, oq, ocw, c0v, c1v, c2v, c3v, rbase, adm ? fastm : 0ull, cntb, rr);
+          rbase += cntb;
+          if (v && (uint32_t)lane < k) {
+            const uint32_t rj = (ocw >> LW_RJ_SHIFT) & LW_RJ_MASK;
+            res[oi] = (ocw & LW_CX) ? a_result_cx(rj, rr) : a_result(oq, (ocw & LW_MKT) ? 4u : 0u, rj, rr);
+          }
+          if (k < cntb) {
+            hidx = a_ghand(bk, s, g, blk + k, cnt, 0u, 0u);
+            stop = true;
+            break;
+          }
+        }
+      }
+      if (lane == 0) sh.stop[g & 1u] = stop ? 1u : 0u;
+      __syncthreads();
+      if (stop) {
+        gstop = g;
+        break;
+      }
+    }
+    for (uint32_t g = (gstop < ng ? gstop + 1u : ng) + (uint32_t)lane; g <= ng; g += 64)
+      *a_gtab(ag.gev, s, g) = eb + w.evp;
+    if (gstop < ng && lane == 0) *a_gtab(ag.gev, s, gstop + 1u) = eb + w.evp;
+    le_end(w);
+    if (lok) lw_end(lw, bk, s);
+    const int bb = lw.bb, ba = lw.ba;
+    if (lane == 0) {
+      slot->ev_cnt = w.evp;
+      slot->bb = bb;
+      slot->ba = ba;
+      slot->active = 1;
+      slot->hidx = hidx;
+      slot->pos = gstop;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ grouped launches: one workgroup per symbol
 // k_agg_gres does the work of the hot path's k_agg_group ... k_agg_out for a grouped launch in ONE launch,
 // one 512-thread workgroup per symbol (the walk's workgroup of the same symbol ran on the same XCD,
@@ -2605,6 +3154,11 @@ struct GrStage {  // a wave's maker / emptied-chunk staging (phases B and D)
   AggMk mk[GR_STAGE];
   uint32_t fr[GR_STAGE];
 };
+struct GrCxStage {  // (walks with cancels) a wave's staging of its level's cancels (the walk takes <= GW_CXN)
+  uint32_t cxu[64], cxr[64], cxp[64];
+};
+// the cancel events' flags in the sorted entries (k_agg_gwalk_cx's AGG_CX* record-field flags << 16)
+constexpr uint32_t GR_CXF = AGG_CXF << 16, GR_CXU = AGG_CXU << 16, GR_CXP = AGG_CXP << 16;
 template <int NW>
 struct GrShared {
   union {
@@ -2629,9 +3183,10 @@ __device__ __forceinline__ uint32_t gr_take(uint32_t* ctr) {
   return rl32(i, 0);
 }
 
-template <int NW, bool kLds>
+template <int NW, bool kLds, bool CX>
 __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& ga, const AggSrc& src, const AggDev& ag,
-                                            uint32_t s, const AggSlot& sl, GrShared<NW>& sh, uint32_t* nf) {
+                                            uint32_t s, const AggSlot& sl, GrShared<NW>& sh, uint32_t* nf,
+                                            GrCxStage* cxs) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint32_t L = bk.L;  // <= 128
   const uint32_t eb = sl.ev_base, n = sl.ev_cnt, ng = ga.ng;
@@ -2752,6 +3307,71 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
       }
       return entry(start, cnt, b, er);
     };
+    // 0. (CX) the level's cancels: pairs {removed} {maker position} into lanes (lane k: entry k, in log order).
+    //    An in-group target's position is its offset in the group's rests (R before it), an older order's its
+    //    live quantity ahead in the initial FIFO (flag AGG_CXP).
+    uint32_t ncx = 0, tu = 0, tr = 0, tpv = 0, npre = 0;
+    bool hasin = false;
+    unsigned long long umax = 0;
+    if constexpr (CX) {
+      GrCxStage& X = cxs[wv];
+      for (uint32_t b = 0; b < cnt; b += 64) {
+        uint32_t er;
+        const AggGEv E = ent(b, er);
+        const bool v = b + (uint32_t)lane < cnt;
+        const bool cu = v && (E.w & (GR_CXF | GR_CXU)) == (GR_CXF | GR_CXU);
+        const unsigned long long m = __ballot(cu);
+        if (!m) continue;
+        const uint32_t k = ncx + (uint32_t)__popcll(m & lanemask_lt());
+        if (cu && k < 64u) {
+          X.cxu[k] = (uint32_t)E.qty;
+          X.cxr[k] = (uint32_t)srt[start + b + lane - 1].qty;  // its first event, just before it
+          X.cxp[k] = (E.w & GR_CXP) ? 1u : 0u;
+        }
+        ncx += (uint32_t)__popcll(m);
+      }
+      if (ncx > 64u) {  // (the walk takes at most GW_CXN per level and group)
+        a_set_err(bk, ERR_INCONSISTENT);
+        ncx = 64u;
+      }
+      wave_mem_order();
+      if ((uint32_t)lane < ncx) {
+        tu = X.cxu[lane];
+        tr = X.cxr[lane];
+        tpv = X.cxp[lane];
+      }
+      const unsigned long long pm = __ballot((uint32_t)lane < ncx && tpv);
+      npre = (uint32_t)__popcll(pm);
+      hasin = __ballot((uint32_t)lane < ncx && !tpv) != 0ull;
+      for (unsigned long long m = pm; m; m &= m - 1ull) {
+        const unsigned long long uk = rl32(tu, __builtin_ctzll(m));
+        umax = uk > umax ? uk : umax;
+      }
+    }
+    // (CX) a rest's effective quantity: its full quantity less what a cancel removed (ru: its offset in the
+    // group's rests at the level, RU the running offset)
+    auto reff = [&](bool rs, long long rqf, unsigned long long& RU) -> long long {
+      if constexpr (!CX) {
+        return rqf;
+      } else {
+        if (!hasin) return rqf;
+        const long long incu = wave_incl_scan(rqf);
+        const unsigned long long ru = RU + (unsigned long long)(incu - rqf);
+        RU += (unsigned long long)rli64(incu, 63);
+        uint32_t dec = 0;
+        for (uint32_t k = 0; k < ncx; ++k) {
+          const uint32_t uk = rl32(tu, (int)k), rk = rl32(tr, (int)k), pk = rl32(tpv, (int)k);
+          if (!pk && rs && ru == (unsigned long long)uk) dec = rk;
+        }
+        return rqf - (long long)dec;
+      }
+    };
+    auto is_rest = [&](bool v, const AggGEv& E) -> bool {
+      if constexpr (CX)
+        return v && (E.w & (AGG_TAKE | GR_CXF)) == 0u;
+      else
+        return v && (E.w & AGG_TAKE) == 0u;
+    };
     // 1. C: the takes' total
     unsigned long long C = 0;
     for (uint32_t b = 0; b < cnt; b += 64) {
@@ -2768,63 +3388,141 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
     int pq = 0;
     unsigned long long pen = 0;
     bool exhausted = false;
-    for (;;) {
-      if (ch == NIL) {
-        exhausted = true;
-        break;
+    uint32_t ntail = NIL, nte = 0;  // (CX slow path) the FIFO's tail and its fill after the group
+    const bool slow = CX && npre != 0u;
+    // (CX) the slow path — cancels of orders from before the group at this level: one FIFO chunk as the
+    // maker space sees it (per slot: its effective quantity after a cancel, where it starts and ends, what
+    // is left of it after the group)
+    struct SlowChunk {
+      uint32_t uq, qe, nq, nx;
+      unsigned long long cs, ce, sq, iu, ic;
+    };
+    auto slow_chunk = [&](uint32_t c, unsigned long long Wu, unsigned long long Wc) -> SlowChunk {
+      SlowChunk o;
+      const int q = act ? bk.chunks[c].qty[lane] : 0;
+      o.sq = act ? bk.chunks[c].seq[lane] : 0ull;
+      o.nx = auniu(bk.chunks[c].hdr.next);
+      o.uq = (uint32_t)max(q, 0);
+      const long long iu = wave_incl_scan((long long)o.uq);
+      const unsigned long long us = Wu + (unsigned long long)(iu - (long long)o.uq);
+      uint32_t dec = 0;
+      for (uint32_t k = 0; k < ncx; ++k) {
+        const uint32_t uk = rl32(tu, (int)k), rk = rl32(tr, (int)k), pk = rl32(tpv, (int)k);
+        if (pk && o.uq && us == (unsigned long long)uk) dec = rk;
       }
-      if (W >= C) {
+      o.qe = o.uq - dec;
+      const long long ic = wave_incl_scan((long long)o.qe);
+      o.cs = Wc + (unsigned long long)(ic - (long long)o.qe);
+      o.ce = Wc + (unsigned long long)ic;
+      o.nq = !o.uq ? 0u : dec ? 0u : o.ce <= C ? 0u : o.cs >= C ? o.uq : (uint32_t)(o.ce - C);
+      o.iu = (unsigned long long)rli64(iu, 63);
+      o.ic = (unsigned long long)rli64(ic, 63);
+      return o;
+    };
+    if (slow) {
+      // pass 1 (counts): up to the first chunk the group leaves untouched (the takes covered and every
+      // cancelled order passed), or the FIFO's end
+      unsigned long long Wu = 0;
+      uint32_t lastkept = NIL;
+      bool reached_end = false;
+      for (uint32_t guard = 0;; ++guard) {
+        if (ch == NIL) {
+          reached_end = true;
+          break;
+        }
+        if (W >= C && Wu > umax) break;
+        if (guard > bk.nchunks) {  // (a cycle in the chain: corrupt)
+          a_set_err(bk, ERR_INCONSISTENT);
+          reached_end = true;
+          ch = NIL;
+          break;
+        }
+        if (ch >= bk.nchunks) {
+          a_set_err(bk, ERR_INCONSISTENT);
+          reached_end = true;
+          ch = NIL;
+          break;
+        }
+        const SlowChunk o = slow_chunk(ch, Wu, W);
+        nmk += (uint32_t)__popcll(__ballot(o.qe > 0u && o.cs < C));
+        nfull += (uint32_t)__popcll(__ballot(o.uq > 0u && o.nq == 0u));  // initial orders leaving the book
+        if (__ballot(o.nq > 0u) == 0ull) {
+          ++nfreed;
+        } else {
+          if (newhead == NIL) newhead = ch;
+          lastkept = ch;
+        }
+        Wu += o.iu;
+        W += o.ic;
+        ch = o.nx;
+      }
+      if (newhead == NIL) newhead = reached_end ? NIL : ch;
+      exhausted = reached_end && W <= C;
+      ntail = reached_end ? lastkept : auniu(sh.ltail[lvl]);
+      nte = !reached_end ? auniu(te_raw) : lastkept == NIL ? 0u : lastkept == auniu(sh.ltail[lvl]) ? auniu(te_raw) : (uint32_t)ME_C;
+    } else {
+      for (;;) {
+        if (ch == NIL) {
+          exhausted = true;
+          break;
+        }
+        if (W >= C) {
+          newhead = ch;
+          break;
+        }
+        if (ch >= bk.nchunks) {
+          a_set_err(bk, ERR_INCONSISTENT);
+          exhausted = true;
+          break;
+        }
+        const int q = act ? bk.chunks[ch].qty[lane] : 0;
+        const unsigned long long sq = act ? bk.chunks[ch].seq[lane] : 0ull;
+        const uint32_t nx = auniu(bk.chunks[ch].hdr.next);
+        const long long inc = wave_incl_scan((long long)q);
+        const unsigned long long ex = (unsigned long long)(inc - q), en = W + (unsigned long long)inc;
+        const unsigned long long live = (unsigned long long)rli64(inc, 63);
+        const bool cons = q > 0 && W + ex < C;
+        const unsigned long long cm = __ballot(cons);
+        const uint32_t r = nmk + (uint32_t)__popcll(cm & lanemask_lt());
+        if (cons && r < GR_STAGE) {
+          mkl[r].seq = sq;
+          mkl[r].end = en;
+        }
+        nmk += (uint32_t)__popcll(cm);
+        nfull += (uint32_t)__popcll(__ballot(q > 0 && en <= C));
+        if (W + live <= C) {  // emptied
+          if (lane == 0 && nfreed < GR_STAGE) frl[nfreed] = ch;
+          ++nfreed;
+          W += live;
+          ch = nx;
+          continue;
+        }
+        pch = ch;  // C ends inside this chunk
+        pq = q;
+        pen = en;
         newhead = ch;
         break;
       }
-      if (ch >= bk.nchunks) {
-        a_set_err(bk, ERR_INCONSISTENT);
-        exhausted = true;
-        break;
+      if (newhead != NIL) {
+        ntail = auniu(sh.ltail[lvl]);
+        nte = auniu(te_raw);
       }
-      const int q = act ? bk.chunks[ch].qty[lane] : 0;
-      const unsigned long long sq = act ? bk.chunks[ch].seq[lane] : 0ull;
-      const uint32_t nx = auniu(bk.chunks[ch].hdr.next);
-      const long long inc = wave_incl_scan((long long)q);
-      const unsigned long long ex = (unsigned long long)(inc - q), en = W + (unsigned long long)inc;
-      const unsigned long long live = (unsigned long long)rli64(inc, 63);
-      const bool cons = q > 0 && W + ex < C;
-      const unsigned long long cm = __ballot(cons);
-      const uint32_t r = nmk + (uint32_t)__popcll(cm & lanemask_lt());
-      if (cons && r < GR_STAGE) {
-        mkl[r].seq = sq;
-        mkl[r].end = en;
-      }
-      nmk += (uint32_t)__popcll(cm);
-      nfull += (uint32_t)__popcll(__ballot(q > 0 && en <= C));
-      if (W + live <= C) {  // emptied
-        if (lane == 0 && nfreed < GR_STAGE) frl[nfreed] = ch;
-        ++nfreed;
-        W += live;
-        ch = nx;
-        continue;
-      }
-      pch = ch;  // C ends inside this chunk
-      pq = q;
-      pen = en;
-      newhead = ch;
-      break;
     }
     const unsigned long long T0 = exhausted ? W : ~0ull;
     const unsigned long long Cr = exhausted && C > W ? C - W : 0ull;  // taken from this group's rests
     // 3. the rests: those C reaches are makers too (after the FIFO's), the others survive
     uint32_t nrc = 0, ks = 0;
     {
-      unsigned long long RR = 0;
+      unsigned long long RR = 0, RU = 0;
       for (uint32_t b = 0; b < cnt; b += 64) {
         uint32_t er;
         const AggGEv E = ent(b, er);
         const bool v = b + (uint32_t)lane < cnt;
-        const bool rs = v && (E.w & AGG_TAKE) == 0u;
-        const long long rq = rs ? (long long)E.qty : 0ll;
+        const bool rs = is_rest(v, E);
+        const long long rq = reff(rs, rs ? (long long)E.qty : 0ll, RU);
         const long long inc = wave_incl_scan(rq);
         const unsigned long long st0 = RR + (unsigned long long)(inc - rq), en = RR + (unsigned long long)inc;
-        const bool cons = rs && st0 < Cr;
+        const bool cons = rs && rq > 0 && st0 < Cr;
         const unsigned long long cm = __ballot(cons);
         const uint32_t r = nmk + nrc + (uint32_t)__popcll(cm & lanemask_lt());
         if (cons && r < GR_STAGE) {
@@ -2832,11 +3530,11 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
           mkl[r].end = T0 + en;
         }
         nrc += (uint32_t)__popcll(cm);
-        ks += (uint32_t)__popcll(__ballot(rs && en > Cr));
+        ks += (uint32_t)__popcll(__ballot(rs && rq > 0 && en > Cr));
         RR += (unsigned long long)rli64(inc, 63);
       }
     }
-    const uint32_t te0 = newhead != NIL ? auniu(te_raw) : 0u;  // the tail survives iff newhead does
+    const uint32_t te0 = newhead != NIL ? nte : 0u;  // the FIFO's tail fill, if anything of it survives
     const uint32_t tailfree = newhead != NIL ? (uint32_t)ME_C - te0 : 0u;
     const uint32_t need = ks > tailfree ? (ks - tailfree + ME_C - 1) / ME_C : 0u;
     const uint32_t own = min(need, nfreed), deficit = need - own;
@@ -2868,7 +3566,7 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
       wave_mem_order();
       continue;
     }
-    const bool staged = nmkt <= GR_STAGE && nfreed <= GR_STAGE;
+    const bool staged = !slow && nmkt <= GR_STAGE && nfreed <= GR_STAGE;
     // 4. makers and emptied chunks to HBM: from LDS, or past GR_STAGE by a second read of the FIFO
     wave_mem_order();
     if (staged) {
@@ -2878,39 +3576,78 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
       unsigned long long Wv = 0;
       uint32_t mi = 0, fi = 0;
       ch = head0;
-      while (Wv < C && ch < bk.nchunks) {
-        const int q = act ? bk.chunks[ch].qty[lane] : 0;
-        const unsigned long long sq = act ? bk.chunks[ch].seq[lane] : 0ull;
-        const uint32_t nx = auniu(bk.chunks[ch].hdr.next);
-        const long long inc = wave_incl_scan((long long)q);
-        const unsigned long long ex = (unsigned long long)(inc - q), en = Wv + (unsigned long long)inc;
-        const unsigned long long live = (unsigned long long)rli64(inc, 63);
-        const bool cons = q > 0 && Wv + ex < C;
-        const unsigned long long cm = __ballot(cons);
-        if (cons) {
-          AggMk m;
-          m.seq = sq;
-          m.end = en;
-          ag.mk[mk_base + mi + (uint32_t)__popcll(cm & lanemask_lt())] = m;
+      if (slow) {
+        // pass 2 (writes): the same chunks; consumed makers, freed chunks, the slots' new quantities, and the
+        // surviving chunks linked to each other (a chunk a cancel left without live orders leaves the FIFO)
+        unsigned long long Wu = 0;
+        uint32_t pk = NIL;
+        for (uint32_t guard = 0;; ++guard) {
+          if (ch == NIL || (Wv >= C && Wu > umax) || ch >= bk.nchunks || guard > bk.nchunks) break;
+          const SlowChunk o = slow_chunk(ch, Wu, Wv);
+          const bool cons = o.qe > 0u && o.cs < C;
+          const unsigned long long cm = __ballot(cons);
+          if (cons) {
+            AggMk m;
+            m.seq = o.sq;
+            m.end = o.ce;
+            ag.mk[mk_base + mi + (uint32_t)__popcll(cm & lanemask_lt())] = m;
+          }
+          mi += (uint32_t)__popcll(cm);
+          if (act && o.nq != o.uq) bk.chunks[ch].qty[lane] = (int)o.nq;
+          if (__ballot(o.nq > 0u) == 0ull) {
+            if (lane == 0) ag.fr[fr_base + fi] = ch;
+            ++fi;
+          } else {
+            if (lane == 0) {
+              bk.chunks[ch].hdr.prev = pk;
+              if (pk != NIL) bk.chunks[pk].hdr.next = ch;
+            }
+            pk = ch;
+          }
+          Wu += o.iu;
+          Wv += o.ic;
+          ch = o.nx;
         }
-        mi += (uint32_t)__popcll(cm);
-        if (Wv + live > C) break;
-        if (lane == 0) ag.fr[fr_base + fi] = ch;
-        ++fi;
-        Wv += live;
-        ch = nx;
+        if (lane == 0) {
+          const uint32_t stop = ch < bk.nchunks ? ch : NIL;  // the first chunk the group left alone
+          if (pk != NIL) bk.chunks[pk].hdr.next = stop;
+          if (stop != NIL) bk.chunks[stop].hdr.prev = pk;
+        }
+      } else {
+        while (Wv < C && ch < bk.nchunks) {
+          const int q = act ? bk.chunks[ch].qty[lane] : 0;
+          const unsigned long long sq = act ? bk.chunks[ch].seq[lane] : 0ull;
+          const uint32_t nx = auniu(bk.chunks[ch].hdr.next);
+          const long long inc = wave_incl_scan((long long)q);
+          const unsigned long long ex = (unsigned long long)(inc - q), en = Wv + (unsigned long long)inc;
+          const unsigned long long live = (unsigned long long)rli64(inc, 63);
+          const bool cons = q > 0 && Wv + ex < C;
+          const unsigned long long cm = __ballot(cons);
+          if (cons) {
+            AggMk m;
+            m.seq = sq;
+            m.end = en;
+            ag.mk[mk_base + mi + (uint32_t)__popcll(cm & lanemask_lt())] = m;
+          }
+          mi += (uint32_t)__popcll(cm);
+          if (Wv + live > C) break;
+          if (lane == 0) ag.fr[fr_base + fi] = ch;
+          ++fi;
+          Wv += live;
+          ch = nx;
+        }
       }
       if (Cr) {
-        unsigned long long RR = 0;
+        unsigned long long RR = 0, RU = 0;
         for (uint32_t b = 0; b < cnt; b += 64) {
           uint32_t er;
           const AggGEv E = ent(b, er);
           const bool v = b + (uint32_t)lane < cnt;
-          const bool rs = v && (E.w & AGG_TAKE) == 0u;
-          const long long rq = rs ? (long long)E.qty : 0ll;
+          const bool rs = is_rest(v, E);
+          const long long rq = reff(rs, rs ? (long long)E.qty : 0ll, RU);
           const long long inc = wave_incl_scan(rq);
           const unsigned long long st0 = RR + (unsigned long long)(inc - rq), en = RR + (unsigned long long)inc;
-          const bool cons = rs && st0 < Cr;
+          const bool cons = rs && rq > 0 && st0 < Cr;
           const unsigned long long cm = __ballot(cons);
           if (cons) {
             AggMk m;
@@ -2923,17 +3660,20 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
         }
       }
     }
-    // 5. the FIFO's new state: emptied chunks hold qty 0, the chunk C ends in keeps what is left
+    // 5. the FIFO's new state: emptied chunks hold qty 0, the chunk C ends in keeps what is left (the slow
+    //    path wrote its chunks in pass 2)
     wave_mem_order();
-    for (uint32_t f0 = 0; f0 < nfreed; f0 += 4) {
-      const uint32_t f = f0 + (uint32_t)lane / ME_C;
-      if (f < nfreed) {
-        const uint32_t c = staged ? frl[f] : ag.fr[fr_base + f];
-        if (c < bk.nchunks) bk.chunks[c].qty[lane % ME_C] = 0;
+    if (!slow) {
+      for (uint32_t f0 = 0; f0 < nfreed; f0 += 4) {
+        const uint32_t f = f0 + (uint32_t)lane / ME_C;
+        if (f < nfreed) {
+          const uint32_t c = staged ? frl[f] : ag.fr[fr_base + f];
+          if (c < bk.nchunks) bk.chunks[c].qty[lane % ME_C] = 0;
+        }
       }
+      if (pch != NIL && act && pq > 0 && pen - (unsigned long long)pq < C)
+        bk.chunks[pch].qty[lane] = pen <= C ? 0 : (int)(pen - C);
     }
-    if (pch != NIL && act && pq > 0 && pen - (unsigned long long)pq < C)
-      bk.chunks[pch].qty[lane] = pen <= C ? 0 : (int)(pen - C);
     // 6. each take's fill count: the makers overlapping its interval of the level's maker space
     wave_mem_order();
     {
@@ -2967,6 +3707,11 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
       o.d_off = d_off;
       o.ks = ks;
       sh.lv[lvl] = o;
+      // (CX) the FIFO's tail after the group for phase D (a cancel may have taken the old tail chunk out)
+      if constexpr (CX) {
+        sh.ltail[lvl] = newhead != NIL ? ntail : NIL;
+        sh.ltend[lvl] = (uint8_t)te0;
+      }
     }
     wave_mem_order();  // the next level reuses the staging
   }
@@ -3162,6 +3907,31 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
     const uint32_t head0 = auniu(sh.lhead[lvl]), tail0 = auniu(sh.ltail[lvl]);
     const uint32_t te0 = newhead != NIL ? auniu((uint32_t)sh.ltend[lvl]) : 0u;
     const uint32_t tailfree = newhead != NIL ? (uint32_t)ME_C - te0 : 0u;
+    // (CX) the level's cancels of this group's rests: {offset in the rests, removed} in lanes
+    uint32_t ncx = 0, tu = 0, tr = 0;
+    if constexpr (CX) {
+      GrCxStage& X = cxs[wv];
+      for (uint32_t b = 0; b < cnt; b += 64) {
+        uint32_t er;
+        const AggGEv E = entry(start, cnt, b, er);
+        const bool v = b + (uint32_t)lane < cnt;
+        const bool cu = v && (E.w & (GR_CXF | GR_CXU | GR_CXP)) == (GR_CXF | GR_CXU);
+        const unsigned long long m = __ballot(cu);
+        if (!m) continue;
+        const uint32_t k = ncx + (uint32_t)__popcll(m & lanemask_lt());
+        if (cu && k < 64u) {
+          X.cxu[k] = (uint32_t)E.qty;
+          X.cxr[k] = (uint32_t)srt[start + b + lane - 1].qty;
+        }
+        ncx += (uint32_t)__popcll(m);
+      }
+      ncx = min(ncx, 64u);
+      wave_mem_order();
+      if ((uint32_t)lane < ncx) {
+        tu = X.cxu[lane];
+        tr = X.cxr[lane];
+      }
+    }
     auto newchunk = [&](uint32_t c) -> uint32_t {
       return c < own ? ag.fr[fr_base + c] : ag.fr[alloc_base + d_off + (c - own)];
     };
@@ -3171,16 +3941,29 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
     if (nmk && staged && (uint32_t)lane < nmk) mkl[lane] = ag.mk[mk_base + lane];
     wave_mem_order();
     const long long price = sl.base + (long long)lvl;
-    unsigned long long A0 = 0, RR = 0;
+    unsigned long long A0 = 0, RR = 0, RU = 0;
     uint32_t g0 = 0;
     for (uint32_t b = 0; b < cnt; b += 64) {
       uint32_t er;
       const AggGEv E = entry(start, cnt, b, er);
       const bool v = b + (uint32_t)lane < cnt;
-      const bool tk = v && (E.w & AGG_TAKE) != 0u, rs = v && !tk;
-      const long long tq = tk ? (long long)E.qty : 0ll, rq = rs ? (long long)E.qty : 0ll;
+      const bool tk = v && (E.w & AGG_TAKE) != 0u;
+      const bool rs = CX ? v && (E.w & (AGG_TAKE | GR_CXF)) == 0u : v && !tk;
+      const long long tq = tk ? (long long)E.qty : 0ll;
+      long long rq = rs ? (long long)E.qty : 0ll;
+      if (CX && ncx) {  // a rest a cancel shortened keeps its consumed part only
+        const long long incu = wave_incl_scan(rq);
+        const unsigned long long ru = RU + (unsigned long long)(incu - rq);
+        RU += (unsigned long long)rli64(incu, 63);
+        uint32_t dec = 0;
+        for (uint32_t k = 0; k < ncx; ++k) {
+          const uint32_t uk = rl32(tu, (int)k), rk = rl32(tr, (int)k);
+          if (rs && ru == (unsigned long long)uk) dec = rk;
+        }
+        rq -= (long long)dec;
+      }
       const long long tinc = wave_incl_scan(tq), rinc = wave_incl_scan(rq);
-      const unsigned long long sq = gmin + rsq[srec(E.w)];
+      const unsigned long long sq = gmin + rsq[(tk || rs) ? srec(E.w) : 0u];
       if (tk && nmk) {  // fills
         const uint32_t x0 = nf[er], nfl = EX(er + 1) - x0;
         if (nfl) {
@@ -3206,7 +3989,7 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
       }
       // surviving rests
       const unsigned long long st0 = RR + (unsigned long long)(rinc - rq), en = RR + (unsigned long long)rinc;
-      const bool surv = rs && en > Cr;
+      const bool surv = rs && rq > 0 && en > Cr;
       const unsigned long long sm = __ballot(surv);
       if (surv) {
         const uint32_t gi = g0 + (uint32_t)__popcll(sm & lanemask_lt());
@@ -3257,10 +4040,11 @@ __device__ __forceinline__ void gres_symbol(const BookDev& bk, const AggGArgs& g
   GR_STAMP(bk, s, 7);
 }
 
-template <int NW>
+template <int NW, bool CX>
 __global__ __launch_bounds__(NW * 64, GR_WPE) void k_agg_gres(BookDev bk, AggGArgs ga, AggSrc src, AggDev ag,
                                                        uint32_t ne) {
   __shared__ GrShared<NW> sh;
+  __shared__ GrCxStage cxs[CX ? NW : 1];
   extern __shared__ uint32_t gr_dyn[];  // [ne] fill counts / offsets
   for (uint32_t s = blockIdx.x; s < bk.S; s += gridDim.x) {
     const AggSlot sl = ag.slot[s];
@@ -3270,9 +4054,9 @@ __global__ __launch_bounds__(NW * 64, GR_WPE) void k_agg_gres(BookDev bk, AggGAr
       continue;
     }
     if (sl.ev_cnt <= ne)
-      gres_symbol<NW, true>(bk, ga, src, ag, s, sl, sh, gr_dyn);
+      gres_symbol<NW, true, CX>(bk, ga, src, ag, s, sl, sh, gr_dyn, cxs);
     else
-      gres_symbol<NW, false>(bk, ga, src, ag, s, sl, sh, ag.evn + sl.ev_base);
+      gres_symbol<NW, false, CX>(bk, ga, src, ag, s, sl, sh, ag.evn + sl.ev_base, cxs);
     __syncthreads();
   }
 }
@@ -3336,7 +4120,10 @@ hipError_t launch_agg_group(hipStream_t st, const BookDev& bk, const BatchDev* b
     const char* e = getenv("ME_GW_HELPER");
     return !e || atoi(e) != 0;
   }();
-  if (helper)
+  const bool cx = ag.gw_cx != 0u;  // groups with cancels: the walk that covers them, and its resolve
+  if (cx)
+    hipLaunchKernelGGL(k_agg_gwalk_cx, dim3(grid), dim3(128), 0, st, bk, ga, ag);
+  else if (helper)
     hipLaunchKernelGGL(k_agg_gwalk2, dim3(grid), dim3(128), 0, st, bk, ga, ag);
   else
     hipLaunchKernelGGL(k_agg_gwalk, dim3(grid), dim3(64), 0, st, bk, ga, ag);
@@ -3353,17 +4140,26 @@ hipError_t launch_agg_group(hipStream_t st, const BookDev& bk, const BatchDev* b
     return e ? atoi(e) : 0;
   }();
   const uint64_t per_sym = recs / (bk.S ? bk.S : 1u);
-  const int nw = gw_env == 2 || gw_env == 4 || gw_env == 8 ? gw_env : per_sym < GR_FOUR_BELOW ? 4 : 8;
+  int nw = gw_env == 2 || gw_env == 4 || gw_env == 8 ? gw_env : per_sym < GR_FOUR_BELOW ? 4 : 8;
+  if (cx && nw == 2) nw = 4;  // (the 2-wave form is a measurement switch; the resolve with cancels has 4 or 8)
   const size_t shb = nw == 2 ? sizeof(GrShared<2>) : nw == 4 ? sizeof(GrShared<4>) : sizeof(GrShared<GR_WAVES>);
   const uint64_t ne_cap = ((64u << 10) - shb) / 4u & ~63ull;
   if (ne > ne_cap) ne = ne_cap;
-  if (nw == 2)
-    hipLaunchKernelGGL(k_agg_gres<2>, dim3(grid), dim3(128), (size_t)ne * 4u, st, bk, ga, src, ag, (uint32_t)ne);
-  else if (nw == 4)
-    hipLaunchKernelGGL(k_agg_gres<4>, dim3(grid), dim3(256), (size_t)ne * 4u, st, bk, ga, src, ag, (uint32_t)ne);
-  else
-    hipLaunchKernelGGL(k_agg_gres<GR_WAVES>, dim3(grid), dim3(GR_THREADS), (size_t)ne * 4u, st, bk, ga, src, ag,
-                       (uint32_t)ne);
+  if (nw == 2) {
+    hipLaunchKernelGGL((k_agg_gres<2, false>), dim3(grid), dim3(128), (size_t)ne * 4u, st, bk, ga, src, ag, (uint32_t)ne);
+  } else if (nw == 4) {
+    if (cx)
+      hipLaunchKernelGGL((k_agg_gres<4, true>), dim3(grid), dim3(256), (size_t)ne * 4u, st, bk, ga, src, ag, (uint32_t)ne);
+    else
+      hipLaunchKernelGGL((k_agg_gres<4, false>), dim3(grid), dim3(256), (size_t)ne * 4u, st, bk, ga, src, ag, (uint32_t)ne);
+  } else {
+    if (cx)
+      hipLaunchKernelGGL((k_agg_gres<GR_WAVES, true>), dim3(grid), dim3(GR_THREADS), (size_t)ne * 4u, st, bk, ga, src,
+                         ag, (uint32_t)ne);
+    else
+      hipLaunchKernelGGL((k_agg_gres<GR_WAVES, false>), dim3(grid), dim3(GR_THREADS), (size_t)ne * 4u, st, bk, ga, src,
+                         ag, (uint32_t)ne);
+  }
   return hipGetLastError();
 }
 }  // namespace me

@@ -280,6 +280,11 @@ struct me_engine {
   // far prices — config 5's stream), which then pays both paths
   bool reg_agg_auto = false;
   uint64_t ho_k = 0, ho_h = 0;  // the last {launch, hand-offs} sample
+  // groups with cancels through the walk that covers them (k_agg_gwalk_cx, hot.ag.gw_cx): ME_GW_CANCEL=1 from
+  // the start, =0 never; unset, from the first sample whose hand-off rate would have turned the grouped path
+  // off (only if hand-offs stay that high with it does the grouped path go)
+  bool gw_cx_auto = false;
+  uint64_t cx_from = 0;  // (auto) samples of launches before the switch do not count against the new walk
   uint32_t launch_no = 0;                  // match launches enqueued
   uint64_t adm_total = 0;                  // records accepted
   uint64_t adm_matched = 0;                // records of the batches those launches matched
@@ -547,6 +552,9 @@ extern "C" me_engine* me_create(const me_config* cfg) {
                                            (uint64_t)cfg->max_batch * grp <= (8ull << 20));  // (pools of a
                                                                                              // group's records)
     e->reg_agg_auto = e->hot.agg_reg && !vr;
+    const char* vc = getenv("ME_GW_CANCEL");
+    e->hot.ag.gw_cx = e->hot.agg_reg && vc && atoi(vc) != 0 ? 1u : 0u;
+    e->gw_cx_auto = e->hot.agg_reg && !vc;
     // the grouped aggregate path's side jobs on a stream of their own (ME_SIDE_STREAM=0: in line)
     const char* vs = getenv("ME_SIDE_STREAM");
     if (e->hot.agg_reg && !(vs && atoi(vs) == 0)) {
@@ -965,11 +973,18 @@ static int pipe_launch(me_engine* e, const me_engine::Group* nb) {
     rc = timing_slot(e, orders, gm.n, tl, timed);
     if (rc) return rc;
   }
-  if (e->reg_agg_auto && e->hot.agg_reg) {  // the hand-off rate since the last sample k_seq_sweep published
-    const unsigned long long p = *(volatile unsigned long long*)(e->pub_host + 1);
+  if ((e->reg_agg_auto || e->gw_cx_auto) && e->hot.agg_reg) {  // the hand-off rate since the last sample
+    const unsigned long long p = *(volatile unsigned long long*)(e->pub_host + 1);  // (k_seq_sweep publishes it)
     const uint64_t k = p >> 32, h = p & 0xFFFFFFFFull;
     if (k > e->ho_k) {
-      if ((h - e->ho_h) * 16 > (k - e->ho_k) * (uint64_t)e->bk.S) e->hot.agg_reg = false;
+      if (e->ho_k >= e->cx_from && (h - e->ho_h) * 16 > (k - e->ho_k) * (uint64_t)e->bk.S) {
+        if (e->gw_cx_auto && !e->hot.ag.gw_cx) {  // cancels (config 5): the walk that covers them first
+          e->hot.ag.gw_cx = 1u;
+          e->cx_from = (uint64_t)e->launch_no + 1u;
+        } else if (e->reg_agg_auto) {
+          e->hot.agg_reg = false;
+        }
+      }
       e->ho_k = k;
       e->ho_h = h;
     }
@@ -1839,7 +1854,8 @@ extern "C" int me_chunk_stats(me_engine* e, uint64_t* reclaims, uint64_t* high_w
 
 extern "C" int me_paths_read(const me_engine* e, uint32_t* flags) {
   if (!e || !flags) return ME_E_INVALID;
-  *flags = (e->hot.agg_reg ? ME_PATH_GROUPED_AGG : 0u) | (e->bk.hot_min && e->hot.agg ? ME_PATH_HOT_AGG : 0u);
+  *flags = (e->hot.agg_reg ? ME_PATH_GROUPED_AGG : 0u) | (e->bk.hot_min && e->hot.agg ? ME_PATH_HOT_AGG : 0u) |
+           (e->hot.agg_reg && e->hot.ag.gw_cx ? ME_PATH_GROUPED_CANCELS : 0u);
   return ME_OK;
 }
 

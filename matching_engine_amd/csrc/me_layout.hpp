@@ -255,6 +255,7 @@ struct AggDev {
   uint32_t ladder_max;         // k_agg_walk: windows up to this many levels take the ladder walk
   uint32_t lw_occ;             // k_agg_walk: ladders deeper than this search the next level through an LDS
                                // occupancy bitmap (0: the 64-level total scan at every depth)
+  uint32_t gw_cx;              // grouped launches: the walk that covers cancels (k_agg_gwalk_cx) and its resolve
   // grouped launches (register-window path, k_agg_gwalk): per symbol and batch of the group, [S][ME_GMAX + 1]
   uint32_t* gev;               // the symbol's first log index of batch g (g = ng: the log's end)
   uint32_t* gex;               // the fill offset (k_agg_fin's scan) at gev

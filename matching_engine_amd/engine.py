@@ -334,7 +334,7 @@ class Engine:
         aggregate path (me_agg.hip)."""
         f = C.c_uint32(0)
         _check(self.lib, self.h, self.lib.me_paths_read(self.h, C.byref(f)))
-        return {"grouped_agg": bool(f.value & 1), "hot_agg": bool(f.value & 2)}
+        return {"grouped_agg": bool(f.value & 1), "hot_agg": bool(f.value & 2), "grouped_cancels": bool(f.value & 4)}
 
     def admits(self, b: Batch) -> bool:
         """Would submit_batch(b) be admitted now (me_admission_check)? Nothing is enqueued."""

@@ -201,11 +201,15 @@ def test_agg_groups_cancels_tight_chunk_pool(me, orc, group):
         assert eng.paths()["grouped_agg"]
 
 
-def test_agg_auto_mode_turns_off_under_cancels(me, orc):
+@pytest.mark.parametrize("cx", ["auto", "0"])
+def test_agg_auto_mode_turns_off_under_cancels(me, orc, monkeypatch, cx):
     """Automatic path choice (ME_REG_AGG unset) at a shape that picks the grouped aggregate path (8,192-
     record batches, 128 records per symbol): a cancel-free first phase runs on it; a second phase with
-    30 % cancels hands symbols off until the engine turns it off for good. max_chunks = max_resting + 2S,
-    every batch of both phases against the oracle."""
+    30 % cancels hands symbols off. By default the engine then switches to the grouped walk that covers
+    cancels (k_agg_gwalk_cx) and stays on the grouped path; with ME_GW_CANCEL=0 it turns the grouped path
+    off for good. max_chunks = max_resting + 2S, every batch of both phases against the oracle."""
+    if cx == "0":
+        monkeypatch.setenv("ME_GW_CANCEL", "0")
     sc = me.preset(5, num_symbols=64, levels=128, batch=8192, cancel_pct=30, market_pct=15, market_qty_mult=3)
     st = me.Stream(sc)
     base = st.base_prices()
@@ -222,9 +226,14 @@ def test_agg_auto_mode_turns_off_under_cancels(me, orc):
         outs = _pipelined(eng, batches[:16], 9)
         assert eng.paths()["grouped_agg"], "phase 1 should run on the grouped aggregate path"
         assert eng.stats()["handoffs"] == 0
+        assert not eng.paths()["grouped_cancels"]
         outs += _pipelined(eng, batches[16:], 9)
-        assert not eng.paths()["grouped_agg"], "hand-offs should have turned the aggregate path off"
-        _check(eng, ob, batches, outs, "agg auto flip")
+        p = eng.paths()
+        if cx == "0":
+            assert not p["grouped_agg"], "hand-offs should have turned the aggregate path off"
+        else:
+            assert p["grouped_agg"] and p["grouped_cancels"], f"the walk with cancels should have taken over: {p}"
+        _check(eng, ob, batches, outs, f"agg auto flip (ME_GW_CANCEL={cx})")
 
 
 @pytest.mark.parametrize("symbols,agg", [(768, True), (2048, False)])

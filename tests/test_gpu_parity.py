@@ -424,13 +424,14 @@ def test_edge_symbol_count_sort_plans(me, orc):
             run_both(eng, ob, batches, book_symbols=range(0, S, max(1, S // 50)), ctx=f"S={S}")
 
 
-@pytest.mark.parametrize("reg_agg", ["0", "1"])
+@pytest.mark.parametrize("reg_agg", ["0", "1", "cx"])
 def test_cancelled_chunks_are_unlinked(me, orc, monkeypatch, reg_agg):
     """A level that never empties, with chunk after chunk filled and then cancelled: dead chunks
     (head, middle, tail) must be unlinked and reused, so a 4-chunk pool suffices for 30 rounds.
     ME_REG_AGG=1: the adds go through the grouped aggregate path and the cancels through k_match_reg's
     continuation, which parks freed chunks in fcache — the walk must reuse them (k_agg_gwalk)."""
-    monkeypatch.setenv("ME_REG_AGG", reg_agg)
+    monkeypatch.setenv("ME_REG_AGG", "1" if reg_agg == "cx" else reg_agg)
+    monkeypatch.setenv("ME_GW_CANCEL", "1" if reg_agg == "cx" else "0")  # cx: the cancels inside the grouped walk
     B, S, L, M = me.SIDE_BUY, me.SIDE_SELL, me.TYPE_LIMIT, me.TYPE_MARKET
     C = me._abi.CHUNK_SLOTS
     ob = orc.OracleBook(1)
@@ -452,7 +453,7 @@ def test_cancelled_chunks_are_unlinked(me, orc, monkeypatch, reg_agg):
             run_both(eng, ob, [b, cancels], ctx=f"round {rnd}")
         sweep = _rows(me, [(0, S, M, 0, 0, 5)], start_seq=seq)
         run_both(eng, ob, [sweep], ctx="final sweep")
-        assert eng.paths()["grouped_agg"] == (reg_agg == "1")
+        assert eng.paths()["grouped_agg"] == (reg_agg != "0")
 
 
 def test_capacity_exhaustion_is_loud(me):
