@@ -2603,16 +2603,23 @@ constexpr uint32_t LW_RJ_MASK = 0x1FFFu;
 constexpr uint32_t AGG_CXF = 1u << 14, AGG_CXU = 1u << 13, AGG_CXP = 1u << 12;
 constexpr uint32_t RI_BIG = 0xFFFFFFFFu;  // rest info of a rest too large to pack (>= 2^25): its cancel hands off
 
+struct alignas(16) GwLv {  // per level: initial total, the group's rests, its cancels, the quantity they removed
+  uint32_t t0, rl, n, xl;
+};
+struct alignas(16) GwRi {  // a LIMIT's rest: maker position U, qty << 7 | level (0: none), F at the rest
+  uint32_t u, lq, f, pad;
+};
 struct GwCx {
   uint32_t ct0[2][BK_CAP], ct1[2][BK_CAP], ct2[2][BK_CAP], ct3[2][BK_CAP];  // per batch buffer: each cancel's
-                                            // target {CT_PRE | level << 24 | qty, U, -, 0} or {record | CT_RING,
-                                            // -, -, -} or {record, U, qty << 7 | level, F at its rest}
-  uint32_t t0[128], rl[128], n[128], xl[128];  // per level: initial total, the group's rests, its cancels, the
-                                               // quantity they removed
-  uint32_t u[128 * GW_CXL], rm[128 * GW_CXL];  // per level: its first GW_CXL cancels {maker position, removed}
-  uint32_t ru[GW_RING], rlq[GW_RING], rf[GW_RING];  // rest ring: U, qty << 7 | level (0: no rest), F at the rest
-  uint32_t dbit[ME_GMAX * BK_CAP / 32];     // per record: its rest was cancelled
-  uint32_t npre, preu[GW_CXP], prel[GW_CXP];  // cancelled orders from before the group {position, level}
+                                            // target {CT_PRE | level << 24 | qty, U, -, -} or {record | level << 16
+                                            // | CT_RING, -, -, -} or {record | level << 16, U, lq, F} (from HBM)
+  GwLv lv[128];
+  uint2 ent[128 * GW_CXL];                  // per level: its first GW_CXL cancels {maker position, removed}
+  GwRi ring[GW_RING];                       // the rests of the batch being walked and the one before
+  // (the helper's) targets of the group's cancels so far: a second cancel of one is UNKNOWN — the first left
+  // the order dead, whether it removed anything or found it consumed
+  uint32_t tbit[ME_GMAX * BK_CAP / 32];     // per record of the group
+  uint32_t npre, preu[GW_CXP], prel[GW_CXP];  // orders from before the group {position, level}
 };
 
 __device__ __forceinline__ uint32_t a_ldg(const uint32_t* p) {  // (past the L1: another wave's recent store)
@@ -2662,17 +2669,19 @@ __device__ __forceinline__ uint32_t gw_pre_target(const BookDev& bk, uint32_t s,
 
 // The symbol's per-record rest info in HBM (beside rsq / rjs in its log region): U, qty << 7 | level, F.
 struct GwRest {
-  gptr<uint32_t> u, lq, f;
+  gptr<GwRi> r;  // [total] (16-B aligned: the log region starts 64-event aligned)
 };
 
 // gw_prepare with cancels: the same batch set-up, the group's LIMITs tagged in the seq ring (and their rest
 // info cleared), then every cancel's target classified (cw: unknown -> ME_RJ_UNKNOWN_ORDER; fastm: hand-offs
-// cleared; the descriptor). cut: the first record of the batch the walker walks now (older ones: HBM).
-__device__ __forceinline__ void gw_prepare_cx(GwBuf& B, GwCx& X, uint32_t bsel, AStage& stg, const AggGArgs& ga,
-                                              const BookDev& bk, uint32_t s, uint32_t g, uint32_t cnt, size_t bko,
-                                              long long base, int L, uint32_t nfar0, uint32_t nfar1,
-                                              gptr<uint32_t> rsq, gptr<uint32_t> rjs, const GwRest& rr,
-                                              unsigned long long gmin, uint32_t& rbase, uint32_t cut) {
+// cleared; the descriptor). cut: the first record of the batch the walker walks now (older ones: from HBM);
+// Bp: that batch's buffer (the targets' levels in their control words).
+__device__ __forceinline__ void gw_prepare_cx(GwBuf& B, const GwBuf& Bp, GwCx& X, uint32_t bsel, AStage& stg,
+                                              const AggGArgs& ga, const BookDev& bk, uint32_t s, uint32_t g,
+                                              uint32_t cnt, size_t bko, long long base, int L, uint32_t nfar0,
+                                              uint32_t nfar1, gptr<uint32_t> rsq, gptr<uint32_t> rjs,
+                                              const GwRest& ri, unsigned long long gmin, uint32_t& rbase,
+                                              uint32_t cut) {
   const int lane = lane_id();
   BkRec r0{}, r1{};
   if ((uint32_t)lane < cnt) r0 = ga.b_rec[g][bko + lane];
@@ -2720,9 +2729,12 @@ __device__ __forceinline__ void gw_prepare_cx(GwBuf& B, GwCx& X, uint32_t bsel, 
     if (v) {
       rsq[j] = (uint32_t)(oseq - gmin);
       rjs[j] = (g << AGG_GSHIFT) | oi;
-      rr.lq[j] = 0u;  // (the walker writes a rest's)
       // a LIMIT of this group the walk may rest: its ring entry names its record until k_agg_gres places it
-      if (!cancel && !((okd >> 2) & 1u) && cov && rj == 0u) bk.loc[oseq & bk.ring_mask] = CX_TAG | j;
+      // (and its rest info reads "none" until the walker writes it)
+      if (!cancel && !((okd >> 2) & 1u) && cov && rj == 0u) {
+        bk.loc[oseq & bk.ring_mask] = CX_TAG | j;
+        ri.r[j].lq = 0u;
+      }
     }
     tgt[blk >> 6] = opx;
     isc[blk >> 6] = cancel;
@@ -2740,13 +2752,15 @@ __device__ __forceinline__ void gw_prepare_cx(GwBuf& B, GwCx& X, uint32_t bsel, 
       const uint32_t jj = e & ~CX_TAG;
       if ((e & CX_TAG) && jj < jself && a_ldg((const uint32_t*)&rsq[jj]) == (uint32_t)(T - gmin)) {
         cls = 0u;
-        if (jj >= cut) {  // walked in this batch or the one before: the walker reads the ring
-          d0 = jj | CT_RING;
+        if (jj >= cut) {  // walked in this batch or the one before: the walker reads the ring; its level now
+          const uint32_t cwt = jj >= rb0 ? B.cw[jj - rb0] : Bp.cw[jj - cut];
+          d0 = jj | ((cwt & 127u) << 16) | CT_RING;
         } else {  // walked before: its rest info from HBM now
-          d0 = jj;
-          d1 = a_ldg((const uint32_t*)&rr.u[jj]);
-          d2 = a_ldg((const uint32_t*)&rr.lq[jj]);
-          d3 = a_ldg((const uint32_t*)&rr.f[jj]);
+          const GwRi q = ri.r[jj];
+          d0 = jj | ((q.lq & 127u) << 16);
+          d1 = q.u;
+          d2 = q.lq;
+          d3 = q.f;
         }
       }
     }
@@ -2762,6 +2776,32 @@ __device__ __forceinline__ void gw_prepare_cx(GwBuf& B, GwCx& X, uint32_t bsel, 
         d1 = e1;
       }
     }
+    // a target some earlier cancel of the group named is dead: UNKNOWN (records in order, lane by lane)
+    for (unsigned long long m = __ballot(c && cls == 0u); m; m &= m - 1ull) {
+      const int i = __builtin_ctzll(m);
+      const uint32_t e0 = rl32(d0, i);
+      uint32_t r = 0;  // 0 first, 1 seen, 2 no room
+      if (e0 & CT_PRE) {
+        const uint32_t pu = rl32(d1, i), pl = (e0 >> 24) & 127u, np = auniu(X.npre);
+        const bool vp = (uint32_t)lane < np;
+        if (__ballot(vp && X.preu[vp ? lane : 0] == pu && X.prel[vp ? lane : 0] == pl)) {
+          r = 1u;
+        } else if (np >= GW_CXP) {
+          r = 2u;
+        } else if (lane == 0) {
+          X.preu[np] = pu;
+          X.prel[np] = pl;
+          X.npre = np + 1u;
+        }
+      } else {
+        const uint32_t jj = e0 & 0xFFFu, wd = auniu(X.tbit[jj >> 5]);
+        if ((wd >> (jj & 31u)) & 1u)
+          r = 1u;
+        else if (lane == 0)
+          X.tbit[jj >> 5] = wd | (1u << (jj & 31u));
+      }
+      if (lane == i && r) cls = r;
+    }
     if (c) {
       X.ct0[bsel][blk + lane] = d0;
       X.ct1[bsel][blk + lane] = d1;
@@ -2774,8 +2814,8 @@ __device__ __forceinline__ void gw_prepare_cx(GwBuf& B, GwCx& X, uint32_t bsel, 
   }
 }
 
-// The chain of a block with cancels (lw_block's loop; rests also record their maker position, cancels as
-// above). Returns the records walked: fewer than cnt at the first one the walk does not cover.
+// The chain of a block with cancels (lw_block's loop; a LIMIT also records its rest info, cancels as above).
+// Returns the records walked: fewer than cnt at the first one the walk does not cover.
 __device__ __forceinline__ uint32_t lw_block_cx(LEvG& e, LWalk& w, GwCx& X, const GwRest& ri, int oq, uint32_t ocw,
                                                 uint32_t c0v, uint32_t c1v, uint32_t c2v, uint32_t c3v, uint32_t jb,
                                                 unsigned long long fastm, uint32_t cnt, int& rr) {
@@ -2790,96 +2830,60 @@ __device__ __forceinline__ uint32_t lw_block_cx(LEvG& e, LWalk& w, GwCx& X, cons
     const uint32_t cw = rl32(ocw, r);
     const uint32_t jr = jb + (uint32_t)r;
     if (cw & LW_CX) {
-      const uint32_t d0 = rl32(c0v, r), d1 = rl32(c1v, r);
-      uint32_t l, U, q, Fr, flg, uev, jt = 0;
-      bool dup;
-      if (d0 & CT_PRE) {
-        l = (d0 >> 24) & 127u;
-        q = d0 & 0xFFFFFFu;
-        U = d1;
-        Fr = 0u;  // (nothing was consumed at the group start)
-        flg = AGG_CXF | AGG_CXP;
-        const uint32_t np = auniu(X.npre);  // an older order cancelled before in this group: same {U, level}
-        const bool vp = (uint32_t)lane < np;
-        dup = __ballot(vp && X.preu[vp ? lane : 0] == U && X.prel[vp ? lane : 0] == l) != 0ull;
-      } else {
-        jt = d0 & 0xFFFFu;
-        uint32_t lq;
-        if (d0 & CT_RING) {
-          const uint32_t x = jt & (GW_RING - 1u);
-          lq = auniu(X.rlq[x]);
-          U = auniu(X.ru[x]);
-          Fr = auniu(X.rf[x]);
-        } else {
-          lq = rl32(c2v, r);
-          U = d1;
-          Fr = rl32(c3v, r);
-        }
-        if (lq == RI_BIG) return (uint32_t)r;  // (before anything changed: the continuation from here)
-        l = lq & 127u;
-        q = lq >> 7;
-        flg = AGG_CXF;
-        dup = lq == 0u || ((auniu(X.dbit[jt >> 5]) >> (jt & 31u)) & 1u);  // never rested, or cancelled already
+      // the target (descriptor: its level; older orders and records from before the ring with their rest info,
+      // others in the ring), its level's state and live total, loaded together
+      const uint32_t d0 = rl32(c0v, r);
+      // (a PRE descriptor's level spans bits 24-30, CT_RING's bit among them: test CT_RING only without CT_PRE)
+      const bool pre = (d0 & CT_PRE) != 0u, inring = (d0 & (CT_PRE | CT_RING)) == CT_RING;
+      const uint32_t l = pre ? (d0 >> 24) & 127u : (d0 >> 16) & 127u;
+      const GwLv V = X.lv[l];
+      const GwRi R = X.ring[d0 & (GW_RING - 1u)];
+      const uint32_t tv = w.tot[l];
+      const uint32_t U = inring ? auniu(R.u) : rl32(c1v, r);
+      const uint32_t lq = pre ? ((d0 & 0xFFFFFFu) << 7) | l : inring ? auniu(R.lq) : rl32(c2v, r);
+      const uint32_t Fr = pre ? 0u : inring ? auniu(R.f) : rl32(c3v, r);  // (nothing consumed at the group start)
+      if (lq == RI_BIG) return (uint32_t)r;  // (before anything changed: the continuation from here)
+      const uint32_t q = lq >> 7;  // (0: never rested — a LIMIT filled at once)
+      const uint32_t tot = (int)l == w.bb ? w.cbb : (int)l == w.ba ? w.cba : auniu(tv);
+      const uint32_t n = auniu(V.n), xl = auniu(V.xl), t0 = auniu(V.t0);
+      const uint32_t F = t0 + auniu(V.rl) - xl - tot;     // consumed by the group's takes
+      const uint32_t lo = max(Fr, U > xl ? U - xl : 0u);  // X's start is at least this, and at most U
+      uint32_t cons = F <= lo ? 0u : q;
+      if (ME_UNLIKELY(F > lo && F < U + q)) {  // the bounds do not decide: the exact start from the list
+        if (n > GW_CXL) return (uint32_t)r;    // it no longer holds every cancel: the continuation
+        const bool vl = (uint32_t)lane < n;
+        const uint2 ce = vl ? X.ent[l * GW_CXL + lane] : make_uint2(0u, 0u);
+        const uint32_t st = U - a_wsum(vl && ce.x < U ? ce.y : 0u);
+        cons = F > st ? min(F - st, q) : 0u;
       }
-      uint32_t rem = 0;
-      if (!dup) {
-        const uint32_t n = auniu(X.n[l]), xl = auniu(X.xl[l]);
-        const uint32_t tot = (int)l == w.bb ? w.cbb : (int)l == w.ba ? w.cba : lw_get(w, (int)l);
-        const uint32_t F = auniu(X.t0[l]) + auniu(X.rl[l]) - xl - tot;  // consumed by the group's takes
-        const uint32_t lo = max(Fr, U > xl ? U - xl : 0u);  // X's start is at least this, and at most U
-        uint32_t cons;
-        if (F <= lo) {
-          cons = 0u;
-        } else if (F >= U + q) {
-          cons = q;
+      const uint32_t rem = q - cons;
+      if (rem) {
+        if (n + 1u >= GW_CXN) return (uint32_t)r;
+        if (lane == 0) {
+          if (n < GW_CXL) X.ent[l * GW_CXL + n] = make_uint2(U, rem);
+          X.lv[l].n = n + 1u;
+          X.lv[l].xl = xl + rem;
+        }
+        if ((int)l == w.bb) {
+          w.cbb -= rem;
+          if (!w.cbb) {
+            lw_put(w, w.bb, 0u);
+            w.bb = lw_prev(w, w.bb - 1, w.cbb);
+          }
+        } else if ((int)l == w.ba) {
+          w.cba -= rem;
+          if (!w.cba) {
+            lw_put(w, w.ba, 0u);
+            w.ba = lw_next(w, w.ba + 1, w.cba);
+          }
         } else {
-          if (n > GW_CXL) return (uint32_t)r;  // the list no longer holds every cancel: the continuation
-          const bool vl = (uint32_t)lane < n;
-          const uint32_t cu = vl ? X.u[l * GW_CXL + lane] : 0u, cr = vl ? X.rm[l * GW_CXL + lane] : 0u;
-          const uint32_t st = U - a_wsum(vl && cu < U ? cr : 0u);
-          cons = F > st ? min(F - st, q) : 0u;
+          lw_add(w, (int)l, 0u - rem);
         }
-        rem = q - cons;
-        if (rem) {
-          if (n + 1u >= GW_CXN || ((d0 & CT_PRE) && auniu(X.npre) >= GW_CXP)) return (uint32_t)r;
-          if (lane == 0) {
-            if (n < GW_CXL) {
-              X.u[l * GW_CXL + n] = U;
-              X.rm[l * GW_CXL + n] = rem;
-            }
-            X.n[l] = n + 1u;
-            X.xl[l] = xl + rem;
-            if (d0 & CT_PRE) {
-              const uint32_t np = X.npre;
-              X.preu[np] = U;
-              X.prel[np] = l;
-              X.npre = np + 1u;
-            } else {
-              X.dbit[jt >> 5] |= 1u << (jt & 31u);
-            }
-          }
-          if ((int)l == w.bb) {
-            w.cbb -= rem;
-            if (!w.cbb) {
-              lw_put(w, w.bb, 0u);
-              w.bb = lw_prev(w, w.bb - 1, w.cbb);
-            }
-          } else if ((int)l == w.ba) {
-            w.cba -= rem;
-            if (!w.cba) {
-              lw_put(w, w.ba, 0u);
-              w.ba = lw_next(w, w.ba + 1, w.cba);
-            }
-          } else {
-            lw_add(w, (int)l, 0u - rem);
-          }
-          uev = (d0 & CT_PRE) ? U : U - auniu(X.t0[l]);  // in the resolve: the FIFO's or the rests' position
-          le_emit(e, auniu(l), auniu((jr | flg) << AGG_GREC_SHIFT), auniu(rem));
-          le_emit(e, auniu(l), auniu((jr | flg | AGG_CXU) << AGG_GREC_SHIFT), auniu(uev));
-        }
+        const uint32_t flg = pre ? AGG_CXF | AGG_CXP : AGG_CXF;
+        le_emit(e, l, (jr | flg) << AGG_GREC_SHIFT, rem);
+        le_emit(e, l, (jr | flg | AGG_CXU) << AGG_GREC_SHIFT, pre ? U : U - t0);  // the FIFO's / the rests' position
       }
-      if (lane == 0) X.rlq[jr & (GW_RING - 1u)] = 0u;  // (a cancel never rests)
-      asm volatile("s_mov_b32 m0, %1\n\tv_writelane_b32 %0, %2, m0" : "+v"(rr) : "s"(r), "s"(auniu(rem)) : "m0");
+      asm volatile("s_mov_b32 m0, %1\n\tv_writelane_b32 %0, %2, m0" : "+v"(rr) : "s"(r), "s"(rem) : "m0");
       continue;
     }
     uint32_t rem = (uint32_t)rli32(oq, r);
@@ -2897,26 +2901,24 @@ __device__ __forceinline__ uint32_t lw_block_cx(LEvG& e, LWalk& w, GwCx& X, cons
       asm volatile("" : "+s"(rq));
       if (rq) lw_rest_sell<LEvG>(e, w, lim, rq, jt);
     }
-    // the record's rest info (none: 0) in the ring and, for a rest, in HBM: its maker position, and what the
-    // level's takes had consumed when it rested (a lower bound on its start ever after)
-    uint32_t lq = 0, U = 0, Fr = 0;
-    if (rq) {
-      uint32_t R0 = 0;
-      if (lane == 0) R0 = __hip_atomic_fetch_add(&X.rl[lim], rq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      U = auniu(X.t0[lim]) + rl32(R0, 0);
-      const uint32_t tot = lim == w.bb ? w.cbb : lim == w.ba ? w.cba : lw_get(w, lim);
-      Fr = U + rq - auniu(X.xl[lim]) - tot;
-      lq = rq < (1u << 25) ? (rq << 7) | (uint32_t)lim : RI_BIG;
-    }
-    if (lane == 0) {
-      const uint32_t x = jr & (GW_RING - 1u);
-      X.rlq[x] = lq;
+    // a LIMIT's rest info in the ring (a cancel finds only LIMITs: none for a MARKET) and, for a rest, in
+    // HBM: its maker position and what the level's takes had consumed when it rested (a lower bound on its
+    // start ever after)
+    if (!(cw & LW_MKT)) {
+      GwRi o{0u, 0u, 0u, 0u};
       if (rq) {
-        X.ru[x] = U;
-        X.rf[x] = Fr;
-        ri.u[jr] = U;
-        ri.lq[jr] = lq;
-        ri.f[jr] = Fr;
+        const GwLv V = X.lv[lim];
+        const uint32_t tv = w.tot[lim];
+        const uint32_t rl = auniu(V.rl);
+        const uint32_t tot = lim == w.bb ? w.cbb : lim == w.ba ? w.cba : auniu(tv);
+        o.u = auniu(V.t0) + rl;
+        o.f = o.u + rq - auniu(V.xl) - tot;
+        o.lq = rq < (1u << 25) ? (rq << 7) | (uint32_t)lim : RI_BIG;
+        if (lane == 0) X.lv[lim].rl = rl + rq;
+      }
+      if (lane == 0) {
+        X.ring[jr & (GW_RING - 1u)] = o;
+        if (rq) ri.r[jr] = o;
       }
     }
     asm volatile("s_mov_b32 m0, %1\n\tv_writelane_b32 %0, %2, m0" : "+v"(rr) : "s"(r), "s"(auniu(rem)) : "m0");
@@ -2998,14 +3000,12 @@ __global__ __launch_bounds__(128) void k_agg_gwalk_cx(BookDev bk, AggGArgs ga, A
     __syncthreads();
     if (!go) continue;
     AggGEv* const log8 = reinterpret_cast<AggGEv*>(ag.ev + eb);
-    // the region: evneed 8-B events, then the records' seqs, positions and rest info [total] each
-    // (8 evneed + 20 total <= 16 evneed bytes: evneed >= 3 total)
+    // the region: evneed 8-B events, then the records' seqs and positions [total] each, then (16-B aligned)
+    // their rest info [total] (8 evneed + 24 total + 16 <= 16 evneed bytes: evneed >= 3 total + 64)
     const gptr<uint32_t> rsq = vptr(reinterpret_cast<uint32_t*>(log8 + evneed));
     const gptr<uint32_t> rjs = rsq + total;
     GwRest ri;
-    ri.u = rjs + total;
-    ri.lq = ri.u + total;
-    ri.f = ri.lq + total;
+    ri.r = vptr(reinterpret_cast<GwRi*>((reinterpret_cast<uintptr_t>(log8 + evneed) + 8ull * total + 15ull) & ~15ull));
     const size_t bko = (size_t)s * BK_CAP;
     if (walker) {
       const uint32_t nfc = min(rl32(st.nfree, 0), 64u);
@@ -3019,39 +3019,61 @@ __global__ __launch_bounds__(128) void k_agg_gwalk_cx(BookDev bk, AggGArgs ga, A
       uint32_t hrb = 0;
       const unsigned long long gmin = *ga.seq0;
       const uint32_t c0 = rl32(nsv, 0);
+      for (uint32_t j = (uint32_t)lane; j < ME_GMAX * BK_CAP / 32; j += 64) cx.tbit[j] = 0u;
+      if (lane == 0) cx.npre = 0u;
+      wave_mem_order();
+#ifdef ME_STAMPS
+      unsigned long long h_t = 0, h_m = stamp_now();
+#endif
       if (c0 && c0 <= (uint32_t)BK_CAP)
-        gw_prepare_cx(sh.buf[0], cx, 0u, sh.stg, ga, bk, s, 0u, c0, bko, base, L, nfar0, nfar1, rsq, rjs, ri, gmin,
-                      hrb, 0u);
+        gw_prepare_cx(sh.buf[0], sh.buf[1], cx, 0u, sh.stg, ga, bk, s, 0u, c0, bko, base, L, nfar0, nfar1, rsq, rjs,
+                      ri, gmin, hrb, 0u);
+#ifdef ME_STAMPS
+      h_t += stamp_now() - h_m;
+#endif
       __syncthreads();
       for (uint32_t g = 0; g < ng; ++g) {
         const uint32_t c = g + 1u < ng ? rl32(nsv, (int)(g + 1u)) : 0u;
         // batch g's first record: when batch g + 1 is walked the ring holds batches g and g + 1
         const uint32_t cg = rl32(nsv, (int)g);
         const uint32_t cut = hrb - (cg <= (uint32_t)BK_CAP ? cg : 0u);
+#ifdef ME_STAMPS
+        h_m = stamp_now();
+#endif
         if (c && c <= (uint32_t)BK_CAP)
-          gw_prepare_cx(sh.buf[(g + 1u) & 1u], cx, (g + 1u) & 1u, sh.stg, ga, bk, s, g + 1u, c, bko, base, L, nfar0,
-                        nfar1, rsq, rjs, ri, gmin, hrb, cut);
+          gw_prepare_cx(sh.buf[(g + 1u) & 1u], sh.buf[g & 1u], cx, (g + 1u) & 1u, sh.stg, ga, bk, s, g + 1u, c, bko,
+                        base, L, nfar0, nfar1, rsq, rjs, ri, gmin, hrb, cut);
+#ifdef ME_STAMPS
+        h_t += stamp_now() - h_m;
+#endif
         __syncthreads();
         if (auniu(sh.stop[g & 1u])) break;
       }
+#ifdef ME_STAMPS
+      if (lane == 0) bk.dbg[(size_t)s * 24u + 5u] = h_t;
+#endif
       continue;
     }
+    GR_STAMP(bk, s, 0);
+#ifdef ME_STAMPS
+    unsigned long long gw_t[4] = {0ull, 0ull, 0ull, 0ull}, gw_m = stamp_now();
+#endif
     LEvG w;
     le_init(w, log8, 0u);
     uint32_t rbase = 0;
     LWalk lw;
     const bool lok = lw_init(lw, bk, s, sh.ltot, bb0, ba0);
     for (int l = lane; l < L; l += 64) {  // the levels' initial totals, no rests or cancels yet
-      cx.t0[l] = sh.ltot[l];
-      cx.rl[l] = 0u;
-      cx.n[l] = 0u;
-      cx.xl[l] = 0u;
+      GwLv v;
+      v.t0 = sh.ltot[l];
+      v.rl = v.n = v.xl = 0u;
+      cx.lv[l] = v;
     }
-    for (uint32_t j = (uint32_t)lane; j < ME_GMAX * BK_CAP / 32; j += 64) cx.dbit[j] = 0u;
-    if (lane == 0) cx.npre = 0u;
     wave_mem_order();
     uint32_t hidx = NIL, gstop = ng;
+    GW_T(1);
     __syncthreads();  // batch 0 prepared
+    GW_T(0);
     for (uint32_t g = 0; g < ng; ++g) {
       if (lane == 0) *a_gtab(ag.gev, s, g) = eb + w.evp;
       const uint32_t cnt = rl32(nsv, (int)g);
@@ -3079,7 +3101,12 @@ __global__ __launch_bounds__(128) void k_agg_gwalk_cx(BookDev bk, AggGArgs ga, A
             lw.ub += (unsigned long long)rli64(B.qsum[blk >> 6], 0);
             adm = lw.ub < LW_CAP;
           }
+          GW_T(1);
           const uint32_t k = lw_block_cx(w, lw, cx, ri, oq, ocw, c0v, c1v, c2v, c3v, rbase, adm ? fastm : 0ull, cntb, rr);
+          GW_T(2);
+#ifdef ME_STAMPS
+          gw_t[3] += k;
+#endif
           rbase += cntb;
           if (v && (uint32_t)lane < k) {
             const uint32_t rj = (ocw >> LW_RJ_SHIFT) & LW_RJ_MASK;
@@ -3093,7 +3120,9 @@ __global__ __launch_bounds__(128) void k_agg_gwalk_cx(BookDev bk, AggGArgs ga, A
         }
       }
       if (lane == 0) sh.stop[g & 1u] = stop ? 1u : 0u;
+      GW_T(1);
       __syncthreads();
+      GW_T(0);
       if (stop) {
         gstop = g;
         break;
@@ -3113,6 +3142,11 @@ __global__ __launch_bounds__(128) void k_agg_gwalk_cx(BookDev bk, AggGArgs ga, A
       slot->hidx = hidx;
       slot->pos = gstop;
     }
+    GR_STAMP(bk, s, 1);
+#ifdef ME_STAMPS
+    if (lane == 0)
+      for (int q = 0; q < 4; ++q) bk.dbg[(size_t)s * 24u + q] = gw_t[q];
+#endif
   }
 }
 

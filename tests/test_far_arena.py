@@ -130,3 +130,45 @@ def test_far_levels_in_book_snapshots(me, orc):
         assert len(bids) == 601
         assert bids["price_q4"][0] == 100000 and bids["price_q4"][-1] == 1000
         assert np.all(np.diff(bids["price_q4"]) < 0)
+
+
+@pytest.mark.parametrize("path", ["reg", "agg"])
+def test_far_arena_worst_case_default_sizing(me, orc, monkeypatch, path):
+    """The far arena's bound at its DEFAULT sizing (no ME_FAR_GC_AT, default far_levels) with max_resting
+    close to the live count: in ONE launch group four symbols each grow a side far past its inline region
+    (300 far asks), cancel every one of them and grow it again. Nothing may fail, every record equals the
+    oracle, and the active half's use stays within its size (6 x (max_resting + 64) + 4 x far_levels,
+    me_engine.cpp), which the copying collection ahead of the next group brings back down."""
+    monkeypatch.delenv("ME_FAR_GC_AT", raising=False)
+    monkeypatch.setenv("ME_REG_AGG", "1" if path == "agg" else "0")
+    B, S_, L, X = me.SIDE_BUY, me.SIDE_SELL, me.TYPE_LIMIT, me.OP_CANCEL
+    S, nf = 4, 300
+    seq = 1
+    rows1 = []
+    for s in range(S):
+        rows1 += [(s, B, L, 0, 1010, 5), (s, S_, L, 0, 1020, 5)]  # a window around the market
+        rows1 += [(s, S_, L, 0, 2000 + 3 * k, 1 + k % 4) for k in range(nf)]  # far asks above it
+    b1 = _rows(me, rows1, seq)
+    first = {s: seq + s * (nf + 2) + 2 for s in range(S)}
+    seq += len(rows1)
+    rows2 = [(s, B, L, X, first[s] + k, 0) for s in range(S) for k in range(nf)]  # every far ask cancelled
+    rows2 += [(s, S_, L, 0, 5000 + 7 * k, 2) for s in range(S) for k in range(nf)]  # and a far side again
+    b2 = _rows(me, rows2, seq)
+    # admission counts every LIMIT of the batches accepted but not matched yet: both batches of the group
+    max_resting = S * (nf + 2) + S * nf + 16
+    ob = orc.OracleBook(S)
+    with me.Engine(S, 128, [1000] * S, max_batch=len(rows2), max_resting=max_resting, seq_ring=1 << 22,
+                   batches_per_launch=4) as eng:
+        fcap = eng.config()["far_levels"]
+        assert fcap == 256 and nf > fcap
+        t1, t2 = eng.submit_host(b1), eng.submit_host(b2)  # one launch group
+        outs = [eng.collect(t1), eng.collect(t2)]
+        for k, b in enumerate([b1, b2]):
+            ro, fo = ob.submit(b)
+            assert_results_equal(outs[k][0], ro, f"{path} batch {k}")
+            assert_fills_equal(outs[k][1], fo, f"{path} batch {k}")
+        assert_books_equal(eng, ob, range(S), f"far worst case {path}")
+        st = eng.far_stats()
+        assert st["moves"] >= S, st
+        assert st["arena_used"] <= 6 * (max_resting + 64) + 4 * fcap, st
+        assert eng.resting_count() == ob.resting()
