@@ -677,8 +677,8 @@ __device__ __forceinline__ void le_end(LEvG& e) {
 
 // A taker's partial take from the best level is the common case and stays out of the loop (no loop
 // entry, so none of the loop's register copies); the loop runs only when the best level empties.
-template <class LE, bool OCC = false>
-__device__ __forceinline__ void lw_take_buy(LE& e, LWalk& w, int lim, uint32_t& rem, uint32_t jt) {
+template <class LE, bool OCC = false, class W>
+__device__ __forceinline__ void lw_take_buy(LE& e, W& w, int lim, uint32_t& rem, uint32_t jt) {
   if (w.ba > lim) return;  // (rem > 0: rejected records never reach the chain)
   if (ME_LIKELY(w.cba > rem)) {
     w.cba -= rem;
@@ -701,8 +701,8 @@ __device__ __forceinline__ void lw_take_buy(LE& e, LWalk& w, int lim, uint32_t& 
     }
   }
 }
-template <class LE, bool OCC = false>
-__device__ __forceinline__ void lw_take_sell(LE& e, LWalk& w, int lim, uint32_t& rem, uint32_t jt) {
+template <class LE, bool OCC = false, class W>
+__device__ __forceinline__ void lw_take_sell(LE& e, W& w, int lim, uint32_t& rem, uint32_t jt) {
   if (w.bb < lim) return;
   if (ME_LIKELY(w.cbb > rem)) {
     w.cbb -= rem;
@@ -726,8 +726,8 @@ __device__ __forceinline__ void lw_take_sell(LE& e, LWalk& w, int lim, uint32_t&
   }
 }
 // a bid rests at l (< ba: every ask up to the limit was taken)
-template <class LE, bool OCC = false>
-__device__ __forceinline__ void lw_rest_buy(LE& e, LWalk& w, int l, uint32_t q, uint32_t jt) {
+template <class LE, bool OCC = false, class W>
+__device__ __forceinline__ void lw_rest_buy(LE& e, W& w, int l, uint32_t q, uint32_t jt) {
   if (l == w.bb) {
     w.cbb += q;
   } else if (l > w.bb) {  // a new best bid (an empty level)
@@ -741,8 +741,8 @@ __device__ __forceinline__ void lw_rest_buy(LE& e, LWalk& w, int l, uint32_t q, 
   }
   le_emit(e, (uint32_t)l, jt, q);
 }
-template <class LE, bool OCC = false>
-__device__ __forceinline__ void lw_rest_sell(LE& e, LWalk& w, int l, uint32_t q, uint32_t jt) {
+template <class LE, bool OCC = false, class W>
+__device__ __forceinline__ void lw_rest_sell(LE& e, W& w, int l, uint32_t q, uint32_t jt) {
   if (l == w.ba) {
     w.cba += q;
   } else if (l < w.ba) {
@@ -840,10 +840,123 @@ __device__ __forceinline__ void lw_end(LWalk& w, const BookDev& bk, uint32_t s) 
   }
 }
 // The block's quantities onto the bound; false: the block could take the book to LW_CAP
-__device__ __forceinline__ bool lw_admit(LWalk& w, int oq) {
+template <class W>
+__device__ __forceinline__ bool lw_admit(W& w, int oq) {
   unsigned long long q = (unsigned long long)(uint32_t)max(oq, 0);
   w.ub += (unsigned long long)rli64(wave_incl_scan((long long)q), 63);
   return w.ub < LW_CAP;
+}
+
+// The ladder in registers (windows of L <= 128 levels: the grouped path, config 1's hot symbol): level l's
+// total is lane l & 63 of VGPR t[l >> 6]. A rest's add is two VALU ops, a read one v_readlane, and the
+// search for the next occupied level a ballot and a bit scan — no LDS round trip on the chain (the LDS form
+// waits on one per emptied level, and config 5's cancels empty a best level 2 times in 3). The best
+// levels' totals are cached in SGPRs as in LWalk (their register copies stale while cached); levels >= L
+// hold 0.
+struct RWalk {
+  uint32_t t0, t1;   // VGPRs: levels lane, 64 + lane
+  int bb, ba;
+  uint32_t cbb, cba;
+  int L;
+  unsigned long long ub;
+};
+__device__ __forceinline__ uint32_t lw_get(const RWalk& w, int l) {
+  return l < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)w.t0, l)
+                : (uint32_t)__builtin_amdgcn_readlane((int)w.t1, l - 64);
+}
+__device__ __forceinline__ void lw_put(RWalk& w, int l, uint32_t v) {
+  if (l < 64)
+    asm volatile("s_mov_b32 m0, %1\n\tv_writelane_b32 %0, %2, m0" : "+v"(w.t0) : "s"(l), "s"(v) : "m0");
+  else
+    asm volatile("s_mov_b32 m0, %1\n\tv_writelane_b32 %0, %2, m0" : "+v"(w.t1) : "s"(l - 64), "s"(v) : "m0");
+}
+__device__ __forceinline__ void lw_add(RWalk& w, int l, uint32_t d) {
+  const int lane = lane_id();
+  if (l < 64)
+    w.t0 += lane == l ? d : 0u;
+  else
+    w.t1 += lane == l - 64 ? d : 0u;
+}
+template <bool OCC>
+__device__ __forceinline__ void lw_occ_set(RWalk&, int) {}
+template <bool OCC>
+__device__ __forceinline__ void lw_occ_clr(RWalk&, int) {}
+// smallest occupied level >= x (x in [0, 128]), or L
+template <bool OCC = false>
+__device__ __forceinline__ int lw_next(const RWalk& w, int x, uint32_t& tot) {
+  const unsigned long long m0 = __ballot(w.t0 != 0u), m1 = __ballot(w.t1 != 0u);
+  if (x < 64) {
+    const unsigned long long a = m0 & (~0ull << x);
+    if (a) {
+      const int l = __builtin_ctzll(a);
+      tot = (uint32_t)__builtin_amdgcn_readlane((int)w.t0, l);
+      return l;
+    }
+    x = 64;
+  }
+  if (x < 128) {
+    const unsigned long long a = m1 & (~0ull << (x - 64));
+    if (a) {
+      const int l = __builtin_ctzll(a);
+      tot = (uint32_t)__builtin_amdgcn_readlane((int)w.t1, l);
+      return 64 + l;
+    }
+  }
+  tot = 0u;
+  return w.L;
+}
+// largest occupied level <= x (x in [-1, 127]), or -1
+template <bool OCC = false>
+__device__ __forceinline__ int lw_prev(const RWalk& w, int x, uint32_t& tot) {
+  const unsigned long long m0 = __ballot(w.t0 != 0u), m1 = __ballot(w.t1 != 0u);
+  if (x >= 64) {
+    const unsigned long long a = m1 & (~0ull >> (127 - x));
+    if (a) {
+      const int l = 63 - __builtin_clzll(a);
+      tot = (uint32_t)__builtin_amdgcn_readlane((int)w.t1, l);
+      return 64 + l;
+    }
+    x = 63;
+  }
+  if (x >= 0) {
+    const unsigned long long a = m0 & (~0ull >> (63 - x));
+    if (a) {
+      const int l = 63 - __builtin_clzll(a);
+      tot = (uint32_t)__builtin_amdgcn_readlane((int)w.t0, l);
+      return l;
+    }
+  }
+  tot = 0u;
+  return -1;
+}
+// the ladder from HBM (as lw_init: false if the book's sum reaches LW_CAP)
+__device__ __forceinline__ bool lw_init(RWalk& w, const BookDev& bk, uint32_t s, int bb, int ba) {
+  const int lane = lane_id();
+  w.L = (int)bk.L;
+  const Level* lv = bk.levels + (size_t)s * bk.L;
+  const long long a = lane < w.L ? lv[lane].total : 0ll;
+  const long long b = 64 + lane < w.L ? lv[64 + lane].total : 0ll;
+  w.t0 = (uint32_t)a;
+  w.t1 = (uint32_t)b;
+  w.ub = (unsigned long long)rli64(wave_incl_scan(a + b), 63);
+  w.bb = bb;
+  w.ba = ba;
+  w.cbb = bb >= 0 ? lw_get(w, bb) : 0u;
+  w.cba = ba < w.L ? lw_get(w, ba) : 0u;
+  return w.ub < LW_CAP;
+}
+// the ladder back to HBM: totals and occupancy words (the cached totals first)
+__device__ __forceinline__ void lw_end(RWalk& w, const BookDev& bk, uint32_t s) {
+  const int lane = lane_id();
+  if (w.bb >= 0) lw_put(w, w.bb, w.cbb);
+  if (w.ba < w.L) lw_put(w, w.ba, w.cba);
+  Level* lv = bk.levels + (size_t)s * bk.L;
+  unsigned long long* oc = bk.occ + (size_t)s * bk.Lwords;
+  if (lane < w.L) lv[lane].total = (long long)w.t0;
+  if (64 + lane < w.L) lv[64 + lane].total = (long long)w.t1;
+  const unsigned long long m0 = __ballot(w.t0 != 0u), m1 = __ballot(w.t1 != 0u);
+  if (lane == 0 && bk.Lwords > 0u) oc[0] = m0;
+  if (lane == 0 && w.L > 64 && bk.Lwords > 1u) oc[1] = m1;
 }
 
 // Control word of a record in vector form: the level a LIMIT rests at / the last level a taker may
@@ -855,8 +968,8 @@ __device__ __forceinline__ uint32_t lw_cw(uint32_t okd, int olm, uint32_t rj, in
 }
 
 // (record r of the block logs its events with jt = (jb + r) << JS: scalar arithmetic, no v_readlane)
-template <int JS, class LE, bool OCC = false>
-__device__ __forceinline__ uint32_t lw_block(LE& e, LWalk& w, int oq, uint32_t ocw, uint32_t jb,
+template <int JS, class LE, bool OCC = false, class W>
+__device__ __forceinline__ uint32_t lw_block(LE& e, W& w, int oq, uint32_t ocw, uint32_t jb,
                                              unsigned long long fastm, uint32_t cnt, int& rr) {
   // the records the walk covers run up to the first it does not (k); rejected ones need no chain work:
   // the loop visits the set bits of `work` (a scalar bit scan, no per-record tests)
@@ -1000,6 +1113,8 @@ __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const Agg
   // the ladder walk; the top-of-book lists (64-bit totals) for a book the ladder cannot hold, or beyond
   // ag.ladder_max levels
   AList A, B;  // asks (side 1), bids (side 0)
+  // (the LDS ladder also at L <= 128: config 1 ran 4.5 -> 4.25M orders/s with the register form, whose
+  // one-lane adds cost more on its rest-heavy chain than the rare emptied-level scans it saves)
   LWalk lw;
   LEv le;
   le_init(le, ag, eb);
@@ -2159,7 +2274,6 @@ __device__ __forceinline__ uint32_t a_ghand(const BookDev& bk, uint32_t s, uint3
 
 __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDev ag) {
   __shared__ AStage stg;
-  __shared__ uint32_t ltot[128 + 64];
   const int lane = lane_id();
   const int L = (int)bk.L;  // <= 128
   const uint32_t ng = ga.ng;
@@ -2226,8 +2340,8 @@ __global__ __launch_bounds__(64) void k_agg_gwalk(BookDev bk, AggGArgs ga, AggDe
     const gptr<uint32_t> rjs = rsq + total;
     const unsigned long long gmin = *ga.seq0;
     uint32_t rbase = 0;
-    LWalk lw;
-    const bool lok = lw_init(lw, bk, s, ltot, bb0, ba0);  // else: the continuation from the first record
+    RWalk lw;
+    const bool lok = lw_init(lw, bk, s, bb0, ba0);  // else: the continuation from the first record
     uint32_t hidx = NIL, gstop = ng;
     // a batch's bucket is loaded while the batch before it runs (no HBM round trip between batches)
     // (only the lanes of the bucket's records load: a 128-slot bucket holds ~64 at config 2)
@@ -2348,7 +2462,6 @@ struct GwBuf {
 struct GwShared {
   AStage stg;  // the helper's staging of the raw bucket
   GwBuf buf[2];
-  uint32_t ltot[128 + 64];
   uint32_t go, eb, stop[2];
 };
 
@@ -2494,8 +2607,8 @@ __global__ __launch_bounds__(128) void k_agg_gwalk2(BookDev bk, AggGArgs ga, Agg
     LEvG w;
     le_init(w, log8, 0u);
     uint32_t rbase = 0;
-    LWalk lw;
-    const bool lok = lw_init(lw, bk, s, sh.ltot, bb0, ba0);
+    RWalk lw;
+    const bool lok = lw_init(lw, bk, s, bb0, ba0);
     uint32_t hidx = NIL, gstop = ng;
     __syncthreads();  // batch 0 prepared
     for (uint32_t g = 0; g < ng; ++g) {
@@ -2603,9 +2716,6 @@ constexpr uint32_t LW_RJ_MASK = 0x1FFFu;
 constexpr uint32_t AGG_CXF = 1u << 14, AGG_CXU = 1u << 13, AGG_CXP = 1u << 12;
 constexpr uint32_t RI_BIG = 0xFFFFFFFFu;  // rest info of a rest too large to pack (>= 2^25): its cancel hands off
 
-struct alignas(16) GwLv {  // per level: initial total, the group's rests, its cancels, the quantity they removed
-  uint32_t t0, rl, n, xl;
-};
 struct alignas(16) GwRi {  // a LIMIT's rest: maker position U, qty << 7 | level (0: none), F at the rest
   uint32_t u, lq, f, pad;
 };
@@ -2613,7 +2723,6 @@ struct GwCx {
   uint32_t ct0[2][BK_CAP], ct1[2][BK_CAP], ct2[2][BK_CAP], ct3[2][BK_CAP];  // per batch buffer: each cancel's
                                             // target {CT_PRE | level << 24 | qty, U, -, -} or {record | level << 16
                                             // | CT_RING, -, -, -} or {record | level << 16, U, lq, F} (from HBM)
-  GwLv lv[128];
   uint2 ent[128 * GW_CXL];                  // per level: its first GW_CXL cancels {maker position, removed}
   GwRi ring[GW_RING];                       // the rests of the batch being walked and the one before
   // (the helper's) targets of the group's cancels so far: a second cancel of one is UNKNOWN — the first left
@@ -2814,43 +2923,115 @@ __device__ __forceinline__ void gw_prepare_cx(GwBuf& B, const GwBuf& Bp, GwCx& X
   }
 }
 
+// The group's per-level state in registers (level l: lane l & 63 of [l >> 6]), beside the ladder's totals:
+// initial total, the group's rests, its cancels, the quantity they removed. Reads are v_readlane, writes
+// v_writelane — no LDS round trip on the chain.
+struct GwLvR {
+  uint32_t t0[2], rl[2], n[2], xl[2];
+};
+__device__ __forceinline__ uint32_t gv_get(const uint32_t (&v)[2], uint32_t l) {
+  return l < 64u ? rl32(v[0], (int)l) : rl32(v[1], (int)l - 64);
+}
+__device__ __forceinline__ void gv_put(uint32_t (&v)[2], uint32_t l, uint32_t x) {
+  if (l < 64u)
+    asm volatile("s_mov_b32 m0, %1\n\tv_writelane_b32 %0, %2, m0" : "+v"(v[0]) : "s"(l), "s"(x) : "m0");
+  else
+    asm volatile("s_mov_b32 m0, %1\n\tv_writelane_b32 %0, %2, m0" : "+v"(v[1]) : "s"(l - 64u), "s"(x) : "m0");
+}
+
 // The chain of a block with cancels (lw_block's loop; a LIMIT also records its rest info, cancels as above).
 // Returns the records walked: fewer than cnt at the first one the walk does not cover.
-__device__ __forceinline__ uint32_t lw_block_cx(LEvG& e, LWalk& w, GwCx& X, const GwRest& ri, int oq, uint32_t ocw,
-                                                uint32_t c0v, uint32_t c1v, uint32_t c2v, uint32_t c3v, uint32_t jb,
-                                                unsigned long long fastm, uint32_t cnt, int& rr) {
+// Rest info: record r of the block keeps its {U, qty << 7 | level, F} in lane r of three VGPRs (a cancel of
+// it later in the block reads them there); at the block's end the lanes store them to the LDS ring and, for
+// rests, to HBM. A cancel of a record from an earlier block has its target's rest info loaded at the block's
+// start, one vector LDS read for the block, so the chain reads it with v_readlane too.
+__device__ __forceinline__ uint32_t lw_block_cx(LEvG& e, RWalk& w, GwLvR& V, GwCx& X, const GwRest& ri, int oq,
+                                                uint32_t ocw, uint32_t c0v, uint32_t c1v, uint32_t c2v, uint32_t c3v,
+                                                uint32_t jb, unsigned long long fastm, uint32_t cnt, int& rr,
+                                                unsigned long long* rt) {
   const int lane = lane_id();
   const unsigned long long upto = (cnt >= 64u ? ~0ull : ((1ull << cnt) - 1ull)) & ~fastm;
-  const uint32_t k = upto ? (uint32_t)__builtin_ctzll(upto) : cnt;
+  uint32_t k = upto ? (uint32_t)__builtin_ctzll(upto) : cnt;
   const unsigned long long rjm = __ballot(((ocw >> LW_RJ_SHIFT) & LW_RJ_MASK) != 0u);
+  // the cancels' targets: {U, lq, F} per cancel lane (older orders: from the descriptor; earlier records:
+  // HBM's from the helper, or the ring's now); a target earlier in this block: its lane of bu / blq / bf
+  // (a PRE descriptor's level spans bits 24-30, CT_RING's bit among them: test CT_RING only without CT_PRE)
+  const bool isx = (uint32_t)lane < cnt && (ocw & LW_CX) != 0u;
+  const bool xpre = isx && (c0v & CT_PRE) != 0u;
+  const bool xring = isx && (c0v & (CT_PRE | CT_RING)) == CT_RING;
+  const uint32_t xj = c0v & 0xFFFFu;
+  const unsigned long long samem = __ballot(xring && xj >= jb);
+  uint32_t su = c1v, slq = c2v, sf = c3v;
+  if (xring && xj < jb) {
+    const GwRi R = X.ring[xj & (GW_RING - 1u)];
+    su = R.u;
+    slq = R.lq;
+    sf = R.f;
+  }
+  if (xpre) {
+    slq = ((c0v & 0xFFFFFFu) << 7) | ((c0v >> 24) & 127u);
+    sf = 0u;  // (nothing consumed at the group start)
+  }
+  uint32_t bu = 0u, blq = 0u, bf = 0u;
+#ifdef ME_STAMPS
+  // (the stamps build: cycles by record kind — cancels the bounds decide, LIMITs, MARKETs, cancels that read
+  // the level's list — in rt[0..3], counts in rt[4..7]; rt[8]: cancels that emptied a best level, rt[9]: of
+  // orders from before the group)
+  unsigned long long rt_m = stamp_now();
+  int rt_k = -1;
+#define RT_MARK(kind)                            \
+  do {                                           \
+    const unsigned long long _n = stamp_now();   \
+    if (rt_k >= 0) {                             \
+      rt[rt_k] += _n - rt_m;                     \
+      rt[rt_k + 4] += 1ull;                      \
+    }                                            \
+    rt_m = _n;                                   \
+    rt_k = (kind);                               \
+  } while (0)
+#else
+#define RT_MARK(kind) ((void)0)
+#endif
   unsigned long long work = (k >= 64u ? ~0ull : ((1ull << k) - 1ull)) & ~rjm;
   while (work) {
     const int r = __builtin_ctzll(work);
     asm volatile("s_bitset0_b64 %0, %1" : "+s"(work) : "s"(r));
     const uint32_t cw = rl32(ocw, r);
     const uint32_t jr = jb + (uint32_t)r;
+    RT_MARK((cw & LW_CX) ? 0 : (cw & LW_MKT) ? 2 : 1);
     if (cw & LW_CX) {
-      // the target (descriptor: its level; older orders and records from before the ring with their rest info,
-      // others in the ring), its level's state and live total, loaded together
       const uint32_t d0 = rl32(c0v, r);
-      // (a PRE descriptor's level spans bits 24-30, CT_RING's bit among them: test CT_RING only without CT_PRE)
-      const bool pre = (d0 & CT_PRE) != 0u, inring = (d0 & (CT_PRE | CT_RING)) == CT_RING;
+      const bool pre = (d0 & CT_PRE) != 0u;
       const uint32_t l = pre ? (d0 >> 24) & 127u : (d0 >> 16) & 127u;
-      const GwLv V = X.lv[l];
-      const GwRi R = X.ring[d0 & (GW_RING - 1u)];
-      const uint32_t tv = w.tot[l];
-      const uint32_t U = inring ? auniu(R.u) : rl32(c1v, r);
-      const uint32_t lq = pre ? ((d0 & 0xFFFFFFu) << 7) | l : inring ? auniu(R.lq) : rl32(c2v, r);
-      const uint32_t Fr = pre ? 0u : inring ? auniu(R.f) : rl32(c3v, r);  // (nothing consumed at the group start)
-      if (lq == RI_BIG) return (uint32_t)r;  // (before anything changed: the continuation from here)
+      uint32_t U, lq, Fr;
+      if ((samem >> r) & 1ull) {
+        const int x = (int)((d0 & 0xFFFFu) - jb);
+        U = rl32(bu, x);
+        lq = rl32(blq, x);
+        Fr = rl32(bf, x);
+      } else {
+        U = rl32(su, r);
+        lq = rl32(slq, r);
+        Fr = rl32(sf, r);
+      }
+      if (lq == RI_BIG) {  // (before anything changed: the continuation from here)
+        k = (uint32_t)r;
+        break;
+      }
       const uint32_t q = lq >> 7;  // (0: never rested — a LIMIT filled at once)
-      const uint32_t tot = (int)l == w.bb ? w.cbb : (int)l == w.ba ? w.cba : auniu(tv);
-      const uint32_t n = auniu(V.n), xl = auniu(V.xl), t0 = auniu(V.t0);
-      const uint32_t F = t0 + auniu(V.rl) - xl - tot;     // consumed by the group's takes
-      const uint32_t lo = max(Fr, U > xl ? U - xl : 0u);  // X's start is at least this, and at most U
+      const uint32_t tot = (int)l == w.bb ? w.cbb : (int)l == w.ba ? w.cba : lw_get(w, (int)l);
+      const uint32_t n = gv_get(V.n, l), xl = gv_get(V.xl, l), t0 = gv_get(V.t0, l);
+      const uint32_t F = t0 + gv_get(V.rl, l) - xl - tot;  // consumed by the group's takes
+      const uint32_t lo = max(Fr, U > xl ? U - xl : 0u);    // X's start is at least this, and at most U
       uint32_t cons = F <= lo ? 0u : q;
       if (ME_UNLIKELY(F > lo && F < U + q)) {  // the bounds do not decide: the exact start from the list
-        if (n > GW_CXL) return (uint32_t)r;    // it no longer holds every cancel: the continuation
+        if (n > GW_CXL) {                      // it no longer holds every cancel: the continuation
+          k = (uint32_t)r;
+          break;
+        }
+#ifdef ME_STAMPS
+        rt_k = 3;
+#endif
         const bool vl = (uint32_t)lane < n;
         const uint2 ce = vl ? X.ent[l * GW_CXL + lane] : make_uint2(0u, 0u);
         const uint32_t st = U - a_wsum(vl && ce.x < U ? ce.y : 0u);
@@ -2858,27 +3039,37 @@ __device__ __forceinline__ uint32_t lw_block_cx(LEvG& e, LWalk& w, GwCx& X, cons
       }
       const uint32_t rem = q - cons;
       if (rem) {
-        if (n + 1u >= GW_CXN) return (uint32_t)r;
-        if (lane == 0) {
-          if (n < GW_CXL) X.ent[l * GW_CXL + n] = make_uint2(U, rem);
-          X.lv[l].n = n + 1u;
-          X.lv[l].xl = xl + rem;
+        if (n + 1u >= GW_CXN) {
+          k = (uint32_t)r;
+          break;
         }
+        if (n < GW_CXL && lane == 0) X.ent[l * GW_CXL + n] = make_uint2(U, rem);
+        gv_put(V.n, l, n + 1u);
+        gv_put(V.xl, l, xl + rem);
         if ((int)l == w.bb) {
           w.cbb -= rem;
           if (!w.cbb) {
+#ifdef ME_STAMPS
+            rt[8] += 1ull;
+#endif
             lw_put(w, w.bb, 0u);
             w.bb = lw_prev(w, w.bb - 1, w.cbb);
           }
         } else if ((int)l == w.ba) {
           w.cba -= rem;
           if (!w.cba) {
+#ifdef ME_STAMPS
+            rt[8] += 1ull;
+#endif
             lw_put(w, w.ba, 0u);
             w.ba = lw_next(w, w.ba + 1, w.cba);
           }
         } else {
           lw_add(w, (int)l, 0u - rem);
         }
+#ifdef ME_STAMPS
+        if (pre) rt[9] += 1ull;
+#endif
         const uint32_t flg = pre ? AGG_CXF | AGG_CXP : AGG_CXF;
         le_emit(e, l, (jr | flg) << AGG_GREC_SHIFT, rem);
         le_emit(e, l, (jr | flg | AGG_CXU) << AGG_GREC_SHIFT, pre ? U : U - t0);  // the FIFO's / the rests' position
@@ -2901,27 +3092,34 @@ __device__ __forceinline__ uint32_t lw_block_cx(LEvG& e, LWalk& w, GwCx& X, cons
       asm volatile("" : "+s"(rq));
       if (rq) lw_rest_sell<LEvG>(e, w, lim, rq, jt);
     }
-    // a LIMIT's rest info in the ring (a cancel finds only LIMITs: none for a MARKET) and, for a rest, in
-    // HBM: its maker position and what the level's takes had consumed when it rested (a lower bound on its
-    // start ever after)
-    if (!(cw & LW_MKT)) {
-      GwRi o{0u, 0u, 0u, 0u};
-      if (rq) {
-        const GwLv V = X.lv[lim];
-        const uint32_t tv = w.tot[lim];
-        const uint32_t rl = auniu(V.rl);
-        const uint32_t tot = lim == w.bb ? w.cbb : lim == w.ba ? w.cba : auniu(tv);
-        o.u = auniu(V.t0) + rl;
-        o.f = o.u + rq - auniu(V.xl) - tot;
-        o.lq = rq < (1u << 25) ? (rq << 7) | (uint32_t)lim : RI_BIG;
-        if (lane == 0) X.lv[lim].rl = rl + rq;
-      }
-      if (lane == 0) {
-        X.ring[jr & (GW_RING - 1u)] = o;
-        if (rq) ri.r[jr] = o;
-      }
+    // a rest's info: its maker position and what the level's takes had consumed when it rested (a lower
+    // bound on its start ever after); a LIMIT that did not rest keeps lq 0 ("none")
+    if (rq) {
+      const uint32_t rl = gv_get(V.rl, (uint32_t)lim);
+      const uint32_t tot = lim == w.bb ? w.cbb : lim == w.ba ? w.cba : lw_get(w, lim);
+      const uint32_t ou = gv_get(V.t0, (uint32_t)lim) + rl;
+      const uint32_t of = ou + rq - gv_get(V.xl, (uint32_t)lim) - tot;
+      const uint32_t olq = rq < (1u << 25) ? (rq << 7) | (uint32_t)lim : RI_BIG;
+      gv_put(V.rl, (uint32_t)lim, rl + rq);
+      asm volatile("s_mov_b32 m0, %3\n\tv_writelane_b32 %0, %4, m0\n\tv_writelane_b32 %1, %5, m0\n\tv_writelane_b32 %2, %6, m0"
+                   : "+v"(bu), "+v"(blq), "+v"(bf)
+                   : "s"(r), "s"(ou), "s"(olq), "s"(of)
+                   : "m0");
     }
     asm volatile("s_mov_b32 m0, %1\n\tv_writelane_b32 %0, %2, m0" : "+v"(rr) : "s"(r), "s"(auniu(rem)) : "m0");
+  }
+  RT_MARK(-1);
+#undef RT_MARK
+  // the block's rest info: the ring (cancels in later blocks of this batch and the next) and, for rests, HBM
+  // (the helper's, for cancels in later batches)
+  if ((uint32_t)lane < k) {
+    GwRi o;
+    o.u = bu;
+    o.lq = blq;
+    o.f = bf;
+    o.pad = 0u;
+    X.ring[(jb + (uint32_t)lane) & (GW_RING - 1u)] = o;
+    if (blq) ri.r[jb + (uint32_t)lane] = o;
   }
   return k;
 }
@@ -3057,19 +3255,19 @@ __global__ __launch_bounds__(128) void k_agg_gwalk_cx(BookDev bk, AggGArgs ga, A
     GR_STAMP(bk, s, 0);
 #ifdef ME_STAMPS
     unsigned long long gw_t[4] = {0ull, 0ull, 0ull, 0ull}, gw_m = stamp_now();
+    unsigned long long gw_rt[10] = {0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull, 0ull};
+#else
+    unsigned long long* const gw_rt = nullptr;
 #endif
     LEvG w;
     le_init(w, log8, 0u);
     uint32_t rbase = 0;
-    LWalk lw;
-    const bool lok = lw_init(lw, bk, s, sh.ltot, bb0, ba0);
-    for (int l = lane; l < L; l += 64) {  // the levels' initial totals, no rests or cancels yet
-      GwLv v;
-      v.t0 = sh.ltot[l];
-      v.rl = v.n = v.xl = 0u;
-      cx.lv[l] = v;
-    }
-    wave_mem_order();
+    RWalk lw;
+    const bool lok = lw_init(lw, bk, s, bb0, ba0);
+    GwLvR lv;  // the levels' initial totals (the ladder's, exact at its start), no rests or cancels yet
+    lv.t0[0] = lw.t0;
+    lv.t0[1] = lw.t1;
+    lv.rl[0] = lv.rl[1] = lv.n[0] = lv.n[1] = lv.xl[0] = lv.xl[1] = 0u;
     uint32_t hidx = NIL, gstop = ng;
     GW_T(1);
     __syncthreads();  // batch 0 prepared
@@ -3102,7 +3300,8 @@ __global__ __launch_bounds__(128) void k_agg_gwalk_cx(BookDev bk, AggGArgs ga, A
             adm = lw.ub < LW_CAP;
           }
           GW_T(1);
-          const uint32_t k = lw_block_cx(w, lw, cx, ri, oq, ocw, c0v, c1v, c2v, c3v, rbase, adm ? fastm : 0ull, cntb, rr);
+          const uint32_t k = lw_block_cx(w, lw, lv, cx, ri, oq, ocw, c0v, c1v, c2v, c3v, rbase, adm ? fastm : 0ull, cntb, rr,
+                                         gw_rt);
           GW_T(2);
 #ifdef ME_STAMPS
           gw_t[3] += k;
@@ -3146,6 +3345,8 @@ __global__ __launch_bounds__(128) void k_agg_gwalk_cx(BookDev bk, AggGArgs ga, A
 #ifdef ME_STAMPS
     if (lane == 0)
       for (int q = 0; q < 4; ++q) bk.dbg[(size_t)s * 24u + q] = gw_t[q];
+    if (lane == 0)
+      for (int q = 0; q < 10; ++q) bk.dbg[(size_t)s * 24u + 6u + q] = gw_rt[q];
 #endif
   }
 }

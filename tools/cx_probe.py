@@ -44,7 +44,12 @@ def main():
     for i, n in enumerate(["barrier waits", "set-up+results", "record loop"]):
         print(f"walker {n:15s} median {np.median(d[:, i]):10.0f}  per record {np.median(d[:, i] / rec):7.1f}")
     print(f"helper prepare         median {np.median(d[:, 5]):10.0f}  per record {np.median(d[:, 5] / rec):7.1f}")
-
+    # the record loop by record kind (k_agg_gwalk_cx only: dbg[s * 24 + 6..15])
+    if d[:, 10:14].sum() > 0:
+        for i, n in enumerate(["cancel (bounds)", "LIMIT", "MARKET", "cancel (list)"]):
+            cyc, cnt = d[:, 6 + i].sum(), d[:, 10 + i].sum()
+            print(f"record kind {n:15s} count {cnt:10.0f}  cycles per record {cyc / max(cnt, 1):7.1f}")
+        print(f"cancels that emptied a best level {d[:, 14].sum():.0f}, removing from orders before the group {d[:, 15].sum():.0f}")
 
 if __name__ == "__main__":
     main()
