@@ -860,9 +860,12 @@ struct RWalk {
   int L;
   unsigned long long ub;
 };
+// (a read takes both VGPRs' lanes and selects the SGPR result: the compiler turned a branch on l's half into
+// VALU-materialized conditions; writes branch on the half — same box, k_match per 32 batches: branchless
+// writes 460-469 us on config 2, these 450-458, the old read 455-460; config 5 714-734 / 706-712 / 724-731)
 __device__ __forceinline__ uint32_t lw_get(const RWalk& w, int l) {
-  return l < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)w.t0, l)
-                : (uint32_t)__builtin_amdgcn_readlane((int)w.t1, l - 64);
+  const uint32_t a = rl32(w.t0, l & 63), b = rl32(w.t1, l & 63);
+  return (l & 64) ? b : a;
 }
 __device__ __forceinline__ void lw_put(RWalk& w, int l, uint32_t v) {
   if (l < 64)
@@ -2929,14 +2932,14 @@ __device__ __forceinline__ void gw_prepare_cx(GwBuf& B, const GwBuf& Bp, GwCx& X
 struct GwLvR {
   uint32_t t0[2], rl[2], n[2], xl[2];
 };
-__device__ __forceinline__ uint32_t gv_get(const uint32_t (&v)[2], uint32_t l) {
-  return l < 64u ? rl32(v[0], (int)l) : rl32(v[1], (int)l - 64);
+__device__ __forceinline__ uint32_t gv_get(const uint32_t (&v)[2], uint32_t l) {  // (as lw_get)
+  const uint32_t a = rl32(v[0], (int)(l & 63u)), b = rl32(v[1], (int)(l & 63u));
+  return (l & 64u) ? b : a;
 }
 __device__ __forceinline__ void gv_put(uint32_t (&v)[2], uint32_t l, uint32_t x) {
-  if (l < 64u)
-    asm volatile("s_mov_b32 m0, %1\n\tv_writelane_b32 %0, %2, m0" : "+v"(v[0]) : "s"(l), "s"(x) : "m0");
-  else
-    asm volatile("s_mov_b32 m0, %1\n\tv_writelane_b32 %0, %2, m0" : "+v"(v[1]) : "s"(l - 64u), "s"(x) : "m0");
+  const int lane = lane_id();
+  v[0] = lane == (int)l ? x : v[0];
+  v[1] = lane == (int)l - 64 ? x : v[1];
 }
 
 // The chain of a block with cancels (lw_block's loop; a LIMIT also records its rest info, cancels as above).
