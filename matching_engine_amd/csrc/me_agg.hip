@@ -2963,8 +2963,9 @@ __device__ __forceinline__ uint32_t lw_block_cx(LEvG& e, RWalk& w, GwLvR& V, GwC
   const bool xpre = isx && (c0v & CT_PRE) != 0u;
   const bool xring = isx && (c0v & (CT_PRE | CT_RING)) == CT_RING;
   const uint32_t xj = c0v & 0xFFFFu;
-  const unsigned long long samem = __ballot(xring && xj >= jb);
-  uint32_t su = c1v, slq = c2v, sf = c3v;
+  const unsigned long long samem = __ballot(xring && xj >= jb), prem = __ballot(xpre);
+  const uint32_t tlv = xpre ? (c0v >> 24) & 127u : (c0v >> 16) & 127u;  // the target's level
+  uint32_t su = xring && xj >= jb ? xj - jb : c1v, slq = c2v, sf = c3v;  // (same block: the target's lane)
   if (xring && xj < jb) {
     const GwRi R = X.ring[xj & (GW_RING - 1u)];
     su = R.u;
@@ -3003,12 +3004,11 @@ __device__ __forceinline__ uint32_t lw_block_cx(LEvG& e, RWalk& w, GwLvR& V, GwC
     const uint32_t jr = jb + (uint32_t)r;
     RT_MARK((cw & LW_CX) ? 0 : (cw & LW_MKT) ? 2 : 1);
     if (cw & LW_CX) {
-      const uint32_t d0 = rl32(c0v, r);
-      const bool pre = (d0 & CT_PRE) != 0u;
-      const uint32_t l = pre ? (d0 >> 24) & 127u : (d0 >> 16) & 127u;
+      const bool pre = (prem >> r) & 1ull;
+      const uint32_t l = rl32(tlv, r);
       uint32_t U, lq, Fr;
       if ((samem >> r) & 1ull) {
-        const int x = (int)((d0 & 0xFFFFu) - jb);
+        const int x = (int)rl32(su, r);
         U = rl32(bu, x);
         lq = rl32(blq, x);
         Fr = rl32(bf, x);
@@ -3023,9 +3023,9 @@ __device__ __forceinline__ uint32_t lw_block_cx(LEvG& e, RWalk& w, GwLvR& V, GwC
       }
       const uint32_t q = lq >> 7;  // (0: never rested — a LIMIT filled at once)
       const uint32_t tot = (int)l == w.bb ? w.cbb : (int)l == w.ba ? w.cba : lw_get(w, (int)l);
-      const uint32_t n = gv_get(V.n, l), xl = gv_get(V.xl, l), t0 = gv_get(V.t0, l);
-      const uint32_t F = t0 + gv_get(V.rl, l) - xl - tot;  // consumed by the group's takes
-      const uint32_t lo = max(Fr, U > xl ? U - xl : 0u);    // X's start is at least this, and at most U
+      const uint32_t n = gv_get(V.n, l), xr = gv_get(V.xl, l), t0 = gv_get(V.t0, l);
+      const uint32_t F = t0 + gv_get(V.rl, l) - xr - tot;  // consumed by the group's takes
+      const uint32_t lo = max(Fr, U > xr ? U - xr : 0u);    // X's start is at least this, and at most U
       uint32_t cons = F <= lo ? 0u : q;
       if (ME_UNLIKELY(F > lo && F < U + q)) {  // the bounds do not decide: the exact start from the list
         if (n > GW_CXL) {                      // it no longer holds every cancel: the continuation
@@ -3048,7 +3048,7 @@ __device__ __forceinline__ uint32_t lw_block_cx(LEvG& e, RWalk& w, GwLvR& V, GwC
         }
         if (n < GW_CXL && lane == 0) X.ent[l * GW_CXL + n] = make_uint2(U, rem);
         gv_put(V.n, l, n + 1u);
-        gv_put(V.xl, l, xl + rem);
+        gv_put(V.xl, l, xr + rem);
         if ((int)l == w.bb) {
           w.cbb -= rem;
           if (!w.cbb) {
