@@ -666,6 +666,21 @@ __device__ __forceinline__ void le_emit(LEvG& e, uint32_t lvl, uint32_t j, uint3
   e.evp += 1u;
   if (ME_UNLIKELY(slot == 63u)) le_store(e, e.evp - 64u, 64u);
 }
+// two events, one slot test (the second lands in the same 64-event block unless the first fills it)
+__device__ __forceinline__ void le_emit2(LEvG& e, uint32_t lvl, uint32_t j0, uint32_t q0, uint32_t j1, uint32_t q1) {
+  const uint32_t slot = e.evp & 63u;
+  if (ME_LIKELY(slot < 62u)) {
+    asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %3, m0\n\tv_writelane_b32 %1, %4, m0\n\t"
+                 "s_add_u32 m0, m0, 1\n\tv_writelane_b32 %0, %5, m0\n\tv_writelane_b32 %1, %6, m0"
+                 : "+v"(e.vw), "+v"(e.vq)
+                 : "s"(slot), "s"(lvl | j0), "s"(q0), "s"(lvl | j1), "s"(q1)
+                 : "m0", "scc");
+    e.evp += 2u;
+  } else {
+    le_emit(e, lvl, j0, q0);
+    le_emit(e, lvl, j1, q1);
+  }
+}
 __device__ __forceinline__ void le_init(LEvG& e, AggGEv* ev, uint32_t eb) {
   e.ev = (gptr<AggGEv>)vptr(ev);
   e.vw = e.vq = 0u;
@@ -2727,6 +2742,8 @@ struct GwCx {
                                             // target {CT_PRE | level << 24 | qty, U, -, -} or {record | level << 16
                                             // | CT_RING, -, -, -} or {record | level << 16, U, lq, F} (from HBM)
   uint2 ent[128 * GW_CXL];                  // per level: its first GW_CXL cancels {maker position, removed}
+  uint2 edum[64];                           // the other lanes' targets of a one-lane list write (and the
+                                            // writes of a level's cancels past its first GW_CXL)
   GwRi ring[GW_RING];                       // the rests of the batch being walked and the one before
   // (the helper's) targets of the group's cancels so far: a second cancel of one is UNKNOWN — the first left
   // the order dead, whether it removed anything or found it consumed
@@ -3046,7 +3063,10 @@ __device__ __forceinline__ uint32_t lw_block_cx(LEvG& e, RWalk& w, GwLvR& V, GwC
           k = (uint32_t)r;
           break;
         }
-        if (n < GW_CXL && lane == 0) X.ent[l * GW_CXL + n] = make_uint2(U, rem);
+        {  // (one-lane write without an exec change: the other lanes, and a full list, write dummy slots)
+          uint2* ep = lane == 0 && n < GW_CXL ? &X.ent[l * GW_CXL + n] : &X.edum[lane];
+          *ep = make_uint2(U, rem);
+        }
         gv_put(V.n, l, n + 1u);
         gv_put(V.xl, l, xr + rem);
         if ((int)l == w.bb) {
@@ -3074,8 +3094,8 @@ __device__ __forceinline__ uint32_t lw_block_cx(LEvG& e, RWalk& w, GwLvR& V, GwC
         if (pre) rt[9] += 1ull;
 #endif
         const uint32_t flg = pre ? AGG_CXF | AGG_CXP : AGG_CXF;
-        le_emit(e, l, (jr | flg) << AGG_GREC_SHIFT, rem);
-        le_emit(e, l, (jr | flg | AGG_CXU) << AGG_GREC_SHIFT, pre ? U : U - t0);  // the FIFO's / the rests' position
+        le_emit2(e, l, (jr | flg) << AGG_GREC_SHIFT, rem, (jr | flg | AGG_CXU) << AGG_GREC_SHIFT,
+                 pre ? U : U - t0);  // the FIFO's / the rests' position
       }
       asm volatile("s_mov_b32 m0, %1\n\tv_writelane_b32 %0, %2, m0" : "+v"(rr) : "s"(r), "s"(rem) : "m0");
       continue;
