@@ -48,10 +48,15 @@ for step in "$@"; do
     python3 $R/tools/prof_summary.py trace $O/trace_${wl}_$k --steps $k > $O/trace_${wl}_$k.txt && cat $O/trace_${wl}_$k.txt
     ;;
   traffic)
+    # (config 4: its 20 seeding batches run through the same kernels before the warmup — dropped with
+    # --from-sweep 20; config 3: no cluster leg, whose separate engines would add their dispatches)
+    FS=""; XA=""
+    [ $wl = c4 ] && FS="--from-sweep 20"
+    [ $wl = c3 ] && XA="--cluster-steps 0"
     for c in FETCH_SIZE WRITE_SIZE; do
-      timeout -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex "$KRE" --output-format csv -d $O/pmc_${wl}_$c -o pmc -- $(bench_cmd $wl 64 32) > $O/pmc_${wl}_$c.log 2>&1 || { echo "PMC_FAIL $wl $c"; tail -5 $O/pmc_${wl}_$c.log; exit 1; }
+      timeout -s KILL 300 rocprofv3 --pmc $c --kernel-include-regex "$KRE" --output-format csv -d $O/pmc_${wl}_$c -o pmc -- $(bench_cmd $wl 64 32) $XA > $O/pmc_${wl}_$c.log 2>&1 || { echo "PMC_FAIL $wl $c"; tail -5 $O/pmc_${wl}_$c.log; exit 1; }
     done
-    python3 $R/tools/prof_summary.py traffic $O/pmc_${wl}_FETCH_SIZE $O/pmc_${wl}_WRITE_SIZE --bench $O/pmc_${wl}_WRITE_SIZE.log > $O/pmc_traffic_$wl.json && cat $O/pmc_traffic_$wl.json
+    python3 $R/tools/prof_summary.py traffic $O/pmc_${wl}_FETCH_SIZE $O/pmc_${wl}_WRITE_SIZE --bench $O/pmc_${wl}_WRITE_SIZE.log $FS > $O/pmc_traffic_$wl.json && cat $O/pmc_traffic_$wl.json
     ;;
   dram)
     timeout -s KILL 300 rocprofv3 --pmc TCC_EA0_RDREQ_DRAM_32B TCC_EA0_WRREQ_WRITE_DRAM_32B TCC_EA0_WRREQ_WRITE_ATOMIC_32B TCC_EA0_RDREQ --kernel-include-regex "$KRE" --output-format csv -d $O/dram_$wl -o pmc -- $(bench_cmd $wl 64 32) > $O/dram_$wl.log 2>&1 || { echo "DRAM_FAIL $wl"; tail -5 $O/dram_$wl.log; exit 1; }
