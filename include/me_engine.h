@@ -114,7 +114,7 @@ typedef struct me_config {
                                   than seq_ring seqs */
   const int64_t* base_price;   /* [num_symbols] initial window base (price_q4 of level 0) per symbol */
   const uint32_t* symbol_ids;  /* optional [num_symbols] ids written to me_fill.symbol (NULL = local id) */
-  uint32_t batches_per_launch; /* L <= 128: device batches matched per kernel launch, 1..64 (0 = 32). Back-to-back
+  uint32_t batches_per_launch; /* L <= 128: device batches matched per kernel launch, 1..32 (0 = 32). Back-to-back
                                   me_submit_batch_device calls fill a group; me_sync flushes a partial one */
   uint32_t far_levels;         /* far levels (price levels outside the window) each symbol and side holds in
                                   its inline region, 0 = 256. Not a limit: a side that outgrows it moves to

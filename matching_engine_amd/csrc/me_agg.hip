@@ -2923,6 +2923,7 @@ __device__ __forceinline__ void gw_prepare_cx(GwBuf& B, const GwBuf& Bp, GwCx& X
           X.npre = np + 1u;
         }
       } else {
+        static_assert(ME_GMAX * BK_CAP <= 4096, "a group's record numbers fit the descriptor's 12-bit mask");
         const uint32_t jj = e0 & 0xFFFu, wd = auniu(X.tbit[jj >> 5]);
         if ((wd >> (jj & 31u)) & 1u)
           r = 1u;
