@@ -27,6 +27,8 @@
 #include <atomic>
 #include <cmath>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
 #include <deque>
 #include <memory>
 #include <mutex>
@@ -54,8 +56,81 @@ double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-// f(t, lo, hi) over [0, n) in T contiguous chunks on T threads (the caller runs chunk 0); one thread below
-// `grain` records per chunk. The host halves of a large slice (split, pack, merge) are memory-bound loops.
+// A persistent pool of up to 15 host threads for the parallel regions below (created on first use, parked
+// on a condition variable between regions): a region used to start and join its threads, ~0.5-1 ms of the
+// 5 ms rank 0 spends per 1M-order slice at W = 8. One region runs at a time (regions from the service's
+// flusher and persister threads queue on `run_mu_`).
+class ParPool {
+ public:
+  static ParPool& get() {
+    static ParPool p;
+    return p;
+  }
+  // job(t) for t in [0, T); the caller runs its share too
+  void run(size_t T, const std::function<void(size_t)>& job) {
+    std::lock_guard<std::mutex> rl(run_mu_);
+    std::unique_lock<std::mutex> lk(mu_);
+    while (th_.size() + 1 < T) th_.emplace_back([this] { worker(); });
+    job_ = &job;
+    T_ = T;
+    next_.store(0);
+    done_ = 0;
+    ++gen_;
+    cv_.notify_all();
+    lk.unlock();
+    size_t mine = 0;
+    for (size_t t; (t = next_.fetch_add(1)) < T;) {
+      job(t);
+      ++mine;
+    }
+    lk.lock();
+    done_ += mine;
+    done_cv_.wait(lk, [&] { return done_ == T_; });
+    job_ = nullptr;
+  }
+  ~ParPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+
+ private:
+  void worker() {
+    uint64_t seen = 0;
+    std::unique_lock<std::mutex> lk(mu_);
+    for (;;) {
+      cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+      if (stop_) return;
+      seen = gen_;
+      const std::function<void(size_t)>* job = job_;
+      const size_t T = T_;
+      lk.unlock();
+      size_t mine = 0;
+      for (size_t t; job && (t = next_.fetch_add(1)) < T;) {
+        (*job)(t);
+        ++mine;
+      }
+      lk.lock();
+      done_ += mine;
+      if (done_ == T_) done_cv_.notify_all();
+    }
+  }
+  std::mutex run_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  std::vector<std::thread> th_;
+  const std::function<void(size_t)>* job_ = nullptr;
+  size_t T_ = 0, done_ = 0;
+  std::atomic<size_t> next_{0};
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
+// f(t, lo, hi) over [0, n) in T contiguous chunks on T threads of the pool (the caller takes chunks too);
+// one thread below `grain` records per chunk. The host halves of a large slice (split, pack, merge) are
+// memory-bound loops.
 template <class F>
 void par_chunks(size_t n, size_t grain, F f) {
   const size_t hw = std::max<unsigned>(1u, std::thread::hardware_concurrency());
@@ -64,11 +139,8 @@ void par_chunks(size_t n, size_t grain, F f) {
     f(0, 0, n);
     return;
   }
-  std::vector<std::thread> th;
-  th.reserve(T - 1);
-  for (size_t t = 1; t < T; ++t) th.emplace_back(f, t, n * t / T, n * (t + 1) / T);
-  f(0, 0, n / T);
-  for (auto& x : th) x.join();
+  const std::function<void(size_t)> job = [&](size_t t) { f(t, n * t / T, n * (t + 1) / T); };
+  ParPool::get().run(T, job);
 }
 size_t par_threads(size_t n, size_t grain) {
   const size_t hw = std::max<unsigned>(1u, std::thread::hardware_concurrency());
