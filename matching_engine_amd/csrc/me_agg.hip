@@ -862,8 +862,8 @@ __device__ __forceinline__ bool lw_admit(W& w, int oq) {
   return w.ub < LW_CAP;
 }
 
-// The ladder in registers (windows of L <= 128 levels: the grouped path, config 1's hot symbol): level l's
-// total is lane l & 63 of VGPR t[l >> 6]. A rest's add is two VALU ops, a read one v_readlane, and the
+// The ladder in registers (windows of L <= 128 levels: the grouped walks): level l's total is lane l & 63
+// of VGPR t[l >> 6]. A rest's add is a lane-masked VALU add, a read two v_readlanes and a select, and the
 // search for the next occupied level a ballot and a bit scan — no LDS round trip on the chain (the LDS form
 // waits on one per emptied level, and config 5's cancels empty a best level 2 times in 3). The best
 // levels' totals are cached in SGPRs as in LWalk (their register copies stale while cached); levels >= L
@@ -1131,8 +1131,9 @@ __device__ void agg_walk_symbol(const BookDev& bk, const BatchDev& bt, const Agg
   // the ladder walk; the top-of-book lists (64-bit totals) for a book the ladder cannot hold, or beyond
   // ag.ladder_max levels
   AList A, B;  // asks (side 1), bids (side 0)
-  // (the LDS ladder also at L <= 128: config 1 ran 4.5 -> 4.25M orders/s with the register form, whose
-  // one-lane adds cost more on its rest-heavy chain than the rare emptied-level scans it saves)
+  // (the LDS ladder here: the register form widened to four VGPRs for config 1's 256 levels ran it at
+  // 3.9-4.0M against 4.4-4.5M orders/s, same box — its rest-heavy chain prefers the LDS ladder's
+  // fire-and-forget adds, and its emptied-level scans are rare; profiles/r6/ab_rw4)
   LWalk lw;
   LEv le;
   le_init(le, ag, eb);
