@@ -161,6 +161,39 @@ def test_agg_groups_device_back_to_back(me, orc):
             db.free()
 
 
+@pytest.mark.parametrize("early", ["0", "3", "8"])
+def test_agg_groups_early_fill_after_flush(me, orc, monkeypatch, early):
+    """Groups submitted after a flush bucket every ME_EARLY_FILL batches while the rest are still being
+    submitted (me_engine.cpp early_fill); the flush buckets what is left, if anything. Device batches in
+    groups of 5, 8, 9, 16, 20, 32 and 3 at G = 32, a sync after each: every batch of every group against
+    the oracle."""
+    monkeypatch.setenv("ME_EARLY_FILL", early)
+    sc = me.preset(2, num_symbols=96, batch=4096)
+    st = me.Stream(sc)
+    base = st.base_prices()
+    sizes = [5, 8, 9, 16, 20, 32, 3]
+    batches = [st.next(sc.batch) for _ in range(sum(sizes))]
+    ob = orc.OracleBook(sc.num_symbols)
+    with _engine(me, sc, base, batches, batches_per_launch=32) as eng:
+        dbs = [eng.upload(b) for b in batches]
+        k0 = 0
+        for n in sizes:
+            for db in dbs[k0:k0 + n]:
+                eng.submit_device(db)
+            eng.sync()
+            assert eng.last_group_size() == n
+            for k in range(n):
+                r, f = eng.fetch_group_outputs(k, len(batches[k0 + k]))
+                ro, fo = ob.submit(batches[k0 + k])
+                assert_results_equal(r, ro, f"early={early} group of {n} batch {k}")
+                assert_fills_equal(f, fo, f"early={early} group of {n} batch {k}")
+            k0 += n
+        assert_books_equal(eng, ob, range(sc.num_symbols), f"early={early}")
+        assert eng.resting_count() == ob.resting()
+        for db in dbs:
+            db.free()
+
+
 def _peak_resting(orc, sc, batches):
     """The most orders resting at any record of the stream (the oracle fed one record at a time)."""
     ob = orc.OracleBook(sc.num_symbols)
