@@ -218,6 +218,11 @@ struct LadderMem {
   unsigned long long* occ;
   uint8_t* tend;
   uint32_t L, Lwords;
+  // words the first step of an occupancy scan reads past the start word: the HBM ladder (k_match<LAD_HBM>,
+  // config 4's cold symbols) reads one 64-B line first — a sparse book's next level is usually within
+  // 512 levels — before 512-B steps
+  int span0 = 64;
+  bool occ_reads = false;  // window scans read only the occupied levels (k_match<LAD_HBM>)
 
   __device__ __forceinline__ Level get(int l) const {
     Level x = lv[l];
@@ -257,9 +262,9 @@ struct LadderMem {
     if (word) return (w << 6) + __builtin_ctzll(word);
     const int lane = lane_id();
     const int nw = (int)Lwords;
-    for (int b = w + 1; b < nw; b += 64) {
+    for (int b = w + 1, span = span0; b < nw; b += span, span = 64) {
       int idx = b + lane;
-      unsigned long long v = idx < nw ? occ[idx] : 0ull;
+      unsigned long long v = lane < span && idx < nw ? occ[idx] : 0ull;
       unsigned long long m = __ballot(v != 0ull);
       if (m) {
         int t = __builtin_ctzll(m);
@@ -280,9 +285,9 @@ struct LadderMem {
     unsigned long long word = occ[w] & keep;
     if (word) return (w << 6) + 63 - __builtin_clzll(word);
     const int lane = lane_id();
-    for (int t0 = w - 1; t0 >= 0; t0 -= 64) {
+    for (int t0 = w - 1, span = span0; t0 >= 0; t0 -= span, span = 64) {
       int idx = t0 - lane;
-      unsigned long long v = idx >= 0 ? occ[idx] : 0ull;
+      unsigned long long v = lane < span && idx >= 0 ? occ[idx] : 0ull;
       unsigned long long m = __ballot(v != 0ull);
       if (m) {
         int t = __builtin_ctzll(m);
@@ -651,7 +656,10 @@ __device__ __forceinline__ long long sweep(WaveCtx& c, int dir, int lim, long lo
   while (rem > 0) {
     if (dir > 0 ? (cur > lim || cur >= L) : (cur < lim || cur < 0)) break;
     const int lv = cur + dir * lane;
-    const bool valid = (dir > 0) ? (lv <= lim && lv < L) : (lv >= lim && lv >= 0);
+    bool valid = (dir > 0) ? (lv <= lim && lv < L) : (lv >= lim && lv >= 0);
+    // the HBM ladder reads only the occupied levels of the 64 (one 8-B word load per lane, the same one or
+    // two words for the whole wave): an empty level holds total 0 and would add nothing to the scan
+    if (c.lad.occ_reads && valid) valid = (c.lad.occ[lv >> 6] >> (lv & 63)) & 1ull;
     const Level W = c.lad.lane_get(lv, valid);
     const long long tot = W.total;
     const long long inc = wave_incl_scan(tot);
@@ -1263,6 +1271,8 @@ __global__ __launch_bounds__(256) void k_match(BookDev bk, BatchDev bt) {
     c.lad.lv = g_lv;
     c.lad.occ = g_occ;
     c.lad.tend = g_tend;
+    c.lad.span0 = 8;
+    c.lad.occ_reads = true;
     c.cache = nullptr;
     c.cmask = 0;
   }
