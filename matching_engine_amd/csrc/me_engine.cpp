@@ -36,6 +36,9 @@ hipError_t launch_match(hipStream_t st, const BookDev& bk, const BatchDev& bt, h
                         const HotLaunch& hot);
 hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* bt, uint32_t ng, const AuxDev& ax, hipEvent_t ev0,
                             hipEvent_t ev1, const HotLaunch* hot);
+namespace rc64 {
+hipError_t launch_fill_early(hipStream_t st, const BookDev& bk, const AuxDev& ax, bool& done);
+}
 uint32_t sort_tile(uint32_t n);
 hipError_t launch_tape(hipStream_t st, const BatchDev& bt, me_fill* tape, unsigned long long tape_cap,
                        unsigned long long* tape_count, unsigned long long* fills_acc, uint32_t* err,
@@ -225,8 +228,8 @@ struct me_engine {
   } g_fill, g_match, g_tape;
   // Early fill: while nothing is in flight (the first group after a flush), every `early_fill` submitted
   // batches are bucketed at once, so the fill overlaps the submits of the rest of the group (0: off;
-  // ME_EARLY_FILL). Config 2's driver shape, same box: 8 -> +2.4 % over off, 4 and 16 no better
-  // (profiles/r6/early_fill).
+  // ME_EARLY_FILL). Config 2's driver shape, same box: 8 -> +0.9 % over off (-0.6 to +2.4 % in earlier
+  // pairs), 4 and 16 no better (profiles/r6/early_fill).
   uint32_t early_fill = 8;
   uint32_t group = 1;     // batches per launch (me_config.batches_per_launch)
   uint64_t ngroup = 0;    // groups launched
@@ -1036,7 +1039,9 @@ static int early_fill(me_engine* e) {
   ax.nb = gf.n - gf.filled;
   for (uint32_t j = 0; j < ax.nb; ++j) bucket_job(e, gf.b[gf.filled + j], ax.b[j]);
   ax.fills_acc = e->d_fills_acc;
-  hipError_t he = launch_match_reg(e->stream, e->bk, nullptr, 0, ax, nullptr, nullptr, &e->hot);
+  bool done = false;
+  hipError_t he = rc64::launch_fill_early(e->stream, e->bk, ax, done);
+  if (he == hipSuccess && !done) he = launch_match_reg(e->stream, e->bk, nullptr, 0, ax, nullptr, nullptr, &e->hot);
   if (he != hipSuccess) return e->hip_fail(he, "early fill launch");
   gf.filled = gf.n;
   return ME_OK;

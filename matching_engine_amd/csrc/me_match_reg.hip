@@ -1151,8 +1151,23 @@ __device__ __forceinline__ uint32_t flat_first(uint32_t off, uint32_t a, uint32_
   return off + (a + A - off % A) % A;
 }
 
+// The early fill's launch (me_engine.cpp early_fill): bucket jobs only, at most FILL_NB of them — a
+// ~0.8-KB argument block instead of SideArgs' ~5.7 KB (the host's launch call is the early fill's cost:
+// ~13 us per launch with SideArgs).
+constexpr uint32_t FILL_NB = 8;
+struct FillArgs {
+  struct {
+    uint32_t* err;
+  } bk;
+  struct {
+    uint32_t S, nb;
+    AuxBucket b[FILL_NB];
+  } ax;
+};
+
 // Bucket records [r0, r1) of bucket job j with a workgroup histogram (cnt: S + 1 LDS counters).
-__device__ __forceinline__ void side_bucket_wg(const SideArgs& G, uint32_t j, uint32_t r0, uint32_t r1, uint32_t* cnt) {
+template <class GA>
+__device__ __forceinline__ void side_bucket_wg(const GA& G, uint32_t j, uint32_t r0, uint32_t r1, uint32_t* cnt) {
   const uint32_t tid = threadIdx.x;
   const AuxBucket& J = G.ax.b[j];
   const uint32_t S = ldsu(G.ax.S);
@@ -1217,6 +1232,24 @@ __device__ __forceinline__ void side_bucket_wg(const SideArgs& G, uint32_t j, ui
       brec[d].qty = q[k];
       brec[d].ok = i | ((k8[k] & 15u) << BK_KIND_SHIFT);
     }
+  }
+}
+
+// Grid: 8 x the most units a batch has; batch j on the blocks b = j (mod 8), its units in turn (k_side's
+// xseq form, one batch per XCD).
+__global__ __launch_bounds__(SIDE_THREADS) void k_side_fill(FillArgs args) {
+  __shared__ FillArgs G;
+  extern __shared__ uint32_t side_cnt[];
+  static_assert(sizeof(FillArgs) % 8 == 0, "FillArgs copy");
+  for (uint32_t i = threadIdx.x; i < sizeof(FillArgs) / 8; i += SIDE_THREADS)
+    reinterpret_cast<unsigned long long*>(&G)[i] = reinterpret_cast<const unsigned long long*>(&args)[i];
+  __syncthreads();
+  const uint32_t nb = ldsu(G.ax.nb), x = blockIdx.x % 8u, k = blockIdx.x / 8u;
+  for (uint32_t j = x; j < nb; j += 8) {
+    const uint32_t n = ldsu(G.ax.b[j].n), r0 = k * SB_REC;
+    if (r0 >= n) continue;  // (uniform over the workgroup)
+    side_bucket_wg(G, j, r0, min(n, r0 + SB_REC), side_cnt);
+    __syncthreads();  // the LDS counters are zeroed again by the next batch
   }
 }
 
@@ -1852,6 +1885,26 @@ __global__ __launch_bounds__(128 * REG_WAVES) void k_match_reg(ColdArgs args) {
 // sort path's bad-symbol bin) and the side jobs of ax on the first dispatch round's extra waves; then,
 // when it matched anything, the continuation launch over the symbols it handed off (one wave per
 // symbol, like the common launch; workgroups with nothing to do leave at once). ev0 / ev1 bracket both.
+// The early fill (bucket jobs of at most FILL_NB batches, symbols within the LDS histogram); false: not
+// this launch's shape (the caller uses launch_match_reg's side launch).
+hipError_t launch_fill_early(hipStream_t st, const BookDev& bk, const AuxDev& ax, bool& done) {
+  done = false;
+  if (ax.nb == 0 || ax.nb > FILL_NB || ax.S > SB_SMAX || ax.nt) return hipSuccess;
+  FillArgs FA{};
+  FA.bk.err = bk.err;
+  FA.ax.S = ax.S;
+  FA.ax.nb = ax.nb;
+  uint32_t per = 0;
+  for (uint32_t j = 0; j < ax.nb; ++j) {
+    FA.ax.b[j] = ax.b[j];
+    per = max(per, (ax.b[j].n + SB_REC - 1) / SB_REC);
+  }
+  hipLaunchKernelGGL(k_side_fill, dim3(8u * max(per, 1u)), dim3(SIDE_THREADS), (size_t)(ax.S + 1) * sizeof(uint32_t),
+                     st, FA);
+  done = true;
+  return hipGetLastError();
+}
+
 hipError_t launch_match_reg(hipStream_t st, const BookDev& bk, const BatchDev* bt, uint32_t ng, const AuxDev& ax,
                             hipEvent_t ev0, hipEvent_t ev1) {
   if (bk.L > (uint32_t)RL || bk.L < 64u || !bk.fcache || !bk.gsym || !bk.hand || !bk.hcount)
