@@ -228,8 +228,8 @@ struct me_engine {
   } g_fill, g_match, g_tape;
   // Early fill: while nothing is in flight (the first group after a flush), every `early_fill` submitted
   // batches are bucketed at once, so the fill overlaps the submits of the rest of the group (0: off;
-  // ME_EARLY_FILL). Config 2's driver shape, same box: 8 -> +0.9 % over off (-0.6 to +2.4 % in earlier
-  // pairs), 4 and 16 no better (profiles/r6/early_fill).
+  // ME_EARLY_FILL). Config 2's driver shape, same box: 8 -> +1.6 % over off (-0.6 to +2.4 % for earlier
+  // forms), 4 and 16 no better (profiles/r6/early_fill).
   uint32_t early_fill = 8;
   uint32_t group = 1;     // batches per launch (me_config.batches_per_launch)
   uint64_t ngroup = 0;    // groups launched
@@ -1050,6 +1050,12 @@ static int early_fill(me_engine* e) {
 // Finish every submitted batch (the last one's outputs are then final).
 static int flush_pipeline(me_engine* e) {
   if (e->g_fill.n) {  // a partial group goes out as it is
+    // with early fills on and nothing in flight, the rest of the group through the light fill launch too:
+    // the fill-only pipe_launch then has nothing to launch
+    if (e->early_fill && e->g_fill.n > e->g_fill.filled && !e->g_match.n && !e->g_tape.n) {
+      int rc = early_fill(e);
+      if (rc) return rc;
+    }
     int rc = pipe_launch(e, &e->g_fill);
     e->g_fill = me_engine::Group{};
     if (rc) return rc;
